@@ -1,0 +1,156 @@
+/*
+ * posfeat_hip.h -- C ABI of libposfeat_hip.so, the MI355X (gfx950) engine for
+ * the PoSFeat extraction + correlation hot path.
+ *
+ * The reference (The-Learning-And-Vision-Atelier-LAVA/PoSFeat) has no FFI: its
+ * hot path is duck-typed Python over PyTorch ATen.  Each entry point below
+ * replaces the ATen work behind one reference Python surface (cited), and the
+ * Python shims in posfeat_amd/ (networks/, losses/, managers/) keep those
+ * surfaces' names, argument meanings and error behaviour.
+ *
+ * Conventions
+ *   - All pointers are device pointers unless stated; all tensors are
+ *     caller-owned (the library never allocates device memory except inside
+ *     posfeat_model_create, which allocates nothing either: the caller passes
+ *     workspace).  Scratch comes from a caller workspace sized by *_workspace.
+ *   - `stream` is a hipStream_t passed as void*; every call is stream-ordered
+ *     and never synchronises the host (graph-capturable), except where noted.
+ *   - Return 0 on success or a negative POSFEAT_E_* code; posfeat_strerror()
+ *     describes it.  No C++ exception crosses the ABI.
+ *   - Feature maps inside the engine are NHWC fp32 with an explicit pixel
+ *     stride (`*_cstride`, in floats) so channel concatenation is free.
+ */
+#ifndef POSFEAT_HIP_H
+#define POSFEAT_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define POSFEAT_OK 0
+#define POSFEAT_E_INVALID (-1)     /* bad argument / unsupported shape     */
+#define POSFEAT_E_HIP (-2)         /* a HIP runtime call failed            */
+#define POSFEAT_E_WORKSPACE (-3)   /* workspace too small                  */
+#define POSFEAT_E_UNSUPPORTED (-4) /* option the engine does not implement */
+
+#define POSFEAT_ACT_NONE 0
+#define POSFEAT_ACT_RELU 1
+#define POSFEAT_ACT_ELU 2
+
+const char *posfeat_strerror(int code);
+int posfeat_abi_version(void);
+/* 1 if a gfx950 device is visible and the code object loads on it. */
+int posfeat_device_ok(void);
+
+/* ------------------------------------------------------------------------
+ * Fused convolution (implicit GEMM on v_mfma_f32_32x32x2_f32).
+ * Replaces: nn.Conv2d + eval BatchNorm2d + ReLU/ELU (+ residual add) of
+ *   networks/DescNet.py:167-179 (conv), 182-190 (upconv's conv) and the
+ *   torchvision Bottleneck convs behind DescNet.py:27-35; and the bias-only
+ *   convs of networks/DeteNet.py:11-21.
+ * x: NHWC, pixel stride x_cstride >= cin (cin multiple of 4).
+ * w: packed [cout][Kpad], K ordered (kh, kw, cin), Kpad = roundup(K, 32),
+ *    zero-padded (posfeat_conv_packed_k).  BN already folded into w/bias.
+ * y[p, c] = act(sum + bias[c] + res[p, c])   (res may be NULL)
+ * ------------------------------------------------------------------------ */
+typedef struct {
+  int n, h, w;       /* input batch / height / width                      */
+  int cin;           /* input channels, multiple of 4                     */
+  int x_cstride;     /* floats between consecutive input pixels           */
+  int cout, kh, kw, stride, pad;
+  int y_cstride;     /* floats between consecutive output pixels          */
+  int res_cstride;   /* floats between consecutive residual pixels        */
+  int act;           /* POSFEAT_ACT_*                                     */
+} posfeat_conv_desc;
+
+int posfeat_conv_packed_k(int cin, int kh, int kw); /* returns Kpad */
+int posfeat_conv2d_nhwc(const posfeat_conv_desc *d, const float *x, const float *w,
+                        const float *bias, const float *res, float *y, void *stream);
+
+/* ------------------------------------------------------------------------
+ * Keypoint selection.
+ * Replaces: losses/preprocess_utils.py:215-278 generate_kpts_single
+ *   (stable=True) with nms (449-464), threshold (232-240), 3x3 soft-argmax
+ *   refine + 3x3 max score (242-247), num_pts clamp (249-261), topk+gather
+ *   (263-267).
+ * kp_map: b x h x w fp32 (the 1-channel local_point).  Tie rule: NMS keeps
+ *   p iff S[p] > every earlier and >= every later element of its
+ *   reflect-padded window (row-major); top-k orders by (score desc, inner
+ *   flat index asc).
+ * thr_mode: 0 = no threshold (thr=False), 1 = 'abs', 2 = 'max', 3 = 'mean'.
+ * num_pts <= 0 means "all survivors" (num_pts=False).
+ * Outputs (capacity `cap` rows per image, cap >= max(num_pts,128) or h*w):
+ *   idx [b][cap] int32 inner flat index, coord [b][cap][2] normalised (x,y),
+ *   score [b][cap], n_sel[1] (device int32) = rows valid per image (same for
+ *   all images, as in the reference), counts[b] (device int32) survivors.
+ * ------------------------------------------------------------------------ */
+int posfeat_detect_workspace(int b, int h, int w, int cap, size_t *bytes);
+int posfeat_detect(const float *kp_map, int b, int h, int w, int nms_radius, int use_nms,
+                   int thr_mode, float thr, int num_pts, int cap, int32_t *idx, float *coord,
+                   float *score, int32_t *n_sel, int32_t *counts, void *ws, size_t ws_bytes,
+                   void *stream);
+
+/* ------------------------------------------------------------------------
+ * Descriptor sampling.
+ * Replaces: losses/preprocess_utils.py:40-53 sample_feat_by_coord
+ *   (grid_sample bilinear, zeros padding, align_corners=False, then
+ *   F.normalize p=2 dim=1 eps 1e-12 when `normalize`).
+ * fmap: NHWC [b][h][w] with pixel stride cstride, c channels (c <= 1024).
+ * coord: [b][npts][2] normalised (x, y); n_valid: optional device int32
+ *   (rows beyond *n_valid are written as zeros); out: [b][npts][c].
+ * ------------------------------------------------------------------------ */
+int posfeat_sample_desc(const float *fmap, int b, int c, int h, int w, int cstride,
+                        const float *coord, int npts, const int32_t *n_valid, int normalize,
+                        float *out, void *stream);
+
+/* NCHW <-> NHWC helpers used at the API boundary (torch tensors are NCHW). */
+int posfeat_nchw_to_nhwc(const float *x, int n, int c, int h, int w, int cstride_out,
+                         float *y, void *stream);
+int posfeat_nhwc_to_nchw(const float *x, int n, int c, int h, int w, int cstride_in,
+                         float *y, void *stream);
+
+/* ------------------------------------------------------------------------
+ * Whole-model extraction engine.
+ * Replaces: networks/PoSFeat_model.py:91-134 PoSFeat.extract for the
+ *   effective model ResUNet(resnet50, 128/128) + KeypointDet(192, 1,
+ *   'identity', 'Softplus') (configs/train_desc.yaml:16-31), i.e.
+ *   networks/DescNet.py:64-84 and networks/DeteNet.py:102-121.
+ * Weights: one packed fp32 blob; layer i occupies w_off/b_off floats (from
+ *   posfeat_model_conv_spec).  The spec named "head.prelu" holds the shared
+ *   PReLU scalar at b_off.
+ * ------------------------------------------------------------------------ */
+typedef struct posfeat_model posfeat_model;
+
+typedef struct {
+  float *local_map;       /* [b][128][h/4][w/4]  NCHW (may be NULL)        */
+  float *global_map;      /* [b][128][h/16][w/16] NCHW (may be NULL)       */
+  float *global_feat;     /* [b][128]                 (may be NULL)        */
+  float *local_point;     /* [b][1][h][w]                                  */
+  float *local_map_small; /* [b][64][h/4][w/4]  NCHW (may be NULL)         */
+  const float *local_map_nhwc; /* OUT: engine-internal NHWC local_map     */
+  int local_map_cstride;       /* OUT: its pixel stride in floats          */
+} posfeat_extract_out;
+
+int posfeat_model_num_specs(void);
+int posfeat_model_conv_spec(int i, const char **name, int *cout, int *cin, int *kh, int *kw,
+                            long long *w_off, long long *b_off);
+long long posfeat_model_weight_floats(void);
+int posfeat_model_create(int batch, int h, int w, const float *weights, posfeat_model **out);
+size_t posfeat_model_workspace(const posfeat_model *m);
+int posfeat_model_extract(posfeat_model *m, const float *img_nchw, posfeat_extract_out *out,
+                          void *ws, size_t ws_bytes, void *stream);
+/* Optional per-kernel timing: when enabled, extract() records hipEvents
+ * around every launch; posfeat_model_timing() returns the summed ms of the
+ * last call for launches whose label starts with `prefix`. */
+int posfeat_model_set_timing(posfeat_model *m, int enable);
+int posfeat_model_timing(posfeat_model *m, const char *prefix, double *ms, double *flops,
+                         int *launches);
+void posfeat_model_destroy(posfeat_model *m);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* POSFEAT_HIP_H */

@@ -1,0 +1,125 @@
+"""ctypes binding of libposfeat_hip.so (the C ABI in include/posfeat_hip.h).
+
+The library is loaded lazily on first use and NEVER silently replaced: if the
+.so is missing, or no gfx950 device is visible when a GPU op is called, the op
+raises.  There is no CPU fallback in the product path.
+
+``torch`` is imported before the library so that the HIP runtime torch bundles
+(SONAME libamdhip64.so.7) is the one our library binds to -- one runtime per
+process, so torch's caching-allocator pointers and streams are valid here.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the dlopen, see module docstring)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("POSFEAT_HIP_LIB", os.path.join(_HERE, "libposfeat_hip.so"))
+
+_lib = None
+
+c_int, c_float, c_void_p, c_size_t = ctypes.c_int, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t
+c_ll = ctypes.c_longlong
+P_int = ctypes.POINTER(ctypes.c_int)
+
+
+class ConvDesc(ctypes.Structure):
+    _fields_ = [(n, c_int) for n in ("n", "h", "w", "cin", "x_cstride", "cout", "kh", "kw",
+                                     "stride", "pad", "y_cstride", "res_cstride", "act")]
+
+
+class ExtractOut(ctypes.Structure):
+    _fields_ = [("local_map", c_void_p), ("global_map", c_void_p), ("global_feat", c_void_p),
+                ("local_point", c_void_p), ("local_map_small", c_void_p),
+                ("local_map_nhwc", c_void_p), ("local_map_cstride", c_int)]
+
+
+# name -> (restype, argtypes); mirrors include/posfeat_hip.h
+SIGNATURES = {
+    "posfeat_strerror": (ctypes.c_char_p, [c_int]),
+    "posfeat_abi_version": (c_int, []),
+    "posfeat_device_ok": (c_int, []),
+    "posfeat_conv_packed_k": (c_int, [c_int, c_int, c_int]),
+    "posfeat_conv2d_nhwc": (c_int, [ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_void_p,
+                                    c_void_p, c_void_p, c_void_p]),
+    "posfeat_detect_workspace": (c_int, [c_int, c_int, c_int, c_int, ctypes.POINTER(c_size_t)]),
+    "posfeat_detect": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int,
+                               c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                               c_size_t, c_void_p]),
+    "posfeat_sample_desc": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int,
+                                    c_void_p, c_int, c_void_p, c_void_p]),
+    "posfeat_nchw_to_nhwc": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
+                                     c_void_p]),
+    "posfeat_nhwc_to_nchw": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
+                                     c_void_p]),
+    "posfeat_model_num_specs": (c_int, []),
+    "posfeat_model_conv_spec": (c_int, [c_int, ctypes.POINTER(ctypes.c_char_p), P_int, P_int,
+                                        P_int, P_int, ctypes.POINTER(c_ll),
+                                        ctypes.POINTER(c_ll)]),
+    "posfeat_model_weight_floats": (c_ll, []),
+    "posfeat_model_create": (c_int, [c_int, c_int, c_int, c_void_p, ctypes.POINTER(c_void_p)]),
+    "posfeat_model_workspace": (c_size_t, [c_void_p]),
+    "posfeat_model_extract": (c_int, [c_void_p, c_void_p, ctypes.POINTER(ExtractOut), c_void_p,
+                                      c_size_t, c_void_p]),
+    "posfeat_model_set_timing": (c_int, [c_void_p, c_int]),
+    "posfeat_model_timing": (c_int, [c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
+                                     ctypes.POINTER(ctypes.c_double), P_int]),
+    "posfeat_model_destroy": (None, [c_void_p]),
+}
+
+
+def lib():
+    """Load (once) and return the ctypes library; raise if it is missing."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                "libposfeat_hip.so not found at %s -- build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (or make -C "
+                "posfeat_amd/csrc). There is no CPU fallback." % LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(code):
+    if code != 0:
+        raise RuntimeError(lib().posfeat_strerror(code).decode())
+
+
+def require_device(t=None):
+    """Raise unless a gfx950 GPU is visible (and ``t`` lives on it)."""
+    if not torch.cuda.is_available():
+        raise RuntimeError("posfeat_amd: no GPU visible; the HIP path has no CPU fallback")
+    if t is not None and not t.is_cuda:
+        raise RuntimeError("posfeat_amd: tensor must be on the GPU (got %s)" % t.device)
+    if not lib().posfeat_device_ok():
+        raise RuntimeError("posfeat_amd: current device is not gfx950 (MI355X)")
+
+
+def stream_ptr(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def model_specs():
+    """[(name, cout, cin, kh, kw, w_off, b_off)] from the engine's layer table."""
+    L = lib()
+    out = []
+    for i in range(L.posfeat_model_num_specs()):
+        name = ctypes.c_char_p()
+        co, ci, kh, kw = c_int(), c_int(), c_int(), c_int()
+        wo, bo = c_ll(), c_ll()
+        check(L.posfeat_model_conv_spec(i, ctypes.byref(name), ctypes.byref(co), ctypes.byref(ci),
+                                        ctypes.byref(kh), ctypes.byref(kw), ctypes.byref(wo),
+                                        ctypes.byref(bo)))
+        out.append((name.value.decode(), co.value, ci.value, kh.value, kw.value, wo.value,
+                    bo.value))
+    return out

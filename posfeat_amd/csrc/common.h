@@ -1,0 +1,44 @@
+// common.h -- shared helpers for the gfx950 kernels of libposfeat_hip.so
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/posfeat_hip.h"
+
+#define PF_WAVE 64
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+#define PF_CHECK_LAUNCH()                                  \
+  do {                                                     \
+    hipError_t _e = hipGetLastError();                     \
+    if (_e != hipSuccess) return POSFEAT_E_HIP;            \
+  } while (0)
+
+#define PF_TRY(expr)                  \
+  do {                                \
+    int _r = (expr);                  \
+    if (_r != POSFEAT_OK) return _r;  \
+  } while (0)
+
+static inline hipStream_t pf_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
+
+static inline size_t pf_align(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+__device__ __forceinline__ float pf_wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float pf_elu(float x) { return x > 0.f ? x : expm1f(x); }
+
+// torch softplus(beta=1, threshold=20)
+__device__ __forceinline__ float pf_softplus(float x) { return x > 20.f ? x : log1pf(expf(x)); }
+
+// order-preserving uint32 key of a float (+0 == -0)
+__device__ __forceinline__ uint32_t pf_fkey(float v) {
+  uint32_t u = __float_as_uint(v + 0.0f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}

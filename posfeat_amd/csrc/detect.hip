@@ -1,0 +1,325 @@
+// detect.hip -- keypoint selection on the score map (gfx950).
+//
+// Replaces losses/preprocess_utils.py:215-278 generate_kpts_single (stable
+// branch) incl. nms (449-464).  Three launches per call:
+//   K0 (thr 'max'/'mean' only) per-image threshold statistic
+//   K1 det_mask    : reflect-padded NMS with the first-occurrence tie rule,
+//                    threshold, order-preserving uint32 key of the masked
+//                    score, per-image survivor count
+//   K2 det_select  : one workgroup per image -- n = clamp(min count), 4-pass
+//                    8-bit radix select of the n-th largest key in LDS
+//                    histograms, then an ordered (ascending index) ballot
+//                    compaction of the n selected cells
+//   K3 det_rank    : rank each selected cell by (key desc, index asc) with an
+//                    LDS-tiled counting sort (n^2 compares, exact, no
+//                    atomics), compute the 3x3 soft-argmax refine and 3x3 max
+//                    score and scatter to the output row = rank
+// Everything is integer/compare work, so the result is bit-exact and
+// deterministic.
+#include "common.h"
+
+namespace {
+
+__device__ __forceinline__ int reflect_idx(int i, int n) {
+  i = i < 0 ? -i : i;
+  return i >= n ? 2 * (n - 1) - i : i;
+}
+
+// torch.linspace(-1, 1, n)[i] in float32 (ATen's two-sided formula)
+__device__ __forceinline__ float lin_m11(int i, int n) {
+  const float step = __fdiv_rn(2.0f, (float)(n - 1));
+  return i < n / 2 ? __fadd_rn(-1.0f, __fmul_rn(step, (float)i))
+                   : __fsub_rn(1.0f, __fmul_rn(step, (float)(n - 1 - i)));
+}
+
+__global__ void det_thr_kernel(const float* __restrict__ kp, int h, int w, int mode, float thr,
+                               float* __restrict__ tout) {
+  const int b = blockIdx.x;
+  const int Hi = h - 2, Wi = w - 2, P = Hi * Wi;
+  const float* m = kp + (long long)b * h * w;
+  double s = 0.0;
+  float mx = -INFINITY;
+  for (int p = threadIdx.x; p < P; p += blockDim.x) {
+    const int i = p / Wi, j = p - (p / Wi) * Wi;
+    const float v = m[(i + 1) * w + j + 1];
+    s += v;
+    mx = fmaxf(mx, v);
+  }
+  __shared__ double rs[256];
+  __shared__ float rm[256];
+  rs[threadIdx.x] = s;
+  rm[threadIdx.x] = mx;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      rs[threadIdx.x] += rs[threadIdx.x + o];
+      rm[threadIdx.x] = fmaxf(rm[threadIdx.x], rm[threadIdx.x + o]);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float stat = mode == 2 ? rm[0] : (float)(rs[0] / (double)P);
+    tout[b] = __fmul_rn(thr, stat);
+  }
+}
+
+__global__ void det_mask_kernel(const float* __restrict__ kp, int h, int w, int r, int use_nms,
+                                int use_thr, const float* __restrict__ thr_t,
+                                uint32_t* __restrict__ keys, int32_t* __restrict__ counts) {
+  const int b = blockIdx.y;  // one image per grid row: block-uniform counter
+  const int Hi = h - 2, Wi = w - 2, P = Hi * Wi;
+  const int ws = 2 * r + 1, center = r * ws + r;
+  const float* m = kp + (long long)b * h * w;
+  const float t = use_thr ? thr_t[b] : 0.f;
+  int local = 0;
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
+    const int i = p / Wi, j = p - (p / Wi) * Wi;
+    const float S = m[(i + 1) * w + j + 1];
+    bool keep = use_thr ? (S > t) : true;
+    if (keep && use_nms) {
+      int pos = 0;
+      for (int dy = -r; dy <= r && keep; ++dy) {
+        const int yy = reflect_idx(i + dy, Hi) + 1;
+        for (int dx = -r; dx <= r; ++dx, ++pos) {
+          if (pos == center) continue;
+          const float v = m[yy * w + reflect_idx(j + dx, Wi) + 1];
+          if (pos < center ? !(v < S) : !(v <= S)) {
+            keep = false;
+            break;
+          }
+        }
+      }
+    }
+    keys[(long long)b * P + p] = pf_fkey(keep ? S : 0.0f);
+    local += keep ? 1 : 0;
+  }
+  // block reduce, one atomic per block
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) local += __shfl_xor(local, o, 64);
+  __shared__ int wsum[16];
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = local;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int s = 0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) s += wsum[k];
+    if (s) atomicAdd(&counts[b], s);
+  }
+}
+
+// block-wide exclusive scan of per-thread 0/1 flags in ascending thread order
+// (1024 threads = 16 waves).  Returns the exclusive prefix, sets *total.
+__device__ __forceinline__ int block_scan_flag(bool f, int* wsum, int* total) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const unsigned long long bal = __ballot(f);
+  const int pre = __popcll(bal & ((1ull << lane) - 1ull));
+  if (lane == 0) wsum[wv] = __popcll(bal);
+  __syncthreads();
+  int off = 0, tot = 0;
+  const int nw = blockDim.x >> 6;
+  for (int k = 0; k < nw; ++k) {
+    const int v = wsum[k];
+    off += (k < wv) ? v : 0;
+    tot += v;
+  }
+  __syncthreads();
+  *total = tot;
+  return off + pre;
+}
+
+__global__ __launch_bounds__(1024) void det_select_kernel(
+    const uint32_t* __restrict__ keys, int nb, int P, const int32_t* __restrict__ counts,
+    int num_pts, int cap, int32_t* __restrict__ sel, uint32_t* __restrict__ selkey,
+    int32_t* __restrict__ n_sel) {
+  const int b = blockIdx.x;
+  const uint32_t* kb = keys + (long long)b * P;
+  __shared__ int hist[256];
+  __shared__ int wsum[16];
+  __shared__ uint32_t s_prefix;
+  __shared__ int s_krem;
+  __shared__ int s_n;
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    int minc = counts[0];
+    for (int k = 1; k < nb; ++k) minc = min(minc, counts[k]);
+    int n = num_pts > 0 ? min(num_pts, minc) : minc;
+    if (n < 128) n = 128;
+    n = min(n, P);
+    n = min(n, cap);
+    s_n = n;
+    s_krem = n;
+    s_prefix = 0u;
+    if (b == 0) *n_sel = n;
+  }
+  __syncthreads();
+  const int n = s_n;
+  uint32_t pmask = 0u;
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    for (int k = tid; k < 256; k += blockDim.x) hist[k] = 0;
+    __syncthreads();
+    const uint32_t prefix = s_prefix;
+    const uint32_t ZKEY = 0x80000000u;  // key of a masked-out (0.0) cell
+    const bool zmatch = (ZKEY & pmask) == prefix;
+    for (int base = 0; base < P; base += blockDim.x) {
+      const int p = base + tid;
+      const uint32_t k = p < P ? kb[p] : ZKEY ^ 1u;
+      const bool z = p < P && k == ZKEY;
+      const unsigned long long zb = __ballot(z);
+      if (zmatch && (tid & 63) == 0 && zb) atomicAdd(&hist[(ZKEY >> shift) & 0xFF], __popcll(zb));
+      if (p < P && !z && (k & pmask) == prefix) atomicAdd(&hist[(k >> shift) & 0xFF], 1);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int krem = s_krem, above = 0, d = 255;
+      for (; d > 0; --d) {
+        if (above + hist[d] >= krem) break;
+        above += hist[d];
+      }
+      s_krem = krem - above;
+      s_prefix = prefix | ((uint32_t)d << shift);
+    }
+    pmask |= 0xFFu << shift;
+    __syncthreads();
+  }
+  const uint32_t T = s_prefix;
+  const int need_eq = s_krem;  // how many keys == T are taken (>= 1)
+  // ordered compaction: keys > T, plus the first need_eq keys == T by index
+  int eq_seen = 0, taken = 0;
+  for (int base = 0; base < P; base += blockDim.x) {
+    const int p = base + tid;
+    const uint32_t k = p < P ? kb[p] : 0u;
+    const bool gt = p < P && k > T;
+    const bool eq = p < P && k == T;
+    int eq_tot;
+    const int eq_pre = block_scan_flag(eq, wsum, &eq_tot);
+    const bool take = gt || (eq && (eq_seen + eq_pre) < need_eq);
+    int tk_tot;
+    const int tk_pre = block_scan_flag(take, wsum, &tk_tot);
+    if (take) {
+      const int pos = taken + tk_pre;
+      sel[(long long)b * cap + pos] = p;
+      selkey[(long long)b * cap + pos] = k;
+    }
+    eq_seen += eq_tot;
+    taken += tk_tot;
+    if (taken >= n) break;  // uniform across the block
+  }
+}
+
+__global__ void det_rank_kernel(const float* __restrict__ kp, int h, int w, int cap,
+                                const int32_t* __restrict__ sel, const uint32_t* __restrict__ selkey,
+                                const int32_t* __restrict__ n_sel, int32_t* __restrict__ idx_out,
+                                float* __restrict__ coord, float* __restrict__ score) {
+  const int b = blockIdx.y;
+  const int n = *n_sel;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if ((int)(blockIdx.x * blockDim.x) >= n) return;  // block-uniform
+  const bool active = t < n;
+  const uint32_t* kb = selkey + (long long)b * cap;
+  const uint32_t myk = active ? kb[t] : 0u;
+  __shared__ uint32_t tile[1024];
+  int rank = 0;
+  for (int base = 0; base < n; base += 1024) {
+    for (int k = threadIdx.x; k < 1024; k += blockDim.x)
+      tile[k] = (base + k < n) ? kb[base + k] : 0u;
+    __syncthreads();
+    const int lim = min(1024, n - base);
+    if (active) {
+      for (int k = 0; k < lim; ++k) {
+        const uint32_t o = tile[k];
+        rank += (o > myk) || (o == myk && base + k < t);
+      }
+    }
+    __syncthreads();
+  }
+  if (!active) return;
+  const int Wi = w - 2;
+  const int p = sel[(long long)b * cap + t];
+  const int i = p / Wi, j = p - (p / Wi) * Wi;
+  const float* m = kp + (long long)b * h * w;
+  float sx = 0.f, sy = 0.f, sw = 0.f, mx = -INFINITY;
+  for (int dy = 0; dy < 3; ++dy) {
+    const float gy = lin_m11(i + dy, h);
+    for (int dx = 0; dx < 3; ++dx) {
+      const float v = m[(i + dy) * w + j + dx];
+      const float gx = lin_m11(j + dx, w);
+      sx = __fadd_rn(sx, __fmul_rn(v, gx));
+      sy = __fadd_rn(sy, __fmul_rn(v, gy));
+      sw = __fadd_rn(sw, v);
+      mx = fmaxf(mx, v);
+    }
+  }
+  const float aw = __fdiv_rn(sw, 9.0f);
+  const long long o = (long long)b * cap + rank;
+  idx_out[o] = p;
+  coord[o * 2 + 0] = __fdiv_rn(__fdiv_rn(sx, 9.0f), aw);
+  coord[o * 2 + 1] = __fdiv_rn(__fdiv_rn(sy, 9.0f), aw);
+  score[o] = mx;
+}
+
+}  // namespace
+
+extern "C" int posfeat_detect_workspace(int b, int h, int w, int cap, size_t* bytes) {
+  if (b <= 0 || h < 3 || w < 3 || cap <= 0 || !bytes) return POSFEAT_E_INVALID;
+  const size_t P = (size_t)(h - 2) * (w - 2);
+  size_t s = pf_align((size_t)b * P * sizeof(uint32_t), 256);    // keys
+  s += pf_align((size_t)b * cap * sizeof(int32_t), 256);         // sel
+  s += pf_align((size_t)b * cap * sizeof(uint32_t), 256);        // selkey
+  s += pf_align((size_t)b * sizeof(float), 256);                 // thr
+  *bytes = s;
+  return POSFEAT_OK;
+}
+
+extern "C" int posfeat_detect(const float* kp_map, int b, int h, int w, int nms_radius,
+                              int use_nms, int thr_mode, float thr, int num_pts, int cap,
+                              int32_t* idx, float* coord, float* score, int32_t* n_sel,
+                              int32_t* counts, void* ws, size_t ws_bytes, void* stream) {
+  if (!kp_map || !idx || !coord || !score || !n_sel || !counts || !ws) return POSFEAT_E_INVALID;
+  if (b <= 0 || h < 3 || w < 3 || nms_radius < 0 || thr_mode < 0 || thr_mode > 3)
+    return POSFEAT_E_INVALID;
+  const int Hi = h - 2, Wi = w - 2, P = Hi * Wi;
+  if (use_nms && (nms_radius >= Hi || nms_radius >= Wi)) return POSFEAT_E_INVALID;  // reflect pad limit
+  const int need = num_pts > 0 ? (num_pts < 128 ? 128 : num_pts) : P;
+  if (cap < (need < P ? need : P)) return POSFEAT_E_INVALID;
+  size_t need_ws = 0;
+  posfeat_detect_workspace(b, h, w, cap, &need_ws);
+  if (ws_bytes < need_ws) return POSFEAT_E_WORKSPACE;
+  hipStream_t st = pf_stream(stream);
+  char* base = static_cast<char*>(ws);
+  uint32_t* keys = reinterpret_cast<uint32_t*>(base);
+  base += pf_align((size_t)b * P * sizeof(uint32_t), 256);
+  int32_t* sel = reinterpret_cast<int32_t*>(base);
+  base += pf_align((size_t)b * cap * sizeof(int32_t), 256);
+  uint32_t* selkey = reinterpret_cast<uint32_t*>(base);
+  base += pf_align((size_t)b * cap * sizeof(uint32_t), 256);
+  float* thr_t = reinterpret_cast<float*>(base);
+
+  if (hipMemsetAsync(counts, 0, sizeof(int32_t) * b, st) != hipSuccess) return POSFEAT_E_HIP;
+  const int use_thr = thr_mode != 0;
+  if (thr_mode == 1) {
+    // 'abs': thr * tensor(1.)  (preprocess_utils.py:237-239)
+    float t[64];
+    if (b > 64) return POSFEAT_E_INVALID;
+    for (int k = 0; k < b; ++k) t[k] = thr * 1.0f;
+    if (hipMemcpyAsync(thr_t, t, sizeof(float) * b, hipMemcpyHostToDevice, st) != hipSuccess)
+      return POSFEAT_E_HIP;
+  } else if (thr_mode >= 2) {
+    hipLaunchKernelGGL(det_thr_kernel, dim3(b), dim3(256), 0, st, kp_map, h, w, thr_mode, thr,
+                       thr_t);
+    PF_CHECK_LAUNCH();
+  }
+  {
+    int g = (P + 255) / 256;
+    if (g > 2048) g = 2048;
+    hipLaunchKernelGGL(det_mask_kernel, dim3(g, b), dim3(256), 0, st, kp_map, h, w, nms_radius,
+                       use_nms, use_thr, thr_t, keys, counts);
+    PF_CHECK_LAUNCH();
+  }
+  hipLaunchKernelGGL(det_select_kernel, dim3(b), dim3(1024), 0, st, keys, b, P, counts, num_pts,
+                     cap, sel, selkey, n_sel);
+  PF_CHECK_LAUNCH();
+  const int maxn = cap < P ? cap : P;
+  hipLaunchKernelGGL(det_rank_kernel, dim3((maxn + 255) / 256, b), dim3(256), 0, st, kp_map, h, w,
+                     cap, sel, selkey, n_sel, idx, coord, score);
+  PF_CHECK_LAUNCH();
+  return POSFEAT_OK;
+}

@@ -1,0 +1,432 @@
+// engine.hip -- whole-model extraction engine: PoSFeat.extract on gfx950.
+//
+// Replaces networks/PoSFeat_model.py:91-134 (PoSFeat.extract) for the
+// effective extraction model (configs/train_desc.yaml:16-31):
+//   ResUNet(resnet50, coarse 128, fine 128)   networks/DescNet.py:12-84
+//   KeypointDet(192, 1, 'identity', 'Softplus') networks/DeteNet.py:9-121
+// The host side only sequences launches on the caller's stream; every byte of
+// arithmetic is in the gfx950 kernels (conv.hip, fmap.hip).  Activations live
+// in one caller-provided workspace, NHWC fp32, with concat buffers laid out
+// so each producer writes straight into its channel slice:
+//   headcat [b][h/4][w/4][192] = [local_map(128) | local_map_small(64)]
+//   cat2    [b][h/4][w/4][512] = [upconv2 out(256) | layer1 out(256)]
+//   cat3    [b][h/8][w/8][1024]= [upconv3 out(512) | layer2 out(512)]
+//   hcat    [b][h][w][256]     = [up4(PReLU(IN(conv1)))(192) | IN(convimg)(64)]
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "fmap.h"
+
+int pf_sample_desc(const float* fmap, int b, int c, int h, int w, int cs, const float* coord,
+                   int npts, const int32_t* n_valid, int normalize, float* out, hipStream_t st);
+
+namespace {
+
+struct Spec {
+  std::string name;
+  int cout, cin, kh, kw;
+  long long w_off, b_off;
+};
+
+struct SpecTable {
+  std::vector<Spec> v;
+  long long total = 0;
+  SpecTable() {
+    auto add = [&](const std::string& n, int co, int ci, int k) {
+      Spec s{n, co, ci, k, k, 0, 0};
+      const int kpad = posfeat_conv_packed_k(ci, k, k);
+      s.w_off = total;
+      total += ((long long)co * kpad + 63) / 64 * 64;
+      s.b_off = total;
+      total += (co + 63) / 64 * 64;
+      v.push_back(s);
+    };
+    add("firstconv", 64, 3, 7);
+    const int planes[3] = {64, 128, 256}, blocks[3] = {3, 4, 6};
+    int inpl = 64;
+    for (int l = 0; l < 3; ++l) {
+      for (int bi = 0; bi < blocks[l]; ++bi) {
+        const std::string p = "layer" + std::to_string(l + 1) + "." + std::to_string(bi);
+        add(p + ".conv1", planes[l], inpl, 1);
+        add(p + ".conv2", planes[l], planes[l], 3);
+        add(p + ".conv3", planes[l] * 4, planes[l], 1);
+        if (bi == 0) add(p + ".downsample", planes[l] * 4, inpl, 1);
+        inpl = planes[l] * 4;
+      }
+    }
+    add("conv_coarse", 128, 1024, 1);
+    add("upconv3.conv", 512, 1024, 3);
+    add("iconv3", 512, 1024, 3);
+    add("upconv2.conv", 256, 512, 3);
+    add("iconv2", 256, 512, 3);
+    add("conv_fine", 128, 256, 1);
+    add("head.conv1", 192, 192, 3);
+    add("head.convimg", 64, 3, 3);
+    add("head.conv2", 128, 256, 3);
+    add("head.conv3", 1, 128, 1);
+    Spec pr{"head.prelu", 1, 0, 0, 0, total, total};
+    total += 64;
+    v.push_back(pr);
+  }
+  const Spec* find(const std::string& n) const {
+    for (auto& s : v)
+      if (s.name == n) return &s;
+    return nullptr;
+  }
+};
+
+const SpecTable& specs() {
+  static SpecTable t;
+  return t;
+}
+
+struct Buf {
+  size_t off = 0, floats = 0;
+};
+
+}  // namespace
+
+struct posfeat_model {
+  int B, H, W;
+  const float* wts;
+  // layout
+  size_t ws_bytes = 0;
+  Buf img4, stem, headcat, t1, t2, ds, oa, ob, cat2, cat3, l3out, gmap, up3, d3, up2, d2;
+  Buf c1raw, hcat, c2raw, yraw;
+  Buf st_mean, st_rstd, st_part;  // instance-norm scratch (floats / doubles)
+  Buf st_mean1, st_rstd1;
+  // timing
+  bool timing = false;
+  struct Ev {
+    std::string label;
+    double flops;
+    hipEvent_t a, b;
+  };
+  std::vector<Ev> evs;
+  size_t ev_used = 0;
+};
+
+namespace {
+
+struct Ctx {
+  posfeat_model* m;
+  char* ws;
+  hipStream_t st;
+  float* f(const Buf& b) const { return reinterpret_cast<float*>(ws + b.off); }
+  double* d(const Buf& b) const { return reinterpret_cast<double*>(ws + b.off); }
+  const float* W(const std::string& n) const { return m->wts + specs().find(n)->w_off; }
+  const float* Bi(const std::string& n) const { return m->wts + specs().find(n)->b_off; }
+};
+
+// record-and-run helper for optional per-launch timing
+template <class F>
+int timed(Ctx& c, const std::string& label, double flops, F&& fn) {
+  posfeat_model* m = c.m;
+  if (!m->timing) return fn();
+  if (m->ev_used == m->evs.size()) {
+    posfeat_model::Ev e;
+    if (hipEventCreate(&e.a) != hipSuccess || hipEventCreate(&e.b) != hipSuccess)
+      return POSFEAT_E_HIP;
+    m->evs.push_back(e);
+  }
+  auto& e = m->evs[m->ev_used++];
+  e.label = label;
+  e.flops = flops;
+  if (hipEventRecord(e.a, c.st) != hipSuccess) return POSFEAT_E_HIP;
+  const int r = fn();
+  if (hipEventRecord(e.b, c.st) != hipSuccess) return POSFEAT_E_HIP;
+  return r;
+}
+
+int conv(Ctx& c, const std::string& name, const float* x, int n, int h, int w, int xcs, float* y,
+         int ycs, int stride, int act, const float* res = nullptr, int rcs = 0) {
+  const Spec* s = specs().find(name);
+  if (!s) return POSFEAT_E_INVALID;
+  posfeat_conv_desc d;
+  d.n = n;
+  d.h = h;
+  d.w = w;
+  d.cin = (s->cin + 3) / 4 * 4;
+  d.x_cstride = xcs;
+  d.cout = s->cout;
+  d.kh = s->kh;
+  d.kw = s->kw;
+  d.stride = stride;
+  d.pad = (s->kh - 1) / 2;
+  d.y_cstride = ycs;
+  d.res_cstride = rcs;
+  d.act = act;
+  const int oh = (h + 2 * d.pad - d.kh) / stride + 1, ow = (w + 2 * d.pad - d.kw) / stride + 1;
+  const double flops = 2.0 * n * oh * ow * (double)s->cout * s->cin * s->kh * s->kw;
+  return timed(c, "conv:" + name, flops, [&] {
+    return posfeat_conv2d_nhwc(&d, x, c.W(name), c.Bi(name), res, y, c.st);
+  });
+}
+
+void plan(posfeat_model* m) {
+  size_t cur = 0;
+  auto alloc = [&](Buf& b, size_t floats, size_t elem = 4) {
+    b.off = cur;
+    b.floats = floats;
+    cur += pf_align(floats * elem, 256);
+  };
+  const size_t B = m->B, H = m->H, W = m->W;
+  const size_t h2 = H / 2, w2 = W / 2, h4 = H / 4, w4 = W / 4, h8 = H / 8, w8 = W / 8,
+               h16 = H / 16, w16 = W / 16;
+  alloc(m->img4, B * H * W * 4);
+  alloc(m->stem, B * h2 * w2 * 64);
+  alloc(m->headcat, B * h4 * w4 * 192);
+  alloc(m->t1, B * h4 * w4 * 256);
+  alloc(m->t2, B * h4 * w4 * 256);
+  alloc(m->ds, B * h4 * w4 * 256);
+  alloc(m->oa, B * h4 * w4 * 256);
+  alloc(m->ob, B * h4 * w4 * 256);
+  alloc(m->cat2, B * h4 * w4 * 512);
+  alloc(m->cat3, B * h8 * w8 * 1024);
+  alloc(m->l3out, B * h16 * w16 * 1024);
+  alloc(m->gmap, B * h16 * w16 * 128);
+  alloc(m->up3, B * h8 * w8 * 1024);
+  alloc(m->d3, B * h8 * w8 * 512);
+  alloc(m->up2, B * h4 * w4 * 512);
+  alloc(m->d2, B * h4 * w4 * 256);
+  alloc(m->c1raw, B * h4 * w4 * 192);
+  alloc(m->hcat, B * H * W * 256);
+  alloc(m->c2raw, B * H * W * 128);
+  alloc(m->yraw, B * H * W);
+  alloc(m->st_mean, B * 256);
+  alloc(m->st_rstd, B * 256);
+  alloc(m->st_mean1, B * 4);
+  alloc(m->st_rstd1, B * 4);
+  const size_t part = pf_in_stats_ws_bytes((int)B, (int)(H * W), 256);
+  alloc(m->st_part, part / 4 + 1);
+  m->ws_bytes = cur;
+}
+
+// torchvision Bottleneck at (n, h, w): in -> out (out may be a concat slice)
+int bottleneck(Ctx& c, const std::string& p, const float* in, int n, int h, int w, int ics,
+               int planes, int stride, bool has_ds, float* out, int ocs) {
+  posfeat_model* m = c.m;
+  const int oh = (h - 1) / stride + 1, ow = (w - 1) / stride + 1;
+  float* t1 = c.f(m->t1);
+  float* t2 = c.f(m->t2);
+  PF_TRY(conv(c, p + ".conv1", in, n, h, w, ics, t1, planes, 1, POSFEAT_ACT_RELU));
+  PF_TRY(conv(c, p + ".conv2", t1, n, h, w, planes, t2, planes, stride, POSFEAT_ACT_RELU));
+  const float* res = in;
+  int rcs = ics;
+  if (has_ds) {
+    float* ds = c.f(m->ds);
+    PF_TRY(conv(c, p + ".downsample", in, n, h, w, ics, ds, planes * 4, stride, POSFEAT_ACT_NONE));
+    res = ds;
+    rcs = planes * 4;
+  }
+  PF_TRY(conv(c, p + ".conv3", t2, n, oh, ow, planes, out, ocs, 1, POSFEAT_ACT_RELU, res, rcs));
+  return POSFEAT_OK;
+}
+
+int run_layer(Ctx& c, int li, const float* in, int n, int h, int w, int ics, float* out, int ocs) {
+  posfeat_model* m = c.m;
+  const int planes[3] = {64, 128, 256}, blocks[3] = {3, 4, 6};
+  const int stride = li == 0 ? 1 : 2;
+  const int pl = planes[li];
+  const int oh = (h - 1) / stride + 1, ow = (w - 1) / stride + 1;
+  const float* x = in;
+  int xcs = ics;
+  int ch = h, cw = w;
+  for (int bi = 0; bi < blocks[li]; ++bi) {
+    const std::string p = "layer" + std::to_string(li + 1) + "." + std::to_string(bi);
+    const bool last = bi == blocks[li] - 1;
+    float* dst = last ? out : ((bi & 1) ? c.f(m->ob) : c.f(m->oa));
+    const int dcs = last ? ocs : pl * 4;
+    PF_TRY(bottleneck(c, p, x, n, ch, cw, xcs, pl, bi == 0 ? stride : 1, bi == 0, dst, dcs));
+    x = dst;
+    xcs = dcs;
+    ch = oh;
+    cw = ow;
+  }
+  return POSFEAT_OK;
+}
+
+int forward(Ctx& c, const float* img, posfeat_extract_out* out) {
+  posfeat_model* m = c.m;
+  const int B = m->B, H = m->H, W = m->W;
+  const int h2 = H / 2, w2 = W / 2, h4 = H / 4, w4 = W / 4, h8 = H / 8, w8 = W / 8, h16 = H / 16,
+            w16 = W / 16;
+  const float* slope = m->wts + specs().find("head.prelu")->b_off;
+  float* img4 = c.f(m->img4);
+  // ---- ResUNet (DescNet.py:64-84) -----------------------------------------
+  PF_TRY(timed(c, "layout:img", 0, [&] { return pf_nchw_to_nhwc(img, B, 3, H, W, 4, img4, c.st); }));
+  PF_TRY(conv(c, "firstconv", img4, B, H, W, 4, c.f(m->stem), 64, 2, POSFEAT_ACT_RELU));
+  float* headcat = c.f(m->headcat);
+  PF_TRY(timed(c, "maxpool", 0, [&] {
+    return pf_maxpool3s2(c.f(m->stem), B, h2, w2, 64, 64, headcat + 128, 192, c.st);
+  }));
+  float* cat2 = c.f(m->cat2);
+  float* cat3 = c.f(m->cat3);
+  PF_TRY(run_layer(c, 0, headcat + 128, B, h4, w4, 192, cat2 + 256, 512));  // layer1 -> cat2[256:]
+  PF_TRY(run_layer(c, 1, cat2 + 256, B, h4, w4, 512, cat3 + 512, 1024));    // layer2 -> cat3[512:]
+  PF_TRY(run_layer(c, 2, cat3 + 512, B, h8, w8, 1024, c.f(m->l3out), 1024));
+  PF_TRY(conv(c, "conv_coarse", c.f(m->l3out), B, h16, w16, 1024, c.f(m->gmap), 128, 1,
+              POSFEAT_ACT_ELU));
+  PF_TRY(timed(c, "upsample2x", 0, [&] {
+    return pf_upsample2x_ac(c.f(m->l3out), B, h16, w16, 1024, 1024, c.f(m->up3), 1024, c.st);
+  }));
+  PF_TRY(conv(c, "upconv3.conv", c.f(m->up3), B, h8, w8, 1024, cat3, 1024, 1, POSFEAT_ACT_ELU));
+  PF_TRY(conv(c, "iconv3", cat3, B, h8, w8, 1024, c.f(m->d3), 512, 1, POSFEAT_ACT_ELU));
+  PF_TRY(timed(c, "upsample2x", 0, [&] {
+    return pf_upsample2x_ac(c.f(m->d3), B, h8, w8, 512, 512, c.f(m->up2), 512, c.st);
+  }));
+  PF_TRY(conv(c, "upconv2.conv", c.f(m->up2), B, h4, w4, 512, cat2, 512, 1, POSFEAT_ACT_ELU));
+  PF_TRY(conv(c, "iconv2", cat2, B, h4, w4, 512, c.f(m->d2), 256, 1, POSFEAT_ACT_ELU));
+  PF_TRY(conv(c, "conv_fine", c.f(m->d2), B, h4, w4, 256, headcat, 192, 1, POSFEAT_ACT_ELU));
+  // ---- KeypointDet (DeteNet.py:102-121), identity prior == exact 1.0 -------
+  float* mean = c.f(m->st_mean);
+  float* rstd = c.f(m->st_rstd);
+  double* part = c.d(m->st_part);
+  float* c1 = c.f(m->c1raw);
+  float* hcat = c.f(m->hcat);
+  PF_TRY(conv(c, "head.conv1", headcat, B, h4, w4, 192, c1, 192, 1, POSFEAT_ACT_NONE));
+  PF_TRY(timed(c, "instnorm", 0, [&] { return pf_in_stats(c1, B, h4 * w4, 192, 192, mean, rstd, part, c.st); }));
+  PF_TRY(timed(c, "norm_prelu_up4", 0, [&] {
+    return pf_norm_prelu_upsample(c1, B, h4, w4, 192, 192, mean, rstd, slope, H, W, hcat, 256, c.st);
+  }));
+  PF_TRY(conv(c, "head.convimg", img4, B, H, W, 4, hcat + 192, 256, 1, POSFEAT_ACT_NONE));
+  PF_TRY(timed(c, "instnorm", 0, [&] {
+    return pf_in_stats(hcat + 192, B, H * W, 64, 256, mean, rstd, part, c.st);
+  }));
+  PF_TRY(timed(c, "instnorm_apply", 0, [&] {
+    return pf_in_apply(hcat + 192, B, H * W, 64, 256, mean, rstd, nullptr, c.st);
+  }));
+  float* c2 = c.f(m->c2raw);
+  PF_TRY(conv(c, "head.conv2", hcat, B, H, W, 256, c2, 128, 1, POSFEAT_ACT_NONE));
+  PF_TRY(timed(c, "instnorm", 0, [&] { return pf_in_stats(c2, B, H * W, 128, 128, mean, rstd, part, c.st); }));
+  PF_TRY(timed(c, "head_tail", 2.0 * B * H * W * 128, [&] {
+    return pf_head_tail(c2, B, H * W, 128, mean, rstd, slope, c.W("head.conv3"),
+                        c.Bi("head.conv3"), c.f(m->yraw), out->local_point, c.f(m->st_mean1),
+                        c.f(m->st_rstd1), part, c.st);
+  }));
+  // ---- outputs -------------------------------------------------------------
+  if (out->global_feat)
+    PF_TRY(timed(c, "global_feat", 0, [&] { return pf_global_feat(c.f(m->gmap), B, h16 * w16, 128, out->global_feat, c.st); }));
+  if (out->local_map)
+    PF_TRY(timed(c, "layout:out", 0, [&] { return pf_nhwc_to_nchw(headcat, B, 128, h4, w4, 192, out->local_map, c.st); }));
+  if (out->local_map_small)
+    PF_TRY(timed(c, "layout:out", 0, [&] {
+      return pf_nhwc_to_nchw(headcat + 128, B, 64, h4, w4, 192, out->local_map_small, c.st);
+    }));
+  if (out->global_map)
+    PF_TRY(timed(c, "layout:out", 0, [&] { return pf_nhwc_to_nchw(c.f(m->gmap), B, 128, h16, w16, 128, out->global_map, c.st); }));
+  out->local_map_nhwc = headcat;
+  out->local_map_cstride = 192;
+  return POSFEAT_OK;
+}
+
+}  // namespace
+
+extern "C" int posfeat_model_num_specs(void) { return (int)specs().v.size(); }
+
+extern "C" int posfeat_model_conv_spec(int i, const char** name, int* cout, int* cin, int* kh,
+                                       int* kw, long long* w_off, long long* b_off) {
+  const auto& v = specs().v;
+  if (i < 0 || i >= (int)v.size()) return POSFEAT_E_INVALID;
+  const Spec& s = v[i];
+  if (name) *name = s.name.c_str();
+  if (cout) *cout = s.cout;
+  if (cin) *cin = s.cin;
+  if (kh) *kh = s.kh;
+  if (kw) *kw = s.kw;
+  if (w_off) *w_off = s.w_off;
+  if (b_off) *b_off = s.b_off;
+  return POSFEAT_OK;
+}
+
+extern "C" long long posfeat_model_weight_floats(void) { return specs().total; }
+
+extern "C" int posfeat_model_create(int batch, int h, int w, const float* weights,
+                                    posfeat_model** out) {
+  if (!out || !weights || batch <= 0 || h < 16 || w < 16 || h % 16 || w % 16)
+    return POSFEAT_E_INVALID;
+  posfeat_model* m = new (std::nothrow) posfeat_model();
+  if (!m) return POSFEAT_E_INVALID;
+  m->B = batch;
+  m->H = h;
+  m->W = w;
+  m->wts = weights;
+  plan(m);
+  *out = m;
+  return POSFEAT_OK;
+}
+
+extern "C" size_t posfeat_model_workspace(const posfeat_model* m) { return m ? m->ws_bytes : 0; }
+
+extern "C" int posfeat_model_extract(posfeat_model* m, const float* img_nchw,
+                                     posfeat_extract_out* out, void* ws, size_t ws_bytes,
+                                     void* stream) {
+  if (!m || !img_nchw || !out || !out->local_point || !ws) return POSFEAT_E_INVALID;
+  if (ws_bytes < m->ws_bytes) return POSFEAT_E_WORKSPACE;
+  if (reinterpret_cast<uintptr_t>(ws) & 255) return POSFEAT_E_INVALID;
+  Ctx c{m, static_cast<char*>(ws), pf_stream(stream)};
+  m->ev_used = 0;
+  return forward(c, img_nchw, out);
+}
+
+extern "C" int posfeat_model_set_timing(posfeat_model* m, int enable) {
+  if (!m) return POSFEAT_E_INVALID;
+  m->timing = enable != 0;
+  return POSFEAT_OK;
+}
+
+extern "C" int posfeat_model_timing(posfeat_model* m, const char* prefix, double* ms,
+                                    double* flops, int* launches) {
+  if (!m || !prefix) return POSFEAT_E_INVALID;
+  double t = 0, f = 0;
+  int k = 0;
+  const size_t pl = strlen(prefix);
+  for (size_t i = 0; i < m->ev_used; ++i) {
+    auto& e = m->evs[i];
+    if (e.label.compare(0, pl, prefix) != 0) continue;
+    if (hipEventSynchronize(e.b) != hipSuccess) return POSFEAT_E_HIP;
+    float dt = 0.f;
+    if (hipEventElapsedTime(&dt, e.a, e.b) != hipSuccess) return POSFEAT_E_HIP;
+    t += dt;
+    f += e.flops;
+    ++k;
+  }
+  if (ms) *ms = t;
+  if (flops) *flops = f;
+  if (launches) *launches = k;
+  return POSFEAT_OK;
+}
+
+extern "C" void posfeat_model_destroy(posfeat_model* m) {
+  if (!m) return;
+  for (auto& e : m->evs) {
+    (void)hipEventDestroy(e.a);
+    (void)hipEventDestroy(e.b);
+  }
+  delete m;
+}
+
+extern "C" const char* posfeat_strerror(int code) {
+  switch (code) {
+    case POSFEAT_OK: return "ok";
+    case POSFEAT_E_INVALID: return "posfeat: invalid argument or unsupported shape";
+    case POSFEAT_E_HIP: return "posfeat: HIP runtime error";
+    case POSFEAT_E_WORKSPACE: return "posfeat: workspace too small";
+    case POSFEAT_E_UNSUPPORTED: return "posfeat: unsupported option";
+    default: return "posfeat: unknown error";
+  }
+}
+
+extern "C" int posfeat_abi_version(void) { return 1; }
+
+extern "C" int posfeat_device_ok(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return 0;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  hipDeviceProp_t p;
+  if (hipGetDeviceProperties(&p, dev) != hipSuccess) return 0;
+  return strncmp(p.gcnArchName, "gfx950", 6) == 0 ? 1 : 0;
+}

@@ -1,0 +1,23 @@
+// fmap.h -- internal (non-ABI) launchers shared by the engine.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+
+int pf_nchw_to_nhwc(const float* x, int n, int c, int h, int w, int cso, float* y, hipStream_t st);
+int pf_nhwc_to_nchw(const float* x, int n, int c, int h, int w, int csi, float* y, hipStream_t st);
+int pf_maxpool3s2(const float* x, int n, int h, int w, int c, int csi, float* y, int cso,
+                  hipStream_t st);
+int pf_upsample2x_ac(const float* x, int n, int h, int w, int c, int csi, float* y, int cso,
+                     hipStream_t st);
+size_t pf_in_stats_ws_bytes(int n, int hw, int C);
+int pf_in_stats(const float* x, int n, int hw, int C, int cs, float* mean, float* rstd,
+                double* part, hipStream_t st);
+int pf_in_apply(float* x, int n, int hw, int C, int cs, const float* mean, const float* rstd,
+                const float* prelu_slope, hipStream_t st);
+int pf_norm_prelu_upsample(const float* x, int n, int h, int w, int C, int csi, const float* mean,
+                           const float* rstd, const float* slope, int OH, int OW, float* y,
+                           int cso, hipStream_t st);
+int pf_head_tail(const float* x, int n, int hw, int cs, const float* mean, const float* rstd,
+                 const float* slope, const float* w3, const float* b3, float* yraw, float* out,
+                 float* mean1, float* rstd1, double* part, hipStream_t st);
+int pf_global_feat(const float* g, int n, int hw, int cs, float* out, hipStream_t st);

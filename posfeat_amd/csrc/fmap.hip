@@ -1,0 +1,474 @@
+// fmap.hip -- memory-bound feature-map kernels of the extraction path (gfx950).
+//
+//   layout      NCHW <-> NHWC (API boundary; torch tensors are NCHW)
+//   maxpool     ResNet stem max_pool2d(3, 2, 1)             (DescNet.py:66 via torchvision)
+//   upsample2x  bilinear x2, align_corners=True            (DescNet.py:189)
+//   instance norm stats / apply (+PReLU)                   (DeteNet.py:12-22, 108-113)
+//   norm_prelu_upsample  IN+PReLU then bilinear to image size, align_corners=False
+//                                                          (DeteNet.py:108-109)
+//   head tail   conv3 1x1 on PReLU(IN(conv2)) + IN + Softplus (DeteNet.py:112-113)
+//   global_feat F.normalize(global_map).mean([2,3])        (PoSFeat_model.py:115-117)
+//
+// All are HBM/L2-bound; feature maps are NHWC with a pixel stride so a
+// producer can write straight into a channel slice of a concat buffer.
+#include "common.h"
+#include "fmap.h"
+
+namespace {
+
+// ---------------------------------------------------------------- layout
+__global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, int n, int c, int hw, int cso,
+                                    float* __restrict__ y) {
+  const long long total = (long long)n * hw * cso;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int ch = (int)(i % cso);
+    const long long p = i / cso;
+    const int b = (int)(p / hw);
+    const int pix = (int)(p - (long long)b * hw);
+    y[i] = ch < c ? x[((long long)b * c + ch) * hw + pix] : 0.f;
+  }
+}
+
+// 64 pixels x 64 channels tile through LDS.
+__global__ void nhwc_to_nchw_kernel(const float* __restrict__ x, int c, int hw, int csi,
+                                    float* __restrict__ y) {
+  __shared__ float t[64][65];
+  const int b = blockIdx.z;
+  const int p0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 256 threads: ty 0..3
+  for (int r = ty; r < 64; r += 4) {
+    const int p = p0 + r, ch = c0 + tx;
+    t[r][tx] = (p < hw && ch < c) ? x[((long long)b * hw + p) * csi + ch] : 0.f;
+  }
+  __syncthreads();
+  for (int r = ty; r < 64; r += 4) {
+    const int ch = c0 + r, p = p0 + tx;
+    if (ch < c && p < hw) y[((long long)b * c + ch) * hw + p] = t[tx][r];
+  }
+}
+
+// ---------------------------------------------------------------- maxpool 3x3 s2 p1
+__global__ void maxpool3s2_kernel(const float* __restrict__ x, int n, int h, int w, int c4,
+                                  int csi, int oh, int ow, int cso, float* __restrict__ y) {
+  const long long total = (long long)n * oh * ow * c4;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int q = (int)(i % c4);
+    long long p = i / c4;
+    const int ox = (int)(p % ow);
+    p /= ow;
+    const int oy = (int)(p % oh);
+    const int b = (int)(p / oh);
+    f32x4 m = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    for (int dy = -1; dy <= 1; ++dy) {
+      const int iy = 2 * oy + dy;
+      if ((unsigned)iy >= (unsigned)h) continue;
+      for (int dx = -1; dx <= 1; ++dx) {
+        const int ix = 2 * ox + dx;
+        if ((unsigned)ix >= (unsigned)w) continue;
+        const f32x4 v =
+            *reinterpret_cast<const f32x4*>(x + (((long long)b * h + iy) * w + ix) * csi + q * 4);
+        m.x = fmaxf(m.x, v.x);
+        m.y = fmaxf(m.y, v.y);
+        m.z = fmaxf(m.z, v.z);
+        m.w = fmaxf(m.w, v.w);
+      }
+    }
+    *reinterpret_cast<f32x4*>(y + (((long long)b * oh + oy) * ow + ox) * cso + q * 4) = m;
+  }
+}
+
+// ---------------------------------------------------------------- bilinear x2, align_corners=True
+__global__ void upsample2x_ac_kernel(const float* __restrict__ x, int n, int h, int w, int c4,
+                                     int csi, float* __restrict__ y, int cso) {
+  const int oh = 2 * h, ow = 2 * w;
+  const float sh = oh > 1 ? (float)(h - 1) / (float)(oh - 1) : 0.f;
+  const float sw = ow > 1 ? (float)(w - 1) / (float)(ow - 1) : 0.f;
+  const long long total = (long long)n * oh * ow * c4;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int q = (int)(i % c4);
+    long long p = i / c4;
+    const int ox = (int)(p % ow);
+    p /= ow;
+    const int oy = (int)(p % oh);
+    const int b = (int)(p / oh);
+    const float ry = sh * oy, rx = sw * ox;
+    const int y0 = (int)ry, x0 = (int)rx;
+    const int y1 = y0 + (y0 < h - 1 ? 1 : 0), x1 = x0 + (x0 < w - 1 ? 1 : 0);
+    const float ly = ry - y0, lx = rx - x0, hy = 1.f - ly, hx = 1.f - lx;
+    const float* base = x + (long long)b * h * w * csi + q * 4;
+    const f32x4 v00 = *reinterpret_cast<const f32x4*>(base + ((long long)y0 * w + x0) * csi);
+    const f32x4 v01 = *reinterpret_cast<const f32x4*>(base + ((long long)y0 * w + x1) * csi);
+    const f32x4 v10 = *reinterpret_cast<const f32x4*>(base + ((long long)y1 * w + x0) * csi);
+    const f32x4 v11 = *reinterpret_cast<const f32x4*>(base + ((long long)y1 * w + x1) * csi);
+    const f32x4 o = hy * (hx * v00 + lx * v01) + ly * (hx * v10 + lx * v11);
+    *reinterpret_cast<f32x4*>(y + (((long long)b * oh + oy) * ow + ox) * cso + q * 4) = o;
+  }
+}
+
+// ---------------------------------------------------------------- instance norm statistics
+// Partial shifted sums: block (chunk, b) covers `chunk_px` pixels of image b for
+// all C channels (C % 4 == 0).  shift = value at pixel 0 (keeps sum-of-squares
+// well conditioned).  part[b][chunk][c] = {sum(x-s), sum((x-s)^2)} as double.
+__global__ void in_partial_kernel(const float* __restrict__ x, int hw, int C, int cs,
+                                  int chunk_px, double* __restrict__ part) {
+  const int b = blockIdx.y, chunk = blockIdx.x, nchunk = gridDim.x;
+  const int c4n = C / 4;
+  const int tid = threadIdx.x;
+  const int rows = blockDim.x / c4n;  // pixel lanes
+  const int q = tid % c4n, pl = tid / c4n;
+  const float* xb = x + (long long)b * hw * cs;
+  f32x4 s1 = {0, 0, 0, 0}, s2 = {0, 0, 0, 0};
+  f32x4 sh = {0, 0, 0, 0};
+  if (pl < rows) {
+    sh = *reinterpret_cast<const f32x4*>(xb + q * 4);
+    const int p0 = chunk * chunk_px, p1 = min(hw, p0 + chunk_px);
+    for (int p = p0 + pl; p < p1; p += rows) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(xb + (long long)p * cs + q * 4) - sh;
+      s1 += v;
+      s2 += v * v;
+    }
+  }
+  // reduce over pixel lanes in a fixed order through LDS (deterministic)
+  extern __shared__ __attribute__((aligned(16))) double red[];  // [blockDim][8]
+  red[tid * 8 + 0] = s1.x;
+  red[tid * 8 + 1] = s1.y;
+  red[tid * 8 + 2] = s1.z;
+  red[tid * 8 + 3] = s1.w;
+  red[tid * 8 + 4] = s2.x;
+  red[tid * 8 + 5] = s2.y;
+  red[tid * 8 + 6] = s2.z;
+  red[tid * 8 + 7] = s2.w;
+  __syncthreads();
+  if (tid < c4n) {
+    double a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int r = 0; r < rows; ++r)
+      for (int k = 0; k < 8; ++k) a[k] += red[(r * c4n + tid) * 8 + k];
+    double* o = part + ((long long)b * nchunk + chunk) * C * 2;
+    for (int k = 0; k < 4; ++k) {
+      o[(tid * 4 + k) * 2 + 0] = a[k];
+      o[(tid * 4 + k) * 2 + 1] = a[4 + k];
+    }
+  }
+}
+
+__global__ void in_finalize_kernel(const float* __restrict__ x, int hw, int C, int cs,
+                                   int nchunk, const double* __restrict__ part, float eps,
+                                   float* __restrict__ mean, float* __restrict__ rstd, int nb) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nb * C) return;
+  const int b = i / C, c = i - b * C;
+  double s1 = 0, s2 = 0;
+  const double* p = part + (long long)b * nchunk * C * 2;
+  for (int k = 0; k < nchunk; ++k) {
+    s1 += p[(k * C + c) * 2];
+    s2 += p[(k * C + c) * 2 + 1];
+  }
+  const double sh = x[(long long)b * hw * cs + c];
+  const double m1 = s1 / hw;
+  double var = s2 / hw - m1 * m1;
+  if (var < 0) var = 0;
+  mean[i] = (float)(sh + m1);
+  rstd[i] = (float)(1.0 / sqrt(var + (double)eps));
+}
+
+// single-channel map (norm3 over the 1-channel score): block partial sums
+__global__ void in1_partial_kernel(const float* __restrict__ x, int hw, int chunk_px,
+                                   double* __restrict__ part) {
+  const int b = blockIdx.y, chunk = blockIdx.x, nchunk = gridDim.x;
+  const float* xb = x + (long long)b * hw;
+  const float sh = xb[0];
+  float s1 = 0.f, s2 = 0.f;
+  const int p0 = chunk * chunk_px, p1 = min(hw, p0 + chunk_px);
+  for (int p = p0 + threadIdx.x; p < p1; p += blockDim.x) {
+    const float v = xb[p] - sh;
+    s1 += v;
+    s2 += v * v;
+  }
+  __shared__ double r1[256], r2[256];
+  r1[threadIdx.x] = s1;
+  r2[threadIdx.x] = s2;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      r1[threadIdx.x] += r1[threadIdx.x + o];
+      r2[threadIdx.x] += r2[threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    part[((long long)b * nchunk + chunk) * 2] = r1[0];
+    part[((long long)b * nchunk + chunk) * 2 + 1] = r2[0];
+  }
+}
+
+// ---------------------------------------------------------------- apply
+__global__ void in_apply_kernel(float* __restrict__ x, int n, int hw, int c4n, int cs,
+                                const float* __restrict__ mean, const float* __restrict__ rstd,
+                                int prelu, const float* __restrict__ slope) {
+  const long long total = (long long)n * hw * c4n;
+  const int C = c4n * 4;
+  const float a = prelu ? *slope : 0.f;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int q = (int)(i % c4n);
+    const long long p = i / c4n;
+    const int b = (int)(p / hw);
+    float* ptr = x + p * cs + q * 4;
+    f32x4 v = *reinterpret_cast<f32x4*>(ptr);
+    const f32x4 m = *reinterpret_cast<const f32x4*>(mean + b * C + q * 4);
+    const f32x4 r = *reinterpret_cast<const f32x4*>(rstd + b * C + q * 4);
+    v = (v - m) * r;
+    if (prelu) {
+      v.x = v.x > 0.f ? v.x : a * v.x;
+      v.y = v.y > 0.f ? v.y : a * v.y;
+      v.z = v.z > 0.f ? v.z : a * v.z;
+      v.w = v.w > 0.f ? v.w : a * v.w;
+    }
+    *reinterpret_cast<f32x4*>(ptr) = v;
+  }
+}
+
+__device__ __forceinline__ f32x4 norm_prelu4(f32x4 v, f32x4 m, f32x4 r, float a) {
+  v = (v - m) * r;
+  v.x = v.x > 0.f ? v.x : a * v.x;
+  v.y = v.y > 0.f ? v.y : a * v.y;
+  v.z = v.z > 0.f ? v.z : a * v.z;
+  v.w = v.w > 0.f ? v.w : a * v.w;
+  return v;
+}
+
+// PReLU(IN(x)) at low resolution, then bilinear resize (align_corners=False)
+// to (OH, OW), written into a channel slice of the output.
+__global__ void norm_prelu_upsample_kernel(const float* __restrict__ x, int n, int h, int w,
+                                           int c4n, int csi, const float* __restrict__ mean,
+                                           const float* __restrict__ rstd,
+                                           const float* __restrict__ slope, int OH, int OW,
+                                           float* __restrict__ y, int cso) {
+  const float a = *slope;
+  const int C = c4n * 4;
+  const float sh = (float)h / (float)OH, sw = (float)w / (float)OW;
+  const long long total = (long long)n * OH * OW * c4n;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int q = (int)(i % c4n);
+    long long p = i / c4n;
+    const int ox = (int)(p % OW);
+    p /= OW;
+    const int oy = (int)(p % OH);
+    const int b = (int)(p / OH);
+    float ry = sh * (oy + 0.5f) - 0.5f;
+    float rx = sw * (ox + 0.5f) - 0.5f;
+    ry = ry < 0.f ? 0.f : ry;
+    rx = rx < 0.f ? 0.f : rx;
+    const int y0 = (int)ry, x0 = (int)rx;
+    const int y1 = y0 + (y0 < h - 1 ? 1 : 0), x1 = x0 + (x0 < w - 1 ? 1 : 0);
+    const float ly = ry - y0, lx = rx - x0, hy = 1.f - ly, hx = 1.f - lx;
+    const float* base = x + (long long)b * h * w * csi + q * 4;
+    const f32x4 m = *reinterpret_cast<const f32x4*>(mean + b * C + q * 4);
+    const f32x4 r = *reinterpret_cast<const f32x4*>(rstd + b * C + q * 4);
+    const f32x4 v00 =
+        norm_prelu4(*reinterpret_cast<const f32x4*>(base + ((long long)y0 * w + x0) * csi), m, r, a);
+    const f32x4 v01 =
+        norm_prelu4(*reinterpret_cast<const f32x4*>(base + ((long long)y0 * w + x1) * csi), m, r, a);
+    const f32x4 v10 =
+        norm_prelu4(*reinterpret_cast<const f32x4*>(base + ((long long)y1 * w + x0) * csi), m, r, a);
+    const f32x4 v11 =
+        norm_prelu4(*reinterpret_cast<const f32x4*>(base + ((long long)y1 * w + x1) * csi), m, r, a);
+    const f32x4 o = hy * (hx * v00 + lx * v01) + ly * (hx * v10 + lx * v11);
+    *reinterpret_cast<f32x4*>(y + (((long long)b * OH + oy) * OW + ox) * cso + q * 4) = o;
+  }
+}
+
+// y[b][p] = bias + sum_c w[c] * PReLU((x[b][p][c]-mean)*rstd), C == 128.
+// One wave handles two pixels per step (32 lanes x float4 each).
+__global__ void head_tail_conv3_kernel(const float* __restrict__ x, int n, int hw, int cs,
+                                       const float* __restrict__ mean,
+                                       const float* __restrict__ rstd,
+                                       const float* __restrict__ slope,
+                                       const float* __restrict__ w3,
+                                       const float* __restrict__ b3, float* __restrict__ y) {
+  const float a = *slope;
+  const int lane = threadIdx.x & 63;
+  const int half = lane >> 5, l32 = lane & 31;
+  const long long waves = (long long)gridDim.x * (blockDim.x >> 6);
+  const long long wid = blockIdx.x * (long long)(blockDim.x >> 6) + (threadIdx.x >> 6);
+  const f32x4 wv = *reinterpret_cast<const f32x4*>(w3 + l32 * 4);
+  const float bias = *b3;
+  const long long total = (long long)n * hw;
+  for (long long p2 = wid * 2; p2 < total; p2 += waves * 2) {
+    const long long p = p2 + half;
+    float s = 0.f;
+    if (p < total) {
+      const int b = (int)(p / hw);
+      const f32x4 m = *reinterpret_cast<const f32x4*>(mean + b * 128 + l32 * 4);
+      const f32x4 r = *reinterpret_cast<const f32x4*>(rstd + b * 128 + l32 * 4);
+      const f32x4 v = norm_prelu4(*reinterpret_cast<const f32x4*>(x + p * cs + l32 * 4), m, r, a);
+      s = v.x * wv.x + v.y * wv.y + v.z * wv.z + v.w * wv.w;
+    }
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if (l32 == 0 && p < total) y[p] = s + bias;
+  }
+}
+
+__global__ void softplus_norm_kernel(const float* __restrict__ x, int n, int hw,
+                                     const float* __restrict__ mean,
+                                     const float* __restrict__ rstd, float* __restrict__ y) {
+  const long long total = (long long)n * hw;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int b = (int)(i / hw);
+    y[i] = pf_softplus((x[i] - mean[b]) * rstd[b]);
+  }
+}
+
+// global_feat[b][c] = mean_p normalize(gmap[b][p][:])[c], C == 128, one block per image
+__global__ void global_feat_kernel(const float* __restrict__ g, int hw, int cs,
+                                   float* __restrict__ out) {
+  const int b = blockIdx.x;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  float a0 = 0.f, a1 = 0.f;
+  for (int p = wv; p < hw; p += nw) {
+    const float* v = g + ((long long)b * hw + p) * cs;
+    const float x0 = v[lane], x1 = v[lane + 64];
+    const float ss = pf_wave_sum(x0 * x0 + x1 * x1);
+    const float inv = 1.f / fmaxf(sqrtf(ss), 1e-12f);
+    a0 += x0 * inv;
+    a1 += x1 * inv;
+  }
+  __shared__ float red[16][128];
+  red[wv][lane] = a0;
+  red[wv][lane + 64] = a1;
+  __syncthreads();
+  if (threadIdx.x < 128) {
+    float s = 0.f;
+    for (int k = 0; k < nw; ++k) s += red[k][threadIdx.x];
+    out[b * 128 + threadIdx.x] = s / (float)hw;
+  }
+}
+
+inline int grid_for(long long total, int block) {
+  long long g = (total + block - 1) / block;
+  if (g > 65536) g = 65536;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ launchers
+int pf_nchw_to_nhwc(const float* x, int n, int c, int h, int w, int cso, float* y, hipStream_t st) {
+  const long long total = (long long)n * h * w * cso;
+  hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3(grid_for(total, 256)), dim3(256), 0, st, x, n, c,
+                     h * w, cso, y);
+  PF_CHECK_LAUNCH();
+  return POSFEAT_OK;
+}
+
+int pf_nhwc_to_nchw(const float* x, int n, int c, int h, int w, int csi, float* y, hipStream_t st) {
+  dim3 grid((h * w + 63) / 64, (c + 63) / 64, n);
+  hipLaunchKernelGGL(nhwc_to_nchw_kernel, grid, dim3(256), 0, st, x, c, h * w, csi, y);
+  PF_CHECK_LAUNCH();
+  return POSFEAT_OK;
+}
+
+int pf_maxpool3s2(const float* x, int n, int h, int w, int c, int csi, float* y, int cso,
+                  hipStream_t st) {
+  const int oh = (h + 2 - 3) / 2 + 1, ow = (w + 2 - 3) / 2 + 1;
+  const long long total = (long long)n * oh * ow * (c / 4);
+  hipLaunchKernelGGL(maxpool3s2_kernel, dim3(grid_for(total, 256)), dim3(256), 0, st, x, n, h, w,
+                     c / 4, csi, oh, ow, cso, y);
+  PF_CHECK_LAUNCH();
+  return POSFEAT_OK;
+}
+
+int pf_upsample2x_ac(const float* x, int n, int h, int w, int c, int csi, float* y, int cso,
+                     hipStream_t st) {
+  const long long total = (long long)n * 4 * h * w * (c / 4);
+  hipLaunchKernelGGL(upsample2x_ac_kernel, dim3(grid_for(total, 256)), dim3(256), 0, st, x, n, h,
+                     w, c / 4, csi, y, cso);
+  PF_CHECK_LAUNCH();
+  return POSFEAT_OK;
+}
+
+size_t pf_in_stats_ws_bytes(int n, int hw, int C) {
+  const int chunk = 2048;
+  const int nchunk = (hw + chunk - 1) / chunk;
+  return (size_t)n * nchunk * (C < 1 ? 1 : C) * 2 * sizeof(double);
+}
+
+int pf_in_stats(const float* x, int n, int hw, int C, int cs, float* mean, float* rstd,
+                double* part, hipStream_t st) {
+  const int chunk = 2048;
+  const int nchunk = (hw + chunk - 1) / chunk;
+  if (C == 1 && cs == 1) {
+    hipLaunchKernelGGL(in1_partial_kernel, dim3(nchunk, n), dim3(256), 0, st, x, hw, chunk, part);
+  } else {
+    if (C % 4 || C / 4 > 256) return POSFEAT_E_INVALID;
+    const int threads = 256;
+    hipLaunchKernelGGL(in_partial_kernel, dim3(nchunk, n), dim3(threads),
+                       threads * 8 * sizeof(double), st, x, hw, C, cs, chunk, part);
+  }
+  PF_CHECK_LAUNCH();
+  hipLaunchKernelGGL(in_finalize_kernel, dim3((n * C + 255) / 256), dim3(256), 0, st, x, hw, C,
+                     cs, nchunk, part, 1e-5f, mean, rstd, n);
+  PF_CHECK_LAUNCH();
+  return POSFEAT_OK;
+}
+
+int pf_in_apply(float* x, int n, int hw, int C, int cs, const float* mean, const float* rstd,
+                const float* prelu_slope, hipStream_t st) {
+  const long long total = (long long)n * hw * (C / 4);
+  hipLaunchKernelGGL(in_apply_kernel, dim3(grid_for(total, 256)), dim3(256), 0, st, x, n, hw,
+                     C / 4, cs, mean, rstd, prelu_slope ? 1 : 0, prelu_slope);
+  PF_CHECK_LAUNCH();
+  return POSFEAT_OK;
+}
+
+int pf_norm_prelu_upsample(const float* x, int n, int h, int w, int C, int csi, const float* mean,
+                           const float* rstd, const float* slope, int OH, int OW, float* y,
+                           int cso, hipStream_t st) {
+  const long long total = (long long)n * OH * OW * (C / 4);
+  hipLaunchKernelGGL(norm_prelu_upsample_kernel, dim3(grid_for(total, 256)), dim3(256), 0, st, x,
+                     n, h, w, C / 4, csi, mean, rstd, slope, OH, OW, y, cso);
+  PF_CHECK_LAUNCH();
+  return POSFEAT_OK;
+}
+
+int pf_head_tail(const float* x, int n, int hw, int cs, const float* mean, const float* rstd,
+                 const float* slope, const float* w3, const float* b3, float* yraw, float* out,
+                 float* mean1, float* rstd1, double* part, hipStream_t st) {
+  const long long total = (long long)n * hw;
+  int blocks = (int)((total / 2 + 3) / 4);
+  if (blocks > 8192) blocks = 8192;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(head_tail_conv3_kernel, dim3(blocks), dim3(256), 0, st, x, n, hw, cs, mean,
+                     rstd, slope, w3, b3, yraw);
+  PF_CHECK_LAUNCH();
+  PF_TRY(pf_in_stats(yraw, n, hw, 1, 1, mean1, rstd1, part, st));
+  hipLaunchKernelGGL(softplus_norm_kernel, dim3(grid_for(total, 256)), dim3(256), 0, st, yraw, n,
+                     hw, mean1, rstd1, out);
+  PF_CHECK_LAUNCH();
+  return POSFEAT_OK;
+}
+
+int pf_global_feat(const float* g, int n, int hw, int cs, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(global_feat_kernel, dim3(n), dim3(1024), 0, st, g, hw, cs, out);
+  PF_CHECK_LAUNCH();
+  return POSFEAT_OK;
+}
+
+extern "C" int posfeat_nchw_to_nhwc(const float* x, int n, int c, int h, int w, int cstride_out,
+                                    float* y, void* stream) {
+  if (!x || !y || n <= 0 || c <= 0 || h <= 0 || w <= 0 || cstride_out < c) return POSFEAT_E_INVALID;
+  return pf_nchw_to_nhwc(x, n, c, h, w, cstride_out, y, pf_stream(stream));
+}
+
+extern "C" int posfeat_nhwc_to_nchw(const float* x, int n, int c, int h, int w, int cstride_in,
+                                    float* y, void* stream) {
+  if (!x || !y || n <= 0 || c <= 0 || h <= 0 || w <= 0 || cstride_in < c) return POSFEAT_E_INVALID;
+  return pf_nhwc_to_nchw(x, n, c, h, w, cstride_in, y, pf_stream(stream));
+}

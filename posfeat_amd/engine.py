@@ -1,0 +1,106 @@
+"""Python handle over the C++/HIP whole-model engine (posfeat_model_* in the C ABI).
+
+``ExtractionEngine`` owns the packed, BN-folded weight blob on the device
+(built once from the reference-layout state dicts, or received by RCCL
+broadcast) and one engine instance + workspace per input shape.  ``run``
+issues the whole ResUNet + KeypointDet forward on the current stream with a
+single C call (~70 kernel launches, no host synchronisation).
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib, weights
+from ._lib import check, lib, ptr, stream_ptr
+
+
+class ExtractionEngine:
+    def __init__(self, backbone_sd=None, head_sd=None, device="cuda", blob=None):
+        _lib.require_device()
+        self.device = torch.device(device)
+        self.specs = _lib.model_specs()
+        nfl = lib().posfeat_model_weight_floats()
+        if blob is None:
+            host = weights.pack_for_device(backbone_sd, head_sd, self.specs)
+            blob = torch.from_numpy(np.ascontiguousarray(host))
+        if blob.numel() > nfl:
+            raise ValueError("weight blob larger than the engine layout")
+        self.wdev = torch.zeros(nfl, dtype=torch.float32, device=self.device)
+        self.wdev[:blob.numel()].copy_(blob.reshape(-1).to(self.device))
+        self._inst = {}
+
+    # ------------------------------------------------------------------
+    def _instance(self, b, h, w):
+        key = (b, h, w)
+        inst = self._inst.get(key)
+        if inst is None:
+            handle = ctypes.c_void_p()
+            check(lib().posfeat_model_create(b, h, w, ptr(self.wdev), ctypes.byref(handle)))
+            nbytes = lib().posfeat_model_workspace(handle)
+            ws = torch.empty(nbytes + 256, dtype=torch.uint8, device=self.device)
+            off = (-ws.data_ptr()) % 256
+            inst = (handle, ws, off)
+            self._inst[key] = inst
+        return inst
+
+    def set_timing(self, b, h, w, enable=True):
+        handle, _, _ = self._instance(b, h, w)
+        check(lib().posfeat_model_set_timing(handle, 1 if enable else 0))
+
+    def timing(self, b, h, w, prefix):
+        """(ms, flops, launches) summed over launches whose label starts with prefix
+        in the last timed run (host-synchronises)."""
+        handle, _, _ = self._instance(b, h, w)
+        ms, fl, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
+        check(lib().posfeat_model_timing(handle, prefix.encode(), ctypes.byref(ms),
+                                         ctypes.byref(fl), ctypes.byref(n)))
+        return ms.value, fl.value, n.value
+
+    def run(self, img, outputs=("local_map", "global_map", "global_feat", "local_map_small")):
+        """img: [b,3,h,w] fp32 on the device (h, w multiples of 16).
+
+        Returns a dict of NCHW tensors plus ``_local_map_nhwc`` -- a view into
+        the engine workspace (valid until the next ``run`` of the same shape).
+        """
+        if img.dtype != torch.float32 or img.dim() != 4 or img.shape[1] != 3:
+            raise ValueError("img must be float32 [b,3,h,w]")
+        img = img.contiguous()
+        _lib.require_device(img)
+        b, _, h, w = img.shape
+        if h % 16 or w % 16:
+            raise ValueError("image height/width must be multiples of 16 (datasets crop to /16)")
+        handle, ws, off = self._instance(b, h, w)
+        dev = img.device
+        res = {"local_point": torch.empty(b, 1, h, w, device=dev)}
+        if "local_map" in outputs:
+            res["local_map"] = torch.empty(b, 128, h // 4, w // 4, device=dev)
+        if "global_map" in outputs:
+            res["global_map"] = torch.empty(b, 128, h // 16, w // 16, device=dev)
+        if "global_feat" in outputs:
+            res["global_feat"] = torch.empty(b, 128, device=dev)
+        if "local_map_small" in outputs:
+            res["local_map_small"] = torch.empty(b, 64, h // 4, w // 4, device=dev)
+        o = _lib.ExtractOut()
+        for k in ("local_map", "global_map", "global_feat", "local_point", "local_map_small"):
+            setattr(o, k, res[k].data_ptr() if k in res else None)
+        check(lib().posfeat_model_extract(handle, ptr(img), ctypes.byref(o),
+                                          ctypes.c_void_p(ws.data_ptr() + off),
+                                          ws.numel() - off, stream_ptr()))
+        base = o.local_map_nhwc - ws.data_ptr()
+        cs = o.local_map_cstride
+        nfl = b * (h // 4) * (w // 4) * cs
+        res["_local_map_nhwc"] = ws[base:base + nfl * 4].view(torch.float32).view(
+            b, h // 4, w // 4, cs)
+        return res
+
+    def close(self):
+        for handle, _, _ in self._inst.values():
+            lib().posfeat_model_destroy(handle)
+        self._inst.clear()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

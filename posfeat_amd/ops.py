@@ -1,0 +1,162 @@
+"""torch-tensor wrappers over the C ABI (device pointers + the current stream).
+
+Every function here runs a hand-written gfx950 kernel; none has a CPU path.
+Inputs must be contiguous fp32 CUDA(HIP) tensors on the current device.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import check, lib, ptr, stream_ptr
+
+ACT = {"none": 0, "relu": 1, "elu": 2}
+THR_MODE = {"abs": 1, "max": 2, "mean": 3}
+
+
+def _f32(t, name):
+    if t.dtype != torch.float32:
+        raise TypeError("%s must be float32 (got %s)" % (name, t.dtype))
+    if not t.is_contiguous():
+        raise ValueError("%s must be contiguous" % name)
+    _lib.require_device(t)
+    return t
+
+
+def packed_k(cin, kh, kw):
+    return lib().posfeat_conv_packed_k(cin, kh, kw)
+
+
+def pack_conv_weight(w, b=None):
+    """[Cout,Cin,KH,KW] (any device) -> (packed [Cout,Kpad] fp32, bias [Cout]) on w's device."""
+    cout, cin, kh, kw = w.shape
+    cinp = (cin + 3) // 4 * 4
+    k = kh * kw * cinp
+    kpad = packed_k(cin, kh, kw)
+    wp = torch.zeros(cout, kh, kw, cinp, dtype=torch.float32, device=w.device)
+    wp[..., :cin] = w.permute(0, 2, 3, 1).float()
+    out = torch.zeros(cout, kpad, dtype=torch.float32, device=w.device)
+    out[:, :k] = wp.reshape(cout, k)
+    bias = b.float().contiguous() if b is not None else torch.zeros(cout, device=w.device)
+    return out.contiguous(), bias
+
+
+def conv2d_nhwc(x, w_packed, bias, cout, kh, kw, stride=1, pad=None, act="none", res=None,
+                out=None, cin=None):
+    """Fused conv on an NHWC tensor x [n,h,w,cs] (first ``cin`` channels used)."""
+    _f32(x, "x")
+    n, h, w, xcs = x.shape
+    cin = xcs if cin is None else cin
+    pad = (kh - 1) // 2 if pad is None else pad
+    oh = (h + 2 * pad - kh) // stride + 1
+    ow = (w + 2 * pad - kw) // stride + 1
+    if out is None:
+        out = torch.empty(n, oh, ow, cout, device=x.device, dtype=torch.float32)
+    d = _lib.ConvDesc(n=n, h=h, w=w, cin=cin, x_cstride=xcs, cout=cout, kh=kh, kw=kw,
+                      stride=stride, pad=pad, y_cstride=out.shape[-1],
+                      res_cstride=(res.shape[-1] if res is not None else 0), act=ACT[act])
+    check(lib().posfeat_conv2d_nhwc(ctypes.byref(d), ptr(x), ptr(_f32(w_packed, "w")),
+                                    ptr(bias), ptr(res), ptr(out), stream_ptr()))
+    return out
+
+
+def nchw_to_nhwc(x, cstride=None):
+    _f32(x, "x")
+    n, c, h, w = x.shape
+    cs = c if cstride is None else cstride
+    y = torch.empty(n, h, w, cs, device=x.device, dtype=torch.float32)
+    check(lib().posfeat_nchw_to_nhwc(ptr(x), n, c, h, w, cs, ptr(y), stream_ptr()))
+    return y
+
+
+def nhwc_to_nchw(x, c=None):
+    _f32(x, "x")
+    n, h, w, cs = x.shape
+    c = cs if c is None else c
+    y = torch.empty(n, c, h, w, device=x.device, dtype=torch.float32)
+    check(lib().posfeat_nhwc_to_nchw(ptr(x), n, c, h, w, cs, ptr(y), stream_ptr()))
+    return y
+
+
+class DetectWorkspace:
+    """Reusable device scratch for ``detect`` (avoid per-call allocation)."""
+
+    def __init__(self):
+        self.key = None
+        self.buf = None
+
+    def get(self, b, h, w, cap, device):
+        key = (b, h, w, cap, str(device))
+        if key != self.key:
+            n = ctypes.c_size_t()
+            check(lib().posfeat_detect_workspace(b, h, w, cap, ctypes.byref(n)))
+            self.buf = torch.empty(n.value, dtype=torch.uint8, device=device)
+            self.key = key
+        return self.buf
+
+
+_DEFAULT_WS = DetectWorkspace()
+
+
+def detect(kp_map, nms_radius, num_pts=False, use_nms=True, thr=False, thr_mod="mean",
+           ws=None, sync=True):
+    """GPU generate_kpts_single core.  kp_map: [b,1,h,w] fp32 on the GPU.
+
+    Returns (idx [b,n] int32, coord_n [b,n,2], kp_score [b,n,1], counts [b], n).
+    With ``sync=False`` the buffers are full-capacity and ``n`` is a device
+    scalar tensor (no host synchronisation).
+    """
+    _f32(kp_map, "kp_map")
+    b, c, h, w = kp_map.shape
+    if c != 1:
+        raise ValueError("kp_map must have one channel")
+    P = (h - 2) * (w - 2)
+    if num_pts:
+        cap = min(max(int(num_pts), 128), P)
+    else:
+        cap = P
+    if thr is False or thr is None or not thr:
+        mode, tval = 0, 0.0
+    else:
+        if thr_mod not in THR_MODE:
+            raise ValueError("thr_mod must be one of %s" % list(THR_MODE))
+        mode, tval = THR_MODE[thr_mod], float(thr)
+    dev = kp_map.device
+    idx = torch.empty(b, cap, dtype=torch.int32, device=dev)
+    coord = torch.empty(b, cap, 2, dtype=torch.float32, device=dev)
+    score = torch.empty(b, cap, 1, dtype=torch.float32, device=dev)
+    meta = torch.empty(b + 1, dtype=torch.int32, device=dev)  # [n_sel, counts...]
+    wsb = (ws or _DEFAULT_WS).get(b, h, w, cap, dev)
+    check(lib().posfeat_detect(ptr(kp_map), b, h, w, int(nms_radius), 1 if use_nms else 0, mode,
+                               tval, int(num_pts) if num_pts else 0, cap, ptr(idx), ptr(coord),
+                               ptr(score), ptr(meta), ctypes.c_void_p(meta.data_ptr() + 4),
+                               ptr(wsb), wsb.numel(), stream_ptr()))
+    counts = meta[1:]
+    if not sync:
+        return idx, coord, score, counts, meta[:1]
+    n = int(meta[0].item())
+    return idx[:, :n], coord[:, :n], score[:, :n], counts, n
+
+
+def sample_desc_nhwc(fmap_nhwc, coord_n, c=None, normalize=True, n_valid=None):
+    """Bilinear (align_corners=False, zeros) sampling of an NHWC map at coord_n [b,n,2]."""
+    _f32(fmap_nhwc, "fmap")
+    coord_n = _f32(coord_n.contiguous(), "coord_n")
+    b, h, w, cs = fmap_nhwc.shape
+    c = cs if c is None else c
+    npts = coord_n.shape[1]
+    out = torch.empty(b, npts, c, device=fmap_nhwc.device, dtype=torch.float32)
+    check(lib().posfeat_sample_desc(ptr(fmap_nhwc), b, c, h, w, cs, ptr(coord_n), npts,
+                                    ptr(n_valid), 1 if normalize else 0, ptr(out), stream_ptr()))
+    return out
+
+
+def sample_desc_strided(fmap_base, b, c, h, w, cs, coord_n, normalize=True, n_valid=None):
+    """Same, on a raw NHWC pointer owned by the engine workspace."""
+    coord_n = _f32(coord_n.contiguous(), "coord_n")
+    npts = coord_n.shape[1]
+    out = torch.empty(b, npts, c, device=coord_n.device, dtype=torch.float32)
+    check(lib().posfeat_sample_desc(ctypes.c_void_p(fmap_base), b, c, h, w, cs, ptr(coord_n),
+                                    npts, ptr(n_valid), 1 if normalize else 0, ptr(out),
+                                    stream_ptr()))
+    return out

@@ -1,0 +1,252 @@
+"""Generate golden vectors by running the REFERENCE's own Python (build container only).
+
+Run from the repo root:  ``python tests/golden/gen_golden.py``  (needs /root/reference).
+
+What is imported from the reference (unmodified, read-only):
+* ``losses`` package (losses/__init__.py: preprocess, preprocess_utils,
+  epipolarloss, kploss) -- torch-only, imports cleanly;
+* ``networks/DeteNet.py`` (KeypointDet) and ``networks/DescNet.py`` (ResUNet,
+  conv, upconv) loaded by file path.  ``networks/__init__.py`` is NOT used
+  because PoSFeat_model.py imports the absent ``path`` package.
+
+Third-party pieces that are absent here and restated instead:
+* torchvision ``resnet50`` (DescNet.py:25): the ResUNet instance is assembled
+  with ``ResUNet.__new__`` and its encoder modules are taken from
+  ``oracle/torchvision_resnet.py``; decoder modules are the reference's own
+  ``conv``/``upconv`` classes, and ``ResUNet.forward`` is the reference code.
+* ``PoSFeat.extract`` glue (PoSFeat_model.py:91-134) is restated inline below
+  (cat + detach + [local_input, img] + ones global prior + global_feat).
+
+Outputs (small .npz fixtures, inputs are regenerated from seeds by the tests):
+  model_small.npz, detector.npz, sampler.npz, extract_full.npz
+"""
+import importlib.util
+import os
+import sys
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, REF)
+
+from posfeat_amd.weights import seeded_state_dicts, seeded_image  # noqa: E402
+from oracle.torchvision_resnet import ResNet50Stem  # noqa: E402
+import losses as ref_losses  # noqa: E402  (reference package)
+from losses import preprocess_utils as ref_putils  # noqa: E402
+
+
+def _load(name, path):
+    spec = importlib.util.spec_from_file_location(name, path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+ref_desc = _load("ref_DescNet", os.path.join(REF, "networks", "DescNet.py"))
+ref_dete = _load("ref_DeteNet", os.path.join(REF, "networks", "DeteNet.py"))
+
+
+def build_ref_resunet():
+    """ResUNet(encoder='resnet50', coarse_out_ch=128, fine_out_ch=128) assembled
+    without torchvision; attribute order mirrors DescNet.py:12-48."""
+    m = ref_desc.ResUNet.__new__(ref_desc.ResUNet)
+    nn.Module.__init__(m)
+    r = ResNet50Stem()
+    filters = [256, 512, 1024, 2048]
+    m.firstconv, m.firstbn, m.firstrelu, m.firstmaxpool = r.conv1, r.bn1, r.relu, r.maxpool
+    m.layer1, m.layer2, m.layer3 = r.layer1, r.layer2, r.layer3
+    m.conv_coarse = ref_desc.conv(filters[2], 128, 1, 1)
+    m.upconv3 = ref_desc.upconv(filters[2], 512, 3, 2)
+    m.iconv3 = ref_desc.conv(filters[1] + 512, 512, 3, 1)
+    m.upconv2 = ref_desc.upconv(512, 256, 3, 2)
+    m.iconv2 = ref_desc.conv(filters[0] + 256, 256, 3, 1)
+    m.conv_fine = ref_desc.conv(256, 128, 1, 1)
+    m.out_channels = [128, 128]
+    return m
+
+
+def build_ref_models(seed=0):
+    bb_sd, hd_sd = seeded_state_dicts(seed)
+    bb = build_ref_resunet()
+    bb.load_state_dict(bb_sd, strict=True)
+    hd = ref_dete.KeypointDet(in_channels=192, out_channels=1, prior="identity", act="Softplus")
+    hd.load_state_dict(hd_sd, strict=True)
+    bb.eval()
+    hd.eval()
+    return bb, hd
+
+
+@torch.no_grad()
+def ref_extract(bb, hd, img):
+    """Restatement of PoSFeat.extract glue (PoSFeat_model.py:91-134) around the
+    reference modules."""
+    feat_maps = bb(img)
+    b, c, h, w = feat_maps["global_map"].shape
+    g_map = torch.ones(b, 1, h, w).type_as(feat_maps["local_map"])
+    local_input = torch.cat([feat_maps["local_map"], feat_maps["local_map_small"]], dim=1).detach()
+    l_map = hd([local_input, img])
+    g_desc = F.normalize(g_map * feat_maps["global_map"], p=2, dim=1).mean([2, 3])
+    return {"local_map": feat_maps["local_map"], "global_map": feat_maps["global_map"],
+            "local_map_small": feat_maps["local_map_small"], "local_point": l_map,
+            "global_feat": g_desc}
+
+
+@torch.no_grad()
+def ref_detect_with_idx(kp_map, nms_radius, num_pts, use_nms=True, thr=False, thr_mod="mean"):
+    """Reference generate_kpts_single outputs plus the idx of its line 264
+    (recomputed with the reference's own ``nms`` and the same expression), and
+    canonicalised to the (score desc, idx asc) tie rule."""
+    kps, kp_score = ref_putils.generate_kpts_single(
+        kp_map, nms_radius, num_pts, stable=True, use_nms=use_nms, thr=thr, thr_mod=thr_mod)
+    b, _, h, w = kp_map.shape
+    inner = kp_map[:, :, 1:-1, 1:-1]
+    nms_mask = ref_putils.nms(inner, nms_radius) if use_nms else torch.ones_like(inner)
+    if thr:
+        if thr_mod == "max":
+            kp_thr = inner.reshape(b, 1, -1).max(2)[0]
+        elif thr_mod == "mean":
+            kp_thr = inner.reshape(b, 1, -1).mean(2)
+        else:
+            kp_thr = torch.tensor(1.).to(kp_map).repeat(b)
+        nms_mask = (inner > thr * kp_thr.view(b, 1, 1, 1)) * nms_mask
+    count = nms_mask.reshape(b, -1).sum(1)
+    n = kps.shape[1]
+    masked = (nms_mask * inner).permute(0, 2, 3, 1).contiguous().view(b, -1)
+    vals, idx = masked.topk(n)
+    # canonicalise runs of equal values: idx ascending
+    vals = vals.numpy()
+    idx = idx.numpy().copy()
+    kps = kps.numpy().copy()
+    kp_score = kp_score.numpy().copy()
+    for i in range(b):
+        order = np.lexsort((idx[i], -vals[i].astype(np.float64)))
+        idx[i] = idx[i][order]
+        kps[i] = kps[i][order]
+        kp_score[i] = kp_score[i][order]
+        vals[i] = vals[i][order]
+    return {"idx": idx.astype(np.int32), "coord_n": kps.astype(np.float32),
+            "kp_score": kp_score.astype(np.float32), "count": count.numpy().astype(np.int64),
+            "masked": vals.astype(np.float32)}
+
+
+def crafted_maps():
+    """Small hand-made score maps exercising ties, plateaus, borders (1x1x20x28)."""
+    maps = []
+    rs = np.random.RandomState(7)
+    a = rs.rand(20, 28).astype(np.float32)
+    # adjacent equal peaks
+    a[5, 5] = a[5, 6] = 2.0
+    a[10, 10] = a[11, 10] = 2.0
+    # flat plateau
+    a[14:17, 3:6] = 3.0
+    # border ties (inner-map border rows/cols 0 and -1 -> map rows 1, -2)
+    a[1, 12] = 2.5
+    a[2, 12] = 2.5
+    a[1, 20] = 1.7
+    a[3, 20] = 1.7  # reflected copy at r=... tie with reflection
+    a[18, 1] = 1.9
+    a[18, 3] = 1.9
+    maps.append(a)
+    b = np.full((20, 28), 0.95, np.float32)   # fully flat map (no peaks -> n=128 fill)
+    b[6, 7] = 1.5
+    maps.append(b)
+    c = (rs.randint(0, 4, (20, 28)).astype(np.float32) / 3.0).astype(np.float32)  # many exact ties
+    maps.append(c)
+    d = rs.randn(20, 28).astype(np.float32)   # negative values
+    maps.append(d)
+    return [m[None, None] for m in maps]
+
+
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+from golden_cfg import DET_CONFIGS, CRAFTED_CONFIGS  # noqa: E402
+
+
+def gen_detector(out):
+    res = {}
+    for s in range(3):
+        km = torch.from_numpy(np.random.RandomState(s).rand(1, 1, 480, 640).astype(np.float32))
+        for name, r, n, un, thr, tm in DET_CONFIGS:
+            d = ref_detect_with_idx(km, r, n, un, thr, tm)
+            for k, v in d.items():
+                res["rand%d_%s_%s" % (s, name, k)] = v
+    for j, m in enumerate(crafted_maps()):
+        km = torch.from_numpy(m)
+        res["crafted%d_map" % j] = m
+        for name, r, n, un, thr, tm in CRAFTED_CONFIGS:
+            d = ref_detect_with_idx(km, r, n, un, thr, tm)
+            for k, v in d.items():
+                res["crafted%d_%s_%s" % (j, name, k)] = v
+    np.savez_compressed(out, **res)
+
+
+@torch.no_grad()
+def gen_sampler(out):
+    rs = np.random.RandomState(11)
+    fmap = rs.randn(2, 128, 24, 32).astype(np.float32)
+    coords = rs.uniform(-1.1, 1.1, (2, 160, 2)).astype(np.float32)
+    coords[:, :4] = [[-1, -1], [1, 1], [-1, 1], [0, 0]]
+    t_f, t_c = torch.from_numpy(fmap), torch.from_numpy(coords)
+    res = {"coords": coords,
+           "desc_norm": ref_putils.sample_feat_by_coord(t_f, t_c, True).numpy(),
+           "desc_raw": ref_putils.sample_feat_by_coord(t_f, t_c, False).numpy(),
+           "denorm": ref_putils.denormalize_coords(t_c, 480, 640).numpy(),
+           "renorm": ref_putils.normalize_coords(ref_putils.denormalize_coords(t_c, 480, 640),
+                                                 480, 640).numpy()}
+    np.savez_compressed(out, **res)
+
+
+def gen_model_small(out):
+    bb, hd = build_ref_models(0)
+    res = {}
+    for tag, (h, w, i) in {"a": (96, 128, 0), "b": (64, 96, 1)}.items():
+        img = torch.from_numpy(seeded_image(i, h, w))[None]
+        o = ref_extract(bb, hd, img)
+        for k, v in o.items():
+            res["%s_%s" % (tag, k)] = v.numpy()
+        d = ref_detect_with_idx(o["local_point"], 1, 256, True, 0.9, "abs")
+        for k, v in d.items():
+            res["%s_det_%s" % (tag, k)] = v
+        cn = torch.from_numpy(d["coord_n"])
+        res["%s_desc" % tag] = ref_putils.sample_feat_by_coord(o["local_map"], cn, True).numpy()
+    np.savez_compressed(out, **res)
+
+
+def gen_extract_full(out):
+    bb, hd = build_ref_models(0)
+    img = torch.from_numpy(seeded_image(0, 480, 640))[None]
+    o = ref_extract(bb, hd, img)
+    lp = o["local_point"]
+    d = ref_detect_with_idx(lp, 1, 2048, True, 0.9, "abs")
+    cn = torch.from_numpy(d["coord_n"])
+    desc = ref_putils.sample_feat_by_coord(o["local_map"], cn, True).numpy()
+    kpt = ref_putils.denormalize_coords(cn, 480, 640).numpy()
+    res = {"idx": d["idx"], "coord_n": d["coord_n"], "kp_score": d["kp_score"],
+           "count": d["count"], "masked": d["masked"], "kpt": kpt,
+           "desc_first256": desc[:, :256],
+           "local_point_rows": lp[0, 0, ::40].numpy(),          # 12 full rows
+           "local_map_px": o["local_map"][0, :, ::20, ::20].numpy(),  # 6x8 pixels
+           "global_feat": o["global_feat"].numpy(),
+           "local_point_sum": np.float64(lp.double().sum()),
+           "local_map_sum": np.float64(o["local_map"].double().sum()),
+           "global_map_sum": np.float64(o["global_map"].double().sum())}
+    np.savez_compressed(out, **res)
+
+
+if __name__ == "__main__":
+    torch.set_num_threads(os.cpu_count() or 8)
+    which = sys.argv[1:] or ["detector", "sampler", "model_small", "extract_full"]
+    if "detector" in which:
+        gen_detector(os.path.join(HERE, "detector.npz"))
+    if "sampler" in which:
+        gen_sampler(os.path.join(HERE, "sampler.npz"))
+    if "model_small" in which:
+        gen_model_small(os.path.join(HERE, "model_small.npz"))
+    if "extract_full" in which:
+        gen_extract_full(os.path.join(HERE, "extract_full.npz"))
+    print("golden fixtures written to", HERE)

@@ -1,0 +1,108 @@
+"""GPU parity of the whole-model engine (PoSFeat.extract) against the golden
+vectors produced by the reference's own modules (tests/golden/gen_golden.py)
+and against the torch-CPU oracle on the same seeded weights and images."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+# fp32 tolerance of SURVEY §8c / north_star: 1e-4 (scaled by magnitude for
+# the unnormalised backbone maps, whose values reach O(10))
+RTOL, ATOL = 1e-4, 1e-4
+
+
+@pytest.fixture(scope="module")
+def engine():
+    import torch as _t
+    assert _t.cuda.is_available()
+    from posfeat_amd.engine import ExtractionEngine
+    from posfeat_amd.weights import seeded_state_dicts
+    bb, hd = seeded_state_dicts(0)
+    return ExtractionEngine(bb, hd, device="cuda")
+
+
+def _close(got, ref, name, rtol=RTOL, atol=ATOL):
+    got = got.detach().cpu().numpy() if torch.is_tensor(got) else got
+    scale = max(1.0, float(np.abs(ref).max()))
+    err = np.abs(got - ref).max()
+    assert err <= atol * scale + rtol * 0, "%s: max abs err %g (scale %g)" % (name, err, scale)
+
+
+@pytest.mark.parametrize("tag,hw,seed", [("a", (96, 128), 0), ("b", (64, 96), 1)])
+def test_engine_vs_golden_small(gpu, engine, tag, hw, seed):
+    from posfeat_amd.weights import seeded_image
+    d = np.load(os.path.join(GOLDEN, "model_small.npz"))
+    img = torch.from_numpy(seeded_image(seed, *hw))[None].to(gpu)
+    out = engine.run(img)
+    torch.cuda.synchronize()
+    for k in ("local_map", "global_map", "local_map_small", "local_point", "global_feat"):
+        _close(out[k], d["%s_%s" % (tag, k)], k)
+
+
+def test_engine_batch_consistency(gpu, engine):
+    from posfeat_amd.weights import seeded_image
+    ims = [torch.from_numpy(seeded_image(s, 64, 96)) for s in (1, 2)]
+    both = engine.run(torch.stack(ims).to(gpu))
+    one = engine.run(ims[1][None].to(gpu))
+    for k in ("local_point", "local_map", "global_feat"):
+        assert torch.equal(both[k][1:2], one[k]), k
+
+
+def test_engine_deterministic(gpu, engine):
+    from posfeat_amd.weights import seeded_image
+    img = torch.from_numpy(seeded_image(3, 96, 128))[None].to(gpu)
+    a = engine.run(img)["local_point"].clone()
+    b = engine.run(img)["local_point"].clone()
+    assert torch.equal(a, b)
+
+
+def test_engine_full_480x640(gpu, engine):
+    """Full-size image vs the reference run (extract_full.npz): maps within
+    tolerance, and the detector's 2048 keypoints identical except at near-ties
+    of the score map (|dS| < 1e-5 at the deciding comparison)."""
+    from posfeat_amd import ops
+    from posfeat_amd.weights import seeded_image
+    d = np.load(os.path.join(GOLDEN, "extract_full.npz"))
+    img = torch.from_numpy(seeded_image(0, 480, 640))[None].to(gpu)
+    out = engine.run(img)
+    lp = out["local_point"]
+    _close(lp[0, 0, ::40], d["local_point_rows"], "local_point rows")
+    _close(out["local_map"][0, :, ::20, ::20], d["local_map_px"], "local_map px")
+    _close(out["global_feat"], d["global_feat"], "global_feat")
+    assert abs(float(lp.double().sum()) - float(d["local_point_sum"])) < 1e-6 * 480 * 640 * 4
+    # oracle (torch CPU restatement) on the same image and weights
+    from oracle import model_ref, detect_ref
+    from posfeat_amd.weights import seeded_state_dicts
+    from near_tie import explain_differences
+    bb, hd = seeded_state_dicts(0)
+    torch.set_num_threads(min(16, os.cpu_count() or 4))
+    ref_out = model_ref.posfeat_extract(bb, hd, img.cpu())
+    S_ref = ref_out["local_point"][0, 0].numpy()
+    S_gpu = lp[0, 0].cpu().numpy()
+    delta = float(np.abs(S_gpu - S_ref).max())
+    assert delta < 1e-4, "local_point max abs err %g" % delta
+    idx, coord, score, counts, n = ops.detect(lp, 1, 2048, thr=0.9, thr_mod="abs")
+    assert n == 2048
+    c_ref, s_ref, i_ref = detect_ref.generate_kpts_single(S_ref[None, None], 1, 2048, thr=0.9,
+                                                          thr_mod="abs", return_idx=True)
+    got = idx[0].cpu().numpy()
+    unexplained, overlap = explain_differences(S_ref, got, i_ref[0], 1, 0.9, delta)
+    print("full-size: delta=%.2e overlap=%.4f unexplained=%d" % (delta, overlap, unexplained.size))
+    assert unexplained.size == 0, "keypoint differences not explained by near-ties: %s" % unexplained[:10]
+    assert overlap > 0.97
+    # common keypoints: coordinates, scores and descriptors within 1e-4
+    common, ia, ib = np.intersect1d(got, i_ref[0], return_indices=True)
+    np.testing.assert_allclose(coord[0].cpu().numpy()[ia], c_ref[0][ib], atol=1e-4)
+    np.testing.assert_allclose(score[0, :, 0].cpu().numpy()[ia], s_ref[0, :, 0][ib], atol=1e-4)
+    desc = ops.sample_desc_nhwc(out["_local_map_nhwc"], coord, c=128)[0].cpu().numpy()
+    d_ref = detect_ref.sample_feat_by_coord(ref_out["local_map"].numpy(), c_ref, True)[0]
+    np.testing.assert_allclose(desc[ia], d_ref[ib], atol=1e-4)
+    # and the same detector on the REFERENCE's own map is bit-exact (golden)
+    idx2, _, score2, _, _ = ops.detect(torch.from_numpy(S_ref)[None, None].to(gpu), 1, 2048,
+                                       thr=0.9, thr_mod="abs")
+    np.testing.assert_array_equal(idx2[0].cpu().numpy(), i_ref[0])

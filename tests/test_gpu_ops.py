@@ -1,0 +1,160 @@
+"""GPU parity of the individual HIP kernels, through the C ABI.
+
+Floating-point kernels (conv, sampler, layout) are compared with a plain
+torch fp32/fp64 CPU reference of the same op; the detector (integer/index
+work) must be bit-exact against the numpy oracle and the golden fixtures
+generated from the reference's own generate_kpts_single.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+def _conv_ref64(x, w, b, stride, pad, res=None, act="none"):
+    y = F.conv2d(x.double(), w.double(), b.double() if b is not None else None, stride=stride,
+                 padding=pad)
+    if res is not None:
+        y = y + res.double()
+    if act == "relu":
+        y = torch.relu(y)
+    elif act == "elu":
+        y = F.elu(y)
+    bound = F.conv2d(x.double().abs(), w.double().abs(), None, stride=stride, padding=pad)
+    return y, bound
+
+
+CONV_CASES = [
+    # n, h, w, cin, cout, k, stride, act, residual, in_extra, out_extra
+    (2, 17, 23, 64, 96, 3, 1, "none", False, 0, 0),
+    (1, 20, 30, 256, 64, 1, 1, "relu", True, 0, 0),
+    (2, 19, 21, 128, 128, 3, 2, "relu", False, 64, 0),
+    (1, 33, 47, 3, 64, 7, 2, "relu", False, 1, 0),      # stem: cin 3 padded to 4
+    (1, 24, 40, 3, 64, 3, 1, "none", False, 1, 192),    # convimg into a 256-wide slice
+    (1, 16, 20, 512, 256, 1, 2, "none", False, 0, 0),   # downsample 1x1 s2
+    (1, 12, 16, 1024, 512, 3, 1, "elu", False, 0, 0),
+    (1, 256, 256, 64, 128, 3, 1, "elu", True, 0, 0),    # 128x128-tile path
+    (1, 30, 40, 192, 192, 3, 1, "none", False, 0, 0),   # cout 192 (tile guard)
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_vs_torch(gpu, case):
+    from posfeat_amd import ops
+    n, h, w, cin, cout, k, s, act, has_res, in_extra, out_extra = case
+    g = torch.Generator().manual_seed(hash(case) % 1000)
+    x = torch.randn(n, cin, h, w, generator=g)
+    wt = torch.randn(cout, cin, k, k, generator=g) * (2.0 / (cin * k * k)) ** 0.5
+    b = torch.randn(cout, generator=g) * 0.1
+    pad = (k - 1) // 2
+    oh, ow = (h + 2 * pad - k) // s + 1, (w + 2 * pad - k) // s + 1
+    res = torch.randn(n, cout, oh, ow, generator=g) if has_res else None
+    ref, bound = _conv_ref64(x, wt, b, s, pad, res, act)
+    cinp = (cin + 3) // 4 * 4
+    xcs = cinp + in_extra * 4
+    xd = torch.zeros(n, h, w, xcs)
+    xd[..., :cin] = x.permute(0, 2, 3, 1)
+    xd = xd.to(gpu)
+    wp, bp = ops.pack_conv_weight(wt.to(gpu), b.to(gpu))
+    out = torch.full((n, oh, ow, cout + out_extra), 7.0, device=gpu)
+    rd = res.permute(0, 2, 3, 1).contiguous().to(gpu) if has_res else None
+    ops.conv2d_nhwc(xd, wp, bp, cout, k, k, stride=s, pad=pad, act=act, res=rd, out=out, cin=cinp)
+    torch.cuda.synchronize()
+    got = out[..., :cout].permute(0, 3, 1, 2).double().cpu()
+    err = (got - ref).abs()
+    tol = 2e-6 * bound + 1e-6
+    assert torch.all(err <= tol), "max err %g (bound %g)" % (err.max(), (err / tol).max())
+    if out_extra:
+        assert torch.all(out[..., cout:] == 7.0).item(), "wrote outside its channel slice"
+
+
+def test_conv_deterministic(gpu):
+    from posfeat_amd import ops
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(1, 64, 96, 128, generator=g).permute(0, 2, 3, 1).contiguous().to(gpu)
+    wt = torch.randn(128, 64, 3, 3, generator=g).to(gpu)
+    wp, bp = ops.pack_conv_weight(wt)
+    a = ops.conv2d_nhwc(x, wp, bp, 128, 3, 3)
+    b = ops.conv2d_nhwc(x, wp, bp, 128, 3, 3)
+    assert torch.equal(a, b)
+
+
+def test_layout_roundtrip(gpu):
+    from posfeat_amd import ops
+    x = torch.randn(2, 40, 13, 17, device=gpu)
+    y = ops.nchw_to_nhwc(x, cstride=44)
+    assert torch.equal(y[..., :40], x.permute(0, 2, 3, 1))
+    assert torch.all(y[..., 40:] == 0)
+    z = ops.nhwc_to_nchw(y, c=40)
+    assert torch.equal(z, x)
+
+
+# ------------------------------------------------------------------ detector
+def _check_det(gpu, km_np, prefix, d, r, n, un, thr, tm):
+    from posfeat_amd import ops
+    km = torch.from_numpy(km_np).to(gpu)
+    idx, coord, score, counts, nsel = ops.detect(km, r, n, use_nms=un, thr=thr, thr_mod=tm)
+    ref_idx = d[prefix + "_idx"][0]
+    ref_masked = d[prefix + "_masked"][0]
+    assert nsel == ref_idx.shape[0]
+    assert int(counts[0].item()) == int(d[prefix + "_count"][0])
+    idx = idx[0].cpu().numpy()
+    coord = coord[0].cpu().numpy()
+    score = score[0].cpu().numpy()
+    pos = ref_masked > 0  # zero-score fill rows are compared by count only
+    np.testing.assert_array_equal(idx[pos], ref_idx[pos])
+    np.testing.assert_array_equal(score[pos], d[prefix + "_kp_score"][0][pos])
+    np.testing.assert_allclose(coord[pos], d[prefix + "_coord_n"][0][pos], atol=1e-5, rtol=0)
+
+
+def test_detector_golden_random(gpu):
+    d = np.load(os.path.join(GOLDEN, "detector.npz"))
+    from golden_cfg import DET_CONFIGS
+    for s in range(3):
+        km = np.random.RandomState(s).rand(1, 1, 480, 640).astype(np.float32)
+        for name, r, n, un, thr, tm in DET_CONFIGS:
+            _check_det(gpu, km, "rand%d_%s" % (s, name), d, r, n, un, thr, tm)
+
+
+def test_detector_golden_crafted(gpu):
+    d = np.load(os.path.join(GOLDEN, "detector.npz"))
+    for j in range(4):
+        km = d["crafted%d_map" % j]
+        from golden_cfg import CRAFTED_CONFIGS
+        for name, r, n, un, thr, tm in CRAFTED_CONFIGS:
+            _check_det(gpu, km, "crafted%d_%s" % (j, name), d, r, n, un, thr, tm)
+
+
+def test_detector_batch_min_count(gpu):
+    """b>1: n = min count over the batch (preprocess_utils.py:256-257)."""
+    from posfeat_amd import ops
+    from oracle import detect_ref
+    km = np.stack([np.random.RandomState(s).rand(1, 120, 160).astype(np.float32)
+                   for s in (5, 6, 7)])
+    c_ref, s_ref, i_ref = detect_ref.generate_kpts_single(km, 1, 4000, thr=0.9, thr_mod="abs",
+                                                          return_idx=True)
+    idx, coord, score, counts, n = ops.detect(torch.from_numpy(km).to(gpu), 1, 4000, thr=0.9,
+                                              thr_mod="abs")
+    assert n == i_ref.shape[1]
+    np.testing.assert_array_equal(idx.cpu().numpy(), i_ref)
+    np.testing.assert_array_equal(score.cpu().numpy(), s_ref)
+    np.testing.assert_allclose(coord.cpu().numpy(), c_ref, atol=1e-5)
+
+
+# ------------------------------------------------------------------ sampler
+def test_sampler_golden(gpu):
+    from posfeat_amd import ops
+    d = np.load(os.path.join(GOLDEN, "sampler.npz"))
+    fmap = np.random.RandomState(11).randn(2, 128, 24, 32).astype(np.float32)
+    x = torch.from_numpy(fmap).to(gpu)
+    xn = ops.nchw_to_nhwc(x)
+    c = torch.from_numpy(d["coords"]).to(gpu)
+    for norm, key, tol in ((True, "desc_norm", 1e-5), (False, "desc_raw", 1e-4)):
+        out = ops.sample_desc_nhwc(xn, c, normalize=norm).cpu().numpy()
+        np.testing.assert_allclose(out, d[key], atol=tol, rtol=0)
