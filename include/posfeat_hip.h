@@ -93,6 +93,11 @@ int posfeat_detect(const float *kp_map, int b, int h, int w, int nms_radius, int
                    float *score, int32_t *n_sel, int32_t *counts, void *ws, size_t ws_bytes,
                    void *stream);
 
+/* NMS mask alone (losses/preprocess_utils.py:449-464 nms): mask[b][h][w] = 1
+ * iff the pixel is its reflect-padded (2r+1)^2 window's first-occurrence max. */
+int posfeat_nms_mask(const float *score, int b, int h, int w, int radius, uint8_t *mask,
+                     void *stream);
+
 /* ------------------------------------------------------------------------
  * Descriptor sampling.
  * Replaces: losses/preprocess_utils.py:40-53 sample_feat_by_coord

@@ -46,6 +46,7 @@ SIGNATURES = {
     "posfeat_detect": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int,
                                c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                c_size_t, c_void_p]),
+    "posfeat_nms_mask": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     "posfeat_sample_desc": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int,
                                     c_void_p, c_int, c_void_p, c_void_p]),
     "posfeat_nchw_to_nhwc": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
@@ -91,13 +92,20 @@ def check(code):
         raise RuntimeError(lib().posfeat_strerror(code).decode())
 
 
+_DEV_OK = {}
+
+
 def require_device(t=None):
     """Raise unless a gfx950 GPU is visible (and ``t`` lives on it)."""
-    if not torch.cuda.is_available():
-        raise RuntimeError("posfeat_amd: no GPU visible; the HIP path has no CPU fallback")
     if t is not None and not t.is_cuda:
         raise RuntimeError("posfeat_amd: tensor must be on the GPU (got %s)" % t.device)
-    if not lib().posfeat_device_ok():
+    if not torch.cuda.is_available():
+        raise RuntimeError("posfeat_amd: no GPU visible; the HIP path has no CPU fallback")
+    dev = torch.cuda.current_device()
+    ok = _DEV_OK.get(dev)
+    if ok is None:
+        ok = _DEV_OK[dev] = bool(lib().posfeat_device_ok())
+    if not ok:
         raise RuntimeError("posfeat_amd: current device is not gfx950 (MI355X)")
 
 

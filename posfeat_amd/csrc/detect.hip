@@ -63,12 +63,38 @@ __global__ void det_thr_kernel(const float* __restrict__ kp, int h, int w, int m
   }
 }
 
+// NMS decision for pixel (i, j) of an Hi x Wi map stored with row pitch `w`
+// at offset (off, off): reflect padding, first-occurrence tie rule.
+__device__ __forceinline__ bool nms_keep(const float* __restrict__ m, int w, int Hi, int Wi, int off,
+                                         int i, int j, int r, float S) {
+  const int ws = 2 * r + 1, center = r * ws + r;
+  int pos = 0;
+  for (int dy = -r; dy <= r; ++dy) {
+    const int yy = reflect_idx(i + dy, Hi) + off;
+    for (int dx = -r; dx <= r; ++dx, ++pos) {
+      if (pos == center) continue;
+      const float v = m[yy * w + reflect_idx(j + dx, Wi) + off];
+      if (pos < center ? !(v < S) : !(v <= S)) return false;
+    }
+  }
+  return true;
+}
+
+__global__ void nms_mask_kernel(const float* __restrict__ score, int h, int w, int r,
+                                uint8_t* __restrict__ mask) {
+  const int b = blockIdx.y;
+  const float* m = score + (long long)b * h * w;
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < h * w; p += gridDim.x * blockDim.x) {
+    const int i = p / w, j = p - (p / w) * w;
+    mask[(long long)b * h * w + p] = nms_keep(m, w, h, w, 0, i, j, r, m[p]) ? 1 : 0;
+  }
+}
+
 __global__ void det_mask_kernel(const float* __restrict__ kp, int h, int w, int r, int use_nms,
                                 int use_thr, const float* __restrict__ thr_t,
                                 uint32_t* __restrict__ keys, int32_t* __restrict__ counts) {
   const int b = blockIdx.y;  // one image per grid row: block-uniform counter
   const int Hi = h - 2, Wi = w - 2, P = Hi * Wi;
-  const int ws = 2 * r + 1, center = r * ws + r;
   const float* m = kp + (long long)b * h * w;
   const float t = use_thr ? thr_t[b] : 0.f;
   int local = 0;
@@ -76,20 +102,7 @@ __global__ void det_mask_kernel(const float* __restrict__ kp, int h, int w, int 
     const int i = p / Wi, j = p - (p / Wi) * Wi;
     const float S = m[(i + 1) * w + j + 1];
     bool keep = use_thr ? (S > t) : true;
-    if (keep && use_nms) {
-      int pos = 0;
-      for (int dy = -r; dy <= r && keep; ++dy) {
-        const int yy = reflect_idx(i + dy, Hi) + 1;
-        for (int dx = -r; dx <= r; ++dx, ++pos) {
-          if (pos == center) continue;
-          const float v = m[yy * w + reflect_idx(j + dx, Wi) + 1];
-          if (pos < center ? !(v < S) : !(v <= S)) {
-            keep = false;
-            break;
-          }
-        }
-      }
-    }
+    if (keep && use_nms) keep = nms_keep(m, w, Hi, Wi, 1, i, j, r, S);
     keys[(long long)b * P + p] = pf_fkey(keep ? S : 0.0f);
     local += keep ? 1 : 0;
   }
@@ -320,6 +333,18 @@ extern "C" int posfeat_detect(const float* kp_map, int b, int h, int w, int nms_
   const int maxn = cap < P ? cap : P;
   hipLaunchKernelGGL(det_rank_kernel, dim3((maxn + 255) / 256, b), dim3(256), 0, st, kp_map, h, w,
                      cap, sel, selkey, n_sel, idx, coord, score);
+  PF_CHECK_LAUNCH();
+  return POSFEAT_OK;
+}
+
+extern "C" int posfeat_nms_mask(const float* score, int b, int h, int w, int radius,
+                                uint8_t* mask, void* stream) {
+  if (!score || !mask || b <= 0 || h <= 0 || w <= 0 || radius < 0) return POSFEAT_E_INVALID;
+  if (radius >= h || radius >= w) return POSFEAT_E_INVALID;  // reflect pad limit (as torch)
+  int g = (h * w + 255) / 256;
+  if (g > 4096) g = 4096;
+  hipLaunchKernelGGL(nms_mask_kernel, dim3(g, b), dim3(256), 0, pf_stream(stream), score, h, w,
+                     radius, mask);
   PF_CHECK_LAUNCH();
   return POSFEAT_OK;
 }

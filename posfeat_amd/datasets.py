@@ -1,0 +1,136 @@
+"""Extraction datasets with the reference's file discovery and input contract.
+
+Reference: datasets/hpatches.py:8-46, datasets/aachen.py:10-64,
+datasets/ETH_local_feature.py:10-59.  Each item is
+``{'im1': [3,h,w] ImageNet-normalised float, 'im1_ori': uint8 HxWx3,
+'coord1': SIFT keypoints, 'name1': relative name, 'pad1': (0,0,0,0)}`` with h, w
+cropped down to multiples of 16.  The reference ALWAYS runs OpenCV SIFT per
+image (only consumed when ``use_sift: True``); OpenCV is not part of this
+stack, so ``coord1`` is an empty [0,2] tensor and the Extractor refuses
+``use_sift: True`` loudly.  Decoding uses PIL (skimage is absent).
+"""
+import glob
+import os
+
+import numpy as np
+import torch
+from torch.utils.data import Dataset
+
+MEAN = np.array([0.485, 0.456, 0.406], np.float32)
+STD = np.array([0.229, 0.224, 0.225], np.float32)
+
+
+def to_input(im):
+    """uint8 HxWx3 -> (normalised [3,h16,w16] float tensor, cropped uint8 image):
+    transforms.ToTensor + Normalize then crop to /16 (hpatches.py:14-17, 35-38)."""
+    if im.ndim == 2:
+        im = np.stack([im] * 3, -1)
+    im = im[..., :3]
+    h, w = im.shape[:2]
+    im = im[:h - h % 16, :w - w % 16]
+    x = (im.astype(np.float32) / np.float32(255.0) - MEAN) / STD
+    return torch.from_numpy(np.ascontiguousarray(x.transpose(2, 0, 1))), np.ascontiguousarray(im)
+
+
+def _read(path):
+    from PIL import Image
+    return np.asarray(Image.open(path).convert("RGB"))
+
+
+class _FileDataset(Dataset):
+    def __init__(self, configs):
+        super().__init__()
+        self.configs = configs
+        self.imfs = []
+
+    def name_of(self, path):
+        raise NotImplementedError
+
+    def __getitem__(self, item):
+        imf = self.imfs[item]
+        x, im = to_input(_read(imf))
+        return {"im1": x, "im1_ori": im, "coord1": torch.zeros(0, 2), "name1": self.name_of(imf),
+                "pad1": (0, 0, 0, 0)}
+
+    def __len__(self):
+        return len(self.imfs)
+
+
+class HPatch_SIFT(_FileDataset):
+    """``<data_path>/*/*.ppm``, name = 'seq/idx.ppm' (hpatches.py:19-30)."""
+
+    def __init__(self, configs):
+        super().__init__(configs)
+        self.imfs = sorted(glob.glob(os.path.join(configs["data_path"], "*", "*.ppm")))
+
+    def name_of(self, p):
+        return "/".join(p.split("/")[-2:])
+
+
+class Aachen_Day_Night(_FileDataset):
+    """db/*.jpg, query/*/*/*.jpg, sequences/... (aachen.py:20-47)."""
+
+    def __init__(self, configs):
+        super().__init__(configs)
+        r = configs["data_path"]
+        imfs = glob.glob(os.path.join(r, "db", "*.jpg"))
+        imfs += glob.glob(os.path.join(r, "query", "*", "*", "*.jpg"))
+        imfs += glob.glob(os.path.join(r, "sequences", "gopro3_undistorted", "*.png"))
+        imfs += glob.glob(os.path.join(r, "sequences", "nexus4_sequences", "*", "*.png"))
+        self.imfs = sorted(imfs)
+
+    def name_of(self, p):
+        s = p.split("/")
+        if "db" in s:
+            return "/".join(s[-2:])
+        if "gopro3_undistorted" in s:
+            return "/".join(s[-3:])
+        return "/".join(s[-4:])
+
+
+class ETH_LFB(_FileDataset):
+    """<data_path>/<subfolder>/images/* (ETH_local_feature.py:20-31)."""
+
+    def __init__(self, configs):
+        super().__init__(configs)
+        self.imfs = sorted(glob.glob(os.path.join(configs["data_path"], configs["subfolder"],
+                                                  "images", "*")))
+
+    def name_of(self, p):
+        return "{}/{}".format(self.configs["subfolder"], os.path.basename(p))
+
+
+class SyntheticImages(Dataset):
+    """Seeded synthetic images for plumbing and benchmarks:
+    ``num_images`` uint8 RandomState(1000+i) images of ``height x width``."""
+
+    def __init__(self, configs):
+        super().__init__()
+        self.configs = configs
+        self.n = int(configs.get("num_images", 8))
+        self.h = int(configs.get("height", 480))
+        self.w = int(configs.get("width", 640))
+
+    def __getitem__(self, item):
+        rs = np.random.RandomState(1000 + item)
+        x, im = to_input(rs.randint(0, 256, (self.h, self.w, 3)).astype(np.uint8))
+        return {"im1": x, "im1_ori": im, "coord1": torch.zeros(0, 2),
+                "name1": "synthetic/%05d.ppm" % item, "pad1": (0, 0, 0, 0)}
+
+    def __len__(self):
+        return self.n
+
+
+class ShardSampler(torch.utils.data.Sampler):
+    """Static image sharding for multi-GPU extraction: rank r takes
+    {i : i mod world == r} -- no padding, no duplicated images (the
+    reference's DistributedSampler pads; extractor.py:95-97)."""
+
+    def __init__(self, n, rank, world):
+        self.idx = list(range(rank, n, world))
+
+    def __iter__(self):
+        return iter(self.idx)
+
+    def __len__(self):
+        return len(self.idx)

@@ -104,3 +104,24 @@ class ExtractionEngine:
             self.close()
         except Exception:
             pass
+
+
+_BB_CACHE = {}
+
+
+def backbone_forward(module, x):
+    """ResUNet.forward through the engine (DescNet.py:64-84 outputs).  The head
+    runs with zero weights and its outputs are discarded."""
+    from . import weights
+    key = (id(module), tuple(p._version for p in module.state_dict(keep_vars=True).values()),
+           str(x.device))
+    eng = _BB_CACHE.get(key)
+    if eng is None:
+        for k in [k for k in _BB_CACHE if k[0] == id(module)]:
+            del _BB_CACHE[k]
+        zero_head = {k: torch.zeros(s) for k, s in weights.head_param_shapes()}
+        eng = ExtractionEngine(module.state_dict(), zero_head, device=x.device)
+        _BB_CACHE[key] = eng
+    out = eng.run(x.float(), outputs=("local_map", "global_map", "local_map_small"))
+    return {"global_map": out["global_map"], "local_map": out["local_map"],
+            "local_map_small": out["local_map_small"]}

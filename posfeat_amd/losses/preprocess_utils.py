@@ -1,0 +1,81 @@
+"""Drop-in for the hot-path functions of losses/preprocess_utils.py.
+
+Same names, arguments and return shapes as the reference; GPU tensors go
+through the HIP kernels of libposfeat_hip.so.  Options the reference's
+configs never select (stable=False gumbel sampling, 'softnms') raise
+NotImplementedError rather than fall back.
+
+  normalize_coords      preprocess_utils.py:14-26
+  denormalize_coords    preprocess_utils.py:28-38
+  sample_feat_by_coord  preprocess_utils.py:40-53
+  gen_grid              preprocess_utils.py:84-87
+  generate_kpts_single  preprocess_utils.py:215-278
+  nms                   preprocess_utils.py:449-464
+  mnn_matcher           preprocess_utils.py:795-803
+"""
+import torch
+
+from .. import ops
+
+
+def homogenize(coord):
+    return torch.cat((coord, torch.ones_like(coord[..., [0]])), -1)
+
+
+def normalize_coords(coord, h, w):
+    c = torch.tensor([(w - 1) / 2.0, (h - 1) / 2.0], dtype=torch.float32, device=coord.device)
+    return (coord - c) / c
+
+
+def denormalize_coords(coord_norm, h, w):
+    c = torch.tensor([(w - 1) / 2.0, (h - 1) / 2.0], dtype=torch.float32,
+                     device=coord_norm.device)
+    return coord_norm * c + c
+
+
+def gen_grid(h_min, h_max, w_min, w_max, len_h, len_w):
+    x = torch.linspace(w_min, w_max, len_w)
+    y = torch.linspace(h_min, h_max, len_h)
+    yy, xx = torch.meshgrid(y, x, indexing="ij")
+    return torch.stack((xx, yy), -1).reshape(-1, 2).float()
+
+
+def sample_feat_by_coord(x, coord_n, norm=False, nhwc=None):
+    """x: [b,c,h,w] feature map, coord_n: [b,n,2] -> [b,n,c].
+
+    ``nhwc`` (optional) is an NHWC copy of ``x`` (e.g. the engine's
+    ``ExtractOutputs.local_map_nhwc``); without it the map is relaid out once
+    by the HIP layout kernel."""
+    b, c, h, w = x.shape
+    if nhwc is None:
+        nhwc = ops.nchw_to_nhwc(x.float().contiguous())
+    return ops.sample_desc_nhwc(nhwc, coord_n.float(), c=c, normalize=bool(norm))
+
+
+def generate_kpts_single(kp_map, nms_radius, num_pts=False, scale=4, stable=True, temperature=1,
+                         stride=1, use_nms=True, thr=False, thr_mod="mean"):
+    if not stable:
+        raise NotImplementedError("stable=False (gumbel sampling) is not implemented")
+    if use_nms == "softnms":
+        raise NotImplementedError("use_nms='softnms' is not implemented")
+    if stride != 1:
+        raise NotImplementedError("stride != 1 is not implemented")
+    _, coord, score, _, _ = ops.detect(kp_map.float().contiguous(), nms_radius, num_pts,
+                                       use_nms=bool(use_nms), thr=thr, thr_mod=thr_mod)
+    return coord, score
+
+
+def nms(score, patch_radius):
+    """Bool mask of window maxima of ``score`` [b,1,h,w] (reflect padding,
+    first-occurrence tie rule; preprocess_utils.py:449-464)."""
+    return ops.nms_mask(score.float().contiguous(), patch_radius)
+
+
+def mnn_matcher(descriptors_a, descriptors_b):
+    sim = descriptors_a @ descriptors_b.t()
+    nn12 = torch.max(sim, dim=1)[1]
+    nn21 = torch.max(sim, dim=0)[1]
+    ids1 = torch.arange(0, sim.shape[0], device=sim.device)
+    mask = ids1 == nn21[nn12]
+    matches = torch.stack([ids1[mask], nn12[mask]])
+    return matches.t().data.cpu().numpy()

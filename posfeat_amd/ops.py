@@ -138,6 +138,17 @@ def detect(kp_map, nms_radius, num_pts=False, use_nms=True, thr=False, thr_mod="
     return idx[:, :n], coord[:, :n], score[:, :n], counts, n
 
 
+def nms_mask(score, radius):
+    """score [b,1,h,w] -> bool mask [b,1,h,w] (reference nms tie rule)."""
+    _f32(score, "score")
+    b, c, h, w = score.shape
+    if c != 1:
+        raise ValueError("score must have one channel")
+    m = torch.empty(b, 1, h, w, dtype=torch.uint8, device=score.device)
+    check(lib().posfeat_nms_mask(ptr(score), b, h, w, int(radius), ptr(m), stream_ptr()))
+    return m.bool()
+
+
 def sample_desc_nhwc(fmap_nhwc, coord_n, c=None, normalize=True, n_valid=None):
     """Bilinear (align_corners=False, zeros) sampling of an NHWC map at coord_n [b,n,2]."""
     _f32(fmap_nhwc, "fmap")

@@ -1,0 +1,29 @@
+"""Multi-GPU plumbing for the extraction path.
+
+Extraction shards images across ranks with no data-path collective; the only
+collective is making every rank hold rank 0's weights.  All float tensors of
+the given state dicts are flattened into ONE buffer and sent with a single
+broadcast (RCCL over xGMI on the GPU box, gloo in CPU tests) -- one large
+message instead of the reference DDP's per-parameter broadcast at wrap time
+and its per-forward buffer broadcasts (PoSFeat_model.py:48-55).
+"""
+import torch
+import torch.distributed as dist
+
+
+def broadcast_weights(state_dicts, device, src=0):
+    """In-place broadcast of every tensor in ``state_dicts`` from ``src``."""
+    floats, ints = [], []
+    for sd in state_dicts:
+        for k, v in sd.items():
+            (floats if v.is_floating_point() else ints).append(v)
+    for group, dtype in ((floats, torch.float32), (ints, torch.int64)):
+        if not group:
+            continue
+        flat = torch.cat([t.detach().reshape(-1).to(dtype) for t in group]).to(device)
+        dist.broadcast(flat, src=src)
+        off = 0
+        for t in group:
+            n = t.numel()
+            t.data.copy_(flat[off:off + n].view(t.shape).to(t.device, t.dtype))
+            off += n

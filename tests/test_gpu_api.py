@@ -1,0 +1,150 @@
+"""GPU tests of the drop-in Python surfaces (networks.PoSFeat, losses.
+preprocess_utils, managers.extractor.Extractor, extract.py) -- each checked
+against the oracle / golden vectors."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, ROOT
+
+pytestmark = pytest.mark.gpu
+
+MODEL_CONFIG = {
+    "backbone": "ResUNet",
+    "backbone_config": {"encoder": "resnet50", "pretrained": True, "coarse_out_ch": 128,
+                        "fine_out_ch": 128},
+    "localheader": "KeypointDet",
+    "localheader_config": {"in_channels": 192, "prior": "identity", "act": "Softplus"},
+    "align_local_grad": False,
+    "local_input_elements": ["local_map", "local_map_small"],
+    "local_with_img": True,
+}
+
+
+@pytest.fixture(scope="module")
+def model():
+    from posfeat_amd import networks
+    m = networks.PoSFeat(MODEL_CONFIG, torch.device("cuda"))
+    m.set_eval()
+    return m
+
+
+def test_posfeat_extract_matches_golden(gpu, model):
+    from posfeat_amd.weights import seeded_image
+    d = np.load(os.path.join(GOLDEN, "model_small.npz"))
+    img = torch.from_numpy(seeded_image(0, 96, 128))[None].to(gpu)
+    out = model.extract(img)
+    assert set(out.keys()) == {"local_map", "global_map", "global_feat", "local_point",
+                               "local_thr", "global_point"}
+    assert out["local_thr"].abs().sum() == 0 and out["global_point"].shape == (1, 1, 6, 8)
+    for k in ("local_map", "global_map", "local_point", "global_feat"):
+        ref = d["a_" + k]
+        err = np.abs(out[k].cpu().numpy() - ref).max()
+        assert err <= 1e-4 * max(1.0, np.abs(ref).max()), k
+
+
+def test_checkpoint_roundtrip(gpu, model, tmp_path):
+    from posfeat_amd import networks
+    from posfeat_amd.weights import seeded_image, seeded_state_dicts
+    bb, hd = seeded_state_dicts(3)
+    model2 = networks.PoSFeat(MODEL_CONFIG, torch.device("cuda"))
+    model2.backbone.load_state_dict(bb)
+    model2.localheader.load_state_dict(hd)
+    model2.save_checkpoint(str(tmp_path))
+    assert sorted(os.listdir(tmp_path)) == ["backbone.pth", "localheader.pth"]
+    model3 = networks.PoSFeat(MODEL_CONFIG, torch.device("cuda"))
+    model3.load_checkpoint(str(tmp_path))
+    model2.set_eval()
+    model3.set_eval()
+    img = torch.from_numpy(seeded_image(5, 64, 96))[None].to(gpu)
+    a = model2.extract(img)["local_point"]
+    b = model3.extract(img)["local_point"]
+    assert torch.equal(a, b)
+    c = model.extract(img)["local_point"]   # different weights -> different map
+    assert not torch.equal(a, c)
+    # DDP-prefixed checkpoints load too
+    sd = {"module." + k: v for k, v in torch.load(tmp_path / "backbone.pth").items()}
+    torch.save(sd, tmp_path / "backbone.pth")
+    model3.load_checkpoint(str(tmp_path))
+    assert torch.equal(model3.extract(img)["local_point"], a)
+
+
+def test_resunet_forward(gpu, model):
+    from oracle import model_ref
+    from posfeat_amd.weights import seeded_image
+    img = torch.from_numpy(seeded_image(2, 64, 96))[None]
+    out = model.backbone(img.to(gpu))
+    ref = model_ref.resunet_forward(model.backbone.state_dict(), img)
+    for k in ("global_map", "local_map", "local_map_small"):
+        err = (out[k].cpu() - ref[k]).abs().max().item()
+        assert err <= 1e-4 * max(1.0, ref[k].abs().max().item()), k
+
+
+def test_preprocess_utils_dropins(gpu):
+    from oracle import detect_ref
+    from posfeat_amd.losses import preprocess_utils as pu
+    km = np.random.RandomState(9).rand(2, 1, 96, 128).astype(np.float32)
+    coord, score = pu.generate_kpts_single(torch.from_numpy(km).to(gpu), 1, 300, thr=0.9,
+                                           thr_mod="abs")
+    c_ref, s_ref = detect_ref.generate_kpts_single(km, 1, 300, thr=0.9, thr_mod="abs")
+    np.testing.assert_array_equal(score.cpu().numpy(), s_ref)
+    np.testing.assert_allclose(coord.cpu().numpy(), c_ref, atol=1e-5)
+    d = np.load(os.path.join(GOLDEN, "detector.npz"))
+    for j in range(4):
+        m = d["crafted%d_map" % j]
+        for r in (1, 2, 3):
+            got = pu.nms(torch.from_numpy(m).to(gpu), r)[0, 0].cpu().numpy()
+            np.testing.assert_array_equal(got, detect_ref.nms(m[0, 0], r))
+    s = np.load(os.path.join(GOLDEN, "sampler.npz"))
+    fmap = torch.from_numpy(np.random.RandomState(11).randn(2, 128, 24, 32).astype(np.float32))
+    desc = pu.sample_feat_by_coord(fmap.to(gpu), torch.from_numpy(s["coords"]).to(gpu), True)
+    np.testing.assert_allclose(desc.cpu().numpy(), s["desc_norm"], atol=1e-5)
+    with pytest.raises(NotImplementedError):
+        pu.generate_kpts_single(torch.from_numpy(km).to(gpu), 1, 300, stable=False)
+
+
+def test_extract_cli_synthetic(gpu, tmp_path):
+    """extract.py end to end on the synthetic config: npz files in the
+    reference format, identical (near-tie aware) to the oracle's process()."""
+    import yaml
+    cfg = yaml.safe_load(open(os.path.join(ROOT, "configs", "extract_synthetic.yaml")))
+    cfg["data_config_extract"].update(num_images=2, height=128, width=160)
+    cfg["detector_config"]["num_pts"] = 512
+    p = tmp_path / "cfg.yaml"
+    yaml.safe_dump(cfg, open(p, "w"))
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "extract.py"), "--config", str(p)],
+                       cwd=tmp_path, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out_dir = tmp_path / "ckpts" / cfg["output_root"] / "desc" / "synthetic"
+    files = sorted(os.listdir(out_dir))
+    assert files == ["00000.ppm.PoSFeat_seeded", "00001.ppm.PoSFeat_seeded"]
+    from oracle import model_ref, detect_ref
+    from posfeat_amd.datasets import SyntheticImages
+    from posfeat_amd.weights import seeded_state_dicts
+    from near_tie import explain_differences
+    bb, hd = seeded_state_dicts(0)
+    ds = SyntheticImages(cfg["data_config_extract"])
+    for i, f in enumerate(files):
+        z = np.load(out_dir / f)
+        assert z["keypoints"].dtype == np.float32 and z["keypoints"].shape[1] == 2
+        assert z["scores"].shape == (z["keypoints"].shape[0], 1)
+        assert z["descriptors"].shape == (z["keypoints"].shape[0], 128)
+        np.testing.assert_allclose(np.linalg.norm(z["descriptors"], axis=1), 1.0, atol=1e-5)
+        img = ds[i]["im1"][None]
+        o = model_ref.posfeat_extract(bb, hd, img)
+        ref = detect_ref.process_image(o["local_point"].numpy(), o["local_map"].numpy(),
+                                       cfg["detector_config"], 128, 160)
+        assert z["keypoints"].shape[0] == ref["kpt"].shape[0]
+        # match keypoints by position: common ones must agree in desc/score
+        kp = np.round(z["keypoints"], 3)
+        rk = np.round(ref["kpt"], 3)
+        common = {tuple(k): j for j, k in enumerate(rk)}
+        hit = [(i2, common[tuple(k)]) for i2, k in enumerate(kp) if tuple(k) in common]
+        assert len(hit) >= 0.97 * len(kp)
+        a, b = np.array(hit).T
+        np.testing.assert_allclose(z["descriptors"][a], ref["desc"][0][b], atol=1e-4)
+        np.testing.assert_allclose(z["scores"][a], ref["kp_score"][0][b], atol=1e-4)

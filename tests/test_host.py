@@ -1,0 +1,100 @@
+"""CPU tests of the host-side logic: dataset input contract, sharding,
+config plumbing, loud failure without a GPU, and the multi-process
+weight-broadcast + image-sharding protocol on gloo (world_size 2)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import ROOT
+
+
+def test_to_input_matches_reference_transform():
+    """ToTensor + Normalize(ImageNet) + crop to /16 (datasets/hpatches.py:14-17, 35-38)."""
+    from posfeat_amd.datasets import to_input
+    im = np.random.RandomState(0).randint(0, 256, (37, 50, 3)).astype(np.uint8)
+    x, crop = to_input(im)
+    assert x.shape == (3, 32, 48) and crop.shape == (32, 48, 3)
+    t = torch.from_numpy(im).permute(2, 0, 1).float() / 255.0
+    mean = torch.tensor([0.485, 0.456, 0.406])[:, None, None]
+    std = torch.tensor([0.229, 0.224, 0.225])[:, None, None]
+    ref = ((t - mean) / std)[:, :32, :48]
+    assert torch.allclose(x, ref, atol=1e-6)
+
+
+def test_hpatches_discovery(tmp_path):
+    from PIL import Image
+    from posfeat_amd.datasets import HPatch_SIFT
+    for seq in ("i_ajuntament", "v_boat"):
+        os.makedirs(tmp_path / seq)
+        for k in (1, 2):
+            Image.fromarray(np.zeros((40, 52, 3), np.uint8)).save(tmp_path / seq / ("%d.ppm" % k))
+    ds = HPatch_SIFT({"data_path": str(tmp_path)})
+    assert len(ds) == 4
+    it = ds[3]
+    assert it["name1"] == "v_boat/2.ppm" and it["im1"].shape == (3, 32, 48)
+    assert it["coord1"].shape == (0, 2)
+
+
+def test_shard_sampler_disjoint_cover():
+    from posfeat_amd.datasets import ShardSampler
+    for world in (1, 2, 3, 8):
+        got = sorted(i for r in range(world) for i in ShardSampler(21, r, world))
+        assert got == list(range(21))
+
+
+def test_no_cpu_fallback():
+    """Without a GPU the product path raises instead of running on the CPU."""
+    if torch.cuda.is_available():
+        pytest.skip("has a GPU")
+    from posfeat_amd import ops
+    with pytest.raises(RuntimeError):
+        ops.detect(torch.rand(1, 1, 16, 16), 1, 128)
+    from posfeat_amd.losses import preprocess_utils as pu
+    with pytest.raises(RuntimeError):
+        pu.sample_feat_by_coord(torch.rand(1, 8, 4, 4), torch.zeros(1, 3, 2), True)
+
+
+def test_configs_have_reference_keys():
+    import yaml
+    for name in ("extract_hpatches", "extract_aachen", "extract_ETH", "extract_synthetic"):
+        c = yaml.safe_load(open(os.path.join(ROOT, "configs", name + ".yaml")))
+        for k in ("output_root", "postfix", "load_path", "loss_distance", "output_desc", "model",
+                  "model_config", "data", "data_config_extract", "use_sift", "detector",
+                  "detector_config"):
+            assert k in c, (name, k)
+        assert c["detector"] == "generate_kpts_single"
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from posfeat_amd.datasets import ShardSampler
+    from posfeat_amd.parallel import broadcast_weights
+    from posfeat_amd.weights import seeded_state_dicts
+    # rank 0 holds the real weights, the others garbage -> broadcast fixes it
+    bb, hd = seeded_state_dicts(0 if rank == 0 else 7)
+    broadcast_weights([bb, hd], device="cpu")
+    ref_bb, ref_hd = seeded_state_dicts(0)
+    ok = all(torch.equal(bb[k], ref_bb[k]) for k in bb) and \
+        all(torch.equal(hd[k], ref_hd[k]) for k in hd)
+    shard = list(ShardSampler(10, rank, world))
+    q.put((rank, ok, shard))
+    dist.destroy_process_group()
+
+
+def test_gloo_broadcast_and_shard():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + os.getpid() % 1000
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(60)
+    assert all(ok for _, ok, _ in res)
+    assert sorted(res[0][2] + res[1][2]) == list(range(10))
