@@ -51,7 +51,8 @@ int posfeat_device_ok(void);
  *   networks/DescNet.py:167-179 (conv), 182-190 (upconv's conv) and the
  *   torchvision Bottleneck convs behind DescNet.py:27-35; and the bias-only
  *   convs of networks/DeteNet.py:11-21.
- * x: NHWC, pixel stride x_cstride >= cin (cin multiple of 4).
+ * x: NHWC, pixel stride x_cstride >= cin (cin multiple of 4); cout, y/res
+ *    strides multiple of 4 and x/w/y/res/bias 16-B aligned (vector epilogue).
  * w: packed [cout][Kpad], K ordered (kh, kw, cin), Kpad = roundup(K, 32),
  *    zero-padded (posfeat_conv_packed_k).  BN already folded into w/bias.
  * y[p, c] = act(sum + bias[c] + res[p, c])   (res may be NULL)
@@ -69,6 +70,22 @@ typedef struct {
 int posfeat_conv_packed_k(int cin, int kh, int kw); /* returns Kpad */
 int posfeat_conv2d_nhwc(const posfeat_conv_desc *d, const float *x, const float *w,
                         const float *bias, const float *res, float *y, void *stream);
+/* Same, allowed to split K over workgroups (deterministic: fp32 partial slabs
+ * summed in split order by a second kernel) when the tile count would leave
+ * the last wave of workgroups underfilled.  Scratch: *_workspace bytes
+ * (0 = this shape never splits). */
+size_t posfeat_conv2d_workspace(const posfeat_conv_desc *d);
+int posfeat_conv2d_nhwc_ws(const posfeat_conv_desc *d, const float *x, const float *w,
+                           const float *bias, const float *res, float *y, void *ws,
+                           size_t ws_bytes, void *stream);
+/* Conv (no residual, no activation) whose epilogue also reduces per-tile
+ * channel sums for InstanceNorm2d (networks/DeteNet.py:12-22): writes y and
+ * mean/rstd [n][cout] of y over each image (biased var, rstd=1/sqrt(var+eps)).
+ * Needs out-height*out-width >= 128 (returns POSFEAT_E_UNSUPPORTED otherwise). */
+size_t posfeat_conv2d_stats_workspace(const posfeat_conv_desc *d);
+int posfeat_conv2d_nhwc_stats(const posfeat_conv_desc *d, const float *x, const float *w,
+                              const float *bias, float *y, void *ws, size_t ws_bytes,
+                              float *mean, float *rstd, float eps, void *stream);
 
 /* ------------------------------------------------------------------------
  * Keypoint selection.

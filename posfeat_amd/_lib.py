@@ -42,6 +42,13 @@ SIGNATURES = {
     "posfeat_conv_packed_k": (c_int, [c_int, c_int, c_int]),
     "posfeat_conv2d_nhwc": (c_int, [ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_void_p,
                                     c_void_p, c_void_p, c_void_p]),
+    "posfeat_conv2d_workspace": (c_size_t, [ctypes.POINTER(ConvDesc)]),
+    "posfeat_conv2d_nhwc_ws": (c_int, [ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_void_p,
+                                       c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "posfeat_conv2d_stats_workspace": (c_size_t, [ctypes.POINTER(ConvDesc)]),
+    "posfeat_conv2d_nhwc_stats": (c_int, [ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_void_p,
+                                          c_void_p, c_void_p, c_size_t, c_void_p, c_void_p,
+                                          c_float, c_void_p]),
     "posfeat_detect_workspace": (c_int, [c_int, c_int, c_int, c_int, ctypes.POINTER(c_size_t)]),
     "posfeat_detect": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int,
                                c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -5,17 +5,20 @@
 //   K0 (thr 'max'/'mean' only) per-image threshold statistic
 //   K1 det_mask    : reflect-padded NMS with the first-occurrence tie rule,
 //                    threshold, order-preserving uint32 key of the masked
-//                    score, per-image survivor count
+//                    score; survivors compacted (wave ballot + one atomic per
+//                    block) into a per-image candidate list, whose length is
+//                    the survivor count
 //   K2 det_select  : one workgroup per image -- n = clamp(min count), 4-pass
-//                    8-bit radix select of the n-th largest key in LDS
-//                    histograms, then an ordered (ascending index) ballot
-//                    compaction of the n selected cells
+//                    8-bit radix select of the n-th largest key over the
+//                    candidates only (masked-out cells are counted, not
+//                    read); keys == T resolved by smallest index
 //   K3 det_rank    : rank each selected cell by (key desc, index asc) with an
-//                    LDS-tiled counting sort (n^2 compares, exact, no
-//                    atomics), compute the 3x3 soft-argmax refine and 3x3 max
-//                    score and scatter to the output row = rank
+//                    LDS-tiled counting sort (n^2 compares, exact; the
+//                    selected list may be in any order), compute the 3x3
+//                    soft-argmax refine and 3x3 max score and scatter to the
+//                    output row = rank
 // Everything is integer/compare work, so the result is bit-exact and
-// deterministic.
+// deterministic (the candidate order depends on atomics; the output does not).
 #include "common.h"
 
 namespace {
@@ -92,35 +95,55 @@ __global__ void nms_mask_kernel(const float* __restrict__ score, int h, int w, i
 
 __global__ void det_mask_kernel(const float* __restrict__ kp, int h, int w, int r, int use_nms,
                                 int use_thr, const float* __restrict__ thr_t,
-                                uint32_t* __restrict__ keys, int32_t* __restrict__ counts) {
+                                uint32_t* __restrict__ keys, uint32_t* __restrict__ cand_key,
+                                int32_t* __restrict__ cand_idx, int32_t* __restrict__ counts) {
   const int b = blockIdx.y;  // one image per grid row: block-uniform counter
   const int Hi = h - 2, Wi = w - 2, P = Hi * Wi;
   const float* m = kp + (long long)b * h * w;
   const float t = use_thr ? thr_t[b] : 0.f;
-  int local = 0;
-  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
-    const int i = p / Wi, j = p - (p / Wi) * Wi;
-    const float S = m[(i + 1) * w + j + 1];
-    bool keep = use_thr ? (S > t) : true;
-    if (keep && use_nms) keep = nms_keep(m, w, Hi, Wi, 1, i, j, r, S);
-    keys[(long long)b * P + p] = pf_fkey(keep ? S : 0.0f);
-    local += keep ? 1 : 0;
-  }
-  // block reduce, one atomic per block
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) local += __shfl_xor(local, o, 64);
-  __shared__ int wsum[16];
-  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = local;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int s = 0;
-    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) s += wsum[k];
-    if (s) atomicAdd(&counts[b], s);
+  __shared__ uint32_t s_key[1024];
+  __shared__ int32_t s_idx[1024];
+  __shared__ int s_cnt, s_base;
+  const int lane = threadIdx.x & 63;
+  const int stride = gridDim.x * blockDim.x;
+  for (int base = blockIdx.x * blockDim.x; base < P; base += stride) {
+    if (threadIdx.x == 0) s_cnt = 0;
+    __syncthreads();
+    const int p = base + threadIdx.x;
+    bool keep = false;
+    uint32_t key = 0x80000000u;
+    if (p < P) {
+      const int i = p / Wi, j = p - (p / Wi) * Wi;
+      const float S = m[(i + 1) * w + j + 1];
+      keep = use_thr ? (S > t) : true;
+      if (keep && use_nms) keep = nms_keep(m, w, Hi, Wi, 1, i, j, r, S);
+      key = pf_fkey(keep ? S : 0.0f);
+      keys[(long long)b * P + p] = key;
+    }
+    // wave-aggregated LDS compaction of the survivors
+    const unsigned long long bal = __ballot(keep);
+    int wbase = 0;
+    if (lane == 0 && bal) wbase = atomicAdd(&s_cnt, __popcll(bal));
+    wbase = __shfl(wbase, 0, 64);
+    if (keep) {
+      const int o = wbase + __popcll(bal & ((1ull << lane) - 1ull));
+      s_key[o] = key;
+      s_idx[o] = p;
+    }
+    __syncthreads();
+    const int cnt = s_cnt;
+    if (threadIdx.x == 0 && cnt) s_base = atomicAdd(&counts[b], cnt);
+    __syncthreads();
+    for (int k = threadIdx.x; k < cnt; k += blockDim.x) {
+      cand_key[(long long)b * P + s_base + k] = s_key[k];
+      cand_idx[(long long)b * P + s_base + k] = s_idx[k];
+    }
+    __syncthreads();
   }
 }
 
-// block-wide exclusive scan of per-thread 0/1 flags in ascending thread order
-// (1024 threads = 16 waves).  Returns the exclusive prefix, sets *total.
+// block-wide exclusive scan of per-thread 0/1 flags in ascending thread order.
+// Returns the exclusive prefix, sets *total.
 __device__ __forceinline__ int block_scan_flag(bool f, int* wsum, int* total) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const unsigned long long bal = __ballot(f);
@@ -139,18 +162,37 @@ __device__ __forceinline__ int block_scan_flag(bool f, int* wsum, int* total) {
   return off + pre;
 }
 
+// One workgroup per image.  Selects the n cells ranking first by (key desc,
+// index asc) among all P inner cells: the survivors live in the candidate
+// list, every other cell has the masked-out key ZKEY.
+//   1. n = clamp(min count); 8-bit radix select of the n-th key over the
+//      candidates + (P - count) virtual ZKEY entries
+//   2. take every key > T (all candidates when T >= ZKEY); of the keys == T
+//      take the need_eq with the smallest index (candidates sorted in LDS, or
+//      an ascending scan of the full key array when T == ZKEY)
+//   3. rare T < ZKEY (negative kept scores, n close to P): ascending scan of
+//      the full key array, as in the single-pass formulation
 __global__ __launch_bounds__(1024) void det_select_kernel(
-    const uint32_t* __restrict__ keys, int nb, int P, const int32_t* __restrict__ counts,
+    const uint32_t* __restrict__ keys, const uint32_t* __restrict__ cand_key,
+    const int32_t* __restrict__ cand_idx, int nb, int P, const int32_t* __restrict__ counts,
     int num_pts, int cap, int32_t* __restrict__ sel, uint32_t* __restrict__ selkey,
     int32_t* __restrict__ n_sel) {
   const int b = blockIdx.x;
+  const uint32_t ZKEY = 0x80000000u;
   const uint32_t* kb = keys + (long long)b * P;
+  const uint32_t* ck = cand_key + (long long)b * P;
+  const int32_t* ci = cand_idx + (long long)b * P;
+  int32_t* so = sel + (long long)b * cap;
+  uint32_t* sko = selkey + (long long)b * cap;
   __shared__ int hist[256];
   __shared__ int wsum[16];
   __shared__ uint32_t s_prefix;
-  __shared__ int s_krem;
-  __shared__ int s_n;
+  __shared__ int s_krem, s_n, s_taken;
+  __shared__ int s_eqidx[1024];
+  __shared__ int s_eqn;
   const int tid = threadIdx.x;
+  const int count = counts[b];
+  const int nzero = P - count;  // masked-out cells, key ZKEY
   if (tid == 0) {
     int minc = counts[0];
     for (int k = 1; k < nb; ++k) minc = min(minc, counts[k]);
@@ -161,6 +203,8 @@ __global__ __launch_bounds__(1024) void det_select_kernel(
     s_n = n;
     s_krem = n;
     s_prefix = 0u;
+    s_taken = 0;
+    s_eqn = 0;
     if (b == 0) *n_sel = n;
   }
   __syncthreads();
@@ -170,15 +214,11 @@ __global__ __launch_bounds__(1024) void det_select_kernel(
     for (int k = tid; k < 256; k += blockDim.x) hist[k] = 0;
     __syncthreads();
     const uint32_t prefix = s_prefix;
-    const uint32_t ZKEY = 0x80000000u;  // key of a masked-out (0.0) cell
-    const bool zmatch = (ZKEY & pmask) == prefix;
-    for (int base = 0; base < P; base += blockDim.x) {
-      const int p = base + tid;
-      const uint32_t k = p < P ? kb[p] : ZKEY ^ 1u;
-      const bool z = p < P && k == ZKEY;
-      const unsigned long long zb = __ballot(z);
-      if (zmatch && (tid & 63) == 0 && zb) atomicAdd(&hist[(ZKEY >> shift) & 0xFF], __popcll(zb));
-      if (p < P && !z && (k & pmask) == prefix) atomicAdd(&hist[(k >> shift) & 0xFF], 1);
+    if (tid == 0 && nzero > 0 && (ZKEY & pmask) == prefix)
+      atomicAdd(&hist[(ZKEY >> shift) & 0xFF], nzero);
+    for (int k = tid; k < count; k += blockDim.x) {
+      const uint32_t key = ck[k];
+      if ((key & pmask) == prefix) atomicAdd(&hist[(key >> shift) & 0xFF], 1);
     }
     __syncthreads();
     if (tid == 0) {
@@ -195,7 +235,65 @@ __global__ __launch_bounds__(1024) void det_select_kernel(
   }
   const uint32_t T = s_prefix;
   const int need_eq = s_krem;  // how many keys == T are taken (>= 1)
-  // ordered compaction: keys > T, plus the first need_eq keys == T by index
+  if (T > ZKEY) {
+    // (a) every candidate key > T; collect the == T ones
+    for (int k = tid; k < count; k += blockDim.x) {
+      const uint32_t key = ck[k];
+      if (key > T) {
+        const int pos = atomicAdd(&s_taken, 1);
+        so[pos] = ci[k];
+        sko[pos] = key;
+      } else if (key == T) {
+        const int e = atomicAdd(&s_eqn, 1);
+        if (e < 1024) s_eqidx[e] = ci[k];
+      }
+    }
+    __syncthreads();
+    const int neq = s_eqn;
+    if (neq <= 1024) {
+      const int base = s_taken;
+      // (b) the need_eq smallest indices among the equal keys (rank by index)
+      for (int e = tid; e < neq; e += blockDim.x) {
+        const int my = s_eqidx[e];
+        int rk = 0;
+        for (int f = 0; f < neq; ++f) rk += s_eqidx[f] < my;
+        if (rk < need_eq) {
+          so[base + rk] = my;
+          sko[base + rk] = T;
+        }
+      }
+      return;
+    }
+    // > 1024 exact ties at the cut: fall through to the ordered scan (rewrites)
+  }
+  else if (T == ZKEY) {
+    // all positive candidates, then the need_eq lowest-index cells with key ZKEY
+    for (int k = tid; k < count; k += blockDim.x) {
+      const uint32_t key = ck[k];
+      if (key > ZKEY) {
+        const int pos = atomicAdd(&s_taken, 1);
+        so[pos] = ci[k];
+        sko[pos] = key;
+      }
+    }
+    __syncthreads();
+    int taken = s_taken, eq_seen = 0;
+    for (int base = 0; base < P && eq_seen < need_eq; base += blockDim.x) {
+      const int p = base + tid;
+      const bool eq = p < P && kb[p] == ZKEY;
+      int tot;
+      const int pre = block_scan_flag(eq, wsum, &tot);
+      if (eq && eq_seen + pre < need_eq) {
+        so[taken + pre] = p;
+        sko[taken + pre] = ZKEY;
+      }
+      const int add = min(tot, need_eq - eq_seen);
+      eq_seen += add;
+      taken += add;
+    }
+    return;
+  }
+  // T < ZKEY: ordered compaction over the full key array
   int eq_seen = 0, taken = 0;
   for (int base = 0; base < P; base += blockDim.x) {
     const int p = base + tid;
@@ -208,9 +306,8 @@ __global__ __launch_bounds__(1024) void det_select_kernel(
     int tk_tot;
     const int tk_pre = block_scan_flag(take, wsum, &tk_tot);
     if (take) {
-      const int pos = taken + tk_pre;
-      sel[(long long)b * cap + pos] = p;
-      selkey[(long long)b * cap + pos] = k;
+      so[taken + tk_pre] = p;
+      sko[taken + tk_pre] = k;
     }
     eq_seen += eq_tot;
     taken += tk_tot;
@@ -228,18 +325,23 @@ __global__ void det_rank_kernel(const float* __restrict__ kp, int h, int w, int 
   if ((int)(blockIdx.x * blockDim.x) >= n) return;  // block-uniform
   const bool active = t < n;
   const uint32_t* kb = selkey + (long long)b * cap;
+  const int32_t* ib = sel + (long long)b * cap;
   const uint32_t myk = active ? kb[t] : 0u;
+  const int myi = active ? ib[t] : 0;
   __shared__ uint32_t tile[1024];
+  __shared__ int32_t tidx[1024];
   int rank = 0;
   for (int base = 0; base < n; base += 1024) {
-    for (int k = threadIdx.x; k < 1024; k += blockDim.x)
+    for (int k = threadIdx.x; k < 1024; k += blockDim.x) {
       tile[k] = (base + k < n) ? kb[base + k] : 0u;
+      tidx[k] = (base + k < n) ? ib[base + k] : 0;
+    }
     __syncthreads();
     const int lim = min(1024, n - base);
     if (active) {
       for (int k = 0; k < lim; ++k) {
         const uint32_t o = tile[k];
-        rank += (o > myk) || (o == myk && base + k < t);
+        rank += (o > myk) || (o == myk && tidx[k] < myi);
       }
     }
     __syncthreads();
@@ -275,6 +377,8 @@ extern "C" int posfeat_detect_workspace(int b, int h, int w, int cap, size_t* by
   if (b <= 0 || h < 3 || w < 3 || cap <= 0 || !bytes) return POSFEAT_E_INVALID;
   const size_t P = (size_t)(h - 2) * (w - 2);
   size_t s = pf_align((size_t)b * P * sizeof(uint32_t), 256);    // keys
+  s += pf_align((size_t)b * P * sizeof(uint32_t), 256);          // cand_key
+  s += pf_align((size_t)b * P * sizeof(int32_t), 256);           // cand_idx
   s += pf_align((size_t)b * cap * sizeof(int32_t), 256);         // sel
   s += pf_align((size_t)b * cap * sizeof(uint32_t), 256);        // selkey
   s += pf_align((size_t)b * sizeof(float), 256);                 // thr
@@ -300,6 +404,10 @@ extern "C" int posfeat_detect(const float* kp_map, int b, int h, int w, int nms_
   char* base = static_cast<char*>(ws);
   uint32_t* keys = reinterpret_cast<uint32_t*>(base);
   base += pf_align((size_t)b * P * sizeof(uint32_t), 256);
+  uint32_t* cand_key = reinterpret_cast<uint32_t*>(base);
+  base += pf_align((size_t)b * P * sizeof(uint32_t), 256);
+  int32_t* cand_idx = reinterpret_cast<int32_t*>(base);
+  base += pf_align((size_t)b * P * sizeof(int32_t), 256);
   int32_t* sel = reinterpret_cast<int32_t*>(base);
   base += pf_align((size_t)b * cap * sizeof(int32_t), 256);
   uint32_t* selkey = reinterpret_cast<uint32_t*>(base);
@@ -321,14 +429,14 @@ extern "C" int posfeat_detect(const float* kp_map, int b, int h, int w, int nms_
     PF_CHECK_LAUNCH();
   }
   {
-    int g = (P + 255) / 256;
-    if (g > 2048) g = 2048;
-    hipLaunchKernelGGL(det_mask_kernel, dim3(g, b), dim3(256), 0, st, kp_map, h, w, nms_radius,
-                       use_nms, use_thr, thr_t, keys, counts);
+    int g = (P + 1023) / 1024;
+    if (g > 1024) g = 1024;
+    hipLaunchKernelGGL(det_mask_kernel, dim3(g, b), dim3(1024), 0, st, kp_map, h, w, nms_radius,
+                       use_nms, use_thr, thr_t, keys, cand_key, cand_idx, counts);
     PF_CHECK_LAUNCH();
   }
-  hipLaunchKernelGGL(det_select_kernel, dim3(b), dim3(1024), 0, st, keys, b, P, counts, num_pts,
-                     cap, sel, selkey, n_sel);
+  hipLaunchKernelGGL(det_select_kernel, dim3(b), dim3(1024), 0, st, keys, cand_key, cand_idx, b,
+                     P, counts, num_pts, cap, sel, selkey, n_sel);
   PF_CHECK_LAUNCH();
   const int maxn = cap < P ? cap : P;
   hipLaunchKernelGGL(det_rank_kernel, dim3((maxn + 255) / 256, b), dim3(256), 0, st, kp_map, h, w,

@@ -97,6 +97,8 @@ struct posfeat_model {
   Buf c1raw, hcat, c2raw, yraw;
   Buf st_mean, st_rstd, st_part;  // instance-norm scratch (floats / doubles)
   Buf st_mean1, st_rstd1;
+  Buf splitk;                      // split-K partial slabs (max over layers)
+  size_t splitk_need = 0;
   // timing
   bool timing = false;
   struct Ev {
@@ -114,6 +116,7 @@ struct Ctx {
   posfeat_model* m;
   char* ws;
   hipStream_t st;
+  bool dry = false;  // planning pass: record scratch needs, launch nothing
   float* f(const Buf& b) const { return reinterpret_cast<float*>(ws + b.off); }
   double* d(const Buf& b) const { return reinterpret_cast<double*>(ws + b.off); }
   const float* W(const std::string& n) const { return m->wts + specs().find(n)->w_off; }
@@ -124,6 +127,7 @@ struct Ctx {
 template <class F>
 int timed(Ctx& c, const std::string& label, double flops, F&& fn) {
   posfeat_model* m = c.m;
+  if (c.dry) return POSFEAT_OK;
   if (!m->timing) return fn();
   if (m->ev_used == m->evs.size()) {
     posfeat_model::Ev e;
@@ -160,8 +164,57 @@ int conv(Ctx& c, const std::string& name, const float* x, int n, int h, int w, i
   d.act = act;
   const int oh = (h + 2 * d.pad - d.kh) / stride + 1, ow = (w + 2 * d.pad - d.kw) / stride + 1;
   const double flops = 2.0 * n * oh * ow * (double)s->cout * s->cin * s->kh * s->kw;
+  const size_t need = posfeat_conv2d_workspace(&d);
+  if (c.dry) {
+    if (need > c.m->splitk_need) c.m->splitk_need = need;
+    return POSFEAT_OK;
+  }
+  float* part = c.f(c.m->splitk);
+  const size_t have = c.m->splitk.floats * sizeof(float);
   return timed(c, "conv:" + name, flops, [&] {
-    return posfeat_conv2d_nhwc(&d, x, c.W(name), c.Bi(name), res, y, c.st);
+    return posfeat_conv2d_nhwc_ws(&d, x, c.W(name), c.Bi(name), res, y, part, have, c.st);
+  });
+}
+
+int forward(Ctx& c, const float* img, posfeat_extract_out* out);
+
+// conv whose epilogue also produces the InstanceNorm mean/rstd of its output
+// (falls back to a separate statistics pass when a tile could span >2 images)
+int conv_in(Ctx& c, const std::string& name, const float* x, int n, int h, int w, int xcs,
+            float* y, int ycs, float* mean, float* rstd) {
+  const Spec* s = specs().find(name);
+  if (!s) return POSFEAT_E_INVALID;
+  posfeat_conv_desc d;
+  d.n = n;
+  d.h = h;
+  d.w = w;
+  d.cin = (s->cin + 3) / 4 * 4;
+  d.x_cstride = xcs;
+  d.cout = s->cout;
+  d.kh = s->kh;
+  d.kw = s->kw;
+  d.stride = 1;
+  d.pad = (s->kh - 1) / 2;
+  d.y_cstride = ycs;
+  d.res_cstride = 0;
+  d.act = POSFEAT_ACT_NONE;
+  const size_t need = posfeat_conv2d_stats_workspace(&d);
+  if (need == 0 || c.dry) {
+    if (c.dry) {
+      if (need > c.m->splitk_need) c.m->splitk_need = need;
+      return POSFEAT_OK;
+    }
+    PF_TRY(conv(c, name, x, n, h, w, xcs, y, ycs, 1, POSFEAT_ACT_NONE));
+    return timed(c, "instnorm", 0, [&] {
+      return pf_in_stats(y, n, h * w, s->cout, ycs, mean, rstd, c.d(c.m->st_part), c.st);
+    });
+  }
+  const double flops = 2.0 * n * h * w * (double)s->cout * s->cin * s->kh * s->kw;
+  float* part = c.f(c.m->splitk);
+  const size_t have = c.m->splitk.floats * sizeof(float);
+  return timed(c, "conv:" + name, flops, [&] {
+    return posfeat_conv2d_nhwc_stats(&d, x, c.W(name), c.Bi(name), y, part, have, mean, rstd,
+                                     1e-5f, c.st);
   });
 }
 
@@ -201,6 +254,15 @@ void plan(posfeat_model* m) {
   alloc(m->st_rstd1, B * 4);
   const size_t part = pf_in_stats_ws_bytes((int)B, (int)(H * W), 256);
   alloc(m->st_part, part / 4 + 1);
+  // split-K scratch: sized by a dry pass over the forward
+  m->splitk_need = 0;
+  {
+    Ctx c{m, nullptr, nullptr, true};
+    posfeat_extract_out o{};
+    o.local_point = reinterpret_cast<float*>(16);
+    forward(c, reinterpret_cast<const float*>(16), &o);
+  }
+  alloc(m->splitk, m->splitk_need / 4 + 4);
   m->ws_bytes = cur;
 }
 
@@ -286,21 +348,16 @@ int forward(Ctx& c, const float* img, posfeat_extract_out* out) {
   double* part = c.d(m->st_part);
   float* c1 = c.f(m->c1raw);
   float* hcat = c.f(m->hcat);
-  PF_TRY(conv(c, "head.conv1", headcat, B, h4, w4, 192, c1, 192, 1, POSFEAT_ACT_NONE));
-  PF_TRY(timed(c, "instnorm", 0, [&] { return pf_in_stats(c1, B, h4 * w4, 192, 192, mean, rstd, part, c.st); }));
+  PF_TRY(conv_in(c, "head.conv1", headcat, B, h4, w4, 192, c1, 192, mean, rstd));
   PF_TRY(timed(c, "norm_prelu_up4", 0, [&] {
     return pf_norm_prelu_upsample(c1, B, h4, w4, 192, 192, mean, rstd, slope, H, W, hcat, 256, c.st);
   }));
-  PF_TRY(conv(c, "head.convimg", img4, B, H, W, 4, hcat + 192, 256, 1, POSFEAT_ACT_NONE));
-  PF_TRY(timed(c, "instnorm", 0, [&] {
-    return pf_in_stats(hcat + 192, B, H * W, 64, 256, mean, rstd, part, c.st);
-  }));
+  PF_TRY(conv_in(c, "head.convimg", img4, B, H, W, 4, hcat + 192, 256, mean, rstd));
   PF_TRY(timed(c, "instnorm_apply", 0, [&] {
     return pf_in_apply(hcat + 192, B, H * W, 64, 256, mean, rstd, nullptr, c.st);
   }));
   float* c2 = c.f(m->c2raw);
-  PF_TRY(conv(c, "head.conv2", hcat, B, H, W, 256, c2, 128, 1, POSFEAT_ACT_NONE));
-  PF_TRY(timed(c, "instnorm", 0, [&] { return pf_in_stats(c2, B, H * W, 128, 128, mean, rstd, part, c.st); }));
+  PF_TRY(conv_in(c, "head.conv2", hcat, B, H, W, 256, c2, 128, mean, rstd));
   PF_TRY(timed(c, "head_tail", 2.0 * B * H * W * 128, [&] {
     return pf_head_tail(c2, B, H * W, 128, mean, rstd, slope, c.W("head.conv3"),
                         c.Bi("head.conv3"), c.f(m->yraw), out->local_point, c.f(m->st_mean1),

@@ -33,17 +33,22 @@ def pack_conv_weight(w, b=None):
     cinp = (cin + 3) // 4 * 4
     k = kh * kw * cinp
     kpad = packed_k(cin, kh, kw)
-    wp = torch.zeros(cout, kh, kw, cinp, dtype=torch.float32, device=w.device)
-    wp[..., :cin] = w.permute(0, 2, 3, 1).float()
     out = torch.zeros(cout, kpad, dtype=torch.float32, device=w.device)
-    out[:, :k] = wp.reshape(cout, k)
+    if cin % 32 == 0:   # K = (cin/32, kh, kw, cin%32), see conv.hip
+        wp = w.float().reshape(cout, cin // 32, 32, kh, kw).permute(0, 1, 3, 4, 2)
+        out[:, :k] = wp.reshape(cout, k)
+    else:               # K = (kh, kw, cin4), zero-padded
+        wp = torch.zeros(cout, kh, kw, cinp, dtype=torch.float32, device=w.device)
+        wp[..., :cin] = w.permute(0, 2, 3, 1).float()
+        out[:, :k] = wp.reshape(cout, k)
     bias = b.float().contiguous() if b is not None else torch.zeros(cout, device=w.device)
     return out.contiguous(), bias
 
 
 def conv2d_nhwc(x, w_packed, bias, cout, kh, kw, stride=1, pad=None, act="none", res=None,
-                out=None, cin=None):
-    """Fused conv on an NHWC tensor x [n,h,w,cs] (first ``cin`` channels used)."""
+                out=None, cin=None, allow_split=False):
+    """Fused conv on an NHWC tensor x [n,h,w,cs] (first ``cin`` channels used).
+    ``allow_split`` lets the library split K over workgroups (deterministic)."""
     _f32(x, "x")
     n, h, w, xcs = x.shape
     cin = xcs if cin is None else cin
@@ -55,9 +60,37 @@ def conv2d_nhwc(x, w_packed, bias, cout, kh, kw, stride=1, pad=None, act="none",
     d = _lib.ConvDesc(n=n, h=h, w=w, cin=cin, x_cstride=xcs, cout=cout, kh=kh, kw=kw,
                       stride=stride, pad=pad, y_cstride=out.shape[-1],
                       res_cstride=(res.shape[-1] if res is not None else 0), act=ACT[act])
+    if allow_split:
+        need = lib().posfeat_conv2d_workspace(ctypes.byref(d))
+        ws = torch.empty(max(need, 16), dtype=torch.uint8, device=x.device)
+        check(lib().posfeat_conv2d_nhwc_ws(ctypes.byref(d), ptr(x), ptr(_f32(w_packed, "w")),
+                                           ptr(bias), ptr(res), ptr(out), ptr(ws), need,
+                                           stream_ptr()))
+        return out
     check(lib().posfeat_conv2d_nhwc(ctypes.byref(d), ptr(x), ptr(_f32(w_packed, "w")),
                                     ptr(bias), ptr(res), ptr(out), stream_ptr()))
     return out
+
+
+def conv2d_nhwc_instnorm_stats(x, w_packed, bias, cout, kh, kw, eps=1e-5, out=None, cin=None):
+    """Conv (stride 1, 'same' pad, no act) + per-image channel mean/rstd of its
+    output from the fused epilogue.  Returns (y, mean [n,cout], rstd [n,cout])."""
+    _f32(x, "x")
+    n, h, w, xcs = x.shape
+    cin = xcs if cin is None else cin
+    pad = (kh - 1) // 2
+    if out is None:
+        out = torch.empty(n, h, w, cout, device=x.device, dtype=torch.float32)
+    d = _lib.ConvDesc(n=n, h=h, w=w, cin=cin, x_cstride=xcs, cout=cout, kh=kh, kw=kw, stride=1,
+                      pad=pad, y_cstride=out.shape[-1], res_cstride=0, act=0)
+    need = lib().posfeat_conv2d_stats_workspace(ctypes.byref(d))
+    ws = torch.empty(max(need, 16), dtype=torch.uint8, device=x.device)
+    mean = torch.empty(n, cout, device=x.device)
+    rstd = torch.empty(n, cout, device=x.device)
+    check(lib().posfeat_conv2d_nhwc_stats(ctypes.byref(d), ptr(x), ptr(_f32(w_packed, "w")),
+                                          ptr(bias), ptr(out), ptr(ws), need, ptr(mean),
+                                          ptr(rstd), float(eps), stream_ptr()))
+    return out, mean, rstd
 
 
 def nchw_to_nhwc(x, cstride=None):

@@ -208,13 +208,20 @@ def packed_k(cin, kh, kw):
 
 
 def pack_conv(w, b):
-    """[Cout,Cin,KH,KW] -> float32 [Cout][Kpad] with K ordered (kh, kw, cin_pad)."""
+    """[Cout,Cin,KH,KW] -> float32 [Cout][Kpad].
+
+    K order (must match conv.hip): (cin/32, kh, kw, cin%32) when Cin % 32 == 0,
+    else (kh, kw, cin padded to 4) zero-padded to a multiple of 32."""
     cout, cin, kh, kw = w.shape
     cinp, k, kpad = packed_k(cin, kh, kw)
-    wp = np.zeros((cout, kh, kw, cinp), np.float64)
-    wp[:, :, :, :cin] = w.transpose(0, 2, 3, 1)
     out = np.zeros((cout, kpad), np.float32)
-    out[:, :k] = wp.reshape(cout, k)
+    if cin % 32 == 0:
+        wp = w.reshape(cout, cin // 32, 32, kh, kw).transpose(0, 1, 3, 4, 2)
+        out[:, :k] = wp.reshape(cout, k)
+    else:
+        wp = np.zeros((cout, kh, kw, cinp), np.float64)
+        wp[:, :, :, :cin] = w.transpose(0, 2, 3, 1)
+        out[:, :k] = wp.reshape(cout, k)
     return out, b.astype(np.float32)
 
 

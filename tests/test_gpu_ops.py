@@ -74,6 +74,54 @@ def test_conv_vs_torch(gpu, case):
         assert torch.all(out[..., cout:] == 7.0).item(), "wrote outside its channel slice"
 
 
+@pytest.mark.parametrize("act,has_res", [("elu", False), ("relu", True)])
+def test_conv_splitk_vs_torch(gpu, act, has_res):
+    """Deep-K shape that takes the split-K path (partials + ordered reduce)."""
+    import ctypes
+    from posfeat_amd import ops, _lib
+    n, h, w, cin, cout = 1, 20, 24, 1024, 512
+    d = _lib.ConvDesc(n=n, h=h, w=w, cin=cin, x_cstride=cin, cout=cout, kh=3, kw=3, stride=1,
+                      pad=1, y_cstride=cout, res_cstride=cout if has_res else 0, act=0)
+    assert _lib.lib().posfeat_conv2d_workspace(ctypes.byref(d)) > 0, "shape should split"
+    g = torch.Generator().manual_seed(21)
+    x = torch.randn(n, cin, h, w, generator=g)
+    wt = torch.randn(cout, cin, 3, 3, generator=g) * (2.0 / (cin * 9)) ** 0.5
+    b = torch.randn(cout, generator=g) * 0.1
+    res = torch.randn(n, cout, h, w, generator=g) if has_res else None
+    ref, bound = _conv_ref64(x, wt, b, 1, 1, res, act)
+    wp, bp = ops.pack_conv_weight(wt.to(gpu), b.to(gpu))
+    rd = res.permute(0, 2, 3, 1).contiguous().to(gpu) if has_res else None
+    xd = x.permute(0, 2, 3, 1).contiguous().to(gpu)
+    out = ops.conv2d_nhwc(xd, wp, bp, cout, 3, 3, act=act, res=rd, allow_split=True)
+    got = out.permute(0, 3, 1, 2).double().cpu()
+    err = (got - ref).abs()
+    assert torch.all(err <= 2e-6 * bound + 1e-6), "max err %g" % err.max()
+    again = ops.conv2d_nhwc(xd, wp, bp, cout, 3, 3, act=act, res=rd, allow_split=True)
+    assert torch.equal(out, again)
+
+
+@pytest.mark.parametrize("n,h,w,cin,cout", [(3, 20, 28, 64, 128),     # tiles cross images
+                                             (2, 48, 64, 192, 192),
+                                             (1, 96, 80, 4, 64)])
+def test_conv_fused_instnorm_stats(gpu, n, h, w, cin, cout):
+    """Conv epilogue IN statistics == torch instance_norm statistics."""
+    from posfeat_amd import ops
+    g = torch.Generator().manual_seed(n * 7 + h)
+    x = torch.randn(n, cin, h, w, generator=g)
+    wt = torch.randn(cout, cin, 3, 3, generator=g) * (2.0 / (cin * 9)) ** 0.5
+    b = torch.randn(cout, generator=g) + 0.5
+    ref = F.conv2d(x.double(), wt.double(), b.double(), padding=1)
+    mu = ref.mean((2, 3))
+    var = ref.var((2, 3), unbiased=False)
+    xd = x.permute(0, 2, 3, 1).contiguous().to(gpu)
+    wp, bp = ops.pack_conv_weight(wt.to(gpu), b.to(gpu))
+    y, mean, rstd = ops.conv2d_nhwc_instnorm_stats(xd, wp, bp, cout, 3, 3)
+    torch.cuda.synchronize()
+    assert torch.allclose(mean.double().cpu(), mu, atol=1e-5, rtol=1e-5)
+    assert torch.allclose(rstd.double().cpu(), 1.0 / torch.sqrt(var + 1e-5), rtol=1e-4)
+    assert torch.allclose(y.permute(0, 3, 1, 2).double().cpu(), ref, atol=1e-4)
+
+
 def test_conv_deterministic(gpu):
     from posfeat_amd import ops
     g = torch.Generator().manual_seed(3)
@@ -145,6 +193,23 @@ def test_detector_batch_min_count(gpu):
     np.testing.assert_array_equal(idx.cpu().numpy(), i_ref)
     np.testing.assert_array_equal(score.cpu().numpy(), s_ref)
     np.testing.assert_allclose(coord.cpu().numpy(), c_ref, atol=1e-5)
+
+
+def test_detector_many_ties_at_cut(gpu):
+    """> 1024 exactly-equal scores straddling the top-k cut (fallback path) and
+    the masked-zero fill path (n raised to 128)."""
+    from posfeat_amd import ops
+    from oracle import detect_ref
+    rs = np.random.RandomState(4)
+    km = (rs.randint(0, 4, (1, 1, 200, 260)).astype(np.float32) / 3.0).astype(np.float32)
+    for r, n, thr in ((1, 2048, False), (1, 5000, False), (3, 300, 0.5), (2, 64, 0.99)):
+        c_ref, s_ref, i_ref = detect_ref.generate_kpts_single(km, r, n, thr=thr, thr_mod="abs",
+                                                              return_idx=True)
+        idx, coord, score, counts, nn = ops.detect(torch.from_numpy(km).to(gpu), r, n, thr=thr,
+                                                   thr_mod="abs")
+        assert nn == i_ref.shape[1]
+        np.testing.assert_array_equal(idx.cpu().numpy(), i_ref)
+        np.testing.assert_array_equal(score.cpu().numpy(), s_ref)
 
 
 # ------------------------------------------------------------------ sampler

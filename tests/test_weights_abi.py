@@ -59,6 +59,16 @@ def test_pack_layout_kh_kw_cin():
     assert np.all(wp[:, 36:] == 0)
 
 
+def test_pack_layout_chunk_major():
+    from posfeat_amd import weights
+    w = np.random.RandomState(0).randn(3, 64, 3, 3)
+    wp, _ = weights.pack_conv(w, np.zeros(3))
+    assert wp.shape == (3, 576)
+    # K index = ((c // 32) * 9 + kh * 3 + kw) * 32 + c % 32
+    for (o, c, kh, kw) in [(0, 0, 0, 0), (2, 33, 1, 2), (1, 63, 2, 0), (2, 31, 2, 2)]:
+        assert wp[o, ((c // 32) * 9 + kh * 3 + kw) * 32 + c % 32] == np.float32(w[o, c, kh, kw])
+
+
 def _header_functions():
     txt = open(os.path.join(ROOT, "include", "posfeat_hip.h")).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
