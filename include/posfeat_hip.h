@@ -135,6 +135,59 @@ int posfeat_nhwc_to_nchw(const float *x, int n, int c, int h, int w, int cstride
                          float *y, void *stream);
 
 /* ------------------------------------------------------------------------
+ * Training-side dense correlation (forward values).
+ * Replaces: losses/preprocess.py:27-121 Preprocess_Line2Window.forward with
+ *   generate_kpts_regular_grid_random (preprocess_utils.py:598-659, identity
+ *   map), epipolar_line_search (661-694, use_nn, loc_rand), get_endpoints
+ *   (696-719), get_expected_correspondence_within_window (721-758); and
+ *   losses/epipolarloss.py:38-101 EpipolarLoss_full.forward.
+ * xf1/xf2: NHWC local maps [b][H/4][W/4] (128 channels, pixel stride cs).
+ * F1/F2: [b][3][3].  sel1/sel2: [b][n] Categorical draw (0..grid^2-1) per
+ * grid cell; rand1/rand2: [b][n][2] U(0,1) (loc_rand jitter).  The caller owns
+ * the RNG; n = (H/grid)*(W/grid).  Outputs (caller buffers, [b][n][...]):
+ * ------------------------------------------------------------------------ */
+typedef struct {
+  float *coord1, *coord2;       /* grid points, pixels [b][n][2]             */
+  float *g1, *g2;               /* feat{1,2}g_corloc, pixels                 */
+  float *g1_std, *g2_std;       /* feat{1,2}g_std [b][n]                     */
+  float *l1_exp_n, *l2_exp_n;   /* line expectation + jitter, normalised     */
+  float *l1_org_n, *l2_org_n;   /* line expectation before jitter, normalised*/
+  uint8_t *valid1, *valid2;     /* valid_epi{1,2}                            */
+  float *w1, *w2;               /* feat{1,2}w_corloc, pixels                 */
+  float *w1_std, *w2_std;       /* feat{1,2}w_std                            */
+} posfeat_l2w_out;
+
+size_t posfeat_line2window_workspace(int b, int H1, int W1, int H2, int W2, int grid);
+int posfeat_line2window(const float *xf1, int cs1, const float *xf2, int cs2, int b, int H1,
+                        int W1, int H2, int W2, const float *F1, const float *F2,
+                        const int32_t *sel1, const int32_t *sel2, const float *rand1,
+                        const float *rand2, float temperature, int grid, float window_size,
+                        int line_step, posfeat_l2w_out *out, void *ws, size_t ws_bytes,
+                        void *stream);
+/* out[7] = {loss, loss_g1, loss_w1, loss_g2, loss_w2, percent_g, percent_w} */
+int posfeat_epipolar_loss(int b, int n, const float *F1, const float *F2, const float *c1,
+                          const float *c2, const float *g1, const float *g2, const float *w1,
+                          const float *w2, const float *sg1, const float *sg2, const float *sw1,
+                          const float *sw2, const uint8_t *v1, const uint8_t *v2,
+                          float short_edge, float grid_thr, float win_thr, float weight_grid,
+                          float weight_window, float *out, void *stream);
+
+/* DiskLoss forward (losses/kploss.py:132-197, constant_reward, grid 8):
+ * kp1/kp2 [b][H][W] score maps, xf1/xf2 NHWC local maps [b][H/4][W/4] (pixel
+ * stride cs), F1/F2 [b][3][3].  Either prop1,prop2,acc1,acc2 ([b][n] Categorical proposal
+ * 0..63 and Bernoulli acceptance) are given, or uni1/uni2 ([b][n][65] U(0,1):
+ * 64 Gumbel-max uniforms + 1 acceptance uniform) and the kernel samples.
+ * out[4] = {loss, reinforce, kp_penalty, n_kps}. */
+size_t posfeat_disk_loss_workspace(int b, int H, int W);
+int posfeat_disk_loss(const float *kp1, const float *kp2, const float *xf1, int cs1,
+                      const float *xf2, int cs2, int b, int H, int W, const float *F1,
+                      const float *F2, const int32_t *prop1, const int32_t *prop2,
+                      const uint8_t *acc1, const uint8_t *acc2, const float *uni1,
+                      const float *uni2, float temperature, float reward_thr, float good_reward,
+                      float bad_reward, float kp_penalty, float *out, void *ws, size_t ws_bytes,
+                      void *stream);
+
+/* ------------------------------------------------------------------------
  * Whole-model extraction engine.
  * Replaces: networks/PoSFeat_model.py:91-134 PoSFeat.extract for the
  *   effective model ResUNet(resnet50, 128/128) + KeypointDet(192, 1,

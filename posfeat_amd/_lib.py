@@ -34,6 +34,12 @@ class ExtractOut(ctypes.Structure):
                 ("local_map_nhwc", c_void_p), ("local_map_cstride", c_int)]
 
 
+class L2WOut(ctypes.Structure):
+    _fields_ = [(n, c_void_p) for n in ("coord1", "coord2", "g1", "g2", "g1_std", "g2_std",
+                                        "l1_exp_n", "l2_exp_n", "l1_org_n", "l2_org_n", "valid1",
+                                        "valid2", "w1", "w2", "w1_std", "w2_std")]
+
+
 # name -> (restype, argtypes); mirrors include/posfeat_hip.h
 SIGNATURES = {
     "posfeat_strerror": (ctypes.c_char_p, [c_int]),
@@ -60,6 +66,17 @@ SIGNATURES = {
                                      c_void_p]),
     "posfeat_nhwc_to_nchw": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
                                      c_void_p]),
+    "posfeat_line2window_workspace": (c_size_t, [c_int] * 6),
+    "posfeat_line2window": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int,
+                                    c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                    c_void_p, c_float, c_int, c_float, c_int,
+                                    ctypes.POINTER(L2WOut), c_void_p, c_size_t, c_void_p]),
+    "posfeat_epipolar_loss": (c_int, [c_int, c_int] + [c_void_p] * 14 + [c_float] * 5 +
+                              [c_void_p, c_void_p]),
+    "posfeat_disk_loss_workspace": (c_size_t, [c_int, c_int, c_int]),
+    "posfeat_disk_loss": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int,
+                                  c_int, c_int] + [c_void_p] * 8 + [c_float] * 5 +
+                          [c_void_p, c_void_p, c_size_t, c_void_p]),
     "posfeat_model_num_specs": (c_int, []),
     "posfeat_model_conv_spec": (c_int, [c_int, ctypes.POINTER(ctypes.c_char_p), P_int, P_int,
                                         P_int, P_int, ctypes.POINTER(c_ll),

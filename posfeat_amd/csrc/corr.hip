@@ -1,0 +1,549 @@
+// corr.hip -- training-side dense descriptor correlation on gfx950.
+//
+// Replaces (forward) Preprocess_Line2Window.forward (losses/preprocess.py:27-121)
+// with its helpers generate_kpts_regular_grid_random (preprocess_utils.py:598-659),
+// epipolar_line_search (661-694), get_endpoints (696-719),
+// get_expected_correspondence_within_window (721-758), and
+// EpipolarLoss_full.forward (losses/epipolarloss.py:38-101).
+//
+// Pipeline per call (B pairs, n = (H/g)*(W/g) grid points per image):
+//   grid_points      sel (Categorical draw per g x g cell) -> normalised+pixel coords
+//   sample_desc      L2-normalised descriptors at the grid points (sample.hip)
+//   l2norm_scale     fm = T * normalize(xf) per pixel (NHWC)
+//   cos-sim          S = f1 f2^T  (conv_mfma 1x1 implicit GEMM, FP32 MFMA)
+//   row/col stats    softmax(T S) along n and along m with the coordinate
+//                    expectations and stds (online softmax, fp32)
+//   line_window      one wave per query point: epipolar endpoints, 100
+//                    border-padded bilinear samples of fm along the line,
+//                    dot/softmax/arg-max (+ loc_rand jitter), then the
+//                    12x16 window of zero-padded samples around it,
+//                    softmax expectation + std
+//   epipolar_loss    one workgroup: costs, masks, std weights, means
+// Random draws (grid sel, jitter) are inputs: the caller owns the RNG.
+#include "common.h"
+
+int pf_sample_desc(const float* fmap, int b, int c, int h, int w, int cs, const float* coord,
+                   int npts, const int32_t* n_valid, int normalize, float* out, hipStream_t st);
+
+namespace {
+
+// torch.linspace(lo, hi, n)[i] in float32 (ATen's two-sided formula)
+__device__ __forceinline__ float linspace_f(float lo, float hi, int n, int i) {
+  if (n == 1) return lo;
+  const float step = __fdiv_rn(__fsub_rn(hi, lo), (float)(n - 1));
+  return i < n / 2 ? __fadd_rn(lo, __fmul_rn(step, (float)i))
+                   : __fsub_rn(hi, __fmul_rn(step, (float)(n - 1 - i)));
+}
+
+__global__ void grid_points_kernel(const int32_t* __restrict__ sel, int nb, int H, int W, int g,
+                                   float* __restrict__ cn, float* __restrict__ cp) {
+  const int hc = H / g, wc = W / g, n = hc * wc;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nb * n) return;
+  const int k = i % n;
+  const int cy = k / wc, cx = k - cy * wc;
+  const int s = sel[i];
+  const int iy = cy * g + s / g, ix = cx * g + s % g;
+  const float xn = linspace_f(-1.f, 1.f, W, ix), yn = linspace_f(-1.f, 1.f, H, iy);
+  cn[2 * i] = xn;
+  cn[2 * i + 1] = yn;
+  // denormalize_coords: n * c + c, c = ((W-1)/2, (H-1)/2)
+  const float c0 = (float)((W - 1) / 2.0), c1 = (float)((H - 1) / 2.0);
+  cp[2 * i] = __fadd_rn(__fmul_rn(xn, c0), c0);
+  cp[2 * i + 1] = __fadd_rn(__fmul_rn(yn, c1), c1);
+}
+
+// y[p][c] = scale * x[p][c] / max(||x[p]||, 1e-12), C == 128, one wave per pixel
+__global__ void l2norm_scale_kernel(const float* __restrict__ x, long long npix, int cs,
+                                    float scale, float* __restrict__ y) {
+  const int lane = threadIdx.x & 63;
+  const long long wid = blockIdx.x * (long long)(blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (wid >= npix) return;
+  const float a = x[wid * cs + lane], b = x[wid * cs + lane + 64];
+  const float inv = 1.f / fmaxf(sqrtf(pf_wave_sum(a * a + b * b)), 1e-12f);
+  y[wid * 128 + lane] = scale * (a * inv);
+  y[wid * 128 + lane + 64] = scale * (b * inv);
+}
+
+// softmax_n(T*S[m][:]) expectations; one wave per row m.
+//   g  = sum_n p c2px[n]       (pixels)
+//   sd = sum_d sqrt(max(sum_n p c2n[n]_d^2 - normalize(g)_d^2, 1e-6))
+__global__ void corr_row_kernel(const float* __restrict__ S, int nb, int n1, int n2, float T,
+                                const float* __restrict__ c2px, const float* __restrict__ c2n,
+                                int H2, int W2, float* __restrict__ g, float* __restrict__ sd) {
+  const int lane = threadIdx.x & 63;
+  const long long wid = blockIdx.x * (long long)(blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (wid >= (long long)nb * n1) return;
+  const int b = (int)(wid / n1);
+  const float* row = S + wid * n2;
+  const float* cp = c2px + (long long)b * n2 * 2;
+  const float* cn = c2n + (long long)b * n2 * 2;
+  float mx = -INFINITY;
+  for (int k = lane; k < n2; k += 64) mx = fmaxf(mx, T * row[k]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  float se = 0.f, gx = 0.f, gy = 0.f, qx = 0.f, qy = 0.f;
+  for (int k = lane; k < n2; k += 64) {
+    const float e = expf(T * row[k] - mx);
+    se += e;
+    gx += e * cp[2 * k];
+    gy += e * cp[2 * k + 1];
+    qx += e * cn[2 * k] * cn[2 * k];
+    qy += e * cn[2 * k + 1] * cn[2 * k + 1];
+  }
+  se = pf_wave_sum(se);
+  gx = pf_wave_sum(gx) / se;
+  gy = pf_wave_sum(gy) / se;
+  qx = pf_wave_sum(qx) / se;
+  qy = pf_wave_sum(qy) / se;
+  if (lane == 0) {
+    g[wid * 2] = gx;
+    g[wid * 2 + 1] = gy;
+    const float c0 = (float)((W2 - 1) / 2.0), c1 = (float)((H2 - 1) / 2.0);
+    const float nx = (gx - c0) / c0, ny = (gy - c1) / c1;
+    sd[wid] = sqrtf(fmaxf(qx - nx * nx, 1e-6f)) + sqrtf(fmaxf(qy - ny * ny, 1e-6f));
+  }
+}
+
+// softmax_m(T*S[:][n]) expectations; one thread per column n (coalesced rows).
+__global__ void corr_col_kernel(const float* __restrict__ S, int nb, int n1, int n2, float T,
+                                const float* __restrict__ c1px, const float* __restrict__ c1n,
+                                int H1, int W1, float* __restrict__ g, float* __restrict__ sd) {
+  const int b = blockIdx.y;
+  const int col = blockIdx.x * blockDim.x + threadIdx.x;
+  if (col >= n2) return;
+  const float* Sb = S + (long long)b * n1 * n2;
+  const float* cp = c1px + (long long)b * n1 * 2;
+  const float* cn = c1n + (long long)b * n1 * 2;
+  float mx = -INFINITY;
+  for (int m = 0; m < n1; ++m) mx = fmaxf(mx, T * Sb[(long long)m * n2 + col]);
+  float se = 0.f, gx = 0.f, gy = 0.f, qx = 0.f, qy = 0.f;
+  for (int m = 0; m < n1; ++m) {
+    const float e = expf(T * Sb[(long long)m * n2 + col] - mx);
+    se += e;
+    gx += e * cp[2 * m];
+    gy += e * cp[2 * m + 1];
+    qx += e * cn[2 * m] * cn[2 * m];
+    qy += e * cn[2 * m + 1] * cn[2 * m + 1];
+  }
+  gx /= se;
+  gy /= se;
+  qx /= se;
+  qy /= se;
+  const long long o = (long long)b * n2 + col;
+  g[o * 2] = gx;
+  g[o * 2 + 1] = gy;
+  const float c0 = (float)((W1 - 1) / 2.0), c1 = (float)((H1 - 1) / 2.0);
+  const float nx = (gx - c0) / c0, ny = (gy - c1) / c1;
+  sd[o] = sqrtf(fmaxf(qx - nx * nx, 1e-6f)) + sqrtf(fmaxf(qy - ny * ny, 1e-6f));
+}
+
+// bilinear sample of a 128-channel NHWC map at normalised (x, y), align_corners
+// False; border: clamp the source index (padding_mode='border'), else zeros.
+// Returns this lane's two channels (lane, lane+64).
+template <bool BORDER>
+__device__ __forceinline__ float2 bilinear128(const float* __restrict__ fm, int h, int w, float gx,
+                                              float gy, int lane) {
+  float ix = ((gx + 1.f) * w - 1.f) / 2.f;
+  float iy = ((gy + 1.f) * h - 1.f) / 2.f;
+  if (BORDER) {
+    ix = fminf(fmaxf(ix, 0.f), (float)(w - 1));
+    iy = fminf(fmaxf(iy, 0.f), (float)(h - 1));
+  }
+  const float fx = floorf(ix), fy = floorf(iy);
+  const int x0 = (int)fx, y0 = (int)fy, x1 = x0 + 1, y1 = y0 + 1;
+  const float wx1 = ix - fx, wx0 = 1.f - wx1;  // (x1 - ix), (ix - x0)
+  const float wy1 = iy - fy, wy0 = 1.f - wy1;
+  float2 r = {0.f, 0.f};
+  const bool bx0 = (unsigned)x0 < (unsigned)w, bx1 = (unsigned)x1 < (unsigned)w;
+  const bool by0 = (unsigned)y0 < (unsigned)h, by1 = (unsigned)y1 < (unsigned)h;
+  if (by0 && bx0) {
+    const float* p = fm + ((long long)y0 * w + x0) * 128;
+    const float wt = ((float)x1 - ix) * ((float)y1 - iy);
+    r.x += p[lane] * wt;
+    r.y += p[lane + 64] * wt;
+  }
+  if (by0 && bx1) {
+    const float* p = fm + ((long long)y0 * w + x1) * 128;
+    const float wt = (ix - (float)x0) * ((float)y1 - iy);
+    r.x += p[lane] * wt;
+    r.y += p[lane + 64] * wt;
+  }
+  if (by1 && bx0) {
+    const float* p = fm + ((long long)y1 * w + x0) * 128;
+    const float wt = ((float)x1 - ix) * (iy - (float)y0);
+    r.x += p[lane] * wt;
+    r.y += p[lane + 64] * wt;
+  }
+  if (by1 && bx1) {
+    const float* p = fm + ((long long)y1 * w + x1) * 128;
+    const float wt = (ix - (float)x0) * (iy - (float)y0);
+    r.x += p[lane] * wt;
+    r.y += p[lane + 64] * wt;
+  }
+  (void)wx0;
+  (void)wx1;
+  (void)wy0;
+  (void)wy1;
+  return r;
+}
+
+constexpr int MAX_LINE = 128;   // line_step <= 128 (2 logits per lane)
+constexpr int MAX_WIN = 512;    // window taps <= 512 (8 logits per lane)
+
+// One wave per query point: epipolar line search + window expectation.
+__global__ void line_window_kernel(const float* __restrict__ cpx,   // [b][n][2] query pixels
+                                   const float* __restrict__ Fm,    // [b][3][3]
+                                   const float* __restrict__ f1,    // [b][n][128] L2-normed
+                                   const float* __restrict__ fm2,   // [b][h2][w2][128] T*norm
+                                   const float* __restrict__ rnd,   // [b][n][2] U(0,1)
+                                   int nb, int n, int h2, int w2, int H2, int W2, int line_step,
+                                   int win_h, int win_w, float window_size,
+                                   float* __restrict__ l_exp_n, float* __restrict__ l_org_n,
+                                   uint8_t* __restrict__ valid, float* __restrict__ w_px,
+                                   float* __restrict__ w_std) {
+  const int lane = threadIdx.x & 63;
+  const long long wid = blockIdx.x * (long long)(blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (wid >= (long long)nb * n) return;
+  const int b = (int)(wid / n);
+  const float* F = Fm + b * 9;
+  const float* fmb = fm2 + (long long)b * h2 * w2 * 128;
+  const float q0 = f1[wid * 128 + lane], q1 = f1[wid * 128 + lane + 64];
+  const float x = cpx[wid * 2], y = cpx[wid * 2 + 1];
+  // ---- get_endpoints (preprocess_utils.py:696-719), image size H2 x W2
+  const float la = fmaf(F[2], 1.f, fmaf(F[1], y, F[0] * x));
+  const float lb = fmaf(F[5], 1.f, fmaf(F[4], y, F[3] * x));
+  const float lc = fmaf(F[8], 1.f, fmaf(F[7], y, F[6] * x));
+  const float Wm = (float)(W2 - 1), Hm = (float)(H2 - 1);
+  float px[4], py[4];
+  px[0] = 0.f;
+  py[0] = -lc / lb;
+  px[1] = Wm;
+  py[1] = -(la * Wm + lc) / lb;
+  px[2] = -(lb * Hm + lc) / la;
+  py[2] = Hm;
+  px[3] = -lc / la;
+  py[3] = 0.f;
+  int cnt = 0, first = -1, second = -1;
+  for (int k = 0; k < 4; ++k) {
+    const bool in = px[k] >= 0.f && px[k] <= Wm && py[k] >= 0.f && py[k] <= Hm;
+    if (in) {
+      if (first < 0) first = k;
+      else if (second < 0) second = k;
+      ++cnt;
+    }
+  }
+  bool ok = cnt == 2;
+  if (!ok) {
+    first = 0;
+    second = 1;
+  }
+  const float c0 = (float)((W2 - 1) / 2.0), c1 = (float)((H2 - 1) / 2.0);
+  const float e1x = (px[first] - c0) / c0, e1y = (py[first] - c1) / c1;
+  const float e2x = (px[second] - c0) / c0, e2y = (py[second] - c1) / c1;
+  const float dx = e2x - e1x, dy = e2y - e1y;
+  // ---- line samples: logits (lane s holds logit s and s+64)
+  float lg[2] = {-INFINITY, -INFINITY};
+  for (int s = 0; s < line_step; ++s) {
+    const float t = linspace_f(0.f, 1.f, line_step, s);
+    const float gx = __fadd_rn(__fmul_rn(dx, t), e1x), gy = __fadd_rn(__fmul_rn(dy, t), e1y);
+    const float2 v = bilinear128<true>(fmb, h2, w2, gx, gy, lane);
+    const float d = pf_wave_sum(q0 * v.x + q1 * v.y);
+    if ((s & 63) == lane) lg[s >> 6] = d;
+  }
+  float mx = fmaxf(lg[0], lg[1]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  // use_nn: sum of the grid points whose prob equals the max
+  float ox = 0.f, oy = 0.f;
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int s = lane + 64 * r;
+    if (s < line_step && lg[r] == mx) {
+      const float t = linspace_f(0.f, 1.f, line_step, s);
+      ox += __fadd_rn(__fmul_rn(dx, t), e1x);
+      oy += __fadd_rn(__fmul_rn(dy, t), e1y);
+    }
+  }
+  ox = pf_wave_sum(ox);
+  oy = pf_wave_sum(oy);
+  const float jx = ox + 0.707f * window_size * (2.f * rnd[wid * 2] - 1.f);
+  const float jy = oy + 0.707f * window_size * (2.f * rnd[wid * 2 + 1] - 1.f);
+  ok = ok && jx >= -1.f && jx <= 1.f && jy >= -1.f && jy <= 1.f;
+  // ---- window around the jittered line expectation
+  const int nw = win_h * win_w;
+  float wl[MAX_WIN / 64];
+#pragma unroll
+  for (int r = 0; r < MAX_WIN / 64; ++r) wl[r] = -INFINITY;
+  for (int s = 0; s < nw; ++s) {
+    const int iy = s / win_w, ix = s - iy * win_w;
+    const float gx = jx + linspace_f(-window_size, window_size, win_w, ix);
+    const float gy = jy + linspace_f(-window_size, window_size, win_h, iy);
+    const float2 v = bilinear128<false>(fmb, h2, w2, gx, gy, lane);
+    const float d = pf_wave_sum(q0 * v.x + q1 * v.y);
+#pragma unroll
+    for (int r = 0; r < MAX_WIN / 64; ++r)
+      if (s == lane + 64 * r) wl[r] = d;
+  }
+  float wm = -INFINITY;
+#pragma unroll
+  for (int r = 0; r < MAX_WIN / 64; ++r) wm = fmaxf(wm, wl[r]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) wm = fmaxf(wm, __shfl_xor(wm, o, 64));
+  float se = 0.f, ex = 0.f, ey = 0.f, vx = 0.f, vy = 0.f;
+#pragma unroll
+  for (int r = 0; r < MAX_WIN / 64; ++r) {
+    const int s = lane + 64 * r;
+    if (s < nw) {
+      const int iy = s / win_w, ix = s - iy * win_w;
+      const float gx = jx + linspace_f(-window_size, window_size, win_w, ix);
+      const float gy = jy + linspace_f(-window_size, window_size, win_h, iy);
+      const float e = expf(wl[r] - wm);
+      se += e;
+      ex += e * gx;
+      ey += e * gy;
+      vx += e * gx * gx;
+      vy += e * gy * gy;
+    }
+  }
+  se = pf_wave_sum(se);
+  ex = pf_wave_sum(ex) / se;
+  ey = pf_wave_sum(ey) / se;
+  vx = pf_wave_sum(vx) / se - ex * ex;
+  vy = pf_wave_sum(vy) / se - ey * ey;
+  if (lane == 0) {
+    l_exp_n[wid * 2] = jx;
+    l_exp_n[wid * 2 + 1] = jy;
+    l_org_n[wid * 2] = ox;
+    l_org_n[wid * 2 + 1] = oy;
+    valid[wid] = ok ? 1 : 0;
+    w_px[wid * 2] = ex * c0 + c0;
+    w_px[wid * 2 + 1] = ey * c1 + c1;
+    w_std[wid] = sqrtf(fmaxf(vx, 1e-10f)) + sqrtf(fmaxf(vy, 1e-10f));
+  }
+}
+
+// |x2^T l| with l = F x1 / ||l[:2]|| (epipolarloss.py:16-22)
+__device__ __forceinline__ float epi_cost(const float* F, float x1, float y1, float x2, float y2) {
+  const float a = F[0] * x1 + F[1] * y1 + F[2];
+  const float b = F[3] * x1 + F[4] * y1 + F[5];
+  const float c = F[6] * x1 + F[7] * y1 + F[8];
+  const float nrm = fmaxf(sqrtf(a * a + b * b), 1e-8f);
+  return fabsf(x2 * (a / nrm) + y2 * (b / nrm) + (c / nrm));
+}
+
+// EpipolarLoss_full.forward: one workgroup.  out[0] = loss, out[1..6] =
+// loss_g1, loss_w1, loss_g2, loss_w2, percent_g, percent_w.
+__global__ __launch_bounds__(1024) void epipolar_loss_kernel(
+    int nb, int n, const float* __restrict__ F1, const float* __restrict__ F2,
+    const float* __restrict__ c1, const float* __restrict__ c2, const float* __restrict__ g1,
+    const float* __restrict__ g2, const float* __restrict__ w1, const float* __restrict__ w2,
+    const float* __restrict__ sg1, const float* __restrict__ sg2, const float* __restrict__ sw1,
+    const float* __restrict__ sw2, const uint8_t* __restrict__ v1, const uint8_t* __restrict__ v2,
+    float short_edge, float gthr, float wthr, float wg, float ww, float* __restrict__ out) {
+  const int tid = threadIdx.x;
+  const int total = nb * n;
+  __shared__ double red[16][8];
+  // four (cost, std, mask, F, coords) sets: g1, w1, g2, w2
+  double lsum[4], msum[4];
+  for (int k = 0; k < 4; ++k) {
+    // pass 1: mean of inverse std, masked count
+    double a1 = 0.0, a2 = 0.0;
+    for (int i = tid; i < total; i += blockDim.x) {
+      const int b = i / n;
+      const float* F = (k < 2 ? F1 : F2) + b * 9;
+      const float* p = (k < 2 ? c1 : c2) + 2 * i;
+      const float* q = (k == 0 ? g1 : k == 1 ? w1 : k == 2 ? g2 : w2) + 2 * i;
+      const float sd = (k == 0 ? sg1 : k == 1 ? sw1 : k == 2 ? sg2 : sw2)[i];
+      const float cost = epi_cost(F, p[0], p[1], q[0], q[1]);
+      const bool m = cost < short_edge * ((k & 1) ? wthr : gthr) && (k < 2 ? v1 : v2)[i];
+      a1 += 1.0 / fmaxf(sd, 1e-10f);
+      a2 += m ? 1.0 : 0.0;
+    }
+    // block reduce (fixed order)
+    double r1 = a1, r2 = a2;
+    for (int o = 32; o > 0; o >>= 1) {
+      r1 += __shfl_xor(r1, o, 64);
+      r2 += __shfl_xor(r2, o, 64);
+    }
+    if ((tid & 63) == 0) {
+      red[tid >> 6][0] = r1;
+      red[tid >> 6][1] = r2;
+    }
+    __syncthreads();
+    double inv_mean = 0.0, cnt = 0.0;
+    for (int wv = 0; wv < (int)(blockDim.x >> 6); ++wv) {
+      inv_mean += red[wv][0];
+      cnt += red[wv][1];
+    }
+    inv_mean /= total;
+    __syncthreads();
+    // set_weight: w = (inv/mean) * mask; w /= (mean(w) + 1e-8); loss = mean(w * cost)
+    double b1 = 0.0, b2 = 0.0;
+    for (int i = tid; i < total; i += blockDim.x) {
+      const int b = i / n;
+      const float* F = (k < 2 ? F1 : F2) + b * 9;
+      const float* p = (k < 2 ? c1 : c2) + 2 * i;
+      const float* q = (k == 0 ? g1 : k == 1 ? w1 : k == 2 ? g2 : w2) + 2 * i;
+      const float sd = (k == 0 ? sg1 : k == 1 ? sw1 : k == 2 ? sg2 : sw2)[i];
+      const float cost = epi_cost(F, p[0], p[1], q[0], q[1]);
+      const bool m = cost < short_edge * ((k & 1) ? wthr : gthr) && (k < 2 ? v1 : v2)[i];
+      const double wt = m ? (1.0 / fmaxf(sd, 1e-10f)) / inv_mean : 0.0;
+      b1 += wt;
+      b2 += wt * cost;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      b1 += __shfl_xor(b1, o, 64);
+      b2 += __shfl_xor(b2, o, 64);
+    }
+    if ((tid & 63) == 0) {
+      red[tid >> 6][0] = b1;
+      red[tid >> 6][1] = b2;
+    }
+    __syncthreads();
+    double sw = 0.0, swc = 0.0;
+    for (int wv = 0; wv < (int)(blockDim.x >> 6); ++wv) {
+      sw += red[wv][0];
+      swc += red[wv][1];
+    }
+    __syncthreads();
+    const double wmean = sw / total + 1e-8;
+    lsum[k] = swc / wmean / total;
+    msum[k] = cnt / total;
+  }
+  if (tid == 0) {
+    out[1] = (float)lsum[0];
+    out[2] = (float)lsum[1];
+    out[3] = (float)lsum[2];
+    out[4] = (float)lsum[3];
+    out[0] = (float)(wg * (lsum[0] + lsum[2]) + ww * (lsum[1] + lsum[3]));
+    out[5] = (float)((msum[0] + msum[2]) / 2);
+    out[6] = (float)((msum[1] + msum[3]) / 2);
+  }
+}
+
+}  // namespace
+
+extern "C" size_t posfeat_line2window_workspace(int b, int H1, int W1, int H2, int W2, int grid) {
+  if (b <= 0 || grid <= 0) return 0;
+  const size_t n1 = (size_t)(H1 / grid) * (W1 / grid), n2 = (size_t)(H2 / grid) * (W2 / grid);
+  size_t s = 0;
+  s += pf_align(b * n1 * 2 * 4, 256) * 2;           // c1n, c1px
+  s += pf_align(b * n2 * 2 * 4, 256) * 2;           // c2n, c2px
+  s += pf_align(b * n1 * 128 * 4, 256);             // f1
+  s += pf_align(b * n2 * 128 * 4, 256);             // f2
+  s += pf_align(b * n1 * n2 * 4, 256);              // S
+  s += pf_align((size_t)b * (H1 / 4) * (W1 / 4) * 128 * 4, 256);  // fm1
+  s += pf_align((size_t)b * (H2 / 4) * (W2 / 4) * 128 * 4, 256);  // fm2
+  return s;
+}
+
+extern "C" int posfeat_line2window(const float* xf1, int cs1, const float* xf2, int cs2, int b,
+                                   int H1, int W1, int H2, int W2, const float* F1,
+                                   const float* F2, const int32_t* sel1, const int32_t* sel2,
+                                   const float* rand1, const float* rand2, float temperature,
+                                   int grid, float window_size, int line_step,
+                                   posfeat_l2w_out* out, void* ws, size_t ws_bytes,
+                                   void* stream) {
+  if (!xf1 || !xf2 || !F1 || !F2 || !sel1 || !sel2 || !rand1 || !rand2 || !out || !ws)
+    return POSFEAT_E_INVALID;
+  if (b <= 0 || grid <= 0 || H1 % 4 || W1 % 4 || H2 % 4 || W2 % 4 || cs1 < 128 || cs2 < 128 ||
+      line_step <= 1 || line_step > MAX_LINE)
+    return POSFEAT_E_INVALID;
+  const int h1 = H1 / 4, w1 = W1 / 4, h2 = H2 / 4, w2 = W2 / 4;
+  const int win_h2 = (int)(window_size * h2), win_w2 = (int)(window_size * w2);
+  const int win_h1 = (int)(window_size * h1), win_w1 = (int)(window_size * w1);
+  if (win_h2 * win_w2 > MAX_WIN || win_h1 * win_w1 > MAX_WIN || win_h1 < 1 || win_w1 < 1 ||
+      win_h2 < 1 || win_w2 < 1)
+    return POSFEAT_E_UNSUPPORTED;
+  if (ws_bytes < posfeat_line2window_workspace(b, H1, W1, H2, W2, grid)) return POSFEAT_E_WORKSPACE;
+  const int n1 = (H1 / grid) * (W1 / grid), n2 = (H2 / grid) * (W2 / grid);
+  hipStream_t st = pf_stream(stream);
+  char* p = static_cast<char*>(ws);
+  auto take = [&](size_t bytes) {
+    char* r = p;
+    p += pf_align(bytes, 256);
+    return reinterpret_cast<float*>(r);
+  };
+  float* c1n = take((size_t)b * n1 * 8);
+  float* c1p = take((size_t)b * n1 * 8);
+  float* c2n = take((size_t)b * n2 * 8);
+  float* c2p = take((size_t)b * n2 * 8);
+  float* f1 = take((size_t)b * n1 * 512);
+  float* f2 = take((size_t)b * n2 * 512);
+  float* S = take((size_t)b * n1 * n2 * 4);
+  float* fm1 = take((size_t)b * h1 * w1 * 512);
+  float* fm2 = take((size_t)b * h2 * w2 * 512);
+  // grid points
+  hipLaunchKernelGGL(grid_points_kernel, dim3((b * n1 + 255) / 256), dim3(256), 0, st, sel1, b,
+                     H1, W1, grid, c1n, c1p);
+  hipLaunchKernelGGL(grid_points_kernel, dim3((b * n2 + 255) / 256), dim3(256), 0, st, sel2, b,
+                     H2, W2, grid, c2n, c2p);
+  PF_CHECK_LAUNCH();
+  if (out->coord1 &&
+      hipMemcpyAsync(out->coord1, c1p, (size_t)b * n1 * 8, hipMemcpyDeviceToDevice, st) != hipSuccess)
+    return POSFEAT_E_HIP;
+  if (out->coord2 &&
+      hipMemcpyAsync(out->coord2, c2p, (size_t)b * n2 * 8, hipMemcpyDeviceToDevice, st) != hipSuccess)
+    return POSFEAT_E_HIP;
+  // descriptors at the grid points (sample_feat_by_coord, norm=True)
+  PF_TRY(pf_sample_desc(xf1, b, 128, h1, w1, cs1, c1n, n1, nullptr, 1, f1, st));
+  PF_TRY(pf_sample_desc(xf2, b, 128, h2, w2, cs2, c2n, n2, nullptr, 1, f2, st));
+  // T * normalize(xf) maps
+  hipLaunchKernelGGL(l2norm_scale_kernel, dim3((unsigned)(((long long)b * h1 * w1 + 3) / 4)),
+                     dim3(256), 0, st, xf1, (long long)b * h1 * w1, cs1, temperature, fm1);
+  hipLaunchKernelGGL(l2norm_scale_kernel, dim3((unsigned)(((long long)b * h2 * w2 + 3) / 4)),
+                     dim3(256), 0, st, xf2, (long long)b * h2 * w2, cs2, temperature, fm2);
+  PF_CHECK_LAUNCH();
+  // S = f1 f2^T per pair on the MFMA conv engine (1x1 conv, weights = f2)
+  if (n2 % 4 == 0) {
+    for (int i = 0; i < b; ++i) {
+      posfeat_conv_desc d;
+      d.n = 1;
+      d.h = 1;
+      d.w = n1;
+      d.cin = 128;
+      d.x_cstride = 128;
+      d.cout = n2;
+      d.kh = d.kw = d.stride = 1;
+      d.pad = 0;
+      d.y_cstride = n2;
+      d.res_cstride = 0;
+      d.act = POSFEAT_ACT_NONE;
+      PF_TRY(posfeat_conv2d_nhwc(&d, f1 + (size_t)i * n1 * 128, f2 + (size_t)i * n2 * 128, nullptr,
+                                 nullptr, S + (size_t)i * n1 * n2, st));
+    }
+  } else {
+    return POSFEAT_E_UNSUPPORTED;
+  }
+  hipLaunchKernelGGL(corr_row_kernel, dim3((b * n1 + 3) / 4), dim3(256), 0, st, S, b, n1, n2,
+                     temperature, c2p, c2n, H2, W2, out->g1, out->g1_std);
+  hipLaunchKernelGGL(corr_col_kernel, dim3((n2 + 255) / 256, b), dim3(256), 0, st, S, b, n1, n2,
+                     temperature, c1p, c1n, H1, W1, out->g2, out->g2_std);
+  PF_CHECK_LAUNCH();
+  // line search + window, both directions
+  hipLaunchKernelGGL(line_window_kernel, dim3((b * n1 + 3) / 4), dim3(256), 0, st, c1p, F1, f1,
+                     fm2, rand1, b, n1, h2, w2, H2, W2, line_step, win_h2, win_w2, window_size,
+                     out->l1_exp_n, out->l1_org_n, out->valid1, out->w1, out->w1_std);
+  hipLaunchKernelGGL(line_window_kernel, dim3((b * n2 + 3) / 4), dim3(256), 0, st, c2p, F2, f2,
+                     fm1, rand2, b, n2, h1, w1, H1, W1, line_step, win_h1, win_w1, window_size,
+                     out->l2_exp_n, out->l2_org_n, out->valid2, out->w2, out->w2_std);
+  PF_CHECK_LAUNCH();
+  return POSFEAT_OK;
+}
+
+extern "C" int posfeat_epipolar_loss(int b, int n, const float* F1, const float* F2,
+                                     const float* c1, const float* c2, const float* g1,
+                                     const float* g2, const float* w1, const float* w2,
+                                     const float* sg1, const float* sg2, const float* sw1,
+                                     const float* sw2, const uint8_t* v1, const uint8_t* v2,
+                                     float short_edge, float grid_thr, float win_thr,
+                                     float weight_grid, float weight_window, float* out,
+                                     void* stream) {
+  if (b <= 0 || n <= 0 || !out) return POSFEAT_E_INVALID;
+  hipLaunchKernelGGL(epipolar_loss_kernel, dim3(1), dim3(1024), 0, pf_stream(stream), b, n, F1,
+                     F2, c1, c2, g1, g2, w1, w2, sg1, sg2, sw1, sw2, v1, v2, short_edge, grid_thr,
+                     win_thr, weight_grid, weight_window, out);
+  PF_CHECK_LAUNCH();
+  return POSFEAT_OK;
+}

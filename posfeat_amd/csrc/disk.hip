@@ -1,0 +1,326 @@
+// disk.hip -- DiskLoss forward on gfx950 (keypoint-head REINFORCE loss).
+//
+// Replaces losses/kploss.py:132-197 DiskLoss.forward with point_distribution
+// (20-35), point_sample (37-48) and constant_reward (50-89), configuration of
+// configs/train_kp.yaml:56-73 (grid 8, T 60, reward_thr 2, +1 / -0.25,
+// kp_penalty -0.001, cor_detach).
+//
+//   disk_point       one wave per 8x8 cell (64 lanes = 64 logits): log-softmax,
+//                    Categorical proposal (given, or Gumbel-max from uniforms),
+//                    Bernoulli acceptance (given, or u < sigmoid(l)), logp, pixel
+//                    and normalised coordinates
+//   sample_desc      L2-normalised descriptors at the proposals (sample.hip)
+//   S = f1 f2^T      conv_mfma 1x1 implicit GEMM (FP32 MFMA), [n1][n2] per pair
+//   row/col lse      logsumexp of aff = -T(1 - S) along n and along m
+//   epi lines        normalised epipolar lines l1 = F1 x1/|..|, l2 = F2 x2/|..|
+//   reinforce        sum over accepted pairs of reward * p * (logp_dense + logp1 +
+//                    logp2), p = softmax_row * softmax_col, fixed-order block
+//                    partials (fp64) + one final workgroup -> deterministic
+// The dense B x n x n probability matrices of the reference are never
+// materialised; only S is (n = 4800 at 480x640: 92 MB per pair).
+#include "common.h"
+
+int pf_sample_desc(const float* fmap, int b, int c, int h, int w, int cs, const float* coord,
+                   int npts, const int32_t* n_valid, int normalize, float* out, hipStream_t st);
+
+namespace {
+
+// torch binary_cross_entropy_with_logits(x, y) -> logp = -loss
+__device__ __forceinline__ float bern_logp(float x, bool y) {
+  const float t = log1pf(expf(-fabsf(x)));
+  return y ? -(fmaxf(-x, 0.f) + t) : -(fmaxf(x, 0.f) + t);
+}
+
+__global__ void disk_point_kernel(const float* __restrict__ kp, int nb, int H, int W,
+                                  const int32_t* __restrict__ prop_in,
+                                  const uint8_t* __restrict__ acc_in,
+                                  const float* __restrict__ uni,  // [b][n][65] if sampling
+                                  int32_t* __restrict__ prop_out, uint8_t* __restrict__ acc_out,
+                                  float* __restrict__ cpx, float* __restrict__ cn,
+                                  float* __restrict__ logp) {
+  constexpr int G = 8;
+  const int lane = threadIdx.x & 63;
+  const int hc = H / G, wc = W / G, n = hc * wc;
+  const long long wid = blockIdx.x * (long long)(blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (wid >= (long long)nb * n) return;
+  const int b = (int)(wid / n), k = (int)(wid - (long long)b * n);
+  const int cy = k / wc, cx = k - cy * wc;
+  const float v = kp[((long long)b * H + cy * G + lane / G) * W + cx * G + lane % G];
+  float mx = v;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  const float lse = mx + logf(pf_wave_sum(expf(v - mx)));
+  int p;
+  bool a;
+  if (uni) {  // Gumbel-max == Categorical(logits) sample; accept ~ Bernoulli(sigmoid)
+    const float u = fminf(fmaxf(uni[wid * 65 + lane], 1e-20f), 1.f - 1e-7f);
+    float key = v - logf(-logf(u));
+    int arg = lane;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ok = __shfl_xor(key, o, 64);
+      const int oa = __shfl_xor(arg, o, 64);
+      if (ok > key || (ok == key && oa < arg)) {
+        key = ok;
+        arg = oa;
+      }
+    }
+    p = arg;
+    const float lp = __shfl(v, p, 64);
+    a = uni[wid * 65 + 64] < 1.f / (1.f + expf(-lp));
+  } else {
+    p = prop_in[wid];
+    a = acc_in[wid] != 0;
+  }
+  const float lv = __shfl(v, p, 64);
+  if (lane == 0) {
+    prop_out[wid] = p;
+    acc_out[wid] = a ? 1 : 0;
+    logp[wid] = (lv - lse) + bern_logp(lv, a);
+    const float x = (float)(cx * G + p % G), y = (float)(cy * G + p / G);
+    cpx[wid * 2] = x;
+    cpx[wid * 2 + 1] = y;
+    const float c0 = (float)((W - 1) / 2.0), c1 = (float)((H - 1) / 2.0);
+    cn[wid * 2] = (x - c0) / c0;
+    cn[wid * 2 + 1] = (y - c1) / c1;
+  }
+}
+
+// lse_r[m] = logsumexp_n(T*S[m][n] - T); one wave per row
+__global__ void row_lse_kernel(const float* __restrict__ S, long long rows, int n2, float T,
+                               float* __restrict__ lse) {
+  const int lane = threadIdx.x & 63;
+  const long long wid = blockIdx.x * (long long)(blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (wid >= rows) return;
+  const float* r = S + wid * n2;
+  float mx = -INFINITY;
+  for (int k = lane; k < n2; k += 64) mx = fmaxf(mx, T * r[k] - T);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  float s = 0.f;
+  for (int k = lane; k < n2; k += 64) s += expf((T * r[k] - T) - mx);
+  s = pf_wave_sum(s);
+  if (lane == 0) lse[wid] = mx + logf(s);
+}
+
+// lse_c[n] = logsumexp_m(T*S[m][n] - T); one thread per column
+__global__ void col_lse_kernel(const float* __restrict__ S, int n1, int n2, float T,
+                               float* __restrict__ lse) {
+  const int b = blockIdx.y;
+  const int col = blockIdx.x * blockDim.x + threadIdx.x;
+  if (col >= n2) return;
+  const float* Sb = S + (long long)b * n1 * n2;
+  float mx = -INFINITY;
+  for (int m = 0; m < n1; ++m) mx = fmaxf(mx, T * Sb[(long long)m * n2 + col] - T);
+  float s = 0.f;
+  for (int m = 0; m < n1; ++m) s += expf((T * Sb[(long long)m * n2 + col] - T) - mx);
+  lse[(long long)b * n2 + col] = mx + logf(s);
+}
+
+// normalised epipolar line of each point: l = F x / max(|l[:2]|, 1e-8)
+__global__ void epi_line_kernel(const float* __restrict__ Fm, const float* __restrict__ cpx,
+                                int nb, int n, float* __restrict__ line) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nb * n) return;
+  const float* F = Fm + (i / n) * 9;
+  const float x = cpx[2 * i], y = cpx[2 * i + 1];
+  const float a = F[0] * x + F[1] * y + F[2];
+  const float b = F[3] * x + F[4] * y + F[5];
+  const float c = F[6] * x + F[7] * y + F[8];
+  const float nr = fmaxf(sqrtf(a * a + b * b), 1e-8f);
+  line[3 * i] = a / nr;
+  line[3 * i + 1] = b / nr;
+  line[3 * i + 2] = c / nr;
+}
+
+constexpr int RB = 256;  // threads per reinforce block
+
+// per-block partial of sum_{acc1[m] & acc2[n]} reward * p * (logp_dense + logp1 + logp2)
+// block = (row tile of 4 rows, pair); threads sweep the columns
+__global__ __launch_bounds__(RB) void reinforce_kernel(
+    const float* __restrict__ S, int n1, int n2, float T, const float* __restrict__ lse_r,
+    const float* __restrict__ lse_c, const uint8_t* __restrict__ acc1,
+    const uint8_t* __restrict__ acc2, const float* __restrict__ logp1,
+    const float* __restrict__ logp2, const float* __restrict__ line1,
+    const float* __restrict__ line2, const float* __restrict__ c1px, const float* __restrict__ c2px,
+    float thr, float good, float bad, double* __restrict__ part) {
+  const int b = blockIdx.y;
+  const int m0 = blockIdx.x * 4;
+  const float* Sb = S + (long long)b * n1 * n2;
+  double acc = 0.0;
+  for (int mm = 0; mm < 4; ++mm) {
+    const int m = m0 + mm;
+    if (m >= n1) break;
+    const long long gm = (long long)b * n1 + m;
+    if (!acc1[gm]) continue;  // uniform per block
+    const float lr = lse_r[gm], lp1 = logp1[gm];
+    const float a1 = line1[3 * gm], b1 = line1[3 * gm + 1], k1 = line1[3 * gm + 2];
+    const float x1 = c1px[2 * gm], y1 = c1px[2 * gm + 1];
+    float rowsum = 0.f;
+    for (int nn = threadIdx.x; nn < n2; nn += RB) {
+      const long long gn = (long long)b * n2 + nn;
+      if (!acc2[gn]) continue;
+      const float aff = T * Sb[(long long)m * n2 + nn] - T;
+      const float lpr = aff - lr, lpc = aff - lse_c[gn];
+      const float p = expf(lpr) * expf(lpc);
+      const float x2 = c2px[2 * gn], y2 = c2px[2 * gn + 1];
+      const float d1 = fabsf(a1 * x2 + b1 * y2 + k1);
+      const float d2 = fabsf(line2[3 * gn] * x1 + line2[3 * gn + 1] * y1 + line2[3 * gn + 2]);
+      const float rw = (d1 < thr && d2 < thr) ? good : bad;
+      rowsum += rw * (p * ((lpr + lpc) + (lp1 + logp2[gn])));
+    }
+    acc += rowsum;
+  }
+  // fixed-order block reduction
+  __shared__ double red[RB];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = RB / 2; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[(long long)b * gridDim.x + blockIdx.x] = red[0];
+}
+
+// out[0] = loss, out[1] = reinforce, out[2] = kp_penalty, out[3] = n_kps
+__global__ __launch_bounds__(1024) void disk_final_kernel(const double* __restrict__ part,
+                                                          int nparts, const uint8_t* acc1,
+                                                          const uint8_t* acc2, const float* logp1,
+                                                          const float* logp2, int nb, int n1,
+                                                          int n2, float kp_penalty,
+                                                          float* __restrict__ out) {
+  __shared__ double r1[1024], r2[1024], r3[1024];
+  double s = 0.0, lp = 0.0, nk = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += blockDim.x) s += part[i];
+  for (int i = threadIdx.x; i < nb * n1; i += blockDim.x)
+    if (acc1[i]) {
+      lp += logp1[i];
+      nk += 1.0;
+    }
+  for (int i = threadIdx.x; i < nb * n2; i += blockDim.x)
+    if (acc2[i]) {
+      lp += logp2[i];
+      nk += 1.0;
+    }
+  r1[threadIdx.x] = s;
+  r2[threadIdx.x] = lp;
+  r3[threadIdx.x] = nk;
+  __syncthreads();
+  for (int o = 512; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      r1[threadIdx.x] += r1[threadIdx.x + o];
+      r2[threadIdx.x] += r2[threadIdx.x + o];
+      r3[threadIdx.x] += r3[threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const double reinforce = r1[0], pen = (double)kp_penalty * r2[0];
+    out[0] = (float)(-reinforce - pen);
+    out[1] = (float)reinforce;
+    out[2] = (float)pen;
+    out[3] = (float)(r3[0] / nb);
+  }
+}
+
+}  // namespace
+
+extern "C" size_t posfeat_disk_loss_workspace(int b, int H, int W) {
+  if (b <= 0 || H % 8 || W % 8) return 0;
+  const size_t n = (size_t)(H / 8) * (W / 8);
+  size_t s = 0;
+  s += 2 * pf_align(b * n * 2 * 4, 256);          // cpx1/2
+  s += 2 * pf_align(b * n * 2 * 4, 256);          // cn1/2
+  s += 2 * pf_align(b * n * 4, 256);              // logp1/2
+  s += 2 * pf_align(b * n * 4, 256);              // prop1/2
+  s += 2 * pf_align(b * n, 256);                  // acc1/2
+  s += 2 * pf_align(b * n * 128 * 4, 256);        // f1/f2
+  s += pf_align(b * n * n * 4, 256);              // S
+  s += 2 * pf_align(b * n * 4, 256);              // lse_r, lse_c
+  s += 2 * pf_align(b * n * 3 * 4, 256);          // lines
+  s += pf_align(b * ((n + 3) / 4) * 8, 256);      // partials
+  return s;
+}
+
+extern "C" int posfeat_disk_loss(const float* kp1, const float* kp2, const float* xf1, int cs1,
+                                 const float* xf2, int cs2, int b, int H, int W, const float* F1,
+                                 const float* F2, const int32_t* prop1, const int32_t* prop2,
+                                 const uint8_t* acc1, const uint8_t* acc2, const float* uni1,
+                                 const float* uni2, float temperature, float reward_thr,
+                                 float good_reward, float bad_reward, float kp_penalty,
+                                 float* out, void* ws, size_t ws_bytes, void* stream) {
+  if (!kp1 || !kp2 || !xf1 || !xf2 || !F1 || !F2 || !out || !ws) return POSFEAT_E_INVALID;
+  if (b <= 0 || H % 8 || W % 8 || H % 4 || cs1 < 128 || cs2 < 128) return POSFEAT_E_INVALID;
+  const bool sampled = uni1 && uni2;
+  if (!sampled && !(prop1 && prop2 && acc1 && acc2)) return POSFEAT_E_INVALID;
+  if (ws_bytes < posfeat_disk_loss_workspace(b, H, W)) return POSFEAT_E_WORKSPACE;
+  const int n = (H / 8) * (W / 8);
+  if (n % 4) return POSFEAT_E_UNSUPPORTED;
+  hipStream_t st = pf_stream(stream);
+  char* p = static_cast<char*>(ws);
+  auto take = [&](size_t bytes) {
+    char* r = p;
+    p += pf_align(bytes, 256);
+    return static_cast<void*>(r);
+  };
+  float* cpx1 = static_cast<float*>(take((size_t)b * n * 8));
+  float* cpx2 = static_cast<float*>(take((size_t)b * n * 8));
+  float* cn1 = static_cast<float*>(take((size_t)b * n * 8));
+  float* cn2 = static_cast<float*>(take((size_t)b * n * 8));
+  float* lp1 = static_cast<float*>(take((size_t)b * n * 4));
+  float* lp2 = static_cast<float*>(take((size_t)b * n * 4));
+  int32_t* pr1 = static_cast<int32_t*>(take((size_t)b * n * 4));
+  int32_t* pr2 = static_cast<int32_t*>(take((size_t)b * n * 4));
+  uint8_t* ac1 = static_cast<uint8_t*>(take((size_t)b * n));
+  uint8_t* ac2 = static_cast<uint8_t*>(take((size_t)b * n));
+  float* f1 = static_cast<float*>(take((size_t)b * n * 512));
+  float* f2 = static_cast<float*>(take((size_t)b * n * 512));
+  float* S = static_cast<float*>(take((size_t)b * n * n * 4));
+  float* lr = static_cast<float*>(take((size_t)b * n * 4));
+  float* lc = static_cast<float*>(take((size_t)b * n * 4));
+  float* ln1 = static_cast<float*>(take((size_t)b * n * 12));
+  float* ln2 = static_cast<float*>(take((size_t)b * n * 12));
+  double* part = static_cast<double*>(take((size_t)b * ((n + 3) / 4) * 8));
+  const unsigned pts_blocks = (unsigned)(((long long)b * n + 3) / 4);
+  hipLaunchKernelGGL(disk_point_kernel, dim3(pts_blocks), dim3(256), 0, st, kp1, b, H, W, prop1,
+                     acc1, sampled ? uni1 : nullptr, pr1, ac1, cpx1, cn1, lp1);
+  hipLaunchKernelGGL(disk_point_kernel, dim3(pts_blocks), dim3(256), 0, st, kp2, b, H, W, prop2,
+                     acc2, sampled ? uni2 : nullptr, pr2, ac2, cpx2, cn2, lp2);
+  PF_CHECK_LAUNCH();
+  PF_TRY(pf_sample_desc(xf1, b, 128, H / 4, W / 4, cs1, cn1, n, nullptr, 1, f1, st));
+  PF_TRY(pf_sample_desc(xf2, b, 128, H / 4, W / 4, cs2, cn2, n, nullptr, 1, f2, st));
+  for (int i = 0; i < b; ++i) {
+    posfeat_conv_desc d;
+    d.n = 1;
+    d.h = 1;
+    d.w = n;
+    d.cin = 128;
+    d.x_cstride = 128;
+    d.cout = n;
+    d.kh = d.kw = d.stride = 1;
+    d.pad = 0;
+    d.y_cstride = n;
+    d.res_cstride = 0;
+    d.act = POSFEAT_ACT_NONE;
+    PF_TRY(posfeat_conv2d_nhwc(&d, f1 + (size_t)i * n * 128, f2 + (size_t)i * n * 128, nullptr,
+                               nullptr, S + (size_t)i * n * n, st));
+  }
+  hipLaunchKernelGGL(row_lse_kernel, dim3(pts_blocks), dim3(256), 0, st, S, (long long)b * n, n,
+                     temperature, lr);
+  hipLaunchKernelGGL(col_lse_kernel, dim3((n + 255) / 256, b), dim3(256), 0, st, S, n, n,
+                     temperature, lc);
+  hipLaunchKernelGGL(epi_line_kernel, dim3((b * n + 255) / 256), dim3(256), 0, st, F1, cpx1, b, n,
+                     ln1);
+  hipLaunchKernelGGL(epi_line_kernel, dim3((b * n + 255) / 256), dim3(256), 0, st, F2, cpx2, b, n,
+                     ln2);
+  PF_CHECK_LAUNCH();
+  const int mblocks = (n + 3) / 4;
+  hipLaunchKernelGGL(reinforce_kernel, dim3(mblocks, b), dim3(RB), 0, st, S, n, n, temperature,
+                     lr, lc, ac1, ac2, lp1, lp2, ln1, ln2, cpx1, cpx2, reward_thr, good_reward,
+                     bad_reward, part);
+  PF_CHECK_LAUNCH();
+  hipLaunchKernelGGL(disk_final_kernel, dim3(1), dim3(1024), 0, st, part, b * mblocks, ac1, ac2,
+                     lp1, lp2, b, n, n, kp_penalty, out);
+  PF_CHECK_LAUNCH();
+  return POSFEAT_OK;
+}

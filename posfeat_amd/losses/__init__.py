@@ -1,5 +1,9 @@
-"""Drop-in for the reference's ``losses`` package: ``preprocess_utils`` (the
-extraction-path detector / sampler).  The training-side correlation modules
-(Preprocess_Line2Window, EpipolarLoss_full, DiskLoss) are SURVEY §8 rows
-a9-a11 and land in later rounds."""
+"""Drop-in for the reference's ``losses`` package (losses/__init__.py):
+``preprocess_utils`` (extraction detector / sampler), ``Preprocess_Line2Window``
+and ``Preprocess_Skip`` (preprocess.py), ``EpipolarLoss_full``
+(epipolarloss.py) and ``DiskLoss`` (kploss.py) -- forward values on the HIP
+path."""
 from . import preprocess_utils  # noqa: F401
+from .preprocess import Preprocess_Line2Window, Preprocess_Skip  # noqa: F401
+from .epipolarloss import EpipolarLoss_full  # noqa: F401
+from .kploss import DiskLoss  # noqa: F401

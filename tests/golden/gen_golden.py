@@ -238,9 +238,94 @@ def gen_extract_full(out):
     np.savez_compressed(out, **res)
 
 
+def synthetic_fundamental(b, h, w, seed):
+    """F1/F2 from K, R, t exactly as datasets/megadepth.py:426-448 builds them
+    (E = [t]x R, F = K2^-T E K1^-1, normalised by F[2,2]); K with f = w*0.8,
+    principal point at the centre, R = exp(small rotvec), t = random unit."""
+    from posfeat_amd.correlation import synthetic_fundamental as sf
+    return sf(b, h, w, seed)
+
+
+DESC_CFG = {"kps_generator": "generate_kpts_regular_grid_random",
+            "kps_generator_config": {"grid_size": 16, "map_init": "identity",
+                                     "keep_spatial": True, "random_select": "random"},
+            "window_size": 0.1, "loss_distance": "cos", "use_nn_grid": False,
+            "use_line_search": True,
+            "line_search_config": {"line_step": 100, "use_nn": True, "loc_rand": True},
+            "temperature_base": 60, "temperature_max": 60}
+EPI_CFG = {"grid_cost_thr": 0.5, "win_cost_thr": 0.1, "use_std_as_weight": True,
+           "weight_grid": 0, "weight_window": 1}
+DISK_CFG = {"grid_size": 8, "loss_distance": "cos", "temperature_base": 60,
+            "temperature_max": 60, "epipolar_reward": "constant_reward",
+            "reward_config": {"reward_thr": 2, "rescale_thr": False}, "cor_detach": True,
+            "good_reward": 1, "bad_reward": -0.25, "kp_penalty": -0.001, "match_grad": False}
+
+
+def corr_inputs(b, H, W, seed):
+    rs = np.random.RandomState(seed)
+    xf1 = torch.from_numpy(rs.randn(b, 128, H // 4, W // 4).astype(np.float32))
+    xf2 = torch.from_numpy(rs.randn(b, 128, H // 4, W // 4).astype(np.float32))
+    # smooth the maps a little so correlations have structure
+    xf1 = F.avg_pool2d(xf1, 3, 1, 1)
+    xf2 = F.avg_pool2d(xf2, 3, 1, 1)
+    kp1 = torch.from_numpy(rs.rand(b, 1, H, W).astype(np.float32) * 3)
+    kp2 = torch.from_numpy(rs.rand(b, 1, H, W).astype(np.float32) * 3)
+    F1, F2 = synthetic_fundamental(b, H, W, seed)
+    return xf1, xf2, kp1, kp2, torch.from_numpy(F1), torch.from_numpy(F2)
+
+
+@torch.no_grad()
+def gen_correlation(out):
+    res = {}
+    for tag, (b, H, W, seed) in {"s": (2, 240, 320, 3), "f": (1, 480, 640, 4)}.items():
+        xf1, xf2, kp1, kp2, F1, F2 = corr_inputs(b, H, W, seed)
+        inputs = {"im1": torch.zeros(b, 3, H, W), "im2": torch.zeros(b, 3, H, W), "F1": F1, "F2": F2}
+        outputs = {"preds1": {"global_map": xf1[:, :, ::4, ::4], "local_map": xf1,
+                              "local_point": kp1},
+                   "preds2": {"global_map": xf2[:, :, ::4, ::4], "local_map": xf2,
+                              "local_point": kp2}, "epoch": 0}
+        pre = ref_losses.Preprocess_Line2Window(DESC_CFG)
+        torch.manual_seed(100 + seed)
+        proc = pre(inputs, outputs)
+        # replay the RNG draws (same seed, same call sequence)
+        torch.manual_seed(100 + seed)
+        k1, k2, _, _ = ref_putils.generate_kpts_regular_grid_random(
+            inputs, outputs, **DESC_CFG["kps_generator_config"])
+        n = k1.shape[1] * k1.shape[2]
+        r1 = torch.rand(b, n, 2)
+        r2 = torch.rand(b, n, 2)
+        for name, k, hh, ww in (("sel1", k1, H, W), ("sel2", k2, H, W)):
+            ix = torch.round((k[..., 0] + 1) / 2 * (ww - 1)).long()
+            iy = torch.round((k[..., 1] + 1) / 2 * (hh - 1)).long()
+            res["%s_%s" % (tag, name)] = ((iy % 16) * 16 + ix % 16).int().numpy()
+        res[tag + "_rand1"] = r1.numpy()
+        res[tag + "_rand2"] = r2.numpy()
+        for k, v in proc.items():
+            if torch.is_tensor(v):
+                res["%s_proc_%s" % (tag, k)] = v.numpy()
+        loss, comp = ref_losses.EpipolarLoss_full(EPI_CFG)(inputs, outputs, proc)
+        res[tag + "_epi_loss"] = loss.numpy()
+        for k, v in comp.items():
+            res["%s_epi_%s" % (tag, k)] = v.numpy()
+        # DiskLoss on the same maps
+        dl = ref_losses.DiskLoss(DISK_CFG)
+        torch.manual_seed(200 + seed)
+        dloss, dcomp = dl(inputs, outputs, None)
+        torch.manual_seed(200 + seed)
+        for i, km in ((1, kp1), (2, kp2)):
+            kps, logp, acc = dl.point_sample(km)
+            ix, iy = kps[..., 0].long(), kps[..., 1].long()
+            res["%s_prop%d" % (tag, i)] = ((iy % 8) * 8 + ix % 8).int().numpy()[:, None]
+            res["%s_acc%d" % (tag, i)] = acc.numpy()
+        res[tag + "_disk_loss"] = dloss.numpy()
+        for k in ("reinforce", "kp_penalty", "n_kps"):
+            res["%s_disk_%s" % (tag, k)] = dcomp[k].numpy()
+    np.savez_compressed(out, **res)
+
+
 if __name__ == "__main__":
     torch.set_num_threads(os.cpu_count() or 8)
-    which = sys.argv[1:] or ["detector", "sampler", "model_small", "extract_full"]
+    which = sys.argv[1:] or ["detector", "sampler", "model_small", "extract_full", "correlation"]
     if "detector" in which:
         gen_detector(os.path.join(HERE, "detector.npz"))
     if "sampler" in which:
@@ -249,4 +334,6 @@ if __name__ == "__main__":
         gen_model_small(os.path.join(HERE, "model_small.npz"))
     if "extract_full" in which:
         gen_extract_full(os.path.join(HERE, "extract_full.npz"))
+    if "correlation" in which:
+        gen_correlation(os.path.join(HERE, "correlation.npz"))
     print("golden fixtures written to", HERE)
