@@ -43,6 +43,120 @@ struct ConvArgs {
   int hw;            // OH*OW (image boundary inside a tile for `stats`)
 };
 
+// Epilogue shared by both kernels: acc -> LDS T[BM][BN+4] (conflict-free: a
+// half-wave writes 32 consecutive floats of one row), then each thread owns a
+// fixed 4-column group and walks rows: residual loads are all issued before
+// use, stores are float4.  Optional fused instance-norm partials.  Requires
+// the caller's K loop to have ended with a barrier (smem is reused).
+// `rowm(row)` maps a tile row to its output pixel m (or -1: outside); img0 is
+// the image of the tile's first row (stats slot 0).
+template <int BM, int BN, int WM, int WN, class RowMap>
+__device__ __forceinline__ void conv_epilogue(const ConvArgs& a,
+                                              f32x16 (&acc)[BM / WM / 32][BN / WN / 32],
+                                              float* smem, int tm, int n0, int split,
+                                              RowMap rowm, int img0) {
+  constexpr int THREADS = WM * WN * 64;
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int MI = TM / 32, NI = TN / 32;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  constexpr int TP = BN + 4;
+  float* T = smem;  // the K loop ended with a barrier: staging LDS is free
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        T[(wm * TM + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * TP + wn * TN + ni * 32 +
+          (lane & 31)] = acc[mi][ni][r];
+  __syncthreads();
+  constexpr int C4 = BN / 4;
+  constexpr int RPP = THREADS / C4;  // rows per pass
+  constexpr int NP = BM / RPP;
+  const int q = tid % C4, r0 = tid / C4;
+  const int col = n0 + 4 * q;
+  const bool colok = col < a.Cout;
+  if (a.ksplit > 1) {  // raw partial sums; conv_splitk_reduce finishes
+    float* pp = a.part + (size_t)split * a.M * a.Cout;
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const int row = r0 + p * RPP;
+      const int m = rowm(row);
+      if (colok && m >= 0)
+        *reinterpret_cast<f32x4*>(pp + (size_t)m * a.Cout + col) =
+            *reinterpret_cast<const f32x4*>(T + row * TP + 4 * q);
+    }
+    return;
+  }
+  f32x4 rv[NP];
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const int m = rowm(r0 + p * RPP);
+    rv[p] = (a.res && colok && m >= 0)
+                ? *reinterpret_cast<const f32x4*>(a.res + (size_t)m * a.rcs + col)
+                : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const f32x4 bv = (a.bias && colok) ? *reinterpret_cast<const f32x4*>(a.bias + col)
+                                     : f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 s1[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}}, s2[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const int row = r0 + p * RPP;
+    const int m = rowm(row);
+    if (!colok || m < 0) continue;
+    f32x4 v = *reinterpret_cast<const f32x4*>(T + row * TP + 4 * q) + bv + rv[p];
+    if (a.act == POSFEAT_ACT_RELU) {
+      v.x = fmaxf(v.x, 0.f);
+      v.y = fmaxf(v.y, 0.f);
+      v.z = fmaxf(v.z, 0.f);
+      v.w = fmaxf(v.w, 0.f);
+    } else if (a.act == POSFEAT_ACT_ELU) {
+      v.x = pf_elu(v.x);
+      v.y = pf_elu(v.y);
+      v.z = pf_elu(v.z);
+      v.w = pf_elu(v.w);
+    }
+    *reinterpret_cast<f32x4*>(a.y + (size_t)m * a.ycs + col) = v;
+    if (a.stats) {
+      const int sl = (m / a.hw) != img0;
+      if (sl) {
+        s1[1] += v;
+        s2[1] += v * v;
+      } else {
+        s1[0] += v;
+        s2[0] += v * v;
+      }
+    }
+  }
+  if (a.stats) {  // reduce the RPP row groups of each column in a fixed order
+    __syncthreads();
+    float* R = smem;  // [RPP][2 slots][BN][2]
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        R[((r0 * 2 + sl) * BN + 4 * q + k) * 2 + 0] = s1[sl][k];
+        R[((r0 * 2 + sl) * BN + 4 * q + k) * 2 + 1] = s2[sl][k];
+      }
+    __syncthreads();
+    for (int e = tid; e < 2 * BN; e += THREADS) {
+      const int sl = e / BN, c = e - sl * BN;
+      if (n0 + c >= a.Cout) continue;
+      float t1 = 0.f, t2 = 0.f;
+      for (int rr = 0; rr < RPP; ++rr) {
+        t1 += R[((rr * 2 + sl) * BN + c) * 2 + 0];
+        t2 += R[((rr * 2 + sl) * BN + c) * 2 + 1];
+      }
+      float* o = a.stats + (((size_t)tm * 2 + sl) * a.Cout + n0 + c) * 2;
+      o[0] = t1;
+      o[1] = t2;
+    }
+  }
+}
+
 template <int BM, int BN, int WM, int WN, bool CIN32>
 __global__ __launch_bounds__(WM* WN * 64) void conv_mfma_kernel(ConvArgs a) {
   constexpr int THREADS = WM * WN * 64;
@@ -212,104 +326,334 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_mfma_kernel(ConvArgs a) {
     __syncthreads();
   }
 
-  // ---- epilogue, staged through LDS so global traffic is 16-B per lane ----
-  // acc -> T[BM][BN+4] (conflict-free: a half-wave writes 32 consecutive
-  // floats of one row), then each thread owns a fixed 4-column group and walks
-  // rows: residual loads are all issued before use, stores are float4.
-  constexpr int TP = BN + 4;
-  float* T = smem;  // the K loop ended with a barrier: staging LDS is free
+  conv_epilogue<BM, BN, WM, WN>(
+      a, acc, smem, tm, n0, split, [&](int row) { return m0 + row < a.M ? m0 + row : -1; },
+      m0 / a.hw);
+}
+
+// ---------------------------------------------------------------------------
+// Direct-to-LDS variant for Cin % 32 == 0 (every deep layer).  The register-
+// staged loop above spends ~18% of the head.conv2 time on staging (global
+// loads into VGPRs + ds_write_b128, whose VGPR->LDS transfer competes with the
+// MFMA issue; ablation in DESIGN.md).  Here each lane issues
+// global_load_lds_dwordx4: one wave-instruction fills 8 LDS rows of 128 B
+// (one 32-channel chunk of 8 pixels / 8 couts) with no VGPR round trip.
+// LDS rows carry no padding (the DMA destination is lane-linear), so bank
+// conflicts on the MFMA operand reads are removed by an XOR swizzle: 16-B slot
+// s of row r is stored at slot s ^ ((r >> 1) & 7) -- distinct banks for every
+// 16-lane group of ds_read_b128.  The swizzle is applied on the per-lane
+// global SOURCE address (LDS image stays lane-linear) and undone on the read.
+// Zero padding (out-of-image taps, M / Cout tails) loads from a zeroed
+// 16-B device word.  Two LDS stages: chunk c+1 is in flight while chunk c is
+// multiplied; vmcnt(0) + barrier at the end of each chunk.
+__device__ __attribute__((aligned(16))) float pf_conv_zero16[4];
+
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(WM* WN * 64) void conv_glds_kernel(ConvArgs a) {
+  constexpr int THREADS = WM * WN * 64;
+  constexpr int NW = THREADS / 64;
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int MI = TM / 32, NI = TN / 32;
+  constexpr int A_G = BM / 8 / NW;  // DMA wave-instructions per chunk for A
+  constexpr int B_G = BN / 8 / NW;
+  static_assert(A_G >= 1 && B_G >= 1 && BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "tile");
+  static_assert(MI >= 1 && NI >= 1, "wave tile must be >= 32x32");
+  constexpr int RING = 2 * (BM + BN) * BK;
+  constexpr int STAGE = BM * (BN + 4);
+  __shared__ __attribute__((aligned(16))) float smem[RING > STAGE ? RING : STAGE];
+  float* As = smem;                // [2][BM][BK] swizzled
+  float* Bs = smem + 2 * BM * BK;  // [2][BN][BK] swizzled
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+
+  int bid = blockIdx.x % a.nwg;
+  const int split = blockIdx.x / a.nwg;
+  {
+    const int nwg = a.nwg, q = nwg >> 3, r = nwg & 7, xcd = bid & 7, slot = bid >> 3;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+  }
+  const int tm = bid / a.tiles_n, tn = bid - tm * a.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // ---- per-lane DMA sources (fixed across K) -------------------------------
+  // instruction i of this wave fills rows [(wave*G + i)*8, +8); lane L -> row
+  // +(L>>3), LDS slot L&7, which holds source k-slot (L&7) ^ ((row>>1)&7)
+  const int lrow = lane >> 3;
+  const float* xsrc[A_G];
+  unsigned tapok[A_G];  // bit t: tap t of this pixel is inside the image
+#pragma unroll
+  for (int i = 0; i < A_G; ++i) {
+    const int row = (wave * A_G + i) * 8 + lrow;
+    const int sslot = (lane & 7) ^ ((row >> 1) & 7);
+    const int m = m0 + row;
+    tapok[i] = 0u;
+    xsrc[i] = a.x;
+    if (m < a.M) {
+      const int n = m / a.hw;
+      const int rem = m - n * a.hw;
+      const int oh = rem / a.OW;
+      const int ow = rem - oh * a.OW;
+      const int ih0 = oh * a.stride - a.pad, iw0 = ow * a.stride - a.pad;
+      for (int kh = 0; kh < a.KH; ++kh)
+        for (int kw = 0; kw < a.KW; ++kw)
+          if ((unsigned)(ih0 + kh) < (unsigned)a.H && (unsigned)(iw0 + kw) < (unsigned)a.W)
+            tapok[i] |= 1u << (kh * a.KW + kw);
+      // base of tap (0,0); taps add a uniform offset (may point outside the
+      // image for masked taps: never dereferenced)
+      xsrc[i] = a.x + (long long)n * a.H * a.W * a.xcs + ((long long)ih0 * a.W + iw0) * a.xcs +
+                sslot * 4;
+    }
+  }
+  const float* wsrc[B_G];
+#pragma unroll
+  for (int i = 0; i < B_G; ++i) {
+    const int row = (wave * B_G + i) * 8 + lrow;
+    const int sslot = (lane & 7) ^ ((row >> 1) & 7);
+    wsrc[i] = (n0 + row < a.Cout) ? a.w + (size_t)(n0 + row) * a.Kpad + sslot * 4 : nullptr;
+  }
+
+  const int ntap = a.KH * a.KW;
+  const int nch_all = a.Kpad / BK;
+  const int ch0 = (int)((long long)nch_all * split / a.ksplit);
+  const int ch1 = (int)((long long)nch_all * (split + 1) / a.ksplit);
+
+  // issue the DMA of absolute chunk c into stage `buf`
+  auto issue_chunk = [&](int c, int buf) {
+    const int slab = c / ntap, tap = c - slab * ntap;
+    const int kh = tap / a.KW, kw = tap - kh * a.KW;
+    const long long delta = ((long long)kh * a.W + kw) * a.xcs + slab * BK;
+#pragma unroll
+    for (int i = 0; i < A_G; ++i) {
+      const float* src = ((tapok[i] >> tap) & 1u) ? xsrc[i] + delta : pf_conv_zero16;
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)src,
+          (__attribute__((address_space(3))) void*)(As + (buf * BM + (wave * A_G + i) * 8) * BK),
+          16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < B_G; ++i) {
+      const float* src = wsrc[i] ? wsrc[i] + (size_t)c * BK : pf_conv_zero16;
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)src,
+          (__attribute__((address_space(3))) void*)(Bs + (buf * BN + (wave * B_G + i) * 8) * BK),
+          16, 0, 0);
+    }
+  };
+
+  f32x16 acc[MI][NI];
 #pragma unroll
   for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
     for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
-      for (int r = 0; r < 16; ++r)
-        T[(wm * TM + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * TP + wn * TN + ni * 32 +
-          (lane & 31)] = acc[mi][ni][r];
+      for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
+
+  // operand reads: row R = 32-aligned base + (lane & 31), k-slot (lane>>5) + 2kk
+  const int sw = ((lane & 31) >> 1) & 7;
+  const int arow = wm * TM + (lane & 31);
+  const int brow = wn * TN + (lane & 31);
+  int kofs[BK / 8];
+#pragma unroll
+  for (int kk = 0; kk < BK / 8; ++kk) kofs[kk] = (((lane >> 5) + 2 * kk) ^ sw) * 4;
+
+  issue_chunk(ch0, 0);
+  __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0): the DMA has landed (this wave)
   __syncthreads();
-  constexpr int C4 = BN / 4;
-  constexpr int RPP = THREADS / C4;  // rows per pass
-  constexpr int NP = BM / RPP;
-  const int q = tid % C4, r0 = tid / C4;
-  const int col = n0 + 4 * q;
-  const bool colok = col < a.Cout;
-  if (a.ksplit > 1) {  // raw partial sums; conv_splitk_reduce finishes
-    float* pp = a.part + (size_t)split * a.M * a.Cout;
+
+  for (int c = ch0; c < ch1; ++c) {
+    const int cur = (c - ch0) & 1;
+    if (c + 1 < ch1) issue_chunk(c + 1, cur ^ 1);
+    const float* Ab = As + (cur * BM + arow) * BK;
+    const float* Bb = Bs + (cur * BN + brow) * BK;
 #pragma unroll
-    for (int p = 0; p < NP; ++p) {
-      const int row = r0 + p * RPP;
-      const int m = m0 + row;
-      if (colok && m < a.M)
-        *reinterpret_cast<f32x4*>(pp + (size_t)m * a.Cout + col) =
-            *reinterpret_cast<const f32x4*>(T + row * TP + 4 * q);
-    }
-    return;
-  }
-  f32x4 rv[NP];
+    for (int kk = 0; kk < BK / 8; ++kk) {
+      f32x4 av[MI], bv[NI];
 #pragma unroll
-  for (int p = 0; p < NP; ++p) {
-    const int m = m0 + r0 + p * RPP;
-    rv[p] = (a.res && colok && m < a.M)
-                ? *reinterpret_cast<const f32x4*>(a.res + (size_t)m * a.rcs + col)
-                : f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-  const f32x4 bv = (a.bias && colok) ? *reinterpret_cast<const f32x4*>(a.bias + col)
-                                     : f32x4{0.f, 0.f, 0.f, 0.f};
-  f32x4 s1[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}}, s2[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
-  const int img0 = m0 / a.hw;
+      for (int mi = 0; mi < MI; ++mi)
+        av[mi] = *reinterpret_cast<const f32x4*>(Ab + mi * 32 * BK + kofs[kk]);
 #pragma unroll
-  for (int p = 0; p < NP; ++p) {
-    const int row = r0 + p * RPP;
-    const int m = m0 + row;
-    if (!colok || m >= a.M) continue;
-    f32x4 v = *reinterpret_cast<const f32x4*>(T + row * TP + 4 * q) + bv + rv[p];
-    if (a.act == POSFEAT_ACT_RELU) {
-      v.x = fmaxf(v.x, 0.f);
-      v.y = fmaxf(v.y, 0.f);
-      v.z = fmaxf(v.z, 0.f);
-      v.w = fmaxf(v.w, 0.f);
-    } else if (a.act == POSFEAT_ACT_ELU) {
-      v.x = pf_elu(v.x);
-      v.y = pf_elu(v.y);
-      v.z = pf_elu(v.z);
-      v.w = pf_elu(v.w);
+      for (int ni = 0; ni < NI; ++ni)
+        bv[ni] = *reinterpret_cast<const f32x4*>(Bb + ni * 32 * BK + kofs[kk]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < NI; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[mi][j], bv[ni][j], acc[mi][ni],
+                                                                0, 0, 0);
     }
-    *reinterpret_cast<f32x4*>(a.y + (size_t)m * a.ycs + col) = v;
-    if (a.stats) {
-      const int sl = (m / a.hw) != img0;
-      if (sl) {
-        s1[1] += v;
-        s2[1] += v * v;
-      } else {
-        s1[0] += v;
-        s2[0] += v * v;
-      }
-    }
-  }
-  if (a.stats) {  // reduce the RPP row groups of each column in a fixed order
+    __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
-    float* R = smem;  // [RPP][2 slots][BN][2]
-#pragma unroll
-    for (int sl = 0; sl < 2; ++sl)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        R[((r0 * 2 + sl) * BN + 4 * q + k) * 2 + 0] = s1[sl][k];
-        R[((r0 * 2 + sl) * BN + 4 * q + k) * 2 + 1] = s2[sl][k];
-      }
-    __syncthreads();
-    for (int e = tid; e < 2 * BN; e += THREADS) {
-      const int sl = e / BN, c = e - sl * BN;
-      if (n0 + c >= a.Cout) continue;
-      float t1 = 0.f, t2 = 0.f;
-      for (int rr = 0; rr < RPP; ++rr) {
-        t1 += R[((rr * 2 + sl) * BN + c) * 2 + 0];
-        t2 += R[((rr * 2 + sl) * BN + c) * 2 + 1];
-      }
-      float* o = a.stats + (((size_t)tm * 2 + sl) * a.Cout + n0 + c) * 2;
-      o[0] = t1;
-      o[1] = t2;
-    }
   }
+
+  conv_epilogue<BM, BN, WM, WN>(
+      a, acc, smem, tm, n0, split, [&](int row) { return m0 + row < a.M ? m0 + row : -1; },
+      m0 / a.hw);
+}
+
+// ---------------------------------------------------------------------------
+// Spatial-halo variant for stride-1 convs with Cin % 32 == 0 (every 3x3
+// decoder/head layer).  The M tile is a PH x 16 patch of output pixels of one
+// image; for each 32-channel slab its (PH+KH-1) x (16+KW-1) input halo is
+// DMA'd into LDS ONCE and all KH*KW taps read it at shifted rows, so the A
+// staging per slab drops from KH*KW*BM pixel rows to the halo (180 vs 1152
+// for 8x16, 3x3).  B (weights) is staged per (slab, tap) chunk as above.
+// LDS halo row hp = hy*(16+KW-1) + hx holds 128 B (32 channels) with 16-B slot
+// s stored at s ^ ((hx >> 1) & 7): the 16 lanes of a ds_read_b128 group cover
+// 16 consecutive output columns, i.e. 16 distinct hx mod 16 for every tap
+// shift -> conflict-free.  Next slab's halo and next chunk's weights are in
+// flight while the current chunk is multiplied (two LDS stages each).
+template <int PH, int BN, int WM, int WN, int KH, int KW>
+__global__ __launch_bounds__(WM* WN * 64) void conv_halo_kernel(ConvArgs a) {
+  constexpr int PW = 16;
+  constexpr int BM = PH * PW;
+  constexpr int THREADS = WM * WN * 64;
+  constexpr int NW = THREADS / 64;
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int MI = TM / 32, NI = TN / 32;
+  constexpr int NTAP = KH * KW;
+  constexpr int HX = PW + KW - 1, HY = PH + KH - 1, HP = HX * HY;
+  constexpr int A_G = (HP + 8 * NW - 1) / (8 * NW);  // halo DMA instructions per wave
+  constexpr int HPR = A_G * 8 * NW;                  // LDS halo rows (>= HP)
+  constexpr int B_G = BN / 8 / NW;
+  static_assert(TM % 32 == 0 && MI >= 1 && NI >= 1 && B_G >= 1 && BN % (8 * NW) == 0, "tile");
+  constexpr int RING = 2 * (HPR + BN) * BK;
+  constexpr int STAGE = BM * (BN + 4);
+  __shared__ __attribute__((aligned(16))) float smem[RING > STAGE ? RING : STAGE];
+  float* As = smem;                 // [2][HPR][BK] halo, swizzled by hx
+  float* Bs = smem + 2 * HPR * BK;  // [2][BN][BK] swizzled by row
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+
+  int bid = blockIdx.x % a.nwg;
+  const int split = blockIdx.x / a.nwg;
+  {
+    const int nwg = a.nwg, q = nwg >> 3, r = nwg & 7, xcd = bid & 7, slot = bid >> 3;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+  }
+  const int tm = bid / a.tiles_n, tn = bid - tm * a.tiles_n;
+  const int n0 = tn * BN;
+  const int ptx = (a.OW + PW - 1) / PW, ppi = ptx * ((a.OH + PH - 1) / PH);
+  const int img = tm / ppi, prem = tm - img * ppi;
+  const int oy0 = (prem / ptx) * PH, ox0 = (prem - (prem / ptx) * ptx) * PW;
+
+  // ---- per-lane halo DMA sources (slab 0) ----------------------------------
+  const int lrow = lane >> 3;
+  const float* hsrc[A_G];
+#pragma unroll
+  for (int i = 0; i < A_G; ++i) {
+    const int hp = (wave * A_G + i) * 8 + lrow;
+    const int hy = hp / HX, hx = hp - (hp / HX) * HX;
+    const int ih = oy0 - a.pad + hy, iw = ox0 - a.pad + hx;
+    const int sslot = (lane & 7) ^ ((hx >> 1) & 7);
+    hsrc[i] = (hp < HP && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
+                  ? a.x + (((long long)img * a.H + ih) * a.W + iw) * a.xcs + sslot * 4
+                  : nullptr;
+  }
+  const float* wsrc[B_G];
+#pragma unroll
+  for (int i = 0; i < B_G; ++i) {
+    const int row = (wave * B_G + i) * 8 + lrow;
+    const int sslot = (lane & 7) ^ ((row >> 1) & 7);
+    wsrc[i] = (n0 + row < a.Cout) ? a.w + (size_t)(n0 + row) * a.Kpad + sslot * 4 : nullptr;
+  }
+  auto issue_halo = [&](int slab, int buf) {
+#pragma unroll
+    for (int i = 0; i < A_G; ++i) {
+      const float* src = hsrc[i] ? hsrc[i] + slab * BK : pf_conv_zero16;
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)src,
+          (__attribute__((address_space(3))) void*)(As + (buf * HPR + (wave * A_G + i) * 8) * BK),
+          16, 0, 0);
+    }
+  };
+  auto issue_w = [&](int c, int buf) {
+#pragma unroll
+    for (int i = 0; i < B_G; ++i) {
+      const float* src = wsrc[i] ? wsrc[i] + (size_t)c * BK : pf_conv_zero16;
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)src,
+          (__attribute__((address_space(3))) void*)(Bs + (buf * BN + (wave * B_G + i) * 8) * BK),
+          16, 0, 0);
+    }
+  };
+
+  f32x16 acc[MI][NI];
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
+
+  // operand rows: tile row R = wm*TM + mi*32 + (lane&31) -> patch (R>>4, R&15)
+  const int px = lane & 15;
+  const int hrow0 = ((wm * TM + (lane & 31)) >> 4) * HX + px;  // tap (0,0), mi = 0
+  const int brow = wn * TN + (lane & 31);
+  const int bsw = ((lane & 31) >> 1) & 7;
+
+  const int nch_all = a.Kpad / BK;
+  const int ch0 = (int)((long long)nch_all * split / a.ksplit);
+  const int ch1 = (int)((long long)nch_all * (split + 1) / a.ksplit);
+  int slab = ch0 / NTAP, tap = ch0 - slab * NTAP;
+  issue_halo(slab, 0);
+  issue_w(ch0, 0);
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+
+  int abuf = 0;
+  for (int c = ch0; c < ch1; ++c) {
+    const int bcur = (c - ch0) & 1;
+    if (c + 1 < ch1) {
+      issue_w(c + 1, bcur ^ 1);
+      if (tap == NTAP - 1) issue_halo(slab + 1, abuf ^ 1);
+    }
+    const int kh = tap / KW, kw = tap - (tap / KW) * KW;
+    const int hsw = ((px + kw) >> 1) & 7;
+    const float* Ab = As + (abuf * HPR + hrow0 + kh * HX + kw) * BK;
+    const float* Bb = Bs + (bcur * BN + brow) * BK;
+#pragma unroll
+    for (int kk = 0; kk < BK / 8; ++kk) {
+      const int s = (lane >> 5) + 2 * kk;
+      f32x4 av[MI], bv[NI];
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi)
+        av[mi] = *reinterpret_cast<const f32x4*>(Ab + mi * 2 * HX * BK + (s ^ hsw) * 4);
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni)
+        bv[ni] = *reinterpret_cast<const f32x4*>(Bb + ni * 32 * BK + (s ^ bsw) * 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < NI; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[mi][j], bv[ni][j], acc[mi][ni],
+                                                                0, 0, 0);
+    }
+    if (++tap == NTAP) {
+      tap = 0;
+      ++slab;
+      abuf ^= 1;
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+  }
+
+  conv_epilogue<BM, BN, WM, WN>(
+      a, acc, smem, tm, n0, split,
+      [&](int row) {
+        const int oy = oy0 + (row >> 4), ox = ox0 + (row & 15);
+        return (oy < a.OH && ox < a.OW) ? (img * a.OH + oy) * a.OW + ox : -1;
+      },
+      img);
 }
 
 // Instance-norm statistics from the per-tile partials of the conv epilogue.
@@ -321,17 +665,19 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_mfma_kernel(ConvArgs a) {
 constexpr int STAT_CHUNK = 256;
 
 __global__ __launch_bounds__(1024) void conv_stats_chunk(const float* __restrict__ part, int BM,
-                                                         int hw, int C, int nchunk,
+                                                         int ppi, int hw, int C, int nchunk,
                                                          double* __restrict__ chunks) {
   const int b = blockIdx.z, cg = blockIdx.y, ch = blockIdx.x;
   const int c = cg * 64 + (threadIdx.x & 63), tl = threadIdx.x >> 6;  // 16 tile lanes
-  const long long t0 = (long long)b * hw / BM, t1 = ((long long)(b + 1) * hw - 1) / BM;
+  // image b's tiles: contiguous rows [b*hw/BM, ((b+1)*hw-1)/BM] or patches [b*ppi, (b+1)*ppi)
+  const long long t0 = ppi ? (long long)b * ppi : (long long)b * hw / BM;
+  const long long t1 = ppi ? (long long)(b + 1) * ppi - 1 : ((long long)(b + 1) * hw - 1) / BM;
   const long long ts = t0 + (long long)ch * STAT_CHUNK;
   const long long te = min(t1 + 1, ts + STAT_CHUNK);
   double s1 = 0.0, s2 = 0.0;
   if (c < C) {
     for (long long t = ts + tl; t < te; t += 16) {
-      const int sl = (t * BM) / hw == b ? 0 : 1;
+      const int sl = (ppi || (t * BM) / hw == b) ? 0 : 1;
       const float* p = part + ((t * 2 + sl) * C + c) * 2;
       s1 += p[0];
       s2 += p[1];
@@ -402,32 +748,41 @@ __global__ void conv_splitk_reduce(const float* __restrict__ part, int ks, int M
   }
 }
 
-template <int BM, int BN, int WM, int WN>
-int launch_cfg(ConvArgs& a, bool cin32, hipStream_t st) {
-  const int tiles_m = (a.M + BM - 1) / BM;
-  a.tiles_n = (a.Cout + BN - 1) / BN;
-  a.nwg = tiles_m * a.tiles_n;
-  dim3 grid(a.nwg * a.ksplit), block(WM * WN * 64);
-  if (cin32)
-    hipLaunchKernelGGL((conv_mfma_kernel<BM, BN, WM, WN, true>), grid, block, 0, st, a);
-  else
-    hipLaunchKernelGGL((conv_mfma_kernel<BM, BN, WM, WN, false>), grid, block, 0, st, a);
-  PF_CHECK_LAUNCH();
-  if (a.ksplit > 1) {
-    const long long total = (long long)a.M * (a.Cout / 4);
-    long long g = (total + 255) / 256;
-    if (g > 16384) g = 16384;
-    hipLaunchKernelGGL(conv_splitk_reduce, dim3((int)g), dim3(256), 0, st, a.part, a.ksplit, a.M,
-                       a.Cout, a.bias, a.res, a.rcs, a.act, a.y, a.ycs);
-    PF_CHECK_LAUNCH();
+// ---------------------------------------------------------------------------
+// Launch planning: one Plan decides kernel, tile and split for a conv so the
+// launch, the split-K workspace and the stats reduction agree on the tiling.
+enum ConvKern { KERN_STAGED = 0, KERN_GLDS = 1, KERN_HALO = 2 };
+enum ConvTile {
+  TILE_128x128 = 0, TILE_128x64 = 1, TILE_64x64 = 2, TILE_256x128 = 3,  // contiguous rows
+  TILE_H8x128 = 10, TILE_H8x64 = 11, TILE_H16x128 = 12                  // 8/16 x 16 patches
+};
+struct Plan {
+  int kern, tile, bm, bn, ppi;  // ppi: patches per image (halo), 0 = contiguous rows
+  long long tiles_m;
+  int ksplit;
+};
+
+// Environment switches for A/B timing only (defaults are the tuned choice):
+// POSFEAT_CONV_KERNEL=staged|glds|halo caps the kernel family, POSFEAT_CONV_TILE
+// forces a tile id where legal.
+struct ConvEnv {
+  int kmax = KERN_HALO, tile = -1;
+  ConvEnv() {
+    if (const char* e = getenv("POSFEAT_CONV_KERNEL")) {
+      if (e[0] == 's') kmax = KERN_STAGED;
+      else if (e[0] == 'g') kmax = KERN_GLDS;
+    }
+    if (const char* e = getenv("POSFEAT_CONV_TILE")) tile = atoi(e);
   }
-  return POSFEAT_OK;
+};
+const ConvEnv& conv_env() {
+  static const ConvEnv e;
+  return e;
 }
 
-// Split-K factor for the 128x128 tile: only for deep K (>= 32 chunks) where
-// the tile count leaves the last wave of workgroups badly underfilled.
-int choose_ksplit(long long tiles, int nch) {
-  const double slots = 256.0 * 2.0;  // CUs x resident 128x128 blocks
+// Split-K factor: only for deep K (>= 64 chunks) where the tile count leaves
+// the last round of resident workgroups badly underfilled.
+int choose_ksplit(long long tiles, int nch, double slots) {
   if (nch < 64) return 1;
   int best = 1;
   double best_eff = 0.0;
@@ -441,6 +796,93 @@ int choose_ksplit(long long tiles, int nch) {
     }
   }
   return best;
+}
+
+Plan conv_plan(const ConvArgs& a, bool allow_split) {
+  const ConvEnv& env = conv_env();
+  Plan p{};
+  const bool cin32 = a.Cin % BK == 0;
+  const int nch = a.Kpad / BK;
+  const bool halo_ok = cin32 && env.kmax >= KERN_HALO && a.stride == 1 && a.KH == 3 &&
+                       a.KW == 3 && a.OW >= 16 && a.OH >= 8 && a.Cout % 64 == 0;
+  if (halo_ok) {
+    p.kern = KERN_HALO;
+    if (a.Cout % 128 == 0)
+      p.tile = env.tile == TILE_H16x128 ? TILE_H16x128 : TILE_H8x128;
+    else
+      p.tile = TILE_H8x64;
+    const int ph = p.tile == TILE_H16x128 ? 16 : 8;
+    p.bm = ph * 16;
+    p.bn = p.tile == TILE_H8x64 ? 64 : 128;
+    p.ppi = ((a.OW + 15) / 16) * ((a.OH + ph - 1) / ph);
+    p.tiles_m = (long long)(a.M / a.hw) * p.ppi;
+    const double slots = p.tile == TILE_H16x128 ? 256.0 : 512.0;
+    p.ksplit = allow_split ? choose_ksplit(p.tiles_m * ((a.Cout + p.bn - 1) / p.bn), nch, slots)
+                           : 1;
+    return p;
+  }
+  p.kern = !cin32 ? KERN_STAGED
+                  : (env.kmax >= KERN_GLDS && a.KH * a.KW <= 32 ? KERN_GLDS : KERN_STAGED);
+  p.ppi = 0;
+  const long long t128 = (long long)((a.M + 127) / 128) * ((a.Cout + 127) / 128);
+  const long long t256 = (long long)((a.M + 255) / 256) * ((a.Cout + 127) / 128);
+  p.ksplit = (allow_split && a.Cout > 64) ? choose_ksplit(t128, nch, 512.0) : 1;
+  if (env.tile == TILE_256x128 && cin32 && a.Cout % 128 == 0 && t256 >= 256 && p.ksplit == 1)
+    p.tile = TILE_256x128;
+  else if (a.Cout > 64 && (t128 >= 512 || p.ksplit > 1))
+    p.tile = TILE_128x128;
+  else if ((long long)((a.M + 127) / 128) * ((a.Cout + 63) / 64) >= 512)
+    p.tile = TILE_128x64;
+  else
+    p.tile = TILE_64x64;
+  p.bm = p.tile == TILE_64x64 ? 64 : p.tile == TILE_256x128 ? 256 : 128;
+  p.bn = (p.tile == TILE_128x128 || p.tile == TILE_256x128) ? 128 : 64;
+  if (p.tile != TILE_128x128) p.ksplit = 1;
+  p.tiles_m = (a.M + p.bm - 1) / p.bm;
+  return p;
+}
+
+template <int BM, int BN, int WM, int WN>
+void launch_rows(ConvArgs& a, int kern, hipStream_t st) {
+  dim3 grid(a.nwg * a.ksplit), block(WM * WN * 64);
+  if (kern == KERN_GLDS)
+    hipLaunchKernelGGL((conv_glds_kernel<BM, BN, WM, WN>), grid, block, 0, st, a);
+  else if (a.Cin % BK == 0)
+    hipLaunchKernelGGL((conv_mfma_kernel<BM, BN, WM, WN, true>), grid, block, 0, st, a);
+  else
+    hipLaunchKernelGGL((conv_mfma_kernel<BM, BN, WM, WN, false>), grid, block, 0, st, a);
+}
+
+int conv_run(ConvArgs& a, const Plan& p, hipStream_t st) {
+  a.tiles_n = (a.Cout + p.bn - 1) / p.bn;
+  a.nwg = (int)(p.tiles_m * a.tiles_n);
+  a.ksplit = p.ksplit;
+  const dim3 grid(a.nwg * a.ksplit);
+  switch (p.tile) {
+    case TILE_H8x128:
+      hipLaunchKernelGGL((conv_halo_kernel<8, 128, 2, 2, 3, 3>), grid, dim3(256), 0, st, a);
+      break;
+    case TILE_H8x64:
+      hipLaunchKernelGGL((conv_halo_kernel<8, 64, 2, 2, 3, 3>), grid, dim3(256), 0, st, a);
+      break;
+    case TILE_H16x128:
+      hipLaunchKernelGGL((conv_halo_kernel<16, 128, 4, 2, 3, 3>), grid, dim3(512), 0, st, a);
+      break;
+    case TILE_256x128: launch_rows<256, 128, 4, 2>(a, p.kern, st); break;
+    case TILE_128x128: launch_rows<128, 128, 2, 2>(a, p.kern, st); break;
+    case TILE_128x64: launch_rows<128, 64, 2, 2>(a, p.kern, st); break;
+    default: launch_rows<64, 64, 2, 2>(a, p.kern, st); break;
+  }
+  PF_CHECK_LAUNCH();
+  if (a.ksplit > 1) {
+    const long long total = (long long)a.M * (a.Cout / 4);
+    long long g = (total + 255) / 256;
+    if (g > 16384) g = 16384;
+    hipLaunchKernelGGL(conv_splitk_reduce, dim3((int)g), dim3(256), 0, st, a.part, a.ksplit, a.M,
+                       a.Cout, a.bias, a.res, a.rcs, a.act, a.y, a.ycs);
+    PF_CHECK_LAUNCH();
+  }
+  return POSFEAT_OK;
 }
 
 }  // namespace
@@ -495,42 +937,19 @@ static int conv_prepare(const posfeat_conv_desc* d, const float* x, const float*
   return POSFEAT_OK;
 }
 
-// Tile choice: the largest tile that still gives >= 2 workgroups per CU.
-// 0: 128x128, 1: 128x64, 2: 64x64
-static int conv_cfg(const ConvArgs& a) {
-  const long long t128 = (long long)((a.M + 127) / 128) * ((a.Cout + 127) / 128);
-  const long long t128x64 = (long long)((a.M + 127) / 128) * ((a.Cout + 63) / 64);
-  if (a.Cout > 64 && (t128 >= 512 || a.ksplit > 1)) return 0;
-  if (t128x64 >= 512) return 1;
-  return 2;
-}
-
-static int cfg_bm(int cfg) { return cfg == 2 ? 64 : 128; }
-
-static int conv_launch(ConvArgs& a, hipStream_t st) {
-  const bool cin32 = (a.Cin % BK) == 0;
-  switch (conv_cfg(a)) {
-    case 0: return launch_cfg<128, 128, 2, 2>(a, cin32, st);
-    case 1: return launch_cfg<128, 64, 2, 2>(a, cin32, st);
-    default: return launch_cfg<64, 64, 2, 2>(a, cin32, st);
-  }
-}
-
 extern "C" int posfeat_conv2d_nhwc(const posfeat_conv_desc* d, const float* x, const float* w,
                                    const float* bias, const float* res, float* y, void* stream) {
   ConvArgs a;
   PF_TRY(conv_prepare(d, x, w, bias, res, y, a));
-  return conv_launch(a, pf_stream(stream));
+  return conv_run(a, conv_plan(a, false), pf_stream(stream));
 }
 
 extern "C" size_t posfeat_conv2d_workspace(const posfeat_conv_desc* d) {
   ConvArgs a;
   float dummy[4] __attribute__((aligned(16)));
   if (conv_prepare(d, dummy, dummy, nullptr, nullptr, dummy, a) != POSFEAT_OK) return 0;
-  const long long t128 = (long long)((a.M + 127) / 128) * ((a.Cout + 127) / 128);
-  if (a.Cout % 4 || a.Cout <= 64) return 0;
-  const int ks = choose_ksplit(t128, a.Kpad / BK);
-  return ks > 1 ? (size_t)ks * a.M * a.Cout * sizeof(float) : 0;
+  const Plan p = conv_plan(a, true);
+  return p.ksplit > 1 ? (size_t)p.ksplit * a.M * a.Cout * sizeof(float) : 0;
 }
 
 extern "C" int posfeat_conv2d_nhwc_ws(const posfeat_conv_desc* d, const float* x, const float* w,
@@ -539,24 +958,26 @@ extern "C" int posfeat_conv2d_nhwc_ws(const posfeat_conv_desc* d, const float* x
   ConvArgs a;
   PF_TRY(conv_prepare(d, x, w, bias, res, y, a));
   const size_t need = posfeat_conv2d_workspace(d);
-  if (need > 0 && ws && ws_bytes >= need) {
-    const long long t128 = (long long)((a.M + 127) / 128) * ((a.Cout + 127) / 128);
-    a.ksplit = choose_ksplit(t128, a.Kpad / BK);
-    a.part = static_cast<float*>(ws);
-  }
-  return conv_launch(a, pf_stream(stream));
+  const bool split = need > 0 && ws && ws_bytes >= need;
+  const Plan p = conv_plan(a, split);
+  if (p.ksplit > 1) a.part = static_cast<float*>(ws);
+  return conv_run(a, p, pf_stream(stream));
+}
+
+// Stats tiling: contiguous-row tiles may straddle two images (slot 1 holds the
+// second image's rows); patch tiles belong to one image.
+static size_t stats_tiles_per_img(const ConvArgs& a, const Plan& p) {
+  return p.ppi > 0 ? (size_t)p.ppi : (size_t)(a.hw + p.bm - 1) / p.bm + 1;
 }
 
 extern "C" size_t posfeat_conv2d_stats_workspace(const posfeat_conv_desc* d) {
   ConvArgs a;
   float dummy[4] __attribute__((aligned(16)));
   if (conv_prepare(d, dummy, dummy, nullptr, nullptr, dummy, a) != POSFEAT_OK) return 0;
-  const int bm = cfg_bm(conv_cfg(a));
-  if (a.hw < bm) return 0;  // a tile may span > 2 images: not supported
-  const size_t tiles_m = (a.M + bm - 1) / bm;
-  const size_t per_img = (size_t)(a.hw + bm - 1) / bm + 1;
-  const size_t nchunk = (per_img + STAT_CHUNK - 1) / STAT_CHUNK;
-  return pf_align(tiles_m * 2 * a.Cout * 2 * sizeof(float), 256) +
+  const Plan p = conv_plan(a, false);
+  if (p.ppi == 0 && a.hw < p.bm) return 0;  // a tile may span > 2 images: not supported
+  const size_t nchunk = (stats_tiles_per_img(a, p) + STAT_CHUNK - 1) / STAT_CHUNK;
+  return pf_align((size_t)p.tiles_m * 2 * a.Cout * 2 * sizeof(float), 256) +
          (size_t)d->n * nchunk * a.Cout * 2 * sizeof(double);
 }
 
@@ -571,16 +992,14 @@ extern "C" int posfeat_conv2d_nhwc_stats(const posfeat_conv_desc* d, const float
   if (!ws || ws_bytes < need || !mean || !rstd) return POSFEAT_E_WORKSPACE;
   a.stats = static_cast<float*>(ws);
   hipStream_t st = pf_stream(stream);
-  const int bm = cfg_bm(conv_cfg(a));
-  PF_TRY(conv_launch(a, st));
+  const Plan p = conv_plan(a, false);
+  PF_TRY(conv_run(a, p, st));
   const int nb = d->n;
-  const size_t tiles_m = (a.M + bm - 1) / bm;
-  const int per_img = (a.hw + bm - 1) / bm + 1;
-  const int nchunk = (per_img + STAT_CHUNK - 1) / STAT_CHUNK;
-  double* chunks = reinterpret_cast<double*>(static_cast<char*>(ws) +
-                                             pf_align(tiles_m * 2 * a.Cout * 2 * sizeof(float), 256));
+  const int nchunk = (int)((stats_tiles_per_img(a, p) + STAT_CHUNK - 1) / STAT_CHUNK);
+  double* chunks = reinterpret_cast<double*>(
+      static_cast<char*>(ws) + pf_align((size_t)p.tiles_m * 2 * a.Cout * 2 * sizeof(float), 256));
   hipLaunchKernelGGL(conv_stats_chunk, dim3(nchunk, (a.Cout + 63) / 64, nb), dim3(1024), 0, st,
-                     a.stats, bm, a.hw, a.Cout, nchunk, chunks);
+                     a.stats, p.bm, p.ppi, a.hw, a.Cout, nchunk, chunks);
   PF_CHECK_LAUNCH();
   hipLaunchKernelGGL(conv_stats_finalize, dim3((nb * a.Cout + 255) / 256), dim3(256), 0, st,
                      chunks, nchunk, a.hw, a.Cout, nb, eps, mean, rstd);

@@ -41,6 +41,8 @@ CONV_CASES = [
     (1, 12, 16, 1024, 512, 3, 1, "elu", False, 0, 0),
     (1, 256, 256, 64, 128, 3, 1, "elu", True, 0, 0),    # 128x128-tile path
     (1, 30, 40, 192, 192, 3, 1, "none", False, 0, 0),   # cout 192 (tile guard)
+    (3, 21, 37, 96, 128, 3, 1, "relu", True, 8, 64),    # halo: slice in/out, ragged patches
+    (2, 9, 17, 32, 64, 3, 1, "elu", False, 0, 0),       # halo: 8x16 patches, both edges partial
 ]
 
 

@@ -1,5 +1,6 @@
 """Run the head.conv2-shaped conv (B x 480x640, 3x3, 256->128, NHWC) alone,
-for PMC counter passes (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE)."""
+for PMC counter passes (rocprofv3 --pmc ...) and ablation timing.
+Prints the mean ms per launch over REPS timed launches (after one warmup)."""
 import os
 import sys
 
@@ -15,8 +16,17 @@ x = torch.randn(B, 480, 640, 256, device="cuda", generator=g)
 w = torch.randn(128, 256, 3, 3, device="cuda", generator=g) * 0.03
 wp, bp = ops.pack_conv_weight(w, torch.zeros(128, device="cuda"))
 y = torch.empty(B, 480, 640, 128, device="cuda")
+ops.conv2d_nhwc(x, wp, bp, 128, 3, 3, out=y)
+torch.cuda.synchronize()
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record()
 for _ in range(REPS):
     ops.conv2d_nhwc(x, wp, bp, 128, 3, 3, out=y)
+e1.record()
 torch.cuda.synchronize()
+ms = e0.elapsed_time(e1) / REPS
+flop = 2.0 * B * 480 * 640 * 128 * 256 * 9
+print("lib=%s ms/launch=%.3f TFLOP/s=%.1f" % (os.environ.get("POSFEAT_HIP_LIB", "default"), ms,
+                                             flop / ms / 1e9))
 print("algorithmic bytes/launch: read %.1f MB + write %.1f MB" % (
     x.numel() * 4 / 1e6 + wp.numel() * 4 / 1e6, y.numel() * 4 / 1e6))
