@@ -192,7 +192,7 @@ def main():
                                    "2048) + sample_feat_by_coord",
                        "global_batch": args.batch * world, "image": [H, W],
                        "num_pts": NUM_PTS, "parallelism": "dp%d (image-sharded)" % world},
-            "roofline": {"kernel": "conv_mfma_kernel<128,128> (head.conv2 3x3 256->128 @480x640)",
+            "roofline": {"kernel": "conv_halo_kernel<8x16 patch, BN=128> (head.conv2 3x3 256->128 @480x640)",
                          "bound": "mfma", "achieved": round(achieved, 3),
                          "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4),
