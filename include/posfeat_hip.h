@@ -87,6 +87,26 @@ int posfeat_conv2d_nhwc_stats(const posfeat_conv_desc *d, const float *x, const 
                               const float *bias, float *y, void *ws, size_t ws_bytes,
                               float *mean, float *rstd, float eps, void *stream);
 
+/* KeypointDet's conv2 over cat[F.interpolate(L, x4, bilinear,
+ * align_corners=False), G] + InstanceNorm statistics, without materialising
+ * the upsampled map.  Replaces networks/DeteNet.py:109-112 (interpolate, cat,
+ * conv2, the statistics of norm2).  L: n x H/4 x W/4 x 192 (pitch lcs), the
+ * already normalised PReLU(IN(conv1)); G: n x H x W x 64 (pitch gcs),
+ * IN(convimg); w_packed/bias: conv2 (256 -> 128, 3x3) packed as for
+ * posfeat_conv2d_nhwc (only read by posfeat_conv2_up4_weights);
+ * wph: posfeat_conv2_up4_weights_floats() floats (16 phase-combined weight
+ * sets + transposed border taps) built from w_packed (rebuild after changing
+ * the weights).
+ * Writes y (n x H x W x 128, pitch ycs; bias added, no activation) and
+ * mean/rstd [n][128] of y (biased var).  H, W multiples of 4, >= 16. */
+size_t posfeat_conv2_up4_weights_floats(void);
+size_t posfeat_conv2_up4_workspace(int n, int H, int W);
+int posfeat_conv2_up4_weights(const float *w_packed, float *wph, void *stream);
+int posfeat_conv2_up4(int n, int H, int W, const float *L, int lcs, const float *G, int gcs,
+                      const float *wph, const float *w_packed, const float *bias, float *y,
+                      int ycs, void *ws, size_t ws_bytes, float *mean, float *rstd, float eps,
+                      void *stream);
+
 /* ------------------------------------------------------------------------
  * Keypoint selection.
  * Replaces: losses/preprocess_utils.py:215-278 generate_kpts_single

@@ -55,6 +55,12 @@ SIGNATURES = {
     "posfeat_conv2d_nhwc_stats": (c_int, [ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_void_p,
                                           c_void_p, c_void_p, c_size_t, c_void_p, c_void_p,
                                           c_float, c_void_p]),
+    "posfeat_conv2_up4_weights_floats": (c_size_t, []),
+    "posfeat_conv2_up4_workspace": (c_size_t, [c_int, c_int, c_int]),
+    "posfeat_conv2_up4_weights": (c_int, [c_void_p, c_void_p, c_void_p]),
+    "posfeat_conv2_up4": (c_int, [c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p,
+                                  c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_size_t,
+                                  c_void_p, c_void_p, c_float, c_void_p]),
     "posfeat_detect_workspace": (c_int, [c_int, c_int, c_int, c_int, ctypes.POINTER(c_size_t)]),
     "posfeat_detect": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int,
                                c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

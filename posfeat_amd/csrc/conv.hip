@@ -41,6 +41,9 @@ struct ConvArgs {
   float* part;       // [ksplit][M][Cout] fp32 partial sums
   float* stats;      // optional [tiles_m][2 slots][Cout][2] per-tile (sum, sumsq)
   int hw;            // OH*OW (image boundary inside a tile for `stats`)
+  // conv_up4_kernel only: full-res second input and the low-res grid
+  const float* x2;
+  int x2cs, lh, lw;
 };
 
 // Epilogue shared by both kernels: acc -> LDS T[BM][BN+4] (conflict-free: a
@@ -50,11 +53,12 @@ struct ConvArgs {
 // the caller's K loop to have ended with a barrier (smem is reused).
 // `rowm(row)` maps a tile row to its output pixel m (or -1: outside); img0 is
 // the image of the tile's first row (stats slot 0).
-template <int BM, int BN, int WM, int WN, class RowMap>
+// `resp(row, m)` returns the residual row (channels n0..) or nullptr.
+template <int BM, int BN, int WM, int WN, class RowMap, class ResMap>
 __device__ __forceinline__ void conv_epilogue(const ConvArgs& a,
                                               f32x16 (&acc)[BM / WM / 32][BN / WN / 32],
                                               float* smem, int tm, int n0, int split,
-                                              RowMap rowm, int img0) {
+                                              RowMap rowm, int img0, ResMap resp) {
   constexpr int THREADS = WM * WN * 64;
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int MI = TM / 32, NI = TN / 32;
@@ -94,10 +98,10 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a,
   f32x4 rv[NP];
 #pragma unroll
   for (int p = 0; p < NP; ++p) {
-    const int m = rowm(r0 + p * RPP);
-    rv[p] = (a.res && colok && m >= 0)
-                ? *reinterpret_cast<const f32x4*>(a.res + (size_t)m * a.rcs + col)
-                : f32x4{0.f, 0.f, 0.f, 0.f};
+    const int row = r0 + p * RPP;
+    const int m = rowm(row);
+    const float* rp = (colok && m >= 0) ? resp(row, m) : nullptr;
+    rv[p] = rp ? *reinterpret_cast<const f32x4*>(rp + col) : f32x4{0.f, 0.f, 0.f, 0.f};
   }
   const f32x4 bv = (a.bias && colok) ? *reinterpret_cast<const f32x4*>(a.bias + col)
                                      : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -328,7 +332,8 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_mfma_kernel(ConvArgs a) {
 
   conv_epilogue<BM, BN, WM, WN>(
       a, acc, smem, tm, n0, split, [&](int row) { return m0 + row < a.M ? m0 + row : -1; },
-      m0 / a.hw);
+      m0 / a.hw,
+      [&](int, int m) { return a.res ? a.res + (size_t)m * a.rcs : (const float*)nullptr; });
 }
 
 // ---------------------------------------------------------------------------
@@ -347,6 +352,8 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_mfma_kernel(ConvArgs a) {
 // 16-B device word.  Two LDS stages: chunk c+1 is in flight while chunk c is
 // multiplied; vmcnt(0) + barrier at the end of each chunk.
 __device__ __attribute__((aligned(16))) float pf_conv_zero16[4];
+#define PF_GPTR(p) ((const __attribute__((address_space(1))) void*)(p))
+#define PF_LPTR(p) ((__attribute__((address_space(3))) void*)(p))
 
 template <int BM, int BN, int WM, int WN>
 __global__ __launch_bounds__(WM* WN * 64) void conv_glds_kernel(ConvArgs a) {
@@ -492,7 +499,8 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_glds_kernel(ConvArgs a) {
 
   conv_epilogue<BM, BN, WM, WN>(
       a, acc, smem, tm, n0, split, [&](int row) { return m0 + row < a.M ? m0 + row : -1; },
-      m0 / a.hw);
+      m0 / a.hw,
+      [&](int, int m) { return a.res ? a.res + (size_t)m * a.rcs : (const float*)nullptr; });
 }
 
 // ---------------------------------------------------------------------------
@@ -653,7 +661,352 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_halo_kernel(ConvArgs a) {
         const int oy = oy0 + (row >> 4), ox = ox0 + (row & 15);
         return (oy < a.OH && ox < a.OW) ? (img * a.OH + oy) * a.OW + ox : -1;
       },
-      img);
+      img,
+      [&](int, int m) { return a.res ? a.res + (size_t)m * a.rcs : (const float*)nullptr; });
+}
+
+// ---------------------------------------------------------------------------
+// head.conv2 by bilinear phases (networks/DeteNet.py:108-112).  The input is
+// cat[up4(L) (192 ch), G (64 ch)] with up4 = F.interpolate(x4, bilinear,
+// align_corners=False).  For output row Y = 4q + r every upsampled row the 3x3
+// taps touch is a fixed combination (weights k/8) of low-res rows q+e,
+// e in E(r) = {-1,0} (r=0), {-1,0,1} (r=1,2), {0,1} (r=3), once the low-res
+// map is replicate-extended by one row/col (which is exactly how the
+// interpolation clamps).  So at phase (ry, rx) the 192-channel part is a
+// |E(ry)| x |E(rx)| conv on the LOW-RES map with combined weights (6.25 taps
+// on average instead of 9: -23% MACs for the whole layer) and the ×4
+// upsampled 256-channel map is never materialised.  The 64 full-res channels
+// (G) keep their 3x3 taps (gathered at stride 4).  Conv zero padding breaks
+// the periodicity only on the outermost rows/cols: those 2(H+W)-4 pixels per
+// image are excluded here and computed by an im2col + GEMM side path
+// (posfeat_conv2_up4).  Tile: an 8x16 patch of low-res positions of one phase;
+// the L halo (10x18, replicate-clamped) is staged once per slab like
+// conv_halo_kernel, G chunks are DMA-gathered per tap.
+constexpr int UP4_CU = 192, UP4_CG = 64, UP4_COUT = 128;
+constexpr int UP4_GCH = (UP4_CG / 32) * 9;  // G chunks (first in the phase K order)
+constexpr int UP4_KP = 2304;                // per-phase packed K capacity (<= 9 taps x 256)
+
+__device__ __forceinline__ int up4_ne(int r) { return (r == 0 || r == 3) ? 2 : 3; }
+// index of border pixel (Y, X) in the order of up4_border_pixel, -1 inside
+__device__ __forceinline__ int up4_border_index(int Y, int X, int H, int W) {
+  if (Y == 0) return X;
+  if (Y == H - 1) return W + X;
+  if (X == 0) return 2 * W + Y - 1;
+  if (X == W - 1) return 2 * W + (H - 2) + Y - 1;
+  return -1;
+}
+__device__ __forceinline__ int up4_e0(int r) { return r == 3 ? 0 : -1; }
+
+template <int PH>
+__global__ __launch_bounds__(256) void conv_up4_kernel(ConvArgs a) {
+  constexpr int PW = 16, BM = PH * PW, BN = UP4_COUT, WM = 2, WN = 2, NW = 4;
+  constexpr int TM = BM / WM, TN = BN / WN, MI = TM / 32, NI = TN / 32;
+  constexpr int HX = PW + 2, HY = PH + 2, HP = HX * HY;
+  constexpr int A_G = (HP + 8 * NW - 1) / (8 * NW);
+  constexpr int HPR = A_G * 8 * NW;
+  constexpr int G_G = BM / 8 / NW;  // gather DMA instructions per wave per G chunk
+  constexpr int B_G = BN / 8 / NW;
+  static_assert(HPR >= BM && MI >= 1 && NI >= 1, "tile");
+  constexpr int RING = 2 * (HPR + BN) * BK;
+  constexpr int STAGE = BM * (BN + 4);
+  __shared__ __attribute__((aligned(16))) float smem[RING > STAGE ? RING : STAGE];
+  float* As = smem;
+  float* Bs = smem + 2 * HPR * BK;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+
+  int bid = blockIdx.x;
+  {
+    const int nwg = a.nwg, q = nwg >> 3, r = nwg & 7, xcd = bid & 7, slot = bid >> 3;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+  }
+  // tile = ((img * ppi + patch) * 16 + phase): the 16 phases of a patch are
+  // neighbours in the remapped order, so they share the L halo in L2
+  const int phase = bid & 15, t2 = bid >> 4;
+  const int ptx = (a.lw + PW - 1) / PW, ppi = ptx * ((a.lh + PH - 1) / PH);
+  const int img = t2 / ppi, prem = t2 - img * ppi;
+  const int qy0 = (prem / ptx) * PH, qx0 = (prem - (prem / ptx) * ptx) * PW;
+  const int ry = phase >> 2, rx = phase & 3;
+  const int ney = up4_ne(ry), nex = up4_ne(rx), ey0 = up4_e0(ry), ex0 = up4_e0(rx);
+  const int T = ney * nex;
+  const int nch = UP4_GCH + (UP4_CU / 32) * T;
+  const int H = a.H, W = a.W;
+
+  const int lrow = lane >> 3;
+  // L halo sources: low-res (qy0-1+hy, qx0-1+hx), replicate-clamped
+  const float* hsrc[A_G];
+#pragma unroll
+  for (int i = 0; i < A_G; ++i) {
+    const int hp = (wave * A_G + i) * 8 + lrow;
+    const int hy = hp / HX, hx = hp - (hp / HX) * HX;
+    const int ly = min(max(qy0 - 1 + hy, 0), a.lh - 1), lx = min(max(qx0 - 1 + hx, 0), a.lw - 1);
+    const int sslot = (lane & 7) ^ ((hx >> 1) & 7);
+    hsrc[i] = hp < HP ? a.x + (((long long)img * a.lh + ly) * a.lw + lx) * a.xcs + sslot * 4
+                      : nullptr;
+  }
+  // G gather sources: tile row -> full-res pixel of this phase; 9-bit tap mask
+  const float* gsrc[G_G];
+  unsigned gok[G_G];
+#pragma unroll
+  for (int i = 0; i < G_G; ++i) {
+    const int row = (wave * G_G + i) * 8 + lrow;
+    const int qy = qy0 + (row >> 4), qx = qx0 + (row & 15);
+    const int Y = 4 * qy + ry, X = 4 * qx + rx;
+    const int sslot = (lane & 7) ^ ((row >> 1) & 7);
+    gok[i] = 0u;
+    gsrc[i] = a.x2;
+    if (qy < a.lh && qx < a.lw) {
+      for (int t = 0; t < 9; ++t) {
+        const int yy = Y + t / 3 - 1, xx = X + t % 3 - 1;
+        if ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W) gok[i] |= 1u << t;
+      }
+      gsrc[i] = a.x2 + (((long long)img * H + Y) * W + X) * a.x2cs + sslot * 4;
+    }
+  }
+  const float* wsrc[B_G];
+#pragma unroll
+  for (int i = 0; i < B_G; ++i) {
+    const int row = (wave * B_G + i) * 8 + lrow;
+    const int sslot = (lane & 7) ^ ((row >> 1) & 7);
+    wsrc[i] = a.w + ((size_t)phase * BN + row) * UP4_KP + sslot * 4;
+  }
+  // A for chunk c into stage buf (G chunk: gathered rows; U chunk: slab halo)
+  auto issue_a = [&](int c, int buf) {
+    if (c < UP4_GCH) {
+      const int gs = c / 9, t = c - gs * 9;
+      const long long d = ((long long)(t / 3 - 1) * W + (t % 3 - 1)) * a.x2cs + gs * BK;
+#pragma unroll
+      for (int i = 0; i < G_G; ++i) {
+        const float* src = ((gok[i] >> t) & 1u) ? gsrc[i] + d : pf_conv_zero16;
+        __builtin_amdgcn_global_load_lds(PF_GPTR(src), PF_LPTR(As + (buf * HPR + (wave * G_G + i) * 8) * BK),
+                                         16, 0, 0);
+      }
+    } else {
+      const int slab = (c - UP4_GCH) / T;
+#pragma unroll
+      for (int i = 0; i < A_G; ++i) {
+        const float* src = hsrc[i] ? hsrc[i] + slab * BK : pf_conv_zero16;
+        __builtin_amdgcn_global_load_lds(PF_GPTR(src), PF_LPTR(As + (buf * HPR + (wave * A_G + i) * 8) * BK),
+                                         16, 0, 0);
+      }
+    }
+  };
+  auto issue_w = [&](int c, int buf) {
+#pragma unroll
+    for (int i = 0; i < B_G; ++i)
+      __builtin_amdgcn_global_load_lds(PF_GPTR(wsrc[i] + (size_t)c * BK),
+                                       PF_LPTR(Bs + (buf * BN + (wave * B_G + i) * 8) * BK), 16, 0, 0);
+  };
+  auto needs_a = [&](int c) { return c < UP4_GCH || (c - UP4_GCH) % T == 0; };
+
+  f32x16 acc[MI][NI];
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
+
+  const int px = lane & 15;
+  const int arow = wm * TM + (lane & 31);
+  const int hrow0 = (arow >> 4) * HX + px;
+  const int asw = ((lane & 31) >> 1) & 7;  // row swizzle (G chunks), same for B
+  const int brow = wn * TN + (lane & 31);
+
+  issue_a(0, 0);
+  issue_w(0, 0);
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+
+  int abuf = 0;
+  for (int c = 0; c < nch; ++c) {
+    const int bcur = c & 1;
+    const bool nexta = c + 1 < nch && needs_a(c + 1);
+    if (c + 1 < nch) {
+      issue_w(c + 1, bcur ^ 1);
+      if (nexta) issue_a(c + 1, abuf ^ 1);
+    }
+    const float* Ab;
+    int sw, mstep;
+    if (c < UP4_GCH) {
+      Ab = As + (abuf * HPR + arow) * BK;
+      sw = asw;
+      mstep = 32 * BK;
+    } else {
+      const int tj = (c - UP4_GCH) % T;
+      const int ey = ey0 + tj / nex, ex = ex0 + tj % nex;
+      Ab = As + (abuf * HPR + hrow0 + (ey + 1) * HX + ex + 1) * BK;
+      sw = ((px + ex + 1) >> 1) & 7;
+      mstep = 2 * HX * BK;
+    }
+    const float* Bb = Bs + (bcur * BN + brow) * BK;
+#pragma unroll
+    for (int kk = 0; kk < BK / 8; ++kk) {
+      const int s = (lane >> 5) + 2 * kk;
+      f32x4 av[MI], bv[NI];
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi)
+        av[mi] = *reinterpret_cast<const f32x4*>(Ab + mi * mstep + (s ^ sw) * 4);
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni)
+        bv[ni] = *reinterpret_cast<const f32x4*>(Bb + ni * 32 * BK + (s ^ asw) * 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < NI; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[mi][j], bv[ni][j], acc[mi][ni],
+                                                                0, 0, 0);
+    }
+    if (nexta) abuf ^= 1;
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+  }
+
+  // border pixels: subtract the taps that fall into the conv zero padding
+  // (a.res = -correction rows from up4_border_corr_kernel, one per border pixel)
+  conv_epilogue<BM, BN, WM, WN>(
+      a, acc, smem, bid, 0, 0,
+      [&](int row) {
+        const int qy = qy0 + (row >> 4), qx = qx0 + (row & 15);
+        return (qy < a.lh && qx < a.lw) ? (img * H + 4 * qy + ry) * W + 4 * qx + rx : -1;
+      },
+      img,
+      [&](int row, int) {
+        const int Y = 4 * (qy0 + (row >> 4)) + ry, X = 4 * (qx0 + (row & 15)) + rx;
+        const int j = up4_border_index(Y, X, H, W);
+        return j < 0 ? (const float*)nullptr : a.res + ((size_t)img * a.rcs + j) * UP4_COUT;
+      });
+}
+
+// Phase weights from the packed conv2 weights ([128][2304], K order
+// (cin/32, kh, kw, cin%32)): wph[phase][cout][c*32 + ci] for the phase's chunk
+// order (G chunks, then per low-res slab its |E(ry)|x|E(rx)| taps), combined in
+// fp64: W'(ey,ex) = sum_{dy,dx} cy(dy,ey) cx(dx,ex) W(dy,dx).
+__device__ double up4_coef(int r, int d, int e) {
+  // coefficient of low-res row q+e in upsampled row 4q+r+d (d in -1..1)
+  const int t = r + d;                    // -1..4
+  const int qo = t < 0 ? -1 : (t > 3 ? 1 : 0);
+  const int rr = t - 4 * qo;              // 0..3
+  const int lo = rr < 2 ? -1 : 0;         // first low-res neighbour (relative to q+qo)
+  const double wl = rr == 0 ? 0.375 : rr == 1 ? 0.125 : rr == 2 ? 0.875 : 0.625;
+  if (e == qo + lo) return wl;
+  if (e == qo + lo + 1) return 1.0 - wl;
+  return 0.0;
+}
+
+__global__ void up4_phase_weights_kernel(const float* __restrict__ wpk, float* __restrict__ wph) {
+  const int phase = blockIdx.y, o = blockIdx.x, ci = threadIdx.x & 31, cg = threadIdx.x >> 5;
+  const int ry = phase >> 2, rx = phase & 3;
+  const int ney = up4_ne(ry), nex = up4_ne(rx), ey0 = up4_e0(ry), ex0 = up4_e0(rx), T = ney * nex;
+  const int nch = UP4_GCH + (UP4_CU / 32) * T;
+  const float* w = wpk + (size_t)o * UP4_KP;
+  float* dst = wph + ((size_t)phase * UP4_COUT + o) * UP4_KP;
+  for (int c = cg; c < UP4_KP / 32; c += blockDim.x / 32) {
+    float v = 0.f;
+    if (c < UP4_GCH) {
+      const int gs = c / 9, t = c - gs * 9;
+      v = w[((UP4_CU / 32 + gs) * 9 + t) * 32 + ci];
+    } else if (c < nch) {
+      const int u = c - UP4_GCH, slab = u / T, tj = u - slab * T;
+      const int ey = ey0 + tj / nex, ex = ex0 + tj % nex;
+      double acc = 0.0;
+      for (int dy = -1; dy <= 1; ++dy) {
+        const double cy = up4_coef(ry, dy, ey);
+        if (cy == 0.0) continue;
+        for (int dx = -1; dx <= 1; ++dx) {
+          const double cx = up4_coef(rx, dx, ex);
+          if (cx == 0.0) continue;
+          acc += cy * cx * (double)w[(slab * 9 + (dy + 1) * 3 + (dx + 1)) * 32 + ci];
+        }
+      }
+      v = (float)acc;
+    }
+    dst[c * 32 + ci] = v;
+  }
+  // transposed 3x3 taps of the 192 upsampled channels for the border correction
+  if (phase == 0) {
+    float* wct = wph + (size_t)16 * UP4_COUT * UP4_KP;
+    for (int e = threadIdx.x; e < 9 * UP4_CU; e += blockDim.x) {
+      const int t = e / UP4_CU, ch = e % UP4_CU;
+      wct[((size_t)t * UP4_CU + ch) * UP4_COUT + o] = w[((ch >> 5) * 9 + t) * 32 + (ch & 31)];
+    }
+  }
+}
+
+// Border pixel j of an image (rows 0 and H-1, then cols 0 and W-1 without the
+// corners): 2W + 2(H-2) pixels.
+__device__ __forceinline__ void up4_border_pixel(int j, int H, int W, int& Y, int& X) {
+  if (j < W) { Y = 0; X = j; }
+  else if (j < 2 * W) { Y = H - 1; X = j - W; }
+  else {
+    const int k = j - 2 * W;
+    if (k < H - 2) { Y = 1 + k; X = 0; }
+    else { Y = 1 + (k - (H - 2)); X = W - 1; }
+  }
+}
+
+// Border correction.  On the outermost rows/cols the phase formula also sums
+// taps that fall into conv2's zero padding, reading the replicate extension of
+// the upsampled map there -- which equals the nearest in-image upsampled
+// pixel.  corr[img][j][co] = -sum over out-of-image taps (dy,dx) of
+// W[co][c][dy][dx] * up4(L)[clamp(Y+dy)][clamp(X+dx)][c]  (c < 192; the G
+// channels are gathered with exact zero padding).  8 border pixels per block,
+// one thread per cout, weights transposed to wct[tap][c][co] (coalesced).
+constexpr int UP4_CPB = 8;
+__global__ __launch_bounds__(UP4_COUT) void up4_border_corr_kernel(
+    const float* __restrict__ L, int lcs, int lh, int lw, int H, int W, int nbp,
+    const float* __restrict__ wct, float* __restrict__ corr) {
+  __shared__ float u[UP4_CPB][9][UP4_CU];
+  __shared__ int bad[UP4_CPB];
+  const int img = blockIdx.y, j0 = blockIdx.x * UP4_CPB, tid = threadIdx.x;
+  const float sh = (float)lh / (float)H, sw = (float)lw / (float)W;
+  if (tid < UP4_CPB) {
+    int Y = 0, X = 0, mask = 0;
+    if (j0 + tid < nbp) {
+      up4_border_pixel(j0 + tid, H, W, Y, X);
+      for (int t = 0; t < 9; ++t) {
+        const int yy = Y + t / 3 - 1, xx = X + t % 3 - 1;
+        if ((unsigned)yy >= (unsigned)H || (unsigned)xx >= (unsigned)W) mask |= 1 << t;
+      }
+    }
+    bad[tid] = mask;
+  }
+  for (int e = tid; e < UP4_CPB * 9 * UP4_CU; e += UP4_COUT) {
+    const int p = e / (9 * UP4_CU), t = (e / UP4_CU) % 9, c = e % UP4_CU;
+    float v = 0.f;
+    if (j0 + p < nbp) {
+      int Y, X;
+      up4_border_pixel(j0 + p, H, W, Y, X);
+      const int yy = min(max(Y + t / 3 - 1, 0), H - 1), xx = min(max(X + t % 3 - 1, 0), W - 1);
+      // PyTorch upsample_bilinear2d, align_corners=False (as norm_prelu_upsample)
+      float fy = sh * (yy + 0.5f) - 0.5f, fx = sw * (xx + 0.5f) - 0.5f;
+      fy = fy < 0.f ? 0.f : fy;
+      fx = fx < 0.f ? 0.f : fx;
+      const int y0 = (int)fy, x0 = (int)fx;
+      const int y1 = y0 + (y0 < lh - 1 ? 1 : 0), x1 = x0 + (x0 < lw - 1 ? 1 : 0);
+      const float ly = fy - y0, lx = fx - x0, hy = 1.f - ly, hx = 1.f - lx;
+      const float* b = L + (size_t)img * lh * lw * lcs + c;
+      const float v00 = b[((size_t)y0 * lw + x0) * lcs], v01 = b[((size_t)y0 * lw + x1) * lcs];
+      const float v10 = b[((size_t)y1 * lw + x0) * lcs], v11 = b[((size_t)y1 * lw + x1) * lcs];
+      v = hy * (hx * v00 + lx * v01) + ly * (hx * v10 + lx * v11);
+    }
+    u[p][t][c] = v;
+  }
+  __syncthreads();
+  for (int p = 0; p < UP4_CPB && j0 + p < nbp; ++p) {
+    float acc = 0.f;
+    for (int t = 0; t < 9; ++t) {
+      if (!((bad[p] >> t) & 1)) continue;
+      const float* w = wct + (size_t)t * UP4_CU * UP4_COUT + tid;
+      for (int c = 0; c < UP4_CU; ++c) acc = fmaf(w[(size_t)c * UP4_COUT], u[p][t][c], acc);
+    }
+    corr[((size_t)img * nbp + j0 + p) * UP4_COUT + tid] = -acc;
+  }
 }
 
 // Instance-norm statistics from the per-tile partials of the conv epilogue.
@@ -701,13 +1054,20 @@ __global__ __launch_bounds__(1024) void conv_stats_chunk(const float* __restrict
 
 __global__ void conv_stats_finalize(const double* __restrict__ chunks, int nchunk, int hw, int C,
                                     int nb, float eps, float* __restrict__ mean,
-                                    float* __restrict__ rstd) {
+                                    float* __restrict__ rstd,
+                                    const double* __restrict__ chunks2 = nullptr,
+                                    int nchunk2 = 0) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nb * C) return;
   const int b = i / C, c = i - b * C;
   double s1 = 0.0, s2 = 0.0;
   for (int k = 0; k < nchunk; ++k) {
     const double* p = chunks + (((long long)b * nchunk + k) * C + c) * 2;
+    s1 += p[0];
+    s2 += p[1];
+  }
+  for (int k = 0; k < nchunk2; ++k) {  // second tiling of the same images (disjoint pixels)
+    const double* p = chunks2 + (((long long)b * nchunk2 + k) * C + c) * 2;
     s1 += p[0];
     s2 += p[1];
   }
@@ -885,6 +1245,15 @@ int conv_run(ConvArgs& a, const Plan& p, hipStream_t st) {
   return POSFEAT_OK;
 }
 
+void launch_up4(const ConvArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(conv_up4_kernel<8>, dim3(a.nwg), dim3(256), 0, st, a);
+}
+
+void launch_up4_weights(const float* w_packed, float* wph, hipStream_t st) {
+  hipLaunchKernelGGL(up4_phase_weights_kernel, dim3(UP4_COUT, 16), dim3(256), 0, st, w_packed,
+                     wph);
+}
+
 }  // namespace
 
 extern "C" int posfeat_conv_packed_k(int cin, int kh, int kw) {
@@ -1003,6 +1372,115 @@ extern "C" int posfeat_conv2d_nhwc_stats(const posfeat_conv_desc* d, const float
   PF_CHECK_LAUNCH();
   hipLaunchKernelGGL(conv_stats_finalize, dim3((nb * a.Cout + 255) / 256), dim3(256), 0, st,
                      chunks, nchunk, a.hw, a.Cout, nb, eps, mean, rstd);
+  PF_CHECK_LAUNCH();
+  return POSFEAT_OK;
+}
+
+// ---------------------------------------------------------------------------
+// head.conv2 by bilinear phases (see conv_up4_kernel).
+static int up4_nbp(int H, int W) { return 2 * W + 2 * (H - 2); }
+static int up4_ppi(int H, int W) { return ((W / 4 + 15) / 16) * ((H / 4 + 7) / 8); }
+static const size_t UP4_WPH_FLOATS = (size_t)16 * UP4_COUT * UP4_KP + (size_t)9 * UP4_CU * UP4_COUT;
+
+struct Up4Ws {
+  size_t stats, chunks, corr, total;
+  int nch;
+};
+
+static Up4Ws up4_layout(int n, int H, int W) {
+  Up4Ws L{};
+  const int ppi = up4_ppi(H, W);
+  L.nch = (16 * ppi + STAT_CHUNK - 1) / STAT_CHUNK;
+  size_t cur = 0;
+  auto take = [&](size_t bytes) {
+    const size_t at = cur;
+    cur += pf_align(bytes, 256);
+    return at;
+  };
+  L.stats = take((size_t)n * ppi * 16 * 2 * UP4_COUT * 2 * sizeof(float));
+  L.chunks = take((size_t)n * L.nch * UP4_COUT * 2 * sizeof(double));
+  L.corr = take((size_t)n * up4_nbp(H, W) * UP4_COUT * sizeof(float));
+  L.total = cur;
+  return L;
+}
+
+extern "C" size_t posfeat_conv2_up4_weights_floats(void) { return UP4_WPH_FLOATS; }
+
+extern "C" size_t posfeat_conv2_up4_workspace(int n, int H, int W) {
+  if (n <= 0 || H < 16 || W < 16 || H % 4 || W % 4) return 0;
+  return up4_layout(n, H, W).total;
+}
+
+extern "C" int posfeat_conv2_up4_weights(const float* w_packed, float* wph, void* stream) {
+  if (!w_packed || !wph) return POSFEAT_E_INVALID;
+  launch_up4_weights(w_packed, wph, pf_stream(stream));
+  PF_CHECK_LAUNCH();
+  return POSFEAT_OK;
+}
+
+extern "C" int posfeat_conv2_up4(int n, int H, int W, const float* L, int lcs, const float* G,
+                                 int gcs, const float* wph, const float* w_packed,
+                                 const float* bias, float* y, int ycs, void* ws, size_t ws_bytes,
+                                 float* mean, float* rstd, float eps, void* stream) {
+  (void)w_packed;  // folded into wph (phase weights + transposed border taps)
+  if (n <= 0 || H < 16 || W < 16 || H % 4 || W % 4 || !L || !G || !wph || !y || !mean || !rstd)
+    return POSFEAT_E_INVALID;
+  if (lcs < UP4_CU || lcs % 4 || gcs < UP4_CG || gcs % 4 || ycs < UP4_COUT || ycs % 4)
+    return POSFEAT_E_INVALID;
+  const uintptr_t al = reinterpret_cast<uintptr_t>(L) | reinterpret_cast<uintptr_t>(G) |
+                       reinterpret_cast<uintptr_t>(wph) | reinterpret_cast<uintptr_t>(y) |
+                       reinterpret_cast<uintptr_t>(bias);
+  if (al & 15) return POSFEAT_E_INVALID;
+  const Up4Ws lay = up4_layout(n, H, W);
+  if (!ws || ws_bytes < lay.total) return POSFEAT_E_WORKSPACE;
+  char* base = static_cast<char*>(ws);
+  hipStream_t st = pf_stream(stream);
+  const int nbp = up4_nbp(H, W), ppi = up4_ppi(H, W);
+  float* corr = reinterpret_cast<float*>(base + lay.corr);
+
+  // 1. border corrections (taps in conv2's zero padding)
+  hipLaunchKernelGGL(up4_border_corr_kernel, dim3((nbp + UP4_CPB - 1) / UP4_CPB, n),
+                     dim3(UP4_COUT), 0, st, L, lcs, H / 4, W / 4, H, W, nbp,
+                     wph + (size_t)16 * UP4_COUT * UP4_KP, corr);
+  PF_CHECK_LAUNCH();
+
+  // 2. all pixels, 16 phases, fused IN partials; border rows add corr
+  ConvArgs a{};
+  a.x = L;
+  a.xcs = lcs;
+  a.x2 = G;
+  a.x2cs = gcs;
+  a.w = wph;
+  a.bias = bias;
+  a.res = corr;
+  a.rcs = nbp;  // rows per image of corr (see the epilogue residual map)
+  a.y = y;
+  a.ycs = ycs;
+  a.H = H;
+  a.W = W;
+  a.OH = H;
+  a.OW = W;
+  a.lh = H / 4;
+  a.lw = W / 4;
+  a.Cin = UP4_CU + UP4_CG;
+  a.Cout = UP4_COUT;
+  a.M = n * H * W;
+  a.hw = H * W;
+  a.act = POSFEAT_ACT_NONE;
+  a.ksplit = 1;
+  a.tiles_n = 1;
+  a.nwg = n * ppi * 16;
+  a.stats = reinterpret_cast<float*>(base + lay.stats);
+  launch_up4(a, st);
+  PF_CHECK_LAUNCH();
+
+  // 3. IN statistics (deterministic, fp64 merge)
+  double* ch = reinterpret_cast<double*>(base + lay.chunks);
+  hipLaunchKernelGGL(conv_stats_chunk, dim3(lay.nch, UP4_COUT / 64, n), dim3(1024), 0, st,
+                     a.stats, 128, 16 * ppi, a.hw, UP4_COUT, lay.nch, ch);
+  PF_CHECK_LAUNCH();
+  hipLaunchKernelGGL(conv_stats_finalize, dim3((n * UP4_COUT + 255) / 256), dim3(256), 0, st, ch,
+                     lay.nch, H * W, UP4_COUT, n, eps, mean, rstd, nullptr, 0);
   PF_CHECK_LAUNCH();
   return POSFEAT_OK;
 }

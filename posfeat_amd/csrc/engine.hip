@@ -11,7 +11,9 @@
 //   headcat [b][h/4][w/4][192] = [local_map(128) | local_map_small(64)]
 //   cat2    [b][h/4][w/4][512] = [upconv2 out(256) | layer1 out(256)]
 //   cat3    [b][h/8][w/8][1024]= [upconv3 out(512) | layer2 out(512)]
-//   hcat    [b][h][w][256]     = [up4(PReLU(IN(conv1)))(192) | IN(convimg)(64)]
+//   c1raw   [b][h/4][w/4][192] = conv1, then PReLU(IN(conv1)) in place (the
+//                                 low-res map head.conv2 reads per bilinear phase)
+//   g64     [b][h][w][64]      = IN(convimg)
 #include <cstring>
 #include <string>
 #include <vector>
@@ -95,6 +97,8 @@ struct posfeat_model {
   size_t ws_bytes = 0;
   Buf img4, stem, headcat, t1, t2, ds, oa, ob, cat2, cat3, l3out, gmap, up3, d3, up2, d2;
   Buf c1raw, hcat, c2raw, yraw;
+  Buf g64, wph, up4ws;             // phase-decomposed head.conv2 (conv.hip conv_up4_kernel)
+  bool up4 = true;
   Buf st_mean, st_rstd, st_part;  // instance-norm scratch (floats / doubles)
   Buf st_mean1, st_rstd1;
   Buf splitk;                      // split-K partial slabs (max over layers)
@@ -245,7 +249,17 @@ void plan(posfeat_model* m) {
   alloc(m->up2, B * h4 * w4 * 512);
   alloc(m->d2, B * h4 * w4 * 256);
   alloc(m->c1raw, B * h4 * w4 * 192);
-  alloc(m->hcat, B * H * W * 256);
+  {
+    const char* e = getenv("POSFEAT_HEAD_UP4");  // 0: materialise the x4 upsample (A/B only)
+    m->up4 = !(e && e[0] == '0');
+  }
+  if (m->up4) {
+    alloc(m->g64, B * H * W * 64);
+    alloc(m->wph, posfeat_conv2_up4_weights_floats());
+    alloc(m->up4ws, posfeat_conv2_up4_workspace((int)B, (int)H, (int)W) / 4 + 4);
+  } else {
+    alloc(m->hcat, B * H * W * 256);
+  }
   alloc(m->c2raw, B * H * W * 128);
   alloc(m->yraw, B * H * W);
   alloc(m->st_mean, B * 256);
@@ -347,17 +361,37 @@ int forward(Ctx& c, const float* img, posfeat_extract_out* out) {
   float* rstd = c.f(m->st_rstd);
   double* part = c.d(m->st_part);
   float* c1 = c.f(m->c1raw);
-  float* hcat = c.f(m->hcat);
-  PF_TRY(conv_in(c, "head.conv1", headcat, B, h4, w4, 192, c1, 192, mean, rstd));
-  PF_TRY(timed(c, "norm_prelu_up4", 0, [&] {
-    return pf_norm_prelu_upsample(c1, B, h4, w4, 192, 192, mean, rstd, slope, H, W, hcat, 256, c.st);
-  }));
-  PF_TRY(conv_in(c, "head.convimg", img4, B, H, W, 4, hcat + 192, 256, mean, rstd));
-  PF_TRY(timed(c, "instnorm_apply", 0, [&] {
-    return pf_in_apply(hcat + 192, B, H * W, 64, 256, mean, rstd, nullptr, c.st);
-  }));
   float* c2 = c.f(m->c2raw);
-  PF_TRY(conv_in(c, "head.conv2", hcat, B, H, W, 256, c2, 128, mean, rstd));
+  PF_TRY(conv_in(c, "head.conv1", headcat, B, h4, w4, 192, c1, 192, mean, rstd));
+  if (m->up4) {
+    // L = PReLU(IN(conv1)) stays at 1/4 resolution; conv2 reads it per phase
+    PF_TRY(timed(c, "norm_prelu", 0, [&] {
+      return pf_in_apply(c1, B, h4 * w4, 192, 192, mean, rstd, slope, c.st);
+    }));
+    float* g64 = c.f(m->g64);
+    PF_TRY(conv_in(c, "head.convimg", img4, B, H, W, 4, g64, 64, mean, rstd));
+    PF_TRY(timed(c, "instnorm_apply", 0, [&] {
+      return pf_in_apply(g64, B, H * W, 64, 64, mean, rstd, nullptr, c.st);
+    }));
+    const double fl = 2.0 * B * H * W * 128.0 * 256 * 9;  // reference conv2 FLOPs
+    PF_TRY(timed(c, "conv:head.conv2", fl, [&] {
+      PF_TRY(posfeat_conv2_up4_weights(c.W("head.conv2"), c.f(m->wph), c.st));
+      return posfeat_conv2_up4(B, H, W, c1, 192, g64, 64, c.f(m->wph), c.W("head.conv2"),
+                               c.Bi("head.conv2"), c2, 128, c.f(m->up4ws),
+                               m->up4ws.floats * sizeof(float), mean, rstd, 1e-5f, c.st);
+    }));
+  } else {
+    float* hcat = c.f(m->hcat);
+    PF_TRY(timed(c, "norm_prelu_up4", 0, [&] {
+      return pf_norm_prelu_upsample(c1, B, h4, w4, 192, 192, mean, rstd, slope, H, W, hcat, 256,
+                                    c.st);
+    }));
+    PF_TRY(conv_in(c, "head.convimg", img4, B, H, W, 4, hcat + 192, 256, mean, rstd));
+    PF_TRY(timed(c, "instnorm_apply", 0, [&] {
+      return pf_in_apply(hcat + 192, B, H * W, 64, 256, mean, rstd, nullptr, c.st);
+    }));
+    PF_TRY(conv_in(c, "head.conv2", hcat, B, H, W, 256, c2, 128, mean, rstd));
+  }
   PF_TRY(timed(c, "head_tail", 2.0 * B * H * W * 128, [&] {
     return pf_head_tail(c2, B, H * W, 128, mean, rstd, slope, c.W("head.conv3"),
                         c.Bi("head.conv3"), c.f(m->yraw), out->local_point, c.f(m->st_mean1),

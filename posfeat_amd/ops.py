@@ -93,6 +93,29 @@ def conv2d_nhwc_instnorm_stats(x, w_packed, bias, cout, kh, kw, eps=1e-5, out=No
     return out, mean, rstd
 
 
+def conv2_up4_instnorm_stats(L, G, w_packed, bias, eps=1e-5, out=None):
+    """KeypointDet conv2 over cat[up4(L), G] (DeteNet.py:109-112) without the
+    upsampled map: L n x h x w x 192 NHWC (h = H/4), G n x H x W x 64 NHWC.
+    Returns (y n x H x W x 128, mean [n,128], rstd [n,128])."""
+    _f32(L, "L")
+    _f32(G, "G")
+    n, H, W, gcs = G.shape
+    lcs = L.shape[-1]
+    if out is None:
+        out = torch.empty(n, H, W, 128, device=G.device, dtype=torch.float32)
+    wph = torch.empty(lib().posfeat_conv2_up4_weights_floats(), device=G.device,
+                      dtype=torch.float32)
+    check(lib().posfeat_conv2_up4_weights(ptr(_f32(w_packed, "w")), ptr(wph), stream_ptr()))
+    need = lib().posfeat_conv2_up4_workspace(n, H, W)
+    ws = torch.empty(max(need, 16), dtype=torch.uint8, device=G.device)
+    mean = torch.empty(n, 128, device=G.device)
+    rstd = torch.empty(n, 128, device=G.device)
+    check(lib().posfeat_conv2_up4(n, H, W, ptr(L), lcs, ptr(G), gcs, ptr(wph), ptr(w_packed),
+                                  ptr(bias), ptr(out), out.shape[-1], ptr(ws), need, ptr(mean),
+                                  ptr(rstd), float(eps), stream_ptr()))
+    return out, mean, rstd
+
+
 def nchw_to_nhwc(x, cstride=None):
     _f32(x, "x")
     n, c, h, w = x.shape

@@ -124,6 +124,38 @@ def test_conv_fused_instnorm_stats(gpu, n, h, w, cin, cout):
     assert torch.allclose(y.permute(0, 3, 1, 2).double().cpu(), ref, atol=1e-4)
 
 
+@pytest.mark.parametrize("n,H,W", [(2, 64, 96), (1, 48, 80), (1, 96, 144)])
+def test_conv2_up4_vs_torch(gpu, n, H, W):
+    """head.conv2 by bilinear phases == conv2(cat[interpolate(L, x4), G]) in fp64
+    (DeteNet.py:109-112), including the border lines and the IN statistics.
+    Ragged sizes: low-res grids that do not fill the 8x16 phase patches."""
+    from posfeat_amd import ops
+    g = torch.Generator().manual_seed(H * 7 + W)
+    h, w = H // 4, W // 4
+    L = torch.randn(n, 192, h, w, generator=g)
+    G = torch.randn(n, 64, H, W, generator=g)
+    wt = torch.randn(128, 256, 3, 3, generator=g) * (2.0 / (256 * 9)) ** 0.5
+    b = torch.randn(128, generator=g) * 0.1
+    up = F.interpolate(L.double(), size=(H, W), mode="bilinear", align_corners=False)
+    ref = F.conv2d(torch.cat([up, G.double()], 1), wt.double(), b.double(), padding=1)
+    bound = F.conv2d(torch.cat([up.abs(), G.double().abs()], 1), wt.double().abs(), padding=1)
+    wp, bp = ops.pack_conv_weight(wt.to(gpu), b.to(gpu))
+    Ld = L.permute(0, 2, 3, 1).contiguous().to(gpu)
+    Gd = G.permute(0, 2, 3, 1).contiguous().to(gpu)
+    y, mean, rstd = ops.conv2_up4_instnorm_stats(Ld, Gd, wp, bp)
+    torch.cuda.synchronize()
+    got = y.permute(0, 3, 1, 2).double().cpu()
+    err = (got - ref).abs()
+    tol = 4e-6 * bound + 1e-6
+    assert torch.all(err <= tol), "max err %g at %s" % (err.max(), (err / tol).argmax())
+    mu = ref.mean((2, 3))
+    var = ref.var((2, 3), unbiased=False)
+    assert torch.allclose(mean.double().cpu(), mu, atol=1e-5, rtol=1e-5)
+    assert torch.allclose(rstd.double().cpu(), 1.0 / torch.sqrt(var + 1e-5), rtol=1e-4)
+    again, _, _ = ops.conv2_up4_instnorm_stats(Ld, Gd, wp, bp)
+    assert torch.equal(y, again)
+
+
 def test_conv_deterministic(gpu):
     from posfeat_amd import ops
     g = torch.Generator().manual_seed(3)

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Counter passes over the head.conv2-shaped probe (tools/conv2_probe.py).
 # One rocprofv3 run per counter group (SQ/GRBM, TCC FETCH, TCC WRITE, LDS).
-# usage: tools/pmc_conv2.sh <outdir>
+# usage: [PROBE=tools/up4_probe.py] tools/pmc_conv2.sh <outdir>
 out=${1:-gpurun_out/pmc}
 mkdir -p "$out"
 cd /tmp && export TMPDIR=/tmp
@@ -9,7 +9,7 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 run() {
   tag=$1; shift
   timeout -k 10 240 rocprofv3 --pmc "$@" -d "$out/$tag" -o pmc --output-format csv \
-    -- python3 tools/conv2_probe.py 8 3 > "$out/$tag.log" 2>&1
+    -- python3 ${PROBE:-tools/conv2_probe.py} 8 3 > "$out/$tag.log" 2>&1
   rc=$?
   echo "[pmc] $tag rc=$rc" >> "$out/$tag.log"
   [ $rc -lt 124 ] || exit 100
