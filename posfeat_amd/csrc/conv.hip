@@ -41,9 +41,8 @@ struct ConvArgs {
   float* part;       // [ksplit][M][Cout] fp32 partial sums
   float* stats;      // optional [tiles_m][2 slots][Cout][2] per-tile (sum, sumsq)
   int hw;            // OH*OW (image boundary inside a tile for `stats`)
-  // conv_up4_kernel only: full-res second input and the low-res grid
-  const float* x2;
-  int x2cs, lh, lw;
+  // conv_up4_kernel only: the low-res grid
+  int lh, lw;
 };
 
 // Epilogue shared by both kernels: acc -> LDS T[BM][BN+4] (conflict-free: a
@@ -674,17 +673,17 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_halo_kernel(ConvArgs a) {
 // map is replicate-extended by one row/col (which is exactly how the
 // interpolation clamps).  So at phase (ry, rx) the 192-channel part is a
 // |E(ry)| x |E(rx)| conv on the LOW-RES map with combined weights (6.25 taps
-// on average instead of 9: -23% MACs for the whole layer) and the ×4
+// on average instead of 9: -23% MACs for the whole layer) and the x4
 // upsampled 256-channel map is never materialised.  The 64 full-res channels
-// (G) keep their 3x3 taps (gathered at stride 4).  Conv zero padding breaks
-// the periodicity only on the outermost rows/cols: those 2(H+W)-4 pixels per
-// image are excluded here and computed by an im2col + GEMM side path
-// (posfeat_conv2_up4).  Tile: an 8x16 patch of low-res positions of one phase;
-// the L halo (10x18, replicate-clamped) is staged once per slab like
-// conv_halo_kernel, G chunks are DMA-gathered per tap.
+// (G) are an ordinary 3x3 conv done first by conv_halo_kernel into y; this
+// kernel adds y as a same-thread residual.  Conv zero padding breaks the
+// periodicity only on the outermost rows/cols: up4_border_corr_kernel
+// subtracts those taps from y beforehand.  Tile: an 8x16 patch of low-res
+// positions of one phase; the L halo (10x18, replicate-clamped) is staged once
+// per 32-channel slab like conv_halo_kernel.
 constexpr int UP4_CU = 192, UP4_CG = 64, UP4_COUT = 128;
-constexpr int UP4_GCH = (UP4_CG / 32) * 9;  // G chunks (first in the phase K order)
-constexpr int UP4_KP = 2304;                // per-phase packed K capacity (<= 9 taps x 256)
+constexpr int UP4_KP = (UP4_CU / 32) * 9 * 32;  // per-phase packed K capacity (<= 9 taps)
+constexpr int UP4_GK = (UP4_CG / 32) * 9 * 32;  // K of the G conv (576)
 
 __device__ __forceinline__ int up4_ne(int r) { return (r == 0 || r == 3) ? 2 : 3; }
 // index of border pixel (Y, X) in the order of up4_border_pixel, -1 inside
@@ -704,9 +703,8 @@ __global__ __launch_bounds__(256) void conv_up4_kernel(ConvArgs a) {
   constexpr int HX = PW + 2, HY = PH + 2, HP = HX * HY;
   constexpr int A_G = (HP + 8 * NW - 1) / (8 * NW);
   constexpr int HPR = A_G * 8 * NW;
-  constexpr int G_G = BM / 8 / NW;  // gather DMA instructions per wave per G chunk
   constexpr int B_G = BN / 8 / NW;
-  static_assert(HPR >= BM && MI >= 1 && NI >= 1, "tile");
+  static_assert(MI >= 1 && NI >= 1, "tile");
   constexpr int RING = 2 * (HPR + BN) * BK;
   constexpr int STAGE = BM * (BN + 4);
   __shared__ __attribute__((aligned(16))) float smem[RING > STAGE ? RING : STAGE];
@@ -723,16 +721,18 @@ __global__ __launch_bounds__(256) void conv_up4_kernel(ConvArgs a) {
     const int nwg = a.nwg, q = nwg >> 3, r = nwg & 7, xcd = bid & 7, slot = bid >> 3;
     bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
   }
-  // tile = ((img * ppi + patch) * 16 + phase): the 16 phases of a patch are
-  // neighbours in the remapped order, so they share the L halo in L2
-  const int phase = bid & 15, t2 = bid >> 4;
+  // tile = (img * 16 + phase) * ppi + patch: after the XCD remap each XCD
+  // sweeps whole phases of an image, so one phase's combined weights stay in
+  // its L2 (interleaving all 16 phase weight sets streamed them from HBM for
+  // every block)
   const int ptx = (a.lw + PW - 1) / PW, ppi = ptx * ((a.lh + PH - 1) / PH);
-  const int img = t2 / ppi, prem = t2 - img * ppi;
+  const int t2 = bid / ppi, prem = bid - t2 * ppi;
+  const int img = t2 >> 4, phase = t2 & 15;
   const int qy0 = (prem / ptx) * PH, qx0 = (prem - (prem / ptx) * ptx) * PW;
   const int ry = phase >> 2, rx = phase & 3;
-  const int ney = up4_ne(ry), nex = up4_ne(rx), ey0 = up4_e0(ry), ex0 = up4_e0(rx);
-  const int T = ney * nex;
-  const int nch = UP4_GCH + (UP4_CU / 32) * T;
+  const int nex = up4_ne(rx), ey0 = up4_e0(ry), ex0 = up4_e0(rx);
+  const int T = up4_ne(ry) * nex;
+  const int nch = (UP4_CU / 32) * T;
   const int H = a.H, W = a.W;
 
   const int lrow = lane >> 3;
@@ -747,25 +747,6 @@ __global__ __launch_bounds__(256) void conv_up4_kernel(ConvArgs a) {
     hsrc[i] = hp < HP ? a.x + (((long long)img * a.lh + ly) * a.lw + lx) * a.xcs + sslot * 4
                       : nullptr;
   }
-  // G gather sources: tile row -> full-res pixel of this phase; 9-bit tap mask
-  const float* gsrc[G_G];
-  unsigned gok[G_G];
-#pragma unroll
-  for (int i = 0; i < G_G; ++i) {
-    const int row = (wave * G_G + i) * 8 + lrow;
-    const int qy = qy0 + (row >> 4), qx = qx0 + (row & 15);
-    const int Y = 4 * qy + ry, X = 4 * qx + rx;
-    const int sslot = (lane & 7) ^ ((row >> 1) & 7);
-    gok[i] = 0u;
-    gsrc[i] = a.x2;
-    if (qy < a.lh && qx < a.lw) {
-      for (int t = 0; t < 9; ++t) {
-        const int yy = Y + t / 3 - 1, xx = X + t % 3 - 1;
-        if ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W) gok[i] |= 1u << t;
-      }
-      gsrc[i] = a.x2 + (((long long)img * H + Y) * W + X) * a.x2cs + sslot * 4;
-    }
-  }
   const float* wsrc[B_G];
 #pragma unroll
   for (int i = 0; i < B_G; ++i) {
@@ -773,34 +754,22 @@ __global__ __launch_bounds__(256) void conv_up4_kernel(ConvArgs a) {
     const int sslot = (lane & 7) ^ ((row >> 1) & 7);
     wsrc[i] = a.w + ((size_t)phase * BN + row) * UP4_KP + sslot * 4;
   }
-  // A for chunk c into stage buf (G chunk: gathered rows; U chunk: slab halo)
-  auto issue_a = [&](int c, int buf) {
-    if (c < UP4_GCH) {
-      const int gs = c / 9, t = c - gs * 9;
-      const long long d = ((long long)(t / 3 - 1) * W + (t % 3 - 1)) * a.x2cs + gs * BK;
+  auto issue_halo = [&](int slab, int buf) {
 #pragma unroll
-      for (int i = 0; i < G_G; ++i) {
-        const float* src = ((gok[i] >> t) & 1u) ? gsrc[i] + d : pf_conv_zero16;
-        __builtin_amdgcn_global_load_lds(PF_GPTR(src), PF_LPTR(As + (buf * HPR + (wave * G_G + i) * 8) * BK),
-                                         16, 0, 0);
-      }
-    } else {
-      const int slab = (c - UP4_GCH) / T;
-#pragma unroll
-      for (int i = 0; i < A_G; ++i) {
-        const float* src = hsrc[i] ? hsrc[i] + slab * BK : pf_conv_zero16;
-        __builtin_amdgcn_global_load_lds(PF_GPTR(src), PF_LPTR(As + (buf * HPR + (wave * A_G + i) * 8) * BK),
-                                         16, 0, 0);
-      }
+    for (int i = 0; i < A_G; ++i) {
+      const float* src = hsrc[i] ? hsrc[i] + slab * BK : pf_conv_zero16;
+      __builtin_amdgcn_global_load_lds(PF_GPTR(src),
+                                       PF_LPTR(As + (buf * HPR + (wave * A_G + i) * 8) * BK), 16,
+                                       0, 0);
     }
   };
   auto issue_w = [&](int c, int buf) {
 #pragma unroll
     for (int i = 0; i < B_G; ++i)
       __builtin_amdgcn_global_load_lds(PF_GPTR(wsrc[i] + (size_t)c * BK),
-                                       PF_LPTR(Bs + (buf * BN + (wave * B_G + i) * 8) * BK), 16, 0, 0);
+                                       PF_LPTR(Bs + (buf * BN + (wave * B_G + i) * 8) * BK), 16,
+                                       0, 0);
   };
-  auto needs_a = [&](int c) { return c < UP4_GCH || (c - UP4_GCH) % T == 0; };
 
   f32x16 acc[MI][NI];
 #pragma unroll
@@ -811,37 +780,26 @@ __global__ __launch_bounds__(256) void conv_up4_kernel(ConvArgs a) {
       for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
 
   const int px = lane & 15;
-  const int arow = wm * TM + (lane & 31);
-  const int hrow0 = (arow >> 4) * HX + px;
-  const int asw = ((lane & 31) >> 1) & 7;  // row swizzle (G chunks), same for B
+  const int hrow0 = ((wm * TM + (lane & 31)) >> 4) * HX + px;
+  const int bsw = ((lane & 31) >> 1) & 7;
   const int brow = wn * TN + (lane & 31);
 
-  issue_a(0, 0);
+  issue_halo(0, 0);
   issue_w(0, 0);
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
 
-  int abuf = 0;
+  int abuf = 0, slab = 0, tj = 0;
   for (int c = 0; c < nch; ++c) {
     const int bcur = c & 1;
-    const bool nexta = c + 1 < nch && needs_a(c + 1);
+    const bool last_tap = tj == T - 1;
     if (c + 1 < nch) {
       issue_w(c + 1, bcur ^ 1);
-      if (nexta) issue_a(c + 1, abuf ^ 1);
+      if (last_tap) issue_halo(slab + 1, abuf ^ 1);
     }
-    const float* Ab;
-    int sw, mstep;
-    if (c < UP4_GCH) {
-      Ab = As + (abuf * HPR + arow) * BK;
-      sw = asw;
-      mstep = 32 * BK;
-    } else {
-      const int tj = (c - UP4_GCH) % T;
-      const int ey = ey0 + tj / nex, ex = ex0 + tj % nex;
-      Ab = As + (abuf * HPR + hrow0 + (ey + 1) * HX + ex + 1) * BK;
-      sw = ((px + ex + 1) >> 1) & 7;
-      mstep = 2 * HX * BK;
-    }
+    const int ey = ey0 + tj / nex, ex = ex0 + (tj - (tj / nex) * nex);
+    const float* Ab = As + (abuf * HPR + hrow0 + (ey + 1) * HX + ex + 1) * BK;
+    const int hsw = ((px + ex + 1) >> 1) & 7;
     const float* Bb = Bs + (bcur * BN + brow) * BK;
 #pragma unroll
     for (int kk = 0; kk < BK / 8; ++kk) {
@@ -849,10 +807,10 @@ __global__ __launch_bounds__(256) void conv_up4_kernel(ConvArgs a) {
       f32x4 av[MI], bv[NI];
 #pragma unroll
       for (int mi = 0; mi < MI; ++mi)
-        av[mi] = *reinterpret_cast<const f32x4*>(Ab + mi * mstep + (s ^ sw) * 4);
+        av[mi] = *reinterpret_cast<const f32x4*>(Ab + mi * 2 * HX * BK + (s ^ hsw) * 4);
 #pragma unroll
       for (int ni = 0; ni < NI; ++ni)
-        bv[ni] = *reinterpret_cast<const f32x4*>(Bb + ni * 32 * BK + (s ^ asw) * 4);
+        bv[ni] = *reinterpret_cast<const f32x4*>(Bb + ni * 32 * BK + (s ^ bsw) * 4);
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -862,31 +820,33 @@ __global__ __launch_bounds__(256) void conv_up4_kernel(ConvArgs a) {
             acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[mi][j], bv[ni][j], acc[mi][ni],
                                                                 0, 0, 0);
     }
-    if (nexta) abuf ^= 1;
+    if (last_tap) {
+      tj = 0;
+      ++slab;
+      abuf ^= 1;
+    } else {
+      ++tj;
+    }
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
   }
 
-  // border pixels: subtract the taps that fall into the conv zero padding
-  // (a.res = -correction rows from up4_border_corr_kernel, one per border pixel)
+  // y already holds G-conv + bias (- border corrections): same-thread residual
   conv_epilogue<BM, BN, WM, WN>(
       a, acc, smem, bid, 0, 0,
       [&](int row) {
         const int qy = qy0 + (row >> 4), qx = qx0 + (row & 15);
         return (qy < a.lh && qx < a.lw) ? (img * H + 4 * qy + ry) * W + 4 * qx + rx : -1;
       },
-      img,
-      [&](int row, int) {
-        const int Y = 4 * (qy0 + (row >> 4)) + ry, X = 4 * (qx0 + (row & 15)) + rx;
-        const int j = up4_border_index(Y, X, H, W);
-        return j < 0 ? (const float*)nullptr : a.res + ((size_t)img * a.rcs + j) * UP4_COUT;
-      });
+      img, [&](int, int m) { return (const float*)a.y + (size_t)m * a.ycs; });
 }
 
 // Phase weights from the packed conv2 weights ([128][2304], K order
-// (cin/32, kh, kw, cin%32)): wph[phase][cout][c*32 + ci] for the phase's chunk
-// order (G chunks, then per low-res slab its |E(ry)|x|E(rx)| taps), combined in
-// fp64: W'(ey,ex) = sum_{dy,dx} cy(dy,ey) cx(dx,ex) W(dy,dx).
+// (cin/32, kh, kw, cin%32)): wph[phase][cout][c*32 + ci] in the phase's chunk
+// order (per low-res slab its |E(ry)|x|E(rx)| taps), combined in fp64:
+// W'(ey,ex) = sum_{dy,dx} cy(dy,ey) cx(dx,ex) W(dy,dx).  Followed by the
+// transposed 3x3 taps of the 192 upsampled channels (border correction) and
+// the packed 64-channel G conv ([128][576], a contiguous slice of each row).
 __device__ double up4_coef(int r, int d, int e) {
   // coefficient of low-res row q+e in upsampled row 4q+r+d (d in -1..1)
   const int t = r + d;                    // -1..4
@@ -902,17 +862,14 @@ __device__ double up4_coef(int r, int d, int e) {
 __global__ void up4_phase_weights_kernel(const float* __restrict__ wpk, float* __restrict__ wph) {
   const int phase = blockIdx.y, o = blockIdx.x, ci = threadIdx.x & 31, cg = threadIdx.x >> 5;
   const int ry = phase >> 2, rx = phase & 3;
-  const int ney = up4_ne(ry), nex = up4_ne(rx), ey0 = up4_e0(ry), ex0 = up4_e0(rx), T = ney * nex;
-  const int nch = UP4_GCH + (UP4_CU / 32) * T;
-  const float* w = wpk + (size_t)o * UP4_KP;
+  const int nex = up4_ne(rx), ey0 = up4_e0(ry), ex0 = up4_e0(rx), T = up4_ne(ry) * nex;
+  const int nch = (UP4_CU / 32) * T;
+  const float* w = wpk + (size_t)o * 2304;
   float* dst = wph + ((size_t)phase * UP4_COUT + o) * UP4_KP;
   for (int c = cg; c < UP4_KP / 32; c += blockDim.x / 32) {
     float v = 0.f;
-    if (c < UP4_GCH) {
-      const int gs = c / 9, t = c - gs * 9;
-      v = w[((UP4_CU / 32 + gs) * 9 + t) * 32 + ci];
-    } else if (c < nch) {
-      const int u = c - UP4_GCH, slab = u / T, tj = u - slab * T;
+    if (c < nch) {
+      const int slab = c / T, tj = c - slab * T;
       const int ey = ey0 + tj / nex, ex = ex0 + tj % nex;
       double acc = 0.0;
       for (int dy = -1; dy <= 1; ++dy) {
@@ -928,13 +885,16 @@ __global__ void up4_phase_weights_kernel(const float* __restrict__ wpk, float* _
     }
     dst[c * 32 + ci] = v;
   }
-  // transposed 3x3 taps of the 192 upsampled channels for the border correction
   if (phase == 0) {
     float* wct = wph + (size_t)16 * UP4_COUT * UP4_KP;
     for (int e = threadIdx.x; e < 9 * UP4_CU; e += blockDim.x) {
       const int t = e / UP4_CU, ch = e % UP4_CU;
       wct[((size_t)t * UP4_CU + ch) * UP4_COUT + o] = w[((ch >> 5) * 9 + t) * 32 + (ch & 31)];
     }
+  } else if (phase == 1) {
+    float* wg = wph + (size_t)16 * UP4_COUT * UP4_KP + (size_t)9 * UP4_CU * UP4_COUT;
+    for (int e = threadIdx.x; e < UP4_GK; e += blockDim.x)
+      wg[(size_t)o * UP4_GK + e] = w[(UP4_CU / 32) * 9 * 32 + e];
   }
 }
 
@@ -953,21 +913,39 @@ __device__ __forceinline__ void up4_border_pixel(int j, int H, int W, int& Y, in
 // Border correction.  On the outermost rows/cols the phase formula also sums
 // taps that fall into conv2's zero padding, reading the replicate extension of
 // the upsampled map there -- which equals the nearest in-image upsampled
-// pixel.  corr[img][j][co] = -sum over out-of-image taps (dy,dx) of
+// pixel.  y[border pixel][co] -= sum over out-of-image taps (dy,dx) of
 // W[co][c][dy][dx] * up4(L)[clamp(Y+dy)][clamp(X+dx)][c]  (c < 192; the G
-// channels are gathered with exact zero padding).  8 border pixels per block,
-// one thread per cout, weights transposed to wct[tap][c][co] (coalesced).
-constexpr int UP4_CPB = 8;
-__global__ __launch_bounds__(UP4_COUT) void up4_border_corr_kernel(
+// conv has exact zero padding), before conv_up4_kernel adds its sum to y.  8 border pixels per block,
+// (pixel half, cout) per thread, weights transposed to wct[tap][c][co].
+constexpr int UP4_CPB = 16;
+__global__ __launch_bounds__(2 * UP4_COUT) void up4_border_corr_kernel(
     const float* __restrict__ L, int lcs, int lh, int lw, int H, int W, int nbp,
-    const float* __restrict__ wct, float* __restrict__ corr) {
-  __shared__ float u[UP4_CPB][9][UP4_CU];
-  __shared__ int bad[UP4_CPB];
-  const int img = blockIdx.y, j0 = blockIdx.x * UP4_CPB, tid = threadIdx.x;
+    const float* __restrict__ wct, float* __restrict__ y, int ycs) {
+  // u[k][c][p]: up4(L) at the clamped position of tap tl[k] for pixel p, or 0
+  // where that tap is inside the image for p (k over the union of the block's
+  // out-of-image taps: <= 5).  Each weight load then serves all 16 pixels.
+  __shared__ float u[5][UP4_CU][UP4_CPB];
+  __shared__ int tl[5], nt, bad[UP4_CPB], pyx[UP4_CPB][2];
+  // blocks never straddle two border segments (top, bottom, left, right):
+  // the union of out-of-image taps then has <= 5 members
+  const int img = blockIdx.y, tid = threadIdx.x;
+  const int bw = (W + UP4_CPB - 1) / UP4_CPB, bh = (H - 2 + UP4_CPB - 1) / UP4_CPB;
+  int seg = blockIdx.x, sb;
+  if (seg < 2 * bw) {
+    sb = seg % bw;
+    seg = seg / bw;
+  } else {
+    sb = (seg - 2 * bw) % bh;
+    seg = 2 + (seg - 2 * bw) / bh;
+  }
+  const int seglen = seg < 2 ? W : H - 2;
+  const int segbase = seg < 2 ? seg * W : 2 * W + (seg - 2) * (H - 2);
+  const int j0 = segbase + sb * UP4_CPB;
+  const int jend = segbase + seglen;
   const float sh = (float)lh / (float)H, sw = (float)lw / (float)W;
   if (tid < UP4_CPB) {
     int Y = 0, X = 0, mask = 0;
-    if (j0 + tid < nbp) {
+    if (j0 + tid < jend) {
       up4_border_pixel(j0 + tid, H, W, Y, X);
       for (int t = 0; t < 9; ++t) {
         const int yy = Y + t / 3 - 1, xx = X + t % 3 - 1;
@@ -975,14 +953,27 @@ __global__ __launch_bounds__(UP4_COUT) void up4_border_corr_kernel(
       }
     }
     bad[tid] = mask;
+    pyx[tid][0] = Y;
+    pyx[tid][1] = X;
   }
-  for (int e = tid; e < UP4_CPB * 9 * UP4_CU; e += UP4_COUT) {
-    const int p = e / (9 * UP4_CU), t = (e / UP4_CU) % 9, c = e % UP4_CU;
+  __syncthreads();
+  if (tid == 0) {
+    int um = 0;
+    for (int p = 0; p < UP4_CPB; ++p) um |= bad[p];
+    int k = 0;
+    for (int t = 0; t < 9; ++t)
+      if ((um >> t) & 1) tl[k++] = t;
+    nt = k;
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (int e = tid; e < nt * UP4_CU * UP4_CPB; e += 2 * UP4_COUT) {
+    const int k = e / (UP4_CU * UP4_CPB), c = (e / UP4_CPB) % UP4_CU, p = e % UP4_CPB;
+    const int t = tl[k];
     float v = 0.f;
-    if (j0 + p < nbp) {
-      int Y, X;
-      up4_border_pixel(j0 + p, H, W, Y, X);
-      const int yy = min(max(Y + t / 3 - 1, 0), H - 1), xx = min(max(X + t % 3 - 1, 0), W - 1);
+    if ((bad[p] >> t) & 1) {
+      const int yy = min(max(pyx[p][0] + t / 3 - 1, 0), H - 1);
+      const int xx = min(max(pyx[p][1] + t % 3 - 1, 0), W - 1);
       // PyTorch upsample_bilinear2d, align_corners=False (as norm_prelu_upsample)
       float fy = sh * (yy + 0.5f) - 0.5f, fx = sw * (xx + 0.5f) - 0.5f;
       fy = fy < 0.f ? 0.f : fy;
@@ -995,18 +986,30 @@ __global__ __launch_bounds__(UP4_COUT) void up4_border_corr_kernel(
       const float v10 = b[((size_t)y1 * lw + x0) * lcs], v11 = b[((size_t)y1 * lw + x1) * lcs];
       v = hy * (hx * v00 + lx * v01) + ly * (hx * v10 + lx * v11);
     }
-    u[p][t][c] = v;
+    u[k][c][p] = v;
   }
   __syncthreads();
-  for (int p = 0; p < UP4_CPB && j0 + p < nbp; ++p) {
-    float acc = 0.f;
-    for (int t = 0; t < 9; ++t) {
-      if (!((bad[p] >> t) & 1)) continue;
-      const float* w = wct + (size_t)t * UP4_CU * UP4_COUT + tid;
-      for (int c = 0; c < UP4_CU; ++c) acc = fmaf(w[(size_t)c * UP4_COUT], u[p][t][c], acc);
+  // thread = (pixel half, cout); fixed (tap, channel) order -> deterministic
+  constexpr int PH2 = UP4_CPB / 2;
+  const int co = tid & (UP4_COUT - 1), p0 = (tid >> 7) * PH2;
+  float acc[PH2];
+#pragma unroll
+  for (int p = 0; p < PH2; ++p) acc[p] = 0.f;
+  for (int k = 0; k < nt; ++k) {
+    const float* w = wct + (size_t)tl[k] * UP4_CU * UP4_COUT + co;
+    for (int c = 0; c < UP4_CU; ++c) {
+      const float wv = w[(size_t)c * UP4_COUT];
+#pragma unroll
+      for (int p = 0; p < PH2; ++p) acc[p] = fmaf(wv, u[k][c][p0 + p], acc[p]);
     }
-    corr[((size_t)img * nbp + j0 + p) * UP4_COUT + tid] = -acc;
   }
+#pragma unroll
+  for (int p = 0; p < PH2; ++p)
+    if (j0 + p0 + p < jend) {
+      int Y, X;
+      up4_border_pixel(j0 + p0 + p, H, W, Y, X);
+      y[(((size_t)img * H + Y) * W + X) * ycs + co] -= acc[p];
+    }
 }
 
 // Instance-norm statistics from the per-tile partials of the conv epilogue.
@@ -1380,10 +1383,11 @@ extern "C" int posfeat_conv2d_nhwc_stats(const posfeat_conv_desc* d, const float
 // head.conv2 by bilinear phases (see conv_up4_kernel).
 static int up4_nbp(int H, int W) { return 2 * W + 2 * (H - 2); }
 static int up4_ppi(int H, int W) { return ((W / 4 + 15) / 16) * ((H / 4 + 7) / 8); }
-static const size_t UP4_WPH_FLOATS = (size_t)16 * UP4_COUT * UP4_KP + (size_t)9 * UP4_CU * UP4_COUT;
+static const size_t UP4_WPH_FLOATS = (size_t)16 * UP4_COUT * UP4_KP +
+                                     (size_t)9 * UP4_CU * UP4_COUT + (size_t)UP4_COUT * UP4_GK;
 
 struct Up4Ws {
-  size_t stats, chunks, corr, total;
+  size_t stats, chunks, total;
   int nch;
 };
 
@@ -1399,7 +1403,6 @@ static Up4Ws up4_layout(int n, int H, int W) {
   };
   L.stats = take((size_t)n * ppi * 16 * 2 * UP4_COUT * 2 * sizeof(float));
   L.chunks = take((size_t)n * L.nch * UP4_COUT * 2 * sizeof(double));
-  L.corr = take((size_t)n * up4_nbp(H, W) * UP4_COUT * sizeof(float));
   L.total = cur;
   return L;
 }
@@ -1422,7 +1425,7 @@ extern "C" int posfeat_conv2_up4(int n, int H, int W, const float* L, int lcs, c
                                  int gcs, const float* wph, const float* w_packed,
                                  const float* bias, float* y, int ycs, void* ws, size_t ws_bytes,
                                  float* mean, float* rstd, float eps, void* stream) {
-  (void)w_packed;  // folded into wph (phase weights + transposed border taps)
+  (void)w_packed;  // folded into wph (phase weights, border taps, G conv)
   if (n <= 0 || H < 16 || W < 16 || H % 4 || W % 4 || !L || !G || !wph || !y || !mean || !rstd)
     return POSFEAT_E_INVALID;
   if (lcs < UP4_CU || lcs % 4 || gcs < UP4_CG || gcs % 4 || ycs < UP4_COUT || ycs % 4)
@@ -1436,24 +1439,41 @@ extern "C" int posfeat_conv2_up4(int n, int H, int W, const float* L, int lcs, c
   char* base = static_cast<char*>(ws);
   hipStream_t st = pf_stream(stream);
   const int nbp = up4_nbp(H, W), ppi = up4_ppi(H, W);
-  float* corr = reinterpret_cast<float*>(base + lay.corr);
+  const float* wct = wph + (size_t)16 * UP4_COUT * UP4_KP;
+  const float* wg = wct + (size_t)9 * UP4_CU * UP4_COUT;
 
-  // 1. border corrections (taps in conv2's zero padding)
-  hipLaunchKernelGGL(up4_border_corr_kernel, dim3((nbp + UP4_CPB - 1) / UP4_CPB, n),
-                     dim3(UP4_COUT), 0, st, L, lcs, H / 4, W / 4, H, W, nbp,
-                     wph + (size_t)16 * UP4_COUT * UP4_KP, corr);
+  // 1. y = conv3x3(G, W[:, 192:]) + bias  (full-res halo kernel)
+  posfeat_conv_desc d{};
+  d.n = n;
+  d.h = H;
+  d.w = W;
+  d.cin = UP4_CG;
+  d.x_cstride = gcs;
+  d.cout = UP4_COUT;
+  d.kh = 3;
+  d.kw = 3;
+  d.stride = 1;
+  d.pad = 1;
+  d.y_cstride = ycs;
+  d.res_cstride = 0;
+  d.act = POSFEAT_ACT_NONE;
+  ConvArgs g;
+  PF_TRY(conv_prepare(&d, G, wg, bias, nullptr, y, g));
+  PF_TRY(conv_run(g, conv_plan(g, false), st));
+
+  // 2. border lines: remove the taps that fall into conv2's zero padding
+  const int ncb = 2 * ((W + UP4_CPB - 1) / UP4_CPB) + 2 * ((H - 2 + UP4_CPB - 1) / UP4_CPB);
+  hipLaunchKernelGGL(up4_border_corr_kernel, dim3(ncb, n), dim3(2 * UP4_COUT), 0, st, L, lcs,
+                     H / 4, W / 4, H, W, nbp, wct, y, ycs);
   PF_CHECK_LAUNCH();
 
-  // 2. all pixels, 16 phases, fused IN partials; border rows add corr
+  // 3. the 192 upsampled channels by phases, + y, fused IN partials
   ConvArgs a{};
   a.x = L;
   a.xcs = lcs;
-  a.x2 = G;
-  a.x2cs = gcs;
   a.w = wph;
-  a.bias = bias;
-  a.res = corr;
-  a.rcs = nbp;  // rows per image of corr (see the epilogue residual map)
+  a.bias = nullptr;
+  a.res = nullptr;
   a.y = y;
   a.ycs = ycs;
   a.H = H;
@@ -1462,7 +1482,7 @@ extern "C" int posfeat_conv2_up4(int n, int H, int W, const float* L, int lcs, c
   a.OW = W;
   a.lh = H / 4;
   a.lw = W / 4;
-  a.Cin = UP4_CU + UP4_CG;
+  a.Cin = UP4_CU;
   a.Cout = UP4_COUT;
   a.M = n * H * W;
   a.hw = H * W;
@@ -1474,7 +1494,7 @@ extern "C" int posfeat_conv2_up4(int n, int H, int W, const float* L, int lcs, c
   launch_up4(a, st);
   PF_CHECK_LAUNCH();
 
-  // 3. IN statistics (deterministic, fp64 merge)
+  // 4. IN statistics (deterministic, fp64 merge)
   double* ch = reinterpret_cast<double*>(base + lay.chunks);
   hipLaunchKernelGGL(conv_stats_chunk, dim3(lay.nch, UP4_COUT / 64, n), dim3(1024), 0, st,
                      a.stats, 128, 16 * ppi, a.hw, UP4_COUT, lay.nch, ch);
