@@ -1421,28 +1421,10 @@ extern "C" int posfeat_conv2_up4_weights(const float* w_packed, float* wph, void
   return POSFEAT_OK;
 }
 
-extern "C" int posfeat_conv2_up4(int n, int H, int W, const float* L, int lcs, const float* G,
-                                 int gcs, const float* wph, const float* w_packed,
-                                 const float* bias, float* y, int ycs, void* ws, size_t ws_bytes,
-                                 float* mean, float* rstd, float eps, void* stream) {
-  (void)w_packed;  // folded into wph (phase weights, border taps, G conv)
-  if (n <= 0 || H < 16 || W < 16 || H % 4 || W % 4 || !L || !G || !wph || !y || !mean || !rstd)
-    return POSFEAT_E_INVALID;
-  if (lcs < UP4_CU || lcs % 4 || gcs < UP4_CG || gcs % 4 || ycs < UP4_COUT || ycs % 4)
-    return POSFEAT_E_INVALID;
-  const uintptr_t al = reinterpret_cast<uintptr_t>(L) | reinterpret_cast<uintptr_t>(G) |
-                       reinterpret_cast<uintptr_t>(wph) | reinterpret_cast<uintptr_t>(y) |
-                       reinterpret_cast<uintptr_t>(bias);
-  if (al & 15) return POSFEAT_E_INVALID;
-  const Up4Ws lay = up4_layout(n, H, W);
-  if (!ws || ws_bytes < lay.total) return POSFEAT_E_WORKSPACE;
-  char* base = static_cast<char*>(ws);
-  hipStream_t st = pf_stream(stream);
-  const int nbp = up4_nbp(H, W), ppi = up4_ppi(H, W);
-  const float* wct = wph + (size_t)16 * UP4_COUT * UP4_KP;
-  const float* wg = wct + (size_t)9 * UP4_CU * UP4_COUT;
-
-  // 1. y = conv3x3(G, W[:, 192:]) + bias  (full-res halo kernel)
+// The three steps (also sequenced and timed one by one by engine.hip).
+int pf_up4_gconv(int n, int H, int W, const float* G, int gcs, const float* wph,
+                 const float* bias, float* y, int ycs, hipStream_t st) {
+  const float* wg = wph + (size_t)16 * UP4_COUT * UP4_KP + (size_t)9 * UP4_CU * UP4_COUT;
   posfeat_conv_desc d{};
   d.n = n;
   d.h = H;
@@ -1459,15 +1441,25 @@ extern "C" int posfeat_conv2_up4(int n, int H, int W, const float* L, int lcs, c
   d.act = POSFEAT_ACT_NONE;
   ConvArgs g;
   PF_TRY(conv_prepare(&d, G, wg, bias, nullptr, y, g));
-  PF_TRY(conv_run(g, conv_plan(g, false), st));
+  return conv_run(g, conv_plan(g, false), st);
+}
 
-  // 2. border lines: remove the taps that fall into conv2's zero padding
+int pf_up4_border(int n, int H, int W, const float* L, int lcs, const float* wph, float* y,
+                  int ycs, hipStream_t st) {
   const int ncb = 2 * ((W + UP4_CPB - 1) / UP4_CPB) + 2 * ((H - 2 + UP4_CPB - 1) / UP4_CPB);
   hipLaunchKernelGGL(up4_border_corr_kernel, dim3(ncb, n), dim3(2 * UP4_COUT), 0, st, L, lcs,
-                     H / 4, W / 4, H, W, nbp, wct, y, ycs);
+                     H / 4, W / 4, H, W, up4_nbp(H, W), wph + (size_t)16 * UP4_COUT * UP4_KP, y,
+                     ycs);
   PF_CHECK_LAUNCH();
+  return POSFEAT_OK;
+}
 
-  // 3. the 192 upsampled channels by phases, + y, fused IN partials
+int pf_up4_main(int n, int H, int W, const float* L, int lcs, const float* wph, float* y, int ycs,
+                void* ws, size_t ws_bytes, float* mean, float* rstd, float eps, hipStream_t st) {
+  const Up4Ws lay = up4_layout(n, H, W);
+  if (!ws || ws_bytes < lay.total) return POSFEAT_E_WORKSPACE;
+  char* base = static_cast<char*>(ws);
+  const int ppi = up4_ppi(H, W);
   ConvArgs a{};
   a.x = L;
   a.xcs = lcs;
@@ -1493,8 +1485,6 @@ extern "C" int posfeat_conv2_up4(int n, int H, int W, const float* L, int lcs, c
   a.stats = reinterpret_cast<float*>(base + lay.stats);
   launch_up4(a, st);
   PF_CHECK_LAUNCH();
-
-  // 4. IN statistics (deterministic, fp64 merge)
   double* ch = reinterpret_cast<double*>(base + lay.chunks);
   hipLaunchKernelGGL(conv_stats_chunk, dim3(lay.nch, UP4_COUT / 64, n), dim3(1024), 0, st,
                      a.stats, 128, 16 * ppi, a.hw, UP4_COUT, lay.nch, ch);
@@ -1503,4 +1493,26 @@ extern "C" int posfeat_conv2_up4(int n, int H, int W, const float* L, int lcs, c
                      lay.nch, H * W, UP4_COUT, n, eps, mean, rstd, nullptr, 0);
   PF_CHECK_LAUNCH();
   return POSFEAT_OK;
+}
+
+extern "C" int posfeat_conv2_up4(int n, int H, int W, const float* L, int lcs, const float* G,
+                                 int gcs, const float* wph, const float* w_packed,
+                                 const float* bias, float* y, int ycs, void* ws, size_t ws_bytes,
+                                 float* mean, float* rstd, float eps, void* stream) {
+  (void)w_packed;  // folded into wph (phase weights, border taps, G conv)
+  if (n <= 0 || H < 16 || W < 16 || H % 4 || W % 4 || !L || !G || !wph || !y || !mean || !rstd)
+    return POSFEAT_E_INVALID;
+  if (lcs < UP4_CU || lcs % 4 || gcs < UP4_CG || gcs % 4 || ycs < UP4_COUT || ycs % 4)
+    return POSFEAT_E_INVALID;
+  const uintptr_t al = reinterpret_cast<uintptr_t>(L) | reinterpret_cast<uintptr_t>(G) |
+                       reinterpret_cast<uintptr_t>(wph) | reinterpret_cast<uintptr_t>(y) |
+                       reinterpret_cast<uintptr_t>(bias);
+  if (al & 15) return POSFEAT_E_INVALID;
+  hipStream_t st = pf_stream(stream);
+  // 1. y = conv3x3(G, W[:, 192:]) + bias  (full-res halo kernel)
+  PF_TRY(pf_up4_gconv(n, H, W, G, gcs, wph, bias, y, ycs, st));
+  // 2. border lines: remove the taps that fall into conv2's zero padding
+  PF_TRY(pf_up4_border(n, H, W, L, lcs, wph, y, ycs, st));
+  // 3. the 192 upsampled channels by phases, + y, IN statistics
+  return pf_up4_main(n, H, W, L, lcs, wph, y, ycs, ws, ws_bytes, mean, rstd, eps, st);
 }

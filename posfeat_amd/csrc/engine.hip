@@ -373,12 +373,21 @@ int forward(Ctx& c, const float* img, posfeat_extract_out* out) {
     PF_TRY(timed(c, "instnorm_apply", 0, [&] {
       return pf_in_apply(g64, B, H * W, 64, 64, mean, rstd, nullptr, c.st);
     }));
-    const double fl = 2.0 * B * H * W * 128.0 * 256 * 9;  // reference conv2 FLOPs
-    PF_TRY(timed(c, "conv:head.conv2", fl, [&] {
-      PF_TRY(posfeat_conv2_up4_weights(c.W("head.conv2"), c.f(m->wph), c.st));
-      return posfeat_conv2_up4(B, H, W, c1, 192, g64, 64, c.f(m->wph), c.W("head.conv2"),
-                               c.Bi("head.conv2"), c2, 128, c.f(m->up4ws),
-                               m->up4ws.floats * sizeof(float), mean, rstd, 1e-5f, c.st);
+    // executed MFMA work: 64 full-res channels x 9 taps, 192 low-res channels
+    // x 6.25 taps on average over the 16 phases (the reference layer: 256 x 9)
+    const float* wph = c.f(m->wph);
+    PF_TRY(timed(c, "head.conv2.weights", 0, [&] {
+      return posfeat_conv2_up4_weights(c.W("head.conv2"), c.f(m->wph), c.st);
+    }));
+    PF_TRY(timed(c, "conv:head.conv2.g", 2.0 * B * H * W * 128.0 * 64 * 9, [&] {
+      return pf_up4_gconv(B, H, W, g64, 64, wph, c.Bi("head.conv2"), c2, 128, c.st);
+    }));
+    PF_TRY(timed(c, "head.conv2.border", 0, [&] {
+      return pf_up4_border(B, H, W, c1, 192, wph, c2, 128, c.st);
+    }));
+    PF_TRY(timed(c, "conv:head.conv2.up4", 2.0 * B * H * W * 128.0 * 192 * 6.25, [&] {
+      return pf_up4_main(B, H, W, c1, 192, wph, c2, 128, c.f(m->up4ws),
+                         m->up4ws.floats * sizeof(float), mean, rstd, 1e-5f, c.st);
     }));
   } else {
     float* hcat = c.f(m->hcat);

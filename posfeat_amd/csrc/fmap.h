@@ -21,3 +21,11 @@ int pf_head_tail(const float* x, int n, int hw, int cs, const float* mean, const
                  const float* slope, const float* w3, const float* b3, float* yraw, float* out,
                  float* mean1, float* rstd1, double* part, hipStream_t st);
 int pf_global_feat(const float* g, int n, int hw, int cs, float* out, hipStream_t st);
+
+// head.conv2 by bilinear phases, step by step (conv.hip; see posfeat_conv2_up4)
+int pf_up4_gconv(int n, int H, int W, const float* G, int gcs, const float* wph,
+                 const float* bias, float* y, int ycs, hipStream_t st);
+int pf_up4_border(int n, int H, int W, const float* L, int lcs, const float* wph, float* y,
+                  int ycs, hipStream_t st);
+int pf_up4_main(int n, int H, int W, const float* L, int lcs, const float* wph, float* y, int ycs,
+                void* ws, size_t ws_bytes, float* mean, float* rstd, float eps, hipStream_t st);

@@ -1,10 +1,10 @@
-"""HBM traffic of the head.conv2 launch from rocprofv3 PMC passes
-(tools/pmc_conv2.sh): bytes = 2 x FETCH_SIZE + WRITE_SIZE (KB units; gfx950
-FETCH_SIZE counts half the bytes of wide streaming reads, MI355X_MICROARCH.md
-"FETCH_SIZE").  Averaged over the conv dispatches of the probe (B images per
-launch); writes {"bytes_per_launch_per_image": ...} for bench.py.
+"""HBM traffic of one kernel from rocprofv3 PMC passes (tools/pmc_conv2.sh):
+bytes = 2 x FETCH_SIZE + WRITE_SIZE (KB units; gfx950 FETCH_SIZE counts half
+the bytes of wide streaming reads, MI355X_MICROARCH.md "FETCH_SIZE").
+Averaged over the dispatches of the kernel whose name contains <kernel>
+(B images per launch); writes {"bytes_per_launch_per_image": ...} for bench.py.
 
-usage: python tools/traffic_json.py <pmc_dir> <out.json> [batch]
+usage: python tools/traffic_json.py <pmc_dir> <out.json> [batch] [kernel] [algorithmic_bytes]
 """
 import collections
 import csv
@@ -13,10 +13,10 @@ import os
 import sys
 
 
-def per_dispatch(path, counter):
+def per_dispatch(path, counter, kernel):
     vals = collections.defaultdict(float)
     for r in csv.DictReader(open(path)):
-        if "conv_" in r["Kernel_Name"] and "kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter:
+        if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
             vals[r["Dispatch_Id"]] += float(r["Counter_Value"])
     return list(vals.values())
 
@@ -24,13 +24,17 @@ def per_dispatch(path, counter):
 def main():
     d, out = sys.argv[1], sys.argv[2]
     batch = int(sys.argv[3]) if len(sys.argv) > 3 else 8
-    fetch = per_dispatch(os.path.join(d, "fetch", "pmc_counter_collection.csv"), "FETCH_SIZE")
-    write = per_dispatch(os.path.join(d, "write", "pmc_counter_collection.csv"), "WRITE_SIZE")
+    kernel = sys.argv[4] if len(sys.argv) > 4 else "conv_up4_kernel"
+    fetch = per_dispatch(os.path.join(d, "fetch", "pmc_counter_collection.csv"), "FETCH_SIZE", kernel)
+    write = per_dispatch(os.path.join(d, "write", "pmc_counter_collection.csv"), "WRITE_SIZE", kernel)
     f_kb = sum(fetch) / len(fetch)
     w_kb = sum(write) / len(write)
     total = (2.0 * f_kb + w_kb) * 1024.0
-    alg = batch * 480 * 640 * (256 + 128) * 4 + 128 * 2304 * 4
-    rec = {"kernel": "head.conv2 3x3 256->128 @480x640 (tools/conv2_probe.py)",
+    # conv_up4_kernel: L (120x160x192) + y residual read + y write + its
+    # phase weights (16 x 128 x 1728)
+    alg = float(sys.argv[5]) if len(sys.argv) > 5 else (
+        batch * (120 * 160 * 192 + 2 * 480 * 640 * 128) * 4 + 16 * 128 * 1728 * 4)
+    rec = {"kernel": kernel, "probe": "tools/up4_probe.py (B=%d, 480x640)" % batch,
            "batch": batch, "fetch_kb_raw": f_kb, "write_kb": w_kb,
            "bytes_per_launch": total, "bytes_per_launch_per_image": total / batch,
            "algorithmic_bytes_per_launch": alg, "ratio_to_algorithmic": total / alg,
