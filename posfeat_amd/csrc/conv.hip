@@ -20,6 +20,7 @@
 // of 8 contracts k-pair {j, 4+j} -- the same permutation on A and B, so the
 // product is exact f32 fmaf chains in a fixed (deterministic) order.
 #include "common.h"
+#include "fmap.h"
 
 namespace {
 
@@ -1129,8 +1130,9 @@ struct Plan {
 // POSFEAT_CONV_KERNEL=staged|glds|halo caps the kernel family, POSFEAT_CONV_TILE
 // forces a tile id where legal.
 struct ConvEnv {
-  int kmax = KERN_HALO, tile = -1;
+  int kmax = KERN_HALO, tile = -1, maxsplit = 4;
   ConvEnv() {
+    if (const char* e = getenv("POSFEAT_CONV_MAXSPLIT")) maxsplit = atoi(e);
     if (const char* e = getenv("POSFEAT_CONV_KERNEL")) {
       if (e[0] == 's') kmax = KERN_STAGED;
       else if (e[0] == 'g') kmax = KERN_GLDS;
@@ -1149,11 +1151,12 @@ int choose_ksplit(long long tiles, int nch, double slots) {
   if (nch < 64) return 1;
   int best = 1;
   double best_eff = 0.0;
-  for (int ks = 1; ks <= 4; ++ks) {
+  for (int ks = 1; ks <= conv_env().maxsplit; ++ks) {
     if (nch / ks < 32) break;
     const double r = tiles * ks / slots;
     const double eff = r / ceil(r) * (ks == 1 ? 1.0 : 0.97);  // ~3% for the reduce pass
-    if (eff > best_eff + 1e-9) {
+    // split only for a clear gain (A/B at 480x640: decoder layers gain nothing)
+    if (eff > best_eff * 1.08) {
       best_eff = eff;
       best = ks;
     }
@@ -1161,48 +1164,86 @@ int choose_ksplit(long long tiles, int nch, double slots) {
   return best;
 }
 
-Plan conv_plan(const ConvArgs& a, bool allow_split) {
-  const ConvEnv& env = conv_env();
+// Geometry of one tile id for this conv (ksplit = 1); kern = -1 if illegal.
+Plan plan_for_tile(const ConvArgs& a, int tile) {
   Plan p{};
+  p.kern = -1;
+  p.tile = tile;
+  p.ksplit = 1;
   const bool cin32 = a.Cin % BK == 0;
-  const int nch = a.Kpad / BK;
-  const bool halo_ok = cin32 && env.kmax >= KERN_HALO && a.stride == 1 && a.KH == 3 &&
+  const bool halo_ok = cin32 && conv_env().kmax >= KERN_HALO && a.stride == 1 && a.KH == 3 &&
                        a.KW == 3 && a.OW >= 16 && a.OH >= 8 && a.Cout % 64 == 0;
-  if (halo_ok) {
-    p.kern = KERN_HALO;
-    if (a.Cout % 128 == 0)
-      p.tile = env.tile == TILE_H16x128 ? TILE_H16x128 : TILE_H8x128;
-    else
-      p.tile = TILE_H8x64;
-    const int ph = p.tile == TILE_H16x128 ? 16 : 8;
-    p.bm = ph * 16;
-    p.bn = p.tile == TILE_H8x64 ? 64 : 128;
-    p.ppi = ((a.OW + 15) / 16) * ((a.OH + ph - 1) / ph);
-    p.tiles_m = (long long)(a.M / a.hw) * p.ppi;
-    const double slots = p.tile == TILE_H16x128 ? 256.0 : 512.0;
-    p.ksplit = allow_split ? choose_ksplit(p.tiles_m * ((a.Cout + p.bn - 1) / p.bn), nch, slots)
-                           : 1;
-    return p;
+  switch (tile) {
+    case TILE_H8x128:
+    case TILE_H16x128:
+    case TILE_H8x64: {
+      if (!halo_ok || (tile != TILE_H8x64 && a.Cout % 128)) return p;
+      const int ph = tile == TILE_H16x128 ? 16 : 8;
+      p.kern = KERN_HALO;
+      p.bm = ph * 16;
+      p.bn = tile == TILE_H8x64 ? 64 : 128;
+      p.ppi = ((a.OW + 15) / 16) * ((a.OH + ph - 1) / ph);
+      p.tiles_m = (long long)(a.M / a.hw) * p.ppi;
+      return p;
+    }
+    case TILE_256x128:
+      if (!cin32 || a.Cout % 128) return p;
+      p.bm = 256;
+      p.bn = 128;
+      break;
+    case TILE_128x128: p.bm = 128; p.bn = 128; break;
+    case TILE_128x64: p.bm = 128; p.bn = 64; break;
+    case TILE_64x64: p.bm = 64; p.bn = 64; break;
+    default: return p;
   }
   p.kern = !cin32 ? KERN_STAGED
-                  : (env.kmax >= KERN_GLDS && a.KH * a.KW <= 32 ? KERN_GLDS : KERN_STAGED);
+                  : (conv_env().kmax >= KERN_GLDS && a.KH * a.KW <= 32 ? KERN_GLDS : KERN_STAGED);
+  if (tile == TILE_256x128 && p.kern != KERN_GLDS) {
+    p.kern = -1;
+    return p;
+  }
   p.ppi = 0;
-  const long long t128 = (long long)((a.M + 127) / 128) * ((a.Cout + 127) / 128);
-  const long long t256 = (long long)((a.M + 255) / 256) * ((a.Cout + 127) / 128);
-  p.ksplit = (allow_split && a.Cout > 64) ? choose_ksplit(t128, nch, 512.0) : 1;
-  if (env.tile == TILE_256x128 && cin32 && a.Cout % 128 == 0 && t256 >= 256 && p.ksplit == 1)
-    p.tile = TILE_256x128;
-  else if (a.Cout > 64 && (t128 >= 512 || p.ksplit > 1))
-    p.tile = TILE_128x128;
-  else if ((long long)((a.M + 127) / 128) * ((a.Cout + 63) / 64) >= 512)
-    p.tile = TILE_128x64;
-  else
-    p.tile = TILE_64x64;
-  p.bm = p.tile == TILE_64x64 ? 64 : p.tile == TILE_256x128 ? 256 : 128;
-  p.bn = (p.tile == TILE_128x128 || p.tile == TILE_256x128) ? 128 : 64;
-  if (p.tile != TILE_128x128) p.ksplit = 1;
   p.tiles_m = (a.M + p.bm - 1) / p.bm;
   return p;
+}
+
+// Default plan (heuristic), optionally overridden by a legal tile id.  The
+// split factor comes from the default choice whatever the tile, and every
+// kernel/tile runs the same fmaf sequence per output, so results do not
+// depend on the tile (the engine's autotuner relies on this).
+Plan conv_plan(const ConvArgs& a, bool allow_split, int forced = -1) {
+  const ConvEnv& env = conv_env();
+  const bool cin32 = a.Cin % BK == 0;
+  const int nch = a.Kpad / BK;
+  Plan d = plan_for_tile(a, a.Cout % 128 == 0 ? TILE_H8x128 : TILE_H8x64);
+  if (d.kern == KERN_HALO) {
+    if ((env.tile == TILE_H16x128) && a.Cout % 128 == 0) d = plan_for_tile(a, TILE_H16x128);
+    const double slots = d.tile == TILE_H16x128 ? 256.0 : 512.0;
+    d.ksplit = allow_split ? choose_ksplit(d.tiles_m * ((a.Cout + d.bn - 1) / d.bn), nch, slots) : 1;
+  } else {
+    const long long t128 = (long long)((a.M + 127) / 128) * ((a.Cout + 127) / 128);
+    const long long t256 = (long long)((a.M + 255) / 256) * ((a.Cout + 127) / 128);
+    const int ks = (allow_split && a.Cout > 64) ? choose_ksplit(t128, nch, 512.0) : 1;
+    int tile;
+    if (env.tile == TILE_256x128 && cin32 && a.Cout % 128 == 0 && t256 >= 256 && ks == 1)
+      tile = TILE_256x128;
+    else if (a.Cout > 64 && (t128 >= 512 || ks > 1))
+      tile = TILE_128x128;
+    else if ((long long)((a.M + 127) / 128) * ((a.Cout + 63) / 64) >= 512)
+      tile = TILE_128x64;
+    else
+      tile = TILE_64x64;
+    d = plan_for_tile(a, tile);
+    d.ksplit = tile == TILE_128x128 ? ks : 1;
+  }
+  if (forced >= 0) {
+    Plan f = plan_for_tile(a, forced);
+    if (f.kern >= 0) {
+      f.ksplit = d.ksplit;
+      return f;
+    }
+  }
+  return d;
 }
 
 template <int BM, int BN, int WM, int WN>
@@ -1357,14 +1398,68 @@ extern "C" int posfeat_conv2d_nhwc_stats(const posfeat_conv_desc* d, const float
                                          const float* w, const float* bias, float* y, void* ws,
                                          size_t ws_bytes, float* mean, float* rstd, float eps,
                                          void* stream) {
+  return pf_conv_stats_run_tile(d, x, w, bias, y, ws, ws_bytes, mean, rstd, eps, -1,
+                                pf_stream(stream));
+}
+
+// ---------------------------------------------------------------------------
+// Tile-aware entry points for the engine's autotuner (fmap.h).
+static const int kAllTiles[] = {TILE_H8x128, TILE_H8x64, TILE_128x128, TILE_128x64, TILE_64x64,
+                                TILE_256x128};
+
+int pf_conv_candidates(const posfeat_conv_desc* d, int* tiles, int max) {
+  ConvArgs a;
+  float dummy[4] __attribute__((aligned(16)));
+  if (conv_prepare(d, dummy, dummy, nullptr, nullptr, dummy, a) != POSFEAT_OK) return 0;
+  int n = 0;
+  for (int t : kAllTiles)
+    if (plan_for_tile(a, t).kern >= 0 && n < max) tiles[n++] = t;
+  return n;
+}
+
+int pf_conv_run_tile(const posfeat_conv_desc* d, const float* x, const float* w,
+                     const float* bias, const float* res, float* y, void* ws, size_t ws_bytes,
+                     int tile, hipStream_t st) {
+  ConvArgs a;
+  PF_TRY(conv_prepare(d, x, w, bias, res, y, a));
+  const size_t need = posfeat_conv2d_workspace(d);
+  const bool split = need > 0 && ws && ws_bytes >= need;
+  const Plan p = conv_plan(a, split, tile);
+  if (p.ksplit > 1) a.part = static_cast<float*>(ws);
+  return conv_run(a, p, st);
+}
+
+static size_t stats_ws_for(const ConvArgs& a, const Plan& p, int n) {
+  if (p.ppi == 0 && a.hw < p.bm) return 0;
+  const size_t nchunk = (stats_tiles_per_img(a, p) + STAT_CHUNK - 1) / STAT_CHUNK;
+  return pf_align((size_t)p.tiles_m * 2 * a.Cout * 2 * sizeof(float), 256) +
+         (size_t)n * nchunk * a.Cout * 2 * sizeof(double);
+}
+
+size_t pf_conv_stats_ws_max(const posfeat_conv_desc* d) {
+  ConvArgs a;
+  float dummy[4] __attribute__((aligned(16)));
+  if (conv_prepare(d, dummy, dummy, nullptr, nullptr, dummy, a) != POSFEAT_OK) return 0;
+  size_t mx = 0;
+  for (int t : kAllTiles) {
+    const Plan p = plan_for_tile(a, t);
+    if (p.kern < 0) continue;
+    const size_t s = stats_ws_for(a, p, d->n);
+    if (s > mx) mx = s;
+  }
+  return mx;
+}
+
+int pf_conv_stats_run_tile(const posfeat_conv_desc* d, const float* x, const float* w,
+                           const float* bias, float* y, void* ws, size_t ws_bytes, float* mean,
+                           float* rstd, float eps, int tile, hipStream_t st) {
   ConvArgs a;
   PF_TRY(conv_prepare(d, x, w, bias, nullptr, y, a));
-  const size_t need = posfeat_conv2d_stats_workspace(d);
+  const Plan p = conv_plan(a, false, tile);
+  const size_t need = stats_ws_for(a, p, d->n);
   if (need == 0) return POSFEAT_E_UNSUPPORTED;
   if (!ws || ws_bytes < need || !mean || !rstd) return POSFEAT_E_WORKSPACE;
   a.stats = static_cast<float*>(ws);
-  hipStream_t st = pf_stream(stream);
-  const Plan p = conv_plan(a, false);
   PF_TRY(conv_run(a, p, st));
   const int nb = d->n;
   const int nchunk = (int)((stats_tiles_per_img(a, p) + STAT_CHUNK - 1) / STAT_CHUNK);
@@ -1374,7 +1469,7 @@ extern "C" int posfeat_conv2d_nhwc_stats(const posfeat_conv_desc* d, const float
                      a.stats, p.bm, p.ppi, a.hw, a.Cout, nchunk, chunks);
   PF_CHECK_LAUNCH();
   hipLaunchKernelGGL(conv_stats_finalize, dim3((nb * a.Cout + 255) / 256), dim3(256), 0, st,
-                     chunks, nchunk, a.hw, a.Cout, nb, eps, mean, rstd);
+                     chunks, nchunk, a.hw, a.Cout, nb, eps, mean, rstd, nullptr, 0);
   PF_CHECK_LAUNCH();
   return POSFEAT_OK;
 }

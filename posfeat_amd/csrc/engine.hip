@@ -14,7 +14,9 @@
 //   c1raw   [b][h/4][w/4][192] = conv1, then PReLU(IN(conv1)) in place (the
 //                                 low-res map head.conv2 reads per bilinear phase)
 //   g64     [b][h][w][64]      = IN(convimg)
+#include <cstdio>
 #include <cstring>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -103,6 +105,10 @@ struct posfeat_model {
   Buf st_mean1, st_rstd1;
   Buf splitk;                      // split-K partial slabs (max over layers)
   size_t splitk_need = 0;
+  // per-layer conv tile chosen by timing the legal candidates on the first
+  // forward of this shape (results do not depend on the tile)
+  std::map<std::string, int> tuned;
+  bool autotune = true;
   // timing
   bool timing = false;
   struct Ev {
@@ -148,6 +154,46 @@ int timed(Ctx& c, const std::string& label, double flops, F&& fn) {
   return r;
 }
 
+// Time each legal tile for this conv (1 warm-up + 3 timed launches on the
+// layer's real inputs) and return the fastest; -1 (default plan) if only one.
+template <class Run>
+int tune(const std::string& name, const posfeat_conv_desc& d, hipStream_t st, Run&& run) {
+  static const bool log = [] {
+    const char* e = getenv("POSFEAT_AUTOTUNE_LOG");
+    return e && e[0] == '1';
+  }();
+  int cand[8];
+  const int nc = pf_conv_candidates(&d, cand, 8);
+  if (nc <= 1) return -1;
+  hipEvent_t e0, e1;
+  if (hipEventCreate(&e0) != hipSuccess) return -1;
+  if (hipEventCreate(&e1) != hipSuccess) {
+    (void)hipEventDestroy(e0);
+    return -1;
+  }
+  int best = -1;
+  float best_ms = 1e30f;
+  for (int i = 0; i < nc; ++i) {
+    if (run(cand[i]) != POSFEAT_OK) continue;  // e.g. stats unsupported for this tile
+    if (hipEventRecord(e0, st) != hipSuccess) break;
+    bool ok = true;
+    for (int r = 0; r < 3 && ok; ++r) ok = run(cand[i]) == POSFEAT_OK;
+    float ms = 0.f;
+    if (!ok || hipEventRecord(e1, st) != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
+        hipEventElapsedTime(&ms, e0, e1) != hipSuccess)
+      continue;
+    if (log) fprintf(stderr, "[autotune] %-24s tile %2d  %8.4f ms\n", name.c_str(), cand[i], ms / 3);
+    if (ms < best_ms) {
+      best_ms = ms;
+      best = cand[i];
+    }
+  }
+  if (log) fprintf(stderr, "[autotune] %-24s -> tile %d\n", name.c_str(), best);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return best;
+}
+
 int conv(Ctx& c, const std::string& name, const float* x, int n, int h, int w, int xcs, float* y,
          int ycs, int stride, int act, const float* res = nullptr, int rcs = 0) {
   const Spec* s = specs().find(name);
@@ -175,9 +221,18 @@ int conv(Ctx& c, const std::string& name, const float* x, int n, int h, int w, i
   }
   float* part = c.f(c.m->splitk);
   const size_t have = c.m->splitk.floats * sizeof(float);
-  return timed(c, "conv:" + name, flops, [&] {
-    return posfeat_conv2d_nhwc_ws(&d, x, c.W(name), c.Bi(name), res, y, part, have, c.st);
-  });
+  auto run = [&](int tile) {
+    return pf_conv_run_tile(&d, x, c.W(name), c.Bi(name), res, y, part, have, tile, c.st);
+  };
+  int tile = -1;
+  auto it = c.m->tuned.find(name);
+  if (it != c.m->tuned.end()) {
+    tile = it->second;
+  } else if (c.m->autotune) {
+    tile = tune(name, d, c.st, run);
+    c.m->tuned[name] = tile;
+  }
+  return timed(c, "conv:" + name, flops, [&] { return run(tile); });
 }
 
 int forward(Ctx& c, const float* img, posfeat_extract_out* out);
@@ -202,7 +257,7 @@ int conv_in(Ctx& c, const std::string& name, const float* x, int n, int h, int w
   d.y_cstride = ycs;
   d.res_cstride = 0;
   d.act = POSFEAT_ACT_NONE;
-  const size_t need = posfeat_conv2d_stats_workspace(&d);
+  const size_t need = pf_conv_stats_ws_max(&d);
   if (need == 0 || c.dry) {
     if (c.dry) {
       if (need > c.m->splitk_need) c.m->splitk_need = need;
@@ -216,10 +271,19 @@ int conv_in(Ctx& c, const std::string& name, const float* x, int n, int h, int w
   const double flops = 2.0 * n * h * w * (double)s->cout * s->cin * s->kh * s->kw;
   float* part = c.f(c.m->splitk);
   const size_t have = c.m->splitk.floats * sizeof(float);
-  return timed(c, "conv:" + name, flops, [&] {
-    return posfeat_conv2d_nhwc_stats(&d, x, c.W(name), c.Bi(name), y, part, have, mean, rstd,
-                                     1e-5f, c.st);
-  });
+  auto run = [&](int tile) {
+    return pf_conv_stats_run_tile(&d, x, c.W(name), c.Bi(name), y, part, have, mean, rstd, 1e-5f,
+                                  tile, c.st);
+  };
+  int tile = -1;
+  auto it = c.m->tuned.find(name);
+  if (it != c.m->tuned.end()) {
+    tile = it->second;
+  } else if (c.m->autotune) {
+    tile = tune(name, d, c.st, run);
+    c.m->tuned[name] = tile;
+  }
+  return timed(c, "conv:" + name, flops, [&] { return run(tile); });
 }
 
 void plan(posfeat_model* m) {
@@ -252,6 +316,8 @@ void plan(posfeat_model* m) {
   {
     const char* e = getenv("POSFEAT_HEAD_UP4");  // 0: materialise the x4 upsample (A/B only)
     m->up4 = !(e && e[0] == '0');
+    const char* t = getenv("POSFEAT_AUTOTUNE");  // 0: heuristic tiles only
+    m->autotune = !(t && t[0] == '0');
   }
   if (m->up4) {
     alloc(m->g64, B * H * W * 64);

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 
+#include "../../include/posfeat_hip.h"
+
 int pf_nchw_to_nhwc(const float* x, int n, int c, int h, int w, int cso, float* y, hipStream_t st);
 int pf_nhwc_to_nchw(const float* x, int n, int c, int h, int w, int csi, float* y, hipStream_t st);
 int pf_maxpool3s2(const float* x, int n, int h, int w, int c, int csi, float* y, int cso,
@@ -29,3 +31,14 @@ int pf_up4_border(int n, int H, int W, const float* L, int lcs, const float* wph
                   int ycs, hipStream_t st);
 int pf_up4_main(int n, int H, int W, const float* L, int lcs, const float* wph, float* y, int ycs,
                 void* ws, size_t ws_bytes, float* mean, float* rstd, float eps, hipStream_t st);
+
+// conv tile control (conv.hip): legal tile ids for a shape, and runs with a
+// given tile (-1 = default).  All tiles of one shape give bit-identical results.
+int pf_conv_candidates(const posfeat_conv_desc* d, int* tiles, int max);
+int pf_conv_run_tile(const posfeat_conv_desc* d, const float* x, const float* w,
+                     const float* bias, const float* res, float* y, void* ws, size_t ws_bytes,
+                     int tile, hipStream_t st);
+size_t pf_conv_stats_ws_max(const posfeat_conv_desc* d);
+int pf_conv_stats_run_tile(const posfeat_conv_desc* d, const float* x, const float* w,
+                           const float* bias, float* y, void* ws, size_t ws_bytes, float* mean,
+                           float* rstd, float eps, int tile, hipStream_t st);
