@@ -105,32 +105,91 @@ __global__ void corr_row_kernel(const float* __restrict__ S, int nb, int n1, int
   }
 }
 
-// softmax_m(T*S[:][n]) expectations; one thread per column n (coalesced rows).
-__global__ void corr_col_kernel(const float* __restrict__ S, int nb, int n1, int n2, float T,
-                                const float* __restrict__ c1px, const float* __restrict__ c1n,
-                                int H1, int W1, float* __restrict__ g, float* __restrict__ sd) {
-  const int b = blockIdx.y;
-  const int col = blockIdx.x * blockDim.x + threadIdx.x;
-  if (col >= n2) return;
+// softmax_m(T*S[:][n]) expectations, two levels: block = 64 columns x one of
+// COL_CH row chunks with 4 row lanes per column (coalesced 256-B row reads),
+// online max-rescaled accumulation of (sum e, e*px, e*py, e*nx^2, e*ny^2);
+// then the chunk partials are merged in order (deterministic).
+constexpr int COL_CH = 8;
+struct ColAcc {
+  float mx, se, gx, gy, qx, qy;
+};
+
+__global__ __launch_bounds__(256) void corr_col_partial_kernel(
+    const float* __restrict__ S, int n1, int n2, float T, const float* __restrict__ c1px,
+    const float* __restrict__ c1n, ColAcc* __restrict__ part) {
+  const int b = blockIdx.z, ch = blockIdx.y, rg = threadIdx.x >> 6, cl = threadIdx.x & 63;
+  const int col = blockIdx.x * 64 + cl;
+  const int m0 = (int)((long long)n1 * ch / COL_CH), m1 = (int)((long long)n1 * (ch + 1) / COL_CH);
   const float* Sb = S + (long long)b * n1 * n2;
   const float* cp = c1px + (long long)b * n1 * 2;
   const float* cn = c1n + (long long)b * n1 * 2;
-  float mx = -INFINITY;
-  for (int m = 0; m < n1; ++m) mx = fmaxf(mx, T * Sb[(long long)m * n2 + col]);
+  ColAcc a{-INFINITY, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (col < n2) {
+    for (int m = m0 + rg; m < m1; m += 4) {
+      const float v = T * Sb[(long long)m * n2 + col];
+      const float px = cp[2 * m], py = cp[2 * m + 1], nx = cn[2 * m], ny = cn[2 * m + 1];
+      float e;
+      if (v > a.mx) {
+        const float f = expf(a.mx - v);
+        a.se *= f;
+        a.gx *= f;
+        a.gy *= f;
+        a.qx *= f;
+        a.qy *= f;
+        a.mx = v;
+        e = 1.f;
+      } else {
+        e = expf(v - a.mx);
+      }
+      a.se += e;
+      a.gx += e * px;
+      a.gy += e * py;
+      a.qx += e * nx * nx;
+      a.qy += e * ny * ny;
+    }
+  }
+  __shared__ ColAcc sh[4][64];
+  sh[rg][cl] = a;
+  __syncthreads();
+  if (rg == 0 && col < n2) {
+    float M = sh[0][cl].mx;
+    for (int r = 1; r < 4; ++r) M = fmaxf(M, sh[r][cl].mx);
+    ColAcc o{M, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < 4; ++r) {
+      const ColAcc& q = sh[r][cl];
+      const float f = expf(q.mx - M);
+      o.se += q.se * f;
+      o.gx += q.gx * f;
+      o.gy += q.gy * f;
+      o.qx += q.qx * f;
+      o.qy += q.qy * f;
+    }
+    part[((long long)b * COL_CH + ch) * n2 + col] = o;
+  }
+}
+
+__global__ void corr_col_final_kernel(const ColAcc* __restrict__ part, int nb, int n2, int H1,
+                                      int W1, float* __restrict__ g, float* __restrict__ sd) {
+  const long long o = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (o >= (long long)nb * n2) return;
+  const int b = (int)(o / n2), col = (int)(o - (long long)b * n2);
+  const ColAcc* p = part + (long long)b * COL_CH * n2 + col;
+  float M = -INFINITY;
+  for (int ch = 0; ch < COL_CH; ++ch) M = fmaxf(M, p[(long long)ch * n2].mx);
   float se = 0.f, gx = 0.f, gy = 0.f, qx = 0.f, qy = 0.f;
-  for (int m = 0; m < n1; ++m) {
-    const float e = expf(T * Sb[(long long)m * n2 + col] - mx);
-    se += e;
-    gx += e * cp[2 * m];
-    gy += e * cp[2 * m + 1];
-    qx += e * cn[2 * m] * cn[2 * m];
-    qy += e * cn[2 * m + 1] * cn[2 * m + 1];
+  for (int ch = 0; ch < COL_CH; ++ch) {
+    const ColAcc& q = p[(long long)ch * n2];
+    const float f = expf(q.mx - M);
+    se += q.se * f;
+    gx += q.gx * f;
+    gy += q.gy * f;
+    qx += q.qx * f;
+    qy += q.qy * f;
   }
   gx /= se;
   gy /= se;
   qx /= se;
   qy /= se;
-  const long long o = (long long)b * n2 + col;
   g[o * 2] = gx;
   g[o * 2 + 1] = gy;
   const float c0 = (float)((W1 - 1) / 2.0), c1 = (float)((H1 - 1) / 2.0);
@@ -435,6 +494,7 @@ extern "C" size_t posfeat_line2window_workspace(int b, int H1, int W1, int H2, i
   s += pf_align(b * n1 * n2 * 4, 256);              // S
   s += pf_align((size_t)b * (H1 / 4) * (W1 / 4) * 128 * 4, 256);  // fm1
   s += pf_align((size_t)b * (H2 / 4) * (W2 / 4) * 128 * 4, 256);  // fm2
+  s += pf_align((size_t)b * COL_CH * n2 * sizeof(ColAcc), 256);   // column partials
   return s;
 }
 
@@ -474,6 +534,7 @@ extern "C" int posfeat_line2window(const float* xf1, int cs1, const float* xf2, 
   float* S = take((size_t)b * n1 * n2 * 4);
   float* fm1 = take((size_t)b * h1 * w1 * 512);
   float* fm2 = take((size_t)b * h2 * w2 * 512);
+  ColAcc* colp = reinterpret_cast<ColAcc*>(take((size_t)b * COL_CH * n2 * sizeof(ColAcc)));
   // grid points
   hipLaunchKernelGGL(grid_points_kernel, dim3((b * n1 + 255) / 256), dim3(256), 0, st, sel1, b,
                      H1, W1, grid, c1n, c1p);
@@ -518,8 +579,10 @@ extern "C" int posfeat_line2window(const float* xf1, int cs1, const float* xf2, 
   }
   hipLaunchKernelGGL(corr_row_kernel, dim3((b * n1 + 3) / 4), dim3(256), 0, st, S, b, n1, n2,
                      temperature, c2p, c2n, H2, W2, out->g1, out->g1_std);
-  hipLaunchKernelGGL(corr_col_kernel, dim3((n2 + 255) / 256, b), dim3(256), 0, st, S, b, n1, n2,
-                     temperature, c1p, c1n, H1, W1, out->g2, out->g2_std);
+  hipLaunchKernelGGL(corr_col_partial_kernel, dim3((n2 + 63) / 64, COL_CH, b), dim3(256), 0, st,
+                     S, n1, n2, temperature, c1p, c1n, colp);
+  hipLaunchKernelGGL(corr_col_final_kernel, dim3((b * n2 + 255) / 256), dim3(256), 0, st, colp, b,
+                     n2, H1, W1, out->g2, out->g2_std);
   PF_CHECK_LAUNCH();
   // line search + window, both directions
   hipLaunchKernelGGL(line_window_kernel, dim3((b * n1 + 3) / 4), dim3(256), 0, st, c1p, F1, f1,

@@ -103,18 +103,56 @@ __global__ void row_lse_kernel(const float* __restrict__ S, long long rows, int 
   if (lane == 0) lse[wid] = mx + logf(s);
 }
 
-// lse_c[n] = logsumexp_m(T*S[m][n] - T); one thread per column
-__global__ void col_lse_kernel(const float* __restrict__ S, int n1, int n2, float T,
-                               float* __restrict__ lse) {
-  const int b = blockIdx.y;
-  const int col = blockIdx.x * blockDim.x + threadIdx.x;
-  if (col >= n2) return;
+// lse_c[n] = logsumexp_m(T*S[m][n] - T), two levels: block = 64 columns x
+// one of COL_CH row chunks, 4 row lanes per column (each wave reads 256
+// contiguous bytes of a row), online max-rescaled sums; then the chunk
+// partials of each column are merged in chunk order (deterministic).
+constexpr int COL_CH = 8;
+__global__ __launch_bounds__(256) void col_lse_partial_kernel(const float* __restrict__ S, int n1,
+                                                              int n2, float T,
+                                                              float2* __restrict__ part) {
+  const int b = blockIdx.z, ch = blockIdx.y, rg = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int m0 = (int)((long long)n1 * ch / COL_CH), m1 = (int)((long long)n1 * (ch + 1) / COL_CH);
   const float* Sb = S + (long long)b * n1 * n2;
-  float mx = -INFINITY;
-  for (int m = 0; m < n1; ++m) mx = fmaxf(mx, T * Sb[(long long)m * n2 + col] - T);
-  float s = 0.f;
-  for (int m = 0; m < n1; ++m) s += expf((T * Sb[(long long)m * n2 + col] - T) - mx);
-  lse[(long long)b * n2 + col] = mx + logf(s);
+  float mx = -INFINITY, sm = 0.f;
+  if (col < n2) {
+    for (int m = m0 + rg; m < m1; m += 4) {
+      const float v = T * Sb[(long long)m * n2 + col] - T;
+      if (v > mx) {
+        sm = sm * expf(mx - v) + 1.f;
+        mx = v;
+      } else {
+        sm += expf(v - mx);
+      }
+    }
+  }
+  __shared__ float smx[4][64], ssm[4][64];
+  smx[rg][threadIdx.x & 63] = mx;
+  ssm[rg][threadIdx.x & 63] = sm;
+  __syncthreads();
+  if (rg == 0 && col < n2) {
+    float M = smx[0][threadIdx.x];
+    for (int r = 1; r < 4; ++r) M = fmaxf(M, smx[r][threadIdx.x]);
+    float t = 0.f;
+    for (int r = 0; r < 4; ++r) t += ssm[r][threadIdx.x] * expf(smx[r][threadIdx.x] - M);
+    part[((long long)b * COL_CH + ch) * n2 + col] = make_float2(M, t);
+  }
+}
+
+__global__ void col_lse_final_kernel(const float2* __restrict__ part, int nb, int n2,
+                                     float* __restrict__ lse) {
+  const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (i >= (long long)nb * n2) return;
+  const int b = (int)(i / n2), col = (int)(i - (long long)b * n2);
+  float M = -INFINITY;
+  for (int ch = 0; ch < COL_CH; ++ch) M = fmaxf(M, part[((long long)b * COL_CH + ch) * n2 + col].x);
+  float t = 0.f;
+  for (int ch = 0; ch < COL_CH; ++ch) {
+    const float2 q = part[((long long)b * COL_CH + ch) * n2 + col];
+    t += q.y * expf(q.x - M);
+  }
+  lse[i] = M + logf(t);
 }
 
 // normalised epipolar line of each point: l = F x / max(|l[:2]|, 1e-8)
@@ -239,6 +277,7 @@ extern "C" size_t posfeat_disk_loss_workspace(int b, int H, int W) {
   s += 2 * pf_align(b * n * 4, 256);              // lse_r, lse_c
   s += 2 * pf_align(b * n * 3 * 4, 256);          // lines
   s += pf_align(b * ((n + 3) / 4) * 8, 256);      // partials
+  s += pf_align(b * COL_CH * n * 8, 256);         // column LSE chunk partials
   return s;
 }
 
@@ -281,6 +320,7 @@ extern "C" int posfeat_disk_loss(const float* kp1, const float* kp2, const float
   float* ln1 = static_cast<float*>(take((size_t)b * n * 12));
   float* ln2 = static_cast<float*>(take((size_t)b * n * 12));
   double* part = static_cast<double*>(take((size_t)b * ((n + 3) / 4) * 8));
+  float2* colp = static_cast<float2*>(take((size_t)b * COL_CH * n * 8));
   const unsigned pts_blocks = (unsigned)(((long long)b * n + 3) / 4);
   hipLaunchKernelGGL(disk_point_kernel, dim3(pts_blocks), dim3(256), 0, st, kp1, b, H, W, prop1,
                      acc1, sampled ? uni1 : nullptr, pr1, ac1, cpx1, cn1, lp1);
@@ -307,8 +347,10 @@ extern "C" int posfeat_disk_loss(const float* kp1, const float* kp2, const float
   }
   hipLaunchKernelGGL(row_lse_kernel, dim3(pts_blocks), dim3(256), 0, st, S, (long long)b * n, n,
                      temperature, lr);
-  hipLaunchKernelGGL(col_lse_kernel, dim3((n + 255) / 256, b), dim3(256), 0, st, S, n, n,
-                     temperature, lc);
+  hipLaunchKernelGGL(col_lse_partial_kernel, dim3((n + 63) / 64, COL_CH, b), dim3(256), 0, st, S,
+                     n, n, temperature, colp);
+  hipLaunchKernelGGL(col_lse_final_kernel, dim3((b * n + 255) / 256), dim3(256), 0, st, colp, b,
+                     n, lc);
   hipLaunchKernelGGL(epi_line_kernel, dim3((b * n + 255) / 256), dim3(256), 0, st, F1, cpx1, b, n,
                      ln1);
   hipLaunchKernelGGL(epi_line_kernel, dim3((b * n + 255) / 256), dim3(256), 0, st, F2, cpx2, b, n,
