@@ -1,3 +1,3 @@
 set -e
-POSFEAT_AUTOTUNE_LOG=1 timeout -k 10 300 python tools/layer_timing.py 8 480 640 > gpurun_out/lt_tune.log 2> gpurun_out/tune.log
-POSFEAT_AUTOTUNE=0 timeout -k 10 300 python tools/layer_timing.py 8 480 640 > gpurun_out/lt_notune.log 2>&1
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_corr -o c -- python3 tools/bench_correlation.py 8 5 > gpurun_out/prof_corr.log 2>&1
