@@ -45,6 +45,9 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--timing-steps", type=int, default=3)
+    p.add_argument("--workload", choices=("extract", "train_kp"), default="extract",
+                   help="extract: configs[1] (the metric); train_kp: configs[4], the keypoint-"
+                        "head training step (DiskLoss) with --batch pairs per GPU")
     return p.parse_args()
 
 
@@ -59,7 +62,7 @@ def setup_dist(args):
     return world, rank, local
 
 
-def build_engine(world, rank, dev):
+def build_engine(world, rank, dev, train=False):
     """Rank 0 packs the seeded weights; one RCCL broadcast ships the blob."""
     from posfeat_amd.engine import ExtractionEngine
     from posfeat_amd import _lib, weights
@@ -74,7 +77,7 @@ def build_engine(world, rank, dev):
     if world > 1:
         import torch.distributed as dist
         dist.broadcast(buf, src=0)
-    return ExtractionEngine(device=dev, blob=buf)
+    return ExtractionEngine(device=dev, blob=buf, train=train)
 
 
 def make_images(rank, batch, dev):
@@ -123,6 +126,8 @@ def main():
     world, rank, local = setup_dist(args)
     dev = torch.device("cuda", local if world > 1 else torch.cuda.current_device())
     torch.cuda.set_device(dev)
+    if args.workload == "train_kp":
+        return train_main(args, world, rank, dev)
     from posfeat_amd import ops
     engine = build_engine(world, rank, dev)
     ws = ops.DetectWorkspace()
@@ -216,6 +221,84 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+# ----------------------------------------------------------------------------
+# configs[4]: keypoint-head training step (configs/train_kp.yaml, DiskLoss)
+WGRAD2_FLOP_PER_IMAGE = 2.0 * 480 * 640 * 128 * 256 * 9   # head.conv2 weight gradient
+
+
+def train_main(args, world, rank, dev):
+    """One step = PoSFeat.forward over b pairs (2b images: backbone eval +
+    KeypointDet), DiskLoss forward + gradient, KeypointDet backward, RCCL
+    all-reduce of the 2.5 MB head gradient (world > 1), SGD update -- the
+    reference's managers/trainer.py:297-356 for configs/train_kp.yaml."""
+    import torch.distributed as dist
+    from posfeat_amd.correlation import synthetic_fundamental
+    from posfeat_amd.training import KeypointTrainStep
+    b = args.batch
+    engine = build_engine(world, rank, dev, train=True)
+    step = KeypointTrainStep(engine, lr=1e-3)
+    im1 = make_images(rank * 2 * b, b, dev)
+    im2 = make_images(rank * 2 * b + b, b, dev)
+    F1, F2 = [torch.from_numpy(f).to(dev) for f in synthetic_fundamental(b, H, W, 100 + rank)]
+    torch.manual_seed(1234 + rank)
+    for _ in range(args.warmup):
+        step.step(im1, im2, F1, F2, epoch=1)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out, _ = step.step(im1, im2, F1, F2, epoch=1)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    pairs = world * args.steps * b
+    # per-kernel timing of one extra step (HIP events on the engine's stream)
+    engine.set_timing(2 * b, H, W, True)
+    step.step(im1, im2, F1, F2, epoch=1)
+    wg_ms = engine.timing(2 * b, H, W, "bwdconv:head.conv2.wgrad")[0]
+    dg_ms = engine.timing(2 * b, H, W, "bwdconv:head.conv2.dgrad")[0]
+    bwd_ms, _, _ = engine.timing(2 * b, H, W, "bwd")
+    fwd_ms = engine.timing(2 * b, H, W, "conv:")[0]
+    all_ms = engine.timing(2 * b, H, W, "")[0]
+    engine.set_timing(2 * b, H, W, False)
+    wg_flops = WGRAD2_FLOP_PER_IMAGE * 2 * b
+    ach = wg_flops / (wg_ms * 1e-3) / 1e12
+    if rank == 0:
+        rec = {
+            "metric": "pairs/sec keypoint-head training step (640x480, DiskLoss, SGD)",
+            "value": round(pairs / el, 3), "unit": "pairs/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic (seeded 480x640 image pairs, synthetic fundamental matrices as "
+                    "datasets/megadepth.py:426-448 builds them; seeded random-init weights)",
+            "config": {"workload": "configs[4]: MegaDepth-style keypoint training step "
+                                   "(configs/train_kp.yaml: localheader only, DiskLoss grid 8, "
+                                   "SGD lr 1e-3), %d pairs per GPU" % b,
+                       "global_batch_pairs": b * world, "image": [H, W],
+                       "parallelism": "dp%d (RCCL all-reduce of head grads)" % world},
+            "roofline": {"kernel": "conv_wgrad_kernel<128,128> (head.conv2 weight gradient)",
+                         "bound": "mfma", "achieved": round(ach, 3),
+                         "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(ach / PEAK_FP32_MFMA_TFLOPS, 4), "traffic": None,
+                         "avg_launch_ms": round(wg_ms, 4), "flop_per_launch": wg_flops},
+            "breakdown_ms": {"forward_convs": round(fwd_ms, 3), "backward_all": round(bwd_ms, 3),
+                             "conv2_wgrad": round(wg_ms, 3), "conv2_dgrad": round(dg_ms, 3),
+                             "engine_all": round(all_ms, 3)},
+            "loss_last": float(out[0].item()),
+        }
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -207,6 +207,35 @@ int posfeat_disk_loss(const float *kp1, const float *kp2, const float *xf1, int 
                       float bad_reward, float kp_penalty, float *out, void *ws, size_t ws_bytes,
                       void *stream);
 
+/* DiskLoss forward + gradient w.r.t. both score maps (the backward of
+ * losses/kploss.py:132-197 with cor_detach=True, match_grad=False as in
+ * configs/train_kp.yaml:69-73: only the keypoint log-probabilities of
+ * point_distribution (20-35) carry gradient).  Same arguments as
+ * posfeat_disk_loss plus dkp1/dkp2 [b][H][W] (overwritten). */
+size_t posfeat_disk_loss_grad_workspace(int b, int H, int W);
+int posfeat_disk_loss_grad(const float *kp1, const float *kp2, const float *xf1, int cs1,
+                           const float *xf2, int cs2, int b, int H, int W, const float *F1,
+                           const float *F2, const int32_t *prop1, const int32_t *prop2,
+                           const uint8_t *acc1, const uint8_t *acc2, const float *uni1,
+                           const float *uni2, float temperature, float reward_thr,
+                           float good_reward, float bad_reward, float kp_penalty, float *out,
+                           float *dkp1, float *dkp2, void *ws, size_t ws_bytes, void *stream);
+
+/* Weight gradient of a stride-1 "same" conv (the autograd conv2d weight/bias
+ * backward behind managers/trainer.py:331): dw [cout][Kpad] in the packed K
+ * order of posfeat_conv2d_nhwc (so it lines up with the packed weights),
+ * db [cout] (may be NULL).  dy: NHWC [n][h][w] pitch dy_cstride; x: NHWC
+ * input pitch x_cstride; cin % 32 == 0 or cin == 4; cout % 32 == 0; odd
+ * square kernel.  Deterministic (pixel-split partials summed in order). */
+size_t posfeat_conv_wgrad_workspace(int n, int h, int w, int cin, int cout, int kh, int kw);
+int posfeat_conv_wgrad(const float *dy, int dy_cstride, const float *x, int x_cstride, int n,
+                       int h, int w, int cin, int cout, int kh, int kw, float *dw, float *db,
+                       void *ws, size_t ws_bytes, void *stream);
+
+/* torch.optim.SGD step without momentum/weight decay (train_kp.yaml:11-13,
+ * managers/trainer.py:118-119, 356): w -= lr * g over n floats. */
+int posfeat_sgd(float *w, const float *g, long long n, float lr, void *stream);
+
 /* ------------------------------------------------------------------------
  * Whole-model extraction engine.
  * Replaces: networks/PoSFeat_model.py:91-134 PoSFeat.extract for the
@@ -244,6 +273,24 @@ int posfeat_model_set_timing(posfeat_model *m, int enable);
 int posfeat_model_timing(posfeat_model *m, const char *prefix, double *ms, double *flops,
                          int *launches);
 void posfeat_model_destroy(posfeat_model *m);
+
+/* Keypoint-head training (config 5, configs/train_kp.yaml: optimal_modules
+ * ['localheader'], backbone frozen and detached, PoSFeat_model.py:97-102).
+ * A model made by posfeat_model_create_train keeps in its workspace what the
+ * backward needs (it materialises head.conv2's input instead of the phase
+ * path; results identical within fp32 rounding).
+ * posfeat_model_head_backward: given dL/d local_point [b][h][w] of the LAST
+ * extract() on the same workspace, writes dL/d(head parameters) into grad
+ * (posfeat_model_head_floats() floats, laid out exactly like the weight blob
+ * from float posfeat_model_head_offset() on: conv1, convimg, conv2, conv3,
+ * prelu).  Replaces the autograd backward of networks/DeteNet.py:102-121
+ * (managers/trainer.py:330-331). */
+int posfeat_model_create_train(int batch, int h, int w, const float *weights,
+                               posfeat_model **out);
+long long posfeat_model_head_offset(void);
+long long posfeat_model_head_floats(void);
+int posfeat_model_head_backward(posfeat_model *m, const float *dlocal_point, float *grad,
+                                void *ws, size_t ws_bytes, void *stream);
 
 #ifdef __cplusplus
 }

@@ -83,6 +83,20 @@ SIGNATURES = {
     "posfeat_disk_loss": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int,
                                   c_int, c_int] + [c_void_p] * 8 + [c_float] * 5 +
                           [c_void_p, c_void_p, c_size_t, c_void_p]),
+    "posfeat_disk_loss_grad_workspace": (c_size_t, [c_int, c_int, c_int]),
+    "posfeat_disk_loss_grad": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_int, c_int,
+                                       c_int, c_int] + [c_void_p] * 8 + [c_float] * 5 +
+                               [c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "posfeat_conv_wgrad_workspace": (c_size_t, [c_int] * 7),
+    "posfeat_conv_wgrad": (c_int, [c_void_p, c_int, c_void_p, c_int] + [c_int] * 7 +
+                           [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "posfeat_sgd": (c_int, [c_void_p, c_void_p, c_ll, c_float, c_void_p]),
+    "posfeat_model_create_train": (c_int, [c_int, c_int, c_int, c_void_p,
+                                           ctypes.POINTER(c_void_p)]),
+    "posfeat_model_head_offset": (c_ll, []),
+    "posfeat_model_head_floats": (c_ll, []),
+    "posfeat_model_head_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
+                                            c_void_p]),
     "posfeat_model_num_specs": (c_int, []),
     "posfeat_model_conv_spec": (c_int, [c_int, ctypes.POINTER(ctypes.c_char_p), P_int, P_int,
                                         P_int, P_int, ctypes.POINTER(c_ll),

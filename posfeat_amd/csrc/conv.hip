@@ -1229,8 +1229,8 @@ Plan conv_plan(const ConvArgs& a, bool allow_split, int forced = -1) {
       tile = TILE_256x128;
     else if (a.Cout > 64 && (t128 >= 512 || ks > 1))
       tile = TILE_128x128;
-    else if ((long long)((a.M + 127) / 128) * ((a.Cout + 63) / 64) >= 512)
-      tile = TILE_128x64;
+    else if (cin32 && (long long)((a.M + 127) / 128) * ((a.Cout + 63) / 64) >= 512)
+      tile = TILE_128x64;  // Cin = 4 layers (stem, convimg): 64x64 measured faster
     else
       tile = TILE_64x64;
     d = plan_for_tile(a, tile);

@@ -220,6 +220,110 @@ __global__ __launch_bounds__(RB) void reinforce_kernel(
   if (threadIdx.x == 0) part[(long long)b * gridDim.x + blockIdx.x] = red[0];
 }
 
+// ---------------------------------------------------------------- backward
+// With cor_detach (sample_p detached) and match_grad False the loss depends on
+// the score maps only through kps_logp (kploss.py:175-182):
+//   dL/dlogp1[m] = acc1[m] * (-sum_{n: acc2} reward p - kp_penalty), likewise for 2
+// and logp = log_softmax(cell)[prop] + log sigmoid(+/- logit[prop]) (20-35).
+struct PairCtx {
+  const float* S;
+  int n1, n2;
+  float T, thr, good, bad;
+  const float *lse_r, *lse_c, *line1, *line2, *c1px, *c2px;
+};
+
+// reward * p for accepted pair (m, n) of pair b: the same float expression as
+// reinforce_kernel
+__device__ __forceinline__ float pair_rp(const PairCtx& c, int b, int m, int nn) {
+  const long long gm = (long long)b * c.n1 + m, gn = (long long)b * c.n2 + nn;
+  const float aff = c.T * c.S[((long long)b * c.n1 + m) * c.n2 + nn] - c.T;
+  const float p = expf(aff - c.lse_r[gm]) * expf(aff - c.lse_c[gn]);
+  const float x1 = c.c1px[2 * gm], y1 = c.c1px[2 * gm + 1];
+  const float x2 = c.c2px[2 * gn], y2 = c.c2px[2 * gn + 1];
+  const float d1 = fabsf(c.line1[3 * gm] * x2 + c.line1[3 * gm + 1] * y2 + c.line1[3 * gm + 2]);
+  const float d2 = fabsf(c.line2[3 * gn] * x1 + c.line2[3 * gn + 1] * y1 + c.line2[3 * gn + 2]);
+  return ((d1 < c.thr && d2 < c.thr) ? c.good : c.bad) * p;
+}
+
+// g1[m] = dL/dlogp1[m]; one wave per row
+__global__ void grad_row_kernel(PairCtx c, int nb, const uint8_t* __restrict__ acc1,
+                                const uint8_t* __restrict__ acc2, float kp_penalty,
+                                float* __restrict__ g1) {
+  const int lane = threadIdx.x & 63;
+  const long long wid = blockIdx.x * (long long)(blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (wid >= (long long)nb * c.n1) return;
+  const int b = (int)(wid / c.n1), m = (int)(wid - (long long)b * c.n1);
+  if (!acc1[wid]) {
+    if (lane == 0) g1[wid] = 0.f;
+    return;
+  }
+  float s = 0.f;
+  for (int nn = lane; nn < c.n2; nn += 64)
+    if (acc2[(long long)b * c.n2 + nn]) s += pair_rp(c, b, m, nn);
+  s = pf_wave_sum(s);
+  if (lane == 0) g1[wid] = -s - kp_penalty;
+}
+
+// g2[n] = dL/dlogp2[n]: column sums in COL_CH row chunks (4 row lanes per
+// column), merged in chunk order
+__global__ __launch_bounds__(256) void grad_col_partial_kernel(PairCtx c,
+                                                               const uint8_t* __restrict__ acc1,
+                                                               const uint8_t* __restrict__ acc2,
+                                                               float* __restrict__ part) {
+  const int b = blockIdx.z, ch = blockIdx.y, rg = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int m0 = (int)((long long)c.n1 * ch / COL_CH), m1 = (int)((long long)c.n1 * (ch + 1) / COL_CH);
+  float s = 0.f;
+  if (col < c.n2 && acc2[(long long)b * c.n2 + col])
+    for (int m = m0 + rg; m < m1; m += 4)
+      if (acc1[(long long)b * c.n1 + m]) s += pair_rp(c, b, m, col);
+  __shared__ float ss[4][64];
+  ss[rg][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (rg == 0 && col < c.n2)
+    part[((long long)b * COL_CH + ch) * c.n2 + col] =
+        ((ss[0][threadIdx.x] + ss[1][threadIdx.x]) + ss[2][threadIdx.x]) + ss[3][threadIdx.x];
+}
+
+__global__ void grad_col_final_kernel(const float* __restrict__ part, int nb, int n2,
+                                      const uint8_t* __restrict__ acc2, float kp_penalty,
+                                      float* __restrict__ g2) {
+  const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (i >= (long long)nb * n2) return;
+  const int b = (int)(i / n2), col = (int)(i - (long long)b * n2);
+  float t = 0.f;
+  for (int ch = 0; ch < COL_CH; ++ch) t += part[((long long)b * COL_CH + ch) * n2 + col];
+  g2[i] = acc2[i] ? -t - kp_penalty : 0.f;
+}
+
+// dkp over one 8x8 cell (one wave): g * ([j == prop] (1 + d alogp/dl) - softmax_j),
+// d alogp/dl = accepted ? 1 - sigmoid(l) : -sigmoid(l)
+__global__ void disk_point_grad_kernel(const float* __restrict__ kp, int nb, int H, int W,
+                                       const int32_t* __restrict__ prop,
+                                       const uint8_t* __restrict__ acc,
+                                       const float* __restrict__ g, float* __restrict__ dkp) {
+  constexpr int G = 8;
+  const int lane = threadIdx.x & 63;
+  const int hc = H / G, wc = W / G, n = hc * wc;
+  const long long wid = blockIdx.x * (long long)(blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (wid >= (long long)nb * n) return;
+  const int b = (int)(wid / n), k = (int)(wid - (long long)b * n);
+  const int cy = k / wc, cx = k - cy * wc;
+  const long long pix = ((long long)b * H + cy * G + lane / G) * W + cx * G + lane % G;
+  const float v = kp[pix];
+  float mx = v;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  const float e = expf(v - mx);
+  const float sm = e / pf_wave_sum(e);
+  const int p = prop[wid];
+  const float lv = __shfl(v, p, 64);
+  const float sg = 1.f / (1.f + expf(-lv));
+  const float dacc = acc[wid] ? 1.f - sg : -sg;
+  const float gg = g[wid];
+  dkp[pix] = gg * ((lane == p ? 1.f + dacc : 0.f) - sm);
+}
+
 // out[0] = loss, out[1] = reinforce, out[2] = kp_penalty, out[3] = n_kps
 __global__ __launch_bounds__(1024) void disk_final_kernel(const double* __restrict__ part,
                                                           int nparts, const uint8_t* acc1,
@@ -281,18 +385,28 @@ extern "C" size_t posfeat_disk_loss_workspace(int b, int H, int W) {
   return s;
 }
 
-extern "C" int posfeat_disk_loss(const float* kp1, const float* kp2, const float* xf1, int cs1,
-                                 const float* xf2, int cs2, int b, int H, int W, const float* F1,
-                                 const float* F2, const int32_t* prop1, const int32_t* prop2,
-                                 const uint8_t* acc1, const uint8_t* acc2, const float* uni1,
-                                 const float* uni2, float temperature, float reward_thr,
-                                 float good_reward, float bad_reward, float kp_penalty,
-                                 float* out, void* ws, size_t ws_bytes, void* stream) {
+extern "C" size_t posfeat_disk_loss_grad_workspace(int b, int H, int W) {
+  if (b <= 0 || H % 8 || W % 8) return 0;
+  const size_t n = (size_t)(H / 8) * (W / 8);
+  return posfeat_disk_loss_workspace(b, H, W) + 2 * pf_align(b * n * 4, 256) +
+         pf_align(b * COL_CH * n * 4, 256);
+}
+
+static int disk_loss_impl(const float* kp1, const float* kp2, const float* xf1, int cs1,
+                          const float* xf2, int cs2, int b, int H, int W, const float* F1,
+                          const float* F2, const int32_t* prop1, const int32_t* prop2,
+                          const uint8_t* acc1, const uint8_t* acc2, const float* uni1,
+                          const float* uni2, float temperature, float reward_thr,
+                          float good_reward, float bad_reward, float kp_penalty, float* out,
+                          float* dkp1, float* dkp2, void* ws, size_t ws_bytes, void* stream) {
   if (!kp1 || !kp2 || !xf1 || !xf2 || !F1 || !F2 || !out || !ws) return POSFEAT_E_INVALID;
   if (b <= 0 || H % 8 || W % 8 || H % 4 || cs1 < 128 || cs2 < 128) return POSFEAT_E_INVALID;
   const bool sampled = uni1 && uni2;
+  const bool grad = dkp1 && dkp2;
   if (!sampled && !(prop1 && prop2 && acc1 && acc2)) return POSFEAT_E_INVALID;
-  if (ws_bytes < posfeat_disk_loss_workspace(b, H, W)) return POSFEAT_E_WORKSPACE;
+  if (ws_bytes < (grad ? posfeat_disk_loss_grad_workspace(b, H, W)
+                       : posfeat_disk_loss_workspace(b, H, W)))
+    return POSFEAT_E_WORKSPACE;
   const int n = (H / 8) * (W / 8);
   if (n % 4) return POSFEAT_E_UNSUPPORTED;
   hipStream_t st = pf_stream(stream);
@@ -364,5 +478,47 @@ extern "C" int posfeat_disk_loss(const float* kp1, const float* kp2, const float
   hipLaunchKernelGGL(disk_final_kernel, dim3(1), dim3(1024), 0, st, part, b * mblocks, ac1, ac2,
                      lp1, lp2, b, n, n, kp_penalty, out);
   PF_CHECK_LAUNCH();
+  if (!grad) return POSFEAT_OK;
+  float* g1 = static_cast<float*>(take((size_t)b * n * 4));
+  float* g2 = static_cast<float*>(take((size_t)b * n * 4));
+  float* gcp = static_cast<float*>(take((size_t)b * COL_CH * n * 4));
+  PairCtx pc{S, n, n, temperature, reward_thr, good_reward, bad_reward, lr, lc, ln1, ln2, cpx1, cpx2};
+  hipLaunchKernelGGL(grad_row_kernel, dim3(pts_blocks), dim3(256), 0, st, pc, b, ac1, ac2,
+                     kp_penalty, g1);
+  hipLaunchKernelGGL(grad_col_partial_kernel, dim3((n + 63) / 64, COL_CH, b), dim3(256), 0, st, pc,
+                     ac1, ac2, gcp);
+  hipLaunchKernelGGL(grad_col_final_kernel, dim3((b * n + 255) / 256), dim3(256), 0, st, gcp, b, n,
+                     ac2, kp_penalty, g2);
+  hipLaunchKernelGGL(disk_point_grad_kernel, dim3(pts_blocks), dim3(256), 0, st, kp1, b, H, W, pr1,
+                     ac1, g1, dkp1);
+  hipLaunchKernelGGL(disk_point_grad_kernel, dim3(pts_blocks), dim3(256), 0, st, kp2, b, H, W, pr2,
+                     ac2, g2, dkp2);
+  PF_CHECK_LAUNCH();
   return POSFEAT_OK;
+}
+
+extern "C" int posfeat_disk_loss(const float* kp1, const float* kp2, const float* xf1, int cs1,
+                                 const float* xf2, int cs2, int b, int H, int W, const float* F1,
+                                 const float* F2, const int32_t* prop1, const int32_t* prop2,
+                                 const uint8_t* acc1, const uint8_t* acc2, const float* uni1,
+                                 const float* uni2, float temperature, float reward_thr,
+                                 float good_reward, float bad_reward, float kp_penalty,
+                                 float* out, void* ws, size_t ws_bytes, void* stream) {
+  return disk_loss_impl(kp1, kp2, xf1, cs1, xf2, cs2, b, H, W, F1, F2, prop1, prop2, acc1, acc2,
+                        uni1, uni2, temperature, reward_thr, good_reward, bad_reward, kp_penalty,
+                        out, nullptr, nullptr, ws, ws_bytes, stream);
+}
+
+extern "C" int posfeat_disk_loss_grad(const float* kp1, const float* kp2, const float* xf1,
+                                      int cs1, const float* xf2, int cs2, int b, int H, int W,
+                                      const float* F1, const float* F2, const int32_t* prop1,
+                                      const int32_t* prop2, const uint8_t* acc1,
+                                      const uint8_t* acc2, const float* uni1, const float* uni2,
+                                      float temperature, float reward_thr, float good_reward,
+                                      float bad_reward, float kp_penalty, float* out, float* dkp1,
+                                      float* dkp2, void* ws, size_t ws_bytes, void* stream) {
+  if (!dkp1 || !dkp2) return POSFEAT_E_INVALID;
+  return disk_loss_impl(kp1, kp2, xf1, cs1, xf2, cs2, b, H, W, F1, F2, prop1, prop2, acc1, acc2,
+                        uni1, uni2, temperature, reward_thr, good_reward, bad_reward, kp_penalty,
+                        out, dkp1, dkp2, ws, ws_bytes, stream);
 }

@@ -14,6 +14,7 @@
 //   c1raw   [b][h/4][w/4][192] = conv1, then PReLU(IN(conv1)) in place (the
 //                                 low-res map head.conv2 reads per bilinear phase)
 //   g64     [b][h][w][64]      = IN(convimg)
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -22,6 +23,7 @@
 
 #include "common.h"
 #include "fmap.h"
+#include "train.h"
 
 int pf_sample_desc(const float* fmap, int b, int c, int h, int w, int cs, const float* coord,
                    int npts, const int32_t* n_valid, int normalize, float* out, hipStream_t st);
@@ -101,6 +103,10 @@ struct posfeat_model {
   Buf c1raw, hcat, c2raw, yraw;
   Buf g64, wph, up4ws;             // phase-decomposed head.conv2 (conv.hip conv_up4_kernel)
   bool up4 = true;
+  // keypoint-head training (config 5): forward keeps what the backward reads
+  // (raw conv1 output, the materialised conv2 input `hcat`, per-layer IN stats)
+  bool train = false;
+  Buf dy3, dc2, dhcat, upt, dc1, wt2, wgws, inbws, tailws;
   Buf st_mean, st_rstd, st_part;  // instance-norm scratch (floats / doubles)
   Buf st_mean1, st_rstd1;
   Buf splitk;                      // split-K partial slabs (max over layers)
@@ -271,19 +277,32 @@ int conv_in(Ctx& c, const std::string& name, const float* x, int n, int h, int w
   const double flops = 2.0 * n * h * w * (double)s->cout * s->cin * s->kh * s->kw;
   float* part = c.f(c.m->splitk);
   const size_t have = c.m->splitk.floats * sizeof(float);
-  auto run = [&](int tile) {
+  // No autotuning here: the fused statistics are per-tile partial sums, so a
+  // different tile would change mean/rstd in the last bits and make results
+  // depend on a timing race.  The default plan is the tuned winner for these
+  // layers anyway (profiles/r01/autotune_choices_b8_480x640.txt).
+  return timed(c, "conv:" + name, flops, [&] {
     return pf_conv_stats_run_tile(&d, x, c.W(name), c.Bi(name), y, part, have, mean, rstd, 1e-5f,
-                                  tile, c.st);
-  };
-  int tile = -1;
-  auto it = c.m->tuned.find(name);
-  if (it != c.m->tuned.end()) {
-    tile = it->second;
-  } else if (c.m->autotune) {
-    tile = tune(name, d, c.st, run);
-    c.m->tuned[name] = tile;
-  }
-  return timed(c, "conv:" + name, flops, [&] { return run(tile); });
+                                  -1, c.st);
+  });
+}
+
+// input-gradient conv of head.conv2: d(conv2 out) (128 ch) -> d(cat) (256 ch)
+posfeat_conv_desc dgrad_desc(const posfeat_model* m) {
+  posfeat_conv_desc d;
+  d.n = m->B;
+  d.h = m->H;
+  d.w = m->W;
+  d.cin = 128;
+  d.x_cstride = 128;
+  d.cout = 256;
+  d.kh = d.kw = 3;
+  d.stride = 1;
+  d.pad = 1;
+  d.y_cstride = 256;
+  d.res_cstride = 0;
+  d.act = POSFEAT_ACT_NONE;
+  return d;
 }
 
 void plan(posfeat_model* m) {
@@ -319,6 +338,7 @@ void plan(posfeat_model* m) {
     const char* t = getenv("POSFEAT_AUTOTUNE");  // 0: heuristic tiles only
     m->autotune = !(t && t[0] == '0');
   }
+  if (m->train) m->up4 = false;  // the backward reads the materialised conv2 input
   if (m->up4) {
     alloc(m->g64, B * H * W * 64);
     alloc(m->wph, posfeat_conv2_up4_weights_floats());
@@ -328,8 +348,25 @@ void plan(posfeat_model* m) {
   }
   alloc(m->c2raw, B * H * W * 128);
   alloc(m->yraw, B * H * W);
-  alloc(m->st_mean, B * 256);
-  alloc(m->st_rstd, B * 256);
+  // instance-norm statistics, one slot of B*256 per layer: conv1, convimg, conv2
+  alloc(m->st_mean, B * 256 * 3);
+  alloc(m->st_rstd, B * 256 * 3);
+  if (m->train) {
+    alloc(m->dy3, B * H * W);
+    alloc(m->dc2, B * H * W * 128);
+    alloc(m->dhcat, B * H * W * 256);
+    alloc(m->upt, B * H * w4 * 192);
+    alloc(m->dc1, B * h4 * w4 * 192);
+    alloc(m->wt2, (size_t)256 * posfeat_conv_packed_k(128, 3, 3));
+    size_t wg = pf_conv_wgrad_ws_bytes((int)B, (int)H, (int)W, 256, 128, 3, 3);
+    wg = std::max(wg, pf_conv_wgrad_ws_bytes((int)B, (int)H, (int)W, 4, 64, 3, 3));
+    wg = std::max(wg, pf_conv_wgrad_ws_bytes((int)B, (int)h4, (int)w4, 192, 192, 3, 3));
+    alloc(m->wgws, wg / 4 + 4);
+    const size_t ib = std::max(pf_in_bwd_ws_bytes((int)B, (int)(H * W), 64),
+                               pf_in_bwd_ws_bytes((int)B, (int)(h4 * w4), 192));
+    alloc(m->inbws, ib / 4 + 4);
+    alloc(m->tailws, pf_tail_bwd_ws_bytes((int)B, (int)(H * W)) / 4 + 4);
+  }
   alloc(m->st_mean1, B * 4);
   alloc(m->st_rstd1, B * 4);
   const size_t part = pf_in_stats_ws_bytes((int)B, (int)(H * W), 256);
@@ -341,6 +378,10 @@ void plan(posfeat_model* m) {
     posfeat_extract_out o{};
     o.local_point = reinterpret_cast<float*>(16);
     forward(c, reinterpret_cast<const float*>(16), &o);
+  }
+  if (m->train) {
+    const posfeat_conv_desc d = dgrad_desc(m);
+    m->splitk_need = std::max(m->splitk_need, posfeat_conv2d_workspace(&d));
   }
   alloc(m->splitk, m->splitk_need / 4 + 4);
   m->ws_bytes = cur;
@@ -423,21 +464,27 @@ int forward(Ctx& c, const float* img, posfeat_extract_out* out) {
   PF_TRY(conv(c, "iconv2", cat2, B, h4, w4, 512, c.f(m->d2), 256, 1, POSFEAT_ACT_ELU));
   PF_TRY(conv(c, "conv_fine", c.f(m->d2), B, h4, w4, 256, headcat, 192, 1, POSFEAT_ACT_ELU));
   // ---- KeypointDet (DeteNet.py:102-121), identity prior == exact 1.0 -------
-  float* mean = c.f(m->st_mean);
-  float* rstd = c.f(m->st_rstd);
+  // IN statistics slots: conv1, convimg, conv2 (the backward reads all three)
+  const size_t SL = (size_t)B * 256;
+  float* mean = c.f(m->st_mean) + 2 * SL;
+  float* rstd = c.f(m->st_rstd) + 2 * SL;
+  float* mean1 = c.f(m->st_mean);
+  float* rstd1 = c.f(m->st_rstd);
+  float* meanI = c.f(m->st_mean) + SL;
+  float* rstdI = c.f(m->st_rstd) + SL;
   double* part = c.d(m->st_part);
   float* c1 = c.f(m->c1raw);
   float* c2 = c.f(m->c2raw);
-  PF_TRY(conv_in(c, "head.conv1", headcat, B, h4, w4, 192, c1, 192, mean, rstd));
+  PF_TRY(conv_in(c, "head.conv1", headcat, B, h4, w4, 192, c1, 192, mean1, rstd1));
   if (m->up4) {
     // L = PReLU(IN(conv1)) stays at 1/4 resolution; conv2 reads it per phase
     PF_TRY(timed(c, "norm_prelu", 0, [&] {
-      return pf_in_apply(c1, B, h4 * w4, 192, 192, mean, rstd, slope, c.st);
+      return pf_in_apply(c1, B, h4 * w4, 192, 192, mean1, rstd1, slope, c.st);
     }));
     float* g64 = c.f(m->g64);
-    PF_TRY(conv_in(c, "head.convimg", img4, B, H, W, 4, g64, 64, mean, rstd));
+    PF_TRY(conv_in(c, "head.convimg", img4, B, H, W, 4, g64, 64, meanI, rstdI));
     PF_TRY(timed(c, "instnorm_apply", 0, [&] {
-      return pf_in_apply(g64, B, H * W, 64, 64, mean, rstd, nullptr, c.st);
+      return pf_in_apply(g64, B, H * W, 64, 64, meanI, rstdI, nullptr, c.st);
     }));
     // executed MFMA work: 64 full-res channels x 9 taps, 192 low-res channels
     // x 6.25 taps on average over the 16 phases (the reference layer: 256 x 9)
@@ -458,12 +505,12 @@ int forward(Ctx& c, const float* img, posfeat_extract_out* out) {
   } else {
     float* hcat = c.f(m->hcat);
     PF_TRY(timed(c, "norm_prelu_up4", 0, [&] {
-      return pf_norm_prelu_upsample(c1, B, h4, w4, 192, 192, mean, rstd, slope, H, W, hcat, 256,
+      return pf_norm_prelu_upsample(c1, B, h4, w4, 192, 192, mean1, rstd1, slope, H, W, hcat, 256,
                                     c.st);
     }));
-    PF_TRY(conv_in(c, "head.convimg", img4, B, H, W, 4, hcat + 192, 256, mean, rstd));
+    PF_TRY(conv_in(c, "head.convimg", img4, B, H, W, 4, hcat + 192, 256, meanI, rstdI));
     PF_TRY(timed(c, "instnorm_apply", 0, [&] {
-      return pf_in_apply(hcat + 192, B, H * W, 64, 256, mean, rstd, nullptr, c.st);
+      return pf_in_apply(hcat + 192, B, H * W, 64, 256, meanI, rstdI, nullptr, c.st);
     }));
     PF_TRY(conv_in(c, "head.conv2", hcat, B, H, W, 256, c2, 128, mean, rstd));
   }
@@ -488,7 +535,119 @@ int forward(Ctx& c, const float* img, posfeat_extract_out* out) {
   return POSFEAT_OK;
 }
 
+const Spec& spec(const char* n) { return *specs().find(n); }
+long long head_offset() { return spec("head.conv1").w_off; }
+
+// KeypointDet backward (networks/DeteNet.py:102-121 under autograd, as
+// managers/trainer.py:331 runs it for configs/train_kp.yaml): given dL/d
+// local_point of the last forward on this workspace, writes dL/d(every head
+// parameter) into `grad`, laid out like the weight blob from head.conv1 on.
+int head_backward(Ctx& c, const float* dlp, float* grad) {
+  posfeat_model* m = c.m;
+  const int B = m->B, H = m->H, W = m->W, h4 = H / 4, w4 = W / 4;
+  const long long hoff = head_offset();
+  auto G = [&](const char* n) { return grad + (spec(n).w_off - hoff); };
+  auto GB = [&](const char* n) { return grad + (spec(n).b_off - hoff); };
+  const float* slope = m->wts + spec("head.prelu").b_off;
+  const size_t SL = (size_t)B * 256;
+  const float* mean1 = c.f(m->st_mean);
+  const float* rstd1 = c.f(m->st_rstd);
+  const float* mean2 = c.f(m->st_mean) + 2 * SL;
+  const float* rstd2 = c.f(m->st_rstd) + 2 * SL;
+  float* hcat = c.f(m->hcat);
+  float* dhcat = c.f(m->dhcat);
+  float* dc1 = c.f(m->dc1);
+  float* dc2 = c.f(m->dc2);
+  const size_t wgb = m->wgws.floats * sizeof(float);
+  PF_TRY(timed(c, "bwd:zero", 0, [&] {
+    return hipMemsetAsync(grad, 0, (specs().total - hoff) * sizeof(float), c.st) == hipSuccess
+               ? POSFEAT_OK
+               : POSFEAT_E_HIP;
+  }));
+  // Softplus / norm3 / conv3 / PReLU / norm2  ->  d(conv2 out)
+  double* t2s = nullptr;
+  int t2n = 0;
+  PF_TRY(timed(c, "bwd:tail", 0, [&] {
+    return pf_tail_backward(dlp, c.f(m->yraw), c.f(m->st_mean1), c.f(m->st_rstd1), c.f(m->c2raw),
+                            128, mean2, rstd2, slope, c.W("head.conv3"), B, H * W, c.f(m->dy3),
+                            dc2, 128, G("head.conv3"), c.f(m->tailws), &t2s, &t2n, c.st);
+  }));
+  // conv2: weight gradient over the materialised cat[up4(L), IN(convimg)]
+  PF_TRY(timed(c, "bwdconv:head.conv2.wgrad", 2.0 * B * H * W * 128.0 * 256 * 9, [&] {
+    return pf_conv_wgrad(dc2, 128, hcat, 256, B, H, W, 256, 128, 3, 3, G("head.conv2"),
+                         GB("head.conv2"), c.f(m->wgws), wgb, c.st);
+  }));
+  // conv2: input gradient = conv of dc2 with the flipped, transposed kernel
+  PF_TRY(timed(c, "bwd:dgrad_weights", 0, [&] {
+    return pf_dgrad_weights(c.W("head.conv2"), 128, 256, 3, 3, c.f(m->wt2), c.st);
+  }));
+  {
+    const posfeat_conv_desc d = dgrad_desc(m);
+    PF_TRY(timed(c, "bwdconv:head.conv2.dgrad", 2.0 * B * H * W * 128.0 * 256 * 9, [&] {
+      return posfeat_conv2d_nhwc_ws(&d, dc2, c.f(m->wt2), nullptr, nullptr, dhcat,
+                                    c.f(m->splitk), m->splitk.floats * sizeof(float), c.st);
+    }));
+  }
+  // image branch: normimg backward in place on channels 192..255, then convimg dW
+  PF_TRY(timed(c, "bwd:in_img", 0, [&] {
+    return pf_in_backward(hcat + 192, 256, dhcat + 192, 256, B, H * W, 64, nullptr,
+                          c.f(m->st_rstd) + SL, nullptr, dhcat + 192, 256, c.f(m->inbws), nullptr,
+                          nullptr, c.st);
+  }));
+  PF_TRY(timed(c, "bwdconv:head.convimg.wgrad", 2.0 * B * H * W * 64.0 * 3 * 9, [&] {
+    return pf_conv_wgrad(dhcat + 192, 256, c.f(m->img4), 4, B, H, W, 4, 64, 3, 3,
+                         G("head.convimg"), GB("head.convimg"), c.f(m->wgws), wgb, c.st);
+  }));
+  // x4 upsample adjoint of the 192 upsampled channels -> d PReLU(IN(conv1))
+  PF_TRY(timed(c, "bwd:up4_adjoint", 0, [&] {
+    return pf_up4_adjoint(dhcat, 256, B, H, W, h4, w4, 192, c.f(m->upt), dc1, 192, c.st);
+  }));
+  double* c1s = nullptr;
+  int c1n = 0;
+  PF_TRY(timed(c, "bwd:in_conv1", 0, [&] {
+    return pf_in_backward(c.f(m->c1raw), 192, dc1, 192, B, h4 * w4, 192, mean1, rstd1, slope, dc1,
+                          192, c.f(m->inbws), &c1s, &c1n, c.st);
+  }));
+  PF_TRY(timed(c, "bwdconv:head.conv1.wgrad", 2.0 * B * h4 * w4 * 192.0 * 192 * 9, [&] {
+    return pf_conv_wgrad(dc1, 192, c.f(m->headcat), 192, B, h4, w4, 192, 192, 3, 3,
+                         G("head.conv1"), GB("head.conv1"), c.f(m->wgws), wgb, c.st);
+  }));
+  PF_TRY(timed(c, "bwd:scalars", 0, [&] {
+    return pf_head_scalars(t2s, t2n, c1s, c1n, GB("head.conv3"), GB("head.prelu"), c.st);
+  }));
+  return POSFEAT_OK;
+}
+
 }  // namespace
+
+extern "C" long long posfeat_model_head_offset(void) { return head_offset(); }
+extern "C" long long posfeat_model_head_floats(void) { return specs().total - head_offset(); }
+
+extern "C" int posfeat_model_create_train(int batch, int h, int w, const float* weights,
+                                          posfeat_model** out) {
+  if (!out || !weights || batch <= 0 || h < 16 || w < 16 || h % 16 || w % 16)
+    return POSFEAT_E_INVALID;
+  posfeat_model* m = new (std::nothrow) posfeat_model();
+  if (!m) return POSFEAT_E_INVALID;
+  m->B = batch;
+  m->H = h;
+  m->W = w;
+  m->wts = weights;
+  m->train = true;
+  plan(m);
+  *out = m;
+  return POSFEAT_OK;
+}
+
+extern "C" int posfeat_model_head_backward(posfeat_model* m, const float* dlocal_point,
+                                           float* grad, void* ws, size_t ws_bytes, void* stream) {
+  if (!m || !dlocal_point || !grad || !ws) return POSFEAT_E_INVALID;
+  if (!m->train) return POSFEAT_E_UNSUPPORTED;
+  if (ws_bytes < m->ws_bytes) return POSFEAT_E_WORKSPACE;
+  if (reinterpret_cast<uintptr_t>(ws) & 255) return POSFEAT_E_INVALID;
+  Ctx c{m, static_cast<char*>(ws), pf_stream(stream)};
+  return head_backward(c, dlocal_point, grad);
+}
 
 extern "C" int posfeat_model_num_specs(void) { return (int)specs().v.size(); }
 

@@ -1,0 +1,34 @@
+// train.h -- internal (non-ABI) launchers of the keypoint-head backward (train.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+
+#include "../../include/posfeat_hip.h"
+
+// dW [Cout][Kpad] (engine-packed K order) and db [Cout] of a stride-1 "same"
+// conv: dw = sum_p dy[p] (x) im2col(x)[p].  Cin % 32 == 0 or Cin == 4.
+size_t pf_conv_wgrad_ws_bytes(int n, int H, int W, int Cin, int Cout, int KH, int KW);
+int pf_conv_wgrad(const float* dy, int ldy, const float* x, int xcs, int n, int H, int W, int Cin,
+                  int Cout, int KH, int KW, float* dw, float* db, void* ws, size_t ws_bytes,
+                  hipStream_t st);
+// packed weights of the input-gradient conv (flipped taps, cin <-> cout)
+int pf_dgrad_weights(const float* w, int Cout, int Cin, int KH, int KW, float* wt, hipStream_t st);
+// adjoint of the bilinear (align_corners=False) resize h x w -> OH x OW over C
+// channels: g [nb][OH][OW] (pitch gcs) -> d [nb][h][w] (pitch dcs); t: nb*OH*w*C floats
+int pf_up4_adjoint(const float* g, int gcs, int nb, int OH, int OW, int h, int w, int C, float* t,
+                   float* d, int dcs, hipStream_t st);
+// InstanceNorm (+ optional PReLU) backward: x is the raw conv output (PReLU
+// mode, with mean/rstd) or the normalised map (identity mode, slope == NULL,
+// mean unused); rstd is always required (dx = rstd (dx^ - E - x^ E'))
+size_t pf_in_bwd_ws_bytes(int nb, int hw, int C);
+int pf_in_backward(const float* x, int xcs, const float* g, int gcs, int nb, int hw, int C,
+                   const float* mean, const float* rstd, const float* slope, float* dx, int dxcs,
+                   void* ws, double** slope_part, int* slope_nparts, hipStream_t st);
+// Softplus(IN(conv3(PReLU(IN(conv2))))) backward to d(conv2 output)
+size_t pf_tail_bwd_ws_bytes(int nb, int hw);
+int pf_tail_backward(const float* dlp, const float* y3, const float* m3, const float* r3,
+                     const float* c2, int c2cs, const float* m2, const float* r2,
+                     const float* slope, const float* w3, int nb, int hw, float* dy3, float* dc2,
+                     int dcs, float* dw3, void* ws, double** t2s, int* t2n, hipStream_t st);
+int pf_head_scalars(const double* t2s, int n2, const double* c1s, int n1, float* db3,
+                    float* dslope, hipStream_t st);

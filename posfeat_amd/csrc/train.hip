@@ -1,0 +1,843 @@
+// train.hip -- backward kernels of the keypoint-head training step on gfx950.
+//
+// Config 5 of BASELINE.json (configs/train_kp.yaml): only `localheader`
+// (KeypointDet, networks/DeteNet.py:9-121) is optimised (train_kp.yaml:11-13,
+// SGD lr 1e-3); the backbone output is detached (PoSFeat_model.py:97-102) and
+// the loss is DiskLoss (losses/kploss.py:132-197).  The reference gets these
+// gradients from autograd over ATen (managers/trainer.py:330-331); here each
+// adjoint is an explicit gfx950 kernel:
+//
+//   conv_wgrad_kernel     dW[co][k] = sum_p dy[p][co] * im2col(x)[p][k]  (FP32 MFMA,
+//                         K in the engine's packed order so dW lands in the
+//                         weight blob's layout; pixel-split partials summed in a
+//                         fixed order -> deterministic), + db[co] = sum_p dy
+//   dgrad_weights_kernel  W'[ci][(co/32, kh', kw', co%32)] = W[co][flip][ci]: the
+//                         input gradient is then an ordinary forward conv
+//                         (conv.hip) of dy with W'
+//   up4_adj_x/y_kernel    adjoint of F.interpolate(x4, bilinear,
+//                         align_corners=False) (DeteNet.py:109), separable gather
+//   in_bwd_*              InstanceNorm2d (affine=False, biased var) backward,
+//                         optionally through the shared PReLU (DeteNet.py:108,112)
+//   tail_bwd_*            Softplus(IN(conv3(PReLU(IN(conv2))))) backward
+//                         (DeteNet.py:112-113) down to d(conv2 output)
+//   sgd_kernel            torch.optim.SGD step (no momentum / weight decay)
+#include <algorithm>
+
+#include "common.h"
+#include "fmap.h"
+#include "train.h"
+
+namespace {
+
+constexpr int WG_RB = 32;  // pixels per reduction chunk
+
+struct WgradArgs {
+  const float* dy;
+  int ldy;
+  const float* x;
+  int xcs;
+  int H, W, Cin, KH, KW, pad;
+  int Cout, Kpad, K, M;
+  int tiles_n, ntiles, nsplit, nchunks;
+  float* part;   // [nsplit][Cout][Kpad]
+  float* partb;  // [nsplit][Cout] or nullptr
+};
+
+__device__ __attribute__((aligned(16))) float pf_wg_zero16[4];
+
+// One 256-thread workgroup computes a BM x BN tile of dW over one pixel range.
+// Per 32-pixel chunk both operands are DMA'd (global_load_lds_dwordx4) into LDS
+// rows [pixel][channel]: A = dy rows (couts), B = the im2col rows (packed k).
+// The MFMA reduction index is the pixel: lane l feeds A[co = l%32][px = l/32]
+// and B[px = l/32][k = l%32] with ds_read_b32 (32 consecutive dwords per lane
+// group: conflict-free).  Two LDS stages: chunk c+1 is in flight while chunk c
+// is multiplied.
+template <int BM, int BN>
+__global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
+  constexpr int WN = 2;
+  constexpr int TM = BM / 2, TN = BN / WN;
+  constexpr int MI = TM / 32, NI = TN / 32;
+  constexpr int A_G = BM / 32, B_G = BN / 32;  // DMA wave-instructions per chunk per wave
+  static_assert(MI >= 1 && NI >= 1, "tile");
+  __shared__ __attribute__((aligned(16))) float smem[2 * WG_RB * (BM + BN)];
+  float* As = smem;                    // [2][32][BM]
+  float* Bs = smem + 2 * WG_RB * BM;   // [2][32][BN]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  int bid = blockIdx.x;
+  {  // XCD-aware bijective remap: consecutive logical ids share an XCD's L2, so
+     // the tiles of one pixel range (same dy rows, same input pixels) do too
+    const int nwg = gridDim.x, q = nwg >> 3, r = nwg & 7, xcd = bid & 7, slot = bid >> 3;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+  }
+  const int split = bid / a.ntiles, tile = bid - split * a.ntiles;
+  const int tm = tile / a.tiles_n, tn = tile - tm * a.tiles_n;
+  const int co0 = tm * BM, n0 = tn * BN;
+  const int c_begin = (int)((long long)a.nchunks * split / a.nsplit);
+  const int c_end = (int)((long long)a.nchunks * (split + 1) / a.nsplit);
+
+  // ---- per-lane DMA roles (fixed across chunks) ----------------------------
+  // A: instruction i of this wave covers stage bytes [(wave*A_G+i)*1024, +1024)
+  int a_row[A_G], a_col[A_G];
+#pragma unroll
+  for (int i = 0; i < A_G; ++i) {
+    const int e = ((wave * A_G + i) * 1024 + lane * 16) / 4;  // float index in the stage
+    a_row[i] = e / BM;
+    a_col[i] = e - a_row[i] * BM;
+  }
+  // B: row (pixel in chunk), k column -> (kh-pad, kw-pad, ci)
+  int b_row[B_G], b_dy[B_G], b_dx[B_G], b_ci[B_G];
+  bool b_kok[B_G];
+  const int ntap = a.KH * a.KW;
+#pragma unroll
+  for (int i = 0; i < B_G; ++i) {
+    const int e = ((wave * B_G + i) * 1024 + lane * 16) / 4;
+    b_row[i] = e / BN;
+    const int k = n0 + (e - b_row[i] * BN);
+    int tap, ci;
+    bool ok;
+    if ((a.Cin & 31) == 0) {
+      const int c = k >> 5, slab = c / ntap;
+      tap = c - slab * ntap;
+      ci = slab * 32 + (k & 31);
+      ok = k < a.Kpad;
+    } else {  // Cin == 4: K = (kh, kw, cin4), zero-padded to Kpad
+      tap = k >> 2;
+      ci = 0;
+      ok = k < a.K;
+    }
+    b_kok[i] = ok;
+    b_dy[i] = ok ? tap / a.KW - a.pad : 0;
+    b_dx[i] = ok ? tap - (tap / a.KW) * a.KW - a.pad : 0;
+    b_ci[i] = ci;
+  }
+  const int HW = a.H * a.W;
+  auto issue = [&](int chunk, int buf) {
+    const int m0 = chunk * WG_RB;
+#pragma unroll
+    for (int i = 0; i < A_G; ++i) {
+      const int m = m0 + a_row[i], co = co0 + a_col[i];
+      const float* src = (m < a.M && co < a.Cout) ? a.dy + (long long)m * a.ldy + co : pf_wg_zero16;
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)src,
+          (__attribute__((address_space(3))) void*)(As + buf * WG_RB * BM + (wave * A_G + i) * 256),
+          16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < B_G; ++i) {
+      const int m = m0 + b_row[i];
+      const float* src = pf_wg_zero16;
+      if (b_kok[i] && m < a.M) {
+        const int img = m / HW, rem = m - img * HW;
+        const int oh = rem / a.W, ow = rem - oh * a.W;
+        const int ih = oh + b_dy[i], iw = ow + b_dx[i];
+        if ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
+          src = a.x + ((long long)img * HW + (long long)ih * a.W + iw) * a.xcs + b_ci[i];
+      }
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)src,
+          (__attribute__((address_space(3))) void*)(Bs + buf * WG_RB * BN + (wave * B_G + i) * 256),
+          16, 0, 0);
+    }
+  };
+
+  f32x16 acc[MI][NI];
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
+  float bsum[MI];
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi) bsum[mi] = 0.f;
+  const bool do_bias = a.partb && tn == 0 && wn == 0;
+
+  if (c_begin < c_end) {
+    issue(c_begin, 0);
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+  }
+  const int acol = wm * TM + (lane & 31), bcol = wn * TN + (lane & 31), rsel = lane >> 5;
+  for (int c = c_begin; c < c_end; ++c) {
+    const int cur = (c - c_begin) & 1;
+    if (c + 1 < c_end) issue(c + 1, cur ^ 1);
+    const float* Ab = As + cur * WG_RB * BM + rsel * BM + acol;
+    const float* Bb = Bs + cur * WG_RB * BN + rsel * BN + bcol;
+#pragma unroll
+    for (int kk = 0; kk < WG_RB / 2; ++kk) {
+      float av[MI], bv[NI];
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi) av[mi] = Ab[2 * kk * BM + mi * 32];
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) bv[ni] = Bb[2 * kk * BN + ni * 32];
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[mi], bv[ni], acc[mi][ni], 0, 0, 0);
+      if (do_bias) {
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi) bsum[mi] += av[mi];
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+  }
+
+  // ---- raw partials: row (cout) = (r&3) + 8(r>>2) + 4(lane>>5), col = lane&31
+  float* pp = a.part + (long long)split * a.Cout * a.Kpad;
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) {
+      const int k = n0 + wn * TN + ni * 32 + (lane & 31);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int co = co0 + wm * TM + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (co < a.Cout && k < a.Kpad) pp[(long long)co * a.Kpad + k] = acc[mi][ni][r];
+      }
+    }
+  if (do_bias) {
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi) {
+      const float s = bsum[mi] + __shfl_xor(bsum[mi], 32, 64);
+      const int co = co0 + wm * TM + mi * 32 + (lane & 31);
+      if (lane < 32 && co < a.Cout) a.partb[(long long)split * a.Cout + co] = s;
+    }
+  }
+}
+
+// dw[co][k] = sum_s part[s][co][k] (split order: deterministic); db likewise
+__global__ void wgrad_reduce_kernel(const float* __restrict__ part, const float* __restrict__ partb,
+                                    int nsplit, int Cout, int Kpad, float* __restrict__ dw,
+                                    float* __restrict__ db) {
+  const long long n = (long long)Cout * Kpad;
+  const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (i < n) {
+    float s = 0.f;
+    for (int k = 0; k < nsplit; ++k) s += part[(long long)k * n + i];
+    dw[i] = s;
+  }
+  if (db && i < Cout) {
+    float s = 0.f;
+    for (int k = 0; k < nsplit; ++k) s += partb[(long long)k * Cout + i];
+    db[i] = s;
+  }
+}
+
+// W'[ci][k'] with k' = ((co/32)*ntap + tap')*32 + co%32, tap' = ntap-1-tap:
+// the spatially flipped, channel-transposed kernel (stride 1, same padding)
+__global__ void dgrad_weights_kernel(const float* __restrict__ w, int Cout, int Cin, int ntap,
+                                     int kpad_f, float* __restrict__ wt, int kpad_t) {
+  const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (i >= (long long)Cin * kpad_t) return;
+  const int ci = (int)(i / kpad_t), kp = (int)(i - (long long)ci * kpad_t);
+  const int c = kp >> 5, slab = c / ntap, tapp = c - slab * ntap, co = slab * 32 + (kp & 31);
+  float v = 0.f;
+  if (co < Cout) {
+    const int tap = ntap - 1 - tapp;
+    v = w[(long long)co * kpad_f + ((ci >> 5) * ntap + tap) * 32 + (ci & 31)];
+  }
+  wt[i] = v;
+}
+
+// ---------------------------------------------------------------- x4 upsample adjoint
+// forward (fmap.hip norm_prelu_upsample_kernel / ATen upsample_bilinear2d,
+// align_corners=False): src = s*(o+0.5)-0.5 clamped at 0, i0 = floor, i1 =
+// i0 + (i0 < n-1), weights (1-l, l).  Weight of output o on input q:
+__device__ __forceinline__ float up_w(int o, int q, float s, int n) {
+  float f = s * (o + 0.5f) - 0.5f;
+  f = f < 0.f ? 0.f : f;
+  const int i0 = (int)f;
+  const int i1 = i0 + (i0 < n - 1 ? 1 : 0);
+  const float l = f - i0;
+  return (i0 == q ? 1.f - l : 0.f) + (i1 == q ? l : 0.f);
+}
+
+// t[b][oy][qx][c] = sum_ox w(ox, qx) g[b][oy][ox][c]   (c < C, quads)
+__global__ void up4_adj_x_kernel(const float* __restrict__ g, int gcs, int nb, int OH, int OW,
+                                 int w, int c4n, float* __restrict__ t) {
+  const float s = (float)w / (float)OW;
+  const long long total = (long long)nb * OH * w * c4n;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int q = (int)(i % c4n);
+    long long p = i / c4n;
+    const int qx = (int)(p % w);
+    const long long row = p / w;  // b*OH + oy
+    const float* gr = g + row * OW * gcs + q * 4;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    const int o0 = max(0, 4 * qx - 4), o1 = min(OW - 1, 4 * qx + 5);
+    for (int ox = o0; ox <= o1; ++ox) {
+      const float wt = up_w(ox, qx, s, w);
+      if (wt != 0.f) acc += wt * *reinterpret_cast<const f32x4*>(gr + (long long)ox * gcs);
+    }
+    *reinterpret_cast<f32x4*>(t + p * (c4n * 4) + q * 4) = acc;
+  }
+}
+
+// d[b][qy][qx][c] = sum_oy w(oy, qy) t[b][oy][qx][c]
+__global__ void up4_adj_y_kernel(const float* __restrict__ t, int nb, int OH, int h, int w,
+                                 int c4n, float* __restrict__ d, int dcs) {
+  const float s = (float)h / (float)OH;
+  const long long total = (long long)nb * h * w * c4n;
+  const int C = c4n * 4;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int q = (int)(i % c4n);
+    long long p = i / c4n;
+    const int qx = (int)(p % w);
+    p /= w;
+    const int qy = (int)(p % h);
+    const int b = (int)(p / h);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    const int o0 = max(0, 4 * qy - 4), o1 = min(OH - 1, 4 * qy + 5);
+    for (int oy = o0; oy <= o1; ++oy) {
+      const float wt = up_w(oy, qy, s, h);
+      if (wt != 0.f)
+        acc += wt * *reinterpret_cast<const f32x4*>(t + (((long long)b * OH + oy) * w + qx) * C + q * 4);
+    }
+    *reinterpret_cast<f32x4*>(d + (((long long)b * h + qy) * w + qx) * dcs + q * 4) = acc;
+  }
+}
+
+// ---------------------------------------------------------------- instance-norm backward
+// For x^ = (x - mean) * rstd and upstream g = dL/d(act(x^)) with act = PReLU
+// (slope a) or identity:  dx^ = act'(x^) g,  dx = rstd (dx^ - E[dx^] - x^ E[dx^ x^]).
+// Partials per (image, pixel chunk): sum dx^, sum dx^ x^ per channel (fp64) and,
+// for PReLU, sum x^<=0 ? x^ g : 0 (the slope gradient, torch prelu backward).
+constexpr int INB_CHUNK = 2048;
+
+template <bool PRELU>
+__device__ __forceinline__ void inb_load(const float* xr, const float* gr, f32x4 m, f32x4 r,
+                                         float a, f32x4& xh, f32x4& dxh, f32x4& sg) {
+  const f32x4 xv = *reinterpret_cast<const f32x4*>(xr);
+  const f32x4 gv = *reinterpret_cast<const f32x4*>(gr);
+  if (PRELU) {
+    xh = (xv - m) * r;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const bool pos = xh[k] > 0.f;
+      dxh[k] = pos ? gv[k] : a * gv[k];
+      sg[k] = pos ? 0.f : xh[k] * gv[k];
+    }
+  } else {
+    xh = xv;  // already normalised
+    dxh = gv;
+    sg = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+}
+
+template <bool PRELU>
+__global__ __launch_bounds__(256) void in_bwd_partial_kernel(
+    const float* __restrict__ x, int xcs, const float* __restrict__ g, int gcs, int hw, int C,
+    const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ slope,
+    double* __restrict__ part, double* __restrict__ spart) {
+  const int b = blockIdx.y, chunk = blockIdx.x, nchunk = gridDim.x;
+  const int c4n = C / 4, tid = threadIdx.x;
+  const int rows = blockDim.x / c4n;
+  const int q = tid % c4n, pl = tid / c4n;
+  const float a = PRELU ? *slope : 0.f;
+  f32x4 s1 = {0, 0, 0, 0}, s2 = {0, 0, 0, 0}, s3 = {0, 0, 0, 0};
+  if (pl < rows) {
+    f32x4 m = {0, 0, 0, 0}, r = {1, 1, 1, 1};
+    if (PRELU) {
+      m = *reinterpret_cast<const f32x4*>(mean + b * C + q * 4);
+      r = *reinterpret_cast<const f32x4*>(rstd + b * C + q * 4);
+    }
+    const int p0 = chunk * INB_CHUNK, p1 = min(hw, p0 + INB_CHUNK);
+    for (int p = p0 + pl; p < p1; p += rows) {
+      const long long pix = (long long)b * hw + p;
+      f32x4 xh, dxh, sg;
+      inb_load<PRELU>(x + pix * xcs + q * 4, g + pix * gcs + q * 4, m, r, a, xh, dxh, sg);
+      s1 += dxh;
+      s2 += dxh * xh;
+      s3 += sg;
+    }
+  }
+  __shared__ double red[256 * 9];
+  for (int k = 0; k < 4; ++k) {
+    red[tid * 9 + k] = s1[k];
+    red[tid * 9 + 4 + k] = s2[k];
+  }
+  red[tid * 9 + 8] = (double)s3[0] + s3[1] + s3[2] + s3[3];
+  __syncthreads();
+  if (tid < c4n) {
+    double t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int rr = 0; rr < rows; ++rr)
+      for (int k = 0; k < 8; ++k) t[k] += red[(rr * c4n + tid) * 9 + k];
+    double* o = part + ((long long)b * nchunk + chunk) * C * 2;
+    for (int k = 0; k < 4; ++k) {
+      o[(tid * 4 + k) * 2] = t[k];
+      o[(tid * 4 + k) * 2 + 1] = t[4 + k];
+    }
+  }
+  if (PRELU && tid == 0) {
+    double t = 0;
+    for (int k = 0; k < rows * c4n; ++k) t += red[k * 9 + 8];
+    spart[(long long)b * nchunk + chunk] = t;
+  }
+}
+
+// E[dx^], E[dx^ x^] per (image, channel)
+__global__ void in_bwd_finalize_kernel(const double* __restrict__ part, int nchunk, int nb, int C,
+                                       int hw, float* __restrict__ e1, float* __restrict__ e2) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nb * C) return;
+  const int b = i / C, c = i - b * C;
+  double s1 = 0, s2 = 0;
+  const double* p = part + (long long)b * nchunk * C * 2;
+  for (int k = 0; k < nchunk; ++k) {
+    s1 += p[(k * C + c) * 2];
+    s2 += p[(k * C + c) * 2 + 1];
+  }
+  e1[i] = (float)(s1 / hw);
+  e2[i] = (float)(s2 / hw);
+}
+
+template <bool PRELU>
+__global__ void in_bwd_apply_kernel(const float* __restrict__ x, int xcs, const float* g, int gcs,
+                                    int nb, int hw, int c4n, const float* __restrict__ mean,
+                                    const float* __restrict__ rstd,
+                                    const float* __restrict__ slope, const float* __restrict__ e1,
+                                    const float* __restrict__ e2, float* dx, int dxcs) {
+  const long long total = (long long)nb * hw * c4n;
+  const int C = c4n * 4;
+  const float a = PRELU ? *slope : 0.f;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int q = (int)(i % c4n);
+    const long long pix = i / c4n;
+    const int b = (int)(pix / hw);
+    // identity mode: x is already normalised (mean is NULL); rstd still scales dx
+    const f32x4 m = PRELU ? *reinterpret_cast<const f32x4*>(mean + b * C + q * 4)
+                          : f32x4{0.f, 0.f, 0.f, 0.f};
+    const f32x4 r = *reinterpret_cast<const f32x4*>(rstd + b * C + q * 4);
+    f32x4 xh, dxh, sg;
+    inb_load<PRELU>(x + pix * xcs + q * 4, g + pix * gcs + q * 4, m, r, a, xh, dxh, sg);
+    const f32x4 m1 = *reinterpret_cast<const f32x4*>(e1 + b * C + q * 4);
+    const f32x4 m2 = *reinterpret_cast<const f32x4*>(e2 + b * C + q * 4);
+    *reinterpret_cast<f32x4*>(dx + pix * dxcs + q * 4) = r * (dxh - m1 - xh * m2);
+  }
+}
+
+// ---------------------------------------------------------------- head tail backward
+// local_point = softplus(z^), z^ = (y3 - m3) r3, y3 = conv3(a2) + b3, a2 = PReLU(x2^),
+// x2^ = (c2 - m2) r2  (DeteNet.py:112-113; Softplus beta 1 threshold 20)
+// tail1: per image sums of dz and dz z^ (dz = dLP * softplus'(z^))
+__device__ __forceinline__ float softplus_grad(float z) {
+  // torch softplus_backward: z > threshold ? 1 : exp(z) / (exp(z) + 1)
+  if (z > 20.f) return 1.f;
+  const float e = expf(z);
+  return e / (e + 1.f);
+}
+
+__global__ __launch_bounds__(256) void tail1_partial_kernel(const float* __restrict__ dlp,
+                                                            const float* __restrict__ y3, int hw,
+                                                            const float* __restrict__ m3,
+                                                            const float* __restrict__ r3,
+                                                            double* __restrict__ part) {
+  const int b = blockIdx.y, chunk = blockIdx.x, nchunk = gridDim.x;
+  const float m = m3[b], r = r3[b];
+  float s1 = 0.f, s2 = 0.f;
+  const int p0 = chunk * INB_CHUNK, p1 = min(hw, p0 + INB_CHUNK);
+  for (int p = p0 + threadIdx.x; p < p1; p += blockDim.x) {
+    const long long i = (long long)b * hw + p;
+    const float z = (y3[i] - m) * r;
+    const float dz = dlp[i] * softplus_grad(z);
+    s1 += dz;
+    s2 += dz * z;
+  }
+  __shared__ double r1[256], r2[256];
+  r1[threadIdx.x] = s1;
+  r2[threadIdx.x] = s2;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      r1[threadIdx.x] += r1[threadIdx.x + o];
+      r2[threadIdx.x] += r2[threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    part[((long long)b * nchunk + chunk) * 2] = r1[0];
+    part[((long long)b * nchunk + chunk) * 2 + 1] = r2[0];
+  }
+}
+
+// tail2: dy3 per pixel (stored), then per channel of conv2's output the partial
+// sums sum dx2^, sum dx2^ x2^ (norm2 backward), sum dy3 a2 (dW3), and per block
+// sum dy3 (db3) and the PReLU slope term.  Block = 32 channel quads x 8 pixel
+// lanes over one chunk of one image.
+__global__ __launch_bounds__(256) void tail2_partial_kernel(
+    const float* __restrict__ dlp, const float* __restrict__ y3, const float* __restrict__ c2,
+    int c2cs, int hw, const float* __restrict__ m3, const float* __restrict__ r3,
+    const double* __restrict__ t1part, int t1chunks, const float* __restrict__ m2,
+    const float* __restrict__ r2, const float* __restrict__ slope, const float* __restrict__ w3,
+    float* __restrict__ dy3, double* __restrict__ part, double* __restrict__ spart) {
+  const int b = blockIdx.y, chunk = blockIdx.x, nchunk = gridDim.x;
+  const int tid = threadIdx.x, q = tid & 31, pl = tid >> 5;
+  __shared__ float sh_e[2];
+  if (tid == 0) {
+    double s1 = 0, s2 = 0;
+    for (int k = 0; k < t1chunks; ++k) {
+      s1 += t1part[((long long)b * t1chunks + k) * 2];
+      s2 += t1part[((long long)b * t1chunks + k) * 2 + 1];
+    }
+    sh_e[0] = (float)(s1 / hw);
+    sh_e[1] = (float)(s2 / hw);
+  }
+  __syncthreads();
+  const float e1 = sh_e[0], e2 = sh_e[1];
+  const float mz = m3[b], rz = r3[b], a = *slope;
+  const f32x4 m = *reinterpret_cast<const f32x4*>(m2 + b * 128 + q * 4);
+  const f32x4 r = *reinterpret_cast<const f32x4*>(r2 + b * 128 + q * 4);
+  const f32x4 wv = *reinterpret_cast<const f32x4*>(w3 + q * 4);
+  f32x4 s1 = {0, 0, 0, 0}, s2 = {0, 0, 0, 0}, s3 = {0, 0, 0, 0};
+  float sb = 0.f, ss = 0.f;
+  const int p0 = chunk * INB_CHUNK, p1 = min(hw, p0 + INB_CHUNK);
+  for (int p = p0 + pl; p < p1; p += 8) {
+    const long long i = (long long)b * hw + p;
+    const float z = (y3[i] - mz) * rz;
+    const float dz = dlp[i] * softplus_grad(z);
+    const float d3 = rz * (dz - e1 - z * e2);
+    if (q == 0) {
+      dy3[i] = d3;
+      sb += d3;
+    }
+    const f32x4 xh = (*reinterpret_cast<const f32x4*>(c2 + i * c2cs + q * 4) - m) * r;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const bool pos = xh[k] > 0.f;
+      const float a2 = pos ? xh[k] : a * xh[k];
+      const float da2 = d3 * wv[k];
+      const float dxh = pos ? da2 : a * da2;
+      s1[k] += dxh;
+      s2[k] += dxh * xh[k];
+      s3[k] += d3 * a2;
+      ss += pos ? 0.f : xh[k] * da2;
+    }
+  }
+  __shared__ double red[256 * 12];
+  for (int k = 0; k < 4; ++k) {
+    red[tid * 12 + k] = s1[k];
+    red[tid * 12 + 4 + k] = s2[k];
+    red[tid * 12 + 8 + k] = s3[k];
+  }
+  __syncthreads();
+  if (tid < 32) {
+    double t[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int rr = 0; rr < 8; ++rr)
+      for (int k = 0; k < 12; ++k) t[k] += red[(rr * 32 + tid) * 12 + k];
+    double* o = part + ((long long)b * nchunk + chunk) * 128 * 3;
+    for (int k = 0; k < 4; ++k) {
+      o[(tid * 4 + k) * 3] = t[k];
+      o[(tid * 4 + k) * 3 + 1] = t[4 + k];
+      o[(tid * 4 + k) * 3 + 2] = t[8 + k];
+    }
+  }
+  __syncthreads();
+  red[tid * 2] = sb;
+  red[tid * 2 + 1] = ss;
+  __syncthreads();
+  if (tid == 0) {
+    double tb = 0, ts = 0;
+    for (int k = 0; k < 256; ++k) {
+      tb += red[k * 2];
+      ts += red[k * 2 + 1];
+    }
+    spart[((long long)b * nchunk + chunk) * 2] = tb;
+    spart[((long long)b * nchunk + chunk) * 2 + 1] = ts;
+  }
+}
+
+// per (image, channel): E[dx2^], E[dx2^ x2^]; summed over images: dW3[c]
+__global__ void tail2_finalize_kernel(const double* __restrict__ part, int nchunk, int nb, int hw,
+                                      float* __restrict__ e1, float* __restrict__ e2,
+                                      float* __restrict__ dw3) {
+  const int c = threadIdx.x;  // 128 threads
+  double w = 0;
+  for (int b = 0; b < nb; ++b) {
+    double s1 = 0, s2 = 0;
+    const double* p = part + (long long)b * nchunk * 128 * 3;
+    for (int k = 0; k < nchunk; ++k) {
+      s1 += p[(k * 128 + c) * 3];
+      s2 += p[(k * 128 + c) * 3 + 1];
+      w += p[(k * 128 + c) * 3 + 2];
+    }
+    e1[b * 128 + c] = (float)(s1 / hw);
+    e2[b * 128 + c] = (float)(s2 / hw);
+  }
+  dw3[c] = (float)w;
+}
+
+// dc2 = r2 (dx2^ - E[dx2^] - x2^ E[dx2^ x2^]), dx2^ recomputed from dy3
+__global__ void tail3_kernel(const float* __restrict__ dy3, const float* __restrict__ c2, int c2cs,
+                             int nb, int hw, const float* __restrict__ m2,
+                             const float* __restrict__ r2, const float* __restrict__ slope,
+                             const float* __restrict__ w3, const float* __restrict__ e1,
+                             const float* __restrict__ e2, float* __restrict__ dc2, int dcs) {
+  const long long total = (long long)nb * hw * 32;
+  const float a = *slope;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int q = (int)(i & 31);
+    const long long pix = i >> 5;
+    const int b = (int)(pix / hw);
+    const f32x4 m = *reinterpret_cast<const f32x4*>(m2 + b * 128 + q * 4);
+    const f32x4 r = *reinterpret_cast<const f32x4*>(r2 + b * 128 + q * 4);
+    const f32x4 wv = *reinterpret_cast<const f32x4*>(w3 + q * 4);
+    const f32x4 xh = (*reinterpret_cast<const f32x4*>(c2 + pix * c2cs + q * 4) - m) * r;
+    const float d3 = dy3[pix];
+    f32x4 dxh;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float da2 = d3 * wv[k];
+      dxh[k] = xh[k] > 0.f ? da2 : a * da2;
+    }
+    const f32x4 me1 = *reinterpret_cast<const f32x4*>(e1 + b * 128 + q * 4);
+    const f32x4 me2 = *reinterpret_cast<const f32x4*>(e2 + b * 128 + q * 4);
+    *reinterpret_cast<f32x4*>(dc2 + pix * dcs + q * 4) = r * (dxh - me1 - xh * me2);
+  }
+}
+
+// small scalars of the head gradient, fixed order:
+//   db3 = sum dy3;  dslope = sum(tail slope terms) + sum(conv1-path slope terms)
+__global__ void head_scalars_kernel(const double* __restrict__ t2s, int n2,
+                                    const double* __restrict__ c1s, int n1,
+                                    float* __restrict__ db3, float* __restrict__ dslope) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double b = 0, s = 0;
+  for (int i = 0; i < n2; ++i) {
+    b += t2s[2 * i];
+    s += t2s[2 * i + 1];
+  }
+  for (int i = 0; i < n1; ++i) s += c1s[i];
+  *db3 = (float)b;
+  *dslope = (float)s;
+}
+
+__global__ void sgd_kernel(float* __restrict__ w, const float* __restrict__ g, long long n,
+                           float lr) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x)
+    w[i] -= lr * g[i];
+}
+
+inline int grid_for(long long total, int block) {
+  long long g = (total + block - 1) / block;
+  if (g > 65536) g = 65536;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+struct WgPlan {
+  int BM, BN, tiles_m, tiles_n, nsplit, nchunks, Kpad, K;
+};
+
+WgPlan wgrad_plan(int n, int H, int W, int Cin, int Cout, int KH, int KW) {
+  WgPlan p;
+  p.Kpad = posfeat_conv_packed_k(Cin, KH, KW);
+  p.K = KH * KW * Cin;
+  p.BM = (Cout % 128 == 0) ? 128 : 64;
+  p.BN = (p.Kpad % 128 == 0) ? 128 : 64;
+  p.tiles_m = (Cout + p.BM - 1) / p.BM;
+  p.tiles_n = (p.Kpad + p.BN - 1) / p.BN;
+  const long long M = (long long)n * H * W;
+  p.nchunks = (int)((M + WG_RB - 1) / WG_RB);
+  const int ntiles = p.tiles_m * p.tiles_n;
+  int s = (2048 + ntiles - 1) / ntiles;          // ~8 waves of 256 CUs
+  const int maxs = std::max(1, p.nchunks / 8);   // >= 8 chunks per workgroup
+  p.nsplit = std::max(1, std::min(s, maxs));
+  return p;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ launchers
+size_t pf_conv_wgrad_ws_bytes(int n, int H, int W, int Cin, int Cout, int KH, int KW) {
+  const WgPlan p = wgrad_plan(n, H, W, Cin, Cout, KH, KW);
+  return pf_align((size_t)p.nsplit * Cout * p.Kpad * 4, 256) + pf_align((size_t)p.nsplit * Cout * 4, 256);
+}
+
+int pf_conv_wgrad(const float* dy, int ldy, const float* x, int xcs, int n, int H, int W, int Cin,
+                  int Cout, int KH, int KW, float* dw, float* db, void* ws, size_t ws_bytes,
+                  hipStream_t st) {
+  if ((Cin % 32 != 0 && Cin != 4) || Cout % 32 || ldy % 4 || xcs % 4 || KH != KW || KH % 2 == 0)
+    return POSFEAT_E_INVALID;
+  if (reinterpret_cast<uintptr_t>(dy) % 16 || reinterpret_cast<uintptr_t>(x) % 16)
+    return POSFEAT_E_INVALID;
+  if (ws_bytes < pf_conv_wgrad_ws_bytes(n, H, W, Cin, Cout, KH, KW)) return POSFEAT_E_WORKSPACE;
+  const WgPlan p = wgrad_plan(n, H, W, Cin, Cout, KH, KW);
+  WgradArgs a;
+  a.dy = dy;
+  a.ldy = ldy;
+  a.x = x;
+  a.xcs = xcs;
+  a.H = H;
+  a.W = W;
+  a.Cin = Cin;
+  a.KH = KH;
+  a.KW = KW;
+  a.pad = (KH - 1) / 2;
+  a.Cout = Cout;
+  a.Kpad = p.Kpad;
+  a.K = p.K;
+  a.M = n * H * W;
+  a.tiles_n = p.tiles_n;
+  a.ntiles = p.tiles_m * p.tiles_n;
+  a.nsplit = p.nsplit;
+  a.nchunks = p.nchunks;
+  a.part = static_cast<float*>(ws);
+  a.partb = db ? reinterpret_cast<float*>(static_cast<char*>(ws) +
+                                          pf_align((size_t)p.nsplit * Cout * p.Kpad * 4, 256))
+               : nullptr;
+  const dim3 grid(a.ntiles * a.nsplit);
+  if (p.BM == 128 && p.BN == 128)
+    hipLaunchKernelGGL((conv_wgrad_kernel<128, 128>), grid, dim3(256), 0, st, a);
+  else if (p.BM == 128)
+    hipLaunchKernelGGL((conv_wgrad_kernel<128, 64>), grid, dim3(256), 0, st, a);
+  else if (p.BN == 128)
+    hipLaunchKernelGGL((conv_wgrad_kernel<64, 128>), grid, dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((conv_wgrad_kernel<64, 64>), grid, dim3(256), 0, st, a);
+  PF_CHECK_LAUNCH();
+  const long long ne = (long long)Cout * p.Kpad;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, st,
+                     a.part, a.partb, p.nsplit, Cout, p.Kpad, dw, db);
+  PF_CHECK_LAUNCH();
+  return POSFEAT_OK;
+}
+
+int pf_dgrad_weights(const float* w, int Cout, int Cin, int KH, int KW, float* wt,
+                     hipStream_t st) {
+  if (Cout % 32 || Cin % 32) return POSFEAT_E_INVALID;
+  const int kf = posfeat_conv_packed_k(Cin, KH, KW), kt = posfeat_conv_packed_k(Cout, KH, KW);
+  const long long n = (long long)Cin * kt;
+  hipLaunchKernelGGL(dgrad_weights_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, w,
+                     Cout, Cin, KH * KW, kf, wt, kt);
+  PF_CHECK_LAUNCH();
+  return POSFEAT_OK;
+}
+
+int pf_up4_adjoint(const float* g, int gcs, int nb, int OH, int OW, int h, int w, int C, float* t,
+                   float* d, int dcs, hipStream_t st) {
+  if (C % 4 || gcs % 4 || dcs % 4) return POSFEAT_E_INVALID;
+  const int c4n = C / 4;
+  hipLaunchKernelGGL(up4_adj_x_kernel, dim3(grid_for((long long)nb * OH * w * c4n, 256)), dim3(256),
+                     0, st, g, gcs, nb, OH, OW, w, c4n, t);
+  hipLaunchKernelGGL(up4_adj_y_kernel, dim3(grid_for((long long)nb * h * w * c4n, 256)), dim3(256),
+                     0, st, t, nb, OH, h, w, c4n, d, dcs);
+  PF_CHECK_LAUNCH();
+  return POSFEAT_OK;
+}
+
+size_t pf_in_bwd_ws_bytes(int nb, int hw, int C) {
+  const int nchunk = (hw + INB_CHUNK - 1) / INB_CHUNK;
+  return pf_align((size_t)nb * nchunk * C * 2 * 8, 256) + pf_align((size_t)nb * nchunk * 8, 256) +
+         2 * pf_align((size_t)nb * C * 4, 256);
+}
+
+int pf_in_backward(const float* x, int xcs, const float* g, int gcs, int nb, int hw, int C,
+                   const float* mean, const float* rstd, const float* slope, float* dx, int dxcs,
+                   void* ws, double** slope_part, int* slope_nparts, hipStream_t st) {
+  if (C % 4 || C / 4 > 256 || xcs % 4 || gcs % 4 || dxcs % 4) return POSFEAT_E_INVALID;
+  const int nchunk = (hw + INB_CHUNK - 1) / INB_CHUNK;
+  char* p = static_cast<char*>(ws);
+  double* part = reinterpret_cast<double*>(p);
+  p += pf_align((size_t)nb * nchunk * C * 2 * 8, 256);
+  double* spart = reinterpret_cast<double*>(p);
+  p += pf_align((size_t)nb * nchunk * 8, 256);
+  float* e1 = reinterpret_cast<float*>(p);
+  p += pf_align((size_t)nb * C * 4, 256);
+  float* e2 = reinterpret_cast<float*>(p);
+  const bool prelu = slope != nullptr;
+  if (prelu)
+    hipLaunchKernelGGL(in_bwd_partial_kernel<true>, dim3(nchunk, nb), dim3(256), 0, st, x, xcs, g,
+                       gcs, hw, C, mean, rstd, slope, part, spart);
+  else
+    hipLaunchKernelGGL(in_bwd_partial_kernel<false>, dim3(nchunk, nb), dim3(256), 0, st, x, xcs, g,
+                       gcs, hw, C, mean, rstd, slope, part, spart);
+  PF_CHECK_LAUNCH();
+  hipLaunchKernelGGL(in_bwd_finalize_kernel, dim3((nb * C + 255) / 256), dim3(256), 0, st, part,
+                     nchunk, nb, C, hw, e1, e2);
+  const long long total = (long long)nb * hw * (C / 4);
+  if (prelu)
+    hipLaunchKernelGGL(in_bwd_apply_kernel<true>, dim3(grid_for(total, 256)), dim3(256), 0, st, x,
+                       xcs, g, gcs, nb, hw, C / 4, mean, rstd, slope, e1, e2, dx, dxcs);
+  else
+    hipLaunchKernelGGL(in_bwd_apply_kernel<false>, dim3(grid_for(total, 256)), dim3(256), 0, st,
+                       x, xcs, g, gcs, nb, hw, C / 4, mean, rstd, slope, e1, e2, dx, dxcs);
+  PF_CHECK_LAUNCH();
+  if (slope_part) *slope_part = spart;
+  if (slope_nparts) *slope_nparts = nb * nchunk;
+  return POSFEAT_OK;
+}
+
+size_t pf_tail_bwd_ws_bytes(int nb, int hw) {
+  const int nchunk = (hw + INB_CHUNK - 1) / INB_CHUNK;
+  return pf_align((size_t)nb * nchunk * 2 * 8, 256) + pf_align((size_t)nb * nchunk * 128 * 3 * 8, 256) +
+         pf_align((size_t)nb * nchunk * 2 * 8, 256) + 2 * pf_align((size_t)nb * 128 * 4, 256);
+}
+
+int pf_tail_backward(const float* dlp, const float* y3, const float* m3, const float* r3,
+                     const float* c2, int c2cs, const float* m2, const float* r2,
+                     const float* slope, const float* w3, int nb, int hw, float* dy3, float* dc2,
+                     int dcs, float* dw3, void* ws, double** t2s, int* t2n, hipStream_t st) {
+  const int nchunk = (hw + INB_CHUNK - 1) / INB_CHUNK;
+  char* p = static_cast<char*>(ws);
+  double* t1 = reinterpret_cast<double*>(p);
+  p += pf_align((size_t)nb * nchunk * 2 * 8, 256);
+  double* part = reinterpret_cast<double*>(p);
+  p += pf_align((size_t)nb * nchunk * 128 * 3 * 8, 256);
+  double* spart = reinterpret_cast<double*>(p);
+  p += pf_align((size_t)nb * nchunk * 2 * 8, 256);
+  float* e1 = reinterpret_cast<float*>(p);
+  p += pf_align((size_t)nb * 128 * 4, 256);
+  float* e2 = reinterpret_cast<float*>(p);
+  hipLaunchKernelGGL(tail1_partial_kernel, dim3(nchunk, nb), dim3(256), 0, st, dlp, y3, hw, m3, r3,
+                     t1);
+  hipLaunchKernelGGL(tail2_partial_kernel, dim3(nchunk, nb), dim3(256), 0, st, dlp, y3, c2, c2cs,
+                     hw, m3, r3, t1, nchunk, m2, r2, slope, w3, dy3, part, spart);
+  hipLaunchKernelGGL(tail2_finalize_kernel, dim3(1), dim3(128), 0, st, part, nchunk, nb, hw, e1, e2,
+                     dw3);
+  const long long total = (long long)nb * hw * 32;
+  hipLaunchKernelGGL(tail3_kernel, dim3(grid_for(total, 256)), dim3(256), 0, st, dy3, c2, c2cs, nb,
+                     hw, m2, r2, slope, w3, e1, e2, dc2, dcs);
+  PF_CHECK_LAUNCH();
+  *t2s = spart;
+  *t2n = nb * nchunk;
+  return POSFEAT_OK;
+}
+
+int pf_head_scalars(const double* t2s, int n2, const double* c1s, int n1, float* db3,
+                    float* dslope, hipStream_t st) {
+  hipLaunchKernelGGL(head_scalars_kernel, dim3(1), dim3(64), 0, st, t2s, n2, c1s, n1, db3, dslope);
+  PF_CHECK_LAUNCH();
+  return POSFEAT_OK;
+}
+
+extern "C" int posfeat_sgd(float* w, const float* g, long long n, float lr, void* stream) {
+  if (!w || !g || n < 0) return POSFEAT_E_INVALID;
+  if (n == 0) return POSFEAT_OK;
+  hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n, 256)), dim3(256), 0, pf_stream(stream), w, g, n,
+                     lr);
+  PF_CHECK_LAUNCH();
+  return POSFEAT_OK;
+}
+
+extern "C" size_t posfeat_conv_wgrad_workspace(int n, int h, int w, int cin, int cout, int kh,
+                                               int kw) {
+  if (n <= 0 || h <= 0 || w <= 0 || cout <= 0 || cin <= 0) return 0;
+  return pf_conv_wgrad_ws_bytes(n, h, w, cin, cout, kh, kw);
+}
+
+extern "C" int posfeat_conv_wgrad(const float* dy, int dy_cstride, const float* x, int x_cstride,
+                                  int n, int h, int w, int cin, int cout, int kh, int kw,
+                                  float* dw, float* db, void* ws, size_t ws_bytes, void* stream) {
+  if (!dy || !x || !dw || !ws || n <= 0 || h <= 0 || w <= 0) return POSFEAT_E_INVALID;
+  return pf_conv_wgrad(dy, dy_cstride, x, x_cstride, n, h, w, cin, cout, kh, kw, dw, db, ws,
+                       ws_bytes, pf_stream(stream));
+}

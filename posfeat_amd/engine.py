@@ -16,8 +16,12 @@ from ._lib import check, lib, ptr, stream_ptr
 
 
 class ExtractionEngine:
-    def __init__(self, backbone_sd=None, head_sd=None, device="cuda", blob=None):
+    """``train=True`` builds instances that keep the head's intermediates for
+    ``head_backward`` (keypoint-head training, configs/train_kp.yaml)."""
+
+    def __init__(self, backbone_sd=None, head_sd=None, device="cuda", blob=None, train=False):
         _lib.require_device()
+        self.train = bool(train)
         self.device = torch.device(device)
         self.specs = _lib.model_specs()
         nfl = lib().posfeat_model_weight_floats()
@@ -36,7 +40,8 @@ class ExtractionEngine:
         inst = self._inst.get(key)
         if inst is None:
             handle = ctypes.c_void_p()
-            check(lib().posfeat_model_create(b, h, w, ptr(self.wdev), ctypes.byref(handle)))
+            create = lib().posfeat_model_create_train if self.train else lib().posfeat_model_create
+            check(create(b, h, w, ptr(self.wdev), ctypes.byref(handle)))
             nbytes = lib().posfeat_model_workspace(handle)
             ws = torch.empty(nbytes + 256, dtype=torch.uint8, device=self.device)
             off = (-ws.data_ptr()) % 256
@@ -93,6 +98,40 @@ class ExtractionEngine:
         res["_local_map_nhwc"] = ws[base:base + nfl * 4].view(torch.float32).view(
             b, h // 4, w // 4, cs)
         return res
+
+    # ------------------------------------------------------------ training
+    @property
+    def head_offset(self):
+        return int(lib().posfeat_model_head_offset())
+
+    @property
+    def head_floats(self):
+        return int(lib().posfeat_model_head_floats())
+
+    def head_weights(self):
+        """View of the trainable KeypointDet region of the device blob."""
+        return self.wdev[self.head_offset:self.head_offset + self.head_floats]
+
+    def head_backward(self, dlocal_point, grad=None):
+        """dL/d(head params) (packed like ``head_weights()``) from dL/d local_point
+        [b,1,h,w] of the last ``run`` of that shape.  Needs ``train=True``."""
+        if not self.train:
+            raise RuntimeError("head_backward needs an engine built with train=True")
+        b, _, h, w = dlocal_point.shape
+        handle, ws, off = self._instance(b, h, w)
+        if grad is None:
+            grad = torch.empty(self.head_floats, dtype=torch.float32, device=self.device)
+        dl = dlocal_point.float().contiguous()
+        _lib.require_device(dl)
+        check(lib().posfeat_model_head_backward(handle, ptr(dl), ptr(grad),
+                                                ctypes.c_void_p(ws.data_ptr() + off),
+                                                ws.numel() - off, stream_ptr()))
+        return grad
+
+    def sgd_step(self, grad, lr):
+        """torch.optim.SGD (no momentum) on the head region: w -= lr * grad."""
+        check(lib().posfeat_sgd(ptr(self.head_weights()), ptr(grad), self.head_floats,
+                                float(lr), stream_ptr()))
 
     def close(self):
         for handle, _, _ in self._inst.values():

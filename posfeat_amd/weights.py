@@ -225,6 +225,60 @@ def pack_conv(w, b):
     return out, b.astype(np.float32)
 
 
+def unpack_conv(wp, cout, cin, kh, kw):
+    """Inverse of ``pack_conv`` for the weight: [Cout][Kpad] -> [Cout,Cin,KH,KW]."""
+    cinp, k, kpad = packed_k(cin, kh, kw)
+    wp = np.asarray(wp, np.float32).reshape(cout, kpad)[:, :k]
+    if cin % 32 == 0:
+        return np.ascontiguousarray(
+            wp.reshape(cout, cin // 32, kh, kw, 32).transpose(0, 1, 4, 2, 3).reshape(cout, cin, kh, kw))
+    return np.ascontiguousarray(wp.reshape(cout, kh, kw, cinp)[..., :cin].transpose(0, 3, 1, 2))
+
+
+def head_offset(specs):
+    """First float of the KeypointDet region of the blob (the head specs are
+    the contiguous tail of the engine's layer table)."""
+    return min(s[5] for s in specs if s[0].startswith("head."))
+
+
+def pack_head(head_sd, specs, total, head_prelu_key="relu.weight"):
+    """The KeypointDet part of the blob (floats [head_offset, total)) from a
+    head state dict -- also used to lay reference gradients out like the
+    engine's packed gradient buffer."""
+    hoff = head_offset(specs)
+    out = np.zeros(total - hoff, np.float32)
+    for name, cout, cin, kh, kw, w_off, b_off in specs:
+        if not name.startswith("head."):
+            continue
+        if name == "head.prelu":
+            out[b_off - hoff] = float(_np(head_sd[head_prelu_key]).reshape(-1)[0])
+            continue
+        _, wk, bk, _ = conv_sources(name)
+        wp, bp = pack_conv(_np(head_sd[wk]).astype(np.float64), _np(head_sd[bk]).astype(np.float64))
+        out[w_off - hoff:w_off - hoff + wp.size] = wp.reshape(-1)
+        out[b_off - hoff:b_off - hoff + cout] = bp
+    return out
+
+
+def unpack_head(region, specs, head_prelu_key="relu.weight"):
+    """Head state dict (KeypointDet key order, DeteNet.py:9-22) from the blob's
+    head region -- PoSFeat.save_checkpoint's localheader.pth after training."""
+    hoff = head_offset(specs)
+    region = np.asarray(region, np.float32)
+    vals = {}
+    for name, cout, cin, kh, kw, w_off, b_off in specs:
+        if not name.startswith("head."):
+            continue
+        if name == "head.prelu":
+            vals[head_prelu_key] = region[b_off - hoff:b_off - hoff + 1].copy()
+            continue
+        _, wk, bk, _ = conv_sources(name)
+        kpad = packed_k(cin, kh, kw)[2]
+        vals[wk] = unpack_conv(region[w_off - hoff:w_off - hoff + cout * kpad], cout, cin, kh, kw)
+        vals[bk] = region[b_off - hoff:b_off - hoff + cout].copy()
+    return OrderedDict((k, vals[k]) for k, _ in head_param_shapes())
+
+
 def pack_for_device(backbone_sd, head_sd, specs, head_prelu_key="relu.weight"):
     """Build the flat float32 weight blob in the order of ``specs``.
 

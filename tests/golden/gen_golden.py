@@ -323,9 +323,61 @@ def gen_correlation(out):
     np.savez_compressed(out, **res)
 
 
+TRAIN_KP_CASES = {"a": (2, 64, 96, 5, 300), "b": (1, 96, 128, 6, 301)}
+
+
+def gen_train_kp(out):
+    """Config-5 step on the reference's own modules: KeypointDet (DeteNet.py)
+    in train mode on detached backbone maps (PoSFeat_model.py:97-102), the
+    reference DiskLoss (kploss.py) with torch.manual_seed, loss.backward()
+    through autograd (trainer.py:330-331).  Stores the loss, every head
+    parameter's gradient and the replayed draws (same seed, same call order:
+    point_sample(kp1) then point_sample(kp2), kploss.py:141-142)."""
+    bb, hd = build_ref_models(0)
+    res = {}
+    for tag, (b, H, W, fseed, tseed) in TRAIN_KP_CASES.items():
+        im1 = torch.from_numpy(np.stack([seeded_image(10 + i + 7 * fseed, H, W) for i in range(b)]))
+        im2 = torch.from_numpy(np.stack([seeded_image(20 + i + 7 * fseed, H, W) for i in range(b)]))
+        F1, F2 = synthetic_fundamental(b, H, W, fseed)
+        F1, F2 = torch.from_numpy(F1), torch.from_numpy(F2)
+        hd.train()
+        hd.zero_grad()
+        preds = {}
+        for key, im in (("preds1", im1), ("preds2", im2)):
+            with torch.no_grad():
+                feat = bb(im)
+            local_input = torch.cat([feat["local_map"], feat["local_map_small"]], dim=1).detach()
+            lp = hd([local_input, im])
+            preds[key] = {"local_map": feat["local_map"], "local_point": lp,
+                          "global_map": feat["global_map"]}
+        outputs = dict(preds, epoch=1)
+        inputs = {"im1": im1, "im2": im2, "F1": F1, "F2": F2}
+        dl = ref_losses.DiskLoss(DISK_CFG)
+        torch.manual_seed(tseed)
+        loss, comp = dl(inputs, outputs, None)
+        loss.backward()
+        res[tag + "_loss"] = loss.detach().numpy()
+        for k in ("reinforce", "kp_penalty", "n_kps"):
+            res["%s_%s" % (tag, k)] = comp[k].detach().numpy()
+        for k, p in hd.named_parameters():
+            res["%s_grad_%s" % (tag, k)] = p.grad.detach().numpy().copy()
+        torch.manual_seed(tseed)
+        for i, key in ((1, "preds1"), (2, "preds2")):
+            kps, _, acc = dl.point_sample(preds[key]["local_point"].detach())
+            ix, iy = kps[..., 0].long(), kps[..., 1].long()
+            res["%s_prop%d" % (tag, i)] = ((iy % 8) * 8 + ix % 8).int().numpy()[:, None]
+            res["%s_acc%d" % (tag, i)] = acc.numpy()
+            res["%s_lp%d" % (tag, i)] = preds[key]["local_point"].detach().numpy()
+        hd.eval()
+    np.savez_compressed(out, **res)
+
+
 if __name__ == "__main__":
     torch.set_num_threads(os.cpu_count() or 8)
-    which = sys.argv[1:] or ["detector", "sampler", "model_small", "extract_full", "correlation"]
+    which = sys.argv[1:] or ["detector", "sampler", "model_small", "extract_full", "correlation",
+                             "train_kp"]
+    if "train_kp" in which:
+        gen_train_kp(os.path.join(HERE, "train_kp.npz"))
     if "detector" in which:
         gen_detector(os.path.join(HERE, "detector.npz"))
     if "sampler" in which:
