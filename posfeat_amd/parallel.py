@@ -27,3 +27,17 @@ def broadcast_weights(state_dicts, device, src=0):
             n = t.numel()
             t.data.copy_(flat[off:off + n].view(t.shape).to(t.device, t.dtype))
             off += n
+
+
+def allreduce_head_grad(grad, group=None):
+    """Keypoint-head training (configs/train_kp.yaml under DDP): ONE all-reduce
+    (sum) of the flat packed head gradient (2.5 MB; RCCL over xGMI on the GPU
+    box, gloo in CPU tests) replaces DDP's bucketed per-parameter all-reduce
+    (trainer.py:331, PoSFeat_model.py:53-55).  Returns the factor the SGD step
+    applies (1/world: DDP averages gradients over ranks)."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return 1.0
+    world = dist.get_world_size(group)
+    if world > 1:
+        dist.all_reduce(grad, group=group)
+    return 1.0 / world

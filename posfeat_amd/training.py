@@ -20,11 +20,11 @@ of arithmetic is in libposfeat_hip.so; torch provides memory, the RNG for the
 sampling uniforms and ``torch.distributed``.
 """
 import torch
-import torch.distributed as dist
 
 from . import _lib
 from ._lib import check, lib, ptr, stream_ptr
 from .engine import ExtractionEngine
+from .parallel import allreduce_head_grad
 
 DISK_DEFAULTS = {"grid_size": 8, "loss_distance": "cos", "temperature_base": 60,
                  "temperature_max": 60, "epipolar_reward": "constant_reward",
@@ -54,8 +54,6 @@ class KeypointTrainStep:
         _check_disk_config(self.cfg)
         self.lr = float(lr)
         self.group = group
-        self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() \
-            else 1
         self._ws = {}
         self._grad = None
 
@@ -113,8 +111,7 @@ class KeypointTrainStep:
             self._grad = torch.empty(self.engine.head_floats, dtype=torch.float32,
                                      device=imgs.device)
         grad = self.engine.head_backward(dkp, self._grad)
-        if self.world > 1:
-            dist.all_reduce(grad, group=self.group)   # RCCL over xGMI, 2.5 MB
+        scale = allreduce_head_grad(grad, self.group)   # RCCL over xGMI, 2.5 MB
         if update:
-            self.engine.sgd_step(grad, self.lr / self.world)
+            self.engine.sgd_step(grad, self.lr * scale)
         return out, grad

@@ -98,3 +98,35 @@ def test_gloo_broadcast_and_shard():
         p.join(60)
     assert all(ok for _, ok, _ in res)
     assert sorted(res[0][2] + res[1][2]) == list(range(10))
+
+
+def _grad_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from posfeat_amd.parallel import allreduce_head_grad
+    g = torch.from_numpy(np.random.RandomState(rank).randn(1000).astype(np.float32))
+    w = torch.from_numpy(np.random.RandomState(99).randn(1000).astype(np.float32))
+    scale = allreduce_head_grad(g)
+    w_new = w - 1e-3 * scale * g          # the posfeat_sgd update with lr * scale
+    q.put((rank, scale, w_new.numpy()))
+    dist.destroy_process_group()
+
+
+def test_gloo_head_grad_allreduce_is_ddp_mean():
+    """The training step's one all-reduce + lr/world SGD equals DDP's mean-gradient
+    update and leaves every rank with identical weights (trainer.py:331-356)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29600 + os.getpid() % 1000
+    procs = [ctx.Process(target=_grad_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=300) for _ in procs), key=lambda r: r[0])
+    for p in procs:
+        p.join(60)
+    gs = [np.random.RandomState(r).randn(1000).astype(np.float32) for r in range(2)]
+    w = np.random.RandomState(99).randn(1000).astype(np.float32)
+    ref = w - 1e-3 * (gs[0] + gs[1]) / 2
+    assert res[0][1] == 0.5
+    np.testing.assert_array_equal(res[0][2], res[1][2])
+    np.testing.assert_allclose(res[0][2], ref, rtol=1e-6, atol=1e-7)
