@@ -192,6 +192,28 @@ int posfeat_epipolar_loss(int b, int n, const float *F1, const float *F2, const 
                           float short_edge, float grid_thr, float win_thr, float weight_grid,
                           float weight_window, float *out, void *stream);
 
+/* Backward of the descriptor loss (configs/train_desc.yaml: weight_grid 0,
+ * weight_window 1, use_std_as_weight): dL/d local_map for both images, i.e.
+ * what loss.backward() sends from losses/epipolarloss.py:38-101 through
+ * losses/preprocess.py:98-101 (window expectation, preprocess_utils.py:
+ * 721-758) and the query descriptors (sample_feat_by_coord, 40-53) into the
+ * backbone (managers/trainer.py:331).  The std weights are detached
+ * (epipolarloss.py:29-31) and the line search runs under no_grad
+ * (preprocess_utils.py:661), so no other path carries gradient.
+ * Call after posfeat_line2window on the SAME fwd_ws with its outputs `fwd`
+ * (coord*, l*_exp_n, w*, w*_std, valid* are read).  dxf1/dxf2: NHWC
+ * [b][H/4][W/4] (pixel stride dcs, 128 channels), overwritten.  Scatters
+ * accumulate in 64-bit fixed point, so the result is deterministic.
+ * weight_grid != 0 returns POSFEAT_E_UNSUPPORTED. */
+size_t posfeat_line2window_backward_workspace(int b, int H1, int W1, int H2, int W2, int grid);
+int posfeat_line2window_backward(const float *xf1, int cs1, const float *xf2, int cs2, int b,
+                                 int H1, int W1, int H2, int W2, const float *F1,
+                                 const float *F2, const posfeat_l2w_out *fwd, const void *fwd_ws,
+                                 float temperature, int grid, float window_size,
+                                 float short_edge, float grid_thr, float win_thr,
+                                 float weight_grid, float weight_window, float *dxf1, int dcs1,
+                                 float *dxf2, int dcs2, void *ws, size_t ws_bytes, void *stream);
+
 /* DiskLoss forward (losses/kploss.py:132-197, constant_reward, grid 8):
  * kp1/kp2 [b][H][W] score maps, xf1/xf2 NHWC local maps [b][H/4][W/4] (pixel
  * stride cs), F1/F2 [b][3][3].  Either prop1,prop2,acc1,acc2 ([b][n] Categorical proposal

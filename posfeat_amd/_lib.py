@@ -97,6 +97,12 @@ SIGNATURES = {
     "posfeat_model_head_floats": (c_ll, []),
     "posfeat_model_head_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
                                             c_void_p]),
+    "posfeat_line2window_backward_workspace": (c_size_t, [c_int] * 6),
+    "posfeat_line2window_backward": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int,
+                                             c_int, c_int, c_void_p, c_void_p,
+                                             ctypes.POINTER(L2WOut), c_void_p, c_float, c_int] +
+                                     [c_float] * 6 + [c_void_p, c_int, c_void_p, c_int, c_void_p,
+                                                      c_size_t, c_void_p]),
     "posfeat_model_num_specs": (c_int, []),
     "posfeat_model_conv_spec": (c_int, [c_int, ctypes.POINTER(ctypes.c_char_p), P_int, P_int,
                                         P_int, P_int, ctypes.POINTER(c_ll),

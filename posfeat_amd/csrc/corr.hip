@@ -481,21 +481,323 @@ __global__ __launch_bounds__(1024) void epipolar_loss_kernel(
   }
 }
 
+// ---------------------------------------------------------------- backward
+// Descriptor training (configs/train_desc.yaml: weight_grid 0, weight_window 1,
+// use_std_as_weight): the weights are detached (epipolarloss.py:25-36), the
+// line search runs under no_grad (preprocess_utils.py:661), so dL/d local_map
+// flows only through the window expectation (721-758): its softmax over the
+// window taps, the zero-padded bilinear samples of T*normalize(xf) (scatter to
+// the map) and the query descriptor (normalize(grid_sample(xf)) at the grid
+// point).  Scatters accumulate in 64-bit fixed point (2^-40): integer adds
+// commute, so the result does not depend on the order the atomics land in.
+constexpr double FX_SCALE = 1099511627776.0;  // 2^40
+
+__device__ __forceinline__ void fx_add(unsigned long long* p, float v) {
+  const long long q = llrint((double)v * FX_SCALE);
+  if (q != 0) atomicAdd(p, (unsigned long long)q);
+}
+
+// dL/d(window expectation, normalised) per point for one direction (k = 1: w1
+// with F1, coords1, image-2 size; k = 3: w2): one workgroup, the forward's
+// fixed-order reductions recomputed.  d loss/d cost_i = ww * wt_i / total,
+// d cost/d x2 = sign(x2^T l) l[:2] (l normalised), x2 = E * c + c.
+__global__ __launch_bounds__(1024) void epi_loss_bwd_kernel(
+    int nb, int n, const float* __restrict__ Fm, const float* __restrict__ cq,
+    const float* __restrict__ wpx, const float* __restrict__ wsd, const uint8_t* __restrict__ v,
+    float short_edge, float wthr, float ww, float c0, float c1, float* __restrict__ gE) {
+  const int tid = threadIdx.x;
+  const int total = nb * n;
+  __shared__ double red[16][2];
+  double a1 = 0.0;
+  for (int i = tid; i < total; i += blockDim.x) a1 += 1.0 / fmaxf(wsd[i], 1e-10f);
+  for (int o = 32; o > 0; o >>= 1) a1 += __shfl_xor(a1, o, 64);
+  if ((tid & 63) == 0) red[tid >> 6][0] = a1;
+  __syncthreads();
+  double inv_mean = 0.0;
+  for (int wv = 0; wv < (int)(blockDim.x >> 6); ++wv) inv_mean += red[wv][0];
+  inv_mean /= total;
+  __syncthreads();
+  double b1 = 0.0;
+  for (int i = tid; i < total; i += blockDim.x) {
+    const float* F = Fm + (i / n) * 9;
+    const float cost = epi_cost(F, cq[2 * i], cq[2 * i + 1], wpx[2 * i], wpx[2 * i + 1]);
+    const bool m = cost < short_edge * wthr && v[i];
+    b1 += m ? (1.0 / fmaxf(wsd[i], 1e-10f)) / inv_mean : 0.0;
+  }
+  for (int o = 32; o > 0; o >>= 1) b1 += __shfl_xor(b1, o, 64);
+  if ((tid & 63) == 0) red[tid >> 6][0] = b1;
+  __syncthreads();
+  double sw = 0.0;
+  for (int wv = 0; wv < (int)(blockDim.x >> 6); ++wv) sw += red[wv][0];
+  const double wmean = sw / total + 1e-8;
+  for (int i = tid; i < total; i += blockDim.x) {
+    const float* F = Fm + (i / n) * 9;
+    const float x1 = cq[2 * i], y1 = cq[2 * i + 1], x2 = wpx[2 * i], y2 = wpx[2 * i + 1];
+    const float a = F[0] * x1 + F[1] * y1 + F[2];
+    const float b = F[3] * x1 + F[4] * y1 + F[5];
+    const float c = F[6] * x1 + F[7] * y1 + F[8];
+    const float nrm = fmaxf(sqrtf(a * a + b * b), 1e-8f);
+    const float sv = x2 * (a / nrm) + y2 * (b / nrm) + (c / nrm);
+    const bool m = fabsf(sv) < short_edge * wthr && v[i];
+    float gx = 0.f, gy = 0.f;
+    if (m) {
+      const double wt = (1.0 / fmaxf(wsd[i], 1e-10f)) / inv_mean / wmean;
+      const float coef = (float)(ww * wt / total) * (sv > 0.f ? 1.f : (sv < 0.f ? -1.f : 0.f));
+      gx = coef * (a / nrm) * c0;
+      gy = coef * (b / nrm) * c1;
+    }
+    gE[2 * i] = gx;
+    gE[2 * i + 1] = gy;
+  }
+}
+
+// Window-expectation backward, one wave per query point (mirrors the window
+// part of line_window_kernel): recompute the logits and softmax, then
+//   dp_s = gE . g_s,  dsim_s = p_s (dp_s - sum p dp),
+//   dq   = sum_s dsim_s v_s            (query descriptor, written to dq)
+//   d fm[corner] += bilinear_w * dsim_s * q   (fixed-point scatter)
+__global__ void window_bwd_kernel(const float* __restrict__ f1, const float* __restrict__ fm2,
+                                  const float* __restrict__ center, const float* __restrict__ gE,
+                                  int nb, int n, int h2, int w2, int win_h, int win_w,
+                                  float window_size, float* __restrict__ dq,
+                                  unsigned long long* __restrict__ acc) {
+  const int lane = threadIdx.x & 63;
+  const long long wid = blockIdx.x * (long long)(blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (wid >= (long long)nb * n) return;
+  const int b = (int)(wid / n);
+  const float gx0 = gE[wid * 2], gy0 = gE[wid * 2 + 1];
+  if (gx0 == 0.f && gy0 == 0.f) {  // masked point: no gradient
+    dq[wid * 128 + lane] = 0.f;
+    dq[wid * 128 + lane + 64] = 0.f;
+    return;
+  }
+  const float* fmb = fm2 + (long long)b * h2 * w2 * 128;
+  unsigned long long* accb = acc + (long long)b * h2 * w2 * 128;
+  const float q0 = f1[wid * 128 + lane], q1 = f1[wid * 128 + lane + 64];
+  const float jx = center[wid * 2], jy = center[wid * 2 + 1];
+  const int nw = win_h * win_w;
+  float wl[MAX_WIN / 64];
+#pragma unroll
+  for (int r = 0; r < MAX_WIN / 64; ++r) wl[r] = -INFINITY;
+  for (int s = 0; s < nw; ++s) {
+    const int iy = s / win_w, ix = s - iy * win_w;
+    const float gx = jx + linspace_f(-window_size, window_size, win_w, ix);
+    const float gy = jy + linspace_f(-window_size, window_size, win_h, iy);
+    const float2 vv = bilinear128<false>(fmb, h2, w2, gx, gy, lane);
+    const float d = pf_wave_sum(q0 * vv.x + q1 * vv.y);
+#pragma unroll
+    for (int r = 0; r < MAX_WIN / 64; ++r)
+      if (s == lane + 64 * r) wl[r] = d;
+  }
+  float wm = -INFINITY;
+#pragma unroll
+  for (int r = 0; r < MAX_WIN / 64; ++r) wm = fmaxf(wm, wl[r]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) wm = fmaxf(wm, __shfl_xor(wm, o, 64));
+  float se = 0.f;
+  float pr[MAX_WIN / 64], dp[MAX_WIN / 64];
+#pragma unroll
+  for (int r = 0; r < MAX_WIN / 64; ++r) {
+    const int s = lane + 64 * r;
+    pr[r] = s < nw ? expf(wl[r] - wm) : 0.f;
+    se += pr[r];
+  }
+  se = pf_wave_sum(se);
+  float sdp = 0.f;
+#pragma unroll
+  for (int r = 0; r < MAX_WIN / 64; ++r) {
+    const int s = lane + 64 * r;
+    pr[r] /= se;
+    dp[r] = 0.f;
+    if (s < nw) {
+      const int iy = s / win_w, ix = s - iy * win_w;
+      const float gx = jx + linspace_f(-window_size, window_size, win_w, ix);
+      const float gy = jy + linspace_f(-window_size, window_size, win_h, iy);
+      dp[r] = gx0 * gx + gy0 * gy;
+      sdp += pr[r] * dp[r];
+    }
+  }
+  sdp = pf_wave_sum(sdp);
+  float ds[MAX_WIN / 64];
+#pragma unroll
+  for (int r = 0; r < MAX_WIN / 64; ++r) ds[r] = pr[r] * (dp[r] - sdp);
+  float dq0 = 0.f, dq1 = 0.f;
+  for (int s = 0; s < nw; ++s) {
+    float dsv = 0.f;
+#pragma unroll
+    for (int r = 0; r < MAX_WIN / 64; ++r)
+      if ((s >> 6) == r) dsv = __shfl(ds[r], s & 63, 64);
+    const int iy = s / win_w, ix = s - iy * win_w;
+    const float gx = jx + linspace_f(-window_size, window_size, win_w, ix);
+    const float gy = jy + linspace_f(-window_size, window_size, win_h, iy);
+    const float2 vv = bilinear128<false>(fmb, h2, w2, gx, gy, lane);
+    dq0 += dsv * vv.x;
+    dq1 += dsv * vv.y;
+    // scatter dsv * q over the 4 zero-padded corners (same weights as bilinear128)
+    const float fx = ((gx + 1.f) * w2 - 1.f) / 2.f, fy = ((gy + 1.f) * h2 - 1.f) / 2.f;
+    const float flx = floorf(fx), fly = floorf(fy);
+    const int x0 = (int)flx, y0 = (int)fly, x1 = x0 + 1, y1 = y0 + 1;
+    const float t0 = dsv * q0, t1 = dsv * q1;
+    const bool bx0 = (unsigned)x0 < (unsigned)w2, bx1 = (unsigned)x1 < (unsigned)w2;
+    const bool by0 = (unsigned)y0 < (unsigned)h2, by1 = (unsigned)y1 < (unsigned)h2;
+    if (by0 && bx0) {
+      const float wt = ((float)x1 - fx) * ((float)y1 - fy);
+      unsigned long long* p = accb + ((long long)y0 * w2 + x0) * 128;
+      fx_add(p + lane, wt * t0);
+      fx_add(p + lane + 64, wt * t1);
+    }
+    if (by0 && bx1) {
+      const float wt = (fx - (float)x0) * ((float)y1 - fy);
+      unsigned long long* p = accb + ((long long)y0 * w2 + x1) * 128;
+      fx_add(p + lane, wt * t0);
+      fx_add(p + lane + 64, wt * t1);
+    }
+    if (by1 && bx0) {
+      const float wt = ((float)x1 - fx) * (fy - (float)y0);
+      unsigned long long* p = accb + ((long long)y1 * w2 + x0) * 128;
+      fx_add(p + lane, wt * t0);
+      fx_add(p + lane + 64, wt * t1);
+    }
+    if (by1 && bx1) {
+      const float wt = (fx - (float)x0) * (fy - (float)y0);
+      unsigned long long* p = accb + ((long long)y1 * w2 + x1) * 128;
+      fx_add(p + lane, wt * t0);
+      fx_add(p + lane + 64, wt * t1);
+    }
+  }
+  dq[wid * 128 + lane] = dq0;
+  dq[wid * 128 + lane + 64] = dq1;
+}
+
+// Query-descriptor backward: f = normalize(s), s = grid_sample(xf, c) (zeros,
+// align_corners=False): ds = (dq - f (f.dq)) / max(|s|, 1e-12) scattered over
+// the 4 corners of c into acc (raw-map gradient, fixed point).  One wave/point.
+__global__ void query_bwd_kernel(const float* __restrict__ xf, int cs, const float* __restrict__ cn,
+                                 const float* __restrict__ f, const float* __restrict__ dq, int nb,
+                                 int n, int h, int w, unsigned long long* __restrict__ acc) {
+  const int lane = threadIdx.x & 63;
+  const long long wid = blockIdx.x * (long long)(blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (wid >= (long long)nb * n) return;
+  const int b = (int)(wid / n);
+  const float d0 = dq[wid * 128 + lane], d1 = dq[wid * 128 + lane + 64];
+  if (pf_wave_sum(fabsf(d0) + fabsf(d1)) == 0.f) return;
+  const float* xb = xf + (long long)b * h * w * cs;
+  unsigned long long* accb = acc + (long long)b * h * w * 128;
+  const float gx = cn[wid * 2], gy = cn[wid * 2 + 1];
+  const float fx = ((gx + 1.f) * w - 1.f) / 2.f, fy = ((gy + 1.f) * h - 1.f) / 2.f;
+  const float flx = floorf(fx), fly = floorf(fy);
+  const int x0 = (int)flx, y0 = (int)fly, x1 = x0 + 1, y1 = y0 + 1;
+  const bool bx0 = (unsigned)x0 < (unsigned)w, bx1 = (unsigned)x1 < (unsigned)w;
+  const bool by0 = (unsigned)y0 < (unsigned)h, by1 = (unsigned)y1 < (unsigned)h;
+  const float w00 = ((float)x1 - fx) * ((float)y1 - fy), w01 = (fx - (float)x0) * ((float)y1 - fy);
+  const float w10 = ((float)x1 - fx) * (fy - (float)y0), w11 = (fx - (float)x0) * (fy - (float)y0);
+  float s0 = 0.f, s1 = 0.f;  // the raw sample (for |s|), same order as sample.hip
+  if (by0 && bx0) {
+    const float* p = xb + ((long long)y0 * w + x0) * cs;
+    s0 += p[lane] * w00;
+    s1 += p[lane + 64] * w00;
+  }
+  if (by0 && bx1) {
+    const float* p = xb + ((long long)y0 * w + x1) * cs;
+    s0 += p[lane] * w01;
+    s1 += p[lane + 64] * w01;
+  }
+  if (by1 && bx0) {
+    const float* p = xb + ((long long)y1 * w + x0) * cs;
+    s0 += p[lane] * w10;
+    s1 += p[lane + 64] * w10;
+  }
+  if (by1 && bx1) {
+    const float* p = xb + ((long long)y1 * w + x1) * cs;
+    s0 += p[lane] * w11;
+    s1 += p[lane + 64] * w11;
+  }
+  const float nrm = sqrtf(pf_wave_sum(s0 * s0 + s1 * s1));
+  const float f0 = f[wid * 128 + lane], f1v = f[wid * 128 + lane + 64];
+  const float fd = pf_wave_sum(f0 * d0 + f1v * d1);
+  const float inv = 1.f / fmaxf(nrm, 1e-12f);
+  const float g0 = nrm > 1e-12f ? (d0 - f0 * fd) * inv : d0 * inv;
+  const float g1 = nrm > 1e-12f ? (d1 - f1v * fd) * inv : d1 * inv;
+  if (by0 && bx0) {
+    unsigned long long* p = accb + ((long long)y0 * w + x0) * 128;
+    fx_add(p + lane, w00 * g0);
+    fx_add(p + lane + 64, w00 * g1);
+  }
+  if (by0 && bx1) {
+    unsigned long long* p = accb + ((long long)y0 * w + x1) * 128;
+    fx_add(p + lane, w01 * g0);
+    fx_add(p + lane + 64, w01 * g1);
+  }
+  if (by1 && bx0) {
+    unsigned long long* p = accb + ((long long)y1 * w + x0) * 128;
+    fx_add(p + lane, w10 * g0);
+    fx_add(p + lane + 64, w10 * g1);
+  }
+  if (by1 && bx1) {
+    unsigned long long* p = accb + ((long long)y1 * w + x1) * 128;
+    fx_add(p + lane, w11 * g0);
+    fx_add(p + lane + 64, w11 * g1);
+  }
+}
+
+// dxf = normalize_bwd(T * acc_fm) + acc_x, one wave per pixel:
+// y = x / max(|x|, 1e-12); dx = (dy - y (y.dy)) / |x| (|x| > eps), dy / eps otherwise
+__global__ void l2norm_bwd_kernel(const float* __restrict__ x, int cs,
+                                  const unsigned long long* __restrict__ afm,
+                                  const unsigned long long* __restrict__ ax, long long npix,
+                                  float T, float* __restrict__ dx, int dcs) {
+  const int lane = threadIdx.x & 63;
+  const long long pix = blockIdx.x * (long long)(blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (pix >= npix) return;
+  const float x0 = x[pix * cs + lane], x1 = x[pix * cs + lane + 64];
+  const float nrm = sqrtf(pf_wave_sum(x0 * x0 + x1 * x1));
+  const float inv = 1.f / fmaxf(nrm, 1e-12f);
+  const float y0 = x0 * inv, y1 = x1 * inv;
+  const float g0 = T * (float)((double)(long long)afm[pix * 128 + lane] / FX_SCALE);
+  const float g1 = T * (float)((double)(long long)afm[pix * 128 + lane + 64] / FX_SCALE);
+  const float yg = pf_wave_sum(y0 * g0 + y1 * g1);
+  float r0 = nrm > 1e-12f ? (g0 - y0 * yg) * inv : g0 * inv;
+  float r1 = nrm > 1e-12f ? (g1 - y1 * yg) * inv : g1 * inv;
+  r0 += (float)((double)(long long)ax[pix * 128 + lane] / FX_SCALE);
+  r1 += (float)((double)(long long)ax[pix * 128 + lane + 64] / FX_SCALE);
+  dx[pix * dcs + lane] = r0;
+  dx[pix * dcs + lane + 64] = r1;
+}
+
 }  // namespace
+
+// Forward workspace layout (shared with posfeat_line2window_backward, which
+// reads the grid points, descriptors and T*normalize maps the forward left).
+struct L2WLayout {
+  size_t c1n, c1p, c2n, c2p, f1, f2, S, fm1, fm2, colp, total;
+};
+
+static L2WLayout l2w_layout(int b, int H1, int W1, int H2, int W2, int grid) {
+  L2WLayout L{};
+  const size_t n1 = (size_t)(H1 / grid) * (W1 / grid), n2 = (size_t)(H2 / grid) * (W2 / grid);
+  size_t cur = 0;
+  auto take = [&](size_t bytes) {
+    const size_t at = cur;
+    cur += pf_align(bytes, 256);
+    return at;
+  };
+  L.c1n = take(b * n1 * 8);
+  L.c1p = take(b * n1 * 8);
+  L.c2n = take(b * n2 * 8);
+  L.c2p = take(b * n2 * 8);
+  L.f1 = take(b * n1 * 512);
+  L.f2 = take(b * n2 * 512);
+  L.S = take(b * n1 * n2 * 4);
+  L.fm1 = take((size_t)b * (H1 / 4) * (W1 / 4) * 512);
+  L.fm2 = take((size_t)b * (H2 / 4) * (W2 / 4) * 512);
+  L.colp = take((size_t)b * COL_CH * n2 * sizeof(ColAcc));
+  L.total = cur;
+  return L;
+}
 
 extern "C" size_t posfeat_line2window_workspace(int b, int H1, int W1, int H2, int W2, int grid) {
   if (b <= 0 || grid <= 0) return 0;
-  const size_t n1 = (size_t)(H1 / grid) * (W1 / grid), n2 = (size_t)(H2 / grid) * (W2 / grid);
-  size_t s = 0;
-  s += pf_align(b * n1 * 2 * 4, 256) * 2;           // c1n, c1px
-  s += pf_align(b * n2 * 2 * 4, 256) * 2;           // c2n, c2px
-  s += pf_align(b * n1 * 128 * 4, 256);             // f1
-  s += pf_align(b * n2 * 128 * 4, 256);             // f2
-  s += pf_align(b * n1 * n2 * 4, 256);              // S
-  s += pf_align((size_t)b * (H1 / 4) * (W1 / 4) * 128 * 4, 256);  // fm1
-  s += pf_align((size_t)b * (H2 / 4) * (W2 / 4) * 128 * 4, 256);  // fm2
-  s += pf_align((size_t)b * COL_CH * n2 * sizeof(ColAcc), 256);   // column partials
-  return s;
+  return l2w_layout(b, H1, W1, H2, W2, grid).total;
 }
 
 extern "C" int posfeat_line2window(const float* xf1, int cs1, const float* xf2, int cs2, int b,
@@ -519,22 +821,18 @@ extern "C" int posfeat_line2window(const float* xf1, int cs1, const float* xf2, 
   if (ws_bytes < posfeat_line2window_workspace(b, H1, W1, H2, W2, grid)) return POSFEAT_E_WORKSPACE;
   const int n1 = (H1 / grid) * (W1 / grid), n2 = (H2 / grid) * (W2 / grid);
   hipStream_t st = pf_stream(stream);
-  char* p = static_cast<char*>(ws);
-  auto take = [&](size_t bytes) {
-    char* r = p;
-    p += pf_align(bytes, 256);
-    return reinterpret_cast<float*>(r);
-  };
-  float* c1n = take((size_t)b * n1 * 8);
-  float* c1p = take((size_t)b * n1 * 8);
-  float* c2n = take((size_t)b * n2 * 8);
-  float* c2p = take((size_t)b * n2 * 8);
-  float* f1 = take((size_t)b * n1 * 512);
-  float* f2 = take((size_t)b * n2 * 512);
-  float* S = take((size_t)b * n1 * n2 * 4);
-  float* fm1 = take((size_t)b * h1 * w1 * 512);
-  float* fm2 = take((size_t)b * h2 * w2 * 512);
-  ColAcc* colp = reinterpret_cast<ColAcc*>(take((size_t)b * COL_CH * n2 * sizeof(ColAcc)));
+  const L2WLayout lay = l2w_layout(b, H1, W1, H2, W2, grid);
+  char* wb = static_cast<char*>(ws);
+  float* c1n = reinterpret_cast<float*>(wb + lay.c1n);
+  float* c1p = reinterpret_cast<float*>(wb + lay.c1p);
+  float* c2n = reinterpret_cast<float*>(wb + lay.c2n);
+  float* c2p = reinterpret_cast<float*>(wb + lay.c2p);
+  float* f1 = reinterpret_cast<float*>(wb + lay.f1);
+  float* f2 = reinterpret_cast<float*>(wb + lay.f2);
+  float* S = reinterpret_cast<float*>(wb + lay.S);
+  float* fm1 = reinterpret_cast<float*>(wb + lay.fm1);
+  float* fm2 = reinterpret_cast<float*>(wb + lay.fm2);
+  ColAcc* colp = reinterpret_cast<ColAcc*>(wb + lay.colp);
   // grid points
   hipLaunchKernelGGL(grid_points_kernel, dim3((b * n1 + 255) / 256), dim3(256), 0, st, sel1, b,
                      H1, W1, grid, c1n, c1p);
@@ -607,6 +905,92 @@ extern "C" int posfeat_epipolar_loss(int b, int n, const float* F1, const float*
   hipLaunchKernelGGL(epipolar_loss_kernel, dim3(1), dim3(1024), 0, pf_stream(stream), b, n, F1,
                      F2, c1, c2, g1, g2, w1, w2, sg1, sg2, sw1, sw2, v1, v2, short_edge, grid_thr,
                      win_thr, weight_grid, weight_window, out);
+  PF_CHECK_LAUNCH();
+  return POSFEAT_OK;
+}
+
+extern "C" size_t posfeat_line2window_backward_workspace(int b, int H1, int W1, int H2, int W2,
+                                                        int grid) {
+  if (b <= 0 || grid <= 0) return 0;
+  const size_t n1 = (size_t)(H1 / grid) * (W1 / grid), n2 = (size_t)(H2 / grid) * (W2 / grid);
+  const size_t p1 = (size_t)b * (H1 / 4) * (W1 / 4) * 128, p2 = (size_t)b * (H2 / 4) * (W2 / 4) * 128;
+  return pf_align(b * n1 * 8, 256) + pf_align(b * n2 * 8, 256) + pf_align(b * n1 * 512, 256) +
+         pf_align(b * n2 * 512, 256) + 2 * pf_align(p1 * 8, 256) + 2 * pf_align(p2 * 8, 256);
+}
+
+extern "C" int posfeat_line2window_backward(
+    const float* xf1, int cs1, const float* xf2, int cs2, int b, int H1, int W1, int H2, int W2,
+    const float* F1, const float* F2, const posfeat_l2w_out* fwd, const void* fwd_ws,
+    float temperature, int grid, float window_size, float short_edge, float grid_thr,
+    float win_thr, float weight_grid, float weight_window, float* dxf1, int dcs1, float* dxf2,
+    int dcs2, void* ws, size_t ws_bytes, void* stream) {
+  (void)grid_thr;
+  if (!xf1 || !xf2 || !F1 || !F2 || !fwd || !fwd_ws || !dxf1 || !dxf2 || !ws)
+    return POSFEAT_E_INVALID;
+  if (!fwd->coord1 || !fwd->coord2 || !fwd->l1_exp_n || !fwd->l2_exp_n || !fwd->w1 || !fwd->w2 ||
+      !fwd->w1_std || !fwd->w2_std || !fwd->valid1 || !fwd->valid2)
+    return POSFEAT_E_INVALID;
+  if (weight_grid != 0.f) return POSFEAT_E_UNSUPPORTED;  // train_desc.yaml: weight_grid 0
+  if (b <= 0 || grid <= 0 || H1 % 4 || W1 % 4 || H2 % 4 || W2 % 4 || cs1 < 128 || cs2 < 128 ||
+      dcs1 < 128 || dcs2 < 128)
+    return POSFEAT_E_INVALID;
+  if (ws_bytes < posfeat_line2window_backward_workspace(b, H1, W1, H2, W2, grid))
+    return POSFEAT_E_WORKSPACE;
+  const int h1 = H1 / 4, w1 = W1 / 4, h2 = H2 / 4, w2 = W2 / 4;
+  const int win_h2 = (int)(window_size * h2), win_w2 = (int)(window_size * w2);
+  const int win_h1 = (int)(window_size * h1), win_w1 = (int)(window_size * w1);
+  if (win_h2 * win_w2 > MAX_WIN || win_h1 * win_w1 > MAX_WIN) return POSFEAT_E_UNSUPPORTED;
+  const int n1 = (H1 / grid) * (W1 / grid), n2 = (H2 / grid) * (W2 / grid);
+  hipStream_t st = pf_stream(stream);
+  const L2WLayout lay = l2w_layout(b, H1, W1, H2, W2, grid);
+  const char* fb = static_cast<const char*>(fwd_ws);
+  const float* c1n = reinterpret_cast<const float*>(fb + lay.c1n);
+  const float* c2n = reinterpret_cast<const float*>(fb + lay.c2n);
+  const float* f1 = reinterpret_cast<const float*>(fb + lay.f1);
+  const float* f2 = reinterpret_cast<const float*>(fb + lay.f2);
+  const float* fm1 = reinterpret_cast<const float*>(fb + lay.fm1);
+  const float* fm2 = reinterpret_cast<const float*>(fb + lay.fm2);
+  char* p = static_cast<char*>(ws);
+  auto take = [&](size_t bytes) {
+    char* r = p;
+    p += pf_align(bytes, 256);
+    return r;
+  };
+  float* gE1 = reinterpret_cast<float*>(take((size_t)b * n1 * 8));
+  float* gE2 = reinterpret_cast<float*>(take((size_t)b * n2 * 8));
+  float* dq1 = reinterpret_cast<float*>(take((size_t)b * n1 * 512));
+  float* dq2 = reinterpret_cast<float*>(take((size_t)b * n2 * 512));
+  const size_t p1 = (size_t)b * h1 * w1 * 128, p2 = (size_t)b * h2 * w2 * 128;
+  char* accs = p;
+  unsigned long long* afm1 = reinterpret_cast<unsigned long long*>(take(p1 * 8));
+  unsigned long long* ax1 = reinterpret_cast<unsigned long long*>(take(p1 * 8));
+  unsigned long long* afm2 = reinterpret_cast<unsigned long long*>(take(p2 * 8));
+  unsigned long long* ax2 = reinterpret_cast<unsigned long long*>(take(p2 * 8));
+  if (hipMemsetAsync(accs, 0, p - accs, st) != hipSuccess) return POSFEAT_E_HIP;
+  // d loss / d window expectations (w1 lives in image 2, w2 in image 1)
+  hipLaunchKernelGGL(epi_loss_bwd_kernel, dim3(1), dim3(1024), 0, st, b, n1, F1, fwd->coord1,
+                     fwd->w1, fwd->w1_std, fwd->valid1, short_edge, win_thr, weight_window,
+                     (float)((W2 - 1) / 2.0), (float)((H2 - 1) / 2.0), gE1);
+  hipLaunchKernelGGL(epi_loss_bwd_kernel, dim3(1), dim3(1024), 0, st, b, n2, F2, fwd->coord2,
+                     fwd->w2, fwd->w2_std, fwd->valid2, short_edge, win_thr, weight_window,
+                     (float)((W1 - 1) / 2.0), (float)((H1 - 1) / 2.0), gE2);
+  PF_CHECK_LAUNCH();
+  // window softmax backward: direction 1 scatters into image 2's map, and back
+  hipLaunchKernelGGL(window_bwd_kernel, dim3((b * n1 + 3) / 4), dim3(256), 0, st, f1, fm2,
+                     fwd->l1_exp_n, gE1, b, n1, h2, w2, win_h2, win_w2, window_size, dq1, afm2);
+  hipLaunchKernelGGL(window_bwd_kernel, dim3((b * n2 + 3) / 4), dim3(256), 0, st, f2, fm1,
+                     fwd->l2_exp_n, gE2, b, n2, h1, w1, win_h1, win_w1, window_size, dq2, afm1);
+  // query descriptors: normalize + grid_sample backward into the raw maps
+  hipLaunchKernelGGL(query_bwd_kernel, dim3((b * n1 + 3) / 4), dim3(256), 0, st, xf1, cs1, c1n, f1,
+                     dq1, b, n1, h1, w1, ax1);
+  hipLaunchKernelGGL(query_bwd_kernel, dim3((b * n2 + 3) / 4), dim3(256), 0, st, xf2, cs2, c2n, f2,
+                     dq2, b, n2, h2, w2, ax2);
+  PF_CHECK_LAUNCH();
+  const long long np1 = (long long)b * h1 * w1, np2 = (long long)b * h2 * w2;
+  hipLaunchKernelGGL(l2norm_bwd_kernel, dim3((unsigned)((np1 + 3) / 4)), dim3(256), 0, st, xf1, cs1,
+                     afm1, ax1, np1, temperature, dxf1, dcs1);
+  hipLaunchKernelGGL(l2norm_bwd_kernel, dim3((unsigned)((np2 + 3) / 4)), dim3(256), 0, st, xf2, cs2,
+                     afm2, ax2, np2, temperature, dxf2, dcs2);
   PF_CHECK_LAUNCH();
   return POSFEAT_OK;
 }

@@ -115,3 +115,94 @@ class KeypointTrainStep:
         if update:
             self.engine.sgd_step(grad, self.lr * scale)
         return out, grad
+
+
+class DescriptorLossGrad:
+    """Descriptor-training loss (configs/train_desc.yaml) with its gradient:
+    Preprocess_Line2Window (losses/preprocess.py:27-121) + EpipolarLoss_full
+    (losses/epipolarloss.py:38-101) forward, then dL/d local_map for both
+    images (what ``total_loss.backward()`` sends into the backbone at
+    managers/trainer.py:331).  Three HIP calls: ``posfeat_line2window``,
+    ``posfeat_epipolar_loss``, ``posfeat_line2window_backward``.
+
+    ``__call__(x1, x2, F1, F2, hw1, hw2, epoch, draws=None)`` with x1/x2 the NHWC
+    local maps ([b, h, w, >=128], channel stride = last dim) returns
+    (out[7] = loss, loss_g1, loss_w1, loss_g2, loss_w2, percent_g, percent_w;
+    dx1, dx2 NHWC [b, h, w, 128]; the processed dict's tensors)."""
+
+    def __init__(self, pre_cfg, epi_cfg):
+        from .losses.preprocess import Preprocess_Line2Window
+        Preprocess_Line2Window(pre_cfg)            # validates the configuration
+        if epi_cfg.get("weight_grid", 0) != 0 or not epi_cfg.get("use_std_as_weight", True):
+            raise NotImplementedError("posfeat_amd implements the configs/train_desc.yaml "
+                                      "EpipolarLoss_full (weight_grid 0, std weights)")
+        self.pre = pre_cfg
+        self.epi = epi_cfg
+        self.grid = int(pre_cfg["kps_generator_config"]["grid_size"])
+        self.line_step = int(pre_cfg.get("line_search_config", {}).get("line_step", 100))
+        self._ws = {}
+
+    def _buf(self, key, nbytes, dev):
+        t = self._ws.get(key)
+        if t is None or t.numel() < nbytes:
+            t = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)
+            self._ws[key] = t
+        return t
+
+    def __call__(self, x1, x2, F1, F2, hw1, hw2, epoch=1, draws=None):
+        import ctypes
+        b, h1, w1, cs1 = x1.shape
+        _, h2, w2, cs2 = x2.shape
+        (H1, W1), (H2, W2) = hw1, hw2
+        dev = x1.device
+        _lib.require_device(x1)
+        g = self.grid
+        n1, n2 = (H1 // g) * (W1 // g), (H2 // g) * (W2 // g)
+        T = float(min(self.pre["temperature_base"] + epoch, self.pre["temperature_max"]))
+        win = float(self.pre["window_size"])
+        if draws is None:
+            sel1 = torch.randint(0, g * g, (b, n1), device=dev, dtype=torch.int32)
+            sel2 = torch.randint(0, g * g, (b, n2), device=dev, dtype=torch.int32)
+            rand1 = torch.rand(b, n1, 2, device=dev)
+            rand2 = torch.rand(b, n2, 2, device=dev)
+        else:
+            sel1, sel2, rand1, rand2 = [d.to(dev).contiguous() for d in draws]
+            sel1, sel2 = sel1.reshape(b, n1).int(), sel2.reshape(b, n2).int()
+        F1 = F1.to(dev).float().contiguous()
+        F2 = F2.to(dev).float().contiguous()
+        f = lambda *s: torch.empty(*s, device=dev)  # noqa: E731
+        res = {"coord1": f(b, n1, 2), "coord2": f(b, n2, 2), "g1": f(b, n1, 2), "g2": f(b, n2, 2),
+               "g1_std": f(b, n1), "g2_std": f(b, n2), "l1_exp_n": f(b, n1, 2),
+               "l2_exp_n": f(b, n2, 2), "l1_org_n": f(b, n1, 2), "l2_org_n": f(b, n2, 2),
+               "valid1": torch.empty(b, n1, dtype=torch.uint8, device=dev),
+               "valid2": torch.empty(b, n2, dtype=torch.uint8, device=dev),
+               "w1": f(b, n1, 2), "w2": f(b, n2, 2), "w1_std": f(b, n1), "w2_std": f(b, n2)}
+        o = _lib.L2WOut(**{k: v.data_ptr() for k, v in res.items()})
+        L = lib()
+        need = L.posfeat_line2window_workspace(b, H1, W1, H2, W2, g)
+        fws = self._buf("fwd", need, dev)
+        check(L.posfeat_line2window(ptr(x1), cs1, ptr(x2), cs2, b, H1, W1, H2, W2, ptr(F1),
+                                    ptr(F2), ptr(sel1), ptr(sel2), ptr(rand1), ptr(rand2), T, g,
+                                    win, self.line_step, ctypes.byref(o), ptr(fws), need,
+                                    stream_ptr()))
+        out = torch.empty(7, device=dev)
+        short = float(min(H1, W1))
+        args = [res[k] for k in ("coord1", "coord2", "g1", "g2", "w1", "w2", "g1_std", "g2_std",
+                                 "w1_std", "w2_std")]
+        check(L.posfeat_epipolar_loss(b, n1, ptr(F1), ptr(F2), *[ptr(a) for a in args],
+                                      ptr(res["valid1"]), ptr(res["valid2"]), short,
+                                      float(self.epi["grid_cost_thr"]),
+                                      float(self.epi["win_cost_thr"]),
+                                      float(self.epi["weight_grid"]),
+                                      float(self.epi["weight_window"]), ptr(out), stream_ptr()))
+        dx1 = torch.empty(b, h1, w1, 128, device=dev)
+        dx2 = torch.empty(b, h2, w2, 128, device=dev)
+        bneed = L.posfeat_line2window_backward_workspace(b, H1, W1, H2, W2, g)
+        bws = self._buf("bwd", bneed, dev)
+        check(L.posfeat_line2window_backward(
+            ptr(x1), cs1, ptr(x2), cs2, b, H1, W1, H2, W2, ptr(F1), ptr(F2), ctypes.byref(o),
+            ptr(fws), T, g, win, short, float(self.epi["grid_cost_thr"]),
+            float(self.epi["win_cost_thr"]), float(self.epi["weight_grid"]),
+            float(self.epi["weight_window"]), ptr(dx1), 128, ptr(dx2), 128, ptr(bws), bneed,
+            stream_ptr()))
+        return out, dx1, dx2, res

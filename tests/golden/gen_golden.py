@@ -323,7 +323,56 @@ def gen_correlation(out):
     np.savez_compressed(out, **res)
 
 
-TRAIN_KP_CASES = {"a": (2, 64, 96, 5, 300), "b": (1, 96, 128, 6, 301)}
+DESC_GRAD_CASES = {"m": (1, 160, 224, 7), "l": (1, 240, 320, 8)}
+
+
+def gen_desc_grad(out):
+    """Descriptor-training loss gradient on the reference's own modules:
+    Preprocess_Line2Window + EpipolarLoss_full (train_desc.yaml configs) with
+    the local maps as autograd leaves, loss.backward() (trainer.py:331).
+    Case m: full dL/d maps; case l: every 4th pixel in each direction plus
+    full-map sums.  Draws replayed as in gen_correlation."""
+    res = {}
+    for tag, (b, H, W, seed) in DESC_GRAD_CASES.items():
+        xf1, xf2, _, _, F1, F2 = corr_inputs(b, H, W, seed)
+        xf1.requires_grad_(True)
+        xf2.requires_grad_(True)
+        inputs = {"im1": torch.zeros(b, 3, H, W), "im2": torch.zeros(b, 3, H, W), "F1": F1, "F2": F2}
+        kz = torch.zeros(b, 1, H, W)
+        outputs = {"preds1": {"global_map": xf1[:, :, ::4, ::4], "local_map": xf1,
+                              "local_point": kz},
+                   "preds2": {"global_map": xf2[:, :, ::4, ::4], "local_map": xf2,
+                              "local_point": kz}, "epoch": 0}
+        pre = ref_losses.Preprocess_Line2Window(DESC_CFG)
+        torch.manual_seed(100 + seed)
+        proc = pre(inputs, outputs)
+        loss, _ = ref_losses.EpipolarLoss_full(EPI_CFG)(inputs, outputs, proc)
+        loss.backward()
+        g1, g2 = xf1.grad.numpy(), xf2.grad.numpy()
+        torch.manual_seed(100 + seed)
+        k1, k2, _, _ = ref_putils.generate_kpts_regular_grid_random(
+            inputs, outputs, **DESC_CFG["kps_generator_config"])
+        n = k1.shape[1] * k1.shape[2]
+        r1 = torch.rand(b, n, 2)
+        r2 = torch.rand(b, n, 2)
+        for name, k in (("sel1", k1), ("sel2", k2)):
+            ix = torch.round((k[..., 0] + 1) / 2 * (W - 1)).long()
+            iy = torch.round((k[..., 1] + 1) / 2 * (H - 1)).long()
+            res["%s_%s" % (tag, name)] = ((iy % 16) * 16 + ix % 16).int().numpy()
+        res[tag + "_rand1"] = r1.numpy()
+        res[tag + "_rand2"] = r2.numpy()
+        res[tag + "_loss"] = loss.detach().numpy()
+        res[tag + "_w1"] = proc["feat1w_corloc"].detach().numpy()
+        if tag == "m":
+            res[tag + "_dxf1"], res[tag + "_dxf2"] = g1, g2
+        else:
+            res[tag + "_dxf1_sub"], res[tag + "_dxf2_sub"] = g1[:, :, ::4, ::4], g2[:, :, ::4, ::4]
+            res[tag + "_dxf_sums"] = np.array([g1.astype(np.float64).sum(), np.abs(g1).sum(),
+                                               g2.astype(np.float64).sum(), np.abs(g2).sum()])
+    np.savez_compressed(out, **res)
+
+
+TRAIN_KP_CASES ={"a": (2, 64, 96, 5, 300), "b": (1, 96, 128, 6, 301)}
 
 
 def gen_train_kp(out):
@@ -378,6 +427,8 @@ if __name__ == "__main__":
                              "train_kp"]
     if "train_kp" in which:
         gen_train_kp(os.path.join(HERE, "train_kp.npz"))
+    if "desc_grad" in which:
+        gen_desc_grad(os.path.join(HERE, "desc_grad.npz"))
     if "detector" in which:
         gen_detector(os.path.join(HERE, "detector.npz"))
     if "sampler" in which:
