@@ -314,6 +314,50 @@ long long posfeat_model_head_floats(void);
 int posfeat_model_head_backward(posfeat_model *m, const float *dlocal_point, float *grad,
                                 void *ws, size_t ws_bytes, void *stream);
 
+/* ------------------------------------------------------------------------
+ * Descriptor training (config 3, configs/train_desc.yaml: optimal_modules
+ * ['backbone'], Adam lr 1e-4).  Train-mode ResUNet (BatchNorm with batch
+ * statistics and running-stat update) forward and backward.
+ * Replaces: the autograd forward/backward of networks/DescNet.py:64-84 under
+ *   backbone.train() (managers/trainer.py:293-297, 330-331) and
+ *   torch.optim.Adam.step (trainer.py:118-119, 356).
+ * Layout: one packed fp32 parameter blob (per layer: conv weight [cout][Kpad]
+ *   as the engine packs it, conv bias when the layer has one, BN weight, BN
+ *   bias -- offsets from posfeat_bbtrain_layer offs[0..3]); the gradient blob
+ *   has the same layout; running mean / var live in a second blob
+ *   (offs[4], offs[5]).  Layer names follow posfeat_model_conv_spec.
+ * Workspaces: forward() fills `act` (posfeat_bbtrain_act_bytes, one per image
+ *   batch: im1 and im2 keep separate BN statistics, PoSFeat_model.py:144-145);
+ *   backward() reads the same `act`; `scratch` is shared.  All 256-B aligned.
+ * forward: img [b][3][h][w] NCHW; *local_map_nhwc = the NHWC local map
+ *   [b][h/4][w/4][128] inside `act`.  stats may be NULL (no running update).
+ * backward: dlocal_map NHWC (pixel stride dcs); grad = (accumulate ? grad : 0)
+ *   + dL/d params.  h and w must be multiples of 16.
+ * posfeat_adam: torch.optim.Adam (no amsgrad) on n floats; g is scaled by
+ *   grad_scale first (1/world after a summing all-reduce = DDP's mean). */
+typedef struct posfeat_bbtrain posfeat_bbtrain;
+int posfeat_bbtrain_num_layers(void);
+int posfeat_bbtrain_layer(int i, const char **name, int *cin, int *cout, int *k, int *stride,
+                          int *has_bias, long long *offs /* [6] */);
+long long posfeat_bbtrain_param_floats(void);
+long long posfeat_bbtrain_stat_floats(void);
+int posfeat_bbtrain_create(int batch, int h, int w, posfeat_bbtrain **out);
+size_t posfeat_bbtrain_act_bytes(const posfeat_bbtrain *m);
+size_t posfeat_bbtrain_scratch_bytes(const posfeat_bbtrain *m);
+int posfeat_bbtrain_forward(posfeat_bbtrain *m, const float *params, float *stats, float momentum,
+                            const float *img_nchw, void *act, void *scratch,
+                            float **local_map_nhwc, void *stream);
+int posfeat_bbtrain_backward(posfeat_bbtrain *m, const float *params, const void *act,
+                             const float *dlocal_map_nhwc, int dcs, float *grad, int accumulate,
+                             void *scratch, void *stream);
+int posfeat_bbtrain_set_timing(posfeat_bbtrain *m, int enable);
+int posfeat_bbtrain_timing(posfeat_bbtrain *m, const char *prefix, double *ms, double *flops,
+                           int *launches);
+void posfeat_bbtrain_destroy(posfeat_bbtrain *m);
+int posfeat_adam(float *p, const float *g, float *m, float *v, long long n, float lr, float beta1,
+                 float beta2, float eps, float weight_decay, long long step, float grad_scale,
+                 void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -14,32 +14,37 @@ import torch.nn.functional as F
 BN_EPS = 1e-5
 
 
-def _bn(x, sd, p):
+def _bn(x, sd, p, train=False):
+    """BatchNorm2d; train=True: batch statistics and the in-place running-stat
+    update of nn.BatchNorm2d.train() (momentum 0.1)."""
     return F.batch_norm(x, sd[p + ".running_mean"], sd[p + ".running_var"],
-                        sd[p + ".weight"], sd[p + ".bias"], training=False, eps=BN_EPS)
+                        sd[p + ".weight"], sd[p + ".bias"], training=train, momentum=0.1,
+                        eps=BN_EPS)
 
 
-def _bottleneck(x, sd, p, stride, has_ds):
+def _bottleneck(x, sd, p, stride, has_ds, train=False):
     """torchvision Bottleneck.forward (restated)."""
     idt = x
-    out = F.relu(_bn(F.conv2d(x, sd[p + ".conv1.weight"]), sd, p + ".bn1"))
-    out = F.relu(_bn(F.conv2d(out, sd[p + ".conv2.weight"], stride=stride, padding=1), sd, p + ".bn2"))
-    out = _bn(F.conv2d(out, sd[p + ".conv3.weight"]), sd, p + ".bn3")
+    out = F.relu(_bn(F.conv2d(x, sd[p + ".conv1.weight"]), sd, p + ".bn1", train))
+    out = F.relu(_bn(F.conv2d(out, sd[p + ".conv2.weight"], stride=stride, padding=1), sd,
+                     p + ".bn2", train))
+    out = _bn(F.conv2d(out, sd[p + ".conv3.weight"]), sd, p + ".bn3", train)
     if has_ds:
-        idt = _bn(F.conv2d(x, sd[p + ".downsample.0.weight"], stride=stride), sd, p + ".downsample.1")
+        idt = _bn(F.conv2d(x, sd[p + ".downsample.0.weight"], stride=stride), sd,
+                  p + ".downsample.1", train)
     return F.relu(out + idt)
 
 
-def _conv_bn_elu(x, sd, p, k):
+def _conv_bn_elu(x, sd, p, k, train=False):
     """DescNet.conv.forward: elu(bn(conv(x))) with padding (k-1)//2 (DescNet.py:167-179)."""
     y = F.conv2d(x, sd[p + ".conv.weight"], sd[p + ".conv.bias"], padding=(k - 1) // 2)
-    return F.elu(_bn(y, sd, p + ".bn"))
+    return F.elu(_bn(y, sd, p + ".bn", train))
 
 
-def _upconv(x, sd, p):
+def _upconv(x, sd, p, train=False):
     """DescNet.upconv.forward: bilinear x2 align_corners=True then conv (DescNet.py:182-190)."""
     x = F.interpolate(x, scale_factor=2, align_corners=True, mode="bilinear")
-    return _conv_bn_elu(x, sd, p + ".conv", 3)
+    return _conv_bn_elu(x, sd, p + ".conv", 3, train)
 
 
 def _skipconnect(x1, x2):
@@ -50,25 +55,27 @@ def _skipconnect(x1, x2):
     return torch.cat([x2, x1], dim=1)
 
 
-def resunet_forward(sd, x):
-    """ResUNet.forward (DescNet.py:64-84) with the ResNet-50 encoder restated."""
-    x = F.relu(_bn(F.conv2d(x, sd["firstconv.weight"], stride=2, padding=3), sd, "firstbn"))
+def resunet_forward(sd, x, train=False):
+    """ResUNet.forward (DescNet.py:64-84) with the ResNet-50 encoder restated.
+    train=True: BatchNorm in training mode (backbone.train(), trainer.py:293-296);
+    the running statistics in ``sd`` are updated in place."""
+    x = F.relu(_bn(F.conv2d(x, sd["firstconv.weight"], stride=2, padding=3), sd, "firstbn", train))
     x_first = F.max_pool2d(x, 3, 2, 1)
     h = x_first
     feats = []
     for lname, blocks, stride in (("layer1", 3, 1), ("layer2", 4, 2), ("layer3", 6, 2)):
         for bi in range(blocks):
-            h = _bottleneck(h, sd, "%s.%d" % (lname, bi), stride if bi == 0 else 1, bi == 0)
+            h = _bottleneck(h, sd, "%s.%d" % (lname, bi), stride if bi == 0 else 1, bi == 0, train)
         feats.append(h)
     x1, x2, x3 = feats
-    x_coarse = _conv_bn_elu(x3, sd, "conv_coarse", 1)
-    x = _upconv(x3, sd, "upconv3")
+    x_coarse = _conv_bn_elu(x3, sd, "conv_coarse", 1, train)
+    x = _upconv(x3, sd, "upconv3", train)
     x = _skipconnect(x2, x)
-    x = _conv_bn_elu(x, sd, "iconv3", 3)
-    x = _upconv(x, sd, "upconv2")
+    x = _conv_bn_elu(x, sd, "iconv3", 3, train)
+    x = _upconv(x, sd, "upconv2", train)
     x = _skipconnect(x1, x)
-    x = _conv_bn_elu(x, sd, "iconv2", 3)
-    x_fine = _conv_bn_elu(x, sd, "conv_fine", 1)
+    x = _conv_bn_elu(x, sd, "iconv2", 3, train)
+    x_fine = _conv_bn_elu(x, sd, "conv_fine", 1, train)
     return {"global_map": x_coarse, "local_map": x_fine, "local_map_small": x_first}
 
 

@@ -97,6 +97,23 @@ SIGNATURES = {
     "posfeat_model_head_floats": (c_ll, []),
     "posfeat_model_head_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
                                             c_void_p]),
+    "posfeat_bbtrain_num_layers": (c_int, []),
+    "posfeat_bbtrain_layer": (c_int, [c_int, ctypes.POINTER(ctypes.c_char_p), P_int, P_int, P_int,
+                                      P_int, P_int, ctypes.POINTER(c_ll)]),
+    "posfeat_bbtrain_param_floats": (c_ll, []),
+    "posfeat_bbtrain_stat_floats": (c_ll, []),
+    "posfeat_bbtrain_create": (c_int, [c_int, c_int, c_int, ctypes.POINTER(c_void_p)]),
+    "posfeat_bbtrain_act_bytes": (c_size_t, [c_void_p]),
+    "posfeat_bbtrain_scratch_bytes": (c_size_t, [c_void_p]),
+    "posfeat_bbtrain_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_void_p,
+                                        c_void_p, ctypes.POINTER(c_void_p), c_void_p]),
+    "posfeat_bbtrain_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
+                                         c_int, c_void_p, c_void_p]),
+    "posfeat_bbtrain_set_timing": (c_int, [c_void_p, c_int]),
+    "posfeat_bbtrain_timing": (c_int, [c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
+                                       ctypes.POINTER(ctypes.c_double), P_int]),
+    "posfeat_bbtrain_destroy": (None, [c_void_p]),
+    "posfeat_adam": (c_int, [c_void_p] * 4 + [c_ll] + [c_float] * 5 + [c_ll, c_float, c_void_p]),
     "posfeat_line2window_backward_workspace": (c_size_t, [c_int] * 6),
     "posfeat_line2window_backward": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int,
                                              c_int, c_int, c_void_p, c_void_p,
@@ -165,6 +182,22 @@ def stream_ptr(device=None):
 
 def ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def bbtrain_table():
+    """Train-mode backbone layer table: ([(name, cin, cout, k, stride, has_bias,
+    (w_off, b_off, g_off, be_off, rm_off, rv_off))], param_floats, stat_floats)."""
+    L = lib()
+    layers = []
+    for i in range(L.posfeat_bbtrain_num_layers()):
+        name = ctypes.c_char_p()
+        ci, co, k, s, hb = c_int(), c_int(), c_int(), c_int(), c_int()
+        offs = (c_ll * 6)()
+        check(L.posfeat_bbtrain_layer(i, ctypes.byref(name), ctypes.byref(ci), ctypes.byref(co),
+                                      ctypes.byref(k), ctypes.byref(s), ctypes.byref(hb), offs))
+        layers.append((name.value.decode(), ci.value, co.value, k.value, s.value, bool(hb.value),
+                       tuple(int(o) for o in offs)))
+    return layers, int(L.posfeat_bbtrain_param_floats()), int(L.posfeat_bbtrain_stat_floats())
 
 
 def model_specs():

@@ -1,0 +1,329 @@
+// bbtrain_kernels.h -- device kernels of the train-mode ResUNet (bbtrain.hip):
+// BatchNorm statistics / apply / backward, stride-2 zero insertion, max-pool
+// and x2-upsample adjoints, Adam.  Included by bbtrain.hip only.
+#pragma once
+#include "common.h"
+
+namespace bbt {
+
+enum { ACT_NONE = 0, ACT_RELU = 1, ACT_ELU = 2 };
+constexpr float BN_EPS = 1e-5f;
+
+__device__ __forceinline__ float act_grad(int act, float a) {
+  return act == ACT_RELU ? (a > 0.f ? 1.f : 0.f) : act == ACT_ELU ? (a > 0.f ? 1.f : a + 1.f) : 1.f;
+}
+
+// BatchNorm partial sums: block = (pixel chunk, group of <= 64 channel quads);
+// lanes own one quad each, the R = 256/qpb rows of the block stride over the
+// chunk's pixels; fp64 accumulation, LDS sum over rows, part[chunk][2][C].
+// MODE 0 (forward statistics): sums of y and y^2.
+// MODE 1 (backward): g = da act'(a); sums of g and g x^, x^ = (y - mean) rstd.
+template <int MODE>
+__global__ __launch_bounds__(256) void bn_partial_kernel(
+    const float* __restrict__ y, long long P, int C, int chunk, const float* __restrict__ a, int acs,
+    const float* __restrict__ da, int dacs, int act, const float* __restrict__ mean,
+    const float* __restrict__ rstd, double* __restrict__ part) {
+  __shared__ double red[256][8];
+  const int c4n = C / 4, qpb = c4n < 64 ? c4n : 64, R = 256 / qpb;
+  const int tid = threadIdx.x, ql = tid % qpb, r = tid / qpb;
+  const int q = blockIdx.y * qpb + ql;
+  const long long p0 = (long long)blockIdx.x * chunk;
+  const long long p1 = p0 + chunk < P ? p0 + chunk : P;
+  double s0[4] = {0, 0, 0, 0}, s1[4] = {0, 0, 0, 0};
+  f32x4 mu = {0, 0, 0, 0}, rs = {0, 0, 0, 0};
+  if (MODE == 1) {
+    mu = *reinterpret_cast<const f32x4*>(mean + q * 4);
+    rs = *reinterpret_cast<const f32x4*>(rstd + q * 4);
+  }
+  for (long long p = p0 + r; p < p1; p += R) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(y + p * C + q * 4);
+    if (MODE == 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        s0[j] += (double)v[j];
+        s1[j] += (double)v[j] * (double)v[j];
+      }
+    } else {
+      const f32x4 gd = *reinterpret_cast<const f32x4*>(da + p * dacs + q * 4);
+      f32x4 av = {0, 0, 0, 0};
+      if (act != ACT_NONE) av = *reinterpret_cast<const f32x4*>(a + p * acs + q * 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float g = gd[j] * act_grad(act, av[j]);
+        const float xh = (v[j] - mu[j]) * rs[j];
+        s0[j] += (double)g;
+        s1[j] += (double)g * (double)xh;
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    red[tid][j] = s0[j];
+    red[tid][4 + j] = s1[j];
+  }
+  __syncthreads();
+  if (r == 0) {
+    for (int rr = 1; rr < R; ++rr)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[tid][j] += red[rr * qpb + ql][j];
+    double* o = part + (long long)blockIdx.x * 2 * C;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      o[q * 4 + j] = red[tid][j];
+      o[C + q * 4 + j] = red[tid][4 + j];
+    }
+  }
+}
+
+// batch mean / rstd (biased variance) and the running-stat update
+// (torch: running = (1 - m) running + m batch, with the unbiased variance)
+__global__ void bn_stats_final_kernel(const double* __restrict__ part, int nchunk, int C, long long P,
+                                      float mom, float* __restrict__ mean, float* __restrict__ rstd,
+                                      float* __restrict__ rm, float* __restrict__ rv) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0, ss = 0.0;
+  for (int k = 0; k < nchunk; ++k) {
+    s += part[(long long)k * 2 * C + c];
+    ss += part[(long long)k * 2 * C + C + c];
+  }
+  const double mu = s / (double)P;
+  double var = ss / (double)P - mu * mu;
+  var = var > 0.0 ? var : 0.0;
+  mean[c] = (float)mu;
+  rstd[c] = (float)(1.0 / sqrt(var + (double)BN_EPS));
+  if (rm) {
+    const float vu = (float)(P > 1 ? var * (double)P / (double)(P - 1) : var);
+    rm[c] = (1.f - mom) * rm[c] + mom * (float)mu;
+    rv[c] = (1.f - mom) * rv[c] + mom * vu;
+  }
+}
+
+// out = act(gamma (y - mean) rstd + beta [+ res])
+__global__ void bn_apply_kernel(const float* __restrict__ y, long long P, int c4n,
+                                const float* __restrict__ mean, const float* __restrict__ rstd,
+                                const float* __restrict__ gam, const float* __restrict__ bet,
+                                const float* __restrict__ res, int rcs, int act,
+                                float* __restrict__ out, int ocs) {
+  const long long total = P * c4n;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int q = (int)(i % c4n);
+    const long long p = i / c4n;
+    const f32x4 v = *reinterpret_cast<const f32x4*>(y + i * 4);
+    const f32x4 mu = *reinterpret_cast<const f32x4*>(mean + q * 4);
+    const f32x4 rs = *reinterpret_cast<const f32x4*>(rstd + q * 4);
+    const f32x4 g = *reinterpret_cast<const f32x4*>(gam + q * 4);
+    const f32x4 b = *reinterpret_cast<const f32x4*>(bet + q * 4);
+    f32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = g[j] * (v[j] - mu[j]) * rs[j] + b[j];
+    if (res) o += *reinterpret_cast<const f32x4*>(res + p * rcs + q * 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      o[j] = act == ACT_RELU ? fmaxf(o[j], 0.f) : act == ACT_ELU ? pf_elu(o[j]) : o[j];
+    *reinterpret_cast<f32x4*>(out + p * ocs + q * 4) = o;
+  }
+}
+
+// dgamma / dbeta (accumulated over the step's batches) and the apply coefficients
+__global__ void bn_bwd_final_kernel(const double* __restrict__ part, int nchunk, int C, long long P,
+                                    const float* __restrict__ gam, const float* __restrict__ rstd,
+                                    float* __restrict__ dgam, float* __restrict__ dbet, int acc,
+                                    float* __restrict__ coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double sg = 0.0, sgx = 0.0;
+  for (int k = 0; k < nchunk; ++k) {
+    sg += part[(long long)k * 2 * C + c];
+    sgx += part[(long long)k * 2 * C + C + c];
+  }
+  dgam[c] = acc ? dgam[c] + (float)sgx : (float)sgx;
+  dbet[c] = acc ? dbet[c] + (float)sg : (float)sg;
+  coef[c] = gam[c] * rstd[c];
+  coef[C + c] = (float)(sg / (double)P);
+  coef[2 * C + c] = (float)(sgx / (double)P);
+}
+
+// dy = gamma rstd (g - E[g] - x^ E[g x^]) (compact); gout = g (optional)
+__global__ void bn_bwd_apply_kernel(const float* __restrict__ y, long long P, int c4n,
+                                    const float* __restrict__ a, int acs,
+                                    const float* __restrict__ da, int dacs, int act,
+                                    const float* __restrict__ mean, const float* __restrict__ rstd,
+                                    const float* __restrict__ coef, float* __restrict__ dy,
+                                    float* __restrict__ gout) {
+  const int C = c4n * 4;
+  const long long total = P * c4n;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int q = (int)(i % c4n);
+    const long long p = i / c4n;
+    const f32x4 v = *reinterpret_cast<const f32x4*>(y + i * 4);
+    const f32x4 gd = *reinterpret_cast<const f32x4*>(da + p * dacs + q * 4);
+    f32x4 av = {0, 0, 0, 0};
+    if (act != ACT_NONE) av = *reinterpret_cast<const f32x4*>(a + p * acs + q * 4);
+    const f32x4 mu = *reinterpret_cast<const f32x4*>(mean + q * 4);
+    const f32x4 rs = *reinterpret_cast<const f32x4*>(rstd + q * 4);
+    const f32x4 c0 = *reinterpret_cast<const f32x4*>(coef + q * 4);
+    const f32x4 c1 = *reinterpret_cast<const f32x4*>(coef + C + q * 4);
+    const f32x4 c2 = *reinterpret_cast<const f32x4*>(coef + 2 * C + q * 4);
+    f32x4 g, o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      g[j] = gd[j] * act_grad(act, av[j]);
+      const float xh = (v[j] - mu[j]) * rs[j];
+      o[j] = c0[j] * (g[j] - c1[j] - xh * c2[j]);
+    }
+    *reinterpret_cast<f32x4*>(dy + i * 4) = o;
+    if (gout) *reinterpret_cast<f32x4*>(gout + i * 4) = g;
+  }
+}
+
+// dst [n][h][w][C] = src [n][h/2][w/2][C] at even (y, x), 0 elsewhere: the
+// input grid of a stride-2 conv (its output pixel i reads input 2i - pad + k)
+__global__ void zero_insert_kernel(const float* __restrict__ src, int n, int h, int w, int c4n,
+                                   float* __restrict__ dst) {
+  const int oh = (h + 1) / 2, ow = (w + 1) / 2;
+  const long long total = (long long)n * h * w * c4n;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int q = (int)(i % c4n);
+    long long p = i / c4n;
+    const int x = (int)(p % w);
+    p /= w;
+    const int yy = (int)(p % h);
+    const int b = (int)(p / h);
+    f32x4 v = {0, 0, 0, 0};
+    if (!(x & 1) && !(yy & 1))
+      v = *reinterpret_cast<const f32x4*>(
+          src + ((((long long)b * oh + (yy >> 1)) * ow + (x >> 1)) * c4n + q) * 4);
+    *reinterpret_cast<f32x4*>(dst + i * 4) = v;
+  }
+}
+
+// max_pool2d(3, 2, 1) adjoint as a gather: input pixel (iy, ix) collects the
+// gradient of every window whose arg-max it is; the arg-max is recomputed with
+// ATen's rule (scan order, replace on '>' or NaN, start at the window's first
+// valid pixel).
+__global__ void maxpool_adjoint_kernel(const float* __restrict__ x, int xcs, int n, int h, int w,
+                                       int c4n, const float* __restrict__ g, int gcs, int oh, int ow,
+                                       float* __restrict__ dx, int dxcs) {
+  const long long total = (long long)n * h * w * c4n;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int q = (int)(i % c4n);
+    long long p = i / c4n;
+    const int ix = (int)(p % w);
+    p /= w;
+    const int iy = (int)(p % h);
+    const int b = (int)(p / h);
+    const float* xb = x + (long long)b * h * w * xcs + q * 4;
+    f32x4 acc = {0, 0, 0, 0};
+    const int oy0 = iy / 2, oy1 = min(oh - 1, (iy + 1) / 2);
+    const int ox0 = ix / 2, ox1 = min(ow - 1, (ix + 1) / 2);
+    for (int oy = oy0; oy <= oy1; ++oy) {
+      for (int ox = ox0; ox <= ox1; ++ox) {
+        const int ys = max(2 * oy - 1, 0), ye = min(2 * oy + 1, h - 1);
+        const int xs = max(2 * ox - 1, 0), xe = min(2 * ox + 1, w - 1);
+        f32x4 mv = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+        int my[4] = {ys, ys, ys, ys}, mx[4] = {xs, xs, xs, xs};
+        for (int yy = ys; yy <= ye; ++yy)
+          for (int xx = xs; xx <= xe; ++xx) {
+            const f32x4 v = *reinterpret_cast<const f32x4*>(xb + ((long long)yy * w + xx) * xcs);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (v[j] > mv[j] || isnan(v[j])) {
+                mv[j] = v[j];
+                my[j] = yy;
+                mx[j] = xx;
+              }
+          }
+        const f32x4 gv =
+            *reinterpret_cast<const f32x4*>(g + (((long long)b * oh + oy) * ow + ox) * gcs + q * 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (my[j] == iy && mx[j] == ix) acc[j] += gv[j];
+      }
+    }
+    *reinterpret_cast<f32x4*>(dx + (((long long)b * h + iy) * w + ix) * dxcs + q * 4) = acc;
+  }
+}
+
+// bilinear x2, align_corners=True (fmap.hip upsample2x_ac_kernel): weight of
+// output o on input q, with the forward's own float arithmetic
+__device__ __forceinline__ float ac_w(int o, int q, float sc, int nin) {
+  const float r = sc * o;
+  const int i0 = (int)r;
+  const int i1 = i0 + (i0 < nin - 1 ? 1 : 0);
+  const float l = r - i0;
+  return (i0 == q ? 1.f - l : 0.f) + (i1 == q ? l : 0.f);
+}
+
+// t[b][oy][qx][c] = sum_ox w(ox, qx) g[b][oy][ox][c]
+__global__ void up2_adj_x_kernel(const float* __restrict__ g, int gcs, int nb, int OH, int OW, int w,
+                                 int c4n, float* __restrict__ t) {
+  const float sc = OW > 1 ? (float)(w - 1) / (float)(OW - 1) : 0.f;
+  const long long total = (long long)nb * OH * w * c4n;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int q = (int)(i % c4n);
+    const long long p = i / c4n;
+    const int qx = (int)(p % w);
+    const long long row = p / w;
+    const float* gr = g + row * OW * gcs + q * 4;
+    f32x4 acc = {0, 0, 0, 0};
+    const int o0 = max(0, 2 * qx - 2), o1 = min(OW - 1, 2 * qx + 4);
+    for (int ox = o0; ox <= o1; ++ox) {
+      const float wt = ac_w(ox, qx, sc, w);
+      if (wt != 0.f) acc += wt * *reinterpret_cast<const f32x4*>(gr + (long long)ox * gcs);
+    }
+    *reinterpret_cast<f32x4*>(t + p * (c4n * 4) + q * 4) = acc;
+  }
+}
+
+// d[b][qy][qx][c] = sum_oy w(oy, qy) t[b][oy][qx][c]
+__global__ void up2_adj_y_kernel(const float* __restrict__ t, int nb, int OH, int h, int w, int c4n,
+                                 float* __restrict__ d, int dcs) {
+  const float sc = OH > 1 ? (float)(h - 1) / (float)(OH - 1) : 0.f;
+  const int C = c4n * 4;
+  const long long total = (long long)nb * h * w * c4n;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int q = (int)(i % c4n);
+    long long p = i / c4n;
+    const int qx = (int)(p % w);
+    p /= w;
+    const int qy = (int)(p % h);
+    const int b = (int)(p / h);
+    f32x4 acc = {0, 0, 0, 0};
+    const int o0 = max(0, 2 * qy - 2), o1 = min(OH - 1, 2 * qy + 4);
+    for (int oy = o0; oy <= o1; ++oy) {
+      const float wt = ac_w(oy, qy, sc, h);
+      if (wt != 0.f)
+        acc += wt * *reinterpret_cast<const f32x4*>(t + (((long long)b * OH + oy) * w + qx) * C + q * 4);
+    }
+    *reinterpret_cast<f32x4*>(d + (((long long)b * h + qy) * w + qx) * dcs + q * 4) = acc;
+  }
+}
+
+// torch.optim.Adam (no amsgrad): m.lerp_(g, 1-b1); v = b2 v + (1-b2) g^2;
+// p += (-lr/bc1) * m / (sqrt(v)/sqrt(bc2) + eps)   (torch/optim/adam.py)
+__global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                            float* __restrict__ v, long long n, float neg_step, float b1, float b2,
+                            float eps, float bc2_sqrt, float gscale, float wd) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    float gi = g[i] * gscale;
+    if (wd != 0.f) gi += wd * p[i];
+    const float w1 = 1.f - b1;
+    float mi = m[i];
+    mi = w1 < 0.5f ? mi + w1 * (gi - mi) : gi - (gi - mi) * (1.f - w1);
+    const float vi = v[i] * b2 + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    const float den = sqrtf(vi) / bc2_sqrt + eps;
+    p[i] = p[i] + neg_step * (mi / den);
+  }
+}
+
+}  // namespace bbt

@@ -358,9 +358,9 @@ void plan(posfeat_model* m) {
     alloc(m->upt, B * H * w4 * 192);
     alloc(m->dc1, B * h4 * w4 * 192);
     alloc(m->wt2, (size_t)256 * posfeat_conv_packed_k(128, 3, 3));
-    size_t wg = pf_conv_wgrad_ws_bytes((int)B, (int)H, (int)W, 256, 128, 3, 3);
-    wg = std::max(wg, pf_conv_wgrad_ws_bytes((int)B, (int)H, (int)W, 4, 64, 3, 3));
-    wg = std::max(wg, pf_conv_wgrad_ws_bytes((int)B, (int)h4, (int)w4, 192, 192, 3, 3));
+    size_t wg = pf_conv_wgrad_ws_bytes((int)B, (int)H, (int)W, 256, 128, 3, 3, 1);
+    wg = std::max(wg, pf_conv_wgrad_ws_bytes((int)B, (int)H, (int)W, 4, 64, 3, 3, 1));
+    wg = std::max(wg, pf_conv_wgrad_ws_bytes((int)B, (int)h4, (int)w4, 192, 192, 3, 3, 1));
     alloc(m->wgws, wg / 4 + 4);
     const size_t ib = std::max(pf_in_bwd_ws_bytes((int)B, (int)(H * W), 64),
                                pf_in_bwd_ws_bytes((int)B, (int)(h4 * w4), 192));
@@ -574,8 +574,8 @@ int head_backward(Ctx& c, const float* dlp, float* grad) {
   }));
   // conv2: weight gradient over the materialised cat[up4(L), IN(convimg)]
   PF_TRY(timed(c, "bwdconv:head.conv2.wgrad", 2.0 * B * H * W * 128.0 * 256 * 9, [&] {
-    return pf_conv_wgrad(dc2, 128, hcat, 256, B, H, W, 256, 128, 3, 3, G("head.conv2"),
-                         GB("head.conv2"), c.f(m->wgws), wgb, c.st);
+    return pf_conv_wgrad(dc2, 128, hcat, 256, B, H, W, 256, 128, 3, 3, 1, G("head.conv2"),
+                         GB("head.conv2"), 0, c.f(m->wgws), wgb, c.st);
   }));
   // conv2: input gradient = conv of dc2 with the flipped, transposed kernel
   PF_TRY(timed(c, "bwd:dgrad_weights", 0, [&] {
@@ -595,8 +595,8 @@ int head_backward(Ctx& c, const float* dlp, float* grad) {
                           nullptr, c.st);
   }));
   PF_TRY(timed(c, "bwdconv:head.convimg.wgrad", 2.0 * B * H * W * 64.0 * 3 * 9, [&] {
-    return pf_conv_wgrad(dhcat + 192, 256, c.f(m->img4), 4, B, H, W, 4, 64, 3, 3,
-                         G("head.convimg"), GB("head.convimg"), c.f(m->wgws), wgb, c.st);
+    return pf_conv_wgrad(dhcat + 192, 256, c.f(m->img4), 4, B, H, W, 4, 64, 3, 3, 1,
+                         G("head.convimg"), GB("head.convimg"), 0, c.f(m->wgws), wgb, c.st);
   }));
   // x4 upsample adjoint of the 192 upsampled channels -> d PReLU(IN(conv1))
   PF_TRY(timed(c, "bwd:up4_adjoint", 0, [&] {
@@ -609,8 +609,8 @@ int head_backward(Ctx& c, const float* dlp, float* grad) {
                           192, c.f(m->inbws), &c1s, &c1n, c.st);
   }));
   PF_TRY(timed(c, "bwdconv:head.conv1.wgrad", 2.0 * B * h4 * w4 * 192.0 * 192 * 9, [&] {
-    return pf_conv_wgrad(dc1, 192, c.f(m->headcat), 192, B, h4, w4, 192, 192, 3, 3,
-                         G("head.conv1"), GB("head.conv1"), c.f(m->wgws), wgb, c.st);
+    return pf_conv_wgrad(dc1, 192, c.f(m->headcat), 192, B, h4, w4, 192, 192, 3, 3, 1,
+                         G("head.conv1"), GB("head.conv1"), 0, c.f(m->wgws), wgb, c.st);
   }));
   PF_TRY(timed(c, "bwd:scalars", 0, [&] {
     return pf_head_scalars(t2s, t2n, c1s, c1n, GB("head.conv3"), GB("head.prelu"), c.st);

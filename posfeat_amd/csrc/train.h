@@ -5,12 +5,14 @@
 
 #include "../../include/posfeat_hip.h"
 
-// dW [Cout][Kpad] (engine-packed K order) and db [Cout] of a stride-1 "same"
-// conv: dw = sum_p dy[p] (x) im2col(x)[p].  Cin % 32 == 0 or Cin == 4.
-size_t pf_conv_wgrad_ws_bytes(int n, int H, int W, int Cin, int Cout, int KH, int KW);
+// dW [Cout][Kpad] (engine-packed K order) and db [Cout] of a conv with
+// padding (K-1)/2 and stride 1 or 2 over an H x W input (dy at the output
+// size): dw = sum_p dy[p] (x) im2col(x)[p].  Cin % 32 == 0 or Cin == 4.
+// acc != 0 adds to dw / db instead of overwriting them.
+size_t pf_conv_wgrad_ws_bytes(int n, int H, int W, int Cin, int Cout, int KH, int KW, int stride);
 int pf_conv_wgrad(const float* dy, int ldy, const float* x, int xcs, int n, int H, int W, int Cin,
-                  int Cout, int KH, int KW, float* dw, float* db, void* ws, size_t ws_bytes,
-                  hipStream_t st);
+                  int Cout, int KH, int KW, int stride, float* dw, float* db, int acc, void* ws,
+                  size_t ws_bytes, hipStream_t st);
 // packed weights of the input-gradient conv (flipped taps, cin <-> cout)
 int pf_dgrad_weights(const float* w, int Cout, int Cin, int KH, int KW, float* wt, hipStream_t st);
 // adjoint of the bilinear (align_corners=False) resize h x w -> OH x OW over C

@@ -36,7 +36,9 @@ struct WgradArgs {
   int ldy;
   const float* x;
   int xcs;
-  int H, W, Cin, KH, KW, pad;
+  int H, W, Cin, KH, KW, pad;  // H, W: dy (output) dims
+  int Hin, Win, stride;         // input dims and conv stride (halo kernel: stride 1)
+  long long d_row, d_img;       // x offset corrections when a pixel walk wraps a row / image
   int Cout, Kpad, K, M;
   int tiles_n, ntiles, nsplit, nchunks;
   float* part;   // [nsplit][Cout][Kpad]
@@ -114,8 +116,9 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
   }
   // Pixel of each B slot tracked incrementally (chunks of one workgroup are
   // consecutive): no integer division in the loop.  bp = element offset of
-  // the tap's source pixel (+ channel) from x, valid iff in the image.
-  const int HW = a.H * a.W;
+  // the tap's source pixel (+ channel) from x, valid iff in the image; output
+  // pixel (oh, ow) reads input (s*oh + dy, s*ow + dx).
+  const int HW = a.H * a.W, s = a.stride;
   int b_oh[B_G], b_ow[B_G];
   long long b_ptr[B_G];
   {
@@ -123,13 +126,14 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
 #pragma unroll
     for (int i = 0; i < B_G; ++i) {
       const long long m = m0 + b_row[i];
-      const long long rem = m % HW;
+      const long long img = m / HW, rem = m - img * HW;
       b_oh[i] = (int)(rem / a.W);
       b_ow[i] = (int)(rem - (long long)b_oh[i] * a.W);
-      b_ptr[i] = (m + (long long)b_dy[i] * a.W + b_dx[i]) * a.xcs + b_ci[i];
+      b_ptr[i] = ((img * a.Hin + s * b_oh[i] + b_dy[i]) * a.Win + s * b_ow[i] + b_dx[i]) * a.xcs +
+                 b_ci[i];
     }
   }
-  const long long a_step = (long long)WG_RB * a.ldy, b_step = (long long)WG_RB * a.xcs;
+  const long long a_step = (long long)WG_RB * a.ldy, b_step = (long long)WG_RB * s * a.xcs;
   long long a_ptr[A_G];
 #pragma unroll
   for (int i = 0; i < A_G; ++i)
@@ -149,14 +153,18 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
 #pragma unroll
     for (int i = 0; i < B_G; ++i) {
       const bool ok = b_kok[i] && m0 + b_row[i] < a.M &&
-                      (unsigned)(b_oh[i] + b_dy[i]) < (unsigned)a.H &&
-                      (unsigned)(b_ow[i] + b_dx[i]) < (unsigned)a.W;
+                      (unsigned)(s * b_oh[i] + b_dy[i]) < (unsigned)a.Hin &&
+                      (unsigned)(s * b_ow[i] + b_dx[i]) < (unsigned)a.Win;
       const float* src = ok ? a.x + b_ptr[i] : pf_wg_zero16;
       b_ptr[i] += b_step;
       b_ow[i] += WG_RB;
       while (b_ow[i] >= a.W) {
         b_ow[i] -= a.W;
-        if (++b_oh[i] == a.H) b_oh[i] = 0;
+        b_ptr[i] += a.d_row;
+        if (++b_oh[i] == a.H) {
+          b_oh[i] = 0;
+          b_ptr[i] += a.d_img;
+        }
       }
       __builtin_amdgcn_global_load_lds(
           (const __attribute__((address_space(1))) void*)src,
@@ -363,21 +371,22 @@ __global__ __launch_bounds__(NW * 64) void conv_wgrad_halo_kernel(WgradArgs a) {
   }
 }
 
-// dw[co][k] = sum_s part[s][co][k] (split order: deterministic); db likewise
+// dw[co][k] = sum_s part[s][co][k] (split order: deterministic); db likewise.
+// acc: add to the existing gradient (the two image batches of one step)
 __global__ void wgrad_reduce_kernel(const float* __restrict__ part, const float* __restrict__ partb,
                                     int nsplit, int Cout, int Kpad, float* __restrict__ dw,
-                                    float* __restrict__ db) {
+                                    float* __restrict__ db, int acc) {
   const long long n = (long long)Cout * Kpad;
   const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
   if (i < n) {
     float s = 0.f;
     for (int k = 0; k < nsplit; ++k) s += part[(long long)k * n + i];
-    dw[i] = s;
+    dw[i] = acc ? dw[i] + s : s;
   }
   if (db && i < Cout) {
     float s = 0.f;
     for (int k = 0; k < nsplit; ++k) s += partb[(long long)k * Cout + i];
-    db[i] = s;
+    db[i] = acc ? db[i] + s : s;
   }
 }
 
@@ -792,11 +801,12 @@ struct WgPlan {
   int BM, BN, tiles_m, tiles_n, nsplit, nchunks, Kpad, K, ntiles;
 };
 
-WgPlan wgrad_plan(int n, int H, int W, int Cin, int Cout, int KH, int KW) {
+// H, W: output (dy) dims
+WgPlan wgrad_plan(int n, int H, int W, int Cin, int Cout, int KH, int KW, int stride) {
   WgPlan p;
   p.Kpad = posfeat_conv_packed_k(Cin, KH, KW);
   p.K = KH * KW * Cin;
-  p.halo = Cin % 32 == 0 && KH == 3 && KW == 3;
+  p.halo = Cin % 32 == 0 && KH == 3 && KW == 3 && stride == 1;
   if (p.halo) {
     // tiles = (cout block, input slab); chunks = 32-pixel row segments
     p.BM = (Cout % 192 == 0) ? 192 : (Cout % 128 == 0) ? 128 : 64;
@@ -824,27 +834,38 @@ WgPlan wgrad_plan(int n, int H, int W, int Cin, int Cout, int KH, int KW) {
 }  // namespace
 
 // ------------------------------------------------------------------ launchers
-size_t pf_conv_wgrad_ws_bytes(int n, int H, int W, int Cin, int Cout, int KH, int KW) {
-  const WgPlan p = wgrad_plan(n, H, W, Cin, Cout, KH, KW);
+static inline int wg_out(int H, int K, int stride) { return (H + 2 * ((K - 1) / 2) - K) / stride + 1; }
+
+size_t pf_conv_wgrad_ws_bytes(int n, int H, int W, int Cin, int Cout, int KH, int KW, int stride) {
+  const WgPlan p = wgrad_plan(n, wg_out(H, KH, stride), wg_out(W, KW, stride), Cin, Cout, KH, KW,
+                              stride);
   return pf_align((size_t)p.nsplit * Cout * p.Kpad * 4, 256) + pf_align((size_t)p.nsplit * Cout * 4, 256);
 }
 
 int pf_conv_wgrad(const float* dy, int ldy, const float* x, int xcs, int n, int H, int W, int Cin,
-                  int Cout, int KH, int KW, float* dw, float* db, void* ws, size_t ws_bytes,
-                  hipStream_t st) {
-  if ((Cin % 32 != 0 && Cin != 4) || Cout % 32 || ldy % 4 || xcs % 4 || KH != KW || KH % 2 == 0)
+                  int Cout, int KH, int KW, int stride, float* dw, float* db, int acc, void* ws,
+                  size_t ws_bytes, hipStream_t st) {
+  if ((Cin % 32 != 0 && Cin != 4) || Cout % 32 || ldy % 4 || xcs % 4 || KH != KW || KH % 2 == 0 ||
+      stride < 1 || stride > 2)
     return POSFEAT_E_INVALID;
   if (reinterpret_cast<uintptr_t>(dy) % 16 || reinterpret_cast<uintptr_t>(x) % 16)
     return POSFEAT_E_INVALID;
-  if (ws_bytes < pf_conv_wgrad_ws_bytes(n, H, W, Cin, Cout, KH, KW)) return POSFEAT_E_WORKSPACE;
-  const WgPlan p = wgrad_plan(n, H, W, Cin, Cout, KH, KW);
+  if (ws_bytes < pf_conv_wgrad_ws_bytes(n, H, W, Cin, Cout, KH, KW, stride))
+    return POSFEAT_E_WORKSPACE;
+  const int OH = wg_out(H, KH, stride), OW = wg_out(W, KW, stride);
+  const WgPlan p = wgrad_plan(n, OH, OW, Cin, Cout, KH, KW, stride);
   WgradArgs a;
   a.dy = dy;
   a.ldy = ldy;
   a.x = x;
   a.xcs = xcs;
-  a.H = H;
-  a.W = W;
+  a.H = OH;
+  a.W = OW;
+  a.Hin = H;
+  a.Win = W;
+  a.stride = stride;
+  a.d_row = (long long)(stride * W - stride * OW) * xcs;
+  a.d_img = ((long long)H * W - (long long)stride * OH * W) * xcs;
   a.Cin = Cin;
   a.KH = KH;
   a.KW = KW;
@@ -852,7 +873,7 @@ int pf_conv_wgrad(const float* dy, int ldy, const float* x, int xcs, int n, int 
   a.Cout = Cout;
   a.Kpad = p.Kpad;
   a.K = p.K;
-  a.M = n * H * W;
+  a.M = n * OH * OW;
   a.tiles_n = p.tiles_n;
   a.ntiles = p.ntiles;
   a.nsplit = p.nsplit;
@@ -880,7 +901,7 @@ int pf_conv_wgrad(const float* dy, int ldy, const float* x, int xcs, int n, int 
   PF_CHECK_LAUNCH();
   const long long ne = (long long)Cout * p.Kpad;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, st,
-                     a.part, a.partb, p.nsplit, Cout, p.Kpad, dw, db);
+                     a.part, a.partb, p.nsplit, Cout, p.Kpad, dw, db, acc);
   PF_CHECK_LAUNCH();
   return POSFEAT_OK;
 }
@@ -1005,13 +1026,13 @@ extern "C" int posfeat_sgd(float* w, const float* g, long long n, float lr, void
 extern "C" size_t posfeat_conv_wgrad_workspace(int n, int h, int w, int cin, int cout, int kh,
                                                int kw) {
   if (n <= 0 || h <= 0 || w <= 0 || cout <= 0 || cin <= 0) return 0;
-  return pf_conv_wgrad_ws_bytes(n, h, w, cin, cout, kh, kw);
+  return pf_conv_wgrad_ws_bytes(n, h, w, cin, cout, kh, kw, 1);
 }
 
 extern "C" int posfeat_conv_wgrad(const float* dy, int dy_cstride, const float* x, int x_cstride,
                                   int n, int h, int w, int cin, int cout, int kh, int kw,
                                   float* dw, float* db, void* ws, size_t ws_bytes, void* stream) {
   if (!dy || !x || !dw || !ws || n <= 0 || h <= 0 || w <= 0) return POSFEAT_E_INVALID;
-  return pf_conv_wgrad(dy, dy_cstride, x, x_cstride, n, h, w, cin, cout, kh, kw, dw, db, ws,
+  return pf_conv_wgrad(dy, dy_cstride, x, x_cstride, n, h, w, cin, cout, kh, kw, 1, dw, db, 0, ws,
                        ws_bytes, pf_stream(stream));
 }

@@ -19,10 +19,11 @@ and ``posfeat_sgd`` on the head region of the device weight blob.  Every byte
 of arithmetic is in libposfeat_hip.so; torch provides memory, the RNG for the
 sampling uniforms and ``torch.distributed``.
 """
+import numpy as np
 import torch
 
 from . import _lib
-from ._lib import check, lib, ptr, stream_ptr
+from ._lib import c_int, check, lib, ptr, stream_ptr
 from .engine import ExtractionEngine
 from .parallel import allreduce_head_grad
 
@@ -206,3 +207,135 @@ class DescriptorLossGrad:
             float(self.epi["weight_window"]), ptr(dx1), 128, ptr(dx2), 128, ptr(bws), bneed,
             stream_ptr()))
         return out, dx1, dx2, res
+
+
+class BackboneTrainer:
+    """Descriptor-training step (config 3, configs/train_desc.yaml): ResUNet in
+    train mode (BatchNorm batch statistics + running update), the
+    Line2Window/EpipolarLoss_full gradient, the backbone backward and Adam --
+    one inner iteration of managers/trainer.py:293-356 with
+    ``optimal_modules: ['backbone']``.
+
+    State on the device: the packed parameter blob, its gradient, Adam's two
+    moments (same layout) and the running-statistics blob.  One activation
+    workspace per image batch (im1 and im2 are separate backbone calls in
+    PoSFeat.forward, PoSFeat_model.py:144-145, so each has its own BN batch
+    statistics and the running stats are updated twice per step); one
+    scratch workspace shared by both.
+
+    The keypoint head is not run: its output feeds neither this loss nor any
+    state."""
+
+    def __init__(self, backbone_sd, batch, h, w, device="cuda", lr=1e-4, betas=(0.9, 0.999),
+                 eps=1e-8, weight_decay=0.0, momentum=0.1, group=None):
+        import ctypes
+        from . import weights
+        _lib.require_device()
+        L = lib()
+        self.table = _lib.bbtrain_table()
+        params, stats = weights.pack_bbtrain(backbone_sd, self.table)
+        dev = torch.device(device)
+        self.device = dev
+        self.params = torch.from_numpy(params).to(dev)
+        self.stats = torch.from_numpy(stats).to(dev)
+        self.grad = torch.zeros_like(self.params)   # conv_coarse never receives a gradient
+        self.exp_avg = torch.zeros_like(self.params)
+        self.exp_avg_sq = torch.zeros_like(self.params)
+        nbt = [int(np.asarray(v).reshape(-1)[0]) for k, v in backbone_sd.items()
+               if k.endswith("num_batches_tracked")] if backbone_sd is not None else []
+        self.num_batches_tracked = max(nbt) if nbt else 0
+        self.adam_steps = 0
+        self.lr, self.betas, self.eps, self.wd = float(lr), betas, float(eps), float(weight_decay)
+        self.momentum = float(momentum)
+        self.group = group
+        self.batch, self.h, self.w = batch, h, w
+        hnd = ctypes.c_void_p()
+        check(L.posfeat_bbtrain_create(batch, h, w, ctypes.byref(hnd)))
+        self._h = hnd
+        na = L.posfeat_bbtrain_act_bytes(hnd)
+        ns = L.posfeat_bbtrain_scratch_bytes(hnd)
+        self.act = [torch.empty(na, dtype=torch.uint8, device=dev) for _ in range(2)]
+        self.scratch = torch.empty(ns, dtype=torch.uint8, device=dev)
+        self._lm = [None, None]
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                lib().posfeat_bbtrain_destroy(h)
+            except Exception:  # pragma: no cover - interpreter shutdown
+                pass
+            self._h = None
+
+    def forward(self, img, slot):
+        """Train-mode ResUNet on img [b,3,h,w] into workspace `slot` (0: im1,
+        1: im2); returns the NHWC local map [b, h/4, w/4, 128] (a view into the
+        workspace, valid until the next forward on that slot)."""
+        import ctypes
+        _lib.require_device(img)
+        img = img.float().contiguous()
+        out = ctypes.c_void_p()
+        act = self.act[slot]
+        check(lib().posfeat_bbtrain_forward(self._h, ptr(self.params), ptr(self.stats),
+                                            self.momentum, ptr(img), ptr(act), ptr(self.scratch),
+                                            ctypes.byref(out), stream_ptr()))
+        self.num_batches_tracked += 1
+        off = out.value - act.data_ptr()
+        n = self.batch * (self.h // 4) * (self.w // 4) * 128
+        lm = act[off:off + 4 * n].view(torch.float32).view(self.batch, self.h // 4, self.w // 4, 128)
+        self._lm[slot] = lm
+        return lm
+
+    def backward(self, dlocal_map, slot, accumulate):
+        """dL/d(local map of `slot`) (NHWC, last dim = pixel stride >= 128) ->
+        grad (+)= dL/d params."""
+        d = dlocal_map.float()
+        if d.stride(-1) != 1 or d.stride(-2) != d.shape[-1]:
+            d = d.contiguous()
+        check(lib().posfeat_bbtrain_backward(self._h, ptr(self.params), ptr(self.act[slot]), ptr(d),
+                                             d.shape[-1], ptr(self.grad), 1 if accumulate else 0,
+                                             ptr(self.scratch), stream_ptr()))
+
+    def adam_step(self, grad_scale=1.0):
+        self.adam_steps += 1
+        check(lib().posfeat_adam(ptr(self.params), ptr(self.grad), ptr(self.exp_avg),
+                                 ptr(self.exp_avg_sq), self.params.numel(), self.lr,
+                                 float(self.betas[0]), float(self.betas[1]), self.eps, self.wd,
+                                 self.adam_steps, float(grad_scale), stream_ptr()))
+
+    def step(self, im1, im2, F1, F2, loss, epoch=1, draws=None, update=True):
+        """One training iteration: forward(im1), forward(im2), the loss and
+        its map gradients (``loss``: a DescriptorLossGrad), backward of both
+        batches into one gradient, RCCL all-reduce (world > 1), Adam.
+        Returns (out[7], processed dict) as DescriptorLossGrad does."""
+        x1 = self.forward(im1, 0)
+        x2 = self.forward(im2, 1)
+        hw = (int(im1.shape[2]), int(im1.shape[3]))
+        out, dx1, dx2, res = loss(x1, x2, F1, F2, hw, (int(im2.shape[2]), int(im2.shape[3])),
+                                  epoch=epoch, draws=draws)
+        self.backward(dx1, 0, accumulate=False)
+        self.backward(dx2, 1, accumulate=True)
+        scale = allreduce_head_grad(self.grad, self.group)
+        if update:
+            self.adam_step(scale)
+        return out, res
+
+    def set_timing(self, enable):
+        check(lib().posfeat_bbtrain_set_timing(self._h, 1 if enable else 0))
+
+    def timing(self, prefix):
+        import ctypes
+        ms, fl, n = ctypes.c_double(), ctypes.c_double(), c_int()
+        check(lib().posfeat_bbtrain_timing(self._h, prefix.encode(), ctypes.byref(ms),
+                                           ctypes.byref(fl), ctypes.byref(n)))
+        return ms.value, fl.value, n.value
+
+    def state_dict(self):
+        """backbone.pth contents (reference key order, PoSFeat_model.py:74-81)."""
+        from . import weights
+        return weights.unpack_bbtrain(self.params.cpu().numpy(), self.table,
+                                      self.stats.cpu().numpy(), self.num_batches_tracked)
+
+    def grad_dict(self):
+        from . import weights
+        return weights.unpack_bbtrain(self.grad.cpu().numpy(), self.table)

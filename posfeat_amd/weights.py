@@ -306,3 +306,55 @@ def pack_for_device(backbone_sd, head_sd, specs, head_prelu_key="relu.weight"):
         blob[w_off:w_off + wp.size] = wp.reshape(-1)
         blob[b_off:b_off + cout] = bp
     return blob
+
+
+# ----------------------------------------------------------------------------
+# Train-mode backbone (configs/train_desc.yaml): raw conv weights + BatchNorm
+# affine parameters in one blob, running statistics in a second one (the C-ABI
+# table posfeat_bbtrain_layer gives the offsets; _lib.bbtrain_table()).
+def pack_bbtrain(sd, table):
+    """(params, stats) float32 blobs from a ResUNet state dict (DescNet.py key
+    names).  Conv weights are packed like ``pack_conv``; the gradient blob the
+    backward writes has the params layout."""
+    layers, npar, nst = table
+    params = np.zeros(npar, np.float32)
+    stats = np.zeros(nst, np.float32)
+    for name, cin, cout, k, stride, has_bias, offs in layers:
+        _, wk, bk, bn = conv_sources(name)
+        w = _np(sd[wk]).astype(np.float64)
+        if w.shape != (cout, cin, k, k):
+            raise ValueError("weight %s has shape %s, expected %s" % (wk, w.shape, (cout, cin, k, k)))
+        b = _np(sd[bk]).astype(np.float64) if has_bias else np.zeros(cout)
+        wp, bp = pack_conv(w, b)
+        params[offs[0]:offs[0] + wp.size] = wp.reshape(-1)
+        if has_bias:
+            params[offs[1]:offs[1] + cout] = bp
+        params[offs[2]:offs[2] + cout] = _np(sd[bn + ".weight"])
+        params[offs[3]:offs[3] + cout] = _np(sd[bn + ".bias"])
+        stats[offs[4]:offs[4] + cout] = _np(sd[bn + ".running_mean"])
+        stats[offs[5]:offs[5] + cout] = _np(sd[bn + ".running_var"])
+    return params, stats
+
+
+def unpack_bbtrain(params, table, stats=None, num_batches_tracked=None):
+    """Inverse of ``pack_bbtrain``: an OrderedDict in the ResUNet state-dict key
+    order (``backbone_param_shapes``).  With ``stats`` it is a full
+    ``backbone.pth`` (PoSFeat.save_checkpoint, PoSFeat_model.py:74-81);
+    without, only the trainable tensors (e.g. a gradient blob)."""
+    layers, _, _ = table
+    params = np.asarray(params, np.float32)
+    vals = {}
+    for name, cin, cout, k, stride, has_bias, offs in layers:
+        _, wk, bk, bn = conv_sources(name)
+        kpad = packed_k(cin, k, k)[2]
+        vals[wk] = unpack_conv(params[offs[0]:offs[0] + cout * kpad], cout, cin, k, k)
+        if has_bias:
+            vals[bk] = params[offs[1]:offs[1] + cout].copy()
+        vals[bn + ".weight"] = params[offs[2]:offs[2] + cout].copy()
+        vals[bn + ".bias"] = params[offs[3]:offs[3] + cout].copy()
+        if stats is not None:
+            st = np.asarray(stats, np.float32)
+            vals[bn + ".running_mean"] = st[offs[4]:offs[4] + cout].copy()
+            vals[bn + ".running_var"] = st[offs[5]:offs[5] + cout].copy()
+            vals[bn + ".num_batches_tracked"] = np.array(int(num_batches_tracked or 0), np.int64)
+    return OrderedDict((k, vals[k]) for k, _ in backbone_param_shapes() if k in vals)

@@ -421,6 +421,80 @@ def gen_train_kp(out):
     np.savez_compressed(out, **res)
 
 
+BB_GRAD_CASE = (2, 128, 160, 9)
+
+
+def gen_bb_grad(out):
+    """Config-3 backbone step on the reference's own ResUNet (DescNet.py) in
+    train mode (trainer.py:293-296): two backbone calls (im1, im2:
+    PoSFeat_model.py:144-145 -- separate BatchNorm batch statistics, running
+    statistics updated twice), loss = sum(local_map1 * R1) + sum(local_map2 *
+    R2) with seeded cotangents R (any dL/d local_map drives the same
+    backward), loss.backward().  Stores the local maps (every 2nd pixel), per
+    parameter [sum g, sum |g|, sum g^2] (fp64), full gradients of tensors of
+    <= 40000 elements, 512 seeded entries of the larger ones, and the running
+    statistics after both forwards.  conv_coarse gets no gradient (global_map
+    is not in the loss)."""
+    import zlib
+    bb, _ = build_ref_models(0)
+    b, H, W, seed = BB_GRAD_CASE
+    im1 = torch.from_numpy(np.stack([seeded_image(30 + i, H, W) for i in range(b)]))
+    im2 = torch.from_numpy(np.stack([seeded_image(40 + i, H, W) for i in range(b)]))
+    rs = np.random.RandomState(seed)
+    R1 = torch.from_numpy(rs.randn(b, 128, H // 4, W // 4).astype(np.float32))
+    R2 = torch.from_numpy(rs.randn(b, 128, H // 4, W // 4).astype(np.float32))
+    bb.train()
+    bb.zero_grad()
+    o1 = bb(im1)
+    o2 = bb(im2)
+    loss = (o1["local_map"] * R1).sum() + (o2["local_map"] * R2).sum()
+    loss.backward()
+    res = {"lm1_sub": o1["local_map"].detach()[:, :, ::2, ::2].numpy().copy(),
+           "lm2_sub": o2["local_map"].detach()[:, :, ::2, ::2].numpy().copy(),
+           "loss": loss.detach().numpy()}
+    for k, p in bb.named_parameters():
+        if p.grad is None:
+            continue
+        g = p.grad.detach().numpy()
+        g64 = g.astype(np.float64)
+        res["stat_" + k] = np.array([g64.sum(), np.abs(g64).sum(), (g64 * g64).sum()])
+        if g.size <= 40000:
+            res["grad_" + k] = g.copy()
+        else:
+            idx = np.random.RandomState(zlib.crc32(k.encode())).choice(g.size, 512, replace=False)
+            res["idx_" + k] = idx.astype(np.int64)
+            res["val_" + k] = g.reshape(-1)[idx].copy()
+    for k, v in bb.state_dict().items():
+        if "running" in k:
+            res["rs_" + k] = v.numpy().copy()
+    bb.eval()
+    # the same step on the reference modules in fp64: the fp32 gradients of this
+    # 13-block train-mode network carry up to ~3e-2 relative rounding noise
+    # (BatchNorm backward cancels), so the HIP path is judged against fp64 with
+    # a per-tensor tolerance set by the reference's own fp32 error ("noise_")
+    bb64, _ = build_ref_models(0)
+    bb64 = bb64.double()
+    bb64.train()
+    bb64.zero_grad()
+    p1 = bb64(im1.double())
+    p2 = bb64(im2.double())
+    ((p1["local_map"] * R1.double()).sum() + (p2["local_map"] * R2.double()).sum()).backward()
+    for k, p in bb64.named_parameters():
+        if p.grad is None:
+            continue
+        g = p.grad.detach().numpy()
+        if "grad_" + k in res:
+            res["g64_" + k] = g.copy()
+            ref32 = res["grad_" + k].astype(np.float64)
+            g = g.reshape(ref32.shape)
+        else:
+            g = g.reshape(-1)[res["idx_" + k]]
+            res["v64_" + k] = g.copy()
+            ref32 = res["val_" + k].astype(np.float64)
+        res["noise_" + k] = np.array(np.abs(ref32 - g).max() / max(np.abs(g).max(), 1e-300))
+    np.savez_compressed(out, **res)
+
+
 if __name__ == "__main__":
     torch.set_num_threads(os.cpu_count() or 8)
     which = sys.argv[1:] or ["detector", "sampler", "model_small", "extract_full", "correlation",
@@ -429,6 +503,8 @@ if __name__ == "__main__":
         gen_train_kp(os.path.join(HERE, "train_kp.npz"))
     if "desc_grad" in which:
         gen_desc_grad(os.path.join(HERE, "desc_grad.npz"))
+    if "bb_grad" in which:
+        gen_bb_grad(os.path.join(HERE, "bb_grad.npz"))
     if "detector" in which:
         gen_detector(os.path.join(HERE, "detector.npz"))
     if "sampler" in which:

@@ -1,0 +1,278 @@
+"""Descriptor-training backbone step (config 3, configs/train_desc.yaml).
+
+CPU: the oracle (oracle/model_ref.resunet_forward(train=True) + torch autograd)
+against the reference's own ResUNet in train mode (tests/golden/bb_grad.npz,
+tests/golden/gen_golden.py:gen_bb_grad) -- pins the oracle; the packing round
+trip of the parameter / running-stat blobs.
+GPU: posfeat_bbtrain forward (BatchNorm batch statistics, running update) and
+backward against the same fixture; Adam against torch.optim.Adam;
+determinism; one full step (forward x2, Line2Window/EpipolarLoss gradient,
+backward x2, Adam) against the oracle on the GPU's own window centres and
+loss weights.
+
+Tolerances: the oracle matches the fp32 reference per tensor within 1e-4 of
+max|g_ref| (same CPU kernels).  The HIP path is compared with the reference
+run in fp64: the fp32 gradients of this 13-block train-mode network carry up
+to ~3e-2 relative rounding noise of their own (tools/bb_fp64_noise.py), so
+each tensor must sit within max(3 x the reference's own fp32 error, 1e-2) of
+fp64 (max-abs error over max |g64|), and all tensors together within 2e-3
+(relative L2 over the concatenated checked entries).  Conv biases that feed a BatchNorm have an exact gradient of 0; they
+are compared with an absolute bound scaled by the layer's weight gradient.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+
+CASE = (2, 128, 160, 9)
+
+
+def _inputs():
+    from posfeat_amd.weights import seeded_image
+    b, H, W, seed = CASE
+    im1 = torch.from_numpy(np.stack([seeded_image(30 + i, H, W) for i in range(b)]))
+    im2 = torch.from_numpy(np.stack([seeded_image(40 + i, H, W) for i in range(b)]))
+    rs = np.random.RandomState(seed)
+    R1 = torch.from_numpy(rs.randn(b, 128, H // 4, W // 4).astype(np.float32))
+    R2 = torch.from_numpy(rs.randn(b, 128, H // 4, W // 4).astype(np.float32))
+    return np.load(os.path.join(GOLDEN, "bb_grad.npz")), im1, im2, R1, R2
+
+
+def _check_grads(got, d, rel):
+    """got: key -> gradient array (reference shapes).  Collects every failing
+    tensor (with its relative error) before asserting."""
+    keys = [k[5:] for k in d.files if k.startswith("stat_")]
+    assert len(keys) > 100
+    bad = []
+    for k in keys:
+        g = np.asarray(got[k], np.float64)
+        st = d["stat_" + k]
+        if k.endswith("conv.bias"):       # conv bias feeding a BatchNorm: exact gradient 0
+            wk = k[:-4] + "weight"
+            wmax = np.abs(np.asarray(got[wk])).max()
+            if np.abs(g).max() > 1e-4 * max(wmax, 1e-3):
+                bad.append((k, "bias", float(np.abs(g).max()), float(wmax)))
+            continue
+        e_sum = abs(g.sum() - st[0]) / max(st[1], 1e-30)
+        e_nrm = abs(np.sqrt((g * g).sum()) - np.sqrt(st[2])) / max(np.sqrt(st[2]), 1e-30)
+        if "grad_" + k in d.files:
+            ref = d["grad_" + k].astype(np.float64)
+            g = g.reshape(ref.shape)
+        else:
+            ref = d["val_" + k].astype(np.float64)
+            g = g.reshape(-1)[d["idx_" + k]]
+        e_max = np.abs(g - ref).max() / max(np.abs(ref).max(), 1e-30)
+        if max(e_sum, e_nrm, e_max) > rel:
+            bad.append((k, round(e_sum, 6), round(e_nrm, 6), round(e_max, 6)))
+    assert not bad, "tensors over rel %.1e (key, sum, norm, max): %s" % (rel, bad)
+
+
+def _check_grads64(got, d, floor=1e-2, mult=3.0):
+    """The HIP gradients against the reference run in fp64 (g64_/v64_): per
+    tensor max|g - g64| / max|g64| <= max(mult * noise, floor), where noise is
+    the same measure for the reference's own fp32 gradients -- this 13-block
+    train-mode network's fp32 gradients carry up to ~3e-2 relative rounding
+    noise (BatchNorm backward cancellation), so a fixed fp32-vs-fp32 bound would
+    test summation order, not correctness."""
+    keys = [k[5:] for k in d.files if k.startswith("stat_")]
+    bad = []
+    for k in keys:
+        if k.endswith("conv.bias"):
+            continue
+        g = np.asarray(got[k], np.float64)
+        if "g64_" + k in d.files:
+            ref = d["g64_" + k]
+            g = g.reshape(ref.shape)
+        else:
+            ref = d["v64_" + k]
+            g = g.reshape(-1)[d["idx_" + k]]
+        e = np.abs(g - ref).max() / max(np.abs(ref).max(), 1e-30)
+        tol = max(mult * float(d["noise_" + k]), floor)
+        if e > tol:
+            bad.append((k, round(float(e), 6), round(tol, 6)))
+    assert not bad, "tensors over tolerance (key, err, tol): %s" % bad
+    num = sum(float(((np.asarray(got[k], np.float64).reshape(-1)[d["idx_" + k]] - d["v64_" + k])
+                     ** 2).sum()) if "v64_" + k in d.files else
+              float(((np.asarray(got[k], np.float64).reshape(d["g64_" + k].shape) - d["g64_" + k])
+                     ** 2).sum()) for k in keys if not k.endswith("conv.bias"))
+    den = sum(float((d[("v64_" if "v64_" + k in d.files else "g64_") + k] ** 2).sum())
+              for k in keys if not k.endswith("conv.bias"))
+    assert np.sqrt(num / den) <= 2e-3, np.sqrt(num / den)
+
+
+def _check_stats(stats_sd, d, rel):
+    for k in d.files:
+        if not k.startswith("rs_"):
+            continue
+        ref = d[k]
+        got = np.asarray(stats_sd[k[3:]]).reshape(ref.shape)
+        np.testing.assert_allclose(got, ref, rtol=rel, atol=rel * np.abs(ref).max(), err_msg=k)
+
+
+def test_oracle_bb_grad_vs_reference():
+    from oracle.model_ref import resunet_forward
+    from posfeat_amd.weights import seeded_state_dicts
+    d, im1, im2, R1, R2 = _inputs()
+    bb, _ = seeded_state_dicts(0)
+    sd = {k: v.clone() for k, v in bb.items()}
+    params = {k: v.requires_grad_(True) for k, v in sd.items()
+              if not ("running" in k or "num_batches" in k)}
+    o1 = resunet_forward(sd, im1, train=True)
+    o2 = resunet_forward(sd, im2, train=True)
+    np.testing.assert_allclose(o1["local_map"].detach()[:, :, ::2, ::2].numpy(), d["lm1_sub"],
+                               atol=1e-5)
+    loss = (o1["local_map"] * R1).sum() + (o2["local_map"] * R2).sum()
+    keys = [k for k in params if "stat_" + k in d.files]
+    grads = torch.autograd.grad(loss, [params[k] for k in keys])
+    _check_grads({k: g.numpy() for k, g in zip(keys, grads)}, d, rel=1e-4)
+    _check_stats({k: v.detach() for k, v in sd.items()}, d, rel=1e-5)
+
+
+def test_pack_bbtrain_roundtrip():
+    from posfeat_amd import _lib, weights
+    try:
+        table = _lib.bbtrain_table()
+    except Exception:  # pragma: no cover - library missing
+        pytest.skip("libposfeat_hip.so not built")
+    bb, _ = weights.seeded_state_dicts(4, as_torch=False)
+    params, stats = weights.pack_bbtrain(bb, table)
+    assert params.size == table[1] and stats.size == table[2]
+    back = weights.unpack_bbtrain(params, table, stats, 0)
+    assert list(back) == list(bb)
+    for k in bb:
+        np.testing.assert_array_equal(np.asarray(back[k]).reshape(np.shape(bb[k])), bb[k],
+                                      err_msg=k)
+
+
+# ------------------------------------------------------------------ GPU
+def _trainer(gpu, lr=1e-4):
+    from posfeat_amd.training import BackboneTrainer
+    from posfeat_amd.weights import seeded_state_dicts
+    b, H, W, _ = CASE
+    bb, _ = seeded_state_dicts(0)
+    return BackboneTrainer(bb, b, H, W, device=gpu, lr=lr)
+
+
+def _gpu_grads(gpu):
+    d, im1, im2, R1, R2 = _inputs()
+    tr = _trainer(gpu)
+    lm1 = tr.forward(im1.to(gpu), 0).permute(0, 3, 1, 2).cpu().numpy()
+    lm2 = tr.forward(im2.to(gpu), 1).permute(0, 3, 1, 2).cpu().numpy()
+    tr.backward(R1.permute(0, 2, 3, 1).contiguous().to(gpu), 0, accumulate=False)
+    tr.backward(R2.permute(0, 2, 3, 1).contiguous().to(gpu), 1, accumulate=True)
+    torch.cuda.synchronize()
+    return d, tr, lm1, lm2
+
+
+@pytest.mark.gpu
+def test_gpu_bb_grad_vs_reference(gpu):
+    d, tr, lm1, lm2 = _gpu_grads(gpu)
+    for lm, ref in ((lm1, d["lm1_sub"]), (lm2, d["lm2_sub"])):
+        np.testing.assert_allclose(lm[:, :, ::2, ::2], ref, atol=2e-4 * np.abs(ref).max())
+    _check_grads64(tr.grad_dict(), d)
+    _check_stats(tr.state_dict(), d, rel=1e-4)
+    # conv_coarse (global_map is not in the loss) keeps a zero gradient
+    g = tr.grad_dict()
+    assert not np.any(g["conv_coarse.conv.weight"]) and not np.any(g["conv_coarse.bn.weight"])
+
+
+@pytest.mark.gpu
+def test_gpu_bb_grad_deterministic(gpu):
+    _, tr1, _, _ = _gpu_grads(gpu)
+    _, tr2, _, _ = _gpu_grads(gpu)
+    assert torch.equal(tr1.grad, tr2.grad)
+    assert torch.equal(tr1.stats, tr2.stats)
+
+
+@pytest.mark.gpu
+def test_gpu_adam_matches_torch(gpu):
+    """posfeat_adam against torch.optim.Adam (defaults: betas (0.9, 0.999),
+    eps 1e-8) over 3 steps, gradient pre-scaled by 0.5 (the 1/world factor)."""
+    from posfeat_amd._lib import check, lib, ptr, stream_ptr
+    rs = np.random.RandomState(3)
+    n = 10007
+    p0 = rs.randn(n).astype(np.float32)
+    gs = [rs.randn(n).astype(np.float32) * 10 ** rs.uniform(-3, 1, n).astype(np.float32)
+          for _ in range(3)]
+    tp = torch.nn.Parameter(torch.from_numpy(p0.copy()))
+    opt = torch.optim.Adam([tp], lr=1e-3)
+    p = torch.from_numpy(p0.copy()).to(gpu)
+    m = torch.zeros(n, device=gpu)
+    v = torch.zeros(n, device=gpu)
+    for step, g in enumerate(gs, 1):
+        tp.grad = torch.from_numpy(0.5 * g)
+        opt.step()
+        gd = torch.from_numpy(g).to(gpu)
+        check(lib().posfeat_adam(ptr(p), ptr(gd), ptr(m), ptr(v), n, 1e-3, 0.9, 0.999, 1e-8, 0.0,
+                                 step, 0.5, stream_ptr()))
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(p.cpu().numpy(), tp.detach().numpy(), rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.gpu
+def test_gpu_desc_train_step_vs_oracle(gpu):
+    """Full config-3 step: GPU forward x2 -> DescriptorLossGrad -> backward x2
+    against the oracle's autograd through oracle ResUNet + desc loss, sharing
+    the GPU's window centres and loss weights (arg-max near-ties); then one
+    Adam update moves every trained tensor and leaves conv_coarse untouched."""
+    from oracle.desc_train_ref import desc_loss_grad, loss_weights
+    from oracle.model_ref import resunet_forward
+    from posfeat_amd.correlation import synthetic_fundamental
+    from posfeat_amd.training import DescriptorLossGrad
+    from posfeat_amd.weights import seeded_state_dicts
+    from test_desc_grad import EPI_CFG, PRE_CFG
+    d, im1, im2, _, _ = _inputs()
+    b, H, W, seed = CASE
+    F1, F2 = [torch.from_numpy(f) for f in synthetic_fundamental(b, H, W, seed)]
+    n = (H // 16) * (W // 16)
+    g = torch.Generator().manual_seed(seed)
+    hg, wg = H // 16, W // 16
+    draws = (torch.randint(0, 256, (b, hg, wg), generator=g),
+             torch.randint(0, 256, (b, hg, wg), generator=g),
+             torch.rand(b, n, 2, generator=g), torch.rand(b, n, 2, generator=g))
+    tr = _trainer(gpu, lr=1e-3)
+    p_before = tr.params.clone()
+    out, res = tr.step(im1.to(gpu), im2.to(gpu), F1, F2, DescriptorLossGrad(PRE_CFG, EPI_CFG),
+                       epoch=0, draws=(draws[0].int(), draws[1].int(), draws[2], draws[3]),
+                       update=False)
+    torch.cuda.synchronize()
+    res = {k: v.cpu() for k, v in res.items()}
+    # oracle: the desc loss gradient (fp32, validated in test_desc_grad.py) on
+    # the GPU's centres and weights, then autograd through the train-mode
+    # ResUNet in fp64 (the fp32 backbone gradients carry up to ~3e-2 rounding
+    # noise of their own, see the module docstring)
+    bb, _ = seeded_state_dicts(0)
+    sd = {k: (v.clone().double() if v.is_floating_point() else v.clone()) for k, v in bb.items()}
+    params = {k: v.requires_grad_(True) for k, v in sd.items()
+              if not ("running" in k or "num_batches" in k)}
+    x1 = resunet_forward(sd, im1.double(), train=True)["local_map"]
+    x2 = resunet_forward(sd, im2.double(), train=True)["local_map"]
+    wts = [loss_weights(res["coord%d" % i], res["w%d" % i], res["w%d_std" % i],
+                        res["valid%d" % i].bool(), Fm, min(H, W)) for i, Fm in ((1, F1), (2, F2))]
+    loss, g1, g2, _ = desc_loss_grad(x1.detach().float(), x2.detach().float(), F1, F2, (H, W),
+                                     (H, W), *draws, centers=(res["l1_exp_n"], res["l2_exp_n"]),
+                                     weights=wts)
+    np.testing.assert_allclose(float(out[0]), float(loss), rtol=2e-3)
+    keys = [k for k in params if "stat_" + k in d.files and not k.endswith("conv.bias")]
+    grads = torch.autograd.grad([x1, x2], [params[k] for k in keys],
+                                grad_outputs=[g1.double(), g2.double()])
+    got = tr.grad_dict()
+    num = den = 0.0
+    for k, gr in zip(keys, grads):
+        ref = gr.numpy()
+        gk = np.asarray(got[k], np.float64).reshape(ref.shape)
+        err = np.abs(gk - ref).max()
+        assert err <= 3e-2 * max(np.abs(ref).max(), 1e-12), (k, err, np.abs(ref).max())
+        num += float(((gk - ref) ** 2).sum())
+        den += float((ref ** 2).sum())
+    assert np.sqrt(num / den) <= 5e-3, np.sqrt(num / den)
+    tr.adam_step()
+    torch.cuda.synchronize()
+    moved = tr.params != p_before
+    layers, _, _ = tr.table
+    for name, cin, cout, k, s, hb, offs in layers:
+        w = moved[offs[0]:offs[0] + cout]
+        assert bool(w.any()) == (name != "conv_coarse"), name
