@@ -45,9 +45,11 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--timing-steps", type=int, default=3)
-    p.add_argument("--workload", choices=("extract", "train_kp"), default="extract",
+    p.add_argument("--workload", choices=("extract", "train_kp", "train_desc"), default="extract",
                    help="extract: configs[1] (the metric); train_kp: configs[4], the keypoint-"
-                        "head training step (DiskLoss) with --batch pairs per GPU")
+                        "head training step (DiskLoss); train_desc: configs[2], the descriptor "
+                        "training step (backbone, Line2Window + EpipolarLoss, Adam); training "
+                        "workloads use --batch pairs per GPU")
     return p.parse_args()
 
 
@@ -128,6 +130,8 @@ def main():
     torch.cuda.set_device(dev)
     if args.workload == "train_kp":
         return train_main(args, world, rank, dev)
+    if args.workload == "train_desc":
+        return train_desc_main(args, world, rank, dev)
     from posfeat_amd import ops
     engine = build_engine(world, rank, dev)
     ws = ops.DetectWorkspace()
@@ -297,6 +301,96 @@ def train_main(args, world, rank, dev):
             "breakdown_ms": {"forward_convs": round(fwd_ms, 3), "backward_all": round(bwd_ms, 3),
                              "conv2_wgrad": round(wg_ms, 3), "conv2_dgrad": round(dg_ms, 3),
                              "engine_all": round(all_ms, 3)},
+            "loss_last": float(out[0].item()),
+        }
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+# ----------------------------------------------------------------------------
+# configs[2]: descriptor training step (configs/train_desc.yaml)
+def train_desc_main(args, world, rank, dev):
+    """One step = the two train-mode backbone calls of PoSFeat.forward (im1,
+    im2: b images each, BatchNorm batch statistics + running update),
+    Preprocess_Line2Window + EpipolarLoss_full forward and gradient, the
+    backbone backward of both batches into one gradient, RCCL all-reduce of
+    the 82 MB gradient (world > 1), Adam -- managers/trainer.py:293-356 for
+    configs/train_desc.yaml (the keypoint head's forward feeds neither this
+    loss nor any state and is not run)."""
+    import torch.distributed as dist
+    from posfeat_amd.correlation import synthetic_fundamental
+    from posfeat_amd.training import (BackboneTrainer, DescriptorLossGrad, DESC_EPI_DEFAULTS,
+                                      DESC_PRE_DEFAULTS)
+    from posfeat_amd.weights import seeded_state_dicts
+    b = args.batch
+    bb, _ = seeded_state_dicts(0)
+    tr = BackboneTrainer(bb, b, H, W, device=dev, lr=1e-4)
+    if world > 1:
+        dist.broadcast(tr.params, src=0)
+        dist.broadcast(tr.stats, src=0)
+    loss = DescriptorLossGrad(DESC_PRE_DEFAULTS, DESC_EPI_DEFAULTS)
+    im1 = make_images(rank * 2 * b, b, dev)
+    im2 = make_images(rank * 2 * b + b, b, dev)
+    F1, F2 = [torch.from_numpy(f).to(dev) for f in synthetic_fundamental(b, H, W, 200 + rank)]
+    torch.manual_seed(4321 + rank)
+    for _ in range(args.warmup):
+        tr.step(im1, im2, F1, F2, loss, epoch=1)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out, _ = tr.step(im1, im2, F1, F2, loss, epoch=1)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    pairs = world * args.steps * b
+    # per-kernel-class timing of one extra step (HIP events on the trainer's stream)
+    tr.set_timing(True)
+    tr.step(im1, im2, F1, F2, loss, epoch=1)
+    cls = {k: tr.timing(k) for k in ("fwd:conv", "fwd:bn", "fwd:misc", "bwd:bn", "bwd:wgrad",
+                                      "bwd:dgrad", "bwd:misc")}
+    all_ms = tr.timing("")[0]
+    tr.set_timing(False)
+    dom = max(("fwd:conv", "bwd:wgrad", "bwd:dgrad"), key=lambda k: cls[k][0])
+    d_ms, d_fl, d_n = cls[dom]
+    ach = d_fl / (d_ms * 1e-3) / 1e12
+    conv_ms = sum(cls[k][0] for k in ("fwd:conv", "bwd:wgrad", "bwd:dgrad"))
+    conv_fl = sum(cls[k][1] for k in ("fwd:conv", "bwd:wgrad", "bwd:dgrad"))
+    if rank == 0:
+        rec = {
+            "metric": "pairs/sec descriptor training step (640x480, Line2Window + EpipolarLoss, "
+                      "Adam)",
+            "value": round(pairs / el, 3), "unit": "pairs/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic (seeded 480x640 image pairs, synthetic fundamental matrices as "
+                    "datasets/megadepth.py:426-448 builds them; seeded random-init ResUNet weights)",
+            "config": {"workload": "configs[2]: MegaDepth-style descriptor training step "
+                                   "(configs/train_desc.yaml: backbone in train mode, "
+                                   "Preprocess_Line2Window + EpipolarLoss_full, Adam 1e-4), "
+                                   "%d pairs per GPU" % b,
+                       "global_batch_pairs": b * world, "image": [H, W],
+                       "parallelism": "dp%d (RCCL all-reduce of backbone grads)" % world},
+            "roofline": {"kernel": "%s class (%d launches: %s MFMA convs of the train-mode "
+                                   "ResUNet, flop-weighted)" % (dom, d_n, dom),
+                         "bound": "mfma", "achieved": round(ach, 3),
+                         "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(ach / PEAK_FP32_MFMA_TFLOPS, 4), "traffic": None,
+                         "avg_launch_ms": round(d_ms / max(d_n, 1), 4),
+                         "flop_per_launch": d_fl / max(d_n, 1)},
+            "breakdown_ms": {k: round(v[0], 3) for k, v in cls.items()},
+            "conv_total": {"ms_per_step": round(conv_ms, 3),
+                           "tflops": round(conv_fl / (conv_ms * 1e-3) / 1e12, 3),
+                           "backbone_kernels_ms": round(all_ms, 3)},
             "loss_last": float(out[0].item()),
         }
         print(json.dumps(rec), flush=True)

@@ -389,7 +389,7 @@ int layer_fwd(Ctx& c, int li, const float* x, int xcs, int h, int w, float* out,
     hipLaunchKernelGGL(bn_partial_kernel<0>, dim3(g.nchunk, g.gy), dim3(256), 0, c.st, y, P,
                        L.cout, g.chunk, nullptr, 0, nullptr, 0, 0, nullptr, nullptr,
                        c.sd(m->part));
-    hipLaunchKernelGGL(bn_stats_final_kernel, dim3((L.cout + 255) / 256), dim3(256), 0, c.st,
+    hipLaunchKernelGGL(bn_stats_final_kernel, dim3((L.cout + 3) / 4), dim3(256), 0, c.st,
                        c.sd(m->part), g.nchunk, L.cout, P, mom, mean, rstd,
                        stats ? stats + L.rm_off : nullptr, stats ? stats + L.rv_off : nullptr);
     if (out)
@@ -435,7 +435,7 @@ int layer_bwd(Ctx& c, int li, const float* x, int xcs, int h, int w, const float
   PF_TRY(timed(c, "bwd:bn", 0, [&] {
     hipLaunchKernelGGL(bn_partial_kernel<1>, dim3(g.nchunk, g.gy), dim3(256), 0, c.st, y, P, C,
                        g.chunk, a, acs, da, dacs, L.act, mean, rstd, c.sd(m->part));
-    hipLaunchKernelGGL(bn_bwd_final_kernel, dim3((C + 255) / 256), dim3(256), 0, c.st,
+    hipLaunchKernelGGL(bn_bwd_final_kernel, dim3((C + 3) / 4), dim3(256), 0, c.st,
                        c.sd(m->part), g.nchunk, C, P, c.prm + L.g_off, rstd, grad + L.g_off,
                        grad + L.be_off, acc, coef);
     hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(P * c4n, 256)), dim3(256), 0, c.st, y, P,

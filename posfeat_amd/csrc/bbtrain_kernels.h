@@ -75,18 +75,44 @@ __global__ __launch_bounds__(256) void bn_partial_kernel(
   }
 }
 
+// Chunk partials -> per-channel totals: block = 4 channels x 64 chunk lanes,
+// fixed-order strided sums + LDS tree (deterministic, no serial 1000-deep
+// dependent-load chain per channel).
+__device__ __forceinline__ void bn_chunk_sum(const double* __restrict__ part, int nchunk, int C,
+                                             double (*red)[64][4], double& s0, double& s1) {
+  const int cl = threadIdx.x & 3, kl = threadIdx.x >> 2;
+  const int c = blockIdx.x * 4 + cl;
+  double a = 0.0, b = 0.0;
+  if (c < C)
+    for (int k = kl; k < nchunk; k += 64) {
+      a += part[(long long)k * 2 * C + c];
+      b += part[(long long)k * 2 * C + C + c];
+    }
+  red[0][kl][cl] = a;
+  red[1][kl][cl] = b;
+  __syncthreads();
+  for (int o = 32; o > 0; o >>= 1) {
+    if (kl < o) {
+      red[0][kl][cl] += red[0][kl + o][cl];
+      red[1][kl][cl] += red[1][kl + o][cl];
+    }
+    __syncthreads();
+  }
+  s0 = red[0][0][cl];
+  s1 = red[1][0][cl];
+}
+
 // batch mean / rstd (biased variance) and the running-stat update
 // (torch: running = (1 - m) running + m batch, with the unbiased variance)
-__global__ void bn_stats_final_kernel(const double* __restrict__ part, int nchunk, int C, long long P,
-                                      float mom, float* __restrict__ mean, float* __restrict__ rstd,
-                                      float* __restrict__ rm, float* __restrict__ rv) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s = 0.0, ss = 0.0;
-  for (int k = 0; k < nchunk; ++k) {
-    s += part[(long long)k * 2 * C + c];
-    ss += part[(long long)k * 2 * C + C + c];
-  }
+__global__ __launch_bounds__(256) void bn_stats_final_kernel(
+    const double* __restrict__ part, int nchunk, int C, long long P, float mom,
+    float* __restrict__ mean, float* __restrict__ rstd, float* __restrict__ rm,
+    float* __restrict__ rv) {
+  __shared__ double red[2][64][4];
+  double s, ss;
+  bn_chunk_sum(part, nchunk, C, red, s, ss);
+  const int c = blockIdx.x * 4 + (threadIdx.x & 3);
+  if ((threadIdx.x >> 2) != 0 || c >= C) return;
   const double mu = s / (double)P;
   double var = ss / (double)P - mu * mu;
   var = var > 0.0 ? var : 0.0;
@@ -127,17 +153,15 @@ __global__ void bn_apply_kernel(const float* __restrict__ y, long long P, int c4
 }
 
 // dgamma / dbeta (accumulated over the step's batches) and the apply coefficients
-__global__ void bn_bwd_final_kernel(const double* __restrict__ part, int nchunk, int C, long long P,
-                                    const float* __restrict__ gam, const float* __restrict__ rstd,
-                                    float* __restrict__ dgam, float* __restrict__ dbet, int acc,
-                                    float* __restrict__ coef) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double sg = 0.0, sgx = 0.0;
-  for (int k = 0; k < nchunk; ++k) {
-    sg += part[(long long)k * 2 * C + c];
-    sgx += part[(long long)k * 2 * C + C + c];
-  }
+__global__ __launch_bounds__(256) void bn_bwd_final_kernel(
+    const double* __restrict__ part, int nchunk, int C, long long P, const float* __restrict__ gam,
+    const float* __restrict__ rstd, float* __restrict__ dgam, float* __restrict__ dbet, int acc,
+    float* __restrict__ coef) {
+  __shared__ double red[2][64][4];
+  double sg, sgx;
+  bn_chunk_sum(part, nchunk, C, red, sg, sgx);
+  const int c = blockIdx.x * 4 + (threadIdx.x & 3);
+  if ((threadIdx.x >> 2) != 0 || c >= C) return;
   dgam[c] = acc ? dgam[c] + (float)sgx : (float)sgx;
   dbet[c] = acc ? dbet[c] + (float)sg : (float)sg;
   coef[c] = gam[c] * rstd[c];

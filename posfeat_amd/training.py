@@ -34,6 +34,18 @@ DISK_DEFAULTS = {"grid_size": 8, "loss_distance": "cos", "temperature_base": 60,
                  "match_grad": False}
 
 
+# configs/train_desc.yaml:61-91 (preprocess_train_config, EpipolarLoss_full_config)
+DESC_PRE_DEFAULTS = {"kps_generator": "generate_kpts_regular_grid_random",
+                     "kps_generator_config": {"grid_size": 16, "map_init": "identity",
+                                              "keep_spatial": True, "random_select": "random"},
+                     "window_size": 0.1, "loss_distance": "cos", "use_nn_grid": False,
+                     "use_line_search": True,
+                     "line_search_config": {"line_step": 100, "use_nn": True, "loc_rand": True},
+                     "temperature_base": 60, "temperature_max": 60}
+DESC_EPI_DEFAULTS = {"grid_cost_thr": 0.5, "win_cost_thr": 0.1, "use_std_as_weight": True,
+                     "weight_grid": 0, "weight_window": 1}
+
+
 def _check_disk_config(cfg):
     rc = cfg.get("reward_config", {})
     if (cfg["grid_size"] != 8 or cfg["epipolar_reward"] != "constant_reward"
