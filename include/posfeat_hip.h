@@ -254,6 +254,18 @@ int posfeat_conv_wgrad(const float *dy, int dy_cstride, const float *x, int x_cs
                        int h, int w, int cin, int cout, int kh, int kw, float *dw, float *db,
                        void *ws, size_t ws_bytes, void *stream);
 
+/* Winograd F(2x2,3x3) 3x3 stride-1 pad-1 conv (the decoder layers,
+ * networks/DescNet.py:41-45, as the engine runs them): U = 16 transformed
+ * weight matrices [16][cout][cin] from the engine-packed weights
+ * (posfeat_wino_weights), then input transform -> 16 GEMMs (one launch) ->
+ * output transform + bias + act into y (pixel stride y_cstride).  h, w even;
+ * cin % 32 == 0.  Same result as posfeat_conv2d_nhwc within fp32 rounding. */
+size_t posfeat_wino_workspace(int n, int h, int w, int cin, int cout);
+int posfeat_wino_weights(const float *w_packed, int cout, int cin, float *U, void *stream);
+int posfeat_conv3x3_wino(const float *x, int x_cstride, int n, int h, int w, int cin,
+                         const float *U, const float *bias, int cout, int act, float *y,
+                         int y_cstride, void *ws, size_t ws_bytes, void *stream);
+
 /* torch.optim.SGD step without momentum/weight decay (train_kp.yaml:11-13,
  * managers/trainer.py:118-119, 356): w -= lr * g over n floats. */
 int posfeat_sgd(float *w, const float *g, long long n, float lr, void *stream);

@@ -44,6 +44,9 @@ struct ConvArgs {
   int hw;            // OH*OW (image boundary inside a tile for `stats`)
   // conv_up4_kernel only: the low-res grid
   int lh, lw;
+  // batched 1x1 GEMMs (conv_glds_kernel only): blockIdx.y selects x/w/y + z*stride
+  int nbatch;
+  long long bx, bw, by;
 };
 
 // Epilogue shared by both kernels: acc -> LDS T[BM][BN+4] (conflict-free: a
@@ -381,6 +384,12 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_glds_kernel(ConvArgs a) {
   {
     const int nwg = a.nwg, q = nwg >> 3, r = nwg & 7, xcd = bid & 7, slot = bid >> 3;
     bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+  }
+  if (a.nbatch > 1) {  // batched GEMMs (Winograd): one operand set per blockIdx.y
+    const long long zb = blockIdx.y;
+    a.x += zb * a.bx;
+    a.w += zb * a.bw;
+    a.y += zb * a.by;
   }
   const int tm = bid / a.tiles_n, tn = bid - tm * a.tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
@@ -1248,7 +1257,7 @@ Plan conv_plan(const ConvArgs& a, bool allow_split, int forced = -1) {
 
 template <int BM, int BN, int WM, int WN>
 void launch_rows(ConvArgs& a, int kern, hipStream_t st) {
-  dim3 grid(a.nwg * a.ksplit), block(WM * WN * 64);
+  dim3 grid(a.nwg * a.ksplit, a.nbatch), block(WM * WN * 64);
   if (kern == KERN_GLDS)
     hipLaunchKernelGGL((conv_glds_kernel<BM, BN, WM, WN>), grid, block, 0, st, a);
   else if (a.Cin % BK == 0)
@@ -1347,6 +1356,8 @@ static int conv_prepare(const posfeat_conv_desc* d, const float* x, const float*
   a.part = nullptr;
   a.stats = nullptr;
   a.hw = a.OH * a.OW;
+  a.nbatch = 1;
+  a.bx = a.bw = a.by = 0;
   return POSFEAT_OK;
 }
 
@@ -1610,4 +1621,34 @@ extern "C" int posfeat_conv2_up4(int n, int H, int W, const float* L, int lcs, c
   PF_TRY(pf_up4_border(n, H, W, L, lcs, wph, y, ycs, st));
   // 3. the 192 upsampled channels by phases, + y, IN statistics
   return pf_up4_main(n, H, W, L, lcs, wph, y, ycs, ws, ws_bytes, mean, rstd, eps, st);
+}
+
+// C[z] [M][N] = A[z] [M][K] (row pitch lda) x B[z]^T, B[z] packed [N][K] (K % 32
+// == 0, the 1x1-conv weight layout), z < nb: ONE launch of conv_glds_kernel with
+// blockIdx.y = z (Winograd's 16 transform-domain GEMMs, wino.hip).
+int pf_gemm_batched(const float* A, int lda, long long sa, const float* B, long long sb, float* C,
+                    int ldc, long long sc, int nb, int M, int N, int K, hipStream_t st) {
+  if (K % BK || N % 4 || nb < 1) return POSFEAT_E_INVALID;
+  posfeat_conv_desc d;
+  d.n = 1;
+  d.h = 1;
+  d.w = M;
+  d.cin = K;
+  d.x_cstride = lda;
+  d.cout = N;
+  d.kh = d.kw = 1;
+  d.stride = 1;
+  d.pad = 0;
+  d.y_cstride = ldc;
+  d.res_cstride = 0;
+  d.act = POSFEAT_ACT_NONE;
+  ConvArgs a;
+  PF_TRY(conv_prepare(&d, A, B, nullptr, nullptr, C, a));
+  const Plan p = conv_plan(a, false);
+  if (p.kern != KERN_GLDS) return POSFEAT_E_UNSUPPORTED;
+  a.nbatch = nb;
+  a.bx = sa;
+  a.bw = sb;
+  a.by = sc;
+  return conv_run(a, p, st);
 }

@@ -110,6 +110,10 @@ struct posfeat_model {
   Buf st_mean, st_rstd, st_part;  // instance-norm scratch (floats / doubles)
   Buf st_mean1, st_rstd1;
   Buf splitk;                      // split-K partial slabs (max over layers)
+  // Winograd F(2x2,3x3) for the four decoder 3x3 convs (wino.hip): transformed
+  // weights (rebuilt each forward: the blob may change between calls) + V/M
+  bool wino = true;
+  Buf wino_u, wino_ws;
   size_t splitk_need = 0;
   // per-layer conv tile chosen by timing the legal candidates on the first
   // forward of this shape (results do not depend on the tile)
@@ -243,6 +247,38 @@ int conv(Ctx& c, const std::string& name, const float* x, int n, int h, int w, i
 
 int forward(Ctx& c, const float* img, posfeat_extract_out* out);
 
+// The decoder's 3x3 stride-1 convs (DescNet.py:41-45) through Winograd
+// F(2x2,3x3) when enabled (default; POSFEAT_WINO=0 for the direct conv)
+const char* const kWinoLayers[4] = {"upconv3.conv", "iconv3", "upconv2.conv", "iconv2"};
+
+long long wino_u_offset(const std::string& name) {
+  long long off = 0;
+  for (const char* n : kWinoLayers) {
+    if (name == n) return off;
+    const Spec* s = specs().find(n);
+    off += (long long)16 * s->cout * s->cin;
+  }
+  return -1;
+}
+
+int conv3x3(Ctx& c, const std::string& name, const float* x, int n, int h, int w, int xcs, float* y,
+            int ycs, int act) {
+  posfeat_model* m = c.m;
+  const long long uo = wino_u_offset(name);
+  if (!m->wino || uo < 0 || (h & 1) || (w & 1))
+    return conv(c, name, x, n, h, w, xcs, y, ycs, 1, act);
+  const Spec* s = specs().find(name);
+  if (c.dry) return POSFEAT_OK;
+  float* U = c.f(m->wino_u) + uo;
+  PF_TRY(timed(c, "wino:weights", 0,
+               [&] { return pf_wino_weights(c.W(name), s->cout, s->cin, U, c.st); }));
+  const double T = (double)n * (h / 2) * (w / 2);
+  return timed(c, "conv:" + name + ".wino", 2.0 * T * 16 * s->cin * s->cout, [&] {
+    return pf_wino_conv(x, xcs, n, h, w, s->cin, U, c.Bi(name), s->cout, act, y, ycs,
+                        c.f(m->wino_ws), m->wino_ws.floats * sizeof(float), c.st);
+  });
+}
+
 // conv whose epilogue also produces the InstanceNorm mean/rstd of its output
 // (falls back to a separate statistics pass when a tile could span >2 images)
 int conv_in(Ctx& c, const std::string& name, const float* x, int n, int h, int w, int xcs,
@@ -337,6 +373,20 @@ void plan(posfeat_model* m) {
     m->up4 = !(e && e[0] == '0');
     const char* t = getenv("POSFEAT_AUTOTUNE");  // 0: heuristic tiles only
     m->autotune = !(t && t[0] == '0');
+    const char* wv = getenv("POSFEAT_WINO");  // 0: direct conv for the decoder 3x3 layers
+    m->wino = !(wv && wv[0] == '0');
+  }
+  if (m->wino) {
+    size_t uf = 0, wb = 0;
+    const int dims[4][2] = {{(int)h8, (int)w8}, {(int)h8, (int)w8}, {(int)h4, (int)w4},
+                            {(int)h4, (int)w4}};
+    for (int i = 0; i < 4; ++i) {
+      const Spec* s = specs().find(kWinoLayers[i]);
+      uf += (size_t)16 * s->cout * s->cin;
+      wb = std::max(wb, pf_wino_ws_bytes((int)B, dims[i][0], dims[i][1], s->cin, s->cout));
+    }
+    alloc(m->wino_u, uf);
+    alloc(m->wino_ws, wb / 4 + 4);
   }
   if (m->train) m->up4 = false;  // the backward reads the materialised conv2 input
   if (m->up4) {
@@ -455,13 +505,13 @@ int forward(Ctx& c, const float* img, posfeat_extract_out* out) {
   PF_TRY(timed(c, "upsample2x", 0, [&] {
     return pf_upsample2x_ac(c.f(m->l3out), B, h16, w16, 1024, 1024, c.f(m->up3), 1024, c.st);
   }));
-  PF_TRY(conv(c, "upconv3.conv", c.f(m->up3), B, h8, w8, 1024, cat3, 1024, 1, POSFEAT_ACT_ELU));
-  PF_TRY(conv(c, "iconv3", cat3, B, h8, w8, 1024, c.f(m->d3), 512, 1, POSFEAT_ACT_ELU));
+  PF_TRY(conv3x3(c, "upconv3.conv", c.f(m->up3), B, h8, w8, 1024, cat3, 1024, POSFEAT_ACT_ELU));
+  PF_TRY(conv3x3(c, "iconv3", cat3, B, h8, w8, 1024, c.f(m->d3), 512, POSFEAT_ACT_ELU));
   PF_TRY(timed(c, "upsample2x", 0, [&] {
     return pf_upsample2x_ac(c.f(m->d3), B, h8, w8, 512, 512, c.f(m->up2), 512, c.st);
   }));
-  PF_TRY(conv(c, "upconv2.conv", c.f(m->up2), B, h4, w4, 512, cat2, 512, 1, POSFEAT_ACT_ELU));
-  PF_TRY(conv(c, "iconv2", cat2, B, h4, w4, 512, c.f(m->d2), 256, 1, POSFEAT_ACT_ELU));
+  PF_TRY(conv3x3(c, "upconv2.conv", c.f(m->up2), B, h4, w4, 512, cat2, 512, POSFEAT_ACT_ELU));
+  PF_TRY(conv3x3(c, "iconv2", cat2, B, h4, w4, 512, c.f(m->d2), 256, POSFEAT_ACT_ELU));
   PF_TRY(conv(c, "conv_fine", c.f(m->d2), B, h4, w4, 256, headcat, 192, 1, POSFEAT_ACT_ELU));
   // ---- KeypointDet (DeteNet.py:102-121), identity prior == exact 1.0 -------
   // IN statistics slots: conv1, convimg, conv2 (the backward reads all three)

@@ -42,3 +42,14 @@ size_t pf_conv_stats_ws_max(const posfeat_conv_desc* d);
 int pf_conv_stats_run_tile(const posfeat_conv_desc* d, const float* x, const float* w,
                            const float* bias, float* y, void* ws, size_t ws_bytes, float* mean,
                            float* rstd, float eps, int tile, hipStream_t st);
+
+// batched GEMM on the conv engine (conv.hip): C[z] = A[z] x B[z]^T, z < nb
+int pf_gemm_batched(const float* A, int lda, long long sa, const float* B, long long sb, float* C,
+                    int ldc, long long sc, int nb, int M, int N, int K, hipStream_t st);
+// Winograd F(2x2,3x3) (wino.hip): U = [16][Cout][Cin] transformed weights
+size_t pf_wino_ws_bytes(int n, int h, int w, int Cin, int Cout);
+size_t pf_wino_weights_floats(int Cin, int Cout);
+int pf_wino_weights(const float* wpk, int Cout, int Cin, float* U, hipStream_t st);
+int pf_wino_conv(const float* x, int xcs, int n, int h, int w, int Cin, const float* U,
+                 const float* bias, int Cout, int act, float* y, int ycs, void* ws, size_t ws_bytes,
+                 hipStream_t st);

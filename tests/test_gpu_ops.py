@@ -76,6 +76,50 @@ def test_conv_vs_torch(gpu, case):
         assert torch.all(out[..., cout:] == 7.0).item(), "wrote outside its channel slice"
 
 
+WINO_CASES = [
+    # n, h, w, cin, cout, act, in_extra, out_extra
+    (2, 16, 24, 64, 64, "none", 0, 0),
+    (1, 30, 40, 1024, 512, "elu", 0, 512),   # upconv3 shape into a concat slice
+    (2, 14, 10, 512, 256, "elu", 64, 0),     # ragged tile grid, strided input
+    (1, 60, 80, 512, 256, "relu", 0, 256),
+]
+
+
+@pytest.mark.parametrize("case", WINO_CASES)
+def test_conv3x3_wino_vs_torch(gpu, case):
+    """Winograd F(2x2,3x3) path (wino.hip) against the fp64 conv: the transforms
+    use exact +-1, 1/2 weights, so the error bound is the direct conv's times a
+    small factor (transform-domain sums grow the rounding by ~4x)."""
+    from posfeat_amd import ops
+    from posfeat_amd._lib import check, lib, ptr, stream_ptr
+    n, h, w, cin, cout, act, in_extra, out_extra = case
+    g = torch.Generator().manual_seed(sum(case[:5]))
+    x = torch.randn(n, cin, h, w, generator=g)
+    wt = torch.randn(cout, cin, 3, 3, generator=g) * (2.0 / (cin * 9)) ** 0.5
+    b = torch.randn(cout, generator=g) * 0.1
+    ref, bound = _conv_ref64(x, wt, b, 1, 1, None, act)
+    xcs = cin + in_extra
+    xd = torch.zeros(n, h, w, xcs)
+    xd[..., :cin] = x.permute(0, 2, 3, 1)
+    xd = xd.to(gpu)
+    wp, bp = ops.pack_conv_weight(wt.to(gpu), b.to(gpu))
+    U = torch.empty(16 * cout * cin, device=gpu)
+    check(lib().posfeat_wino_weights(ptr(wp), cout, cin, ptr(U), stream_ptr()))
+    need = lib().posfeat_wino_workspace(n, h, w, cin, cout)
+    ws = torch.empty(need, dtype=torch.uint8, device=gpu)
+    out = torch.full((n, h, w, cout + out_extra), 7.0, device=gpu)
+    actc = {"none": 0, "relu": 1, "elu": 2}[act]
+    check(lib().posfeat_conv3x3_wino(ptr(xd), xcs, n, h, w, cin, ptr(U), ptr(bp), cout, actc,
+                                     ptr(out), cout + out_extra, ptr(ws), need, stream_ptr()))
+    torch.cuda.synchronize()
+    got = out[..., :cout].permute(0, 3, 1, 2).double().cpu()
+    err = (got - ref).abs()
+    tol = 8e-6 * bound + 1e-6
+    assert torch.all(err <= tol), "max err %g (ratio %g)" % (err.max(), (err / tol).max())
+    if out_extra:
+        assert torch.all(out[..., cout:] == 7.0).item(), "wrote outside its channel slice"
+
+
 @pytest.mark.parametrize("act,has_res", [("elu", False), ("relu", True)])
 def test_conv_splitk_vs_torch(gpu, act, has_res):
     """Deep-K shape that takes the split-K path (partials + ordered reduce)."""
