@@ -155,6 +155,10 @@ struct posfeat_bbtrain {
   // scratch (shared by the batches: forward transients + backward)
   size_t scr_bytes = 0;
   Buf dsn, part, coef, ga, gb, gc, gd, gres, dy, dz, dcat2, dcat3, dup, upt, wt, wgws, splitk;
+  // Winograd F(2x2,3x3) for the decoder's 3x3 convs, forward and input
+  // gradient (wino.hip; POSFEAT_WINO=0: direct conv)
+  bool wino = true;
+  Buf wu, wino_ws;
   // optional per-launch timing (labels "fwd:conv", "bwd:wgrad", ...)
   bool timing = false;
   struct Ev {
@@ -250,6 +254,13 @@ posfeat_conv_desc make_desc(int n, int h, int w, int cin, int xcs, int cout, int
 }
 
 inline int out_dim(int h, int k, int s) { return (h + 2 * ((k - 1) / 2) - k) / s + 1; }
+
+// the decoder's 3x3 stride-1 convs go through Winograd F(2x2,3x3)
+bool use_wino(const posfeat_bbtrain* m, int li, int h, int w) {
+  const TTable& T = tab();
+  return m->wino && (li == T.up3 || li == T.ic3 || li == T.up2 || li == T.ic2) && !(h & 1) &&
+         !(w & 1);
+}
 
 // input spatial size of every layer (forward order of DescNet.py:64-84)
 void layer_inputs(int H, int W, std::vector<int>& ih, std::vector<int>& iw) {
@@ -363,6 +374,21 @@ void plan(posfeat_bbtrain* m) {
   alloc(m->wt, fl(wt));
   alloc(m->wgws, wg);
   alloc(m->splitk, std::max<size_t>(sk, 256));
+  {
+    const char* e = getenv("POSFEAT_WINO");
+    m->wino = !(e && e[0] == '0');
+  }
+  if (m->wino) {
+    size_t uf = 0, wb = 0;
+    for (int li : {T.up3, T.ic3, T.up2, T.ic2}) {
+      const TLayer& L = T.v[li];
+      uf = std::max(uf, (size_t)16 * L.cin * L.cout);
+      wb = std::max(wb, pf_wino_ws_bytes((int)B, lih[li], liw[li], L.cin, L.cout));
+      wb = std::max(wb, pf_wino_ws_bytes((int)B, lih[li], liw[li], L.cout, L.cin));
+    }
+    alloc(m->wu, fl(uf));
+    alloc(m->wino_ws, wb);
+  }
   m->scr_bytes = cur;
 }
 
@@ -377,10 +403,19 @@ int layer_fwd(Ctx& c, int li, const float* x, int xcs, int h, int w, float* out,
   const long long P = (long long)m->B * oh * ow;
   float* y = c.f(m->y[li]);
   posfeat_conv_desc d = make_desc(m->B, h, w, L.cin, xcs, L.cout, L.k, L.stride, L.cout, 0);
-  PF_TRY(timed(c, "fwd:conv", 2.0 * P * L.cout * L.cin * L.k * L.k, [&] {
-    return pf_conv_run_tile(&d, x, c.prm + L.w_off, L.bias ? c.prm + L.b_off : nullptr, nullptr, y,
-                            c.s(m->splitk), m->splitk.bytes, -1, c.st);
-  }));
+  if (use_wino(m, li, h, w)) {
+    float* U = c.s(m->wu);
+    PF_TRY(timed(c, "fwd:conv", 2.0 * P * L.cout * L.cin * L.k * L.k, [&] {
+      PF_TRY(pf_wino_weights(c.prm + L.w_off, L.cout, L.cin, U, c.st));
+      return pf_wino_conv(x, xcs, m->B, h, w, L.cin, U, c.prm + L.b_off, L.cout, ACT_NONE, y,
+                          L.cout, c.s(m->wino_ws), m->wino_ws.bytes, c.st);
+    }));
+  } else {
+    PF_TRY(timed(c, "fwd:conv", 2.0 * P * L.cout * L.cin * L.k * L.k, [&] {
+      return pf_conv_run_tile(&d, x, c.prm + L.w_off, L.bias ? c.prm + L.b_off : nullptr, nullptr,
+                              y, c.s(m->splitk), m->splitk.bytes, -1, c.st);
+    }));
+  }
   float* mean = c.f(m->st[li]);
   float* rstd = mean + L.cout;
   const BnGrid g = bn_grid(P, L.cout);
@@ -464,6 +499,14 @@ int layer_bwd(Ctx& c, int li, const float* x, int xcs, int h, int w, const float
     }
     return (int)POSFEAT_OK;
   }));
+  if (!add && use_wino(m, li, h, w)) {
+    float* U = c.s(m->wu);
+    return timed(c, "bwd:dgrad", flops, [&] {
+      PF_TRY(pf_wino_weights(wt, L.cin, C, U, c.st));
+      return pf_wino_conv(src, C, B, h, w, C, U, nullptr, L.cin, ACT_NONE, dx, dxcs,
+                          c.s(m->wino_ws), m->wino_ws.bytes, c.st);
+    });
+  }
   posfeat_conv_desc d = make_desc(B, h, w, C, C, L.cin, L.k, 1, dxcs, add ? addcs : 0);
   return timed(c, "bwd:dgrad", flops, [&] {
     return pf_conv_run_tile(&d, src, wt, nullptr, add, dx, c.s(m->splitk), m->splitk.bytes, -1,
