@@ -114,6 +114,9 @@ struct posfeat_model {
   // weights (rebuilt each forward: the blob may change between calls) + V/M
   bool wino = true;
   Buf wino_u, wino_ws;
+  // head.conv2's G part as a per-image 5x5 conv of the image (gfuse.hip)
+  bool gfuse = true;
+  Buf gf_w, gf_b;
   size_t splitk_need = 0;
   // per-layer conv tile chosen by timing the legal candidates on the first
   // forward of this shape (results do not depend on the tile)
@@ -375,6 +378,12 @@ void plan(posfeat_model* m) {
     m->autotune = !(t && t[0] == '0');
     const char* wv = getenv("POSFEAT_WINO");  // 0: direct conv for the decoder 3x3 layers
     m->wino = !(wv && wv[0] == '0');
+    const char* gv = getenv("POSFEAT_GFUSE");  // 0: conv2's G part as the 64-ch 3x3 conv
+    m->gfuse = !(gv && gv[0] == '0');
+  }
+  if (m->up4 && m->gfuse) {
+    alloc(m->gf_w, B * 128 * 128);
+    alloc(m->gf_b, B * 128);
   }
   if (m->wino) {
     size_t uf = 0, wb = 0;
@@ -533,18 +542,33 @@ int forward(Ctx& c, const float* img, posfeat_extract_out* out) {
     }));
     float* g64 = c.f(m->g64);
     PF_TRY(conv_in(c, "head.convimg", img4, B, H, W, 4, g64, 64, meanI, rstdI));
-    PF_TRY(timed(c, "instnorm_apply", 0, [&] {
-      return pf_in_apply(g64, B, H * W, 64, 64, meanI, rstdI, nullptr, c.st);
-    }));
+    if (!m->gfuse)
+      PF_TRY(timed(c, "instnorm_apply", 0, [&] {
+        return pf_in_apply(g64, B, H * W, 64, 64, meanI, rstdI, nullptr, c.st);
+      }));
     // executed MFMA work: 64 full-res channels x 9 taps, 192 low-res channels
     // x 6.25 taps on average over the 16 phases (the reference layer: 256 x 9)
     const float* wph = c.f(m->wph);
     PF_TRY(timed(c, "head.conv2.weights", 0, [&] {
       return posfeat_conv2_up4_weights(c.W("head.conv2"), c.f(m->wph), c.st);
     }));
-    PF_TRY(timed(c, "conv:head.conv2.g", 2.0 * B * H * W * 128.0 * 64 * 9, [&] {
-      return pf_up4_gconv(B, H, W, g64, 64, wph, c.Bi("head.conv2"), c2, 128, c.st);
-    }));
+    if (m->gfuse) {
+      // G = IN(convimg(img)) folded into a per-image 5x5 conv of the image
+      // (+ the exact one-pixel border ring); g64 holds the raw convimg output
+      PF_TRY(timed(c, "head.conv2.gfuse_w", 0, [&] {
+        return pf_gfuse_weights(c.W("head.conv2"), c.Bi("head.conv2"), c.W("head.convimg"),
+                                c.Bi("head.convimg"), meanI, rstdI, B, c.f(m->gf_w),
+                                c.f(m->gf_b), c.st);
+      }));
+      PF_TRY(timed(c, "conv:head.conv2.g", 2.0 * B * H * W * 128.0 * 4 * 25, [&] {
+        return pf_gfuse_conv(img4, g64, 64, B, H, W, c.f(m->gf_w), c.f(m->gf_b), meanI, rstdI,
+                             c.W("head.conv2"), c.Bi("head.conv2"), c2, 128, c.st);
+      }));
+    } else {
+      PF_TRY(timed(c, "conv:head.conv2.g", 2.0 * B * H * W * 128.0 * 64 * 9, [&] {
+        return pf_up4_gconv(B, H, W, g64, 64, wph, c.Bi("head.conv2"), c2, 128, c.st);
+      }));
+    }
     PF_TRY(timed(c, "head.conv2.border", 0, [&] {
       return pf_up4_border(B, H, W, c1, 192, wph, c2, 128, c.st);
     }));

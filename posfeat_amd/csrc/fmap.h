@@ -53,3 +53,11 @@ int pf_wino_weights(const float* wpk, int Cout, int Cin, float* U, hipStream_t s
 int pf_wino_conv(const float* x, int xcs, int n, int h, int w, int Cin, const float* U,
                  const float* bias, int Cout, int act, float* y, int ycs, void* ws, size_t ws_bytes,
                  hipStream_t st);
+// head.conv2's G part as one per-image 5x5 conv of the image (gfuse.hip)
+size_t pf_gfuse_weights_floats(int n);
+int pf_gfuse_weights(const float* w2_packed, const float* b2, const float* w1_packed,
+                     const float* b1, const float* mean, const float* rstd, int n, float* wc,
+                     float* bc, hipStream_t st);
+int pf_gfuse_conv(const float* img4, const float* c, int ccs, int n, int H, int W,
+                  const float* wc, const float* bc, const float* mean, const float* rstd,
+                  const float* w2_packed, const float* b2, float* y, int ycs, hipStream_t st);
