@@ -254,14 +254,17 @@ int posfeat_conv_wgrad(const float *dy, int dy_cstride, const float *x, int x_cs
                        int h, int w, int cin, int cout, int kh, int kw, float *dw, float *db,
                        void *ws, size_t ws_bytes, void *stream);
 
-/* Winograd F(2x2,3x3) 3x3 stride-1 pad-1 conv (the decoder layers,
- * networks/DescNet.py:41-45, as the engine runs them): U = 16 transformed
- * weight matrices [16][cout][cin] from the engine-packed weights
- * (posfeat_wino_weights), then input transform -> 16 GEMMs (one launch) ->
- * output transform + bias + act into y (pixel stride y_cstride).  h, w even;
- * cin % 32 == 0.  Same result as posfeat_conv2d_nhwc within fp32 rounding. */
+/* Winograd 3x3 stride-1 pad-1 conv (the decoder layers,
+ * networks/DescNet.py:41-45, as the engine runs them): F(4x4,3x3) when h and w
+ * are multiples of 4 (36 transformed weight matrices), else F(2x2,3x3) (16).
+ * U ([36][cout][cin] floats) from the engine-packed weights by
+ * posfeat_wino_weights for the same (h, w); then input transform -> the
+ * transform-domain GEMMs (one launch) -> output transform + bias + act into y
+ * (pixel stride y_cstride).  h, w even; cin % 32 == 0.  Same result as
+ * posfeat_conv2d_nhwc within fp32 rounding (transform-grown). */
 size_t posfeat_wino_workspace(int n, int h, int w, int cin, int cout);
-int posfeat_wino_weights(const float *w_packed, int cout, int cin, float *U, void *stream);
+int posfeat_wino_weights(const float *w_packed, int cout, int cin, int h, int w, float *U,
+                         void *stream);
 int posfeat_conv3x3_wino(const float *x, int x_cstride, int n, int h, int w, int cin,
                          const float *U, const float *bias, int cout, int act, float *y,
                          int y_cstride, void *ws, size_t ws_bytes, void *stream);

@@ -98,7 +98,7 @@ SIGNATURES = {
     "posfeat_model_head_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
                                             c_void_p]),
     "posfeat_wino_workspace": (c_size_t, [c_int] * 5),
-    "posfeat_wino_weights": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "posfeat_wino_weights": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     "posfeat_conv3x3_wino": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
                                      c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_size_t,
                                      c_void_p]),

@@ -382,7 +382,7 @@ void plan(posfeat_bbtrain* m) {
     size_t uf = 0, wb = 0;
     for (int li : {T.up3, T.ic3, T.up2, T.ic2}) {
       const TLayer& L = T.v[li];
-      uf = std::max(uf, (size_t)16 * L.cin * L.cout);
+      uf = std::max(uf, (size_t)36 * L.cin * L.cout);
       wb = std::max(wb, pf_wino_ws_bytes((int)B, lih[li], liw[li], L.cin, L.cout));
       wb = std::max(wb, pf_wino_ws_bytes((int)B, lih[li], liw[li], L.cout, L.cin));
     }
@@ -406,7 +406,7 @@ int layer_fwd(Ctx& c, int li, const float* x, int xcs, int h, int w, float* out,
   if (use_wino(m, li, h, w)) {
     float* U = c.s(m->wu);
     PF_TRY(timed(c, "fwd:conv", 2.0 * P * L.cout * L.cin * L.k * L.k, [&] {
-      PF_TRY(pf_wino_weights(c.prm + L.w_off, L.cout, L.cin, U, c.st));
+      PF_TRY(pf_wino_weights_hw(c.prm + L.w_off, L.cout, L.cin, h, w, U, c.st));
       return pf_wino_conv(x, xcs, m->B, h, w, L.cin, U, c.prm + L.b_off, L.cout, ACT_NONE, y,
                           L.cout, c.s(m->wino_ws), m->wino_ws.bytes, c.st);
     }));
@@ -502,7 +502,7 @@ int layer_bwd(Ctx& c, int li, const float* x, int xcs, int h, int w, const float
   if (!add && use_wino(m, li, h, w)) {
     float* U = c.s(m->wu);
     return timed(c, "bwd:dgrad", flops, [&] {
-      PF_TRY(pf_wino_weights(wt, L.cin, C, U, c.st));
+      PF_TRY(pf_wino_weights_hw(wt, L.cin, C, h, w, U, c.st));
       return pf_wino_conv(src, C, B, h, w, C, U, nullptr, L.cin, ACT_NONE, dx, dxcs,
                           c.s(m->wino_ws), m->wino_ws.bytes, c.st);
     });

@@ -259,7 +259,7 @@ long long wino_u_offset(const std::string& name) {
   for (const char* n : kWinoLayers) {
     if (name == n) return off;
     const Spec* s = specs().find(n);
-    off += (long long)16 * s->cout * s->cin;
+    off += (long long)36 * s->cout * s->cin;
   }
   return -1;
 }
@@ -274,7 +274,7 @@ int conv3x3(Ctx& c, const std::string& name, const float* x, int n, int h, int w
   if (c.dry) return POSFEAT_OK;
   float* U = c.f(m->wino_u) + uo;
   PF_TRY(timed(c, "wino:weights", 0,
-               [&] { return pf_wino_weights(c.W(name), s->cout, s->cin, U, c.st); }));
+               [&] { return pf_wino_weights_hw(c.W(name), s->cout, s->cin, h, w, U, c.st); }));
   const double T = (double)n * (h / 2) * (w / 2);
   return timed(c, "conv:" + name + ".wino", 2.0 * T * 16 * s->cin * s->cout, [&] {
     return pf_wino_conv(x, xcs, n, h, w, s->cin, U, c.Bi(name), s->cout, act, y, ycs,
@@ -391,7 +391,7 @@ void plan(posfeat_model* m) {
                             {(int)h4, (int)w4}};
     for (int i = 0; i < 4; ++i) {
       const Spec* s = specs().find(kWinoLayers[i]);
-      uf += (size_t)16 * s->cout * s->cin;
+      uf += (size_t)36 * s->cout * s->cin;
       wb = std::max(wb, pf_wino_ws_bytes((int)B, dims[i][0], dims[i][1], s->cin, s->cout));
     }
     alloc(m->wino_u, uf);

@@ -49,7 +49,10 @@ int pf_gemm_batched(const float* A, int lda, long long sa, const float* B, long 
 // Winograd F(2x2,3x3) (wino.hip): U = [16][Cout][Cin] transformed weights
 size_t pf_wino_ws_bytes(int n, int h, int w, int Cin, int Cout);
 size_t pf_wino_weights_floats(int Cin, int Cout);
-int pf_wino_weights(const float* wpk, int Cout, int Cin, float* U, hipStream_t st);
+int pf_wino_weights(const float* wpk, int Cout, int Cin, float* U, hipStream_t st);  // F(2x2)
+// U for the variant pf_wino_conv picks at (h, w): F(4x4) if h, w % 4 == 0
+int pf_wino_weights_hw(const float* wpk, int Cout, int Cin, int h, int w, float* U,
+                       hipStream_t st);
 int pf_wino_conv(const float* x, int xcs, int n, int h, int w, int Cin, const float* U,
                  const float* bias, int Cout, int act, float* y, int ycs, void* ws, size_t ws_bytes,
                  hipStream_t st);

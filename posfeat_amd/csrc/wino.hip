@@ -1,4 +1,4 @@
-// wino.hip -- Winograd F(2x2, 3x3) for the decoder's 3x3 stride-1 convs
+// wino.hip -- Winograd F(4x4, 3x3) / F(2x2, 3x3) for the decoder's 3x3 stride-1 convs
 // (upconv3/iconv3/upconv2/iconv2, DescNet.py:41-45: 4 x 45.3 GFLOP per
 // 480x640 image, 43 % of the extraction's conv work).
 //
@@ -8,8 +8,10 @@
 //                        conv_glds_kernel (blockIdx.y = xi)   ([16][T][Cout])
 //   Y = A^T M A (+ bias, activation) into the NHWC output (channel slice)
 //
-// 16 instead of 36 MACs per tile and channel pair: the GEMM is 2.25x smaller
-// than the direct conv; the transforms are two HBM passes.  Transforms are
+// F(2x2): 16 instead of 36 MACs per 2x2 tile and channel pair (GEMM 2.25x
+// smaller than the direct conv); F(4x4) (used when h, w % 4 == 0): 36 instead
+// of 144 per 4x4 tile (4x smaller), 36 transform-domain GEMMs, and 2.25/4 of
+// F(2x2)'s transform traffic.  The transforms are two HBM passes.  Transforms are
 // exact-weight (+-1, 1/2) so the result differs from the direct conv by fp32
 // rounding only (tests/test_gpu_ops.py).
 #include "common.h"
@@ -155,30 +157,216 @@ __global__ void wino_output_kernel(const float* __restrict__ M, int n, int h, in
   }
 }
 
+// ---------------------------------------------------------------- F(4x4, 3x3)
+// 36 multiplies per 16 outputs (4x fewer MACs than direct; 1.78x fewer than
+// F(2x2)), transform matrices of Lavin & Gray (2016):
+constexpr float W4_BT[6][6] = {{4, 0, -5, 0, 1, 0},  {0, -4, -4, 1, 1, 0},
+                                  {0, 4, -4, -1, 1, 0}, {0, -2, -1, 2, 1, 0},
+                                  {0, 2, -1, -2, 1, 0}, {0, 4, 0, -5, 0, 1}};
+constexpr float W4_G[6][3] = {{0.25f, 0, 0},
+                                 {-1.f / 6, -1.f / 6, -1.f / 6},
+                                 {-1.f / 6, 1.f / 6, -1.f / 6},
+                                 {1.f / 24, 1.f / 12, 1.f / 6},
+                                 {1.f / 24, -1.f / 12, 1.f / 6},
+                                 {0, 0, 1}};
+constexpr float W4_AT[4][6] = {
+    {1, 1, 1, 1, 1, 0}, {0, 1, -1, 2, -2, 0}, {0, 1, 1, 4, 4, 0}, {0, 1, -1, 8, -8, 1}};
+
+__global__ void wino4_weights_kernel(const float* __restrict__ wpk, int Cout, int Cin, int kpad,
+                                     float* __restrict__ U) {
+  const long long n = (long long)Cout * Cin;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int co = (int)(i / Cin), ci = (int)(i - (long long)co * Cin);
+    const float* w = wpk + (long long)co * kpad + (ci >> 5) * 9 * 32 + (ci & 31);
+    float g[3][3];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) g[t / 3][t % 3] = w[t * 32];
+    float r[6][3];
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        r[a][c] = W4_G[a][0] * g[0][c] + W4_G[a][1] * g[1][c] + W4_G[a][2] * g[2][c];
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+#pragma unroll
+      for (int b = 0; b < 6; ++b)
+        U[((long long)(a * 6 + b) * Cout + co) * Cin + ci] =
+            r[a][0] * W4_G[b][0] + r[a][1] * W4_G[b][1] + r[a][2] * W4_G[b][2];
+  }
+}
+
+// V[xi][tile][c], 6x6 patch at rows 4ty-1.., cols 4tx-1..
+__global__ __launch_bounds__(256) void wino4_input_kernel(const float* __restrict__ x, int xcs,
+                                                          int n, int h, int w, int c4n,
+                                                          float* __restrict__ V) {
+  const int th = h / 4, tw = w / 4;
+  const long long T = (long long)n * th * tw;
+  const long long total = T * c4n;
+  const int C = c4n * 4;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int q = (int)(i % c4n);
+    const long long tile = i / c4n;
+    const int tx = (int)(tile % tw);
+    const long long r0 = tile / tw;
+    const int ty = (int)(r0 % th);
+    const int b = (int)(r0 / th);
+    f32x4 t[6][6];  // B^T d, built row by row of d
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+#pragma unroll
+      for (int c = 0; c < 6; ++c) t[a][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      const int yy = 4 * ty - 1 + r;
+      f32x4 d[6];
+#pragma unroll
+      for (int c = 0; c < 6; ++c) {
+        const int xx = 4 * tx - 1 + c;
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+        if ((unsigned)yy < (unsigned)h && (unsigned)xx < (unsigned)w)
+          v = *reinterpret_cast<const f32x4*>(x + (((long long)b * h + yy) * w + xx) * xcs + q * 4);
+        d[c] = v;
+      }
+#pragma unroll
+      for (int a = 0; a < 6; ++a)
+        if (W4_BT[a][r] != 0.f)
+#pragma unroll
+          for (int c = 0; c < 6; ++c) t[a][c] += W4_BT[a][r] * d[c];
+    }
+    float* vo = V + tile * C + q * 4;
+    const long long xs = T * C;
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+#pragma unroll
+      for (int bb = 0; bb < 6; ++bb) {
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < 6; ++c)
+          if (W4_BT[bb][c] != 0.f) v += W4_BT[bb][c] * t[a][c];
+        *reinterpret_cast<f32x4*>(vo + (a * 6 + bb) * xs) = v;
+      }
+  }
+}
+
+__global__ __launch_bounds__(256) void wino4_output_kernel(const float* __restrict__ M, int n,
+                                                           int h, int w, int c4n,
+                                                           const float* __restrict__ bias, int act,
+                                                           float* __restrict__ y, int ycs) {
+  const int th = h / 4, tw = w / 4;
+  const long long T = (long long)n * th * tw;
+  const long long total = T * c4n;
+  const int C = c4n * 4;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int q = (int)(i % c4n);
+    const long long tile = i / c4n;
+    const int tx = (int)(tile % tw);
+    const long long r0 = tile / tw;
+    const int ty = (int)(r0 % th);
+    const int b = (int)(r0 / th);
+    const float* mi = M + tile * C + q * 4;
+    const long long xs = T * C;
+    f32x4 s[4][6];  // A^T M
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int c = 0; c < 6; ++c) s[a][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      f32x4 m[6];
+#pragma unroll
+      for (int c = 0; c < 6; ++c) m[c] = *reinterpret_cast<const f32x4*>(mi + (r * 6 + c) * xs);
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+        if (W4_AT[a][r] != 0.f)
+#pragma unroll
+          for (int c = 0; c < 6; ++c) s[a][c] += W4_AT[a][r] * m[c];
+    }
+    f32x4 bv = {0.f, 0.f, 0.f, 0.f};
+    if (bias) bv = *reinterpret_cast<const f32x4*>(bias + q * 4);
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int bb = 0; bb < 4; ++bb) {
+        f32x4 o = bv;
+#pragma unroll
+        for (int c = 0; c < 6; ++c)
+          if (W4_AT[bb][c] != 0.f) o += W4_AT[bb][c] * s[a][c];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float v = o[j];
+          o[j] = act == POSFEAT_ACT_RELU ? fmaxf(v, 0.f) : act == POSFEAT_ACT_ELU ? pf_elu(v) : v;
+        }
+        *reinterpret_cast<f32x4*>(
+            y + (((long long)b * h + 4 * ty + a) * w + 4 * tx + bb) * ycs + q * 4) = o;
+      }
+  }
+}
+
+// F(4x4) when both dims are multiples of 4 (all decoder layers at 480x640)
+// unless POSFEAT_WINO=1 (F(2x2) only)
+bool use_f4(int h, int w) {
+  static const bool f2only = [] {
+    const char* e = getenv("POSFEAT_WINO");
+    return e && e[0] == '1';
+  }();
+  return !f2only && h % 4 == 0 && w % 4 == 0;
+}
+
 }  // namespace
 
+// workspace / weights sized for the larger of the two variants (F(2x2):
+// 16 x T2, F(4x4): 36 x T2 / 4), so callers need not know which runs
 size_t pf_wino_ws_bytes(int n, int h, int w, int Cin, int Cout) {
   const size_t T = (size_t)n * (h / 2) * (w / 2);
   return pf_align(16 * T * Cin * 4, 256) + pf_align(16 * T * Cout * 4, 256);
 }
 
-size_t pf_wino_weights_floats(int Cin, int Cout) { return (size_t)16 * Cin * Cout; }
+size_t pf_wino_weights_floats(int Cin, int Cout) { return (size_t)36 * Cin * Cout; }
 
-int pf_wino_weights(const float* wpk, int Cout, int Cin, float* U, hipStream_t st) {
+// U for the variant pf_wino_conv will pick at (h, w); h = w = 0: F(2x2)
+int pf_wino_weights_hw(const float* wpk, int Cout, int Cin, int h, int w, float* U,
+                       hipStream_t st) {
   if (Cin % 32 || Cout % 4) return POSFEAT_E_INVALID;
   const int kpad = posfeat_conv_packed_k(Cin, 3, 3);
-  hipLaunchKernelGGL(wino_weights_kernel, dim3(grid_for((long long)Cout * Cin, 256)), dim3(256), 0,
-                     st, wpk, Cout, Cin, kpad, U);
+  if (h > 0 && use_f4(h, w))
+    hipLaunchKernelGGL(wino4_weights_kernel, dim3(grid_for((long long)Cout * Cin, 256)), dim3(256),
+                       0, st, wpk, Cout, Cin, kpad, U);
+  else
+    hipLaunchKernelGGL(wino_weights_kernel, dim3(grid_for((long long)Cout * Cin, 256)), dim3(256),
+                       0, st, wpk, Cout, Cin, kpad, U);
   PF_CHECK_LAUNCH();
   return POSFEAT_OK;
 }
 
-int pf_wino_conv(const float* x, int xcs, int n, int h, int w, int Cin, const float* U,
-                 const float* bias, int Cout, int act, float* y, int ycs, void* ws, size_t ws_bytes,
-                 hipStream_t st) {
+int pf_wino_weights(const float* wpk, int Cout, int Cin, float* U, hipStream_t st) {
+  return pf_wino_weights_hw(wpk, Cout, Cin, 0, 0, U, st);
+}
+
+static int wino_conv_impl(const float* x, int xcs, int n, int h, int w, int Cin, const float* U,
+                          bool U_is_f4, const float* bias, int Cout, int act, float* y, int ycs,
+                          void* ws, size_t ws_bytes, hipStream_t st) {
   if ((h & 1) || (w & 1) || Cin % 32 || Cout % 4 || xcs % 4 || ycs % 4 || n <= 0)
     return POSFEAT_E_INVALID;
   if (ws_bytes < pf_wino_ws_bytes(n, h, w, Cin, Cout)) return POSFEAT_E_WORKSPACE;
+  if (use_f4(h, w) && U_is_f4) {
+    const long long T4 = (long long)n * (h / 4) * (w / 4);
+    float* V4 = static_cast<float*>(ws);
+    float* M4 =
+        reinterpret_cast<float*>(static_cast<char*>(ws) + pf_align(36 * T4 * Cin * 4, 256));
+    hipLaunchKernelGGL(wino4_input_kernel, dim3(grid_for(T4 * (Cin / 4), 256)), dim3(256), 0, st,
+                       x, xcs, n, h, w, Cin / 4, V4);
+    PF_CHECK_LAUNCH();
+    PF_TRY(pf_gemm_batched(V4, Cin, T4 * Cin, U, (long long)Cout * Cin, M4, Cout, T4 * Cout, 36,
+                           (int)T4, Cout, Cin, st));
+    hipLaunchKernelGGL(wino4_output_kernel, dim3(grid_for(T4 * (Cout / 4), 256)), dim3(256), 0,
+                       st, M4, n, h, w, Cout / 4, bias, act, y, ycs);
+    PF_CHECK_LAUNCH();
+    return POSFEAT_OK;
+  }
   const long long T = (long long)n * (h / 2) * (w / 2);
   float* V = static_cast<float*>(ws);
   float* M = reinterpret_cast<float*>(static_cast<char*>(ws) + pf_align(16 * T * Cin * 4, 256));
@@ -193,15 +381,22 @@ int pf_wino_conv(const float* x, int xcs, int n, int h, int w, int Cin, const fl
   return POSFEAT_OK;
 }
 
+// U from pf_wino_weights_hw(.., h, w, ..): the variant is chosen from (h, w)
+int pf_wino_conv(const float* x, int xcs, int n, int h, int w, int Cin, const float* U,
+                 const float* bias, int Cout, int act, float* y, int ycs, void* ws, size_t ws_bytes,
+                 hipStream_t st) {
+  return wino_conv_impl(x, xcs, n, h, w, Cin, U, true, bias, Cout, act, y, ycs, ws, ws_bytes, st);
+}
+
 extern "C" size_t posfeat_wino_workspace(int n, int h, int w, int cin, int cout) {
   if (n <= 0 || h <= 0 || w <= 0 || (h & 1) || (w & 1)) return 0;
   return pf_wino_ws_bytes(n, h, w, cin, cout);
 }
 
-extern "C" int posfeat_wino_weights(const float* w_packed, int cout, int cin, float* U,
-                                    void* stream) {
+extern "C" int posfeat_wino_weights(const float* w_packed, int cout, int cin, int h, int w,
+                                    float* U, void* stream) {
   if (!w_packed || !U) return POSFEAT_E_INVALID;
-  return pf_wino_weights(w_packed, cout, cin, U, pf_stream(stream));
+  return pf_wino_weights_hw(w_packed, cout, cin, h, w, U, pf_stream(stream));
 }
 
 extern "C" int posfeat_conv3x3_wino(const float* x, int x_cstride, int n, int h, int w, int cin,

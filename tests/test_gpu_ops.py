@@ -78,7 +78,8 @@ def test_conv_vs_torch(gpu, case):
 
 WINO_CASES = [
     # n, h, w, cin, cout, act, in_extra, out_extra
-    (2, 16, 24, 64, 64, "none", 0, 0),
+    (2, 16, 24, 64, 64, "none", 0, 0),       # F(4x4)
+    (2, 18, 22, 64, 64, "elu", 0, 0),        # F(2x2) (not multiples of 4)
     (1, 30, 40, 1024, 512, "elu", 0, 512),   # upconv3 shape into a concat slice
     (2, 14, 10, 512, 256, "elu", 64, 0),     # ragged tile grid, strided input
     (1, 60, 80, 512, 256, "relu", 0, 256),
@@ -87,9 +88,10 @@ WINO_CASES = [
 
 @pytest.mark.parametrize("case", WINO_CASES)
 def test_conv3x3_wino_vs_torch(gpu, case):
-    """Winograd F(2x2,3x3) path (wino.hip) against the fp64 conv: the transforms
-    use exact +-1, 1/2 weights, so the error bound is the direct conv's times a
-    small factor (transform-domain sums grow the rounding by ~4x)."""
+    """Winograd path (wino.hip: F(4x4,3x3) when h, w % 4 == 0, else F(2x2,3x3))
+    against the fp64 conv.  Transform-domain sums grow the fp32 rounding
+    (F(4x4)'s coefficients reach 8 and 1/24), so the bound is a multiple of the
+    direct conv's."""
     from posfeat_amd import ops
     from posfeat_amd._lib import check, lib, ptr, stream_ptr
     n, h, w, cin, cout, act, in_extra, out_extra = case
@@ -103,8 +105,8 @@ def test_conv3x3_wino_vs_torch(gpu, case):
     xd[..., :cin] = x.permute(0, 2, 3, 1)
     xd = xd.to(gpu)
     wp, bp = ops.pack_conv_weight(wt.to(gpu), b.to(gpu))
-    U = torch.empty(16 * cout * cin, device=gpu)
-    check(lib().posfeat_wino_weights(ptr(wp), cout, cin, ptr(U), stream_ptr()))
+    U = torch.empty(36 * cout * cin, device=gpu)
+    check(lib().posfeat_wino_weights(ptr(wp), cout, cin, h, w, ptr(U), stream_ptr()))
     need = lib().posfeat_wino_workspace(n, h, w, cin, cout)
     ws = torch.empty(need, dtype=torch.uint8, device=gpu)
     out = torch.full((n, h, w, cout + out_extra), 7.0, device=gpu)
@@ -114,7 +116,7 @@ def test_conv3x3_wino_vs_torch(gpu, case):
     torch.cuda.synchronize()
     got = out[..., :cout].permute(0, 3, 1, 2).double().cpu()
     err = (got - ref).abs()
-    tol = 8e-6 * bound + 1e-6
+    tol = 3e-5 * bound + 1e-6
     assert torch.all(err <= tol), "max err %g (ratio %g)" % (err.max(), (err / tol).max())
     if out_extra:
         assert torch.all(out[..., cout:] == 7.0).item(), "wrote outside its channel slice"
