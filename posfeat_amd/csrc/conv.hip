@@ -1644,7 +1644,10 @@ int pf_gemm_batched(const float* A, int lda, long long sa, const float* B, long 
   d.act = POSFEAT_ACT_NONE;
   ConvArgs a;
   PF_TRY(conv_prepare(&d, A, B, nullptr, nullptr, C, a));
-  const Plan p = conv_plan(a, false);
+  // the heuristic sizes tiles for ONE GEMM; with nb of them in the grid the
+  // 128x128 tile (2x the operand reuse of 64x64) still fills the chip
+  const long long t128 = (long long)((M + 127) / 128) * ((N + 127) / 128) * nb;
+  const Plan p = conv_plan(a, false, (N % 128 == 0 && t128 >= 1024) ? TILE_128x128 : -1);
   if (p.kern != KERN_GLDS) return POSFEAT_E_UNSUPPORTED;
   a.nbatch = nb;
   a.bx = sa;

@@ -275,8 +275,10 @@ int conv3x3(Ctx& c, const std::string& name, const float* x, int n, int h, int w
   float* U = c.f(m->wino_u) + uo;
   PF_TRY(timed(c, "wino:weights", 0,
                [&] { return pf_wino_weights_hw(c.W(name), s->cout, s->cin, h, w, U, c.st); }));
-  const double T = (double)n * (h / 2) * (w / 2);
-  return timed(c, "conv:" + name + ".wino", 2.0 * T * 16 * s->cin * s->cout, [&] {
+  // executed transform-domain MACs: F(4x4) 36 per 4x4 tile, F(2x2) 16 per 2x2 tile
+  const bool f4 = h % 4 == 0 && w % 4 == 0 && !(getenv("POSFEAT_WINO") && getenv("POSFEAT_WINO")[0] == '1');
+  const double T = f4 ? (double)n * (h / 4) * (w / 4) : (double)n * (h / 2) * (w / 2);
+  return timed(c, "conv:" + name + ".wino", 2.0 * T * (f4 ? 36 : 16) * s->cin * s->cout, [&] {
     return pf_wino_conv(x, xcs, n, h, w, s->cin, U, c.Bi(name), s->cout, act, y, ycs,
                         c.f(m->wino_ws), m->wino_ws.floats * sizeof(float), c.st);
   });
@@ -383,7 +385,7 @@ void plan(posfeat_model* m) {
   }
   if (m->up4 && m->gfuse) {
     alloc(m->gf_w, B * 128 * 128);
-    alloc(m->gf_b, B * 128);
+    alloc(m->gf_b, B * 128 + 9 * 64 * 128);  // + the transposed W2 G slice (gfuse.hip)
   }
   if (m->wino) {
     size_t uf = 0, wb = 0;

@@ -23,6 +23,15 @@ namespace {
 constexpr int GF_COUT = 128, GF_CG = 64, GF_CL = 192;  // conv2 out, G channels, L channels
 constexpr int GF_KPAD = 128;                            // 5*5*4 = 100 -> 128
 
+// W2's G slice transposed for the ring kernel: w2t[t][k][co]
+__global__ __launch_bounds__(128) void gfuse_w2t_kernel(const float* __restrict__ w2, int k2pad,
+                                                        float* __restrict__ w2t) {
+  const int t = blockIdx.x / GF_CG, k = blockIdx.x % GF_CG, co = threadIdx.x;
+  const int ci = GF_CL + k;
+  w2t[((size_t)t * GF_CG + k) * GF_COUT + co] =
+      w2[(size_t)co * k2pad + ((ci >> 5) * 9 + t) * 32 + (ci & 31)];
+}
+
 // Wc[b][co][(u*5+v)*4 + ci] (ci < 3; zero-padded to 128), bc[b][co]
 __global__ __launch_bounds__(128) void gfuse_weights_kernel(
     const float* __restrict__ w2, int k2pad, const float* __restrict__ b2,
@@ -67,56 +76,73 @@ __global__ __launch_bounds__(128) void gfuse_weights_kernel(
 }
 
 // Border ring: y[p] = b2 + sum_t sum_k W2[:, 192+k, t] G[p+t-1][k], G = rstd (c - mean)
-// inside the image, 0 outside (conv2's zero padding).  One workgroup = one
-// ring pixel x 128 couts.
+// inside the image, 0 outside (conv2's zero padding).  One workgroup = RP ring
+// pixels x 128 couts; the G taps go through LDS, W2 (transposed, w2t[t][k][co])
+// is read coalesced across couts and reused for the RP pixels.
+constexpr int GF_RP = 8;
 __global__ __launch_bounds__(GF_COUT) void gfuse_ring_kernel(
     const float* __restrict__ c, int ccs, int H, int W, const float* __restrict__ mean,
-    const float* __restrict__ rstd, const float* __restrict__ w2, int k2pad,
-    const float* __restrict__ b2, float* __restrict__ y, int ycs) {
+    const float* __restrict__ rstd, const float* __restrict__ w2t, const float* __restrict__ b2,
+    float* __restrict__ y, int ycs) {
   const int b = blockIdx.y, co = threadIdx.x;
   const int nring = 2 * W + 2 * (H - 2);
-  int r = blockIdx.x, py, px;
-  if (r < W) {
-    py = 0;
-    px = r;
-  } else if ((r -= W) < W) {
-    py = H - 1;
-    px = r;
-  } else if ((r -= W) < H - 2) {
-    py = 1 + r;
-    px = 0;
-  } else {
-    py = 1 + (r - (H - 2));
-    px = W - 1;
-  }
-  (void)nring;
-  __shared__ float g[9][GF_CG];
-  const float* mb = mean + (size_t)b * GF_CG;
-  const float* rb = rstd + (size_t)b * GF_CG;
-  for (int i = threadIdx.x; i < 9 * GF_CG; i += blockDim.x) {
-    const int t = i / GF_CG, k = i - t * GF_CG;
-    const int qy = py + t / 3 - 1, qx = px + t % 3 - 1;
-    float v = 0.f;
-    if ((unsigned)qy < (unsigned)H && (unsigned)qx < (unsigned)W)
-      v = (c[(((size_t)b * H + qy) * W + qx) * ccs + k] - mb[k]) * rb[k];
-    g[t][k] = v;
+  __shared__ float g[GF_RP][9][GF_CG];
+  __shared__ int pys[GF_RP], pxs[GF_RP];
+  if (threadIdx.x < GF_RP) {
+    int r = blockIdx.x * GF_RP + threadIdx.x, py = -1, px = -1;
+    if (r < nring) {
+      if (r < W) {
+        py = 0;
+        px = r;
+      } else if ((r -= W) < W) {
+        py = H - 1;
+        px = r;
+      } else if ((r -= W) < H - 2) {
+        py = 1 + r;
+        px = 0;
+      } else {
+        py = 1 + (r - (H - 2));
+        px = W - 1;
+      }
+    }
+    pys[threadIdx.x] = py;
+    pxs[threadIdx.x] = px;
   }
   __syncthreads();
-  const float* w2r = w2 + (size_t)co * k2pad;
-  float acc = b2[co];
-  for (int t = 0; t < 9; ++t)
-    for (int k = 0; k < GF_CG; ++k) {
-      const int ci = GF_CL + k;
-      acc += w2r[((ci >> 5) * 9 + t) * 32 + (ci & 31)] * g[t][k];
-    }
-  y[(((size_t)b * H + py) * W + px) * ycs + co] = acc;
+  const float* mb = mean + (size_t)b * GF_CG;
+  const float* rb = rstd + (size_t)b * GF_CG;
+  for (int i = threadIdx.x; i < GF_RP * 9 * GF_CG; i += blockDim.x) {
+    const int j = i / (9 * GF_CG), rem = i - j * 9 * GF_CG, t = rem / GF_CG, k = rem - t * GF_CG;
+    const int py = pys[j], px = pxs[j];
+    const int qy = py + t / 3 - 1, qx = px + t % 3 - 1;
+    float v = 0.f;
+    if (py >= 0 && (unsigned)qy < (unsigned)H && (unsigned)qx < (unsigned)W)
+      v = (c[(((size_t)b * H + qy) * W + qx) * ccs + k] - mb[k]) * rb[k];
+    g[j][t][k] = v;
+  }
+  __syncthreads();
+  float acc[GF_RP];
+#pragma unroll
+  for (int j = 0; j < GF_RP; ++j) acc[j] = b2[co];
+  for (int tk = 0; tk < 9 * GF_CG; ++tk) {
+    const float wv = w2t[(size_t)tk * GF_COUT + co];
+#pragma unroll
+    for (int j = 0; j < GF_RP; ++j) acc[j] += wv * (&g[j][0][0])[tk];
+  }
+#pragma unroll
+  for (int j = 0; j < GF_RP; ++j)
+    if (pys[j] >= 0) y[(((size_t)b * H + pys[j]) * W + pxs[j]) * ycs + co] = acc[j];
 }
 
 }  // namespace
 
-size_t pf_gfuse_weights_floats(int n) { return (size_t)n * GF_COUT * (GF_KPAD + 1); }
+// wc (n*128*128) | bc (n*128) | w2t (9*64*128)
+size_t pf_gfuse_weights_floats(int n) {
+  return (size_t)n * GF_COUT * (GF_KPAD + 1) + (size_t)9 * GF_CG * GF_COUT;
+}
 
-// wc: n * 128 * 128 floats (packed 5x5 weights over 4 channels), bc: n * 128
+// wc: n * 128 * 128 floats (packed 5x5 weights over 4 channels), bc: n * 128,
+// followed by the transposed W2 G slice the ring kernel reads
 int pf_gfuse_weights(const float* w2_packed, const float* b2, const float* w1_packed,
                      const float* b1, const float* mean, const float* rstd, int n, float* wc,
                      float* bc, hipStream_t st) {
@@ -124,6 +150,8 @@ int pf_gfuse_weights(const float* w2_packed, const float* b2, const float* w1_pa
   const int k1pad = posfeat_conv_packed_k(3, 3, 3);
   hipLaunchKernelGGL(gfuse_weights_kernel, dim3(GF_COUT, n), dim3(128), 0, st, w2_packed, k2pad,
                      b2, w1_packed, k1pad, b1, mean, rstd, wc, bc);
+  hipLaunchKernelGGL(gfuse_w2t_kernel, dim3(9 * GF_CG), dim3(GF_COUT), 0, st, w2_packed, k2pad,
+                     bc + (size_t)n * GF_COUT);
   PF_CHECK_LAUNCH();
   return POSFEAT_OK;
 }
@@ -151,9 +179,10 @@ int pf_gfuse_conv(const float* img4, const float* c, int ccs, int n, int H, int 
     PF_TRY(pf_conv_run_tile(&d, img4 + (size_t)b * H * W * 4, wc + (size_t)b * GF_COUT * GF_KPAD,
                             bc + (size_t)b * GF_COUT, nullptr, y + (size_t)b * H * W * ycs, nullptr,
                             0, -1, st));
-  const int k2pad = posfeat_conv_packed_k(GF_CL + GF_CG, 3, 3);
-  hipLaunchKernelGGL(gfuse_ring_kernel, dim3(2 * W + 2 * (H - 2), n), dim3(GF_COUT), 0, st, c, ccs,
-                     H, W, mean, rstd, w2_packed, k2pad, b2, y, ycs);
+  (void)w2_packed;
+  const int nring = 2 * W + 2 * (H - 2);
+  hipLaunchKernelGGL(gfuse_ring_kernel, dim3((nring + GF_RP - 1) / GF_RP, n), dim3(GF_COUT), 0, st,
+                     c, ccs, H, W, mean, rstd, bc + (size_t)n * GF_COUT, b2, y, ycs);
   PF_CHECK_LAUNCH();
   return POSFEAT_OK;
 }
