@@ -252,7 +252,8 @@ int forward(Ctx& c, const float* img, posfeat_extract_out* out);
 
 // The decoder's 3x3 stride-1 convs (DescNet.py:41-45) through Winograd
 // F(2x2,3x3) when enabled (default; POSFEAT_WINO=0 for the direct conv)
-const char* const kWinoLayers[4] = {"upconv3.conv", "iconv3", "upconv2.conv", "iconv2"};
+const char* const kWinoLayers[5] = {"upconv3.conv", "iconv3", "upconv2.conv", "iconv2",
+                                    "head.conv1"};
 
 long long wino_u_offset(const std::string& name) {
   long long off = 0;
@@ -389,9 +390,9 @@ void plan(posfeat_model* m) {
   }
   if (m->wino) {
     size_t uf = 0, wb = 0;
-    const int dims[4][2] = {{(int)h8, (int)w8}, {(int)h8, (int)w8}, {(int)h4, (int)w4},
-                            {(int)h4, (int)w4}};
-    for (int i = 0; i < 4; ++i) {
+    const int dims[5][2] = {{(int)h8, (int)w8}, {(int)h8, (int)w8}, {(int)h4, (int)w4},
+                            {(int)h4, (int)w4}, {(int)h4, (int)w4}};
+    for (int i = 0; i < 5; ++i) {
       const Spec* s = specs().find(kWinoLayers[i]);
       uf += (size_t)36 * s->cout * s->cin;
       wb = std::max(wb, pf_wino_ws_bytes((int)B, dims[i][0], dims[i][1], s->cin, s->cout));
@@ -536,7 +537,15 @@ int forward(Ctx& c, const float* img, posfeat_extract_out* out) {
   double* part = c.d(m->st_part);
   float* c1 = c.f(m->c1raw);
   float* c2 = c.f(m->c2raw);
-  PF_TRY(conv_in(c, "head.conv1", headcat, B, h4, w4, 192, c1, 192, mean1, rstd1));
+  if (m->wino && h4 % 2 == 0 && w4 % 2 == 0) {
+    // Winograd conv (bias, no act) + a separate statistics pass
+    PF_TRY(conv3x3(c, "head.conv1", headcat, B, h4, w4, 192, c1, 192, POSFEAT_ACT_NONE));
+    PF_TRY(timed(c, "instnorm", 0, [&] {
+      return pf_in_stats(c1, B, h4 * w4, 192, 192, mean1, rstd1, c.d(m->st_part), c.st);
+    }));
+  } else {
+    PF_TRY(conv_in(c, "head.conv1", headcat, B, h4, w4, 192, c1, 192, mean1, rstd1));
+  }
   if (m->up4) {
     // L = PReLU(IN(conv1)) stays at 1/4 resolution; conv2 reads it per phase
     PF_TRY(timed(c, "norm_prelu", 0, [&] {

@@ -11,6 +11,8 @@
 //
 // All are HBM/L2-bound; feature maps are NHWC with a pixel stride so a
 // producer can write straight into a channel slice of a concat buffer.
+#include <algorithm>
+
 #include "common.h"
 #include "fmap.h"
 
@@ -154,18 +156,37 @@ __global__ void in_partial_kernel(const float* __restrict__ x, int hw, int C, in
   }
 }
 
-__global__ void in_finalize_kernel(const float* __restrict__ x, int hw, int C, int cs,
-                                   int nchunk, const double* __restrict__ part, float eps,
-                                   float* __restrict__ mean, float* __restrict__ rstd, int nb) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nb * C) return;
-  const int b = i / C, c = i - b * C;
+// Chunk partials -> mean / rstd: block = (4 channels x 64 chunk lanes, image);
+// fixed-order strided sums + LDS tree (deterministic, no serial per-channel
+// chain of nchunk dependent loads)
+__global__ __launch_bounds__(256) void in_finalize_kernel(
+    const float* __restrict__ x, int hw, int C, int cs, int nchunk,
+    const double* __restrict__ part, float eps, float* __restrict__ mean,
+    float* __restrict__ rstd, int nb) {
+  __shared__ double red[2][64][4];
+  const int cl = threadIdx.x & 3, kl = threadIdx.x >> 2;
+  const int b = blockIdx.y, c = blockIdx.x * 4 + cl;
   double s1 = 0, s2 = 0;
   const double* p = part + (long long)b * nchunk * C * 2;
-  for (int k = 0; k < nchunk; ++k) {
-    s1 += p[(k * C + c) * 2];
-    s2 += p[(k * C + c) * 2 + 1];
+  if (c < C)
+    for (int k = kl; k < nchunk; k += 64) {
+      s1 += p[((long long)k * C + c) * 2];
+      s2 += p[((long long)k * C + c) * 2 + 1];
+    }
+  red[0][kl][cl] = s1;
+  red[1][kl][cl] = s2;
+  __syncthreads();
+  for (int o = 32; o > 0; o >>= 1) {
+    if (kl < o) {
+      red[0][kl][cl] += red[0][kl + o][cl];
+      red[1][kl][cl] += red[1][kl + o][cl];
+    }
+    __syncthreads();
   }
+  if (kl != 0 || c >= C) return;
+  s1 = red[0][0][cl];
+  s2 = red[1][0][cl];
+  const int i = b * C + c;
   const double sh = x[(long long)b * hw * cs + c];
   const double m1 = s1 / hw;
   double var = s2 / hw - m1 * m1;
@@ -394,15 +415,22 @@ int pf_upsample2x_ac(const float* x, int n, int h, int w, int c, int csi, float*
   return POSFEAT_OK;
 }
 
+// pixels per partial-sum block: ~512 blocks over the batch, >= 64 pixels each
+static int in_chunk(int n, int hw) {
+  const int want = std::max(1, (512 + n - 1) / n);
+  const int chunk = std::max(64, (hw + want - 1) / want);
+  return chunk;
+}
+
 size_t pf_in_stats_ws_bytes(int n, int hw, int C) {
-  const int chunk = 2048;
+  const int chunk = in_chunk(n, hw);
   const int nchunk = (hw + chunk - 1) / chunk;
   return (size_t)n * nchunk * (C < 1 ? 1 : C) * 2 * sizeof(double);
 }
 
 int pf_in_stats(const float* x, int n, int hw, int C, int cs, float* mean, float* rstd,
                 double* part, hipStream_t st) {
-  const int chunk = 2048;
+  const int chunk = in_chunk(n, hw);
   const int nchunk = (hw + chunk - 1) / chunk;
   if (C == 1 && cs == 1) {
     hipLaunchKernelGGL(in1_partial_kernel, dim3(nchunk, n), dim3(256), 0, st, x, hw, chunk, part);
@@ -413,8 +441,8 @@ int pf_in_stats(const float* x, int n, int hw, int C, int cs, float* mean, float
                        threads * 8 * sizeof(double), st, x, hw, C, cs, chunk, part);
   }
   PF_CHECK_LAUNCH();
-  hipLaunchKernelGGL(in_finalize_kernel, dim3((n * C + 255) / 256), dim3(256), 0, st, x, hw, C,
-                     cs, nchunk, part, 1e-5f, mean, rstd, n);
+  hipLaunchKernelGGL(in_finalize_kernel, dim3((C + 3) / 4, n), dim3(256), 0, st, x, hw, C, cs,
+                     nchunk, part, 1e-5f, mean, rstd, n);
   PF_CHECK_LAUNCH();
   return POSFEAT_OK;
 }
