@@ -269,6 +269,18 @@ int posfeat_conv3x3_wino(const float *x, int x_cstride, int n, int h, int w, int
                          const float *U, const float *bias, int cout, int act, float *y,
                          int y_cstride, void *ws, size_t ws_bytes, void *stream);
 
+/* Weight gradient of the same decoder convs by F(4x4,3x3) (the autograd
+ * conv2d weight/bias backward behind managers/trainer.py:331 for
+ * networks/DescNet.py:41-45): dM = A dY A^T per 4x4 output tile, the 36
+ * transform-domain GEMMs dU_xi = sum_tiles dM_xi (x) V_xi (one launch, split
+ * over tiles), dw = G^T dU G written in the packed K order of
+ * posfeat_conv2d_nhwc; db (may be NULL) = sum of dy.  h, w % 4 == 0;
+ * cin, cout % 128 == 0.  Deterministic. */
+size_t posfeat_wino_wgrad_workspace(int n, int h, int w, int cin, int cout);
+int posfeat_conv3x3_wino_wgrad(const float *dy, int dy_cstride, const float *x, int x_cstride,
+                               int n, int h, int w, int cin, int cout, float *dw, float *db,
+                               void *ws, size_t ws_bytes, void *stream);
+
 /* torch.optim.SGD step without momentum/weight decay (train_kp.yaml:11-13,
  * managers/trainer.py:118-119, 356): w -= lr * g over n floats. */
 int posfeat_sgd(float *w, const float *g, long long n, float lr, void *stream);

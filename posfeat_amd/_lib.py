@@ -102,6 +102,9 @@ SIGNATURES = {
     "posfeat_conv3x3_wino": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
                                      c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_size_t,
                                      c_void_p]),
+    "posfeat_wino_wgrad_workspace": (c_size_t, [c_int] * 5),
+    "posfeat_conv3x3_wino_wgrad": (c_int, [c_void_p, c_int, c_void_p, c_int] + [c_int] * 5 +
+                                   [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "posfeat_bbtrain_num_layers": (c_int, []),
     "posfeat_bbtrain_layer": (c_int, [c_int, ctypes.POINTER(ctypes.c_char_p), P_int, P_int, P_int,
                                       P_int, P_int, ctypes.POINTER(c_ll)]),

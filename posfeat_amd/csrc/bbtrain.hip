@@ -385,11 +385,22 @@ void plan(posfeat_bbtrain* m) {
       uf = std::max(uf, (size_t)36 * L.cin * L.cout);
       wb = std::max(wb, pf_wino_ws_bytes((int)B, lih[li], liw[li], L.cin, L.cout));
       wb = std::max(wb, pf_wino_ws_bytes((int)B, lih[li], liw[li], L.cout, L.cin));
+      if (lih[li] % 4 == 0 && liw[li] % 4 == 0)
+        wb = std::max(wb, pf_wino_wgrad_ws_bytes((int)B, lih[li], liw[li], L.cin, L.cout));
     }
     alloc(m->wu, fl(uf));
     alloc(m->wino_ws, wb);
   }
   m->scr_bytes = cur;
+}
+
+// executed transform-domain MACs x2 of a Winograd layer: F(4x4) 36 per 4x4
+// tile, F(2x2) 16 per 2x2 tile (what the MFMA units run, for the rooflines)
+double wino_flops(int n, int h, int w, int cin, int cout, bool wgrad = false) {
+  const char* e = getenv("POSFEAT_WINO");
+  const bool f4 = h % 4 == 0 && w % 4 == 0 && (wgrad || !(e && e[0] == '1'));
+  const double T = f4 ? (double)n * (h / 4) * (w / 4) : (double)n * (h / 2) * (w / 2);
+  return 2.0 * T * (f4 ? 36 : 16) * cin * cout;
 }
 
 // ------------------------------------------------------------------ layer passes
@@ -405,7 +416,7 @@ int layer_fwd(Ctx& c, int li, const float* x, int xcs, int h, int w, float* out,
   posfeat_conv_desc d = make_desc(m->B, h, w, L.cin, xcs, L.cout, L.k, L.stride, L.cout, 0);
   if (use_wino(m, li, h, w)) {
     float* U = c.s(m->wu);
-    PF_TRY(timed(c, "fwd:conv", 2.0 * P * L.cout * L.cin * L.k * L.k, [&] {
+    PF_TRY(timed(c, "fwd:conv", wino_flops(m->B, h, w, L.cin, L.cout), [&] {
       PF_TRY(pf_wino_weights_hw(c.prm + L.w_off, L.cout, L.cin, h, w, U, c.st));
       return pf_wino_conv(x, xcs, m->B, h, w, L.cin, U, c.prm + L.b_off, L.cout, ACT_NONE, y,
                           L.cout, c.s(m->wino_ws), m->wino_ws.bytes, c.st);
@@ -480,10 +491,19 @@ int layer_bwd(Ctx& c, int li, const float* x, int xcs, int h, int w, const float
   }));
   const double flops = 2.0 * P * C * L.cin * L.k * L.k;
   const int cinp = (L.cin + 3) / 4 * 4;
-  PF_TRY(timed(c, "bwd:wgrad", flops, [&] {
-    return pf_conv_wgrad(dy, C, x, xcs, B, h, w, cinp, C, L.k, L.k, L.stride, grad + L.w_off,
-                         L.bias ? grad + L.b_off : nullptr, acc, c.s(m->wgws), m->wgws.bytes, c.st);
-  }));
+  if (use_wino(m, li, h, w) && h % 4 == 0 && w % 4 == 0 && L.cin % 128 == 0 && C % 128 == 0) {
+    PF_TRY(timed(c, "bwd:wgrad", wino_flops(B, h, w, L.cin, C, true), [&] {
+      return pf_wino_wgrad(dy, C, x, xcs, B, h, w, L.cin, C, grad + L.w_off,
+                           L.bias ? grad + L.b_off : nullptr, acc, c.s(m->wino_ws),
+                           m->wino_ws.bytes, c.st);
+    }));
+  } else {
+    PF_TRY(timed(c, "bwd:wgrad", flops, [&] {
+      return pf_conv_wgrad(dy, C, x, xcs, B, h, w, cinp, C, L.k, L.k, L.stride, grad + L.w_off,
+                           L.bias ? grad + L.b_off : nullptr, acc, c.s(m->wgws), m->wgws.bytes,
+                           c.st);
+    }));
+  }
   if (!dx) return POSFEAT_OK;
   float* wt = c.s(m->wt);
   const float* src = dy;
@@ -501,7 +521,7 @@ int layer_bwd(Ctx& c, int li, const float* x, int xcs, int h, int w, const float
   }));
   if (!add && use_wino(m, li, h, w)) {
     float* U = c.s(m->wu);
-    return timed(c, "bwd:dgrad", flops, [&] {
+    return timed(c, "bwd:dgrad", wino_flops(B, h, w, C, L.cin), [&] {
       PF_TRY(pf_wino_weights_hw(wt, L.cin, C, h, w, U, c.st));
       return pf_wino_conv(src, C, B, h, w, C, U, nullptr, L.cin, ACT_NONE, dx, dxcs,
                           c.s(m->wino_ws), m->wino_ws.bytes, c.st);

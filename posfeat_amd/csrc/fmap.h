@@ -64,3 +64,7 @@ int pf_gfuse_weights(const float* w2_packed, const float* b2, const float* w1_pa
 int pf_gfuse_conv(const float* img4, const float* c, int ccs, int n, int H, int W,
                   const float* wc, const float* bc, const float* mean, const float* rstd,
                   const float* w2_packed, const float* b2, float* y, int ycs, hipStream_t st);
+size_t pf_wino_wgrad_ws_bytes(int n, int h, int w, int Cin, int Cout);
+int pf_wino_wgrad(const float* dy, int ldy, const float* x, int xcs, int n, int h, int w, int Cin,
+                  int Cout, float* dw, float* db, int acc, void* ws, size_t ws_bytes,
+                  hipStream_t st);

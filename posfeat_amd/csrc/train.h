@@ -34,3 +34,7 @@ int pf_tail_backward(const float* dlp, const float* y3, const float* m3, const f
                      int dcs, float* dw3, void* ws, double** t2s, int* t2n, hipStream_t st);
 int pf_head_scalars(const double* t2s, int n2, const double* c1s, int n1, float* db3,
                     float* dslope, hipStream_t st);
+// batched 1x1 weight-gradient GEMMs without split-K (Winograd weight gradient)
+int pf_wgrad_gemm_batched(const float* dy, int ldy, long long sdy, const float* x, int xcs,
+                          long long sx, int M, int Cin, int Cout, int nb, int nsplit, float* part,
+                          float* partb, int zb, hipStream_t st);

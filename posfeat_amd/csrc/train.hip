@@ -41,6 +41,10 @@ struct WgradArgs {
   long long d_row, d_img;       // x offset corrections when a pixel walk wraps a row / image
   int Cout, Kpad, K, M;
   int tiles_n, ntiles, nsplit, nchunks;
+  // batched 1x1 use (Winograd weight gradient): blockIdx.y = z selects
+  // dy/x/part + z * stride; only batch zb writes the bias partial
+  long long bdy, bx, bpart;
+  int zb;
   float* part;   // [nsplit][Cout][Kpad]
   float* partb;  // [nsplit][Cout] or nullptr
 };
@@ -76,6 +80,13 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
   const int split = bid / a.ntiles, tile = bid - split * a.ntiles;
   const int tm = tile / a.tiles_n, tn = tile - tm * a.tiles_n;
   const int co0 = tm * BM, n0 = tn * BN;
+  if (gridDim.y > 1) {
+    const long long z = blockIdx.y;
+    a.dy += z * a.bdy;
+    a.x += z * a.bx;
+    a.part += z * a.bpart;
+    if ((int)z != a.zb) a.partb = nullptr;
+  }
   const int c_begin = (int)((long long)a.nchunks * split / a.nsplit);
   const int c_end = (int)((long long)a.nchunks * (split + 1) / a.nsplit);
 
@@ -878,6 +889,8 @@ int pf_conv_wgrad(const float* dy, int ldy, const float* x, int xcs, int n, int 
   a.ntiles = p.ntiles;
   a.nsplit = p.nsplit;
   a.nchunks = p.nchunks;
+  a.bdy = a.bx = a.bpart = 0;
+  a.zb = 0;
   a.part = static_cast<float*>(ws);
   a.partb = db ? reinterpret_cast<float*>(static_cast<char*>(ws) +
                                           pf_align((size_t)p.nsplit * Cout * p.Kpad * 4, 256))
@@ -902,6 +915,51 @@ int pf_conv_wgrad(const float* dy, int ldy, const float* x, int xcs, int n, int 
   const long long ne = (long long)Cout * p.Kpad;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, st,
                      a.part, a.partb, p.nsplit, Cout, p.Kpad, dw, db, acc);
+  PF_CHECK_LAUNCH();
+  return POSFEAT_OK;
+}
+
+// part[z][s] [Cout][Cin] = sum_{m in split s} dy[z][m][co] x[z][m][ci], z < nb,
+// in ONE launch (blockIdx.y = z): the Winograd weight gradient's 36
+// transform-domain GEMMs (wino.hip), whose output transform sums the nsplit
+// partials.  Cin, Cout % 128 == 0; partb (optional) [nsplit][Cout] receives
+// the split sums of dy[zb].
+int pf_wgrad_gemm_batched(const float* dy, int ldy, long long sdy, const float* x, int xcs,
+                          long long sx, int M, int Cin, int Cout, int nb, int nsplit, float* part,
+                          float* partb, int zb, hipStream_t st) {
+  if (Cin % 128 || Cout % 128 || ldy % 4 || xcs % 4 || nb < 1 || M < 1 || nsplit < 1)
+    return POSFEAT_E_INVALID;
+  WgradArgs a;
+  a.dy = dy;
+  a.ldy = ldy;
+  a.x = x;
+  a.xcs = xcs;
+  a.H = 1;
+  a.W = M;
+  a.Hin = 1;
+  a.Win = M;
+  a.stride = 1;
+  a.d_row = 0;
+  a.d_img = 0;
+  a.Cin = Cin;
+  a.KH = a.KW = 1;
+  a.pad = 0;
+  a.Cout = Cout;
+  a.Kpad = Cin;
+  a.K = Cin;
+  a.M = M;
+  a.tiles_n = Cin / 128;
+  a.ntiles = (Cout / 128) * a.tiles_n;
+  a.nsplit = nsplit;
+  a.nchunks = (M + WG_RB - 1) / WG_RB;
+  a.part = part;
+  a.partb = partb;
+  a.bdy = sdy;
+  a.bx = sx;
+  a.bpart = (long long)nsplit * Cout * Cin;
+  a.zb = zb;
+  hipLaunchKernelGGL((conv_wgrad_kernel<128, 128>), dim3(a.ntiles * nsplit, nb), dim3(256), 0, st,
+                     a);
   PF_CHECK_LAUNCH();
   return POSFEAT_OK;
 }

@@ -14,8 +14,11 @@
 // F(2x2)'s transform traffic.  The transforms are two HBM passes.  Transforms are
 // exact-weight (+-1, 1/2) so the result differs from the direct conv by fp32
 // rounding only (tests/test_gpu_ops.py).
+#include <algorithm>
+
 #include "common.h"
 #include "fmap.h"
+#include "train.h"
 
 namespace {
 
@@ -306,6 +309,110 @@ __global__ __launch_bounds__(256) void wino4_output_kernel(const float* __restri
   }
 }
 
+// ---------------------------------------------------------------- F(4x4) weight gradient
+// Y = A^T [U (.) V] A with U = G g G^T  =>  dM = A dY A^T (6x6 per 4x4 output
+// tile), dU_xi = sum_tiles dM_xi (x) V_xi (36 batched GEMMs over the tiles),
+// dg = G^T dU G.  The Winograd identity holds for the gradient exactly as for
+// the forward, so this is the same reduction in a 4x smaller MAC count.
+__global__ __launch_bounds__(256) void wino4_dy_kernel(const float* __restrict__ dy, int ldy, int n,
+                                                       int h, int w, int c4n,
+                                                       float* __restrict__ dM) {
+  const int th = h / 4, tw = w / 4;
+  const long long T = (long long)n * th * tw;
+  const long long total = T * c4n;
+  const int C = c4n * 4;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int q = (int)(i % c4n);
+    const long long tile = i / c4n;
+    const int tx = (int)(tile % tw);
+    const long long r0 = tile / tw;
+    const int ty = (int)(r0 % th);
+    const int b = (int)(r0 / th);
+    f32x4 t[6][4];  // A dY
+#pragma unroll
+    for (int r = 0; r < 6; ++r)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) t[r][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii) {
+      f32x4 g[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        g[j] = *reinterpret_cast<const f32x4*>(
+            dy + (((long long)b * h + 4 * ty + ii) * w + 4 * tx + j) * ldy + q * 4);
+#pragma unroll
+      for (int r = 0; r < 6; ++r)
+        if (W4_AT[ii][r] != 0.f)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) t[r][j] += W4_AT[ii][r] * g[j];
+    }
+    float* mo = dM + tile * C + q * 4;
+    const long long xs = T * C;
+#pragma unroll
+    for (int r = 0; r < 6; ++r)
+#pragma unroll
+      for (int c = 0; c < 6; ++c) {
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (W4_AT[j][c] != 0.f) v += W4_AT[j][c] * t[r][j];
+        *reinterpret_cast<f32x4*>(mo + (r * 6 + c) * xs) = v;
+      }
+  }
+}
+
+// dU = sum of the nsplit GEMM partials; dW[co][(ci/32, tap, ci%32)] (+)=
+// (G^T dU G)[tap]; db (+)= sum of the bias partials
+__global__ void wino4_wgrad_out_kernel(const float* __restrict__ part, int nsplit, int Cout,
+                                       int Cin, int kpad, float* __restrict__ dw,
+                                       const float* __restrict__ partb, float* __restrict__ db,
+                                       int acc) {
+  const long long n = (long long)Cout * Cin;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int co = (int)(i / Cin), ci = (int)(i - (long long)co * Cin);
+    float u[6][6];
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+#pragma unroll
+      for (int b = 0; b < 6; ++b) {
+        const float* pz = part + (long long)(a * 6 + b) * nsplit * n + i;
+        float v = 0.f;
+        for (int s = 0; s < nsplit; ++s) v += pz[s * n];
+        u[a][b] = v;
+      }
+    float sv[3][6];
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+      for (int b = 0; b < 6; ++b) {
+        float v = 0.f;
+#pragma unroll
+        for (int a = 0; a < 6; ++a)
+          if (W4_G[a][kh] != 0.f) v += W4_G[a][kh] * u[a][b];
+        sv[kh][b] = v;
+      }
+    float* out = dw + (long long)co * kpad + (ci >> 5) * 9 * 32 + (ci & 31);
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        float v = 0.f;
+#pragma unroll
+        for (int b = 0; b < 6; ++b)
+          if (W4_G[b][kw] != 0.f) v += sv[kh][b] * W4_G[b][kw];
+        float* o = out + (kh * 3 + kw) * 32;
+        *o = acc ? *o + v : v;
+      }
+    if (db && ci == 0) {
+      float v = 0.f;
+      for (int s = 0; s < nsplit; ++s) v += partb[s * Cout + co];
+      db[co] = acc ? db[co] + v : v;
+    }
+  }
+}
+
 // F(4x4) when both dims are multiples of 4 (all decoder layers at 480x640)
 // unless POSFEAT_WINO=1 (F(2x2) only)
 bool use_f4(int h, int w) {
@@ -386,6 +493,72 @@ int pf_wino_conv(const float* x, int xcs, int n, int h, int w, int Cin, const fl
                  const float* bias, int Cout, int act, float* y, int ycs, void* ws, size_t ws_bytes,
                  hipStream_t st) {
   return wino_conv_impl(x, xcs, n, h, w, Cin, U, true, bias, Cout, act, y, ycs, ws, ws_bytes, st);
+}
+
+namespace {
+// split the tile reduction so the 36 x (Cout/128) x (Cin/128) GEMM tiles reach >= 1024 workgroups
+int wino_wgrad_nsplit(long long T, int Cin, int Cout) {
+  const long long tiles = 36LL * (Cout / 128) * (Cin / 128);
+  long long s = (1024 + tiles - 1) / tiles;
+  const long long chunks = (T + 63) / 64;
+  s = std::min(s, std::max(1LL, chunks / 8));  // >= 8 row chunks per split
+  return (int)std::max(1LL, std::min(s, 16LL));
+}
+}  // namespace
+
+// V [36][T][Cin] | dM [36][T][Cout] | GEMM partials [36][nsplit][Cout][Cin] | bias partials
+size_t pf_wino_wgrad_ws_bytes(int n, int h, int w, int Cin, int Cout) {
+  const long long T = (long long)n * (h / 4) * (w / 4);
+  const int ns = wino_wgrad_nsplit(T, Cin, Cout);
+  return pf_align(36 * T * Cin * 4, 256) + pf_align(36 * T * Cout * 4, 256) +
+         pf_align((size_t)36 * ns * Cout * Cin * 4, 256) + pf_align((size_t)ns * Cout * 4, 256);
+}
+
+// Weight gradient of a 3x3 stride-1 pad-1 conv by F(4x4) (h, w % 4 == 0;
+// Cin, Cout % 128 == 0): dy compact [n][h][w][Cout] (pitch ldy), x the layer
+// input (pitch xcs); dw packed like the engine's weights, db optional; acc adds.
+int pf_wino_wgrad(const float* dy, int ldy, const float* x, int xcs, int n, int h, int w, int Cin,
+                  int Cout, float* dw, float* db, int acc, void* ws, size_t ws_bytes,
+                  hipStream_t st) {
+  if (h % 4 || w % 4 || Cin % 128 || Cout % 128 || ldy % 4 || xcs % 4) return POSFEAT_E_INVALID;
+  if (ws_bytes < pf_wino_wgrad_ws_bytes(n, h, w, Cin, Cout)) return POSFEAT_E_WORKSPACE;
+  const long long T = (long long)n * (h / 4) * (w / 4);
+  const int ns = wino_wgrad_nsplit(T, Cin, Cout);
+  char* p = static_cast<char*>(ws);
+  float* V = reinterpret_cast<float*>(p);
+  p += pf_align(36 * T * Cin * 4, 256);
+  float* dM = reinterpret_cast<float*>(p);
+  p += pf_align(36 * T * Cout * 4, 256);
+  float* part = reinterpret_cast<float*>(p);
+  p += pf_align((size_t)36 * ns * Cout * Cin * 4, 256);
+  float* partb = reinterpret_cast<float*>(p);
+  hipLaunchKernelGGL(wino4_input_kernel, dim3(grid_for(T * (Cin / 4), 256)), dim3(256), 0, st, x,
+                     xcs, n, h, w, Cin / 4, V);
+  hipLaunchKernelGGL(wino4_dy_kernel, dim3(grid_for(T * (Cout / 4), 256)), dim3(256), 0, st, dy,
+                     ldy, n, h, w, Cout / 4, dM);
+  PF_CHECK_LAUNCH();
+  // xi = (1, 1): A^T's column 1 is all ones, so sum_tiles dM_7 = sum_pixels dy (the bias)
+  PF_TRY(pf_wgrad_gemm_batched(dM, Cout, T * Cout, V, Cin, T * Cin, (int)T, Cin, Cout, 36, ns,
+                               part, db ? partb : nullptr, 7, st));
+  const int kpad = posfeat_conv_packed_k(Cin, 3, 3);
+  hipLaunchKernelGGL(wino4_wgrad_out_kernel, dim3(grid_for((long long)Cout * Cin, 256)), dim3(256),
+                     0, st, part, ns, Cout, Cin, kpad, dw, partb, db, acc);
+  PF_CHECK_LAUNCH();
+  return POSFEAT_OK;
+}
+
+extern "C" size_t posfeat_wino_wgrad_workspace(int n, int h, int w, int cin, int cout) {
+  if (n <= 0 || h <= 0 || w <= 0 || (h & 3) || (w & 3)) return 0;
+  return pf_wino_wgrad_ws_bytes(n, h, w, cin, cout);
+}
+
+extern "C" int posfeat_conv3x3_wino_wgrad(const float* dy, int dy_cstride, const float* x,
+                                          int x_cstride, int n, int h, int w, int cin, int cout,
+                                          float* dw, float* db, void* ws, size_t ws_bytes,
+                                          void* stream) {
+  if (!dy || !x || !dw || !ws || n <= 0) return POSFEAT_E_INVALID;
+  return pf_wino_wgrad(dy, dy_cstride, x, x_cstride, n, h, w, cin, cout, dw, db, 0, ws, ws_bytes,
+                       pf_stream(stream));
 }
 
 extern "C" size_t posfeat_wino_workspace(int n, int h, int w, int cin, int cout) {

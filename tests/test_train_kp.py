@@ -169,3 +169,40 @@ def test_gpu_wgrad_vs_torch(gpu):
         assert np.abs(got - ref_w).max() <= 2e-6 * scale
         assert np.abs(db.cpu().numpy() - ref_b).max() <= 2e-6 * np.abs(dy).max() * n * h * w
 
+
+@pytest.mark.gpu
+def test_gpu_wino_wgrad_vs_torch(gpu):
+    """posfeat_conv3x3_wino_wgrad (F(4x4,3x3) weight gradient: dY transform,
+    36 split transform-domain GEMMs, G^T dU G into the packed K order) against
+    torch's fp64 conv2d weight/bias gradient; the last case splits the tile
+    reduction (nsplit 3)."""
+    from posfeat_amd import weights
+    from posfeat_amd._lib import check, lib, ptr, stream_ptr
+    rs = np.random.RandomState(1)
+    for (n, h, w, cin, cout) in ((2, 16, 20, 128, 128), (1, 12, 24, 256, 128),
+                                 (4, 64, 96, 128, 128)):
+        x = rs.randn(n, cin, h, w).astype(np.float32)
+        dy = rs.randn(n, cout, h, w).astype(np.float32)
+        xt = torch.from_numpy(x).double()
+        wt = torch.zeros(cout, cin, 3, 3, dtype=torch.float64, requires_grad=True)
+        torch.nn.functional.conv2d(xt, wt, padding=1).backward(torch.from_numpy(dy).double())
+        ref_w = wt.grad.numpy()
+        ref_b = dy.astype(np.float64).sum((0, 2, 3))
+        xd = torch.from_numpy(np.ascontiguousarray(x.transpose(0, 2, 3, 1))).to(gpu)
+        dyd = torch.from_numpy(np.ascontiguousarray(dy.transpose(0, 2, 3, 1))).to(gpu)
+        kpad = lib().posfeat_conv_packed_k(cin, 3, 3)
+        dw = torch.full((cout * kpad,), float("nan"), device=gpu)
+        db = torch.empty(cout, device=gpu)
+        need = lib().posfeat_wino_wgrad_workspace(n, h, w, cin, cout)
+        assert need > 0
+        ws = torch.empty(need, dtype=torch.uint8, device=gpu)
+        check(lib().posfeat_conv3x3_wino_wgrad(ptr(dyd), cout, ptr(xd), cin, n, h, w, cin, cout,
+                                               ptr(dw), ptr(db), ptr(ws), need, stream_ptr()))
+        torch.cuda.synchronize()
+        got = weights.unpack_conv(dw.cpu().numpy(), cout, cin, 3, 3)
+        # |dw| sums n*h*w products of unit normals: rms sqrt(n h w); the
+        # Winograd transforms grow the fp32 rounding by ~10x over direct
+        err = np.abs(got - ref_w).max() / np.sqrt(n * h * w)
+        assert err <= 2e-4, err
+        assert np.abs(db.cpu().numpy() - ref_b).max() <= 1e-4 * np.sqrt(n * h * w)
+
