@@ -669,6 +669,204 @@ __global__ void window_bwd_kernel(const float* __restrict__ f1, const float* __r
   dq[wid * 128 + lane + 64] = dq1;
 }
 
+// The same backward over the window's pixel patch instead of its taps.  Every
+// tap's 4 bilinear corners land in a patch of at most (win_w+4) x (win_h+4)
+// pixels, and both the logits and the map gradient factor through it:
+//   logit_s = q . v_s = sum_corners w_c (q . fm[c])     (qd: one dot per pixel)
+//   d fm[p] = (sum_s w(s, p) dsim_s) q = c_p q           (c: separable adjoint)
+//   dq      = sum_p c_p fm[p]
+// so the map is read twice per patch pixel (not 2 x 4 per tap) and each patch
+// pixel takes one 128-wide fixed-point scatter (not up to 4 per tap).  One
+// wave per query point, wave-private LDS; the 16-lane groups of a wave own 4
+// patch pixels at a time (8 channels per lane).
+constexpr int WB_PATCH = 1024, WB_TAPS = MAX_WIN, WB_AXES = 256;
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// bilinear weight of pixel coordinate p for sample position f (0 unless p is
+// one of f's two neighbours): the 1-D factors of bilinear128's corner weights
+__device__ __forceinline__ float lin_w(float f, int p) {
+  const float fl = floorf(f);
+  const int p0 = (int)fl;
+  return p == p0 ? (float)(p0 + 1) - f : (p == p0 + 1 ? f - fl : 0.f);
+}
+
+__global__ __launch_bounds__(256) void window_bwd_patch_kernel(
+    const float* __restrict__ f1, const float* __restrict__ fm2, const float* __restrict__ center,
+    const float* __restrict__ gE, int nb, int n, int h2, int w2, int win_h, int win_w,
+    float window_size, float* __restrict__ dq, unsigned long long* __restrict__ acc) {
+  __shared__ float s_pc[4][WB_PATCH];  // q . fm per patch pixel, then c
+  __shared__ float s_t[4][WB_PATCH];   // separable adjoint, first stage [iy][px]
+  __shared__ float s_ds[4][WB_TAPS];   // dsim per tap
+  __shared__ float s_ax[4][WB_AXES];   // fx per ix, then fy per iy
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int grp = lane >> 4, cl = lane & 15;
+  const long long wid = blockIdx.x * 4LL + wv;
+  if (wid >= (long long)nb * n) return;
+  const float gx0 = gE[wid * 2], gy0 = gE[wid * 2 + 1];
+  if (gx0 == 0.f && gy0 == 0.f) {  // masked point: no gradient
+    dq[wid * 128 + lane] = 0.f;
+    dq[wid * 128 + lane + 64] = 0.f;
+    return;
+  }
+  const int b = (int)(wid / n);
+  const float* fmb = fm2 + (long long)b * h2 * w2 * 128;
+  unsigned long long* accb = acc + (long long)b * h2 * w2 * 128;
+  float* pc = s_pc[wv];
+  float* tt = s_t[wv];
+  float* dsv = s_ds[wv];
+  float* ax = s_ax[wv];
+  const float jx = center[wid * 2], jy = center[wid * 2 + 1];
+  for (int i = lane; i < win_w; i += 64)
+    ax[i] = ((jx + linspace_f(-window_size, window_size, win_w, i) + 1.f) * w2 - 1.f) / 2.f;
+  for (int i = lane; i < win_h; i += 64)
+    ax[win_w + i] = ((jy + linspace_f(-window_size, window_size, win_h, i) + 1.f) * h2 - 1.f) / 2.f;
+  wave_lds_sync();
+  const int px0 = (int)floorf(ax[0]), py0 = (int)floorf(ax[win_w]);
+  const int PW = (int)floorf(ax[win_w - 1]) + 2 - px0;
+  const int PH = (int)floorf(ax[win_w + win_h - 1]) + 2 - py0;
+  const int np = PW * PH;
+  // query channels: contiguous 8 per lane (map loads), strided by 16 (scatter)
+  const float* qp = f1 + wid * 128;
+  const f32x4 qa = *reinterpret_cast<const f32x4*>(qp + cl * 8);
+  const f32x4 qb = *reinterpret_cast<const f32x4*>(qp + cl * 8 + 4);
+  float qs[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) qs[k] = qp[cl + 16 * k];
+  // pass 1: qd[p] = q . fm[p] (0 outside the map: the zero padding)
+  for (int base = 0; base < np; base += 4) {
+    const int pp = base + grp;
+    const int py = py0 + pp / PW, px = px0 + pp % PW;
+    float v = 0.f;
+    if (pp < np && (unsigned)py < (unsigned)h2 && (unsigned)px < (unsigned)w2) {
+      const float* src = fmb + ((long long)py * w2 + px) * 128 + cl * 8;
+      const f32x4 a = *reinterpret_cast<const f32x4*>(src);
+      const f32x4 c = *reinterpret_cast<const f32x4*>(src + 4);
+      v = qa.x * a.x + qa.y * a.y + qa.z * a.z + qa.w * a.w + qb.x * c.x + qb.y * c.y +
+          qb.z * c.z + qb.w * c.w;
+    }
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (cl == 0 && pp < np) pc[pp] = v;
+  }
+  wave_lds_sync();
+  // logits, softmax and dsim (the tap layout of window_bwd_kernel)
+  const int nw = win_h * win_w;
+  float wl[MAX_WIN / 64];
+  float wm = -INFINITY;
+#pragma unroll
+  for (int r = 0; r < MAX_WIN / 64; ++r) {
+    const int s = lane + 64 * r;
+    wl[r] = -INFINITY;
+    if (s < nw) {
+      const int iy = s / win_w, ix = s - iy * win_w;
+      const float fx = ax[ix], fy = ax[win_w + iy];
+      const float flx = floorf(fx), fly = floorf(fy);
+      const int cx = (int)flx - px0, cy = (int)fly - py0;
+      const float* r0 = pc + cy * PW + cx;
+      const float ax1 = fx - flx, ay1 = fy - fly, ax0 = 1.f - ax1, ay0 = 1.f - ay1;
+      wl[r] = ay0 * (ax0 * r0[0] + ax1 * r0[1]) + ay1 * (ax0 * r0[PW] + ax1 * r0[PW + 1]);
+      wm = fmaxf(wm, wl[r]);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) wm = fmaxf(wm, __shfl_xor(wm, o, 64));
+  float pr[MAX_WIN / 64], dp[MAX_WIN / 64];
+  float se = 0.f;
+#pragma unroll
+  for (int r = 0; r < MAX_WIN / 64; ++r) {
+    const int s = lane + 64 * r;
+    pr[r] = s < nw ? expf(wl[r] - wm) : 0.f;
+    se += pr[r];
+  }
+  se = pf_wave_sum(se);
+  float sdp = 0.f;
+#pragma unroll
+  for (int r = 0; r < MAX_WIN / 64; ++r) {
+    const int s = lane + 64 * r;
+    pr[r] /= se;
+    dp[r] = 0.f;
+    if (s < nw) {
+      const int iy = s / win_w, ix = s - iy * win_w;
+      const float gx = jx + linspace_f(-window_size, window_size, win_w, ix);
+      const float gy = jy + linspace_f(-window_size, window_size, win_h, iy);
+      dp[r] = gx0 * gx + gy0 * gy;
+      sdp += pr[r] * dp[r];
+    }
+  }
+  sdp = pf_wave_sum(sdp);
+#pragma unroll
+  for (int r = 0; r < MAX_WIN / 64; ++r) {
+    const int s = lane + 64 * r;
+    if (s < nw) dsv[s] = pr[r] * (dp[r] - sdp);
+  }
+  wave_lds_sync();
+  // c = Wy^T dsim Wx, separably: t[iy][px] = sum_ix wx(ix, px) dsim[iy][ix]
+  for (int e = lane; e < win_h * PW; e += 64) {
+    const int iy = e / PW, px = px0 + e % PW;
+    float v = 0.f;
+    for (int ix = 0; ix < win_w; ++ix) {
+      const float wx = lin_w(ax[ix], px);
+      if (wx != 0.f) v += wx * dsv[iy * win_w + ix];
+    }
+    tt[e] = v;
+  }
+  wave_lds_sync();
+  for (int e = lane; e < np; e += 64) {
+    const int py = py0 + e / PW, pxl = e % PW;
+    float v = 0.f;
+    for (int iy = 0; iy < win_h; ++iy) {
+      const float wy = lin_w(ax[win_w + iy], py);
+      if (wy != 0.f) v += wy * tt[iy * PW + pxl];
+    }
+    pc[e] = v;
+  }
+  wave_lds_sync();
+  // pass 2: dq = sum_p c_p fm[p];  d fm[p] += c_p q (fixed point)
+  f32x4 da = {0.f, 0.f, 0.f, 0.f}, db = {0.f, 0.f, 0.f, 0.f};
+  for (int base = 0; base < np; base += 4) {
+    const int pp = base + grp;
+    const int py = py0 + pp / PW, px = px0 + pp % PW;
+    if (pp < np && (unsigned)py < (unsigned)h2 && (unsigned)px < (unsigned)w2) {
+      const float c = pc[pp];
+      if (c != 0.f) {
+        const long long off = ((long long)py * w2 + px) * 128;
+        const float* src = fmb + off + cl * 8;
+        da += c * *reinterpret_cast<const f32x4*>(src);
+        db += c * *reinterpret_cast<const f32x4*>(src + 4);
+        unsigned long long* dst = accb + off + cl;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) fx_add(dst + 16 * k, c * qs[k]);
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 16; o < 64; o <<= 1) {
+    da.x += __shfl_xor(da.x, o, 64);
+    da.y += __shfl_xor(da.y, o, 64);
+    da.z += __shfl_xor(da.z, o, 64);
+    da.w += __shfl_xor(da.w, o, 64);
+    db.x += __shfl_xor(db.x, o, 64);
+    db.y += __shfl_xor(db.y, o, 64);
+    db.z += __shfl_xor(db.z, o, 64);
+    db.w += __shfl_xor(db.w, o, 64);
+  }
+  if (grp == 0) {
+    *reinterpret_cast<f32x4*>(dq + wid * 128 + cl * 8) = da;
+    *reinterpret_cast<f32x4*>(dq + wid * 128 + cl * 8 + 4) = db;
+  }
+}
+
+// the patch kernel's LDS bounds (patch <= (win + 4)^2, see above)
+bool window_patch_fits(int win_h, int win_w) {
+  return (win_w + 4) * (win_h + 4) <= WB_PATCH && win_w + win_h <= WB_AXES &&
+         win_h * win_w <= WB_TAPS;
+}
+
 // Query-descriptor backward: f = normalize(s), s = grid_sample(xf, c) (zeros,
 // align_corners=False): ds = (dq - f (f.dq)) / max(|s|, 1e-12) scattered over
 // the 4 corners of c into acc (raw-map gradient, fixed point).  One wave/point.
@@ -976,10 +1174,18 @@ extern "C" int posfeat_line2window_backward(
                      (float)((W1 - 1) / 2.0), (float)((H1 - 1) / 2.0), gE2);
   PF_CHECK_LAUNCH();
   // window softmax backward: direction 1 scatters into image 2's map, and back
-  hipLaunchKernelGGL(window_bwd_kernel, dim3((b * n1 + 3) / 4), dim3(256), 0, st, f1, fm2,
-                     fwd->l1_exp_n, gE1, b, n1, h2, w2, win_h2, win_w2, window_size, dq1, afm2);
-  hipLaunchKernelGGL(window_bwd_kernel, dim3((b * n2 + 3) / 4), dim3(256), 0, st, f2, fm1,
-                     fwd->l2_exp_n, gE2, b, n2, h1, w1, win_h1, win_w1, window_size, dq2, afm1);
+  {
+    const char* e = getenv("POSFEAT_WINBWD");
+    const bool taps = e && e[0] == '0';
+    auto wbwd = (!taps && window_patch_fits(win_h2, win_w2)) ? window_bwd_patch_kernel
+                                                             : window_bwd_kernel;
+    hipLaunchKernelGGL(wbwd, dim3((b * n1 + 3) / 4), dim3(256), 0, st, f1, fm2, fwd->l1_exp_n,
+                       gE1, b, n1, h2, w2, win_h2, win_w2, window_size, dq1, afm2);
+    wbwd = (!taps && window_patch_fits(win_h1, win_w1)) ? window_bwd_patch_kernel
+                                                        : window_bwd_kernel;
+    hipLaunchKernelGGL(wbwd, dim3((b * n2 + 3) / 4), dim3(256), 0, st, f2, fm1, fwd->l2_exp_n,
+                       gE2, b, n2, h1, w1, win_h1, win_w1, window_size, dq2, afm1);
+  }
   // query descriptors: normalize + grid_sample backward into the raw maps
   hipLaunchKernelGGL(query_bwd_kernel, dim3((b * n1 + 3) / 4), dim3(256), 0, st, xf1, cs1, c1n, f1,
                      dq1, b, n1, h1, w1, ax1);
