@@ -250,6 +250,81 @@ __device__ __forceinline__ float2 bilinear128(const float* __restrict__ fm, int 
 constexpr int MAX_LINE = 128;   // line_step <= 128 (2 logits per lane)
 constexpr int MAX_WIN = 512;    // window taps <= 512 (8 logits per lane)
 
+constexpr int WB_PATCH = 1024, WB_TAPS = MAX_WIN, WB_AXES = 256;
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// bilinear weight of pixel coordinate p for sample position f (0 unless p is
+// one of f's two neighbours): the 1-D factors of bilinear128's corner weights
+__device__ __forceinline__ float lin_w(float f, int p) {
+  const float fl = floorf(f);
+  const int p0 = (int)fl;
+  return p == p0 ? (float)(p0 + 1) - f : (p == p0 + 1 ? f - fl : 0.f);
+}
+
+// Window logits over the patch (shared by the forward and the backward):
+// fills ax (fx per ix, fy per iy), pc (q . fm per patch pixel, 0 outside the
+// map) and the tap logits wl[r] of taps lane + 64 r (-inf past nw).
+struct WinPatch {
+  int px0, py0, PW, PH;
+};
+
+__device__ __forceinline__ WinPatch window_patch_logits(const float* __restrict__ fmb, int h2,
+                                                        int w2, const float* __restrict__ qp,
+                                                        float jx, float jy, int win_h, int win_w,
+                                                        float window_size, float* pc, float* ax,
+                                                        float (&wl)[MAX_WIN / 64]) {
+  const int lane = threadIdx.x & 63, grp = lane >> 4, cl = lane & 15;
+  for (int i = lane; i < win_w; i += 64)
+    ax[i] = ((jx + linspace_f(-window_size, window_size, win_w, i) + 1.f) * w2 - 1.f) / 2.f;
+  for (int i = lane; i < win_h; i += 64)
+    ax[win_w + i] = ((jy + linspace_f(-window_size, window_size, win_h, i) + 1.f) * h2 - 1.f) / 2.f;
+  wave_lds_sync();
+  WinPatch P;
+  P.px0 = (int)floorf(ax[0]);
+  P.py0 = (int)floorf(ax[win_w]);
+  P.PW = (int)floorf(ax[win_w - 1]) + 2 - P.px0;
+  P.PH = (int)floorf(ax[win_w + win_h - 1]) + 2 - P.py0;
+  const int np = P.PW * P.PH;
+  const f32x4 qa = *reinterpret_cast<const f32x4*>(qp + cl * 8);
+  const f32x4 qb = *reinterpret_cast<const f32x4*>(qp + cl * 8 + 4);
+  for (int base = 0; base < np; base += 4) {
+    const int pp = base + grp;
+    const int py = P.py0 + pp / P.PW, px = P.px0 + pp % P.PW;
+    float v = 0.f;
+    if (pp < np && (unsigned)py < (unsigned)h2 && (unsigned)px < (unsigned)w2) {
+      const float* src = fmb + ((long long)py * w2 + px) * 128 + cl * 8;
+      const f32x4 a = *reinterpret_cast<const f32x4*>(src);
+      const f32x4 c = *reinterpret_cast<const f32x4*>(src + 4);
+      v = qa.x * a.x + qa.y * a.y + qa.z * a.z + qa.w * a.w + qb.x * c.x + qb.y * c.y +
+          qb.z * c.z + qb.w * c.w;
+    }
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (cl == 0 && pp < np) pc[pp] = v;
+  }
+  wave_lds_sync();
+  const int nw = win_h * win_w;
+#pragma unroll
+  for (int r = 0; r < MAX_WIN / 64; ++r) {
+    const int s = lane + 64 * r;
+    wl[r] = -INFINITY;
+    if (s < nw) {
+      const int iy = s / win_w, ix = s - iy * win_w;
+      const float fx = ax[ix], fy = ax[win_w + iy];
+      const float flx = floorf(fx), fly = floorf(fy);
+      const float* r0 = pc + ((int)fly - P.py0) * P.PW + ((int)flx - P.px0);
+      const float ax1 = fx - flx, ay1 = fy - fly, ax0 = 1.f - ax1, ay0 = 1.f - ay1;
+      wl[r] = ay0 * (ax0 * r0[0] + ax1 * r0[1]) + ay1 * (ax0 * r0[P.PW] + ax1 * r0[P.PW + 1]);
+    }
+  }
+  return P;
+}
+
 // One wave per query point: epipolar line search + window expectation.
 __global__ void line_window_kernel(const float* __restrict__ cpx,   // [b][n][2] query pixels
                                    const float* __restrict__ Fm,    // [b][3][3]
@@ -260,7 +335,9 @@ __global__ void line_window_kernel(const float* __restrict__ cpx,   // [b][n][2]
                                    int win_h, int win_w, float window_size,
                                    float* __restrict__ l_exp_n, float* __restrict__ l_org_n,
                                    uint8_t* __restrict__ valid, float* __restrict__ w_px,
-                                   float* __restrict__ w_std) {
+                                   float* __restrict__ w_std, int use_patch) {
+  __shared__ float s_pc[4][WB_PATCH];
+  __shared__ float s_ax[4][WB_AXES];
   const int lane = threadIdx.x & 63;
   const long long wid = blockIdx.x * (long long)(blockDim.x >> 6) + (threadIdx.x >> 6);
   if (wid >= (long long)nb * n) return;
@@ -332,17 +409,23 @@ __global__ void line_window_kernel(const float* __restrict__ cpx,   // [b][n][2]
   // ---- window around the jittered line expectation
   const int nw = win_h * win_w;
   float wl[MAX_WIN / 64];
+  if (use_patch) {  // logits through the window's pixel patch (see window_patch_logits)
+    const int wv = threadIdx.x >> 6;
+    window_patch_logits(fmb, h2, w2, f1 + wid * 128, jx, jy, win_h, win_w, window_size, s_pc[wv],
+                        s_ax[wv], wl);
+  } else {
 #pragma unroll
-  for (int r = 0; r < MAX_WIN / 64; ++r) wl[r] = -INFINITY;
-  for (int s = 0; s < nw; ++s) {
-    const int iy = s / win_w, ix = s - iy * win_w;
-    const float gx = jx + linspace_f(-window_size, window_size, win_w, ix);
-    const float gy = jy + linspace_f(-window_size, window_size, win_h, iy);
-    const float2 v = bilinear128<false>(fmb, h2, w2, gx, gy, lane);
-    const float d = pf_wave_sum(q0 * v.x + q1 * v.y);
+    for (int r = 0; r < MAX_WIN / 64; ++r) wl[r] = -INFINITY;
+    for (int s = 0; s < nw; ++s) {
+      const int iy = s / win_w, ix = s - iy * win_w;
+      const float gx = jx + linspace_f(-window_size, window_size, win_w, ix);
+      const float gy = jy + linspace_f(-window_size, window_size, win_h, iy);
+      const float2 v = bilinear128<false>(fmb, h2, w2, gx, gy, lane);
+      const float d = pf_wave_sum(q0 * v.x + q1 * v.y);
 #pragma unroll
-    for (int r = 0; r < MAX_WIN / 64; ++r)
-      if (s == lane + 64 * r) wl[r] = d;
+      for (int r = 0; r < MAX_WIN / 64; ++r)
+        if (s == lane + 64 * r) wl[r] = d;
+    }
   }
   float wm = -INFINITY;
 #pragma unroll
@@ -679,22 +762,6 @@ __global__ void window_bwd_kernel(const float* __restrict__ f1, const float* __r
 // pixel takes one 128-wide fixed-point scatter (not up to 4 per tap).  One
 // wave per query point, wave-private LDS; the 16-lane groups of a wave own 4
 // patch pixels at a time (8 channels per lane).
-constexpr int WB_PATCH = 1024, WB_TAPS = MAX_WIN, WB_AXES = 256;
-
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// bilinear weight of pixel coordinate p for sample position f (0 unless p is
-// one of f's two neighbours): the 1-D factors of bilinear128's corner weights
-__device__ __forceinline__ float lin_w(float f, int p) {
-  const float fl = floorf(f);
-  const int p0 = (int)fl;
-  return p == p0 ? (float)(p0 + 1) - f : (p == p0 + 1 ? f - fl : 0.f);
-}
-
 __global__ __launch_bounds__(256) void window_bwd_patch_kernel(
     const float* __restrict__ f1, const float* __restrict__ fm2, const float* __restrict__ center,
     const float* __restrict__ gE, int nb, int n, int h2, int w2, int win_h, int win_w,
@@ -721,58 +788,18 @@ __global__ __launch_bounds__(256) void window_bwd_patch_kernel(
   float* dsv = s_ds[wv];
   float* ax = s_ax[wv];
   const float jx = center[wid * 2], jy = center[wid * 2 + 1];
-  for (int i = lane; i < win_w; i += 64)
-    ax[i] = ((jx + linspace_f(-window_size, window_size, win_w, i) + 1.f) * w2 - 1.f) / 2.f;
-  for (int i = lane; i < win_h; i += 64)
-    ax[win_w + i] = ((jy + linspace_f(-window_size, window_size, win_h, i) + 1.f) * h2 - 1.f) / 2.f;
-  wave_lds_sync();
-  const int px0 = (int)floorf(ax[0]), py0 = (int)floorf(ax[win_w]);
-  const int PW = (int)floorf(ax[win_w - 1]) + 2 - px0;
-  const int PH = (int)floorf(ax[win_w + win_h - 1]) + 2 - py0;
-  const int np = PW * PH;
-  // query channels: contiguous 8 per lane (map loads), strided by 16 (scatter)
   const float* qp = f1 + wid * 128;
-  const f32x4 qa = *reinterpret_cast<const f32x4*>(qp + cl * 8);
-  const f32x4 qb = *reinterpret_cast<const f32x4*>(qp + cl * 8 + 4);
-  float qs[8];
+  float wl[MAX_WIN / 64];
+  const WinPatch P =
+      window_patch_logits(fmb, h2, w2, qp, jx, jy, win_h, win_w, window_size, pc, ax, wl);
+  const int px0 = P.px0, py0 = P.py0, PW = P.PW, np = P.PW * P.PH;
+  float qs[8];  // query channels strided by 16 (the scatter's coalesced order)
 #pragma unroll
   for (int k = 0; k < 8; ++k) qs[k] = qp[cl + 16 * k];
-  // pass 1: qd[p] = q . fm[p] (0 outside the map: the zero padding)
-  for (int base = 0; base < np; base += 4) {
-    const int pp = base + grp;
-    const int py = py0 + pp / PW, px = px0 + pp % PW;
-    float v = 0.f;
-    if (pp < np && (unsigned)py < (unsigned)h2 && (unsigned)px < (unsigned)w2) {
-      const float* src = fmb + ((long long)py * w2 + px) * 128 + cl * 8;
-      const f32x4 a = *reinterpret_cast<const f32x4*>(src);
-      const f32x4 c = *reinterpret_cast<const f32x4*>(src + 4);
-      v = qa.x * a.x + qa.y * a.y + qa.z * a.z + qa.w * a.w + qb.x * c.x + qb.y * c.y +
-          qb.z * c.z + qb.w * c.w;
-    }
-#pragma unroll
-    for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    if (cl == 0 && pp < np) pc[pp] = v;
-  }
-  wave_lds_sync();
-  // logits, softmax and dsim (the tap layout of window_bwd_kernel)
   const int nw = win_h * win_w;
-  float wl[MAX_WIN / 64];
   float wm = -INFINITY;
 #pragma unroll
-  for (int r = 0; r < MAX_WIN / 64; ++r) {
-    const int s = lane + 64 * r;
-    wl[r] = -INFINITY;
-    if (s < nw) {
-      const int iy = s / win_w, ix = s - iy * win_w;
-      const float fx = ax[ix], fy = ax[win_w + iy];
-      const float flx = floorf(fx), fly = floorf(fy);
-      const int cx = (int)flx - px0, cy = (int)fly - py0;
-      const float* r0 = pc + cy * PW + cx;
-      const float ax1 = fx - flx, ay1 = fy - fly, ax0 = 1.f - ax1, ay0 = 1.f - ay1;
-      wl[r] = ay0 * (ax0 * r0[0] + ax1 * r0[1]) + ay1 * (ax0 * r0[PW] + ax1 * r0[PW + 1]);
-      wm = fmaxf(wm, wl[r]);
-    }
-  }
+  for (int r = 0; r < MAX_WIN / 64; ++r) wm = fmaxf(wm, wl[r]);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) wm = fmaxf(wm, __shfl_xor(wm, o, 64));
   float pr[MAX_WIN / 64], dp[MAX_WIN / 64];
@@ -862,6 +889,12 @@ __global__ __launch_bounds__(256) void window_bwd_patch_kernel(
 }
 
 // the patch kernel's LDS bounds (patch <= (win + 4)^2, see above)
+// POSFEAT_WINPATCH=0: the per-tap kernels (A/B runs)
+bool window_patch_on() {
+  const char* e = getenv("POSFEAT_WINPATCH");
+  return !(e && e[0] == '0');
+}
+
 bool window_patch_fits(int win_h, int win_w) {
   return (win_w + 4) * (win_h + 4) <= WB_PATCH && win_w + win_h <= WB_AXES &&
          win_h * win_w <= WB_TAPS;
@@ -1083,10 +1116,12 @@ extern "C" int posfeat_line2window(const float* xf1, int cs1, const float* xf2, 
   // line search + window, both directions
   hipLaunchKernelGGL(line_window_kernel, dim3((b * n1 + 3) / 4), dim3(256), 0, st, c1p, F1, f1,
                      fm2, rand1, b, n1, h2, w2, H2, W2, line_step, win_h2, win_w2, window_size,
-                     out->l1_exp_n, out->l1_org_n, out->valid1, out->w1, out->w1_std);
+                     out->l1_exp_n, out->l1_org_n, out->valid1, out->w1, out->w1_std,
+                     (int)(window_patch_on() && window_patch_fits(win_h2, win_w2)));
   hipLaunchKernelGGL(line_window_kernel, dim3((b * n2 + 3) / 4), dim3(256), 0, st, c2p, F2, f2,
                      fm1, rand2, b, n2, h1, w1, H1, W1, line_step, win_h1, win_w1, window_size,
-                     out->l2_exp_n, out->l2_org_n, out->valid2, out->w2, out->w2_std);
+                     out->l2_exp_n, out->l2_org_n, out->valid2, out->w2, out->w2_std,
+                     (int)(window_patch_on() && window_patch_fits(win_h1, win_w1)));
   PF_CHECK_LAUNCH();
   return POSFEAT_OK;
 }
@@ -1175,8 +1210,7 @@ extern "C" int posfeat_line2window_backward(
   PF_CHECK_LAUNCH();
   // window softmax backward: direction 1 scatters into image 2's map, and back
   {
-    const char* e = getenv("POSFEAT_WINBWD");
-    const bool taps = e && e[0] == '0';
+    const bool taps = !window_patch_on();
     auto wbwd = (!taps && window_patch_fits(win_h2, win_w2)) ? window_bwd_patch_kernel
                                                              : window_bwd_kernel;
     hipLaunchKernelGGL(wbwd, dim3((b * n1 + 3) / 4), dim3(256), 0, st, f1, fm2, fwd->l1_exp_n,
