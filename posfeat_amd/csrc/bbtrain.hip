@@ -433,8 +433,8 @@ int layer_fwd(Ctx& c, int li, const float* x, int xcs, int h, int w, float* out,
   const int c4n = L.cout / 4;
   return timed(c, "fwd:bn", 0, [&] {
     hipLaunchKernelGGL(bn_partial_kernel<0>, dim3(g.nchunk, g.gy), dim3(256), 0, c.st, y, P,
-                       L.cout, g.chunk, nullptr, 0, nullptr, 0, 0, nullptr, nullptr,
-                       c.sd(m->part));
+                       L.cout, g.chunk, nullptr, 0, nullptr, 0, 0, nullptr, nullptr, nullptr,
+                       nullptr, c.sd(m->part));
     hipLaunchKernelGGL(bn_stats_final_kernel, dim3((L.cout + 3) / 4), dim3(256), 0, c.st,
                        c.sd(m->part), g.nchunk, L.cout, P, mom, mean, rstd,
                        stats ? stats + L.rm_off : nullptr, stats ? stats + L.rv_off : nullptr);
@@ -465,10 +465,13 @@ int upsample_adjoint(Ctx& c, const float* g, int gcs, int h, int w, int C, float
 // dx (cs dxcs): input gradient (+ add, cs addcs) when non-null.
 int layer_bwd(Ctx& c, int li, const float* x, int xcs, int h, int w, const float* a, int acs,
               const float* da, int dacs, float* grad, int acc, float* gres, float* dx, int dxcs,
-              const float* add, int addcs) {
+              const float* add, int addcs, bool residual = false) {
   const TLayer& L = tab().v[li];
   posfeat_bbtrain* m = c.m;
   const int B = m->B;
+  // act'(a) of a non-residual layer from y (a = act(BN(y)), recomputed exactly
+  // as the forward did) rather than another read of the stored activation
+  const float* as = residual ? a : nullptr;
   const int oh = out_dim(h, L.k, L.stride), ow = out_dim(w, L.k, L.stride);
   const long long P = (long long)B * oh * ow;
   const int C = L.cout, c4n = C / 4;
@@ -480,12 +483,14 @@ int layer_bwd(Ctx& c, int li, const float* x, int xcs, int h, int w, const float
   const BnGrid g = bn_grid(P, C);
   PF_TRY(timed(c, "bwd:bn", 0, [&] {
     hipLaunchKernelGGL(bn_partial_kernel<1>, dim3(g.nchunk, g.gy), dim3(256), 0, c.st, y, P, C,
-                       g.chunk, a, acs, da, dacs, L.act, mean, rstd, c.sd(m->part));
+                       g.chunk, as, acs, da, dacs, L.act, mean, rstd, c.prm + L.g_off,
+                       c.prm + L.be_off, c.sd(m->part));
     hipLaunchKernelGGL(bn_bwd_final_kernel, dim3((C + 3) / 4), dim3(256), 0, c.st,
                        c.sd(m->part), g.nchunk, C, P, c.prm + L.g_off, rstd, grad + L.g_off,
                        grad + L.be_off, acc, coef);
     hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(P * c4n, 256)), dim3(256), 0, c.st, y, P,
-                       c4n, a, acs, da, dacs, L.act, mean, rstd, coef, dy, gres);
+                       c4n, as, acs, da, dacs, L.act, mean, rstd, c.prm + L.g_off, c.prm + L.be_off,
+                       coef, dy, gres);
     PF_CHECK_LAUNCH();
     return POSFEAT_OK;
   }));
@@ -670,7 +675,7 @@ int backward(Ctx& c, const float* dfa, int dfcs, float* grad, int acc) {
     float* d2 = c.s(m->gd);  // d a2
     float* d1 = c.s(m->gc);  // d a1
     PF_TRY(layer_bwd(c, b.c3, c.f(m->a2[i]), b.pl, oh, ow, io[i].out, io[i].ocs, cur, ccs, grad,
-                     acc, gres, d2, b.pl, nullptr, 0));
+                     acc, gres, d2, b.pl, nullptr, 0, true));
     PF_TRY(layer_bwd(c, b.c2, c.f(m->a1[i]), b.pl, ih, iw, c.f(m->a2[i]), b.pl, d2, b.pl, grad,
                      acc, nullptr, d1, b.pl, nullptr, 0));
     const float* radd;

@@ -18,11 +18,22 @@ __device__ __forceinline__ float act_grad(int act, float a) {
 // chunk's pixels; fp64 accumulation, LDS sum over rows, part[chunk][2][C].
 // MODE 0 (forward statistics): sums of y and y^2.
 // MODE 1 (backward): g = da act'(a); sums of g and g x^, x^ = (y - mean) rstd.
+// the BN output before the residual add, and the activation, exactly as
+// bn_apply_kernel evaluates them (the backward recomputes a = act(z) from y
+// for non-residual layers instead of re-reading the stored activation)
+__device__ __forceinline__ float bn_z(float g, float v, float mu, float rs, float b) {
+  return g * (v - mu) * rs + b;
+}
+__device__ __forceinline__ float act_fwd(int act, float z) {
+  return act == ACT_RELU ? fmaxf(z, 0.f) : act == ACT_ELU ? pf_elu(z) : z;
+}
+
 template <int MODE>
 __global__ __launch_bounds__(256) void bn_partial_kernel(
     const float* __restrict__ y, long long P, int C, int chunk, const float* __restrict__ a, int acs,
     const float* __restrict__ da, int dacs, int act, const float* __restrict__ mean,
-    const float* __restrict__ rstd, double* __restrict__ part) {
+    const float* __restrict__ rstd, const float* __restrict__ gam, const float* __restrict__ bet,
+    double* __restrict__ part) {
   __shared__ double red[256][8];
   const int c4n = C / 4, qpb = c4n < 64 ? c4n : 64, R = 256 / qpb;
   const int tid = threadIdx.x, ql = tid % qpb, r = tid / qpb;
@@ -30,10 +41,14 @@ __global__ __launch_bounds__(256) void bn_partial_kernel(
   const long long p0 = (long long)blockIdx.x * chunk;
   const long long p1 = p0 + chunk < P ? p0 + chunk : P;
   double s0[4] = {0, 0, 0, 0}, s1[4] = {0, 0, 0, 0};
-  f32x4 mu = {0, 0, 0, 0}, rs = {0, 0, 0, 0};
+  f32x4 mu = {0, 0, 0, 0}, rs = {0, 0, 0, 0}, gm = {0, 0, 0, 0}, bt = {0, 0, 0, 0};
   if (MODE == 1) {
     mu = *reinterpret_cast<const f32x4*>(mean + q * 4);
     rs = *reinterpret_cast<const f32x4*>(rstd + q * 4);
+    if (!a && act != ACT_NONE) {
+      gm = *reinterpret_cast<const f32x4*>(gam + q * 4);
+      bt = *reinterpret_cast<const f32x4*>(bet + q * 4);
+    }
   }
   for (long long p = p0 + r; p < p1; p += R) {
     const f32x4 v = *reinterpret_cast<const f32x4*>(y + p * C + q * 4);
@@ -46,7 +61,14 @@ __global__ __launch_bounds__(256) void bn_partial_kernel(
     } else {
       const f32x4 gd = *reinterpret_cast<const f32x4*>(da + p * dacs + q * 4);
       f32x4 av = {0, 0, 0, 0};
-      if (act != ACT_NONE) av = *reinterpret_cast<const f32x4*>(a + p * acs + q * 4);
+      if (act != ACT_NONE) {
+        if (a) {
+          av = *reinterpret_cast<const f32x4*>(a + p * acs + q * 4);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) av[j] = act_fwd(act, bn_z(gm[j], v[j], mu[j], rs[j], bt[j]));
+        }
+      }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const float g = gd[j] * act_grad(act, av[j]);
@@ -143,11 +165,10 @@ __global__ void bn_apply_kernel(const float* __restrict__ y, long long P, int c4
     const f32x4 b = *reinterpret_cast<const f32x4*>(bet + q * 4);
     f32x4 o;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) o[j] = g[j] * (v[j] - mu[j]) * rs[j] + b[j];
+    for (int j = 0; j < 4; ++j) o[j] = bn_z(g[j], v[j], mu[j], rs[j], b[j]);
     if (res) o += *reinterpret_cast<const f32x4*>(res + p * rcs + q * 4);
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      o[j] = act == ACT_RELU ? fmaxf(o[j], 0.f) : act == ACT_ELU ? pf_elu(o[j]) : o[j];
+    for (int j = 0; j < 4; ++j) o[j] = act_fwd(act, o[j]);
     *reinterpret_cast<f32x4*>(out + p * ocs + q * 4) = o;
   }
 }
@@ -174,6 +195,7 @@ __global__ void bn_bwd_apply_kernel(const float* __restrict__ y, long long P, in
                                     const float* __restrict__ a, int acs,
                                     const float* __restrict__ da, int dacs, int act,
                                     const float* __restrict__ mean, const float* __restrict__ rstd,
+                                    const float* __restrict__ gam, const float* __restrict__ bet,
                                     const float* __restrict__ coef, float* __restrict__ dy,
                                     float* __restrict__ gout) {
   const int C = c4n * 4;
@@ -184,10 +206,19 @@ __global__ void bn_bwd_apply_kernel(const float* __restrict__ y, long long P, in
     const long long p = i / c4n;
     const f32x4 v = *reinterpret_cast<const f32x4*>(y + i * 4);
     const f32x4 gd = *reinterpret_cast<const f32x4*>(da + p * dacs + q * 4);
-    f32x4 av = {0, 0, 0, 0};
-    if (act != ACT_NONE) av = *reinterpret_cast<const f32x4*>(a + p * acs + q * 4);
     const f32x4 mu = *reinterpret_cast<const f32x4*>(mean + q * 4);
     const f32x4 rs = *reinterpret_cast<const f32x4*>(rstd + q * 4);
+    f32x4 av = {0, 0, 0, 0};
+    if (act != ACT_NONE) {
+      if (a) {
+        av = *reinterpret_cast<const f32x4*>(a + p * acs + q * 4);
+      } else {
+        const f32x4 gm = *reinterpret_cast<const f32x4*>(gam + q * 4);
+        const f32x4 bt = *reinterpret_cast<const f32x4*>(bet + q * 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) av[j] = act_fwd(act, bn_z(gm[j], v[j], mu[j], rs[j], bt[j]));
+      }
+    }
     const f32x4 c0 = *reinterpret_cast<const f32x4*>(coef + q * 4);
     const f32x4 c1 = *reinterpret_cast<const f32x4*>(coef + C + q * 4);
     const f32x4 c2 = *reinterpret_cast<const f32x4*>(coef + 2 * C + q * 4);

@@ -1,0 +1,3 @@
+set -e
+timeout -k 10 300 python -u -m pytest tests/test_bb_train.py tests/test_desc_grad.py -m gpu -x -q --timeout 240 --timeout-method thread > gpurun_out/bn_tests.log 2>&1
+timeout -k 10 300 python bench.py --workload train_desc --steps 10 --warmup 3 > gpurun_out/bench_desc.json 2> gpurun_out/bench_desc.err
