@@ -158,6 +158,7 @@ struct posfeat_bbtrain {
   // Winograd F(2x2,3x3) for the decoder's 3x3 convs, forward and input
   // gradient (wino.hip; POSFEAT_WINO=0: direct conv)
   bool wino = true;
+  bool s2phase = true;  // stride-2 input gradients by output phases (POSFEAT_S2PHASE=0: zero insertion)
   Buf wu, wino_ws;
   // optional per-launch timing (labels "fwd:conv", "bwd:wgrad", ...)
   bool timing = false;
@@ -350,12 +351,12 @@ void plan(posfeat_bbtrain* m) {
   alloc(m->gd, fl(MAXG));
   alloc(m->gres, fl(MAXG));
   alloc(m->dy, fl(MAXG));
-  alloc(m->dz, fl(2 * MAXG));
+
   alloc(m->dcat2, fl(B * h4 * w4 * 512));
   alloc(m->dcat3, fl(B * h8 * w8 * 1024));
   alloc(m->dup, fl(std::max(B * h4 * w4 * 512, B * h8 * w8 * 1024)));
   alloc(m->upt, fl(std::max(B * h4 * w8 * 512, B * h8 * w16 * 1024)));
-  size_t wt = 0, wg = 0, sk = 0;
+  size_t wt = 0, wg = 0, sk = 0, dzf = 0;
   for (size_t li = 0; li < T.v.size(); ++li) {
     const TLayer& L = T.v[li];
     const int cinp = (L.cin + 3) / 4 * 4;
@@ -366,17 +367,30 @@ void plan(posfeat_bbtrain* m) {
     sk = std::max(sk, posfeat_conv2d_workspace(&d));
     if ((int)li != T.first) {
       wt = std::max(wt, (size_t)L.cin * posfeat_conv_packed_k(L.cout, L.k, L.k));
+      if (L.stride == 2 && L.k == 3) {
+        wt = std::max(wt, (size_t)4 * L.cin * posfeat_conv_packed_k(L.cout, 2, 2));
+        posfeat_conv_desc e2 = make_desc((int)B, lih[li] / 2, liw[li] / 2, L.cout, L.cout,
+                                         4 * L.cin, 2, 1, 4 * L.cin, 0);
+        e2.pad = 1;
+        sk = std::max(sk, posfeat_conv2d_workspace(&e2));
+        dzf = std::max(dzf, (size_t)B * (lih[li] / 2 + 1) * (liw[li] / 2 + 1) * 4 * L.cin);
+      }
       posfeat_conv_desc e = make_desc((int)B, lih[li], liw[li], L.cout, L.cout, L.cin, L.k, 1,
                                       L.cin, L.cin);
       sk = std::max(sk, posfeat_conv2d_workspace(&e));
     }
   }
   alloc(m->wt, fl(wt));
+  alloc(m->dz, fl(std::max(dzf, 2 * MAXG)));
   alloc(m->wgws, wg);
   alloc(m->splitk, std::max<size_t>(sk, 256));
   {
     const char* e = getenv("POSFEAT_WINO");
     m->wino = !(e && e[0] == '0');
+  }
+  {
+    const char* e = getenv("POSFEAT_S2PHASE");
+    m->s2phase = !(e && e[0] == '0');
   }
   if (m->wino) {
     size_t uf = 0, wb = 0;
@@ -511,6 +525,39 @@ int layer_bwd(Ctx& c, int li, const float* x, int xcs, int h, int w, const float
   }
   if (!dx) return POSFEAT_OK;
   float* wt = c.s(m->wt);
+  if (L.stride == 2 && m->s2phase) {
+    // output-phase input gradient (bbtrain_kernels.h): 1x1 -> compact GEMM,
+    // 3x3 -> one 2x2 pad-1 conv with 4 Cin phase channels; then one scatter
+    if ((h & 1) || (w & 1) || L.cin % 32 || C % 32 || (L.k != 1 && L.k != 3))
+      return POSFEAT_E_UNSUPPORTED;
+    const int oh2 = h / 2, ow2 = w / 2;
+    float* dz = c.s(m->dz);
+    const bool k3 = L.k == 3;
+    PF_TRY(timed(c, "bwd:misc", 0, [&] {
+      if (!k3) return pf_dgrad_weights(c.prm + L.w_off, C, L.cin, 1, 1, wt, c.st);
+      hipLaunchKernelGGL(s2_phase_weights_kernel,
+                         dim3(grid_for(16LL * L.cin * C, 256)), dim3(256), 0, c.st,
+                         c.prm + L.w_off, C, L.cin, wt);
+      PF_CHECK_LAUNCH();
+      return (int)POSFEAT_OK;
+    }));
+    posfeat_conv_desc d = make_desc(B, oh2, ow2, C, C, k3 ? 4 * L.cin : L.cin, k3 ? 2 : 1, 1,
+                                    k3 ? 4 * L.cin : L.cin, 0);
+    d.pad = k3 ? 1 : 0;
+    const double pf = k3 ? 2.0 * B * (oh2 + 1) * (ow2 + 1) * 4 * C * 4 * L.cin
+                         : 2.0 * B * oh2 * ow2 * C * L.cin;
+    PF_TRY(timed(c, "bwd:dgrad", pf, [&] {
+      return pf_conv_run_tile(&d, dy, wt, nullptr, nullptr, dz, c.s(m->splitk), m->splitk.bytes,
+                              -1, c.st);
+    }));
+    return timed(c, "bwd:misc", 0, [&] {
+      hipLaunchKernelGGL(s2_scatter_kernel, dim3(grid_for((long long)B * h * w * (L.cin / 4), 256)),
+                         dim3(256), 0, c.st, dz, k3 ? 1 : 0, B, h, w, L.cin / 4, add, addcs, dx,
+                         dxcs);
+      PF_CHECK_LAUNCH();
+      return (int)POSFEAT_OK;
+    });
+  }
   const float* src = dy;
   PF_TRY(timed(c, "bwd:misc", 0, [&] {
     PF_TRY(pf_dgrad_weights(c.prm + L.w_off, C, L.cin, L.k, L.k, wt, c.st));

@@ -234,6 +234,65 @@ __global__ void bn_bwd_apply_kernel(const float* __restrict__ y, long long P, in
   }
 }
 
+// Input gradient of a 3x3 stride-2 pad-1 conv by output phases.  dx row iy
+// reads dy rows oy with 2 oy - 1 + ky = iy, so the dx row pair (2t-1, 2t)
+// depends on dy rows {t-1, t} only: one 2x2 pad-1 conv over dy with 4·Cin
+// output channels (phase pe_y·2 + pe_x, pe = 1 for the even row/column of the
+// pair) computes all four phases with 16/9 of the exact MACs (zero insertion:
+// 4x).  Tap (r, c) of phase (pe_y, pe_x) is the forward tap (kmap(pe_y, r),
+// kmap(pe_x, c)), kmap = {(0,0): 2, (0,1): 0, (1,0): none, (1,1): 1}.
+// wp [4 Cin][((c/32)*4 + tap)*32 + c%32] from the forward's packed
+// w [C][((ci/32)*9 + tap)*32 + ci%32]; Cin, C % 32 == 0.
+__device__ __forceinline__ int s2_kmap(int pe, int r) { return pe ? (r ? 1 : -1) : (r ? 0 : 2); }
+
+__global__ void s2_phase_weights_kernel(const float* __restrict__ w, int C, int Cin,
+                                        float* __restrict__ wp) {
+  const int kp4 = C * 4, kp9 = C * 9;
+  const long long total = 4LL * Cin * kp4;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int o = (int)(i / kp4), k = (int)(i - (long long)o * kp4);
+    const int ph = o / Cin, ci = o - ph * Cin;
+    const int tap = (k >> 5) & 3, c = (k >> 7) * 32 + (k & 31);
+    const int ky = s2_kmap(ph >> 1, tap >> 1), kx = s2_kmap(ph & 1, tap & 1);
+    wp[i] = (ky >= 0 && kx >= 0)
+                ? w[(long long)c * kp9 + ((ci >> 5) * 9 + ky * 3 + kx) * 32 + (ci & 31)]
+                : 0.f;
+  }
+}
+
+// dx [n][h][w] (pitch dxcs) = the stride-2 input gradient from
+//   mode 1: the phase conv's output src [n][h/2+1][w/2+1][4 Cin]
+//   mode 0: a 1x1 conv's compact output src [n][h/2][w/2][Cin] (even pixels; 0 elsewhere)
+// plus add (pitch addcs) when given
+__global__ void s2_scatter_kernel(const float* __restrict__ src, int mode, int n, int h, int w,
+                                  int c4n, const float* __restrict__ add, int addcs,
+                                  float* __restrict__ dx, int dxcs) {
+  const int Cin = c4n * 4, oh = h / 2, ow = w / 2;
+  const long long total = (long long)n * h * w * c4n;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int q = (int)(i % c4n);
+    const long long p = i / c4n;
+    const int ix = (int)(p % w);
+    const long long r = p / w;
+    const int iy = (int)(r % h);
+    const int b = (int)(r / h);
+    f32x4 v = {0, 0, 0, 0};
+    if (mode == 1) {
+      const int t = (iy + 1) >> 1, s = (ix + 1) >> 1;
+      const int ph = (1 - (iy & 1)) * 2 + (1 - (ix & 1));
+      v = *reinterpret_cast<const f32x4*>(
+          src + (((long long)b * (oh + 1) + t) * (ow + 1) + s) * 4 * Cin + ph * Cin + q * 4);
+    } else if (!(iy & 1) && !(ix & 1)) {
+      v = *reinterpret_cast<const f32x4*>(
+          src + (((long long)b * oh + (iy >> 1)) * ow + (ix >> 1)) * Cin + q * 4);
+    }
+    if (add) v += *reinterpret_cast<const f32x4*>(add + p * addcs + q * 4);
+    *reinterpret_cast<f32x4*>(dx + p * dxcs + q * 4) = v;
+  }
+}
+
 // dst [n][h][w][C] = src [n][h/2][w/2][C] at even (y, x), 0 elsewhere: the
 // input grid of a stride-2 conv (its output pixel i reads input 2i - pad + k)
 __global__ void zero_insert_kernel(const float* __restrict__ src, int n, int h, int w, int c4n,
