@@ -30,9 +30,14 @@ NUM_PTS, NMS_R, THR = 2048, 1, 0.9
 # Conv work per 480x640 image: 2 x 208.99 GMAC
 CONV_FLOP_PER_IMAGE = 417.98e9
 HEAD_CONV2_FLOP_PER_IMAGE = 2.0 * 480 * 640 * 128 * 256 * 9   # reference layer
-# dominant kernel: conv_up4_kernel, the 192 x4-upsampled channels of head.conv2
-# by bilinear phases on the low-res map (6.25 taps on average)
-UP4_FLOP_PER_IMAGE = 2.0 * 480 * 640 * 128 * 192 * 6.25
+# dominant kernel: the 192 x4-upsampled channels of head.conv2.  Default: the
+# 36 transform-domain GEMMs of the low-res Winograd F(4x4) form (DESIGN.md
+# §4.1a''), 2 x 36 x (120/4 x 160/4 tiles) x 2048 phase channels x 192 per
+# image; POSFEAT_UP4WINO=0: conv_up4_kernel by bilinear phases (6.25 taps on
+# average, §4.1).  The executed FLOPs come from the engine's timing label.
+UP4_WINO = os.environ.get("POSFEAT_UP4WINO", "1") != "0"
+UP4_FLOP_PER_IMAGE = (2.0 * 36 * 30 * 40 * 2048 * 192 if UP4_WINO
+                      else 2.0 * 480 * 640 * 128 * 192 * 6.25)
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md, dense FP32 matrix (spec)
 
 
@@ -157,7 +162,7 @@ def main():
     images = world * args.steps * args.batch
     value = images / el
 
-    # ---- roofline of the dominant kernel (conv_up4_kernel), HIP events on the
+    # ---- roofline of the dominant kernel (see UP4_FLOP_PER_IMAGE), HIP events on the
     # engine's stream around each launch, averaged over a few extra steps
     engine.set_timing(args.batch, H, W, True)
     k_ms, c2_ms, conv_ms, conv_fl, all_ms = [], [], [], [], []
@@ -178,7 +183,7 @@ def main():
     conv_total = float(np.mean(conv_ms))
     conv_ach = float(np.mean(conv_fl)) / (conv_total * 1e-3) / 1e12
     traffic = None
-    tfile = os.path.join(ROOT, "profiles", "up4_traffic.json")
+    tfile = os.path.join(ROOT, "profiles", "up4w_traffic.json" if UP4_WINO else "up4_traffic.json")
     if os.path.exists(tfile):
         try:
             traffic = json.load(open(tfile)).get("bytes_per_launch_per_image")
@@ -206,8 +211,11 @@ def main():
                                    "2048) + sample_feat_by_coord",
                        "global_batch": args.batch * world, "image": [H, W],
                        "num_pts": NUM_PTS, "parallelism": "dp%d (image-sharded)" % world},
-            "roofline": {"kernel": "conv_up4_kernel<8> (head.conv2: 192 x4-upsampled channels "
-                                   "by bilinear phases on the 120x160 map, 8x16 patches)",
+            "roofline": {"kernel": ("conv_glds_kernel<128,128,2,2> x36 batched (head.conv2's 192 "
+                                    "x4-upsampled channels: Winograd F(4x4) GEMMs on the 120x160 "
+                                    "map, 2048 phase channels)") if UP4_WINO else
+                                   ("conv_up4_kernel<8> (head.conv2: 192 x4-upsampled channels "
+                                    "by bilinear phases on the 120x160 map, 8x16 patches)"),
                          "bound": "mfma", "achieved": round(achieved, 3),
                          "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4),

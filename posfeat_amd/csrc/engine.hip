@@ -116,6 +116,9 @@ struct posfeat_model {
   Buf wino_u, wino_ws;
   // head.conv2's G part as a per-image 5x5 conv of the image (gfuse.hip)
   bool gfuse = true;
+  // head.conv2's upsampled part as a low-res Winograd F(4x4) conv (wino.hip)
+  bool up4wino = true;
+  Buf u4u, u4ws;
   Buf gf_w, gf_b;
   size_t splitk_need = 0;
   // per-layer conv tile chosen by timing the legal candidates on the first
@@ -383,6 +386,8 @@ void plan(posfeat_model* m) {
     m->wino = !(wv && wv[0] == '0');
     const char* gv = getenv("POSFEAT_GFUSE");  // 0: conv2's G part as the 64-ch 3x3 conv
     m->gfuse = !(gv && gv[0] == '0');
+    const char* uv = getenv("POSFEAT_UP4WINO");  // 0: conv_up4_kernel (bilinear phases)
+    m->up4wino = !(uv && uv[0] == '0') && H % 16 == 0 && W % 16 == 0;
   }
   if (m->up4 && m->gfuse) {
     alloc(m->gf_w, B * 128 * 128);
@@ -405,6 +410,10 @@ void plan(posfeat_model* m) {
     alloc(m->g64, B * H * W * 64);
     alloc(m->wph, posfeat_conv2_up4_weights_floats());
     alloc(m->up4ws, posfeat_conv2_up4_workspace((int)B, (int)H, (int)W) / 4 + 4);
+    if (m->up4wino) {
+      alloc(m->u4u, pf_up4_wino_weights_floats());
+      alloc(m->u4ws, pf_up4_wino_ws_bytes((int)B, (int)H, (int)W) / 4 + 4);
+    }
   } else {
     alloc(m->hcat, B * H * W * 256);
   }
@@ -583,10 +592,29 @@ int forward(Ctx& c, const float* img, posfeat_extract_out* out) {
     PF_TRY(timed(c, "head.conv2.border", 0, [&] {
       return pf_up4_border(B, H, W, c1, 192, wph, c2, 128, c.st);
     }));
-    PF_TRY(timed(c, "conv:head.conv2.up4", 2.0 * B * H * W * 128.0 * 192 * 6.25, [&] {
-      return pf_up4_main(B, H, W, c1, 192, wph, c2, 128, c.f(m->up4ws),
-                         m->up4ws.floats * sizeof(float), mean, rstd, 1e-5f, c.st);
-    }));
+    if (m->up4wino) {
+      // executed: 36 transform-domain MACs per 4x4 low-res tile, 2048 phase
+      // channels x 192 (vs 6.25 taps per full-res pixel for the phase kernel)
+      PF_TRY(timed(c, "head.conv2.up4w", 0, [&] {
+        return pf_up4_wino_weights(wph, c.f(m->u4u), c.st);
+      }));
+      auto up4w = [&](int stages) {
+        return pf_up4_wino(B, H, W, c1, 192, c.f(m->u4u), c2, 128, c.f(m->u4ws),
+                           m->u4ws.floats * sizeof(float), c.st, stages);
+      };
+      PF_TRY(timed(c, "head.conv2.up4.vt", 0, [&] { return up4w(1); }));
+      PF_TRY(timed(c, "conv:head.conv2.up4", 2.0 * 36 * B * (H / 16) * (W / 16) * 2048.0 * 192,
+                   [&] { return up4w(2); }));
+      PF_TRY(timed(c, "head.conv2.up4.ot", 0, [&] { return up4w(4); }));
+      PF_TRY(timed(c, "instnorm", 0, [&] {
+        return pf_in_stats(c2, B, H * W, 128, 128, mean, rstd, c.d(m->st_part), c.st);
+      }));
+    } else {
+      PF_TRY(timed(c, "conv:head.conv2.up4", 2.0 * B * H * W * 128.0 * 192 * 6.25, [&] {
+        return pf_up4_main(B, H, W, c1, 192, wph, c2, 128, c.f(m->up4ws),
+                           m->up4ws.floats * sizeof(float), mean, rstd, 1e-5f, c.st);
+      }));
+    }
   } else {
     float* hcat = c.f(m->hcat);
     PF_TRY(timed(c, "norm_prelu_up4", 0, [&] {

@@ -68,3 +68,8 @@ size_t pf_wino_wgrad_ws_bytes(int n, int h, int w, int Cin, int Cout);
 int pf_wino_wgrad(const float* dy, int ldy, const float* x, int xcs, int n, int h, int w, int Cin,
                   int Cout, float* dw, float* db, int acc, void* ws, size_t ws_bytes,
                   hipStream_t st);
+size_t pf_up4_wino_weights_floats();
+size_t pf_up4_wino_ws_bytes(int n, int H, int W);
+int pf_up4_wino_weights(const float* wph, float* U, hipStream_t st);
+int pf_up4_wino(int n, int H, int W, const float* L, int lcs, const float* U, float* y, int ycs,
+                void* ws, size_t ws_bytes, hipStream_t st, int stages = 7);

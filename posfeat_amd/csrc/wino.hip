@@ -203,7 +203,7 @@ __global__ void wino4_weights_kernel(const float* __restrict__ wpk, int Cout, in
 // V[xi][tile][c], 6x6 patch at rows 4ty-1.., cols 4tx-1..
 __global__ __launch_bounds__(256) void wino4_input_kernel(const float* __restrict__ x, int xcs,
                                                           int n, int h, int w, int c4n,
-                                                          float* __restrict__ V) {
+                                                          float* __restrict__ V, int clamp = 0) {
   const int th = h / 4, tw = w / 4;
   const long long T = (long long)n * th * tw;
   const long long total = T * c4n;
@@ -223,11 +223,13 @@ __global__ __launch_bounds__(256) void wino4_input_kernel(const float* __restric
       for (int c = 0; c < 6; ++c) t[a][c] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int r = 0; r < 6; ++r) {
-      const int yy = 4 * ty - 1 + r;
+      int yy = 4 * ty - 1 + r;
+      if (clamp) yy = min(max(yy, 0), h - 1);  // replicate extension (conv_up4's L halo)
       f32x4 d[6];
 #pragma unroll
       for (int c = 0; c < 6; ++c) {
-        const int xx = 4 * tx - 1 + c;
+        int xx = 4 * tx - 1 + c;
+        if (clamp) xx = min(max(xx, 0), w - 1);
         f32x4 v = {0.f, 0.f, 0.f, 0.f};
         if ((unsigned)yy < (unsigned)h && (unsigned)xx < (unsigned)w)
           v = *reinterpret_cast<const f32x4*>(x + (((long long)b * h + yy) * w + xx) * xcs + q * 4);
@@ -413,6 +415,144 @@ __global__ void wino4_wgrad_out_kernel(const float* __restrict__ part, int nspli
   }
 }
 
+// ---------------------------------------------------------------- head.conv2 L part
+// conv_up4_kernel's per-phase low-res convs (conv.hip: phase (ry, rx) applies
+// |E(ry)| x |E(rx)| combined taps, E = {-1,0} / {-1,0,1} / {0,1}, to the
+// replicate-extended L) are one 3x3 conv of L with 16 x 128 = 2048 output
+// channels whose missing taps are zero.  That conv is a Winograd F(4x4,3x3)
+// on the LOW-RES grid: 36 MACs per 16 low-res positions and output channel
+// instead of 6.25 per position on average -- 2.78x fewer than the phase
+// kernel.  The output transform scatters each (position, phase) to its
+// full-res pixel (4 qy + ry, 4 qx + rx) and adds it to y, which already holds
+// the G part + bias - the zero-padding border terms (pf_up4_border).
+constexpr int UW_CU = 192, UW_COUT = 128, UW_NO = 16 * UW_COUT;
+constexpr int UW_KP = (UW_CU / 32) * 9 * 32;  // conv.hip UP4_KP: per-phase packed K
+
+__global__ void up4_wino_weights_kernel(const float* __restrict__ wph, float* __restrict__ U) {
+  const long long n = (long long)UW_NO * UW_CU;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int o = (int)(i / UW_CU), ci = (int)(i - (long long)o * UW_CU);
+    const int phase = o / UW_COUT, ry = phase >> 2, rx = phase & 3;
+    const int ney = (ry == 0 || ry == 3) ? 2 : 3, nex = (rx == 0 || rx == 3) ? 2 : 3;
+    const int ey0 = ry == 3 ? 0 : -1, ex0 = rx == 3 ? 0 : -1;
+    const int T = ney * nex, slab = ci >> 5;
+    const float* w = wph + (long long)o * UW_KP + (ci & 31);
+    float g[3][3] = {{0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}, {0.f, 0.f, 0.f}};
+    for (int tj = 0; tj < T; ++tj)
+      g[ey0 + tj / nex + 1][ex0 + tj % nex + 1] = w[(slab * T + tj) * 32];
+    float r[6][3];
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        r[a][c] = W4_G[a][0] * g[0][c] + W4_G[a][1] * g[1][c] + W4_G[a][2] * g[2][c];
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+#pragma unroll
+      for (int b = 0; b < 6; ++b)
+        U[((long long)(a * 6 + b) * UW_NO + o) * UW_CU + ci] =
+            r[a][0] * W4_G[b][0] + r[a][1] * W4_G[b][1] + r[a][2] * W4_G[b][2];
+  }
+}
+
+// y[(b, 4 qy + ry, 4 qx + rx)][co] += (A^T M A)[qy, qx] for o = phase * 128 + co
+__global__ __launch_bounds__(256) void up4_wino_output_kernel(const float* __restrict__ M, int n,
+                                                              int lh, int lw,
+                                                              float* __restrict__ y, int ycs) {
+  const int th = lh / 4, tw = lw / 4, H = 4 * lh, W = 4 * lw;
+  constexpr int c4n = UW_NO / 4;
+  const long long T = (long long)n * th * tw;
+  const long long total = T * c4n;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int q = (int)(i % c4n);
+    const long long tile = i / c4n;
+    const int tx = (int)(tile % tw);
+    const long long r0 = tile / tw;
+    const int ty = (int)(r0 % th);
+    const int b = (int)(r0 / th);
+    const int phase = (q * 4) / UW_COUT, co = q * 4 - phase * UW_COUT;
+    const int ry = phase >> 2, rx = phase & 3;
+    const float* mi = M + tile * UW_NO + q * 4;
+    const long long xs = T * UW_NO;
+    f32x4 s[4][6];  // A^T M
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int c = 0; c < 6; ++c) s[a][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      f32x4 m[6];
+#pragma unroll
+      for (int c = 0; c < 6; ++c) m[c] = *reinterpret_cast<const f32x4*>(mi + (r * 6 + c) * xs);
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+        if (W4_AT[a][r] != 0.f)
+#pragma unroll
+          for (int c = 0; c < 6; ++c) s[a][c] += W4_AT[a][r] * m[c];
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int bb = 0; bb < 4; ++bb) {
+        f32x4 o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < 6; ++c)
+          if (W4_AT[bb][c] != 0.f) o += W4_AT[bb][c] * s[a][c];
+        const int Y = 4 * (4 * ty + a) + ry, X = 4 * (4 * tx + bb) + rx;
+        f32x4* dst = reinterpret_cast<f32x4*>(y + (((long long)b * H + Y) * W + X) * ycs + co);
+        *dst = *dst + o;
+      }
+  }
+}
+
+}  // namespace
+
+size_t pf_up4_wino_weights_floats() { return (size_t)36 * UW_NO * UW_CU; }
+
+size_t pf_up4_wino_ws_bytes(int n, int H, int W) {
+  const long long T = (long long)n * (H / 16) * (W / 16);
+  return pf_align(36 * T * UW_CU * 4, 256) + pf_align(36 * T * UW_NO * 4, 256);
+}
+
+int pf_up4_wino_weights(const float* wph, float* U, hipStream_t st) {
+  hipLaunchKernelGGL(up4_wino_weights_kernel, dim3(grid_for((long long)UW_NO * UW_CU, 256)),
+                     dim3(256), 0, st, wph, U);
+  PF_CHECK_LAUNCH();
+  return POSFEAT_OK;
+}
+
+// y (n x H x W x 128, pitch ycs) += the 192 upsampled channels' part of
+// head.conv2 from L (n x H/4 x W/4 x 192, pitch lcs); H/4, W/4 % 4 == 0
+// stages: bit 0 input transform, bit 1 the 36 GEMMs, bit 2 output transform
+// (the engine times them separately)
+int pf_up4_wino(int n, int H, int W, const float* L, int lcs, const float* U, float* y, int ycs,
+                void* ws, size_t ws_bytes, hipStream_t st, int stages) {
+  const int lh = H / 4, lw = W / 4;
+  if (H % 16 || W % 16 || lcs % 4 || ycs % 4) return POSFEAT_E_INVALID;
+  if (!ws || ws_bytes < pf_up4_wino_ws_bytes(n, H, W)) return POSFEAT_E_WORKSPACE;
+  const long long T = (long long)n * (lh / 4) * (lw / 4);
+  float* V = static_cast<float*>(ws);
+  float* M = reinterpret_cast<float*>(static_cast<char*>(ws) + pf_align(36 * T * UW_CU * 4, 256));
+  if (stages & 1) {
+    hipLaunchKernelGGL(wino4_input_kernel, dim3(grid_for(T * (UW_CU / 4), 256)), dim3(256), 0, st,
+                       L, lcs, n, lh, lw, UW_CU / 4, V, 1);
+    PF_CHECK_LAUNCH();
+  }
+  if (stages & 2)
+    PF_TRY(pf_gemm_batched(V, UW_CU, T * UW_CU, U, (long long)UW_NO * UW_CU, M, UW_NO, T * UW_NO,
+                           36, (int)T, UW_NO, UW_CU, st));
+  if (stages & 4) {
+    hipLaunchKernelGGL(up4_wino_output_kernel, dim3(grid_for(T * (UW_NO / 4), 256)), dim3(256), 0,
+                       st, M, n, lh, lw, y, ycs);
+    PF_CHECK_LAUNCH();
+  }
+  return POSFEAT_OK;
+}
+
+namespace {
+
 // F(4x4) when both dims are multiples of 4 (all decoder layers at 480x640)
 // unless POSFEAT_WINO=1 (F(2x2) only)
 bool use_f4(int h, int w) {
@@ -465,7 +605,7 @@ static int wino_conv_impl(const float* x, int xcs, int n, int h, int w, int Cin,
     float* M4 =
         reinterpret_cast<float*>(static_cast<char*>(ws) + pf_align(36 * T4 * Cin * 4, 256));
     hipLaunchKernelGGL(wino4_input_kernel, dim3(grid_for(T4 * (Cin / 4), 256)), dim3(256), 0, st,
-                       x, xcs, n, h, w, Cin / 4, V4);
+                       x, xcs, n, h, w, Cin / 4, V4, 0);
     PF_CHECK_LAUNCH();
     PF_TRY(pf_gemm_batched(V4, Cin, T4 * Cin, U, (long long)Cout * Cin, M4, Cout, T4 * Cout, 36,
                            (int)T4, Cout, Cin, st));
@@ -534,7 +674,7 @@ int pf_wino_wgrad(const float* dy, int ldy, const float* x, int xcs, int n, int 
   p += pf_align((size_t)36 * ns * Cout * Cin * 4, 256);
   float* partb = reinterpret_cast<float*>(p);
   hipLaunchKernelGGL(wino4_input_kernel, dim3(grid_for(T * (Cin / 4), 256)), dim3(256), 0, st, x,
-                     xcs, n, h, w, Cin / 4, V);
+                     xcs, n, h, w, Cin / 4, V, 0);
   hipLaunchKernelGGL(wino4_dy_kernel, dim3(grid_for(T * (Cout / 4), 256)), dim3(256), 0, st, dy,
                      ldy, n, h, w, Cout / 4, dM);
   PF_CHECK_LAUNCH();

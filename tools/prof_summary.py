@@ -1,6 +1,6 @@
 """Summarise a rocprofv3 kernel trace: per-kernel (name, grid) groups, so the
-dominant kernel (head.conv2: conv_halo_kernel<8,128,...> with 2400*8 blocks at
-B=8) can be read separately from the other convs of the same template.
+dominant kernel can be read separately from the other convs of the same
+template (batched launches show as "<blocks>x<grid_y>").
 
 usage: python tools/prof_summary.py <kernel_trace.csv | results.db> [top] [--stats out.csv]
 Accepts rocprofv3's CSV kernel trace or its SQLite output (`kernels` view);
@@ -18,8 +18,10 @@ def load(path):
     out = []
     if path.endswith(".db"):
         c = sqlite3.connect(path)
-        for name, gx, wx, dur in c.execute("select name, grid_x, workgroup_x, duration from kernels"):
-            out.append((name, int(gx) // max(1, int(wx)), int(wx), int(dur)))
+        for name, gx, gy, wx, dur in c.execute(
+                "select name, grid_x, grid_y, workgroup_x, duration from kernels"):
+            b = int(gx) // max(1, int(wx))
+            out.append((name, b if int(gy) <= 1 else "%dx%d" % (b, int(gy)), int(wx), int(dur)))
         return out
     for r in csv.DictReader(open(path)):
         out.append((r["Kernel_Name"], int(r["Grid_Size_X"]) // max(1, int(r["Workgroup_Size_X"])),
@@ -43,7 +45,7 @@ def main():
     tot = sum(sum(v) for v in g.values())
     print("%-72s %8s %5s %6s %12s %7s" % ("kernel", "blocks", "wg", "calls", "avg_us", "pct"))
     for (name, blocks, wg), v in sorted(g.items(), key=lambda kv: -sum(kv[1]))[:top]:
-        print("%-72s %8d %5d %6d %12.1f %6.2f%%" % (name, blocks, wg, len(v), sum(v) / len(v) / 1e3,
+        print("%-72s %8s %5d %6d %12.1f %6.2f%%" % (name, blocks, wg, len(v), sum(v) / len(v) / 1e3,
                                                   100.0 * sum(v) / tot))
     if "--stats" in sys.argv:
         out = sys.argv[sys.argv.index("--stats") + 1]

@@ -5,6 +5,7 @@ Averaged over the dispatches of the kernel whose name contains <kernel>
 (B images per launch); writes {"bytes_per_launch_per_image": ...} for bench.py.
 
 usage: python tools/traffic_json.py <pmc_dir> <out.json> [batch] [kernel] [algorithmic_bytes]
+       [column=value ...]   (extra dispatch filters, e.g. Grid_Size=11059200)
 """
 import collections
 import csv
@@ -13,15 +14,23 @@ import os
 import sys
 
 
+FILTERS = {}
+
+
 def per_dispatch(path, counter, kernel):
     vals = collections.defaultdict(float)
     for r in csv.DictReader(open(path)):
+        if any(r.get(k) != v for k, v in FILTERS.items()):
+            continue
         if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
             vals[r["Dispatch_Id"]] += float(r["Counter_Value"])
     return list(vals.values())
 
 
 def main():
+    for a in sys.argv[6:]:
+        k, v = a.split("=", 1)
+        FILTERS[k] = v
     d, out = sys.argv[1], sys.argv[2]
     batch = int(sys.argv[3]) if len(sys.argv) > 3 else 8
     kernel = sys.argv[4] if len(sys.argv) > 4 else "conv_up4_kernel"
@@ -34,7 +43,8 @@ def main():
     # phase weights (16 x 128 x 1728)
     alg = float(sys.argv[5]) if len(sys.argv) > 5 else (
         batch * (120 * 160 * 192 + 2 * 480 * 640 * 128) * 4 + 16 * 128 * 1728 * 4)
-    rec = {"kernel": kernel, "probe": "tools/up4_probe.py (B=%d, 480x640)" % batch,
+    rec = {"kernel": kernel, "filters": FILTERS,
+           "probe": os.environ.get("PROBE", "tools/up4_probe.py") + " (B=%d, 480x640)" % batch,
            "batch": batch, "fetch_kb_raw": f_kb, "write_kb": w_kb,
            "bytes_per_launch": total, "bytes_per_launch_per_image": total / batch,
            "algorithmic_bytes_per_launch": alg, "ratio_to_algorithmic": total / alg,
