@@ -121,6 +121,14 @@ struct posfeat_model {
   Buf u4u, u4ws;
   Buf gf_w, gf_b;
   size_t splitk_need = 0;
+  // the image branch of KeypointDet (convimg + its IN statistics + the folded
+  // G part of head.conv2 + head.conv2's weight transforms) depends on the
+  // image only: it runs on a second stream, overlapping the ResUNet, and
+  // joins before head.conv2's border/upsampled part (POSFEAT_SIDE=0: serial)
+  bool side = true;
+  hipStream_t side_st = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  Buf splitk2;  // the side stream's own split-K / statistics scratch
   // per-layer conv tile chosen by timing the legal candidates on the first
   // forward of this shape (results do not depend on the tile)
   std::map<std::string, int> tuned;
@@ -143,6 +151,7 @@ struct Ctx {
   char* ws;
   hipStream_t st;
   bool dry = false;  // planning pass: record scratch needs, launch nothing
+  bool side = false;  // running on the model's side stream (own scratch)
   float* f(const Buf& b) const { return reinterpret_cast<float*>(ws + b.off); }
   double* d(const Buf& b) const { return reinterpret_cast<double*>(ws + b.off); }
   const float* W(const std::string& n) const { return m->wts + specs().find(n)->w_off; }
@@ -235,8 +244,9 @@ int conv(Ctx& c, const std::string& name, const float* x, int n, int h, int w, i
     if (need > c.m->splitk_need) c.m->splitk_need = need;
     return POSFEAT_OK;
   }
-  float* part = c.f(c.m->splitk);
-  const size_t have = c.m->splitk.floats * sizeof(float);
+  const Buf& sk = c.side ? c.m->splitk2 : c.m->splitk;
+  float* part = c.f(sk);
+  const size_t have = sk.floats * sizeof(float);
   auto run = [&](int tile) {
     return pf_conv_run_tile(&d, x, c.W(name), c.Bi(name), res, y, part, have, tile, c.st);
   };
@@ -316,12 +326,14 @@ int conv_in(Ctx& c, const std::string& name, const float* x, int n, int h, int w
     }
     PF_TRY(conv(c, name, x, n, h, w, xcs, y, ycs, 1, POSFEAT_ACT_NONE));
     return timed(c, "instnorm", 0, [&] {
-      return pf_in_stats(y, n, h * w, s->cout, ycs, mean, rstd, c.d(c.m->st_part), c.st);
+      return pf_in_stats(y, n, h * w, s->cout, ycs, mean, rstd,
+                         c.side ? c.d(c.m->splitk2) : c.d(c.m->st_part), c.st);
     });
   }
   const double flops = 2.0 * n * h * w * (double)s->cout * s->cin * s->kh * s->kw;
-  float* part = c.f(c.m->splitk);
-  const size_t have = c.m->splitk.floats * sizeof(float);
+  const Buf& sk = c.side ? c.m->splitk2 : c.m->splitk;
+  float* part = c.f(sk);
+  const size_t have = sk.floats * sizeof(float);
   // No autotuning here: the fused statistics are per-tile partial sums, so a
   // different tile would change mean/rstd in the last bits and make results
   // depend on a timing race.  The default plan is the tuned winner for these
@@ -455,6 +467,11 @@ void plan(posfeat_model* m) {
     m->splitk_need = std::max(m->splitk_need, posfeat_conv2d_workspace(&d));
   }
   alloc(m->splitk, m->splitk_need / 4 + 4);
+  {
+    const char* e = getenv("POSFEAT_SIDE");
+    m->side = !(e && e[0] == '0') && m->up4 && m->gfuse && !m->train;
+  }
+  if (m->side) alloc(m->splitk2, std::max(m->splitk_need, part) / 4 + 4);
   m->ws_bytes = cur;
 }
 
@@ -502,6 +519,52 @@ int run_layer(Ctx& c, int li, const float* in, int n, int h, int w, int ics, flo
   return POSFEAT_OK;
 }
 
+// KeypointDet's image branch on the side stream (see posfeat_model::side):
+// convimg + IN statistics (DeteNet.py:110-111), the folded G part of
+// head.conv2 into y (gfuse.hip), head.conv2's phase and Winograd weights
+int image_branch(Ctx& c, const float* img4) {
+  posfeat_model* m = c.m;
+  const int B = m->B, H = m->H, W = m->W;
+  Ctx s = c;
+  s.side = true;
+  if (!c.dry) {
+    if (!m->side_st) {
+      if (hipStreamCreateWithFlags(&m->side_st, hipStreamNonBlocking) != hipSuccess ||
+          hipEventCreateWithFlags(&m->ev_fork, hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&m->ev_join, hipEventDisableTiming) != hipSuccess)
+        return POSFEAT_E_HIP;
+    }
+    if (hipEventRecord(m->ev_fork, c.st) != hipSuccess ||
+        hipStreamWaitEvent(m->side_st, m->ev_fork, 0) != hipSuccess)
+      return POSFEAT_E_HIP;
+    s.st = m->side_st;
+  }
+  const size_t SL = (size_t)B * 256;
+  float* meanI = c.f(m->st_mean) + SL;
+  float* rstdI = c.f(m->st_rstd) + SL;
+  float* g64 = c.f(m->g64);
+  float* c2 = c.f(m->c2raw);
+  PF_TRY(conv_in(s, "head.convimg", img4, B, H, W, 4, g64, 64, meanI, rstdI));
+  PF_TRY(timed(s, "head.conv2.weights", 0, [&] {
+    return posfeat_conv2_up4_weights(s.W("head.conv2"), s.f(m->wph), s.st);
+  }));
+  PF_TRY(timed(s, "head.conv2.gfuse_w", 0, [&] {
+    return pf_gfuse_weights(s.W("head.conv2"), s.Bi("head.conv2"), s.W("head.convimg"),
+                            s.Bi("head.convimg"), meanI, rstdI, B, s.f(m->gf_w), s.f(m->gf_b),
+                            s.st);
+  }));
+  PF_TRY(timed(s, "conv:head.conv2.g", 2.0 * B * H * W * 128.0 * 4 * 25, [&] {
+    return pf_gfuse_conv(img4, g64, 64, B, H, W, s.f(m->gf_w), s.f(m->gf_b), meanI, rstdI,
+                         s.W("head.conv2"), s.Bi("head.conv2"), c2, 128, s.st);
+  }));
+  if (m->up4wino)
+    PF_TRY(timed(s, "head.conv2.up4w", 0, [&] {
+      return pf_up4_wino_weights(s.f(m->wph), s.f(m->u4u), s.st);
+    }));
+  if (!c.dry && hipEventRecord(m->ev_join, s.st) != hipSuccess) return POSFEAT_E_HIP;
+  return POSFEAT_OK;
+}
+
 int forward(Ctx& c, const float* img, posfeat_extract_out* out) {
   posfeat_model* m = c.m;
   const int B = m->B, H = m->H, W = m->W;
@@ -511,6 +574,8 @@ int forward(Ctx& c, const float* img, posfeat_extract_out* out) {
   float* img4 = c.f(m->img4);
   // ---- ResUNet (DescNet.py:64-84) -----------------------------------------
   PF_TRY(timed(c, "layout:img", 0, [&] { return pf_nchw_to_nhwc(img, B, 3, H, W, 4, img4, c.st); }));
+  const bool side = m->side;
+  if (side) PF_TRY(image_branch(c, img4));
   PF_TRY(conv(c, "firstconv", img4, B, H, W, 4, c.f(m->stem), 64, 2, POSFEAT_ACT_RELU));
   float* headcat = c.f(m->headcat);
   PF_TRY(timed(c, "maxpool", 0, [&] {
@@ -561,7 +626,7 @@ int forward(Ctx& c, const float* img, posfeat_extract_out* out) {
       return pf_in_apply(c1, B, h4 * w4, 192, 192, mean1, rstd1, slope, c.st);
     }));
     float* g64 = c.f(m->g64);
-    PF_TRY(conv_in(c, "head.convimg", img4, B, H, W, 4, g64, 64, meanI, rstdI));
+    if (!side) PF_TRY(conv_in(c, "head.convimg", img4, B, H, W, 4, g64, 64, meanI, rstdI));
     if (!m->gfuse)
       PF_TRY(timed(c, "instnorm_apply", 0, [&] {
         return pf_in_apply(g64, B, H * W, 64, 64, meanI, rstdI, nullptr, c.st);
@@ -569,10 +634,14 @@ int forward(Ctx& c, const float* img, posfeat_extract_out* out) {
     // executed MFMA work: 64 full-res channels x 9 taps, 192 low-res channels
     // x 6.25 taps on average over the 16 phases (the reference layer: 256 x 9)
     const float* wph = c.f(m->wph);
-    PF_TRY(timed(c, "head.conv2.weights", 0, [&] {
-      return posfeat_conv2_up4_weights(c.W("head.conv2"), c.f(m->wph), c.st);
-    }));
-    if (m->gfuse) {
+    if (!side)
+      PF_TRY(timed(c, "head.conv2.weights", 0, [&] {
+        return posfeat_conv2_up4_weights(c.W("head.conv2"), c.f(m->wph), c.st);
+      }));
+    if (side) {
+      // join the image branch (it wrote the G part into y)
+      if (!c.dry && hipStreamWaitEvent(c.st, m->ev_join, 0) != hipSuccess) return POSFEAT_E_HIP;
+    } else if (m->gfuse) {
       // G = IN(convimg(img)) folded into a per-image 5x5 conv of the image
       // (+ the exact one-pixel border ring); g64 holds the raw convimg output
       PF_TRY(timed(c, "head.conv2.gfuse_w", 0, [&] {
@@ -595,9 +664,10 @@ int forward(Ctx& c, const float* img, posfeat_extract_out* out) {
     if (m->up4wino) {
       // executed: 36 transform-domain MACs per 4x4 low-res tile, 2048 phase
       // channels x 192 (vs 6.25 taps per full-res pixel for the phase kernel)
-      PF_TRY(timed(c, "head.conv2.up4w", 0, [&] {
-        return pf_up4_wino_weights(wph, c.f(m->u4u), c.st);
-      }));
+      if (!side)
+        PF_TRY(timed(c, "head.conv2.up4w", 0, [&] {
+          return pf_up4_wino_weights(wph, c.f(m->u4u), c.st);
+        }));
       auto up4w = [&](int stages) {
         return pf_up4_wino(B, H, W, c1, 192, c.f(m->u4u), c2, 128, c.f(m->u4ws),
                            m->u4ws.floats * sizeof(float), c.st, stages);
@@ -843,6 +913,9 @@ extern "C" void posfeat_model_destroy(posfeat_model* m) {
     (void)hipEventDestroy(e.a);
     (void)hipEventDestroy(e.b);
   }
+  if (m->ev_fork) (void)hipEventDestroy(m->ev_fork);
+  if (m->ev_join) (void)hipEventDestroy(m->ev_join);
+  if (m->side_st) (void)hipStreamDestroy(m->side_st);
   delete m;
 }
 
