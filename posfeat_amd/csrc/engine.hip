@@ -675,9 +675,10 @@ int forward(Ctx& c, const float* img, posfeat_extract_out* out) {
       PF_TRY(timed(c, "head.conv2.up4.vt", 0, [&] { return up4w(1); }));
       PF_TRY(timed(c, "conv:head.conv2.up4", 2.0 * 36 * B * (H / 16) * (W / 16) * 2048.0 * 192,
                    [&] { return up4w(2); }));
-      PF_TRY(timed(c, "head.conv2.up4.ot", 0, [&] { return up4w(4); }));
-      PF_TRY(timed(c, "instnorm", 0, [&] {
-        return pf_in_stats(c2, B, H * W, 128, 128, mean, rstd, c.d(m->st_part), c.st);
+      // output transform + the instance-norm statistics of the finished conv2 output
+      PF_TRY(timed(c, "head.conv2.up4.ot", 0, [&] {
+        return pf_up4_wino(B, H, W, c1, 192, c.f(m->u4u), c2, 128, c.f(m->u4ws),
+                           m->u4ws.floats * sizeof(float), c.st, 4, mean, rstd);
       }));
     } else {
       PF_TRY(timed(c, "conv:head.conv2.up4", 2.0 * B * H * W * 128.0 * 192 * 6.25, [&] {

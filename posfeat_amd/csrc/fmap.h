@@ -72,4 +72,7 @@ size_t pf_up4_wino_weights_floats();
 size_t pf_up4_wino_ws_bytes(int n, int H, int W);
 int pf_up4_wino_weights(const float* wph, float* U, hipStream_t st);
 int pf_up4_wino(int n, int H, int W, const float* L, int lcs, const float* U, float* y, int ycs,
-                void* ws, size_t ws_bytes, hipStream_t st, int stages = 7);
+                void* ws, size_t ws_bytes, hipStream_t st, int stages = 7, float* mean = nullptr,
+                float* rstd = nullptr);
+int pf_in_finalize(const double* part, int n, int nchunk, int hw, int C, float* mean, float* rstd,
+                   hipStream_t st);

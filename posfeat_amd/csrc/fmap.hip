@@ -187,7 +187,7 @@ __global__ __launch_bounds__(256) void in_finalize_kernel(
   s1 = red[0][0][cl];
   s2 = red[1][0][cl];
   const int i = b * C + c;
-  const double sh = x[(long long)b * hw * cs + c];
+  const double sh = x ? x[(long long)b * hw * cs + c] : 0.0;  // x null: unshifted partials
   const double m1 = s1 / hw;
   double var = s2 / hw - m1 * m1;
   if (var < 0) var = 0;
@@ -442,6 +442,16 @@ int pf_in_stats(const float* x, int n, int hw, int C, int cs, float* mean, float
   }
   PF_CHECK_LAUNCH();
   hipLaunchKernelGGL(in_finalize_kernel, dim3((C + 3) / 4, n), dim3(256), 0, st, x, hw, C, cs,
+                     nchunk, part, 1e-5f, mean, rstd, n);
+  PF_CHECK_LAUNCH();
+  return POSFEAT_OK;
+}
+
+// mean / rstd from unshifted partials part[b][nchunk][C][2] (sum, sum of squares)
+// produced by a fused producer (e.g. wino.hip's head.conv2 output transform)
+int pf_in_finalize(const double* part, int n, int nchunk, int hw, int C, float* mean, float* rstd,
+                   hipStream_t st) {
+  hipLaunchKernelGGL(in_finalize_kernel, dim3((C + 3) / 4, n), dim3(256), 0, st, nullptr, hw, C, 0,
                      nchunk, part, 1e-5f, mean, rstd, n);
   PF_CHECK_LAUNCH();
   return POSFEAT_OK;

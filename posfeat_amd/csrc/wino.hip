@@ -456,16 +456,21 @@ __global__ void up4_wino_weights_kernel(const float* __restrict__ wph, float* __
   }
 }
 
-// y[(b, 4 qy + ry, 4 qx + rx)][co] += (A^T M A)[qy, qx] for o = phase * 128 + co
+// y[(b, 4 qy + ry, 4 qx + rx)][co] += (A^T M A)[qy, qx] for o = phase * 128 + co.
+// One item per thread, exact grid (T * 512 / 256 blocks): a block is one
+// tile x 8 phases x 32 channel quads, so with part != null it also reduces
+// the final y values over its 8 phases (fixed order, LDS) into the instance-
+// norm partials part[b][(tile in image) * 2 + half][co][2] (sum, sum of squares).
 __global__ __launch_bounds__(256) void up4_wino_output_kernel(const float* __restrict__ M, int n,
                                                               int lh, int lw,
-                                                              float* __restrict__ y, int ycs) {
+                                                              float* __restrict__ y, int ycs,
+                                                              double* __restrict__ part) {
+  __shared__ double red[8][32][8];
   const int th = lh / 4, tw = lw / 4, H = 4 * lh, W = 4 * lw;
   constexpr int c4n = UW_NO / 4;
   const long long T = (long long)n * th * tw;
-  const long long total = T * c4n;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
+  {
+    const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
     const int q = (int)(i % c4n);
     const long long tile = i / c4n;
     const int tx = (int)(tile % tw);
@@ -492,6 +497,7 @@ __global__ __launch_bounds__(256) void up4_wino_output_kernel(const float* __res
 #pragma unroll
           for (int c = 0; c < 6; ++c) s[a][c] += W4_AT[a][r] * m[c];
     }
+    double s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
@@ -502,8 +508,38 @@ __global__ __launch_bounds__(256) void up4_wino_output_kernel(const float* __res
           if (W4_AT[bb][c] != 0.f) o += W4_AT[bb][c] * s[a][c];
         const int Y = 4 * (4 * ty + a) + ry, X = 4 * (4 * tx + bb) + rx;
         f32x4* dst = reinterpret_cast<f32x4*>(y + (((long long)b * H + Y) * W + X) * ycs + co);
-        *dst = *dst + o;
+        o = *dst + o;
+        *dst = o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          s1[j] += (double)o[j];
+          s2[j] += (double)o[j] * (double)o[j];
+        }
       }
+    if (part) {
+      const int pl = threadIdx.x >> 5, cq = threadIdx.x & 31;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        red[pl][cq][j] = s1[j];
+        red[pl][cq][4 + j] = s2[j];
+      }
+      __syncthreads();
+      if (pl == 0) {
+        double a[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) a[k] = 0.0;
+        for (int r = 0; r < 8; ++r)
+#pragma unroll
+          for (int k = 0; k < 8; ++k) a[k] += red[r][cq][k];
+        const long long tin = tile - (long long)b * th * tw;
+        double* o = part + (((long long)b * th * tw + tin) * 2 + (phase >> 3)) * UW_COUT * 2;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          o[(co + j) * 2] = a[j];
+          o[(co + j) * 2 + 1] = a[4 + j];
+        }
+      }
+    }
   }
 }
 
@@ -513,7 +549,8 @@ size_t pf_up4_wino_weights_floats() { return (size_t)36 * UW_NO * UW_CU; }
 
 size_t pf_up4_wino_ws_bytes(int n, int H, int W) {
   const long long T = (long long)n * (H / 16) * (W / 16);
-  return pf_align(36 * T * UW_CU * 4, 256) + pf_align(36 * T * UW_NO * 4, 256);
+  return pf_align(36 * T * UW_CU * 4, 256) + pf_align(36 * T * UW_NO * 4, 256) +
+         pf_align((size_t)T * 2 * UW_COUT * 2 * sizeof(double), 256);
 }
 
 int pf_up4_wino_weights(const float* wph, float* U, hipStream_t st) {
@@ -528,13 +565,15 @@ int pf_up4_wino_weights(const float* wph, float* U, hipStream_t st) {
 // stages: bit 0 input transform, bit 1 the 36 GEMMs, bit 2 output transform
 // (the engine times them separately)
 int pf_up4_wino(int n, int H, int W, const float* L, int lcs, const float* U, float* y, int ycs,
-                void* ws, size_t ws_bytes, hipStream_t st, int stages) {
+                void* ws, size_t ws_bytes, hipStream_t st, int stages, float* mean, float* rstd) {
   const int lh = H / 4, lw = W / 4;
   if (H % 16 || W % 16 || lcs % 4 || ycs % 4) return POSFEAT_E_INVALID;
   if (!ws || ws_bytes < pf_up4_wino_ws_bytes(n, H, W)) return POSFEAT_E_WORKSPACE;
   const long long T = (long long)n * (lh / 4) * (lw / 4);
   float* V = static_cast<float*>(ws);
   float* M = reinterpret_cast<float*>(static_cast<char*>(ws) + pf_align(36 * T * UW_CU * 4, 256));
+  double* part = reinterpret_cast<double*>(reinterpret_cast<char*>(M) +
+                                           pf_align(36 * T * UW_NO * 4, 256));
   if (stages & 1) {
     hipLaunchKernelGGL(wino4_input_kernel, dim3(grid_for(T * (UW_CU / 4), 256)), dim3(256), 0, st,
                        L, lcs, n, lh, lw, UW_CU / 4, V, 1);
@@ -544,9 +583,12 @@ int pf_up4_wino(int n, int H, int W, const float* L, int lcs, const float* U, fl
     PF_TRY(pf_gemm_batched(V, UW_CU, T * UW_CU, U, (long long)UW_NO * UW_CU, M, UW_NO, T * UW_NO,
                            36, (int)T, UW_NO, UW_CU, st));
   if (stages & 4) {
-    hipLaunchKernelGGL(up4_wino_output_kernel, dim3(grid_for(T * (UW_NO / 4), 256)), dim3(256), 0,
-                       st, M, n, lh, lw, y, ycs);
+    // exact grid: the statistics reduce one block = one tile x 8 phases
+    hipLaunchKernelGGL(up4_wino_output_kernel, dim3((unsigned)(T * (UW_NO / 4) / 256)), dim3(256),
+                       0, st, M, n, lh, lw, y, ycs, mean ? part : nullptr);
     PF_CHECK_LAUNCH();
+    if (mean)
+      PF_TRY(pf_in_finalize(part, n, (lh / 4) * (lw / 4) * 2, H * W, UW_COUT, mean, rstd, st));
   }
   return POSFEAT_OK;
 }
