@@ -8,14 +8,23 @@ timed region) through the full extraction path of Extractor.process:
   -> sample_feat_by_coord (+L2; HIP sampler)
 No host synchronisation inside a step (the keypoint count stays on the device).
 
-Multi-GPU (torchrun, one process per GPU): rank 0 builds the packed weights
-and broadcasts them over RCCL (xGMI); ranks then extract disjoint image
-shards with no data-path collective ("weak" scaling).  Timing: barrier +
-synchronize on both sides of exactly K steps, max over ranks.
+Multi-GPU: one process per GPU.  ``--gpus N`` (N > 1) without a torchrun
+environment makes this process a launcher: before any GPU call it starts N
+worker processes of this same script with RANK / LOCAL_RANK / WORLD_SIZE /
+MASTER_ADDR=127.0.0.1 / MASTER_PORT set (torchrun's contract, so a torchrun
+launch works the same way) and exits with the workers' status.  Each worker
+binds cuda:LOCAL_RANK, joins the RCCL process group, receives rank 0's packed
+weights by ONE broadcast over xGMI and extracts its own image shard with no
+data-path collective ("weak" scaling).  Timing: barrier + synchronize on both
+sides of exactly K steps, max over ranks; rank 0 prints the JSON line with
+``ranks_seen`` = dist.get_world_size().
 """
 import argparse
 import json
 import os
+import platform
+import socket
+import subprocess
 import sys
 import time
 
@@ -44,18 +53,60 @@ PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md, dense FP32 matrix (spec)
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=10)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=60)
+    p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--batch", type=int, default=8, help="images per GPU per step")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--timing-steps", type=int, default=3)
-    p.add_argument("--workload", choices=("extract", "train_kp", "train_desc"), default="extract",
+    p.add_argument("--master-port", type=int, default=0,
+                   help="rendezvous port for the --gpus N launcher (0: pick a free one)")
+    p.add_argument("--workload", choices=("extract", "train_kp", "train_desc", "stub"),
+                   default="extract",
                    help="extract: configs[1] (the metric); train_kp: configs[4], the keypoint-"
                         "head training step (DiskLoss); train_desc: configs[2], the descriptor "
                         "training step (backbone, Line2Window + EpipolarLoss, Adam); training "
-                        "workloads use --batch pairs per GPU")
+                        "workloads use --batch pairs per GPU; stub: a CPU-only step over "
+                        "gloo that tests the launcher and the timing protocol")
     return p.parse_args()
+
+
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_workers(args, argv=None):
+    """--gpus N > 1 without WORLD_SIZE in the environment: start N fresh
+    worker processes of this script (one per GPU, torchrun's environment
+    contract) and return their combined exit status.  Runs before anything
+    touches the GPU (no torch.cuda call in this process), and starts the
+    workers as children instead of exec-ing.  A failed worker stops the
+    others, so no rank waits forever in a collective."""
+    argv = sys.argv[1:] if argv is None else argv
+    n = args.gpus
+    port = args.master_port or _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv),
+                                      env=env))
+    status = 0
+    alive = list(procs)
+    while alive:
+        for p in list(alive):
+            rc = p.poll()
+            if rc is None:
+                continue
+            alive.remove(p)
+            if rc != 0 and status == 0:
+                status = rc if rc > 0 else 128 - rc
+                for q in alive:
+                    q.terminate()
+        time.sleep(0.05)
+    return status
 
 
 def setup_dist(args):
@@ -63,10 +114,63 @@ def setup_dist(args):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        torch.cuda.set_device(local)
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.workload == "stub":
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     return world, rank, local
+
+
+def ranks_seen():
+    import torch.distributed as dist
+    return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+
+
+def timed_loop(world, steps, fn, sync):
+    """barrier + sync, exactly ``steps`` calls of fn, sync + barrier; max over ranks."""
+    import torch.distributed as dist
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    sync()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64)
+        if dist.get_backend() == "nccl":
+            t = t.cuda()
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    return el
+
+
+def stub_main(args, world, rank):
+    """CPU-only stand-in step (a small matmul per rank) for the launcher test:
+    same launch, barrier/timing protocol and JSON line as the real workloads."""
+    g = torch.Generator().manual_seed(rank)
+    a = torch.rand(128, 128, generator=g)
+
+    def one():
+        torch.mm(a, a)
+    for _ in range(args.warmup):
+        one()
+    el = timed_loop(world, args.steps, one, lambda: None)
+    if rank == 0:
+        print(json.dumps({"metric": "stub steps/s", "value": round(world * args.steps / el, 3),
+                          "unit": "steps/s", "n_gpus": world, "ranks_seen": ranks_seen(),
+                          "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(el / args.steps * 1e3, 3),
+                          "higher_is_better": True, "scaling": "weak"}), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
 
 
 def build_engine(world, rank, dev, train=False):
@@ -93,19 +197,55 @@ def make_images(rank, batch, dev):
     return torch.from_numpy(np.stack(ims)).to(dev)
 
 
+# PoSFeat.extract's engine outputs (networks/PoSFeat_model.py: local_map,
+# global_map, global_feat, local_point; local_map_small feeds the head only)
+EXTRACT_OUTPUTS = ("local_map", "global_map", "global_feat")
+
+
 def step(engine, ops, ws, imgs):
-    out = engine.run(imgs, outputs=())
-    idx, coord, score, counts, n_dev = ops.detect(out["local_point"], NMS_R, NUM_PTS, thr=THR,
+    """PoSFeat.extract + Extractor.process for one batch: the engine with the
+    NCHW outputs and global_feat PoSFeat.extract returns (plus its local_thr /
+    global_point constants), the detector and the descriptor sampler."""
+    out = engine.run(imgs, outputs=EXTRACT_OUTPUTS)
+    lp = out["local_point"]
+    b, _, h, w = out["global_map"].shape
+    out["local_thr"] = torch.zeros_like(lp)
+    out["global_point"] = torch.ones(b, 1, h, w, device=lp.device)
+    idx, coord, score, counts, n_dev = ops.detect(lp, NMS_R, NUM_PTS, thr=THR,
                                                   thr_mod="abs", ws=ws, sync=False)
     desc = ops.sample_desc_nhwc(out["_local_map_nhwc"], coord, c=128, n_valid=n_dev)
     return desc, coord, score
+
+
+def host_cpu_info():
+    """nproc, the CPUs this process may run on, and the CPU model."""
+    model = platform.processor() or "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    return os.cpu_count() or 1, avail, model
 
 
 def cpu_baseline(seconds):
     """Oracle (torch-CPU restatement of the reference path) on host cores."""
     from oracle import model_ref, detect_ref
     from posfeat_amd.weights import seeded_state_dicts, seeded_image
-    threads = min(16, os.cpu_count() or 1)
+    nproc, avail, model = host_cpu_info()
+    # every CPU this process may use; OMP_NUM_THREADS (set to the box's CPU
+    # share by the GPU pool) caps it, since threads beyond the share only
+    # time-slice against each other
+    threads = avail
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        threads = min(threads, max(1, int(os.environ["OMP_NUM_THREADS"])))
     torch.set_num_threads(threads)
     bb, hd = seeded_state_dicts(0)
 
@@ -124,13 +264,18 @@ def cpu_baseline(seconds):
         if el > seconds or n >= 30:
             break
     return {"value": n / el, "unit": "images/s", "cores": threads, "kind": "port",
+            "nproc": nproc, "cpus_available": avail, "cpu_model": model,
             "sample": "%d seeded 480x640 images, extract+detect(2048)+sample, batch 1, "
                       "torch-CPU oracle (oracle/model_ref.py + oracle/detect_ref.py)" % n}
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_workers(args))
     world, rank, local = setup_dist(args)
+    if args.workload == "stub":
+        return stub_main(args, world, rank)
     dev = torch.device("cuda", local if world > 1 else torch.cuda.current_device())
     torch.cuda.set_device(dev)
     if args.workload == "train_kp":
@@ -138,27 +283,13 @@ def main():
     if args.workload == "train_desc":
         return train_desc_main(args, world, rank, dev)
     from posfeat_amd import ops
+    import torch.distributed as dist
     engine = build_engine(world, rank, dev)
     ws = ops.DetectWorkspace()
     imgs = make_images(rank, args.batch, dev)
     for _ in range(args.warmup):
         step(engine, ops, ws, imgs)
-    torch.cuda.synchronize()
-    if world > 1:
-        import torch.distributed as dist
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(engine, ops, ws, imgs)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    el = timed_loop(world, args.steps, lambda: step(engine, ops, ws, imgs), torch.cuda.synchronize)
     images = world * args.steps * args.batch
     value = images / el
 
@@ -197,6 +328,7 @@ def main():
             "value": round(value, 3),
             "unit": "images/s",
             "n_gpus": world,
+            "ranks_seen": ranks_seen(),
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(el / args.steps * 1e3, 3),
@@ -260,21 +392,12 @@ def train_main(args, world, rank, dev):
     torch.manual_seed(1234 + rank)
     for _ in range(args.warmup):
         step.step(im1, im2, F1, F2, epoch=1)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        out, _ = step.step(im1, im2, F1, F2, epoch=1)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    last = {}
+
+    def one():
+        last["out"] = step.step(im1, im2, F1, F2, epoch=1)[0]
+    el = timed_loop(world, args.steps, one, torch.cuda.synchronize)
+    out = last["out"]
     pairs = world * args.steps * b
     # per-kernel timing of one extra step (HIP events on the engine's stream)
     engine.set_timing(2 * b, H, W, True)
@@ -291,6 +414,7 @@ def train_main(args, world, rank, dev):
         rec = {
             "metric": "pairs/sec keypoint-head training step (640x480, DiskLoss, SGD)",
             "value": round(pairs / el, 3), "unit": "pairs/s", "n_gpus": world,
+            "ranks_seen": ranks_seen(),
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
@@ -344,21 +468,12 @@ def train_desc_main(args, world, rank, dev):
     torch.manual_seed(4321 + rank)
     for _ in range(args.warmup):
         tr.step(im1, im2, F1, F2, loss, epoch=1)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        out, _ = tr.step(im1, im2, F1, F2, loss, epoch=1)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    last = {}
+
+    def one():
+        last["out"] = tr.step(im1, im2, F1, F2, loss, epoch=1)[0]
+    el = timed_loop(world, args.steps, one, torch.cuda.synchronize)
+    out = last["out"]
     pairs = world * args.steps * b
     # per-kernel-class timing of one extra step (HIP events on the trainer's stream)
     tr.set_timing(True)
@@ -377,6 +492,7 @@ def train_desc_main(args, world, rank, dev):
             "metric": "pairs/sec descriptor training step (640x480, Line2Window + EpipolarLoss, "
                       "Adam)",
             "value": round(pairs / el, 3), "unit": "pairs/s", "n_gpus": world,
+            "ranks_seen": ranks_seen(),
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "fp32",

@@ -124,8 +124,11 @@ struct posfeat_model {
   // the image branch of KeypointDet (convimg + its IN statistics + the folded
   // G part of head.conv2 + head.conv2's weight transforms) depends on the
   // image only: it runs on a second stream, overlapping the ResUNet, and
-  // joins before head.conv2's border/upsampled part (POSFEAT_SIDE=0: serial)
-  bool side = true;
+  // joins before head.conv2's border/upsampled part (POSFEAT_SIDE=0: serial).
+  // Set in plan() before the dry pass so the planning forward follows the
+  // path that actually runs.
+  bool side = false;
+  bool tuned_once = false;  // the first forward (autotune) runs serially
   hipStream_t side_st = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   Buf splitk2;  // the side stream's own split-K / statistics scratch
@@ -171,7 +174,9 @@ int timed(Ctx& c, const std::string& label, double flops, F&& fn) {
     m->evs.push_back(e);
   }
   auto& e = m->evs[m->ev_used++];
-  e.label = label;
+  // side-stream launches overlap the main stream: keep them out of the
+  // main-stream prefixes ("conv:", "head.conv2", ...) the bench sums
+  e.label = c.side ? "side:" + label : label;
   e.flops = flops;
   if (hipEventRecord(e.a, c.st) != hipSuccess) return POSFEAT_E_HIP;
   const int r = fn();
@@ -418,6 +423,10 @@ void plan(posfeat_model* m) {
     alloc(m->wino_ws, wb / 4 + 4);
   }
   if (m->train) m->up4 = false;  // the backward reads the materialised conv2 input
+  {
+    const char* e = getenv("POSFEAT_SIDE");
+    m->side = !(e && e[0] == '0') && m->up4 && m->gfuse && !m->train;
+  }
   if (m->up4) {
     alloc(m->g64, B * H * W * 64);
     alloc(m->wph, posfeat_conv2_up4_weights_floats());
@@ -467,10 +476,6 @@ void plan(posfeat_model* m) {
     m->splitk_need = std::max(m->splitk_need, posfeat_conv2d_workspace(&d));
   }
   alloc(m->splitk, m->splitk_need / 4 + 4);
-  {
-    const char* e = getenv("POSFEAT_SIDE");
-    m->side = !(e && e[0] == '0') && m->up4 && m->gfuse && !m->train;
-  }
   if (m->side) alloc(m->splitk2, std::max(m->splitk_need, part) / 4 + 4);
   m->ws_bytes = cur;
 }
@@ -529,10 +534,20 @@ int image_branch(Ctx& c, const float* img4) {
   s.side = true;
   if (!c.dry) {
     if (!m->side_st) {
-      if (hipStreamCreateWithFlags(&m->side_st, hipStreamNonBlocking) != hipSuccess ||
-          hipEventCreateWithFlags(&m->ev_fork, hipEventDisableTiming) != hipSuccess ||
-          hipEventCreateWithFlags(&m->ev_join, hipEventDisableTiming) != hipSuccess)
+      // commit the stream and both events together (a partial set would make
+      // every later extract fail on a null event)
+      hipStream_t st = nullptr;
+      hipEvent_t ef = nullptr, ej = nullptr;
+      if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess ||
+          hipEventCreateWithFlags(&ef, hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&ej, hipEventDisableTiming) != hipSuccess) {
+        if (ef) (void)hipEventDestroy(ef);
+        if (st) (void)hipStreamDestroy(st);
         return POSFEAT_E_HIP;
+      }
+      m->side_st = st;
+      m->ev_fork = ef;
+      m->ev_join = ej;
     }
     if (hipEventRecord(m->ev_fork, c.st) != hipSuccess ||
         hipStreamWaitEvent(m->side_st, m->ev_fork, 0) != hipSuccess)
@@ -574,7 +589,10 @@ int forward(Ctx& c, const float* img, posfeat_extract_out* out) {
   float* img4 = c.f(m->img4);
   // ---- ResUNet (DescNet.py:64-84) -----------------------------------------
   PF_TRY(timed(c, "layout:img", 0, [&] { return pf_nchw_to_nhwc(img, B, 3, H, W, 4, img4, c.st); }));
-  const bool side = m->side;
+  // the first forward of a shape autotunes every main-stream conv by timing
+  // it: run it serially so the side stream's kernels do not contend with
+  // the candidates being timed (the tile choice would depend on that race)
+  const bool side = m->side && (c.dry || m->tuned_once || !m->autotune);
   if (side) PF_TRY(image_branch(c, img4));
   PF_TRY(conv(c, "firstconv", img4, B, H, W, 4, c.f(m->stem), 64, 2, POSFEAT_ACT_RELU));
   float* headcat = c.f(m->headcat);
@@ -877,7 +895,9 @@ extern "C" int posfeat_model_extract(posfeat_model* m, const float* img_nchw,
   if (reinterpret_cast<uintptr_t>(ws) & 255) return POSFEAT_E_INVALID;
   Ctx c{m, static_cast<char*>(ws), pf_stream(stream)};
   m->ev_used = 0;
-  return forward(c, img_nchw, out);
+  const int r = forward(c, img_nchw, out);
+  if (r == POSFEAT_OK) m->tuned_once = true;
+  return r;
 }
 
 extern "C" int posfeat_model_set_timing(posfeat_model* m, int enable) {

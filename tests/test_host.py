@@ -130,3 +130,23 @@ def test_gloo_head_grad_allreduce_is_ddp_mean():
     assert res[0][1] == 0.5
     np.testing.assert_array_equal(res[0][2], res[1][2])
     np.testing.assert_allclose(res[0][2], ref, rtol=1e-6, atol=1e-7)
+
+
+def test_bench_launcher_spawns_world2():
+    """bench.py --gpus 2 with no torchrun environment starts two worker ranks
+    itself (the driver's 1/2/4/8 scaling runs); the stub workload exercises
+    the launch, the gloo rendezvous and the barrier / max-over-ranks timing."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                        "--workload", "stub", "--steps", "3", "--warmup", "1"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout          # rank 0 prints exactly one line
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["ranks_seen"] == 2 and rec["steps"] == 3
+    assert rec["value"] > 0
