@@ -39,14 +39,16 @@ NUM_PTS, NMS_R, THR = 2048, 1, 0.9
 # Conv work per 480x640 image: 2 x 208.99 GMAC
 CONV_FLOP_PER_IMAGE = 417.98e9
 HEAD_CONV2_FLOP_PER_IMAGE = 2.0 * 480 * 640 * 128 * 256 * 9   # reference layer
-# dominant kernel: the 192 x4-upsampled channels of head.conv2.  Default: the
-# 36 transform-domain GEMMs of the low-res Winograd F(4x4) form (DESIGN.md
-# §4.1a''), 2 x 36 x (120/4 x 160/4 tiles) x 2048 phase channels x 192 per
-# image; POSFEAT_UP4WINO=0: conv_up4_kernel by bilinear phases (6.25 taps on
-# average, §4.1).  The executed FLOPs come from the engine's timing label.
-UP4_WINO = os.environ.get("POSFEAT_UP4WINO", "1") != "0"
-UP4_FLOP_PER_IMAGE = (2.0 * 36 * 30 * 40 * 2048 * 192 if UP4_WINO
-                      else 2.0 * 480 * 640 * 128 * 192 * 6.25)
+# dominant kernel (roofline): the single MFMA launch with the largest time in
+# the step, among the engine's one-launch GEMM labels -- the batched Winograd
+# GEMMs of the decoder (conv:<layer>.wino) and head.conv2's low-res tap GEMM
+# (conv:head.conv2.up4tap).  The engine's timing events carry the FLOPs each
+# launch executes.
+GEMM_LABEL_KERNELS = {
+    ".wino": "conv_glds_kernel x36 batched (Winograd F(4x4) transform-domain GEMMs of %s)",
+    "up4tap": "conv_glds_kernel (head.conv2's 192 x4-upsampled channels: nine 1x1 convs on the "
+              "120x160 grid as one [B*19200 x 192] x [192 x 1152] GEMM)",
+}
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md, dense FP32 matrix (spec)
 
 
@@ -293,32 +295,43 @@ def main():
     images = world * args.steps * args.batch
     value = images / el
 
-    # ---- roofline of the dominant kernel (see UP4_FLOP_PER_IMAGE), HIP events on the
-    # engine's stream around each launch, averaged over a few extra steps
+    # ---- roofline of the dominant kernel, HIP events on the engine's stream
+    # around each launch, averaged over a few extra steps
     engine.set_timing(args.batch, H, W, True)
-    k_ms, c2_ms, conv_ms, conv_fl, all_ms = [], [], [], [], []
+    per_label = {}
+    c2_ms, conv_ms, conv_fl, all_ms, side_ms = [], [], [], [], []
     for _ in range(args.timing_steps):
         step(engine, ops, ws, imgs)
-        k_ms.append(engine.timing(args.batch, H, W, "conv:head.conv2.up4")[0])
-        c2_ms.append(engine.timing(args.batch, H, W, "conv:head.conv2")[0] +
-                     engine.timing(args.batch, H, W, "head.conv2")[0])
-        ms2, fl2, nconv = engine.timing(args.batch, H, W, "conv:")
-        conv_ms.append(ms2)
-        conv_fl.append(fl2)
-        all_ms.append(engine.timing(args.batch, H, W, "")[0])
+        ev = engine.timing_events(args.batch, H, W)
+        for lab, ms, fl in ev:
+            if lab.startswith("conv:") and any(lab.endswith(k) for k in GEMM_LABEL_KERNELS):
+                per_label.setdefault(lab, []).append((ms, fl))
+        main = [e for e in ev if not e[0].startswith("side:")]
+        c2_ms.append(sum(ms for lab, ms, _ in main if lab.startswith(("conv:head.conv2",
+                                                                        "head.conv2"))))
+        conv_ms.append(sum(ms for lab, ms, _ in main if lab.startswith("conv:")))
+        conv_fl.append(sum(fl for lab, _, fl in main if lab.startswith("conv:")))
+        all_ms.append(sum(ms for _, ms, _ in main))
+        side_ms.append(sum(ms for lab, ms, _ in ev if lab.startswith("side:")))
     engine.set_timing(args.batch, H, W, False)
-    kms = float(np.mean(k_ms))
-    k_flops = UP4_FLOP_PER_IMAGE * args.batch
+    dom = max(per_label, key=lambda k: np.mean([m for m, _ in per_label[k]]))
+    kms = float(np.mean([m for m, _ in per_label[dom]]))
+    k_flops = float(np.mean([f for _, f in per_label[dom]]))
     achieved = k_flops / (kms * 1e-3) / 1e12
+    kdesc = next(v for k, v in GEMM_LABEL_KERNELS.items() if dom.endswith(k))
+    kdesc = kdesc % dom[len("conv:"):-len(".wino")] if "%s" in kdesc else kdesc
     c2 = float(np.mean(c2_ms))
     conv_total = float(np.mean(conv_ms))
     conv_ach = float(np.mean(conv_fl)) / (conv_total * 1e-3) / 1e12
+    # HBM bytes of that launch from the committed rocprofv3 --pmc passes
+    # (tools/traffic_json.py), when they were measured for the same label
     traffic = None
-    tfile = os.path.join(ROOT, "profiles", "up4w_traffic.json" if UP4_WINO else "up4_traffic.json")
+    tfile = os.path.join(ROOT, "profiles", "dominant_traffic.json")
     if os.path.exists(tfile):
         try:
-            traffic = json.load(open(tfile)).get("bytes_per_launch_per_image")
-            traffic = traffic * args.batch if traffic else None
+            t = json.load(open(tfile))
+            if t.get("label") == dom and t.get("batch") == args.batch:
+                traffic = t.get("bytes_per_launch")
         except Exception:
             traffic = None
 
@@ -343,17 +356,15 @@ def main():
                                    "2048) + sample_feat_by_coord",
                        "global_batch": args.batch * world, "image": [H, W],
                        "num_pts": NUM_PTS, "parallelism": "dp%d (image-sharded)" % world},
-            "roofline": {"kernel": ("conv_glds_kernel<128,128,2,2> x36 batched (head.conv2's 192 "
-                                    "x4-upsampled channels: Winograd F(4x4) GEMMs on the 120x160 "
-                                    "map, 2048 phase channels)") if UP4_WINO else
-                                   ("conv_up4_kernel<8> (head.conv2: 192 x4-upsampled channels "
-                                    "by bilinear phases on the 120x160 map, 8x16 patches)"),
+            "roofline": {"kernel": kdesc, "label": dom,
                          "bound": "mfma", "achieved": round(achieved, 3),
                          "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4),
                          "traffic": traffic,
                          "avg_launch_ms": round(kms, 4), "flop_per_launch": k_flops},
             "head_conv2": {"ms_per_step": round(c2, 3),
+                           "note": "main-stream part (low-res tap GEMM + combine); the G part "
+                                   "(IN(convimg) channels) runs on the side stream",
                            "reference_equivalent_tflops":
                                round(HEAD_CONV2_FLOP_PER_IMAGE * args.batch / (c2 * 1e-3) / 1e12, 3)},
             "conv_total": {"executed_tflops": round(conv_ach, 3),
@@ -361,7 +372,10 @@ def main():
                            "reference_equivalent_tflops":
                                round(CONV_FLOP_PER_IMAGE * args.batch / (conv_total * 1e-3) / 1e12, 3),
                            "ms_per_step": round(conv_total, 3),
-                           "all_kernels_ms_per_step": round(float(np.mean(all_ms)), 3)},
+                           "main_stream_kernels_ms_per_step": round(float(np.mean(all_ms)), 3),
+                           "side_stream_kernels_ms_per_step": round(float(np.mean(side_ms)), 3),
+                           "note": "main-stream launches only; the side stream (KeypointDet's "
+                                   "image branch) overlaps them"},
         }
         if world == 1 and not args.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baseline(args.cpu_seconds)

@@ -321,6 +321,11 @@ int posfeat_model_extract(posfeat_model *m, const float *img_nchw, posfeat_extra
 int posfeat_model_set_timing(posfeat_model *m, int enable);
 int posfeat_model_timing(posfeat_model *m, const char *prefix, double *ms, double *flops,
                          int *launches);
+/* The i-th timed launch of the last call (diagnostic; host-synchronises):
+ * its label (valid until the next call on m), duration and the FLOPs the
+ * engine counts for it.  POSFEAT_E_INVALID past the last launch. */
+int posfeat_model_timing_event(posfeat_model *m, int i, const char **label, double *ms,
+                               double *flops);
 void posfeat_model_destroy(posfeat_model *m);
 
 /* Keypoint-head training (config 5, configs/train_kp.yaml: optimal_modules

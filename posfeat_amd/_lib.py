@@ -140,6 +140,9 @@ SIGNATURES = {
     "posfeat_model_set_timing": (c_int, [c_void_p, c_int]),
     "posfeat_model_timing": (c_int, [c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
                                      ctypes.POINTER(ctypes.c_double), P_int]),
+    "posfeat_model_timing_event": (c_int, [c_void_p, c_int, ctypes.POINTER(ctypes.c_char_p),
+                                           ctypes.POINTER(ctypes.c_double),
+                                           ctypes.POINTER(ctypes.c_double)]),
     "posfeat_model_destroy": (None, [c_void_p]),
 }
 

@@ -119,6 +119,10 @@ struct posfeat_model {
   // head.conv2's upsampled part as a low-res Winograd F(4x4) conv (wino.hip)
   bool up4wino = true;
   Buf u4u, u4ws;
+  // head.conv2's upsampled part with the channel mixing on the low-res grid:
+  // nine 1x1 convs (one GEMM) + the interpolation/tap combine (up4tap.hip)
+  bool up4tap = true;
+  Buf tapw, tapP, tappart;
   Buf gf_w, gf_b;
   size_t splitk_need = 0;
   // the image branch of KeypointDet (convimg + its IN statistics + the folded
@@ -224,6 +228,30 @@ int tune(const std::string& name, const posfeat_conv_desc& d, hipStream_t st, Ru
   return best;
 }
 
+// run (autotuned on the first forward of the instance, keyed by `key`) one
+// conv described by d with packed weights w
+int conv_desc_run(Ctx& c, const std::string& key, const posfeat_conv_desc& d, const float* x,
+                  const float* w, const float* bias, const float* res, float* y, double flops) {
+  const size_t need = posfeat_conv2d_workspace(&d);
+  if (c.dry) {
+    if (need > c.m->splitk_need) c.m->splitk_need = need;
+    return POSFEAT_OK;
+  }
+  const Buf& sk = c.side ? c.m->splitk2 : c.m->splitk;
+  float* part = c.f(sk);
+  const size_t have = sk.floats * sizeof(float);
+  auto run = [&](int tile) { return pf_conv_run_tile(&d, x, w, bias, res, y, part, have, tile, c.st); };
+  int tile = -1;
+  auto it = c.m->tuned.find(key);
+  if (it != c.m->tuned.end()) {
+    tile = it->second;
+  } else if (c.m->autotune) {
+    tile = tune(key, d, c.st, run);
+    c.m->tuned[key] = tile;
+  }
+  return timed(c, "conv:" + key, flops, [&] { return run(tile); });
+}
+
 int conv(Ctx& c, const std::string& name, const float* x, int n, int h, int w, int xcs, float* y,
          int ycs, int stride, int act, const float* res = nullptr, int rcs = 0) {
   const Spec* s = specs().find(name);
@@ -244,26 +272,7 @@ int conv(Ctx& c, const std::string& name, const float* x, int n, int h, int w, i
   d.act = act;
   const int oh = (h + 2 * d.pad - d.kh) / stride + 1, ow = (w + 2 * d.pad - d.kw) / stride + 1;
   const double flops = 2.0 * n * oh * ow * (double)s->cout * s->cin * s->kh * s->kw;
-  const size_t need = posfeat_conv2d_workspace(&d);
-  if (c.dry) {
-    if (need > c.m->splitk_need) c.m->splitk_need = need;
-    return POSFEAT_OK;
-  }
-  const Buf& sk = c.side ? c.m->splitk2 : c.m->splitk;
-  float* part = c.f(sk);
-  const size_t have = sk.floats * sizeof(float);
-  auto run = [&](int tile) {
-    return pf_conv_run_tile(&d, x, c.W(name), c.Bi(name), res, y, part, have, tile, c.st);
-  };
-  int tile = -1;
-  auto it = c.m->tuned.find(name);
-  if (it != c.m->tuned.end()) {
-    tile = it->second;
-  } else if (c.m->autotune) {
-    tile = tune(name, d, c.st, run);
-    c.m->tuned[name] = tile;
-  }
-  return timed(c, "conv:" + name, flops, [&] { return run(tile); });
+  return conv_desc_run(c, name, d, x, c.W(name), c.Bi(name), res, y, flops);
 }
 
 int forward(Ctx& c, const float* img, posfeat_extract_out* out);
@@ -297,10 +306,16 @@ int conv3x3(Ctx& c, const std::string& name, const float* x, int n, int h, int w
   // executed transform-domain MACs: F(4x4) 36 per 4x4 tile, F(2x2) 16 per 2x2 tile
   const bool f4 = h % 4 == 0 && w % 4 == 0 && !(getenv("POSFEAT_WINO") && getenv("POSFEAT_WINO")[0] == '1');
   const double T = f4 ? (double)n * (h / 4) * (w / 4) : (double)n * (h / 2) * (w / 2);
-  return timed(c, "conv:" + name + ".wino", 2.0 * T * (f4 ? 36 : 16) * s->cin * s->cout, [&] {
+  // three launches, timed apart: the input transform, the batched GEMMs
+  // (the MFMA work), the output transform (+ bias, activation)
+  auto stage = [&](int st_bits) {
     return pf_wino_conv(x, xcs, n, h, w, s->cin, U, c.Bi(name), s->cout, act, y, ycs,
-                        c.f(m->wino_ws), m->wino_ws.floats * sizeof(float), c.st);
-  });
+                        c.f(m->wino_ws), m->wino_ws.floats * sizeof(float), c.st, st_bits);
+  };
+  PF_TRY(timed(c, "wino:in:" + name, 0, [&] { return stage(1); }));
+  PF_TRY(timed(c, "conv:" + name + ".wino", 2.0 * T * (f4 ? 36 : 16) * s->cin * s->cout,
+               [&] { return stage(2); }));
+  return timed(c, "wino:out:" + name, 0, [&] { return stage(4); });
 }
 
 // conv whose epilogue also produces the InstanceNorm mean/rstd of its output
@@ -405,6 +420,8 @@ void plan(posfeat_model* m) {
     m->gfuse = !(gv && gv[0] == '0');
     const char* uv = getenv("POSFEAT_UP4WINO");  // 0: conv_up4_kernel (bilinear phases)
     m->up4wino = !(uv && uv[0] == '0') && H % 16 == 0 && W % 16 == 0;
+    const char* tv = getenv("POSFEAT_UP4TAP");  // 0: the low-res Winograd / phase forms
+    m->up4tap = !(tv && tv[0] == '0') && H % 16 == 0 && W % 16 == 0;
   }
   if (m->up4 && m->gfuse) {
     alloc(m->gf_w, B * 128 * 128);
@@ -431,7 +448,11 @@ void plan(posfeat_model* m) {
     alloc(m->g64, B * H * W * 64);
     alloc(m->wph, posfeat_conv2_up4_weights_floats());
     alloc(m->up4ws, posfeat_conv2_up4_workspace((int)B, (int)H, (int)W) / 4 + 4);
-    if (m->up4wino) {
+    if (m->up4tap) {
+      alloc(m->tapw, pf_up4tap_weights_floats());
+      alloc(m->tapP, pf_up4tap_p_floats((int)B, (int)H, (int)W));
+      alloc(m->tappart, pf_up4tap_part_bytes((int)B, (int)H, (int)W) / 4 + 4);
+    } else if (m->up4wino) {
       alloc(m->u4u, pf_up4_wino_weights_floats());
       alloc(m->u4ws, pf_up4_wino_ws_bytes((int)B, (int)H, (int)W) / 4 + 4);
     }
@@ -560,9 +581,14 @@ int image_branch(Ctx& c, const float* img4) {
   float* g64 = c.f(m->g64);
   float* c2 = c.f(m->c2raw);
   PF_TRY(conv_in(s, "head.convimg", img4, B, H, W, 4, g64, 64, meanI, rstdI));
-  PF_TRY(timed(s, "head.conv2.weights", 0, [&] {
-    return posfeat_conv2_up4_weights(s.W("head.conv2"), s.f(m->wph), s.st);
-  }));
+  if (!m->up4tap)
+    PF_TRY(timed(s, "head.conv2.weights", 0, [&] {
+      return posfeat_conv2_up4_weights(s.W("head.conv2"), s.f(m->wph), s.st);
+    }));
+  else
+    PF_TRY(timed(s, "head.conv2.tapw", 0, [&] {
+      return pf_up4tap_weights(s.W("head.conv2"), s.f(m->tapw), s.st);
+    }));
   PF_TRY(timed(s, "head.conv2.gfuse_w", 0, [&] {
     return pf_gfuse_weights(s.W("head.conv2"), s.Bi("head.conv2"), s.W("head.convimg"),
                             s.Bi("head.convimg"), meanI, rstdI, B, s.f(m->gf_w), s.f(m->gf_b),
@@ -572,7 +598,7 @@ int image_branch(Ctx& c, const float* img4) {
     return pf_gfuse_conv(img4, g64, 64, B, H, W, s.f(m->gf_w), s.f(m->gf_b), meanI, rstdI,
                          s.W("head.conv2"), s.Bi("head.conv2"), c2, 128, s.st);
   }));
-  if (m->up4wino)
+  if (m->up4wino && !m->up4tap)
     PF_TRY(timed(s, "head.conv2.up4w", 0, [&] {
       return pf_up4_wino_weights(s.f(m->wph), s.f(m->u4u), s.st);
     }));
@@ -652,9 +678,13 @@ int forward(Ctx& c, const float* img, posfeat_extract_out* out) {
     // executed MFMA work: 64 full-res channels x 9 taps, 192 low-res channels
     // x 6.25 taps on average over the 16 phases (the reference layer: 256 x 9)
     const float* wph = c.f(m->wph);
-    if (!side)
+    if (!side && !m->up4tap)
       PF_TRY(timed(c, "head.conv2.weights", 0, [&] {
         return posfeat_conv2_up4_weights(c.W("head.conv2"), c.f(m->wph), c.st);
+      }));
+    if (!side && m->up4tap)
+      PF_TRY(timed(c, "head.conv2.tapw", 0, [&] {
+        return pf_up4tap_weights(c.W("head.conv2"), c.f(m->tapw), c.st);
       }));
     if (side) {
       // join the image branch (it wrote the G part into y)
@@ -676,6 +706,30 @@ int forward(Ctx& c, const float* img, posfeat_extract_out* out) {
         return pf_up4_gconv(B, H, W, g64, 64, wph, c.Bi("head.conv2"), c2, 128, c.st);
       }));
     }
+    if (m->up4tap) {
+      // P_k = W_k[:, :192] . L on the low-res grid (one 1x1-conv GEMM,
+      // N = 9 taps x 128), then y += the tap-summed x4 interpolation of P,
+      // with the instance-norm statistics of the finished conv2 output
+      posfeat_conv_desc d;
+      d.n = B;
+      d.h = h4;
+      d.w = w4;
+      d.cin = 192;
+      d.x_cstride = 192;
+      d.cout = 9 * 128;
+      d.kh = d.kw = 1;
+      d.stride = 1;
+      d.pad = 0;
+      d.y_cstride = 9 * 128;
+      d.res_cstride = 0;
+      d.act = POSFEAT_ACT_NONE;
+      PF_TRY(conv_desc_run(c, "head.conv2.up4tap", d, c1, c.f(m->tapw), nullptr, nullptr,
+                           c.f(m->tapP), 2.0 * B * h4 * w4 * 1152.0 * 192));
+      PF_TRY(timed(c, "head.conv2.combine", 0, [&] {
+        return pf_up4tap_combine(B, H, W, c.f(m->tapP), c2, 128, c.d(m->tappart), mean, rstd,
+                                 c.st);
+      }));
+    } else {
     PF_TRY(timed(c, "head.conv2.border", 0, [&] {
       return pf_up4_border(B, H, W, c1, 192, wph, c2, 128, c.st);
     }));
@@ -703,6 +757,7 @@ int forward(Ctx& c, const float* img, posfeat_extract_out* out) {
         return pf_up4_main(B, H, W, c1, 192, wph, c2, 128, c.f(m->up4ws),
                            m->up4ws.floats * sizeof(float), mean, rstd, 1e-5f, c.st);
       }));
+    }
     }
   } else {
     float* hcat = c.f(m->hcat);
@@ -925,6 +980,19 @@ extern "C" int posfeat_model_timing(posfeat_model* m, const char* prefix, double
   if (ms) *ms = t;
   if (flops) *flops = f;
   if (launches) *launches = k;
+  return POSFEAT_OK;
+}
+
+extern "C" int posfeat_model_timing_event(posfeat_model* m, int i, const char** label, double* ms,
+                                          double* flops) {
+  if (!m || i < 0 || (size_t)i >= m->ev_used) return POSFEAT_E_INVALID;
+  auto& e = m->evs[i];
+  if (hipEventSynchronize(e.b) != hipSuccess) return POSFEAT_E_HIP;
+  float dt = 0.f;
+  if (hipEventElapsedTime(&dt, e.a, e.b) != hipSuccess) return POSFEAT_E_HIP;
+  if (label) *label = e.label.c_str();
+  if (ms) *ms = dt;
+  if (flops) *flops = e.flops;
   return POSFEAT_OK;
 }
 

@@ -53,9 +53,10 @@ int pf_wino_weights(const float* wpk, int Cout, int Cin, float* U, hipStream_t s
 // U for the variant pf_wino_conv picks at (h, w): F(4x4) if h, w % 4 == 0
 int pf_wino_weights_hw(const float* wpk, int Cout, int Cin, int h, int w, float* U,
                        hipStream_t st);
+// stages: bit 0 input transform, bit 1 the batched GEMMs, bit 2 output transform
 int pf_wino_conv(const float* x, int xcs, int n, int h, int w, int Cin, const float* U,
                  const float* bias, int Cout, int act, float* y, int ycs, void* ws, size_t ws_bytes,
-                 hipStream_t st);
+                 hipStream_t st, int stages = 7);
 // head.conv2's G part as one per-image 5x5 conv of the image (gfuse.hip)
 size_t pf_gfuse_weights_floats(int n);
 int pf_gfuse_weights(const float* w2_packed, const float* b2, const float* w1_packed,
@@ -76,3 +77,10 @@ int pf_up4_wino(int n, int H, int W, const float* L, int lcs, const float* U, fl
                 float* rstd = nullptr);
 int pf_in_finalize(const double* part, int n, int nchunk, int hw, int C, float* mean, float* rstd,
                    hipStream_t st);
+// head.conv2's upsampled part with the channel mixing on the low-res grid (up4tap.hip)
+size_t pf_up4tap_weights_floats();
+size_t pf_up4tap_p_floats(int n, int H, int W);
+size_t pf_up4tap_part_bytes(int n, int H, int W);
+int pf_up4tap_weights(const float* w2_packed, float* wt, hipStream_t st);
+int pf_up4tap_combine(int n, int H, int W, const float* P, float* y, int ycs, double* part,
+                      float* mean, float* rstd, hipStream_t st);

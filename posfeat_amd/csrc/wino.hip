@@ -637,7 +637,7 @@ int pf_wino_weights(const float* wpk, int Cout, int Cin, float* U, hipStream_t s
 
 static int wino_conv_impl(const float* x, int xcs, int n, int h, int w, int Cin, const float* U,
                           bool U_is_f4, const float* bias, int Cout, int act, float* y, int ycs,
-                          void* ws, size_t ws_bytes, hipStream_t st) {
+                          void* ws, size_t ws_bytes, hipStream_t st, int stages = 7) {
   if ((h & 1) || (w & 1) || Cin % 32 || Cout % 4 || xcs % 4 || ycs % 4 || n <= 0)
     return POSFEAT_E_INVALID;
   if (ws_bytes < pf_wino_ws_bytes(n, h, w, Cin, Cout)) return POSFEAT_E_WORKSPACE;
@@ -646,35 +646,46 @@ static int wino_conv_impl(const float* x, int xcs, int n, int h, int w, int Cin,
     float* V4 = static_cast<float*>(ws);
     float* M4 =
         reinterpret_cast<float*>(static_cast<char*>(ws) + pf_align(36 * T4 * Cin * 4, 256));
-    hipLaunchKernelGGL(wino4_input_kernel, dim3(grid_for(T4 * (Cin / 4), 256)), dim3(256), 0, st,
-                       x, xcs, n, h, w, Cin / 4, V4, 0);
-    PF_CHECK_LAUNCH();
-    PF_TRY(pf_gemm_batched(V4, Cin, T4 * Cin, U, (long long)Cout * Cin, M4, Cout, T4 * Cout, 36,
-                           (int)T4, Cout, Cin, st));
-    hipLaunchKernelGGL(wino4_output_kernel, dim3(grid_for(T4 * (Cout / 4), 256)), dim3(256), 0,
-                       st, M4, n, h, w, Cout / 4, bias, act, y, ycs);
-    PF_CHECK_LAUNCH();
+    if (stages & 1) {
+      hipLaunchKernelGGL(wino4_input_kernel, dim3(grid_for(T4 * (Cin / 4), 256)), dim3(256), 0, st,
+                         x, xcs, n, h, w, Cin / 4, V4, 0);
+      PF_CHECK_LAUNCH();
+    }
+    if (stages & 2)
+      PF_TRY(pf_gemm_batched(V4, Cin, T4 * Cin, U, (long long)Cout * Cin, M4, Cout, T4 * Cout, 36,
+                             (int)T4, Cout, Cin, st));
+    if (stages & 4) {
+      hipLaunchKernelGGL(wino4_output_kernel, dim3(grid_for(T4 * (Cout / 4), 256)), dim3(256), 0,
+                         st, M4, n, h, w, Cout / 4, bias, act, y, ycs);
+      PF_CHECK_LAUNCH();
+    }
     return POSFEAT_OK;
   }
   const long long T = (long long)n * (h / 2) * (w / 2);
   float* V = static_cast<float*>(ws);
   float* M = reinterpret_cast<float*>(static_cast<char*>(ws) + pf_align(16 * T * Cin * 4, 256));
-  hipLaunchKernelGGL(wino_input_kernel, dim3(grid_for(T * (Cin / 4), 256)), dim3(256), 0, st, x,
-                     xcs, n, h, w, Cin / 4, V);
-  PF_CHECK_LAUNCH();
-  PF_TRY(pf_gemm_batched(V, Cin, T * Cin, U, (long long)Cout * Cin, M, Cout, T * Cout, 16, (int)T,
-                         Cout, Cin, st));
-  hipLaunchKernelGGL(wino_output_kernel, dim3(grid_for(T * (Cout / 4), 256)), dim3(256), 0, st, M,
-                     n, h, w, Cout / 4, bias, act, y, ycs);
-  PF_CHECK_LAUNCH();
+  if (stages & 1) {
+    hipLaunchKernelGGL(wino_input_kernel, dim3(grid_for(T * (Cin / 4), 256)), dim3(256), 0, st, x,
+                       xcs, n, h, w, Cin / 4, V);
+    PF_CHECK_LAUNCH();
+  }
+  if (stages & 2)
+    PF_TRY(pf_gemm_batched(V, Cin, T * Cin, U, (long long)Cout * Cin, M, Cout, T * Cout, 16,
+                           (int)T, Cout, Cin, st));
+  if (stages & 4) {
+    hipLaunchKernelGGL(wino_output_kernel, dim3(grid_for(T * (Cout / 4), 256)), dim3(256), 0, st,
+                       M, n, h, w, Cout / 4, bias, act, y, ycs);
+    PF_CHECK_LAUNCH();
+  }
   return POSFEAT_OK;
 }
 
 // U from pf_wino_weights_hw(.., h, w, ..): the variant is chosen from (h, w)
 int pf_wino_conv(const float* x, int xcs, int n, int h, int w, int Cin, const float* U,
                  const float* bias, int Cout, int act, float* y, int ycs, void* ws, size_t ws_bytes,
-                 hipStream_t st) {
-  return wino_conv_impl(x, xcs, n, h, w, Cin, U, true, bias, Cout, act, y, ycs, ws, ws_bytes, st);
+                 hipStream_t st, int stages) {
+  return wino_conv_impl(x, xcs, n, h, w, Cin, U, true, bias, Cout, act, y, ycs, ws, ws_bytes, st,
+                        stages);
 }
 
 namespace {

@@ -62,6 +62,17 @@ class ExtractionEngine:
                                          ctypes.byref(fl), ctypes.byref(n)))
         return ms.value, fl.value, n.value
 
+    def timing_events(self, b, h, w):
+        """[(label, ms, flops)] of every timed launch of the last run (host-synchronises)."""
+        handle, _, _ = self._instance(b, h, w)
+        out, i = [], 0
+        lab, ms, fl = ctypes.c_char_p(), ctypes.c_double(), ctypes.c_double()
+        while lib().posfeat_model_timing_event(handle, i, ctypes.byref(lab), ctypes.byref(ms),
+                                               ctypes.byref(fl)) == 0:
+            out.append((lab.value.decode(), ms.value, fl.value))
+            i += 1
+        return out
+
     def run(self, img, outputs=("local_map", "global_map", "global_feat", "local_map_small")):
         """img: [b,3,h,w] fp32 on the device (h, w multiples of 16).
 

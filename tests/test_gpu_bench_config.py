@@ -11,8 +11,9 @@
   H/16, W/16 are odd) run end to end against the oracle with the Aachen
   detector configuration (configs/extract_aachen.yaml: nms_radius 3, thr 0.5).
 * The engine's non-default paths behind environment switches (POSFEAT_SIDE=0:
-  serial image branch; POSFEAT_UP4WINO=0: head.conv2 by bilinear phases) agree
-  with the default engine (SIDE: bit-identical; UP4WINO: 1e-4).
+  serial image branch; POSFEAT_UP4TAP=0: head.conv2's upsampled part as the
+  low-res Winograd F(4x4) conv; POSFEAT_UP4WINO=0 with it: by bilinear phases)
+  agree with the default engine (SIDE: bit-identical; the others: 1e-4).
 """
 import os
 
@@ -137,7 +138,8 @@ def test_aachen_shapes_vs_oracle(gpu, hw):
     eng.close()
 
 
-@pytest.mark.parametrize("switch,exact", [("POSFEAT_SIDE", True), ("POSFEAT_UP4WINO", False)])
+@pytest.mark.parametrize("switch,exact", [("POSFEAT_SIDE", True), ("POSFEAT_UP4WINO", False),
+                                          ("POSFEAT_UP4TAP", False)])
 def test_env_switch_paths_match_default(gpu, switch, exact, monkeypatch):
     from posfeat_amd.weights import seeded_image
     imgs = torch.from_numpy(np.stack([seeded_image(s, 96, 128) for s in (4, 5)])).to(gpu)
@@ -146,6 +148,8 @@ def test_env_switch_paths_match_default(gpu, switch, exact, monkeypatch):
     ref = base.run(imgs)
     ref = {k: v.clone() for k, v in ref.items() if not k.startswith("_")}
     monkeypatch.setenv(switch, "0")
+    if switch == "POSFEAT_UP4WINO":
+        monkeypatch.setenv("POSFEAT_UP4TAP", "0")   # the phase kernel sits behind both
     alt = _new_engine(gpu)        # the switch is read when the instance is planned
     alt.run(imgs)
     got = alt.run(imgs)

@@ -1,0 +1,4 @@
+set -e
+timeout -k 10 600 python -u -m pytest tests/test_gpu_bench_config.py tests/test_gpu_model.py tests/test_gpu_api.py -x -v --timeout 300 --timeout-method thread > gpurun_out/gpu_tests_r2b.log 2>&1
+timeout -k 10 300 python tools/layer_timing.py 8 480 640 > gpurun_out/lt_r2b.log 2>&1
+timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/bench_r2b.json 2> gpurun_out/bench_r2b.err
