@@ -315,6 +315,17 @@ int posfeat_model_create(int batch, int h, int w, const float *weights, posfeat_
 size_t posfeat_model_workspace(const posfeat_model *m);
 int posfeat_model_extract(posfeat_model *m, const float *img_nchw, posfeat_extract_out *out,
                           void *ws, size_t ws_bytes, void *stream);
+/* ResUNet.forward alone (networks/DescNet.py:64-84): fills out->local_map,
+ * global_map, local_map_small (and global_feat) when non-NULL; local_point is
+ * not touched.  Eval-mode BatchNorm (folded), as PoSFeat.extract uses it. */
+int posfeat_model_backbone(posfeat_model *m, const float *img_nchw, posfeat_extract_out *out,
+                           void *ws, size_t ws_bytes, void *stream);
+/* KeypointDet.forward([x, img]) alone (networks/DeteNet.py:102-121):
+ * x_nchw = cat[local_map, local_map_small] [b][192][h/4][w/4] (the input
+ * PoSFeat.extract builds, PoSFeat_model.py:97-102), img_nchw [b][3][h][w];
+ * writes local_point [b][1][h][w]. */
+int posfeat_model_keypointdet(posfeat_model *m, const float *x_nchw, const float *img_nchw,
+                              float *local_point, void *ws, size_t ws_bytes, void *stream);
 /* Optional per-kernel timing: when enabled, extract() records hipEvents
  * around every launch; posfeat_model_timing() returns the summed ms of the
  * last call for launches whose label starts with `prefix`. */

@@ -137,6 +137,10 @@ SIGNATURES = {
     "posfeat_model_workspace": (c_size_t, [c_void_p]),
     "posfeat_model_extract": (c_int, [c_void_p, c_void_p, ctypes.POINTER(ExtractOut), c_void_p,
                                       c_size_t, c_void_p]),
+    "posfeat_model_backbone": (c_int, [c_void_p, c_void_p, ctypes.POINTER(ExtractOut), c_void_p,
+                                       c_size_t, c_void_p]),
+    "posfeat_model_keypointdet": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                          c_size_t, c_void_p]),
     "posfeat_model_set_timing": (c_int, [c_void_p, c_int]),
     "posfeat_model_timing": (c_int, [c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
                                      ctypes.POINTER(ctypes.c_double), P_int]),

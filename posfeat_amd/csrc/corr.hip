@@ -27,6 +27,12 @@ int pf_sample_desc(const float* fmap, int b, int c, int h, int w, int cs, const 
 
 namespace {
 
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
 // torch.linspace(lo, hi, n)[i] in float32 (ATen's two-sided formula)
 __device__ __forceinline__ float linspace_f(float lo, float hi, int n, int i) {
   if (n == 1) return lo;
@@ -82,26 +88,30 @@ __global__ void corr_row_kernel(const float* __restrict__ S, int nb, int n1, int
   for (int k = lane; k < n2; k += 64) mx = fmaxf(mx, T * row[k]);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
-  float se = 0.f, gx = 0.f, gy = 0.f, qx = 0.f, qy = 0.f;
+  // fp64 accumulation of the softmax moments: var = E[n^2] - E[n]^2 cancels
+  // catastrophically in fp32 when the softmax is peaked (small std); the
+  // weights e and the coordinates stay the fp32 values the reference uses
+  double se = 0.0, gx = 0.0, gy = 0.0, qx = 0.0, qy = 0.0;
   for (int k = lane; k < n2; k += 64) {
-    const float e = expf(T * row[k] - mx);
+    const double e = (double)expf(T * row[k] - mx);
+    const double nx = cn[2 * k], ny = cn[2 * k + 1];
     se += e;
-    gx += e * cp[2 * k];
-    gy += e * cp[2 * k + 1];
-    qx += e * cn[2 * k] * cn[2 * k];
-    qy += e * cn[2 * k + 1] * cn[2 * k + 1];
+    gx += e * (double)cp[2 * k];
+    gy += e * (double)cp[2 * k + 1];
+    qx += e * nx * nx;
+    qy += e * ny * ny;
   }
-  se = pf_wave_sum(se);
-  gx = pf_wave_sum(gx) / se;
-  gy = pf_wave_sum(gy) / se;
-  qx = pf_wave_sum(qx) / se;
-  qy = pf_wave_sum(qy) / se;
+  se = wave_sum_d(se);
+  gx = wave_sum_d(gx) / se;
+  gy = wave_sum_d(gy) / se;
+  qx = wave_sum_d(qx) / se;
+  qy = wave_sum_d(qy) / se;
   if (lane == 0) {
-    g[wid * 2] = gx;
-    g[wid * 2 + 1] = gy;
-    const float c0 = (float)((W2 - 1) / 2.0), c1 = (float)((H2 - 1) / 2.0);
-    const float nx = (gx - c0) / c0, ny = (gy - c1) / c1;
-    sd[wid] = sqrtf(fmaxf(qx - nx * nx, 1e-6f)) + sqrtf(fmaxf(qy - ny * ny, 1e-6f));
+    g[wid * 2] = (float)gx;
+    g[wid * 2 + 1] = (float)gy;
+    const double c0 = (W2 - 1) / 2.0, c1 = (H2 - 1) / 2.0;
+    const double nx = (gx - c0) / c0, ny = (gy - c1) / c1;
+    sd[wid] = (float)(sqrt(fmax(qx - nx * nx, 1e-6)) + sqrt(fmax(qy - ny * ny, 1e-6)));
   }
 }
 
@@ -110,8 +120,9 @@ __global__ void corr_row_kernel(const float* __restrict__ S, int nb, int n1, int
 // online max-rescaled accumulation of (sum e, e*px, e*py, e*nx^2, e*ny^2);
 // then the chunk partials are merged in order (deterministic).
 constexpr int COL_CH = 8;
-struct ColAcc {
-  float mx, se, gx, gy, qx, qy;
+struct ColAcc {  // running max (fp32, the logits' type) + fp64 moments
+  float mx;
+  double se, gx, gy, qx, qy;
 };
 
 __global__ __launch_bounds__(256) void corr_col_partial_kernel(
@@ -123,23 +134,23 @@ __global__ __launch_bounds__(256) void corr_col_partial_kernel(
   const float* Sb = S + (long long)b * n1 * n2;
   const float* cp = c1px + (long long)b * n1 * 2;
   const float* cn = c1n + (long long)b * n1 * 2;
-  ColAcc a{-INFINITY, 0.f, 0.f, 0.f, 0.f, 0.f};
+  ColAcc a{-INFINITY, 0.0, 0.0, 0.0, 0.0, 0.0};
   if (col < n2) {
     for (int m = m0 + rg; m < m1; m += 4) {
       const float v = T * Sb[(long long)m * n2 + col];
-      const float px = cp[2 * m], py = cp[2 * m + 1], nx = cn[2 * m], ny = cn[2 * m + 1];
-      float e;
+      const double px = cp[2 * m], py = cp[2 * m + 1], nx = cn[2 * m], ny = cn[2 * m + 1];
+      double e;
       if (v > a.mx) {
-        const float f = expf(a.mx - v);
+        const double f = (double)expf(a.mx - v);
         a.se *= f;
         a.gx *= f;
         a.gy *= f;
         a.qx *= f;
         a.qy *= f;
         a.mx = v;
-        e = 1.f;
+        e = 1.0;
       } else {
-        e = expf(v - a.mx);
+        e = (double)expf(v - a.mx);
       }
       a.se += e;
       a.gx += e * px;
@@ -154,10 +165,10 @@ __global__ __launch_bounds__(256) void corr_col_partial_kernel(
   if (rg == 0 && col < n2) {
     float M = sh[0][cl].mx;
     for (int r = 1; r < 4; ++r) M = fmaxf(M, sh[r][cl].mx);
-    ColAcc o{M, 0.f, 0.f, 0.f, 0.f, 0.f};
+    ColAcc o{M, 0.0, 0.0, 0.0, 0.0, 0.0};
     for (int r = 0; r < 4; ++r) {
       const ColAcc& q = sh[r][cl];
-      const float f = expf(q.mx - M);
+      const double f = (double)expf(q.mx - M);
       o.se += q.se * f;
       o.gx += q.gx * f;
       o.gy += q.gy * f;
@@ -176,10 +187,10 @@ __global__ void corr_col_final_kernel(const ColAcc* __restrict__ part, int nb, i
   const ColAcc* p = part + (long long)b * COL_CH * n2 + col;
   float M = -INFINITY;
   for (int ch = 0; ch < COL_CH; ++ch) M = fmaxf(M, p[(long long)ch * n2].mx);
-  float se = 0.f, gx = 0.f, gy = 0.f, qx = 0.f, qy = 0.f;
+  double se = 0.0, gx = 0.0, gy = 0.0, qx = 0.0, qy = 0.0;
   for (int ch = 0; ch < COL_CH; ++ch) {
     const ColAcc& q = p[(long long)ch * n2];
-    const float f = expf(q.mx - M);
+    const double f = (double)expf(q.mx - M);
     se += q.se * f;
     gx += q.gx * f;
     gy += q.gy * f;
@@ -190,11 +201,11 @@ __global__ void corr_col_final_kernel(const ColAcc* __restrict__ part, int nb, i
   gy /= se;
   qx /= se;
   qy /= se;
-  g[o * 2] = gx;
-  g[o * 2 + 1] = gy;
-  const float c0 = (float)((W1 - 1) / 2.0), c1 = (float)((H1 - 1) / 2.0);
-  const float nx = (gx - c0) / c0, ny = (gy - c1) / c1;
-  sd[o] = sqrtf(fmaxf(qx - nx * nx, 1e-6f)) + sqrtf(fmaxf(qy - ny * ny, 1e-6f));
+  g[o * 2] = (float)gx;
+  g[o * 2 + 1] = (float)gy;
+  const double c0 = (W1 - 1) / 2.0, c1 = (H1 - 1) / 2.0;
+  const double nx = (gx - c0) / c0, ny = (gy - c1) / c1;
+  sd[o] = (float)(sqrt(fmax(qx - nx * nx, 1e-6)) + sqrt(fmax(qy - ny * ny, 1e-6)));
 }
 
 // bilinear sample of a 128-channel NHWC map at normalised (x, y), align_corners
@@ -432,15 +443,19 @@ __global__ void line_window_kernel(const float* __restrict__ cpx,   // [b][n][2]
   for (int r = 0; r < MAX_WIN / 64; ++r) wm = fmaxf(wm, wl[r]);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) wm = fmaxf(wm, __shfl_xor(wm, o, 64));
-  float se = 0.f, ex = 0.f, ey = 0.f, vx = 0.f, vy = 0.f;
+  // softmax moments over the window in fp64 (get_expected_correspondence_
+  // within_window, preprocess_utils.py:745-750): the fp32 E[g^2] - E[g]^2 of
+  // the reference loses most of its digits when the window softmax is peaked;
+  // the tap coordinates g stay the fp32 values coord2_n_grid holds
+  double se = 0.0, ex = 0.0, ey = 0.0, vx = 0.0, vy = 0.0;
 #pragma unroll
   for (int r = 0; r < MAX_WIN / 64; ++r) {
     const int s = lane + 64 * r;
     if (s < nw) {
       const int iy = s / win_w, ix = s - iy * win_w;
-      const float gx = jx + linspace_f(-window_size, window_size, win_w, ix);
-      const float gy = jy + linspace_f(-window_size, window_size, win_h, iy);
-      const float e = expf(wl[r] - wm);
+      const double gx = jx + linspace_f(-window_size, window_size, win_w, ix);
+      const double gy = jy + linspace_f(-window_size, window_size, win_h, iy);
+      const double e = (double)expf(wl[r] - wm);
       se += e;
       ex += e * gx;
       ey += e * gy;
@@ -448,20 +463,20 @@ __global__ void line_window_kernel(const float* __restrict__ cpx,   // [b][n][2]
       vy += e * gy * gy;
     }
   }
-  se = pf_wave_sum(se);
-  ex = pf_wave_sum(ex) / se;
-  ey = pf_wave_sum(ey) / se;
-  vx = pf_wave_sum(vx) / se - ex * ex;
-  vy = pf_wave_sum(vy) / se - ey * ey;
+  se = wave_sum_d(se);
+  ex = wave_sum_d(ex) / se;
+  ey = wave_sum_d(ey) / se;
+  vx = wave_sum_d(vx) / se - ex * ex;
+  vy = wave_sum_d(vy) / se - ey * ey;
   if (lane == 0) {
     l_exp_n[wid * 2] = jx;
     l_exp_n[wid * 2 + 1] = jy;
     l_org_n[wid * 2] = ox;
     l_org_n[wid * 2 + 1] = oy;
     valid[wid] = ok ? 1 : 0;
-    w_px[wid * 2] = ex * c0 + c0;
-    w_px[wid * 2 + 1] = ey * c1 + c1;
-    w_std[wid] = sqrtf(fmaxf(vx, 1e-10f)) + sqrtf(fmaxf(vy, 1e-10f));
+    w_px[wid * 2] = (float)ex * c0 + c0;
+    w_px[wid * 2 + 1] = (float)ey * c1 + c1;
+    w_std[wid] = (float)(sqrt(fmax(vx, 1e-10)) + sqrt(fmax(vy, 1e-10)));
   }
 }
 

@@ -132,7 +132,7 @@ struct posfeat_model {
   // Set in plan() before the dry pass so the planning forward follows the
   // path that actually runs.
   bool side = false;
-  bool tuned_once = false;  // the first forward (autotune) runs serially
+  unsigned tuned_modes = 0;  // bit per Mode: its first forward (autotune) ran, serially
   hipStream_t side_st = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   Buf splitk2;  // the side stream's own split-K / statistics scratch
@@ -275,7 +275,14 @@ int conv(Ctx& c, const std::string& name, const float* x, int n, int h, int w, i
   return conv_desc_run(c, name, d, x, c.W(name), c.Bi(name), res, y, flops);
 }
 
-int forward(Ctx& c, const float* img, posfeat_extract_out* out);
+int head_forward(Ctx& c, float* img4, float* local_point, bool side);
+
+// what one forward computes: PoSFeat.extract (ResUNet + KeypointDet),
+// ResUNet.forward alone (DescNet.py:64-84), or KeypointDet.forward([x, img])
+// alone (DeteNet.py:102-121) with x = cat[local_map, local_map_small] given
+enum Mode { MODE_FULL = 0, MODE_BACKBONE = 1, MODE_HEAD = 2 };
+int forward(Ctx& c, const float* img, posfeat_extract_out* out, int mode = MODE_FULL,
+            const float* xhead = nullptr);
 
 // The decoder's 3x3 stride-1 convs (DescNet.py:41-45) through Winograd
 // F(2x2,3x3) when enabled (default; POSFEAT_WINO=0 for the direct conv)
@@ -606,22 +613,29 @@ int image_branch(Ctx& c, const float* img4) {
   return POSFEAT_OK;
 }
 
-int forward(Ctx& c, const float* img, posfeat_extract_out* out) {
+int forward(Ctx& c, const float* img, posfeat_extract_out* out, int mode, const float* xhead) {
   posfeat_model* m = c.m;
   const int B = m->B, H = m->H, W = m->W;
   const int h2 = H / 2, w2 = W / 2, h4 = H / 4, w4 = W / 4, h8 = H / 8, w8 = W / 8, h16 = H / 16,
             w16 = W / 16;
-  const float* slope = m->wts + specs().find("head.prelu")->b_off;
   float* img4 = c.f(m->img4);
+  float* headcat = c.f(m->headcat);
   // ---- ResUNet (DescNet.py:64-84) -----------------------------------------
   PF_TRY(timed(c, "layout:img", 0, [&] { return pf_nchw_to_nhwc(img, B, 3, H, W, 4, img4, c.st); }));
   // the first forward of a shape autotunes every main-stream conv by timing
   // it: run it serially so the side stream's kernels do not contend with
   // the candidates being timed (the tile choice would depend on that race)
-  const bool side = m->side && (c.dry || m->tuned_once || !m->autotune);
+  const bool side = m->side && mode != MODE_BACKBONE &&
+                    (c.dry || ((m->tuned_modes >> mode) & 1u) || !m->autotune);
   if (side) PF_TRY(image_branch(c, img4));
+  if (mode == MODE_HEAD) {
+    // KeypointDet's own input: fine_maps[0] = cat[local_map, local_map_small]
+    // (PoSFeat_model.py:97-102), NCHW 192 channels at H/4 x W/4
+    PF_TRY(timed(c, "layout:head_in", 0, [&] {
+      return pf_nchw_to_nhwc(xhead, B, 192, h4, w4, 192, headcat, c.st);
+    }));
+  } else {
   PF_TRY(conv(c, "firstconv", img4, B, H, W, 4, c.f(m->stem), 64, 2, POSFEAT_ACT_RELU));
-  float* headcat = c.f(m->headcat);
   PF_TRY(timed(c, "maxpool", 0, [&] {
     return pf_maxpool3s2(c.f(m->stem), B, h2, w2, 64, 64, headcat + 128, 192, c.st);
   }));
@@ -643,6 +657,39 @@ int forward(Ctx& c, const float* img, posfeat_extract_out* out) {
   PF_TRY(conv3x3(c, "upconv2.conv", c.f(m->up2), B, h4, w4, 512, cat2, 512, POSFEAT_ACT_ELU));
   PF_TRY(conv3x3(c, "iconv2", cat2, B, h4, w4, 512, c.f(m->d2), 256, POSFEAT_ACT_ELU));
   PF_TRY(conv(c, "conv_fine", c.f(m->d2), B, h4, w4, 256, headcat, 192, 1, POSFEAT_ACT_ELU));
+  }
+  if (mode != MODE_BACKBONE) PF_TRY(head_forward(c, img4, out->local_point, side));
+  // ---- outputs -------------------------------------------------------------
+  if (mode != MODE_HEAD) {
+    if (out->global_feat)
+      PF_TRY(timed(c, "global_feat", 0, [&] {
+        return pf_global_feat(c.f(m->gmap), B, h16 * w16, 128, out->global_feat, c.st);
+      }));
+    if (out->local_map)
+      PF_TRY(timed(c, "layout:out", 0, [&] {
+        return pf_nhwc_to_nchw(headcat, B, 128, h4, w4, 192, out->local_map, c.st);
+      }));
+    if (out->local_map_small)
+      PF_TRY(timed(c, "layout:out", 0, [&] {
+        return pf_nhwc_to_nchw(headcat + 128, B, 64, h4, w4, 192, out->local_map_small, c.st);
+      }));
+    if (out->global_map)
+      PF_TRY(timed(c, "layout:out", 0, [&] {
+        return pf_nhwc_to_nchw(c.f(m->gmap), B, 128, h16, w16, 128, out->global_map, c.st);
+      }));
+  }
+  out->local_map_nhwc = headcat;
+  out->local_map_cstride = 192;
+  return POSFEAT_OK;
+}
+
+// KeypointDet (DeteNet.py:102-121) on headcat = cat[local_map, local_map_small]
+// and the NHWC4 image; `side`: the image branch was forked to the side stream
+int head_forward(Ctx& c, float* img4, float* local_point, bool side) {
+  posfeat_model* m = c.m;
+  const int B = m->B, H = m->H, W = m->W, h4 = H / 4, w4 = W / 4;
+  const float* slope = m->wts + specs().find("head.prelu")->b_off;
+  float* headcat = c.f(m->headcat);
   // ---- KeypointDet (DeteNet.py:102-121), identity prior == exact 1.0 -------
   // IN statistics slots: conv1, convimg, conv2 (the backward reads all three)
   const size_t SL = (size_t)B * 256;
@@ -773,22 +820,9 @@ int forward(Ctx& c, const float* img, posfeat_extract_out* out) {
   }
   PF_TRY(timed(c, "head_tail", 2.0 * B * H * W * 128, [&] {
     return pf_head_tail(c2, B, H * W, 128, mean, rstd, slope, c.W("head.conv3"),
-                        c.Bi("head.conv3"), c.f(m->yraw), out->local_point, c.f(m->st_mean1),
+                        c.Bi("head.conv3"), c.f(m->yraw), local_point, c.f(m->st_mean1),
                         c.f(m->st_rstd1), part, c.st);
   }));
-  // ---- outputs -------------------------------------------------------------
-  if (out->global_feat)
-    PF_TRY(timed(c, "global_feat", 0, [&] { return pf_global_feat(c.f(m->gmap), B, h16 * w16, 128, out->global_feat, c.st); }));
-  if (out->local_map)
-    PF_TRY(timed(c, "layout:out", 0, [&] { return pf_nhwc_to_nchw(headcat, B, 128, h4, w4, 192, out->local_map, c.st); }));
-  if (out->local_map_small)
-    PF_TRY(timed(c, "layout:out", 0, [&] {
-      return pf_nhwc_to_nchw(headcat + 128, B, 64, h4, w4, 192, out->local_map_small, c.st);
-    }));
-  if (out->global_map)
-    PF_TRY(timed(c, "layout:out", 0, [&] { return pf_nhwc_to_nchw(c.f(m->gmap), B, 128, h16, w16, 128, out->global_map, c.st); }));
-  out->local_map_nhwc = headcat;
-  out->local_map_cstride = 192;
   return POSFEAT_OK;
 }
 
@@ -951,7 +985,37 @@ extern "C" int posfeat_model_extract(posfeat_model* m, const float* img_nchw,
   Ctx c{m, static_cast<char*>(ws), pf_stream(stream)};
   m->ev_used = 0;
   const int r = forward(c, img_nchw, out);
-  if (r == POSFEAT_OK) m->tuned_once = true;
+  if (r == POSFEAT_OK) m->tuned_modes |= 1u << MODE_FULL;
+  return r;
+}
+
+extern "C" int posfeat_model_backbone(posfeat_model* m, const float* img_nchw,
+                                      posfeat_extract_out* out, void* ws, size_t ws_bytes,
+                                      void* stream) {
+  if (!m || !img_nchw || !out || !ws || m->train) return m && m->train ? POSFEAT_E_UNSUPPORTED
+                                                                        : POSFEAT_E_INVALID;
+  if (ws_bytes < m->ws_bytes) return POSFEAT_E_WORKSPACE;
+  if (reinterpret_cast<uintptr_t>(ws) & 255) return POSFEAT_E_INVALID;
+  Ctx c{m, static_cast<char*>(ws), pf_stream(stream)};
+  m->ev_used = 0;
+  const int r = forward(c, img_nchw, out, MODE_BACKBONE);
+  if (r == POSFEAT_OK) m->tuned_modes |= 1u << MODE_BACKBONE;
+  return r;
+}
+
+extern "C" int posfeat_model_keypointdet(posfeat_model* m, const float* x_nchw,
+                                         const float* img_nchw, float* local_point, void* ws,
+                                         size_t ws_bytes, void* stream) {
+  if (!m || !x_nchw || !img_nchw || !local_point || !ws) return POSFEAT_E_INVALID;
+  if (m->train) return POSFEAT_E_UNSUPPORTED;
+  if (ws_bytes < m->ws_bytes) return POSFEAT_E_WORKSPACE;
+  if (reinterpret_cast<uintptr_t>(ws) & 255) return POSFEAT_E_INVALID;
+  Ctx c{m, static_cast<char*>(ws), pf_stream(stream)};
+  m->ev_used = 0;
+  posfeat_extract_out o{};
+  o.local_point = local_point;
+  const int r = forward(c, img_nchw, &o, MODE_HEAD, x_nchw);
+  if (r == POSFEAT_OK) m->tuned_modes |= 1u << MODE_HEAD;
   return r;
 }
 

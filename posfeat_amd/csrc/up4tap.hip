@@ -37,7 +37,6 @@ constexpr int TAP_CO = 128;              // head.conv2 output channels
 constexpr int TAP_N = 9 * TAP_CO;        // P channels: tap-major, channel-minor
 constexpr int TAP_KP2 = 256 * 9;         // head.conv2 packed K (Cin 256, 3x3)
 constexpr int TQ = 4;                    // low-res rows per combine block
-constexpr int TXC = 4;                   // full-res columns per combine block
 
 // Wt[k * 128 + co][ci] = W2[co][ci][ky][kx] for ci < 192, from the engine's
 // packed conv2 weights (K order (cin/32, kh, kw, cin%32), conv.hip).
@@ -64,28 +63,66 @@ __device__ __forceinline__ void up4_w(int d, int& lo, float& wa, float& wb) {
   }
 }
 
-// Block = (4 full-res columns, 4 low-res rows = 16 full-res rows, image);
-// wave = one column X = 4 qx + rx, lane = 2 channels (64 lanes x 8 B = one
-// 512-B pixel row: every P / y access of a wave is one contiguous row).  The
-// thread forms R_ky(iy) = sum_kx [X + kx - 1 in image] (wa P_k[iy][ia] +
-// wb P_k[iy][ib]) for the three low-res rows iy = q-1, q, q+1 of a sliding
-// window, then y[4q + r][X] += sum_ky [4q + r + ky - 1 in image]
-// (wa R_ky(q+lo) + wb R_ky(q+lo+1)).  Two channels per lane keep the window,
-// the 18 in-flight tap loads and the fp64 statistics under 128 VGPRs
-// (>= 4 waves per SIMD: the kernel is HBM-bound on the y read-modify-write).
-typedef float f32x2 __attribute__((ext_vector_type(2)));
+// Block = (image, 4 low-res rows = 16 output rows, 8 low-res columns = 32
+// output columns, 32-channel group); thread = (output column X, channel quad).
+// Phase 1 stages the P tile the block needs -- low-res rows q0-1 .. q0+4,
+// columns qx0-1 .. qx0+8, 9 taps, 32 channels (69 KB) -- into LDS with every
+// load independent (17 float4 per thread) and, in the same burst, loads the 16
+// y values the thread will update: the HBM latency is paid once per block.
+// Phase 2 walks the low-res rows with a sliding window of the x-interpolated
+// taps R_ky(iy) = sum_kx [X + kx - 1 in image] (wa P_k[iy][ia] + wb P_k[iy][ib])
+// (conflict-free ds_read_b128: a wave reads 2 low-res columns x 128 B), and
+// y[4q + r][X] += sum_ky [4q + r + ky - 1 in image] (wa R_ky(q+lo) + wb R_ky(q+lo+1)).
+constexpr int CB_QX = 8, CB_CG = 32, CB_RY = TQ + 2, CB_CX = CB_QX + 2;
+constexpr int CB_SEG = CB_RY * CB_CX * 9;  // 128-B (32-channel) segments per block
+constexpr int CB_SEGP = (CB_SEG + 7) / 8 * 8;  // padded to whole DMA wave-instructions
 
 __global__ __launch_bounds__(256) void up4tap_combine_kernel(const float* __restrict__ P, int h,
                                                              int w, float* __restrict__ y, int ycs,
                                                              double* __restrict__ part) {
-  __shared__ double red[TXC][64][4];
+  __shared__ __attribute__((aligned(16))) float sp[CB_SEGP * CB_CG];
   const int H = 4 * h, W = 4 * w;
-  const int c2 = threadIdx.x & 63, xl = threadIdx.x >> 6;
-  const int X = blockIdx.x * TXC + xl;
-  const int q0 = blockIdx.y * TQ;
-  const int b = blockIdx.z;
-  const int qx = X >> 2, rx = X & 3;
-  // column taps: source columns (clamped) and weights, 0 weight for padding
+  const int tid = threadIdx.x;
+  const int c4 = tid & 7, xl = tid >> 3;  // 8 channel quads x 32 output columns
+  const int nxb = (w + CB_QX - 1) / CB_QX, nqb = h / TQ, ncg = TAP_CO / CB_CG;
+  int id = blockIdx.x;
+  const int cg = id % ncg;
+  id /= ncg;
+  const int xb = id % nxb;
+  id /= nxb;
+  const int qb = id % nqb, b = id / nqb;
+  const int q0 = qb * TQ, qx0 = xb * CB_QX;
+  const int X = qx0 * 4 + xl, qx = X >> 2, rx = X & 3;
+  const bool xok = X < W;  // the last column block may be ragged (w % 8 != 0)
+  // ---- phase 1: P tile -> LDS by DMA (global_load_lds: no VGPR round trip,
+  // every request independent), y -> registers -----------------------------
+  // wave-instruction j fills segments 8j .. 8j+7 (lane L: segment 8j + L/8,
+  // 16-B piece L%8); the LDS image is segment-contiguous, i.e. lane-linear
+  const float* Pb = P + (long long)b * h * w * TAP_N + cg * CB_CG;
+  {
+    const int lane = tid & 63, wv = tid >> 6;
+    for (int j = wv; j < CB_SEGP / 8; j += 4) {
+      int seg = j * 8 + (lane >> 3);
+      seg = min(seg, CB_SEG - 1);  // pad segments of the last instruction re-read a valid one
+      const int k = seg % 9, cell = seg / 9;
+      const int cx = cell % CB_CX, ry = cell / CB_CX;
+      const int iy = min(max(q0 - 1 + ry, 0), h - 1), ix = min(max(qx0 - 1 + cx, 0), w - 1);
+      const float* src = Pb + ((long long)iy * w + ix) * TAP_N + k * TAP_CO + (lane & 7) * 4;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(sp + j * 8 * CB_CG),
+                                       16, 0, 0);
+    }
+  }
+  float* yb = y + ((long long)b * H * W + min(X, W - 1)) * ycs + cg * CB_CG + c4 * 4;
+  const long long yrow = (long long)W * ycs;
+  f32x4 o[TQ][4];
+#pragma unroll
+  for (int i = 0; i < TQ; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      o[i][r] = xok ? *reinterpret_cast<const f32x4*>(yb + (4 * (q0 + i) + r) * yrow)
+                    : f32x4{0.f, 0.f, 0.f, 0.f};
+  // column taps: LDS columns (tile-relative) and weights, 0 weight for padding
   int cola[3], colb[3];
   float wxa[3], wxb[3];
 #pragma unroll
@@ -94,62 +131,56 @@ __global__ __launch_bounds__(256) void up4tap_combine_kernel(const float* __rest
     up4_w(rx + kx - 1, lo, wxa[kx], wxb[kx]);
     const int u = X + kx - 1;
     if (u < 0 || u >= W) wxa[kx] = wxb[kx] = 0.f;
-    cola[kx] = min(max(qx + lo, 0), w - 1) * TAP_N;
-    colb[kx] = min(max(qx + lo + 1, 0), w - 1) * TAP_N;
+    // clamped source column, expressed in tile coordinates (the tile's own
+    // clamped columns hold the same data)
+    cola[kx] = min(max(min(qx + lo, w - 1), 0) - (qx0 - 1), CB_CX - 1);
+    colb[kx] = min(max(min(qx + lo + 1, w - 1), 0) - (qx0 - 1), CB_CX - 1);
   }
-  const float* Pb = P + (long long)b * h * w * TAP_N + c2 * 2;
-  auto rowR = [&](int iy, f32x2 (&R)[3]) {
-    iy = min(max(iy, 0), h - 1);
-    const float* pr = Pb + (long long)iy * w * TAP_N;
+  __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA has landed (y too)
+  __syncthreads();                 // ... and every other wave's
+  // ---- phase 2 --------------------------------------------------------------
+  auto rowR = [&](int ry, f32x4 (&R)[3]) {  // ry: tile row (iy = q0 - 1 + ry)
 #pragma unroll
     for (int ky = 0; ky < 3; ++ky) {
-      f32x2 s = {0.f, 0.f};
+      f32x4 s = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kx = 0; kx < 3; ++kx) {
         const int k = ky * 3 + kx;
-        const f32x2 pa = *reinterpret_cast<const f32x2*>(pr + cola[kx] + k * TAP_CO);
-        const f32x2 pb = *reinterpret_cast<const f32x2*>(pr + colb[kx] + k * TAP_CO);
+        const f32x4 pa = *reinterpret_cast<const f32x4*>(
+            sp + ((ry * CB_CX + cola[kx]) * 9 + k) * CB_CG + c4 * 4);
+        const f32x4 pb = *reinterpret_cast<const f32x4*>(
+            sp + ((ry * CB_CX + colb[kx]) * 9 + k) * CB_CG + c4 * 4);
         s += wxa[kx] * pa + wxb[kx] * pb;
       }
       R[ky] = s;
     }
   };
-  // all 16 y values of this thread are loaded up front: the HBM latency of
-  // the read-modify-write is paid once per block, under the tap loads
-  float* yb = y + (long long)b * H * W * ycs + (long long)X * ycs + c2 * 2;
-  const long long yrow = (long long)W * ycs;
-  f32x2 o[TQ][4];
-#pragma unroll
-  for (int i = 0; i < TQ; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      o[i][r] = *reinterpret_cast<const f32x2*>(yb + (4 * (q0 + i) + r) * yrow);
-  f32x2 Rm[3], R0[3], Rp[3];
-  rowR(q0 - 1, Rm);
-  rowR(q0, R0);
-  double s1[2] = {0, 0}, s2[2] = {0, 0};
+  f32x4 Rm[3], R0[3], Rp[3];
+  rowR(0, Rm);
+  rowR(1, R0);
+  double s1[4] = {0, 0, 0, 0}, s2[4] = {0, 0, 0, 0};
 #pragma unroll
   for (int i = 0; i < TQ; ++i) {
-    const int q = q0 + i;
-    rowR(q + 1, Rp);
+    rowR(i + 2, Rp);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int Y = 4 * q + r;
+      const int Y = 4 * (q0 + i) + r;
 #pragma unroll
       for (int ky = 0; ky < 3; ++ky) {
         const int v = Y + ky - 1;
-        if (v < 0 || v >= H) continue;
         int lo;
         float wa, wb;
         up4_w(r + ky - 1, lo, wa, wb);
+        if (v < 0 || v >= H) wa = wb = 0.f;  // conv2's zero padding
         if (lo < 0)
           o[i][r] += wa * Rm[ky] + wb * R0[ky];
         else
           o[i][r] += wa * R0[ky] + wb * Rp[ky];
       }
-      *reinterpret_cast<f32x2*>(yb + Y * yrow) = o[i][r];
+      if (!xok) continue;
+      *reinterpret_cast<f32x4*>(yb + Y * yrow) = o[i][r];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
+      for (int j = 0; j < 4; ++j) {
         s1[j] += (double)o[i][r][j];
         s2[j] += (double)o[i][r][j] * (double)o[i][r][j];
       }
@@ -161,23 +192,23 @@ __global__ __launch_bounds__(256) void up4tap_combine_kernel(const float* __rest
     }
   }
   if (!part) return;
-  red[xl][c2][0] = s1[0];
-  red[xl][c2][1] = s1[1];
-  red[xl][c2][2] = s2[0];
-  red[xl][c2][3] = s2[1];
-  __syncthreads();
-  if (xl != 0) return;
-  double a[4] = {0, 0, 0, 0};
-  for (int r = 0; r < TXC; ++r)
+  // ---- statistics: reduce the 32 columns of each channel (fixed order) -------
+  __syncthreads();  // LDS reuse
+  double* red = reinterpret_cast<double*>(sp);  // [32 columns][32 channels][2]
 #pragma unroll
-    for (int k = 0; k < 4; ++k) a[k] += red[r][c2][k];
-  const long long chunk = (long long)blockIdx.y * gridDim.x + blockIdx.x;
-  const long long nchunk = (long long)gridDim.x * gridDim.y;
-  double* dst = part + (((long long)b * nchunk + chunk) * TAP_CO + c2 * 2) * 2;
-  dst[0] = a[0];
-  dst[1] = a[2];
-  dst[2] = a[1];
-  dst[3] = a[3];
+  for (int j = 0; j < 4; ++j) {
+    red[(xl * CB_CG + c4 * 4 + j) * 2] = s1[j];
+    red[(xl * CB_CG + c4 * 4 + j) * 2 + 1] = s2[j];
+  }
+  __syncthreads();
+  if (tid < 2 * CB_CG) {
+    const int c = tid >> 1, which = tid & 1;
+    double a = 0.0;
+    for (int x = 0; x < 32; ++x) a += red[(x * CB_CG + c) * 2 + which];
+    const long long chunk = (long long)qb * nxb + xb;
+    const long long nchunk = (long long)nxb * nqb;
+    part[(((long long)b * nchunk + chunk) * TAP_CO + cg * CB_CG + c) * 2 + which] = a;
+  }
 }
 
 }  // namespace
@@ -185,7 +216,7 @@ __global__ __launch_bounds__(256) void up4tap_combine_kernel(const float* __rest
 size_t pf_up4tap_weights_floats() { return (size_t)TAP_N * TAP_CU; }
 size_t pf_up4tap_p_floats(int n, int H, int W) { return (size_t)n * (H / 4) * (W / 4) * TAP_N; }
 size_t pf_up4tap_part_bytes(int n, int H, int W) {
-  return (size_t)n * ((H / 4) / TQ) * (W / TXC) * TAP_CO * 2 * sizeof(double);
+  return (size_t)n * ((H / 4) / TQ) * ((W / 4 + CB_QX - 1) / CB_QX) * TAP_CO * 2 * sizeof(double);
 }
 
 int pf_up4tap_weights(const float* w2_packed, float* wt, hipStream_t st) {
@@ -197,16 +228,16 @@ int pf_up4tap_weights(const float* w2_packed, float* wt, hipStream_t st) {
 
 // y (n x H x W x 128, pitch ycs) += the upsampled part of head.conv2 from the
 // nine tap maps P (n x H/4 x W/4 x 1152); mean/rstd (optional) = the
-// instance-norm statistics of the resulting y.  H/4 % 4 == 0, W % 8 == 0.
+// instance-norm statistics of the resulting y.  H, W % 16 == 0.
 int pf_up4tap_combine(int n, int H, int W, const float* P, float* y, int ycs, double* part,
                       float* mean, float* rstd, hipStream_t st) {
   const int h = H / 4, w = W / 4;
-  if (H % 16 || W % TXC || ycs % 4 || n <= 0) return POSFEAT_E_INVALID;
+  if (H % 16 || W % 16 || ycs % 4 || n <= 0) return POSFEAT_E_INVALID;
   if (mean && !part) return POSFEAT_E_INVALID;
-  const dim3 grid(W / TXC, h / TQ, n);
-  hipLaunchKernelGGL(up4tap_combine_kernel, grid, dim3(256), 0, st, P, h, w, y, ycs,
-                     mean ? part : nullptr);
+  const int nchunk = (h / TQ) * ((w + CB_QX - 1) / CB_QX);
+  hipLaunchKernelGGL(up4tap_combine_kernel, dim3(n * nchunk * (TAP_CO / CB_CG)), dim3(256), 0, st,
+                     P, h, w, y, ycs, mean ? part : nullptr);
   PF_CHECK_LAUNCH();
-  if (mean) PF_TRY(pf_in_finalize(part, n, (int)(grid.x * grid.y), H * W, TAP_CO, mean, rstd, st));
+  if (mean) PF_TRY(pf_in_finalize(part, n, nchunk, H * W, TAP_CO, mean, rstd, st));
   return POSFEAT_OK;
 }

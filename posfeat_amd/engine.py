@@ -110,6 +110,52 @@ class ExtractionEngine:
             b, h // 4, w // 4, cs)
         return res
 
+    def run_backbone(self, img, outputs=("local_map", "global_map", "local_map_small")):
+        """ResUNet.forward alone (DescNet.py:64-84): NCHW maps of img [b,3,h,w]."""
+        img, (handle, ws, off), b, h, w = self._prep(img)
+        dev = img.device
+        res = {}
+        if "local_map" in outputs:
+            res["local_map"] = torch.empty(b, 128, h // 4, w // 4, device=dev)
+        if "global_map" in outputs:
+            res["global_map"] = torch.empty(b, 128, h // 16, w // 16, device=dev)
+        if "global_feat" in outputs:
+            res["global_feat"] = torch.empty(b, 128, device=dev)
+        if "local_map_small" in outputs:
+            res["local_map_small"] = torch.empty(b, 64, h // 4, w // 4, device=dev)
+        o = _lib.ExtractOut()
+        for k in ("local_map", "global_map", "global_feat", "local_map_small"):
+            setattr(o, k, res[k].data_ptr() if k in res else None)
+        check(lib().posfeat_model_backbone(handle, ptr(img), ctypes.byref(o),
+                                           ctypes.c_void_p(ws.data_ptr() + off),
+                                           ws.numel() - off, stream_ptr()))
+        return res
+
+    def run_keypointdet(self, x, img):
+        """KeypointDet.forward([x, img]) alone (DeteNet.py:102-121): x =
+        cat[local_map, local_map_small] [b,192,h/4,w/4], img [b,3,h,w] ->
+        local_point [b,1,h,w]."""
+        img, (handle, ws, off), b, h, w = self._prep(img)
+        x = x.float().contiguous()
+        _lib.require_device(x)
+        if tuple(x.shape) != (b, 192, h // 4, w // 4):
+            raise ValueError("x must be [b,192,h/4,w/4] = cat[local_map, local_map_small]")
+        lp = torch.empty(b, 1, h, w, device=img.device)
+        check(lib().posfeat_model_keypointdet(handle, ptr(x), ptr(img), ptr(lp),
+                                              ctypes.c_void_p(ws.data_ptr() + off),
+                                              ws.numel() - off, stream_ptr()))
+        return lp
+
+    def _prep(self, img):
+        if img.dtype != torch.float32 or img.dim() != 4 or img.shape[1] != 3:
+            raise ValueError("img must be float32 [b,3,h,w]")
+        img = img.contiguous()
+        _lib.require_device(img)
+        b, _, h, w = img.shape
+        if h % 16 or w % 16:
+            raise ValueError("image height/width must be multiples of 16 (datasets crop to /16)")
+        return img, self._instance(b, h, w), b, h, w
+
     # ------------------------------------------------------------ training
     @property
     def head_offset(self):
@@ -156,22 +202,49 @@ class ExtractionEngine:
             pass
 
 
-_BB_CACHE = {}
+def _module_key(module, device):
+    return (id(module), tuple(p._version for p in module.state_dict(keep_vars=True).values()),
+            str(device))
+
+
+class _ModuleEngines:
+    """One ExtractionEngine per (module, parameter versions, device): rebuilt
+    (weights re-packed) only when the module's parameters change."""
+
+    def __init__(self):
+        self._c = {}
+
+    def get(self, module, device, make):
+        key = _module_key(module, device)
+        eng = self._c.get(key)
+        if eng is None:
+            for k in [k for k in self._c if k[0] == id(module)]:
+                self._c.pop(k).close()
+            eng = make()
+            self._c[key] = eng
+        return eng
+
+
+_BB = _ModuleEngines()
+_KD = _ModuleEngines()
 
 
 def backbone_forward(module, x):
-    """ResUNet.forward through the engine (DescNet.py:64-84 outputs).  The head
-    runs with zero weights and its outputs are discarded."""
-    from . import weights
-    key = (id(module), tuple(p._version for p in module.state_dict(keep_vars=True).values()),
-           str(x.device))
-    eng = _BB_CACHE.get(key)
-    if eng is None:
-        for k in [k for k in _BB_CACHE if k[0] == id(module)]:
-            del _BB_CACHE[k]
-        zero_head = {k: torch.zeros(s) for k, s in weights.head_param_shapes()}
-        eng = ExtractionEngine(module.state_dict(), zero_head, device=x.device)
-        _BB_CACHE[key] = eng
-    out = eng.run(x.float(), outputs=("local_map", "global_map", "local_map_small"))
-    return {"global_map": out["global_map"], "local_map": out["local_map"],
-            "local_map_small": out["local_map_small"]}
+    """ResUNet.forward through the engine's backbone-only mode (DescNet.py:64-84
+    outputs); KeypointDet is not run."""
+    if module.training:
+        raise NotImplementedError(
+            "train-mode (batch-statistics BN) ResUNet.forward runs in training.BackboneTrainer; "
+            "call .eval() for the eval-mode forward")
+    eng = _BB.get(module, x.device, lambda: ExtractionEngine(
+        module.state_dict(), {k: torch.zeros(s) for k, s in weights.head_param_shapes()},
+        device=x.device))
+    return eng.run_backbone(x.float())
+
+
+def keypointdet_forward(module, x, img):
+    """KeypointDet.forward([x, img]) through the engine's head-only mode."""
+    eng = _KD.get(module, img.device, lambda: ExtractionEngine(
+        {k: torch.zeros(s) for k, s in weights.backbone_param_shapes()}, module.state_dict(),
+        device=img.device))
+    return eng.run_keypointdet(x, img.float())

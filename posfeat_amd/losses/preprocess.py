@@ -88,6 +88,7 @@ class Preprocess_Line2Window(nn.Module):
                                         ptr(rand1), ptr(rand2), T, g,
                                         float(self.config["window_size"]), self.line_step,
                                         ctypes.byref(o), ptr(ws), need, stream_ptr()))
+        self.last_raw = res   # the kernel's raw outputs (line centres etc.), for diagnostics
         c1 = torch.tensor([(w2i - 1) / 2.0, (h2i - 1) / 2.0], device=dev)
         return {
             "coord1": res["coord1"], "coord2": res["coord2"],

@@ -2,8 +2,9 @@
 
 Same constructor and 9-key state dict.  The configuration used by every
 reference config (in_channels=192, out_channels=1, prior='identity',
-act='Softplus') runs inside the fused HIP engine via PoSFeat.extract; other
-priors/activations raise NotImplementedError.
+act='Softplus') runs in the HIP engine: fused with the backbone via
+PoSFeat.extract, or standalone here (``forward([x, img])``, the engine's
+head-only mode); other priors/activations raise NotImplementedError.
 """
 import torch.nn as nn
 
@@ -23,6 +24,10 @@ class KeypointDet(nn.Module):
         self.load_state_dict(hd)
 
     def forward(self, fine_maps):
-        raise NotImplementedError(
-            "KeypointDet runs fused with the backbone in the HIP engine: call "
-            "PoSFeat.extract(img) (networks/PoSFeat_model.py:91-134)")
+        """fine_maps = [x, img]: x = cat[local_map, local_map_small] [b,192,h/4,w/4],
+        img [b,3,h,w] -> score map [b,1,h,w] (DeteNet.py:102-121; the identity
+        prior multiplies by exactly 1).  Eval only: gradients come from the
+        engine's head backward (training.KeypointTrainStep)."""
+        from ..engine import keypointdet_forward
+        x, img = fine_maps[0], fine_maps[1]
+        return keypointdet_forward(self, x, img)

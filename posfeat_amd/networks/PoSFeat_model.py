@@ -122,7 +122,7 @@ class PoSFeat:
                 "train-mode (batch-statistics BN) extraction is not implemented; call set_eval()")
         if tensor.device.type != "cuda":
             tensor = tensor.to(self.device)
-        out = self.engine().run(tensor.float())
+        out = self.engine().run(tensor.float(), outputs=("local_map", "global_map", "global_feat"))
         b, _, h, w = out["global_map"].shape
         g_map = torch.ones(b, 1, h, w, device=tensor.device, dtype=torch.float32)
         res = ExtractOutputs(

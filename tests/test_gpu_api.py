@@ -84,6 +84,31 @@ def test_resunet_forward(gpu, model):
         assert err <= 1e-4 * max(1.0, ref[k].abs().max().item()), k
 
 
+def test_keypointdet_forward_standalone(gpu, model):
+    """KeypointDet.forward([x, img]) on its own (DeteNet.py:102-121; the engine's
+    head-only mode): x = cat[local_map, local_map_small] of the REFERENCE's
+    backbone run (golden), so the head is checked against the reference head."""
+    from posfeat_amd.weights import seeded_image
+    d = np.load(os.path.join(GOLDEN, "model_small.npz"))
+    for tag, hw, seed in (("a", (96, 128), 0), ("b", (64, 96), 1)):
+        img = torch.from_numpy(seeded_image(seed, *hw))[None].to(gpu)
+        x = torch.from_numpy(np.concatenate([d[tag + "_local_map"], d[tag + "_local_map_small"]],
+                                            1)).to(gpu)
+        lp = model.localheader([x, img])
+        ref = d[tag + "_local_point"]
+        assert lp.shape == ref.shape
+        err = np.abs(lp.cpu().numpy() - ref).max()
+        assert err <= 1e-4 * max(1.0, np.abs(ref).max()), (tag, err)
+    # and it equals the fused PoSFeat.extract path on the same inputs
+    img = torch.from_numpy(seeded_image(3, 96, 128))[None].to(gpu)
+    full = model.extract(img)
+    bbo = model.backbone(img)
+    x = torch.cat([bbo["local_map"], bbo["local_map_small"]], 1)
+    lp = model.localheader([x, img])
+    assert (lp - full["local_point"]).abs().max().item() <= 1e-5 * max(
+        1.0, full["local_point"].abs().max().item())
+
+
 def test_preprocess_utils_dropins(gpu):
     from oracle import detect_ref
     from posfeat_amd.losses import preprocess_utils as pu
