@@ -330,7 +330,7 @@ def main():
     if os.path.exists(tfile):
         try:
             t = json.load(open(tfile))
-            if t.get("label") == dom and t.get("batch") == args.batch:
+            if dom in t.get("labels", []) and t.get("batch") == args.batch:
                 traffic = t.get("bytes_per_launch")
         except Exception:
             traffic = None

@@ -24,7 +24,9 @@ def load(path):
             out.append((name, b if int(gy) <= 1 else "%dx%d" % (b, int(gy)), int(wx), int(dur)))
         return out
     for r in csv.DictReader(open(path)):
-        out.append((r["Kernel_Name"], int(r["Grid_Size_X"]) // max(1, int(r["Workgroup_Size_X"])),
+        b = int(r["Grid_Size_X"]) // max(1, int(r["Workgroup_Size_X"]))
+        gy = int(r.get("Grid_Size_Y", 1) or 1) // max(1, int(r.get("Workgroup_Size_Y", 1) or 1))
+        out.append((r["Kernel_Name"], b if gy <= 1 else "%dx%d" % (b, gy),
                     int(r["Workgroup_Size_X"]),
                     int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
     return out

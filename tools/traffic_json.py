@@ -43,7 +43,8 @@ def main():
     # phase weights (16 x 128 x 1728)
     alg = float(sys.argv[5]) if len(sys.argv) > 5 else (
         batch * (120 * 160 * 192 + 2 * 480 * 640 * 128) * 4 + 16 * 128 * 1728 * 4)
-    rec = {"kernel": kernel, "filters": FILTERS,
+    labels = [l for l in os.environ.get("LABELS", "").split(",") if l]
+    rec = {"kernel": kernel, "filters": FILTERS, "labels": labels,
            "probe": os.environ.get("PROBE", "tools/up4_probe.py") + " (B=%d, 480x640)" % batch,
            "batch": batch, "fetch_kb_raw": f_kb, "write_kb": w_kb,
            "bytes_per_launch": total, "bytes_per_launch_per_image": total / batch,
