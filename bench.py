@@ -63,12 +63,14 @@ def parse():
     p.add_argument("--timing-steps", type=int, default=3)
     p.add_argument("--master-port", type=int, default=0,
                    help="rendezvous port for the --gpus N launcher (0: pick a free one)")
-    p.add_argument("--workload", choices=("extract", "train_kp", "train_desc", "stub"),
+    p.add_argument("--workload", choices=("extract", "train_kp", "train_desc", "corr", "stub"),
                    default="extract",
                    help="extract: configs[1] (the metric); train_kp: configs[4], the keypoint-"
                         "head training step (DiskLoss); train_desc: configs[2], the descriptor "
                         "training step (backbone, Line2Window + EpipolarLoss, Adam); training "
-                        "workloads use --batch pairs per GPU; stub: a CPU-only step over "
+                        "workloads use --batch pairs per GPU; corr: the correlation losses of "
+                        "configs[2] and [4] (Line2Window + EpipolarLoss and DiskLoss, value + "
+                        "map gradients) on synthetic maps; stub: a CPU-only step over "
                         "gloo that tests the launcher and the timing protocol")
     return p.parse_args()
 
@@ -284,6 +286,8 @@ def main():
         return train_main(args, world, rank, dev)
     if args.workload == "train_desc":
         return train_desc_main(args, world, rank, dev)
+    if args.workload == "corr":
+        return corr_main(args, world, rank, dev)
     from posfeat_amd import ops
     import torch.distributed as dist
     engine = build_engine(world, rank, dev)
@@ -533,6 +537,93 @@ def train_desc_main(args, world, rank, dev):
         }
         print(json.dumps(rec), flush=True)
     if world > 1:
+        dist.destroy_process_group()
+
+
+# ----------------------------------------------------------------------------
+# correlation losses of the two training configs, forward + map gradients
+def corr_main(args, world, rank, dev):
+    """One step = for b pairs of synthetic 480x640 local maps / score maps:
+    Preprocess_Line2Window + EpipolarLoss_full and their gradient w.r.t. both
+    local maps (configs[2]: training.DescriptorLossGrad), and DiskLoss with its
+    gradient w.r.t. both score maps (configs[4]: KeypointTrainStep.loss_and_grad;
+    flash path, S never stored).  Roofline: DiskLoss's flash LSE pass (the
+    fused MFMA similarity + online logsumexp, 2 b n^2 128 FLOP, n = 4800),
+    timed with HIP events on the stream it runs on."""
+    import ctypes
+    from posfeat_amd import _lib, ops
+    from posfeat_amd.correlation import synthetic_fundamental
+    from posfeat_amd.training import (DESC_EPI_DEFAULTS, DESC_PRE_DEFAULTS, DescriptorLossGrad,
+                                      KeypointTrainStep)
+    b = args.batch
+    g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    # local maps: smooth random fields (as the oracle fixtures use), NHWC
+    xf = torch.randn(2 * b, 128, H // 4, W // 4, device=dev, generator=g)
+    xf = torch.nn.functional.avg_pool2d(xf, 3, 1, 1)
+    lm = ops.nchw_to_nhwc(xf.contiguous())
+    x1, x2 = lm[:b], lm[b:]
+    kp = torch.rand(2 * b, 1, H, W, device=dev, generator=g) * 3
+    F1, F2 = [torch.from_numpy(f).to(dev) for f in synthetic_fundamental(b, H, W, 300 + rank)]
+    desc = DescriptorLossGrad(DESC_PRE_DEFAULTS, DESC_EPI_DEFAULTS)
+    disk = KeypointTrainStep.__new__(KeypointTrainStep)
+    from posfeat_amd.training import DISK_DEFAULTS
+    disk.cfg, disk._ws = dict(DISK_DEFAULTS), {}
+    torch.manual_seed(77 + rank)
+
+    def one():
+        desc(x1, x2, F1, F2, (H, W), (H, W), epoch=1)
+        disk.loss_and_grad(kp, lm, F1, F2, epoch=1)
+    for _ in range(args.warmup):
+        one()
+    el = timed_loop(world, args.steps, one, torch.cuda.synchronize)
+    # dominant MFMA kernel: the flash LSE pass on this step's descriptors
+    n = (H // 8) * (W // 8)
+    fa = torch.nn.functional.normalize(torch.randn(b, n, 128, device=dev, generator=g), dim=-1)
+    fb = torch.nn.functional.normalize(torch.randn(b, n, 128, device=dev, generator=g), dim=-1)
+    lse = torch.empty(b, n, device=dev)
+    L = _lib.lib()
+    need = L.posfeat_disk_flash_lse_workspace(b, n)
+    ws = torch.empty(need, dtype=torch.uint8, device=dev)
+
+    def lse_pass():
+        _lib.check(L.posfeat_disk_flash_lse(_lib.ptr(fa), _lib.ptr(fb), b, n, 60.0, _lib.ptr(lse),
+                                            _lib.ptr(ws), need, _lib.stream_ptr()))
+    lse_pass()
+    reps = 10
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        lse_pass()
+    e1.record()
+    torch.cuda.synchronize()
+    kms = e0.elapsed_time(e1) / reps
+    kfl = 2.0 * b * n * n * 128
+    ach = kfl / (kms * 1e-3) / 1e12
+    if rank == 0:
+        rec = {
+            "metric": "pairs/sec correlation losses + map gradients (640x480: Line2Window + "
+                      "EpipolarLoss_full, DiskLoss)",
+            "value": round(world * args.steps * b / el, 3), "unit": "pairs/s", "n_gpus": world,
+            "ranks_seen": ranks_seen(), "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic (smoothed random 128-d local maps, uniform score maps, synthetic "
+                    "fundamental matrices as datasets/megadepth.py:426-448 builds them)",
+            "config": {"workload": "configs[2]/[4] correlation: Preprocess_Line2Window + "
+                                   "EpipolarLoss_full (train_desc.yaml) and DiskLoss "
+                                   "(train_kp.yaml), forward + gradient, %d pairs per GPU" % b,
+                       "global_batch_pairs": b * world, "image": [H, W],
+                       "parallelism": "dp%d (pairs sharded)" % world},
+            "roofline": {"kernel": "disk_flash_kernel<LSE> (DiskLoss softmax normaliser: MFMA "
+                                   "similarity + online logsumexp, S never stored)",
+                         "bound": "mfma", "achieved": round(ach, 3),
+                         "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(ach / PEAK_FP32_MFMA_TFLOPS, 4), "traffic": None,
+                         "avg_launch_ms": round(kms, 4), "flop_per_launch": kfl},
+        }
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        import torch.distributed as dist
         dist.destroy_process_group()
 
 

@@ -401,6 +401,29 @@ int posfeat_adam(float *p, const float *g, float *m, float *v, long long n, floa
                  float beta2, float eps, float weight_decay, long long step, float grad_scale,
                  void *stream);
 
+/* DiskLoss's flash LSE pass alone (kploss.py:160-166: the normaliser of
+ * Categorical(logits=affinity)): lse[b][j] = logsumexp_i(T <fa_i, fb_j> - T) over
+ * the n rows of fa for each row j of fb, fa/fb [b][n][128]; the n x n
+ * similarity is recomputed by fp32 MFMA and never stored. */
+size_t posfeat_disk_flash_lse_workspace(int b, int n);
+int posfeat_disk_flash_lse(const float *fa, const float *fb, int b, int n, float T, float *lse,
+                           void *ws, size_t ws_bytes, void *stream);
+
+/* ---- evaluation matchers ---------------------------------
+ * Replaces mnn_matcher (losses/preprocess_utils.py:795-803 =
+ * evaluations/hpatches/evaluation.py:28-38), mutual_nn_matcher / ratio_matcher /
+ * mutual_nn_ratio_matcher (evaluations/aachen/matchers.py:5-75, the same code
+ * as evaluations/ETH_local_feature/custom_matcher.py) for L2-normalised
+ * descriptors d1 [n1][dim], d2 [n2][dim] (dim == 128, 16-B aligned).
+ * mode: 0 mutual NN, 1 symmetric Lowe ratio, 2 mutual NN + ratio.
+ * matches: int32 [n1][2] capacity, written in ascending first index;
+ * *count (device) = number written.  Tie rule: the first (lowest) index wins
+ * an arg-max tie; the second-best similarity is the 2nd largest value with
+ * multiplicity (torch.topk(2)).  sim = d1 d2^T is never materialised. */
+size_t posfeat_match_workspace(int n1, int n2);
+int posfeat_match(const float *d1, int n1, const float *d2, int n2, int dim, int mode, float ratio,
+                  int32_t *matches, int32_t *count, void *ws, size_t ws_bytes, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

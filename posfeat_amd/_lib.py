@@ -148,6 +148,12 @@ SIGNATURES = {
                                            ctypes.POINTER(ctypes.c_double),
                                            ctypes.POINTER(ctypes.c_double)]),
     "posfeat_model_destroy": (None, [c_void_p]),
+    "posfeat_match_workspace": (c_size_t, [c_int, c_int]),
+    "posfeat_disk_flash_lse_workspace": (c_size_t, [c_int, c_int]),
+    "posfeat_disk_flash_lse": (c_int, [c_void_p, c_void_p, c_int, c_int, ctypes.c_float, c_void_p,
+                                       c_void_p, c_size_t, c_void_p]),
+    "posfeat_match": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, ctypes.c_float,
+                              c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
 }
 
 

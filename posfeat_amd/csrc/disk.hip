@@ -17,7 +17,22 @@
 //                    logp2), p = softmax_row * softmax_col, fixed-order block
 //                    partials (fp64) + one final workgroup -> deterministic
 // The dense B x n x n probability matrices of the reference are never
-// materialised; only S is (n = 4800 at 480x640: 92 MB per pair).
+// materialised.  Default (flash) path: S is not materialised either --
+// disk_flash_kernel recomputes S = f1 f2^T tiles with fp32 MFMA in four
+// passes and folds them on the fly:
+//   LSE  (A, B) = (f1, f2) -> column logsumexp lse_c;  (f2, f1) -> lse_r
+//   SUM  (A, B) = (f1 acc, f2 acc) -> per accepted column n: sum_m reward p
+//        (= -dL/dlogp2[n] - penalty) and sum_m reward p (logp_dense + logp1 + logp2)
+//        (the reinforce partial);  (f2 acc, f1 acc) -> sum_n reward p per m
+// Each pass keeps, per column lane, a running state over the A rows (B's
+// columns stay in VGPRs as MFMA fragments; A streams through LDS by DMA), so
+// every reduction is a per-lane sequential sum in increasing row order plus
+// fixed-order merges: deterministic, no atomics.  The SUM passes run only over
+// the accepted points (stable compaction first).  POSFEAT_DISK_FLASH=0 keeps
+// the S-materialising path (92 MB per pair at 480x640) for A/B.
+#include <algorithm>
+#include <cstdlib>
+
 #include "common.h"
 
 int pf_sample_desc(const float* fmap, int b, int c, int h, int w, int cs, const float* coord,
@@ -365,11 +380,254 @@ __global__ __launch_bounds__(1024) void disk_final_kernel(const double* __restri
   }
 }
 
+// ---------------------------------------------------------------- flash path
+constexpr int FD = 128;     // descriptor dimension
+constexpr int FCOLS = 128;  // columns (B points) per block: 4 waves x 32
+constexpr int FSTEP = 64;   // A rows per LDS step
+
+struct FlashSide {          // per-point data of one side (1: image 1, 2: image 2)
+  const float* f;           // [b][n][128] L2-normalised descriptors
+  const int32_t* idx;       // SUM: [b][n] compacted accepted point ids, else null
+  const int32_t* cnt;       // SUM: [b] accepted count
+  const float* lse;         // SUM: [b][n] lse of this side (lse_r for 1, lse_c for 2)
+  const float* line;        // SUM: [b][n][3] normalised epipolar line of each point
+  const float* cpx;         // SUM: [b][n][2] pixel coordinates
+  const float* logp;        // SUM: [b][n] point log-probability
+};
+
+struct FlashArgs {
+  FlashSide A, B;
+  int n, rows_per_split;
+  float T, thr, good, bad;
+  float2* lse_part;         // LSE: [b][split][n] (max, sum)
+  float* g_part;            // SUM: [b][split][n] sum reward p
+  double* r_part;           // SUM (want_r): [b][split][n] sum reward p (logp terms)
+};
+
+template <bool SUM>
+__global__ __launch_bounds__(256) void disk_flash_kernel(FlashArgs a, int want_r) {
+  __shared__ __attribute__((aligned(16))) float As[2 * FSTEP * FD];  // 2 x 32 KB
+  __shared__ float meta[2][FSTEP][8];  // SUM: lse, line(3), cpx(2), logp per A row
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const int b = blockIdx.z, split = blockIdx.y;
+  const int ncolB = SUM ? a.B.cnt[b] : a.n;
+  const int nrowA = SUM ? a.A.cnt[b] : a.n;
+  const int cbase = blockIdx.x * FCOLS;
+  const int r0 = split * a.rows_per_split;
+  const int r1 = min(nrowA, r0 + a.rows_per_split);
+  const long long pb = (long long)b * a.n;
+  if (cbase >= ncolB) return;  // block-uniform: nothing to do (accepted subsets)
+  const int cl = cbase + wave * 32 + (lane & 31);
+  const bool cok = cl < ncolB;
+  const int cpt = SUM ? a.B.idx[pb + min(cl, ncolB - 1)] : min(cl, ncolB - 1);  // point id
+  f32x4 breg[FD / 8];
+  {
+    const float* brow = a.B.f + (pb + cpt) * FD;
+#pragma unroll
+    for (int g = 0; g < FD / 8; ++g) breg[g] = *reinterpret_cast<const f32x4*>(brow + 8 * g + 4 * h);
+  }
+  float bl = 0.f, bl0 = 0.f, bl1 = 0.f, bl2 = 0.f, bx = 0.f, by = 0.f, blp = 0.f;
+  if (SUM) {
+    bl = a.B.lse[pb + cpt];
+    bl0 = a.B.line[(pb + cpt) * 3];
+    bl1 = a.B.line[(pb + cpt) * 3 + 1];
+    bl2 = a.B.line[(pb + cpt) * 3 + 2];
+    bx = a.B.cpx[(pb + cpt) * 2];
+    by = a.B.cpx[(pb + cpt) * 2 + 1];
+    blp = a.B.logp[pb + cpt];
+  }
+  const int nsteps = r1 > r0 ? (r1 - r0 + FSTEP - 1) / FSTEP : 0;
+  auto issue = [&](int s, int buf) {
+#pragma unroll
+    for (int t = 0; t < FSTEP / 8; ++t) {
+      const int lr = (wave * (FSTEP / 8) + t) * 2 + h;
+      const int row = min(r0 + s * FSTEP + lr, r1 - 1);
+      const int pt = SUM ? a.A.idx[pb + row] : row;
+      const int slot = (lane & 31) ^ (lr & 15);
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(a.A.f + (pb + pt) * FD + slot * 4),
+          (__attribute__((address_space(3))) void*)(As + buf * FSTEP * FD +
+                                                     (wave * (FSTEP / 8) + t) * 2 * FD),
+          16, 0, 0);
+    }
+    if (SUM && tid < FSTEP) {  // row metadata (plain loads; consumed after the barrier)
+      const int row = min(r0 + s * FSTEP + tid, r1 - 1);
+      const long long q = pb + a.A.idx[pb + row];
+      float* mm = meta[buf][tid];
+      mm[0] = a.A.lse[q];
+      mm[1] = a.A.line[q * 3];
+      mm[2] = a.A.line[q * 3 + 1];
+      mm[3] = a.A.line[q * 3 + 2];
+      mm[4] = a.A.cpx[q * 2];
+      mm[5] = a.A.cpx[q * 2 + 1];
+      mm[6] = a.A.logp[q];
+    }
+  };
+  float run_m = -INFINITY, run_s = 0.f;  // LSE: running max / sum of exp
+  float gs = 0.f;                        // SUM: sum reward p
+  double rs = 0.0;                       // SUM: sum reward p (logp terms)
+  if (nsteps > 0) issue(0, 0);
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  for (int s = 0; s < nsteps; ++s) {
+    const int cur = s & 1;
+    if (s + 1 < nsteps) issue(s + 1, cur ^ 1);
+    const float* Ab = As + cur * FSTEP * FD;
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) {
+      f32x16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+      const int lr0 = mi * 32 + (lane & 31);
+      const float* arow = Ab + lr0 * FD;
+#pragma unroll
+      for (int g = 0; g < FD / 8; ++g) {
+        const f32x4 av = *reinterpret_cast<const f32x4*>(arow + (((2 * g + h) ^ (lr0 & 15)) * 4));
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j], breg[g][j], acc, 0, 0, 0);
+      }
+      // acc[r] = S(A row, B column cl) for A row r0 + s*64 + mi*32 + (r&3) + 8(r>>2) + 4h
+      const int rb = s * FSTEP + mi * 32 + 4 * h;
+      if (!SUM) {
+        float smax = -INFINITY;
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (r0 + rb + (r & 3) + 8 * (r >> 2) < r1) smax = fmaxf(smax, a.T * acc[r] - a.T);
+        if (smax > -INFINITY) {
+          const float nm = fmaxf(run_m, smax);
+          float add = 0.f;
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (r0 + rb + (r & 3) + 8 * (r >> 2) < r1) add += expf((a.T * acc[r] - a.T) - nm);
+          run_s = run_s * expf(run_m - nm) + add;
+          run_m = nm;
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int lr = rb - s * FSTEP + (r & 3) + 8 * (r >> 2);  // row within the step
+          if (r0 + s * FSTEP + lr >= r1) continue;
+          const float* mm = meta[cur][lr];
+          const float aff = a.T * acc[r] - a.T;
+          const float lpa = aff - mm[0], lpb = aff - bl;
+          const float p = expf(lpa) * expf(lpb);
+          const float dA = fabsf(mm[1] * bx + mm[2] * by + mm[3]);  // A's line at B's point
+          const float dB = fabsf(bl0 * mm[4] + bl1 * mm[5] + bl2);  // B's line at A's point
+          const float rp = ((dA < a.thr && dB < a.thr) ? a.good : a.bad) * p;
+          gs += rp;
+          if (want_r) rs += (double)(rp * ((lpa + lpb) + (mm[6] + blp)));
+        }
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+  }
+  // merge the two lane halves (interleaved row sets) in a fixed order
+  const long long o = ((long long)b * gridDim.y + split) * a.n + cl;
+  if (!SUM) {
+    const float om = __shfl_xor(run_m, 32, 64), os = __shfl_xor(run_s, 32, 64);
+    if (h == 0 && cok) {
+      const float M = fmaxf(run_m, om);
+      const float t = (M == -INFINITY) ? 0.f : run_s * expf(run_m - M) + os * expf(om - M);
+      a.lse_part[o] = make_float2(M, t);
+    }
+  } else {
+    const float og = __shfl_xor(gs, 32, 64);
+    const double orr = __shfl_xor(rs, 32, 64);
+    if (h == 0 && cok) {
+      a.g_part[o] = gs + og;
+      if (want_r) a.r_part[o] = rs + orr;
+    }
+  }
+}
+
+// lse[b][p] = merge of the split (max, sum) partials in split order
+__global__ void flash_lse_final_kernel(const float2* __restrict__ part, int nb, int ns, int n,
+                                       float* __restrict__ lse) {
+  const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (i >= (long long)nb * n) return;
+  const int b = (int)(i / n), c = (int)(i - (long long)b * n);
+  float M = -INFINITY;
+  for (int s = 0; s < ns; ++s) M = fmaxf(M, part[((long long)b * ns + s) * n + c].x);
+  float t = 0.f;
+  for (int s = 0; s < ns; ++s) {
+    const float2 q = part[((long long)b * ns + s) * n + c];
+    if (q.y > 0.f) t += q.y * expf(q.x - M);
+  }
+  lse[i] = M + logf(t);
+}
+
+// stable compaction of the accepted points of each image (one block per image)
+__global__ __launch_bounds__(1024) void flash_compact_kernel(const uint8_t* __restrict__ acc,
+                                                             int n, int32_t* __restrict__ idx,
+                                                             int32_t* __restrict__ cnt) {
+  __shared__ int off[1024];
+  const int b = blockIdx.x, t = threadIdx.x, per = (n + 1023) / 1024;
+  const uint8_t* ab = acc + (long long)b * n;
+  const int i0 = min(n, t * per), i1 = min(n, i0 + per);
+  int c = 0;
+  for (int i = i0; i < i1; ++i) c += ab[i] ? 1 : 0;
+  off[t] = c;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {
+    const int v = t >= d ? off[t - d] : 0;
+    __syncthreads();
+    off[t] += v;
+    __syncthreads();
+  }
+  int o = off[t] - c;
+  for (int i = i0; i < i1; ++i)
+    if (ab[i]) idx[(long long)b * n + o++] = i;
+  if (t == 1023) cnt[b] = off[1023];
+}
+
+// per point of one side: dL/dlogp (accepted: -sum_s g_part - penalty; else 0)
+// and, for the side whose SUM pass ran with want_r, the reinforce partial of
+// each accepted column (sum over splits in order) -> rcol
+__global__ void flash_sum_final_kernel(const float* __restrict__ gpart,
+                                       const double* __restrict__ rpart, int nb, int ns, int n,
+                                       const int32_t* __restrict__ idx,
+                                       const int32_t* __restrict__ cnt, float kp_penalty,
+                                       float* __restrict__ g, double* __restrict__ rcol) {
+  const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (i >= (long long)nb * n) return;
+  const int b = (int)(i / n), c = (int)(i - (long long)b * n);
+  if (rcol) rcol[i] = 0.0;
+  if (c >= cnt[b]) return;
+  float t = 0.f;
+  double r = 0.0;
+  for (int s = 0; s < ns; ++s) {
+    t += gpart[((long long)b * ns + s) * n + c];
+    if (rpart) r += rpart[((long long)b * ns + s) * n + c];
+  }
+  const long long pt = (long long)b * n + idx[(long long)b * n + c];
+  if (g) g[pt] = -t - kp_penalty;
+  if (rcol) rcol[i] = r;
+}
+
+// zero dL/dlogp of the rejected points (the accepted ones are written above)
+__global__ void flash_grad_init_kernel(const uint8_t* __restrict__ acc, long long total,
+                                       float* __restrict__ g) {
+  const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (i < total && !acc[i]) g[i] = 0.f;
+}
+
+int flash_nsplit(int n, int nb) {
+  const int ncb = (n + FCOLS - 1) / FCOLS;
+  int s = (1024 + ncb * nb - 1) / (ncb * nb);
+  return std::max(1, std::min(s, std::max(1, n / (2 * FSTEP))));
+}
+
+// read per call (a few getenv per loss) so tests can A/B both paths in-process
+bool use_flash() {
+  const char* e = getenv("POSFEAT_DISK_FLASH");
+  return !(e && e[0] == '0');
+}
+
 }  // namespace
 
-extern "C" size_t posfeat_disk_loss_workspace(int b, int H, int W) {
-  if (b <= 0 || H % 8 || W % 8) return 0;
-  const size_t n = (size_t)(H / 8) * (W / 8);
+static size_t disk_common_bytes(size_t b, size_t n) {
   size_t s = 0;
   s += 2 * pf_align(b * n * 2 * 4, 256);          // cpx1/2
   s += 2 * pf_align(b * n * 2 * 4, 256);          // cn1/2
@@ -377,19 +635,37 @@ extern "C" size_t posfeat_disk_loss_workspace(int b, int H, int W) {
   s += 2 * pf_align(b * n * 4, 256);              // prop1/2
   s += 2 * pf_align(b * n, 256);                  // acc1/2
   s += 2 * pf_align(b * n * 128 * 4, 256);        // f1/f2
-  s += pf_align(b * n * n * 4, 256);              // S
   s += 2 * pf_align(b * n * 4, 256);              // lse_r, lse_c
   s += 2 * pf_align(b * n * 3 * 4, 256);          // lines
-  s += pf_align(b * ((n + 3) / 4) * 8, 256);      // partials
-  s += pf_align(b * COL_CH * n * 8, 256);         // column LSE chunk partials
   return s;
+}
+
+static size_t disk_flash_bytes(size_t b, size_t n) {  // flash path scratch after the common part
+  const size_t ns = (size_t)flash_nsplit((int)n, (int)b);
+  return pf_align(b * ns * n * 8, 256) +            // LSE partials (max, sum)
+         pf_align(b * ns * n * 4, 256) +            // reward p partials
+         pf_align(b * ns * n * 8, 256) +            // reinforce partials (fp64)
+         2 * pf_align(b * n * 4, 256) +             // compacted ids
+         pf_align(2 * b * 4, 256) +                 // counts
+         pf_align(b * n * 8, 256);                  // reinforce per column (fp64)
+}
+
+static size_t disk_dense_bytes(size_t b, size_t n) {  // S-materialising path
+  return pf_align(b * n * n * 4, 256) + pf_align(b * ((n + 3) / 4) * 8, 256) +
+         pf_align(b * COL_CH * n * 8, 256);
+}
+
+extern "C" size_t posfeat_disk_loss_workspace(int b, int H, int W) {
+  if (b <= 0 || H % 8 || W % 8) return 0;
+  const size_t n = (size_t)(H / 8) * (W / 8);
+  return disk_common_bytes(b, n) + (use_flash() ? disk_flash_bytes(b, n) : disk_dense_bytes(b, n));
 }
 
 extern "C" size_t posfeat_disk_loss_grad_workspace(int b, int H, int W) {
   if (b <= 0 || H % 8 || W % 8) return 0;
   const size_t n = (size_t)(H / 8) * (W / 8);
   return posfeat_disk_loss_workspace(b, H, W) + 2 * pf_align(b * n * 4, 256) +
-         pf_align(b * COL_CH * n * 4, 256);
+         (use_flash() ? 0 : pf_align(b * COL_CH * n * 4, 256));
 }
 
 static int disk_loss_impl(const float* kp1, const float* kp2, const float* xf1, int cs1,
@@ -428,13 +704,10 @@ static int disk_loss_impl(const float* kp1, const float* kp2, const float* xf1, 
   uint8_t* ac2 = static_cast<uint8_t*>(take((size_t)b * n));
   float* f1 = static_cast<float*>(take((size_t)b * n * 512));
   float* f2 = static_cast<float*>(take((size_t)b * n * 512));
-  float* S = static_cast<float*>(take((size_t)b * n * n * 4));
   float* lr = static_cast<float*>(take((size_t)b * n * 4));
   float* lc = static_cast<float*>(take((size_t)b * n * 4));
   float* ln1 = static_cast<float*>(take((size_t)b * n * 12));
   float* ln2 = static_cast<float*>(take((size_t)b * n * 12));
-  double* part = static_cast<double*>(take((size_t)b * ((n + 3) / 4) * 8));
-  float2* colp = static_cast<float2*>(take((size_t)b * COL_CH * n * 8));
   const unsigned pts_blocks = (unsigned)(((long long)b * n + 3) / 4);
   hipLaunchKernelGGL(disk_point_kernel, dim3(pts_blocks), dim3(256), 0, st, kp1, b, H, W, prop1,
                      acc1, sampled ? uni1 : nullptr, pr1, ac1, cpx1, cn1, lp1);
@@ -443,6 +716,83 @@ static int disk_loss_impl(const float* kp1, const float* kp2, const float* xf1, 
   PF_CHECK_LAUNCH();
   PF_TRY(pf_sample_desc(xf1, b, 128, H / 4, W / 4, cs1, cn1, n, nullptr, 1, f1, st));
   PF_TRY(pf_sample_desc(xf2, b, 128, H / 4, W / 4, cs2, cn2, n, nullptr, 1, f2, st));
+  hipLaunchKernelGGL(epi_line_kernel, dim3((b * n + 255) / 256), dim3(256), 0, st, F1, cpx1, b, n,
+                     ln1);
+  hipLaunchKernelGGL(epi_line_kernel, dim3((b * n + 255) / 256), dim3(256), 0, st, F2, cpx2, b, n,
+                     ln2);
+  PF_CHECK_LAUNCH();
+  if (use_flash()) {
+    const int ns = flash_nsplit(n, b);
+    float2* lsep = static_cast<float2*>(take((size_t)b * ns * n * 8));
+    float* gp = static_cast<float*>(take((size_t)b * ns * n * 4));
+    double* rp = static_cast<double*>(take((size_t)b * ns * n * 8));
+    int32_t* id1 = static_cast<int32_t*>(take((size_t)b * n * 4));
+    int32_t* id2 = static_cast<int32_t*>(take((size_t)b * n * 4));
+    int32_t* cnt = static_cast<int32_t*>(take((size_t)2 * b * 4));
+    double* rcol = static_cast<double*>(take((size_t)b * n * 8));
+    const int rps = ((n + ns - 1) / ns + FSTEP - 1) / FSTEP * FSTEP;
+    const dim3 fgrid((n + FCOLS - 1) / FCOLS, ns, b);
+    FlashArgs fa{};
+    fa.n = n;
+    fa.rows_per_split = rps;
+    fa.T = temperature;
+    fa.thr = reward_thr;
+    fa.good = good_reward;
+    fa.bad = bad_reward;
+    fa.lse_part = lsep;
+    fa.g_part = gp;
+    fa.r_part = rp;
+    const FlashSide s1{f1, id1, cnt, lr, ln1, cpx1, lp1}, s2{f2, id2, cnt + b, lc, ln2, cpx2, lp2};
+    // column LSE (over image-1 points) and row LSE (over image-2 points), all points
+    fa.A = FlashSide{f1};
+    fa.B = FlashSide{f2};
+    hipLaunchKernelGGL(disk_flash_kernel<false>, fgrid, dim3(256), 0, st, fa, 0);
+    hipLaunchKernelGGL(flash_lse_final_kernel, dim3((b * n + 255) / 256), dim3(256), 0, st, lsep,
+                       b, ns, n, lc);
+    fa.A = FlashSide{f2};
+    fa.B = FlashSide{f1};
+    hipLaunchKernelGGL(disk_flash_kernel<false>, fgrid, dim3(256), 0, st, fa, 0);
+    hipLaunchKernelGGL(flash_lse_final_kernel, dim3((b * n + 255) / 256), dim3(256), 0, st, lsep,
+                       b, ns, n, lr);
+    hipLaunchKernelGGL(flash_compact_kernel, dim3(b), dim3(1024), 0, st, ac1, n, id1, cnt);
+    hipLaunchKernelGGL(flash_compact_kernel, dim3(b), dim3(1024), 0, st, ac2, n, id2, cnt + b);
+    PF_CHECK_LAUNCH();
+    // accepted pairs, columns = image-2 points: sum_m reward p and the reinforce
+    float* g1 = grad ? static_cast<float*>(take((size_t)b * n * 4)) : nullptr;
+    float* g2 = grad ? static_cast<float*>(take((size_t)b * n * 4)) : nullptr;
+    if (grad) {
+      hipLaunchKernelGGL(flash_grad_init_kernel, dim3((b * n + 255) / 256), dim3(256), 0, st, ac1,
+                         (long long)b * n, g1);
+      hipLaunchKernelGGL(flash_grad_init_kernel, dim3((b * n + 255) / 256), dim3(256), 0, st, ac2,
+                         (long long)b * n, g2);
+    }
+    fa.A = s1;
+    fa.B = s2;
+    hipLaunchKernelGGL(disk_flash_kernel<true>, fgrid, dim3(256), 0, st, fa, 1);
+    hipLaunchKernelGGL(flash_sum_final_kernel, dim3((b * n + 255) / 256), dim3(256), 0, st, gp, rp,
+                       b, ns, n, id2, cnt + b, kp_penalty, g2, rcol);
+    PF_CHECK_LAUNCH();
+    hipLaunchKernelGGL(disk_final_kernel, dim3(1), dim3(1024), 0, st, rcol, b * n, ac1, ac2, lp1,
+                       lp2, b, n, n, kp_penalty, out);
+    PF_CHECK_LAUNCH();
+    if (!grad) return POSFEAT_OK;
+    // columns = image-1 points: sum_n reward p
+    fa.A = s2;
+    fa.B = s1;
+    hipLaunchKernelGGL(disk_flash_kernel<true>, fgrid, dim3(256), 0, st, fa, 0);
+    hipLaunchKernelGGL(flash_sum_final_kernel, dim3((b * n + 255) / 256), dim3(256), 0, st, gp,
+                       (const double*)nullptr, b, ns, n, id1, cnt, kp_penalty, g1,
+                       (double*)nullptr);
+    hipLaunchKernelGGL(disk_point_grad_kernel, dim3(pts_blocks), dim3(256), 0, st, kp1, b, H, W,
+                       pr1, ac1, g1, dkp1);
+    hipLaunchKernelGGL(disk_point_grad_kernel, dim3(pts_blocks), dim3(256), 0, st, kp2, b, H, W,
+                       pr2, ac2, g2, dkp2);
+    PF_CHECK_LAUNCH();
+    return POSFEAT_OK;
+  }
+  float* S = static_cast<float*>(take((size_t)b * n * n * 4));
+  double* part = static_cast<double*>(take((size_t)b * ((n + 3) / 4) * 8));
+  float2* colp = static_cast<float2*>(take((size_t)b * COL_CH * n * 8));
   for (int i = 0; i < b; ++i) {
     posfeat_conv_desc d;
     d.n = 1;
@@ -465,10 +815,6 @@ static int disk_loss_impl(const float* kp1, const float* kp2, const float* xf1, 
                      n, n, temperature, colp);
   hipLaunchKernelGGL(col_lse_final_kernel, dim3((b * n + 255) / 256), dim3(256), 0, st, colp, b,
                      n, lc);
-  hipLaunchKernelGGL(epi_line_kernel, dim3((b * n + 255) / 256), dim3(256), 0, st, F1, cpx1, b, n,
-                     ln1);
-  hipLaunchKernelGGL(epi_line_kernel, dim3((b * n + 255) / 256), dim3(256), 0, st, F2, cpx2, b, n,
-                     ln2);
   PF_CHECK_LAUNCH();
   const int mblocks = (n + 3) / 4;
   hipLaunchKernelGGL(reinforce_kernel, dim3(mblocks, b), dim3(RB), 0, st, S, n, n, temperature,
@@ -493,6 +839,35 @@ static int disk_loss_impl(const float* kp1, const float* kp2, const float* xf1, 
                      ac1, g1, dkp1);
   hipLaunchKernelGGL(disk_point_grad_kernel, dim3(pts_blocks), dim3(256), 0, st, kp2, b, H, W, pr2,
                      ac2, g2, dkp2);
+  PF_CHECK_LAUNCH();
+  return POSFEAT_OK;
+}
+
+// The flash LSE pass on its own (the softmax normaliser of DiskLoss,
+// kploss.py:160-166): lse[b][j] = logsumexp_i(T <fa_i, fb_j> - T) over the n
+// rows of fa, for each of the n rows of fb; fa, fb [b][n][128] L2-normalised.
+extern "C" size_t posfeat_disk_flash_lse_workspace(int b, int n) {
+  if (b <= 0 || n <= 0) return 0;
+  return pf_align((size_t)b * flash_nsplit(n, b) * n * 8, 256);
+}
+
+extern "C" int posfeat_disk_flash_lse(const float* fa, const float* fb, int b, int n, float T,
+                                      float* lse, void* ws, size_t ws_bytes, void* stream) {
+  if (!fa || !fb || !lse || !ws || b <= 0 || n <= 0) return POSFEAT_E_INVALID;
+  if (ws_bytes < posfeat_disk_flash_lse_workspace(b, n)) return POSFEAT_E_WORKSPACE;
+  hipStream_t st = pf_stream(stream);
+  const int ns = flash_nsplit(n, b);
+  FlashArgs fa_{};
+  fa_.A = FlashSide{fa};
+  fa_.B = FlashSide{fb};
+  fa_.n = n;
+  fa_.rows_per_split = ((n + ns - 1) / ns + FSTEP - 1) / FSTEP * FSTEP;
+  fa_.T = T;
+  fa_.lse_part = static_cast<float2*>(ws);
+  hipLaunchKernelGGL(disk_flash_kernel<false>, dim3((n + FCOLS - 1) / FCOLS, ns, b), dim3(256), 0,
+                     st, fa_, 0);
+  hipLaunchKernelGGL(flash_lse_final_kernel, dim3((b * n + 255) / 256), dim3(256), 0, st,
+                     fa_.lse_part, b, ns, n, lse);
   PF_CHECK_LAUNCH();
   return POSFEAT_OK;
 }

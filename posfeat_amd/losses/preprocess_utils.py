@@ -72,10 +72,7 @@ def nms(score, patch_radius):
 
 
 def mnn_matcher(descriptors_a, descriptors_b):
-    sim = descriptors_a @ descriptors_b.t()
-    nn12 = torch.max(sim, dim=1)[1]
-    nn21 = torch.max(sim, dim=0)[1]
-    ids1 = torch.arange(0, sim.shape[0], device=sim.device)
-    mask = ids1 == nn21[nn12]
-    matches = torch.stack([ids1[mask], nn12[mask]])
-    return matches.t().data.cpu().numpy()
+    """Mutual nearest neighbours (preprocess_utils.py:795-803) on the fused
+    MFMA similarity + arg-max kernel (posfeat_amd.matchers)."""
+    from ..matchers import mnn_matcher as _mnn
+    return _mnn(descriptors_a, descriptors_b)

@@ -495,6 +495,31 @@ def gen_bb_grad(out):
     np.savez_compressed(out, **res)
 
 
+# evaluation matchers: the reference's own functions on seeded
+# descriptor sets (oracle.match_ref.seeded_descriptors regenerates the inputs)
+MATCH_CASES = [(11, 1000, 1200), (12, 2048, 2048), (13, 500, 300), (14, 4096, 3000)]
+
+
+def gen_matchers(out):
+    from oracle.match_ref import seeded_descriptors
+    am = _load("ref_aachen_matchers", os.path.join(REF, "evaluations", "aachen", "matchers.py"))
+    em = _load("ref_eth_matchers", os.path.join(REF, "evaluations", "ETH_local_feature",
+                                                 "custom_matcher.py"))
+    res = {}
+    for seed, n1, n2 in MATCH_CASES:
+        d1, d2 = seeded_descriptors(seed, n1, n2)
+        t1, t2 = torch.from_numpy(d1), torch.from_numpy(d2)
+        tag = "m%d" % seed
+        res[tag + "_shape"] = np.array([n1, n2], np.int64)
+        res[tag + "_mnn"] = ref_putils.mnn_matcher(t1, t2)
+        res[tag + "_mutual_nn"] = am.mutual_nn_matcher(t1, t2)
+        res[tag + "_eth_mutual_nn"] = em.mutual_nn_matcher(t1, t2)
+        for r in (0.95, 0.8):
+            res["%s_ratio_%g" % (tag, r)] = am.ratio_matcher(t1, t2, ratio=r)
+            res["%s_mnn_ratio_%g" % (tag, r)] = am.mutual_nn_ratio_matcher(t1, t2, ratio=r)
+    np.savez_compressed(out, **res)
+
+
 if __name__ == "__main__":
     torch.set_num_threads(os.cpu_count() or 8)
     which = sys.argv[1:] or ["detector", "sampler", "model_small", "extract_full", "correlation",
@@ -515,4 +540,6 @@ if __name__ == "__main__":
         gen_extract_full(os.path.join(HERE, "extract_full.npz"))
     if "correlation" in which:
         gen_correlation(os.path.join(HERE, "correlation.npz"))
+    if "matchers" in which:
+        gen_matchers(os.path.join(HERE, "matchers.npz"))
     print("golden fixtures written to", HERE)

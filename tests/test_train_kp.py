@@ -62,7 +62,11 @@ def test_oracle_train_step_vs_reference(tag):
                                                 (p1.long(), p2.long(), a1, a2))
     np.testing.assert_allclose(lps[0].numpy(), d[tag + "_lp1"], atol=1e-5)
     np.testing.assert_allclose(float(loss), float(d[tag + "_loss"]), rtol=1e-4)
-    _assert_grads({k: v.numpy() for k, v in grads.items()}, d, tag, rel=1e-4)
+    # 5e-4: the oracle and the reference both run torch-CPU fp32, but conv
+    # weight gradients over 2x96x128 pixels sum in BLAS/oneDNN order, which
+    # differs between host CPUs (2.3e-4 relative on conv2.weight on an EPYC
+    # host vs the Xeon the fixture was made on)
+    _assert_grads({k: v.numpy() for k, v in grads.items()}, d, tag, rel=5e-4)
 
 
 def test_pack_head_roundtrip():
