@@ -20,6 +20,8 @@
 //                    softmax expectation + std
 //   epipolar_loss    one workgroup: costs, masks, std weights, means
 // Random draws (grid sel, jitter) are inputs: the caller owns the RNG.
+#include <algorithm>
+
 #include "common.h"
 
 int pf_sample_desc(const float* fmap, int b, int c, int h, int w, int cs, const float* coord,
@@ -780,7 +782,8 @@ __global__ void window_bwd_kernel(const float* __restrict__ f1, const float* __r
 __global__ __launch_bounds__(256) void window_bwd_patch_kernel(
     const float* __restrict__ f1, const float* __restrict__ fm2, const float* __restrict__ center,
     const float* __restrict__ gE, int nb, int n, int h2, int w2, int win_h, int win_w,
-    float window_size, float* __restrict__ dq, unsigned long long* __restrict__ acc) {
+    float window_size, float* __restrict__ dq, int rec_stride, float* __restrict__ crec,
+    int4* __restrict__ prec) {
   __shared__ float s_pc[4][WB_PATCH];  // q . fm per patch pixel, then c
   __shared__ float s_t[4][WB_PATCH];   // separable adjoint, first stage [iy][px]
   __shared__ float s_ds[4][WB_TAPS];   // dsim per tap
@@ -793,11 +796,11 @@ __global__ __launch_bounds__(256) void window_bwd_patch_kernel(
   if (gx0 == 0.f && gy0 == 0.f) {  // masked point: no gradient
     dq[wid * 128 + lane] = 0.f;
     dq[wid * 128 + lane + 64] = 0.f;
+    if (lane == 0) prec[wid] = make_int4(0, 0, 0, 0);
     return;
   }
   const int b = (int)(wid / n);
   const float* fmb = fm2 + (long long)b * h2 * w2 * 128;
-  unsigned long long* accb = acc + (long long)b * h2 * w2 * 128;
   float* pc = s_pc[wv];
   float* tt = s_t[wv];
   float* dsv = s_ds[wv];
@@ -808,9 +811,6 @@ __global__ __launch_bounds__(256) void window_bwd_patch_kernel(
   const WinPatch P =
       window_patch_logits(fmb, h2, w2, qp, jx, jy, win_h, win_w, window_size, pc, ax, wl);
   const int px0 = P.px0, py0 = P.py0, PW = P.PW, np = P.PW * P.PH;
-  float qs[8];  // query channels strided by 16 (the scatter's coalesced order)
-#pragma unroll
-  for (int k = 0; k < 8; ++k) qs[k] = qp[cl + 16 * k];
   const int nw = win_h * win_w;
   float wm = -INFINITY;
 #pragma unroll
@@ -868,7 +868,11 @@ __global__ __launch_bounds__(256) void window_bwd_patch_kernel(
     pc[e] = v;
   }
   wave_lds_sync();
-  // pass 2: dq = sum_p c_p fm[p];  d fm[p] += c_p q (fixed point)
+  // the patch's c values and geometry for window_gather_kernel, which forms
+  // d fm[p] = sum_points c_p q per pixel tile (a gather: no atomics)
+  for (int e = lane; e < np && e < rec_stride; e += 64) crec[wid * rec_stride + e] = pc[e];
+  if (lane == 0) prec[wid] = make_int4(px0, py0, PW, P.PH);
+  // pass 2: dq = sum_p c_p fm[p]
   f32x4 da = {0.f, 0.f, 0.f, 0.f}, db = {0.f, 0.f, 0.f, 0.f};
   for (int base = 0; base < np; base += 4) {
     const int pp = base + grp;
@@ -880,9 +884,6 @@ __global__ __launch_bounds__(256) void window_bwd_patch_kernel(
         const float* src = fmb + off + cl * 8;
         da += c * *reinterpret_cast<const f32x4*>(src);
         db += c * *reinterpret_cast<const f32x4*>(src + 4);
-        unsigned long long* dst = accb + off + cl;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) fx_add(dst + 16 * k, c * qs[k]);
       }
     }
   }
@@ -900,6 +901,85 @@ __global__ __launch_bounds__(256) void window_bwd_patch_kernel(
   if (grp == 0) {
     *reinterpret_cast<f32x4*>(dq + wid * 128 + cl * 8) = da;
     *reinterpret_cast<f32x4*>(dq + wid * 128 + cl * 8 + 4) = db;
+  }
+}
+
+// d fm[p] = sum_i c_i(p) q_i for every pixel p of one 8 x 8 tile of image b,
+// over the query points i whose window patch (window_bwd_patch_kernel's
+// record) overlaps the tile, in increasing i: deterministic, no atomics.  The
+// list is built by a block-wide ordered compaction; c and q of 16 points at a
+// time are staged in LDS; thread = (tile row, channel quad), 8 pixels x 4
+// channels of accumulators.
+constexpr int WG_T = 8, WG_CH = 16, WG_MAXN = 4096;
+__global__ __launch_bounds__(256) void window_gather_kernel(
+    const float* __restrict__ q, const float* __restrict__ crec, const int4* __restrict__ prec,
+    int rec_stride, int n, int h2, int w2, float* __restrict__ dfm) {
+  __shared__ int s_list[WG_MAXN];
+  __shared__ int s_cnt[256];
+  __shared__ __attribute__((aligned(16))) float s_q[WG_CH][128];
+  __shared__ float s_c[WG_CH][WG_T * WG_T];
+  const int t = threadIdx.x, b = blockIdx.y;
+  const int ntx = (w2 + WG_T - 1) / WG_T;
+  const int tx0 = (blockIdx.x % ntx) * WG_T, ty0 = (blockIdx.x / ntx) * WG_T;
+  const int4* pb = prec + (long long)b * n;
+  // ordered list of the overlapping points
+  int total = 0;
+  for (int base = 0; base < n; base += 256) {
+    const int i = base + t;
+    int f = 0;
+    if (i < n) {
+      const int4 r = pb[i];
+      f = r.z > 0 && r.x < tx0 + WG_T && r.x + r.z > tx0 && r.y < ty0 + WG_T && r.y + r.w > ty0;
+    }
+    s_cnt[t] = f;
+    __syncthreads();
+    for (int d = 1; d < 256; d <<= 1) {
+      const int v = t >= d ? s_cnt[t - d] : 0;
+      __syncthreads();
+      s_cnt[t] += v;
+      __syncthreads();
+    }
+    if (f) s_list[total + s_cnt[t] - 1] = i;
+    total += s_cnt[255];
+    __syncthreads();
+  }
+  const int row = t >> 5, cq = t & 31;
+  f32x4 acc[WG_T];
+#pragma unroll
+  for (int j = 0; j < WG_T; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const float* qb = q + (long long)b * n * 128;
+  const float* cb = crec + (long long)b * n * rec_stride;
+  for (int c0 = 0; c0 < total; c0 += WG_CH) {
+    const int m = min(WG_CH, total - c0);
+    for (int e = t; e < m * 32; e += 256) {  // q rows, float4 each
+      const int k = e >> 5, qq = e & 31;
+      *reinterpret_cast<f32x4*>(&s_q[k][qq * 4]) =
+          *reinterpret_cast<const f32x4*>(qb + (long long)s_list[c0 + k] * 128 + qq * 4);
+    }
+    for (int e = t; e < m * WG_T * WG_T; e += 256) {  // c of the tile pixels
+      const int k = e / (WG_T * WG_T), pp = e - k * (WG_T * WG_T);
+      const int i = s_list[c0 + k];
+      const int4 r = pb[i];
+      const int px = tx0 + (pp % WG_T) - r.x, py = ty0 + (pp / WG_T) - r.y;
+      s_c[k][pp] = ((unsigned)px < (unsigned)r.z && (unsigned)py < (unsigned)r.w)
+                       ? cb[(long long)i * rec_stride + py * r.z + px]
+                       : 0.f;
+    }
+    __syncthreads();
+    for (int k = 0; k < m; ++k) {
+      const f32x4 qv = *reinterpret_cast<const f32x4*>(&s_q[k][cq * 4]);
+#pragma unroll
+      for (int j = 0; j < WG_T; ++j) acc[j] += s_c[k][row * WG_T + j] * qv;
+    }
+    __syncthreads();
+  }
+  const int py = ty0 + row;
+  if (py >= h2) return;
+#pragma unroll
+  for (int j = 0; j < WG_T; ++j) {
+    const int px = tx0 + j;
+    if (px < w2)
+      *reinterpret_cast<f32x4*>(dfm + (((long long)b * h2 + py) * w2 + px) * 128 + cq * 4) = acc[j];
   }
 }
 
@@ -988,8 +1068,11 @@ __global__ void query_bwd_kernel(const float* __restrict__ xf, int cs, const flo
 
 // dxf = normalize_bwd(T * acc_fm) + acc_x, one wave per pixel:
 // y = x / max(|x|, 1e-12); dx = (dy - y (y.dy)) / |x| (|x| > eps), dy / eps otherwise
+// afm: the window-backward map gradient, fixed point (per-tap scatter path) or
+// fp32 (dfm, from window_gather_kernel) when dfm != null
 __global__ void l2norm_bwd_kernel(const float* __restrict__ x, int cs,
                                   const unsigned long long* __restrict__ afm,
+                                  const float* __restrict__ dfm,
                                   const unsigned long long* __restrict__ ax, long long npix,
                                   float T, float* __restrict__ dx, int dcs) {
   const int lane = threadIdx.x & 63;
@@ -999,8 +1082,10 @@ __global__ void l2norm_bwd_kernel(const float* __restrict__ x, int cs,
   const float nrm = sqrtf(pf_wave_sum(x0 * x0 + x1 * x1));
   const float inv = 1.f / fmaxf(nrm, 1e-12f);
   const float y0 = x0 * inv, y1 = x1 * inv;
-  const float g0 = T * (float)((double)(long long)afm[pix * 128 + lane] / FX_SCALE);
-  const float g1 = T * (float)((double)(long long)afm[pix * 128 + lane + 64] / FX_SCALE);
+  const float g0 = T * (dfm ? dfm[pix * 128 + lane]
+                            : (float)((double)(long long)afm[pix * 128 + lane] / FX_SCALE));
+  const float g1 = T * (dfm ? dfm[pix * 128 + lane + 64]
+                            : (float)((double)(long long)afm[pix * 128 + lane + 64] / FX_SCALE));
   const float yg = pf_wave_sum(y0 * g0 + y1 * g1);
   float r0 = nrm > 1e-12f ? (g0 - y0 * yg) * inv : g0 * inv;
   float r1 = nrm > 1e-12f ? (g1 - y1 * yg) * inv : g1 * inv;
@@ -1157,13 +1242,24 @@ extern "C" int posfeat_epipolar_loss(int b, int n, const float* F1, const float*
   return POSFEAT_OK;
 }
 
+// per-point window patch record (window_bwd_patch_kernel -> window_gather_kernel):
+// sized for the largest patch the patch kernel accepts on an h x w map at the
+// configs' window_size 0.1 ... 0.125 -- (0.125 w + 4) x (0.125 h + 4), at most WB_PATCH
+static size_t wb_rec_stride(int h, int w) {
+  const size_t s = (size_t)((int)(0.125f * w) + 4) * (size_t)((int)(0.125f * h) + 4);
+  return std::min(s, (size_t)WB_PATCH);
+}
+
 extern "C" size_t posfeat_line2window_backward_workspace(int b, int H1, int W1, int H2, int W2,
                                                         int grid) {
   if (b <= 0 || grid <= 0) return 0;
   const size_t n1 = (size_t)(H1 / grid) * (W1 / grid), n2 = (size_t)(H2 / grid) * (W2 / grid);
   const size_t p1 = (size_t)b * (H1 / 4) * (W1 / 4) * 128, p2 = (size_t)b * (H2 / 4) * (W2 / 4) * 128;
+  const size_t r1 = wb_rec_stride(H2 / 4, W2 / 4), r2 = wb_rec_stride(H1 / 4, W1 / 4);
   return pf_align(b * n1 * 8, 256) + pf_align(b * n2 * 8, 256) + pf_align(b * n1 * 512, 256) +
-         pf_align(b * n2 * 512, 256) + 2 * pf_align(p1 * 8, 256) + 2 * pf_align(p2 * 8, 256);
+         pf_align(b * n2 * 512, 256) + 2 * pf_align(p1 * 8, 256) + 2 * pf_align(p2 * 8, 256) +
+         pf_align(b * n1 * r1 * 4, 256) + pf_align(b * n2 * r2 * 4, 256) +
+         pf_align(b * n1 * 16, 256) + pf_align(b * n2 * 16, 256);
 }
 
 extern "C" int posfeat_line2window_backward(
@@ -1214,7 +1310,19 @@ extern "C" int posfeat_line2window_backward(
   unsigned long long* ax1 = reinterpret_cast<unsigned long long*>(take(p1 * 8));
   unsigned long long* afm2 = reinterpret_cast<unsigned long long*>(take(p2 * 8));
   unsigned long long* ax2 = reinterpret_cast<unsigned long long*>(take(p2 * 8));
-  if (hipMemsetAsync(accs, 0, p - accs, st) != hipSuccess) return POSFEAT_E_HIP;
+  const size_t rs1 = wb_rec_stride(h2, w2), rs2 = wb_rec_stride(h1, w1);
+  float* crec1 = reinterpret_cast<float*>(take((size_t)b * n1 * rs1 * 4));
+  float* crec2 = reinterpret_cast<float*>(take((size_t)b * n2 * rs2 * 4));
+  int4* prec1 = reinterpret_cast<int4*>(take((size_t)b * n1 * 16));
+  int4* prec2 = reinterpret_cast<int4*>(take((size_t)b * n2 * 16));
+  // patch path (default): the window gradient w.r.t. fm is gathered per pixel
+  // tile into fp32 buffers that reuse the afm storage (no fixed-point scatter)
+  const bool gather1 = window_patch_on() && window_patch_fits(win_h2, win_w2) &&
+                       (size_t)(win_w2 + 4) * (win_h2 + 4) <= rs1 && n1 <= WG_MAXN;
+  const bool gather2 = window_patch_on() && window_patch_fits(win_h1, win_w1) &&
+                       (size_t)(win_w1 + 4) * (win_h1 + 4) <= rs2 && n2 <= WG_MAXN;
+  if (hipMemsetAsync(accs, 0, reinterpret_cast<char*>(crec1) - accs, st) != hipSuccess)
+    return POSFEAT_E_HIP;
   // d loss / d window expectations (w1 lives in image 2, w2 in image 1)
   hipLaunchKernelGGL(epi_loss_bwd_kernel, dim3(1), dim3(1024), 0, st, b, n1, F1, fwd->coord1,
                      fwd->w1, fwd->w1_std, fwd->valid1, short_edge, win_thr, weight_window,
@@ -1224,16 +1332,29 @@ extern "C" int posfeat_line2window_backward(
                      (float)((W1 - 1) / 2.0), (float)((H1 - 1) / 2.0), gE2);
   PF_CHECK_LAUNCH();
   // window softmax backward: direction 1 scatters into image 2's map, and back
-  {
-    const bool taps = !window_patch_on();
-    auto wbwd = (!taps && window_patch_fits(win_h2, win_w2)) ? window_bwd_patch_kernel
-                                                             : window_bwd_kernel;
-    hipLaunchKernelGGL(wbwd, dim3((b * n1 + 3) / 4), dim3(256), 0, st, f1, fm2, fwd->l1_exp_n,
-                       gE1, b, n1, h2, w2, win_h2, win_w2, window_size, dq1, afm2);
-    wbwd = (!taps && window_patch_fits(win_h1, win_w1)) ? window_bwd_patch_kernel
-                                                        : window_bwd_kernel;
-    hipLaunchKernelGGL(wbwd, dim3((b * n2 + 3) / 4), dim3(256), 0, st, f2, fm1, fwd->l2_exp_n,
-                       gE2, b, n2, h1, w1, win_h1, win_w1, window_size, dq2, afm1);
+  float* dfm2 = gather1 ? reinterpret_cast<float*>(afm2) : nullptr;
+  float* dfm1 = gather2 ? reinterpret_cast<float*>(afm1) : nullptr;
+  if (gather1) {
+    hipLaunchKernelGGL(window_bwd_patch_kernel, dim3((b * n1 + 3) / 4), dim3(256), 0, st, f1, fm2,
+                       fwd->l1_exp_n, gE1, b, n1, h2, w2, win_h2, win_w2, window_size, dq1,
+                       (int)rs1, crec1, prec1);
+    hipLaunchKernelGGL(window_gather_kernel,
+                       dim3(((w2 + WG_T - 1) / WG_T) * ((h2 + WG_T - 1) / WG_T), b), dim3(256), 0,
+                       st, f1, crec1, prec1, (int)rs1, n1, h2, w2, dfm2);
+  } else {
+    hipLaunchKernelGGL(window_bwd_kernel, dim3((b * n1 + 3) / 4), dim3(256), 0, st, f1, fm2,
+                       fwd->l1_exp_n, gE1, b, n1, h2, w2, win_h2, win_w2, window_size, dq1, afm2);
+  }
+  if (gather2) {
+    hipLaunchKernelGGL(window_bwd_patch_kernel, dim3((b * n2 + 3) / 4), dim3(256), 0, st, f2, fm1,
+                       fwd->l2_exp_n, gE2, b, n2, h1, w1, win_h1, win_w1, window_size, dq2,
+                       (int)rs2, crec2, prec2);
+    hipLaunchKernelGGL(window_gather_kernel,
+                       dim3(((w1 + WG_T - 1) / WG_T) * ((h1 + WG_T - 1) / WG_T), b), dim3(256), 0,
+                       st, f2, crec2, prec2, (int)rs2, n2, h1, w1, dfm1);
+  } else {
+    hipLaunchKernelGGL(window_bwd_kernel, dim3((b * n2 + 3) / 4), dim3(256), 0, st, f2, fm1,
+                       fwd->l2_exp_n, gE2, b, n2, h1, w1, win_h1, win_w1, window_size, dq2, afm1);
   }
   // query descriptors: normalize + grid_sample backward into the raw maps
   hipLaunchKernelGGL(query_bwd_kernel, dim3((b * n1 + 3) / 4), dim3(256), 0, st, xf1, cs1, c1n, f1,
@@ -1243,9 +1364,9 @@ extern "C" int posfeat_line2window_backward(
   PF_CHECK_LAUNCH();
   const long long np1 = (long long)b * h1 * w1, np2 = (long long)b * h2 * w2;
   hipLaunchKernelGGL(l2norm_bwd_kernel, dim3((unsigned)((np1 + 3) / 4)), dim3(256), 0, st, xf1, cs1,
-                     afm1, ax1, np1, temperature, dxf1, dcs1);
+                     afm1, dfm1, ax1, np1, temperature, dxf1, dcs1);
   hipLaunchKernelGGL(l2norm_bwd_kernel, dim3((unsigned)((np2 + 3) / 4)), dim3(256), 0, st, xf2, cs2,
-                     afm2, ax2, np2, temperature, dxf2, dcs2);
+                     afm2, dfm2, ax2, np2, temperature, dxf2, dcs2);
   PF_CHECK_LAUNCH();
   return POSFEAT_OK;
 }

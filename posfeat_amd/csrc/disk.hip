@@ -31,6 +31,7 @@
 // the accepted points (stable compaction first).  POSFEAT_DISK_FLASH=0 keeps
 // the S-materialising path (92 MB per pair at 480x640) for A/B.
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 
 #include "common.h"
@@ -473,20 +474,30 @@ __global__ __launch_bounds__(256) void disk_flash_kernel(FlashArgs a, int want_r
     const int cur = s & 1;
     if (s + 1 < nsteps) issue(s + 1, cur ^ 1);
     const float* Ab = As + cur * FSTEP * FD;
+    // both 32-row blocks at once: two independent accumulation chains per B
+    // fragment (the MFMA pipe never waits on one chain's ds_read)
+    f32x16 accs[2];
 #pragma unroll
-    for (int mi = 0; mi < 2; ++mi) {
-      f32x16 acc;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-      const int lr0 = mi * 32 + (lane & 31);
-      const float* arow = Ab + lr0 * FD;
+    for (int r = 0; r < 16; ++r) accs[0][r] = accs[1][r] = 0.f;
+    {
+      const int la = lane & 31;  // rows la and 32 + la share the swizzle (la & 15)
+      const float* arow0 = Ab + la * FD;
+      const float* arow1 = Ab + (32 + la) * FD;
 #pragma unroll
       for (int g = 0; g < FD / 8; ++g) {
-        const f32x4 av = *reinterpret_cast<const f32x4*>(arow + (((2 * g + h) ^ (lr0 & 15)) * 4));
+        const int off = ((2 * g + h) ^ (la & 15)) * 4;
+        const f32x4 a0 = *reinterpret_cast<const f32x4*>(arow0 + off);
+        const f32x4 a1 = *reinterpret_cast<const f32x4*>(arow1 + off);
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j], breg[g][j], acc, 0, 0, 0);
+        for (int j = 0; j < 4; ++j) {
+          accs[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[j], breg[g][j], accs[0], 0, 0, 0);
+          accs[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[j], breg[g][j], accs[1], 0, 0, 0);
+        }
       }
+    }
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) {
+      const f32x16& acc = accs[mi];
       // acc[r] = S(A row, B column cl) for A row r0 + s*64 + mi*32 + (r&3) + 8(r>>2) + 4h
       const int rb = s * FSTEP + mi * 32 + 4 * h;
       if (!SUM) {
@@ -613,10 +624,24 @@ __global__ void flash_grad_init_kernel(const uint8_t* __restrict__ acc, long lon
   if (i < total && !acc[i]) g[i] = 0.f;
 }
 
+// A-row split: fill whole rounds of the 512 resident workgroups (2 per CU)
+// -- the fraction of the last round left idle is the tail loss -- with at
+// least two 64-row steps per split
 int flash_nsplit(int n, int nb) {
   const int ncb = (n + FCOLS - 1) / FCOLS;
-  int s = (1024 + ncb * nb - 1) / (ncb * nb);
-  return std::max(1, std::min(s, std::max(1, n / (2 * FSTEP))));
+  const int smax = std::max(1, std::min(32, n / (2 * FSTEP)));
+  int best = 1;
+  double best_eff = 0.0;
+  for (int s = 1; s <= smax; ++s) {
+    const double r = (double)ncb * nb * s / 512.0;
+    const double eff = r / std::ceil(r) * (r < 1.0 ? r : 1.0);
+    if (eff >= 0.94) return s;  // the fewest splits that keep the tail small
+    if (eff > best_eff + 1e-9) {
+      best_eff = eff;
+      best = s;
+    }
+  }
+  return best;
 }
 
 // read per call (a few getenv per loss) so tests can A/B both paths in-process

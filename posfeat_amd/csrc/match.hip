@@ -28,6 +28,7 @@
 // kernel applies the reference's mask (mutual, ratio via sqrt(2 - 2 s) in
 // fp32, or both) and compacts the matches in ascending first index.
 #include <algorithm>
+#include <cmath>
 
 #include "common.h"
 
@@ -96,20 +97,29 @@ __global__ __launch_bounds__(256) void match_top2_kernel(const float* __restrict
     const int cur = s & 1;
     if (s + 1 < nsteps) issue(s + 1, cur ^ 1);
     const float* Ab = As + cur * MSTEP * MD;
+    // both 32-row blocks at once: two independent accumulation chains
+    f32x16 accs[2];
 #pragma unroll
-    for (int mi = 0; mi < 2; ++mi) {
-      f32x16 acc;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-      const int lr = mi * 32 + (lane & 31);
-      const float* arow = Ab + lr * MD;
+    for (int r = 0; r < 16; ++r) accs[0][r] = accs[1][r] = 0.f;
+    {
+      const int la = lane & 31;  // rows la and 32 + la share the swizzle (la & 15)
+      const float* arow0 = Ab + la * MD;
+      const float* arow1 = Ab + (32 + la) * MD;
 #pragma unroll
       for (int g = 0; g < MD / 8; ++g) {
-        const f32x4 a = *reinterpret_cast<const f32x4*>(arow + (((2 * g + h) ^ (lr & 15)) * 4));
+        const int off = ((2 * g + h) ^ (la & 15)) * 4;
+        const f32x4 a0 = *reinterpret_cast<const f32x4*>(arow0 + off);
+        const f32x4 a1 = *reinterpret_cast<const f32x4*>(arow1 + off);
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j], breg[g][j], acc, 0, 0, 0);
+        for (int j = 0; j < 4; ++j) {
+          accs[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[j], breg[g][j], accs[0], 0, 0, 0);
+          accs[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[j], breg[g][j], accs[1], 0, 0, 0);
+        }
       }
+    }
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) {
+      const f32x16& acc = accs[mi];
       // acc[r] = sim(A row i, B row col), i = step base + mi*32 + (r&3) + 8(r>>2) + 4h:
       // increasing in r, so strict '>' keeps the first index on ties
       const int ib = r0 + s * MSTEP + mi * 32 + 4 * h;
@@ -209,11 +219,22 @@ __global__ __launch_bounds__(1024) void match_select_kernel(
   if (t == 1023) *count = off[1023];
 }
 
+// A-row split filling whole rounds of the 512 resident workgroups (2 per CU)
 int nsplit_for(int na, int nb) {
   const int ncb = (nb + MCOLS - 1) / MCOLS;
-  int s = (512 + ncb - 1) / ncb;
-  s = std::min(s, std::max(1, (na + MSTEP - 1) / MSTEP));
-  return std::max(1, s);
+  const int smax = std::max(1, std::min(32, (na + MSTEP - 1) / MSTEP));
+  int best = 1;
+  double best_eff = 0.0;
+  for (int s = 1; s <= smax; ++s) {
+    const double r = (double)ncb * s / 512.0;
+    const double eff = r / std::ceil(r) * (r < 1.0 ? r : 1.0);
+    if (eff >= 0.94) return s;  // the fewest splits that keep the tail small
+    if (eff > best_eff + 1e-9) {
+      best_eff = eff;
+      best = s;
+    }
+  }
+  return best;
 }
 
 size_t side_ws(int na, int nb) {  // partials (3 per column per split) + merged (3 per column)
