@@ -154,6 +154,15 @@ int posfeat_nchw_to_nhwc(const float *x, int n, int c, int h, int w, int cstride
 int posfeat_nhwc_to_nchw(const float *x, int n, int c, int h, int w, int cstride_in,
                          float *y, void *stream);
 
+/* Extraction input on the device.  Replaces the per-image host transform of
+ *   datasets/hpatches.py:14-17 / aachen.py / ETH_local_feature.py
+ *   (transforms.ToTensor + Normalize(ImageNet mean/std)) so only the uint8
+ *   image crosses PCIe: src uint8 [b][h][w][3] (row pitch src_pitch bytes),
+ *   dst float [b][3][h][w] = ((u / 255) - mean) / std, bit-identical to the
+ *   host's fp32 numpy/torch computation. */
+int posfeat_normalize_rgb8(const unsigned char *src, int b, int h, int w, int src_pitch,
+                           float *dst, void *stream);
+
 /* ------------------------------------------------------------------------
  * Training-side dense correlation (forward values).
  * Replaces: losses/preprocess.py:27-121 Preprocess_Line2Window.forward with

@@ -72,6 +72,8 @@ SIGNATURES = {
                                      c_void_p]),
     "posfeat_nhwc_to_nchw": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
                                      c_void_p]),
+    "posfeat_normalize_rgb8": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p,
+                                       c_void_p]),
     "posfeat_line2window_workspace": (c_size_t, [c_int] * 6),
     "posfeat_line2window": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int,
                                     c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

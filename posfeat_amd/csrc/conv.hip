@@ -358,7 +358,19 @@ __device__ __attribute__((aligned(16))) float pf_conv_zero16[4];
 #define PF_GPTR(p) ((const __attribute__((address_space(1))) void*)(p))
 #define PF_LPTR(p) ((__attribute__((address_space(3))) void*)(p))
 
-template <int BM, int BN, int WM, int WN>
+// vmcnt(N) with expcnt / lgkmcnt left alone (gfx9 s_waitcnt encoding)
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+// NST = 2: two LDS stages, vmcnt(0) + barrier per chunk (the DMA of chunk c+1
+// overlaps chunk c).  NST = 3: a three-stage ring -- chunks c+1 and c+2 are
+// in flight while c is multiplied; each chunk waits only for its own DMA
+// (counted vmcnt) and one raw s_barrier (no fence, so the younger chunk's
+// DMA stays in flight across it).  96 KB of LDS at 128x128: one block per CU.
+template <int BM, int BN, int WM, int WN, int NST = 2>
 __global__ __launch_bounds__(WM* WN * 64) void conv_glds_kernel(ConvArgs a) {
   constexpr int THREADS = WM * WN * 64;
   constexpr int NW = THREADS / 64;
@@ -368,11 +380,12 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_glds_kernel(ConvArgs a) {
   constexpr int B_G = BN / 8 / NW;
   static_assert(A_G >= 1 && B_G >= 1 && BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "tile");
   static_assert(MI >= 1 && NI >= 1, "wave tile must be >= 32x32");
-  constexpr int RING = 2 * (BM + BN) * BK;
+  static_assert(NST == 2 || NST == 3, "stages");
+  constexpr int RING = NST * (BM + BN) * BK;
   constexpr int STAGE = BM * (BN + 4);
   __shared__ __attribute__((aligned(16))) float smem[RING > STAGE ? RING : STAGE];
-  float* As = smem;                // [2][BM][BK] swizzled
-  float* Bs = smem + 2 * BM * BK;  // [2][BN][BK] swizzled
+  float* As = smem;                  // [NST][BM][BK] swizzled
+  float* Bs = smem + NST * BM * BK;  // [NST][BN][BK] swizzled
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -475,15 +488,9 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_glds_kernel(ConvArgs a) {
 #pragma unroll
   for (int kk = 0; kk < BK / 8; ++kk) kofs[kk] = (((lane >> 5) + 2 * kk) ^ sw) * 4;
 
-  issue_chunk(ch0, 0);
-  __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0): the DMA has landed (this wave)
-  __syncthreads();
-
-  for (int c = ch0; c < ch1; ++c) {
-    const int cur = (c - ch0) & 1;
-    if (c + 1 < ch1) issue_chunk(c + 1, cur ^ 1);
-    const float* Ab = As + (cur * BM + arow) * BK;
-    const float* Bb = Bs + (cur * BN + brow) * BK;
+  auto compute = [&](int slot) {
+    const float* Ab = As + (slot * BM + arow) * BK;
+    const float* Bb = Bs + (slot * BN + brow) * BK;
 #pragma unroll
     for (int kk = 0; kk < BK / 8; ++kk) {
       f32x4 av[MI], bv[NI];
@@ -501,6 +508,36 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_glds_kernel(ConvArgs a) {
           for (int ni = 0; ni < NI; ++ni)
             acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[mi][j], bv[ni][j], acc[mi][ni],
                                                                 0, 0, 0);
+    }
+  };
+
+  if constexpr (NST == 2) {
+    issue_chunk(ch0, 0);
+    __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0): the DMA has landed (this wave)
+    __syncthreads();
+    for (int c = ch0; c < ch1; ++c) {
+      const int cur = (c - ch0) & 1;
+      if (c + 1 < ch1) issue_chunk(c + 1, cur ^ 1);
+      compute(cur);
+      __builtin_amdgcn_s_waitcnt(0);
+      __syncthreads();
+    }
+  } else {
+    const int nch = ch1 - ch0;
+    issue_chunk(ch0, 0);
+    if (nch > 1) issue_chunk(ch0 + 1, 1);
+    int slot = 0;
+    for (int i = 0; i < nch; ++i) {
+      // chunk i has landed (this wave) once only chunk i+1's DMAs may be pending
+      if (i + 1 < nch)
+        wait_vmcnt<A_G + B_G>();
+      else
+        wait_vmcnt<0>();
+      // every wave: chunk i landed, and chunk i-1 (the slot refilled below) consumed
+      __builtin_amdgcn_s_barrier();
+      if (i + 2 < nch) issue_chunk(ch0 + i + 2, slot == 0 ? 2 : slot - 1);
+      compute(slot);
+      slot = slot == 2 ? 0 : slot + 1;
     }
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
@@ -1255,10 +1292,17 @@ Plan conv_plan(const ConvArgs& a, bool allow_split, int forced = -1) {
   return d;
 }
 
+bool glds3_on() {
+  const char* e = getenv("POSFEAT_GLDS3");
+  return e && e[0] == '1';
+}
+
 template <int BM, int BN, int WM, int WN>
 void launch_rows(ConvArgs& a, int kern, hipStream_t st) {
   dim3 grid(a.nwg * a.ksplit, a.nbatch), block(WM * WN * 64);
-  if (kern == KERN_GLDS)
+  if (kern == KERN_GLDS && BM >= 128 && BN >= 128 && glds3_on())
+    hipLaunchKernelGGL((conv_glds_kernel<BM, BN, WM, WN, 3>), grid, block, 0, st, a);
+  else if (kern == KERN_GLDS)
     hipLaunchKernelGGL((conv_glds_kernel<BM, BN, WM, WN>), grid, block, 0, st, a);
   else if (a.Cin % BK == 0)
     hipLaunchKernelGGL((conv_mfma_kernel<BM, BN, WM, WN, true>), grid, block, 0, st, a);

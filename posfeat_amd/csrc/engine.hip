@@ -17,7 +17,9 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <cmath>
 #include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -124,6 +126,10 @@ struct posfeat_model {
   bool up4tap = true;
   Buf tapw, tapP, tappart;
   Buf gf_w, gf_b;
+  // convimg's IN statistics from the image's tap moments instead of running
+  // convimg (gfuse.hip): the full-res 64-channel map is never computed
+  bool imgstats = true;
+  Buf imws;
   size_t splitk_need = 0;
   // the image branch of KeypointDet (convimg + its IN statistics + the folded
   // G part of head.conv2 + head.conv2's weight transforms) depends on the
@@ -228,6 +234,78 @@ int tune(const std::string& name, const posfeat_conv_desc& d, hipStream_t st, Ru
   return best;
 }
 
+// Process-wide tile choices, keyed by the conv's full descriptor (and
+// whether a residual is read): a new instance -- another batch size or image
+// size, or a new engine -- times only the convs it has not met before.  A conv
+// met before with the same class (everything but n, h, w) and a GEMM M
+// (= n * oh * ow) within 25 % reuses that tile without timing (HPatches and
+// Aachen images come in many sizes; POSFEAT_TUNE_SIMILAR=0 turns this off).
+// Results never depend on the tile.
+struct TileCache {
+  std::mutex mu;
+  std::map<std::string, int> exact;
+  std::map<std::string, std::vector<std::pair<double, int>>> by_class;  // (M, tile)
+};
+TileCache& tile_cache() {
+  static TileCache t;
+  return t;
+}
+std::string desc_class(const posfeat_conv_desc& d, bool res) {
+  char b[160];
+  snprintf(b, sizeof b, "%d/%d/%d/%dx%d/s%d/p%d/%d/%d/a%d/r%d", d.cin, d.x_cstride, d.cout, d.kh,
+           d.kw, d.stride, d.pad, d.y_cstride, d.res_cstride, d.act, res ? 1 : 0);
+  return b;
+}
+double desc_m(const posfeat_conv_desc& d) {
+  const int oh = (d.h + 2 * d.pad - d.kh) / d.stride + 1, ow = (d.w + 2 * d.pad - d.kw) / d.stride + 1;
+  return (double)d.n * oh * ow;
+}
+bool tile_lookup(const posfeat_conv_desc& d, bool res, int* tile) {
+  static const bool similar = [] {
+    const char* e = getenv("POSFEAT_TUNE_SIMILAR");
+    return !(e && e[0] == '0');
+  }();
+  const std::string cls = desc_class(d, res);
+  char nhw[48];
+  snprintf(nhw, sizeof nhw, "|%d/%d/%d", d.n, d.h, d.w);
+  TileCache& t = tile_cache();
+  std::lock_guard<std::mutex> g(t.mu);
+  auto it = t.exact.find(cls + nhw);
+  if (it != t.exact.end()) {
+    *tile = it->second;
+    return true;
+  }
+  if (!similar) return false;
+  auto ct = t.by_class.find(cls);
+  if (ct == t.by_class.end()) return false;
+  const double m = desc_m(d);
+  double best = 1e30;
+  int bt = -2;
+  for (auto& e : ct->second) {
+    const double r = std::fabs(std::log(e.first / m));
+    if (r < best) {
+      best = r;
+      bt = e.second;
+    }
+  }
+  if (best > std::log(1.25)) return false;
+  if (bt >= 0) {  // the tile must be legal for this shape too
+    int cand[8];
+    const int nc = pf_conv_candidates(&d, cand, 8);
+    if (std::find(cand, cand + nc, bt) == cand + nc) return false;
+  }
+  *tile = bt;
+  return true;
+}
+void tile_store(const posfeat_conv_desc& d, bool res, int tile) {
+  const std::string cls = desc_class(d, res);
+  char nhw[48];
+  snprintf(nhw, sizeof nhw, "|%d/%d/%d", d.n, d.h, d.w);
+  TileCache& t = tile_cache();
+  std::lock_guard<std::mutex> g(t.mu);
+  if (t.exact.emplace(cls + nhw, tile).second) t.by_class[cls].push_back({desc_m(d), tile});
+}
+
 // run (autotuned on the first forward of the instance, keyed by `key`) one
 // conv described by d with packed weights w
 int conv_desc_run(Ctx& c, const std::string& key, const posfeat_conv_desc& d, const float* x,
@@ -246,7 +324,10 @@ int conv_desc_run(Ctx& c, const std::string& key, const posfeat_conv_desc& d, co
   if (it != c.m->tuned.end()) {
     tile = it->second;
   } else if (c.m->autotune) {
-    tile = tune(key, d, c.st, run);
+    if (!tile_lookup(d, res != nullptr, &tile)) {
+      tile = tune(key, d, c.st, run);
+      tile_store(d, res != nullptr, tile);
+    }
     c.m->tuned[key] = tile;
   }
   return timed(c, "conv:" + key, flops, [&] { return run(tile); });
@@ -429,11 +510,15 @@ void plan(posfeat_model* m) {
     m->up4wino = !(uv && uv[0] == '0') && H % 16 == 0 && W % 16 == 0;
     const char* tv = getenv("POSFEAT_UP4TAP");  // 0: the low-res Winograd / phase forms
     m->up4tap = !(tv && tv[0] == '0') && H % 16 == 0 && W % 16 == 0;
+    const char* iv = getenv("POSFEAT_IMGSTATS");  // 0: convimg conv + fused statistics
+    m->imgstats = !(iv && iv[0] == '0');
   }
   if (m->up4 && m->gfuse) {
     alloc(m->gf_w, B * 128 * 128);
     alloc(m->gf_b, B * 128 + 9 * 64 * 128);  // + the transposed W2 G slice (gfuse.hip)
   }
+  if (!(m->up4 && m->gfuse) || m->train) m->imgstats = false;
+  if (m->imgstats) alloc(m->imws, pf_gfuse_imgstats_ws_bytes((int)B, (int)H) / 4 + 4);
   if (m->wino) {
     size_t uf = 0, wb = 0;
     const int dims[5][2] = {{(int)h8, (int)w8}, {(int)h8, (int)w8}, {(int)h4, (int)w4},
@@ -452,7 +537,7 @@ void plan(posfeat_model* m) {
     m->side = !(e && e[0] == '0') && m->up4 && m->gfuse && !m->train;
   }
   if (m->up4) {
-    alloc(m->g64, B * H * W * 64);
+    if (!m->imgstats) alloc(m->g64, B * H * W * 64);
     alloc(m->wph, posfeat_conv2_up4_weights_floats());
     alloc(m->up4ws, posfeat_conv2_up4_workspace((int)B, (int)H, (int)W) / 4 + 4);
     if (m->up4tap) {
@@ -585,9 +670,15 @@ int image_branch(Ctx& c, const float* img4) {
   const size_t SL = (size_t)B * 256;
   float* meanI = c.f(m->st_mean) + SL;
   float* rstdI = c.f(m->st_rstd) + SL;
-  float* g64 = c.f(m->g64);
+  float* g64 = m->imgstats ? nullptr : c.f(m->g64);
   float* c2 = c.f(m->c2raw);
-  PF_TRY(conv_in(s, "head.convimg", img4, B, H, W, 4, g64, 64, meanI, rstdI));
+  if (m->imgstats)
+    PF_TRY(timed(s, "head.convimg.stats", 0, [&] {
+      return pf_gfuse_imgstats(img4, B, H, W, s.W("head.convimg"), s.Bi("head.convimg"), meanI,
+                               rstdI, s.f(m->imws), m->imws.floats * sizeof(float), s.st);
+    }));
+  else
+    PF_TRY(conv_in(s, "head.convimg", img4, B, H, W, 4, g64, 64, meanI, rstdI));
   if (!m->up4tap)
     PF_TRY(timed(s, "head.conv2.weights", 0, [&] {
       return posfeat_conv2_up4_weights(s.W("head.conv2"), s.f(m->wph), s.st);
@@ -601,9 +692,10 @@ int image_branch(Ctx& c, const float* img4) {
                             s.Bi("head.convimg"), meanI, rstdI, B, s.f(m->gf_w), s.f(m->gf_b),
                             s.st);
   }));
-  PF_TRY(timed(s, "conv:head.conv2.g", 2.0 * B * H * W * 128.0 * 4 * 25, [&] {
+  PF_TRY(timed(s, "conv:head.conv2.g", 2.0 * B * H * W * 128.0 * 4 * 26, [&] {
     return pf_gfuse_conv(img4, g64, 64, B, H, W, s.f(m->gf_w), s.f(m->gf_b), meanI, rstdI,
-                         s.W("head.conv2"), s.Bi("head.conv2"), c2, 128, s.st);
+                         s.W("head.conv2"), s.Bi("head.conv2"), c2, 128, s.st,
+                         s.W("head.convimg"), s.Bi("head.convimg"));
   }));
   if (m->up4wino && !m->up4tap)
     PF_TRY(timed(s, "head.conv2.up4w", 0, [&] {
@@ -716,8 +808,14 @@ int head_forward(Ctx& c, float* img4, float* local_point, bool side) {
     PF_TRY(timed(c, "norm_prelu", 0, [&] {
       return pf_in_apply(c1, B, h4 * w4, 192, 192, mean1, rstd1, slope, c.st);
     }));
-    float* g64 = c.f(m->g64);
-    if (!side) PF_TRY(conv_in(c, "head.convimg", img4, B, H, W, 4, g64, 64, meanI, rstdI));
+    float* g64 = m->imgstats ? nullptr : c.f(m->g64);
+    if (!side && m->imgstats)
+      PF_TRY(timed(c, "head.convimg.stats", 0, [&] {
+        return pf_gfuse_imgstats(img4, B, H, W, c.W("head.convimg"), c.Bi("head.convimg"), meanI,
+                                 rstdI, c.f(m->imws), m->imws.floats * sizeof(float), c.st);
+      }));
+    else if (!side)
+      PF_TRY(conv_in(c, "head.convimg", img4, B, H, W, 4, g64, 64, meanI, rstdI));
     if (!m->gfuse)
       PF_TRY(timed(c, "instnorm_apply", 0, [&] {
         return pf_in_apply(g64, B, H * W, 64, 64, meanI, rstdI, nullptr, c.st);
@@ -744,9 +842,10 @@ int head_forward(Ctx& c, float* img4, float* local_point, bool side) {
                                 c.Bi("head.convimg"), meanI, rstdI, B, c.f(m->gf_w),
                                 c.f(m->gf_b), c.st);
       }));
-      PF_TRY(timed(c, "conv:head.conv2.g", 2.0 * B * H * W * 128.0 * 4 * 25, [&] {
+      PF_TRY(timed(c, "conv:head.conv2.g", 2.0 * B * H * W * 128.0 * 4 * 26, [&] {
         return pf_gfuse_conv(img4, g64, 64, B, H, W, c.f(m->gf_w), c.f(m->gf_b), meanI, rstdI,
-                             c.W("head.conv2"), c.Bi("head.conv2"), c2, 128, c.st);
+                             c.W("head.conv2"), c.Bi("head.conv2"), c2, 128, c.st,
+                             c.W("head.convimg"), c.Bi("head.convimg"));
       }));
     } else {
       PF_TRY(timed(c, "conv:head.conv2.g", 2.0 * B * H * W * 128.0 * 64 * 9, [&] {

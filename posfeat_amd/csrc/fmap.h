@@ -62,9 +62,17 @@ size_t pf_gfuse_weights_floats(int n);
 int pf_gfuse_weights(const float* w2_packed, const float* b2, const float* w1_packed,
                      const float* b1, const float* mean, const float* rstd, int n, float* wc,
                      float* bc, hipStream_t st);
+// c: the raw convimg output for the border ring, or nullptr: recompute those
+// values from the image with w1_packed / b1
 int pf_gfuse_conv(const float* img4, const float* c, int ccs, int n, int H, int W,
                   const float* wc, const float* bc, const float* mean, const float* rstd,
-                  const float* w2_packed, const float* b2, float* y, int ycs, hipStream_t st);
+                  const float* w2_packed, const float* b2, float* y, int ycs, hipStream_t st,
+                  const float* w1_packed = nullptr, const float* b1 = nullptr);
+// convimg's instance-norm statistics from the image's tap moments (no conv)
+size_t pf_gfuse_imgstats_ws_bytes(int n, int H);
+int pf_gfuse_imgstats(const float* img4, int n, int H, int W, const float* w1_packed,
+                      const float* b1, float* mean, float* rstd, void* ws, size_t ws_bytes,
+                      hipStream_t st);
 size_t pf_wino_wgrad_ws_bytes(int n, int h, int w, int Cin, int Cout);
 int pf_wino_wgrad(const float* dy, int ldy, const float* x, int xcs, int n, int h, int w, int Cin,
                   int Cout, float* dw, float* db, int acc, void* ws, size_t ws_bytes,

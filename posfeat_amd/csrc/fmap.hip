@@ -32,6 +32,26 @@ __global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, int n, int c, i
   }
 }
 
+// datasets' to_input on the device: uint8 HWC RGB -> ImageNet-normalised
+// float NCHW, ((u / 255) - mean[c]) / std[c] with IEEE round-to-nearest fp32
+// division and subtraction -- the same three roundings as numpy's
+// (im.astype(float32) / float32(255) - MEAN) / STD, so the result is
+// bit-identical to the host path (transforms.ToTensor + Normalize,
+// datasets/hpatches.py:14-17).  One thread per pixel: 3 bytes in, 3 floats out.
+__global__ void normalize_rgb8_kernel(const unsigned char* __restrict__ src, int hw, int src_pitch,
+                                      int w, float* __restrict__ dst) {
+  const int b = blockIdx.y;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= hw) return;
+  const int y = p / w, x = p - y * w;
+  const unsigned char* s = src + (long long)b * (hw / w) * src_pitch + (long long)y * src_pitch + x * 3;
+  const float mean[3] = {0.485f, 0.456f, 0.406f}, stdv[3] = {0.229f, 0.224f, 0.225f};
+  float* d = dst + (long long)b * 3 * hw + p;
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+    d[(long long)c * hw] = __fdiv_rn(__fsub_rn(__fdiv_rn((float)s[c], 255.f), mean[c]), stdv[c]);
+}
+
 // 64 pixels x 64 channels tile through LDS.
 __global__ void nhwc_to_nchw_kernel(const float* __restrict__ x, int c, int hw, int csi,
                                     float* __restrict__ y) {
@@ -503,6 +523,15 @@ extern "C" int posfeat_nchw_to_nhwc(const float* x, int n, int c, int h, int w, 
                                     float* y, void* stream) {
   if (!x || !y || n <= 0 || c <= 0 || h <= 0 || w <= 0 || cstride_out < c) return POSFEAT_E_INVALID;
   return pf_nchw_to_nhwc(x, n, c, h, w, cstride_out, y, pf_stream(stream));
+}
+
+extern "C" int posfeat_normalize_rgb8(const unsigned char* src, int b, int h, int w,
+                                      int src_pitch, float* dst, void* stream) {
+  if (!src || !dst || b <= 0 || h <= 0 || w <= 0 || src_pitch < 3 * w) return POSFEAT_E_INVALID;
+  hipLaunchKernelGGL(normalize_rgb8_kernel, dim3((h * w + 255) / 256, b), dim3(256), 0,
+                     pf_stream(stream), src, h * w, src_pitch, w, dst);
+  PF_CHECK_LAUNCH();
+  return POSFEAT_OK;
 }
 
 extern "C" int posfeat_nhwc_to_nchw(const float* x, int n, int c, int h, int w, int cstride_in,

@@ -15,6 +15,8 @@
 // exactly wherever the 3x3 window of conv2 stays inside the image; the
 // one-pixel border ring (where conv2 sees G's zero padding, not the
 // continuation of c) is recomputed directly from the raw c.
+#include <algorithm>
+
 #include "common.h"
 #include "fmap.h"
 
@@ -81,9 +83,10 @@ __global__ __launch_bounds__(128) void gfuse_weights_kernel(
 // is read coalesced across couts and reused for the RP pixels.
 constexpr int GF_RP = 8;
 __global__ __launch_bounds__(GF_COUT) void gfuse_ring_kernel(
-    const float* __restrict__ c, int ccs, int H, int W, const float* __restrict__ mean,
-    const float* __restrict__ rstd, const float* __restrict__ w2t, const float* __restrict__ b2,
-    float* __restrict__ y, int ycs) {
+    const float* __restrict__ c, int ccs, const float* __restrict__ img4,
+    const float* __restrict__ w1, int k1pad, const float* __restrict__ b1, int H, int W,
+    const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ w2t,
+    const float* __restrict__ b2, float* __restrict__ y, int ycs) {
   const int b = blockIdx.y, co = threadIdx.x;
   const int nring = 2 * W + 2 * (H - 2);
   __shared__ float g[GF_RP][9][GF_CG];
@@ -116,8 +119,22 @@ __global__ __launch_bounds__(GF_COUT) void gfuse_ring_kernel(
     const int py = pys[j], px = pxs[j];
     const int qy = py + t / 3 - 1, qx = px + t % 3 - 1;
     float v = 0.f;
-    if (py >= 0 && (unsigned)qy < (unsigned)H && (unsigned)qx < (unsigned)W)
-      v = (c[(((size_t)b * H + qy) * W + qx) * ccs + k] - mb[k]) * rb[k];
+    if (py >= 0 && (unsigned)qy < (unsigned)H && (unsigned)qx < (unsigned)W) {
+      float cv;
+      if (c) {
+        cv = c[(((size_t)b * H + qy) * W + qx) * ccs + k];
+      } else {  // convimg at q from the image (zero padded), the conv's own tap order
+        cv = b1[k];
+        for (int s = 0; s < 9; ++s) {
+          const int iy = qy + s / 3 - 1, ix = qx + s % 3 - 1;
+          if ((unsigned)iy >= (unsigned)H || (unsigned)ix >= (unsigned)W) continue;
+          const float* px = img4 + (((size_t)b * H + iy) * W + ix) * 4;
+          const float* wk = w1 + (size_t)k * k1pad + s * 4;
+          cv += wk[0] * px[0] + wk[1] * px[1] + wk[2] * px[2];
+        }
+      }
+      v = (cv - mb[k]) * rb[k];
+    }
     g[j][t][k] = v;
   }
   __syncthreads();
@@ -134,6 +151,214 @@ __global__ __launch_bounds__(GF_COUT) void gfuse_ring_kernel(
     if (pys[j] >= 0) y[(((size_t)b * H + pys[j]) * W + pxs[j]) * ycs + co] = acc[j];
 }
 
+
+// ---- instance-norm statistics of convimg WITHOUT running convimg ------------
+// c_k(p) = b1_k + w_k . x(p), x(p) = the 27 zero-padded 3x3 x 3-channel image
+// taps around p, so per image mean_k = b1_k + w_k . E[x] and var_k =
+// w_k^T (E[x x^T] - E[x] E[x]^T) w_k.  With x extended by a constant 1 (row
+// 27) the moments are one Gram matrix G = X^T X of the [HW x 32] im2col
+// matrix X: G[27][j] = sum x_j, G[i][j] = sum x_i x_j.  X^T X on fp32 MFMA is
+// one v_mfma_f32_32x32x2_f32 per pixel PAIR whose A and B operands are the
+// SAME register (lane l: x_{l%32} of pixel 2s + l/32).  gfuse_imgmom_kernel:
+// one block per band of 4 rows (staged in LDS), each wave a quarter of the
+// band's pixel pairs; the four 32x32 accumulators are summed into an fp64
+// band partial.  gfuse_imgstats_kernel sums the band partials in order (fp64)
+// and forms mean / rstd for the 64 convimg channels.  Replaces the 3x3 4->64
+// conv over the full-resolution image (and its 629 MB output at B = 8,
+// 480x640): the only other reader of that output, the border ring,
+// recomputes the few values it needs from the image.
+constexpr int IM_TAPS = 27, IM_G = 32;  // moments: 27 taps + the constant row
+constexpr int IM_ROWS = 4;              // output rows per band
+
+__global__ __launch_bounds__(256) void gfuse_imgmom_kernel(const float* __restrict__ img4, int H,
+                                                           int W, double* __restrict__ part) {
+  extern __shared__ float tile[];  // [IM_ROWS + 2][W + 2][3], then the fp64 reduction
+  const int b = blockIdx.y, band = blockIdx.x, r0 = band * IM_ROWS;
+  const int TW = W + 2, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;  // 4 waves
+  const float* ib = img4 + (long long)b * H * W * 4;
+  for (int i = threadIdx.x; i < (IM_ROWS + 2) * TW; i += blockDim.x) {
+    const int ty = i / TW, tx = i - ty * TW;
+    const int y = r0 - 1 + ty, x = tx - 1;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W)
+      v = *reinterpret_cast<const f32x4*>(ib + ((long long)y * W + x) * 4);
+    tile[i * 3] = v.x;
+    tile[i * 3 + 1] = v.y;
+    tile[i * 3 + 2] = v.z;
+  }
+  __syncthreads();
+  // this lane's moment index i = lane % 32: tap (ky, kx), channel c, or 27: 1
+  const int i = lane & 31;
+  const int ti = i / 3, ci = i - ti * 3;
+  const int off = i < IM_TAPS ? ((ti / 3) * TW + ti % 3) * 3 + ci : 0;
+  const float cst = i == IM_TAPS ? 1.f : 0.f;
+  const bool tap = i < IM_TAPS;
+  // wave w owns output row r0 + w; two interleaved accumulator chains so
+  // consecutive MFMAs do not wait on each other
+  f32x16 acc0, acc1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc0[r] = acc1[r] = 0.f;
+  if (r0 + wave < H) {
+    const float* trow = tile + wave * TW * 3 + off + (lane >> 5) * 3;
+    int s = 0;
+    for (; s + 8 <= W / 2; s += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = tap ? trow[(2 * (s + u)) * 3] : cst;
+#pragma unroll
+      for (int u = 0; u < 8; u += 2) {
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(v[u], v[u], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(v[u + 1], v[u + 1], acc1, 0, 0, 0);
+      }
+    }
+    for (; s < W / 2; ++s) {
+      const float v = tap ? trow[(2 * s) * 3] : cst;
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(v, v, acc0, 0, 0, 0);
+    }
+  }
+  __syncthreads();  // the tile is dead: reuse LDS for the wave sum
+  double* red = reinterpret_cast<double*>(tile);  // [4 waves][32][32]
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int gi = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5), gj = lane & 31;
+    red[(wave * IM_G + gi) * IM_G + gj] = (double)acc0[r] + (double)acc1[r];
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < IM_G * IM_G; e += blockDim.x)
+    part[((long long)b * gridDim.x + band) * IM_G * IM_G + e] =
+        (red[e] + red[IM_G * IM_G + e]) + (red[2 * IM_G * IM_G + e] + red[3 * IM_G * IM_G + e]);
+}
+
+// one block per image, one thread per Gram entry: sum the band partials
+// (fixed order), then per convimg channel k: mean = b1 + w.m,
+// var = w^T (S/HW - m m^T) w
+__global__ __launch_bounds__(1024) void gfuse_imgstats_kernel(const double* __restrict__ part,
+                                                             int nband, int HW,
+                                                             const float* __restrict__ w1,
+                                                             int k1pad, const float* __restrict__ b1,
+                                                             float eps, float* __restrict__ mean,
+                                                             float* __restrict__ rstd) {
+  __shared__ double G[IM_G * IM_G];
+  const int b = blockIdx.x;
+  {
+    const int e = threadIdx.x;
+    const double* pe = part + (long long)b * nband * IM_G * IM_G + e;
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    int k = 0;
+    for (; k + 4 <= nband; k += 4) {
+      s0 += pe[(k + 0) * IM_G * IM_G];
+      s1 += pe[(k + 1) * IM_G * IM_G];
+      s2 += pe[(k + 2) * IM_G * IM_G];
+      s3 += pe[(k + 3) * IM_G * IM_G];
+    }
+    for (; k < nband; ++k) s0 += pe[k * IM_G * IM_G];
+    G[e] = ((s0 + s1) + (s2 + s3)) / HW;  // E[x_i x_j], row 27: E[x_j]
+  }
+  __syncthreads();
+  const int k = threadIdx.x;
+  if (k >= GF_CG) return;
+  double w[IM_TAPS];
+  for (int i = 0; i < IM_TAPS; ++i) {
+    const int t = i / 3, c = i - t * 3;
+    w[i] = (double)w1[(size_t)k * k1pad + t * 4 + c];  // packed (kh, kw, cin4)
+  }
+  const double* m = G + IM_TAPS * IM_G;
+  double mu = 0.0;
+  for (int i = 0; i < IM_TAPS; ++i) mu += w[i] * m[i];
+  double q = 0.0;
+  for (int i = 0; i < IM_TAPS; ++i) {
+    double t = 0.0;
+    for (int j = 0; j < IM_TAPS; ++j) t += (G[i * IM_G + j] - m[i] * m[j]) * w[j];
+    q += w[i] * t;
+  }
+  if (q < 0.0) q = 0.0;
+  mean[b * GF_CG + k] = (float)(mu + (double)b1[k]);
+  rstd[b * GF_CG + k] = (float)(1.0 / sqrt(q + (double)eps));
+}
+
+// ---- the folded 5x5 conv on fp32 MFMA ---------------------------------------
+// y[p][co] = bc_b[co] + sum_{t < 25, c < 4} Wc_b[co][t][c] img4[p + t - (2,2)][c]
+// Block = 8 x 32 output pixels of one image; wave w owns rows 2w, 2w+1 (two
+// 32-pixel MFMA row blocks) x all 128 couts.  The 12 x 36 x 4 image patch and
+// the image's 128 x 26 x 4 weights (tap 25 zero, rows padded to 108 floats:
+// conflict-free ds_read_b128) sit in LDS.  K = taps x 4 channels: lane half h
+// reads tap 2g + h of group g (16 B = 4 channels), MFMA j contracts channel j
+// of taps (2g, 2g+1) -- the same pairing on the weights.
+constexpr int G5_TR = 8, G5_TC = 32, G5_PR = G5_TR + 4, G5_PC = G5_TC + 4, G5_WP = 108;
+
+__global__ __launch_bounds__(256) void gfuse_conv5_kernel(const float* __restrict__ img4, int H,
+                                                          int W, const float* __restrict__ wc,
+                                                          const float* __restrict__ bc,
+                                                          float* __restrict__ y, int ycs) {
+  __shared__ __attribute__((aligned(16))) float sw[GF_COUT * G5_WP];
+  __shared__ __attribute__((aligned(16))) float sp[G5_PR * G5_PC * 4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const int b = blockIdx.y;
+  const int ntc = (W + G5_TC - 1) / G5_TC;
+  const int ty0 = (blockIdx.x / ntc) * G5_TR, tx0 = (blockIdx.x % ntc) * G5_TC;
+  const float* ib = img4 + (long long)b * H * W * 4;
+  const float* wb = wc + (long long)b * GF_COUT * GF_KPAD;
+  for (int i = tid; i < GF_COUT * 26; i += 256) {  // weights: [co][tap][4] -> padded rows
+    const int co = i / 26, t = i - co * 26;
+    *reinterpret_cast<f32x4*>(sw + co * G5_WP + t * 4) =
+        *reinterpret_cast<const f32x4*>(wb + (long long)co * GF_KPAD + t * 4);
+  }
+  for (int i = tid; i < G5_PR * G5_PC; i += 256) {  // image patch, zero outside
+    const int py = i / G5_PC, px = i - py * G5_PC;
+    const int yy = ty0 - 2 + py, xx = tx0 - 2 + px;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W)
+      v = *reinterpret_cast<const f32x4*>(ib + ((long long)yy * W + xx) * 4);
+    *reinterpret_cast<f32x4*>(sp + i * 4) = v;
+  }
+  __syncthreads();
+  f32x16 acc[2][4];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
+  const int col = lane & 31;
+#pragma unroll
+  for (int g = 0; g < 13; ++g) {
+    const int t = 2 * g + h;
+    const int ta = t < 25 ? t : 24;  // tap 25: zero weights (any finite A)
+    const int u = ta / 5, v = ta - u * 5;
+    f32x4 a[2], bw[4];
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+      a[mi] = *reinterpret_cast<const f32x4*>(sp + (((2 * wave + mi + u) * G5_PC) + col + v) * 4);
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+      bw[ni] = *reinterpret_cast<const f32x4*>(sw + (ni * 32 + col) * G5_WP + t * 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[mi][j], bw[ni][j], acc[mi][ni],
+                                                              0, 0, 0);
+  }
+  // acc[mi][ni][r]: pixel (row 2w + mi, column (r&3) + 8(r>>2) + 4h), cout ni*32 + lane%32
+  const float* bcb = bc + (long long)b * GF_COUT;
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi) {
+    const int yy = ty0 + 2 * wave + mi;
+    if (yy >= H) continue;
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const int co = ni * 32 + col;
+      const float bias = bcb[co];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int xx = tx0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (xx < W) y[((long long)(b * H + yy) * W + xx) * ycs + co] = acc[mi][ni][r] + bias;
+      }
+    }
+  }
+}
 }  // namespace
 
 // wc (n*128*128) | bc (n*128) | w2t (9*64*128)
@@ -161,28 +386,42 @@ int pf_gfuse_weights(const float* w2_packed, const float* b2, const float* w1_pa
 // exact border ring from the raw convimg output c (pitch ccs)
 int pf_gfuse_conv(const float* img4, const float* c, int ccs, int n, int H, int W,
                   const float* wc, const float* bc, const float* mean, const float* rstd,
-                  const float* w2_packed, const float* b2, float* y, int ycs, hipStream_t st) {
-  posfeat_conv_desc d{};
-  d.n = 1;
-  d.h = H;
-  d.w = W;
-  d.cin = 4;
-  d.x_cstride = 4;
-  d.cout = GF_COUT;
-  d.kh = d.kw = 5;
-  d.stride = 1;
-  d.pad = 2;
-  d.y_cstride = ycs;
-  d.res_cstride = 0;
-  d.act = POSFEAT_ACT_NONE;
-  for (int b = 0; b < n; ++b)
-    PF_TRY(pf_conv_run_tile(&d, img4 + (size_t)b * H * W * 4, wc + (size_t)b * GF_COUT * GF_KPAD,
-                            bc + (size_t)b * GF_COUT, nullptr, y + (size_t)b * H * W * ycs, nullptr,
-                            0, -1, st));
+                  const float* w2_packed, const float* b2, float* y, int ycs, hipStream_t st,
+                  const float* w1_packed, const float* b1) {
+  if (!c && !(w1_packed && b1)) return POSFEAT_E_INVALID;
+  if (ycs % 4 || n <= 0) return POSFEAT_E_INVALID;
+  const int ntiles = ((W + G5_TC - 1) / G5_TC) * ((H + G5_TR - 1) / G5_TR);
+  hipLaunchKernelGGL(gfuse_conv5_kernel, dim3(ntiles, n), dim3(256), 0, st, img4, H, W, wc, bc, y,
+                     ycs);
+  PF_CHECK_LAUNCH();
   (void)w2_packed;
+  const int k1pad = posfeat_conv_packed_k(3, 3, 3);
   const int nring = 2 * W + 2 * (H - 2);
   hipLaunchKernelGGL(gfuse_ring_kernel, dim3((nring + GF_RP - 1) / GF_RP, n), dim3(GF_COUT), 0, st,
-                     c, ccs, H, W, mean, rstd, bc + (size_t)n * GF_COUT, b2, y, ycs);
+                     c, ccs, img4, w1_packed, k1pad, b1, H, W, mean, rstd,
+                     bc + (size_t)n * GF_COUT, b2, y, ycs);
+  PF_CHECK_LAUNCH();
+  return POSFEAT_OK;
+}
+
+size_t pf_gfuse_imgstats_ws_bytes(int n, int H) {
+  return pf_align((size_t)n * ((H + IM_ROWS - 1) / IM_ROWS) * IM_G * IM_G * sizeof(double), 256);
+}
+
+// convimg's instance-norm mean / rstd [n][64] from the image moments (no conv)
+int pf_gfuse_imgstats(const float* img4, int n, int H, int W, const float* w1_packed,
+                      const float* b1, float* mean, float* rstd, void* ws, size_t ws_bytes,
+                      hipStream_t st) {
+  if (!ws || ws_bytes < pf_gfuse_imgstats_ws_bytes(n, H)) return POSFEAT_E_WORKSPACE;
+  const int nband = (H + IM_ROWS - 1) / IM_ROWS;
+  const size_t lds = std::max((size_t)(IM_ROWS + 2) * (W + 2) * 3 * sizeof(float),
+                              (size_t)4 * IM_G * IM_G * sizeof(double));
+  if (lds > 160 * 1024 || W % 2) return POSFEAT_E_UNSUPPORTED;
+  double* part = static_cast<double*>(ws);
+  hipLaunchKernelGGL(gfuse_imgmom_kernel, dim3(nband, n), dim3(256), lds, st, img4, H, W, part);
+  PF_CHECK_LAUNCH();
+  hipLaunchKernelGGL(gfuse_imgstats_kernel, dim3(n), dim3(IM_G * IM_G), 0, st, part, nband, H * W,
+                     w1_packed, posfeat_conv_packed_k(3, 3, 3), b1, 1e-5f, mean, rstd);
   PF_CHECK_LAUNCH();
   return POSFEAT_OK;
 }

@@ -2,11 +2,23 @@
 
 ``ExtractionEngine`` owns the packed, BN-folded weight blob on the device
 (built once from the reference-layout state dicts, or received by RCCL
-broadcast) and one engine instance + workspace per input shape.  ``run``
-issues the whole ResUNet + KeypointDet forward on the current stream with a
-single C call (~70 kernel launches, no host synchronisation).
+broadcast) and one engine instance per input shape.  ``run`` issues the whole
+ResUNet + KeypointDet forward on the current stream with a single C call
+(~70 kernel launches, no host synchronisation).
+
+Real datasets (HPatches, Aachen) come in many image sizes.  The instances are
+kept in a least-recently-used map of at most ``POSFEAT_ENGINE_MAX_SHAPES``
+(default 8) shapes, and the inference instances share ONE grow-only workspace
+(the workspace is pure per-run scratch; runs are ordered on the caller's
+stream), so device memory is bounded by the largest shape seen, not by the
+number of shapes.  ``train=True`` instances keep their own workspace: it holds
+the head's intermediates between ``run`` and ``head_backward``.  Conv tile
+choices are cached process-wide by conv descriptor (engine.hip: tile_cache),
+so a new shape times only the convs it has not met.
 """
 import ctypes
+import os
+from collections import OrderedDict
 
 import numpy as np
 import torch
@@ -32,22 +44,50 @@ class ExtractionEngine:
             raise ValueError("weight blob larger than the engine layout")
         self.wdev = torch.zeros(nfl, dtype=torch.float32, device=self.device)
         self.wdev[:blob.numel()].copy_(blob.reshape(-1).to(self.device))
-        self._inst = {}
+        self._inst = OrderedDict()   # (b, h, w) -> (handle, workspace bytes)
+        self._own_ws = {}            # train=True: (b, h, w) -> own workspace
+        self._shared_ws = None       # train=False: one grow-only workspace
+        self.max_shapes = max(1, int(os.environ.get("POSFEAT_ENGINE_MAX_SHAPES", "8")))
 
     # ------------------------------------------------------------------
     def _instance(self, b, h, w):
         key = (b, h, w)
         inst = self._inst.get(key)
         if inst is None:
+            while len(self._inst) >= self.max_shapes:
+                old, (oh, _) = self._inst.popitem(last=False)
+                lib().posfeat_model_destroy(oh)
+                self._own_ws.pop(old, None)
             handle = ctypes.c_void_p()
             create = lib().posfeat_model_create_train if self.train else lib().posfeat_model_create
             check(create(b, h, w, ptr(self.wdev), ctypes.byref(handle)))
-            nbytes = lib().posfeat_model_workspace(handle)
-            ws = torch.empty(nbytes + 256, dtype=torch.uint8, device=self.device)
-            off = (-ws.data_ptr()) % 256
-            inst = (handle, ws, off)
+            inst = (handle, int(lib().posfeat_model_workspace(handle)))
             self._inst[key] = inst
-        return inst
+        else:
+            self._inst.move_to_end(key)
+        handle, nbytes = inst
+        if self.train:
+            ws = self._own_ws.get(key)
+            if ws is None:
+                ws = self._own_ws[key] = torch.empty(nbytes + 256, dtype=torch.uint8,
+                                                     device=self.device)
+        else:
+            ws = self._shared_ws
+            if ws is None or ws.numel() < nbytes + 256:
+                self._shared_ws = None
+                ws = self._shared_ws = torch.empty(nbytes + 256, dtype=torch.uint8,
+                                                   device=self.device)
+        return handle, ws, (-ws.data_ptr()) % 256
+
+    @property
+    def cached_shapes(self):
+        return list(self._inst.keys())
+
+    @property
+    def workspace_bytes(self):
+        """device bytes held in engine workspaces"""
+        n = sum(t.numel() for t in self._own_ws.values())
+        return n + (self._shared_ws.numel() if self._shared_ws is not None else 0)
 
     def set_timing(self, b, h, w, enable=True):
         handle, _, _ = self._instance(b, h, w)
@@ -77,7 +117,7 @@ class ExtractionEngine:
         """img: [b,3,h,w] fp32 on the device (h, w multiples of 16).
 
         Returns a dict of NCHW tensors plus ``_local_map_nhwc`` -- a view into
-        the engine workspace (valid until the next ``run`` of the same shape).
+        the engine workspace (valid until the next ``run`` of this engine).
         """
         if img.dtype != torch.float32 or img.dim() != 4 or img.shape[1] != 3:
             raise ValueError("img must be float32 [b,3,h,w]")
@@ -191,9 +231,11 @@ class ExtractionEngine:
                                 float(lr), stream_ptr()))
 
     def close(self):
-        for handle, _, _ in self._inst.values():
+        for handle, _ in self._inst.values():
             lib().posfeat_model_destroy(handle)
         self._inst.clear()
+        self._own_ws.clear()
+        self._shared_ws = None
 
     def __del__(self):
         try:

@@ -54,15 +54,30 @@ def sample_feat_by_coord(x, coord_n, norm=False, nhwc=None):
 
 def generate_kpts_single(kp_map, nms_radius, num_pts=False, scale=4, stable=True, temperature=1,
                          stride=1, use_nms=True, thr=False, thr_mod="mean"):
+    _, coord, score, _, _ = _detect(kp_map, nms_radius, num_pts, stable, stride, use_nms, thr,
+                                    thr_mod, sync=True)
+    return coord, score
+
+
+def generate_kpts_single_async(kp_map, nms_radius, num_pts=False, scale=4, stable=True,
+                               temperature=1, stride=1, use_nms=True, thr=False, thr_mod="mean"):
+    """generate_kpts_single without the host synchronisation: full-capacity
+    (coord_n [b,cap,2], kp_score [b,cap,1]) plus the per-image counts [b] on
+    the device (rows beyond count are unused)."""
+    _, coord, score, counts, _ = _detect(kp_map, nms_radius, num_pts, stable, stride, use_nms,
+                                         thr, thr_mod, sync=False)
+    return coord, score, counts
+
+
+def _detect(kp_map, nms_radius, num_pts, stable, stride, use_nms, thr, thr_mod, sync):
     if not stable:
         raise NotImplementedError("stable=False (gumbel sampling) is not implemented")
     if use_nms == "softnms":
         raise NotImplementedError("use_nms='softnms' is not implemented")
     if stride != 1:
         raise NotImplementedError("stride != 1 is not implemented")
-    _, coord, score, _, _ = ops.detect(kp_map.float().contiguous(), nms_radius, num_pts,
-                                       use_nms=bool(use_nms), thr=thr, thr_mod=thr_mod)
-    return coord, score
+    return ops.detect(kp_map.float().contiguous(), nms_radius, num_pts, use_nms=bool(use_nms),
+                      thr=thr, thr_mod=thr_mod, sync=sync)
 
 
 def nms(score, patch_radius):

@@ -12,19 +12,40 @@ MI355X-specific behaviour:
 * one process per GPU (torchrun / --local_rank); rank 0 broadcasts weights
   over RCCL (PoSFeat.set_parallel) and ranks extract disjoint image shards;
 * descriptors are sampled from the engine's NHWC local_map (coalesced);
-* no CPU path: without a gfx950 GPU the constructor raises.
-Out of scope (diagnostics): save_imgs visualisation, h5 export.
+* no CPU path: without a gfx950 GPU the constructor raises;
+* the default loop is a pipeline (``_extract_pipelined``): consecutive images
+  of the same size are run as one engine batch (up to
+  ``POSFEAT_EXTRACT_GROUP``, default 8; instance norm and eval BatchNorm are
+  per image, so each image's maps are those of a batch-1 run up to fp32
+  summation order), only the uint8 image crosses PCIe (pinned, normalised on
+  the device by posfeat_normalize_rgb8, bit-identical to the host transform),
+  detection / sampling run without host synchronisation, results come back by
+  async D2H copies, and the files are written by a writer thread while the
+  GPU works on the next group.  Same files, same names, same log lines;
+  ``POSFEAT_EXTRACT_PIPELINE=0`` runs the reference's serial loop;
+* ``POSFEAT_EXTRACT_TIMING=1`` (serial loop) synchronises the device at the stage
+  boundaries and reports per-stage time (load = decode + normalise in the
+  loader, h2d, engine, detect = detector + descriptor sampler, save = D2H +
+  np.savez / h5) in ``self.stats`` and the log; without it only the wall time
+  and images/s are recorded (no extra synchronisation).
+``save_h5`` writes the reference's layout (extractor.py:273-314:
+``<desc_root>h5/<seq>/{keypoints,descriptors,scores,scales}.h5`` keyed by image
+name, plus ``feat.h5`` groups for hloc) through h5py; h5py is not part of this
+image, so the option fails at construction when it is missing.
+Out of scope (diagnostics): save_imgs visualisation.
 """
 import logging
 import os
 import time
+from collections import deque
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 import torch
 import torch.distributed as dist
 import yaml
 
-from .. import datasets, networks
+from .. import datasets, networks, ops
 from ..losses import preprocess_utils as putils
 from ..losses.preprocess_utils import denormalize_coords, normalize_coords, sample_feat_by_coord
 
@@ -44,7 +65,10 @@ class Extractor:
         self.save_npz = self.config.get("save_npz", True)
         self.save_h5 = self.config.get("save_h5", False)
         if self.save_h5:
-            raise NotImplementedError("save_h5 (h5py export) is out of scope")
+            try:
+                import h5py  # noqa: F401
+            except ImportError as e:
+                raise ImportError("save_h5: True needs h5py, which is not installed") from e
 
         cfg_path = os.path.join(os.path.dirname(str(self.config["load_path"])), "config.yaml")
         if os.path.exists(cfg_path):
@@ -76,7 +100,7 @@ class Extractor:
         self.extract_loader = torch.utils.data.DataLoader(
             extract_dataset, batch_size=self.config["data_config_extract"]["batch_size"],
             shuffle=False, num_workers=self.config["data_config_extract"].get("workers", 0),
-            collate_fn=self.my_collate, sampler=sampler)
+            collate_fn=self.my_collate, sampler=sampler, pin_memory=True)
 
     def my_collate(self, batch):
         batch = list(filter(lambda b: b is not None, batch))
@@ -128,12 +152,37 @@ class Extractor:
         save_path = os.path.join(self.desc_root, name)
         os.makedirs(os.path.dirname(save_path), exist_ok=True)
         message = "\nkpts: {}".format(kpt.shape[0])
+        desc = feat_f.squeeze(0).detach().cpu().numpy()
+        scores = kp_score.squeeze(0).detach().cpu().numpy()
         if self.save_npz:
-            desc = feat_f.squeeze(0).detach().cpu().numpy()
-            scores = kp_score.squeeze(0).detach().cpu().numpy()
             with open(save_path + ".{}".format(self.config["postfix"]), "wb") as output_file:
                 np.savez(output_file, keypoints=kpt, scores=scores, descriptors=desc)
+        if self.save_h5:
+            h, w = inputs["im1"].shape[-2:]
+            self._write_h5(name, kpt, desc, scores, w, h)
         return message
+
+    def _write_h5(self, name, kpt, desc, scores, w, h):
+        """The reference's h5 layout (extractor.py:273-314): per sequence
+        keypoints/descriptors/scores/scales.h5 datasets named by the image's
+        base name, and feat.h5 groups (hloc input) named by the full name."""
+        import h5py
+        h5_path = self.desc_root + "h5"          # the reference's path concatenation
+        h5_name = name.split(".")[0]
+        h5_seq = "/".join(h5_name.split("/")[:-1])
+        h5_name = h5_name.split("/")[-1]
+        seq_dir = os.path.join(h5_path, h5_seq)
+        os.makedirs(seq_dir, exist_ok=True)
+        for fname, data in (("keypoints", kpt), ("descriptors", desc), ("scores", scores),
+                            ("scales", np.ones_like(scores))):
+            with h5py.File(os.path.join(seq_dir, fname + ".h5"), "a") as f:
+                f[h5_name] = data
+        with h5py.File(os.path.join(h5_path, "feat.h5"), "a") as f:
+            grp = f.create_group(name)
+            grp.create_dataset("keypoints", data=kpt)
+            grp.create_dataset("scores", data=scores)
+            grp.create_dataset("descriptors", data=desc)
+            grp.create_dataset("image_size", data=np.array([w, h]))
 
     def process(self, inputs, outputs, remove_pad=False):
         desc_f = outputs["local_map"]
@@ -162,27 +211,184 @@ class Extractor:
 
     @torch.no_grad()
     def extract(self):
+        if (os.environ.get("POSFEAT_EXTRACT_PIPELINE", "1") == "0"
+                or os.environ.get("POSFEAT_EXTRACT_TIMING", "0") == "1"
+                or self.detector is not putils.generate_kpts_single):
+            return self._extract_serial()
+        return self._extract_pipelined()
+
+    # ------------------------------------------------------------ pipelined
+    def _det_cfg(self, name):
+        if self.config["data"] == "Aachen_Day_Night" and name.split("/")[0] == "query":
+            return self.config["detector_config_query"]
+        return self.config["detector_config"]
+
+    def _launch_group(self, items):
+        """Engine + detector + sampler for a list of same-size images, all
+        enqueued on the current stream; returns (event, per-image host copies)."""
+        dev = self.device
+        # per-image async copies from the loader's pinned buffers (a host-side
+        # stack would be pageable, and a pageable H2D copy waits for the stream)
+        if all(it[1] is not None for it in items):
+            u8 = torch.empty((len(items),) + tuple(items[0][1].shape), dtype=torch.uint8,
+                             device=dev)
+            for i, it in enumerate(items):
+                u8[i].copy_(it[1], non_blocking=True)
+            im = ops.normalize_rgb8(u8)
+        else:
+            im = torch.empty((len(items),) + tuple(items[0][0].shape), device=dev)
+            for i, it in enumerate(items):
+                im[i].copy_(it[0], non_blocking=True)
+        g, _, h, w = im.shape
+        t1 = time.perf_counter()
+        eng = self.model.engine()
+        t2 = time.perf_counter()
+        out = eng.run(im, outputs=())
+        t3 = time.perf_counter()
+        nhwc = out["_local_map_nhwc"]
+        host = []
+        for i, (_, _, name, scale) in enumerate(items):
+            coord_n, score, counts = putils.generate_kpts_single_async(
+                out["local_point"][i:i + 1], **self._det_cfg(name))
+            desc = ops.sample_desc_nhwc(nhwc[i:i + 1], coord_n, c=128,
+                                        normalize=self.config["loss_distance"] == "cos",
+                                        n_valid=counts)
+            host.append((name, scale, counts.to("cpu", non_blocking=True),
+                         coord_n.to("cpu", non_blocking=True), desc.to("cpu", non_blocking=True),
+                         score.to("cpu", non_blocking=True), w, h))
+        ev = torch.cuda.Event()
+        ev.record()
+        if os.environ.get("POSFEAT_EXTRACT_TRACE", "0") == "1":
+            print("[extract]   engine() %.1f ms, run %.1f ms, detect/sample/D2H %.1f ms" % (
+                1e3 * (t2 - t1), 1e3 * (t3 - t2), 1e3 * (time.perf_counter() - t3)), flush=True)
+        return ev, host
+
+    def _finish_group(self, ev, host, writer, futures):
+        ev.synchronize()
+        for name, scale, counts, kpt, desc, score, w, h in host:
+            n = int(counts[0])
+            # denormalize_coords on the host: the same two fp32 roundings
+            # (x * c, then + c) as the device path; a host->device copy of c
+            # here would wait for the whole queue
+            c = np.array([(w - 1) / 2.0, (h - 1) / 2.0], np.float32)
+            k = kpt[0, :n].numpy() * c + c
+            if scale is not None:
+                k = k * scale
+            processed = {"kpt": k, "desc": desc[:, :n], "kp_score": score[:, :n]}
+            inputs = {"name1": [name], "im1": torch.empty(1, 3, h, w, device="meta")}
+            if self.config["output_desc"]:
+                futures.append(writer.submit(self._save_and_log, inputs, processed))
+            else:
+                self.logger.info(name)
+
+    def _save_and_log(self, inputs, processed):
+        self.logger.info(inputs["name1"][0] + self.save_desc(inputs, None, processed))
+
+    def _extract_pipelined(self):
+        group = max(1, int(os.environ.get("POSFEAT_EXTRACT_GROUP", "8")))
+        writer = ThreadPoolExecutor(1 if self.save_h5 else 4)
+        futures, pending, buf = [], deque(), []
+        self.group_shapes = []
         name_list = ""
-        t0 = time.time()
         n = 0
+        t0 = time.perf_counter()
+
+        trace = os.environ.get("POSFEAT_EXTRACT_TRACE", "0") == "1"
+
+        marks = []   # (launch time, images launched so far): steady-state rate
+
+        def flush():
+            if buf:
+                ta = time.perf_counter()
+                marks.append((ta - t0, n - len(buf)))
+                pending.append(self._launch_group(list(buf)))
+                if trace:
+                    print("[extract] group %d x %s launched in %.1f ms at %.3f s" % (
+                        len(buf), tuple(buf[0][0].shape[1:]), 1e3 * (time.perf_counter() - ta),
+                        ta - t0), flush=True)
+                buf.clear()
+            while len(pending) > 1:   # keep one group in flight behind the host
+                self._finish_group(*pending.popleft(), writer, futures)
+
+        for inputs in self.extract_loader:
+            names = inputs["name1"]
+            im1 = inputs["im1"]
+            ori = inputs.get("im1_ori")
+            scale = inputs.get("scale")
+            for i in range(im1.shape[0]):
+                item = (im1[i], ori[i] if ori is not None and ori.dim() == 4 else None, names[i],
+                        scale[i].numpy() if scale is not None else None)
+                if buf and (buf[0][0].shape != item[0].shape or len(buf) >= group):
+                    self.group_shapes.append(tuple(buf[0][0].shape))
+                    flush()
+                buf.append(item)
+                name_list += "{} {}\n".format(n, names[i])
+                n += 1
+        if buf:
+            self.group_shapes.append(tuple(buf[0][0].shape))
+        flush()
+        while pending:
+            self._finish_group(*pending.popleft(), writer, futures)
+        for f in futures:
+            f.result()
+        writer.shutdown()
+        if self.output_flag:
+            with open(os.path.join(self.img_root, "name_list.txt"), "w") as f:
+                f.write(name_list)
+        dt = time.perf_counter() - t0
+        self.stats = {"images": n, "seconds": dt, "images_per_s": n / dt if dt > 0 else 0.0,
+                      "stage_ms_per_image": None, "pipeline": True, "group": group,
+                      "group_marks": marks}
+        self.logger.info("extracted %d images in %.2fs (%.1f images/s, pipelined)" % (
+            n, dt, self.stats["images_per_s"]))
+        return n
+
+    # ------------------------------------------------------------ serial
+    def _extract_serial(self):
+        prof = os.environ.get("POSFEAT_EXTRACT_TIMING", "0") == "1"
+        stages = dict.fromkeys(("load", "h2d", "engine", "detect", "save"), 0.0)
+
+        def mark(stage, t):
+            if prof:
+                torch.cuda.synchronize(self.device)
+            now = time.perf_counter()
+            stages[stage] += now - t
+            return now
+
+        name_list = ""
+        t0 = time.perf_counter()
+        n = 0
+        t = t0
         for idx, inputs in enumerate(self.extract_loader):
+            t = mark("load", t)
             for key, val in inputs.items():
                 if key in ("name1", "pad1"):
                     continue
                 inputs[key] = val.to(self.device, non_blocking=True)
+            t = mark("h2d", t)
             message = inputs["name1"][0]
             outputs = self.model.extract(inputs["im1"])
+            t = mark("engine", t)
             processed = self.process(inputs, outputs)
+            t = mark("detect", t)
             if self.config["output_desc"]:
                 message += self.save_desc(inputs, outputs, processed)
+            t = mark("save", t)
             self.logger.info(message)
             name_list += "{} {}\n".format(idx, inputs["name1"][0])
             n += 1
+        torch.cuda.synchronize(self.device)
         if self.output_flag:
             with open(os.path.join(self.img_root, "name_list.txt"), "w") as f:
                 f.write(name_list)
-        dt = time.time() - t0
-        self.logger.info("extracted %d images in %.2fs" % (n, dt))
+        dt = time.perf_counter() - t0
+        self.stats = {"images": n, "seconds": dt, "images_per_s": n / dt if dt > 0 else 0.0,
+                      "stage_ms_per_image": ({k: 1e3 * v / max(n, 1) for k, v in stages.items()}
+                                             if prof else None), "pipeline": False}
+        self.logger.info("extracted %d images in %.2fs (%.1f images/s)%s" % (
+            n, dt, self.stats["images_per_s"],
+            "" if not prof else " stages ms/image: " + ", ".join(
+                "%s %.2f" % kv for kv in self.stats["stage_ms_per_image"].items())))
         return n
 
 

@@ -125,6 +125,20 @@ def nchw_to_nhwc(x, cstride=None):
     return y
 
 
+def normalize_rgb8(u8):
+    """uint8 [b,h,w,3] (or [h,w,3]) RGB on the device -> ImageNet-normalised
+    float [b,3,h,w], bit-identical to datasets.to_input's host computation."""
+    if u8.dtype != torch.uint8 or u8.shape[-1] != 3 or u8.dim() not in (3, 4):
+        raise ValueError("expected uint8 [b,h,w,3]")
+    if u8.dim() == 3:
+        u8 = u8[None]
+    u8 = u8.contiguous()
+    b, h, w, _ = u8.shape
+    out = torch.empty(b, 3, h, w, dtype=torch.float32, device=u8.device)
+    check(lib().posfeat_normalize_rgb8(ptr(u8), b, h, w, 3 * w, ptr(out), stream_ptr()))
+    return out
+
+
 def nhwc_to_nchw(x, c=None):
     _f32(x, "x")
     n, h, w, cs = x.shape

@@ -12,8 +12,12 @@
   detector configuration (configs/extract_aachen.yaml: nms_radius 3, thr 0.5).
 * The engine's non-default paths behind environment switches (POSFEAT_SIDE=0:
   serial image branch; POSFEAT_UP4TAP=0: head.conv2's upsampled part as the
-  low-res Winograd F(4x4) conv; POSFEAT_UP4WINO=0 with it: by bilinear phases)
-  agree with the default engine (SIDE: bit-identical; the others: 1e-4).
+  low-res Winograd F(4x4) conv; POSFEAT_UP4WINO=0 with it: by bilinear phases;
+  POSFEAT_IMGSTATS=0: convimg's instance-norm statistics from the convimg conv
+  instead of the image's tap moments) agree with the default engine (SIDE:
+  bit-identical; the others: 1e-4).  (POSFEAT_DISK_FLASH does not touch the
+  extraction engine: a no-op guard here, the DiskLoss A/B is in
+  test_gpu_correlation.py.)
 """
 import os
 
@@ -139,7 +143,8 @@ def test_aachen_shapes_vs_oracle(gpu, hw):
 
 
 @pytest.mark.parametrize("switch,exact", [("POSFEAT_SIDE", True), ("POSFEAT_UP4WINO", False),
-                                          ("POSFEAT_UP4TAP", False)])
+                                          ("POSFEAT_UP4TAP", False), ("POSFEAT_IMGSTATS", False),
+                                          ("POSFEAT_DISK_FLASH", True)])
 def test_env_switch_paths_match_default(gpu, switch, exact, monkeypatch):
     from posfeat_amd.weights import seeded_image
     imgs = torch.from_numpy(np.stack([seeded_image(s, 96, 128) for s in (4, 5)])).to(gpu)
@@ -161,3 +166,33 @@ def test_env_switch_paths_match_default(gpu, switch, exact, monkeypatch):
             assert e <= TOL * s, "%s=0: %s err %g" % (switch, k, e)
     base.close()
     alt.close()
+
+
+def test_engine_shape_cache_lru_and_shared_workspace(gpu, monkeypatch):
+    """Many image sizes (HPatches / Aachen): at most POSFEAT_ENGINE_MAX_SHAPES
+    instances are kept (least recently used evicted), inference instances
+    share one grow-only workspace, and a shape planned after an eviction (its
+    tiles from the process-wide cache, or from a similar shape) gives the
+    same maps as a fresh engine."""
+    from posfeat_amd.weights import seeded_image
+    monkeypatch.setenv("POSFEAT_ENGINE_MAX_SHAPES", "2")
+    eng = _new_engine(gpu)
+    shapes = [(96, 128), (128, 160), (112, 144), (96, 128)]
+    outs = []
+    for h, w in shapes:
+        img = torch.from_numpy(seeded_image(7, h, w))[None].to(gpu)
+        o = eng.run(img)
+        outs.append({k: o[k].clone() for k in ("local_point", "local_map")})
+        assert len(eng.cached_shapes) <= 2
+    assert eng.cached_shapes == [(1, 112, 144), (1, 96, 128)]
+    assert eng.workspace_bytes == eng._shared_ws.numel()
+    for k in ("local_point", "local_map"):          # re-planned shape: same result
+        assert torch.equal(outs[0][k], outs[3][k]), k
+    fresh = _new_engine(gpu)
+    img = torch.from_numpy(seeded_image(7, 112, 144))[None].to(gpu)
+    ref = fresh.run(img)
+    for k in ("local_point", "local_map"):
+        e, s = _maxerr(outs[2][k], ref[k])
+        assert e <= TOL * s, k
+    fresh.close()
+    eng.close()

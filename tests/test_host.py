@@ -150,3 +150,54 @@ def test_bench_launcher_spawns_world2():
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == 2 and rec["ranks_seen"] == 2 and rec["steps"] == 3
     assert rec["value"] > 0
+
+
+def test_h5_export_layout(tmp_path, monkeypatch):
+    """save_h5 writes the reference's layout (managers/extractor.py:273-314):
+    <desc_root>h5/<seq>/{keypoints,descriptors,scores,scales}.h5 datasets named
+    by the image's base name and feat.h5 groups named by the full name.  h5py
+    is not in this image: a recording stand-in checks the calls."""
+    import sys
+    import types
+    files = {}
+
+    class _Group(dict):
+        def create_dataset(self, k, data):
+            self[k] = np.asarray(data)
+
+    class _File(dict):
+        def __init__(self, path, mode):
+            super().__init__()
+            assert mode == "a"
+            self.path = path
+            files.setdefault(path, {})
+
+        def __enter__(self):
+            return self
+
+        def __exit__(self, *a):
+            return False
+
+        def __setitem__(self, k, v):
+            files[self.path][k] = np.asarray(v)
+
+        def create_group(self, k):
+            g = files[self.path][k] = _Group()
+            return g
+
+    monkeypatch.setitem(sys.modules, "h5py", types.SimpleNamespace(File=_File))
+    from posfeat_amd.managers.extractor import Extractor
+    ex = Extractor.__new__(Extractor)
+    ex.desc_root = str(tmp_path / "desc")
+    kpt = np.arange(10, dtype=np.float32).reshape(5, 2)
+    desc = np.ones((5, 128), np.float32)
+    sc = np.full((5, 1), 0.5, np.float32)
+    ex._write_h5("v_seq/3.ppm", kpt, desc, sc, 640, 480)
+    root = str(tmp_path / "desc") + "h5"
+    for f, want in (("keypoints", kpt), ("descriptors", desc), ("scores", sc),
+                    ("scales", np.ones_like(sc))):
+        np.testing.assert_array_equal(files[os.path.join(root, "v_seq", f + ".h5")]["3"], want)
+    g = files[os.path.join(root, "feat.h5")]["v_seq/3.ppm"]
+    np.testing.assert_array_equal(g["image_size"], [640, 480])
+    np.testing.assert_array_equal(g["keypoints"], kpt)
+    assert os.path.isdir(os.path.join(root, "v_seq"))

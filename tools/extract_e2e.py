@@ -1,0 +1,122 @@
+"""extract.py end to end on a synthetic HPatches-layout directory with the
+reference's own configs/extract_hpatches.yaml (batch 1, num_pts 8192, 4
+loader workers), timed per stage.
+
+Builds <tmp>/data/hpatches-sequences-release/<seq>/{1..6}.ppm from seeded
+uint8 noise at HPatches-like sizes (several shapes per run, as the real
+dataset has), a checkpoint directory <tmp>/ckpts/keypoint/005 holding the
+seeded weights (backbone.pth / localheader.pth; the effective model_config in
+<tmp>/ckpts/keypoint/config.yaml, where training writes it), then runs the
+Extractor in this fresh process, as a user would: the whole-run rate includes
+building the engine and planning/autotuning one instance per image size;
+``steady_images_per_s`` counts from the first group of a size met before.
+``--passes 2`` adds a second pass in the same process.  ``--timing``: the
+reference's serial loop with synchronising per-stage timers.  Prints one JSON
+line.
+
+usage: python tools/extract_e2e.py [--seqs 12] [--timing] [--passes 1]
+"""
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+import yaml
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+# (h, w) of HPatches-like images (the dataset crops to multiples of 16)
+SIZES = [(480, 640), (600, 800), (752, 1000)]
+
+
+def make_dataset(root, nseq):
+    from PIL import Image
+    for s in range(nseq):
+        h, w = SIZES[s % len(SIZES)]
+        d = os.path.join(root, "data", "hpatches-sequences-release", "v_synth%02d" % s)
+        os.makedirs(d, exist_ok=True)
+        rs = np.random.RandomState(100 + s)
+        base = rs.randint(0, 256, (h // 8, w // 8, 3)).astype(np.uint8)
+        for i in range(1, 7):
+            im = Image.fromarray(base).resize((w, h), Image.BILINEAR)
+            arr = np.asarray(im).astype(np.int16) + rs.randint(-12, 13, (h, w, 3))
+            Image.fromarray(np.clip(arr, 0, 255).astype(np.uint8)).save(os.path.join(d, "%d.ppm" % i))
+
+
+def make_checkpoint(root):
+    import torch
+    from posfeat_amd.weights import seeded_state_dicts
+    ck = os.path.join(root, "ckpts", "keypoint", "005")
+    os.makedirs(ck, exist_ok=True)
+    bb, hd = seeded_state_dicts(0)
+    torch.save(bb, os.path.join(ck, "backbone.pth"))
+    torch.save(hd, os.path.join(ck, "localheader.pth"))
+    syn = yaml.safe_load(open(os.path.join(ROOT, "configs", "extract_synthetic.yaml")))
+    yaml.safe_dump({"model": "PoSFeat", "model_config": syn["model_config"]},
+                   open(os.path.join(os.path.dirname(ck), "config.yaml"), "w"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seqs", type=int, default=12)
+    ap.add_argument("--timing", action="store_true", help="per-stage (synchronising) timing")
+    ap.add_argument("--passes", type=int, default=1, help="2: a second (warm) pass")
+    args = ap.parse_args()
+    if args.timing:
+        os.environ["POSFEAT_EXTRACT_TIMING"] = "1"
+    tmp = tempfile.mkdtemp(prefix="posfeat_e2e_")
+    make_dataset(tmp, args.seqs)
+    make_checkpoint(tmp)
+    cfg = yaml.safe_load(open(os.path.join(ROOT, "configs", "extract_hpatches.yaml")))
+    cfg["data_config_extract"]["data_path"] = os.path.join(tmp, "data", "hpatches-sequences-release")
+    os.chdir(tmp)
+    from posfeat_amd.managers.extractor import Extractor
+    res = {}
+    for p in ("cold", "warm")[:args.passes]:
+        cfg["output_root"] = "hpatches/e2e_" + p
+        cp = os.path.join(tmp, "cfg_%s.yaml" % p)
+        yaml.safe_dump(cfg, open(cp, "w"))
+        t = time.perf_counter()
+        ex = Extractor(argparse.Namespace(config=cp, local_rank=-1))
+        setup = time.perf_counter() - t
+        ex.extract()
+        st = dict(ex.stats)
+        marks = st.pop("group_marks", None)
+        if marks:   # from the first group of a shape met before, to the end
+            seen, first = set(), None
+            for (t_, k_), shp in zip(marks, ex.group_shapes):
+                if shp in seen and first is None:
+                    first = (t_, k_)
+                seen.add(shp)
+            if first is not None:
+                st["steady_images_per_s"] = (st["images"] - first[1]) / (st["seconds"] - first[0])
+        st["setup_s"] = setup
+        eng = ex.model._engine
+        st["engine_shapes"] = len(eng.cached_shapes)
+        st["engine_workspace_mb"] = eng.workspace_bytes / 2 ** 20
+        res[p] = st
+        ex.model._engine = None
+        files = []
+        for dp, _, fs in os.walk(os.path.join(tmp, "ckpts", cfg["output_root"], "desc")):
+            files += [os.path.join(dp, f) for f in fs]
+        z = np.load(files[0])
+        st["npz_files"] = len(files)
+        st["kpts_first"] = int(z["keypoints"].shape[0])
+        del ex, eng
+        import gc
+        import torch
+        gc.collect()
+        torch.cuda.empty_cache()
+    import torch
+    print(json.dumps({"workload": "extract.py e2e (configs/extract_hpatches.yaml, batch 1)",
+                      "data": "synthetic HPatches layout, %d seqs x 6 ppm, sizes %s" % (
+                          args.seqs, sorted({SIZES[s % len(SIZES)] for s in range(args.seqs)})),
+                      "device": torch.cuda.get_device_name(0), **res}))
+
+
+if __name__ == "__main__":
+    main()
