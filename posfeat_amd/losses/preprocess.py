@@ -7,9 +7,13 @@ softmax expectations, epipolar line search, window expectation).  Random
 draws (the per-cell Categorical sample and the loc_rand jitter) are taken from
 torch's device generator, or passed explicitly (``draws=``) for parity tests.
 
-Forward values only: autograd through these kernels is the next step
-(SURVEY §8f item 1).  Only the configuration of configs/train_desc.yaml is
-implemented; other options raise NotImplementedError.
+Autograd: when a local map requires grad (descriptor training), the forward
+state (NHWC maps, draws, the kernel's workspace) is kept in
+``processed['_l2w']`` and EpipolarLoss_full's differentiable loss runs
+``posfeat_line2window_backward`` for dL/d local maps (the gradient the
+reference's ``total_loss.backward()`` sends through these processed tensors).
+Only the configuration of configs/train_desc.yaml is implemented; other
+options raise NotImplementedError.
 """
 import ctypes
 
@@ -47,7 +51,6 @@ class Preprocess_Line2Window(nn.Module):
     def name(self):
         return self.__lossname__
 
-    @torch.no_grad()
     def forward(self, inputs, outputs, draws=None):
         xf1, xf2 = outputs["preds1"]["local_map"], outputs["preds2"]["local_map"]
         h1i, w1i = inputs["im1"].size()[2:]
@@ -69,8 +72,8 @@ class Preprocess_Line2Window(nn.Module):
             sel1, sel2 = sel1.reshape(b, n1).int(), sel2.reshape(b, n2).int()
         nh1 = getattr(outputs["preds1"], "local_map_nhwc", None)
         nh2 = getattr(outputs["preds2"], "local_map_nhwc", None)
-        x1 = nh1 if nh1 is not None else ops.nchw_to_nhwc(xf1.float().contiguous())
-        x2 = nh2 if nh2 is not None else ops.nchw_to_nhwc(xf2.float().contiguous())
+        x1 = nh1 if nh1 is not None else ops.nchw_to_nhwc(xf1.detach().float().contiguous())
+        x2 = nh2 if nh2 is not None else ops.nchw_to_nhwc(xf2.detach().float().contiguous())
         F1 = inputs["F1"].to(dev).float().contiguous()
         F2 = inputs["F2"].to(dev).float().contiguous()
         f = lambda *s: torch.empty(*s, device=dev)  # noqa: E731
@@ -90,7 +93,14 @@ class Preprocess_Line2Window(nn.Module):
                                         ctypes.byref(o), ptr(ws), need, stream_ptr()))
         self.last_raw = res   # the kernel's raw outputs (line centres etc.), for diagnostics
         c1 = torch.tensor([(w2i - 1) / 2.0, (h2i - 1) / 2.0], device=dev)
+        grad = torch.is_grad_enabled() and (xf1.requires_grad or xf2.requires_grad)
+        state = None
+        if grad:   # everything posfeat_line2window_backward reads, kept alive
+            state = {"xf1": xf1, "xf2": xf2, "x1": x1, "x2": x2, "F1": F1, "F2": F2, "o": o,
+                     "res": res, "ws": ws, "T": T, "g": g, "win": float(self.config["window_size"]),
+                     "hw": (h1i, w1i, h2i, w2i), "b": b}
         return {
+            "_l2w": state,
             "coord1": res["coord1"], "coord2": res["coord2"],
             "feat1g_corloc": res["g1"], "feat2g_corloc": res["g2"],
             "feat1w_corloc": res["w1"], "feat2w_corloc": res["w2"],

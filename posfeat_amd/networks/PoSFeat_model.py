@@ -7,9 +7,22 @@ methods ``set_parallel``, ``load_checkpoint``, ``save_checkpoint``,
 
 ``extract`` runs the whole ResUNet + KeypointDet forward as one call into the
 HIP engine (posfeat_model_extract) with BN folded into packed weights that
-are rebuilt whenever the parameters change.  Differences from the reference
-are loud, never silent: training-mode extraction (batch-stat BN) and CPU
-devices raise.
+are rebuilt whenever the parameters change.  As in the reference the modules
+live on ``device``.
+
+``forward`` under autograd follows the reference Trainer
+(managers/trainer.py:296-331; posfeat_amd.autograd):
+* ``localheader`` in train mode (configs/train_kp.yaml): im1 and im2 run as one
+  batch through an ExtractionEngine(train=True) (instance norm is per image
+  and the frozen backbone uses eval BatchNorm, so batching is exact); the
+  ``local_point`` maps are differentiable w.r.t. ``localheader``'s parameters.
+* ``backbone`` in train mode (configs/train_desc.yaml): im1 and im2 run as two
+  train-mode ResUNet calls (own BatchNorm batch statistics each, running
+  statistics updated twice, as PoSFeat_model.py:144-145 does); ``local_map``
+  is differentiable w.r.t. ``backbone``'s parameters.  The keypoint head's
+  output feeds neither the descriptor loss nor any state, so ``local_point``,
+  ``global_map`` and ``global_feat`` are None there.
+Differences from the reference are loud, never silent: CPU devices raise.
 """
 import os
 
@@ -46,13 +59,13 @@ class PoSFeat:
         self.parameters = []
         if self.config["backbone"] != "ResUNet":
             raise NotImplementedError("backbone must be 'ResUNet'")
-        self.backbone = ResUNet(**self.config["backbone_config"])
+        self.backbone = ResUNet(**self.config["backbone_config"]).to(self.device)
         self.parameters += list(self.backbone.parameters())
         message = "backbone: {}\n".format(self.config["backbone"])
         if "localheader" in list(self.config.keys()) and self.config["localheader"] != "None":
             if self.config["localheader"] != "KeypointDet":
                 raise NotImplementedError("localheader must be 'KeypointDet'")
-            self.localheader = KeypointDet(**self.config["localheader_config"])
+            self.localheader = KeypointDet(**self.config["localheader_config"]).to(self.device)
             message += "localheader: {}\n".format(self.config["localheader"])
         else:
             # reference default: KeypointDet(in_channels=out_channels[0], out_channels=2)
@@ -62,6 +75,8 @@ class PoSFeat:
         self._engine = None
         self._engine_key = None
         self._parallel = False
+        self._head_train = None      # (backbone key, ExtractionEngine(train=True), HeadBinding)
+        self._bb_train = {}          # (b, h, w) -> BackboneBinding
         print(message)
 
     # ------------------------------------------------------------------ engine
@@ -132,11 +147,74 @@ class PoSFeat:
         res.local_map_nhwc = out["_local_map_nhwc"]
         return res
 
+    # ------------------------------------------------------------------ training
+    def _bb_key(self):
+        return tuple(p._version for p in self.backbone.state_dict(keep_vars=True).values())
+
+    def _head_binding(self):
+        from ..autograd import HeadBinding
+        from ..engine import ExtractionEngine
+        key = self._bb_key()
+        if self._head_train is None or self._head_train[0] != key:
+            eng = ExtractionEngine(self.backbone.state_dict(), self.localheader.state_dict(),
+                                   device=self.device, train=True)
+            self._head_train = (key, eng, HeadBinding(eng, self.localheader))
+        binding = self._head_train[2]
+        binding.parallel = self._parallel
+        binding.sync()
+        return binding
+
+    def _forward_head_train(self, im1, im2):
+        from ..autograd import HeadFn
+        binding = self._head_binding()
+        b = im1.shape[0]
+        imgs = torch.cat([im1, im2], 0).float().contiguous()
+        res = binding.engine.run(imgs, outputs=("local_map", "global_map", "global_feat"))
+        binding.token += 1
+        lp = HeadFn.apply(res["local_point"], binding, binding.token, *binding.params)
+        preds = []
+        for sl in (slice(0, b), slice(b, 2 * b)):
+            g = res["global_map"][sl]
+            o = ExtractOutputs(local_map=res["local_map"][sl], global_map=g,
+                               global_feat=res["global_feat"][sl], local_point=lp[sl],
+                               local_thr=torch.zeros_like(lp[sl]),
+                               global_point=torch.ones(g.shape[0], 1, g.shape[2], g.shape[3],
+                                                       device=g.device))
+            o.local_map_nhwc = res["_local_map_nhwc"][sl]
+            preds.append(o)
+        return preds
+
+    def _forward_backbone_train(self, im1, im2):
+        from .. import ops
+        from ..autograd import BackboneBinding, BackboneFn
+        preds = []
+        for slot, im in enumerate((im1, im2)):
+            b, _, h, w = im.shape
+            binding = self._bb_train.get((b, h, w))
+            if binding is None:
+                binding = self._bb_train[(b, h, w)] = BackboneBinding(self.backbone, b, h, w,
+                                                                      self.device)
+            binding.parallel = self._parallel
+            lm_nhwc = binding.forward(im.float().contiguous(), slot)
+            lm = BackboneFn.apply(ops.nhwc_to_nchw(lm_nhwc), binding, slot,
+                                  binding.tokens[slot], *binding.params)
+            o = ExtractOutputs(local_map=lm, global_map=None, global_feat=None, local_point=None,
+                               local_thr=None, global_point=None)
+            o.local_map_nhwc = lm_nhwc
+            preds.append(o)
+        return preds
+
     def forward(self, inputs):
         for key, val in inputs.items():
             if key in self.no_cuda:
                 continue
             inputs[key] = val.to(self.device)
+        if torch.is_grad_enabled() and self.backbone.training:
+            preds1, preds2 = self._forward_backbone_train(inputs["im1"], inputs["im2"])
+            return {"preds1": preds1, "preds2": preds2}
+        if torch.is_grad_enabled() and self.localheader.training:
+            preds1, preds2 = self._forward_head_train(inputs["im1"], inputs["im2"])
+            return {"preds1": preds1, "preds2": preds2}
         preds1 = self.extract(inputs["im1"], 1)
         preds1.local_map_nhwc = None  # workspace is reused by the next extract
         preds2 = self.extract(inputs["im2"], 2)

@@ -253,7 +253,7 @@ class BackboneTrainer:
         self.grad = torch.zeros_like(self.params)   # conv_coarse never receives a gradient
         self.exp_avg = torch.zeros_like(self.params)
         self.exp_avg_sq = torch.zeros_like(self.params)
-        nbt = [int(np.asarray(v).reshape(-1)[0]) for k, v in backbone_sd.items()
+        nbt = [int(weights._np(v).reshape(-1)[0]) for k, v in backbone_sd.items()
                if k.endswith("num_batches_tracked")] if backbone_sd is not None else []
         self.num_batches_tracked = max(nbt) if nbt else 0
         self.adam_steps = 0

@@ -78,7 +78,7 @@ def test_resunet_forward(gpu, model):
     from posfeat_amd.weights import seeded_image
     img = torch.from_numpy(seeded_image(2, 64, 96))[None]
     out = model.backbone(img.to(gpu))
-    ref = model_ref.resunet_forward(model.backbone.state_dict(), img)
+    ref = model_ref.resunet_forward({k: v.cpu() for k, v in model.backbone.state_dict().items()}, img)
     for k in ("global_map", "local_map", "local_map_small"):
         err = (out[k].cpu() - ref[k]).abs().max().item()
         assert err <= 1e-4 * max(1.0, ref[k].abs().max().item()), k
