@@ -388,6 +388,26 @@ int posfeat_model_head_backward(posfeat_model *m, const float *dlocal_point, flo
  * posfeat_adam: torch.optim.Adam (no amsgrad) on n floats; g is scaled by
  *   grad_scale first (1/world after a summing all-reduce = DDP's mean). */
 typedef struct posfeat_bbtrain posfeat_bbtrain;
+
+/* SyncBatchNorm groups (group.hip).  Replaces the SyncBatchNorm conversion of
+ *   networks/PoSFeat_model.py:48-55 (PoSFeat.set_parallel): with a group set
+ *   (posfeat_bbtrain_set_group), every BatchNorm of the train-mode backbone
+ *   sums its statistics over the group's ranks -- forward (sum y, sum y^2,
+ *   count) and backward (sum g, sum g x^) -- as torch's SyncBatchNorm does;
+ *   dgamma / dbeta stay per rank (DDP averages them with the other grads).
+ * RCCL: rank 0 calls posfeat_group_unique_id (128 bytes), the host broadcasts
+ *   them (torch.distributed), every rank calls posfeat_group_create_rccl.
+ * local: `world` ranks that are threads of one process on one device (the
+ *   one-GPU test of the cross-rank semantics). */
+typedef struct posfeat_group posfeat_group;
+typedef struct posfeat_local_group posfeat_local_group;
+int posfeat_group_unique_id(void *out128);
+int posfeat_group_create_rccl(int world, int rank, const void *id128, posfeat_group **out);
+int posfeat_local_group_create(int world, int max_doubles, posfeat_local_group **out);
+int posfeat_group_create_local(posfeat_local_group *L, int rank, posfeat_group **out);
+void posfeat_group_destroy(posfeat_group *g);
+void posfeat_local_group_destroy(posfeat_local_group *L);
+int posfeat_bbtrain_set_group(posfeat_bbtrain *m, posfeat_group *g);
 int posfeat_bbtrain_num_layers(void);
 int posfeat_bbtrain_layer(int i, const char **name, int *cin, int *cout, int *k, int *stride,
                           int *has_bias, long long *offs /* [6] */);

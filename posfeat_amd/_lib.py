@@ -123,6 +123,13 @@ SIGNATURES = {
     "posfeat_bbtrain_timing": (c_int, [c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
                                        ctypes.POINTER(ctypes.c_double), P_int]),
     "posfeat_bbtrain_destroy": (None, [c_void_p]),
+    "posfeat_bbtrain_set_group": (c_int, [c_void_p, c_void_p]),
+    "posfeat_group_unique_id": (c_int, [c_void_p]),
+    "posfeat_group_create_rccl": (c_int, [c_int, c_int, c_void_p, ctypes.POINTER(c_void_p)]),
+    "posfeat_local_group_create": (c_int, [c_int, c_int, ctypes.POINTER(c_void_p)]),
+    "posfeat_group_create_local": (c_int, [c_void_p, c_int, ctypes.POINTER(c_void_p)]),
+    "posfeat_group_destroy": (None, [c_void_p]),
+    "posfeat_local_group_destroy": (None, [c_void_p]),
     "posfeat_adam": (c_int, [c_void_p] * 4 + [c_ll] + [c_float] * 5 + [c_ll, c_float, c_void_p]),
     "posfeat_line2window_backward_workspace": (c_size_t, [c_int] * 6),
     "posfeat_line2window_backward": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int,

@@ -38,6 +38,7 @@
 #include <vector>
 
 #include "bbtrain_kernels.h"
+#include "group.h"
 #include "common.h"
 #include "fmap.h"
 #include "train.h"
@@ -155,6 +156,10 @@ struct posfeat_bbtrain {
   // scratch (shared by the batches: forward transients + backward)
   size_t scr_bytes = 0;
   Buf dsn, part, coef, ga, gb, gc, gd, gres, dy, dz, dcat2, dcat3, dup, upt, wt, wgws, splitk;
+  // SyncBatchNorm (posfeat_bbtrain_set_group): statistics summed over the
+  // group's ranks; bnsum holds [local | group] sums of one layer
+  posfeat_group* group = nullptr;
+  Buf bnsum;
   // Winograd F(2x2,3x3) for the decoder's 3x3 convs, forward and input
   // gradient (wino.hip; POSFEAT_WINO=0: direct conv)
   bool wino = true;
@@ -345,6 +350,7 @@ void plan(posfeat_bbtrain* m) {
   alloc(m->dsn, fl(MAXG));
   alloc(m->part, 2 * 1100 * 1024 * sizeof(double));
   alloc(m->coef, fl(3 * 1024));
+  alloc(m->bnsum, 4 * 1024 * sizeof(double));
   alloc(m->ga, fl(MAXG));
   alloc(m->gb, fl(MAXG));
   alloc(m->gc, fl(MAXG));
@@ -445,13 +451,25 @@ int layer_fwd(Ctx& c, int li, const float* x, int xcs, int h, int w, float* out,
   float* rstd = mean + L.cout;
   const BnGrid g = bn_grid(P, L.cout);
   const int c4n = L.cout / 4;
+  const int world = pf_group_world(m->group);
   return timed(c, "fwd:bn", 0, [&] {
     hipLaunchKernelGGL(bn_partial_kernel<0>, dim3(g.nchunk, g.gy), dim3(256), 0, c.st, y, P,
                        L.cout, g.chunk, nullptr, 0, nullptr, 0, 0, nullptr, nullptr, nullptr,
                        nullptr, c.sd(m->part));
-    hipLaunchKernelGGL(bn_stats_final_kernel, dim3((L.cout + 3) / 4), dim3(256), 0, c.st,
-                       c.sd(m->part), g.nchunk, L.cout, P, mom, mean, rstd,
-                       stats ? stats + L.rm_off : nullptr, stats ? stats + L.rv_off : nullptr);
+    if (world == 1) {
+      hipLaunchKernelGGL(bn_stats_final_kernel, dim3((L.cout + 3) / 4), dim3(256), 0, c.st,
+                         c.sd(m->part), g.nchunk, L.cout, P, mom, mean, rstd,
+                         stats ? stats + L.rm_off : nullptr, stats ? stats + L.rv_off : nullptr);
+    } else {  // SyncBatchNorm: sums over the group, every rank's count P
+      double* sums = c.sd(m->bnsum);
+      hipLaunchKernelGGL(bn_sums_kernel, dim3((L.cout + 3) / 4), dim3(256), 0, c.st,
+                         c.sd(m->part), g.nchunk, L.cout, sums, nullptr);
+      PF_CHECK_LAUNCH();
+      PF_TRY(pf_group_allreduce(m->group, sums, 2 * L.cout, c.st));
+      hipLaunchKernelGGL(bn_stats_from_sums_kernel, dim3((L.cout + 255) / 256), dim3(256), 0,
+                         c.st, sums, L.cout, (double)P * world, mom, mean, rstd,
+                         stats ? stats + L.rm_off : nullptr, stats ? stats + L.rv_off : nullptr);
+    }
     if (out)
       hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for(P * c4n, 256)), dim3(256), 0, c.st, y, P,
                          c4n, mean, rstd, c.prm + L.g_off, c.prm + L.be_off, res, rcs, L.act, out,
@@ -499,9 +517,22 @@ int layer_bwd(Ctx& c, int li, const float* x, int xcs, int h, int w, const float
     hipLaunchKernelGGL(bn_partial_kernel<1>, dim3(g.nchunk, g.gy), dim3(256), 0, c.st, y, P, C,
                        g.chunk, as, acs, da, dacs, L.act, mean, rstd, c.prm + L.g_off,
                        c.prm + L.be_off, c.sd(m->part));
-    hipLaunchKernelGGL(bn_bwd_final_kernel, dim3((C + 3) / 4), dim3(256), 0, c.st,
-                       c.sd(m->part), g.nchunk, C, P, c.prm + L.g_off, rstd, grad + L.g_off,
-                       grad + L.be_off, acc, coef);
+    const int world = pf_group_world(m->group);
+    if (world == 1) {
+      hipLaunchKernelGGL(bn_bwd_final_kernel, dim3((C + 3) / 4), dim3(256), 0, c.st,
+                         c.sd(m->part), g.nchunk, C, P, c.prm + L.g_off, rstd, grad + L.g_off,
+                         grad + L.be_off, acc, coef);
+    } else {  // SyncBatchNorm backward: E[g], E[g x^] over the group
+      double* loc = c.sd(m->bnsum);
+      double* grp = loc + 2 * 1024;
+      hipLaunchKernelGGL(bn_sums_kernel, dim3((C + 3) / 4), dim3(256), 0, c.st, c.sd(m->part),
+                         g.nchunk, C, loc, grp);
+      PF_CHECK_LAUNCH();
+      PF_TRY(pf_group_allreduce(m->group, grp, 2 * C, c.st));
+      hipLaunchKernelGGL(bn_bwd_from_sums_kernel, dim3((C + 255) / 256), dim3(256), 0, c.st, loc,
+                         grp, C, (double)P * world, c.prm + L.g_off, rstd, grad + L.g_off,
+                         grad + L.be_off, acc, coef);
+    }
     hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(P * c4n, 256)), dim3(256), 0, c.st, y, P,
                        c4n, as, acs, da, dacs, L.act, mean, rstd, c.prm + L.g_off, c.prm + L.be_off,
                        coef, dy, gres);
@@ -854,6 +885,12 @@ extern "C" int posfeat_bbtrain_timing(posfeat_bbtrain* m, const char* prefix, do
   if (ms) *ms = t;
   if (flops) *flops = f;
   if (launches) *launches = k;
+  return POSFEAT_OK;
+}
+
+extern "C" int posfeat_bbtrain_set_group(posfeat_bbtrain* m, posfeat_group* g) {
+  if (!m) return POSFEAT_E_INVALID;
+  m->group = g;
   return POSFEAT_OK;
 }
 

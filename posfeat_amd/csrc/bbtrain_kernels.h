@@ -147,6 +147,60 @@ __global__ __launch_bounds__(256) void bn_stats_final_kernel(
   }
 }
 
+// SyncBatchNorm split of the two final kernels: chunk partials -> per-channel
+// sums [2][C] (fp64), then (after the cross-rank sum) the statistics from the
+// group totals over Ptot = the group's pixel count.
+__global__ __launch_bounds__(256) void bn_sums_kernel(const double* __restrict__ part, int nchunk,
+                                                      int C, double* __restrict__ sums,
+                                                      double* __restrict__ sums_copy) {
+  __shared__ double red[2][64][4];
+  double s, ss;
+  bn_chunk_sum(part, nchunk, C, red, s, ss);
+  const int c = blockIdx.x * 4 + (threadIdx.x & 3);
+  if ((threadIdx.x >> 2) != 0 || c >= C) return;
+  sums[c] = s;
+  sums[C + c] = ss;
+  if (sums_copy) {
+    sums_copy[c] = s;
+    sums_copy[C + c] = ss;
+  }
+}
+
+__global__ void bn_stats_from_sums_kernel(const double* __restrict__ sums, int C, double Ptot,
+                                          float mom, float* __restrict__ mean,
+                                          float* __restrict__ rstd, float* __restrict__ rm,
+                                          float* __restrict__ rv) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const double mu = sums[c] / Ptot;
+  double var = sums[C + c] / Ptot - mu * mu;
+  var = var > 0.0 ? var : 0.0;
+  mean[c] = (float)mu;
+  rstd[c] = (float)(1.0 / sqrt(var + (double)BN_EPS));
+  if (rm) {
+    const float vu = (float)(Ptot > 1.0 ? var * Ptot / (Ptot - 1.0) : var);
+    rm[c] = (1.f - mom) * rm[c] + mom * (float)mu;
+    rv[c] = (1.f - mom) * rv[c] + mom * vu;
+  }
+}
+
+// dgamma / dbeta from this rank's sums, the apply coefficients from the group's
+__global__ void bn_bwd_from_sums_kernel(const double* __restrict__ local,
+                                        const double* __restrict__ group, int C, double Ptot,
+                                        const float* __restrict__ gam,
+                                        const float* __restrict__ rstd, float* __restrict__ dgam,
+                                        float* __restrict__ dbet, int acc,
+                                        float* __restrict__ coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const double sg = local[c], sgx = local[C + c];
+  dgam[c] = acc ? dgam[c] + (float)sgx : (float)sgx;
+  dbet[c] = acc ? dbet[c] + (float)sg : (float)sg;
+  coef[c] = gam[c] * rstd[c];
+  coef[C + c] = (float)(group[c] / Ptot);
+  coef[2 * C + c] = (float)(group[C + c] / Ptot);
+}
+
 // out = act(gamma (y - mean) rstd + beta [+ res])
 __global__ void bn_apply_kernel(const float* __restrict__ y, long long P, int c4n,
                                 const float* __restrict__ mean, const float* __restrict__ rstd,

@@ -19,7 +19,10 @@ live on ``device``.
 * ``backbone`` in train mode (configs/train_desc.yaml): im1 and im2 run as two
   train-mode ResUNet calls (own BatchNorm batch statistics each, running
   statistics updated twice, as PoSFeat_model.py:144-145 does); ``local_map``
-  is differentiable w.r.t. ``backbone``'s parameters.  The keypoint head's
+  is differentiable w.r.t. ``backbone``'s parameters; after ``set_parallel``
+  its BatchNorms are SyncBatchNorms (statistics summed over the ranks by RCCL
+  inside the forward/backward) and the gradients are averaged over the ranks,
+  as the reference's SyncBN + DDP wrapping does.  The keypoint head's
   output feeds neither the descriptor loss nor any state, so ``local_point``,
   ``global_map`` and ``global_feat`` are None there.
 Differences from the reference are loud, never silent: CPU devices raise.
@@ -98,7 +101,11 @@ class PoSFeat:
         """Reference: SyncBN + DDP wrappers (PoSFeat_model.py:48-55).  For
         extraction the only collective needed is making every rank hold rank
         0's weights: one RCCL broadcast per tensor; ranks then run
-        independently (no per-forward buffer broadcast, no grad all-reduce)."""
+        independently (no per-forward buffer broadcast, no grad all-reduce).
+        For training through ``forward`` (posfeat_amd.autograd) the gradients
+        are then averaged over the ranks (one all-reduce of the packed
+        gradient per module and step) and the train-mode backbone uses
+        SyncBatchNorm statistics (parallel.SyncBNGroup)."""
         if not dist.is_available() or not dist.is_initialized():
             raise RuntimeError("set_parallel needs an initialised process group")
         from ..parallel import broadcast_weights
@@ -184,6 +191,12 @@ class PoSFeat:
             preds.append(o)
         return preds
 
+    def _syncbn_group(self):
+        if getattr(self, "_sbn", None) is None:
+            from ..parallel import SyncBNGroup
+            self._sbn = SyncBNGroup()
+        return self._sbn
+
     def _forward_backbone_train(self, im1, im2):
         from .. import ops
         from ..autograd import BackboneBinding, BackboneFn
@@ -195,6 +208,8 @@ class PoSFeat:
                 binding = self._bb_train[(b, h, w)] = BackboneBinding(self.backbone, b, h, w,
                                                                       self.device)
             binding.parallel = self._parallel
+            if self._parallel and binding.trainer._group is None:
+                binding.trainer.set_group(self._syncbn_group())   # SyncBatchNorm
             lm_nhwc = binding.forward(im.float().contiguous(), slot)
             lm = BackboneFn.apply(ops.nhwc_to_nchw(lm_nhwc), binding, slot,
                                   binding.tokens[slot], *binding.params)

@@ -7,6 +7,8 @@ broadcast (RCCL over xGMI on the GPU box, gloo in CPU tests) -- one large
 message instead of the reference DDP's per-parameter broadcast at wrap time
 and its per-forward buffer broadcasts (PoSFeat_model.py:48-55).
 """
+import ctypes
+
 import torch
 import torch.distributed as dist
 
@@ -41,3 +43,47 @@ def allreduce_head_grad(grad, group=None):
     if world > 1:
         dist.all_reduce(grad, group=group)
     return 1.0 / world
+
+
+class SyncBNGroup:
+    """SyncBatchNorm group of the train-mode backbone (group.hip): the
+    reference converts the backbone to torch.nn.SyncBatchNorm under DDP
+    (networks/PoSFeat_model.py:49).  Rank 0 draws an RCCL unique id, the id
+    travels by one ``dist.broadcast`` of 128 bytes over the process group
+    already initialised (nccl = RCCL on the GPU box, gloo in CPU tests), and
+    every rank creates its communicator; the BatchNorm statistics are then
+    summed in-stream by ncclAllReduce inside the backbone's forward/backward.
+    ``lib`` is injectable for the host-side test of the bootstrap."""
+
+    def __init__(self, group=None, lib=None):
+        from . import _lib
+        self._lib = lib or _lib.lib()
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        id_host = torch.zeros(128, dtype=torch.uint8)
+        if self.rank == 0:
+            buf = (ctypes.c_ubyte * 128)()
+            _lib.check(self._lib.posfeat_group_unique_id(ctypes.addressof(buf)))
+            id_host.copy_(torch.frombuffer(bytearray(buf), dtype=torch.uint8))
+        backend = dist.get_backend(group)
+        dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else "cpu"
+        t = id_host.to(dev)
+        dist.broadcast(t, src=dist.get_global_rank(group, 0) if group is not None else 0,
+                       group=group)
+        self.id = bytes(t.cpu().numpy().tobytes())
+        raw = (ctypes.c_ubyte * 128).from_buffer_copy(self.id)
+        h = ctypes.c_void_p()
+        _lib.check(self._lib.posfeat_group_create_rccl(self.world, self.rank,
+                                                        ctypes.addressof(raw), ctypes.byref(h)))
+        self.handle = h
+
+    def close(self):
+        if getattr(self, "handle", None) is not None and self.handle.value:
+            self._lib.posfeat_group_destroy(self.handle)
+        self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # pragma: no cover - interpreter shutdown
+            pass

@@ -21,6 +21,7 @@ sampling uniforms and ``torch.distributed``.
 """
 import numpy as np
 import torch
+import torch.distributed as dist
 
 from . import _lib
 from ._lib import c_int, check, lib, ptr, stream_ptr
@@ -226,7 +227,10 @@ class BackboneTrainer:
     train mode (BatchNorm batch statistics + running update), the
     Line2Window/EpipolarLoss_full gradient, the backbone backward and Adam --
     one inner iteration of managers/trainer.py:293-356 with
-    ``optimal_modules: ['backbone']``.
+    ``optimal_modules: ['backbone']``.  ``sync_bn=True`` under a process
+    group of world > 1: SyncBatchNorm statistics over the ranks (RCCL inside
+    the forward/backward, parallel.SyncBNGroup), as the reference's DDP
+    wrapping converts the backbone (PoSFeat_model.py:49).
 
     State on the device: the packed parameter blob, its gradient, Adam's two
     moments (same layout) and the running-statistics blob.  One activation
@@ -239,7 +243,7 @@ class BackboneTrainer:
     state."""
 
     def __init__(self, backbone_sd, batch, h, w, device="cuda", lr=1e-4, betas=(0.9, 0.999),
-                 eps=1e-8, weight_decay=0.0, momentum=0.1, group=None):
+                 eps=1e-8, weight_decay=0.0, momentum=0.1, group=None, sync_bn=False):
         import ctypes
         from . import weights
         _lib.require_device()
@@ -269,6 +273,19 @@ class BackboneTrainer:
         self.act = [torch.empty(na, dtype=torch.uint8, device=dev) for _ in range(2)]
         self.scratch = torch.empty(ns, dtype=torch.uint8, device=dev)
         self._lm = [None, None]
+        self._group = None
+        if sync_bn and dist.is_available() and dist.is_initialized() \
+                and dist.get_world_size(group) > 1:
+            from .parallel import SyncBNGroup
+            self.set_group(SyncBNGroup(group))   # SyncBatchNorm, PoSFeat_model.py:49
+
+    def set_group(self, group):
+        """SyncBatchNorm: sum every BatchNorm's statistics over ``group``'s
+        ranks (a parallel.SyncBNGroup, or a raw posfeat_group handle; None:
+        per-rank statistics).  The group object must outlive its use here."""
+        self._group = group
+        h = getattr(group, "handle", group)
+        check(lib().posfeat_bbtrain_set_group(self._h, h))
 
     def __del__(self):
         h = getattr(self, "_h", None)

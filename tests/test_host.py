@@ -201,3 +201,56 @@ def test_h5_export_layout(tmp_path, monkeypatch):
     np.testing.assert_array_equal(g["image_size"], [640, 480])
     np.testing.assert_array_equal(g["keypoints"], kpt)
     assert os.path.isdir(os.path.join(root, "v_seq"))
+
+
+class _FakeGroupLib:
+    """Records the SyncBN group bootstrap calls (no GPU, no RCCL)."""
+
+    def __init__(self):
+        self.created = None
+
+    def posfeat_group_unique_id(self, addr):
+        import ctypes
+        ctypes.memmove(addr, bytes((7 * i + 3) % 256 for i in range(128)), 128)
+        return 0
+
+    def posfeat_group_create_rccl(self, world, rank, addr, out):
+        import ctypes
+        self.created = (world, rank, ctypes.string_at(addr, 128))
+        out._obj.value = 1000 + rank
+        return 0
+
+    def posfeat_group_destroy(self, h):
+        pass
+
+
+def _syncbn_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from posfeat_amd.parallel import SyncBNGroup
+    fake = _FakeGroupLib()
+    g = SyncBNGroup(lib=fake)
+    q.put((rank, fake.created, g.handle.value))
+    g.close()
+    dist.destroy_process_group()
+
+
+def test_gloo_syncbn_group_bootstrap_world2():
+    """SyncBatchNorm group bootstrap (parallel.SyncBNGroup): rank 0's RCCL
+    unique id reaches every rank through one broadcast over the process group
+    (gloo here, RCCL on the GPU box) and each rank creates its communicator
+    with (world, its rank, that id).  The cross-rank statistics themselves are
+    checked on the GPU (test_gpu_syncbn.py)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29700 + os.getpid() % 1000
+    procs = [ctx.Process(target=_syncbn_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=300) for _ in procs), key=lambda r: r[0])
+    for p in procs:
+        p.join(60)
+    want = bytes((7 * i + 3) % 256 for i in range(128))
+    for rank, created, handle in res:
+        assert created == (2, rank, want)
+        assert handle == 1000 + rank
