@@ -45,11 +45,29 @@ HEAD_CONV2_FLOP_PER_IMAGE = 2.0 * 480 * 640 * 128 * 256 * 9   # reference layer
 # (conv:head.conv2.up4tap).  The engine's timing events carry the FLOPs each
 # launch executes.
 GEMM_LABEL_KERNELS = {
-    ".wino": "conv_glds_kernel x36 batched (Winograd F(4x4) transform-domain GEMMs of %s)",
-    "up4tap": "conv_glds_kernel (head.conv2's 192 x4-upsampled channels: nine 1x1 convs on the "
-              "120x160 grid as one [B*19200 x 192] x [192 x 1152] GEMM)",
+    ".wino": "conv_glds_kernel<128,128,BF6> x36 batched (Winograd F(4x4) transform-domain "
+             "GEMMs of %s)",
+    "up4tap": "conv_glds_kernel<128,128,BF6> (head.conv2's 192 x4-upsampled channels: nine 1x1 "
+              "convs on the 120x160 grid as one [B*19200 x 192] x [192 x 1152] GEMM)",
 }
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md, dense FP32 matrix (spec)
+PEAK_BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md, dense BF16 matrix (no sparsity)
+
+
+def conv_arithmetic():
+    """The row-tile convs' product arithmetic (posfeat_set_conv_precision):
+    bf16x6 runs each fp32 product as 6 bf16 MFMA products (fp32-accurate,
+    tests/test_gpu_precision.py), so its own ceiling is the dense bf16 peak / 6
+    in fp32-equivalent FLOP/s."""
+    from posfeat_amd._lib import lib
+    mode = lib().posfeat_set_conv_precision(-1)
+    if mode >= 1:
+        return {"arithmetic": "bf16x6: fp32 operands split exactly into 3 bf16 terms, 6 products "
+                              "per fp32 product on v_mfma_f32_32x32x16_bf16, fp32 accumulate "
+                              "(per-product error < one fp32 rounding)",
+                "method_peak": round(PEAK_BF16_MFMA_TFLOPS / 6, 1)}
+    return {"arithmetic": "fp32-input MFMA v_mfma_f32_32x32x2_f32", "method_peak":
+            PEAK_FP32_MFMA_TFLOPS}
 
 
 def parse():
@@ -324,6 +342,7 @@ def main():
     achieved = k_flops / (kms * 1e-3) / 1e12
     kdesc = next(v for k, v in GEMM_LABEL_KERNELS.items() if dom.endswith(k))
     kdesc = kdesc % dom[len("conv:"):-len(".wino")] if "%s" in kdesc else kdesc
+    arith = conv_arithmetic()
     c2 = float(np.mean(c2_ms))
     conv_total = float(np.mean(conv_ms))
     conv_ach = float(np.mean(conv_fl)) / (conv_total * 1e-3) / 1e12
@@ -365,7 +384,12 @@ def main():
                          "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4),
                          "traffic": traffic,
-                         "avg_launch_ms": round(kms, 4), "flop_per_launch": k_flops},
+                         "avg_launch_ms": round(kms, 4), "flop_per_launch": k_flops,
+                         **arith,
+                         "method_frac": round(achieved / arith["method_peak"], 4),
+                         "note": "achieved = fp32 FLOP of the GEMM / its HIP-event time; peak = "
+                                 "the dense FP32 MFMA peak (dtype fp32); method_peak = the "
+                                 "ceiling of the arithmetic actually used"},
             "head_conv2": {"ms_per_step": round(c2, 3),
                            "note": "main-stream part (low-res tap GEMM + combine); the G part "
                                    "(IN(convimg) channels) runs on the side stream",
@@ -475,7 +499,8 @@ def train_desc_main(args, world, rank, dev):
     from posfeat_amd.weights import seeded_state_dicts
     b = args.batch
     bb, _ = seeded_state_dicts(0)
-    tr = BackboneTrainer(bb, b, H, W, device=dev, lr=1e-4)
+    # SyncBatchNorm under DDP, as PoSFeat.set_parallel converts the backbone
+    tr = BackboneTrainer(bb, b, H, W, device=dev, lr=1e-4, sync_bn=world > 1)
     if world > 1:
         dist.broadcast(tr.params, src=0)
         dist.broadcast(tr.stats, src=0)
@@ -521,7 +546,8 @@ def train_desc_main(args, world, rank, dev):
                                    "Preprocess_Line2Window + EpipolarLoss_full, Adam 1e-4), "
                                    "%d pairs per GPU" % b,
                        "global_batch_pairs": b * world, "image": [H, W],
-                       "parallelism": "dp%d (RCCL all-reduce of backbone grads)" % world},
+                       "parallelism": "dp%d (RCCL all-reduce of backbone grads%s)" % (
+                           world, ", SyncBatchNorm" if world > 1 else "")},
             "roofline": {"kernel": "%s class (%d launches: %s MFMA convs of the train-mode "
                                    "ResUNet, flop-weighted)" % (dom, d_n, dom),
                          "bound": "mfma", "achieved": round(ach, 3),

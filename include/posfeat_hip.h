@@ -68,6 +68,18 @@ typedef struct {
 } posfeat_conv_desc;
 
 int posfeat_conv_packed_k(int cin, int kh, int kw); /* returns Kpad */
+/* Product arithmetic of the row-tile convolutions (1x1, strided, the batched
+ * Winograd / tap GEMMs); returns the previous mode.  0: fp32-input MFMA
+ * (v_mfma_f32_32x32x2_f32, exact fp32 fmaf chains).  1 (default): "bf16x6" --
+ * each fp32 operand split exactly into three bf16 terms (h + m + l, residual
+ * <= 2^-27 relative) and the six products of order >= 2^-16 accumulated in
+ * fp32 on v_mfma_f32_32x32x16_bf16 (16x the fp32-MFMA rate): per-product error
+ * ~2e-8 relative, below an fp32 fmaf's own rounding -- fp32-accurate results
+ * (tests/test_gpu_precision.py), not a reduced-precision mode.  2: as 1, with
+ * the Winograd / tap GEMM operands split by their producers (A/B only).
+ * 3x3 stride-1 convs always run the fp32 halo kernel.  Instances created
+ * afterwards plan with the new mode.  mode = -1: query only. */
+int posfeat_set_conv_precision(int mode);
 int posfeat_conv2d_nhwc(const posfeat_conv_desc *d, const float *x, const float *w,
                         const float *bias, const float *res, float *y, void *stream);
 /* Same, allowed to split K over workgroups (deterministic: fp32 partial slabs

@@ -163,6 +163,7 @@ struct posfeat_bbtrain {
   // Winograd F(2x2,3x3) for the decoder's 3x3 convs, forward and input
   // gradient (wino.hip; POSFEAT_WINO=0: direct conv)
   bool wino = true;
+  bool bf6p = false;     // conv precision mode 2 at create (pre-split Winograd operands)
   bool s2phase = true;  // stride-2 input gradients by output phases (POSFEAT_S2PHASE=0: zero insertion)
   Buf wu, wino_ws;
   // optional per-launch timing (labels "fwd:conv", "bwd:wgrad", ...)
@@ -398,11 +399,12 @@ void plan(posfeat_bbtrain* m) {
     const char* e = getenv("POSFEAT_S2PHASE");
     m->s2phase = !(e && e[0] == '0');
   }
+  m->bf6p = pf_bf6p_on();  // fixed for the handle: the U buffer size depends on it
   if (m->wino) {
     size_t uf = 0, wb = 0;
     for (int li : {T.up3, T.ic3, T.up2, T.ic2}) {
       const TLayer& L = T.v[li];
-      uf = std::max(uf, (size_t)36 * L.cin * L.cout);
+      uf = std::max(uf, (size_t)(m->bf6p ? 54 : 36) * L.cin * L.cout);
       wb = std::max(wb, pf_wino_ws_bytes((int)B, lih[li], liw[li], L.cin, L.cout));
       wb = std::max(wb, pf_wino_ws_bytes((int)B, lih[li], liw[li], L.cout, L.cin));
       if (lih[li] % 4 == 0 && liw[li] % 4 == 0)
@@ -437,9 +439,9 @@ int layer_fwd(Ctx& c, int li, const float* x, int xcs, int h, int w, float* out,
   if (use_wino(m, li, h, w)) {
     float* U = c.s(m->wu);
     PF_TRY(timed(c, "fwd:conv", wino_flops(m->B, h, w, L.cin, L.cout), [&] {
-      PF_TRY(pf_wino_weights_hw(c.prm + L.w_off, L.cout, L.cin, h, w, U, c.st));
+      PF_TRY(pf_wino_weights_hw(c.prm + L.w_off, L.cout, L.cin, h, w, U, c.st, m->bf6p));
       return pf_wino_conv(x, xcs, m->B, h, w, L.cin, U, c.prm + L.b_off, L.cout, ACT_NONE, y,
-                          L.cout, c.s(m->wino_ws), m->wino_ws.bytes, c.st);
+                          L.cout, c.s(m->wino_ws), m->wino_ws.bytes, c.st, 7, m->bf6p);
     }));
   } else {
     PF_TRY(timed(c, "fwd:conv", 2.0 * P * L.cout * L.cin * L.k * L.k, [&] {
@@ -605,9 +607,9 @@ int layer_bwd(Ctx& c, int li, const float* x, int xcs, int h, int w, const float
   if (!add && use_wino(m, li, h, w)) {
     float* U = c.s(m->wu);
     return timed(c, "bwd:dgrad", wino_flops(B, h, w, C, L.cin), [&] {
-      PF_TRY(pf_wino_weights_hw(wt, L.cin, C, h, w, U, c.st));
+      PF_TRY(pf_wino_weights_hw(wt, L.cin, C, h, w, U, c.st, m->bf6p));
       return pf_wino_conv(src, C, B, h, w, C, U, nullptr, L.cin, ACT_NONE, dx, dxcs,
-                          c.s(m->wino_ws), m->wino_ws.bytes, c.st);
+                          c.s(m->wino_ws), m->wino_ws.bytes, c.st, 7, m->bf6p);
     });
   }
   posfeat_conv_desc d = make_desc(B, h, w, C, C, L.cin, L.k, 1, dxcs, add ? addcs : 0);

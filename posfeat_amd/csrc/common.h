@@ -42,3 +42,25 @@ __device__ __forceinline__ uint32_t pf_fkey(float v) {
   uint32_t u = __float_as_uint(v + 0.0f);
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
+
+// ---- bf16x6 operand split (conv.hip BF6 tiles, gemm6.hip) -----------------
+// x = h + m + l exactly up to 2^-27 |x|: h = RNE_bf16(x), m = RNE_bf16(x - h),
+// l = RNE_bf16(x - h - m) (both differences exact in fp32).
+__device__ __forceinline__ unsigned pf_cvt_pk_bf16(float lo, float hi) {
+  unsigned r;
+  asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
+  return r;
+}
+__device__ __forceinline__ void pf_split3_pair(float a, float b, unsigned& h, unsigned& m,
+                                               unsigned& l) {
+  h = pf_cvt_pk_bf16(a, b);
+  const float ra = a - __uint_as_float(h << 16), rb = b - __uint_as_float(h & 0xffff0000u);
+  m = pf_cvt_pk_bf16(ra, rb);
+  const float sa = ra - __uint_as_float(m << 16), sb = rb - __uint_as_float(m & 0xffff0000u);
+  l = pf_cvt_pk_bf16(sa, sb);
+}
+// 4 floats -> 4 bf16 of each plane (uint2 = elements 0..3 in order)
+__device__ __forceinline__ void pf_split3x4(const f32x4& v, uint2& h, uint2& m, uint2& l) {
+  pf_split3_pair(v.x, v.y, h.x, m.x, l.x);
+  pf_split3_pair(v.z, v.w, h.y, m.y, l.y);
+}

@@ -22,6 +22,28 @@
 #include "common.h"
 #include "fmap.h"
 
+// Product arithmetic of the row-tile convs / GEMMs (posfeat_set_conv_precision):
+// 0 fp32 MFMA (v_mfma_f32_32x32x2_f32), 1 bf16x6 on the bf16 matrix cores
+// (default), 2 bf16x6 with producer-split operands for the Winograd / tap
+// GEMMs (gemm6.hip; measured no faster, A/B only).  POSFEAT_BF6 sets the
+// initial value.
+static int g_conv_precision = -1;
+int pf_conv_precision() {
+  if (g_conv_precision < 0) {
+    const char* e = getenv("POSFEAT_BF6");
+    g_conv_precision = e ? (e[0] == '0' ? 0 : e[0] == '2' ? 2 : 1) : 1;
+  }
+  return g_conv_precision;
+}
+
+extern "C" int posfeat_set_conv_precision(int mode) {
+  const int prev = pf_conv_precision();
+  if (mode == -1) return prev;  // query
+  if (mode < 0 || mode > 2) return -1;
+  g_conv_precision = mode;
+  return prev;
+}
+
 namespace {
 
 constexpr int BK = 32;
@@ -365,12 +387,58 @@ __device__ __forceinline__ void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
 }
 
+// ---- fp32-exact products on the bf16 matrix cores ("bf16x6") -------------
+// gfx950 runs v_mfma_f32_32x32x16_bf16 at 16x the rate of the fp32-input MFMA
+// (32 cycles for 32x32x16 vs 64 for 32x32x2).  Each fp32 operand is split
+// exactly into three bf16 terms, x = h + m + l (h = RNE_bf16(x), m =
+// RNE_bf16(x - h), l = RNE_bf16(x - h - m); both differences are exact in
+// fp32), |x - h - m - l| <= 2^-27 |x|.  The product keeps the six terms of
+// order >= 2^-16: a b ~ hh + hm + mh + hl + lh + mm, dropping ml + lm + ll
+// (<= 3 * 2^-27 |ab|).  Every partial product of two bf16 values is exact in
+// the fp32 accumulator, so the per-product error (~2e-8 relative) is below an
+// fp32 fmaf's own rounding (2^-24 = 6e-8): the result is fp32-accurate, not a
+// reduced-precision approximation, at 6 x 32 = 192 matrix-core cycles per
+// 32x32x16 step instead of 8 x 64 = 512.  The split runs on the VALU beside
+// the MFMAs (v_cvt_pk_bf16_f32, RNE).  Accumulation order is fixed (k, then
+// the six terms in the order above): deterministic, tile-size independent.
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ unsigned cvt_pk_bf16(float lo, float hi) {
+  unsigned r;
+  asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
+  return r;
+}
+
+// 8 fp32 (k order) -> the three bf16 fragments of one MFMA operand
+__device__ __forceinline__ void split3(const f32x4& p0, const f32x4& p1, u32x4_t& h, u32x4_t& m,
+                                       u32x4_t& l) {
+  const float x[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float a = x[2 * i], b = x[2 * i + 1];
+    const unsigned hp = cvt_pk_bf16(a, b);
+    const float ra = a - __uint_as_float(hp << 16), rb = b - __uint_as_float(hp & 0xffff0000u);
+    const unsigned mp = cvt_pk_bf16(ra, rb);
+    const float sa = ra - __uint_as_float(mp << 16), sb = rb - __uint_as_float(mp & 0xffff0000u);
+    h[i] = hp;
+    m[i] = mp;
+    l[i] = cvt_pk_bf16(sa, sb);
+  }
+}
+
+__device__ __forceinline__ f32x16 mfma_bf16(const u32x4_t& a, const u32x4_t& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a),
+                                                 __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
+}
+
 // NST = 2: two LDS stages, vmcnt(0) + barrier per chunk (the DMA of chunk c+1
 // overlaps chunk c).  NST = 3: a three-stage ring -- chunks c+1 and c+2 are
 // in flight while c is multiplied; each chunk waits only for its own DMA
 // (counted vmcnt) and one raw s_barrier (no fence, so the younger chunk's
 // DMA stays in flight across it).  96 KB of LDS at 128x128: one block per CU.
-template <int BM, int BN, int WM, int WN, int NST = 2>
+// BF6: the products on the bf16 matrix cores (split3 / mfma_bf16 above).
+template <int BM, int BN, int WM, int WN, int NST = 2, bool BF6 = false>
 __global__ __launch_bounds__(WM* WN * 64) void conv_glds_kernel(ConvArgs a) {
   constexpr int THREADS = WM * WN * 64;
   constexpr int NW = THREADS / 64;
@@ -380,7 +448,7 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_glds_kernel(ConvArgs a) {
   constexpr int B_G = BN / 8 / NW;
   static_assert(A_G >= 1 && B_G >= 1 && BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "tile");
   static_assert(MI >= 1 && NI >= 1, "wave tile must be >= 32x32");
-  static_assert(NST == 2 || NST == 3, "stages");
+  static_assert(NST >= 2 && NST <= 5, "stages");
   constexpr int RING = NST * (BM + BN) * BK;
   constexpr int STAGE = BM * (BN + 4);
   __shared__ __attribute__((aligned(16))) float smem[RING > STAGE ? RING : STAGE];
@@ -491,6 +559,37 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_glds_kernel(ConvArgs a) {
   auto compute = [&](int slot) {
     const float* Ab = As + (slot * BM + arow) * BK;
     const float* Bb = Bs + (slot * BN + brow) * BK;
+    if constexpr (BF6) {
+      // k16 group g: lane half h holds k = 16g + 8h + j, i.e. k-slots 4g+2h, 4g+2h+1
+#pragma unroll
+      for (int g = 0; g < BK / 16; ++g) {
+        const int s0 = ((4 * g + 2 * (lane >> 5)) ^ sw) * 4;
+        const int s1 = ((4 * g + 2 * (lane >> 5) + 1) ^ sw) * 4;
+        u32x4_t ah[MI], am[MI], al[MI], bh[NI], bm[NI], bl[NI];
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi)
+          split3(*reinterpret_cast<const f32x4*>(Ab + mi * 32 * BK + s0),
+                 *reinterpret_cast<const f32x4*>(Ab + mi * 32 * BK + s1), ah[mi], am[mi], al[mi]);
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni)
+          split3(*reinterpret_cast<const f32x4*>(Bb + ni * 32 * BK + s0),
+                 *reinterpret_cast<const f32x4*>(Bb + ni * 32 * BK + s1), bh[ni], bm[ni], bl[ni]);
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < NI; ++ni) {
+            f32x16 c = acc[mi][ni];
+            c = mfma_bf16(ah[mi], bh[ni], c);
+            c = mfma_bf16(ah[mi], bm[ni], c);
+            c = mfma_bf16(am[mi], bh[ni], c);
+            c = mfma_bf16(ah[mi], bl[ni], c);
+            c = mfma_bf16(al[mi], bh[ni], c);
+            c = mfma_bf16(am[mi], bm[ni], c);
+            acc[mi][ni] = c;
+          }
+      }
+      return;
+    }
 #pragma unroll
     for (int kk = 0; kk < BK / 8; ++kk) {
       f32x4 av[MI], bv[NI];
@@ -523,21 +622,27 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_glds_kernel(ConvArgs a) {
       __syncthreads();
     }
   } else {
+    // NST-stage ring: chunks i+1 .. i+NST-2 are in flight while i is
+    // multiplied; each chunk waits only for its own DMA (counted vmcnt) and
+    // one raw s_barrier (no fence: the younger chunks' DMAs stay in flight)
     const int nch = ch1 - ch0;
-    issue_chunk(ch0, 0);
-    if (nch > 1) issue_chunk(ch0 + 1, 1);
+    for (int j = 0; j < NST - 1 && j < nch; ++j) issue_chunk(ch0 + j, j);
     int slot = 0;
     for (int i = 0; i < nch; ++i) {
-      // chunk i has landed (this wave) once only chunk i+1's DMAs may be pending
-      if (i + 1 < nch)
+      const int ahead = min(NST - 2, nch - 1 - i);  // younger chunks already issued
+      if (ahead >= 3)
+        wait_vmcnt<(NST >= 5 ? 3 : 0) * (A_G + B_G)>();
+      else if (ahead == 2)
+        wait_vmcnt<(NST >= 4 ? 2 : 0) * (A_G + B_G)>();
+      else if (ahead == 1)
         wait_vmcnt<A_G + B_G>();
       else
         wait_vmcnt<0>();
       // every wave: chunk i landed, and chunk i-1 (the slot refilled below) consumed
       __builtin_amdgcn_s_barrier();
-      if (i + 2 < nch) issue_chunk(ch0 + i + 2, slot == 0 ? 2 : slot - 1);
+      if (i + NST - 1 < nch) issue_chunk(ch0 + i + NST - 1, slot == 0 ? NST - 1 : slot - 1);
       compute(slot);
-      slot = slot == 2 ? 0 : slot + 1;
+      slot = slot == NST - 1 ? 0 : slot + 1;
     }
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
@@ -1164,8 +1269,26 @@ __global__ void conv_splitk_reduce(const float* __restrict__ part, int ks, int M
 enum ConvKern { KERN_STAGED = 0, KERN_GLDS = 1, KERN_HALO = 2 };
 enum ConvTile {
   TILE_128x128 = 0, TILE_128x64 = 1, TILE_64x64 = 2, TILE_256x128 = 3,  // contiguous rows
-  TILE_H8x128 = 10, TILE_H8x64 = 11, TILE_H16x128 = 12                  // 8/16 x 16 patches
+  TILE_H8x128 = 10, TILE_H8x64 = 11, TILE_H16x128 = 12,                 // 8/16 x 16 patches
+  TILE_BF6_128x128 = 20, TILE_BF6_128x256 = 21, TILE_BF6_64x128 = 22,   // rows, bf16x6 products
+  TILE_BF6_128x64 = 23
 };
+
+// POSFEAT_BF6=1: every conv the row-tile DMA kernel serves (1x1, strided, the
+// batched Winograd / tap GEMMs) runs its products as bf16x6 (fp32-exact,
+// see split3); 3x3 stride-1 convs keep the fp32 halo kernel.  The candidate
+// set of a conv is then either all-bf16x6 or all-fp32, so the autotuner's
+// choice never changes results.
+bool bf6_on() { return pf_conv_precision() >= 1; }
+// LDS stages of the bf16x6 row tiles (POSFEAT_BF6_NST: 2, 3 or 4)
+int bf6_nst() {
+  static const int n = [] {
+    const char* e = getenv("POSFEAT_BF6_NST");
+    const int v = e ? atoi(e) : 2;
+    return v == 3 || v == 4 ? v : 2;
+  }();
+  return n;
+}
 struct Plan {
   int kern, tile, bm, bn, ppi;  // ppi: patches per image (halo), 0 = contiguous rows
   long long tiles_m;
@@ -1219,7 +1342,25 @@ Plan plan_for_tile(const ConvArgs& a, int tile) {
   const bool cin32 = a.Cin % BK == 0;
   const bool halo_ok = cin32 && conv_env().kmax >= KERN_HALO && a.stride == 1 && a.KH == 3 &&
                        a.KW == 3 && a.OW >= 16 && a.OH >= 8 && a.Cout % 64 == 0;
+  const bool glds_ok = cin32 && conv_env().kmax >= KERN_GLDS && a.KH * a.KW <= 32;
+  // bf16x6 mode: halo-eligible convs keep fp32 halo tiles only, the rest
+  // bf16x6 row tiles only
+  if (bf6_on() && glds_ok) {
+    const bool bf6_tile = tile >= TILE_BF6_128x128 && tile <= TILE_BF6_128x64;
+    if (halo_ok ? bf6_tile || tile < TILE_H8x128 : !bf6_tile) return p;
+  }
   switch (tile) {
+    case TILE_BF6_128x128:
+    case TILE_BF6_128x256:
+    case TILE_BF6_64x128:
+    case TILE_BF6_128x64:
+      if (!glds_ok || !bf6_on() || (tile == TILE_BF6_128x256 && a.Cout % 256)) return p;
+      p.kern = KERN_GLDS;
+      p.bm = tile == TILE_BF6_64x128 ? 64 : 128;
+      p.bn = tile == TILE_BF6_128x256 ? 256 : tile == TILE_BF6_128x64 ? 64 : 128;
+      p.ppi = 0;
+      p.tiles_m = (a.M + p.bm - 1) / p.bm;
+      return p;
     case TILE_H8x128:
     case TILE_H16x128:
     case TILE_H8x64: {
@@ -1281,6 +1422,13 @@ Plan conv_plan(const ConvArgs& a, bool allow_split, int forced = -1) {
       tile = TILE_64x64;
     d = plan_for_tile(a, tile);
     d.ksplit = tile == TILE_128x128 ? ks : 1;
+    if (bf6_on() && cin32 && a.KH * a.KW <= 32 && env.kmax >= KERN_GLDS) {
+      Plan b = plan_for_tile(a, a.Cout > 64 ? TILE_BF6_128x128 : TILE_BF6_128x64);
+      if (b.kern >= 0) {
+        b.ksplit = ks;
+        d = b;
+      }
+    }
   }
   if (forced >= 0) {
     Plan f = plan_for_tile(a, forced);
@@ -1324,6 +1472,33 @@ int conv_run(ConvArgs& a, const Plan& p, hipStream_t st) {
       break;
     case TILE_H16x128:
       hipLaunchKernelGGL((conv_halo_kernel<16, 128, 4, 2, 3, 3>), grid, dim3(512), 0, st, a);
+      break;
+    case TILE_BF6_128x128:
+      if (bf6_nst() == 4)
+        hipLaunchKernelGGL((conv_glds_kernel<128, 128, 2, 2, 4, true>),
+                           dim3(a.nwg * a.ksplit, a.nbatch), dim3(256), 0, st, a);
+      else if (bf6_nst() == 3)
+        hipLaunchKernelGGL((conv_glds_kernel<128, 128, 2, 2, 3, true>),
+                           dim3(a.nwg * a.ksplit, a.nbatch), dim3(256), 0, st, a);
+      else
+        hipLaunchKernelGGL((conv_glds_kernel<128, 128, 2, 2, 2, true>),
+                           dim3(a.nwg * a.ksplit, a.nbatch), dim3(256), 0, st, a);
+      break;
+    case TILE_BF6_128x256:
+      hipLaunchKernelGGL((conv_glds_kernel<128, 256, 2, 2, 2, true>), dim3(a.nwg * a.ksplit, a.nbatch),
+                         dim3(256), 0, st, a);
+      break;
+    case TILE_BF6_64x128:
+      hipLaunchKernelGGL((conv_glds_kernel<64, 128, 2, 2, 2, true>), dim3(a.nwg * a.ksplit, a.nbatch),
+                         dim3(256), 0, st, a);
+      break;
+    case TILE_BF6_128x64:
+      if (bf6_nst() == 4)
+        hipLaunchKernelGGL((conv_glds_kernel<128, 64, 2, 2, 4, true>),
+                           dim3(a.nwg * a.ksplit, a.nbatch), dim3(256), 0, st, a);
+      else
+        hipLaunchKernelGGL((conv_glds_kernel<128, 64, 2, 2, 2, true>),
+                           dim3(a.nwg * a.ksplit, a.nbatch), dim3(256), 0, st, a);
       break;
     case TILE_256x128: launch_rows<256, 128, 4, 2>(a, p.kern, st); break;
     case TILE_128x128: launch_rows<128, 128, 2, 2>(a, p.kern, st); break;
@@ -1459,8 +1634,10 @@ extern "C" int posfeat_conv2d_nhwc_stats(const posfeat_conv_desc* d, const float
 
 // ---------------------------------------------------------------------------
 // Tile-aware entry points for the engine's autotuner (fmap.h).
-static const int kAllTiles[] = {TILE_H8x128, TILE_H8x64, TILE_128x128, TILE_128x64, TILE_64x64,
-                                TILE_256x128};
+static const int kAllTiles[] = {TILE_H8x128,      TILE_H8x64,       TILE_128x128,
+                                TILE_128x64,      TILE_64x64,       TILE_256x128,
+                                TILE_BF6_128x128, TILE_BF6_128x256, TILE_BF6_64x128,
+                                TILE_BF6_128x64};
 
 int pf_conv_candidates(const posfeat_conv_desc* d, int* tiles, int max) {
   ConvArgs a;

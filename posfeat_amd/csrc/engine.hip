@@ -125,6 +125,9 @@ struct posfeat_model {
   // nine 1x1 convs (one GEMM) + the interpolation/tap combine (up4tap.hip)
   bool up4tap = true;
   Buf tapw, tapP, tappart;
+  bool bf6p = false;  // conv precision mode 2 (pre-split Winograd / tap GEMM operands)
+  bool tapb = false;  // bf16x6 tap GEMM on pre-split planes (POSFEAT_BF6=2)
+  Buf tapwb, tapLb;
   Buf gf_w, gf_b;
   // convimg's IN statistics from the image's tap moments instead of running
   // convimg (gfuse.hip): the full-res 64-channel map is never computed
@@ -138,6 +141,7 @@ struct posfeat_model {
   // Set in plan() before the dry pass so the planning forward follows the
   // path that actually runs.
   bool side = false;
+  int side_at = 0;
   unsigned tuned_modes = 0;  // bit per Mode: its first forward (autotune) ran, serially
   hipStream_t side_st = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -202,8 +206,8 @@ int tune(const std::string& name, const posfeat_conv_desc& d, hipStream_t st, Ru
     const char* e = getenv("POSFEAT_AUTOTUNE_LOG");
     return e && e[0] == '1';
   }();
-  int cand[8];
-  const int nc = pf_conv_candidates(&d, cand, 8);
+  int cand[16];
+  const int nc = pf_conv_candidates(&d, cand, 16);
   if (nc <= 1) return -1;
   hipEvent_t e0, e1;
   if (hipEventCreate(&e0) != hipSuccess) return -1;
@@ -252,8 +256,9 @@ TileCache& tile_cache() {
 }
 std::string desc_class(const posfeat_conv_desc& d, bool res) {
   char b[160];
-  snprintf(b, sizeof b, "%d/%d/%d/%dx%d/s%d/p%d/%d/%d/a%d/r%d", d.cin, d.x_cstride, d.cout, d.kh,
-           d.kw, d.stride, d.pad, d.y_cstride, d.res_cstride, d.act, res ? 1 : 0);
+  snprintf(b, sizeof b, "%d/%d/%d/%dx%d/s%d/p%d/%d/%d/a%d/r%d/P%d", d.cin, d.x_cstride, d.cout,
+           d.kh, d.kw, d.stride, d.pad, d.y_cstride, d.res_cstride, d.act, res ? 1 : 0,
+           pf_conv_precision());
   return b;
 }
 double desc_m(const posfeat_conv_desc& d) {
@@ -290,8 +295,8 @@ bool tile_lookup(const posfeat_conv_desc& d, bool res, int* tile) {
   }
   if (best > std::log(1.25)) return false;
   if (bt >= 0) {  // the tile must be legal for this shape too
-    int cand[8];
-    const int nc = pf_conv_candidates(&d, cand, 8);
+    int cand[16];
+    const int nc = pf_conv_candidates(&d, cand, 16);
     if (std::find(cand, cand + nc, bt) == cand + nc) return false;
   }
   *tile = bt;
@@ -370,12 +375,12 @@ int forward(Ctx& c, const float* img, posfeat_extract_out* out, int mode = MODE_
 const char* const kWinoLayers[5] = {"upconv3.conv", "iconv3", "upconv2.conv", "iconv2",
                                     "head.conv1"};
 
-long long wino_u_offset(const std::string& name) {
+long long wino_u_offset(const std::string& name, bool bf6p) {
   long long off = 0;
   for (const char* n : kWinoLayers) {
     if (name == n) return off;
     const Spec* s = specs().find(n);
-    off += (long long)36 * s->cout * s->cin;
+    off += (long long)(bf6p ? 54 : 36) * s->cout * s->cin;  // bf16x6: three planes
   }
   return -1;
 }
@@ -383,14 +388,16 @@ long long wino_u_offset(const std::string& name) {
 int conv3x3(Ctx& c, const std::string& name, const float* x, int n, int h, int w, int xcs, float* y,
             int ycs, int act) {
   posfeat_model* m = c.m;
-  const long long uo = wino_u_offset(name);
+  const long long uo = wino_u_offset(name, m->bf6p);
   if (!m->wino || uo < 0 || (h & 1) || (w & 1))
     return conv(c, name, x, n, h, w, xcs, y, ycs, 1, act);
   const Spec* s = specs().find(name);
   if (c.dry) return POSFEAT_OK;
   float* U = c.f(m->wino_u) + uo;
   PF_TRY(timed(c, "wino:weights", 0,
-               [&] { return pf_wino_weights_hw(c.W(name), s->cout, s->cin, h, w, U, c.st); }));
+               [&] {
+                 return pf_wino_weights_hw(c.W(name), s->cout, s->cin, h, w, U, c.st, m->bf6p);
+               }));
   // executed transform-domain MACs: F(4x4) 36 per 4x4 tile, F(2x2) 16 per 2x2 tile
   const bool f4 = h % 4 == 0 && w % 4 == 0 && !(getenv("POSFEAT_WINO") && getenv("POSFEAT_WINO")[0] == '1');
   const double T = f4 ? (double)n * (h / 4) * (w / 4) : (double)n * (h / 2) * (w / 2);
@@ -398,7 +405,8 @@ int conv3x3(Ctx& c, const std::string& name, const float* x, int n, int h, int w
   // (the MFMA work), the output transform (+ bias, activation)
   auto stage = [&](int st_bits) {
     return pf_wino_conv(x, xcs, n, h, w, s->cin, U, c.Bi(name), s->cout, act, y, ycs,
-                        c.f(m->wino_ws), m->wino_ws.floats * sizeof(float), c.st, st_bits);
+                        c.f(m->wino_ws), m->wino_ws.floats * sizeof(float), c.st, st_bits,
+                        m->bf6p);
   };
   PF_TRY(timed(c, "wino:in:" + name, 0, [&] { return stage(1); }));
   PF_TRY(timed(c, "conv:" + name + ".wino", 2.0 * T * (f4 ? 36 : 16) * s->cin * s->cout,
@@ -519,13 +527,14 @@ void plan(posfeat_model* m) {
   }
   if (!(m->up4 && m->gfuse) || m->train) m->imgstats = false;
   if (m->imgstats) alloc(m->imws, pf_gfuse_imgstats_ws_bytes((int)B, (int)H) / 4 + 4);
+  m->bf6p = pf_bf6p_on();  // fixed for the instance: buffer sizes depend on it
   if (m->wino) {
     size_t uf = 0, wb = 0;
     const int dims[5][2] = {{(int)h8, (int)w8}, {(int)h8, (int)w8}, {(int)h4, (int)w4},
                             {(int)h4, (int)w4}, {(int)h4, (int)w4}};
     for (int i = 0; i < 5; ++i) {
       const Spec* s = specs().find(kWinoLayers[i]);
-      uf += (size_t)36 * s->cout * s->cin;
+      uf += (size_t)(m->bf6p ? 54 : 36) * s->cout * s->cin;
       wb = std::max(wb, pf_wino_ws_bytes((int)B, dims[i][0], dims[i][1], s->cin, s->cout));
     }
     alloc(m->wino_u, uf);
@@ -535,6 +544,8 @@ void plan(posfeat_model* m) {
   {
     const char* e = getenv("POSFEAT_SIDE");
     m->side = !(e && e[0] == '0') && m->up4 && m->gfuse && !m->train;
+    const char* a = getenv("POSFEAT_SIDE_AT");
+    m->side_at = a ? std::min(3, std::max(0, atoi(a))) : 0;
   }
   if (m->up4) {
     if (!m->imgstats) alloc(m->g64, B * H * W * 64);
@@ -542,6 +553,11 @@ void plan(posfeat_model* m) {
     alloc(m->up4ws, posfeat_conv2_up4_workspace((int)B, (int)H, (int)W) / 4 + 4);
     if (m->up4tap) {
       alloc(m->tapw, pf_up4tap_weights_floats());
+      m->tapb = m->bf6p;
+      if (m->tapb) {  // three bf16 planes of the tap weights and of L
+        alloc(m->tapwb, pf_up4tap_weights_floats() * 3 / 2);
+        alloc(m->tapLb, (size_t)B * h4 * w4 * 192 * 3 / 2);
+      }
       alloc(m->tapP, pf_up4tap_p_floats((int)B, (int)H, (int)W));
       alloc(m->tappart, pf_up4tap_part_bytes((int)B, (int)H, (int)W) / 4 + 4);
     } else if (m->up4wino) {
@@ -685,7 +701,10 @@ int image_branch(Ctx& c, const float* img4) {
     }));
   else
     PF_TRY(timed(s, "head.conv2.tapw", 0, [&] {
-      return pf_up4tap_weights(s.W("head.conv2"), s.f(m->tapw), s.st);
+      PF_TRY(pf_up4tap_weights(s.W("head.conv2"), s.f(m->tapw), s.st));
+      return m->tapb ? pf_split3_rows(s.f(m->tapw), 1152, 192, 192,
+                                      reinterpret_cast<unsigned short*>(s.f(m->tapwb)), s.st)
+                     : POSFEAT_OK;
     }));
   PF_TRY(timed(s, "head.conv2.gfuse_w", 0, [&] {
     return pf_gfuse_weights(s.W("head.conv2"), s.Bi("head.conv2"), s.W("head.convimg"),
@@ -719,7 +738,10 @@ int forward(Ctx& c, const float* img, posfeat_extract_out* out, int mode, const 
   // the candidates being timed (the tile choice would depend on that race)
   const bool side = m->side && mode != MODE_BACKBONE &&
                     (c.dry || ((m->tuned_modes >> mode) & 1u) || !m->autotune);
-  if (side) PF_TRY(image_branch(c, img4));
+  // where the image branch forks (POSFEAT_SIDE_AT): 0 after the image layout,
+  // 1 before layer2, 2 before layer3, 3 before the decoder
+  const int side_at = mode == MODE_HEAD ? 0 : m->side_at;
+  if (side && side_at == 0) PF_TRY(image_branch(c, img4));
   if (mode == MODE_HEAD) {
     // KeypointDet's own input: fine_maps[0] = cat[local_map, local_map_small]
     // (PoSFeat_model.py:97-102), NCHW 192 channels at H/4 x W/4
@@ -734,8 +756,11 @@ int forward(Ctx& c, const float* img, posfeat_extract_out* out, int mode, const 
   float* cat2 = c.f(m->cat2);
   float* cat3 = c.f(m->cat3);
   PF_TRY(run_layer(c, 0, headcat + 128, B, h4, w4, 192, cat2 + 256, 512));  // layer1 -> cat2[256:]
+  if (side && side_at == 1) PF_TRY(image_branch(c, img4));
   PF_TRY(run_layer(c, 1, cat2 + 256, B, h4, w4, 512, cat3 + 512, 1024));    // layer2 -> cat3[512:]
+  if (side && side_at == 2) PF_TRY(image_branch(c, img4));
   PF_TRY(run_layer(c, 2, cat3 + 512, B, h8, w8, 1024, c.f(m->l3out), 1024));
+  if (side && side_at == 3) PF_TRY(image_branch(c, img4));
   PF_TRY(conv(c, "conv_coarse", c.f(m->l3out), B, h16, w16, 1024, c.f(m->gmap), 128, 1,
               POSFEAT_ACT_ELU));
   PF_TRY(timed(c, "upsample2x", 0, [&] {
@@ -829,7 +854,10 @@ int head_forward(Ctx& c, float* img4, float* local_point, bool side) {
       }));
     if (!side && m->up4tap)
       PF_TRY(timed(c, "head.conv2.tapw", 0, [&] {
-        return pf_up4tap_weights(c.W("head.conv2"), c.f(m->tapw), c.st);
+        PF_TRY(pf_up4tap_weights(c.W("head.conv2"), c.f(m->tapw), c.st));
+        return m->tapb ? pf_split3_rows(c.f(m->tapw), 1152, 192, 192,
+                                        reinterpret_cast<unsigned short*>(c.f(m->tapwb)), c.st)
+                       : POSFEAT_OK;
       }));
     if (side) {
       // join the image branch (it wrote the G part into y)
@@ -869,8 +897,20 @@ int head_forward(Ctx& c, float* img4, float* local_point, bool side) {
       d.y_cstride = 9 * 128;
       d.res_cstride = 0;
       d.act = POSFEAT_ACT_NONE;
-      PF_TRY(conv_desc_run(c, "head.conv2.up4tap", d, c1, c.f(m->tapw), nullptr, nullptr,
-                           c.f(m->tapP), 2.0 * B * h4 * w4 * 1152.0 * 192));
+      if (m->tapb) {  // bf16x6 on pre-split planes (gemm6.hip)
+        const long long M = (long long)B * h4 * w4;
+        unsigned short* Lb = reinterpret_cast<unsigned short*>(c.f(m->tapLb));
+        PF_TRY(timed(c, "head.conv2.split", 0,
+                     [&] { return pf_split3_rows(c1, M, 192, 192, Lb, c.st); }));
+        PF_TRY(timed(c, "conv:head.conv2.up4tap", 2.0 * M * 1152.0 * 192, [&] {
+          return pf_gemm_bf6p(Lb, 192, M * 192, 0,
+                              reinterpret_cast<const unsigned short*>(c.f(m->tapwb)), 192,
+                              1152LL * 192, 0, c.f(m->tapP), 1152, 0, 1, (int)M, 1152, 192, c.st);
+        }));
+      } else {
+        PF_TRY(conv_desc_run(c, "head.conv2.up4tap", d, c1, c.f(m->tapw), nullptr, nullptr,
+                             c.f(m->tapP), 2.0 * B * h4 * w4 * 1152.0 * 192));
+      }
       PF_TRY(timed(c, "head.conv2.combine", 0, [&] {
         return pf_up4tap_combine(B, H, W, c.f(m->tapP), c2, 128, c.d(m->tappart), mean, rstd,
                                  c.st);

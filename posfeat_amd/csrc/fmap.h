@@ -51,12 +51,15 @@ size_t pf_wino_ws_bytes(int n, int h, int w, int Cin, int Cout);
 size_t pf_wino_weights_floats(int Cin, int Cout);
 int pf_wino_weights(const float* wpk, int Cout, int Cin, float* U, hipStream_t st);  // F(2x2)
 // U for the variant pf_wino_conv picks at (h, w): F(4x4) if h, w % 4 == 0
+// bf6p: (F(4x4) only) U / V as three bf16 planes for the bf16x6 GEMM
+// (gemm6.hip); U then needs pf_wino_weights_floats_bf6p floats
 int pf_wino_weights_hw(const float* wpk, int Cout, int Cin, int h, int w, float* U,
-                       hipStream_t st);
+                       hipStream_t st, bool bf6p = false);
+size_t pf_wino_weights_floats_bf6p(int Cin, int Cout);
 // stages: bit 0 input transform, bit 1 the batched GEMMs, bit 2 output transform
 int pf_wino_conv(const float* x, int xcs, int n, int h, int w, int Cin, const float* U,
                  const float* bias, int Cout, int act, float* y, int ycs, void* ws, size_t ws_bytes,
-                 hipStream_t st, int stages = 7);
+                 hipStream_t st, int stages = 7, bool bf6p = false);
 // head.conv2's G part as one per-image 5x5 conv of the image (gfuse.hip)
 size_t pf_gfuse_weights_floats(int n);
 int pf_gfuse_weights(const float* w2_packed, const float* b2, const float* w1_packed,
@@ -92,3 +95,14 @@ size_t pf_up4tap_part_bytes(int n, int H, int W);
 int pf_up4tap_weights(const float* w2_packed, float* wt, hipStream_t st);
 int pf_up4tap_combine(int n, int H, int W, const float* P, float* y, int ycs, double* part,
                       float* mean, float* rstd, hipStream_t st);
+
+// conv product arithmetic: 0 fp32 MFMA, 1 bf16x6, 2 bf16x6 + pre-split GEMMs
+int pf_conv_precision();
+// bf16x6 GEMMs on pre-split operands (gemm6.hip).  POSFEAT_BF6=2 turns them on
+// for the Winograd transform-domain GEMMs and head.conv2's low-res tap GEMM.
+bool pf_bf6p_on();
+int pf_split3_rows(const float* x, long long rows, int cols, int ldx, unsigned short* out,
+                   hipStream_t st);
+int pf_gemm_bf6p(const unsigned short* A, int lda, long long pa, long long sa,
+                 const unsigned short* B, int ldb, long long pb, long long sb, float* C, int ldc,
+                 long long sc, int nb, int M, int N, int K, hipStream_t st);

@@ -175,8 +175,10 @@ constexpr float W4_G[6][3] = {{0.25f, 0, 0},
 constexpr float W4_AT[4][6] = {
     {1, 1, 1, 1, 1, 0}, {0, 1, -1, 2, -2, 0}, {0, 1, 1, 4, 4, 0}, {0, 1, -1, 8, -8, 1}};
 
+// Ub != nullptr: U as three bf16 planes (plane stride 36 Cout Cin) for the
+// bf16x6 GEMM (gemm6.hip), instead of fp32
 __global__ void wino4_weights_kernel(const float* __restrict__ wpk, int Cout, int Cin, int kpad,
-                                     float* __restrict__ U) {
+                                     float* __restrict__ U, unsigned short* __restrict__ Ub) {
   const long long n = (long long)Cout * Cin;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
        i += (long long)gridDim.x * blockDim.x) {
@@ -194,16 +196,28 @@ __global__ void wino4_weights_kernel(const float* __restrict__ wpk, int Cout, in
 #pragma unroll
     for (int a = 0; a < 6; ++a)
 #pragma unroll
-      for (int b = 0; b < 6; ++b)
-        U[((long long)(a * 6 + b) * Cout + co) * Cin + ci] =
-            r[a][0] * W4_G[b][0] + r[a][1] * W4_G[b][1] + r[a][2] * W4_G[b][2];
+      for (int b = 0; b < 6; ++b) {
+        const float u = r[a][0] * W4_G[b][0] + r[a][1] * W4_G[b][1] + r[a][2] * W4_G[b][2];
+        const long long o = ((long long)(a * 6 + b) * Cout + co) * Cin + ci;
+        if (Ub) {
+          unsigned hh, mm, ll;
+          pf_split3_pair(u, 0.f, hh, mm, ll);
+          Ub[o] = (unsigned short)hh;
+          Ub[o + 36 * n] = (unsigned short)mm;
+          Ub[o + 72 * n] = (unsigned short)ll;
+        } else {
+          U[o] = u;
+        }
+      }
   }
 }
 
-// V[xi][tile][c], 6x6 patch at rows 4ty-1.., cols 4tx-1..
+// V[xi][tile][c], 6x6 patch at rows 4ty-1.., cols 4tx-1..; Vb != nullptr: V
+// as three bf16 planes (plane stride 36 T C) for the bf16x6 GEMM instead
 __global__ __launch_bounds__(256) void wino4_input_kernel(const float* __restrict__ x, int xcs,
                                                           int n, int h, int w, int c4n,
-                                                          float* __restrict__ V, int clamp = 0) {
+                                                          float* __restrict__ V, int clamp = 0,
+                                                          unsigned short* __restrict__ Vb = nullptr) {
   const int th = h / 4, tw = w / 4;
   const long long T = (long long)n * th * tw;
   const long long total = T * c4n;
@@ -241,7 +255,6 @@ __global__ __launch_bounds__(256) void wino4_input_kernel(const float* __restric
 #pragma unroll
           for (int c = 0; c < 6; ++c) t[a][c] += W4_BT[a][r] * d[c];
     }
-    float* vo = V + tile * C + q * 4;
     const long long xs = T * C;
 #pragma unroll
     for (int a = 0; a < 6; ++a)
@@ -251,7 +264,16 @@ __global__ __launch_bounds__(256) void wino4_input_kernel(const float* __restric
 #pragma unroll
         for (int c = 0; c < 6; ++c)
           if (W4_BT[bb][c] != 0.f) v += W4_BT[bb][c] * t[a][c];
-        *reinterpret_cast<f32x4*>(vo + (a * 6 + bb) * xs) = v;
+        const long long o = (a * 6 + bb) * xs + tile * C + q * 4;
+        if (Vb) {
+          uint2 vh, vm, vl;
+          pf_split3x4(v, vh, vm, vl);
+          *reinterpret_cast<uint2*>(Vb + o) = vh;
+          *reinterpret_cast<uint2*>(Vb + o + 36 * xs) = vm;
+          *reinterpret_cast<uint2*>(Vb + o + 72 * xs) = vl;
+        } else {
+          *reinterpret_cast<f32x4*>(V + o) = v;
+        }
       }
   }
 }
@@ -617,13 +639,17 @@ size_t pf_wino_ws_bytes(int n, int h, int w, int Cin, int Cout) {
 size_t pf_wino_weights_floats(int Cin, int Cout) { return (size_t)36 * Cin * Cout; }
 
 // U for the variant pf_wino_conv will pick at (h, w); h = w = 0: F(2x2)
+size_t pf_wino_weights_floats_bf6p(int Cin, int Cout) { return (size_t)54 * Cin * Cout; }
+
 int pf_wino_weights_hw(const float* wpk, int Cout, int Cin, int h, int w, float* U,
-                       hipStream_t st) {
+                       hipStream_t st, bool bf6p) {
   if (Cin % 32 || Cout % 4) return POSFEAT_E_INVALID;
   const int kpad = posfeat_conv_packed_k(Cin, 3, 3);
+  bf6p = bf6p && Cout % 128 == 0;  // the same condition as wino_conv_impl's bf16x6 path
   if (h > 0 && use_f4(h, w))
     hipLaunchKernelGGL(wino4_weights_kernel, dim3(grid_for((long long)Cout * Cin, 256)), dim3(256),
-                       0, st, wpk, Cout, Cin, kpad, U);
+                       0, st, wpk, Cout, Cin, kpad, U,
+                       bf6p ? reinterpret_cast<unsigned short*>(U) : nullptr);
   else
     hipLaunchKernelGGL(wino_weights_kernel, dim3(grid_for((long long)Cout * Cin, 256)), dim3(256),
                        0, st, wpk, Cout, Cin, kpad, U);
@@ -637,10 +663,34 @@ int pf_wino_weights(const float* wpk, int Cout, int Cin, float* U, hipStream_t s
 
 static int wino_conv_impl(const float* x, int xcs, int n, int h, int w, int Cin, const float* U,
                           bool U_is_f4, const float* bias, int Cout, int act, float* y, int ycs,
-                          void* ws, size_t ws_bytes, hipStream_t st, int stages = 7) {
+                          void* ws, size_t ws_bytes, hipStream_t st, int stages = 7,
+                          bool bf6p = false) {
   if ((h & 1) || (w & 1) || Cin % 32 || Cout % 4 || xcs % 4 || ycs % 4 || n <= 0)
     return POSFEAT_E_INVALID;
   if (ws_bytes < pf_wino_ws_bytes(n, h, w, Cin, Cout)) return POSFEAT_E_WORKSPACE;
+  if (use_f4(h, w) && U_is_f4 && bf6p && Cout % 128 == 0) {
+    // bf16x6: V as three bf16 planes (54 T4 Cin bytes <= the F(2x2) V region),
+    // M after them; U holds three planes (pf_wino_weights_hw(..., bf6p))
+    const long long T4 = (long long)n * (h / 4) * (w / 4);
+    unsigned short* Vb = static_cast<unsigned short*>(ws);
+    float* M4 =
+        reinterpret_cast<float*>(static_cast<char*>(ws) + pf_align(36 * T4 * Cin * 6, 256));
+    if (stages & 1) {
+      hipLaunchKernelGGL(wino4_input_kernel, dim3(grid_for(T4 * (Cin / 4), 256)), dim3(256), 0, st,
+                         x, xcs, n, h, w, Cin / 4, nullptr, 0, Vb);
+      PF_CHECK_LAUNCH();
+    }
+    if (stages & 2)
+      PF_TRY(pf_gemm_bf6p(Vb, Cin, 36 * T4 * Cin, T4 * Cin,
+                          reinterpret_cast<const unsigned short*>(U), Cin, 36LL * Cout * Cin,
+                          (long long)Cout * Cin, M4, Cout, T4 * Cout, 36, (int)T4, Cout, Cin, st));
+    if (stages & 4) {
+      hipLaunchKernelGGL(wino4_output_kernel, dim3(grid_for(T4 * (Cout / 4), 256)), dim3(256), 0,
+                         st, M4, n, h, w, Cout / 4, bias, act, y, ycs);
+      PF_CHECK_LAUNCH();
+    }
+    return POSFEAT_OK;
+  }
   if (use_f4(h, w) && U_is_f4) {
     const long long T4 = (long long)n * (h / 4) * (w / 4);
     float* V4 = static_cast<float*>(ws);
@@ -683,9 +733,9 @@ static int wino_conv_impl(const float* x, int xcs, int n, int h, int w, int Cin,
 // U from pf_wino_weights_hw(.., h, w, ..): the variant is chosen from (h, w)
 int pf_wino_conv(const float* x, int xcs, int n, int h, int w, int Cin, const float* U,
                  const float* bias, int Cout, int act, float* y, int ycs, void* ws, size_t ws_bytes,
-                 hipStream_t st, int stages) {
+                 hipStream_t st, int stages, bool bf6p) {
   return wino_conv_impl(x, xcs, n, h, w, Cin, U, true, bias, Cout, act, y, ycs, ws, ws_bytes, st,
-                        stages);
+                        stages, bf6p);
 }
 
 namespace {
