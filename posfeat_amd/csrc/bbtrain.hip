@@ -441,7 +441,7 @@ int layer_fwd(Ctx& c, int li, const float* x, int xcs, int h, int w, float* out,
     PF_TRY(timed(c, "fwd:conv", wino_flops(m->B, h, w, L.cin, L.cout), [&] {
       PF_TRY(pf_wino_weights_hw(c.prm + L.w_off, L.cout, L.cin, h, w, U, c.st, m->bf6p));
       return pf_wino_conv(x, xcs, m->B, h, w, L.cin, U, c.prm + L.b_off, L.cout, ACT_NONE, y,
-                          L.cout, c.s(m->wino_ws), m->wino_ws.bytes, c.st, 7, m->bf6p);
+                          L.cout, c.s(m->wino_ws), m->wino_ws.bytes, c.st, 7, m->bf6p ? 2 : 0);
     }));
   } else {
     PF_TRY(timed(c, "fwd:conv", 2.0 * P * L.cout * L.cin * L.k * L.k, [&] {
@@ -609,7 +609,7 @@ int layer_bwd(Ctx& c, int li, const float* x, int xcs, int h, int w, const float
     return timed(c, "bwd:dgrad", wino_flops(B, h, w, C, L.cin), [&] {
       PF_TRY(pf_wino_weights_hw(wt, L.cin, C, h, w, U, c.st, m->bf6p));
       return pf_wino_conv(src, C, B, h, w, C, U, nullptr, L.cin, ACT_NONE, dx, dxcs,
-                          c.s(m->wino_ws), m->wino_ws.bytes, c.st, 7, m->bf6p);
+                          c.s(m->wino_ws), m->wino_ws.bytes, c.st, 7, m->bf6p ? 2 : 0);
     });
   }
   posfeat_conv_desc d = make_desc(B, h, w, C, C, L.cin, L.k, 1, dxcs, add ? addcs : 0);

@@ -69,6 +69,10 @@ struct ConvArgs {
   // batched 1x1 GEMMs (conv_glds_kernel only): blockIdx.y selects x/w/y + z*stride
   int nbatch;
   long long bx, bw, by;
+  int abl;  // ablation (POSFEAT_ABL, A/B timing only): 1 skip MFMA work, 2 skip DMA
+  // pre-split weights (conv_bf6b_kernel): three bf16 planes of w's layout
+  const unsigned short* wb;
+  long long wplane, bwb;
 };
 
 // Epilogue shared by both kernels: acc -> LDS T[BM][BN+4] (conflict-free: a
@@ -616,8 +620,8 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_glds_kernel(ConvArgs a) {
     __syncthreads();
     for (int c = ch0; c < ch1; ++c) {
       const int cur = (c - ch0) & 1;
-      if (c + 1 < ch1) issue_chunk(c + 1, cur ^ 1);
-      compute(cur);
+      if (c + 1 < ch1 && !(a.abl & 2)) issue_chunk(c + 1, cur ^ 1);
+      if (!(a.abl & 1)) compute(cur);
       __builtin_amdgcn_s_waitcnt(0);
       __syncthreads();
     }
@@ -648,6 +652,170 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_glds_kernel(ConvArgs a) {
     __syncthreads();
   }
 
+  conv_epilogue<BM, BN, WM, WN>(
+      a, acc, smem, tm, n0, split, [&](int row) { return m0 + row < a.M ? m0 + row : -1; },
+      m0 / a.hw,
+      [&](int, int m) { return a.res ? a.res + (size_t)m * a.rcs : (const float*)nullptr; });
+}
+
+// ---------------------------------------------------------------------------
+// bf16x6 with PRE-SPLIT weights (the engine's forward path): B = the packed
+// weights as three bf16 planes of the same [Cout][Kpad] layout (a.wb, plane
+// stride a.wplane; split once per forward), A = the activations split in
+// registers.  The split VALU work bounds the both-operands form (split3 of
+// every A and B fragment per wave; PMC: matrix pipe ~33 % busy, issue-bound
+// with the LDS-DMA pieces).  Here the 4 waves stack along M (wave tile
+// 32 x BN): ONE A fragment is split per k16 step against NI = BN/32 B
+// fragments read ready-made -- 1/4 of the split work per MFMA of the 2x2
+// layout.  LDS stage: A fp32 [BM][32] (swizzled as conv_glds_kernel) + B
+// [3 planes][BN][32] bf16 (16-B slot s of row r holding k-slot
+// s ^ ((r >> 2) & 3): conflict-free ds_read_b128).  Two stages; at
+// BM = BN = 128 that is 80 KB, two blocks per CU.  Products and their order
+// are those of the BF6 tiles: results are bit-identical to them.
+template <int BM, int BN>
+__global__ __launch_bounds__(256) void conv_bf6b_kernel(ConvArgs a) {
+  constexpr int WM = 4, WN = 1, NW = 4;
+  constexpr int TM = BM / WM, TN = BN;
+  constexpr int MI = TM / 32, NI = TN / 32;
+  constexpr int A_G = BM / 8 / NW;
+  constexpr int B_G = 3 * BN / 16 / NW;  // 16 plane-rows (64 B) per DMA piece
+  static_assert(MI == 1 && A_G >= 1 && B_G >= 1 && (3 * BN / 16) % NW == 0, "tile");
+  constexpr int ASTAGE = BM * BK;         // floats
+  constexpr int BSTAGE = 3 * BN * BK / 2; // floats (u16 pairs)
+  constexpr int RING = 2 * (ASTAGE + BSTAGE);
+  constexpr int EPI = BM * (BN + 4);
+  __shared__ __attribute__((aligned(16))) float smem[RING > EPI ? RING : EPI];
+  float* As = smem;
+  unsigned short* Bs = reinterpret_cast<unsigned short*>(smem + 2 * ASTAGE);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave;
+  int bid = blockIdx.x % a.nwg;
+  const int split = blockIdx.x / a.nwg;
+  {
+    const int nwg = a.nwg, q = nwg >> 3, r = nwg & 7, xcd = bid & 7, slot = bid >> 3;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+  }
+  const unsigned short* wb = a.wb;
+  if (a.nbatch > 1) {
+    const long long zb = blockIdx.y;
+    a.x += zb * a.bx;
+    a.y += zb * a.by;
+    wb += zb * a.bwb;
+  }
+  const int tm = bid / a.tiles_n, tn = bid - tm * a.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int lrow = lane >> 3;
+  const float* xsrc[A_G];
+  unsigned tapok[A_G];
+#pragma unroll
+  for (int i = 0; i < A_G; ++i) {
+    const int row = (wave * A_G + i) * 8 + lrow;
+    const int sslot = (lane & 7) ^ ((row >> 1) & 7);
+    const int m = m0 + row;
+    tapok[i] = 0u;
+    xsrc[i] = a.x;
+    if (m < a.M) {
+      const int n = m / a.hw;
+      const int rem = m - n * a.hw;
+      const int oh = rem / a.OW;
+      const int ow = rem - oh * a.OW;
+      const int ih0 = oh * a.stride - a.pad, iw0 = ow * a.stride - a.pad;
+      for (int kh = 0; kh < a.KH; ++kh)
+        for (int kw = 0; kw < a.KW; ++kw)
+          if ((unsigned)(ih0 + kh) < (unsigned)a.H && (unsigned)(iw0 + kw) < (unsigned)a.W)
+            tapok[i] |= 1u << (kh * a.KW + kw);
+      xsrc[i] = a.x + (long long)n * a.H * a.W * a.xcs + ((long long)ih0 * a.W + iw0) * a.xcs +
+                sslot * 4;
+    }
+  }
+  const unsigned short* bsrc[B_G];
+#pragma unroll
+  for (int i = 0; i < B_G; ++i) {
+    const int pr = (wave * B_G + i) * 16 + (lane >> 2);
+    const int plane = pr / BN, row = pr - plane * BN;
+    const int ks = (lane & 3) ^ ((row >> 2) & 3);
+    bsrc[i] = (n0 + row < a.Cout)
+                  ? wb + plane * a.wplane + (long long)(n0 + row) * a.Kpad + ks * 8
+                  : nullptr;
+  }
+  const int ntap = a.KH * a.KW;
+  const int nch_all = a.Kpad / BK;
+  const int ch0 = (int)((long long)nch_all * split / a.ksplit);
+  const int ch1 = (int)((long long)nch_all * (split + 1) / a.ksplit);
+
+  auto issue_chunk = [&](int c, int buf) {
+    const int slab = c / ntap, tap = c - slab * ntap;
+    const int kh = tap / a.KW, kw = tap - kh * a.KW;
+    const long long delta = ((long long)kh * a.W + kw) * a.xcs + slab * BK;
+#pragma unroll
+    for (int i = 0; i < A_G; ++i) {
+      const float* src = ((tapok[i] >> tap) & 1u) ? xsrc[i] + delta : pf_conv_zero16;
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)src,
+          (__attribute__((address_space(3))) void*)(As + buf * ASTAGE + (wave * A_G + i) * 8 * BK),
+          16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < B_G; ++i) {
+      const void* src = bsrc[i] ? (const void*)(bsrc[i] + (long long)c * BK)
+                                : (const void*)pf_conv_zero16;
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)src,
+          (__attribute__((address_space(3))) void*)(Bs + buf * 2 * BSTAGE +
+                                                     (wave * B_G + i) * 16 * BK),
+          16, 0, 0);
+    }
+  };
+
+  f32x16 acc[MI][NI];
+#pragma unroll
+  for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[0][ni][r] = 0.f;
+
+  const int sw = ((lane & 31) >> 1) & 7, hh = lane >> 5, r32 = lane & 31;
+  const int arow = wm * TM + r32;
+  auto compute = [&](int buf) {
+    const float* Ab = As + buf * ASTAGE + arow * BK;
+    const unsigned short* Bb = Bs + buf * 2 * BSTAGE;
+#pragma unroll
+    for (int g = 0; g < BK / 16; ++g) {
+      const int s0 = ((4 * g + 2 * hh) ^ sw) * 4, s1 = ((4 * g + 2 * hh + 1) ^ sw) * 4;
+      u32x4_t ah, am, al;
+      split3(*reinterpret_cast<const f32x4*>(Ab + s0), *reinterpret_cast<const f32x4*>(Ab + s1),
+             ah, am, al);
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) {
+        const int row = ni * 32 + r32;
+        const int slot = (2 * g + hh) ^ ((row >> 2) & 3);
+        const unsigned short* bp = Bb + row * BK + slot * 8;
+        const u32x4_t bh = *reinterpret_cast<const u32x4_t*>(bp);
+        const u32x4_t bm = *reinterpret_cast<const u32x4_t*>(bp + BN * BK);
+        const u32x4_t bl = *reinterpret_cast<const u32x4_t*>(bp + 2 * BN * BK);
+        f32x16 c = acc[0][ni];
+        c = mfma_bf16(ah, bh, c);
+        c = mfma_bf16(ah, bm, c);
+        c = mfma_bf16(am, bh, c);
+        c = mfma_bf16(ah, bl, c);
+        c = mfma_bf16(al, bh, c);
+        c = mfma_bf16(am, bm, c);
+        acc[0][ni] = c;
+      }
+    }
+  };
+
+  issue_chunk(ch0, 0);
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  for (int c = ch0; c < ch1; ++c) {
+    const int cur = (c - ch0) & 1;
+    if (c + 1 < ch1) issue_chunk(c + 1, cur ^ 1);
+    compute(cur);
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+  }
   conv_epilogue<BM, BN, WM, WN>(
       a, acc, smem, tm, n0, split, [&](int row) { return m0 + row < a.M ? m0 + row : -1; },
       m0 / a.hw,
@@ -1271,7 +1439,7 @@ enum ConvTile {
   TILE_128x128 = 0, TILE_128x64 = 1, TILE_64x64 = 2, TILE_256x128 = 3,  // contiguous rows
   TILE_H8x128 = 10, TILE_H8x64 = 11, TILE_H16x128 = 12,                 // 8/16 x 16 patches
   TILE_BF6_128x128 = 20, TILE_BF6_128x256 = 21, TILE_BF6_64x128 = 22,   // rows, bf16x6 products
-  TILE_BF6_128x64 = 23
+  TILE_BF6_128x64 = 23, TILE_BF6B_128x128 = 24, TILE_BF6B_128x64 = 25  // + pre-split weights
 };
 
 // POSFEAT_BF6=1: every conv the row-tile DMA kernel serves (1x1, strided, the
@@ -1346,10 +1514,19 @@ Plan plan_for_tile(const ConvArgs& a, int tile) {
   // bf16x6 mode: halo-eligible convs keep fp32 halo tiles only, the rest
   // bf16x6 row tiles only
   if (bf6_on() && glds_ok) {
-    const bool bf6_tile = tile >= TILE_BF6_128x128 && tile <= TILE_BF6_128x64;
+    const bool bf6_tile = tile >= TILE_BF6_128x128 && tile <= TILE_BF6B_128x64;
     if (halo_ok ? bf6_tile || tile < TILE_H8x128 : !bf6_tile) return p;
   }
   switch (tile) {
+    case TILE_BF6B_128x128:
+    case TILE_BF6B_128x64:
+      if (!glds_ok || !bf6_on() || !a.wb) return p;
+      p.kern = KERN_GLDS;
+      p.bm = 128;
+      p.bn = tile == TILE_BF6B_128x64 ? 64 : 128;
+      p.ppi = 0;
+      p.tiles_m = (a.M + p.bm - 1) / p.bm;
+      return p;
     case TILE_BF6_128x128:
     case TILE_BF6_128x256:
     case TILE_BF6_64x128:
@@ -1423,7 +1600,8 @@ Plan conv_plan(const ConvArgs& a, bool allow_split, int forced = -1) {
     d = plan_for_tile(a, tile);
     d.ksplit = tile == TILE_128x128 ? ks : 1;
     if (bf6_on() && cin32 && a.KH * a.KW <= 32 && env.kmax >= KERN_GLDS) {
-      Plan b = plan_for_tile(a, a.Cout > 64 ? TILE_BF6_128x128 : TILE_BF6_128x64);
+      Plan b = plan_for_tile(a, a.wb ? (a.Cout > 64 ? TILE_BF6B_128x128 : TILE_BF6B_128x64)
+                                     : (a.Cout > 64 ? TILE_BF6_128x128 : TILE_BF6_128x64));
       if (b.kern >= 0) {
         b.ksplit = ks;
         d = b;
@@ -1499,6 +1677,14 @@ int conv_run(ConvArgs& a, const Plan& p, hipStream_t st) {
       else
         hipLaunchKernelGGL((conv_glds_kernel<128, 64, 2, 2, 2, true>),
                            dim3(a.nwg * a.ksplit, a.nbatch), dim3(256), 0, st, a);
+      break;
+    case TILE_BF6B_128x128:
+      hipLaunchKernelGGL((conv_bf6b_kernel<128, 128>), dim3(a.nwg * a.ksplit, a.nbatch), dim3(256),
+                         0, st, a);
+      break;
+    case TILE_BF6B_128x64:
+      hipLaunchKernelGGL((conv_bf6b_kernel<128, 64>), dim3(a.nwg * a.ksplit, a.nbatch), dim3(256),
+                         0, st, a);
       break;
     case TILE_256x128: launch_rows<256, 128, 4, 2>(a, p.kern, st); break;
     case TILE_128x128: launch_rows<128, 128, 2, 2>(a, p.kern, st); break;
@@ -1577,6 +1763,12 @@ static int conv_prepare(const posfeat_conv_desc* d, const float* x, const float*
   a.hw = a.OH * a.OW;
   a.nbatch = 1;
   a.bx = a.bw = a.by = 0;
+  a.wb = nullptr;
+  a.wplane = a.bwb = 0;
+  {
+    static const int abl = getenv("POSFEAT_ABL") ? atoi(getenv("POSFEAT_ABL")) : 0;
+    a.abl = abl;
+  }
   return POSFEAT_OK;
 }
 
@@ -1637,12 +1829,13 @@ extern "C" int posfeat_conv2d_nhwc_stats(const posfeat_conv_desc* d, const float
 static const int kAllTiles[] = {TILE_H8x128,      TILE_H8x64,       TILE_128x128,
                                 TILE_128x64,      TILE_64x64,       TILE_256x128,
                                 TILE_BF6_128x128, TILE_BF6_128x256, TILE_BF6_64x128,
-                                TILE_BF6_128x64};
+                                TILE_BF6_128x64,  TILE_BF6B_128x128, TILE_BF6B_128x64};
 
-int pf_conv_candidates(const posfeat_conv_desc* d, int* tiles, int max) {
+int pf_conv_candidates(const posfeat_conv_desc* d, int* tiles, int max, bool wplanes) {
   ConvArgs a;
   float dummy[4] __attribute__((aligned(16)));
   if (conv_prepare(d, dummy, dummy, nullptr, nullptr, dummy, a) != POSFEAT_OK) return 0;
+  if (wplanes) a.wb = reinterpret_cast<const unsigned short*>(dummy);
   int n = 0;
   for (int t : kAllTiles)
     if (plan_for_tile(a, t).kern >= 0 && n < max) tiles[n++] = t;
@@ -1651,9 +1844,11 @@ int pf_conv_candidates(const posfeat_conv_desc* d, int* tiles, int max) {
 
 int pf_conv_run_tile(const posfeat_conv_desc* d, const float* x, const float* w,
                      const float* bias, const float* res, float* y, void* ws, size_t ws_bytes,
-                     int tile, hipStream_t st) {
+                     int tile, hipStream_t st, const unsigned short* wb, long long wplane) {
   ConvArgs a;
   PF_TRY(conv_prepare(d, x, w, bias, res, y, a));
+  a.wb = wb;
+  a.wplane = wplane;
   const size_t need = posfeat_conv2d_workspace(d);
   const bool split = need > 0 && ws && ws_bytes >= need;
   const Plan p = conv_plan(a, split, tile);
@@ -1684,9 +1879,12 @@ size_t pf_conv_stats_ws_max(const posfeat_conv_desc* d) {
 
 int pf_conv_stats_run_tile(const posfeat_conv_desc* d, const float* x, const float* w,
                            const float* bias, float* y, void* ws, size_t ws_bytes, float* mean,
-                           float* rstd, float eps, int tile, hipStream_t st) {
+                           float* rstd, float eps, int tile, hipStream_t st,
+                           const unsigned short* wb, long long wplane) {
   ConvArgs a;
   PF_TRY(conv_prepare(d, x, w, bias, nullptr, y, a));
+  a.wb = wb;
+  a.wplane = wplane;
   const Plan p = conv_plan(a, false, tile);
   const size_t need = stats_ws_for(a, p, d->n);
   if (need == 0) return POSFEAT_E_UNSUPPORTED;
@@ -1848,7 +2046,8 @@ extern "C" int posfeat_conv2_up4(int n, int H, int W, const float* L, int lcs, c
 // == 0, the 1x1-conv weight layout), z < nb: ONE launch of conv_glds_kernel with
 // blockIdx.y = z (Winograd's 16 transform-domain GEMMs, wino.hip).
 int pf_gemm_batched(const float* A, int lda, long long sa, const float* B, long long sb, float* C,
-                    int ldc, long long sc, int nb, int M, int N, int K, hipStream_t st) {
+                    int ldc, long long sc, int nb, int M, int N, int K, hipStream_t st,
+                    const unsigned short* Bb, long long bplane) {
   if (K % BK || N % 4 || nb < 1) return POSFEAT_E_INVALID;
   posfeat_conv_desc d;
   d.n = 1;
@@ -1865,6 +2064,8 @@ int pf_gemm_batched(const float* A, int lda, long long sa, const float* B, long 
   d.act = POSFEAT_ACT_NONE;
   ConvArgs a;
   PF_TRY(conv_prepare(&d, A, B, nullptr, nullptr, C, a));
+  a.wb = Bb;  // B as three bf16 planes (plane stride bplane, batch stride sb)
+  a.wplane = bplane;
   // the heuristic sizes tiles for ONE GEMM; with nb of them in the grid the
   // 128x128 tile (2x the operand reuse of 64x64) still fills the chip
   const long long t128 = (long long)((M + 127) / 128) * ((N + 127) / 128) * nb;
@@ -1873,6 +2074,7 @@ int pf_gemm_batched(const float* A, int lda, long long sa, const float* B, long 
   a.nbatch = nb;
   a.bx = sa;
   a.bw = sb;
+  a.bwb = sb;
   a.by = sc;
   return conv_run(a, p, st);
 }

@@ -126,6 +126,11 @@ struct posfeat_model {
   bool up4tap = true;
   Buf tapw, tapP, tappart;
   bool bf6p = false;  // conv precision mode 2 (pre-split Winograd / tap GEMM operands)
+  // bf16x6 with pre-split weights (conv_bf6b_kernel, the default in mode 1;
+  // POSFEAT_BF6B=0 off): the weight blob is split into three bf16 planes at
+  // the start of every forward, Winograd U and the tap weights as planes
+  bool wsplit = false;
+  Buf wpl;
   bool tapb = false;  // bf16x6 tap GEMM on pre-split planes (POSFEAT_BF6=2)
   Buf tapwb, tapLb;
   Buf gf_w, gf_b;
@@ -172,8 +177,19 @@ struct Ctx {
   float* f(const Buf& b) const { return reinterpret_cast<float*>(ws + b.off); }
   double* d(const Buf& b) const { return reinterpret_cast<double*>(ws + b.off); }
   const float* W(const std::string& n) const { return m->wts + specs().find(n)->w_off; }
+  // the bf16 planes of blob weights w (posfeat_model::wsplit), else nothing
+  void wplanes_of(const float* w, const unsigned short** wb, long long* wplane) const;
   const float* Bi(const std::string& n) const { return m->wts + specs().find(n)->b_off; }
 };
+
+void Ctx::wplanes_of(const float* w, const unsigned short** wb, long long* wplane) const {
+  *wb = nullptr;
+  *wplane = 0;
+  const long long total = specs().total;
+  if (!m->wsplit || w < m->wts || w >= m->wts + total) return;
+  *wb = reinterpret_cast<const unsigned short*>(ws + m->wpl.off) + (w - m->wts);
+  *wplane = total;
+}
 
 // record-and-run helper for optional per-launch timing
 template <class F>
@@ -201,13 +217,14 @@ int timed(Ctx& c, const std::string& label, double flops, F&& fn) {
 // Time each legal tile for this conv (1 warm-up + 3 timed launches on the
 // layer's real inputs) and return the fastest; -1 (default plan) if only one.
 template <class Run>
-int tune(const std::string& name, const posfeat_conv_desc& d, hipStream_t st, Run&& run) {
+int tune(const std::string& name, const posfeat_conv_desc& d, hipStream_t st, Run&& run,
+         bool wplanes) {
   static const bool log = [] {
     const char* e = getenv("POSFEAT_AUTOTUNE_LOG");
     return e && e[0] == '1';
   }();
   int cand[16];
-  const int nc = pf_conv_candidates(&d, cand, 16);
+  const int nc = pf_conv_candidates(&d, cand, 16, wplanes);
   if (nc <= 1) return -1;
   hipEvent_t e0, e1;
   if (hipEventCreate(&e0) != hipSuccess) return -1;
@@ -254,23 +271,23 @@ TileCache& tile_cache() {
   static TileCache t;
   return t;
 }
-std::string desc_class(const posfeat_conv_desc& d, bool res) {
+std::string desc_class(const posfeat_conv_desc& d, bool res, bool wplanes) {
   char b[160];
-  snprintf(b, sizeof b, "%d/%d/%d/%dx%d/s%d/p%d/%d/%d/a%d/r%d/P%d", d.cin, d.x_cstride, d.cout,
+  snprintf(b, sizeof b, "%d/%d/%d/%dx%d/s%d/p%d/%d/%d/a%d/r%d/P%d%s", d.cin, d.x_cstride, d.cout,
            d.kh, d.kw, d.stride, d.pad, d.y_cstride, d.res_cstride, d.act, res ? 1 : 0,
-           pf_conv_precision());
+           pf_conv_precision(), wplanes ? "B" : "");
   return b;
 }
 double desc_m(const posfeat_conv_desc& d) {
   const int oh = (d.h + 2 * d.pad - d.kh) / d.stride + 1, ow = (d.w + 2 * d.pad - d.kw) / d.stride + 1;
   return (double)d.n * oh * ow;
 }
-bool tile_lookup(const posfeat_conv_desc& d, bool res, int* tile) {
+bool tile_lookup(const posfeat_conv_desc& d, bool res, bool wplanes, int* tile) {
   static const bool similar = [] {
     const char* e = getenv("POSFEAT_TUNE_SIMILAR");
     return !(e && e[0] == '0');
   }();
-  const std::string cls = desc_class(d, res);
+  const std::string cls = desc_class(d, res, wplanes);
   char nhw[48];
   snprintf(nhw, sizeof nhw, "|%d/%d/%d", d.n, d.h, d.w);
   TileCache& t = tile_cache();
@@ -296,14 +313,14 @@ bool tile_lookup(const posfeat_conv_desc& d, bool res, int* tile) {
   if (best > std::log(1.25)) return false;
   if (bt >= 0) {  // the tile must be legal for this shape too
     int cand[16];
-    const int nc = pf_conv_candidates(&d, cand, 16);
+    const int nc = pf_conv_candidates(&d, cand, 16, wplanes);
     if (std::find(cand, cand + nc, bt) == cand + nc) return false;
   }
   *tile = bt;
   return true;
 }
-void tile_store(const posfeat_conv_desc& d, bool res, int tile) {
-  const std::string cls = desc_class(d, res);
+void tile_store(const posfeat_conv_desc& d, bool res, bool wplanes, int tile) {
+  const std::string cls = desc_class(d, res, wplanes);
   char nhw[48];
   snprintf(nhw, sizeof nhw, "|%d/%d/%d", d.n, d.h, d.w);
   TileCache& t = tile_cache();
@@ -313,25 +330,32 @@ void tile_store(const posfeat_conv_desc& d, bool res, int tile) {
 
 // run (autotuned on the first forward of the instance, keyed by `key`) one
 // conv described by d with packed weights w
+// wb / wplane: the weights' bf16 planes (default: w's planes in the
+// per-forward split of the weight blob, when w lies in the blob)
 int conv_desc_run(Ctx& c, const std::string& key, const posfeat_conv_desc& d, const float* x,
-                  const float* w, const float* bias, const float* res, float* y, double flops) {
+                  const float* w, const float* bias, const float* res, float* y, double flops,
+                  const unsigned short* wb = nullptr, long long wplane = 0) {
   const size_t need = posfeat_conv2d_workspace(&d);
   if (c.dry) {
     if (need > c.m->splitk_need) c.m->splitk_need = need;
     return POSFEAT_OK;
   }
+  if (!wb) c.wplanes_of(w, &wb, &wplane);
   const Buf& sk = c.side ? c.m->splitk2 : c.m->splitk;
   float* part = c.f(sk);
   const size_t have = sk.floats * sizeof(float);
-  auto run = [&](int tile) { return pf_conv_run_tile(&d, x, w, bias, res, y, part, have, tile, c.st); };
+  auto run = [&](int tile) {
+    return pf_conv_run_tile(&d, x, w, bias, res, y, part, have, tile, c.st, wb, wplane);
+  };
+  const bool wp = wb != nullptr;
   int tile = -1;
   auto it = c.m->tuned.find(key);
   if (it != c.m->tuned.end()) {
     tile = it->second;
   } else if (c.m->autotune) {
-    if (!tile_lookup(d, res != nullptr, &tile)) {
-      tile = tune(key, d, c.st, run);
-      tile_store(d, res != nullptr, tile);
+    if (!tile_lookup(d, res != nullptr, wp, &tile)) {
+      tile = tune(key, d, c.st, run, wp);
+      tile_store(d, res != nullptr, wp, tile);
     }
     c.m->tuned[key] = tile;
   }
@@ -375,12 +399,12 @@ int forward(Ctx& c, const float* img, posfeat_extract_out* out, int mode = MODE_
 const char* const kWinoLayers[5] = {"upconv3.conv", "iconv3", "upconv2.conv", "iconv2",
                                     "head.conv1"};
 
-long long wino_u_offset(const std::string& name, bool bf6p) {
+long long wino_u_offset(const std::string& name, bool planes) {
   long long off = 0;
   for (const char* n : kWinoLayers) {
     if (name == n) return off;
     const Spec* s = specs().find(n);
-    off += (long long)(bf6p ? 54 : 36) * s->cout * s->cin;  // bf16x6: three planes
+    off += (long long)(planes ? 54 : 36) * s->cout * s->cin;  // bf16x6: three planes
   }
   return -1;
 }
@@ -388,7 +412,7 @@ long long wino_u_offset(const std::string& name, bool bf6p) {
 int conv3x3(Ctx& c, const std::string& name, const float* x, int n, int h, int w, int xcs, float* y,
             int ycs, int act) {
   posfeat_model* m = c.m;
-  const long long uo = wino_u_offset(name, m->bf6p);
+  const long long uo = wino_u_offset(name, m->bf6p || m->wsplit);
   if (!m->wino || uo < 0 || (h & 1) || (w & 1))
     return conv(c, name, x, n, h, w, xcs, y, ycs, 1, act);
   const Spec* s = specs().find(name);
@@ -396,7 +420,8 @@ int conv3x3(Ctx& c, const std::string& name, const float* x, int n, int h, int w
   float* U = c.f(m->wino_u) + uo;
   PF_TRY(timed(c, "wino:weights", 0,
                [&] {
-                 return pf_wino_weights_hw(c.W(name), s->cout, s->cin, h, w, U, c.st, m->bf6p);
+                 return pf_wino_weights_hw(c.W(name), s->cout, s->cin, h, w, U, c.st,
+                                           m->bf6p || m->wsplit);
                }));
   // executed transform-domain MACs: F(4x4) 36 per 4x4 tile, F(2x2) 16 per 2x2 tile
   const bool f4 = h % 4 == 0 && w % 4 == 0 && !(getenv("POSFEAT_WINO") && getenv("POSFEAT_WINO")[0] == '1');
@@ -406,7 +431,7 @@ int conv3x3(Ctx& c, const std::string& name, const float* x, int n, int h, int w
   auto stage = [&](int st_bits) {
     return pf_wino_conv(x, xcs, n, h, w, s->cin, U, c.Bi(name), s->cout, act, y, ycs,
                         c.f(m->wino_ws), m->wino_ws.floats * sizeof(float), c.st, st_bits,
-                        m->bf6p);
+                        m->bf6p ? 2 : m->wsplit ? 1 : 0);
   };
   PF_TRY(timed(c, "wino:in:" + name, 0, [&] { return stage(1); }));
   PF_TRY(timed(c, "conv:" + name + ".wino", 2.0 * T * (f4 ? 36 : 16) * s->cin * s->cout,
@@ -454,9 +479,12 @@ int conv_in(Ctx& c, const std::string& name, const float* x, int n, int h, int w
   // different tile would change mean/rstd in the last bits and make results
   // depend on a timing race.  The default plan is the tuned winner for these
   // layers anyway (profiles/r01/autotune_choices_b8_480x640.txt).
+  const unsigned short* wb = nullptr;
+  long long wplane = 0;
+  c.wplanes_of(c.W(name), &wb, &wplane);
   return timed(c, "conv:" + name, flops, [&] {
     return pf_conv_stats_run_tile(&d, x, c.W(name), c.Bi(name), y, part, have, mean, rstd, 1e-5f,
-                                  -1, c.st);
+                                  -1, c.st, wb, wplane);
   });
 }
 
@@ -528,13 +556,18 @@ void plan(posfeat_model* m) {
   if (!(m->up4 && m->gfuse) || m->train) m->imgstats = false;
   if (m->imgstats) alloc(m->imws, pf_gfuse_imgstats_ws_bytes((int)B, (int)H) / 4 + 4);
   m->bf6p = pf_bf6p_on();  // fixed for the instance: buffer sizes depend on it
+  {
+    const char* e = getenv("POSFEAT_BF6B");
+    m->wsplit = pf_conv_precision() == 1 && !(e && e[0] == '0') && specs().total % 4 == 0;
+  }
+  if (m->wsplit) alloc(m->wpl, (size_t)specs().total * 3 / 2 + 4);
   if (m->wino) {
     size_t uf = 0, wb = 0;
     const int dims[5][2] = {{(int)h8, (int)w8}, {(int)h8, (int)w8}, {(int)h4, (int)w4},
                             {(int)h4, (int)w4}, {(int)h4, (int)w4}};
     for (int i = 0; i < 5; ++i) {
       const Spec* s = specs().find(kWinoLayers[i]);
-      uf += (size_t)(m->bf6p ? 54 : 36) * s->cout * s->cin;
+      uf += (size_t)(m->bf6p || m->wsplit ? 54 : 36) * s->cout * s->cin;
       wb = std::max(wb, pf_wino_ws_bytes((int)B, dims[i][0], dims[i][1], s->cin, s->cout));
     }
     alloc(m->wino_u, uf);
@@ -545,7 +578,7 @@ void plan(posfeat_model* m) {
     const char* e = getenv("POSFEAT_SIDE");
     m->side = !(e && e[0] == '0') && m->up4 && m->gfuse && !m->train;
     const char* a = getenv("POSFEAT_SIDE_AT");
-    m->side_at = a ? std::min(3, std::max(0, atoi(a))) : 0;
+    m->side_at = a ? std::min(3, std::max(0, atoi(a))) : 2;
   }
   if (m->up4) {
     if (!m->imgstats) alloc(m->g64, B * H * W * 64);
@@ -554,10 +587,10 @@ void plan(posfeat_model* m) {
     if (m->up4tap) {
       alloc(m->tapw, pf_up4tap_weights_floats());
       m->tapb = m->bf6p;
-      if (m->tapb) {  // three bf16 planes of the tap weights and of L
+      if (m->tapb || m->wsplit)  // three bf16 planes of the tap weights
         alloc(m->tapwb, pf_up4tap_weights_floats() * 3 / 2);
+      if (m->tapb)  // ... and of L
         alloc(m->tapLb, (size_t)B * h4 * w4 * 192 * 3 / 2);
-      }
       alloc(m->tapP, pf_up4tap_p_floats((int)B, (int)H, (int)W));
       alloc(m->tappart, pf_up4tap_part_bytes((int)B, (int)H, (int)W) / 4 + 4);
     } else if (m->up4wino) {
@@ -702,9 +735,10 @@ int image_branch(Ctx& c, const float* img4) {
   else
     PF_TRY(timed(s, "head.conv2.tapw", 0, [&] {
       PF_TRY(pf_up4tap_weights(s.W("head.conv2"), s.f(m->tapw), s.st));
-      return m->tapb ? pf_split3_rows(s.f(m->tapw), 1152, 192, 192,
-                                      reinterpret_cast<unsigned short*>(s.f(m->tapwb)), s.st)
-                     : POSFEAT_OK;
+      return m->tapb || m->wsplit
+                 ? pf_split3_rows(s.f(m->tapw), 1152, 192, 192,
+                                  reinterpret_cast<unsigned short*>(s.f(m->tapwb)), s.st)
+                 : POSFEAT_OK;
     }));
   PF_TRY(timed(s, "head.conv2.gfuse_w", 0, [&] {
     return pf_gfuse_weights(s.W("head.conv2"), s.Bi("head.conv2"), s.W("head.convimg"),
@@ -732,6 +766,11 @@ int forward(Ctx& c, const float* img, posfeat_extract_out* out, int mode, const 
   float* img4 = c.f(m->img4);
   float* headcat = c.f(m->headcat);
   // ---- ResUNet (DescNet.py:64-84) -----------------------------------------
+  if (m->wsplit)  // the weight blob's bf16 planes for the pre-split bf16x6 tiles
+    PF_TRY(timed(c, "weights.split", 0, [&] {
+      return pf_split3_rows(m->wts, specs().total / 4, 4, 4,
+                            reinterpret_cast<unsigned short*>(c.f(m->wpl)), c.st);
+    }));
   PF_TRY(timed(c, "layout:img", 0, [&] { return pf_nchw_to_nhwc(img, B, 3, H, W, 4, img4, c.st); }));
   // the first forward of a shape autotunes every main-stream conv by timing
   // it: run it serially so the side stream's kernels do not contend with
@@ -739,7 +778,8 @@ int forward(Ctx& c, const float* img, posfeat_extract_out* out, int mode, const 
   const bool side = m->side && mode != MODE_BACKBONE &&
                     (c.dry || ((m->tuned_modes >> mode) & 1u) || !m->autotune);
   // where the image branch forks (POSFEAT_SIDE_AT): 0 after the image layout,
-  // 1 before layer2, 2 before layer3, 3 before the decoder
+  // 1 before layer2, 2 before layer3 (default: the 60x80 layers underfill the
+  // chip; overlapping layer1 slowed its convs 2-4x), 3 before the decoder
   const int side_at = mode == MODE_HEAD ? 0 : m->side_at;
   if (side && side_at == 0) PF_TRY(image_branch(c, img4));
   if (mode == MODE_HEAD) {
@@ -855,9 +895,10 @@ int head_forward(Ctx& c, float* img4, float* local_point, bool side) {
     if (!side && m->up4tap)
       PF_TRY(timed(c, "head.conv2.tapw", 0, [&] {
         PF_TRY(pf_up4tap_weights(c.W("head.conv2"), c.f(m->tapw), c.st));
-        return m->tapb ? pf_split3_rows(c.f(m->tapw), 1152, 192, 192,
-                                        reinterpret_cast<unsigned short*>(c.f(m->tapwb)), c.st)
-                       : POSFEAT_OK;
+        return m->tapb || m->wsplit
+                   ? pf_split3_rows(c.f(m->tapw), 1152, 192, 192,
+                                    reinterpret_cast<unsigned short*>(c.f(m->tapwb)), c.st)
+                   : POSFEAT_OK;
       }));
     if (side) {
       // join the image branch (it wrote the G part into y)
@@ -909,7 +950,10 @@ int head_forward(Ctx& c, float* img4, float* local_point, bool side) {
         }));
       } else {
         PF_TRY(conv_desc_run(c, "head.conv2.up4tap", d, c1, c.f(m->tapw), nullptr, nullptr,
-                             c.f(m->tapP), 2.0 * B * h4 * w4 * 1152.0 * 192));
+                             c.f(m->tapP), 2.0 * B * h4 * w4 * 1152.0 * 192,
+                             m->wsplit ? reinterpret_cast<const unsigned short*>(c.f(m->tapwb))
+                                       : nullptr,
+                             1152LL * 192));
       }
       PF_TRY(timed(c, "head.conv2.combine", 0, [&] {
         return pf_up4tap_combine(B, H, W, c.f(m->tapP), c2, 128, c.d(m->tappart), mean, rstd,

@@ -34,32 +34,40 @@ int pf_up4_main(int n, int H, int W, const float* L, int lcs, const float* wph, 
 
 // conv tile control (conv.hip): legal tile ids for a shape, and runs with a
 // given tile (-1 = default).  All tiles of one shape give bit-identical results.
-int pf_conv_candidates(const posfeat_conv_desc* d, int* tiles, int max);
+// wplanes / wb: the weights also exist as three bf16 planes of w's layout
+// (plane stride wplane elements): enables the pre-split bf16x6 tiles
+int pf_conv_candidates(const posfeat_conv_desc* d, int* tiles, int max, bool wplanes = false);
 int pf_conv_run_tile(const posfeat_conv_desc* d, const float* x, const float* w,
                      const float* bias, const float* res, float* y, void* ws, size_t ws_bytes,
-                     int tile, hipStream_t st);
+                     int tile, hipStream_t st, const unsigned short* wb = nullptr,
+                     long long wplane = 0);
 size_t pf_conv_stats_ws_max(const posfeat_conv_desc* d);
 int pf_conv_stats_run_tile(const posfeat_conv_desc* d, const float* x, const float* w,
                            const float* bias, float* y, void* ws, size_t ws_bytes, float* mean,
-                           float* rstd, float eps, int tile, hipStream_t st);
+                           float* rstd, float eps, int tile, hipStream_t st,
+                           const unsigned short* wb = nullptr, long long wplane = 0);
 
 // batched GEMM on the conv engine (conv.hip): C[z] = A[z] x B[z]^T, z < nb
+// Bb: B also as three bf16 planes (plane stride bplane; batch stride sb)
 int pf_gemm_batched(const float* A, int lda, long long sa, const float* B, long long sb, float* C,
-                    int ldc, long long sc, int nb, int M, int N, int K, hipStream_t st);
+                    int ldc, long long sc, int nb, int M, int N, int K, hipStream_t st,
+                    const unsigned short* Bb = nullptr, long long bplane = 0);
 // Winograd F(2x2,3x3) (wino.hip): U = [16][Cout][Cin] transformed weights
 size_t pf_wino_ws_bytes(int n, int h, int w, int Cin, int Cout);
 size_t pf_wino_weights_floats(int Cin, int Cout);
 int pf_wino_weights(const float* wpk, int Cout, int Cin, float* U, hipStream_t st);  // F(2x2)
 // U for the variant pf_wino_conv picks at (h, w): F(4x4) if h, w % 4 == 0
-// bf6p: (F(4x4) only) U / V as three bf16 planes for the bf16x6 GEMM
-// (gemm6.hip); U then needs pf_wino_weights_floats_bf6p floats
+// bf6p (weights): U written as three bf16 planes (F(4x4), Cout % 128 == 0);
+// U then needs pf_wino_weights_floats_bf6p floats.  pf_wino_conv planes: 0
+// fp32 U, 1 U planes (pre-split-weight bf16x6 tiles), 2 U and V planes
+// (gemm6.hip)
 int pf_wino_weights_hw(const float* wpk, int Cout, int Cin, int h, int w, float* U,
                        hipStream_t st, bool bf6p = false);
 size_t pf_wino_weights_floats_bf6p(int Cin, int Cout);
 // stages: bit 0 input transform, bit 1 the batched GEMMs, bit 2 output transform
 int pf_wino_conv(const float* x, int xcs, int n, int h, int w, int Cin, const float* U,
                  const float* bias, int Cout, int act, float* y, int ycs, void* ws, size_t ws_bytes,
-                 hipStream_t st, int stages = 7, bool bf6p = false);
+                 hipStream_t st, int stages = 7, int planes = 0);
 // head.conv2's G part as one per-image 5x5 conv of the image (gfuse.hip)
 size_t pf_gfuse_weights_floats(int n);
 int pf_gfuse_weights(const float* w2_packed, const float* b2, const float* w1_packed,

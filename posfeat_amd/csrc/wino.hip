@@ -664,7 +664,8 @@ int pf_wino_weights(const float* wpk, int Cout, int Cin, float* U, hipStream_t s
 static int wino_conv_impl(const float* x, int xcs, int n, int h, int w, int Cin, const float* U,
                           bool U_is_f4, const float* bias, int Cout, int act, float* y, int ycs,
                           void* ws, size_t ws_bytes, hipStream_t st, int stages = 7,
-                          bool bf6p = false) {
+                          int planes = 0) {
+  const bool bf6p = planes == 2;
   if ((h & 1) || (w & 1) || Cin % 32 || Cout % 4 || xcs % 4 || ycs % 4 || n <= 0)
     return POSFEAT_E_INVALID;
   if (ws_bytes < pf_wino_ws_bytes(n, h, w, Cin, Cout)) return POSFEAT_E_WORKSPACE;
@@ -701,9 +702,13 @@ static int wino_conv_impl(const float* x, int xcs, int n, int h, int w, int Cin,
                          x, xcs, n, h, w, Cin / 4, V4, 0);
       PF_CHECK_LAUNCH();
     }
-    if (stages & 2)
+    if (stages & 2)  // planes == 1: U holds its bf16 planes (pre-split bf16x6 tiles)
       PF_TRY(pf_gemm_batched(V4, Cin, T4 * Cin, U, (long long)Cout * Cin, M4, Cout, T4 * Cout, 36,
-                             (int)T4, Cout, Cin, st));
+                             (int)T4, Cout, Cin, st,
+                             planes == 1 && Cout % 128 == 0
+                                 ? reinterpret_cast<const unsigned short*>(U)
+                                 : nullptr,
+                             36LL * Cout * Cin));
     if (stages & 4) {
       hipLaunchKernelGGL(wino4_output_kernel, dim3(grid_for(T4 * (Cout / 4), 256)), dim3(256), 0,
                          st, M4, n, h, w, Cout / 4, bias, act, y, ycs);
@@ -733,9 +738,9 @@ static int wino_conv_impl(const float* x, int xcs, int n, int h, int w, int Cin,
 // U from pf_wino_weights_hw(.., h, w, ..): the variant is chosen from (h, w)
 int pf_wino_conv(const float* x, int xcs, int n, int h, int w, int Cin, const float* U,
                  const float* bias, int Cout, int act, float* y, int ycs, void* ws, size_t ws_bytes,
-                 hipStream_t st, int stages, bool bf6p) {
+                 hipStream_t st, int stages, int planes) {
   return wino_conv_impl(x, xcs, n, h, w, Cin, U, true, bias, Cout, act, y, ycs, ws, ws_bytes, st,
-                        stages, bf6p);
+                        stages, planes);
 }
 
 namespace {
