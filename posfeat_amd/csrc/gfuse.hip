@@ -359,6 +359,116 @@ __global__ __launch_bounds__(256) void gfuse_conv5_kernel(const float* __restric
     }
   }
 }
+
+// The same conv with bf16x6 products (conv.hip §bf16x6; the default
+// arithmetic): K = 28 taps x 4 channels (taps 25..27 zero) in 7 k16 steps of
+// v_mfma_f32_32x32x16_bf16 -- lane half h holds taps 4g + 2h, 4g + 2h + 1 (8
+// values) of step g for the pixel and for the weights, both split in
+// registers into three bf16 terms, six products per pair.  2.5x fewer
+// matrix-core cycles than the fp32 form.  Weight rows padded to 116 floats
+// (29 16-B slots, odd: conflict-free ds_read_b128).
+constexpr int G6_WP = 116;
+typedef __bf16 g6_bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned g6_u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void g6_split(const f32x4& p0, const f32x4& p1, g6_u32x4& h,
+                                         g6_u32x4& m, g6_u32x4& l) {
+  uint2 h0, m0, l0, h1, m1, l1;
+  pf_split3x4(p0, h0, m0, l0);
+  pf_split3x4(p1, h1, m1, l1);
+  h = g6_u32x4{h0.x, h0.y, h1.x, h1.y};
+  m = g6_u32x4{m0.x, m0.y, m1.x, m1.y};
+  l = g6_u32x4{l0.x, l0.y, l1.x, l1.y};
+}
+__device__ __forceinline__ f32x16 g6_mfma(const g6_u32x4& a, const g6_u32x4& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(g6_bf16x8, a),
+                                                 __builtin_bit_cast(g6_bf16x8, b), c, 0, 0, 0);
+}
+
+__global__ __launch_bounds__(256) void gfuse_conv5_bf6_kernel(const float* __restrict__ img4,
+                                                              int H, int W,
+                                                              const float* __restrict__ wc,
+                                                              const float* __restrict__ bc,
+                                                              float* __restrict__ y, int ycs) {
+  __shared__ __attribute__((aligned(16))) float sw[GF_COUT * G6_WP];
+  __shared__ __attribute__((aligned(16))) float sp[G5_PR * G5_PC * 4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const int b = blockIdx.y;
+  const int ntc = (W + G5_TC - 1) / G5_TC;
+  const int ty0 = (blockIdx.x / ntc) * G5_TR, tx0 = (blockIdx.x % ntc) * G5_TC;
+  const float* ib = img4 + (long long)b * H * W * 4;
+  const float* wb = wc + (long long)b * GF_COUT * GF_KPAD;
+  for (int i = tid; i < GF_COUT * 28; i += 256) {  // [co][tap][4], taps 25..27 zero
+    const int co = i / 28, t = i - co * 28;
+    const f32x4 v = t < 25 ? *reinterpret_cast<const f32x4*>(wb + (long long)co * GF_KPAD + t * 4)
+                           : f32x4{0.f, 0.f, 0.f, 0.f};
+    *reinterpret_cast<f32x4*>(sw + co * G6_WP + t * 4) = v;
+  }
+  for (int i = tid; i < G5_PR * G5_PC; i += 256) {
+    const int py = i / G5_PC, px = i - py * G5_PC;
+    const int yy = ty0 - 2 + py, xx = tx0 - 2 + px;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W)
+      v = *reinterpret_cast<const f32x4*>(ib + ((long long)yy * W + xx) * 4);
+    *reinterpret_cast<f32x4*>(sp + i * 4) = v;
+  }
+  __syncthreads();
+  f32x16 acc[2][4];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
+  const int col = lane & 31;
+#pragma unroll
+  for (int g = 0; g < 7; ++g) {
+    const int t0 = 4 * g + 2 * h, t1 = t0 + 1;
+    const int a0 = t0 < 25 ? t0 : 24, a1 = t1 < 25 ? t1 : 24;  // zero weights beyond 24
+    g6_u32x4 ah[2], am[2], al[2];
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) {
+      const int r = 2 * wave + mi;
+      g6_split(*reinterpret_cast<const f32x4*>(sp + (((r + a0 / 5) * G5_PC) + col + a0 % 5) * 4),
+               *reinterpret_cast<const f32x4*>(sp + (((r + a1 / 5) * G5_PC) + col + a1 % 5) * 4),
+               ah[mi], am[mi], al[mi]);
+    }
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const float* wr = sw + (ni * 32 + col) * G6_WP + t0 * 4;
+      g6_u32x4 bh, bm, bl;
+      g6_split(*reinterpret_cast<const f32x4*>(wr), *reinterpret_cast<const f32x4*>(wr + 4), bh,
+               bm, bl);
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi) {
+        f32x16 c = acc[mi][ni];
+        c = g6_mfma(ah[mi], bh, c);
+        c = g6_mfma(ah[mi], bm, c);
+        c = g6_mfma(am[mi], bh, c);
+        c = g6_mfma(ah[mi], bl, c);
+        c = g6_mfma(al[mi], bh, c);
+        c = g6_mfma(am[mi], bm, c);
+        acc[mi][ni] = c;
+      }
+    }
+  }
+  const float* bcb = bc + (long long)b * GF_COUT;
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi) {
+    const int yy = ty0 + 2 * wave + mi;
+    if (yy >= H) continue;
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const int co = ni * 32 + col;
+      const float bias = bcb[co];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int xx = tx0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (xx < W) y[((long long)(b * H + yy) * W + xx) * ycs + co] = acc[mi][ni][r] + bias;
+      }
+    }
+  }
+}
 }  // namespace
 
 // wc (n*128*128) | bc (n*128) | w2t (9*64*128)
@@ -391,8 +501,12 @@ int pf_gfuse_conv(const float* img4, const float* c, int ccs, int n, int H, int 
   if (!c && !(w1_packed && b1)) return POSFEAT_E_INVALID;
   if (ycs % 4 || n <= 0) return POSFEAT_E_INVALID;
   const int ntiles = ((W + G5_TC - 1) / G5_TC) * ((H + G5_TR - 1) / G5_TR);
-  hipLaunchKernelGGL(gfuse_conv5_kernel, dim3(ntiles, n), dim3(256), 0, st, img4, H, W, wc, bc, y,
-                     ycs);
+  if (pf_conv_precision() >= 1)  // bf16x6 products (the default conv arithmetic)
+    hipLaunchKernelGGL(gfuse_conv5_bf6_kernel, dim3(ntiles, n), dim3(256), 0, st, img4, H, W, wc,
+                       bc, y, ycs);
+  else
+    hipLaunchKernelGGL(gfuse_conv5_kernel, dim3(ntiles, n), dim3(256), 0, st, img4, H, W, wc, bc,
+                       y, ycs);
   PF_CHECK_LAUNCH();
   (void)w2_packed;
   const int k1pad = posfeat_conv_packed_k(3, 3, 3);
