@@ -834,7 +834,8 @@ __global__ __launch_bounds__(256) void conv_bf6b_kernel(ConvArgs a) {
 // 16 consecutive output columns, i.e. 16 distinct hx mod 16 for every tap
 // shift -> conflict-free.  Next slab's halo and next chunk's weights are in
 // flight while the current chunk is multiplied (two LDS stages each).
-template <int PH, int BN, int WM, int WN, int KH, int KW>
+// BF6: the products as bf16x6 (both operands split in registers, see split3)
+template <int PH, int BN, int WM, int WN, int KH, int KW, bool BF6 = false>
 __global__ __launch_bounds__(WM* WN * 64) void conv_halo_kernel(ConvArgs a) {
   constexpr int PW = 16;
   constexpr int BM = PH * PW;
@@ -946,6 +947,36 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_halo_kernel(ConvArgs a) {
     const int hsw = ((px + kw) >> 1) & 7;
     const float* Ab = As + (abuf * HPR + hrow0 + kh * HX + kw) * BK;
     const float* Bb = Bs + (bcur * BN + brow) * BK;
+    if constexpr (BF6) {
+#pragma unroll
+      for (int g = 0; g < BK / 16; ++g) {
+        const int k0 = 4 * g + 2 * (lane >> 5);
+        u32x4_t ah[MI], am[MI], al[MI], bh[NI], bm[NI], bl[NI];
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi)
+          split3(*reinterpret_cast<const f32x4*>(Ab + mi * 2 * HX * BK + (k0 ^ hsw) * 4),
+                 *reinterpret_cast<const f32x4*>(Ab + mi * 2 * HX * BK + ((k0 + 1) ^ hsw) * 4),
+                 ah[mi], am[mi], al[mi]);
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni)
+          split3(*reinterpret_cast<const f32x4*>(Bb + ni * 32 * BK + (k0 ^ bsw) * 4),
+                 *reinterpret_cast<const f32x4*>(Bb + ni * 32 * BK + ((k0 + 1) ^ bsw) * 4),
+                 bh[ni], bm[ni], bl[ni]);
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < NI; ++ni) {
+            f32x16 cc = acc[mi][ni];
+            cc = mfma_bf16(ah[mi], bh[ni], cc);
+            cc = mfma_bf16(ah[mi], bm[ni], cc);
+            cc = mfma_bf16(am[mi], bh[ni], cc);
+            cc = mfma_bf16(ah[mi], bl[ni], cc);
+            cc = mfma_bf16(al[mi], bh[ni], cc);
+            cc = mfma_bf16(am[mi], bm[ni], cc);
+            acc[mi][ni] = cc;
+          }
+      }
+    } else
 #pragma unroll
     for (int kk = 0; kk < BK / 8; ++kk) {
       const int s = (lane >> 5) + 2 * kk;
@@ -1448,6 +1479,14 @@ enum ConvTile {
 // set of a conv is then either all-bf16x6 or all-fp32, so the autotuner's
 // choice never changes results.
 bool bf6_on() { return pf_conv_precision() >= 1; }
+// the 3x3 stride-1 halo kernel in bf16x6 too (POSFEAT_BF6_HALO=0: fp32 MFMA)
+bool halo_bf6_on() {
+  static const bool off = [] {
+    const char* e = getenv("POSFEAT_BF6_HALO");
+    return e && e[0] == '0';
+  }();
+  return bf6_on() && !off;
+}
 // LDS stages of the bf16x6 row tiles (POSFEAT_BF6_NST: 2, 3 or 4)
 int bf6_nst() {
   static const int n = [] {
@@ -1643,10 +1682,16 @@ int conv_run(ConvArgs& a, const Plan& p, hipStream_t st) {
   const dim3 grid(a.nwg * a.ksplit);
   switch (p.tile) {
     case TILE_H8x128:
-      hipLaunchKernelGGL((conv_halo_kernel<8, 128, 2, 2, 3, 3>), grid, dim3(256), 0, st, a);
+      if (halo_bf6_on())
+        hipLaunchKernelGGL((conv_halo_kernel<8, 128, 2, 2, 3, 3, true>), grid, dim3(256), 0, st, a);
+      else
+        hipLaunchKernelGGL((conv_halo_kernel<8, 128, 2, 2, 3, 3>), grid, dim3(256), 0, st, a);
       break;
     case TILE_H8x64:
-      hipLaunchKernelGGL((conv_halo_kernel<8, 64, 2, 2, 3, 3>), grid, dim3(256), 0, st, a);
+      if (halo_bf6_on())
+        hipLaunchKernelGGL((conv_halo_kernel<8, 64, 2, 2, 3, 3, true>), grid, dim3(256), 0, st, a);
+      else
+        hipLaunchKernelGGL((conv_halo_kernel<8, 64, 2, 2, 3, 3>), grid, dim3(256), 0, st, a);
       break;
     case TILE_H16x128:
       hipLaunchKernelGGL((conv_halo_kernel<16, 128, 4, 2, 3, 3>), grid, dim3(512), 0, st, a);
