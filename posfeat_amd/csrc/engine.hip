@@ -109,6 +109,12 @@ struct posfeat_model {
   // (raw conv1 output, the materialised conv2 input `hcat`, per-layer IN stats)
   bool train = false;
   Buf dy3, dc2, dhcat, upt, dc1, wt2, wgws, inbws, tailws;
+  // ... on the extraction path (POSFEAT_TRAINTAP=0: the materialised conv2
+  // input + direct convs): conv2's upsampled part by the low-res tap GEMM,
+  // its backward as the combine's adjoint D + two GEMMs on the h x w grid,
+  // the image branch through the 32-channel tap image (headgrad.hip)
+  bool traintap = false;
+  Buf Lbuf, gram, x32, tapwT, dwtap, Aimg, imgbrws;
   Buf st_mean, st_rstd, st_part;  // instance-norm scratch (floats / doubles)
   Buf st_mean1, st_rstd1;
   Buf splitk;                      // split-K partial slabs (max over layers)
@@ -506,6 +512,24 @@ posfeat_conv_desc dgrad_desc(const posfeat_model* m) {
   return d;
 }
 
+// dL/dL-map of head.conv2's upsampled part: D (1152 ch) x WtT^T -> 192 ch, 1x1
+posfeat_conv_desc dl_desc(const posfeat_model* m) {
+  posfeat_conv_desc d;
+  d.n = m->B;
+  d.h = m->H / 4;
+  d.w = m->W / 4;
+  d.cin = 9 * 128;
+  d.x_cstride = 9 * 128;
+  d.cout = 192;
+  d.kh = d.kw = 1;
+  d.stride = 1;
+  d.pad = 0;
+  d.y_cstride = 192;
+  d.res_cstride = 0;
+  d.act = POSFEAT_ACT_NONE;
+  return d;
+}
+
 void plan(posfeat_model* m) {
   size_t cur = 0;
   auto alloc = [&](Buf& b, size_t floats, size_t elem = 4) {
@@ -548,12 +572,15 @@ void plan(posfeat_model* m) {
     m->up4tap = !(tv && tv[0] == '0') && H % 16 == 0 && W % 16 == 0;
     const char* iv = getenv("POSFEAT_IMGSTATS");  // 0: convimg conv + fused statistics
     m->imgstats = !(iv && iv[0] == '0');
+    const char* tt = getenv("POSFEAT_TRAINTAP");  // 0: training on the materialised conv2 input
+    m->traintap = m->train && !(tt && tt[0] == '0') && m->up4 && m->gfuse && m->up4tap;
   }
   if (m->up4 && m->gfuse) {
     alloc(m->gf_w, B * 128 * 128);
     alloc(m->gf_b, B * 128 + 9 * 64 * 128);  // + the transposed W2 G slice (gfuse.hip)
   }
-  if (!(m->up4 && m->gfuse) || m->train) m->imgstats = false;
+  if (!(m->up4 && m->gfuse) || (m->train && !m->traintap)) m->imgstats = false;
+  if (m->traintap) m->imgstats = true;  // the backward contracts the image moments
   if (m->imgstats) alloc(m->imws, pf_gfuse_imgstats_ws_bytes((int)B, (int)H) / 4 + 4);
   m->bf6p = pf_bf6p_on();  // fixed for the instance: buffer sizes depend on it
   {
@@ -573,7 +600,7 @@ void plan(posfeat_model* m) {
     alloc(m->wino_u, uf);
     alloc(m->wino_ws, wb / 4 + 4);
   }
-  if (m->train) m->up4 = false;  // the backward reads the materialised conv2 input
+  if (m->train && !m->traintap) m->up4 = false;  // the backward reads the materialised conv2 input
   {
     const char* e = getenv("POSFEAT_SIDE");
     m->side = !(e && e[0] == '0') && m->up4 && m->gfuse && !m->train;
@@ -608,13 +635,25 @@ void plan(posfeat_model* m) {
   if (m->train) {
     alloc(m->dy3, B * H * W);
     alloc(m->dc2, B * H * W * 128);
-    alloc(m->dhcat, B * H * W * 256);
-    alloc(m->upt, B * H * w4 * 192);
     alloc(m->dc1, B * h4 * w4 * 192);
-    alloc(m->wt2, (size_t)256 * posfeat_conv_packed_k(128, 3, 3));
-    size_t wg = pf_conv_wgrad_ws_bytes((int)B, (int)H, (int)W, 256, 128, 3, 3, 1);
-    wg = std::max(wg, pf_conv_wgrad_ws_bytes((int)B, (int)H, (int)W, 4, 64, 3, 3, 1));
-    wg = std::max(wg, pf_conv_wgrad_ws_bytes((int)B, (int)h4, (int)w4, 192, 192, 3, 3, 1));
+    size_t wg = pf_conv_wgrad_ws_bytes((int)B, (int)h4, (int)w4, 192, 192, 3, 3, 1);
+    if (m->traintap) {
+      alloc(m->Lbuf, B * h4 * w4 * 192);
+      alloc(m->gram, B * 32 * 32, sizeof(double));
+      alloc(m->x32, B * H * W * 32);
+      alloc(m->tapwT, pf_up4tap_weights_floats());
+      alloc(m->dwtap, pf_up4tap_weights_floats());
+      alloc(m->Aimg, B * 128 * 288);
+      alloc(m->imgbrws, pf_imgbr_grad_ws_bytes((int)B) / 4 + 4);
+      wg = std::max(wg, pf_conv_wgrad_ws_bytes((int)B, (int)h4, (int)w4, 192, 9 * 128, 1, 1, 1));
+      wg = std::max(wg, pf_conv_wgrad_per_image_ws_bytes((int)B, (int)H, (int)W, 32, 128));
+    } else {
+      alloc(m->dhcat, B * H * W * 256);
+      alloc(m->upt, B * H * w4 * 192);
+      alloc(m->wt2, (size_t)256 * posfeat_conv_packed_k(128, 3, 3));
+      wg = std::max(wg, pf_conv_wgrad_ws_bytes((int)B, (int)H, (int)W, 256, 128, 3, 3, 1));
+      wg = std::max(wg, pf_conv_wgrad_ws_bytes((int)B, (int)H, (int)W, 4, 64, 3, 3, 1));
+    }
     alloc(m->wgws, wg / 4 + 4);
     const size_t ib = std::max(pf_in_bwd_ws_bytes((int)B, (int)(H * W), 64),
                                pf_in_bwd_ws_bytes((int)B, (int)(h4 * w4), 192));
@@ -634,7 +673,7 @@ void plan(posfeat_model* m) {
     forward(c, reinterpret_cast<const float*>(16), &o);
   }
   if (m->train) {
-    const posfeat_conv_desc d = dgrad_desc(m);
+    const posfeat_conv_desc d = m->traintap ? dl_desc(m) : dgrad_desc(m);
     m->splitk_need = std::max(m->splitk_need, posfeat_conv2d_workspace(&d));
   }
   alloc(m->splitk, m->splitk_need / 4 + 4);
@@ -870,14 +909,24 @@ int head_forward(Ctx& c, float* img4, float* local_point, bool side) {
   }
   if (m->up4) {
     // L = PReLU(IN(conv1)) stays at 1/4 resolution; conv2 reads it per phase
+    // (training keeps the raw conv1 output for the backward: L in its own buffer)
+    float* L = m->traintap ? c.f(m->Lbuf) : c1;
+    if (m->traintap)
+      PF_TRY(timed(c, "train:keep_c1", 0, [&] {
+        return hipMemcpyAsync(L, c1, (size_t)B * h4 * w4 * 192 * sizeof(float),
+                              hipMemcpyDeviceToDevice, c.st) == hipSuccess
+                   ? POSFEAT_OK
+                   : POSFEAT_E_HIP;
+      }));
     PF_TRY(timed(c, "norm_prelu", 0, [&] {
-      return pf_in_apply(c1, B, h4 * w4, 192, 192, mean1, rstd1, slope, c.st);
+      return pf_in_apply(L, B, h4 * w4, 192, 192, mean1, rstd1, slope, c.st);
     }));
     float* g64 = m->imgstats ? nullptr : c.f(m->g64);
     if (!side && m->imgstats)
       PF_TRY(timed(c, "head.convimg.stats", 0, [&] {
         return pf_gfuse_imgstats(img4, B, H, W, c.W("head.convimg"), c.Bi("head.convimg"), meanI,
-                                 rstdI, c.f(m->imws), m->imws.floats * sizeof(float), c.st);
+                                 rstdI, c.f(m->imws), m->imws.floats * sizeof(float), c.st,
+                                 m->traintap ? c.d(m->gram) : nullptr);
       }));
     else if (!side)
       PF_TRY(conv_in(c, "head.convimg", img4, B, H, W, 4, g64, 64, meanI, rstdI));
@@ -942,14 +991,14 @@ int head_forward(Ctx& c, float* img4, float* local_point, bool side) {
         const long long M = (long long)B * h4 * w4;
         unsigned short* Lb = reinterpret_cast<unsigned short*>(c.f(m->tapLb));
         PF_TRY(timed(c, "head.conv2.split", 0,
-                     [&] { return pf_split3_rows(c1, M, 192, 192, Lb, c.st); }));
+                     [&] { return pf_split3_rows(L, M, 192, 192, Lb, c.st); }));
         PF_TRY(timed(c, "conv:head.conv2.up4tap", 2.0 * M * 1152.0 * 192, [&] {
           return pf_gemm_bf6p(Lb, 192, M * 192, 0,
                               reinterpret_cast<const unsigned short*>(c.f(m->tapwb)), 192,
                               1152LL * 192, 0, c.f(m->tapP), 1152, 0, 1, (int)M, 1152, 192, c.st);
         }));
       } else {
-        PF_TRY(conv_desc_run(c, "head.conv2.up4tap", d, c1, c.f(m->tapw), nullptr, nullptr,
+        PF_TRY(conv_desc_run(c, "head.conv2.up4tap", d, L, c.f(m->tapw), nullptr, nullptr,
                              c.f(m->tapP), 2.0 * B * h4 * w4 * 1152.0 * 192,
                              m->wsplit ? reinterpret_cast<const unsigned short*>(c.f(m->tapwb))
                                        : nullptr,
@@ -1012,6 +1061,71 @@ int head_forward(Ctx& c, float* img4, float* local_point, bool side) {
 const Spec& spec(const char* n) { return *specs().find(n); }
 long long head_offset() { return spec("head.conv1").w_off; }
 
+// The rest of the KeypointDet backward on the extraction path's factorisation
+// of head.conv2 (traintap), from dc2 = dL/d(conv2 out):
+//   upsampled part: y += sum_k shift_k(up4(P_k)), P_k = W_k[:, :192] L, so
+//     D = dL/dP (the combine's adjoint, up4tap.hip), dW_k = D_k^T L and
+//     dL = sum_k D_k W_k -- two GEMMs on the h x w grid (1/16 of the full-res
+//     weight / input gradients' MACs);
+//   image part + convimg: contractions of the per-image 3x3 weight gradient
+//     of dc2 against the 32-channel tap image (headgrad.hip) -- no G map;
+//   conv1: IN/PReLU backward + weight gradient as before.
+int head_backward_tap(Ctx& c, float* grad, double* t2s, int t2n) {
+  posfeat_model* m = c.m;
+  const int B = m->B, H = m->H, W = m->W, h4 = H / 4, w4 = W / 4;
+  const long long hoff = head_offset();
+  auto G = [&](const char* n) { return grad + (spec(n).w_off - hoff); };
+  auto GB = [&](const char* n) { return grad + (spec(n).b_off - hoff); };
+  const float* slope = m->wts + spec("head.prelu").b_off;
+  const size_t SL = (size_t)B * 256;
+  const float* mean1 = c.f(m->st_mean);
+  const float* rstd1 = c.f(m->st_rstd);
+  float* dc1 = c.f(m->dc1);
+  float* dc2 = c.f(m->dc2);
+  float* D = c.f(m->tapP);  // P is dead after the forward
+  const size_t wgb = m->wgws.floats * sizeof(float);
+  PF_TRY(timed(c, "bwd:up4tap_adjoint", 0,
+               [&] { return pf_up4tap_adjoint(B, H, W, dc2, 128, D, c.st); }));
+  PF_TRY(timed(c, "bwd:tapw_t", 0,
+               [&] { return pf_up4tap_weights_t(c.W("head.conv2"), c.f(m->tapwT), c.st); }));
+  PF_TRY(timed(c, "bwdconv:head.conv2.tap_wgrad", 2.0 * B * h4 * w4 * 1152.0 * 192, [&] {
+    return pf_conv_wgrad(D, 1152, c.f(m->Lbuf), 192, B, h4, w4, 192, 1152, 1, 1, 1, c.f(m->dwtap),
+                         nullptr, 0, c.f(m->wgws), wgb, c.st);
+  }));
+  {
+    const posfeat_conv_desc d = dl_desc(m);
+    PF_TRY(conv_desc_run(c, "bwd.head.conv2.tap_dgrad", d, D, c.f(m->tapwT), nullptr, nullptr, dc1,
+                         2.0 * B * h4 * w4 * 1152.0 * 192));
+  }
+  PF_TRY(timed(c, "bwd:img_taps", 0,
+               [&] { return pf_img_taps32(c.f(m->img4), B, H, W, c.f(m->x32), c.st); }));
+  PF_TRY(timed(c, "bwdconv:head.imgbranch.wgrad", 2.0 * B * H * W * 128.0 * 288, [&] {
+    return pf_conv_wgrad_per_image(dc2, 128, c.f(m->x32), 32, B, H, W, 32, 128, c.f(m->Aimg),
+                                   c.f(m->wgws), wgb, c.st);
+  }));
+  PF_TRY(timed(c, "bwd:imgbranch_grads", 0, [&] {
+    return pf_imgbr_grad(c.f(m->Aimg), B, H * W, c.W("head.conv2"), c.W("head.convimg"),
+                         c.Bi("head.convimg"), c.f(m->st_mean) + SL, c.f(m->st_rstd) + SL,
+                         c.d(m->gram), c.f(m->dwtap), G("head.conv2"), GB("head.conv2"),
+                         G("head.convimg"), GB("head.convimg"), c.f(m->imgbrws),
+                         m->imgbrws.floats * sizeof(float), c.st);
+  }));
+  double* c1s = nullptr;
+  int c1n = 0;
+  PF_TRY(timed(c, "bwd:in_conv1", 0, [&] {
+    return pf_in_backward(c.f(m->c1raw), 192, dc1, 192, B, h4 * w4, 192, mean1, rstd1, slope, dc1,
+                          192, c.f(m->inbws), &c1s, &c1n, c.st);
+  }));
+  PF_TRY(timed(c, "bwdconv:head.conv1.wgrad", 2.0 * B * h4 * w4 * 192.0 * 192 * 9, [&] {
+    return pf_conv_wgrad(dc1, 192, c.f(m->headcat), 192, B, h4, w4, 192, 192, 3, 3, 1,
+                         G("head.conv1"), GB("head.conv1"), 0, c.f(m->wgws), wgb, c.st);
+  }));
+  PF_TRY(timed(c, "bwd:scalars", 0, [&] {
+    return pf_head_scalars(t2s, t2n, c1s, c1n, GB("head.conv3"), GB("head.prelu"), c.st);
+  }));
+  return POSFEAT_OK;
+}
+
 // KeypointDet backward (networks/DeteNet.py:102-121 under autograd, as
 // managers/trainer.py:331 runs it for configs/train_kp.yaml): given dL/d
 // local_point of the last forward on this workspace, writes dL/d(every head
@@ -1046,6 +1160,7 @@ int head_backward(Ctx& c, const float* dlp, float* grad) {
                             128, mean2, rstd2, slope, c.W("head.conv3"), B, H * W, c.f(m->dy3),
                             dc2, 128, G("head.conv3"), c.f(m->tailws), &t2s, &t2n, c.st);
   }));
+  if (m->traintap) return head_backward_tap(c, grad, t2s, t2n);
   // conv2: weight gradient over the materialised cat[up4(L), IN(convimg)]
   PF_TRY(timed(c, "bwdconv:head.conv2.wgrad", 2.0 * B * H * W * 128.0 * 256 * 9, [&] {
     return pf_conv_wgrad(dc2, 128, hcat, 256, B, H, W, 256, 128, 3, 3, 1, G("head.conv2"),

@@ -83,7 +83,7 @@ int pf_gfuse_conv(const float* img4, const float* c, int ccs, int n, int H, int 
 size_t pf_gfuse_imgstats_ws_bytes(int n, int H);
 int pf_gfuse_imgstats(const float* img4, int n, int H, int W, const float* w1_packed,
                       const float* b1, float* mean, float* rstd, void* ws, size_t ws_bytes,
-                      hipStream_t st);
+                      hipStream_t st, double* gram = nullptr);
 size_t pf_wino_wgrad_ws_bytes(int n, int h, int w, int Cin, int Cout);
 int pf_wino_wgrad(const float* dy, int ldy, const float* x, int xcs, int n, int h, int w, int Cin,
                   int Cout, float* dw, float* db, int acc, void* ws, size_t ws_bytes,
@@ -103,6 +103,27 @@ size_t pf_up4tap_part_bytes(int n, int H, int W);
 int pf_up4tap_weights(const float* w2_packed, float* wt, hipStream_t st);
 int pf_up4tap_combine(int n, int H, int W, const float* P, float* y, int ycs, double* part,
                       float* mean, float* rstd, hipStream_t st);
+// training: D = the combine's adjoint of dy (dL/dP), and the transposed tap
+// weights WtT [192][1152] (dL = D . WtT^T)
+int pf_up4tap_adjoint(int n, int H, int W, const float* dy, int dycs, float* D, hipStream_t st);
+int pf_up4tap_weights_t(const float* w2_packed, float* wt, hipStream_t st);
+// keypoint-head training, the image branch (headgrad.hip): X32[p] = the 27
+// zero-padded 3x3 image taps of p (gfuse's moment order), 1, 0 x 4
+int pf_img_taps32(const float* img4, int n, int H, int W, float* x32, hipStream_t st);
+// per image z: A[z][co][t*32 + j] = the 3x3 weight gradient of dy against X32
+// over image z alone (halo wgrad, image-aligned splits)
+size_t pf_conv_wgrad_per_image_ws_bytes(int n, int H, int W, int Cin, int Cout);
+int pf_conv_wgrad_per_image(const float* dy, int ldy, const float* x, int xcs, int n, int H, int W,
+                            int Cin, int Cout, float* dw, void* ws, size_t ws_bytes,
+                            hipStream_t st);
+// gradients of head.conv2's image slice, convimg's weights and bias, and
+// conv2's bias from A, the convimg IN statistics and the image moments, plus
+// the tap-weight gradient dWtap [1152][192] -> the packed head gradient
+size_t pf_imgbr_grad_ws_bytes(int n);
+int pf_imgbr_grad(const float* A, int n, int HW, const float* w2p, const float* w1p,
+                  const float* b1, const float* meanI, const float* rstdI, const double* gram,
+                  const float* dwtap, float* g_w2, float* g_b2, float* g_w1, float* g_b1, void* ws,
+                  size_t ws_bytes, hipStream_t st);
 
 // conv product arithmetic: 0 fp32 MFMA, 1 bf16x6, 2 bf16x6 + pre-split GEMMs
 int pf_conv_precision();

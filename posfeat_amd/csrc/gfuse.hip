@@ -237,7 +237,8 @@ __global__ __launch_bounds__(1024) void gfuse_imgstats_kernel(const double* __re
                                                              const float* __restrict__ w1,
                                                              int k1pad, const float* __restrict__ b1,
                                                              float eps, float* __restrict__ mean,
-                                                             float* __restrict__ rstd) {
+                                                             float* __restrict__ rstd,
+                                                             double* __restrict__ gram) {
   __shared__ double G[IM_G * IM_G];
   const int b = blockIdx.x;
   {
@@ -253,6 +254,7 @@ __global__ __launch_bounds__(1024) void gfuse_imgstats_kernel(const double* __re
     }
     for (; k < nband; ++k) s0 += pe[k * IM_G * IM_G];
     G[e] = ((s0 + s1) + (s2 + s3)) / HW;  // E[x_i x_j], row 27: E[x_j]
+    if (gram) gram[(long long)b * IM_G * IM_G + e] = G[e];  // kept for the training backward
   }
   __syncthreads();
   const int k = threadIdx.x;
@@ -525,7 +527,7 @@ size_t pf_gfuse_imgstats_ws_bytes(int n, int H) {
 // convimg's instance-norm mean / rstd [n][64] from the image moments (no conv)
 int pf_gfuse_imgstats(const float* img4, int n, int H, int W, const float* w1_packed,
                       const float* b1, float* mean, float* rstd, void* ws, size_t ws_bytes,
-                      hipStream_t st) {
+                      hipStream_t st, double* gram) {
   if (!ws || ws_bytes < pf_gfuse_imgstats_ws_bytes(n, H)) return POSFEAT_E_WORKSPACE;
   const int nband = (H + IM_ROWS - 1) / IM_ROWS;
   const size_t lds = std::max((size_t)(IM_ROWS + 2) * (W + 2) * 3 * sizeof(float),
@@ -535,7 +537,7 @@ int pf_gfuse_imgstats(const float* img4, int n, int H, int W, const float* w1_pa
   hipLaunchKernelGGL(gfuse_imgmom_kernel, dim3(nband, n), dim3(256), lds, st, img4, H, W, part);
   PF_CHECK_LAUNCH();
   hipLaunchKernelGGL(gfuse_imgstats_kernel, dim3(n), dim3(IM_G * IM_G), 0, st, part, nband, H * W,
-                     w1_packed, posfeat_conv_packed_k(3, 3, 3), b1, 1e-5f, mean, rstd);
+                     w1_packed, posfeat_conv_packed_k(3, 3, 3), b1, 1e-5f, mean, rstd, gram);
   PF_CHECK_LAUNCH();
   return POSFEAT_OK;
 }

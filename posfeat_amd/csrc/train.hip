@@ -919,6 +919,83 @@ int pf_conv_wgrad(const float* dy, int ldy, const float* x, int xcs, int n, int 
   return POSFEAT_OK;
 }
 
+// Per-image weight gradient of a 3x3 stride-1 conv (halo kernel): with
+// nsplit = n * k the pixel-range splits never straddle an image (split
+// z*k + j covers rows of image z only), so summing splits z*k .. z*k+k-1 in
+// order gives image z's gradient alone.  Used by the keypoint-head backward,
+// whose image-branch gradients contract per-image statistics.
+namespace {
+int per_image_k(int n, int H, int W, int Cin, int Cout) {
+  const WgPlan p = wgrad_plan(n, H, W, Cin, Cout, 3, 3, 1);
+  const int per_img = H * ((W + 31) / 32);
+  const int k = (1024 + n * p.ntiles - 1) / (n * p.ntiles);
+  return std::max(1, std::min(std::min(k, per_img / 8), 128));
+}
+__global__ void wgrad_reduce_images_kernel(const float* __restrict__ part, int k, long long per,
+                                           int n, float* __restrict__ dw) {
+  const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (i >= per * n) return;
+  const long long z = i / per, e = i - z * per;
+  const float* p = part + z * k * per + e;
+  float s = 0.f;
+  for (int j = 0; j < k; ++j) s += p[j * per];
+  dw[i] = s;
+}
+}  // namespace
+
+size_t pf_conv_wgrad_per_image_ws_bytes(int n, int H, int W, int Cin, int Cout) {
+  const int k = per_image_k(n, H, W, Cin, Cout);
+  return pf_align((size_t)n * k * Cout * posfeat_conv_packed_k(Cin, 3, 3) * 4, 256);
+}
+
+int pf_conv_wgrad_per_image(const float* dy, int ldy, const float* x, int xcs, int n, int H, int W,
+                            int Cin, int Cout, float* dw, void* ws, size_t ws_bytes,
+                            hipStream_t st) {
+  if (Cin % 32 || Cout % 32 || ldy % 4 || xcs % 4 || n <= 0) return POSFEAT_E_INVALID;
+  if (reinterpret_cast<uintptr_t>(dy) % 16 || reinterpret_cast<uintptr_t>(x) % 16)
+    return POSFEAT_E_INVALID;
+  if (ws_bytes < pf_conv_wgrad_per_image_ws_bytes(n, H, W, Cin, Cout)) return POSFEAT_E_WORKSPACE;
+  const WgPlan p = wgrad_plan(n, H, W, Cin, Cout, 3, 3, 1);
+  const int k = per_image_k(n, H, W, Cin, Cout);
+  WgradArgs a;
+  a.dy = dy;
+  a.ldy = ldy;
+  a.x = x;
+  a.xcs = xcs;
+  a.H = a.Hin = H;
+  a.W = a.Win = W;
+  a.stride = 1;
+  a.d_row = a.d_img = 0;
+  a.Cin = Cin;
+  a.KH = a.KW = 3;
+  a.pad = 1;
+  a.Cout = Cout;
+  a.Kpad = p.Kpad;
+  a.K = p.K;
+  a.M = n * H * W;
+  a.tiles_n = p.tiles_n;
+  a.ntiles = p.ntiles;
+  a.nsplit = n * k;
+  a.nchunks = p.nchunks;
+  a.bdy = a.bx = a.bpart = 0;
+  a.zb = 0;
+  a.part = static_cast<float*>(ws);
+  a.partb = nullptr;
+  const dim3 grid(a.ntiles * a.nsplit);
+  if (p.BM == 192)
+    hipLaunchKernelGGL(conv_wgrad_halo_kernel<6>, grid, dim3(384), 0, st, a);
+  else if (p.BM == 128)
+    hipLaunchKernelGGL(conv_wgrad_halo_kernel<4>, grid, dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL(conv_wgrad_halo_kernel<2>, grid, dim3(128), 0, st, a);
+  PF_CHECK_LAUNCH();
+  const long long per = (long long)Cout * p.Kpad;
+  hipLaunchKernelGGL(wgrad_reduce_images_kernel, dim3((unsigned)((per * n + 255) / 256)), dim3(256),
+                     0, st, a.part, k, per, n, dw);
+  PF_CHECK_LAUNCH();
+  return POSFEAT_OK;
+}
+
 // part[z][s] [Cout][Cin] = sum_{m in split s} dy[z][m][co] x[z][m][ci], z < nb,
 // in ONE launch (blockIdx.y = z): the Winograd weight gradient's 36
 // transform-domain GEMMs (wino.hip), whose output transform sums the nsplit

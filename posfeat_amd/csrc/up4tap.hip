@@ -211,6 +211,105 @@ __global__ __launch_bounds__(256) void up4tap_combine_kernel(const float* __rest
   }
 }
 
+// ---- adjoint (keypoint-head training, config 5) ------------------------------
+// weight with which low-res index i feeds full-res coordinate u of an n -> 4n
+// bilinear upsample (align_corners=False): u's two clamped source taps
+// (ia, wa), (ib, wb) as in the forward above (a tap clamped onto its partner
+// adds its weight to it, as ATen's weight (1, 0) at the border); 0 outside
+// [0, 4n): the conv's zero padding
+__device__ __forceinline__ float up4_cw(int u, int i, int n) {
+  if (u < 0 || u >= 4 * n) return 0.f;
+  int lo;
+  float wa, wb;
+  up4_w(u & 3, lo, wa, wb);
+  const int q = u >> 2;
+  const int ia = min(max(q + lo, 0), n - 1), ib = min(max(q + lo + 1, 0), n - 1);
+  return (ia == i ? wa : 0.f) + (ib == i ? wb : 0.f);
+}
+
+// D[b][iy][ix][k * 128 + co] = dL/dP_k = sum over the full-res output pixels
+// (Y, X) of cw(v, iy) cw(u, ix) dy[b][Y][X][co], v = Y + ky - 1, u = X + kx - 1:
+// the adjoint of the combine's tap-summed interpolation.  Thread = (low-res
+// column ix, channel quad); block = 8 columns x 32 quads of one image over TQ
+// low-res rows.  Separable: per dy row Y the x-adjoint
+// E_kx = sum_u cw(u, ix) dy[Y][u - kx + 1] (10 float4 loads, 24 FMAs), then
+// each E_kx goes to the (iy, ky) accumulators whose v = Y + ky - 1 lies in iy's
+// support [4 iy - 2, 4 iy + 5] (which pairs those are is fixed at compile time;
+// the weight itself clamps at the borders).
+template <int TQ>
+__global__ __launch_bounds__(256) void up4tap_adjoint_kernel(const float* __restrict__ dy, int dycs,
+                                                             int h, int w, float* __restrict__ D) {
+  const int H = 4 * h, W = 4 * w;
+  const int tid = threadIdx.x, cq = tid & 31, xl = tid >> 5;
+  const int nxb = (w + 7) / 8, nqb = (h + TQ - 1) / TQ;
+  int id = blockIdx.x;
+  const int xb = id % nxb;
+  id /= nxb;
+  const int qb = id % nqb, b = id / nqb;
+  const int ix = xb * 8 + xl, q0 = qb * TQ;
+  const bool active = ix < w;
+  float wx[8];  // u = 4 ix - 2 + j
+#pragma unroll
+  for (int j = 0; j < 8; ++j) wx[j] = active ? up4_cw(4 * ix - 2 + j, ix, w) : 0.f;
+  f32x4 acc[TQ][9];
+#pragma unroll
+  for (int t = 0; t < TQ; ++t)
+#pragma unroll
+    for (int k = 0; k < 9; ++k) acc[t][k] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const float* dyb = dy + (long long)b * H * W * dycs + cq * 4;
+  const int Y0 = 4 * q0 - 3;
+#pragma unroll
+  for (int ry = 0; ry < 4 * TQ + 6; ++ry) {
+    const int Y = Y0 + ry;
+    if (Y < 0 || Y >= H) continue;
+    f32x4 d[10];  // X = 4 ix - 3 + j
+#pragma unroll
+    for (int j = 0; j < 10; ++j) {
+      const int X = 4 * ix - 3 + j;
+      d[j] = active && X >= 0 && X < W
+                 ? *reinterpret_cast<const f32x4*>(dyb + ((long long)Y * W + X) * dycs)
+                 : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    f32x4 E[3];
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      f32x4 s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += wx[j] * d[j + 2 - kx];
+      E[kx] = s;
+    }
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      const int rv = ry + ky - 4;  // v - 4 q0
+#pragma unroll
+      for (int t = 0; t < TQ; ++t) {
+        if (rv < 4 * t - 2 || rv > 4 * t + 5) continue;
+        const float cy = up4_cw(Y + ky - 1, q0 + t, h);
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) acc[t][ky * 3 + kx] += cy * E[kx];
+      }
+    }
+  }
+  if (!active) return;
+#pragma unroll
+  for (int t = 0; t < TQ; ++t) {
+    const int iy = q0 + t;
+    if (iy >= h) break;
+    float* o = D + (((long long)b * h + iy) * w + ix) * TAP_N + cq * 4;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) *reinterpret_cast<f32x4*>(o + k * TAP_CO) = acc[t][k];
+  }
+}
+
+// WtT[ci][k * 128 + co] = W2[co][ci][ky][kx], ci < 192: dL = D . WtT^T
+__global__ void up4tap_weights_t_kernel(const float* __restrict__ w2p, float* __restrict__ wt) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= TAP_N * TAP_CU) return;
+  const int ci = i / TAP_N, o = i - ci * TAP_N;
+  const int k = o / TAP_CO, co = o - k * TAP_CO;
+  wt[i] = w2p[(long long)co * TAP_KP2 + (ci >> 5) * 288 + k * 32 + (ci & 31)];
+}
+
 }  // namespace
 
 size_t pf_up4tap_weights_floats() { return (size_t)TAP_N * TAP_CU; }
@@ -239,5 +338,25 @@ int pf_up4tap_combine(int n, int H, int W, const float* P, float* y, int ycs, do
                      P, h, w, y, ycs, mean ? part : nullptr);
   PF_CHECK_LAUNCH();
   if (mean) PF_TRY(pf_in_finalize(part, n, nchunk, H * W, TAP_CO, mean, rstd, st));
+  return POSFEAT_OK;
+}
+
+// D (n x H/4 x W/4 x 1152) = the adjoint of pf_up4tap_combine applied to dy
+// (n x H x W x 128, pitch dycs): dL/dP.  H, W % 16 == 0.
+int pf_up4tap_adjoint(int n, int H, int W, const float* dy, int dycs, float* D, hipStream_t st) {
+  const int h = H / 4, w = W / 4;
+  constexpr int TQA = 4;
+  if (H % 16 || W % 16 || dycs % 4 || n <= 0) return POSFEAT_E_INVALID;
+  const long long nb = (long long)n * ((h + TQA - 1) / TQA) * ((w + 7) / 8);
+  hipLaunchKernelGGL(up4tap_adjoint_kernel<TQA>, dim3((unsigned)nb), dim3(256), 0, st, dy, dycs, h,
+                     w, D);
+  PF_CHECK_LAUNCH();
+  return POSFEAT_OK;
+}
+
+int pf_up4tap_weights_t(const float* w2_packed, float* wt, hipStream_t st) {
+  hipLaunchKernelGGL(up4tap_weights_t_kernel, dim3((TAP_N * TAP_CU + 255) / 256), dim3(256), 0, st,
+                     w2_packed, wt);
+  PF_CHECK_LAUNCH();
   return POSFEAT_OK;
 }
