@@ -843,6 +843,7 @@ extern "C" int posfeat_bbtrain_forward(posfeat_bbtrain* m, const float* params, 
       (reinterpret_cast<uintptr_t>(params) & 15) || (reinterpret_cast<uintptr_t>(stats) & 15))
     return POSFEAT_E_INVALID;
   Ctx c{m, static_cast<char*>(act), static_cast<char*>(scratch), pf_stream(stream), params};
+  const PfHaloFp32Scope halo32;  // fp32 halo tiles: the fixture-validated numerics
   PF_TRY(forward(c, img_nchw, stats, momentum));
   if (local_map_nhwc) *local_map_nhwc = c.f(m->fa);
   return POSFEAT_OK;
@@ -858,6 +859,7 @@ extern "C" int posfeat_bbtrain_backward(posfeat_bbtrain* m, const float* params,
     return POSFEAT_E_INVALID;
   Ctx c{m, static_cast<char*>(const_cast<void*>(act)), static_cast<char*>(scratch),
         pf_stream(stream), params};
+  const PfHaloFp32Scope halo32;
   return backward(c, dlocal_map_nhwc, dcs, grad, accumulate ? 1 : 0);
 }
 

@@ -823,6 +823,186 @@ __global__ __launch_bounds__(256) void conv_bf6b_kernel(ConvArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// The same products with A straight to REGISTERS.  With the waves stacked
+// along M each wave is the only reader of its 32 A rows, so A needs no LDS
+// round trip: lane (r, h) global-loads the 8 fp32 it feeds the MFMA (row r,
+// k = 16g + 8h .. +7: two 16-B loads per k16 group) one chunk ahead, into a
+// second register set, while the chunk in hand is split and multiplied.  LDS
+// then holds only the B planes (NST stages of 24 KB at BN = 128): per chunk
+// the DMA moves 24 KB instead of 40 and nothing stages A (measured on the
+// LDS-staged form: its DMA and compute did not overlap -- POSFEAT_ABL
+// ablations, r3c).  Products, their order and the epilogue are those of
+// conv_bf6b_kernel: bit-identical results.
+template <int BM, int BN, int NST>
+__global__ __launch_bounds__(256) void conv_bf6r_kernel(ConvArgs a) {
+  constexpr int WM = 4, WN = 1, NW = 4;
+  constexpr int TM = BM / WM, TN = BN;
+  constexpr int MI = TM / 32, NI = TN / 32;
+  constexpr int B_G = 3 * BN / 16 / NW;  // 16 plane-rows (64 B) per DMA piece
+  static_assert(MI == 1 && B_G >= 1 && (3 * BN / 16) % NW == 0, "tile");
+  static_assert(NST == 2 || NST == 3, "stages");
+  constexpr int BSTAGE = 3 * BN * BK / 2;  // floats (u16 pairs)
+  constexpr int RING = NST * BSTAGE;
+  constexpr int EPI = BM * (BN + 4);
+  __shared__ __attribute__((aligned(16))) float smem[RING > EPI ? RING : EPI];
+  unsigned short* Bs = reinterpret_cast<unsigned short*>(smem);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int bid = blockIdx.x % a.nwg;
+  const int split = blockIdx.x / a.nwg;
+  {
+    const int nwg = a.nwg, q = nwg >> 3, r = nwg & 7, xcd = bid & 7, slot = bid >> 3;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+  }
+  const unsigned short* wb = a.wb;
+  if (a.nbatch > 1) {
+    const long long zb = blockIdx.y;
+    a.x += zb * a.bx;
+    a.y += zb * a.by;
+    wb += zb * a.bwb;
+  }
+  const int tm = bid / a.tiles_n, tn = bid - tm * a.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int r32 = lane & 31, hh = lane >> 5;
+
+  // this lane's A row: base of tap (0,0) + its k offset 8h; taps in the image
+  const float* xrow = a.x;
+  unsigned tapok = 0u;
+  {
+    const int m = m0 + wave * 32 + r32;
+    if (m < a.M) {
+      const int n = m / a.hw;
+      const int rem = m - n * a.hw;
+      const int oh = rem / a.OW;
+      const int ow = rem - oh * a.OW;
+      const int ih0 = oh * a.stride - a.pad, iw0 = ow * a.stride - a.pad;
+      for (int kh = 0; kh < a.KH; ++kh)
+        for (int kw = 0; kw < a.KW; ++kw)
+          if ((unsigned)(ih0 + kh) < (unsigned)a.H && (unsigned)(iw0 + kw) < (unsigned)a.W)
+            tapok |= 1u << (kh * a.KW + kw);
+      xrow = a.x + (long long)n * a.H * a.W * a.xcs + ((long long)ih0 * a.W + iw0) * a.xcs + hh * 8;
+    }
+  }
+  const unsigned short* bsrc[B_G];
+#pragma unroll
+  for (int i = 0; i < B_G; ++i) {
+    const int pr = (wave * B_G + i) * 16 + (lane >> 2);
+    const int plane = pr / BN, row = pr - plane * BN;
+    const int ks = (lane & 3) ^ ((row >> 2) & 3);
+    bsrc[i] = (n0 + row < a.Cout)
+                  ? wb + plane * a.wplane + (long long)(n0 + row) * a.Kpad + ks * 8
+                  : nullptr;
+  }
+  const int ntap = a.KH * a.KW;
+  const int nch_all = a.Kpad / BK;
+  const int ch0 = (int)((long long)nch_all * split / a.ksplit);
+  const int ch1 = (int)((long long)nch_all * (split + 1) / a.ksplit);
+
+  auto issue_b = [&](int c, int buf) {
+#pragma unroll
+    for (int i = 0; i < B_G; ++i) {
+      const void* src = bsrc[i] ? (const void*)(bsrc[i] + (long long)c * BK)
+                                : (const void*)pf_conv_zero16;
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)src,
+          (__attribute__((address_space(3))) void*)(Bs + buf * 2 * BSTAGE +
+                                                     (wave * B_G + i) * 16 * BK),
+          16, 0, 0);
+    }
+  };
+  // the lane's 8 A values of each k16 group of chunk c (zero for taps outside)
+  auto load_a = [&](int c, f32x4 (&v)[4]) {
+    const int slab = c / ntap, tap = c - slab * ntap;
+    const int kh = tap / a.KW, kw = tap - kh * a.KW;
+    const float* p = xrow + ((long long)kh * a.W + kw) * a.xcs + slab * BK;
+    if ((tapok >> tap) & 1u) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        v[j] = *reinterpret_cast<const f32x4*>(p + (j >> 1) * 16 + (j & 1) * 4);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+
+  f32x16 acc[MI][NI];
+#pragma unroll
+  for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[0][ni][r] = 0.f;
+
+  auto compute = [&](int buf, const f32x4 (&v)[4]) {
+    const unsigned short* Bb = Bs + buf * 2 * BSTAGE;
+#pragma unroll
+    for (int g = 0; g < BK / 16; ++g) {
+      u32x4_t ah, am, al;
+      split3(v[2 * g], v[2 * g + 1], ah, am, al);
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) {
+        const int row = ni * 32 + r32;
+        const int slot = (2 * g + hh) ^ ((row >> 2) & 3);
+        const unsigned short* bp = Bb + row * BK + slot * 8;
+        const u32x4_t bh = *reinterpret_cast<const u32x4_t*>(bp);
+        const u32x4_t bm = *reinterpret_cast<const u32x4_t*>(bp + BN * BK);
+        const u32x4_t bl = *reinterpret_cast<const u32x4_t*>(bp + 2 * BN * BK);
+        f32x16 c = acc[0][ni];
+        c = mfma_bf16(ah, bh, c);
+        c = mfma_bf16(ah, bm, c);
+        c = mfma_bf16(am, bh, c);
+        c = mfma_bf16(ah, bl, c);
+        c = mfma_bf16(al, bh, c);
+        c = mfma_bf16(am, bm, c);
+        acc[0][ni] = c;
+      }
+    }
+  };
+
+  // Issue order (vector-memory completions count in order): B(0), A(0),
+  // [B(1)]; per chunk ii: A(ii+1), then B(ii+NST-1).  So at the top of chunk
+  // ii everything but the youngest B (NST = 3) must have landed: A(ii) and
+  // B(ii) are older than it.
+  const int nch = ch1 - ch0;
+  f32x4 va[4], vb[4];
+  if (nch > 0) {
+    issue_b(ch0, 0);
+    load_a(ch0, va);
+    if (NST == 3 && nch > 1) issue_b(ch0 + 1, 1);
+  }
+  int slot = 0;
+  for (int i = 0; i < nch; i += 2) {
+    // two chunks per trip so the A register sets alternate without copies
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int ii = i + u;
+      if (ii >= nch) break;
+      if (NST == 3 && ii + 1 < nch)
+        wait_vmcnt<B_G>();
+      else
+        wait_vmcnt<0>();
+      // every wave: chunk ii landed, and chunk ii-1's slot (refilled below) consumed
+      __builtin_amdgcn_s_barrier();
+      if (u == 0) {
+        if (ii + 1 < nch) load_a(ch0 + ii + 1, vb);
+      } else {
+        if (ii + 1 < nch) load_a(ch0 + ii + 1, va);
+      }
+      if (ii + NST - 1 < nch) issue_b(ch0 + ii + NST - 1, slot == 0 ? NST - 1 : slot - 1);
+      if (u == 0)
+        compute(slot, va);
+      else
+        compute(slot, vb);
+      slot = slot == NST - 1 ? 0 : slot + 1;
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  conv_epilogue<BM, BN, WM, WN>(
+      a, acc, smem, tm, n0, split, [&](int row) { return m0 + row < a.M ? m0 + row : -1; },
+      m0 / a.hw,
+      [&](int, int m) { return a.res ? a.res + (size_t)m * a.rcs : (const float*)nullptr; });
+}
+
+// ---------------------------------------------------------------------------
 // Spatial-halo variant for stride-1 convs with Cin % 32 == 0 (every 3x3
 // decoder/head layer).  The M tile is a PH x 16 patch of output pixels of one
 // image; for each 32-channel slab its (PH+KH-1) x (16+KW-1) input halo is
@@ -1470,7 +1650,8 @@ enum ConvTile {
   TILE_128x128 = 0, TILE_128x64 = 1, TILE_64x64 = 2, TILE_256x128 = 3,  // contiguous rows
   TILE_H8x128 = 10, TILE_H8x64 = 11, TILE_H16x128 = 12,                 // 8/16 x 16 patches
   TILE_BF6_128x128 = 20, TILE_BF6_128x256 = 21, TILE_BF6_64x128 = 22,   // rows, bf16x6 products
-  TILE_BF6_128x64 = 23, TILE_BF6B_128x128 = 24, TILE_BF6B_128x64 = 25  // + pre-split weights
+  TILE_BF6_128x64 = 23, TILE_BF6B_128x128 = 24, TILE_BF6B_128x64 = 25,  // + pre-split weights
+  TILE_BF6R_128x128 = 26, TILE_BF6R_128x64 = 27  // + A straight to registers
 };
 
 // POSFEAT_BF6=1: every conv the row-tile DMA kernel serves (1x1, strided, the
@@ -1479,13 +1660,17 @@ enum ConvTile {
 // set of a conv is then either all-bf16x6 or all-fp32, so the autotuner's
 // choice never changes results.
 bool bf6_on() { return pf_conv_precision() >= 1; }
-// the 3x3 stride-1 halo kernel in bf16x6 too (POSFEAT_BF6_HALO=0: fp32 MFMA)
+// the 3x3 stride-1 halo kernel in bf16x6 too (POSFEAT_BF6_HALO=0: fp32 MFMA);
+// PfHaloFp32Scope keeps the calling thread's launches on fp32 halo tiles (the
+// train-mode backbone, whose fp64-pinned gradient fixtures were validated on
+// them, bbtrain.hip)
+thread_local int tl_halo_fp32 = 0;
 bool halo_bf6_on() {
   static const bool off = [] {
     const char* e = getenv("POSFEAT_BF6_HALO");
     return e && e[0] == '0';
   }();
-  return bf6_on() && !off;
+  return bf6_on() && !off && tl_halo_fp32 == 0;
 }
 // LDS stages of the bf16x6 row tiles (POSFEAT_BF6_NST: 2, 3 or 4)
 int bf6_nst() {
@@ -1493,6 +1678,25 @@ int bf6_nst() {
     const char* e = getenv("POSFEAT_BF6_NST");
     const int v = e ? atoi(e) : 2;
     return v == 3 || v == 4 ? v : 2;
+  }();
+  return n;
+}
+// pre-split-weight tiles with A straight to registers (POSFEAT_BF6R=1; A/B
+// only: measured r3j on the decoder's Winograd GEMMs 0.597 ms (2 B stages) /
+// 0.589 ms (3) against 0.564 ms for the LDS-staged conv_bf6b_kernel -- the
+// per-lane 32-B row pieces load worse than the 128-B DMA rows);
+// POSFEAT_BF6R_NST: B stages (2 or 3)
+bool bf6r_on() {
+  static const bool on = [] {
+    const char* e = getenv("POSFEAT_BF6R");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+int bf6r_nst() {
+  static const int n = [] {
+    const char* e = getenv("POSFEAT_BF6R_NST");
+    return e && e[0] == '3' ? 3 : 2;
   }();
   return n;
 }
@@ -1553,16 +1757,18 @@ Plan plan_for_tile(const ConvArgs& a, int tile) {
   // bf16x6 mode: halo-eligible convs keep fp32 halo tiles only, the rest
   // bf16x6 row tiles only
   if (bf6_on() && glds_ok) {
-    const bool bf6_tile = tile >= TILE_BF6_128x128 && tile <= TILE_BF6B_128x64;
+    const bool bf6_tile = tile >= TILE_BF6_128x128 && tile <= TILE_BF6R_128x64;
     if (halo_ok ? bf6_tile || tile < TILE_H8x128 : !bf6_tile) return p;
   }
   switch (tile) {
     case TILE_BF6B_128x128:
     case TILE_BF6B_128x64:
+    case TILE_BF6R_128x128:
+    case TILE_BF6R_128x64:
       if (!glds_ok || !bf6_on() || !a.wb) return p;
       p.kern = KERN_GLDS;
       p.bm = 128;
-      p.bn = tile == TILE_BF6B_128x64 ? 64 : 128;
+      p.bn = tile == TILE_BF6B_128x64 || tile == TILE_BF6R_128x64 ? 64 : 128;
       p.ppi = 0;
       p.tiles_m = (a.M + p.bm - 1) / p.bm;
       return p;
@@ -1639,7 +1845,9 @@ Plan conv_plan(const ConvArgs& a, bool allow_split, int forced = -1) {
     d = plan_for_tile(a, tile);
     d.ksplit = tile == TILE_128x128 ? ks : 1;
     if (bf6_on() && cin32 && a.KH * a.KW <= 32 && env.kmax >= KERN_GLDS) {
-      Plan b = plan_for_tile(a, a.wb ? (a.Cout > 64 ? TILE_BF6B_128x128 : TILE_BF6B_128x64)
+      const bool r = bf6r_on();
+      Plan b = plan_for_tile(a, a.wb ? (a.Cout > 64 ? (r ? TILE_BF6R_128x128 : TILE_BF6B_128x128)
+                                                    : (r ? TILE_BF6R_128x64 : TILE_BF6B_128x64))
                                      : (a.Cout > 64 ? TILE_BF6_128x128 : TILE_BF6_128x64));
       if (b.kern >= 0) {
         b.ksplit = ks;
@@ -1731,6 +1939,22 @@ int conv_run(ConvArgs& a, const Plan& p, hipStream_t st) {
       hipLaunchKernelGGL((conv_bf6b_kernel<128, 64>), dim3(a.nwg * a.ksplit, a.nbatch), dim3(256),
                          0, st, a);
       break;
+    case TILE_BF6R_128x128:
+      if (bf6r_nst() == 3)
+        hipLaunchKernelGGL((conv_bf6r_kernel<128, 128, 3>), dim3(a.nwg * a.ksplit, a.nbatch),
+                           dim3(256), 0, st, a);
+      else
+        hipLaunchKernelGGL((conv_bf6r_kernel<128, 128, 2>), dim3(a.nwg * a.ksplit, a.nbatch),
+                           dim3(256), 0, st, a);
+      break;
+    case TILE_BF6R_128x64:
+      if (bf6r_nst() == 3)
+        hipLaunchKernelGGL((conv_bf6r_kernel<128, 64, 3>), dim3(a.nwg * a.ksplit, a.nbatch),
+                           dim3(256), 0, st, a);
+      else
+        hipLaunchKernelGGL((conv_bf6r_kernel<128, 64, 2>), dim3(a.nwg * a.ksplit, a.nbatch),
+                           dim3(256), 0, st, a);
+      break;
     case TILE_256x128: launch_rows<256, 128, 4, 2>(a, p.kern, st); break;
     case TILE_128x128: launch_rows<128, 128, 2, 2>(a, p.kern, st); break;
     case TILE_128x64: launch_rows<128, 64, 2, 2>(a, p.kern, st); break;
@@ -1758,6 +1982,9 @@ void launch_up4_weights(const float* w_packed, float* wph, hipStream_t st) {
 }
 
 }  // namespace
+
+PfHaloFp32Scope::PfHaloFp32Scope() { ++tl_halo_fp32; }
+PfHaloFp32Scope::~PfHaloFp32Scope() { --tl_halo_fp32; }
 
 extern "C" int posfeat_conv_packed_k(int cin, int kh, int kw) {
   const int cinp = (cin + 3) / 4 * 4;
@@ -1874,7 +2101,8 @@ extern "C" int posfeat_conv2d_nhwc_stats(const posfeat_conv_desc* d, const float
 static const int kAllTiles[] = {TILE_H8x128,      TILE_H8x64,       TILE_128x128,
                                 TILE_128x64,      TILE_64x64,       TILE_256x128,
                                 TILE_BF6_128x128, TILE_BF6_128x256, TILE_BF6_64x128,
-                                TILE_BF6_128x64,  TILE_BF6B_128x128, TILE_BF6B_128x64};
+                                TILE_BF6_128x64,  TILE_BF6B_128x128, TILE_BF6B_128x64,
+                                TILE_BF6R_128x128, TILE_BF6R_128x64};
 
 int pf_conv_candidates(const posfeat_conv_desc* d, int* tiles, int max, bool wplanes) {
   ConvArgs a;

@@ -603,7 +603,7 @@ void plan(posfeat_model* m) {
   if (m->train && !m->traintap) m->up4 = false;  // the backward reads the materialised conv2 input
   {
     const char* e = getenv("POSFEAT_SIDE");
-    m->side = !(e && e[0] == '0') && m->up4 && m->gfuse && !m->train;
+    m->side = !(e && e[0] == '0') && m->up4 && m->gfuse && (!m->train || m->traintap);
     const char* a = getenv("POSFEAT_SIDE_AT");
     m->side_at = a ? std::min(3, std::max(0, atoi(a))) : 2;
   }
@@ -763,7 +763,8 @@ int image_branch(Ctx& c, const float* img4) {
   if (m->imgstats)
     PF_TRY(timed(s, "head.convimg.stats", 0, [&] {
       return pf_gfuse_imgstats(img4, B, H, W, s.W("head.convimg"), s.Bi("head.convimg"), meanI,
-                               rstdI, s.f(m->imws), m->imws.floats * sizeof(float), s.st);
+                               rstdI, s.f(m->imws), m->imws.floats * sizeof(float), s.st,
+                               m->traintap ? s.d(m->gram) : nullptr);
     }));
   else
     PF_TRY(conv_in(s, "head.convimg", img4, B, H, W, 4, g64, 64, meanI, rstdI));

@@ -127,6 +127,13 @@ int pf_imgbr_grad(const float* A, int n, int HW, const float* w2p, const float* 
 
 // conv product arithmetic: 0 fp32 MFMA, 1 bf16x6, 2 bf16x6 + pre-split GEMMs
 int pf_conv_precision();
+// while alive, this thread's 3x3 stride-1 (halo) convs use fp32 MFMA tiles
+struct PfHaloFp32Scope {
+  PfHaloFp32Scope();
+  ~PfHaloFp32Scope();
+  PfHaloFp32Scope(const PfHaloFp32Scope&) = delete;
+  PfHaloFp32Scope& operator=(const PfHaloFp32Scope&) = delete;
+};
 // bf16x6 GEMMs on pre-split operands (gemm6.hip).  POSFEAT_BF6=2 turns them on
 // for the Winograd transform-domain GEMMs and head.conv2's low-res tap GEMM.
 bool pf_bf6p_on();

@@ -78,7 +78,7 @@ def _check_grads64(got, d, floor=1e-2, mult=3.0):
     noise (BatchNorm backward cancellation), so a fixed fp32-vs-fp32 bound would
     test summation order, not correctness."""
     keys = [k[5:] for k in d.files if k.startswith("stat_")]
-    bad = []
+    bad, errs = [], []
     for k in keys:
         if k.endswith("conv.bias"):
             continue
@@ -91,8 +91,10 @@ def _check_grads64(got, d, floor=1e-2, mult=3.0):
             g = g.reshape(-1)[d["idx_" + k]]
         e = np.abs(g - ref).max() / max(np.abs(ref).max(), 1e-30)
         tol = max(mult * float(d["noise_" + k]), floor)
+        errs.append((float(e), k))
         if e > tol:
             bad.append((k, round(float(e), 6), round(tol, 6)))
+    print("largest relative errors vs fp64:", [(k, "%.2e" % e) for e, k in sorted(errs)[-6:]])
     assert not bad, "tensors over tolerance (key, err, tol): %s" % bad
     num = sum(float(((np.asarray(got[k], np.float64).reshape(-1)[d["idx_" + k]] - d["v64_" + k])
                      ** 2).sum()) if "v64_" + k in d.files else

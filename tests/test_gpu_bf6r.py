@@ -1,0 +1,47 @@
+"""conv_bf6r_kernel (pre-split weights, A straight to registers) against
+conv_bf6b_kernel (A staged through LDS): the same bf16x6 products in the same
+order, so the engine's outputs must be BIT-identical with POSFEAT_BF6R=0/1
+(the switch is read once per process: each run is a child process).  The
+B=8 480x640 bench instance covers the batched Winograd GEMMs, the tap GEMM
+and the 1x1 / strided encoder convs; the stage-count variant too."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CODE = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, %(root)r)
+from posfeat_amd.engine import ExtractionEngine
+from posfeat_amd.weights import seeded_image, seeded_state_dicts
+bb, hd = seeded_state_dicts(0)
+eng = ExtractionEngine(bb, hd, device="cuda:0")
+img = torch.from_numpy(np.stack([seeded_image(60 + i, 480, 640) for i in range(8)])).cuda()
+r = eng.run(img, outputs=("local_map", "global_map"))
+torch.cuda.synchronize()
+np.savez(%(out)r, lp=r["local_point"].cpu().numpy(), lm=r["local_map"].cpu().numpy(),
+         gm=r["global_map"].cpu().numpy())
+"""
+
+
+def _run(tmp_path, env_extra, tag):
+    out = str(tmp_path / ("%s.npz" % tag))
+    env = dict(os.environ, **env_extra)
+    subprocess.run([sys.executable, "-c", CODE % {"root": ROOT, "out": out}], env=env,
+                   check=True, timeout=240)
+    return np.load(out)
+
+
+def test_bf6r_bit_identical_to_bf6b(tmp_path):
+    ref = _run(tmp_path, {"POSFEAT_BF6R": "0"}, "b")   # the default
+    for tag, env in (("r2", {"POSFEAT_BF6R": "1"}),
+                     ("r3", {"POSFEAT_BF6R": "1", "POSFEAT_BF6R_NST": "3"})):
+        got = _run(tmp_path, env, tag)
+        for k in ("lp", "lm", "gm"):
+            np.testing.assert_array_equal(got[k], ref[k], err_msg="%s %s" % (tag, k))
