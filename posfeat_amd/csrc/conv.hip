@@ -73,6 +73,7 @@ struct ConvArgs {
   // pre-split weights (conv_bf6b_kernel): three bf16 planes of w's layout
   const unsigned short* wb;
   long long wplane, bwb;
+  const float* zero;  // a zeroed 16-B device word (pf_conv_zero16), read by masked DMA lanes
 };
 
 // Epilogue shared by both kernels: acc -> LDS T[BM][BN+4] (conflict-free: a
@@ -688,7 +689,8 @@ __global__ __launch_bounds__(256) void conv_bf6b_kernel(ConvArgs a) {
   float* As = smem;
   unsigned short* Bs = reinterpret_cast<unsigned short*>(smem + 2 * ASTAGE);
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // wave index as an SGPR value: the DMA's LDS targets (M0) stay scalar math
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave;
   int bid = blockIdx.x % a.nwg;
   const int split = blockIdx.x / a.nwg;
@@ -706,6 +708,12 @@ __global__ __launch_bounds__(256) void conv_bf6b_kernel(ConvArgs a) {
   const int tm = bid / a.tiles_n, tn = bid - tm * a.tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
 
+  // dense: a 1x1 conv without padding (every Winograd / tap GEMM, every 1x1
+  // layer) has no zero taps; rows past M / Cout read the last valid row
+  // instead (the epilogue never stores them), so a chunk's DMA addresses are
+  // the lane's fixed pointer + one uniform offset: no per-DMA select
+  const bool dense = a.KH == 1 && a.KW == 1 && a.pad == 0;
+  const float* zero = a.zero;
   const int lrow = lane >> 3;
   const float* xsrc[A_G];
   unsigned tapok[A_G];
@@ -713,7 +721,7 @@ __global__ __launch_bounds__(256) void conv_bf6b_kernel(ConvArgs a) {
   for (int i = 0; i < A_G; ++i) {
     const int row = (wave * A_G + i) * 8 + lrow;
     const int sslot = (lane & 7) ^ ((row >> 1) & 7);
-    const int m = m0 + row;
+    const int m = dense ? min(m0 + row, a.M - 1) : m0 + row;
     tapok[i] = 0u;
     xsrc[i] = a.x;
     if (m < a.M) {
@@ -736,36 +744,53 @@ __global__ __launch_bounds__(256) void conv_bf6b_kernel(ConvArgs a) {
     const int pr = (wave * B_G + i) * 16 + (lane >> 2);
     const int plane = pr / BN, row = pr - plane * BN;
     const int ks = (lane & 3) ^ ((row >> 2) & 3);
-    bsrc[i] = (n0 + row < a.Cout)
-                  ? wb + plane * a.wplane + (long long)(n0 + row) * a.Kpad + ks * 8
-                  : nullptr;
+    bsrc[i] = wb + plane * a.wplane + (long long)min(n0 + row, a.Cout - 1) * a.Kpad + ks * 8;
   }
   const int ntap = a.KH * a.KW;
   const int nch_all = a.Kpad / BK;
   const int ch0 = (int)((long long)nch_all * split / a.ksplit);
   const int ch1 = (int)((long long)nch_all * (split + 1) / a.ksplit);
 
-  auto issue_chunk = [&](int c, int buf) {
-    const int slab = c / ntap, tap = c - slab * ntap;
-    const int kh = tap / a.KW, kw = tap - kh * a.KW;
-    const long long delta = ((long long)kh * a.W + kw) * a.xcs + slab * BK;
+  // chunks are issued in order: (slab, tap, kh, kw) of the next one advance
+  // incrementally (one division per workgroup, none per chunk)
+  int nx_slab = ch0 / ntap, nx_tap = ch0 - nx_slab * ntap;
+  int nx_kh = nx_tap / a.KW, nx_kw = nx_tap - nx_kh * a.KW;
+  long long nx_b = (long long)ch0 * BK;
+  auto issue_chunk = [&](int buf) {
+    const long long delta = ((long long)nx_kh * a.W + nx_kw) * a.xcs + nx_slab * BK;
+    if (dense) {  // wave-uniform branch
 #pragma unroll
-    for (int i = 0; i < A_G; ++i) {
-      const float* src = ((tapok[i] >> tap) & 1u) ? xsrc[i] + delta : pf_conv_zero16;
-      __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void*)src,
-          (__attribute__((address_space(3))) void*)(As + buf * ASTAGE + (wave * A_G + i) * 8 * BK),
-          16, 0, 0);
+      for (int i = 0; i < A_G; ++i)
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void*)(xsrc[i] + delta),
+            (__attribute__((address_space(3))) void*)(As + buf * ASTAGE + (wave * A_G + i) * 8 * BK),
+            16, 0, 0);
+    } else {
+#pragma unroll
+      for (int i = 0; i < A_G; ++i) {
+        const float* src = ((tapok[i] >> nx_tap) & 1u) ? xsrc[i] + delta : zero;
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void*)src,
+            (__attribute__((address_space(3))) void*)(As + buf * ASTAGE + (wave * A_G + i) * 8 * BK),
+            16, 0, 0);
+      }
     }
 #pragma unroll
-    for (int i = 0; i < B_G; ++i) {
-      const void* src = bsrc[i] ? (const void*)(bsrc[i] + (long long)c * BK)
-                                : (const void*)pf_conv_zero16;
+    for (int i = 0; i < B_G; ++i)
       __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void*)src,
+          (const __attribute__((address_space(1))) void*)(bsrc[i] + nx_b),
           (__attribute__((address_space(3))) void*)(Bs + buf * 2 * BSTAGE +
                                                      (wave * B_G + i) * 16 * BK),
           16, 0, 0);
+    nx_b += BK;
+    ++nx_tap;
+    if (++nx_kw == a.KW) {
+      nx_kw = 0;
+      if (++nx_kh == a.KH) {
+        nx_kh = 0;
+        nx_tap = 0;
+        ++nx_slab;
+      }
     }
   };
 
@@ -806,12 +831,12 @@ __global__ __launch_bounds__(256) void conv_bf6b_kernel(ConvArgs a) {
     }
   };
 
-  issue_chunk(ch0, 0);
+  if (ch0 < ch1) issue_chunk(0);
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
   for (int c = ch0; c < ch1; ++c) {
     const int cur = (c - ch0) & 1;
-    if (c + 1 < ch1) issue_chunk(c + 1, cur ^ 1);
+    if (c + 1 < ch1) issue_chunk(cur ^ 1);
     compute(cur);
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
@@ -1884,6 +1909,7 @@ void launch_rows(ConvArgs& a, int kern, hipStream_t st) {
 }
 
 int conv_run(ConvArgs& a, const Plan& p, hipStream_t st) {
+  if (!a.zero) return POSFEAT_E_HIP;
   a.tiles_n = (a.Cout + p.bn - 1) / p.bn;
   a.nwg = (int)(p.tiles_m * a.tiles_n);
   a.ksplit = p.ksplit;
@@ -1992,6 +2018,21 @@ extern "C" int posfeat_conv_packed_k(int cin, int kh, int kw) {
   return (k + BK - 1) / BK * BK;
 }
 
+// device address of pf_conv_zero16 on the current device (cached per thread)
+static const float* conv_zero_ptr() {
+  thread_local int dev = -1;
+  thread_local const float* p = nullptr;
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess) return nullptr;
+  if (d != dev) {
+    void* q = nullptr;
+    if (hipGetSymbolAddress(&q, HIP_SYMBOL(pf_conv_zero16)) != hipSuccess) return nullptr;
+    p = static_cast<const float*>(q);
+    dev = d;
+  }
+  return p;
+}
+
 static int conv_prepare(const posfeat_conv_desc* d, const float* x, const float* w,
                         const float* bias, const float* res, float* y, ConvArgs& a) {
   if (!d || !x || !w || !y) return POSFEAT_E_INVALID;
@@ -2037,6 +2078,7 @@ static int conv_prepare(const posfeat_conv_desc* d, const float* x, const float*
   a.bx = a.bw = a.by = 0;
   a.wb = nullptr;
   a.wplane = a.bwb = 0;
+  a.zero = conv_zero_ptr();  // checked at launch (planning calls need no device)
   {
     static const int abl = getenv("POSFEAT_ABL") ? atoi(getenv("POSFEAT_ABL")) : 0;
     a.abl = abl;
