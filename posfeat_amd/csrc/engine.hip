@@ -139,7 +139,7 @@ struct posfeat_model {
   Buf wpl;
   bool tapb = false;  // bf16x6 tap GEMM on pre-split planes (POSFEAT_BF6=2)
   Buf tapwb, tapLb;
-  Buf gf_w, gf_b;
+  Buf gf_w, gf_b, gf_wp;
   // convimg's IN statistics from the image's tap moments instead of running
   // convimg (gfuse.hip): the full-res 64-channel map is never computed
   bool imgstats = true;
@@ -578,6 +578,7 @@ void plan(posfeat_model* m) {
   if (m->up4 && m->gfuse) {
     alloc(m->gf_w, B * 128 * 128);
     alloc(m->gf_b, B * 128 + 9 * 64 * 128);  // + the transposed W2 G slice (gfuse.hip)
+    alloc(m->gf_wp, pf_gfuse_wplanes_bytes((int)B) / 4 + 4);  // pre-split K = 80 weights
   }
   if (!(m->up4 && m->gfuse) || (m->train && !m->traintap)) m->imgstats = false;
   if (m->traintap) m->imgstats = true;  // the backward contracts the image moments
@@ -788,7 +789,8 @@ int image_branch(Ctx& c, const float* img4) {
   PF_TRY(timed(s, "conv:head.conv2.g", 2.0 * B * H * W * 128.0 * 4 * 26, [&] {
     return pf_gfuse_conv(img4, g64, 64, B, H, W, s.f(m->gf_w), s.f(m->gf_b), meanI, rstdI,
                          s.W("head.conv2"), s.Bi("head.conv2"), c2, 128, s.st,
-                         s.W("head.convimg"), s.Bi("head.convimg"));
+                         s.W("head.convimg"), s.Bi("head.convimg"),
+                         reinterpret_cast<unsigned short*>(s.f(m->gf_wp)));
   }));
   if (m->up4wino && !m->up4tap)
     PF_TRY(timed(s, "head.conv2.up4w", 0, [&] {
@@ -964,7 +966,8 @@ int head_forward(Ctx& c, float* img4, float* local_point, bool side) {
       PF_TRY(timed(c, "conv:head.conv2.g", 2.0 * B * H * W * 128.0 * 4 * 26, [&] {
         return pf_gfuse_conv(img4, g64, 64, B, H, W, c.f(m->gf_w), c.f(m->gf_b), meanI, rstdI,
                              c.W("head.conv2"), c.Bi("head.conv2"), c2, 128, c.st,
-                             c.W("head.convimg"), c.Bi("head.convimg"));
+                             c.W("head.convimg"), c.Bi("head.convimg"),
+                             reinterpret_cast<unsigned short*>(c.f(m->gf_wp)));
       }));
     } else {
       PF_TRY(timed(c, "conv:head.conv2.g", 2.0 * B * H * W * 128.0 * 64 * 9, [&] {

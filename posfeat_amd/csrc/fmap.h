@@ -78,7 +78,10 @@ int pf_gfuse_weights(const float* w2_packed, const float* b2, const float* w1_pa
 int pf_gfuse_conv(const float* img4, const float* c, int ccs, int n, int H, int W,
                   const float* wc, const float* bc, const float* mean, const float* rstd,
                   const float* w2_packed, const float* b2, float* y, int ycs, hipStream_t st,
-                  const float* w1_packed = nullptr, const float* b1 = nullptr);
+                  const float* w1_packed = nullptr, const float* b1 = nullptr,
+                  unsigned short* wplanes = nullptr);
+// scratch of the pre-split K = 80 weights (gfuse_conv5_k80_kernel)
+size_t pf_gfuse_wplanes_bytes(int n);
 // convimg's instance-norm statistics from the image's tap moments (no conv)
 size_t pf_gfuse_imgstats_ws_bytes(int n, int H);
 int pf_gfuse_imgstats(const float* img4, int n, int H, int W, const float* w1_packed,

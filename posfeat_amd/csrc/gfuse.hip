@@ -471,7 +471,172 @@ __global__ __launch_bounds__(256) void gfuse_conv5_bf6_kernel(const float* __res
     }
   }
 }
+// ---- the folded 5x5 conv: pre-split weights, 3-channel K = 80 (default) ----
+// k = dy*16 + dx*3 + c (dy, dx < 5, c < 3; k % 16 == 15 has zero weight): one
+// k16 step per patch row dy, whose 15 taps x channels are 15 CONSECUTIVE
+// floats of a 3-channel-packed patch row (tile pixel x starts at float 3x).
+// MFMA A = the image's weights, pre-split once per forward into three bf16
+// planes [co][80] (gfuse_wsplit_kernel) and staged in LDS once per block;
+// B = the pixels' taps, split in registers (lane half h: floats 3x + 8h .. +7
+// of row dy; the 16th is the next pixel's channel 0, against a zero weight).
+// 80 instead of the 4-channel form's 112 k per output: 29 % fewer
+// matrix-core cycles, and no weight split per wave.  acc rows = couts, so a
+// lane holds 4 consecutive couts of one pixel: float4 stores.  Block = 8
+// waves on a 16-row x 32-pixel tile (wave = 2 pixel rows x 128 couts),
+// persistent over the tiles of one image; the next tile's patch is loaded
+// into registers while the current one is multiplied.
+constexpr int G8_K = 80, G8_KP = 88;  // K, LDS row pitch (bf16; 176 B: conflict-free b128 per 16 lanes)
+constexpr int G8_TR = 16, G8_TC = 32, G8_PR = G8_TR + 4, G8_PC = G8_TC + 4;
+constexpr int G8_PW = 112;            // patch row pitch (floats): 36 px x 3 + 4 zero
+constexpr int G8_NPX = G8_PR * G8_PC;  // 720 patch pixels, <= 2 per thread
+
+__global__ void gfuse_wsplit_kernel(const float* __restrict__ wc, int n,
+                                    unsigned short* __restrict__ wp) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * GF_COUT * G8_K) return;
+  const int k = i % G8_K, r = i / G8_K, co = r % GF_COUT, b = r / GF_COUT;
+  const int dy = k >> 4, q = k & 15, dx = q / 3, c = q - dx * 3;
+  const float v = q < 15 ? wc[((long long)b * GF_COUT + co) * GF_KPAD + (dy * 5 + dx) * 4 + c] : 0.f;
+  unsigned h, m, l;
+  pf_split3_pair(v, 0.f, h, m, l);
+  const long long pl = (long long)GF_COUT * G8_K;
+  unsigned short* o = wp + (long long)b * 3 * pl + (long long)co * G8_K + k;
+  o[0] = (unsigned short)(h & 0xffffu);
+  o[pl] = (unsigned short)(m & 0xffffu);
+  o[2 * pl] = (unsigned short)(l & 0xffffu);
+}
+
+__global__ __launch_bounds__(512) void gfuse_conv5_k80_kernel(const float* __restrict__ img4, int H,
+                                                              int W,
+                                                              const unsigned short* __restrict__ wp,
+                                                              const float* __restrict__ bc,
+                                                              float* __restrict__ y, int ycs) {
+  __shared__ __attribute__((aligned(16))) unsigned short sw[3 * GF_COUT * G8_KP];
+  __shared__ __attribute__((aligned(16))) float sp[G8_PR * G8_PW];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, col = lane & 31;
+  const int b = blockIdx.y;
+  const int ntc = (W + G8_TC - 1) / G8_TC, ntiles = ntc * ((H + G8_TR - 1) / G8_TR);
+  const float* ib = img4 + (long long)b * H * W * 4;
+  {  // the image's weight planes -> LDS rows of 88 (8-element pieces)
+    const unsigned short* wb = wp + (long long)b * 3 * GF_COUT * G8_K;
+    for (int i = tid; i < 3 * GF_COUT * (G8_K / 8); i += 512) {
+      const int row = i / (G8_K / 8), piece = i - row * (G8_K / 8);
+      *reinterpret_cast<uint4*>(sw + row * G8_KP + piece * 8) =
+          *reinterpret_cast<const uint4*>(wb + (long long)row * G8_K + piece * 8);
+    }
+  }
+  for (int i = tid; i < G8_PR * 4; i += 512)  // the zero tail of every patch row
+    sp[(i >> 2) * G8_PW + 108 + (i & 3)] = 0.f;
+  auto load_patch = [&](int t, f32x4 (&v)[2]) {
+    const int ty0 = (t / ntc) * G8_TR, tx0 = (t % ntc) * G8_TC;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int i = tid + j * 512;
+      v[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (i < G8_NPX) {
+        const int py = i / G8_PC, px = i - py * G8_PC;
+        const int yy = ty0 - 2 + py, xx = tx0 - 2 + px;
+        if ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W)
+          v[j] = *reinterpret_cast<const f32x4*>(ib + ((long long)yy * W + xx) * 4);
+      }
+    }
+  };
+  auto store_patch = [&](const f32x4 (&v)[2]) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int i = tid + j * 512;
+      if (i < G8_NPX) {
+        const int py = i / G8_PC, px = i - py * G8_PC;
+        float* d = sp + py * G8_PW + px * 3;
+        d[0] = v[j].x;
+        d[1] = v[j].y;
+        d[2] = v[j].z;
+      }
+    }
+  };
+  const float* bcb = bc + (long long)b * GF_COUT;
+  f32x4 pv[2];
+  int t = blockIdx.x;
+  if (t < ntiles) load_patch(t, pv);
+  for (; t < ntiles; t += gridDim.x) {
+    __syncthreads();  // the previous tile's patch is consumed
+    store_patch(pv);
+    __syncthreads();
+    if (t + (int)gridDim.x < ntiles) load_patch(t + gridDim.x, pv);  // in flight during the MFMAs
+    f32x16 acc[4][2];
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
+#pragma unroll
+    for (int dy = 0; dy < 5; ++dy) {
+      g6_u32x4 bh[2], bm[2], bl[2];
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) {
+        const float* pr = sp + (2 * wave + ni + dy) * G8_PW + 3 * col + 8 * h;
+        f32x4 p0, p1;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          p0[j] = pr[j];
+          p1[j] = pr[4 + j];
+        }
+        g6_split(p0, p1, bh[ni], bm[ni], bl[ni]);
+      }
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) {
+        const unsigned short* wr = sw + (mi * 32 + col) * G8_KP + dy * 16 + 8 * h;
+        const g6_u32x4 ah = *reinterpret_cast<const g6_u32x4*>(wr);
+        const g6_u32x4 am = *reinterpret_cast<const g6_u32x4*>(wr + GF_COUT * G8_KP);
+        const g6_u32x4 al = *reinterpret_cast<const g6_u32x4*>(wr + 2 * GF_COUT * G8_KP);
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) {
+          f32x16 c = acc[mi][ni];
+          c = g6_mfma(ah, bh[ni], c);
+          c = g6_mfma(ah, bm[ni], c);
+          c = g6_mfma(am, bh[ni], c);
+          c = g6_mfma(ah, bl[ni], c);
+          c = g6_mfma(al, bh[ni], c);
+          c = g6_mfma(am, bm[ni], c);
+          acc[mi][ni] = c;
+        }
+      }
+    }
+    // acc[mi][ni][r]: cout mi*32 + (r&3) + 8(r>>2) + 4h, pixel (row 2*wave + ni, column col)
+    const int ty0 = (t / ntc) * G8_TR, tx0 = (t % ntc) * G8_TC;
+    const int xx = tx0 + col;
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni) {
+      const int yy = ty0 + 2 * wave + ni;
+      if (yy >= H || xx >= W) continue;
+      float* yp = y + ((long long)(b * H + yy) * W + xx) * ycs;
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int co = mi * 32 + 8 * j + 4 * h;
+          const f32x4 bv = *reinterpret_cast<const f32x4*>(bcb + co);
+          f32x4 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = acc[mi][ni][4 * j + e] + bv[e];
+          *reinterpret_cast<f32x4*>(yp + co) = o;
+        }
+    }
+  }
+}
+
+bool gfuse_k80_on() {
+  static const bool on = [] {
+    const char* e = getenv("POSFEAT_GFUSE_K80");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 }  // namespace
+
+size_t pf_gfuse_wplanes_bytes(int n) { return (size_t)n * 3 * GF_COUT * G8_K * 2; }
 
 // wc (n*128*128) | bc (n*128) | w2t (9*64*128)
 size_t pf_gfuse_weights_floats(int n) {
@@ -499,11 +664,20 @@ int pf_gfuse_weights(const float* w2_packed, const float* b2, const float* w1_pa
 int pf_gfuse_conv(const float* img4, const float* c, int ccs, int n, int H, int W,
                   const float* wc, const float* bc, const float* mean, const float* rstd,
                   const float* w2_packed, const float* b2, float* y, int ycs, hipStream_t st,
-                  const float* w1_packed, const float* b1) {
+                  const float* w1_packed, const float* b1, unsigned short* wplanes) {
   if (!c && !(w1_packed && b1)) return POSFEAT_E_INVALID;
   if (ycs % 4 || n <= 0) return POSFEAT_E_INVALID;
   const int ntiles = ((W + G5_TC - 1) / G5_TC) * ((H + G5_TR - 1) / G5_TR);
-  if (pf_conv_precision() >= 1)  // bf16x6 products (the default conv arithmetic)
+  if (pf_conv_precision() >= 1 && wplanes && gfuse_k80_on()) {
+    const int tot = n * GF_COUT * G8_K;
+    hipLaunchKernelGGL(gfuse_wsplit_kernel, dim3((tot + 255) / 256), dim3(256), 0, st, wc, n,
+                       wplanes);
+    const int nt8 = ((W + G8_TC - 1) / G8_TC) * ((H + G8_TR - 1) / G8_TR);
+    // persistent blocks: ~2 per CU over the batch, each on one image's tiles
+    const int per_img = std::max(1, std::min(nt8, (512 + n - 1) / n));
+    hipLaunchKernelGGL(gfuse_conv5_k80_kernel, dim3(per_img, n), dim3(512), 0, st, img4, H, W,
+                       wplanes, bc, y, ycs);
+  } else if (pf_conv_precision() >= 1)  // bf16x6 products (the default conv arithmetic)
     hipLaunchKernelGGL(gfuse_conv5_bf6_kernel, dim3(ntiles, n), dim3(256), 0, st, img4, H, W, wc,
                        bc, y, ycs);
   else
