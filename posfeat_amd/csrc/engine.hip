@@ -401,9 +401,23 @@ int forward(Ctx& c, const float* img, posfeat_extract_out* out, int mode = MODE_
             const float* xhead = nullptr);
 
 // The decoder's 3x3 stride-1 convs (DescNet.py:41-45) through Winograd
-// F(2x2,3x3) when enabled (default; POSFEAT_WINO=0 for the direct conv)
-const char* const kWinoLayers[5] = {"upconv3.conv", "iconv3", "upconv2.conv", "iconv2",
-                                    "head.conv1"};
+// F(4x4,3x3) / F(2x2,3x3) when enabled (default; POSFEAT_WINO=0 for the
+// direct conv); then (POSFEAT_WINO_ENC=1) the encoder's stride-1 bottleneck
+// conv2 layers, with their resolution divisor
+const char* const kWinoLayers[16] = {"upconv3.conv", "iconv3",          "upconv2.conv",
+                                     "iconv2",       "head.conv1",      "layer1.0.conv2",
+                                     "layer1.1.conv2", "layer1.2.conv2", "layer2.1.conv2",
+                                     "layer2.2.conv2", "layer2.3.conv2", "layer3.1.conv2",
+                                     "layer3.2.conv2", "layer3.3.conv2", "layer3.4.conv2",
+                                     "layer3.5.conv2"};
+const int kWinoDiv[16] = {8, 8, 4, 4, 4, 4, 4, 4, 8, 8, 8, 16, 16, 16, 16, 16};
+bool wino_enc_on() {
+  static const bool on = [] {
+    const char* e = getenv("POSFEAT_WINO_ENC");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
 
 long long wino_u_offset(const std::string& name, bool planes) {
   long long off = 0;
@@ -591,12 +605,12 @@ void plan(posfeat_model* m) {
   if (m->wsplit) alloc(m->wpl, (size_t)specs().total * 3 / 2 + 4);
   if (m->wino) {
     size_t uf = 0, wb = 0;
-    const int dims[5][2] = {{(int)h8, (int)w8}, {(int)h8, (int)w8}, {(int)h4, (int)w4},
-                            {(int)h4, (int)w4}, {(int)h4, (int)w4}};
-    for (int i = 0; i < 5; ++i) {
+    const int nl = wino_enc_on() ? 16 : 5;
+    for (int i = 0; i < nl; ++i) {
       const Spec* s = specs().find(kWinoLayers[i]);
       uf += (size_t)(m->bf6p || m->wsplit ? 54 : 36) * s->cout * s->cin;
-      wb = std::max(wb, pf_wino_ws_bytes((int)B, dims[i][0], dims[i][1], s->cin, s->cout));
+      wb = std::max(wb, pf_wino_ws_bytes((int)B, (int)H / kWinoDiv[i], (int)W / kWinoDiv[i],
+                                         s->cin, s->cout));
     }
     alloc(m->wino_u, uf);
     alloc(m->wino_ws, wb / 4 + 4);
@@ -690,7 +704,10 @@ int bottleneck(Ctx& c, const std::string& p, const float* in, int n, int h, int 
   float* t1 = c.f(m->t1);
   float* t2 = c.f(m->t2);
   PF_TRY(conv(c, p + ".conv1", in, n, h, w, ics, t1, planes, 1, POSFEAT_ACT_RELU));
-  PF_TRY(conv(c, p + ".conv2", t1, n, h, w, planes, t2, planes, stride, POSFEAT_ACT_RELU));
+  if (stride == 1 && c.m->wino && wino_enc_on() && !c.side)
+    PF_TRY(conv3x3(c, p + ".conv2", t1, n, h, w, planes, t2, planes, POSFEAT_ACT_RELU));
+  else
+    PF_TRY(conv(c, p + ".conv2", t1, n, h, w, planes, t2, planes, stride, POSFEAT_ACT_RELU));
   const float* res = in;
   int rcs = ics;
   if (has_ds) {
