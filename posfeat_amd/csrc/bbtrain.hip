@@ -166,6 +166,14 @@ struct posfeat_bbtrain {
   bool bf6p = false;     // conv precision mode 2 at create (pre-split Winograd operands)
   bool s2phase = true;  // stride-2 input gradients by output phases (POSFEAT_S2PHASE=0: zero insertion)
   Buf wu, wino_ws;
+  // pre-split bf16x6 operands (conv precision 1, POSFEAT_BF6B=0: off): the
+  // parameter blob's three bf16 planes (split at the start of each forward:
+  // Adam moves the parameters between calls) and those of the transposed
+  // input-gradient weights, so the row-tile convs run conv_bf6b_kernel
+  // (weights read ready-made) instead of splitting both operands per wave --
+  // the same products in the same order: bit-identical results
+  bool wsplit = false;
+  Buf wpl, wtp;
   // optional per-launch timing (labels "fwd:conv", "bwd:wgrad", ...)
   bool timing = false;
   struct Ev {
@@ -221,6 +229,7 @@ struct Ctx {
   float* f(const Buf& b) const { return reinterpret_cast<float*>(act + b.off); }
   float* s(const Buf& b) const { return reinterpret_cast<float*>(scr + b.off); }
   double* sd(const Buf& b) const { return reinterpret_cast<double*>(scr + b.off); }
+  unsigned short* su(const Buf& b) const { return reinterpret_cast<unsigned short*>(scr + b.off); }
 };
 
 template <class F>
@@ -388,6 +397,14 @@ void plan(posfeat_bbtrain* m) {
     }
   }
   alloc(m->wt, fl(wt));
+  {
+    const char* e = getenv("POSFEAT_BF6B");
+    m->wsplit = pf_conv_precision() == 1 && !(e && e[0] == '0') && T.params % 4 == 0;
+  }
+  if (m->wsplit) {
+    alloc(m->wpl, (size_t)T.params * 6);
+    alloc(m->wtp, wt * 6 + 256);
+  }
   alloc(m->dz, fl(std::max(dzf, 2 * MAXG)));
   alloc(m->wgws, wg);
   alloc(m->splitk, std::max<size_t>(sk, 256));
@@ -404,7 +421,7 @@ void plan(posfeat_bbtrain* m) {
     size_t uf = 0, wb = 0;
     for (int li : {T.up3, T.ic3, T.up2, T.ic2}) {
       const TLayer& L = T.v[li];
-      uf = std::max(uf, (size_t)(m->bf6p ? 54 : 36) * L.cin * L.cout);
+      uf = std::max(uf, (size_t)(m->bf6p || m->wsplit ? 54 : 36) * L.cin * L.cout);
       wb = std::max(wb, pf_wino_ws_bytes((int)B, lih[li], liw[li], L.cin, L.cout));
       wb = std::max(wb, pf_wino_ws_bytes((int)B, lih[li], liw[li], L.cout, L.cin));
       if (lih[li] % 4 == 0 && liw[li] % 4 == 0)
@@ -439,14 +456,17 @@ int layer_fwd(Ctx& c, int li, const float* x, int xcs, int h, int w, float* out,
   if (use_wino(m, li, h, w)) {
     float* U = c.s(m->wu);
     PF_TRY(timed(c, "fwd:conv", wino_flops(m->B, h, w, L.cin, L.cout), [&] {
-      PF_TRY(pf_wino_weights_hw(c.prm + L.w_off, L.cout, L.cin, h, w, U, c.st, m->bf6p));
+      PF_TRY(pf_wino_weights_hw(c.prm + L.w_off, L.cout, L.cin, h, w, U, c.st,
+                                m->bf6p || m->wsplit));
       return pf_wino_conv(x, xcs, m->B, h, w, L.cin, U, c.prm + L.b_off, L.cout, ACT_NONE, y,
-                          L.cout, c.s(m->wino_ws), m->wino_ws.bytes, c.st, 7, m->bf6p ? 2 : 0);
+                          L.cout, c.s(m->wino_ws), m->wino_ws.bytes, c.st, 7,
+                          m->bf6p ? 2 : m->wsplit ? 1 : 0);
     }));
   } else {
     PF_TRY(timed(c, "fwd:conv", 2.0 * P * L.cout * L.cin * L.k * L.k, [&] {
       return pf_conv_run_tile(&d, x, c.prm + L.w_off, L.bias ? c.prm + L.b_off : nullptr, nullptr,
-                              y, c.s(m->splitk), m->splitk.bytes, -1, c.st);
+                              y, c.s(m->splitk), m->splitk.bytes, -1, c.st,
+                              m->wsplit ? c.su(m->wpl) + L.w_off : nullptr, tab().params);
     }));
   }
   float* mean = c.f(m->st[li]);
@@ -579,9 +599,14 @@ int layer_bwd(Ctx& c, int li, const float* x, int xcs, int h, int w, const float
     d.pad = k3 ? 1 : 0;
     const double pf = k3 ? 2.0 * B * (oh2 + 1) * (ow2 + 1) * 4 * C * 4 * L.cin
                          : 2.0 * B * oh2 * ow2 * C * L.cin;
+    const long long wrows = k3 ? 4LL * L.cin : L.cin, wcols = posfeat_conv_packed_k(C, d.kh, d.kw);
+    if (m->wsplit)
+      PF_TRY(timed(c, "bwd:misc", 0, [&] {
+        return pf_split3_rows(wt, wrows, (int)wcols, (int)wcols, c.su(m->wtp), c.st);
+      }));
     PF_TRY(timed(c, "bwd:dgrad", pf, [&] {
       return pf_conv_run_tile(&d, dy, wt, nullptr, nullptr, dz, c.s(m->splitk), m->splitk.bytes,
-                              -1, c.st);
+                              -1, c.st, m->wsplit ? c.su(m->wtp) : nullptr, wrows * wcols);
     }));
     return timed(c, "bwd:misc", 0, [&] {
       hipLaunchKernelGGL(s2_scatter_kernel, dim3(grid_for((long long)B * h * w * (L.cin / 4), 256)),
@@ -607,15 +632,21 @@ int layer_bwd(Ctx& c, int li, const float* x, int xcs, int h, int w, const float
   if (!add && use_wino(m, li, h, w)) {
     float* U = c.s(m->wu);
     return timed(c, "bwd:dgrad", wino_flops(B, h, w, C, L.cin), [&] {
-      PF_TRY(pf_wino_weights_hw(wt, L.cin, C, h, w, U, c.st, m->bf6p));
+      PF_TRY(pf_wino_weights_hw(wt, L.cin, C, h, w, U, c.st, m->bf6p || m->wsplit));
       return pf_wino_conv(src, C, B, h, w, C, U, nullptr, L.cin, ACT_NONE, dx, dxcs,
-                          c.s(m->wino_ws), m->wino_ws.bytes, c.st, 7, m->bf6p ? 2 : 0);
+                          c.s(m->wino_ws), m->wino_ws.bytes, c.st, 7,
+                          m->bf6p ? 2 : m->wsplit ? 1 : 0);
     });
   }
   posfeat_conv_desc d = make_desc(B, h, w, C, C, L.cin, L.k, 1, dxcs, add ? addcs : 0);
+  const long long wcols = posfeat_conv_packed_k(C, L.k, L.k);
+  if (m->wsplit)
+    PF_TRY(timed(c, "bwd:misc", 0, [&] {
+      return pf_split3_rows(wt, L.cin, (int)wcols, (int)wcols, c.su(m->wtp), c.st);
+    }));
   return timed(c, "bwd:dgrad", flops, [&] {
     return pf_conv_run_tile(&d, src, wt, nullptr, add, dx, c.s(m->splitk), m->splitk.bytes, -1,
-                            c.st);
+                            c.st, m->wsplit ? c.su(m->wtp) : nullptr, (long long)L.cin * wcols);
   });
 }
 
@@ -658,6 +689,11 @@ std::vector<BlkIO> block_io(Ctx& c) {
 }
 
 int forward(Ctx& c, const float* img, float* stats, float mom) {
+  posfeat_bbtrain* mm = c.m;
+  if (mm->wsplit)  // the parameters' bf16 planes for this call's row-tile convs
+    PF_TRY(timed(c, "fwd:misc", 0, [&] {
+      return pf_split3_rows(c.prm, tab().params / 4, 4, 4, c.su(mm->wpl), c.st);
+    }));
   posfeat_bbtrain* m = c.m;
   const TTable& T = tab();
   const int B = m->B, H = m->H, W = m->W;

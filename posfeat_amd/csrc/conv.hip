@@ -462,7 +462,7 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_glds_kernel(ConvArgs a) {
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wave = tid >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // SGPR: scalar DMA targets
   const int wm = wave / WN, wn = wave % WN;
 
   int bid = blockIdx.x % a.nwg;
@@ -483,6 +483,10 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_glds_kernel(ConvArgs a) {
   // ---- per-lane DMA sources (fixed across K) -------------------------------
   // instruction i of this wave fills rows [(wave*G + i)*8, +8); lane L -> row
   // +(L>>3), LDS slot L&7, which holds source k-slot (L&7) ^ ((row>>1)&7)
+  // dense 1x1 convs without padding: rows past M / Cout read the last valid
+  // row (never stored) instead of a per-DMA zero select (see conv_bf6b_kernel)
+  const bool dense = a.KH == 1 && a.KW == 1 && a.pad == 0;
+  const float* zero = a.zero;
   const int lrow = lane >> 3;
   const float* xsrc[A_G];
   unsigned tapok[A_G];  // bit t: tap t of this pixel is inside the image
@@ -490,7 +494,7 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_glds_kernel(ConvArgs a) {
   for (int i = 0; i < A_G; ++i) {
     const int row = (wave * A_G + i) * 8 + lrow;
     const int sslot = (lane & 7) ^ ((row >> 1) & 7);
-    const int m = m0 + row;
+    const int m = dense ? min(m0 + row, a.M - 1) : m0 + row;
     tapok[i] = 0u;
     xsrc[i] = a.x;
     if (m < a.M) {
@@ -514,7 +518,7 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_glds_kernel(ConvArgs a) {
   for (int i = 0; i < B_G; ++i) {
     const int row = (wave * B_G + i) * 8 + lrow;
     const int sslot = (lane & 7) ^ ((row >> 1) & 7);
-    wsrc[i] = (n0 + row < a.Cout) ? a.w + (size_t)(n0 + row) * a.Kpad + sslot * 4 : nullptr;
+    wsrc[i] = a.w + (size_t)min(n0 + row, a.Cout - 1) * a.Kpad + sslot * 4;
   }
 
   const int ntap = a.KH * a.KW;
@@ -522,26 +526,45 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_glds_kernel(ConvArgs a) {
   const int ch0 = (int)((long long)nch_all * split / a.ksplit);
   const int ch1 = (int)((long long)nch_all * (split + 1) / a.ksplit);
 
-  // issue the DMA of absolute chunk c into stage `buf`
-  auto issue_chunk = [&](int c, int buf) {
-    const int slab = c / ntap, tap = c - slab * ntap;
-    const int kh = tap / a.KW, kw = tap - kh * a.KW;
-    const long long delta = ((long long)kh * a.W + kw) * a.xcs + slab * BK;
+  // issue the DMA of the next chunk (chunks go out in order: (slab, tap, kh,
+  // kw) advance incrementally, no per-chunk division) into stage `buf`
+  int nx_slab = ch0 / ntap, nx_tap = ch0 - nx_slab * ntap;
+  int nx_kh = nx_tap / a.KW, nx_kw = nx_tap - nx_kh * a.KW;
+  long long nx_b = (long long)ch0 * BK;
+  auto issue_chunk = [&](int buf) {
+    const long long delta = ((long long)nx_kh * a.W + nx_kw) * a.xcs + nx_slab * BK;
+    if (dense) {
 #pragma unroll
-    for (int i = 0; i < A_G; ++i) {
-      const float* src = ((tapok[i] >> tap) & 1u) ? xsrc[i] + delta : pf_conv_zero16;
-      __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void*)src,
-          (__attribute__((address_space(3))) void*)(As + (buf * BM + (wave * A_G + i) * 8) * BK),
-          16, 0, 0);
+      for (int i = 0; i < A_G; ++i)
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void*)(xsrc[i] + delta),
+            (__attribute__((address_space(3))) void*)(As + (buf * BM + (wave * A_G + i) * 8) * BK),
+            16, 0, 0);
+    } else {
+#pragma unroll
+      for (int i = 0; i < A_G; ++i) {
+        const float* src = ((tapok[i] >> nx_tap) & 1u) ? xsrc[i] + delta : zero;
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void*)src,
+            (__attribute__((address_space(3))) void*)(As + (buf * BM + (wave * A_G + i) * 8) * BK),
+            16, 0, 0);
+      }
     }
 #pragma unroll
-    for (int i = 0; i < B_G; ++i) {
-      const float* src = wsrc[i] ? wsrc[i] + (size_t)c * BK : pf_conv_zero16;
+    for (int i = 0; i < B_G; ++i)
       __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void*)src,
+          (const __attribute__((address_space(1))) void*)(wsrc[i] + nx_b),
           (__attribute__((address_space(3))) void*)(Bs + (buf * BN + (wave * B_G + i) * 8) * BK),
           16, 0, 0);
+    nx_b += BK;
+    ++nx_tap;
+    if (++nx_kw == a.KW) {
+      nx_kw = 0;
+      if (++nx_kh == a.KH) {
+        nx_kh = 0;
+        nx_tap = 0;
+        ++nx_slab;
+      }
     }
   };
 
@@ -616,12 +639,12 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_glds_kernel(ConvArgs a) {
   };
 
   if constexpr (NST == 2) {
-    issue_chunk(ch0, 0);
+    if (ch0 < ch1) issue_chunk(0);
     __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0): the DMA has landed (this wave)
     __syncthreads();
     for (int c = ch0; c < ch1; ++c) {
       const int cur = (c - ch0) & 1;
-      if (c + 1 < ch1 && !(a.abl & 2)) issue_chunk(c + 1, cur ^ 1);
+      if (c + 1 < ch1 && !(a.abl & 2)) issue_chunk(cur ^ 1);
       if (!(a.abl & 1)) compute(cur);
       __builtin_amdgcn_s_waitcnt(0);
       __syncthreads();
@@ -631,7 +654,7 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_glds_kernel(ConvArgs a) {
     // multiplied; each chunk waits only for its own DMA (counted vmcnt) and
     // one raw s_barrier (no fence: the younger chunks' DMAs stay in flight)
     const int nch = ch1 - ch0;
-    for (int j = 0; j < NST - 1 && j < nch; ++j) issue_chunk(ch0 + j, j);
+    for (int j = 0; j < NST - 1 && j < nch; ++j) issue_chunk(j);
     int slot = 0;
     for (int i = 0; i < nch; ++i) {
       const int ahead = min(NST - 2, nch - 1 - i);  // younger chunks already issued
@@ -645,7 +668,7 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_glds_kernel(ConvArgs a) {
         wait_vmcnt<0>();
       // every wave: chunk i landed, and chunk i-1 (the slot refilled below) consumed
       __builtin_amdgcn_s_barrier();
-      if (i + NST - 1 < nch) issue_chunk(ch0 + i + NST - 1, slot == 0 ? NST - 1 : slot - 1);
+      if (i + NST - 1 < nch) issue_chunk(slot == 0 ? NST - 1 : slot - 1);
       compute(slot);
       slot = slot == NST - 1 ? 0 : slot + 1;
     }

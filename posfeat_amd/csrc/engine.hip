@@ -1107,8 +1107,13 @@ int head_backward_tap(Ctx& c, float* grad, double* t2s, int t2n) {
   const size_t wgb = m->wgws.floats * sizeof(float);
   PF_TRY(timed(c, "bwd:up4tap_adjoint", 0,
                [&] { return pf_up4tap_adjoint(B, H, W, dc2, 128, D, c.st); }));
-  PF_TRY(timed(c, "bwd:tapw_t", 0,
-               [&] { return pf_up4tap_weights_t(c.W("head.conv2"), c.f(m->tapwT), c.st); }));
+  // WtT (+ its bf16 planes in the forward's tap-weight plane buffer, free
+  // after the forward) for the pre-split bf16x6 tiles
+  unsigned short* wtTb = m->wsplit ? reinterpret_cast<unsigned short*>(c.f(m->tapwb)) : nullptr;
+  PF_TRY(timed(c, "bwd:tapw_t", 0, [&] {
+    PF_TRY(pf_up4tap_weights_t(c.W("head.conv2"), c.f(m->tapwT), c.st));
+    return wtTb ? pf_split3_rows(c.f(m->tapwT), 192, 1152, 1152, wtTb, c.st) : POSFEAT_OK;
+  }));
   PF_TRY(timed(c, "bwdconv:head.conv2.tap_wgrad", 2.0 * B * h4 * w4 * 1152.0 * 192, [&] {
     return pf_conv_wgrad(D, 1152, c.f(m->Lbuf), 192, B, h4, w4, 192, 1152, 1, 1, 1, c.f(m->dwtap),
                          nullptr, 0, c.f(m->wgws), wgb, c.st);
@@ -1116,7 +1121,7 @@ int head_backward_tap(Ctx& c, float* grad, double* t2s, int t2n) {
   {
     const posfeat_conv_desc d = dl_desc(m);
     PF_TRY(conv_desc_run(c, "bwd.head.conv2.tap_dgrad", d, D, c.f(m->tapwT), nullptr, nullptr, dc1,
-                         2.0 * B * h4 * w4 * 1152.0 * 192));
+                         2.0 * B * h4 * w4 * 1152.0 * 192, wtTb, 192LL * 1152));
   }
   PF_TRY(timed(c, "bwd:img_taps", 0,
                [&] { return pf_img_taps32(c.f(m->img4), B, H, W, c.f(m->x32), c.st); }));
