@@ -1776,6 +1776,18 @@ const ConvEnv& conv_env() {
 // Split-K factor: only for deep K (>= 64 chunks) where the tile count leaves
 // the last round of resident workgroups badly underfilled.
 int choose_ksplit(long long tiles, int nch, double slots) {
+  // POSFEAT_CONV_SPLIT_SMALL=1 (A/B, off): underfilled grids (fewer tiles
+  // than CUs, e.g. layer3's M = 9600 x 256 1x1 convs) split a shorter K too;
+  // measured r3v: layer3 1x1 0.057 -> 0.050 ms, the step no faster (797 vs 800)
+  static const bool small = [] {
+    const char* e = getenv("POSFEAT_CONV_SPLIT_SMALL");
+    return e && e[0] == '1';
+  }();
+  if (small && tiles < 256 && nch >= 16) {
+    int ks = 1;
+    while (ks < 4 && tiles * (ks + 1) <= 512 && nch / (ks + 1) >= 8) ++ks;
+    return ks;
+  }
   if (nch < 64) return 1;
   int best = 1;
   double best_eff = 0.0;
