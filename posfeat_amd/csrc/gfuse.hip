@@ -173,9 +173,19 @@ constexpr int IM_ROWS = 4;              // output rows per band
 __global__ __launch_bounds__(256) void gfuse_imgmom_kernel(const float* __restrict__ img4, int H,
                                                            int W, double* __restrict__ part) {
   extern __shared__ float tile[];  // [IM_ROWS + 2][W + 2][3], then the fp64 reduction
-  const int b = blockIdx.y, band = blockIdx.x, r0 = band * IM_ROWS;
+  const int b = blockIdx.y;
   const int TW = W + 2, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;  // 4 waves
   const float* ib = img4 + (long long)b * H * W * 4;
+  const int nband = (H + IM_ROWS - 1) / IM_ROWS;
+  // a block walks bands blockIdx.x, + gridDim.x, ...: each band's fp32 MFMA sum
+  // is added into per-lane fp64 totals (the per-band rounding of one band /
+  // block; few blocks leave the CUs to the main stream's kernels)
+  double tot[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) tot[r] = 0.0;
+  for (int band = blockIdx.x; band < nband; band += gridDim.x) {
+  const int r0 = band * IM_ROWS;
+  __syncthreads();  // the previous band's tile is consumed
   for (int i = threadIdx.x; i < (IM_ROWS + 2) * TW; i += blockDim.x) {
     const int ty = i / TW, tx = i - ty * TW;
     const int y = r0 - 1 + ty, x = tx - 1;
@@ -216,16 +226,19 @@ __global__ __launch_bounds__(256) void gfuse_imgmom_kernel(const float* __restri
       acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(v, v, acc0, 0, 0, 0);
     }
   }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) tot[r] += (double)acc0[r] + (double)acc1[r];
+  }
   __syncthreads();  // the tile is dead: reuse LDS for the wave sum
   double* red = reinterpret_cast<double*>(tile);  // [4 waves][32][32]
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int gi = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5), gj = lane & 31;
-    red[(wave * IM_G + gi) * IM_G + gj] = (double)acc0[r] + (double)acc1[r];
+    red[(wave * IM_G + gi) * IM_G + gj] = tot[r];
   }
   __syncthreads();
   for (int e = threadIdx.x; e < IM_G * IM_G; e += blockDim.x)
-    part[((long long)b * gridDim.x + band) * IM_G * IM_G + e] =
+    part[((long long)b * gridDim.x + blockIdx.x) * IM_G * IM_G + e] =
         (red[e] + red[IM_G * IM_G + e]) + (red[2 * IM_G * IM_G + e] + red[3 * IM_G * IM_G + e]);
 }
 
@@ -673,8 +686,14 @@ int pf_gfuse_conv(const float* img4, const float* c, int ccs, int n, int H, int 
     hipLaunchKernelGGL(gfuse_wsplit_kernel, dim3((tot + 255) / 256), dim3(256), 0, st, wc, n,
                        wplanes);
     const int nt8 = ((W + G8_TC - 1) / G8_TC) * ((H + G8_TR - 1) / G8_TR);
-    // persistent blocks: ~2 per CU over the batch, each on one image's tiles
-    const int per_img = std::max(1, std::min(nt8, (512 + n - 1) / n));
+    // persistent blocks (one image's tiles each): POSFEAT_GFUSE_BLOCKS in
+    // total over the batch (default 512); fewer leave CUs to the main stream
+    static const int tot_blocks = [] {
+      const char* e = getenv("POSFEAT_GFUSE_BLOCKS");
+      const int v = e ? atoi(e) : 64;  // r3w sweep: 512 820, 96 830, 64 841, 48 841, 32 837 img/s
+      return v > 0 ? v : 64;
+    }();
+    const int per_img = std::max(1, std::min(nt8, (tot_blocks + n - 1) / n));
     hipLaunchKernelGGL(gfuse_conv5_k80_kernel, dim3(per_img, n), dim3(512), 0, st, img4, H, W,
                        wplanes, bc, y, ycs);
   } else if (pf_conv_precision() >= 1)  // bf16x6 products (the default conv arithmetic)
@@ -703,7 +722,14 @@ int pf_gfuse_imgstats(const float* img4, int n, int H, int W, const float* w1_pa
                       const float* b1, float* mean, float* rstd, void* ws, size_t ws_bytes,
                       hipStream_t st, double* gram) {
   if (!ws || ws_bytes < pf_gfuse_imgstats_ws_bytes(n, H)) return POSFEAT_E_WORKSPACE;
-  const int nband = (H + IM_ROWS - 1) / IM_ROWS;
+  // blocks per image (POSFEAT_IMGMOM_BLOCKS; default one per band -- r3x: 8 or
+  // 16 band-looping blocks per image were no faster); partials = blocks
+  static const int per_img_env = [] {
+    const char* e = getenv("POSFEAT_IMGMOM_BLOCKS");
+    return e ? atoi(e) : 0;
+  }();
+  const int nb_all = (H + IM_ROWS - 1) / IM_ROWS;
+  const int nband = per_img_env > 0 ? std::max(1, std::min(nb_all, per_img_env)) : nb_all;
   const size_t lds = std::max((size_t)(IM_ROWS + 2) * (W + 2) * 3 * sizeof(float),
                               (size_t)4 * IM_G * IM_G * sizeof(double));
   if (lds > 160 * 1024 || W % 2) return POSFEAT_E_UNSUPPORTED;
