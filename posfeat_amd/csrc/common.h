@@ -64,3 +64,22 @@ __device__ __forceinline__ void pf_split3x4(const f32x4& v, uint2& h, uint2& m, 
   pf_split3_pair(v.x, v.y, h.x, m.x, l.x);
   pf_split3_pair(v.z, v.w, h.y, m.y, l.y);
 }
+
+// value of the x2 bilinear upsample (align_corners=True, F.interpolate as
+// DescNet.py:187 calls it) of an h x w NHWC map at output pixel (oy, ox), 4
+// channels from `base` (= map + image offset + channel offset); sh, sw =
+// (h-1)/(2h-1), (w-1)/(2w-1).  Shared by the upsample kernel and the Winograd
+// input transform that reads the low-res map directly: the same arithmetic.
+__device__ __forceinline__ f32x4 pf_up2ac_at(const float* base, int h, int w, int cs, float sh,
+                                             float sw, int oy, int ox) {
+#pragma clang fp contract(off)  // one fixed mul/add sequence wherever it is inlined
+  const float ry = sh * oy, rx = sw * ox;
+  const int y0 = (int)ry, x0 = (int)rx;
+  const int y1 = y0 + (y0 < h - 1 ? 1 : 0), x1 = x0 + (x0 < w - 1 ? 1 : 0);
+  const float ly = ry - y0, lx = rx - x0, hy = 1.f - ly, hx = 1.f - lx;
+  const f32x4 v00 = *reinterpret_cast<const f32x4*>(base + ((long long)y0 * w + x0) * cs);
+  const f32x4 v01 = *reinterpret_cast<const f32x4*>(base + ((long long)y0 * w + x1) * cs);
+  const f32x4 v10 = *reinterpret_cast<const f32x4*>(base + ((long long)y1 * w + x0) * cs);
+  const f32x4 v11 = *reinterpret_cast<const f32x4*>(base + ((long long)y1 * w + x1) * cs);
+  return hy * (hx * v00 + lx * v01) + ly * (hx * v10 + lx * v11);
+}

@@ -429,10 +429,30 @@ long long wino_u_offset(const std::string& name, bool planes) {
   return -1;
 }
 
+// up2: x is the (h/2, w/2) map and the conv input its x2 align_corners
+// upsample (DescNet.py:182-190 upconv), interpolated inside the F(4x4)
+// input transform (POSFEAT_UP2FUSE=0: materialised by the upsample kernel);
+// xup: the full-res buffer for the unfused forms
+bool up2fuse_on() {
+  static const bool on = [] {
+    const char* e = getenv("POSFEAT_UP2FUSE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 int conv3x3(Ctx& c, const std::string& name, const float* x, int n, int h, int w, int xcs, float* y,
-            int ycs, int act) {
+            int ycs, int act, int up2 = 0, float* xup = nullptr) {
   posfeat_model* m = c.m;
   const long long uo = wino_u_offset(name, m->bf6p || m->wsplit);
+  const bool f4ok = m->wino && uo >= 0 && h % 4 == 0 && w % 4 == 0 &&
+                    !(getenv("POSFEAT_WINO") && getenv("POSFEAT_WINO")[0] == '1');
+  if (up2 && !(f4ok && up2fuse_on())) {  // materialise the upsample, then the plain conv
+    PF_TRY(timed(c, "upsample2x", 0, [&] {
+      return pf_upsample2x_ac(x, n, h / 2, w / 2, xcs, xcs, xup, xcs, c.st);
+    }));
+    return conv3x3(c, name, xup, n, h, w, xcs, y, ycs, act);
+  }
   if (!m->wino || uo < 0 || (h & 1) || (w & 1))
     return conv(c, name, x, n, h, w, xcs, y, ycs, 1, act);
   const Spec* s = specs().find(name);
@@ -451,7 +471,7 @@ int conv3x3(Ctx& c, const std::string& name, const float* x, int n, int h, int w
   auto stage = [&](int st_bits) {
     return pf_wino_conv(x, xcs, n, h, w, s->cin, U, c.Bi(name), s->cout, act, y, ycs,
                         c.f(m->wino_ws), m->wino_ws.floats * sizeof(float), c.st, st_bits,
-                        m->bf6p ? 2 : m->wsplit ? 1 : 0);
+                        m->bf6p ? 2 : m->wsplit ? 1 : 0, up2);
   };
   PF_TRY(timed(c, "wino:in:" + name, 0, [&] { return stage(1); }));
   PF_TRY(timed(c, "conv:" + name + ".wino", 2.0 * T * (f4 ? 36 : 16) * s->cin * s->cout,
@@ -862,15 +882,13 @@ int forward(Ctx& c, const float* img, posfeat_extract_out* out, int mode, const 
   if (side && side_at == 3) PF_TRY(image_branch(c, img4));
   PF_TRY(conv(c, "conv_coarse", c.f(m->l3out), B, h16, w16, 1024, c.f(m->gmap), 128, 1,
               POSFEAT_ACT_ELU));
-  PF_TRY(timed(c, "upsample2x", 0, [&] {
-    return pf_upsample2x_ac(c.f(m->l3out), B, h16, w16, 1024, 1024, c.f(m->up3), 1024, c.st);
-  }));
-  PF_TRY(conv3x3(c, "upconv3.conv", c.f(m->up3), B, h8, w8, 1024, cat3, 1024, POSFEAT_ACT_ELU));
+  // upconv (DescNet.py:182-190): x2 upsample + conv, the upsample inside
+  // the Winograd input transform
+  PF_TRY(conv3x3(c, "upconv3.conv", c.f(m->l3out), B, h8, w8, 1024, cat3, 1024, POSFEAT_ACT_ELU,
+                 1, c.f(m->up3)));
   PF_TRY(conv3x3(c, "iconv3", cat3, B, h8, w8, 1024, c.f(m->d3), 512, POSFEAT_ACT_ELU));
-  PF_TRY(timed(c, "upsample2x", 0, [&] {
-    return pf_upsample2x_ac(c.f(m->d3), B, h8, w8, 512, 512, c.f(m->up2), 512, c.st);
-  }));
-  PF_TRY(conv3x3(c, "upconv2.conv", c.f(m->up2), B, h4, w4, 512, cat2, 512, POSFEAT_ACT_ELU));
+  PF_TRY(conv3x3(c, "upconv2.conv", c.f(m->d3), B, h4, w4, 512, cat2, 512, POSFEAT_ACT_ELU, 1,
+                 c.f(m->up2)));
   PF_TRY(conv3x3(c, "iconv2", cat2, B, h4, w4, 512, c.f(m->d2), 256, POSFEAT_ACT_ELU));
   PF_TRY(conv(c, "conv_fine", c.f(m->d2), B, h4, w4, 256, headcat, 192, 1, POSFEAT_ACT_ELU));
   }

@@ -65,9 +65,11 @@ int pf_wino_weights_hw(const float* wpk, int Cout, int Cin, int h, int w, float*
                        hipStream_t st, bool bf6p = false);
 size_t pf_wino_weights_floats_bf6p(int Cin, int Cout);
 // stages: bit 0 input transform, bit 1 the batched GEMMs, bit 2 output transform
+// up2: x is the (h/2, w/2) map; the conv input is its x2 align_corners
+// upsample, interpolated inside the input transform (F(4x4) only)
 int pf_wino_conv(const float* x, int xcs, int n, int h, int w, int Cin, const float* U,
                  const float* bias, int Cout, int act, float* y, int ycs, void* ws, size_t ws_bytes,
-                 hipStream_t st, int stages = 7, int planes = 0);
+                 hipStream_t st, int stages = 7, int planes = 0, int up2 = 0);
 // head.conv2's G part as one per-image 5x5 conv of the image (gfuse.hip)
 size_t pf_gfuse_weights_floats(int n);
 int pf_gfuse_weights(const float* w2_packed, const float* b2, const float* w1_packed,

@@ -116,16 +116,8 @@ __global__ void upsample2x_ac_kernel(const float* __restrict__ x, int n, int h, 
     p /= ow;
     const int oy = (int)(p % oh);
     const int b = (int)(p / oh);
-    const float ry = sh * oy, rx = sw * ox;
-    const int y0 = (int)ry, x0 = (int)rx;
-    const int y1 = y0 + (y0 < h - 1 ? 1 : 0), x1 = x0 + (x0 < w - 1 ? 1 : 0);
-    const float ly = ry - y0, lx = rx - x0, hy = 1.f - ly, hx = 1.f - lx;
-    const float* base = x + (long long)b * h * w * csi + q * 4;
-    const f32x4 v00 = *reinterpret_cast<const f32x4*>(base + ((long long)y0 * w + x0) * csi);
-    const f32x4 v01 = *reinterpret_cast<const f32x4*>(base + ((long long)y0 * w + x1) * csi);
-    const f32x4 v10 = *reinterpret_cast<const f32x4*>(base + ((long long)y1 * w + x0) * csi);
-    const f32x4 v11 = *reinterpret_cast<const f32x4*>(base + ((long long)y1 * w + x1) * csi);
-    const f32x4 o = hy * (hx * v00 + lx * v01) + ly * (hx * v10 + lx * v11);
+    const f32x4 o =
+        pf_up2ac_at(x + (long long)b * h * w * csi + q * 4, h, w, csi, sh, sw, oy, ox);
     *reinterpret_cast<f32x4*>(y + (((long long)b * oh + oy) * ow + ox) * cso + q * 4) = o;
   }
 }

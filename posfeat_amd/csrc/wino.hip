@@ -214,11 +214,19 @@ __global__ void wino4_weights_kernel(const float* __restrict__ wpk, int Cout, in
 
 // V[xi][tile][c], 6x6 patch at rows 4ty-1.., cols 4tx-1..; Vb != nullptr: V
 // as three bf16 planes (plane stride 36 T C) for the bf16x6 GEMM instead
+// up2: x is the h/2 x w/2 map whose x2 align_corners upsample is the conv
+// input (upconv, DescNet.py:182-190): its values are interpolated here
+// (pf_up2ac_at, the upsample kernel's own arithmetic) instead of read from a
+// materialised upsample
 __global__ __launch_bounds__(256) void wino4_input_kernel(const float* __restrict__ x, int xcs,
                                                           int n, int h, int w, int c4n,
                                                           float* __restrict__ V, int clamp = 0,
-                                                          unsigned short* __restrict__ Vb = nullptr) {
+                                                          unsigned short* __restrict__ Vb = nullptr,
+                                                          int up2 = 0) {
   const int th = h / 4, tw = w / 4;
+  const int h2 = h / 2, w2 = w / 2;
+  const float sh = h > 1 ? (float)(h2 - 1) / (float)(h - 1) : 0.f;
+  const float sw = w > 1 ? (float)(w2 - 1) / (float)(w - 1) : 0.f;
   const long long T = (long long)n * th * tw;
   const long long total = T * c4n;
   const int C = c4n * 4;
@@ -246,7 +254,10 @@ __global__ __launch_bounds__(256) void wino4_input_kernel(const float* __restric
         if (clamp) xx = min(max(xx, 0), w - 1);
         f32x4 v = {0.f, 0.f, 0.f, 0.f};
         if ((unsigned)yy < (unsigned)h && (unsigned)xx < (unsigned)w)
-          v = *reinterpret_cast<const f32x4*>(x + (((long long)b * h + yy) * w + xx) * xcs + q * 4);
+          v = up2 ? pf_up2ac_at(x + (long long)b * h2 * w2 * xcs + q * 4, h2, w2, xcs, sh, sw, yy,
+                                xx)
+                  : *reinterpret_cast<const f32x4*>(x + (((long long)b * h + yy) * w + xx) * xcs +
+                                                    q * 4);
         d[c] = v;
       }
 #pragma unroll
@@ -664,8 +675,9 @@ int pf_wino_weights(const float* wpk, int Cout, int Cin, float* U, hipStream_t s
 static int wino_conv_impl(const float* x, int xcs, int n, int h, int w, int Cin, const float* U,
                           bool U_is_f4, const float* bias, int Cout, int act, float* y, int ycs,
                           void* ws, size_t ws_bytes, hipStream_t st, int stages = 7,
-                          int planes = 0) {
+                          int planes = 0, int up2 = 0) {
   const bool bf6p = planes == 2;
+  if (up2 && !(use_f4(h, w) && U_is_f4 && h % 2 == 0 && w % 2 == 0)) return POSFEAT_E_UNSUPPORTED;
   if ((h & 1) || (w & 1) || Cin % 32 || Cout % 4 || xcs % 4 || ycs % 4 || n <= 0)
     return POSFEAT_E_INVALID;
   if (ws_bytes < pf_wino_ws_bytes(n, h, w, Cin, Cout)) return POSFEAT_E_WORKSPACE;
@@ -678,7 +690,7 @@ static int wino_conv_impl(const float* x, int xcs, int n, int h, int w, int Cin,
         reinterpret_cast<float*>(static_cast<char*>(ws) + pf_align(36 * T4 * Cin * 6, 256));
     if (stages & 1) {
       hipLaunchKernelGGL(wino4_input_kernel, dim3(grid_for(T4 * (Cin / 4), 256)), dim3(256), 0, st,
-                         x, xcs, n, h, w, Cin / 4, nullptr, 0, Vb);
+                         x, xcs, n, h, w, Cin / 4, nullptr, 0, Vb, up2);
       PF_CHECK_LAUNCH();
     }
     if (stages & 2)
@@ -699,7 +711,7 @@ static int wino_conv_impl(const float* x, int xcs, int n, int h, int w, int Cin,
         reinterpret_cast<float*>(static_cast<char*>(ws) + pf_align(36 * T4 * Cin * 4, 256));
     if (stages & 1) {
       hipLaunchKernelGGL(wino4_input_kernel, dim3(grid_for(T4 * (Cin / 4), 256)), dim3(256), 0, st,
-                         x, xcs, n, h, w, Cin / 4, V4, 0);
+                         x, xcs, n, h, w, Cin / 4, V4, 0, nullptr, up2);
       PF_CHECK_LAUNCH();
     }
     if (stages & 2)  // planes == 1: U holds its bf16 planes (pre-split bf16x6 tiles)
@@ -738,9 +750,9 @@ static int wino_conv_impl(const float* x, int xcs, int n, int h, int w, int Cin,
 // U from pf_wino_weights_hw(.., h, w, ..): the variant is chosen from (h, w)
 int pf_wino_conv(const float* x, int xcs, int n, int h, int w, int Cin, const float* U,
                  const float* bias, int Cout, int act, float* y, int ycs, void* ws, size_t ws_bytes,
-                 hipStream_t st, int stages, int planes) {
+                 hipStream_t st, int stages, int planes, int up2) {
   return wino_conv_impl(x, xcs, n, h, w, Cin, U, true, bias, Cout, act, y, ycs, ws, ws_bytes, st,
-                        stages, planes);
+                        stages, planes, up2);
 }
 
 namespace {

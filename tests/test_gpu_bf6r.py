@@ -1,4 +1,6 @@
-"""conv_bf6r_kernel (pre-split weights, A straight to registers) against
+"""Switches whose two forms must give BIT-identical engine outputs.
+
+conv_bf6r_kernel (pre-split weights, A straight to registers) against
 conv_bf6b_kernel (A staged through LDS): the same bf16x6 products in the same
 order, so the engine's outputs must be BIT-identical with POSFEAT_BF6R=0/1
 (the switch is read once per process: each run is a child process).  The
@@ -36,6 +38,16 @@ def _run(tmp_path, env_extra, tag):
     subprocess.run([sys.executable, "-c", CODE % {"root": ROOT, "out": out}], env=env,
                    check=True, timeout=240)
     return np.load(out)
+
+
+def test_fused_upsample_bit_identical(tmp_path):
+    """the decoder's x2 upsample interpolated inside the Winograd input
+    transform (pf_up2ac_at: the upsample kernel's own arithmetic) equals the
+    materialised upsample + transform (POSFEAT_UP2FUSE=0) bit for bit"""
+    ref = _run(tmp_path, {"POSFEAT_UP2FUSE": "0"}, "u0")
+    got = _run(tmp_path, {"POSFEAT_UP2FUSE": "1"}, "u1")
+    for k in ("lp", "lm", "gm"):
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
 
 
 def test_bf6r_bit_identical_to_bf6b(tmp_path):
