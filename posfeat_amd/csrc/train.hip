@@ -251,6 +251,202 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradArgs a) {
   }
 }
 
+// bf16x6 variant of the row-tile weight gradient (Cin % 32 == 0, 128 x 128
+// tiles): the same tile / split / partial layout, products on the bf16
+// matrix cores (conv.hip split3: six products per fp32 pair, per-product
+// error below one fp32 rounding).  The MFMA reduction index is the PIXEL,
+// which is the row index of dy and of the im2col rows in memory, so the
+// operands cannot be DMA'd as they lie: each thread global-loads 4 pixels x 4
+// couts of dy and 4 pixels x 4 k of the im2col (one chunk ahead, in
+// registers), splits every value ONCE into three bf16 terms and writes them
+// pixel-contiguous into LDS planes [plane][co or k][32 px] (80-B rows:
+// conflict-free ds_read_b128 per 16 lanes), from which each lane reads its
+// 8 consecutive pixels per k16 group directly.  The split is per element, not
+// per wave read: 176 VALU per 48 MFMAs per wave.
+constexpr int WB_PP = 40;  // LDS row pitch (bf16): 32 pixels + 8
+
+__global__ __launch_bounds__(256) void conv_wgrad_bf6_kernel(WgradArgs a) {
+  constexpr int BM = 128, BN = 128, WN = 2, TM = 64, TN = 64, MI = 2, NI = 2;
+  __shared__ __attribute__((aligned(16))) unsigned short As[3 * BM * WB_PP];
+  __shared__ __attribute__((aligned(16))) unsigned short Bs[3 * BN * WB_PP];
+  __shared__ float red[8 * BM];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  int bid = blockIdx.x;
+  {
+    const int nwg = gridDim.x, q = nwg >> 3, r = nwg & 7, xcd = bid & 7, slot = bid >> 3;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+  }
+  const int split = bid / a.ntiles, tile = bid - split * a.ntiles;
+  const int tm = tile / a.tiles_n, tn = tile - tm * a.tiles_n;
+  const int co0 = tm * BM, n0 = tn * BN;
+  if (gridDim.y > 1) {
+    const long long z = blockIdx.y;
+    a.dy += z * a.bdy;
+    a.x += z * a.bx;
+    a.part += z * a.bpart;
+    if ((int)z != a.zb) a.partb = nullptr;
+  }
+  const int c_begin = (int)((long long)a.nchunks * split / a.nsplit);
+  const int c_end = (int)((long long)a.nchunks * (split + 1) / a.nsplit);
+  // staging role: quad q (4 couts of dy / 4 k of the im2col), pixel group pg (4 px)
+  const int q = tid & 31, pg = tid >> 5;
+  const bool aok = co0 + 4 * q < a.Cout;
+  const int k = n0 + 4 * q;  // 4 consecutive k share one tap (Cin % 32 == 0)
+  const int ntap = a.KH * a.KW;
+  const int cidx = k >> 5, slab = cidx / ntap, tap = cidx - slab * ntap;
+  const bool kok = k < a.Kpad;
+  const int kdy = tap / a.KW - a.pad, kdx = tap - (tap / a.KW) * a.KW - a.pad;
+  const int kci = slab * 32 + (k & 31);
+  const int HW = a.H * a.W, s = a.stride;
+  // pixel (img, oh, ow) of this thread's first pixel of the current chunk
+  int p_img, p_oh, p_ow;
+  {
+    const long long m = (long long)c_begin * WG_RB + pg * 4;
+    p_img = (int)(m / HW);
+    const int rem = (int)(m - (long long)p_img * HW);
+    p_oh = rem / a.W;
+    p_ow = rem - p_oh * a.W;
+  }
+  f32x4 ra[4], rb[4];
+  float bsum[4] = {0.f, 0.f, 0.f, 0.f};
+  const bool do_bias = a.partb && tn == 0;
+  auto load = [&](int c) {
+    const long long m0 = (long long)c * WG_RB + pg * 4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      int img = p_img, oh = p_oh, ow = p_ow + j;
+      if (ow >= a.W) {  // W >= 4: at most one wrap
+        ow -= a.W;
+        if (++oh == a.H) {
+          oh = 0;
+          ++img;
+        }
+      }
+      const bool mok = m0 + j < a.M;
+      ra[j] = mok && aok ? *reinterpret_cast<const f32x4*>(a.dy + (m0 + j) * a.ldy + co0 + 4 * q)
+                         : f32x4{0.f, 0.f, 0.f, 0.f};
+      const int iy = s * oh + kdy, ix = s * ow + kdx;
+      rb[j] = mok && kok && (unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win
+                  ? *reinterpret_cast<const f32x4*>(
+                        a.x + (((long long)img * a.Hin + iy) * a.Win + ix) * a.xcs + kci)
+                  : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    // advance to the next chunk's first pixel (+32)
+    p_ow += WG_RB;
+    while (p_ow >= a.W) {
+      p_ow -= a.W;
+      if (++p_oh == a.H) {
+        p_oh = 0;
+        ++p_img;
+      }
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const f32x4 va = {ra[0][e], ra[1][e], ra[2][e], ra[3][e]};
+      const f32x4 vb = {rb[0][e], rb[1][e], rb[2][e], rb[3][e]};
+      uint2 h, m, l;
+      pf_split3x4(va, h, m, l);
+      unsigned short* pa = As + (4 * q + e) * WB_PP + pg * 4;
+      *reinterpret_cast<uint2*>(pa) = h;
+      *reinterpret_cast<uint2*>(pa + BM * WB_PP) = m;
+      *reinterpret_cast<uint2*>(pa + 2 * BM * WB_PP) = l;
+      pf_split3x4(vb, h, m, l);
+      unsigned short* pb = Bs + (4 * q + e) * WB_PP + pg * 4;
+      *reinterpret_cast<uint2*>(pb) = h;
+      *reinterpret_cast<uint2*>(pb + BN * WB_PP) = m;
+      *reinterpret_cast<uint2*>(pb + 2 * BN * WB_PP) = l;
+      if (do_bias) bsum[e] += (va.x + va.y) + (va.z + va.w);
+    }
+  };
+
+  f32x16 acc[MI][NI];
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
+  typedef __bf16 wb_bf16x8 __attribute__((ext_vector_type(8)));
+  typedef unsigned wb_u32x4 __attribute__((ext_vector_type(4)));
+  auto mf = [](const wb_u32x4& x, const wb_u32x4& y, const f32x16& c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(wb_bf16x8, x),
+                                                   __builtin_bit_cast(wb_bf16x8, y), c, 0, 0, 0);
+  };
+  const int r32 = lane & 31, hh = lane >> 5;
+  if (c_begin < c_end) load(c_begin);
+  for (int c = c_begin; c < c_end; ++c) {
+    __syncthreads();  // the previous chunk's planes are consumed
+    store();
+    __syncthreads();
+    if (c + 1 < c_end) load(c + 1);  // in flight during the MFMAs
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      wb_u32x4 ah[MI], am[MI], al[MI], bh[NI], bm[NI], bl[NI];
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi) {
+        const unsigned short* p = As + (wm * TM + mi * 32 + r32) * WB_PP + 16 * g + 8 * hh;
+        ah[mi] = *reinterpret_cast<const wb_u32x4*>(p);
+        am[mi] = *reinterpret_cast<const wb_u32x4*>(p + BM * WB_PP);
+        al[mi] = *reinterpret_cast<const wb_u32x4*>(p + 2 * BM * WB_PP);
+      }
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) {
+        const unsigned short* p = Bs + (wn * TN + ni * 32 + r32) * WB_PP + 16 * g + 8 * hh;
+        bh[ni] = *reinterpret_cast<const wb_u32x4*>(p);
+        bm[ni] = *reinterpret_cast<const wb_u32x4*>(p + BN * WB_PP);
+        bl[ni] = *reinterpret_cast<const wb_u32x4*>(p + 2 * BN * WB_PP);
+      }
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) {
+          f32x16 cc = acc[mi][ni];
+          cc = mf(ah[mi], bh[ni], cc);
+          cc = mf(ah[mi], bm[ni], cc);
+          cc = mf(am[mi], bh[ni], cc);
+          cc = mf(ah[mi], bl[ni], cc);
+          cc = mf(al[mi], bh[ni], cc);
+          cc = mf(am[mi], bm[ni], cc);
+          acc[mi][ni] = cc;
+        }
+    }
+  }
+  // raw partials: row (cout) = (r&3) + 8(r>>2) + 4(lane>>5), col = lane&31
+  float* pp = a.part + (long long)split * a.Cout * a.Kpad;
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) {
+      const int kk = n0 + wn * TN + ni * 32 + r32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int co = co0 + wm * TM + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        if (co < a.Cout && kk < a.Kpad) pp[(long long)co * a.Kpad + kk] = acc[mi][ni][r];
+      }
+    }
+  if (do_bias) {  // sum the 8 pixel groups of each cout in a fixed order
+#pragma unroll
+    for (int e = 0; e < 4; ++e) red[pg * BM + 4 * q + e] = bsum[e];
+    __syncthreads();
+    if (tid < BM && co0 + tid < a.Cout) {
+      float t = 0.f;
+      for (int g2 = 0; g2 < 8; ++g2) t += red[g2 * BM + tid];
+      a.partb[(long long)split * a.Cout + co0 + tid] = t;
+    }
+  }
+}
+
+bool wgrad_bf6_on() {
+  static const bool off = [] {
+    const char* e = getenv("POSFEAT_WGRAD_BF6");
+    return e && e[0] == '0';
+  }();
+  return pf_conv_precision() >= 1 && !off;
+}
+
 // Halo variant for 3x3 stride-1 convs with Cin % 32 == 0 (head.conv1/conv2).
 // Work item = one 32-pixel row segment (img, y, x0..x0+31) x one 32-channel
 // input slab x BM couts.  Per segment the dy rows [32 px][BM] and the input
@@ -903,7 +1099,9 @@ int pf_conv_wgrad(const float* dy, int ldy, const float* x, int xcs, int n, int 
       hipLaunchKernelGGL(conv_wgrad_halo_kernel<4>, grid, dim3(256), 0, st, a);
     else
       hipLaunchKernelGGL(conv_wgrad_halo_kernel<2>, grid, dim3(128), 0, st, a);
-  } else if (p.BM == 128 && p.BN == 128)
+  } else if (p.BM == 128 && p.BN == 128 && Cin % 32 == 0 && wgrad_bf6_on())
+    hipLaunchKernelGGL(conv_wgrad_bf6_kernel, grid, dim3(256), 0, st, a);
+  else if (p.BM == 128 && p.BN == 128)
     hipLaunchKernelGGL((conv_wgrad_kernel<128, 128>), grid, dim3(256), 0, st, a);
   else if (p.BM == 128)
     hipLaunchKernelGGL((conv_wgrad_kernel<128, 64>), grid, dim3(256), 0, st, a);
@@ -1035,8 +1233,11 @@ int pf_wgrad_gemm_batched(const float* dy, int ldy, long long sdy, const float* 
   a.bx = sx;
   a.bpart = (long long)nsplit * Cout * Cin;
   a.zb = zb;
-  hipLaunchKernelGGL((conv_wgrad_kernel<128, 128>), dim3(a.ntiles * nsplit, nb), dim3(256), 0, st,
-                     a);
+  if (wgrad_bf6_on())
+    hipLaunchKernelGGL(conv_wgrad_bf6_kernel, dim3(a.ntiles * nsplit, nb), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((conv_wgrad_kernel<128, 128>), dim3(a.ntiles * nsplit, nb), dim3(256), 0,
+                       st, a);
   PF_CHECK_LAUNCH();
   return POSFEAT_OK;
 }

@@ -62,19 +62,22 @@ def _gpu_grads(gpu, monkeypatch, flag, imgs, dlp):
     return lp, got, x
 
 
-def _oracle_grads(imgs, dlp, x):
-    """the reference KeypointDet in fp64 on the ENGINE's backbone maps x"""
+def _oracle_grads(imgs, dlp, x, dtype=torch.float64):
+    """the reference KeypointDet (fp64, or fp32 for the noise floor) on the
+    ENGINE's backbone maps x"""
     from oracle.model_ref import keypointdet_forward
     from posfeat_amd.weights import seeded_state_dicts
     _, hd = seeded_state_dicts(0)
-    x = x.double()
-    params = {k: v.clone().double().requires_grad_(True) for k, v in hd.items()}
-    lp = keypointdet_forward(params, x, imgs.double())
-    grads = torch.autograd.grad(lp, [params[k] for k in hd], dlp.double())
-    return {k: g.numpy() for k, g in zip(hd, grads)}
+    x = x.to(dtype)
+    params = {k: v.clone().to(dtype).requires_grad_(True) for k, v in hd.items()}
+    lp = keypointdet_forward(params, x, imgs.to(dtype))
+    grads = torch.autograd.grad(lp, [params[k] for k in hd], dlp.to(dtype))
+    return {k: g.double().numpy() for k, g in zip(hd, grads)}
 
 
-def _compare(got, ref, what, rel):
+def _compare(got, ref, what, rel, floor=None):
+    """per tensor max|got - ref| <= rel * max|ref|, or <= 3x the reference's
+    own fp32 error (floor[k], absolute) where that is larger"""
     bad = []
     for k in KEYS:
         g, r = np.asarray(got[k]).reshape(-1), np.asarray(ref[k]).reshape(-1)
@@ -84,6 +87,8 @@ def _compare(got, ref, what, rel):
             err, lim = np.abs(g - r).max(), 1e-5 * max(1.0, wmax)
         else:
             err, lim = np.abs(g - r).max(), rel * max(np.abs(r).max(), 1e-6)
+            if floor is not None:
+                lim = max(lim, 3.0 * floor[k])
         print("%s %-16s err %.3e  limit %.3e" % (what, k, err, lim))
         if err > lim:
             bad.append(k)
@@ -98,15 +103,22 @@ def test_traintap_backward(gpu, monkeypatch, shape):
     lp_tap, g_tap, _ = _gpu_grads(gpu, monkeypatch, "1", imgs, dlp)
     np.testing.assert_allclose(lp_tap, lp_old, rtol=1e-4, atol=1e-5)
     g_or = _oracle_grads(imgs, dlp, x)
+    # the same reference in fp32 (torch CPU): its own error vs fp64 is the
+    # noise floor of this input (r4c, 2 x 96 x 208: 0.70 on conv1.weight of
+    # scale 176 -- a badly conditioned IN channel -- which the GPU matches)
+    g_32 = _oracle_grads(imgs, dlp, x, torch.float32)
+    _compare(g_32, g_or, "cpu32-vs-ref64", 2e-3)
+    floor = {k: float(np.abs(np.asarray(g_32[k]) - np.asarray(g_or[k])).max()) for k in KEYS}
     # The weight gradients contract zero-mean IN-backward fields against
     # inputs with large means (heavy cancellation): in fp32 BOTH GPU paths sit
     # up to ~8e-4 of a tensor's scale from the fp64 reference (measured r3h:
     # conv2 / convimg weights at 2 x 96 x 208, the two paths within 5 % of
-    # each other's error), so the bound is the golden test's 2e-3; the two
+    # each other's error), so the bound is the golden test's 2e-3 -- or 3x the
+    # fp32 reference's own error on this input where that is larger; the two
     # GPU paths differ by summation order only (<= 4e-4 measured)
     bad = _compare(g_tap, g_old, "tap-vs-old", 1e-3)
-    bad += _compare(g_tap, g_or, "tap-vs-ref64", 2e-3)
-    bad += ["old:" + k for k in _compare(g_old, g_or, "old-vs-ref64", 2e-3)]
+    bad += _compare(g_tap, g_or, "tap-vs-ref64", 2e-3, floor)
+    bad += ["old:" + k for k in _compare(g_old, g_or, "old-vs-ref64", 2e-3, floor)]
     assert not bad, bad
 
 

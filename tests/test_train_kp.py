@@ -139,33 +139,39 @@ def test_gpu_train_step_deterministic_and_sgd(gpu):
 @pytest.mark.gpu
 def test_gpu_wgrad_vs_torch(gpu):
     """posfeat_conv_wgrad (MFMA weight gradient, packed K order) against torch's
-    conv2d weight gradient in fp64, for the three head layer shapes."""
+    conv2d weight gradient in fp64: the three head layer shapes and two 1x1
+    shapes on the bf16x6 row tiles."""
     import ctypes
     from posfeat_amd import _lib, weights
     from posfeat_amd._lib import check, lib, ptr, stream_ptr
     rs = np.random.RandomState(0)
-    for (n, h, w, cin, cout) in ((2, 20, 36, 256, 128), (1, 17, 23, 192, 192), (2, 24, 40, 4, 64)):
+    # 3x3: the halo kernels (and Cin = 4: the fp32 row tiles); 1x1 with 128 x
+    # 128 tiles: the bf16x6 row-tile kernel (conv_wgrad_bf6_kernel), incl. a
+    # ragged last pixel chunk and several pixel splits
+    for (n, h, w, cin, cout, k) in ((2, 20, 36, 256, 128, 3), (1, 17, 23, 192, 192, 3),
+                                    (2, 24, 40, 4, 64, 3), (2, 20, 37, 256, 128, 1),
+                                    (1, 60, 80, 512, 256, 1)):
         x = rs.randn(n, cin, h, w).astype(np.float32)
         if cin == 4:
             x[:, 3] = 0.0
         dy = rs.randn(n, cout, h, w).astype(np.float32)
         xt = torch.from_numpy(x).double().requires_grad_(True)
-        wt = torch.zeros(cout, cin, 3, 3, dtype=torch.float64, requires_grad=True)
-        y = torch.nn.functional.conv2d(xt, wt, padding=1)
+        wt = torch.zeros(cout, cin, k, k, dtype=torch.float64, requires_grad=True)
+        y = torch.nn.functional.conv2d(xt, wt, padding=(k - 1) // 2)
         y.backward(torch.from_numpy(dy).double())
         ref_w = wt.grad.numpy()
         ref_b = dy.astype(np.float64).sum((0, 2, 3))
         xd = torch.from_numpy(np.ascontiguousarray(x.transpose(0, 2, 3, 1))).to(gpu)
         dyd = torch.from_numpy(np.ascontiguousarray(dy.transpose(0, 2, 3, 1))).to(gpu)
-        kpad = lib().posfeat_conv_packed_k(cin, 3, 3)
+        kpad = lib().posfeat_conv_packed_k(cin, k, k)
         dw = torch.empty(cout * kpad, device=gpu)
         db = torch.empty(cout, device=gpu)
-        need = lib().posfeat_conv_wgrad_workspace(n, h, w, cin, cout, 3, 3)
+        need = lib().posfeat_conv_wgrad_workspace(n, h, w, cin, cout, k, k)
         ws = torch.empty(need, dtype=torch.uint8, device=gpu)
-        check(lib().posfeat_conv_wgrad(ptr(dyd), cout, ptr(xd), cin, n, h, w, cin, cout, 3, 3,
+        check(lib().posfeat_conv_wgrad(ptr(dyd), cout, ptr(xd), cin, n, h, w, cin, cout, k, k,
                                        ptr(dw), ptr(db), ptr(ws), need, stream_ptr()))
         torch.cuda.synchronize()
-        got = weights.unpack_conv(dw.cpu().numpy(), cout, cin, 3, 3)
+        got = weights.unpack_conv(dw.cpu().numpy(), cout, cin, k, k)
         if cin == 4:
             ref_w = ref_w[:, :3]
             got = got[:, :3]
