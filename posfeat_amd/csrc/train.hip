@@ -1038,15 +1038,46 @@ WgPlan wgrad_plan(int n, int H, int W, int Cin, int Cout, int KH, int KW, int st
   return p;
 }
 
+// POSFEAT_WGRAD_BF6_ALL=1 (A/B, off): conv_wgrad_bf6_kernel for every
+// Cin % 32 == 0 conv (3x3 stride 1 too, instead of the fp32 halo tiles):
+// 128 x 128 tiles, ragged last cout / k tiles (the kernel guards both).
+// Measured r4e: slower where the halo tiles reuse the staged input across
+// the 9 taps (keypoint head: image-branch A 3.2 -> 5.1 ms, conv1 2.2 -> 3.0)
+bool wgrad_bf6_all() {
+  static const bool on = [] {
+    const char* e = getenv("POSFEAT_WGRAD_BF6_ALL");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+WgPlan wgrad_plan_bf6(int n, int H, int W, int Cin, int Cout, int KH, int KW) {
+  WgPlan p;
+  p.Kpad = posfeat_conv_packed_k(Cin, KH, KW);
+  p.K = KH * KW * Cin;
+  p.halo = false;
+  p.BM = p.BN = 128;
+  p.tiles_m = (Cout + 127) / 128;
+  p.tiles_n = (p.Kpad + 127) / 128;
+  const long long M = (long long)n * H * W;
+  p.nchunks = (int)((M + WG_RB - 1) / WG_RB);
+  p.ntiles = p.tiles_m * p.tiles_n;
+  const int s = (1024 + p.ntiles - 1) / p.ntiles;
+  const int maxs = std::max(1, p.nchunks / 8);
+  p.nsplit = std::max(1, std::min(std::min(s, maxs), 128));
+  return p;
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------ launchers
 static inline int wg_out(int H, int K, int stride) { return (H + 2 * ((K - 1) / 2) - K) / stride + 1; }
 
 size_t pf_conv_wgrad_ws_bytes(int n, int H, int W, int Cin, int Cout, int KH, int KW, int stride) {
-  const WgPlan p = wgrad_plan(n, wg_out(H, KH, stride), wg_out(W, KW, stride), Cin, Cout, KH, KW,
-                              stride);
-  return pf_align((size_t)p.nsplit * Cout * p.Kpad * 4, 256) + pf_align((size_t)p.nsplit * Cout * 4, 256);
+  const int OH = wg_out(H, KH, stride), OW = wg_out(W, KW, stride);
+  const WgPlan p = wgrad_plan(n, OH, OW, Cin, Cout, KH, KW, stride);
+  const WgPlan q = wgrad_plan_bf6(n, OH, OW, Cin, Cout, KH, KW);
+  const int ns = std::max(p.nsplit, q.nsplit);
+  return pf_align((size_t)ns * Cout * p.Kpad * 4, 256) + pf_align((size_t)ns * Cout * 4, 256);
 }
 
 int pf_conv_wgrad(const float* dy, int ldy, const float* x, int xcs, int n, int H, int W, int Cin,
@@ -1060,7 +1091,9 @@ int pf_conv_wgrad(const float* dy, int ldy, const float* x, int xcs, int n, int 
   if (ws_bytes < pf_conv_wgrad_ws_bytes(n, H, W, Cin, Cout, KH, KW, stride))
     return POSFEAT_E_WORKSPACE;
   const int OH = wg_out(H, KH, stride), OW = wg_out(W, KW, stride);
-  const WgPlan p = wgrad_plan(n, OH, OW, Cin, Cout, KH, KW, stride);
+  const bool b6all = Cin % 32 == 0 && wgrad_bf6_on() && wgrad_bf6_all() && OW >= 4;
+  const WgPlan p = b6all ? wgrad_plan_bf6(n, OH, OW, Cin, Cout, KH, KW)
+                         : wgrad_plan(n, OH, OW, Cin, Cout, KH, KW, stride);
   WgradArgs a;
   a.dy = dy;
   a.ldy = ldy;
@@ -1092,7 +1125,9 @@ int pf_conv_wgrad(const float* dy, int ldy, const float* x, int xcs, int n, int 
                                           pf_align((size_t)p.nsplit * Cout * p.Kpad * 4, 256))
                : nullptr;
   const dim3 grid(a.ntiles * a.nsplit);
-  if (p.halo) {
+  if (b6all) {
+    hipLaunchKernelGGL(conv_wgrad_bf6_kernel, grid, dim3(256), 0, st, a);
+  } else if (p.halo) {
     if (p.BM == 192)
       hipLaunchKernelGGL(conv_wgrad_halo_kernel<6>, grid, dim3(384), 0, st, a);
     else if (p.BM == 128)
@@ -1123,9 +1158,13 @@ int pf_conv_wgrad(const float* dy, int ldy, const float* x, int xcs, int n, int 
 // order gives image z's gradient alone.  Used by the keypoint-head backward,
 // whose image-branch gradients contract per-image statistics.
 namespace {
+bool per_image_bf6(int H, int W, int Cin) {
+  return Cin % 32 == 0 && wgrad_bf6_on() && wgrad_bf6_all() && W >= 4 && (H * W) % WG_RB == 0;
+}
 int per_image_k(int n, int H, int W, int Cin, int Cout) {
-  const WgPlan p = wgrad_plan(n, H, W, Cin, Cout, 3, 3, 1);
-  const int per_img = H * ((W + 31) / 32);
+  const WgPlan p = per_image_bf6(H, W, Cin) ? wgrad_plan_bf6(n, H, W, Cin, Cout, 3, 3)
+                                             : wgrad_plan(n, H, W, Cin, Cout, 3, 3, 1);
+  const int per_img = per_image_bf6(H, W, Cin) ? H * W / WG_RB : H * ((W + 31) / 32);
   const int k = (1024 + n * p.ntiles - 1) / (n * p.ntiles);
   return std::max(1, std::min(std::min(k, per_img / 8), 128));
 }
@@ -1153,7 +1192,8 @@ int pf_conv_wgrad_per_image(const float* dy, int ldy, const float* x, int xcs, i
   if (reinterpret_cast<uintptr_t>(dy) % 16 || reinterpret_cast<uintptr_t>(x) % 16)
     return POSFEAT_E_INVALID;
   if (ws_bytes < pf_conv_wgrad_per_image_ws_bytes(n, H, W, Cin, Cout)) return POSFEAT_E_WORKSPACE;
-  const WgPlan p = wgrad_plan(n, H, W, Cin, Cout, 3, 3, 1);
+  const bool b6 = per_image_bf6(H, W, Cin);
+  const WgPlan p = b6 ? wgrad_plan_bf6(n, H, W, Cin, Cout, 3, 3) : wgrad_plan(n, H, W, Cin, Cout, 3, 3, 1);
   const int k = per_image_k(n, H, W, Cin, Cout);
   WgradArgs a;
   a.dy = dy;
@@ -1180,7 +1220,9 @@ int pf_conv_wgrad_per_image(const float* dy, int ldy, const float* x, int xcs, i
   a.part = static_cast<float*>(ws);
   a.partb = nullptr;
   const dim3 grid(a.ntiles * a.nsplit);
-  if (p.BM == 192)
+  if (b6)  // image-aligned 32-pixel chunks (H W % 32 == 0): splits z*k.. stay in image z
+    hipLaunchKernelGGL(conv_wgrad_bf6_kernel, grid, dim3(256), 0, st, a);
+  else if (p.BM == 192)
     hipLaunchKernelGGL(conv_wgrad_halo_kernel<6>, grid, dim3(384), 0, st, a);
   else if (p.BM == 128)
     hipLaunchKernelGGL(conv_wgrad_halo_kernel<4>, grid, dim3(256), 0, st, a);
