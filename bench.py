@@ -480,7 +480,7 @@ def train_main(args, world, rank, dev):
     fwd_ms = sum(ms for lab, ms, _ in evs if lab.startswith("conv:"))
     all_ms = sum(ms for _, ms, _ in evs)
     # dominant MFMA launch of the step (forward or backward)
-    dom = max((e for e in evs if e[2] > 0), key=lambda e: e[1])
+    dom = max((e for e in evs if e[2] > 0 and not e[0].startswith("side:")), key=lambda e: e[1])
     ach = dom[2] / (dom[1] * 1e-3) / 1e12
     by_label = {}
     for lab, ms, _ in evs:
