@@ -36,6 +36,10 @@ sys.path.insert(0, ROOT)
 
 H, W = 480, 640
 NUM_PTS, NMS_R, THR = 2048, 1, 0.9
+# images per GPU per extraction step (one engine instance, autotuned at this
+# shape; tests/test_gpu_bench_config.py checks this instance image by image)
+EXTRACT_BATCH = 32
+
 # Conv work per 480x640 image: 2 x 208.99 GMAC
 CONV_FLOP_PER_IMAGE = 417.98e9
 HEAD_CONV2_FLOP_PER_IMAGE = 2.0 * 480 * 640 * 128 * 256 * 9   # reference layer
@@ -76,7 +80,11 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=60)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--batch", type=int, default=8, help="images per GPU per step")
+    p.add_argument("--batch", type=int, default=None,
+                   help="images (extract) or pairs (training workloads) per GPU per step; "
+                        "default: %d images for extract (r5c sweep on one box: B=8 847, 16 890, "
+                        "32 939, 48 947, 64 951 img/s -- the layer3/decoder grids fill at 32), "
+                        "8 pairs for the training workloads (configs[2]: bs=8)" % EXTRACT_BATCH)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--graph", action="store_true",
                    help="extract: replay the step as one captured hipGraph (r3n: 798.4 vs "
@@ -94,7 +102,10 @@ def parse():
                         "configs[2] and [4] (Line2Window + EpipolarLoss and DiskLoss, value + "
                         "map gradients) on synthetic maps; stub: a CPU-only step over "
                         "gloo that tests the launcher and the timing protocol")
-    return p.parse_args()
+    args = p.parse_args()
+    if args.batch is None:
+        args.batch = EXTRACT_BATCH if args.workload == "extract" else 8
+    return args
 
 
 def _free_port():
