@@ -402,7 +402,7 @@ int forward(Ctx& c, const float* img, posfeat_extract_out* out, int mode = MODE_
 
 // The decoder's 3x3 stride-1 convs (DescNet.py:41-45) through Winograd
 // F(4x4,3x3) / F(2x2,3x3) when enabled (default; POSFEAT_WINO=0 for the
-// direct conv); then (POSFEAT_WINO_ENC=1) the encoder's stride-1 bottleneck
+// direct conv); then (POSFEAT_WINO_ENC, below) the encoder's stride-1 bottleneck
 // conv2 layers, with their resolution divisor
 const char* const kWinoLayers[16] = {"upconv3.conv", "iconv3",          "upconv2.conv",
                                      "iconv2",       "head.conv1",      "layer1.0.conv2",
@@ -411,12 +411,28 @@ const char* const kWinoLayers[16] = {"upconv3.conv", "iconv3",          "upconv2
                                      "layer3.2.conv2", "layer3.3.conv2", "layer3.4.conv2",
                                      "layer3.5.conv2"};
 const int kWinoDiv[16] = {8, 8, 4, 4, 4, 4, 4, 4, 8, 8, 8, 16, 16, 16, 16, 16};
-bool wino_enc_on() {
-  static const bool on = [] {
+// Which encoder stages take Winograd (POSFEAT_WINO_ENC: "0" none, "1" all,
+// else the stage digits; default "23").  Measured per layer (r5f, halo bf16x6
+// tiles vs Winograd, B = 32 / 8): layer2 conv2 0.275 -> 0.24 / 0.111 -> 0.091
+// ms (F(4x4) at 60x80), layer3 0.45 -> 0.36 / 0.125 -> 0.113 ms (F(2x2) at
+// 30x40, whose halo tiles underfill), but layer1 0.333 -> 0.40 / 0.099 -> 0.13
+// (its K = 64 GEMMs are too short for the transform round trip to pay)
+unsigned wino_enc_mask() {
+  static const unsigned mask = [] {
     const char* e = getenv("POSFEAT_WINO_ENC");
-    return e && e[0] == '1';
+    if (!e) return 6u;
+    if (e[0] == '1' && e[1] == 0) return 7u;
+    unsigned m = 0;
+    for (const char* q = e; *q; ++q)
+      if (*q >= '1' && *q <= '3') m |= 1u << (*q - '1');
+    return m;
   }();
-  return on;
+  return mask;
+}
+bool wino_enc_on() { return wino_enc_mask() != 0; }
+// `p`: the bottleneck prefix "layer<k>.<block>"
+bool wino_enc_layer(const std::string& p) {
+  return p.size() > 5 && p[5] >= '1' && p[5] <= '3' && ((wino_enc_mask() >> (p[5] - '1')) & 1u);
 }
 
 long long wino_u_offset(const std::string& name, bool planes) {
@@ -724,7 +740,7 @@ int bottleneck(Ctx& c, const std::string& p, const float* in, int n, int h, int 
   float* t1 = c.f(m->t1);
   float* t2 = c.f(m->t2);
   PF_TRY(conv(c, p + ".conv1", in, n, h, w, ics, t1, planes, 1, POSFEAT_ACT_RELU));
-  if (stride == 1 && c.m->wino && wino_enc_on() && !c.side)
+  if (stride == 1 && c.m->wino && wino_enc_layer(p) && !c.side)
     PF_TRY(conv3x3(c, p + ".conv2", t1, n, h, w, planes, t2, planes, POSFEAT_ACT_RELU));
   else
     PF_TRY(conv(c, p + ".conv2", t1, n, h, w, planes, t2, planes, stride, POSFEAT_ACT_RELU));
