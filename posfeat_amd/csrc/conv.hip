@@ -682,6 +682,22 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_glds_kernel(ConvArgs a) {
       [&](int, int m) { return a.res ? a.res + (size_t)m * a.rcs : (const float*)nullptr; });
 }
 
+// One step of a two-stage LDS-DMA pipeline: the next chunk's DMA into stage
+// (dA, dB), then the MFMA work on stage (sA, sB).  The stages are distinct
+// __restrict__ parameters so that, once inlined, the LDS reads carry alias
+// scopes disjoint from the DMA's and the waitcnt pass can let the DMA fly
+// under the multiply (without them it conservatively waits vmcnt(0) first).
+template <class Issue, class Compute>
+__device__ __forceinline__ void pf_dma_overlap_step(float* __restrict__ dA,
+                                                    unsigned short* __restrict__ dB,
+                                                    const float* __restrict__ sA,
+                                                    const unsigned short* __restrict__ sB,
+                                                    bool issue, Issue& issue_to,
+                                                    Compute& compute_from) {
+  if (issue) issue_to(dA, dB);
+  compute_from(sA, sB);
+}
+
 // ---------------------------------------------------------------------------
 // bf16x6 with PRE-SPLIT weights (the engine's forward path): B = the packed
 // weights as three bf16 planes of the same [Cout][Kpad] layout (a.wb, plane
@@ -779,32 +795,29 @@ __global__ __launch_bounds__(256) void conv_bf6b_kernel(ConvArgs a) {
   int nx_slab = ch0 / ntap, nx_tap = ch0 - nx_slab * ntap;
   int nx_kh = nx_tap / a.KW, nx_kw = nx_tap - nx_kh * a.KW;
   long long nx_b = (long long)ch0 * BK;
-  auto issue_chunk = [&](int buf) {
+  // the next chunk's DMA into stage (dA, dB)
+  auto issue_to = [&](float* dA, unsigned short* dB) {
     const long long delta = ((long long)nx_kh * a.W + nx_kw) * a.xcs + nx_slab * BK;
     if (dense) {  // wave-uniform branch
 #pragma unroll
       for (int i = 0; i < A_G; ++i)
         __builtin_amdgcn_global_load_lds(
             (const __attribute__((address_space(1))) void*)(xsrc[i] + delta),
-            (__attribute__((address_space(3))) void*)(As + buf * ASTAGE + (wave * A_G + i) * 8 * BK),
-            16, 0, 0);
+            (__attribute__((address_space(3))) void*)(dA + (wave * A_G + i) * 8 * BK), 16, 0, 0);
     } else {
 #pragma unroll
       for (int i = 0; i < A_G; ++i) {
         const float* src = ((tapok[i] >> nx_tap) & 1u) ? xsrc[i] + delta : zero;
         __builtin_amdgcn_global_load_lds(
             (const __attribute__((address_space(1))) void*)src,
-            (__attribute__((address_space(3))) void*)(As + buf * ASTAGE + (wave * A_G + i) * 8 * BK),
-            16, 0, 0);
+            (__attribute__((address_space(3))) void*)(dA + (wave * A_G + i) * 8 * BK), 16, 0, 0);
       }
     }
 #pragma unroll
     for (int i = 0; i < B_G; ++i)
       __builtin_amdgcn_global_load_lds(
           (const __attribute__((address_space(1))) void*)(bsrc[i] + nx_b),
-          (__attribute__((address_space(3))) void*)(Bs + buf * 2 * BSTAGE +
-                                                     (wave * B_G + i) * 16 * BK),
-          16, 0, 0);
+          (__attribute__((address_space(3))) void*)(dB + (wave * B_G + i) * 16 * BK), 16, 0, 0);
     nx_b += BK;
     ++nx_tap;
     if (++nx_kw == a.KW) {
@@ -825,9 +838,9 @@ __global__ __launch_bounds__(256) void conv_bf6b_kernel(ConvArgs a) {
 
   const int sw = ((lane & 31) >> 1) & 7, hh = lane >> 5, r32 = lane & 31;
   const int arow = wm * TM + r32;
-  auto compute = [&](int buf) {
-    const float* Ab = As + buf * ASTAGE + arow * BK;
-    const unsigned short* Bb = Bs + buf * 2 * BSTAGE;
+  auto compute_from = [&](const float* sA, const unsigned short* sB) {
+    const float* Ab = sA + arow * BK;
+    const unsigned short* Bb = sB;
 #pragma unroll
     for (int g = 0; g < BK / 16; ++g) {
       const int s0 = ((4 * g + 2 * hh) ^ sw) * 4, s1 = ((4 * g + 2 * hh + 1) ^ sw) * 4;
@@ -854,13 +867,25 @@ __global__ __launch_bounds__(256) void conv_bf6b_kernel(ConvArgs a) {
     }
   };
 
-  if (ch0 < ch1) issue_chunk(0);
+  // Stage s: A at As + s * ASTAGE, B at Bs + 2 * s * BSTAGE.  Each step
+  // issues chunk c+1's DMA into one stage and multiplies chunk c out of the
+  // other through pf_dma_overlap_step's __restrict__ parameters: the compiler
+  // then knows the stage being read is not the one the DMA writes and does
+  // not put a vmcnt(0) before the reads (it did -- ISA r5j: DMA and MFMA
+  // fully serialised, the "no overlap" of the r3c ablations)
+  float* const A0 = As;
+  float* const A1 = As + ASTAGE;
+  unsigned short* const B0 = Bs;
+  unsigned short* const B1 = Bs + 2 * BSTAGE;
+  if (ch0 < ch1) issue_to(A0, B0);
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
   for (int c = ch0; c < ch1; ++c) {
-    const int cur = (c - ch0) & 1;
-    if (c + 1 < ch1) issue_chunk(cur ^ 1);
-    compute(cur);
+    const bool more = c + 1 < ch1;
+    if (((c - ch0) & 1) == 0)
+      pf_dma_overlap_step(A1, B1, A0, B0, more, issue_to, compute_from);
+    else
+      pf_dma_overlap_step(A0, B0, A1, B1, more, issue_to, compute_from);
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
   }
