@@ -437,6 +437,24 @@ __device__ __forceinline__ f32x16 mfma_bf16(const u32x4_t& a, const u32x4_t& b, 
                                                  __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
 }
 
+// One step of an LDS-DMA pipeline: the next chunk's DMA into LDS through
+// (d0, d1), then the MFMA work reading LDS through (s0, s1).  The four are
+// __restrict__ so that, once inlined, the LDS reads carry alias scopes
+// disjoint from the DMA's and the waitcnt pass lets the DMA fly under the
+// multiply; without them it conservatively waits vmcnt(0) before the first
+// read (ISA r5j: DMA and MFMA serialised in every ring kernel here).  Valid
+// because the bytes a step's DMA writes (the stage being refilled) are never
+// read in that step -- the pointers may share a base, the accessed stages
+// are disjoint.
+template <class P0, class P1, class Q0, class Q1, class Issue, class Compute>
+__device__ __forceinline__ void pf_dma_overlap_step(P0* __restrict__ d0, P1* __restrict__ d1,
+                                                    const Q0* __restrict__ s0,
+                                                    const Q1* __restrict__ s1, bool issue,
+                                                    Issue&& issue_to, Compute&& compute_from) {
+  if (issue) issue_to(d0, d1);
+  compute_from(s0, s1);
+}
+
 // NST = 2: two LDS stages, vmcnt(0) + barrier per chunk (the DMA of chunk c+1
 // overlaps chunk c).  NST = 3: a three-stage ring -- chunks c+1 and c+2 are
 // in flight while c is multiplied; each chunk waits only for its own DMA
@@ -531,14 +549,14 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_glds_kernel(ConvArgs a) {
   int nx_slab = ch0 / ntap, nx_tap = ch0 - nx_slab * ntap;
   int nx_kh = nx_tap / a.KW, nx_kw = nx_tap - nx_kh * a.KW;
   long long nx_b = (long long)ch0 * BK;
-  auto issue_chunk = [&](int buf) {
+  auto issue_chunk = [&](float* Ad, float* Bd, int buf) {
     const long long delta = ((long long)nx_kh * a.W + nx_kw) * a.xcs + nx_slab * BK;
     if (dense) {
 #pragma unroll
       for (int i = 0; i < A_G; ++i)
         __builtin_amdgcn_global_load_lds(
             (const __attribute__((address_space(1))) void*)(xsrc[i] + delta),
-            (__attribute__((address_space(3))) void*)(As + (buf * BM + (wave * A_G + i) * 8) * BK),
+            (__attribute__((address_space(3))) void*)(Ad + (buf * BM + (wave * A_G + i) * 8) * BK),
             16, 0, 0);
     } else {
 #pragma unroll
@@ -546,7 +564,7 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_glds_kernel(ConvArgs a) {
         const float* src = ((tapok[i] >> nx_tap) & 1u) ? xsrc[i] + delta : zero;
         __builtin_amdgcn_global_load_lds(
             (const __attribute__((address_space(1))) void*)src,
-            (__attribute__((address_space(3))) void*)(As + (buf * BM + (wave * A_G + i) * 8) * BK),
+            (__attribute__((address_space(3))) void*)(Ad + (buf * BM + (wave * A_G + i) * 8) * BK),
             16, 0, 0);
       }
     }
@@ -554,7 +572,7 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_glds_kernel(ConvArgs a) {
     for (int i = 0; i < B_G; ++i)
       __builtin_amdgcn_global_load_lds(
           (const __attribute__((address_space(1))) void*)(wsrc[i] + nx_b),
-          (__attribute__((address_space(3))) void*)(Bs + (buf * BN + (wave * B_G + i) * 8) * BK),
+          (__attribute__((address_space(3))) void*)(Bd + (buf * BN + (wave * B_G + i) * 8) * BK),
           16, 0, 0);
     nx_b += BK;
     ++nx_tap;
@@ -584,9 +602,9 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_glds_kernel(ConvArgs a) {
 #pragma unroll
   for (int kk = 0; kk < BK / 8; ++kk) kofs[kk] = (((lane >> 5) + 2 * kk) ^ sw) * 4;
 
-  auto compute = [&](int slot) {
-    const float* Ab = As + (slot * BM + arow) * BK;
-    const float* Bb = Bs + (slot * BN + brow) * BK;
+  auto compute = [&](const float* Ar, const float* Br, int slot) {
+    const float* Ab = Ar + (slot * BM + arow) * BK;
+    const float* Bb = Br + (slot * BN + brow) * BK;
     if constexpr (BF6) {
       // k16 group g: lane half h holds k = 16g + 8h + j, i.e. k-slots 4g+2h, 4g+2h+1
 #pragma unroll
@@ -639,13 +657,18 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_glds_kernel(ConvArgs a) {
   };
 
   if constexpr (NST == 2) {
-    if (ch0 < ch1) issue_chunk(0);
+    if (ch0 < ch1) issue_chunk(As, Bs, 0);
     __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0): the DMA has landed (this wave)
     __syncthreads();
     for (int c = ch0; c < ch1; ++c) {
       const int cur = (c - ch0) & 1;
-      if (c + 1 < ch1 && !(a.abl & 2)) issue_chunk(cur ^ 1);
-      if (!(a.abl & 1)) compute(cur);
+      pf_dma_overlap_step(
+          As + (cur ^ 1) * BM * BK, Bs + (cur ^ 1) * BN * BK, As + cur * BM * BK,
+          Bs + cur * BN * BK, c + 1 < ch1 && !(a.abl & 2),
+          [&](float* Ad, float* Bd) { issue_chunk(Ad, Bd, 0); },
+          [&](const float* Ar, const float* Br) {
+            if (!(a.abl & 1)) compute(Ar, Br, 0);
+          });
       __builtin_amdgcn_s_waitcnt(0);
       __syncthreads();
     }
@@ -654,7 +677,7 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_glds_kernel(ConvArgs a) {
     // multiplied; each chunk waits only for its own DMA (counted vmcnt) and
     // one raw s_barrier (no fence: the younger chunks' DMAs stay in flight)
     const int nch = ch1 - ch0;
-    for (int j = 0; j < NST - 1 && j < nch; ++j) issue_chunk(j);
+    for (int j = 0; j < NST - 1 && j < nch; ++j) issue_chunk(As, Bs, j);
     int slot = 0;
     for (int i = 0; i < nch; ++i) {
       const int ahead = min(NST - 2, nch - 1 - i);  // younger chunks already issued
@@ -668,8 +691,11 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_glds_kernel(ConvArgs a) {
         wait_vmcnt<0>();
       // every wave: chunk i landed, and chunk i-1 (the slot refilled below) consumed
       __builtin_amdgcn_s_barrier();
-      if (i + NST - 1 < nch) issue_chunk(slot == 0 ? NST - 1 : slot - 1);
-      compute(slot);
+      const int refill = slot == 0 ? NST - 1 : slot - 1;
+      pf_dma_overlap_step(
+          As + refill * BM * BK, Bs + refill * BN * BK, As + slot * BM * BK, Bs + slot * BN * BK,
+          i + NST - 1 < nch, [&](float* Ad, float* Bd) { issue_chunk(Ad, Bd, 0); },
+          [&](const float* Ar, const float* Br) { compute(Ar, Br, 0); });
       slot = slot == NST - 1 ? 0 : slot + 1;
     }
     __builtin_amdgcn_s_waitcnt(0);
@@ -680,22 +706,6 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_glds_kernel(ConvArgs a) {
       a, acc, smem, tm, n0, split, [&](int row) { return m0 + row < a.M ? m0 + row : -1; },
       m0 / a.hw,
       [&](int, int m) { return a.res ? a.res + (size_t)m * a.rcs : (const float*)nullptr; });
-}
-
-// One step of a two-stage LDS-DMA pipeline: the next chunk's DMA into stage
-// (dA, dB), then the MFMA work on stage (sA, sB).  The stages are distinct
-// __restrict__ parameters so that, once inlined, the LDS reads carry alias
-// scopes disjoint from the DMA's and the waitcnt pass can let the DMA fly
-// under the multiply (without them it conservatively waits vmcnt(0) first).
-template <class Issue, class Compute>
-__device__ __forceinline__ void pf_dma_overlap_step(float* __restrict__ dA,
-                                                    unsigned short* __restrict__ dB,
-                                                    const float* __restrict__ sA,
-                                                    const unsigned short* __restrict__ sB,
-                                                    bool issue, Issue& issue_to,
-                                                    Compute& compute_from) {
-  if (issue) issue_to(dA, dB);
-  compute_from(sA, sB);
 }
 
 // ---------------------------------------------------------------------------
@@ -971,14 +981,14 @@ __global__ __launch_bounds__(256) void conv_bf6r_kernel(ConvArgs a) {
   const int ch0 = (int)((long long)nch_all * split / a.ksplit);
   const int ch1 = (int)((long long)nch_all * (split + 1) / a.ksplit);
 
-  auto issue_b = [&](int c, int buf) {
+  auto issue_b = [&](unsigned short* Bd, int c, int buf) {
 #pragma unroll
     for (int i = 0; i < B_G; ++i) {
       const void* src = bsrc[i] ? (const void*)(bsrc[i] + (long long)c * BK)
                                 : (const void*)pf_conv_zero16;
       __builtin_amdgcn_global_load_lds(
           (const __attribute__((address_space(1))) void*)src,
-          (__attribute__((address_space(3))) void*)(Bs + buf * 2 * BSTAGE +
+          (__attribute__((address_space(3))) void*)(Bd + buf * 2 * BSTAGE +
                                                      (wave * B_G + i) * 16 * BK),
           16, 0, 0);
     }
@@ -1004,8 +1014,8 @@ __global__ __launch_bounds__(256) void conv_bf6r_kernel(ConvArgs a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[0][ni][r] = 0.f;
 
-  auto compute = [&](int buf, const f32x4 (&v)[4]) {
-    const unsigned short* Bb = Bs + buf * 2 * BSTAGE;
+  auto compute = [&](const unsigned short* Br, int buf, const f32x4 (&v)[4]) {
+    const unsigned short* Bb = Br + buf * 2 * BSTAGE;
 #pragma unroll
     for (int g = 0; g < BK / 16; ++g) {
       u32x4_t ah, am, al;
@@ -1037,9 +1047,9 @@ __global__ __launch_bounds__(256) void conv_bf6r_kernel(ConvArgs a) {
   const int nch = ch1 - ch0;
   f32x4 va[4], vb[4];
   if (nch > 0) {
-    issue_b(ch0, 0);
+    issue_b(Bs, ch0, 0);
     load_a(ch0, va);
-    if (NST == 3 && nch > 1) issue_b(ch0 + 1, 1);
+    if (NST == 3 && nch > 1) issue_b(Bs, ch0 + 1, 1);
   }
   int slot = 0;
   for (int i = 0; i < nch; i += 2) {
@@ -1059,11 +1069,18 @@ __global__ __launch_bounds__(256) void conv_bf6r_kernel(ConvArgs a) {
       } else {
         if (ii + 1 < nch) load_a(ch0 + ii + 1, va);
       }
-      if (ii + NST - 1 < nch) issue_b(ch0 + ii + NST - 1, slot == 0 ? NST - 1 : slot - 1);
-      if (u == 0)
-        compute(slot, va);
-      else
-        compute(slot, vb);
+      const int refill = slot == 0 ? NST - 1 : slot - 1;
+      unsigned short* const Bref = Bs + refill * 2 * BSTAGE;
+      const unsigned short* const Bcur = Bs + slot * 2 * BSTAGE;
+      pf_dma_overlap_step(
+          Bref, Bref + BSTAGE, Bcur, Bcur + BSTAGE, ii + NST - 1 < nch,
+          [&](unsigned short* Bd, unsigned short*) { issue_b(Bd, ch0 + ii + NST - 1, 0); },
+          [&](const unsigned short* Br, const unsigned short*) {
+            if (u == 0)
+              compute(Br, 0, va);
+            else
+              compute(Br, 0, vb);
+          });
       slot = slot == NST - 1 ? 0 : slot + 1;
     }
   }
@@ -1145,23 +1162,23 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_halo_kernel(ConvArgs a) {
     const int sslot = (lane & 7) ^ ((row >> 1) & 7);
     wsrc[i] = (n0 + row < a.Cout) ? a.w + (size_t)(n0 + row) * a.Kpad + sslot * 4 : nullptr;
   }
-  auto issue_halo = [&](int slab, int buf) {
+  auto issue_halo = [&](float* Ad, int slab, int buf) {
 #pragma unroll
     for (int i = 0; i < A_G; ++i) {
       const float* src = hsrc[i] ? hsrc[i] + slab * BK : pf_conv_zero16;
       __builtin_amdgcn_global_load_lds(
           (const __attribute__((address_space(1))) void*)src,
-          (__attribute__((address_space(3))) void*)(As + (buf * HPR + (wave * A_G + i) * 8) * BK),
+          (__attribute__((address_space(3))) void*)(Ad + (buf * HPR + (wave * A_G + i) * 8) * BK),
           16, 0, 0);
     }
   };
-  auto issue_w = [&](int c, int buf) {
+  auto issue_w = [&](float* Bd, int c, int buf) {
 #pragma unroll
     for (int i = 0; i < B_G; ++i) {
       const float* src = wsrc[i] ? wsrc[i] + (size_t)c * BK : pf_conv_zero16;
       __builtin_amdgcn_global_load_lds(
           (const __attribute__((address_space(1))) void*)src,
-          (__attribute__((address_space(3))) void*)(Bs + (buf * BN + (wave * B_G + i) * 8) * BK),
+          (__attribute__((address_space(3))) void*)(Bd + (buf * BN + (wave * B_G + i) * 8) * BK),
           16, 0, 0);
     }
   };
@@ -1184,22 +1201,25 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_halo_kernel(ConvArgs a) {
   const int ch0 = (int)((long long)nch_all * split / a.ksplit);
   const int ch1 = (int)((long long)nch_all * (split + 1) / a.ksplit);
   int slab = ch0 / NTAP, tap = ch0 - slab * NTAP;
-  issue_halo(slab, 0);
-  issue_w(ch0, 0);
+  issue_halo(As, slab, 0);
+  issue_w(Bs, ch0, 0);
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
 
   int abuf = 0;
   for (int c = ch0; c < ch1; ++c) {
     const int bcur = (c - ch0) & 1;
-    if (c + 1 < ch1) {
-      issue_w(c + 1, bcur ^ 1);
-      if (tap == NTAP - 1) issue_halo(slab + 1, abuf ^ 1);
-    }
     const int kh = tap / KW, kw = tap - (tap / KW) * KW;
     const int hsw = ((px + kw) >> 1) & 7;
-    const float* Ab = As + (abuf * HPR + hrow0 + kh * HX + kw) * BK;
-    const float* Bb = Bs + (bcur * BN + brow) * BK;
+    pf_dma_overlap_step(As + (abuf ^ 1) * HPR * BK, Bs + (bcur ^ 1) * BN * BK,
+                        As + abuf * HPR * BK, Bs + bcur * BN * BK, c + 1 < ch1,
+                        [&](float* Ad, float* Bd) {
+                          issue_w(Bd, c + 1, 0);
+                          if (tap == NTAP - 1) issue_halo(Ad, slab + 1, 0);
+                        },
+                        [&](const float* Ar, const float* Br) {
+    const float* Ab = Ar + (hrow0 + kh * HX + kw) * BK;
+    const float* Bb = Br + brow * BK;
     if constexpr (BF6) {
 #pragma unroll
       for (int g = 0; g < BK / 16; ++g) {
@@ -1249,6 +1269,7 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_halo_kernel(ConvArgs a) {
             acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[mi][j], bv[ni][j], acc[mi][ni],
                                                                 0, 0, 0);
     }
+                        });
     if (++tap == NTAP) {
       tap = 0;
       ++slab;
