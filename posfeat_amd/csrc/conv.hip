@@ -906,6 +906,183 @@ __global__ __launch_bounds__(256) void conv_bf6b_kernel(ConvArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Persistent form of conv_bf6b_kernel for dense GEMMs (1x1 convs without
+// padding: every Winograd transform-domain GEMM, the tap GEMM, the 1x1
+// layers), ksplit 1, no fused statistics.  Same products in the same order
+// and the same epilogue arithmetic ((acc + bias) + residual, then the
+// activation): bit-identical results.  A grid of at most two blocks per CU
+// walks the tiles; each XCD owns a contiguous range of tile ids (the N-tiles
+// of one M-tile share its L2).  While a tile's last chunk is multiplied, the
+// DMA of the NEXT tile's first chunk is already in flight, and it stays in
+// flight through the epilogue, which stores straight from the accumulators
+// (lanes 0-31 / 32-63 of a store write 128 contiguous bytes of two rows): no
+// LDS staging, no per-tile prologue stall.  K = 192 (the tap GEMM: 6 chunks
+// per tile) paid a full DMA latency plus an LDS round trip per tile before.
+template <int BM, int BN>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void conv_bf6p_kernel(ConvArgs a) {
+  constexpr int WM = 4, NW = 4;
+  constexpr int TM = BM / WM;
+  constexpr int NI = BN / 32;
+  constexpr int A_G = BM / 8 / NW;
+  constexpr int B_G = 3 * BN / 16 / NW;
+  static_assert(TM == 32 && A_G >= 1 && B_G >= 1 && (3 * BN / 16) % NW == 0, "tile");
+  constexpr int ASTAGE = BM * BK;
+  constexpr int BSTAGE = 3 * BN * BK / 2;
+  __shared__ __attribute__((aligned(16))) float smem[2 * (ASTAGE + BSTAGE)];
+  float* const As = smem;
+  unsigned short* const Bs = reinterpret_cast<unsigned short*>(smem + 2 * ASTAGE);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int total = a.nwg * a.nbatch;
+  // tile walk: blocks round-robin over the ng = min(G, 8) XCD groups; group x
+  // (blockIdx % ng) owns ids [x*q, min((x+1)*q, total)) and its nb blocks
+  // stride through that range -- every id exactly once, any G >= 1
+  const int G = gridDim.x, ng = min(G, 8), xcd = blockIdx.x % ng;
+  const int nb = (G - xcd + ng - 1) / ng, q = (total + ng - 1) / ng;
+  const int lo = xcd * q, hi = min(lo + q, total);
+  int t = lo + blockIdx.x / ng;
+  if (t >= hi) return;
+
+  const int lrow = lane >> 3;
+  const int nch = a.Kpad / BK;
+  const float* xs[A_G];
+  const unsigned short* bs[B_G];
+  // per-tile DMA sources (chunk 0) and epilogue geometry
+  int m0 = 0, n0 = 0;
+  float* ybase = a.y;
+  auto setup = [&](int tt) {
+    const int zb = tt / a.nwg, bid = tt - zb * a.nwg;
+    const int tm = bid / a.tiles_n, tn = bid - tm * a.tiles_n;
+    m0 = tm * BM;
+    n0 = tn * BN;
+    const float* xb = a.x + (long long)zb * a.bx;
+    const unsigned short* wbb = a.wb + (long long)zb * a.bwb;
+    ybase = a.y + (long long)zb * a.by;
+#pragma unroll
+    for (int i = 0; i < A_G; ++i) {
+      const int row = (wave * A_G + i) * 8 + lrow;
+      const int sslot = (lane & 7) ^ ((row >> 1) & 7);
+      const int m = min(m0 + row, a.M - 1);  // rows past M re-read the last one (never stored)
+      const int n = m / a.hw, rem = m - n * a.hw;
+      const int oh = rem / a.OW, ow = rem - oh * a.OW;
+      xs[i] = xb + (((long long)n * a.H + oh * a.stride) * a.W + ow * a.stride) * a.xcs + sslot * 4;
+    }
+#pragma unroll
+    for (int i = 0; i < B_G; ++i) {
+      const int pr = (wave * B_G + i) * 16 + (lane >> 2);
+      const int plane = pr / BN, row = pr - plane * BN;
+      const int ks = (lane & 3) ^ ((row >> 2) & 3);
+      bs[i] = wbb + plane * a.wplane + (long long)min(n0 + row, a.Cout - 1) * a.Kpad + ks * 8;
+    }
+  };
+  auto issue_to = [&](int c, float* dA, unsigned short* dB) {
+    const long long off = (long long)c * BK;
+#pragma unroll
+    for (int i = 0; i < A_G; ++i)
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(xs[i] + off),
+          (__attribute__((address_space(3))) void*)(dA + (wave * A_G + i) * 8 * BK), 16, 0, 0);
+#pragma unroll
+    for (int i = 0; i < B_G; ++i)
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(bs[i] + off),
+          (__attribute__((address_space(3))) void*)(dB + (wave * B_G + i) * 16 * BK), 16, 0, 0);
+  };
+
+  f32x16 acc[NI];
+  const int sw = ((lane & 31) >> 1) & 7, hh = lane >> 5, r32 = lane & 31;
+  const int arow = wave * TM + r32;
+  auto compute_from = [&](const float* sA, const unsigned short* sB) {
+    const float* Ab = sA + arow * BK;
+#pragma unroll
+    for (int g = 0; g < BK / 16; ++g) {
+      const int s0 = ((4 * g + 2 * hh) ^ sw) * 4, s1 = ((4 * g + 2 * hh + 1) ^ sw) * 4;
+      u32x4_t ah, am, al;
+      split3(*reinterpret_cast<const f32x4*>(Ab + s0), *reinterpret_cast<const f32x4*>(Ab + s1),
+             ah, am, al);
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) {
+        const int row = ni * 32 + r32;
+        const int slot = (2 * g + hh) ^ ((row >> 2) & 3);
+        const unsigned short* bp = sB + row * BK + slot * 8;
+        const u32x4_t bh = *reinterpret_cast<const u32x4_t*>(bp);
+        const u32x4_t bm = *reinterpret_cast<const u32x4_t*>(bp + BN * BK);
+        const u32x4_t bl = *reinterpret_cast<const u32x4_t*>(bp + 2 * BN * BK);
+        f32x16 cc = acc[ni];
+        cc = mfma_bf16(ah, bh, cc);
+        cc = mfma_bf16(ah, bm, cc);
+        cc = mfma_bf16(am, bh, cc);
+        cc = mfma_bf16(ah, bl, cc);
+        cc = mfma_bf16(al, bh, cc);
+        cc = mfma_bf16(am, bm, cc);
+        acc[ni] = cc;
+      }
+    }
+  };
+  auto stageA = [&](int s) { return As + s * ASTAGE; };
+  auto stageB = [&](int s) { return Bs + s * 2 * BSTAGE; };
+
+  setup(t);
+  issue_to(0, stageA(0), stageB(0));
+  int st0 = 0;  // stage holding the current tile's chunk 0
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  while (true) {
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[ni][r] = 0.f;
+    const int cm0 = m0, cn0 = n0;
+    float* const cy = ybase;
+    const int tn_ = t + nb;
+    const bool more_tiles = tn_ < hi;
+    for (int c = 0; c < nch; ++c) {
+      const int s = st0 ^ (c & 1);
+      const bool last = c + 1 == nch;
+      // at the last chunk: the next tile's first chunk flies under this
+      // chunk's MFMAs and the epilogue
+      if (last && more_tiles) setup(tn_);
+      pf_dma_overlap_step(stageA(s ^ 1), stageB(s ^ 1), stageA(s), stageB(s), !last || more_tiles,
+                          [&](float* dA, unsigned short* dB) { issue_to(last ? 0 : c + 1, dA, dB); },
+                          [&](const float* sA, const unsigned short* sB) { compute_from(sA, sB); });
+      if (last) {
+        st0 = s ^ 1;
+      } else {
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();
+      }
+    }
+    // ---- epilogue straight from the accumulators ---------------------------
+    // acc[ni][r]: row wave*32 + (r&3) + 8*(r>>2) + 4*hh, column ni*32 + r32
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) {
+      const int col = cn0 + ni * 32 + r32;
+      if (col >= a.Cout) continue;
+      const float bv = a.bias ? a.bias[col] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = cm0 + wave * TM + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        if (m >= a.M) continue;
+        // (acc + bias) + residual-or-0, as conv_epilogue (same bits, incl. -0 + 0)
+        float v = acc[ni][r] + bv;
+        v += a.res ? a.res[(size_t)m * a.rcs + col] : 0.f;
+        if (a.act == POSFEAT_ACT_RELU)
+          v = fmaxf(v, 0.f);
+        else if (a.act == POSFEAT_ACT_ELU)
+          v = pf_elu(v);
+        cy[(size_t)m * a.ycs + col] = v;
+      }
+    }
+    // the next tile's chunk 0 has landed; every wave is done with this tile's stages
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (!more_tiles) break;
+    t = tn_;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // The same products with A straight to REGISTERS.  With the waves stacked
 // along M each wave is the only reader of its 32 A rows, so A needs no LDS
 // round trip: lane (r, h) global-loads the 8 fp32 it feeds the MFMA (row r,
@@ -1780,6 +1957,32 @@ int bf6_nst() {
 // 0.589 ms (3) against 0.564 ms for the LDS-staged conv_bf6b_kernel -- the
 // per-lane 32-B row pieces load worse than the 128-B DMA rows);
 // POSFEAT_BF6R_NST: B stages (2 or 3)
+// The persistent pre-split-weight tiles (conv_bf6p_kernel) for dense GEMMs
+// without split-K or fused statistics: POSFEAT_BF6P=1 or
+// posfeat_set_conv_persistent(1) (A/B, off: same-box r5q, 932 vs 946 img/s
+// for one workgroup per tile -- neither the per-tile DMA latency nor the LDS
+// epilogue was what bounds these GEMMs); POSFEAT_BF6P_BLOCKS the resident
+// grid (default 512: two 80-KB blocks on each of the 256 CUs).
+int g_conv_persist = -1;
+int conv_persist_mode() {
+  if (g_conv_persist < 0) {
+    const char* e = getenv("POSFEAT_BF6P");
+    g_conv_persist = (e && e[0] == '1') ? 1 : 0;
+  }
+  return g_conv_persist;
+}
+bool bf6p_persist_ok(const ConvArgs& a) {
+  return conv_persist_mode() == 1 && a.KH == 1 && a.KW == 1 && a.pad == 0 && a.ksplit == 1 && !a.stats && a.wb;
+}
+int bf6p_blocks() {
+  static const int n = [] {
+    const char* e = getenv("POSFEAT_BF6P_BLOCKS");
+    const int v = e ? atoi(e) : 512;
+    return v >= 8 ? v / 8 * 8 : 512;  // a multiple of 8: whole XCD groups
+  }();
+  return n;
+}
+
 bool bf6r_on() {
   static const bool on = [] {
     const char* e = getenv("POSFEAT_BF6R");
@@ -2039,13 +2242,23 @@ int conv_run(ConvArgs& a, const Plan& p, hipStream_t st) {
                            dim3(a.nwg * a.ksplit, a.nbatch), dim3(256), 0, st, a);
       break;
     case TILE_BF6B_128x128:
-      hipLaunchKernelGGL((conv_bf6b_kernel<128, 128>), dim3(a.nwg * a.ksplit, a.nbatch), dim3(256),
-                         0, st, a);
+    case TILE_BF6B_128x64: {
+      const bool wide = p.tile == TILE_BF6B_128x128;
+      if (bf6p_persist_ok(a)) {
+        const int grid = (int)std::min<long long>((long long)a.nwg * a.nbatch, bf6p_blocks());
+        if (wide)
+          hipLaunchKernelGGL((conv_bf6p_kernel<128, 128>), dim3(grid), dim3(256), 0, st, a);
+        else
+          hipLaunchKernelGGL((conv_bf6p_kernel<128, 64>), dim3(grid), dim3(256), 0, st, a);
+      } else if (wide) {
+        hipLaunchKernelGGL((conv_bf6b_kernel<128, 128>), dim3(a.nwg * a.ksplit, a.nbatch),
+                           dim3(256), 0, st, a);
+      } else {
+        hipLaunchKernelGGL((conv_bf6b_kernel<128, 64>), dim3(a.nwg * a.ksplit, a.nbatch),
+                           dim3(256), 0, st, a);
+      }
       break;
-    case TILE_BF6B_128x64:
-      hipLaunchKernelGGL((conv_bf6b_kernel<128, 64>), dim3(a.nwg * a.ksplit, a.nbatch), dim3(256),
-                         0, st, a);
-      break;
+    }
     case TILE_BF6R_128x128:
       if (bf6r_nst() == 3)
         hipLaunchKernelGGL((conv_bf6r_kernel<128, 128, 3>), dim3(a.nwg * a.ksplit, a.nbatch),
@@ -2473,4 +2686,12 @@ int pf_gemm_batched(const float* A, int lda, long long sa, const float* B, long 
   a.bwb = sb;
   a.by = sc;
   return conv_run(a, p, st);
+}
+
+extern "C" int posfeat_set_conv_persistent(int mode) {
+  const int prev = conv_persist_mode();
+  if (mode == -1) return prev;
+  if (mode < 0 || mode > 1) return -1;
+  g_conv_persist = mode;
+  return prev;
 }
