@@ -2678,7 +2678,17 @@ int pf_gemm_batched(const float* A, int lda, long long sa, const float* B, long 
   // the heuristic sizes tiles for ONE GEMM; with nb of them in the grid the
   // 128x128 tile (2x the operand reuse of 64x64) still fills the chip
   const long long t128 = (long long)((M + 127) / 128) * ((N + 127) / 128) * nb;
-  const Plan p = conv_plan(a, false, (N % 128 == 0 && t128 >= 1024) ? TILE_128x128 : -1);
+  // N = 192 (head.conv1's Winograd GEMMs) on pre-split planes: three 64-wide
+  // column tiles instead of two 128-wide ones, the second of them half empty
+  // (POSFEAT_GEMM_N64=0: the 128-wide tiles, A/B)
+  static const bool n64 = [] {
+    const char* e = getenv("POSFEAT_GEMM_N64");
+    return !(e && e[0] == '0');
+  }();
+  const int want = (N % 128 == 0 && t128 >= 1024) ? TILE_128x128
+                   : (Bb && n64 && N % 128 != 0 && N % 64 == 0) ? TILE_BF6B_128x64
+                                                                 : -1;
+  const Plan p = conv_plan(a, false, want);
   if (p.kern != KERN_GLDS) return POSFEAT_E_UNSUPPORTED;
   a.nbatch = nb;
   a.bx = sa;

@@ -31,8 +31,10 @@ int grid_for(long long total, int block) {
 
 // U[xi][co][ci] from the engine-packed 3x3 weights [Cout][Kpad], K order
 // ((ci/32)*9 + tap)*32 + ci%32 (Cin % 32 == 0)
+// Ub != nullptr: U as three bf16 planes (plane stride 16 Cout Cin) for the
+// pre-split bf16x6 GEMM tiles, instead of fp32
 __global__ void wino_weights_kernel(const float* __restrict__ wpk, int Cout, int Cin, int kpad,
-                                    float* __restrict__ U) {
+                                    float* __restrict__ U, unsigned short* __restrict__ Ub = nullptr) {
   const long long n = (long long)Cout * Cin;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
        i += (long long)gridDim.x * blockDim.x) {
@@ -53,10 +55,20 @@ __global__ void wino_weights_kernel(const float* __restrict__ wpk, int Cout, int
     for (int a = 0; a < 4; ++a) {
       const float u0 = r[a][0], u1 = 0.5f * (r[a][0] + r[a][1] + r[a][2]);
       const float u2 = 0.5f * (r[a][0] - r[a][1] + r[a][2]), u3 = r[a][2];
-      U[((long long)(a * 4 + 0) * Cout + co) * Cin + ci] = u0;
-      U[((long long)(a * 4 + 1) * Cout + co) * Cin + ci] = u1;
-      U[((long long)(a * 4 + 2) * Cout + co) * Cin + ci] = u2;
-      U[((long long)(a * 4 + 3) * Cout + co) * Cin + ci] = u3;
+      const float uu[4] = {u0, u1, u2, u3};
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const long long o = ((long long)(a * 4 + b) * Cout + co) * Cin + ci;
+        if (Ub) {
+          unsigned hh, mm, ll;
+          pf_split3_pair(uu[b], 0.f, hh, mm, ll);
+          Ub[o] = (unsigned short)hh;
+          Ub[o + 16 * n] = (unsigned short)mm;
+          Ub[o + 32 * n] = (unsigned short)ll;
+        } else {
+          U[o] = uu[b];
+        }
+      }
     }
   }
 }
@@ -652,18 +664,24 @@ size_t pf_wino_weights_floats(int Cin, int Cout) { return (size_t)36 * Cin * Cou
 // U for the variant pf_wino_conv will pick at (h, w); h = w = 0: F(2x2)
 size_t pf_wino_weights_floats_bf6p(int Cin, int Cout) { return (size_t)54 * Cin * Cout; }
 
+// U as bf16 planes for the pre-split bf16x6 GEMM tiles: Cout a multiple of
+// 64 (128-wide tiles, or 64-wide ones for 192 = head.conv1; the tiles clamp
+// their rows past Cout, the epilogue never stores them)
+static bool wino_planes_ok(int Cout) { return Cout % 64 == 0; }
+
 int pf_wino_weights_hw(const float* wpk, int Cout, int Cin, int h, int w, float* U,
                        hipStream_t st, bool bf6p) {
   if (Cin % 32 || Cout % 4) return POSFEAT_E_INVALID;
   const int kpad = posfeat_conv_packed_k(Cin, 3, 3);
-  bf6p = bf6p && Cout % 128 == 0;  // the same condition as wino_conv_impl's bf16x6 path
+  bf6p = bf6p && wino_planes_ok(Cout);  // the same condition as wino_conv_impl's plane paths
   if (h > 0 && use_f4(h, w))
     hipLaunchKernelGGL(wino4_weights_kernel, dim3(grid_for((long long)Cout * Cin, 256)), dim3(256),
                        0, st, wpk, Cout, Cin, kpad, U,
                        bf6p ? reinterpret_cast<unsigned short*>(U) : nullptr);
   else
     hipLaunchKernelGGL(wino_weights_kernel, dim3(grid_for((long long)Cout * Cin, 256)), dim3(256),
-                       0, st, wpk, Cout, Cin, kpad, U);
+                       0, st, wpk, Cout, Cin, kpad, U,
+                       bf6p && h > 0 ? reinterpret_cast<unsigned short*>(U) : nullptr);
   PF_CHECK_LAUNCH();
   return POSFEAT_OK;
 }
@@ -681,7 +699,7 @@ static int wino_conv_impl(const float* x, int xcs, int n, int h, int w, int Cin,
   if ((h & 1) || (w & 1) || Cin % 32 || Cout % 4 || xcs % 4 || ycs % 4 || n <= 0)
     return POSFEAT_E_INVALID;
   if (ws_bytes < pf_wino_ws_bytes(n, h, w, Cin, Cout)) return POSFEAT_E_WORKSPACE;
-  if (use_f4(h, w) && U_is_f4 && bf6p && Cout % 128 == 0) {
+  if (use_f4(h, w) && U_is_f4 && bf6p && wino_planes_ok(Cout)) {
     // bf16x6: V as three bf16 planes (54 T4 Cin bytes <= the F(2x2) V region),
     // M after them; U holds three planes (pf_wino_weights_hw(..., bf6p))
     const long long T4 = (long long)n * (h / 4) * (w / 4);
@@ -717,7 +735,7 @@ static int wino_conv_impl(const float* x, int xcs, int n, int h, int w, int Cin,
     if (stages & 2)  // planes == 1: U holds its bf16 planes (pre-split bf16x6 tiles)
       PF_TRY(pf_gemm_batched(V4, Cin, T4 * Cin, U, (long long)Cout * Cin, M4, Cout, T4 * Cout, 36,
                              (int)T4, Cout, Cin, st,
-                             planes == 1 && Cout % 128 == 0
+                             planes == 1 && wino_planes_ok(Cout)
                                  ? reinterpret_cast<const unsigned short*>(U)
                                  : nullptr,
                              36LL * Cout * Cin));
@@ -736,9 +754,13 @@ static int wino_conv_impl(const float* x, int xcs, int n, int h, int w, int Cin,
                        xcs, n, h, w, Cin / 4, V);
     PF_CHECK_LAUNCH();
   }
-  if (stages & 2)
+  if (stages & 2)  // planes == 1 (and U from pf_wino_weights_hw for this h, w): bf16 planes
     PF_TRY(pf_gemm_batched(V, Cin, T * Cin, U, (long long)Cout * Cin, M, Cout, T * Cout, 16,
-                           (int)T, Cout, Cin, st));
+                           (int)T, Cout, Cin, st,
+                           planes >= 1 && U_is_f4 && wino_planes_ok(Cout)
+                               ? reinterpret_cast<const unsigned short*>(U)
+                               : nullptr,
+                           16LL * Cout * Cin));
   if (stages & 4) {
     hipLaunchKernelGGL(wino_output_kernel, dim3(grid_for(T * (Cout / 4), 256)), dim3(256), 0, st,
                        M, n, h, w, Cout / 4, bias, act, y, ycs);
