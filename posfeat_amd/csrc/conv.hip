@@ -722,8 +722,11 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_glds_kernel(ConvArgs a) {
 // s ^ ((r >> 2) & 3): conflict-free ds_read_b128).  Two stages; at
 // BM = BN = 128 that is 80 KB, two blocks per CU.  Products and their order
 // are those of the BF6 tiles: results are bit-identical to them.
+// amdgpu_waves_per_eu(2): the accumulators move from AGPRs to VGPRs within
+// the 256-register budget of two waves per SIMD (same box, r5y: +0.6 %)
 template <int BM, int BN>
-__global__ __launch_bounds__(256) void conv_bf6b_kernel(ConvArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+void conv_bf6b_kernel(ConvArgs a) {
   constexpr int WM = 4, WN = 1, NW = 4;
   constexpr int TM = BM / WM, TN = BN;
   constexpr int MI = TM / 32, NI = TN / 32;
