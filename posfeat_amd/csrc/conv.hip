@@ -1097,7 +1097,8 @@ void conv_bf6p_kernel(ConvArgs a) {
 // ablations, r3c).  Products, their order and the epilogue are those of
 // conv_bf6b_kernel: bit-identical results.
 template <int BM, int BN, int NST>
-__global__ __launch_bounds__(256) void conv_bf6r_kernel(ConvArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+void conv_bf6r_kernel(ConvArgs a) {
   constexpr int WM = 4, WN = 1, NW = 4;
   constexpr int TM = BM / WM, TN = BN;
   constexpr int MI = TM / 32, NI = TN / 32;
@@ -1286,7 +1287,8 @@ __global__ __launch_bounds__(256) void conv_bf6r_kernel(ConvArgs a) {
 // flight while the current chunk is multiplied (two LDS stages each).
 // BF6: the products as bf16x6 (both operands split in registers, see split3)
 template <int PH, int BN, int WM, int WN, int KH, int KW, bool BF6 = false>
-__global__ __launch_bounds__(WM* WN * 64) void conv_halo_kernel(ConvArgs a) {
+__global__ __launch_bounds__(WM* WN * 64) __attribute__((amdgpu_waves_per_eu(2)))
+void conv_halo_kernel(ConvArgs a) {
   constexpr int PW = 16;
   constexpr int BM = PH * PW;
   constexpr int THREADS = WM * WN * 64;
