@@ -2136,6 +2136,7 @@ Plan plan_for_tile(const ConvArgs& a, int tile) {
 // depend on the tile (the engine's autotuner relies on this).
 Plan conv_plan(const ConvArgs& a, bool allow_split, int forced = -1) {
   const ConvEnv& env = conv_env();
+  if (forced < 0 && env.tile >= 0) forced = env.tile;  // POSFEAT_CONV_TILE: any legal tile
   const bool cin32 = a.Cin % BK == 0;
   const int nch = a.Kpad / BK;
   Plan d = plan_for_tile(a, a.Cout % 128 == 0 ? TILE_H8x128 : TILE_H8x64);
