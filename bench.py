@@ -83,7 +83,9 @@ def parse():
     p.add_argument("--batch", type=int, default=None,
                    help="images (extract) or pairs (training workloads) per GPU per step; "
                         "default: %d images for extract (r5c sweep on one box: B=8 847, 16 890, "
-                        "32 939, 48 947, 64 951 img/s -- the layer3/decoder grids fill at 32), "
+                        "32 939, 48 947, 64 951 img/s -- the layer3/decoder grids fill at 32; "
+                        "r6g same box: 32 946.9, 64 963.0, but at 64 the side stream's "
+                        "K=80 conv overlaps a decoder GEMM, see DESIGN 4.1m), "
                         "8 pairs for the training workloads (configs[2]: bs=8)" % EXTRACT_BATCH)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--graph", action="store_true",
