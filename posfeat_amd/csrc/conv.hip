@@ -724,10 +724,10 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_glds_kernel(ConvArgs a) {
 // are those of the BF6 tiles: results are bit-identical to them.
 // amdgpu_waves_per_eu(2): the accumulators move from AGPRs to VGPRs within
 // the 256-register budget of two waves per SIMD (same box, r5y: +0.6 %)
-template <int BM, int BN>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+template <int BM, int BN, int NWV = 4>
+__global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(2)))
 void conv_bf6b_kernel(ConvArgs a) {
-  constexpr int WM = 4, WN = 1, NW = 4;
+  constexpr int WM = NWV, WN = 1, NW = NWV;
   constexpr int TM = BM / WM, TN = BN;
   constexpr int MI = TM / 32, NI = TN / 32;
   constexpr int A_G = BM / 8 / NW;
@@ -1083,6 +1083,154 @@ void conv_bf6p_kernel(ConvArgs a) {
     if (!more_tiles) break;
     t = tn_;
   }
+}
+
+// ---------------------------------------------------------------------------
+// Dense pre-split-weight GEMM tiles with a DEEP A prefetch (conv_bf6d_kernel,
+// POSFEAT_BF6D = D).  The LDS ring of conv_bf6b_kernel bounds the bytes
+// in flight per CU (two 40-KB stages per block, half of them being read): with
+// HBM latencies of several thousand cycles under load the next chunk often
+// lands after the current one is multiplied.  Here A (the streaming operand,
+// V / activations) goes straight to registers D chunks ahead (16 VGPRs per
+// chunk per lane), and only the weight planes (L2-resident) use a two-stage
+// LDS ring.  Per chunk: wait for B(c) (the A loads issued after it stay in
+// flight), barrier, DMA B(c+1), split A(c), load A(c+D) into the freed
+// registers, 48 MFMAs.  Same products in the same order as bf6b: bit-identical.
+// The default for the dense pre-split tiles (bf6d_depth below).
+template <int BM, int BN, int D>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+void conv_bf6d_kernel(ConvArgs a) {
+  constexpr int WM = 4, WN = 1, NW = 4;
+  constexpr int TM = BM / WM, TN = BN;
+  constexpr int MI = TM / 32, NI = TN / 32;
+  constexpr int B_G = 3 * BN / 16 / NW;
+  static_assert(MI == 1 && B_G >= 1 && (3 * BN / 16) % NW == 0 && D >= 2 && D <= 4, "tile");
+  constexpr int BSTAGE = 3 * BN * BK / 2;  // floats (u16 pairs)
+  constexpr int RING = 2 * BSTAGE;
+  constexpr int EPI = BM * (BN + 4);
+  __shared__ __attribute__((aligned(16))) float smem[RING > EPI ? RING : EPI];
+  unsigned short* const Bs = reinterpret_cast<unsigned short*>(smem);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  int bid = blockIdx.x % a.nwg;
+  const int split = blockIdx.x / a.nwg;
+  {
+    const int nwg = a.nwg, q = nwg >> 3, r = nwg & 7, xcd = bid & 7, slot = bid >> 3;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+  }
+  const unsigned short* wb = a.wb;
+  if (a.nbatch > 1) {
+    const long long zb = blockIdx.y;
+    a.x += zb * a.bx;
+    a.y += zb * a.by;
+    wb += zb * a.bwb;
+  }
+  const int tm = bid / a.tiles_n, tn = bid - tm * a.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int r32 = lane & 31, hh = lane >> 5;
+  // dense (1x1, no padding): the lane's A row; rows past M re-read the last one
+  const float* xrow;
+  {
+    const int m = min(m0 + wave * 32 + r32, a.M - 1);
+    const int n = m / a.hw, rem = m - n * a.hw;
+    const int oh = rem / a.OW, ow = rem - oh * a.OW;
+    xrow = a.x + (((long long)n * a.H + oh * a.stride) * a.W + ow * a.stride) * a.xcs + hh * 8;
+  }
+  const unsigned short* bsrc[B_G];
+#pragma unroll
+  for (int i = 0; i < B_G; ++i) {
+    const int pr = (wave * B_G + i) * 16 + (lane >> 2);
+    const int plane = pr / BN, row = pr - plane * BN;
+    const int ks = (lane & 3) ^ ((row >> 2) & 3);
+    bsrc[i] = wb + plane * a.wplane + (long long)min(n0 + row, a.Cout - 1) * a.Kpad + ks * 8;
+  }
+  const int nch_all = a.Kpad / BK;
+  const int ch0 = (int)((long long)nch_all * split / a.ksplit);
+  const int ch1 = (int)((long long)nch_all * (split + 1) / a.ksplit);
+  const int nch = ch1 - ch0;
+
+  auto issue_b = [&](unsigned short* Bd, int c) {
+#pragma unroll
+    for (int i = 0; i < B_G; ++i)
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(bsrc[i] + (long long)c * BK),
+          (__attribute__((address_space(3))) void*)(Bd + (wave * B_G + i) * 16 * BK), 16, 0, 0);
+  };
+  auto load_a = [&](int c, f32x4 (&v)[4]) {
+    const float* p = xrow + (long long)c * BK;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = *reinterpret_cast<const f32x4*>(p + (j >> 1) * 16 + (j & 1) * 4);
+  };
+
+  f32x16 acc[NI];
+#pragma unroll
+  for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[ni][r] = 0.f;
+
+  f32x4 va[D][4];
+  if (nch > 0) issue_b(Bs, ch0);
+#pragma unroll
+  for (int j = 0; j < D; ++j)
+    if (j < nch) load_a(ch0 + j, va[j]);
+
+  for (int i = 0; i < nch; i += D) {
+#pragma unroll
+    for (int u = 0; u < D; ++u) {
+      const int ii = i + u;
+      if (ii >= nch) break;
+      // B(ii) landed: it was issued before the 4 A loads of chunk ii-1+D (if any)
+      if (ii - 1 + D < nch && ii > 0)
+        wait_vmcnt<4>();
+      else if (ii == 0 && D < nch)
+        wait_vmcnt<4 * D>();
+      else
+        wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+      const int s = ii & 1;
+      // split this chunk's A (frees va[u] for chunk ii + D)
+      u32x4_t ah[2], am[2], al[2];
+#pragma unroll
+      for (int g = 0; g < 2; ++g) split3(va[u][2 * g], va[u][2 * g + 1], ah[g], am[g], al[g]);
+      pf_dma_overlap_step(
+          Bs + (s ^ 1) * 2 * BSTAGE, Bs + (s ^ 1) * 2 * BSTAGE + BSTAGE, Bs + s * 2 * BSTAGE,
+          Bs + s * 2 * BSTAGE + BSTAGE, ii + 1 < nch,
+          [&](unsigned short* Bd, unsigned short*) {
+            issue_b(Bd, ch0 + ii + 1);
+            if (ii + D < nch) load_a(ch0 + ii + D, va[u]);
+          },
+          [&](const unsigned short* Bb, const unsigned short*) {
+#pragma unroll
+            for (int g = 0; g < 2; ++g)
+#pragma unroll
+              for (int ni = 0; ni < NI; ++ni) {
+                const int row = ni * 32 + r32;
+                const int slot = (2 * g + hh) ^ ((row >> 2) & 3);
+                const unsigned short* bp = Bb + row * BK + slot * 8;
+                const u32x4_t bh = *reinterpret_cast<const u32x4_t*>(bp);
+                const u32x4_t bm = *reinterpret_cast<const u32x4_t*>(bp + BN * BK);
+                const u32x4_t bl = *reinterpret_cast<const u32x4_t*>(bp + 2 * BN * BK);
+                f32x16 c = acc[ni];
+                c = mfma_bf16(ah[g], bh, c);
+                c = mfma_bf16(ah[g], bm, c);
+                c = mfma_bf16(am[g], bh, c);
+                c = mfma_bf16(ah[g], bl, c);
+                c = mfma_bf16(al[g], bh, c);
+                c = mfma_bf16(am[g], bm, c);
+                acc[ni] = c;
+              }
+          });
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  f32x16 accm[1][NI];
+#pragma unroll
+  for (int ni = 0; ni < NI; ++ni) accm[0][ni] = acc[ni];
+  conv_epilogue<BM, BN, WM, WN>(
+      a, accm, smem, tm, n0, split, [&](int row) { return m0 + row < a.M ? m0 + row : -1; },
+      m0 / a.hw,
+      [&](int, int m) { return a.res ? a.res + (size_t)m * a.rcs : (const float*)nullptr; });
 }
 
 // ---------------------------------------------------------------------------
@@ -1927,7 +2075,8 @@ enum ConvTile {
   TILE_H8x128 = 10, TILE_H8x64 = 11, TILE_H16x128 = 12,                 // 8/16 x 16 patches
   TILE_BF6_128x128 = 20, TILE_BF6_128x256 = 21, TILE_BF6_64x128 = 22,   // rows, bf16x6 products
   TILE_BF6_128x64 = 23, TILE_BF6B_128x128 = 24, TILE_BF6B_128x64 = 25,  // + pre-split weights
-  TILE_BF6R_128x128 = 26, TILE_BF6R_128x64 = 27  // + A straight to registers
+  TILE_BF6R_128x128 = 26, TILE_BF6R_128x64 = 27,  // + A straight to registers
+  TILE_BF6B_256x128 = 28  // pre-split weights, 8 waves stacked along M (one 135-KB block per CU)
 };
 
 // POSFEAT_BF6=1: every conv the row-tile DMA kernel serves (1x1, strided, the
@@ -1986,6 +2135,19 @@ int bf6p_blocks() {
     return v >= 8 ? v / 8 * 8 : 512;  // a multiple of 8: whole XCD groups
   }();
   return n;
+}
+
+// Dense pre-split tiles (TILE_BF6B_*) run conv_bf6d_kernel with A prefetched
+// POSFEAT_BF6D = 2..4 chunks ahead in registers (default 3; 0: the LDS-staged
+// conv_bf6b_kernel).  Same box, r6k: 945.6 -> 970 img/s (D = 3), decoder
+// Winograd GEMMs -4..-7 %, tap GEMM -9 %; bit-identical (test_gpu_bf6r.py)
+int bf6d_depth() {
+  static const int d = [] {
+    const char* e = getenv("POSFEAT_BF6D");
+    const int v = e ? atoi(e) : 3;
+    return v >= 2 && v <= 4 ? v : 0;
+  }();
+  return d;
 }
 
 bool bf6r_on() {
@@ -2071,10 +2233,18 @@ Plan plan_for_tile(const ConvArgs& a, int tile) {
   // bf16x6 mode: halo-eligible convs keep fp32 halo tiles only, the rest
   // bf16x6 row tiles only
   if (bf6_on() && glds_ok) {
-    const bool bf6_tile = tile >= TILE_BF6_128x128 && tile <= TILE_BF6R_128x64;
+    const bool bf6_tile = tile >= TILE_BF6_128x128 && tile <= TILE_BF6B_256x128;
     if (halo_ok ? bf6_tile || tile < TILE_H8x128 : !bf6_tile) return p;
   }
   switch (tile) {
+    case TILE_BF6B_256x128:
+      if (!glds_ok || !bf6_on() || !a.wb || a.Cout <= 64) return p;
+      p.kern = KERN_GLDS;
+      p.bm = 256;
+      p.bn = 128;
+      p.ppi = 0;
+      p.tiles_m = (a.M + p.bm - 1) / p.bm;
+      return p;
     case TILE_BF6B_128x128:
     case TILE_BF6B_128x64:
     case TILE_BF6R_128x128:
@@ -2256,6 +2426,21 @@ int conv_run(ConvArgs& a, const Plan& p, hipStream_t st) {
           hipLaunchKernelGGL((conv_bf6p_kernel<128, 128>), dim3(grid), dim3(256), 0, st, a);
         else
           hipLaunchKernelGGL((conv_bf6p_kernel<128, 64>), dim3(grid), dim3(256), 0, st, a);
+      } else if (bf6d_depth() && a.KH == 1 && a.KW == 1 && a.pad == 0) {
+        const dim3 g(a.nwg * a.ksplit, a.nbatch);
+        const int dd = bf6d_depth();
+        if (wide && dd == 2)
+          hipLaunchKernelGGL((conv_bf6d_kernel<128, 128, 2>), g, dim3(256), 0, st, a);
+        else if (wide && dd == 3)
+          hipLaunchKernelGGL((conv_bf6d_kernel<128, 128, 3>), g, dim3(256), 0, st, a);
+        else if (wide)
+          hipLaunchKernelGGL((conv_bf6d_kernel<128, 128, 4>), g, dim3(256), 0, st, a);
+        else if (dd == 2)
+          hipLaunchKernelGGL((conv_bf6d_kernel<128, 64, 2>), g, dim3(256), 0, st, a);
+        else if (dd == 3)
+          hipLaunchKernelGGL((conv_bf6d_kernel<128, 64, 3>), g, dim3(256), 0, st, a);
+        else
+          hipLaunchKernelGGL((conv_bf6d_kernel<128, 64, 4>), g, dim3(256), 0, st, a);
       } else if (wide) {
         hipLaunchKernelGGL((conv_bf6b_kernel<128, 128>), dim3(a.nwg * a.ksplit, a.nbatch),
                            dim3(256), 0, st, a);
@@ -2265,6 +2450,10 @@ int conv_run(ConvArgs& a, const Plan& p, hipStream_t st) {
       }
       break;
     }
+    case TILE_BF6B_256x128:
+      hipLaunchKernelGGL((conv_bf6b_kernel<256, 128, 8>), dim3(a.nwg * a.ksplit, a.nbatch),
+                         dim3(512), 0, st, a);
+      break;
     case TILE_BF6R_128x128:
       if (bf6r_nst() == 3)
         hipLaunchKernelGGL((conv_bf6r_kernel<128, 128, 3>), dim3(a.nwg * a.ksplit, a.nbatch),
@@ -2444,7 +2633,7 @@ static const int kAllTiles[] = {TILE_H8x128,      TILE_H8x64,       TILE_128x128
                                 TILE_128x64,      TILE_64x64,       TILE_256x128,
                                 TILE_BF6_128x128, TILE_BF6_128x256, TILE_BF6_64x128,
                                 TILE_BF6_128x64,  TILE_BF6B_128x128, TILE_BF6B_128x64,
-                                TILE_BF6R_128x128, TILE_BF6R_128x64};
+                                TILE_BF6R_128x128, TILE_BF6R_128x64,  TILE_BF6B_256x128};
 
 int pf_conv_candidates(const posfeat_conv_desc* d, int* tiles, int max, bool wplanes) {
   ConvArgs a;
@@ -2691,7 +2880,13 @@ int pf_gemm_batched(const float* A, int lda, long long sa, const float* B, long 
     const char* e = getenv("POSFEAT_GEMM_N64");
     return !(e && e[0] == '0');
   }();
-  const int want = (N % 128 == 0 && t128 >= 1024) ? TILE_128x128
+  // POSFEAT_GEMM_B256=1 (A/B): the 8-wave 256x128 pre-split tiles
+  static const bool b256 = [] {
+    const char* e = getenv("POSFEAT_GEMM_B256");
+    return e && e[0] == '1';
+  }();
+  const int want = (Bb && b256 && N % 128 == 0) ? TILE_BF6B_256x128
+                   : (N % 128 == 0 && t128 >= 1024) ? TILE_128x128
                    : (Bb && n64 && N % 128 != 0 && N % 64 == 0) ? TILE_BF6B_128x64
                                                                  : -1;
   const Plan p = conv_plan(a, false, want);

@@ -51,9 +51,16 @@ def test_fused_upsample_bit_identical(tmp_path):
 
 
 def test_bf6r_bit_identical_to_bf6b(tmp_path):
-    ref = _run(tmp_path, {"POSFEAT_BF6R": "0"}, "b")   # the default
+    """also the 8-wave 256x128 pre-split tile (TILE_BF6B_256x128 = 28: an
+    autotuner candidate for the 1x1 convs, forced everywhere it is legal, and
+    on the batched Winograd GEMMs via POSFEAT_GEMM_B256) and the deep-A-prefetch
+    tiles (conv_bf6d_kernel, POSFEAT_BF6D=3)"""
+    ref = _run(tmp_path, {"POSFEAT_BF6R": "0", "POSFEAT_BF6D": "0"}, "b")   # LDS-staged bf6b
     for tag, env in (("r2", {"POSFEAT_BF6R": "1"}),
-                     ("r3", {"POSFEAT_BF6R": "1", "POSFEAT_BF6R_NST": "3"})):
+                     ("r3", {"POSFEAT_BF6R": "1", "POSFEAT_BF6R_NST": "3"}),
+                     ("b256", {"POSFEAT_CONV_TILE": "28", "POSFEAT_GEMM_B256": "1"}),
+                     ("d3", {}),                       # the default: deep A prefetch, D = 3
+                     ("d2", {"POSFEAT_BF6D": "2"})):
         got = _run(tmp_path, env, tag)
         for k in ("lp", "lm", "gm"):
             np.testing.assert_array_equal(got[k], ref[k], err_msg="%s %s" % (tag, k))
