@@ -1086,8 +1086,8 @@ void conv_bf6p_kernel(ConvArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Dense pre-split-weight GEMM tiles with a DEEP A prefetch (conv_bf6d_kernel,
-// POSFEAT_BF6D = D).  The LDS ring of conv_bf6b_kernel bounds the bytes
+// Pre-split-weight GEMM / conv tiles with a DEEP A prefetch (conv_bf6d_kernel,
+// POSFEAT_BF6D = D; any KH x KW / stride / pad with Cin % 32 == 0).  The LDS ring of conv_bf6b_kernel bounds the bytes
 // in flight per CU (two 40-KB stages per block, half of them being read): with
 // HBM latencies of several thousand cycles under load the next chunk often
 // lands after the current one is multiplied.  Here A (the streaming operand,
@@ -1128,14 +1128,24 @@ void conv_bf6d_kernel(ConvArgs a) {
   const int tm = bid / a.tiles_n, tn = bid - tm * a.tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
   const int r32 = lane & 31, hh = lane >> 5;
-  // dense (1x1, no padding): the lane's A row; rows past M re-read the last one
-  const float* xrow;
+  // the lane's A row (base of tap (0,0) + its k offset 8h) and the taps that
+  // fall inside the image; rows past M read zeros (never stored)
+  const float* xrow = a.x;
+  unsigned tapok = 0u;
   {
-    const int m = min(m0 + wave * 32 + r32, a.M - 1);
-    const int n = m / a.hw, rem = m - n * a.hw;
-    const int oh = rem / a.OW, ow = rem - oh * a.OW;
-    xrow = a.x + (((long long)n * a.H + oh * a.stride) * a.W + ow * a.stride) * a.xcs + hh * 8;
+    const int m = m0 + wave * 32 + r32;
+    if (m < a.M) {
+      const int n = m / a.hw, rem = m - n * a.hw;
+      const int oh = rem / a.OW, ow = rem - oh * a.OW;
+      const int ih0 = oh * a.stride - a.pad, iw0 = ow * a.stride - a.pad;
+      for (int kh = 0; kh < a.KH; ++kh)
+        for (int kw = 0; kw < a.KW; ++kw)
+          if ((unsigned)(ih0 + kh) < (unsigned)a.H && (unsigned)(iw0 + kw) < (unsigned)a.W)
+            tapok |= 1u << (kh * a.KW + kw);
+      xrow = a.x + (long long)n * a.H * a.W * a.xcs + ((long long)ih0 * a.W + iw0) * a.xcs + hh * 8;
+    }
   }
+  const int ntap = a.KH * a.KW;
   const unsigned short* bsrc[B_G];
 #pragma unroll
   for (int i = 0; i < B_G; ++i) {
@@ -1156,10 +1166,17 @@ void conv_bf6d_kernel(ConvArgs a) {
           (const __attribute__((address_space(1))) void*)(bsrc[i] + (long long)c * BK),
           (__attribute__((address_space(3))) void*)(Bd + (wave * B_G + i) * 16 * BK), 16, 0, 0);
   };
+  // chunk c = (slab, tap): always four loads per lane (a masked tap reads the
+  // zeroed 16-B word), so the per-chunk vmcnt accounting below holds
+  const float* const zero = a.zero;
   auto load_a = [&](int c, f32x4 (&v)[4]) {
-    const float* p = xrow + (long long)c * BK;
+    const int slab = c / ntap, tap = c - slab * ntap;
+    const int kh = tap / a.KW, kw = tap - kh * a.KW;
+    const bool ok = (tapok >> tap) & 1u;
+    const float* p = xrow + ((long long)kh * a.W + kw) * a.xcs + (long long)slab * BK;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = *reinterpret_cast<const f32x4*>(p + (j >> 1) * 16 + (j & 1) * 4);
+    for (int j = 0; j < 4; ++j)
+      v[j] = *reinterpret_cast<const f32x4*>(ok ? p + (j >> 1) * 16 + (j & 1) * 4 : zero);
   };
 
   f32x16 acc[NI];
@@ -2455,7 +2472,15 @@ int conv_run(ConvArgs& a, const Plan& p, hipStream_t st) {
                          dim3(512), 0, st, a);
       break;
     case TILE_BF6R_128x128:
-      if (bf6r_nst() == 3)
+      if (bf6d_depth()) {  // the register-A tiles: A now prefetched D chunks ahead
+        const dim3 g(a.nwg * a.ksplit, a.nbatch);
+        if (bf6d_depth() == 2)
+          hipLaunchKernelGGL((conv_bf6d_kernel<128, 128, 2>), g, dim3(256), 0, st, a);
+        else if (bf6d_depth() == 3)
+          hipLaunchKernelGGL((conv_bf6d_kernel<128, 128, 3>), g, dim3(256), 0, st, a);
+        else
+          hipLaunchKernelGGL((conv_bf6d_kernel<128, 128, 4>), g, dim3(256), 0, st, a);
+      } else if (bf6r_nst() == 3)
         hipLaunchKernelGGL((conv_bf6r_kernel<128, 128, 3>), dim3(a.nwg * a.ksplit, a.nbatch),
                            dim3(256), 0, st, a);
       else
@@ -2463,7 +2488,15 @@ int conv_run(ConvArgs& a, const Plan& p, hipStream_t st) {
                            dim3(256), 0, st, a);
       break;
     case TILE_BF6R_128x64:
-      if (bf6r_nst() == 3)
+      if (bf6d_depth()) {
+        const dim3 g(a.nwg * a.ksplit, a.nbatch);
+        if (bf6d_depth() == 2)
+          hipLaunchKernelGGL((conv_bf6d_kernel<128, 64, 2>), g, dim3(256), 0, st, a);
+        else if (bf6d_depth() == 3)
+          hipLaunchKernelGGL((conv_bf6d_kernel<128, 64, 3>), g, dim3(256), 0, st, a);
+        else
+          hipLaunchKernelGGL((conv_bf6d_kernel<128, 64, 4>), g, dim3(256), 0, st, a);
+      } else if (bf6r_nst() == 3)
         hipLaunchKernelGGL((conv_bf6r_kernel<128, 64, 3>), dim3(a.nwg * a.ksplit, a.nbatch),
                            dim3(256), 0, st, a);
       else
