@@ -49,10 +49,10 @@ HEAD_CONV2_FLOP_PER_IMAGE = 2.0 * 480 * 640 * 128 * 256 * 9   # reference layer
 # (conv:head.conv2.up4tap).  The engine's timing events carry the FLOPs each
 # launch executes.
 GEMM_LABEL_KERNELS = {
-    ".wino": "conv_bf6d_kernel<128,128,3> x36 batched (Winograd F(4x4) transform-domain "
-             "GEMMs of %s; bf16x6 on pre-split U planes, A prefetched 3 chunks ahead in "
+    ".wino": "conv_bf6d_kernel<128,128,2> x36 batched (Winograd F(4x4) transform-domain "
+             "GEMMs of %s; bf16x6 on pre-split U planes, A prefetched 2 chunks ahead in "
              "registers)",
-    "up4tap": "conv_bf6d_kernel<128,128,3> or its autotuned bit-identical twin (head.conv2's 192 "
+    "up4tap": "conv_bf6d_kernel<128,128,2> or its autotuned bit-identical twin (head.conv2's 192 "
               "x4-upsampled channels: nine 1x1 convs on the 120x160 grid as one [B*19200 x 192] "
               "x [192 x 1152] GEMM)",
 }

@@ -1096,7 +1096,7 @@ void conv_bf6p_kernel(ConvArgs a) {
 // LDS ring.  Per chunk: wait for B(c) (the A loads issued after it stay in
 // flight), barrier, DMA B(c+1), split A(c), load A(c+D) into the freed
 // registers, 48 MFMAs.  Same products in the same order as bf6b: bit-identical.
-// The default for the dense pre-split tiles (bf6d_depth below).
+// The default for the pre-split tiles (bf6d_depth below: D = 2).
 template <int BM, int BN, int D>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
 void conv_bf6d_kernel(ConvArgs a) {
@@ -2154,14 +2154,16 @@ int bf6p_blocks() {
   return n;
 }
 
-// Dense pre-split tiles (TILE_BF6B_*) run conv_bf6d_kernel with A prefetched
-// POSFEAT_BF6D = 2..4 chunks ahead in registers (default 3; 0: the LDS-staged
-// conv_bf6b_kernel).  Same box, r6k: 945.6 -> 970 img/s (D = 3), decoder
-// Winograd GEMMs -4..-7 %, tap GEMM -9 %; bit-identical (test_gpu_bf6r.py)
+// Dense pre-split tiles (TILE_BF6B_*) and the register-A candidates
+// (TILE_BF6R_*) run conv_bf6d_kernel with A prefetched POSFEAT_BF6D = 2..4
+// chunks ahead in registers (default 2; 0: conv_bf6b / conv_bf6r).  Same box,
+// r6k: 945.6 -> 970 img/s (D = 3), decoder Winograd GEMMs -4..-7 %, tap GEMM
+// -9 %; r6q, two pairs each: D = 2 973.1, 3 968.4, 4 966.3 img/s;
+// bit-identical (test_gpu_bf6r.py)
 int bf6d_depth() {
   static const int d = [] {
     const char* e = getenv("POSFEAT_BF6D");
-    const int v = e ? atoi(e) : 3;
+    const int v = e ? atoi(e) : 2;
     return v >= 2 && v <= 4 ? v : 0;
   }();
   return d;

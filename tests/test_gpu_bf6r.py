@@ -59,8 +59,8 @@ def test_bf6r_bit_identical_to_bf6b(tmp_path):
     for tag, env in (("r2", {"POSFEAT_BF6R": "1"}),
                      ("r3", {"POSFEAT_BF6R": "1", "POSFEAT_BF6R_NST": "3"}),
                      ("b256", {"POSFEAT_CONV_TILE": "28", "POSFEAT_GEMM_B256": "1"}),
-                     ("d3", {}),                       # the default: deep A prefetch, D = 3
-                     ("d2", {"POSFEAT_BF6D": "2"})):
+                     ("d2", {}),                       # the default: deep A prefetch, D = 2
+                     ("d3", {"POSFEAT_BF6D": "3"})):
         got = _run(tmp_path, env, tag)
         for k in ("lp", "lm", "gm"):
             np.testing.assert_array_equal(got[k], ref[k], err_msg="%s %s" % (tag, k))
