@@ -1097,10 +1097,10 @@ void conv_bf6p_kernel(ConvArgs a) {
 // flight), barrier, DMA B(c+1), split A(c), load A(c+D) into the freed
 // registers, 48 MFMAs.  Same products in the same order as bf6b: bit-identical.
 // The default for the pre-split tiles (bf6d_depth below: D = 2).
-template <int BM, int BN, int D>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+template <int BM, int BN, int D, int NWV = 4>
+__global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(2)))
 void conv_bf6d_kernel(ConvArgs a) {
-  constexpr int WM = 4, WN = 1, NW = 4;
+  constexpr int WM = NWV, WN = 1, NW = NWV;
   constexpr int TM = BM / WM, TN = BN;
   constexpr int MI = TM / 32, NI = TN / 32;
   constexpr int B_G = 3 * BN / 16 / NW;
@@ -2470,8 +2470,15 @@ int conv_run(ConvArgs& a, const Plan& p, hipStream_t st) {
       break;
     }
     case TILE_BF6B_256x128:
-      hipLaunchKernelGGL((conv_bf6b_kernel<256, 128, 8>), dim3(a.nwg * a.ksplit, a.nbatch),
-                         dim3(512), 0, st, a);
+      if (bf6d_depth() == 2)
+        hipLaunchKernelGGL((conv_bf6d_kernel<256, 128, 2, 8>), dim3(a.nwg * a.ksplit, a.nbatch),
+                           dim3(512), 0, st, a);
+      else if (bf6d_depth())
+        hipLaunchKernelGGL((conv_bf6d_kernel<256, 128, 3, 8>), dim3(a.nwg * a.ksplit, a.nbatch),
+                           dim3(512), 0, st, a);
+      else
+        hipLaunchKernelGGL((conv_bf6b_kernel<256, 128, 8>), dim3(a.nwg * a.ksplit, a.nbatch),
+                           dim3(512), 0, st, a);
       break;
     case TILE_BF6R_128x128:
       if (bf6d_depth()) {  // the register-A tiles: A now prefetched D chunks ahead
