@@ -687,10 +687,16 @@ int pf_gfuse_conv(const float* img4, const float* c, int ccs, int n, int H, int 
                        wplanes);
     const int nt8 = ((W + G8_TC - 1) / G8_TC) * ((H + G8_TR - 1) / G8_TR);
     // persistent blocks (one image's tiles each): POSFEAT_GFUSE_BLOCKS in
-    // total over the batch (default 512); fewer leave CUs to the main stream
+    // total over the batch (default 64, at least one per image); fewer leave
+    // CUs to the main stream; tiles are independent, so the count never
+    // changes results
     static const int tot_blocks = [] {
       const char* e = getenv("POSFEAT_GFUSE_BLOCKS");
-      const int v = e ? atoi(e) : 64;  // r3w sweep: 512 820, 96 830, 64 841, 48 841, 32 837 img/s
+      // r3w sweep (B = 8): 512 820, 96 830, 64 841, 48 841, 32 837 img/s;
+      // r6w (B = 32, bf6d main stream, two pairs): 32 977.1, 64 971.4, 128
+      // 970.2 -- but at 32 the longer side stream lands on iconv3's GEMM
+      // (2.39 ms, the dominant launch; r6x), so the default stays 64
+      const int v = e ? atoi(e) : 64;
       return v > 0 ? v : 64;
     }();
     const int per_img = std::max(1, std::min(nt8, (tot_blocks + n - 1) / n));
