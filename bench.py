@@ -44,10 +44,10 @@ EXTRACT_BATCH = 32
 CONV_FLOP_PER_IMAGE = 417.98e9
 HEAD_CONV2_FLOP_PER_IMAGE = 2.0 * 480 * 640 * 128 * 256 * 9   # reference layer
 # dominant kernel (roofline): the single MFMA launch with the largest time in
-# the step, among the engine's one-launch GEMM labels -- the batched Winograd
-# GEMMs of the decoder (conv:<layer>.wino) and head.conv2's low-res tap GEMM
-# (conv:head.conv2.up4tap).  The engine's timing events carry the FLOPs each
-# launch executes.
+# the step, over EVERY main-stream conv label the engine times (the batched
+# Winograd GEMMs of the decoder and the encoder, head.conv2's low-res tap GEMM,
+# the 1x1 / strided / halo convs, the stem).  The engine's timing events carry
+# the FLOPs each launch executes.
 GEMM_LABEL_KERNELS = {
     ".wino": "conv_bf6d_kernel<128,128,2> x36 batched (Winograd F(4x4) transform-domain "
              "GEMMs of %s; bf16x6 on pre-split U planes, A prefetched 2 chunks ahead in "
@@ -55,7 +55,11 @@ GEMM_LABEL_KERNELS = {
     "up4tap": "conv_bf6d_kernel<128,128,2> or its autotuned bit-identical twin (head.conv2's 192 "
               "x4-upsampled channels: nine 1x1 convs on the 120x160 grid as one [B*19200 x 192] "
               "x [192 x 1152] GEMM)",
+    "": "the autotuned conv tile of %s (conv.hip MFMA implicit GEMM)",
 }
+# conv labels whose kernels keep fp32-input MFMA in every precision mode (the
+# Cin = 4 stem on the register-staged tiles)
+FP32_MFMA_LABELS = ("conv:firstconv",)
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md, dense FP32 matrix (spec)
 PEAK_BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md, dense BF16 matrix (no sparsity)
 
@@ -369,7 +373,7 @@ def main():
         step(engine, ops, ws, imgs)
         ev = engine.timing_events(args.batch, H, W)
         for lab, ms, fl in ev:
-            if lab.startswith("conv:") and any(lab.endswith(k) for k in GEMM_LABEL_KERNELS):
+            if lab.startswith("conv:") and fl > 0:
                 per_label.setdefault(lab, []).append((ms, fl))
         main = [e for e in ev if not e[0].startswith("side:")]
         c2_ms.append(sum(ms for lab, ms, _ in main if lab.startswith(("conv:head.conv2",
@@ -383,9 +387,14 @@ def main():
     kms = float(np.mean([m for m, _ in per_label[dom]]))
     k_flops = float(np.mean([f for _, f in per_label[dom]]))
     achieved = k_flops / (kms * 1e-3) / 1e12
-    kdesc = next(v for k, v in GEMM_LABEL_KERNELS.items() if dom.endswith(k))
-    kdesc = kdesc % dom[len("conv:"):-len(".wino")] if "%s" in kdesc else kdesc
+    kkey = next(k for k in GEMM_LABEL_KERNELS if dom.endswith(k))
+    kdesc = GEMM_LABEL_KERNELS[kkey]
+    if "%s" in kdesc:
+        kdesc = kdesc % (dom[len("conv:"):-len(kkey)] if kkey else dom[len("conv:"):])
     arith = conv_arithmetic()
+    if dom in FP32_MFMA_LABELS:   # this launch runs fp32-input MFMA whatever the mode
+        arith = {"arithmetic": "fp32-input MFMA v_mfma_f32_32x32x2_f32",
+                 "method_peak": PEAK_FP32_MFMA_TFLOPS}
     c2 = float(np.mean(c2_ms))
     conv_total = float(np.mean(conv_ms))
     conv_ach = float(np.mean(conv_fl)) / (conv_total * 1e-3) / 1e12
@@ -426,15 +435,18 @@ def main():
                        "num_pts": NUM_PTS, "parallelism": "dp%d (image-sharded)" % world},
             "roofline": {"kernel": kdesc, "label": dom,
                          "bound": "mfma", "achieved": round(achieved, 3),
-                         "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4),
+                         "peak": arith["method_peak"], "unit": "TFLOP/s",
+                         "frac": round(achieved / arith["method_peak"], 4),
                          "traffic": traffic,
                          "avg_launch_ms": round(kms, 4), "flop_per_launch": k_flops,
-                         **arith,
-                         "method_frac": round(achieved / arith["method_peak"], 4),
-                         "note": "achieved = fp32 FLOP of the GEMM / its HIP-event time; peak = "
-                                 "the dense FP32 MFMA peak (dtype fp32); method_peak = the "
-                                 "ceiling of the arithmetic actually used"},
+                         "arithmetic": arith["arithmetic"],
+                         "fp32_mfma_peak": PEAK_FP32_MFMA_TFLOPS,
+                         "frac_of_fp32_mfma_peak": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4),
+                         "note": "achieved = fp32 FLOP the launch executes / its HIP-event time "
+                                 "on the engine stream; peak = the ceiling of the instruction "
+                                 "mix it runs (bf16x6: dense BF16 MFMA 2500 TF / 6 products); "
+                                 "frac_of_fp32_mfma_peak is the same rate against the 157.3 TF "
+                                 "fp32-input MFMA peak"},
             "head_conv2": {"ms_per_step": round(c2, 3),
                            "note": "main-stream part (low-res tap GEMM + combine); the G part "
                                    "(IN(convimg) channels) runs on the side stream",

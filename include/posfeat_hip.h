@@ -80,14 +80,6 @@ int posfeat_conv_packed_k(int cin, int kh, int kw); /* returns Kpad */
  * 3x3 stride-1 convs always run the fp32 halo kernel.  Instances created
  * afterwards plan with the new mode.  mode = -1: query only. */
 int posfeat_set_conv_precision(int mode);
-/* Tile schedule of the dense pre-split-weight GEMMs (1x1 convs without
- * padding: the Winograd transform-domain GEMMs, the tap GEMM, the 1x1
- * layers).  1: persistent workgroups that prefetch the next tile's first
- * chunk under the current tile's last chunk and store straight from the
- * accumulators; 0 (default, measured faster): one workgroup per tile.  Same
- * products, same order: bit-identical outputs.  Read at every launch; returns the previous mode;
- * mode = -1: query only.  (Internal tiling, no reference counterpart.) */
-int posfeat_set_conv_persistent(int mode);
 int posfeat_conv2d_nhwc(const posfeat_conv_desc *d, const float *x, const float *w,
                         const float *bias, const float *res, float *y, void *stream);
 /* Same, allowed to split K over workgroups (deterministic: fp32 partial slabs

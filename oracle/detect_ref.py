@@ -92,6 +92,26 @@ def _mask_and_inner(kp_map, nms_radius, use_nms, thr, thr_mod):
     return inner, mask
 
 
+def refine_maps(km):
+    """Soft-argmax refinement of every inner pixel (preprocess_utils.py:243-246):
+    avgpool3(kp * grid) / avgpool3(kp), normalised coordinates, for a (h, w)
+    score map.  Returns (rx, ry), each (h-2, w-2) float32."""
+    h, w = km.shape
+    km = np.asarray(km, np.float64)
+    grid = gen_grid(-1, 1, -1, 1, h, w).reshape(h, w, 2)
+    gx = km * grid[..., 0]
+    gy = km * grid[..., 1]
+
+    def box(a):
+        s = np.zeros((h - 2, w - 2), np.float64)
+        for dy in range(3):
+            for dx in range(3):
+                s += a[dy:dy + h - 2, dx:dx + w - 2]
+        return s / 9.0
+    wgt = box(km)
+    return (box(gx) / wgt).astype(np.float32), (box(gy) / wgt).astype(np.float32)
+
+
 def generate_kpts_single(kp_map, nms_radius, num_pts=False, use_nms=True, thr=False,
                          thr_mod="mean", return_idx=False):
     """kp_map: (b,1,h,w) float32.  Returns coord_n (b,n,2), kp_score (b,n,1)[, idx (b,n)]."""
@@ -107,23 +127,9 @@ def generate_kpts_single(kp_map, nms_radius, num_pts=False, use_nms=True, thr=Fa
             n = int(counts.min())
     if n < 128:
         n = 128
-    # refine: avgpool3(kp*grid)/avgpool3(kp); score: maxpool3(kp) (preprocess_utils.py:243-247)
-    grid = gen_grid(-1, 1, -1, 1, h, w).reshape(h, w, 2)
     coords, scores, idxs = [], [], []
     for i in range(b):
-        km = kp_map[i, 0].astype(np.float64)
-        gx = km * grid[..., 0]
-        gy = km * grid[..., 1]
-
-        def box(a):
-            s = np.zeros((h - 2, w - 2), np.float64)
-            for dy in range(3):
-                for dx in range(3):
-                    s += a[dy:dy + h - 2, dx:dx + w - 2]
-            return s / 9.0
-        wgt = box(km)
-        rx = (box(gx) / wgt).astype(np.float32)
-        ry = (box(gy) / wgt).astype(np.float32)
+        rx, ry = refine_maps(kp_map[i, 0])
         mx = np.full((h - 2, w - 2), -np.inf, np.float32)
         for dy in range(3):
             for dx in range(3):

@@ -47,7 +47,6 @@ SIGNATURES = {
     "posfeat_device_ok": (c_int, []),
     "posfeat_conv_packed_k": (c_int, [c_int, c_int, c_int]),
     "posfeat_set_conv_precision": (c_int, [c_int]),
-    "posfeat_set_conv_persistent": (c_int, [c_int]),
     "posfeat_conv2d_nhwc": (c_int, [ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_void_p,
                                     c_void_p, c_void_p, c_void_p]),
     "posfeat_conv2d_workspace": (c_size_t, [ctypes.POINTER(ConvDesc)]),

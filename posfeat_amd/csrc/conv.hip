@@ -69,7 +69,6 @@ struct ConvArgs {
   // batched 1x1 GEMMs (conv_glds_kernel only): blockIdx.y selects x/w/y + z*stride
   int nbatch;
   long long bx, bw, by;
-  int abl;  // ablation (POSFEAT_ABL, A/B timing only): 1 skip MFMA work, 2 skip DMA
   // pre-split weights (conv_bf6b_kernel): three bf16 planes of w's layout
   const unsigned short* wb;
   long long wplane, bwb;
@@ -381,9 +380,16 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_mfma_kernel(ConvArgs a) {
 // Zero padding (out-of-image taps, M / Cout tails) loads from a zeroed
 // 16-B device word.  Two LDS stages: chunk c+1 is in flight while chunk c is
 // multiplied; vmcnt(0) + barrier at the end of each chunk.
-__device__ __attribute__((aligned(16))) float pf_conv_zero16[4];
+// 64 floats (not just the one 16-B word the DMA lanes read): conv_bf6d_kernel's
+// masked A rows read 4 DISTINCT 16-B words of it, so the compiler cannot merge
+// them into one load plus register copies (which it did, behind a vmcnt(0))
+__device__ __attribute__((aligned(16))) float pf_conv_zero16[64];
 #define PF_GPTR(p) ((const __attribute__((address_space(1))) void*)(p))
 #define PF_LPTR(p) ((__attribute__((address_space(3))) void*)(p))
+
+// sched_barrier mask: every instruction class except vector memory (0x10 and
+// its read / write sub-classes 0x20 / 0x40) may be scheduled across
+#define PF_SCHED_NO_VMEM 0x78F
 
 // vmcnt(N) with expcnt / lgkmcnt left alone (gfx9 s_waitcnt encoding)
 template <int N>
@@ -664,11 +670,9 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_glds_kernel(ConvArgs a) {
       const int cur = (c - ch0) & 1;
       pf_dma_overlap_step(
           As + (cur ^ 1) * BM * BK, Bs + (cur ^ 1) * BN * BK, As + cur * BM * BK,
-          Bs + cur * BN * BK, c + 1 < ch1 && !(a.abl & 2),
+          Bs + cur * BN * BK, c + 1 < ch1,
           [&](float* Ad, float* Bd) { issue_chunk(Ad, Bd, 0); },
-          [&](const float* Ar, const float* Br) {
-            if (!(a.abl & 1)) compute(Ar, Br, 0);
-          });
+          [&](const float* Ar, const float* Br) { compute(Ar, Br, 0); });
       __builtin_amdgcn_s_waitcnt(0);
       __syncthreads();
     }
@@ -909,183 +913,6 @@ void conv_bf6b_kernel(ConvArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Persistent form of conv_bf6b_kernel for dense GEMMs (1x1 convs without
-// padding: every Winograd transform-domain GEMM, the tap GEMM, the 1x1
-// layers), ksplit 1, no fused statistics.  Same products in the same order
-// and the same epilogue arithmetic ((acc + bias) + residual, then the
-// activation): bit-identical results.  A grid of at most two blocks per CU
-// walks the tiles; each XCD owns a contiguous range of tile ids (the N-tiles
-// of one M-tile share its L2).  While a tile's last chunk is multiplied, the
-// DMA of the NEXT tile's first chunk is already in flight, and it stays in
-// flight through the epilogue, which stores straight from the accumulators
-// (lanes 0-31 / 32-63 of a store write 128 contiguous bytes of two rows): no
-// LDS staging, no per-tile prologue stall.  K = 192 (the tap GEMM: 6 chunks
-// per tile) paid a full DMA latency plus an LDS round trip per tile before.
-template <int BM, int BN>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
-void conv_bf6p_kernel(ConvArgs a) {
-  constexpr int WM = 4, NW = 4;
-  constexpr int TM = BM / WM;
-  constexpr int NI = BN / 32;
-  constexpr int A_G = BM / 8 / NW;
-  constexpr int B_G = 3 * BN / 16 / NW;
-  static_assert(TM == 32 && A_G >= 1 && B_G >= 1 && (3 * BN / 16) % NW == 0, "tile");
-  constexpr int ASTAGE = BM * BK;
-  constexpr int BSTAGE = 3 * BN * BK / 2;
-  __shared__ __attribute__((aligned(16))) float smem[2 * (ASTAGE + BSTAGE)];
-  float* const As = smem;
-  unsigned short* const Bs = reinterpret_cast<unsigned short*>(smem + 2 * ASTAGE);
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int total = a.nwg * a.nbatch;
-  // tile walk: blocks round-robin over the ng = min(G, 8) XCD groups; group x
-  // (blockIdx % ng) owns ids [x*q, min((x+1)*q, total)) and its nb blocks
-  // stride through that range -- every id exactly once, any G >= 1
-  const int G = gridDim.x, ng = min(G, 8), xcd = blockIdx.x % ng;
-  const int nb = (G - xcd + ng - 1) / ng, q = (total + ng - 1) / ng;
-  const int lo = xcd * q, hi = min(lo + q, total);
-  int t = lo + blockIdx.x / ng;
-  if (t >= hi) return;
-
-  const int lrow = lane >> 3;
-  const int nch = a.Kpad / BK;
-  const float* xs[A_G];
-  const unsigned short* bs[B_G];
-  // per-tile DMA sources (chunk 0) and epilogue geometry
-  int m0 = 0, n0 = 0;
-  float* ybase = a.y;
-  auto setup = [&](int tt) {
-    const int zb = tt / a.nwg, bid = tt - zb * a.nwg;
-    const int tm = bid / a.tiles_n, tn = bid - tm * a.tiles_n;
-    m0 = tm * BM;
-    n0 = tn * BN;
-    const float* xb = a.x + (long long)zb * a.bx;
-    const unsigned short* wbb = a.wb + (long long)zb * a.bwb;
-    ybase = a.y + (long long)zb * a.by;
-#pragma unroll
-    for (int i = 0; i < A_G; ++i) {
-      const int row = (wave * A_G + i) * 8 + lrow;
-      const int sslot = (lane & 7) ^ ((row >> 1) & 7);
-      const int m = min(m0 + row, a.M - 1);  // rows past M re-read the last one (never stored)
-      const int n = m / a.hw, rem = m - n * a.hw;
-      const int oh = rem / a.OW, ow = rem - oh * a.OW;
-      xs[i] = xb + (((long long)n * a.H + oh * a.stride) * a.W + ow * a.stride) * a.xcs + sslot * 4;
-    }
-#pragma unroll
-    for (int i = 0; i < B_G; ++i) {
-      const int pr = (wave * B_G + i) * 16 + (lane >> 2);
-      const int plane = pr / BN, row = pr - plane * BN;
-      const int ks = (lane & 3) ^ ((row >> 2) & 3);
-      bs[i] = wbb + plane * a.wplane + (long long)min(n0 + row, a.Cout - 1) * a.Kpad + ks * 8;
-    }
-  };
-  auto issue_to = [&](int c, float* dA, unsigned short* dB) {
-    const long long off = (long long)c * BK;
-#pragma unroll
-    for (int i = 0; i < A_G; ++i)
-      __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void*)(xs[i] + off),
-          (__attribute__((address_space(3))) void*)(dA + (wave * A_G + i) * 8 * BK), 16, 0, 0);
-#pragma unroll
-    for (int i = 0; i < B_G; ++i)
-      __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void*)(bs[i] + off),
-          (__attribute__((address_space(3))) void*)(dB + (wave * B_G + i) * 16 * BK), 16, 0, 0);
-  };
-
-  f32x16 acc[NI];
-  const int sw = ((lane & 31) >> 1) & 7, hh = lane >> 5, r32 = lane & 31;
-  const int arow = wave * TM + r32;
-  auto compute_from = [&](const float* sA, const unsigned short* sB) {
-    const float* Ab = sA + arow * BK;
-#pragma unroll
-    for (int g = 0; g < BK / 16; ++g) {
-      const int s0 = ((4 * g + 2 * hh) ^ sw) * 4, s1 = ((4 * g + 2 * hh + 1) ^ sw) * 4;
-      u32x4_t ah, am, al;
-      split3(*reinterpret_cast<const f32x4*>(Ab + s0), *reinterpret_cast<const f32x4*>(Ab + s1),
-             ah, am, al);
-#pragma unroll
-      for (int ni = 0; ni < NI; ++ni) {
-        const int row = ni * 32 + r32;
-        const int slot = (2 * g + hh) ^ ((row >> 2) & 3);
-        const unsigned short* bp = sB + row * BK + slot * 8;
-        const u32x4_t bh = *reinterpret_cast<const u32x4_t*>(bp);
-        const u32x4_t bm = *reinterpret_cast<const u32x4_t*>(bp + BN * BK);
-        const u32x4_t bl = *reinterpret_cast<const u32x4_t*>(bp + 2 * BN * BK);
-        f32x16 cc = acc[ni];
-        cc = mfma_bf16(ah, bh, cc);
-        cc = mfma_bf16(ah, bm, cc);
-        cc = mfma_bf16(am, bh, cc);
-        cc = mfma_bf16(ah, bl, cc);
-        cc = mfma_bf16(al, bh, cc);
-        cc = mfma_bf16(am, bm, cc);
-        acc[ni] = cc;
-      }
-    }
-  };
-  auto stageA = [&](int s) { return As + s * ASTAGE; };
-  auto stageB = [&](int s) { return Bs + s * 2 * BSTAGE; };
-
-  setup(t);
-  issue_to(0, stageA(0), stageB(0));
-  int st0 = 0;  // stage holding the current tile's chunk 0
-  __builtin_amdgcn_s_waitcnt(0);
-  __syncthreads();
-  while (true) {
-#pragma unroll
-    for (int ni = 0; ni < NI; ++ni)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[ni][r] = 0.f;
-    const int cm0 = m0, cn0 = n0;
-    float* const cy = ybase;
-    const int tn_ = t + nb;
-    const bool more_tiles = tn_ < hi;
-    for (int c = 0; c < nch; ++c) {
-      const int s = st0 ^ (c & 1);
-      const bool last = c + 1 == nch;
-      // at the last chunk: the next tile's first chunk flies under this
-      // chunk's MFMAs and the epilogue
-      if (last && more_tiles) setup(tn_);
-      pf_dma_overlap_step(stageA(s ^ 1), stageB(s ^ 1), stageA(s), stageB(s), !last || more_tiles,
-                          [&](float* dA, unsigned short* dB) { issue_to(last ? 0 : c + 1, dA, dB); },
-                          [&](const float* sA, const unsigned short* sB) { compute_from(sA, sB); });
-      if (last) {
-        st0 = s ^ 1;
-      } else {
-        __builtin_amdgcn_s_waitcnt(0);
-        __syncthreads();
-      }
-    }
-    // ---- epilogue straight from the accumulators ---------------------------
-    // acc[ni][r]: row wave*32 + (r&3) + 8*(r>>2) + 4*hh, column ni*32 + r32
-#pragma unroll
-    for (int ni = 0; ni < NI; ++ni) {
-      const int col = cn0 + ni * 32 + r32;
-      if (col >= a.Cout) continue;
-      const float bv = a.bias ? a.bias[col] : 0.f;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = cm0 + wave * TM + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        if (m >= a.M) continue;
-        // (acc + bias) + residual-or-0, as conv_epilogue (same bits, incl. -0 + 0)
-        float v = acc[ni][r] + bv;
-        v += a.res ? a.res[(size_t)m * a.rcs + col] : 0.f;
-        if (a.act == POSFEAT_ACT_RELU)
-          v = fmaxf(v, 0.f);
-        else if (a.act == POSFEAT_ACT_ELU)
-          v = pf_elu(v);
-        cy[(size_t)m * a.ycs + col] = v;
-      }
-    }
-    // the next tile's chunk 0 has landed; every wave is done with this tile's stages
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
-    if (!more_tiles) break;
-    t = tn_;
-  }
-}
-
-// ---------------------------------------------------------------------------
 // Pre-split-weight GEMM / conv tiles with a DEEP A prefetch (conv_bf6d_kernel,
 // POSFEAT_BF6D = D; any KH x KW / stride / pad with Cin % 32 == 0).  The LDS ring of conv_bf6b_kernel bounds the bytes
 // in flight per CU (two 40-KB stages per block, half of them being read): with
@@ -1169,14 +996,22 @@ void conv_bf6d_kernel(ConvArgs a) {
   // chunk c = (slab, tap): always four loads per lane (a masked tap reads the
   // zeroed 16-B word), so the per-chunk vmcnt accounting below holds
   const float* const zero = a.zero;
+  // A masked lane (tap outside the image, row past M) selects the zero block
+  // as its base and reads the same four offsets from it: one per-lane pointer
+  // select, four distinct addresses, no branch.  (Selecting the one zero word
+  // per load let the compiler branch on the mask and merge the masked lanes'
+  // identical loads into one load + register copies behind an
+  // s_waitcnt vmcnt(0) -- a full drain of the prefetch whenever a wave held a
+  // masked lane, and a wave with every lane masked issued 3 loads, not 4.)
   auto load_a = [&](int c, f32x4 (&v)[4]) {
     const int slab = c / ntap, tap = c - slab * ntap;
     const int kh = tap / a.KW, kw = tap - kh * a.KW;
     const bool ok = (tapok >> tap) & 1u;
     const float* p = xrow + ((long long)kh * a.W + kw) * a.xcs + (long long)slab * BK;
+    const float* base = ok ? p : zero;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-      v[j] = *reinterpret_cast<const f32x4*>(ok ? p + (j >> 1) * 16 + (j & 1) * 4 : zero);
+      v[j] = *reinterpret_cast<const f32x4*>(base + (j >> 1) * 16 + (j & 1) * 4);
   };
 
   f32x16 acc[NI];
@@ -1185,8 +1020,15 @@ void conv_bf6d_kernel(ConvArgs a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[ni][r] = 0.f;
 
+  // The counted waits below (vmcnt(4) / vmcnt(4 D)) assume every B DMA is
+  // issued BEFORE the A loads that follow it in program order: vmcnt retires
+  // in issue order, so B(c) is covered only if exactly the A loads issued
+  // after it are younger.  The A loads read memory the DMA does not write, so
+  // the scheduler could legally hoist them above the DMA; the
+  // sched_barrier(0)s pin the order (and keep the waits where they are).
   f32x4 va[D][4];
   if (nch > 0) issue_b(Bs, ch0);
+  __builtin_amdgcn_sched_barrier(PF_SCHED_NO_VMEM);
 #pragma unroll
   for (int j = 0; j < D; ++j)
     if (j < nch) load_a(ch0 + j, va[j]);
@@ -1197,6 +1039,7 @@ void conv_bf6d_kernel(ConvArgs a) {
       const int ii = i + u;
       if (ii >= nch) break;
       // B(ii) landed: it was issued before the 4 A loads of chunk ii-1+D (if any)
+      __builtin_amdgcn_sched_barrier(PF_SCHED_NO_VMEM);
       if (ii - 1 + D < nch && ii > 0)
         wait_vmcnt<4>();
       else if (ii == 0 && D < nch)
@@ -1214,6 +1057,7 @@ void conv_bf6d_kernel(ConvArgs a) {
           Bs + s * 2 * BSTAGE + BSTAGE, ii + 1 < nch,
           [&](unsigned short* Bd, unsigned short*) {
             issue_b(Bd, ch0 + ii + 1);
+            __builtin_amdgcn_sched_barrier(PF_SCHED_NO_VMEM);  // B(ii+1) strictly before A(ii+D)
             if (ii + D < nch) load_a(ch0 + ii + D, va[u]);
           },
           [&](const unsigned short* Bb, const unsigned short*) {
@@ -1250,193 +1094,6 @@ void conv_bf6d_kernel(ConvArgs a) {
       [&](int, int m) { return a.res ? a.res + (size_t)m * a.rcs : (const float*)nullptr; });
 }
 
-// ---------------------------------------------------------------------------
-// The same products with A straight to REGISTERS.  With the waves stacked
-// along M each wave is the only reader of its 32 A rows, so A needs no LDS
-// round trip: lane (r, h) global-loads the 8 fp32 it feeds the MFMA (row r,
-// k = 16g + 8h .. +7: two 16-B loads per k16 group) one chunk ahead, into a
-// second register set, while the chunk in hand is split and multiplied.  LDS
-// then holds only the B planes (NST stages of 24 KB at BN = 128): per chunk
-// the DMA moves 24 KB instead of 40 and nothing stages A (measured on the
-// LDS-staged form: its DMA and compute did not overlap -- POSFEAT_ABL
-// ablations, r3c).  Products, their order and the epilogue are those of
-// conv_bf6b_kernel: bit-identical results.
-template <int BM, int BN, int NST>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
-void conv_bf6r_kernel(ConvArgs a) {
-  constexpr int WM = 4, WN = 1, NW = 4;
-  constexpr int TM = BM / WM, TN = BN;
-  constexpr int MI = TM / 32, NI = TN / 32;
-  constexpr int B_G = 3 * BN / 16 / NW;  // 16 plane-rows (64 B) per DMA piece
-  static_assert(MI == 1 && B_G >= 1 && (3 * BN / 16) % NW == 0, "tile");
-  static_assert(NST == 2 || NST == 3, "stages");
-  constexpr int BSTAGE = 3 * BN * BK / 2;  // floats (u16 pairs)
-  constexpr int RING = NST * BSTAGE;
-  constexpr int EPI = BM * (BN + 4);
-  __shared__ __attribute__((aligned(16))) float smem[RING > EPI ? RING : EPI];
-  unsigned short* Bs = reinterpret_cast<unsigned short*>(smem);
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  int bid = blockIdx.x % a.nwg;
-  const int split = blockIdx.x / a.nwg;
-  {
-    const int nwg = a.nwg, q = nwg >> 3, r = nwg & 7, xcd = bid & 7, slot = bid >> 3;
-    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
-  }
-  const unsigned short* wb = a.wb;
-  if (a.nbatch > 1) {
-    const long long zb = blockIdx.y;
-    a.x += zb * a.bx;
-    a.y += zb * a.by;
-    wb += zb * a.bwb;
-  }
-  const int tm = bid / a.tiles_n, tn = bid - tm * a.tiles_n;
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int r32 = lane & 31, hh = lane >> 5;
-
-  // this lane's A row: base of tap (0,0) + its k offset 8h; taps in the image
-  const float* xrow = a.x;
-  unsigned tapok = 0u;
-  {
-    const int m = m0 + wave * 32 + r32;
-    if (m < a.M) {
-      const int n = m / a.hw;
-      const int rem = m - n * a.hw;
-      const int oh = rem / a.OW;
-      const int ow = rem - oh * a.OW;
-      const int ih0 = oh * a.stride - a.pad, iw0 = ow * a.stride - a.pad;
-      for (int kh = 0; kh < a.KH; ++kh)
-        for (int kw = 0; kw < a.KW; ++kw)
-          if ((unsigned)(ih0 + kh) < (unsigned)a.H && (unsigned)(iw0 + kw) < (unsigned)a.W)
-            tapok |= 1u << (kh * a.KW + kw);
-      xrow = a.x + (long long)n * a.H * a.W * a.xcs + ((long long)ih0 * a.W + iw0) * a.xcs + hh * 8;
-    }
-  }
-  const unsigned short* bsrc[B_G];
-#pragma unroll
-  for (int i = 0; i < B_G; ++i) {
-    const int pr = (wave * B_G + i) * 16 + (lane >> 2);
-    const int plane = pr / BN, row = pr - plane * BN;
-    const int ks = (lane & 3) ^ ((row >> 2) & 3);
-    bsrc[i] = (n0 + row < a.Cout)
-                  ? wb + plane * a.wplane + (long long)(n0 + row) * a.Kpad + ks * 8
-                  : nullptr;
-  }
-  const int ntap = a.KH * a.KW;
-  const int nch_all = a.Kpad / BK;
-  const int ch0 = (int)((long long)nch_all * split / a.ksplit);
-  const int ch1 = (int)((long long)nch_all * (split + 1) / a.ksplit);
-
-  auto issue_b = [&](unsigned short* Bd, int c, int buf) {
-#pragma unroll
-    for (int i = 0; i < B_G; ++i) {
-      const void* src = bsrc[i] ? (const void*)(bsrc[i] + (long long)c * BK)
-                                : (const void*)pf_conv_zero16;
-      __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void*)src,
-          (__attribute__((address_space(3))) void*)(Bd + buf * 2 * BSTAGE +
-                                                     (wave * B_G + i) * 16 * BK),
-          16, 0, 0);
-    }
-  };
-  // the lane's 8 A values of each k16 group of chunk c (zero for taps outside)
-  auto load_a = [&](int c, f32x4 (&v)[4]) {
-    const int slab = c / ntap, tap = c - slab * ntap;
-    const int kh = tap / a.KW, kw = tap - kh * a.KW;
-    const float* p = xrow + ((long long)kh * a.W + kw) * a.xcs + slab * BK;
-    if ((tapok >> tap) & 1u) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        v[j] = *reinterpret_cast<const f32x4*>(p + (j >> 1) * 16 + (j & 1) * 4);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-  };
-
-  f32x16 acc[MI][NI];
-#pragma unroll
-  for (int ni = 0; ni < NI; ++ni)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[0][ni][r] = 0.f;
-
-  auto compute = [&](const unsigned short* Br, int buf, const f32x4 (&v)[4]) {
-    const unsigned short* Bb = Br + buf * 2 * BSTAGE;
-#pragma unroll
-    for (int g = 0; g < BK / 16; ++g) {
-      u32x4_t ah, am, al;
-      split3(v[2 * g], v[2 * g + 1], ah, am, al);
-#pragma unroll
-      for (int ni = 0; ni < NI; ++ni) {
-        const int row = ni * 32 + r32;
-        const int slot = (2 * g + hh) ^ ((row >> 2) & 3);
-        const unsigned short* bp = Bb + row * BK + slot * 8;
-        const u32x4_t bh = *reinterpret_cast<const u32x4_t*>(bp);
-        const u32x4_t bm = *reinterpret_cast<const u32x4_t*>(bp + BN * BK);
-        const u32x4_t bl = *reinterpret_cast<const u32x4_t*>(bp + 2 * BN * BK);
-        f32x16 c = acc[0][ni];
-        c = mfma_bf16(ah, bh, c);
-        c = mfma_bf16(ah, bm, c);
-        c = mfma_bf16(am, bh, c);
-        c = mfma_bf16(ah, bl, c);
-        c = mfma_bf16(al, bh, c);
-        c = mfma_bf16(am, bm, c);
-        acc[0][ni] = c;
-      }
-    }
-  };
-
-  // Issue order (vector-memory completions count in order): B(0), A(0),
-  // [B(1)]; per chunk ii: A(ii+1), then B(ii+NST-1).  So at the top of chunk
-  // ii everything but the youngest B (NST = 3) must have landed: A(ii) and
-  // B(ii) are older than it.
-  const int nch = ch1 - ch0;
-  f32x4 va[4], vb[4];
-  if (nch > 0) {
-    issue_b(Bs, ch0, 0);
-    load_a(ch0, va);
-    if (NST == 3 && nch > 1) issue_b(Bs, ch0 + 1, 1);
-  }
-  int slot = 0;
-  for (int i = 0; i < nch; i += 2) {
-    // two chunks per trip so the A register sets alternate without copies
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int ii = i + u;
-      if (ii >= nch) break;
-      if (NST == 3 && ii + 1 < nch)
-        wait_vmcnt<B_G>();
-      else
-        wait_vmcnt<0>();
-      // every wave: chunk ii landed, and chunk ii-1's slot (refilled below) consumed
-      __builtin_amdgcn_s_barrier();
-      if (u == 0) {
-        if (ii + 1 < nch) load_a(ch0 + ii + 1, vb);
-      } else {
-        if (ii + 1 < nch) load_a(ch0 + ii + 1, va);
-      }
-      const int refill = slot == 0 ? NST - 1 : slot - 1;
-      unsigned short* const Bref = Bs + refill * 2 * BSTAGE;
-      const unsigned short* const Bcur = Bs + slot * 2 * BSTAGE;
-      pf_dma_overlap_step(
-          Bref, Bref + BSTAGE, Bcur, Bcur + BSTAGE, ii + NST - 1 < nch,
-          [&](unsigned short* Bd, unsigned short*) { issue_b(Bd, ch0 + ii + NST - 1, 0); },
-          [&](const unsigned short* Br, const unsigned short*) {
-            if (u == 0)
-              compute(Br, 0, va);
-            else
-              compute(Br, 0, vb);
-          });
-      slot = slot == NST - 1 ? 0 : slot + 1;
-    }
-  }
-  __builtin_amdgcn_s_waitcnt(0);
-  __syncthreads();
-  conv_epilogue<BM, BN, WM, WN>(
-      a, acc, smem, tm, n0, split, [&](int row) { return m0 + row < a.M ? m0 + row : -1; },
-      m0 / a.hw,
-      [&](int, int m) { return a.res ? a.res + (size_t)m * a.rcs : (const float*)nullptr; });
-}
 
 // ---------------------------------------------------------------------------
 // Spatial-halo variant for stride-1 convs with Cin % 32 == 0 (every 3x3
@@ -2123,40 +1780,13 @@ int bf6_nst() {
   }();
   return n;
 }
-// pre-split-weight tiles with A straight to registers (POSFEAT_BF6R=1; A/B
-// only: measured r3j on the decoder's Winograd GEMMs 0.597 ms (2 B stages) /
-// 0.589 ms (3) against 0.564 ms for the LDS-staged conv_bf6b_kernel -- the
-// per-lane 32-B row pieces load worse than the 128-B DMA rows);
-// POSFEAT_BF6R_NST: B stages (2 or 3)
-// The persistent pre-split-weight tiles (conv_bf6p_kernel) for dense GEMMs
-// without split-K or fused statistics: POSFEAT_BF6P=1 or
-// posfeat_set_conv_persistent(1) (A/B, off: same-box r5q, 932 vs 946 img/s
-// for one workgroup per tile -- neither the per-tile DMA latency nor the LDS
-// epilogue was what bounds these GEMMs); POSFEAT_BF6P_BLOCKS the resident
-// grid (default 512: two 80-KB blocks on each of the 256 CUs).
-int g_conv_persist = -1;
-int conv_persist_mode() {
-  if (g_conv_persist < 0) {
-    const char* e = getenv("POSFEAT_BF6P");
-    g_conv_persist = (e && e[0] == '1') ? 1 : 0;
-  }
-  return g_conv_persist;
-}
-bool bf6p_persist_ok(const ConvArgs& a) {
-  return conv_persist_mode() == 1 && a.KH == 1 && a.KW == 1 && a.pad == 0 && a.ksplit == 1 && !a.stats && a.wb;
-}
-int bf6p_blocks() {
-  static const int n = [] {
-    const char* e = getenv("POSFEAT_BF6P_BLOCKS");
-    const int v = e ? atoi(e) : 512;
-    return v >= 8 ? v / 8 * 8 : 512;  // a multiple of 8: whole XCD groups
-  }();
-  return n;
-}
-
 // Dense pre-split tiles (TILE_BF6B_*) and the register-A candidates
-// (TILE_BF6R_*) run conv_bf6d_kernel with A prefetched POSFEAT_BF6D = 2..4
-// chunks ahead in registers (default 2; 0: conv_bf6b / conv_bf6r).  Same box,
+// (TILE_BF6R_*: any conv, masked taps included) run conv_bf6d_kernel with A
+// prefetched POSFEAT_BF6D = 2..4 chunks ahead in registers (default 2; 0: the
+// LDS-staged conv_bf6b_kernel).  The 8-wave TILE_BF6B_256x128 caps D at 3 (its
+// register budget at two waves per SIMD): D = 4 runs D = 3 there.  (Round 2's
+// register-A twin with a one-chunk prefetch, conv_bf6r_kernel, and the
+// persistent conv_bf6p_kernel lost their A/Bs and are no longer built.)  Same box,
 // r6k: 945.6 -> 970 img/s (D = 3), decoder Winograd GEMMs -4..-7 %, tap GEMM
 // -9 %; r6q, two pairs each: D = 2 973.1, 3 968.4, 4 966.3 img/s;
 // bit-identical (test_gpu_bf6r.py)
@@ -2169,20 +1799,6 @@ int bf6d_depth() {
   return d;
 }
 
-bool bf6r_on() {
-  static const bool on = [] {
-    const char* e = getenv("POSFEAT_BF6R");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-int bf6r_nst() {
-  static const int n = [] {
-    const char* e = getenv("POSFEAT_BF6R_NST");
-    return e && e[0] == '3' ? 3 : 2;
-  }();
-  return n;
-}
 struct Plan {
   int kern, tile, bm, bn, ppi;  // ppi: patches per image (halo), 0 = contiguous rows
   long long tiles_m;
@@ -2349,9 +1965,7 @@ Plan conv_plan(const ConvArgs& a, bool allow_split, int forced = -1) {
     d = plan_for_tile(a, tile);
     d.ksplit = tile == TILE_128x128 ? ks : 1;
     if (bf6_on() && cin32 && a.KH * a.KW <= 32 && env.kmax >= KERN_GLDS) {
-      const bool r = bf6r_on();
-      Plan b = plan_for_tile(a, a.wb ? (a.Cout > 64 ? (r ? TILE_BF6R_128x128 : TILE_BF6B_128x128)
-                                                    : (r ? TILE_BF6R_128x64 : TILE_BF6B_128x64))
+      Plan b = plan_for_tile(a, a.wb ? (a.Cout > 64 ? TILE_BF6B_128x128 : TILE_BF6B_128x64)
                                      : (a.Cout > 64 ? TILE_BF6_128x128 : TILE_BF6_128x64));
       if (b.kern >= 0) {
         b.ksplit = ks;
@@ -2439,13 +2053,7 @@ int conv_run(ConvArgs& a, const Plan& p, hipStream_t st) {
     case TILE_BF6B_128x128:
     case TILE_BF6B_128x64: {
       const bool wide = p.tile == TILE_BF6B_128x128;
-      if (bf6p_persist_ok(a)) {
-        const int grid = (int)std::min<long long>((long long)a.nwg * a.nbatch, bf6p_blocks());
-        if (wide)
-          hipLaunchKernelGGL((conv_bf6p_kernel<128, 128>), dim3(grid), dim3(256), 0, st, a);
-        else
-          hipLaunchKernelGGL((conv_bf6p_kernel<128, 64>), dim3(grid), dim3(256), 0, st, a);
-      } else if (bf6d_depth() && a.KH == 1 && a.KW == 1 && a.pad == 0) {
+      if (bf6d_depth() && a.KH == 1 && a.KW == 1 && a.pad == 0) {
         const dim3 g(a.nwg * a.ksplit, a.nbatch);
         const int dd = bf6d_depth();
         if (wide && dd == 2)
@@ -2489,12 +2097,10 @@ int conv_run(ConvArgs& a, const Plan& p, hipStream_t st) {
           hipLaunchKernelGGL((conv_bf6d_kernel<128, 128, 3>), g, dim3(256), 0, st, a);
         else
           hipLaunchKernelGGL((conv_bf6d_kernel<128, 128, 4>), g, dim3(256), 0, st, a);
-      } else if (bf6r_nst() == 3)
-        hipLaunchKernelGGL((conv_bf6r_kernel<128, 128, 3>), dim3(a.nwg * a.ksplit, a.nbatch),
+      } else {  // POSFEAT_BF6D=0: the LDS-staged form
+        hipLaunchKernelGGL((conv_bf6b_kernel<128, 128>), dim3(a.nwg * a.ksplit, a.nbatch),
                            dim3(256), 0, st, a);
-      else
-        hipLaunchKernelGGL((conv_bf6r_kernel<128, 128, 2>), dim3(a.nwg * a.ksplit, a.nbatch),
-                           dim3(256), 0, st, a);
+      }
       break;
     case TILE_BF6R_128x64:
       if (bf6d_depth()) {
@@ -2505,12 +2111,10 @@ int conv_run(ConvArgs& a, const Plan& p, hipStream_t st) {
           hipLaunchKernelGGL((conv_bf6d_kernel<128, 64, 3>), g, dim3(256), 0, st, a);
         else
           hipLaunchKernelGGL((conv_bf6d_kernel<128, 64, 4>), g, dim3(256), 0, st, a);
-      } else if (bf6r_nst() == 3)
-        hipLaunchKernelGGL((conv_bf6r_kernel<128, 64, 3>), dim3(a.nwg * a.ksplit, a.nbatch),
+      } else {
+        hipLaunchKernelGGL((conv_bf6b_kernel<128, 64>), dim3(a.nwg * a.ksplit, a.nbatch),
                            dim3(256), 0, st, a);
-      else
-        hipLaunchKernelGGL((conv_bf6r_kernel<128, 64, 2>), dim3(a.nwg * a.ksplit, a.nbatch),
-                           dim3(256), 0, st, a);
+      }
       break;
     case TILE_256x128: launch_rows<256, 128, 4, 2>(a, p.kern, st); break;
     case TILE_128x128: launch_rows<128, 128, 2, 2>(a, p.kern, st); break;
@@ -2610,10 +2214,6 @@ static int conv_prepare(const posfeat_conv_desc* d, const float* x, const float*
   a.wb = nullptr;
   a.wplane = a.bwb = 0;
   a.zero = conv_zero_ptr();  // checked at launch (planning calls need no device)
-  {
-    static const int abl = getenv("POSFEAT_ABL") ? atoi(getenv("POSFEAT_ABL")) : 0;
-    a.abl = abl;
-  }
   return POSFEAT_OK;
 }
 
@@ -2941,10 +2541,3 @@ int pf_gemm_batched(const float* A, int lda, long long sa, const float* B, long 
   return conv_run(a, p, st);
 }
 
-extern "C" int posfeat_set_conv_persistent(int mode) {
-  const int prev = conv_persist_mode();
-  if (mode == -1) return prev;
-  if (mode < 0 || mode > 1) return -1;
-  g_conv_persist = mode;
-  return prev;
-}

@@ -32,22 +32,41 @@ def to_input(im):
     return torch.from_numpy(np.ascontiguousarray(x.transpose(2, 0, 1))), np.ascontiguousarray(im)
 
 
+def crop16(im):
+    """uint8 HxWx3 -> the cropped (multiples of 16) contiguous uint8 image that
+    to_input normalises; the pipelined Extractor uploads this and normalises on
+    the device (ops.normalize_rgb8, bit-identical to to_input)."""
+    if im.ndim == 2:
+        im = np.stack([im] * 3, -1)
+    im = im[..., :3]
+    h, w = im.shape[:2]
+    return np.ascontiguousarray(im[:h - h % 16, :w - w % 16])
+
+
 def _read(path):
     from PIL import Image
     return np.asarray(Image.open(path).convert("RGB"))
 
 
 class _FileDataset(Dataset):
+    """``uint8_only`` (set by the pipelined Extractor): items carry only the
+    cropped uint8 image, its name and index -- the float normalisation runs on
+    the device, so the loader workers skip it."""
+
     def __init__(self, configs):
         super().__init__()
         self.configs = configs
         self.imfs = []
+        self.uint8_only = False
 
     def name_of(self, path):
         raise NotImplementedError
 
     def __getitem__(self, item):
         imf = self.imfs[item]
+        if self.uint8_only:
+            return {"im1_ori": torch.from_numpy(crop16(_read(imf))), "name1": self.name_of(imf),
+                    "index": item}
         x, im = to_input(_read(imf))
         return {"im1": x, "im1_ori": im, "coord1": torch.zeros(0, 2), "name1": self.name_of(imf),
                 "pad1": (0, 0, 0, 0)}
@@ -110,10 +129,15 @@ class SyntheticImages(Dataset):
         self.n = int(configs.get("num_images", 8))
         self.h = int(configs.get("height", 480))
         self.w = int(configs.get("width", 640))
+        self.uint8_only = False
 
     def __getitem__(self, item):
         rs = np.random.RandomState(1000 + item)
-        x, im = to_input(rs.randint(0, 256, (self.h, self.w, 3)).astype(np.uint8))
+        raw = rs.randint(0, 256, (self.h, self.w, 3)).astype(np.uint8)
+        if self.uint8_only:
+            return {"im1_ori": torch.from_numpy(crop16(raw)), "name1": "synthetic/%05d.ppm" % item,
+                    "index": item}
+        x, im = to_input(raw)
         return {"im1": x, "im1_ori": im, "coord1": torch.zeros(0, 2),
                 "name1": "synthetic/%05d.ppm" % item, "pad1": (0, 0, 0, 0)}
 

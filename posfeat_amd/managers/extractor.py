@@ -230,6 +230,7 @@ class Extractor:
         # per-image async copies from the loader's pinned buffers (a host-side
         # stack would be pageable, and a pageable H2D copy waits for the stream)
         if all(it[1] is not None for it in items):
+            # items[i][1]: the cropped uint8 image [h, w, 3] from pinned memory
             u8 = torch.empty((len(items),) + tuple(items[0][1].shape), dtype=torch.uint8,
                              device=dev)
             for i, it in enumerate(items):
@@ -284,57 +285,82 @@ class Extractor:
     def _save_and_log(self, inputs, processed):
         self.logger.info(inputs["name1"][0] + self.save_desc(inputs, None, processed))
 
+    def _pipelined_loader(self):
+        """The pipelined loop's own loader over the same dataset and shard:
+        items carry only the cropped uint8 image (the float normalisation runs
+        on the device), ``POSFEAT_EXTRACT_LOAD_BATCH`` items per worker
+        transaction (default 8) collated as a list (sizes may differ), and
+        ``POSFEAT_EXTRACT_WORKERS`` decode workers (default: the config's
+        ``workers``, at least 4).  Order is the sampler's, as the reference
+        loop's."""
+        ds = self.extract_loader.dataset
+        if hasattr(ds, "uint8_only"):
+            ds.uint8_only = True
+        cfg = self.config["data_config_extract"]
+        workers = int(os.environ.get("POSFEAT_EXTRACT_WORKERS",
+                                     max(4, int(cfg.get("workers", 0) or 0))))
+        lb = max(1, int(os.environ.get("POSFEAT_EXTRACT_LOAD_BATCH", "8")))
+        sampler = (datasets.ShardSampler(len(ds), self.rank, self.world)
+                   if self.multi_gpu else None)
+        kw = dict(prefetch_factor=4, persistent_workers=False) if workers > 0 else {}
+        return torch.utils.data.DataLoader(
+            ds, batch_size=lb, shuffle=False, num_workers=workers, sampler=sampler,
+            collate_fn=lambda b: [x for x in b if x is not None], pin_memory=True, **kw)
+
     def _extract_pipelined(self):
-        group = max(1, int(os.environ.get("POSFEAT_EXTRACT_GROUP", "8")))
+        """Images are grouped BY SHAPE across the whole stream (one bucket per
+        size, a bucket runs as one engine batch when it holds
+        ``POSFEAT_EXTRACT_GROUP`` images, default 32 -- the bench batch -- and
+        the remaining buckets at the end): output files are per image, so the
+        processing order is free; name_list.txt keeps the loader order."""
+        group = max(1, int(os.environ.get("POSFEAT_EXTRACT_GROUP", "32")))
         writer = ThreadPoolExecutor(1 if self.save_h5 else 4)
-        futures, pending, buf = [], deque(), []
+        futures, pending = [], deque()
+        buckets = {}
         self.group_shapes = []
-        name_list = ""
+        names = []   # (dataset index, name) in loader order
         n = 0
         t0 = time.perf_counter()
 
         trace = os.environ.get("POSFEAT_EXTRACT_TRACE", "0") == "1"
 
         marks = []   # (launch time, images launched so far): steady-state rate
+        launched = [0]
 
-        def flush():
-            if buf:
-                ta = time.perf_counter()
-                marks.append((ta - t0, n - len(buf)))
-                pending.append(self._launch_group(list(buf)))
-                if trace:
-                    print("[extract] group %d x %s launched in %.1f ms at %.3f s" % (
-                        len(buf), tuple(buf[0][0].shape[1:]), 1e3 * (time.perf_counter() - ta),
-                        ta - t0), flush=True)
-                buf.clear()
+        def launch(items):
+            ta = time.perf_counter()
+            marks.append((ta - t0, launched[0]))
+            self.group_shapes.append(tuple(items[0][0].shape))
+            pending.append(self._launch_group(items))
+            launched[0] += len(items)
+            if trace:
+                print("[extract] group %d x %s launched in %.1f ms at %.3f s" % (
+                    len(items), tuple(items[0][0].shape), 1e3 * (time.perf_counter() - ta),
+                    ta - t0), flush=True)
             while len(pending) > 1:   # keep one group in flight behind the host
                 self._finish_group(*pending.popleft(), writer, futures)
 
-        for inputs in self.extract_loader:
-            names = inputs["name1"]
-            im1 = inputs["im1"]
-            ori = inputs.get("im1_ori")
-            scale = inputs.get("scale")
-            for i in range(im1.shape[0]):
-                item = (im1[i], ori[i] if ori is not None and ori.dim() == 4 else None, names[i],
-                        scale[i].numpy() if scale is not None else None)
-                if buf and (buf[0][0].shape != item[0].shape or len(buf) >= group):
-                    self.group_shapes.append(tuple(buf[0][0].shape))
-                    flush()
-                buf.append(item)
-                name_list += "{} {}\n".format(n, names[i])
+        for batch in self._pipelined_loader():
+            for it in batch:
+                u8 = it["im1_ori"]
+                item = (u8, u8, it["name1"], None)
+                key = tuple(u8.shape)
+                b = buckets.setdefault(key, [])
+                b.append(item)
+                names.append((int(it["index"]), it["name1"]))
                 n += 1
-        if buf:
-            self.group_shapes.append(tuple(buf[0][0].shape))
-        flush()
+                if len(b) >= group:
+                    launch(b)
+                    buckets[key] = []
+        for key in list(buckets):
+            if buckets[key]:
+                launch(buckets.pop(key))
         while pending:
             self._finish_group(*pending.popleft(), writer, futures)
         for f in futures:
             f.result()
         writer.shutdown()
-        if self.output_flag:
-            with open(os.path.join(self.img_root, "name_list.txt"), "w") as f:
-                f.write(name_list)
+        self._write_name_list(names)
         dt = time.perf_counter() - t0
         self.stats = {"images": n, "seconds": dt, "images_per_s": n / dt if dt > 0 else 0.0,
                       "stage_ms_per_image": None, "pipeline": True, "group": group,
@@ -342,6 +368,18 @@ class Extractor:
         self.logger.info("extracted %d images in %.2fs (%.1f images/s, pipelined)" % (
             n, dt, self.stats["images_per_s"]))
         return n
+
+    def _write_name_list(self, names):
+        """name_list.txt = "<dataset index> <name>" per image in dataset order.
+        Under N > 1 every rank's (index, name) pairs are gathered to rank 0 (the
+        reference wrote rank 0's shard only)."""
+        if self.multi_gpu:
+            allp = [None] * self.world
+            dist.all_gather_object(allp, names)
+            names = sorted(p for part in allp for p in part)
+        if self.output_flag:
+            with open(os.path.join(self.img_root, "name_list.txt"), "w") as f:
+                f.write("".join("{} {}\n".format(i, nm) for i, nm in names))
 
     # ------------------------------------------------------------ serial
     def _extract_serial(self):
@@ -355,7 +393,10 @@ class Extractor:
             stages[stage] += now - t
             return now
 
-        name_list = ""
+        names = []
+        # dataset index of each loader item (the sampler's order; batch 1)
+        smp = self.extract_loader.sampler
+        order = list(smp.idx) if isinstance(smp, datasets.ShardSampler) else None
         t0 = time.perf_counter()
         n = 0
         t = t0
@@ -375,12 +416,10 @@ class Extractor:
                 message += self.save_desc(inputs, outputs, processed)
             t = mark("save", t)
             self.logger.info(message)
-            name_list += "{} {}\n".format(idx, inputs["name1"][0])
+            names.append((order[idx] if order is not None else idx, inputs["name1"][0]))
             n += 1
         torch.cuda.synchronize(self.device)
-        if self.output_flag:
-            with open(os.path.join(self.img_root, "name_list.txt"), "w") as f:
-                f.write(name_list)
+        self._write_name_list(names)
         dt = time.perf_counter() - t0
         self.stats = {"images": n, "seconds": dt, "images_per_s": n / dt if dt > 0 else 0.0,
                       "stage_ms_per_image": ({k: 1e3 * v / max(n, 1) for k, v in stages.items()}

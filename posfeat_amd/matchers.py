@@ -44,6 +44,12 @@ def _match(d1, d2, mode, ratio=0.95):
         raise ValueError("descriptors must be [n1, d] and [n2, d]")
     n1, dim = d1.shape
     n2 = d2.shape[0]
+    if mode != "mnn" and min(n1, n2) < 2:
+        # the reference's torch.topk(sim, 2, dim=1) / topk(sim.t(), 2, dim=1)
+        # (aachen/matchers.py:21, 29, 51, 59) raise here; a second-best
+        # similarity of -inf would instead pass every row through the ratio test
+        raise RuntimeError("ratio matchers need at least 2 descriptors on each side "
+                           "(got %d and %d): selected index k out of range" % (n1, n2))
     if n1 == 0 or n2 == 0:
         return np.zeros((0, 2), dtype=np.int64)
     if dim != 128:

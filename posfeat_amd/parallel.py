@@ -53,13 +53,34 @@ class SyncBNGroup:
     already initialised (nccl = RCCL on the GPU box, gloo in CPU tests), and
     every rank creates its communicator; the BatchNorm statistics are then
     summed in-stream by ncclAllReduce inside the backbone's forward/backward.
-    ``lib`` is injectable for the host-side test of the bootstrap."""
+    ``lib`` is injectable for the host-side test of the bootstrap.
 
-    def __init__(self, group=None, lib=None):
+    ``shape`` = this rank's (batch, h, w): the in-stream exchange sums 2 C
+    doubles per BatchNorm and normalises by P * world (P = this rank's pixel
+    count), which is torch.nn.SyncBatchNorm's arithmetic only when every rank
+    holds the same pixel count (torch all-gathers per-rank counts).  The shapes
+    are therefore all-gathered once here and unequal ones are refused.
+
+    Ordering with torch's own communicator: the SyncBN communicator's
+    all-reduces are enqueued on the trainer's stream inside the backbone
+    forward/backward, the gradient all-reduce on torch's process group after
+    the backward; every rank issues the same sequence (same program, no
+    data-dependent collectives), and ProcessGroupNCCL's stream waits for the
+    trainer's stream, so the two communicators' collectives never interleave
+    differently across ranks (the condition under which two RCCL
+    communicators can deadlock)."""
+
+    def __init__(self, group=None, lib=None, shape=None):
         from . import _lib
         self._lib = lib or _lib.lib()
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
+        if shape is not None:
+            shapes = [None] * self.world
+            dist.all_gather_object(shapes, tuple(int(v) for v in shape), group=group)
+            if len(set(shapes)) != 1:
+                raise ValueError("SyncBatchNorm needs the same (batch, h, w) on every rank: "
+                                 "got %s" % shapes)
         id_host = torch.zeros(128, dtype=torch.uint8)
         if self.rank == 0:
             buf = (ctypes.c_ubyte * 128)()

@@ -277,7 +277,8 @@ class BackboneTrainer:
         if sync_bn and dist.is_available() and dist.is_initialized() \
                 and dist.get_world_size(group) > 1:
             from .parallel import SyncBNGroup
-            self.set_group(SyncBNGroup(group))   # SyncBatchNorm, PoSFeat_model.py:49
+            # SyncBatchNorm, PoSFeat_model.py:49 (same batch shape on every rank)
+            self.set_group(SyncBNGroup(group, shape=(batch, h, w)))
 
     def set_group(self, group):
         """SyncBatchNorm: sum every BatchNorm's statistics over ``group``'s

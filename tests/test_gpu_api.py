@@ -132,49 +132,6 @@ def test_preprocess_utils_dropins(gpu):
         pu.generate_kpts_single(torch.from_numpy(km).to(gpu), 1, 300, stable=False)
 
 
-def test_extract_cli_synthetic(gpu, tmp_path):
-    """extract.py end to end on the synthetic config: npz files in the
-    reference format, identical (near-tie aware) to the oracle's process()."""
-    import yaml
-    cfg = yaml.safe_load(open(os.path.join(ROOT, "configs", "extract_synthetic.yaml")))
-    cfg["data_config_extract"].update(num_images=2, height=128, width=160)
-    cfg["detector_config"]["num_pts"] = 512
-    p = tmp_path / "cfg.yaml"
-    yaml.safe_dump(cfg, open(p, "w"))
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "extract.py"), "--config", str(p)],
-                       cwd=tmp_path, capture_output=True, text=True, timeout=600)
-    assert r.returncode == 0, r.stderr[-2000:]
-    out_dir = tmp_path / "ckpts" / cfg["output_root"] / "desc" / "synthetic"
-    files = sorted(os.listdir(out_dir))
-    assert files == ["00000.ppm.PoSFeat_seeded", "00001.ppm.PoSFeat_seeded"]
-    from oracle import model_ref, detect_ref
-    from posfeat_amd.datasets import SyntheticImages
-    from posfeat_amd.weights import seeded_state_dicts
-    from near_tie import explain_differences
-    bb, hd = seeded_state_dicts(0)
-    ds = SyntheticImages(cfg["data_config_extract"])
-    for i, f in enumerate(files):
-        z = np.load(out_dir / f)
-        assert z["keypoints"].dtype == np.float32 and z["keypoints"].shape[1] == 2
-        assert z["scores"].shape == (z["keypoints"].shape[0], 1)
-        assert z["descriptors"].shape == (z["keypoints"].shape[0], 128)
-        np.testing.assert_allclose(np.linalg.norm(z["descriptors"], axis=1), 1.0, atol=1e-5)
-        img = ds[i]["im1"][None]
-        o = model_ref.posfeat_extract(bb, hd, img)
-        ref = detect_ref.process_image(o["local_point"].numpy(), o["local_map"].numpy(),
-                                       cfg["detector_config"], 128, 160)
-        assert z["keypoints"].shape[0] == ref["kpt"].shape[0]
-        # match keypoints by position: common ones must agree in desc/score
-        kp = np.round(z["keypoints"], 3)
-        rk = np.round(ref["kpt"], 3)
-        common = {tuple(k): j for j, k in enumerate(rk)}
-        hit = [(i2, common[tuple(k)]) for i2, k in enumerate(kp) if tuple(k) in common]
-        assert len(hit) >= 0.97 * len(kp)
-        a, b = np.array(hit).T
-        np.testing.assert_allclose(z["descriptors"][a], ref["desc"][0][b], atol=1e-4)
-        np.testing.assert_allclose(z["scores"][a], ref["kp_score"][0][b], atol=1e-4)
-
-
 def test_normalize_rgb8_bit_exact(gpu):
     """The device input transform equals datasets.to_input's host result bit for bit."""
     from posfeat_amd import ops
@@ -186,36 +143,3 @@ def test_normalize_rgb8_bit_exact(gpu):
     for i in range(2):
         ref, _ = to_input(im[i])                  # crops 50x70 to 48x64
         assert torch.equal(got[i, :, :48, :64], ref)
-
-
-def test_extract_pipelined_equals_serial(gpu, tmp_path):
-    """The pipelined loop (same-size grouping, uint8 upload, async D2H, writer
-    thread) writes the same files as the reference's serial loop."""
-    import yaml
-    cfg = yaml.safe_load(open(os.path.join(ROOT, "configs", "extract_synthetic.yaml")))
-    cfg["data_config_extract"].update(num_images=5, height=96, width=128, workers=2)
-    cfg["detector_config"]["num_pts"] = 300
-    outs = {}
-    for mode in ("1", "0"):
-        cfg["output_root"] = "syn_" + mode
-        p = tmp_path / ("cfg%s.yaml" % mode)
-        yaml.safe_dump(cfg, open(p, "w"))
-        env = dict(os.environ, POSFEAT_EXTRACT_PIPELINE=mode, POSFEAT_EXTRACT_GROUP="3")
-        r = subprocess.run([sys.executable, os.path.join(ROOT, "extract.py"), "--config", str(p)],
-                           cwd=tmp_path, capture_output=True, text=True, timeout=600, env=env)
-        assert r.returncode == 0, r.stderr[-2000:]
-        d = tmp_path / "ckpts" / cfg["output_root"] / "desc" / "synthetic"
-        outs[mode] = {f: np.load(d / f) for f in sorted(os.listdir(d))}
-        names = open(tmp_path / "ckpts" / cfg["output_root"] / "image" / "name_list.txt").read()
-        assert names.splitlines()[4] == "4 synthetic/00004.ppm"
-    assert list(outs["1"]) == list(outs["0"]) and len(outs["1"]) == 5
-    for f in outs["1"]:
-        a, b = outs["1"][f], outs["0"][f]
-        assert a["keypoints"].shape == b["keypoints"].shape
-        ka, kb = np.round(a["keypoints"], 3), np.round(b["keypoints"], 3)
-        common = {tuple(k): j for j, k in enumerate(kb)}
-        hit = [(i, common[tuple(k)]) for i, k in enumerate(ka) if tuple(k) in common]
-        assert len(hit) >= 0.97 * len(ka)
-        ia, ib = np.array(hit).T
-        np.testing.assert_allclose(a["descriptors"][ia], b["descriptors"][ib], atol=1e-4)
-        np.testing.assert_allclose(a["scores"][ia], b["scores"][ib], atol=1e-4)

@@ -1,11 +1,12 @@
 """Switches whose two forms must give BIT-identical engine outputs.
 
-conv_bf6r_kernel (pre-split weights, A straight to registers) against
-conv_bf6b_kernel (A staged through LDS): the same bf16x6 products in the same
-order, so the engine's outputs must be BIT-identical with POSFEAT_BF6R=0/1
-(the switch is read once per process: each run is a child process).  The
-B=8 480x640 bench instance covers the batched Winograd GEMMs, the tap GEMM
-and the 1x1 / strided encoder convs; the stage-count variant too."""
+conv_bf6d_kernel (pre-split weights, A prefetched D chunks ahead in registers,
+the default) against conv_bf6b_kernel (A staged through LDS, POSFEAT_BF6D=0):
+the same bf16x6 products in the same order, so the engine's outputs must be
+BIT-identical for every D (the switch is read once per process: each run is a
+child process).  The B=8 480x640 bench instance covers the batched Winograd
+GEMMs, the tap GEMM and the 1x1 / strided encoder convs (masked taps: the
+register-A candidates TILE_BF6R_*)."""
 import os
 import subprocess
 import sys
@@ -50,17 +51,20 @@ def test_fused_upsample_bit_identical(tmp_path):
         np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
 
 
-def test_bf6r_bit_identical_to_bf6b(tmp_path):
-    """also the 8-wave 256x128 pre-split tile (TILE_BF6B_256x128 = 28: an
-    autotuner candidate for the 1x1 convs, forced everywhere it is legal, and
-    on the batched Winograd GEMMs via POSFEAT_GEMM_B256) and the deep-A-prefetch
-    tiles (conv_bf6d_kernel, POSFEAT_BF6D=3)"""
-    ref = _run(tmp_path, {"POSFEAT_BF6R": "0", "POSFEAT_BF6D": "0"}, "b")   # LDS-staged bf6b
-    for tag, env in (("r2", {"POSFEAT_BF6R": "1"}),
-                     ("r3", {"POSFEAT_BF6R": "1", "POSFEAT_BF6R_NST": "3"}),
+def test_bf6d_bit_identical_to_bf6b(tmp_path):
+    """D = 2 (default), 3 and 4, the register-A candidates forced on every conv
+    they serve (POSFEAT_CONV_TILE 26 = TILE_BF6R_128x128), and the 8-wave
+    256x128 pre-split tile (TILE_BF6B_256x128 = 28: an autotuner candidate for
+    the 1x1 convs, forced everywhere it is legal, and on the batched Winograd
+    GEMMs via POSFEAT_GEMM_B256; D capped at 3 there)"""
+    ref = _run(tmp_path, {"POSFEAT_BF6D": "0"}, "b")   # LDS-staged bf6b
+    for tag, env in (("d2", {}),                       # the default: deep A prefetch, D = 2
+                     ("d3", {"POSFEAT_BF6D": "3"}),
+                     ("d4", {"POSFEAT_BF6D": "4"}),
+                     ("r26", {"POSFEAT_CONV_TILE": "26"}),
                      ("b256", {"POSFEAT_CONV_TILE": "28", "POSFEAT_GEMM_B256": "1"}),
-                     ("d2", {}),                       # the default: deep A prefetch, D = 2
-                     ("d3", {"POSFEAT_BF6D": "3"})):
+                     ("b256d4", {"POSFEAT_CONV_TILE": "28", "POSFEAT_GEMM_B256": "1",
+                                 "POSFEAT_BF6D": "4"})):
         got = _run(tmp_path, env, tag)
         for k in ("lp", "lm", "gm"):
             np.testing.assert_array_equal(got[k], ref[k], err_msg="%s %s" % (tag, k))

@@ -88,5 +88,11 @@ def test_matcher_tie_rule_and_edge_cases(gpu):
     np.testing.assert_array_equal(pu.mnn_matcher(torch.from_numpy(d1).to(gpu),
                                                  torch.from_numpy(d2).to(gpu)), ref)
     assert M.mnn_matcher(np.zeros((0, 128), np.float32), d2).shape == (0, 2)
+    # one descriptor on a side: the reference's topk(k=2) raises, and so do we
+    for f in (M.ratio_matcher, M.mutual_nn_ratio_matcher):
+        for a, b in ((d1[:1], d2), (d1, d2[:1])):
+            with pytest.raises(RuntimeError):
+                f(a, b)
+    assert M.mnn_matcher(d1[:1], d2).shape == (1, 2)
     with pytest.raises(NotImplementedError):
         M.mnn_matcher(np.zeros((4, 64), np.float32), np.zeros((4, 64), np.float32))

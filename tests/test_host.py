@@ -229,8 +229,13 @@ def _syncbn_worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from posfeat_amd.parallel import SyncBNGroup
     fake = _FakeGroupLib()
-    g = SyncBNGroup(lib=fake)
-    q.put((rank, fake.created, g.handle.value))
+    g = SyncBNGroup(lib=fake, shape=(4, 96, 128))
+    refused = False
+    try:   # unequal per-rank batches: refused on every rank
+        SyncBNGroup(lib=_FakeGroupLib(), shape=(4 + rank, 96, 128))
+    except ValueError:
+        refused = True
+    q.put((rank, fake.created, g.handle.value, refused))
     g.close()
     dist.destroy_process_group()
 
@@ -251,6 +256,7 @@ def test_gloo_syncbn_group_bootstrap_world2():
     for p in procs:
         p.join(60)
     want = bytes((7 * i + 3) % 256 for i in range(128))
-    for rank, created, handle in res:
+    for rank, created, handle, refused in res:
         assert created == (2, rank, want)
         assert handle == 1000 + rank
+        assert refused

@@ -122,3 +122,16 @@ def test_engine_layer_table_matches_state_dicts():
     blob = weights.pack_for_device(*weights.seeded_state_dicts(0), specs)
     assert blob.size <= _lib.lib().posfeat_model_weight_floats()
     assert np.isfinite(blob).all()
+
+
+def test_isa_bf6d_vmem_order():
+    """conv_bf6d_kernel's counted waits (vmcnt(4) / vmcnt(4 D)) hold only if
+    each step's B-plane DMA is issued before its four A register loads and no
+    vmcnt(0) drain sits between them: checked on the built library's gfx950
+    ISA (tools/isa_check.py; the order is pinned in the source by
+    sched barriers, this catches a compiler that reorders anyway)."""
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "isa_check.py")],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]

@@ -14,7 +14,13 @@ building the engine and planning/autotuning one instance per image size;
 reference's serial loop with synchronising per-stage timers.  Prints one JSON
 line.
 
-usage: python tools/extract_e2e.py [--seqs 12] [--timing] [--passes 1]
+``--sizes 480x640`` (default) builds every image at the metric's size;
+``--sizes mixed`` cycles the three HPatches-like sizes below.  After the run
+the same process times the kernel path (engine + detector + sampler on
+device-resident batches of the pipeline's group size, no I/O, as bench.py's
+step) so the line carries ``steady / kernel_path``.
+
+usage: python tools/extract_e2e.py [--seqs 96] [--sizes 480x640|mixed] [--timing] [--passes 1]
 """
 import argparse
 import json
@@ -33,10 +39,10 @@ sys.path.insert(0, ROOT)
 SIZES = [(480, 640), (600, 800), (752, 1000)]
 
 
-def make_dataset(root, nseq):
+def make_dataset(root, nseq, sizes):
     from PIL import Image
     for s in range(nseq):
-        h, w = SIZES[s % len(SIZES)]
+        h, w = sizes[s % len(sizes)]
         d = os.path.join(root, "data", "hpatches-sequences-release", "v_synth%02d" % s)
         os.makedirs(d, exist_ok=True)
         rs = np.random.RandomState(100 + s)
@@ -60,16 +66,47 @@ def make_checkpoint(root):
                    open(os.path.join(os.path.dirname(ck), "config.yaml"), "w"))
 
 
+def kernel_path_rate(eng, ex, hw, group, steps=5):
+    """bench.py's step (engine + detect + sample, device-resident, no host I/O)
+    at this run's group size and first image size, on the run's own engine."""
+    import torch
+    from posfeat_amd import ops
+    from posfeat_amd.weights import seeded_image
+    h, w = hw
+    cfg = ex.config["detector_config"]
+    imgs = torch.from_numpy(np.stack([seeded_image(i, h, w) for i in range(group)])).cuda()
+    ws = ops.DetectWorkspace()
+
+    def step():
+        out = eng.run(imgs, outputs=())
+        _, coord, _, _, n_dev = ops.detect(out["local_point"], cfg["nms_radius"], cfg["num_pts"],
+                                           thr=cfg["thr"], thr_mod=cfg["thr_mod"], ws=ws,
+                                           sync=False)
+        ops.sample_desc_nhwc(out["_local_map_nhwc"], coord, c=128, n_valid=n_dev)
+    step()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    return steps * group / (time.perf_counter() - t)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--seqs", type=int, default=12)
+    ap.add_argument("--seqs", type=int, default=96)
+    ap.add_argument("--sizes", default="480x640", help="HxW or 'mixed'")
     ap.add_argument("--timing", action="store_true", help="per-stage (synchronising) timing")
     ap.add_argument("--passes", type=int, default=1, help="2: a second (warm) pass")
     args = ap.parse_args()
     if args.timing:
         os.environ["POSFEAT_EXTRACT_TIMING"] = "1"
+    sizes = SIZES if args.sizes == "mixed" else [tuple(int(v) for v in args.sizes.split("x"))]
     tmp = tempfile.mkdtemp(prefix="posfeat_e2e_")
-    make_dataset(tmp, args.seqs)
+    t = time.perf_counter()
+    make_dataset(tmp, args.seqs, sizes)
+    print("[e2e] dataset of %d images built in %.1f s" % (6 * args.seqs, time.perf_counter() - t),
+          flush=True)
     make_checkpoint(tmp)
     cfg = yaml.safe_load(open(os.path.join(ROOT, "configs", "extract_hpatches.yaml")))
     cfg["data_config_extract"]["data_path"] = os.path.join(tmp, "data", "hpatches-sequences-release")
@@ -96,6 +133,9 @@ def main():
                 st["steady_images_per_s"] = (st["images"] - first[1]) / (st["seconds"] - first[0])
         st["setup_s"] = setup
         eng = ex.model._engine
+        st["kernel_path_images_per_s"] = kernel_path_rate(eng, ex, sizes[0], st.get("group", 32))
+        if "steady_images_per_s" in st:
+            st["steady_over_kernel_path"] = st["steady_images_per_s"] / st["kernel_path_images_per_s"]
         st["engine_shapes"] = len(eng.cached_shapes)
         st["engine_workspace_mb"] = eng.workspace_bytes / 2 ** 20
         res[p] = st
@@ -112,9 +152,10 @@ def main():
         gc.collect()
         torch.cuda.empty_cache()
     import torch
-    print(json.dumps({"workload": "extract.py e2e (configs/extract_hpatches.yaml, batch 1)",
+    print(json.dumps({"workload": "extract.py e2e (configs/extract_hpatches.yaml: loader batch 1 "
+                                  "in the reference; the pipelined loop groups by shape)",
                       "data": "synthetic HPatches layout, %d seqs x 6 ppm, sizes %s" % (
-                          args.seqs, sorted({SIZES[s % len(SIZES)] for s in range(args.seqs)})),
+                          args.seqs, sorted({sizes[s % len(sizes)] for s in range(args.seqs)})),
                       "device": torch.cuda.get_device_name(0), **res}))
 
 

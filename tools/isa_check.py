@@ -1,0 +1,151 @@
+"""ISA checks on the built libposfeat_hip.so (CPU only, no GPU needed).
+
+Extracts the gfx950 code objects from the library's clang offload bundles,
+disassembles them with llvm-objdump and checks properties the kernels' counted
+waits rely on but the source cannot pin by itself:
+
+* conv_bf6d_kernel: inside the K loop every wave-instruction batch of B-plane
+  LDS-DMA (global_load_lds_dwordx4) is issued BEFORE the A register loads
+  (global_load_dwordx4) of the same step, and no `s_waitcnt vmcnt(0)` sits
+  between them (the counted vmcnt(4) / vmcnt(4 D) waits assume exactly four
+  younger A loads per chunk).
+
+usage: python tools/isa_check.py [--dump KERNEL_SUBSTRING]
+Exit status 1 on a violated property.  tests/test_weights_abi.py runs it.
+"""
+import argparse
+import os
+import re
+import struct
+import subprocess
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "posfeat_amd", "libposfeat_hip.so")
+OBJDUMP = "/opt/rocm/llvm/bin/llvm-objdump"
+MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+
+
+def code_objects(path=LIB):
+    """The gfx950 ELF code objects of every offload bundle in the library."""
+    data = open(path, "rb").read()
+    out = []
+    pos = data.find(MAGIC)
+    while pos >= 0:
+        n = struct.unpack_from("<Q", data, pos + 24)[0]
+        p = pos + 32
+        for _ in range(n):
+            off, size, tlen = struct.unpack_from("<QQQ", data, p)
+            triple = data[p + 24:p + 24 + tlen].decode()
+            p += 24 + tlen
+            if "gfx950" in triple and size:
+                out.append(data[pos + off:pos + off + size])
+        pos = data.find(MAGIC, pos + 24)
+    return out
+
+
+def disassemble(blobs):
+    text = []
+    with tempfile.TemporaryDirectory() as td:
+        for i, b in enumerate(blobs):
+            f = os.path.join(td, "co%d.o" % i)
+            open(f, "wb").write(b)
+            r = subprocess.run([OBJDUMP, "-d", "--no-show-raw-insn", f], capture_output=True,
+                               text=True, check=True)
+            text.append(r.stdout)
+    return "\n".join(text)
+
+
+def functions(asm):
+    """{symbol: [instruction lines]} from llvm-objdump output."""
+    funcs, cur = {}, None
+    for line in asm.splitlines():
+        m = re.match(r"^[0-9a-f]+ <(.+)>:$", line)
+        if m:
+            cur = m.group(1)
+            funcs[cur] = []
+        elif cur and line.strip() and not line.startswith("Disassembly"):
+            funcs[cur].append(line.strip())
+    return funcs
+
+
+def check_bf6d(name, body):
+    """Per K-loop step: [B DMA batch] then [A loads], no vmcnt(0) in between."""
+    errs = []
+    ops = []
+    for ln in body:
+        op = ln.split()[0]
+        if op.startswith("global_load_lds"):
+            ops.append("B")
+        elif op.startswith("global_load_dwordx4"):
+            ops.append("A")
+        elif op == "s_waitcnt" and "vmcnt(0)" in ln:
+            ops.append("W0")
+        elif op.startswith("v_mfma"):
+            ops.append("M")
+        elif op == "s_barrier":
+            ops.append("S")
+    # collapse runs; inspect every B-batch that has A loads after it before the
+    # next MFMA: between the B batch and its A loads no W0 may occur, and no A
+    # load may precede the B batch within that step
+    seq = []
+    for o in ops:
+        if seq and seq[-1][0] == o:
+            seq[-1][1] += 1
+        else:
+            seq.append([o, 1])
+    nsteps = 0
+    for i, (o, n) in enumerate(seq):
+        if o != "B":
+            continue
+        # the step: from this B batch to the next MFMA run
+        j = i + 1
+        step = []
+        while j < len(seq) and seq[j][0] not in ("M", "B", "S"):
+            step.append(seq[j][0])
+            j += 1
+        if "A" in step:
+            nsteps += 1
+            if "W0" in step[:max(k for k, s in enumerate(step) if s == "A") + 1]:
+                errs.append("%s: s_waitcnt vmcnt(0) between a B-DMA batch and its A loads" % name)
+        # the A loads of a step must all come after its B batch: an A run
+        # between the step's barrier and this B batch is a reordering
+        k = i - 1
+        while k >= 0 and seq[k][0] not in ("M", "S", "B"):
+            if seq[k][0] == "A" and k > 0 and seq[k - 1][0] == "S":
+                errs.append("%s: A loads issued before the B-DMA batch of their step" % name)
+            k -= 1
+    if nsteps == 0:
+        errs.append("%s: no B-DMA -> A-load step found (pattern changed?)" % name)
+    return errs, nsteps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--dump", default=None)
+    args = ap.parse_args()
+    funcs = functions(disassemble(code_objects()))
+    if args.dump:
+        for k, v in funcs.items():
+            if args.dump in k:
+                print("<%s>" % k)
+                print("\n".join(v))
+        return 0
+    errs = []
+    found = 0
+    for k, v in funcs.items():
+        if "conv_bf6d_kernel" in k:
+            found += 1
+            e, n = check_bf6d(k, v)
+            errs += e
+            print("%-90s steps checked %d%s" % (k[:90], n, "  FAIL" if e else ""))
+    if not found:
+        errs.append("no conv_bf6d_kernel instance in %s" % LIB)
+    for e in errs:
+        print("ISA CHECK FAILED:", e)
+    return 1 if errs else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
