@@ -46,10 +46,18 @@ __device__ __forceinline__ uint32_t pf_fkey(float v) {
 // ---- bf16x6 operand split (conv.hip BF6 tiles, gemm6.hip) -----------------
 // x = h + m + l exactly up to 2^-27 |x|: h = RNE_bf16(x), m = RNE_bf16(x - h),
 // l = RNE_bf16(x - h - m) (both differences exact in fp32).
+// Two RNE conversions packed into one dword: hipcc emits ONE v_cvt_pk_bf16_f32
+// for this.  Never an inline-asm v_cvt_pk_bf16_f32: the compiler's hazard
+// recognizer does not see an asm's VGPR write as a VALU write, so it put no
+// wait states between it and an MFMA reading the result as SrcA / SrcB --
+// the MFMA then read the register's previous value whenever the schedule
+// placed it right behind the conversion (timing-dependent, nondeterministic
+// results: conv_glds_kernel<128,64,..,BF6> once its loop was rescheduled, and
+// round 2's bf16x6 stem variant; tools/tile_sweep.py).
+typedef __bf16 pf_bf16x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ unsigned pf_cvt_pk_bf16(float lo, float hi) {
-  unsigned r;
-  asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
-  return r;
+  const pf_bf16x2_t v = {(__bf16)lo, (__bf16)hi};
+  return __builtin_bit_cast(unsigned, v);
 }
 __device__ __forceinline__ void pf_split3_pair(float a, float b, unsigned& h, unsigned& m,
                                                unsigned& l) {

@@ -415,10 +415,10 @@ __device__ __forceinline__ void wait_vmcnt() {
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 
+// common.h: the compiler-visible conversion (an inline-asm one hid its VGPR
+// write from the hazard recognizer: MFMAs read stale operands)
 __device__ __forceinline__ unsigned cvt_pk_bf16(float lo, float hi) {
-  unsigned r;
-  asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
-  return r;
+  return pf_cvt_pk_bf16(lo, hi);
 }
 
 // 8 fp32 (k order) -> the three bf16 fragments of one MFMA operand

@@ -9,6 +9,12 @@ waits rely on but the source cannot pin by itself:
   (global_load_dwordx4) of the same step, and no `s_waitcnt vmcnt(0)` sits
   between them (the counted vmcnt(4) / vmcnt(4 D) waits assume exactly four
   younger A loads per chunk).
+* every kernel: no MFMA reads a VGPR written by v_cvt_pk_bf16_f32 within the
+  two preceding instructions without an s_nop between (the VALU-write ->
+  MFMA-SrcA/B wait states).  The conversion once came from inline asm, whose
+  VGPR write the compiler's hazard recognizer does not see: it padded
+  nothing and the MFMAs read stale operands (nondeterministic results,
+  DESIGN.md 4.1n).
 
 usage: python tools/isa_check.py [--dump KERNEL_SUBSTRING]
 Exit status 1 on a violated property.  tests/test_weights_abi.py runs it.
@@ -121,6 +127,38 @@ def check_bf6d(name, body):
     return errs, nsteps
 
 
+def _regs(s):
+    out = set()
+    for m in re.finditer(r"v\[(\d+):(\d+)\]|v(\d+)\b", s):
+        if m.group(1):
+            out |= set(range(int(m.group(1)), int(m.group(2)) + 1))
+        else:
+            out.add(int(m.group(3)))
+    return out
+
+
+def check_cvt_mfma_hazard(name, body):
+    ins = [ln.split("//")[0].strip() for ln in body if ln.split("//")[0].strip()]
+    errs = []
+    for i, ln in enumerate(ins):
+        if not ln.startswith("v_mfma"):
+            continue
+        ops = ln.split(None, 1)[1].split(",")
+        if len(ops) < 3:
+            continue
+        src = _regs(ops[1]) | _regs(ops[2])
+        for d in (1, 2):
+            if i - d < 0:
+                break
+            p = ins[i - d]
+            if p.startswith("s_nop"):
+                break
+            if p.startswith("v_cvt_pk_bf16_f32") and _regs(p.split(None, 1)[1].split(",")[0]) & src:
+                errs.append("%s: MFMA %d instruction(s) after the v_cvt_pk_bf16_f32 that wrote its "
+                            "operand, no wait state: %s" % (name, d, ln[:60]))
+    return errs
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--dump", default=None)
@@ -138,10 +176,25 @@ def main():
         if "conv_bf6d_kernel" in k:
             found += 1
             e, n = check_bf6d(k, v)
+            # a vmcnt(0) drain is conservative (never wrong) but defeats the
+            # prefetch: an error for the default depth D = 2, a warning for
+            # the A/B depths 3 and 4
+            default = "ELi2ELi" in k
+            drains = [x for x in e if "vmcnt(0)" in x]
+            if not default:
+                e = [x for x in e if x not in drains]
             errs += e
-            print("%-90s steps checked %d%s" % (k[:90], n, "  FAIL" if e else ""))
+            print("%-90s steps checked %d%s%s" % (k[:90], n, "  FAIL" if e else "",
+                                                  "  (warning: vmcnt(0) drain)" if drains and not e
+                                                  else ""))
     if not found:
         errs.append("no conv_bf6d_kernel instance in %s" % LIB)
+    nh = 0
+    for k, v in funcs.items():
+        e = check_cvt_mfma_hazard(k, v)
+        nh += len(e)
+        errs += e
+    print("cvt_pk_bf16 -> MFMA operand hazards: %d" % nh)
     for e in errs:
         print("ISA CHECK FAILED:", e)
     return 1 if errs else 0
