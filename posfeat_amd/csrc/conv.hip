@@ -73,6 +73,10 @@ struct ConvArgs {
   const unsigned short* wb;
   long long wplane, bwb;
   const float* zero;  // a zeroed 16-B device word (pf_conv_zero16), read by masked DMA lanes
+  // pre-split A (conv_bf6s_kernel): three bf16 planes of x's [M][xcs] layout,
+  // plane stride xplane, batch stride bxb (elements)
+  const unsigned short* xb;
+  long long xplane, bxb;
 };
 
 // Epilogue shared by both kernels: acc -> LDS T[BM][BN+4] (conflict-free: a
@@ -190,7 +194,41 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a,
   }
 }
 
-template <int BM, int BN, int WM, int WN, bool CIN32>
+// bf16x6 helpers (described with the row tiles below)
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+
+// common.h: the compiler-visible conversion (an inline-asm one hid its VGPR
+// write from the hazard recognizer: MFMAs read stale operands)
+__device__ __forceinline__ unsigned cvt_pk_bf16(float lo, float hi) {
+  return pf_cvt_pk_bf16(lo, hi);
+}
+
+// 8 fp32 (k order) -> the three bf16 fragments of one MFMA operand
+__device__ __forceinline__ void split3(const f32x4& p0, const f32x4& p1, u32x4_t& h, u32x4_t& m,
+                                       u32x4_t& l) {
+  const float x[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float a = x[2 * i], b = x[2 * i + 1];
+    const unsigned hp = cvt_pk_bf16(a, b);
+    const float ra = a - __uint_as_float(hp << 16), rb = b - __uint_as_float(hp & 0xffff0000u);
+    const unsigned mp = cvt_pk_bf16(ra, rb);
+    const float sa = ra - __uint_as_float(mp << 16), sb = rb - __uint_as_float(mp & 0xffff0000u);
+    h[i] = hp;
+    m[i] = mp;
+    l[i] = cvt_pk_bf16(sa, sb);
+  }
+}
+
+__device__ __forceinline__ f32x16 mfma_bf16(const u32x4_t& a, const u32x4_t& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a),
+                                                 __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
+}
+
+// BF6 (the Cin = 4 stem in bf16x6 mode): the products as six bf16 MFMAs per
+// fp32 product (split3 / mfma_bf16 below, fp32-exact); the staging is the same.
+template <int BM, int BN, int WM, int WN, bool CIN32, bool BF6 = false>
 __global__ __launch_bounds__(WM* WN * 64) void conv_mfma_kernel(ConvArgs a) {
   constexpr int THREADS = WM * WN * 64;
   constexpr int TM = BM / WM, TN = BN / WN;
@@ -335,6 +373,43 @@ __global__ __launch_bounds__(WM* WN * 64) void conv_mfma_kernel(ConvArgs a) {
   for (int c = 0; c < nch; ++c) {
     const int cur = c & 1;
     if (c + 1 < nch) load_chunk(kbase + (c + 1) * BK);
+    if constexpr (BF6) {
+      // lane (r, h) feeds k = 16 g + 8 h .. +7 of rows r: two 16-B reads per
+      // operand row (36-float rows: the 16 rows of a ds_read_b128 lane group
+      // start on distinct 4-bank quads, conflict-free)
+      const float* Ab6 = As + (cur * BM + arow) * LDSP + 8 * (lane >> 5);
+      const float* Bb6 = Bs + (cur * BN + brow) * LDSP + 8 * (lane >> 5);
+#pragma unroll
+      for (int g = 0; g < BK / 16; ++g) {
+        u32x4_t ah[MI], am[MI], al[MI], bh[NI], bm[NI], bl[NI];
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi)
+          split3(*reinterpret_cast<const f32x4*>(Ab6 + mi * 32 * LDSP + 16 * g),
+                 *reinterpret_cast<const f32x4*>(Ab6 + mi * 32 * LDSP + 16 * g + 4), ah[mi],
+                 am[mi], al[mi]);
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni)
+          split3(*reinterpret_cast<const f32x4*>(Bb6 + ni * 32 * LDSP + 16 * g),
+                 *reinterpret_cast<const f32x4*>(Bb6 + ni * 32 * LDSP + 16 * g + 4), bh[ni],
+                 bm[ni], bl[ni]);
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < NI; ++ni) {
+            f32x16 cc = acc[mi][ni];
+            cc = mfma_bf16(ah[mi], bh[ni], cc);
+            cc = mfma_bf16(ah[mi], bm[ni], cc);
+            cc = mfma_bf16(am[mi], bh[ni], cc);
+            cc = mfma_bf16(ah[mi], bl[ni], cc);
+            cc = mfma_bf16(al[mi], bh[ni], cc);
+            cc = mfma_bf16(am[mi], bm[ni], cc);
+            acc[mi][ni] = cc;
+          }
+      }
+      if (c + 1 < nch) store_chunk(cur ^ 1);
+      __syncthreads();
+      continue;
+    }
     const float* Ab = As + (cur * BM + arow) * LDSP + kofs;
     const float* Bb = Bs + (cur * BN + brow) * LDSP + kofs;
 #pragma unroll
@@ -412,36 +487,6 @@ __device__ __forceinline__ void wait_vmcnt() {
 // 32x32x16 step instead of 8 x 64 = 512.  The split runs on the VALU beside
 // the MFMAs (v_cvt_pk_bf16_f32, RNE).  Accumulation order is fixed (k, then
 // the six terms in the order above): deterministic, tile-size independent.
-typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
-
-// common.h: the compiler-visible conversion (an inline-asm one hid its VGPR
-// write from the hazard recognizer: MFMAs read stale operands)
-__device__ __forceinline__ unsigned cvt_pk_bf16(float lo, float hi) {
-  return pf_cvt_pk_bf16(lo, hi);
-}
-
-// 8 fp32 (k order) -> the three bf16 fragments of one MFMA operand
-__device__ __forceinline__ void split3(const f32x4& p0, const f32x4& p1, u32x4_t& h, u32x4_t& m,
-                                       u32x4_t& l) {
-  const float x[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const float a = x[2 * i], b = x[2 * i + 1];
-    const unsigned hp = cvt_pk_bf16(a, b);
-    const float ra = a - __uint_as_float(hp << 16), rb = b - __uint_as_float(hp & 0xffff0000u);
-    const unsigned mp = cvt_pk_bf16(ra, rb);
-    const float sa = ra - __uint_as_float(mp << 16), sb = rb - __uint_as_float(mp & 0xffff0000u);
-    h[i] = hp;
-    m[i] = mp;
-    l[i] = cvt_pk_bf16(sa, sb);
-  }
-}
-
-__device__ __forceinline__ f32x16 mfma_bf16(const u32x4_t& a, const u32x4_t& b, const f32x16& c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a),
-                                                 __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
-}
 
 // One step of an LDS-DMA pipeline: the next chunk's DMA into LDS through
 // (d0, d1), then the MFMA work reading LDS through (s0, s1).  The four are
@@ -993,25 +1038,42 @@ void conv_bf6d_kernel(ConvArgs a) {
           (const __attribute__((address_space(1))) void*)(bsrc[i] + (long long)c * BK),
           (__attribute__((address_space(3))) void*)(Bd + (wave * B_G + i) * 16 * BK), 16, 0, 0);
   };
-  // chunk c = (slab, tap): always four loads per lane (a masked tap reads the
-  // zeroed 16-B word), so the per-chunk vmcnt accounting below holds
+  // A chunk = (slab, tap): always four loads per lane, so the per-chunk vmcnt
+  // accounting below holds.  A masked lane (tap outside the image, row past
+  // M) selects the zero block as its base and reads the same four offsets
+  // from it: one per-lane pointer select, four distinct addresses.  (Selecting
+  // the one zero word per load let the compiler branch on the mask and merge
+  // the masked lanes' identical loads into one load + register copies behind
+  // an s_waitcnt vmcnt(0) -- a full drain of the prefetch -- and a wave with
+  // every lane masked issued 3 loads, not 4.)  The chunk to load next is
+  // tracked incrementally (no per-chunk divisions) and clamped at the last
+  // chunk: EVERY step issues one B DMA and four A loads (past the end they
+  // re-read the last chunk, an L2 hit, never used), so every path through the
+  // loop has the same vector-memory count -- the compiler's own waits for the
+  // A registers then stay counted instead of falling back to vmcnt(0) where
+  // paths with and without loads met.
   const float* const zero = a.zero;
-  // A masked lane (tap outside the image, row past M) selects the zero block
-  // as its base and reads the same four offsets from it: one per-lane pointer
-  // select, four distinct addresses, no branch.  (Selecting the one zero word
-  // per load let the compiler branch on the mask and merge the masked lanes'
-  // identical loads into one load + register copies behind an
-  // s_waitcnt vmcnt(0) -- a full drain of the prefetch whenever a wave held a
-  // masked lane, and a wave with every lane masked issued 3 loads, not 4.)
-  auto load_a = [&](int c, f32x4 (&v)[4]) {
-    const int slab = c / ntap, tap = c - slab * ntap;
-    const int kh = tap / a.KW, kw = tap - kh * a.KW;
-    const bool ok = (tapok >> tap) & 1u;
-    const float* p = xrow + ((long long)kh * a.W + kw) * a.xcs + (long long)slab * BK;
+  int la_c = ch0, la_slab = ch0 / ntap, la_tap = ch0 - (ch0 / ntap) * ntap;
+  int la_kh = la_tap / a.KW, la_kw = la_tap - (la_tap / a.KW) * a.KW;
+  auto load_a_next = [&](f32x4 (&v)[4]) {
+    const bool ok = (tapok >> la_tap) & 1u;
+    const float* p = xrow + ((long long)la_kh * a.W + la_kw) * a.xcs + (long long)la_slab * BK;
     const float* base = ok ? p : zero;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       v[j] = *reinterpret_cast<const f32x4*>(base + (j >> 1) * 16 + (j & 1) * 4);
+    if (la_c + 1 < ch1) {  // uniform
+      ++la_c;
+      ++la_tap;
+      if (++la_kw == a.KW) {
+        la_kw = 0;
+        if (++la_kh == a.KH) {
+          la_kh = 0;
+          la_tap = 0;
+          ++la_slab;
+        }
+      }
+    }
   };
 
   f32x16 acc[NI];
@@ -1024,28 +1086,31 @@ void conv_bf6d_kernel(ConvArgs a) {
   // issued BEFORE the A loads that follow it in program order: vmcnt retires
   // in issue order, so B(c) is covered only if exactly the A loads issued
   // after it are younger.  The A loads read memory the DMA does not write, so
-  // the scheduler could legally hoist them above the DMA; the
-  // sched_barrier(0)s pin the order (and keep the waits where they are).
+  // the scheduler could legally hoist them above the DMA; sched barriers pin
+  // the order of the vector-memory instructions (mask PF_SCHED_NO_VMEM: ALU,
+  // MFMA and LDS instructions may still move across).  tools/isa_check.py
+  // checks the built ISA.
+  // Prologue: A(0) .. A(D-2), then B(0), then A(D-1): B(0) too has exactly
+  // four younger loads, so every step waits vmcnt(4) (one loop body, no
+  // first-step special case for the compiler to peel).
   f32x4 va[D][4];
-  if (nch > 0) issue_b(Bs, ch0);
-  __builtin_amdgcn_sched_barrier(PF_SCHED_NO_VMEM);
+  if (nch > 0) {  // (every plan gives each split >= 1 chunk; no load past the slice)
 #pragma unroll
-  for (int j = 0; j < D; ++j)
-    if (j < nch) load_a(ch0 + j, va[j]);
+    for (int j = 0; j < D - 1; ++j) load_a_next(va[j]);
+    __builtin_amdgcn_sched_barrier(PF_SCHED_NO_VMEM);
+    issue_b(Bs, ch0);
+    __builtin_amdgcn_sched_barrier(PF_SCHED_NO_VMEM);
+    load_a_next(va[D - 1]);
+  }
 
   for (int i = 0; i < nch; i += D) {
 #pragma unroll
     for (int u = 0; u < D; ++u) {
       const int ii = i + u;
-      if (ii >= nch) break;
-      // B(ii) landed: it was issued before the 4 A loads of chunk ii-1+D (if any)
+      // B(ii) landed (and with it every older load, A(ii) included): it was
+      // issued right before the 4 A loads of the previous step / the prologue
       __builtin_amdgcn_sched_barrier(PF_SCHED_NO_VMEM);
-      if (ii - 1 + D < nch && ii > 0)
-        wait_vmcnt<4>();
-      else if (ii == 0 && D < nch)
-        wait_vmcnt<4 * D>();
-      else
-        wait_vmcnt<0>();
+      wait_vmcnt<4>();
       __builtin_amdgcn_s_barrier();
       const int s = ii & 1;
       // split this chunk's A (frees va[u] for chunk ii + D)
@@ -1054,13 +1119,14 @@ void conv_bf6d_kernel(ConvArgs a) {
       for (int g = 0; g < 2; ++g) split3(va[u][2 * g], va[u][2 * g + 1], ah[g], am[g], al[g]);
       pf_dma_overlap_step(
           Bs + (s ^ 1) * 2 * BSTAGE, Bs + (s ^ 1) * 2 * BSTAGE + BSTAGE, Bs + s * 2 * BSTAGE,
-          Bs + s * 2 * BSTAGE + BSTAGE, ii + 1 < nch,
+          Bs + s * 2 * BSTAGE + BSTAGE, true,
           [&](unsigned short* Bd, unsigned short*) {
-            issue_b(Bd, ch0 + ii + 1);
+            issue_b(Bd, min(ch0 + ii + 1, ch1 - 1));
             __builtin_amdgcn_sched_barrier(PF_SCHED_NO_VMEM);  // B(ii+1) strictly before A(ii+D)
-            if (ii + D < nch) load_a(ch0 + ii + D, va[u]);
+            load_a_next(va[u]);
           },
           [&](const unsigned short* Bb, const unsigned short*) {
+            if (ii >= nch) return;  // the tail of the last D-group: loads only
 #pragma unroll
             for (int g = 0; g < 2; ++g)
 #pragma unroll
@@ -1078,6 +1144,156 @@ void conv_bf6d_kernel(ConvArgs a) {
                 c = mfma_bf16(ah[g], bl, c);
                 c = mfma_bf16(al[g], bh, c);
                 c = mfma_bf16(am[g], bm, c);
+                acc[ni] = c;
+              }
+          });
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  f32x16 accm[1][NI];
+#pragma unroll
+  for (int ni = 0; ni < NI; ++ni) accm[0][ni] = acc[ni];
+  conv_epilogue<BM, BN, WM, WN>(
+      a, accm, smem, tm, n0, split, [&](int row) { return m0 + row < a.M ? m0 + row : -1; },
+      m0 / a.hw,
+      [&](int, int m) { return a.res ? a.res + (size_t)m * a.rcs : (const float*)nullptr; });
+}
+
+// ---------------------------------------------------------------------------
+// conv_bf6d_kernel with A PRE-SPLIT by its producer (conv_bf6s_kernel, conv
+// precision mode 2): A arrives as three bf16 planes (h, m, l of split3, the
+// Winograd input transform / head.conv1's output writing them), so the MFMA
+// loop does no conversion at all -- per lane and chunk six 16-B loads (two
+// k16 groups x three planes) that ARE the MFMA operands.  Dense GEMMs only
+// (the Winograd transform-domain GEMMs and the tap GEMM: 1x1, no padding;
+// rows past M re-read the last row, never stored).  The same h, m, l values
+// and the same product order as the in-kernel split: bit-identical to
+// conv_bf6d / conv_bf6b.  Same B ring, waits (now vmcnt(6): six A loads per
+// chunk) and epilogue as conv_bf6d_kernel.
+template <int BM, int BN, int D, int NWV = 4>
+__global__ __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(2)))
+void conv_bf6s_kernel(ConvArgs a) {
+  constexpr int WM = NWV, WN = 1, NW = NWV;
+  constexpr int TM = BM / WM, TN = BN;
+  constexpr int MI = TM / 32, NI = TN / 32;
+  constexpr int B_G = 3 * BN / 16 / NW;
+  static_assert(MI == 1 && B_G >= 1 && (3 * BN / 16) % NW == 0 && D >= 2 && D <= 3, "tile");
+  constexpr int BSTAGE = 3 * BN * BK / 2;  // floats (u16 pairs)
+  constexpr int RING = 2 * BSTAGE;
+  constexpr int EPI = BM * (BN + 4);
+  __shared__ __attribute__((aligned(16))) float smem[RING > EPI ? RING : EPI];
+  unsigned short* const Bs = reinterpret_cast<unsigned short*>(smem);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  int bid = blockIdx.x % a.nwg;
+  const int split = blockIdx.x / a.nwg;
+  {
+    const int nwg = a.nwg, q = nwg >> 3, r = nwg & 7, xcd = bid & 7, slot = bid >> 3;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+  }
+  const unsigned short* wb = a.wb;
+  const unsigned short* xb = a.xb;
+  if (a.nbatch > 1) {
+    const long long zb = blockIdx.y;
+    xb += zb * a.bxb;
+    a.y += zb * a.by;
+    wb += zb * a.bwb;
+  }
+  const int tm = bid / a.tiles_n, tn = bid - tm * a.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int r32 = lane & 31, hh = lane >> 5;
+  const unsigned short* xrow =
+      xb + (long long)min(m0 + wave * 32 + r32, a.M - 1) * a.xcs + hh * 8;
+  const unsigned short* bsrc[B_G];
+#pragma unroll
+  for (int i = 0; i < B_G; ++i) {
+    const int pr = (wave * B_G + i) * 16 + (lane >> 2);
+    const int plane = pr / BN, row = pr - plane * BN;
+    const int ks = (lane & 3) ^ ((row >> 2) & 3);
+    bsrc[i] = wb + plane * a.wplane + (long long)min(n0 + row, a.Cout - 1) * a.Kpad + ks * 8;
+  }
+  const int nch_all = a.Kpad / BK;
+  const int ch0 = (int)((long long)nch_all * split / a.ksplit);
+  const int ch1 = (int)((long long)nch_all * (split + 1) / a.ksplit);
+  const int nch = ch1 - ch0;
+
+  auto issue_b = [&](unsigned short* Bd, int c) {
+#pragma unroll
+    for (int i = 0; i < B_G; ++i)
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(bsrc[i] + (long long)c * BK),
+          (__attribute__((address_space(3))) void*)(Bd + (wave * B_G + i) * 16 * BK), 16, 0, 0);
+  };
+  // six loads per chunk: k16 group g, plane p (h, m, l); clamped at the last
+  // chunk so every step issues the same count (see conv_bf6d_kernel)
+  const long long xpl = a.xplane;
+  int la_c = ch0;
+  auto load_a_next = [&](u32x4_t (&v)[6]) {
+    const unsigned short* p = xrow + (long long)la_c * BK;
+#pragma unroll
+    for (int j = 0; j < 6; ++j)
+      v[j] = *reinterpret_cast<const u32x4_t*>(p + (j % 3) * xpl + (j / 3) * 16);
+    if (la_c + 1 < ch1) ++la_c;
+  };
+
+  f32x16 acc[NI];
+#pragma unroll
+  for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[ni][r] = 0.f;
+
+  u32x4_t va[D][6];
+  if (nch > 0) {
+#pragma unroll
+    for (int j = 0; j < D - 1; ++j) load_a_next(va[j]);
+    __builtin_amdgcn_sched_barrier(PF_SCHED_NO_VMEM);
+    issue_b(Bs, ch0);
+    __builtin_amdgcn_sched_barrier(PF_SCHED_NO_VMEM);
+    load_a_next(va[D - 1]);
+  }
+
+  for (int i = 0; i < nch; i += D) {
+#pragma unroll
+    for (int u = 0; u < D; ++u) {
+      const int ii = i + u;
+      __builtin_amdgcn_sched_barrier(PF_SCHED_NO_VMEM);
+      wait_vmcnt<6>();  // B(ii) and everything older (A(ii) included) landed
+      __builtin_amdgcn_s_barrier();
+      const int s = ii & 1;
+      const u32x4_t ah0 = va[u][0], am0 = va[u][1], al0 = va[u][2];
+      const u32x4_t ah1 = va[u][3], am1 = va[u][4], al1 = va[u][5];
+      pf_dma_overlap_step(
+          Bs + (s ^ 1) * 2 * BSTAGE, Bs + (s ^ 1) * 2 * BSTAGE + BSTAGE, Bs + s * 2 * BSTAGE,
+          Bs + s * 2 * BSTAGE + BSTAGE, true,
+          [&](unsigned short* Bd, unsigned short*) {
+            issue_b(Bd, min(ch0 + ii + 1, ch1 - 1));
+            __builtin_amdgcn_sched_barrier(PF_SCHED_NO_VMEM);
+            load_a_next(va[u]);
+            // the loads go out before this chunk's MFMAs (left to itself the
+            // scheduler put the MFMAs first: a chunk less prefetch lead)
+            __builtin_amdgcn_sched_barrier(0);
+          },
+          [&](const unsigned short* Bb, const unsigned short*) {
+            if (ii >= nch) return;
+#pragma unroll
+            for (int g = 0; g < 2; ++g)
+#pragma unroll
+              for (int ni = 0; ni < NI; ++ni) {
+                const u32x4_t ah = g ? ah1 : ah0, am = g ? am1 : am0, al = g ? al1 : al0;
+                const int row = ni * 32 + r32;
+                const int slot = (2 * g + hh) ^ ((row >> 2) & 3);
+                const unsigned short* bp = Bb + row * BK + slot * 8;
+                const u32x4_t bh = *reinterpret_cast<const u32x4_t*>(bp);
+                const u32x4_t bm = *reinterpret_cast<const u32x4_t*>(bp + BN * BK);
+                const u32x4_t bl = *reinterpret_cast<const u32x4_t*>(bp + 2 * BN * BK);
+                f32x16 c = acc[ni];
+                c = mfma_bf16(ah, bh, c);
+                c = mfma_bf16(ah, bm, c);
+                c = mfma_bf16(am, bh, c);
+                c = mfma_bf16(ah, bl, c);
+                c = mfma_bf16(al, bh, c);
+                c = mfma_bf16(am, bm, c);
                 acc[ni] = c;
               }
           });
@@ -1988,6 +2204,18 @@ bool glds3_on() {
   return e && e[0] == '1';
 }
 
+// The Cin = 4 register-staged convs (the stem) in bf16x6 with the rest of the
+// conv family (POSFEAT_BF6_STEM=0: fp32 MFMA); the train-mode backbone keeps
+// fp32 there as on its halo tiles (PfHaloFp32Scope).  All staged tiles of a
+// conv share the arithmetic, so the autotuner's choice never changes results.
+bool stem_bf6_on() {
+  static const bool off = [] {
+    const char* e = getenv("POSFEAT_BF6_STEM");
+    return e && e[0] == '0';
+  }();
+  return bf6_on() && !off && tl_halo_fp32 == 0;
+}
+
 template <int BM, int BN, int WM, int WN>
 void launch_rows(ConvArgs& a, int kern, hipStream_t st) {
   dim3 grid(a.nwg * a.ksplit, a.nbatch), block(WM * WN * 64);
@@ -1997,6 +2225,8 @@ void launch_rows(ConvArgs& a, int kern, hipStream_t st) {
     hipLaunchKernelGGL((conv_glds_kernel<BM, BN, WM, WN>), grid, block, 0, st, a);
   else if (a.Cin % BK == 0)
     hipLaunchKernelGGL((conv_mfma_kernel<BM, BN, WM, WN, true>), grid, block, 0, st, a);
+  else if (stem_bf6_on())
+    hipLaunchKernelGGL((conv_mfma_kernel<BM, BN, WM, WN, false, true>), grid, block, 0, st, a);
   else
     hipLaunchKernelGGL((conv_mfma_kernel<BM, BN, WM, WN, false>), grid, block, 0, st, a);
 }
@@ -2053,7 +2283,13 @@ int conv_run(ConvArgs& a, const Plan& p, hipStream_t st) {
     case TILE_BF6B_128x128:
     case TILE_BF6B_128x64: {
       const bool wide = p.tile == TILE_BF6B_128x128;
-      if (bf6d_depth() && a.KH == 1 && a.KW == 1 && a.pad == 0) {
+      if (a.xb) {  // A pre-split by its producer (pf_gemm_batched_pre)
+        const dim3 g(a.nwg * a.ksplit, a.nbatch);
+        if (wide)
+          hipLaunchKernelGGL((conv_bf6s_kernel<128, 128, 2>), g, dim3(256), 0, st, a);
+        else
+          hipLaunchKernelGGL((conv_bf6s_kernel<128, 64, 2>), g, dim3(256), 0, st, a);
+      } else if (bf6d_depth() && a.KH == 1 && a.KW == 1 && a.pad == 0) {
         const dim3 g(a.nwg * a.ksplit, a.nbatch);
         const int dd = bf6d_depth();
         if (wide && dd == 2)
@@ -2212,6 +2448,8 @@ static int conv_prepare(const posfeat_conv_desc* d, const float* x, const float*
   a.nbatch = 1;
   a.bx = a.bw = a.by = 0;
   a.wb = nullptr;
+  a.xb = nullptr;
+  a.xplane = a.bxb = 0;
   a.wplane = a.bwb = 0;
   a.zero = conv_zero_ptr();  // checked at launch (planning calls need no device)
   return POSFEAT_OK;
@@ -2491,6 +2729,44 @@ extern "C" int posfeat_conv2_up4(int n, int H, int W, const float* L, int lcs, c
 // C[z] [M][N] = A[z] [M][K] (row pitch lda) x B[z]^T, B[z] packed [N][K] (K % 32
 // == 0, the 1x1-conv weight layout), z < nb: ONE launch of conv_glds_kernel with
 // blockIdx.y = z (Winograd's 16 transform-domain GEMMs, wino.hip).
+// The batched GEMMs with BOTH operands pre-split into three bf16 planes
+// (conv precision mode 2): A [nb][M][lda] planes at Ab + p * pa, batch
+// stride sa; B as pf_gemm_batched's Bb.  conv_bf6s_kernel, 128x128 tiles (or
+// 128x64 where N % 128 != 0).  Replaces round 2's LDS-staged gemm6 kernel.
+int pf_gemm_batched_pre(const unsigned short* Ab, int lda, long long pa, long long sa,
+                        const unsigned short* Bb, long long bplane, long long sb, float* C, int ldc,
+                        long long sc, int nb, int M, int N, int K, hipStream_t st) {
+  if (K % BK || N % 64 || nb < 1 || lda % 8 || !Ab || !Bb) return POSFEAT_E_INVALID;
+  posfeat_conv_desc d;
+  d.n = 1;
+  d.h = 1;
+  d.w = M;
+  d.cin = K;
+  d.x_cstride = lda;
+  d.cout = N;
+  d.kh = d.kw = 1;
+  d.stride = 1;
+  d.pad = 0;
+  d.y_cstride = ldc;
+  d.res_cstride = 0;
+  d.act = POSFEAT_ACT_NONE;
+  ConvArgs a;
+  // x / w are never read (A and B come as planes); any non-null pointers
+  PF_TRY(conv_prepare(&d, reinterpret_cast<const float*>(Ab), reinterpret_cast<const float*>(Bb),
+                      nullptr, nullptr, C, a));
+  a.wb = Bb;
+  a.wplane = bplane;
+  a.xb = Ab;
+  a.xplane = pa;
+  const Plan p = conv_plan(a, false, N % 128 == 0 ? TILE_BF6B_128x128 : TILE_BF6B_128x64);
+  if (p.tile != TILE_BF6B_128x128 && p.tile != TILE_BF6B_128x64) return POSFEAT_E_UNSUPPORTED;
+  a.nbatch = nb;
+  a.bxb = sa;
+  a.bwb = sb;
+  a.by = sc;
+  return conv_run(a, p, st);
+}
+
 int pf_gemm_batched(const float* A, int lda, long long sa, const float* B, long long sb, float* C,
                     int ldc, long long sc, int nb, int M, int N, int K, hipStream_t st,
                     const unsigned short* Bb, long long bplane) {

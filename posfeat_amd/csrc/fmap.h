@@ -144,6 +144,9 @@ struct PfHaloFp32Scope {
 bool pf_bf6p_on();
 int pf_split3_rows(const float* x, long long rows, int cols, int ldx, unsigned short* out,
                    hipStream_t st);
+int pf_gemm_batched_pre(const unsigned short* Ab, int lda, long long pa, long long sa,
+                        const unsigned short* Bb, long long bplane, long long sb, float* C, int ldc,
+                        long long sc, int nb, int M, int N, int K, hipStream_t st);
 int pf_gemm_bf6p(const unsigned short* A, int lda, long long pa, long long sa,
                  const unsigned short* B, int ldb, long long pb, long long sb, float* C, int ldc,
                  long long sc, int nb, int M, int N, int K, hipStream_t st);

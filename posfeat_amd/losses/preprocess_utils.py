@@ -62,11 +62,15 @@ def generate_kpts_single(kp_map, nms_radius, num_pts=False, scale=4, stable=True
 def generate_kpts_single_async(kp_map, nms_radius, num_pts=False, scale=4, stable=True,
                                temperature=1, stride=1, use_nms=True, thr=False, thr_mod="mean"):
     """generate_kpts_single without the host synchronisation: full-capacity
-    (coord_n [b,cap,2], kp_score [b,cap,1]) plus the per-image counts [b] on
-    the device (rows beyond count are unused)."""
-    _, coord, score, counts, _ = _detect(kp_map, nms_radius, num_pts, stable, stride, use_nms,
-                                         thr, thr_mod, sync=False)
-    return coord, score, counts
+    (coord_n [b,cap,2], kp_score [b,cap,1]) plus the number of selected
+    keypoints n as a one-element device tensor (rows beyond n are unused).
+    n is the reference's (preprocess_utils.py:249-261): min(num_pts, the
+    smallest survivor count of the batch), raised to 128 -- NOT the survivor
+    count itself, which is smaller than n whenever the raise pads top-k with
+    zero-score entries (a 128 x 160 Aachen image at r = 3 has ~75 survivors)."""
+    _, coord, score, _, n_sel = _detect(kp_map, nms_radius, num_pts, stable, stride, use_nms,
+                                        thr, thr_mod, sync=False)
+    return coord, score, n_sel
 
 
 def _detect(kp_map, nms_radius, num_pts, stable, stride, use_nms, thr, thr_mod, sync):

@@ -249,12 +249,12 @@ class Extractor:
         nhwc = out["_local_map_nhwc"]
         host = []
         for i, (_, _, name, scale) in enumerate(items):
-            coord_n, score, counts = putils.generate_kpts_single_async(
+            coord_n, score, n_sel = putils.generate_kpts_single_async(
                 out["local_point"][i:i + 1], **self._det_cfg(name))
             desc = ops.sample_desc_nhwc(nhwc[i:i + 1], coord_n, c=128,
                                         normalize=self.config["loss_distance"] == "cos",
-                                        n_valid=counts)
-            host.append((name, scale, counts.to("cpu", non_blocking=True),
+                                        n_valid=n_sel)
+            host.append((name, scale, n_sel.to("cpu", non_blocking=True),
                          coord_n.to("cpu", non_blocking=True), desc.to("cpu", non_blocking=True),
                          score.to("cpu", non_blocking=True), w, h))
         ev = torch.cuda.Event()
@@ -266,8 +266,8 @@ class Extractor:
 
     def _finish_group(self, ev, host, writer, futures):
         ev.synchronize()
-        for name, scale, counts, kpt, desc, score, w, h in host:
-            n = int(counts[0])
+        for name, scale, n_sel, kpt, desc, score, w, h in host:
+            n = int(n_sel[0])   # the selected count (incl. the 128 raise)
             # denormalize_coords on the host: the same two fp32 roundings
             # (x * c, then + c) as the device path; a host->device copy of c
             # here would wait for the whole queue

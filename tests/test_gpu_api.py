@@ -130,6 +130,19 @@ def test_preprocess_utils_dropins(gpu):
     np.testing.assert_allclose(desc.cpu().numpy(), s["desc_norm"], atol=1e-5)
     with pytest.raises(NotImplementedError):
         pu.generate_kpts_single(torch.from_numpy(km).to(gpu), 1, 300, stable=False)
+    # the async form (Extractor's pipelined loop) reports the reference's n,
+    # including the raise to 128 when fewer points survive NMS + threshold
+    small = np.random.RandomState(4).rand(1, 1, 40, 48).astype(np.float32)
+    for r, npts in ((3, 20480), (1, 50), (1, 20000)):
+        c_s, s_s = pu.generate_kpts_single(torch.from_numpy(small).to(gpu), r, npts, thr=0.5,
+                                           thr_mod="abs")
+        c_a, s_a, n_a = pu.generate_kpts_single_async(torch.from_numpy(small).to(gpu), r, npts,
+                                                      thr=0.5, thr_mod="abs")
+        n = int(n_a[0])
+        assert n == c_s.shape[1], (r, npts, n, c_s.shape)
+        assert torch.equal(c_a[:, :n], c_s) and torch.equal(s_a[:, :n], s_s)
+        c_r, _ = detect_ref.generate_kpts_single(small, r, npts, thr=0.5, thr_mod="abs")
+        assert c_r.shape[1] == n
 
 
 def test_normalize_rgb8_bit_exact(gpu):

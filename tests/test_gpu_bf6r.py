@@ -64,7 +64,10 @@ def test_bf6d_bit_identical_to_bf6b(tmp_path):
                      ("r26", {"POSFEAT_CONV_TILE": "26"}),
                      ("b256", {"POSFEAT_CONV_TILE": "28", "POSFEAT_GEMM_B256": "1"}),
                      ("b256d4", {"POSFEAT_CONV_TILE": "28", "POSFEAT_GEMM_B256": "1",
-                                 "POSFEAT_BF6D": "4"})):
+                                 "POSFEAT_BF6D": "4"}),
+                     # conv precision mode 2: the Winograd / tap GEMM A operands
+                     # pre-split by their producers (conv_bf6s_kernel)
+                     ("mode2", {"POSFEAT_BF6": "2"})):
         got = _run(tmp_path, env, tag)
         for k in ("lp", "lm", "gm"):
             np.testing.assert_array_equal(got[k], ref[k], err_msg="%s %s" % (tag, k))

@@ -92,6 +92,12 @@ def check_bf6d(name, body):
             ops.append("M")
         elif op == "s_barrier":
             ops.append("S")
+        elif op.startswith("ds_"):
+            ops.append("L")
+        elif op.startswith(("global_store", "buffer_store", "s_endpgm")):
+            ops.append("G")
+        elif op.startswith("s_cbranch") or op == "s_branch":
+            ops.append("J")
     # collapse runs; inspect every B-batch that has A loads after it before the
     # next MFMA: between the B batch and its A loads no W0 may occur, and no A
     # load may precede the B batch within that step
@@ -108,7 +114,7 @@ def check_bf6d(name, body):
         # the step: from this B batch to the next MFMA run
         j = i + 1
         step = []
-        while j < len(seq) and seq[j][0] not in ("M", "B", "S"):
+        while j < len(seq) and seq[j][0] not in ("M", "B", "S", "L", "G"):
             step.append(seq[j][0])
             j += 1
         if "A" in step:
@@ -117,11 +123,10 @@ def check_bf6d(name, body):
                 errs.append("%s: s_waitcnt vmcnt(0) between a B-DMA batch and its A loads" % name)
         # the A loads of a step must all come after its B batch: an A run
         # between the step's barrier and this B batch is a reordering
-        k = i - 1
-        while k >= 0 and seq[k][0] not in ("M", "S", "B"):
-            if seq[k][0] == "A" and k > 0 and seq[k - 1][0] == "S":
-                errs.append("%s: A loads issued before the B-DMA batch of their step" % name)
-            k -= 1
+        # (straight-line only: barrier, A loads, this B batch with nothing else
+        # between -- the prologue's A(0..D-2) -> B(0) -> A(D-1) order is intended)
+        if i >= 2 and seq[i - 1][0] == "A" and seq[i - 2][0] == "S":
+            errs.append("%s: A loads issued before the B-DMA batch of their step" % name)
     if nsteps == 0:
         errs.append("%s: no B-DMA -> A-load step found (pattern changed?)" % name)
     return errs, nsteps
@@ -173,7 +178,7 @@ def main():
     errs = []
     found = 0
     for k, v in funcs.items():
-        if "conv_bf6d_kernel" in k:
+        if "conv_bf6d_kernel" in k or "conv_bf6s_kernel" in k:
             found += 1
             e, n = check_bf6d(k, v)
             # a vmcnt(0) drain is conservative (never wrong) but defeats the
