@@ -73,6 +73,25 @@ __device__ __forceinline__ void pf_split3x4(const f32x4& v, uint2& h, uint2& m, 
   pf_split3_pair(v.z, v.w, h.y, m.y, l.y);
 }
 
+// one v_mfma_f32_32x32x16_bf16 on 8 bf16 per lane of each operand, given as
+// packed dwords (gfuse.hip, up4tap.hip): g6_split turns 8 fp32 into the three
+// planes' operands
+typedef __bf16 g6_bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned g6_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void g6_split(const f32x4& p0, const f32x4& p1, g6_u32x4& h,
+                                         g6_u32x4& m, g6_u32x4& l) {
+  uint2 h0, m0, l0, h1, m1, l1;
+  pf_split3x4(p0, h0, m0, l0);
+  pf_split3x4(p1, h1, m1, l1);
+  h = g6_u32x4{h0.x, h0.y, h1.x, h1.y};
+  m = g6_u32x4{m0.x, m0.y, m1.x, m1.y};
+  l = g6_u32x4{l0.x, l0.y, l1.x, l1.y};
+}
+__device__ __forceinline__ f32x16 g6_mfma(const g6_u32x4& a, const g6_u32x4& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(g6_bf16x8, a),
+                                                 __builtin_bit_cast(g6_bf16x8, b), c, 0, 0, 0);
+}
+
 // value of the x2 bilinear upsample (align_corners=True, F.interpolate as
 // DescNet.py:187 calls it) of an h x w NHWC map at output pixel (oy, ox), 4
 // channels from `base` (= map + image offset + channel offset); sh, sw =

@@ -140,6 +140,11 @@ struct posfeat_model {
   bool tapb = false;  // bf16x6 tap GEMM on pre-split planes (POSFEAT_BF6=2)
   Buf tapwb, tapLb;
   Buf gf_w, gf_b, gf_wp;
+  // the G part computed inside the tap combine (up4tap_gcombine_kernel; the
+  // default with bf16x6 and the tap form, POSFEAT_HEADFUSE=0 off): no G pass
+  // over y, the border ring's G values in their own small buffer
+  bool hfuse = false;
+  Buf gring;
   // convimg's IN statistics from the image's tap moments instead of running
   // convimg (gfuse.hip): the full-res 64-channel map is never computed
   bool imgstats = true;
@@ -629,6 +634,9 @@ void plan(posfeat_model* m) {
     alloc(m->gf_w, B * 128 * 128);
     alloc(m->gf_b, B * 128 + 9 * 64 * 128);  // + the transposed W2 G slice (gfuse.hip)
     alloc(m->gf_wp, pf_gfuse_wplanes_bytes((int)B) / 4 + 4);  // pre-split K = 80 weights
+    const char* e = getenv("POSFEAT_HEADFUSE");
+    m->hfuse = !(e && e[0] == '0') && m->up4tap && pf_conv_precision() >= 1;
+    if (m->hfuse) alloc(m->gring, pf_gfuse_ring_floats((int)B, (int)H, (int)W));
   }
   if (!(m->up4 && m->gfuse) || (m->train && !m->traintap)) m->imgstats = false;
   if (m->traintap) m->imgstats = true;  // the backward contracts the image moments
@@ -779,6 +787,34 @@ int run_layer(Ctx& c, int li, const float* in, int n, int h, int w, int ics, flo
   return POSFEAT_OK;
 }
 
+// the G part of head.conv2 runs inside the tap combine (posfeat_model::hfuse;
+// the precision is read per call, as the conv tiles do)
+bool hfuse_now(const posfeat_model* m) { return m->hfuse && pf_conv_precision() >= 1; }
+
+// head.conv2's G part from the image (gfuse.hip) once convimg's IN statistics
+// and the folded weights exist: into y (c2) by the folded 5x5 conv, or -- the
+// fused head -- only the weight planes and the border ring's values, the
+// interior being computed by pf_up4tap_gcombine
+int gpart(Ctx& c, const float* img4, const float* g64, float* c2) {
+  posfeat_model* m = c.m;
+  const int B = m->B, H = m->H, W = m->W;
+  const size_t SL = (size_t)B * 256;
+  const float* meanI = c.f(m->st_mean) + SL;
+  const float* rstdI = c.f(m->st_rstd) + SL;
+  unsigned short* wp = reinterpret_cast<unsigned short*>(c.f(m->gf_wp));
+  if (hfuse_now(m))
+    return timed(c, "head.conv2.gprep", 0, [&] {
+      return pf_gfuse_prep(img4, g64, 64, B, H, W, c.f(m->gf_w), c.f(m->gf_b), meanI, rstdI,
+                           c.Bi("head.conv2"), c.W("head.convimg"), c.Bi("head.convimg"), wp,
+                           c.f(m->gring), c.st);
+    });
+  return timed(c, "conv:head.conv2.g", 2.0 * B * H * W * 128.0 * 4 * 26, [&] {
+    return pf_gfuse_conv(img4, g64, 64, B, H, W, c.f(m->gf_w), c.f(m->gf_b), meanI, rstdI,
+                         c.W("head.conv2"), c.Bi("head.conv2"), c2, 128, c.st,
+                         c.W("head.convimg"), c.Bi("head.convimg"), wp);
+  });
+}
+
 // KeypointDet's image branch on the side stream (see posfeat_model::side):
 // convimg + IN statistics (DeteNet.py:110-111), the folded G part of
 // head.conv2 into y (gfuse.hip), head.conv2's phase and Winograd weights
@@ -847,12 +883,7 @@ int image_branch(Ctx& c, const float* img4) {
                             s.Bi("head.convimg"), meanI, rstdI, B, s.f(m->gf_w), s.f(m->gf_b),
                             s.st);
   }));
-  PF_TRY(timed(s, "conv:head.conv2.g", 2.0 * B * H * W * 128.0 * 4 * 26, [&] {
-    return pf_gfuse_conv(img4, g64, 64, B, H, W, s.f(m->gf_w), s.f(m->gf_b), meanI, rstdI,
-                         s.W("head.conv2"), s.Bi("head.conv2"), c2, 128, s.st,
-                         s.W("head.convimg"), s.Bi("head.convimg"),
-                         reinterpret_cast<unsigned short*>(s.f(m->gf_wp)));
-  }));
+  PF_TRY(gpart(s, img4, g64, c2));
   if (m->up4wino && !m->up4tap)
     PF_TRY(timed(s, "head.conv2.up4w", 0, [&] {
       return pf_up4_wino_weights(s.f(m->wph), s.f(m->u4u), s.st);
@@ -1022,12 +1053,7 @@ int head_forward(Ctx& c, float* img4, float* local_point, bool side) {
                                 c.Bi("head.convimg"), meanI, rstdI, B, c.f(m->gf_w),
                                 c.f(m->gf_b), c.st);
       }));
-      PF_TRY(timed(c, "conv:head.conv2.g", 2.0 * B * H * W * 128.0 * 4 * 26, [&] {
-        return pf_gfuse_conv(img4, g64, 64, B, H, W, c.f(m->gf_w), c.f(m->gf_b), meanI, rstdI,
-                             c.W("head.conv2"), c.Bi("head.conv2"), c2, 128, c.st,
-                             c.W("head.convimg"), c.Bi("head.convimg"),
-                             reinterpret_cast<unsigned short*>(c.f(m->gf_wp)));
-      }));
+      PF_TRY(gpart(c, img4, g64, c2));
     } else {
       PF_TRY(timed(c, "conv:head.conv2.g", 2.0 * B * H * W * 128.0 * 64 * 9, [&] {
         return pf_up4_gconv(B, H, W, g64, 64, wph, c.Bi("head.conv2"), c2, 128, c.st);
@@ -1067,10 +1093,18 @@ int head_forward(Ctx& c, float* img4, float* local_point, bool side) {
                                        : nullptr,
                              1152LL * 192));
       }
-      PF_TRY(timed(c, "head.conv2.combine", 0, [&] {
-        return pf_up4tap_combine(B, H, W, c.f(m->tapP), c2, 128, c.d(m->tappart), mean, rstd,
-                                 c.st);
-      }));
+      if (hfuse_now(m))
+        PF_TRY(timed(c, "head.conv2.gcombine", 0, [&] {
+          return pf_up4tap_gcombine(B, H, W, c.f(m->tapP), img4,
+                                    reinterpret_cast<const unsigned short*>(c.f(m->gf_wp)),
+                                    c.f(m->gf_b), c.f(m->gring), c2, 128, c.d(m->tappart), mean,
+                                    rstd, c.st);
+        }));
+      else
+        PF_TRY(timed(c, "head.conv2.combine", 0, [&] {
+          return pf_up4tap_combine(B, H, W, c.f(m->tapP), c2, 128, c.d(m->tappart), mean, rstd,
+                                   c.st);
+        }));
     } else {
     PF_TRY(timed(c, "head.conv2.border", 0, [&] {
       return pf_up4_border(B, H, W, c1, 192, wph, c2, 128, c.st);

@@ -84,6 +84,20 @@ int pf_gfuse_conv(const float* img4, const float* c, int ccs, int n, int H, int 
                   unsigned short* wplanes = nullptr);
 // scratch of the pre-split K = 80 weights (gfuse_conv5_k80_kernel)
 size_t pf_gfuse_wplanes_bytes(int n);
+// the fused head (pf_up4tap_gcombine): weight planes + the border ring's G
+// values ring[b][r][128], r in pf_ring_index order
+size_t pf_gfuse_ring_floats(int n, int H, int W);
+int pf_gfuse_prep(const float* img4, const float* c, int ccs, int n, int H, int W,
+                  const float* wc, const float* bc, const float* mean, const float* rstd,
+                  const float* b2, const float* w1_packed, const float* b1,
+                  unsigned short* wplanes, float* ring, hipStream_t st);
+// ring index of border pixel (Y, X) of an H x W image: the top row, the
+// bottom row, then the left and right columns without the corners
+__host__ __device__ inline int pf_ring_index(int Y, int X, int H, int W) {
+  if (Y == 0) return X;
+  if (Y == H - 1) return W + X;
+  return 2 * W + (X == 0 ? 0 : H - 2) + (Y - 1);
+}
 // convimg's instance-norm statistics from the image's tap moments (no conv)
 size_t pf_gfuse_imgstats_ws_bytes(int n, int H);
 int pf_gfuse_imgstats(const float* img4, int n, int H, int W, const float* w1_packed,
@@ -108,6 +122,10 @@ size_t pf_up4tap_part_bytes(int n, int H, int W);
 int pf_up4tap_weights(const float* w2_packed, float* wt, hipStream_t st);
 int pf_up4tap_combine(int n, int H, int W, const float* P, float* y, int ycs, double* part,
                       float* mean, float* rstd, hipStream_t st);
+// the combine with head.conv2's G part computed in the same kernel (no G pass)
+int pf_up4tap_gcombine(int n, int H, int W, const float* P, const float* img4,
+                       const unsigned short* wp, const float* bc, const float* ring, float* y,
+                       int ycs, double* part, float* mean, float* rstd, hipStream_t st);
 // training: D = the combine's adjoint of dy (dL/dP), and the transposed tap
 // weights WtT [192][1152] (dL = D . WtT^T)
 int pf_up4tap_adjoint(int n, int H, int W, const float* dy, int dycs, float* D, hipStream_t st);

@@ -80,13 +80,15 @@ __global__ __launch_bounds__(128) void gfuse_weights_kernel(
 // Border ring: y[p] = b2 + sum_t sum_k W2[:, 192+k, t] G[p+t-1][k], G = rstd (c - mean)
 // inside the image, 0 outside (conv2's zero padding).  One workgroup = RP ring
 // pixels x 128 couts; the G taps go through LDS, W2 (transposed, w2t[t][k][co])
-// is read coalesced across couts and reused for the RP pixels.
+// is read coalesced across couts and reused for the RP pixels.  y == nullptr:
+// into the ring buffer ring[b][r][128] instead (r = the ring index below, the
+// order pf_ring_index in fmap.h restates), for up4tap_gcombine_kernel.
 constexpr int GF_RP = 8;
 __global__ __launch_bounds__(GF_COUT) void gfuse_ring_kernel(
     const float* __restrict__ c, int ccs, const float* __restrict__ img4,
     const float* __restrict__ w1, int k1pad, const float* __restrict__ b1, int H, int W,
     const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ w2t,
-    const float* __restrict__ b2, float* __restrict__ y, int ycs) {
+    const float* __restrict__ b2, float* __restrict__ y, int ycs, float* __restrict__ ring) {
   const int b = blockIdx.y, co = threadIdx.x;
   const int nring = 2 * W + 2 * (H - 2);
   __shared__ float g[GF_RP][9][GF_CG];
@@ -145,6 +147,14 @@ __global__ __launch_bounds__(GF_COUT) void gfuse_ring_kernel(
     const float wv = w2t[(size_t)tk * GF_COUT + co];
 #pragma unroll
     for (int j = 0; j < GF_RP; ++j) acc[j] += wv * (&g[j][0][0])[tk];
+  }
+  if (!y) {
+#pragma unroll
+    for (int j = 0; j < GF_RP; ++j) {
+      const int r = blockIdx.x * GF_RP + j;
+      if (r < nring) ring[((size_t)b * nring + r) * GF_COUT + co] = acc[j];
+    }
+    return;
   }
 #pragma unroll
   for (int j = 0; j < GF_RP; ++j)
@@ -383,22 +393,6 @@ __global__ __launch_bounds__(256) void gfuse_conv5_kernel(const float* __restric
 // matrix-core cycles than the fp32 form.  Weight rows padded to 116 floats
 // (29 16-B slots, odd: conflict-free ds_read_b128).
 constexpr int G6_WP = 116;
-typedef __bf16 g6_bf16x8 __attribute__((ext_vector_type(8)));
-typedef unsigned g6_u32x4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ void g6_split(const f32x4& p0, const f32x4& p1, g6_u32x4& h,
-                                         g6_u32x4& m, g6_u32x4& l) {
-  uint2 h0, m0, l0, h1, m1, l1;
-  pf_split3x4(p0, h0, m0, l0);
-  pf_split3x4(p1, h1, m1, l1);
-  h = g6_u32x4{h0.x, h0.y, h1.x, h1.y};
-  m = g6_u32x4{m0.x, m0.y, m1.x, m1.y};
-  l = g6_u32x4{l0.x, l0.y, l1.x, l1.y};
-}
-__device__ __forceinline__ f32x16 g6_mfma(const g6_u32x4& a, const g6_u32x4& b, const f32x16& c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(g6_bf16x8, a),
-                                                 __builtin_bit_cast(g6_bf16x8, b), c, 0, 0, 0);
-}
 
 __global__ __launch_bounds__(256) void gfuse_conv5_bf6_kernel(const float* __restrict__ img4,
                                                               int H, int W,
@@ -714,7 +708,31 @@ int pf_gfuse_conv(const float* img4, const float* c, int ccs, int n, int H, int 
   const int nring = 2 * W + 2 * (H - 2);
   hipLaunchKernelGGL(gfuse_ring_kernel, dim3((nring + GF_RP - 1) / GF_RP, n), dim3(GF_COUT), 0, st,
                      c, ccs, img4, w1_packed, k1pad, b1, H, W, mean, rstd,
-                     bc + (size_t)n * GF_COUT, b2, y, ycs);
+                     bc + (size_t)n * GF_COUT, b2, y, ycs, nullptr);
+  PF_CHECK_LAUNCH();
+  return POSFEAT_OK;
+}
+
+size_t pf_gfuse_ring_floats(int n, int H, int W) {
+  return (size_t)n * (2 * W + 2 * (H - 2)) * GF_COUT;
+}
+
+// Everything of the G part but the interior conv itself, which
+// up4tap_gcombine_kernel runs on the fly: the pre-split K = 80 weight planes
+// and the exact border-ring values (ring, pf_gfuse_ring_floats).
+int pf_gfuse_prep(const float* img4, const float* c, int ccs, int n, int H, int W,
+                  const float* wc, const float* bc, const float* mean, const float* rstd,
+                  const float* b2, const float* w1_packed, const float* b1,
+                  unsigned short* wplanes, float* ring, hipStream_t st) {
+  if (!c && !(w1_packed && b1)) return POSFEAT_E_INVALID;
+  if (n <= 0 || H < 2 || W < 2 || !wplanes || !ring) return POSFEAT_E_INVALID;
+  const int tot = n * GF_COUT * G8_K;
+  hipLaunchKernelGGL(gfuse_wsplit_kernel, dim3((tot + 255) / 256), dim3(256), 0, st, wc, n,
+                     wplanes);
+  const int nring = 2 * W + 2 * (H - 2);
+  hipLaunchKernelGGL(gfuse_ring_kernel, dim3((nring + GF_RP - 1) / GF_RP, n), dim3(GF_COUT), 0, st,
+                     c, ccs, img4, w1_packed, posfeat_conv_packed_k(3, 3, 3), b1, H, W, mean, rstd,
+                     bc + (size_t)n * GF_COUT, b2, nullptr, 0, ring);
   PF_CHECK_LAUNCH();
   return POSFEAT_OK;
 }

@@ -211,6 +211,244 @@ __global__ __launch_bounds__(256) void up4tap_combine_kernel(const float* __rest
   }
 }
 
+// ---- the combine with head.conv2's G part computed in place -----------------
+// up4tap_combine_kernel above adds the upsampled part to y = G part + bias,
+// which gfuse_conv5_k80_kernel wrote beforehand: y crosses HBM three times
+// (write, read, write; 3 x 5 GB at B = 32, 480 x 640).  Here the same block
+// (image, 16 output rows, 32 output columns, 32 channels) first computes its G
+// part -- the per-image folded 5x5 conv of the image (gfuse.hip), K = 80
+// bf16x6 over pre-split weight planes -- while its P tile streams into LDS,
+// then adds the tap-summed interpolation and writes y once, with the IN
+// statistics.  The MFMA roles are swapped against the k80 kernel (A = pixels,
+// B = couts), with the 32 M rows of a tile mapped to 16 rows x 2 columns:
+// acc[r] of lane (cout n, half h) is then output row r of column 2p + h, i.e.
+// a lane holds one channel of one output column over all 16 rows -- exactly
+// the combine's per-thread sliding-window layout (one channel instead of a
+// quad), so the accumulators become the combine's running sums with no LDS
+// transpose.  Border-ring pixels take their G value from the ring buffer
+// (pf_gfuse_prep: conv2 sees G's zero padding there, not the fold).
+constexpr int GC_PR = 20, GC_PC = 36;  // image patch rows / pixels (16 x 32 + the 5x5 halo)
+constexpr int GC_PP = 38;              // LDS pixel slots per patch row (conflict-free b128 A reads)
+constexpr int GC_PDMA = 12;            // patch DMA instructions (64 slots each, >= 20 x 38)
+constexpr int GC_K = 80;               // k = dy * 16 + dx * 3 + c, k % 16 == 15: zero weight
+constexpr int GC_DMA = CB_SEGP / 8 / 4;  // P-tile DMA instructions per wave
+static_assert(CB_SEGP % 32 == 0, "P-tile DMA instructions split evenly over the 4 waves");
+static_assert(GC_PDMA % 4 == 0 && GC_PDMA * 64 >= GC_PR * GC_PP, "patch DMA covers the patch");
+__device__ float gc_zero4[4];  // the DMA source of patch pixels outside the image
+
+// wait until at most N vector-memory operations of this wave are outstanding
+template <int N>
+__device__ __forceinline__ void gc_wait_vmcnt() {
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+__global__ __launch_bounds__(256, 2) void up4tap_gcombine_kernel(
+    const float* __restrict__ P, int h, int w, const float* __restrict__ img4,
+    const unsigned short* __restrict__ wp, const float* __restrict__ bc,
+    const float* __restrict__ ring, float* __restrict__ y, int ycs, double* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) float sp[CB_SEGP * CB_CG];
+  __shared__ __attribute__((aligned(16))) float spat[GC_PDMA * 64 * 4];  // [row][38 slots][4]
+  const int H = 4 * h, W = 4 * w;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hl = lane >> 5, ln = lane & 31;
+  const int nxb = (w + CB_QX - 1) / CB_QX, nqb = h / TQ, ncg = TAP_CO / CB_CG;
+  // XCD-aware order: blocks are dealt round-robin over the 8 XCDs, so block i
+  // takes tile (i % 8) * (n / 8) + i / 8 -- neighbouring tiles, which share P
+  // halo columns, run on one XCD's L2
+  int id = blockIdx.x;
+  if ((gridDim.x & 7) == 0) id = (id & 7) * (gridDim.x >> 3) + (id >> 3);
+  const int cg = id % ncg;
+  id /= ncg;
+  const int xb = id % nxb;
+  id /= nxb;
+  const int qb = id % nqb, b = id / nqb;
+  const int q0 = qb * TQ, qx0 = xb * CB_QX, Y0 = 4 * q0, X0 = 4 * qx0;
+  // ---- loads, in this order: the B operands (this channel group's weight
+  // planes) into registers, then the image patch and the P tile by DMA.  The
+  // MFMA phase waits for all but the P tile's 17 instructions --------------
+  const int co = cg * CB_CG + ln;
+  const float bias = bc[(long long)b * TAP_CO + co];
+  g6_u32x4 wv[5][3];
+  {
+    const unsigned short* wb = wp + (long long)b * 3 * TAP_CO * GC_K + (long long)co * GC_K + 8 * hl;
+#pragma unroll
+    for (int dy = 0; dy < 5; ++dy)
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        wv[dy][pl] = *reinterpret_cast<const g6_u32x4*>(wb + (long long)pl * TAP_CO * GC_K + dy * 16);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  const float* ib = img4 + (long long)b * H * W * 4;
+#pragma unroll
+  for (int jj = 0; jj < GC_PDMA / 4; ++jj) {  // slot s -> patch pixel (s / 38, s % 38)
+    const int j = wave + 4 * jj, s = j * 64 + lane;
+    const int py = s / GC_PP, px = s - py * GC_PP;
+    const int yy = Y0 - 2 + py, xx = X0 - 2 + px;
+    const bool ok = py < GC_PR && px < GC_PC && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
+    const float* src = ok ? ib + ((long long)yy * W + xx) * 4 : gc_zero4;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)(spat + j * 64 * 4),
+                                     16, 0, 0);
+  }
+  const float* Pb = P + (long long)b * h * w * TAP_N + cg * CB_CG;
+#pragma unroll
+  for (int jj = 0; jj < GC_DMA; ++jj) {  // as up4tap_combine_kernel's phase 1
+    const int j = wave + 4 * jj;
+    int seg = j * 8 + (lane >> 3);
+    seg = min(seg, CB_SEG - 1);
+    const int k = seg % 9, cell = seg / 9;
+    const int cx = cell % CB_CX, ry = cell / CB_CX;
+    const int iy = min(max(q0 - 1 + ry, 0), h - 1), ix = min(max(qx0 - 1 + cx, 0), w - 1);
+    const float* src = Pb + ((long long)iy * w + ix) * TAP_N + k * TAP_CO + (lane & 7) * 4;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)(sp + j * 8 * CB_CG),
+                                     16, 0, 0);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  gc_wait_vmcnt<GC_DMA>();        // weights + this wave's patch DMA have landed
+  asm volatile("" ::: "memory");  // no LDS access moves across the barrier
+  __builtin_amdgcn_s_barrier();   // ... and every wave's (no fence: it would drain the P tile)
+  asm volatile("" ::: "memory");
+  // ---- G part: wave = 4 column pairs p = 4 wave + t; A row m = pixel (row
+  // (m & 3) + 4 (m >> 3), column 2p + ((m >> 2) & 1)), k half hl: the 8 taps
+  // k = 8 hl .. 8 hl + 7 of row dy are channels of the three pixels from
+  // column 2p + (m's column) + 2 hl on -- (c0 c1 c2 | c0 c1 c2 | c0 c1) for
+  // hl = 0, (c2 | c0 c1 c2 | c0 c1 c2 | 0) for hl = 1 (k = 15: zero weight)
+  const int arow = (ln & 3) + 4 * (ln >> 3), acol = (ln >> 2) & 1;
+  f32x16 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+#pragma unroll
+  for (int dy = 0; dy < 5; ++dy) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const f32x4* pr = reinterpret_cast<const f32x4*>(spat) + (arow + dy) * GC_PP +
+                        2 * (4 * wave + t) + acol + 2 * hl;
+      const f32x4 a = pr[0], bq = pr[1], cq = pr[2];
+      f32x4 p0, p1;
+      p0[0] = hl ? a.z : a.x;
+      p0[1] = hl ? bq.x : a.y;
+      p0[2] = hl ? bq.y : a.z;
+      p0[3] = hl ? bq.z : bq.x;
+      p1[0] = hl ? cq.x : bq.y;
+      p1[1] = hl ? cq.y : bq.z;
+      p1[2] = hl ? cq.z : cq.x;
+      p1[3] = hl ? 0.f : cq.y;
+      g6_u32x4 ph, pm, plo;
+      g6_split(p0, p1, ph, pm, plo);
+      // the k80 kernel's six products in its order, operands swapped
+      f32x16 c = acc[t];
+      c = g6_mfma(ph, wv[dy][0], c);
+      c = g6_mfma(pm, wv[dy][0], c);
+      c = g6_mfma(ph, wv[dy][1], c);
+      c = g6_mfma(plo, wv[dy][0], c);
+      c = g6_mfma(ph, wv[dy][2], c);
+      c = g6_mfma(pm, wv[dy][1], c);
+      acc[t] = c;
+    }
+  }
+  const int nring = 2 * W + 2 * (H - 2);
+  const float* rb = ring + (long long)b * nring * TAP_CO + co;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int X = X0 + 2 * (4 * wave + t) + hl;
+    const bool edge_x = X == 0 || X == W - 1;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int Y = Y0 + r;
+      acc[t][r] = (edge_x || Y == 0 || Y == H - 1) && X < W
+                      ? rb[(long long)pf_ring_index(Y, X, H, W) * TAP_CO]
+                      : acc[t][r] + bias;
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA has landed
+  __syncthreads();                 // ... and every other wave's
+  // ---- the upsampled part: per column, the sliding window of
+  // up4tap_combine_kernel on one channel ---------------------------------------
+  double s1 = 0.0, s2 = 0.0;
+  const long long yrow = (long long)W * ycs;
+  float* yb = y + (long long)b * H * W * ycs + co;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int X = X0 + 2 * (4 * wave + t) + hl, qx = X >> 2, rx = X & 3;
+    const bool xok = X < W;
+    int cola[3], colb[3];
+    float wxa[3], wxb[3];
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      int lo;
+      up4_w(rx + kx - 1, lo, wxa[kx], wxb[kx]);
+      const int u = X + kx - 1;
+      if (u < 0 || u >= W) wxa[kx] = wxb[kx] = 0.f;
+      cola[kx] = min(max(min(qx + lo, w - 1), 0) - (qx0 - 1), CB_CX - 1);
+      colb[kx] = min(max(min(qx + lo + 1, w - 1), 0) - (qx0 - 1), CB_CX - 1);
+    }
+    auto rowR = [&](int ry, float (&R)[3]) {
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky) {
+        float s = 0.f;
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          const int k = ky * 3 + kx;
+          const float pa = sp[((ry * CB_CX + cola[kx]) * 9 + k) * CB_CG + ln];
+          const float pb = sp[((ry * CB_CX + colb[kx]) * 9 + k) * CB_CG + ln];
+          s += wxa[kx] * pa + wxb[kx] * pb;
+        }
+        R[ky] = s;
+      }
+    };
+    float Rm[3], R0[3], Rp[3];
+    rowR(0, Rm);
+    rowR(1, R0);
+#pragma unroll
+    for (int i = 0; i < TQ; ++i) {
+      rowR(i + 2, Rp);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int Y = Y0 + 4 * i + r;
+        float o = acc[t][4 * i + r];
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+          const int v = Y + ky - 1;
+          int lo;
+          float wa, wb;
+          up4_w(r + ky - 1, lo, wa, wb);
+          if (v < 0 || v >= H) wa = wb = 0.f;
+          if (lo < 0)
+            o += wa * Rm[ky] + wb * R0[ky];
+          else
+            o += wa * R0[ky] + wb * Rp[ky];
+        }
+        if (!xok) continue;
+        yb[Y * yrow + (long long)X * ycs] = o;
+        s1 += (double)o;
+        s2 += (double)o * (double)o;
+      }
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky) {
+        Rm[ky] = R0[ky];
+        R0[ky] = Rp[ky];
+      }
+    }
+  }
+  if (!part) return;
+  // ---- statistics: the block's 32 columns of each channel, fixed order ------
+  __syncthreads();  // LDS reuse
+  double* red = reinterpret_cast<double*>(sp);  // [wave][half][32 channels][2]
+  red[((wave * 2 + hl) * CB_CG + ln) * 2] = s1;
+  red[((wave * 2 + hl) * CB_CG + ln) * 2 + 1] = s2;
+  __syncthreads();
+  if (tid < 2 * CB_CG) {
+    const int c = tid >> 1, which = tid & 1;
+    double a = 0.0;
+    for (int x = 0; x < 8; ++x) a += red[(x * CB_CG + c) * 2 + which];
+    const long long chunk = (long long)qb * nxb + xb;
+    const long long nchunk = (long long)nxb * nqb;
+    part[(((long long)b * nchunk + chunk) * TAP_CO + cg * CB_CG + c) * 2 + which] = a;
+  }
+}
+
 // ---- adjoint (keypoint-head training, config 5) ------------------------------
 // weight with which low-res index i feeds full-res coordinate u of an n -> 4n
 // bilinear upsample (align_corners=False): u's two clamped source taps
@@ -336,6 +574,25 @@ int pf_up4tap_combine(int n, int H, int W, const float* P, float* y, int ycs, do
   const int nchunk = (h / TQ) * ((w + CB_QX - 1) / CB_QX);
   hipLaunchKernelGGL(up4tap_combine_kernel, dim3(n * nchunk * (TAP_CO / CB_CG)), dim3(256), 0, st,
                      P, h, w, y, ycs, mean ? part : nullptr);
+  PF_CHECK_LAUNCH();
+  if (mean) PF_TRY(pf_in_finalize(part, n, nchunk, H * W, TAP_CO, mean, rstd, st));
+  return POSFEAT_OK;
+}
+
+// y (n x H x W x 128, pitch ycs) = head.conv2's full output: the G part from
+// the image (img4, pitch 4) with the pre-split weight planes wp and biases bc
+// of pf_gfuse_weights / pf_gfuse_prep, the border ring from `ring`, plus the
+// upsampled part from P; mean/rstd (optional) its instance-norm statistics.
+// The same part layout as pf_up4tap_combine.  H, W % 16 == 0.
+int pf_up4tap_gcombine(int n, int H, int W, const float* P, const float* img4,
+                       const unsigned short* wp, const float* bc, const float* ring, float* y,
+                       int ycs, double* part, float* mean, float* rstd, hipStream_t st) {
+  const int h = H / 4, w = W / 4;
+  if (H % 16 || W % 16 || ycs % 4 || ycs < TAP_CO || n <= 0) return POSFEAT_E_INVALID;
+  if (!P || !img4 || !wp || !bc || !ring || !y || (mean && !part)) return POSFEAT_E_INVALID;
+  const int nchunk = (h / TQ) * ((w + CB_QX - 1) / CB_QX);
+  hipLaunchKernelGGL(up4tap_gcombine_kernel, dim3(n * nchunk * (TAP_CO / CB_CG)), dim3(256), 0, st,
+                     P, h, w, img4, wp, bc, ring, y, ycs, mean ? part : nullptr);
   PF_CHECK_LAUNCH();
   if (mean) PF_TRY(pf_in_finalize(part, n, nchunk, H * W, TAP_CO, mean, rstd, st));
   return POSFEAT_OK;

@@ -170,6 +170,35 @@ def test_env_switch_paths_match_default(gpu, switch, exact, monkeypatch):
     alt.close()
 
 
+@pytest.mark.parametrize("B,hw", [(2, (96, 128)), (2, (112, 144)), (1, (112, 144))])
+def test_fused_head_matches_unfused(gpu, B, hw, monkeypatch):
+    """POSFEAT_HEADFUSE: head.conv2's G part inside the tap combine
+    (up4tap_gcombine_kernel, the default) against the G pass + combine
+    (gfuse_conv5_k80_kernel + up4tap_combine_kernel): the same products, so
+    local_point within 1e-4 of the map scale -- including a ragged last column
+    block (W = 144: 16 of the block's 32 columns), the border ring and both
+    block orders (the XCD remap applies when the grid is a multiple of 8:
+    B = 2 here; B = 1 at 112 x 144 is 140 blocks)."""
+    from posfeat_amd.weights import seeded_image
+    H, W = hw
+    imgs = torch.from_numpy(np.stack([seeded_image(s, H, W) for s in range(3, 3 + B)])).to(gpu)
+    base = _new_engine(gpu)
+    base.run(imgs)
+    ref = {k: v.clone() for k, v in base.run(imgs).items() if not k.startswith("_")}
+    monkeypatch.setenv("POSFEAT_HEADFUSE", "0")
+    alt = _new_engine(gpu)
+    alt.run(imgs)
+    got = alt.run(imgs)
+    e, s = _maxerr(got["local_point"], ref["local_point"])
+    assert e <= TOL * s, "HEADFUSE=0: local_point err %g" % e
+    assert torch.equal(got["local_map"], ref["local_map"])   # the backbone is untouched
+    o = _oracle(imgs[:1].cpu())
+    e, s = _maxerr(ref["local_point"][:1], o["local_point"])
+    assert e <= TOL * s, "fused head vs oracle err %g" % e
+    base.close()
+    alt.close()
+
+
 def test_engine_shape_cache_lru_and_shared_workspace(gpu, monkeypatch):
     """Many image sizes (HPatches / Aachen): at most POSFEAT_ENGINE_MAX_SHAPES
     instances are kept (least recently used evicted), inference instances
