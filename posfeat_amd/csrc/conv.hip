@@ -87,7 +87,12 @@ struct ConvArgs {
 // `rowm(row)` maps a tile row to its output pixel m (or -1: outside); img0 is
 // the image of the tile's first row (stats slot 0).
 // `resp(row, m)` returns the residual row (channels n0..) or nullptr.
-template <int BM, int BN, int WM, int WN, class RowMap, class ResMap>
+// SL > 1: the tile is staged in SL row slices of BM / SL rows (the waves of one
+// slice write, every thread stores, barrier, next slice), so T needs only
+// BM / SL rows of LDS -- the pre-split GEMM tiles use SL = 2 to keep their LDS
+// at the B ring's 48 KB (three blocks per CU instead of two).  Same values,
+// same stores: bit-identical to SL = 1.
+template <int BM, int BN, int WM, int WN, int SL = 1, class RowMap, class ResMap>
 __device__ __forceinline__ void conv_epilogue(const ConvArgs& a,
                                               f32x16 (&acc)[BM / WM / 32][BN / WN / 32],
                                               float* smem, int tm, int n0, int split,
@@ -95,79 +100,89 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a,
   constexpr int THREADS = WM * WN * 64;
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int MI = TM / 32, NI = TN / 32;
+  static_assert(SL == 1 || (WN == 1 && WM % SL == 0), "row slices need whole waves");
+  constexpr int SR = BM / SL;  // rows per slice
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
   constexpr int TP = BN + 4;
   float* T = smem;  // the K loop ended with a barrier: staging LDS is free
-#pragma unroll
-  for (int mi = 0; mi < MI; ++mi)
-#pragma unroll
-    for (int ni = 0; ni < NI; ++ni)
-#pragma unroll
-      for (int r = 0; r < 16; ++r)
-        T[(wm * TM + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * TP + wn * TN + ni * 32 +
-          (lane & 31)] = acc[mi][ni][r];
-  __syncthreads();
   constexpr int C4 = BN / 4;
   constexpr int RPP = THREADS / C4;  // rows per pass
-  constexpr int NP = BM / RPP;
+  constexpr int NP = SR / RPP;       // passes per slice
   const int q = tid % C4, r0 = tid / C4;
   const int col = n0 + 4 * q;
   const bool colok = col < a.Cout;
-  if (a.ksplit > 1) {  // raw partial sums; conv_splitk_reduce finishes
-    float* pp = a.part + (size_t)split * a.M * a.Cout;
+  const f32x4 bv = (a.ksplit <= 1 && a.bias && colok)
+                       ? *reinterpret_cast<const f32x4*>(a.bias + col)
+                       : f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 s1[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}}, s2[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+#pragma unroll
+  for (int s = 0; s < SL; ++s) {
+    if (s > 0) __syncthreads();  // the previous slice's rows are read
+    if (SL == 1 || wm * TM / SR == s) {
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            T[(wm * TM - s * SR + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * TP +
+              wn * TN + ni * 32 + (lane & 31)] = acc[mi][ni][r];
+    }
+    __syncthreads();
+    if (a.ksplit > 1) {  // raw partial sums; conv_splitk_reduce finishes
+      float* pp = a.part + (size_t)split * a.M * a.Cout;
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+        const int row = r0 + p * RPP;
+        const int m = rowm(s * SR + row);
+        if (colok && m >= 0)
+          *reinterpret_cast<f32x4*>(pp + (size_t)m * a.Cout + col) =
+              *reinterpret_cast<const f32x4*>(T + row * TP + 4 * q);
+      }
+      continue;
+    }
+    f32x4 rv[NP];
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const int row = s * SR + r0 + p * RPP;
+      const int m = rowm(row);
+      const float* rp = (colok && m >= 0) ? resp(row, m) : nullptr;
+      rv[p] = rp ? *reinterpret_cast<const f32x4*>(rp + col) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
       const int row = r0 + p * RPP;
-      const int m = rowm(row);
-      if (colok && m >= 0)
-        *reinterpret_cast<f32x4*>(pp + (size_t)m * a.Cout + col) =
-            *reinterpret_cast<const f32x4*>(T + row * TP + 4 * q);
-    }
-    return;
-  }
-  f32x4 rv[NP];
-#pragma unroll
-  for (int p = 0; p < NP; ++p) {
-    const int row = r0 + p * RPP;
-    const int m = rowm(row);
-    const float* rp = (colok && m >= 0) ? resp(row, m) : nullptr;
-    rv[p] = rp ? *reinterpret_cast<const f32x4*>(rp + col) : f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-  const f32x4 bv = (a.bias && colok) ? *reinterpret_cast<const f32x4*>(a.bias + col)
-                                     : f32x4{0.f, 0.f, 0.f, 0.f};
-  f32x4 s1[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}}, s2[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
-#pragma unroll
-  for (int p = 0; p < NP; ++p) {
-    const int row = r0 + p * RPP;
-    const int m = rowm(row);
-    if (!colok || m < 0) continue;
-    f32x4 v = *reinterpret_cast<const f32x4*>(T + row * TP + 4 * q) + bv + rv[p];
-    if (a.act == POSFEAT_ACT_RELU) {
-      v.x = fmaxf(v.x, 0.f);
-      v.y = fmaxf(v.y, 0.f);
-      v.z = fmaxf(v.z, 0.f);
-      v.w = fmaxf(v.w, 0.f);
-    } else if (a.act == POSFEAT_ACT_ELU) {
-      v.x = pf_elu(v.x);
-      v.y = pf_elu(v.y);
-      v.z = pf_elu(v.z);
-      v.w = pf_elu(v.w);
-    }
-    *reinterpret_cast<f32x4*>(a.y + (size_t)m * a.ycs + col) = v;
-    if (a.stats) {
-      const int sl = (m / a.hw) != img0;
-      if (sl) {
-        s1[1] += v;
-        s2[1] += v * v;
-      } else {
-        s1[0] += v;
-        s2[0] += v * v;
+      const int m = rowm(s * SR + row);
+      if (!colok || m < 0) continue;
+      f32x4 v = *reinterpret_cast<const f32x4*>(T + row * TP + 4 * q) + bv + rv[p];
+      if (a.act == POSFEAT_ACT_RELU) {
+        v.x = fmaxf(v.x, 0.f);
+        v.y = fmaxf(v.y, 0.f);
+        v.z = fmaxf(v.z, 0.f);
+        v.w = fmaxf(v.w, 0.f);
+      } else if (a.act == POSFEAT_ACT_ELU) {
+        v.x = pf_elu(v.x);
+        v.y = pf_elu(v.y);
+        v.z = pf_elu(v.z);
+        v.w = pf_elu(v.w);
+      }
+      *reinterpret_cast<f32x4*>(a.y + (size_t)m * a.ycs + col) = v;
+      if (a.stats) {
+        const int sl = (m / a.hw) != img0;
+        if (sl) {
+          s1[1] += v;
+          s2[1] += v * v;
+        } else {
+          s1[0] += v;
+          s2[0] += v * v;
+        }
       }
     }
   }
+  if (a.ksplit > 1) return;
   if (a.stats) {  // reduce the RPP row groups of each column in a fixed order
     __syncthreads();
     float* R = smem;  // [RPP][2 slots][BN][2]
@@ -979,7 +994,10 @@ void conv_bf6d_kernel(ConvArgs a) {
   static_assert(MI == 1 && B_G >= 1 && (3 * BN / 16) % NW == 0 && D >= 2 && D <= 4, "tile");
   constexpr int BSTAGE = 3 * BN * BK / 2;  // floats (u16 pairs)
   constexpr int RING = 2 * BSTAGE;
-  constexpr int EPI = BM * (BN + 4);
+  // the epilogue stages the tile in SL row slices so it fits in the ring's LDS
+  constexpr int SL = BM * (BN + 4) <= RING ? 1 : BM / 2 * (BN + 4) <= RING ? 2 : 4;
+  static_assert(WM % SL == 0, "epilogue slices");
+  constexpr int EPI = BM / SL * (BN + 4);
   __shared__ __attribute__((aligned(16))) float smem[RING > EPI ? RING : EPI];
   unsigned short* const Bs = reinterpret_cast<unsigned short*>(smem);
 
@@ -1154,7 +1172,7 @@ void conv_bf6d_kernel(ConvArgs a) {
   f32x16 accm[1][NI];
 #pragma unroll
   for (int ni = 0; ni < NI; ++ni) accm[0][ni] = acc[ni];
-  conv_epilogue<BM, BN, WM, WN>(
+  conv_epilogue<BM, BN, WM, WN, SL>(
       a, accm, smem, tm, n0, split, [&](int row) { return m0 + row < a.M ? m0 + row : -1; },
       m0 / a.hw,
       [&](int, int m) { return a.res ? a.res + (size_t)m * a.rcs : (const float*)nullptr; });
@@ -1181,7 +1199,10 @@ void conv_bf6s_kernel(ConvArgs a) {
   static_assert(MI == 1 && B_G >= 1 && (3 * BN / 16) % NW == 0 && D >= 2 && D <= 3, "tile");
   constexpr int BSTAGE = 3 * BN * BK / 2;  // floats (u16 pairs)
   constexpr int RING = 2 * BSTAGE;
-  constexpr int EPI = BM * (BN + 4);
+  // the epilogue stages the tile in SL row slices so it fits in the ring's LDS
+  constexpr int SL = BM * (BN + 4) <= RING ? 1 : BM / 2 * (BN + 4) <= RING ? 2 : 4;
+  static_assert(WM % SL == 0, "epilogue slices");
+  constexpr int EPI = BM / SL * (BN + 4);
   __shared__ __attribute__((aligned(16))) float smem[RING > EPI ? RING : EPI];
   unsigned short* const Bs = reinterpret_cast<unsigned short*>(smem);
 
@@ -1304,7 +1325,7 @@ void conv_bf6s_kernel(ConvArgs a) {
   f32x16 accm[1][NI];
 #pragma unroll
   for (int ni = 0; ni < NI; ++ni) accm[0][ni] = acc[ni];
-  conv_epilogue<BM, BN, WM, WN>(
+  conv_epilogue<BM, BN, WM, WN, SL>(
       a, accm, smem, tm, n0, split, [&](int row) { return m0 + row < a.M ? m0 + row : -1; },
       m0 / a.hw,
       [&](int, int m) { return a.res ? a.res + (size_t)m * a.rcs : (const float*)nullptr; });

@@ -8,7 +8,7 @@ for i in $(seq 1 $pairs); do
   for arm in A B; do
     [ $arm = A ] && e=$A || e=$B
     env $e timeout -k 10 300 python bench.py --no-cpu-baseline "$@" > $o/bench_${arm}$i.json 2> $o/bench_${arm}$i.err || exit 100
-    grep -o '"value": [0-9.]*' $o/bench_${arm}$i.json | head -1 | sed "s/^/$arm$i ($e) /"
+    grep -o '"value": [0-9.]*' $o/bench_${arm}$i.json | head -1 | sed "s#^#$arm$i ($e) #"
   done
 done
 for arm in A B; do
