@@ -49,12 +49,11 @@ HEAD_CONV2_FLOP_PER_IMAGE = 2.0 * 480 * 640 * 128 * 256 * 9   # reference layer
 # the 1x1 / strided / halo convs, the stem).  The engine's timing events carry
 # the FLOPs each launch executes.
 GEMM_LABEL_KERNELS = {
-    ".wino": "conv_bf6d_kernel<128,128,2> x36 batched (Winograd F(4x4) transform-domain "
-             "GEMMs of %s; bf16x6 on pre-split U planes, A prefetched 2 chunks ahead in "
-             "registers)",
-    "up4tap": "conv_bf6d_kernel<128,128,2> or its autotuned bit-identical twin (head.conv2's 192 "
-              "x4-upsampled channels: nine 1x1 convs on the 120x160 grid as one [B*19200 x 192] "
-              "x [192 x 1152] GEMM)",
+    ".wino": "conv_bf6x_kernel<128> x36 batched (Winograd F(4x4) transform-domain GEMMs of "
+             "%s; bf16x6 on pre-split U planes, v_mfma_f32_16x16x32_bf16, memory instructions "
+             "interleaved among the MFMAs)",
+    "up4tap": "conv_bf6x_kernel<128> (head.conv2's 192 x4-upsampled channels: nine 1x1 convs "
+              "on the 120x160 grid as one [B*19200 x 192] x [192 x 1152] GEMM)",
     "": "the autotuned conv tile of %s (conv.hip MFMA implicit GEMM)",
 }
 # conv labels whose kernels keep fp32-input MFMA in every precision mode (the
@@ -73,7 +72,7 @@ def conv_arithmetic():
     mode = lib().posfeat_set_conv_precision(-1)
     if mode >= 1:
         return {"arithmetic": "bf16x6: fp32 operands split exactly into 3 bf16 terms, 6 products "
-                              "per fp32 product on v_mfma_f32_32x32x16_bf16, fp32 accumulate "
+                              "per fp32 product on the bf16 MFMAs (16x16x32 dense GEMMs, 32x32x16 other convs), fp32 accumulate "
                               "(per-product error < one fp32 rounding)",
                 "method_peak": round(PEAK_BF16_MFMA_TFLOPS / 6, 1)}
     return {"arithmetic": "fp32-input MFMA v_mfma_f32_32x32x2_f32", "method_peak":

@@ -90,6 +90,16 @@ size_t posfeat_conv2d_workspace(const posfeat_conv_desc *d);
 int posfeat_conv2d_nhwc_ws(const posfeat_conv_desc *d, const float *x, const float *w,
                            const float *bias, const float *res, float *y, void *ws,
                            size_t ws_bytes, void *stream);
+/* Same as posfeat_conv2d_nhwc_ws with the weights ALSO given as their three
+ * bf16 planes (h, m, l of the packed [cout][Kpad] array, plane stride wplane
+ * elements; h = RNE_bf16(w), m = RNE_bf16(w - h), l = RNE_bf16(w - h - m)),
+ * as the engine passes them: the pre-split tiles run (dense 1x1 convs: the
+ * 16x16x32 conv_bf6x_kernel; others: conv_bf6d_kernel).  Replaces the same
+ * reference convs as posfeat_conv2d_nhwc (networks/DescNet.py:167-190). */
+int posfeat_conv2d_nhwc_planes(const posfeat_conv_desc *d, const float *x, const float *w,
+                               const unsigned short *wb, long long wplane, const float *bias,
+                               const float *res, float *y, void *ws, size_t ws_bytes,
+                               void *stream);
 /* Conv (no residual, no activation) whose epilogue also reduces per-tile
  * channel sums for InstanceNorm2d (networks/DeteNet.py:12-22): writes y and
  * mean/rstd [n][cout] of y over each image (biased var, rstd=1/sqrt(var+eps)).

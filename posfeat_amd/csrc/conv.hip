@@ -92,20 +92,16 @@ struct ConvArgs {
 // BM / SL rows of LDS -- the pre-split GEMM tiles use SL = 2 to keep their LDS
 // at the B ring's 48 KB (three blocks per CU instead of two).  Same values,
 // same stores: bit-identical to SL = 1.
-template <int BM, int BN, int WM, int WN, int SL = 1, class RowMap, class ResMap>
-__device__ __forceinline__ void conv_epilogue(const ConvArgs& a,
-                                              f32x16 (&acc)[BM / WM / 32][BN / WN / 32],
-                                              float* smem, int tm, int n0, int split,
-                                              RowMap rowm, int img0, ResMap resp) {
-  constexpr int THREADS = WM * WN * 64;
-  constexpr int TM = BM / WM, TN = BN / WN;
-  constexpr int MI = TM / 32, NI = TN / 32;
-  static_assert(SL == 1 || (WN == 1 && WM % SL == 0), "row slices need whole waves");
+// conv_epilogue_t: the same with the staging of slice s into T (row pitch
+// BN + 4, rows s * BM / SL ..) left to `stage(T, s)` -- the accumulator layout
+// of the MFMA shape the kernel ran (conv_epilogue below: 32x32 blocks;
+// conv_bf6x_kernel: 16x16 blocks).
+template <int BM, int BN, int THREADS, int SL, class RowMap, class ResMap, class Stage>
+__device__ __forceinline__ void conv_epilogue_t(const ConvArgs& a, float* smem, int tm, int n0,
+                                                int split, RowMap rowm, int img0, ResMap resp,
+                                                Stage&& stage) {
   constexpr int SR = BM / SL;  // rows per slice
   const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int wm = wave / WN, wn = wave % WN;
   constexpr int TP = BN + 4;
   float* T = smem;  // the K loop ended with a barrier: staging LDS is free
   constexpr int C4 = BN / 4;
@@ -121,16 +117,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a,
 #pragma unroll
   for (int s = 0; s < SL; ++s) {
     if (s > 0) __syncthreads();  // the previous slice's rows are read
-    if (SL == 1 || wm * TM / SR == s) {
-#pragma unroll
-      for (int mi = 0; mi < MI; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < NI; ++ni)
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            T[(wm * TM - s * SR + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * TP +
-              wn * TN + ni * 32 + (lane & 31)] = acc[mi][ni][r];
-    }
+    stage(T, s);
     __syncthreads();
     if (a.ksplit > 1) {  // raw partial sums; conv_splitk_reduce finishes
       float* pp = a.part + (size_t)split * a.M * a.Cout;
@@ -209,6 +196,32 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a,
   }
 }
 
+template <int BM, int BN, int WM, int WN, int SL = 1, class RowMap, class ResMap>
+__device__ __forceinline__ void conv_epilogue(const ConvArgs& a,
+                                              f32x16 (&acc)[BM / WM / 32][BN / WN / 32],
+                                              float* smem, int tm, int n0, int split,
+                                              RowMap rowm, int img0, ResMap resp) {
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int MI = TM / 32, NI = TN / 32;
+  static_assert(SL == 1 || (WN == 1 && WM % SL == 0), "row slices need whole waves");
+  constexpr int SR = BM / SL, TP = BN + 4;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  conv_epilogue_t<BM, BN, WM * WN * 64, SL>(
+      a, smem, tm, n0, split, rowm, img0, resp, [&](float* T, int s) {
+        if (SL == 1 || wm * TM / SR == s) {
+#pragma unroll
+          for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+              for (int r = 0; r < 16; ++r)
+                T[(wm * TM - s * SR + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * TP +
+                  wn * TN + ni * 32 + (lane & 31)] = acc[mi][ni][r];
+        }
+      });
+}
+
 // bf16x6 helpers (described with the row tiles below)
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
@@ -238,6 +251,10 @@ __device__ __forceinline__ void split3(const f32x4& p0, const f32x4& p1, u32x4_t
 
 __device__ __forceinline__ f32x16 mfma_bf16(const u32x4_t& a, const u32x4_t& b, const f32x16& c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a),
+                                                 __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma16_bf16(const u32x4_t& a, const u32x4_t& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a),
                                                  __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
 }
 
@@ -480,6 +497,10 @@ __device__ __attribute__((aligned(16))) float pf_conv_zero16[64];
 // sched_barrier mask: every instruction class except vector memory (0x10 and
 // its read / write sub-classes 0x20 / 0x40) may be scheduled across
 #define PF_SCHED_NO_VMEM 0x78F
+// sched_barrier mask that lets VALU, SALU, DS and transcendental instructions
+// cross but pins vector-memory instructions AND MFMAs in program order
+// (conv_bf6x_kernel's interleaving)
+#define PF_SCHED_PIN_VMEM_MFMA 0x786
 
 // vmcnt(N) with expcnt / lgkmcnt left alone (gfx9 s_waitcnt encoding)
 template <int N>
@@ -519,6 +540,15 @@ __device__ __forceinline__ void pf_dma_overlap_step(P0* __restrict__ d0, P1* __r
                                                     Issue&& issue_to, Compute&& compute_from) {
   if (issue) issue_to(d0, d1);
   compute_from(s0, s1);
+}
+
+// The refilled stage and the multiplied stage of a step whose DMAs are
+// interleaved with its LDS reads (conv_bf6x_kernel): both as __restrict__
+// parameters of one body, for the same reason as pf_dma_overlap_step.
+template <class F>
+__device__ __forceinline__ void pf_dma_interleave(unsigned short* __restrict__ d,
+                                                  const unsigned short* __restrict__ s, F&& body) {
+  body(d, s);
 }
 
 // NST = 2: two LDS stages, vmcnt(0) + barrier per chunk (the DMA of chunk c+1
@@ -1333,6 +1363,172 @@ void conv_bf6s_kernel(ConvArgs a) {
 
 
 // ---------------------------------------------------------------------------
+// Dense pre-split-weight GEMM tiles on v_mfma_f32_16x16x32_bf16 with the
+// memory instructions interleaved among the MFMAs (conv_bf6x_kernel, the
+// default for the dense GEMMs: the Winograd transform-domain GEMMs and the
+// 1x1 convs / tap GEMM with no padding).  Measured on the upconv2 / iconv2
+// GEMM shape (tools/probe/gemm_probe.hip): the bf6d structure spends its
+// memory time and its MFMA time one after the other -- a chunk's six B DMAs
+// and four A loads go out in one burst after the barrier, the MFMAs follow --
+// so the loop runs at about the sum of a memory-only loop (0.74 ms) and an
+// MFMA-only loop (1.4 ms).  Here one memory instruction follows each group of
+// twelve MFMAs (pinned by sched barriers), so the DMA / load issue and the
+// returns overlap the matrix pipe, and the 16x16x32 shape holds a higher clock
+// under load than 32x32x16 (MI355X_MICROARCH.md "DVFS give-back" 7).
+// Tile BM = 128 x BN (64 or 128), four waves stacked along M, each 32 rows =
+// two 16-row blocks x BN / 16 column blocks; one MFMA covers a 32-wide k chunk.
+// A (fp32 rows, pitch xcs) goes global -> registers one chunk ahead (lane l:
+// row l & 15 of its block, k (l >> 4) * 8 .. + 7 -- sixteen 128-B rows per
+// load instruction), split in registers (split3); B (three bf16 planes) by
+// LDS DMA into a two-stage ring (the bf6d layout and swizzle).  Each step
+// waits vmcnt(0): the chunk's loads were issued a whole step earlier, in the
+// first part of the previous step's MFMA sequence.  Rows past M re-read the
+// last row (never stored).  Products: the same six bf16 terms as bf6d, but
+// the 16x16x32 instruction sums 32 products per step where 32x32x16 sums 16,
+// so results are NOT bit-identical to the 32x32 tiles (fp32-exact products,
+// different fp32 accumulation grouping); the GEMMs that use it use only it.
+template <int BN>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+void conv_bf6x_kernel(ConvArgs a) {
+  constexpr int NW = 4, BM = 128, RB = 2, NB = BN / 16;
+  constexpr int B_G = 3 * BN / 16 / NW;  // B DMA instructions per wave per chunk
+  constexpr int NA = 2 * RB;             // A loads per lane per chunk
+  constexpr int NOPS = B_G + NA;
+  static_assert((3 * BN / 16) % NW == 0 && NOPS <= 2 * NB, "tile");
+  constexpr int BSTAGE = 3 * BN * BK / 2;  // floats (u16 pairs)
+  constexpr int RING = 2 * BSTAGE;
+  constexpr int SL = BM * (BN + 4) <= RING ? 1 : BM / 2 * (BN + 4) <= RING ? 2 : 4;
+  constexpr int EPI = BM / SL * (BN + 4);
+  __shared__ __attribute__((aligned(16))) float smem[RING > EPI ? RING : EPI];
+  unsigned short* const Bs = reinterpret_cast<unsigned short*>(smem);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  int bid = blockIdx.x % a.nwg;
+  const int split = blockIdx.x / a.nwg;
+  {
+    const int nwg = a.nwg, q = nwg >> 3, r = nwg & 7, xcd = bid & 7, slot = bid >> 3;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+  }
+  const unsigned short* wb = a.wb;
+  if (a.nbatch > 1) {
+    const long long zb = blockIdx.y;
+    a.x += zb * a.bx;
+    a.y += zb * a.by;
+    wb += zb * a.bwb;
+  }
+  const int tm = bid / a.tiles_n, tn = bid - tm * a.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int r16 = lane & 15, kq = lane >> 4;
+  const float* xrow[RB];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb)
+    xrow[rb] = a.x + (long long)min(m0 + wave * 32 + rb * 16 + r16, a.M - 1) * a.xcs + kq * 8;
+  const unsigned short* bsrc[B_G];
+#pragma unroll
+  for (int i = 0; i < B_G; ++i) {
+    const int pr = (wave * B_G + i) * 16 + (lane >> 2);
+    const int plane = pr / BN, row = pr - plane * BN;
+    const int ks = (lane & 3) ^ ((row >> 2) & 3);
+    bsrc[i] = wb + plane * a.wplane + (long long)min(n0 + row, a.Cout - 1) * a.Kpad + ks * 8;
+  }
+  const int nch_all = a.Kpad / BK;
+  const int ch0 = (int)((long long)nch_all * split / a.ksplit);
+  const int ch1 = (int)((long long)nch_all * (split + 1) / a.ksplit);
+  const int nch = ch1 - ch0;
+
+  f32x4 acc[RB][NB];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) acc[rb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 va[RB][2];
+  int la_c = ch0;  // chunk of the next A loads (clamped at the last: same count every step)
+  if (nch > 0) {
+#pragma unroll
+    for (int i = 0; i < B_G; ++i)
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(bsrc[i] + (long long)ch0 * BK),
+          (__attribute__((address_space(3))) void*)(Bs + (wave * B_G + i) * 16 * BK), 16, 0, 0);
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        va[rb][j] = *reinterpret_cast<const f32x4*>(xrow[rb] + (long long)ch0 * BK + j * 4);
+    if (la_c + 1 < ch1) ++la_c;
+  }
+  for (int ii = 0; ii < nch; ++ii) {
+    __builtin_amdgcn_s_waitcnt(0);  // (vmcnt 0; lgkm too) B(ii) and A(ii) landed
+    __builtin_amdgcn_s_barrier();   // every wave's B(ii) part landed; stage s^1 free
+    const int s = ii & 1;
+    u32x4_t ah[RB], am[RB], al[RB];
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) split3(va[rb][0], va[rb][1], ah[rb], am[rb], al[rb]);
+    const int cb = min(ch0 + ii + 1, ch1 - 1);  // next B chunk (the last one re-read at the end)
+    pf_dma_interleave(
+        Bs + (s ^ 1) * 2 * BSTAGE, Bs + s * 2 * BSTAGE,
+        [&](unsigned short* __restrict__ Bd, const unsigned short* __restrict__ Bb) {
+          int op = 0;
+          auto mem = [&]() {  // the op-th memory instruction of this step, pinned in place
+            __builtin_amdgcn_sched_barrier(PF_SCHED_PIN_VMEM_MFMA);
+            if (op < B_G) {
+              __builtin_amdgcn_global_load_lds(
+                  (const __attribute__((address_space(1))) void*)(bsrc[op] + (long long)cb * BK),
+                  (__attribute__((address_space(3))) void*)(Bd + (wave * B_G + op) * 16 * BK), 16,
+                  0, 0);
+            } else if (op < NOPS) {
+              const int j = op - B_G, rb = j >> 1, jj = j & 1;
+              va[rb][jj] =
+                  *reinterpret_cast<const f32x4*>(xrow[rb] + (long long)la_c * BK + jj * 4);
+            }
+            __builtin_amdgcn_sched_barrier(PF_SCHED_PIN_VMEM_MFMA);
+            ++op;
+          };
+#pragma unroll
+          for (int nb = 0; nb < NB; ++nb) {
+            const int row = nb * 16 + r16;
+            const int slot = kq ^ ((row >> 2) & 3);
+            const unsigned short* bp = Bb + row * BK + slot * 8;
+            const u32x4_t bh = *reinterpret_cast<const u32x4_t*>(bp);
+            const u32x4_t bm = *reinterpret_cast<const u32x4_t*>(bp + BN * BK);
+            const u32x4_t bl = *reinterpret_cast<const u32x4_t*>(bp + 2 * BN * BK);
+#pragma unroll
+            for (int rb = 0; rb < RB; ++rb) {
+              f32x4 c = acc[rb][nb];
+              c = mfma16_bf16(ah[rb], bh, c);
+              c = mfma16_bf16(ah[rb], bm, c);
+              c = mfma16_bf16(am[rb], bh, c);
+              c = mfma16_bf16(ah[rb], bl, c);
+              c = mfma16_bf16(al[rb], bh, c);
+              c = mfma16_bf16(am[rb], bm, c);
+              acc[rb][nb] = c;
+            }
+            // memory instructions spread evenly over the NB column blocks
+            while (op < (nb + 1) * NOPS / NB) mem();
+          }
+        });
+    if (la_c + 1 < ch1) ++la_c;
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  conv_epilogue_t<BM, BN, 256, SL>(
+      a, smem, tm, n0, split, [&](int row) { return m0 + row < a.M ? m0 + row : -1; }, m0 / a.hw,
+      [&](int, int m) { return a.res ? a.res + (size_t)m * a.rcs : (const float*)nullptr; },
+      [&](float* T, int sl) {
+        constexpr int SR = BM / SL;
+        if (SL == 1 || wave * 32 / SR == sl) {
+#pragma unroll
+          for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+            for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                T[(wave * 32 - sl * SR + rb * 16 + kq * 4 + r) * (BN + 4) + nb * 16 + r16] =
+                    acc[rb][nb][r];
+        }
+      });
+}
+
+// ---------------------------------------------------------------------------
 // Spatial-halo variant for stride-1 convs with Cin % 32 == 0 (every 3x3
 // decoder/head layer).  The M tile is a PH x 16 patch of output pixels of one
 // image; for each 32-channel slab its (PH+KH-1) x (16+KW-1) input halo is
@@ -1987,7 +2183,8 @@ enum ConvTile {
   TILE_BF6_128x128 = 20, TILE_BF6_128x256 = 21, TILE_BF6_64x128 = 22,   // rows, bf16x6 products
   TILE_BF6_128x64 = 23, TILE_BF6B_128x128 = 24, TILE_BF6B_128x64 = 25,  // + pre-split weights
   TILE_BF6R_128x128 = 26, TILE_BF6R_128x64 = 27,  // + A straight to registers
-  TILE_BF6B_256x128 = 28  // pre-split weights, 8 waves stacked along M (one 135-KB block per CU)
+  TILE_BF6B_256x128 = 28,  // pre-split weights, 8 waves stacked along M (one 135-KB block per CU)
+  TILE_BF6X_128x128 = 29, TILE_BF6X_128x64 = 30  // dense, 16x16x32 MFMAs (conv_bf6x_kernel)
 };
 
 // POSFEAT_BF6=1: every conv the row-tile DMA kernel serves (1x1, strided, the
@@ -2034,6 +2231,27 @@ int bf6d_depth() {
     return v >= 2 && v <= 4 ? v : 0;
   }();
   return d;
+}
+
+// Dense pre-split GEMMs / 1x1 convs (no padding, stride 1) run the 16x16x32
+// conv_bf6x_kernel (POSFEAT_BF6X=0: the 32x32x16 bf6d tiles, A/B).  Their
+// candidate set is then the two BF6X tiles only, so the autotuner's choice
+// never changes results (the 16x16x32 sums are not bit-identical to the
+// 32x32x16 tiles').  The train-mode backbone (PfHaloFp32Scope) keeps the
+// 32x32x16 tiles: its one-step gradient against fp64 on the 2 x 128 x 160
+// fixture case (BatchNorm over 160 pixels in layer3) moved from a worst
+// per-tensor error of 0.014 (both 32x32 arithmetics) to 0.117 with the
+// 16x16x32 sums (tools/bb_step_err.py), while every conv
+// and the extraction model stay within the fp32 bounds (test_gpu_bf6x.py).
+bool bf6x_on() {
+  static const bool off = [] {
+    const char* e = getenv("POSFEAT_BF6X");
+    return e && e[0] == '0';
+  }();
+  return bf6_on() && !off && tl_halo_fp32 == 0;
+}
+bool dense_gemm(const ConvArgs& a) {
+  return a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0 && a.wb && !a.xb;
 }
 
 struct Plan {
@@ -2105,10 +2323,22 @@ Plan plan_for_tile(const ConvArgs& a, int tile) {
   // bf16x6 mode: halo-eligible convs keep fp32 halo tiles only, the rest
   // bf16x6 row tiles only
   if (bf6_on() && glds_ok) {
-    const bool bf6_tile = tile >= TILE_BF6_128x128 && tile <= TILE_BF6B_256x128;
+    const bool bf6_tile = tile >= TILE_BF6_128x128 && tile <= TILE_BF6X_128x64;
     if (halo_ok ? bf6_tile || tile < TILE_H8x128 : !bf6_tile) return p;
+    // dense pre-split GEMMs: the 16x16x32 tiles only (and only they)
+    const bool x_tile = tile == TILE_BF6X_128x128 || tile == TILE_BF6X_128x64;
+    if (x_tile != (bf6x_on() && dense_gemm(a))) return p;
   }
   switch (tile) {
+    case TILE_BF6X_128x128:
+    case TILE_BF6X_128x64:
+      if (!glds_ok || !bf6x_on() || !dense_gemm(a)) return p;
+      p.kern = KERN_GLDS;
+      p.bm = 128;
+      p.bn = tile == TILE_BF6X_128x64 ? 64 : 128;
+      p.ppi = 0;
+      p.tiles_m = (a.M + p.bm - 1) / p.bm;
+      return p;
     case TILE_BF6B_256x128:
       if (!glds_ok || !bf6_on() || !a.wb || a.Cout <= 64) return p;
       p.kern = KERN_GLDS;
@@ -2202,8 +2432,10 @@ Plan conv_plan(const ConvArgs& a, bool allow_split, int forced = -1) {
     d = plan_for_tile(a, tile);
     d.ksplit = tile == TILE_128x128 ? ks : 1;
     if (bf6_on() && cin32 && a.KH * a.KW <= 32 && env.kmax >= KERN_GLDS) {
-      Plan b = plan_for_tile(a, a.wb ? (a.Cout > 64 ? TILE_BF6B_128x128 : TILE_BF6B_128x64)
-                                     : (a.Cout > 64 ? TILE_BF6_128x128 : TILE_BF6_128x64));
+      const bool x = bf6x_on() && dense_gemm(a);
+      Plan b = plan_for_tile(a, x ? (a.Cout > 64 ? TILE_BF6X_128x128 : TILE_BF6X_128x64)
+                                : a.wb ? (a.Cout > 64 ? TILE_BF6B_128x128 : TILE_BF6B_128x64)
+                                       : (a.Cout > 64 ? TILE_BF6_128x128 : TILE_BF6_128x64));
       if (b.kern >= 0) {
         b.ksplit = ks;
         d = b;
@@ -2300,6 +2532,14 @@ int conv_run(ConvArgs& a, const Plan& p, hipStream_t st) {
       else
         hipLaunchKernelGGL((conv_glds_kernel<128, 64, 2, 2, 2, true>),
                            dim3(a.nwg * a.ksplit, a.nbatch), dim3(256), 0, st, a);
+      break;
+    case TILE_BF6X_128x128:
+      hipLaunchKernelGGL((conv_bf6x_kernel<128>), dim3(a.nwg * a.ksplit, a.nbatch), dim3(256), 0,
+                         st, a);
+      break;
+    case TILE_BF6X_128x64:
+      hipLaunchKernelGGL((conv_bf6x_kernel<64>), dim3(a.nwg * a.ksplit, a.nbatch), dim3(256), 0,
+                         st, a);
       break;
     case TILE_BF6B_128x128:
     case TILE_BF6B_128x64: {
@@ -2503,6 +2743,14 @@ extern "C" int posfeat_conv2d_nhwc_ws(const posfeat_conv_desc* d, const float* x
   return conv_run(a, p, pf_stream(stream));
 }
 
+extern "C" int posfeat_conv2d_nhwc_planes(const posfeat_conv_desc* d, const float* x,
+                                          const float* w, const unsigned short* wb,
+                                          long long wplane, const float* bias, const float* res,
+                                          float* y, void* ws, size_t ws_bytes, void* stream) {
+  if (!wb || wplane <= 0) return POSFEAT_E_INVALID;
+  return pf_conv_run_tile(d, x, w, bias, res, y, ws, ws_bytes, -1, pf_stream(stream), wb, wplane);
+}
+
 // Stats tiling: contiguous-row tiles may straddle two images (slot 1 holds the
 // second image's rows); patch tiles belong to one image.
 static size_t stats_tiles_per_img(const ConvArgs& a, const Plan& p) {
@@ -2534,7 +2782,8 @@ static const int kAllTiles[] = {TILE_H8x128,      TILE_H8x64,       TILE_128x128
                                 TILE_128x64,      TILE_64x64,       TILE_256x128,
                                 TILE_BF6_128x128, TILE_BF6_128x256, TILE_BF6_64x128,
                                 TILE_BF6_128x64,  TILE_BF6B_128x128, TILE_BF6B_128x64,
-                                TILE_BF6R_128x128, TILE_BF6R_128x64,  TILE_BF6B_256x128};
+                                TILE_BF6R_128x128, TILE_BF6R_128x64,  TILE_BF6B_256x128,
+                                TILE_BF6X_128x128, TILE_BF6X_128x64};
 
 int pf_conv_candidates(const posfeat_conv_desc* d, int* tiles, int max, bool wplanes) {
   ConvArgs a;
@@ -2824,7 +3073,9 @@ int pf_gemm_batched(const float* A, int lda, long long sa, const float* B, long 
     const char* e = getenv("POSFEAT_GEMM_B256");
     return e && e[0] == '1';
   }();
-  const int want = (Bb && b256 && N % 128 == 0) ? TILE_BF6B_256x128
+  const bool x = Bb && bf6x_on();
+  const int want = x ? (N % 128 == 0 ? TILE_BF6X_128x128 : TILE_BF6X_128x64)
+                   : (Bb && b256 && N % 128 == 0) ? TILE_BF6B_256x128
                    : (N % 128 == 0 && t128 >= 1024) ? TILE_128x128
                    : (Bb && n64 && N % 128 != 0 && N % 64 == 0) ? TILE_BF6B_128x64
                                                                  : -1;

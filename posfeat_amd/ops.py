@@ -72,6 +72,42 @@ def conv2d_nhwc(x, w_packed, bias, cout, kh, kw, stride=1, pad=None, act="none",
     return out
 
 
+def split_weight_planes(w_packed):
+    """The packed [cout][Kpad] fp32 weights as three bf16 planes h, m, l
+    (x = h + m + l up to 2^-27 |x|, RNE at each step: the library's split3),
+    returned as one int16 tensor [3][cout][Kpad] (plane stride cout * Kpad)."""
+    w = _f32(w_packed, "w")
+    h = w.to(torch.bfloat16)
+    r = w - h.float()
+    m = r.to(torch.bfloat16)
+    lo = (r - m.float()).to(torch.bfloat16)
+    return torch.stack([h, m, lo]).view(torch.int16).contiguous()
+
+
+def conv2d_nhwc_planes(x, w_packed, planes, bias, cout, kh, kw, stride=1, pad=None, act="none",
+                       res=None, out=None, cin=None, allow_split=False):
+    """conv2d_nhwc with the weights also given as bf16 planes
+    (split_weight_planes), as the engine runs its convs: the pre-split tiles
+    (dense 1x1: the 16x16x32 conv_bf6x_kernel)."""
+    _f32(x, "x")
+    n, h, w, xcs = x.shape
+    cin = xcs if cin is None else cin
+    pad = (kh - 1) // 2 if pad is None else pad
+    oh = (h + 2 * pad - kh) // stride + 1
+    ow = (w + 2 * pad - kw) // stride + 1
+    if out is None:
+        out = torch.empty(n, oh, ow, cout, device=x.device, dtype=torch.float32)
+    d = _lib.ConvDesc(n=n, h=h, w=w, cin=cin, x_cstride=xcs, cout=cout, kh=kh, kw=kw,
+                      stride=stride, pad=pad, y_cstride=out.shape[-1],
+                      res_cstride=(res.shape[-1] if res is not None else 0), act=ACT[act])
+    need = lib().posfeat_conv2d_workspace(ctypes.byref(d)) if allow_split else 0
+    ws = torch.empty(max(need, 16), dtype=torch.uint8, device=x.device)
+    check(lib().posfeat_conv2d_nhwc_planes(ctypes.byref(d), ptr(x), ptr(w_packed), ptr(planes),
+                                           planes[0].numel(), ptr(bias), ptr(res), ptr(out),
+                                           ptr(ws), need, stream_ptr()))
+    return out
+
+
 def conv2d_nhwc_instnorm_stats(x, w_packed, bias, cout, kh, kw, eps=1e-5, out=None, cin=None):
     """Conv (stride 1, 'same' pad, no act) + per-image channel mean/rstd of its
     output from the fused epilogue.  Returns (y, mean [n,cout], rstd [n,cout])."""

@@ -1,7 +1,7 @@
 """Switches whose two forms must give BIT-identical engine outputs.
 
 conv_bf6d_kernel (pre-split weights, A prefetched D chunks ahead in registers,
-the default) against conv_bf6b_kernel (A staged through LDS, POSFEAT_BF6D=0):
+the default for the non-dense convs; the dense ones with POSFEAT_BF6X=0) against conv_bf6b_kernel (A staged through LDS, POSFEAT_BF6D=0):
 the same bf16x6 products in the same order, so the engine's outputs must be
 BIT-identical for every D (the switch is read once per process: each run is a
 child process).  The B=8 480x640 bench instance covers the batched Winograd
@@ -57,7 +57,10 @@ def test_bf6d_bit_identical_to_bf6b(tmp_path):
     256x128 pre-split tile (TILE_BF6B_256x128 = 28: an autotuner candidate for
     the 1x1 convs, forced everywhere it is legal, and on the batched Winograd
     GEMMs via POSFEAT_GEMM_B256; D capped at 3 there)"""
-    ref = _run(tmp_path, {"POSFEAT_BF6D": "0"}, "b")   # LDS-staged bf6b
+    # the dense GEMMs / 1x1 convs run the 32x32x16 family here (POSFEAT_BF6X=0):
+    # the 16x16x32 default is checked in test_gpu_bf6x.py
+    x0 = {"POSFEAT_BF6X": "0"}
+    ref = _run(tmp_path, dict(x0, POSFEAT_BF6D="0"), "b")   # LDS-staged bf6b
     for tag, env in (("d2", {}),                       # the default: deep A prefetch, D = 2
                      ("d3", {"POSFEAT_BF6D": "3"}),
                      ("d4", {"POSFEAT_BF6D": "4"}),
@@ -68,6 +71,6 @@ def test_bf6d_bit_identical_to_bf6b(tmp_path):
                      # conv precision mode 2: the Winograd / tap GEMM A operands
                      # pre-split by their producers (conv_bf6s_kernel)
                      ("mode2", {"POSFEAT_BF6": "2"})):
-        got = _run(tmp_path, env, tag)
+        got = _run(tmp_path, dict(x0, **env), tag)
         for k in ("lp", "lm", "gm"):
             np.testing.assert_array_equal(got[k], ref[k], err_msg="%s %s" % (tag, k))

@@ -1,0 +1,112 @@
+"""The dense pre-split GEMM tiles on v_mfma_f32_16x16x32_bf16
+(conv_bf6x_kernel, conv.hip): the 1x1 convs the engine runs with weight
+planes, and the batched Winograd GEMMs.
+
+The products are the same six bf16 terms as the 32x32x16 tiles (fp32-exact
+per product); only the fp32 accumulation grouping differs,
+so the bound is the bf16x6 one of test_gpu_precision.py: against an fp64
+reference, no more than 1.25x the fp32-input MFMA's own error (mode 0) plus
+1e-7 of sum|x||w|, and <= 2e-6 of sum|x||w|.  Covered: M not a multiple of
+the 128-row tile, Cout 64 / 128 / 192 / 1024 (both column tiles, ragged
+column tiles), bias + residual + ReLU / ELU epilogues, split-K, and K from
+one chunk to 32 chunks."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CASES = [  # n, h, w, cin, cout, act, residual, split
+    (2, 40, 48, 512, 256, "none", False, False),
+    (2, 7, 9, 64, 64, "relu", True, False),        # M = 126 < one tile
+    (1, 30, 40, 1024, 256, "relu", True, True),    # layer3 conv1 shape, split-K
+    (1, 30, 40, 256, 1024, "relu", True, False),   # layer3 conv3 + residual
+    (2, 24, 40, 192, 1152, "none", False, False),  # the tap GEMM's K and N
+    (1, 33, 41, 32, 192, "elu", False, False),     # K = one chunk, ragged M, 3 x 64 columns
+    (1, 16, 20, 256, 96, "elu", True, False),      # Cout % 64 != 0: ragged column tile
+]
+
+
+@pytest.fixture
+def precision():
+    from posfeat_amd._lib import lib
+    prev = lib().posfeat_set_conv_precision(1)
+    yield lambda m: lib().posfeat_set_conv_precision(m)
+    lib().posfeat_set_conv_precision(prev)
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_bf6x_dense_conv_vs_fp64(gpu, precision, case):
+    from posfeat_amd import ops
+    n, h, w, cin, cout, act, residual, split = case
+    g = torch.Generator().manual_seed(7 * cin + cout)
+    x = torch.randn(n, cin, h, w, generator=g)
+    wt = torch.randn(cout, cin, 1, 1, generator=g) / np.sqrt(cin)
+    b = torch.randn(cout, generator=g) * 0.1
+    r = torch.randn(n, h, w, cout, generator=g) if residual else None
+    pre = torch.nn.functional.conv2d(x.double(), wt.double(), b.double()).permute(0, 2, 3, 1)
+    if residual:
+        pre = pre + r.double()
+    ref = {"none": pre, "relu": pre.clamp_min(0),
+           "elu": torch.nn.functional.elu(pre)}[act]
+    mag = torch.nn.functional.conv2d(x.double().abs(), wt.double().abs()).permute(0, 2, 3, 1)
+    if residual:
+        mag = mag + r.double().abs()
+    xg = x.permute(0, 2, 3, 1).contiguous().to(gpu)
+    wp, bb = ops.pack_conv_weight(wt.to(gpu), b.to(gpu))
+    planes = ops.split_weight_planes(wp)
+    rg = r.to(gpu) if residual else None
+    precision(1)
+    y6 = ops.conv2d_nhwc_planes(xg, wp, planes, bb, cout, 1, 1, act=act, res=rg,
+                                allow_split=split).cpu().double()
+    precision(0)
+    y32 = ops.conv2d_nhwc(xg, wp, bb, cout, 1, 1, act=act, res=rg).cpu().double()
+    torch.cuda.synchronize()
+    e32 = float((y32 - ref).abs().max())
+    e6 = float((y6 - ref).abs().max())
+    scale = float(mag.max())
+    print("case", case, "fp32 err %.3e  bf16x6 (16x16x32) err %.3e  scale %.3e" % (e32, e6, scale))
+    assert torch.isfinite(y6).all()
+    assert e6 <= 1.25 * e32 + 1e-7 * scale, (e6, e32)
+    assert e6 <= 2e-6 * scale
+
+
+CODE = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, %(root)r)
+from posfeat_amd.engine import ExtractionEngine
+from posfeat_amd.weights import seeded_image, seeded_state_dicts
+bb, hd = seeded_state_dicts(0)
+eng = ExtractionEngine(bb, hd, device="cuda:0")
+img = torch.from_numpy(np.stack([seeded_image(60 + i, 480, 640) for i in range(4)])).cuda()
+r = eng.run(img, outputs=("local_map", "global_map"))
+torch.cuda.synchronize()
+np.savez(%(out)r, lp=r["local_point"].cpu().numpy(), lm=r["local_map"].cpu().numpy(),
+         gm=r["global_map"].cpu().numpy())
+"""
+
+
+def test_bf6x_engine_vs_bf6d(tmp_path):
+    """The whole extraction model with the 16x16x32 dense tiles (default) vs
+    the 32x32x16 bf6d tiles (POSFEAT_BF6X=0): both fp32-accurate, different
+    accumulation grouping -- within 1e-5 of each map's scale, and not
+    bit-identical (the 16x16x32 path really ran)."""
+    res = {}
+    for tag, env in (("x", {}), ("d", {"POSFEAT_BF6X": "0"})):
+        out = str(tmp_path / ("%s.npz" % tag))
+        subprocess.run([sys.executable, "-c", CODE % {"root": ROOT, "out": out}],
+                       env=dict(os.environ, **env), check=True, timeout=240)
+        res[tag] = np.load(out)
+    differ = False
+    for k in ("lp", "lm", "gm"):
+        a, b = res["x"][k].astype(np.float64), res["d"][k].astype(np.float64)
+        s = max(1.0, np.abs(b).max())
+        assert np.abs(a - b).max() <= 1e-5 * s, (k, np.abs(a - b).max(), s)
+        differ |= not np.array_equal(a, b)
+    assert differ, "the 16x16x32 tiles did not run"
