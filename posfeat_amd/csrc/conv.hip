@@ -1375,8 +1375,13 @@ void conv_bf6s_kernel(ConvArgs a) {
 // twelve MFMAs (pinned by sched barriers), so the DMA / load issue and the
 // returns overlap the matrix pipe, and the 16x16x32 shape holds a higher clock
 // under load than 32x32x16 (MI355X_MICROARCH.md "DVFS give-back" 7).
-// Tile BM = 128 x BN (64 or 128), four waves stacked along M, each 32 rows =
-// two 16-row blocks x BN / 16 column blocks; one MFMA covers a 32-wide k chunk.
+// Strided 1x1 convs (the encoder's downsample layers) too: output row m reads
+// input pixel (n, s oh, s ow).
+// Tile BM = 64 RB x BN (64 or 128), four waves stacked along M, each 16 RB
+// rows = RB 16-row blocks x BN / 16 column blocks; one MFMA covers a 32-wide k
+// chunk.  RB = 4 (TILE_BF6X_256x128) halves the B traffic per MFMA; per
+// output element the MFMA sequence is the same, so RB = 2 and 4 are
+// bit-identical (autotune candidates of each other).
 // A (fp32 rows, pitch xcs) goes global -> registers one chunk ahead (lane l:
 // row l & 15 of its block, k (l >> 4) * 8 .. + 7 -- sixteen 128-B rows per
 // load instruction), split in registers (split3); B (three bf16 planes) by
@@ -1387,14 +1392,14 @@ void conv_bf6s_kernel(ConvArgs a) {
 // the 16x16x32 instruction sums 32 products per step where 32x32x16 sums 16,
 // so results are NOT bit-identical to the 32x32 tiles (fp32-exact products,
 // different fp32 accumulation grouping); the GEMMs that use it use only it.
-template <int BN>
+template <int BN, int RB = 2>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
 void conv_bf6x_kernel(ConvArgs a) {
-  constexpr int NW = 4, BM = 128, RB = 2, NB = BN / 16;
+  constexpr int NW = 4, BM = NW * RB * 16, NB = BN / 16;
   constexpr int B_G = 3 * BN / 16 / NW;  // B DMA instructions per wave per chunk
   constexpr int NA = 2 * RB;             // A loads per lane per chunk
   constexpr int NOPS = B_G + NA;
-  static_assert((3 * BN / 16) % NW == 0 && NOPS <= 2 * NB, "tile");
+  static_assert((3 * BN / 16) % NW == 0 && NOPS <= 2 * NB && (RB == 2 || RB == 4), "tile");
   constexpr int BSTAGE = 3 * BN * BK / 2;  // floats (u16 pairs)
   constexpr int RING = 2 * BSTAGE;
   constexpr int SL = BM * (BN + 4) <= RING ? 1 : BM / 2 * (BN + 4) <= RING ? 2 : 4;
@@ -1421,8 +1426,16 @@ void conv_bf6x_kernel(ConvArgs a) {
   const int r16 = lane & 15, kq = lane >> 4;
   const float* xrow[RB];
 #pragma unroll
-  for (int rb = 0; rb < RB; ++rb)
-    xrow[rb] = a.x + (long long)min(m0 + wave * 32 + rb * 16 + r16, a.M - 1) * a.xcs + kq * 8;
+  for (int rb = 0; rb < RB; ++rb) {
+    const int m = min(m0 + wave * RB * 16 + rb * 16 + r16, a.M - 1);
+    long long pix = m;  // stride 1: output row m is input pixel m
+    if (a.stride != 1) {
+      const int n = m / a.hw, rem = m - n * a.hw;
+      const int oh = rem / a.OW, ow = rem - oh * a.OW;
+      pix = ((long long)n * a.H + oh * a.stride) * a.W + ow * a.stride;
+    }
+    xrow[rb] = a.x + pix * a.xcs + kq * 8;
+  }
   const unsigned short* bsrc[B_G];
 #pragma unroll
   for (int i = 0; i < B_G; ++i) {
@@ -1515,14 +1528,14 @@ void conv_bf6x_kernel(ConvArgs a) {
       [&](int, int m) { return a.res ? a.res + (size_t)m * a.rcs : (const float*)nullptr; },
       [&](float* T, int sl) {
         constexpr int SR = BM / SL;
-        if (SL == 1 || wave * 32 / SR == sl) {
+        if (SL == 1 || wave * RB * 16 / SR == sl) {
 #pragma unroll
           for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
             for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
               for (int r = 0; r < 4; ++r)
-                T[(wave * 32 - sl * SR + rb * 16 + kq * 4 + r) * (BN + 4) + nb * 16 + r16] =
+                T[(wave * RB * 16 - sl * SR + rb * 16 + kq * 4 + r) * (BN + 4) + nb * 16 + r16] =
                     acc[rb][nb][r];
         }
       });
@@ -2184,7 +2197,8 @@ enum ConvTile {
   TILE_BF6_128x64 = 23, TILE_BF6B_128x128 = 24, TILE_BF6B_128x64 = 25,  // + pre-split weights
   TILE_BF6R_128x128 = 26, TILE_BF6R_128x64 = 27,  // + A straight to registers
   TILE_BF6B_256x128 = 28,  // pre-split weights, 8 waves stacked along M (one 135-KB block per CU)
-  TILE_BF6X_128x128 = 29, TILE_BF6X_128x64 = 30  // dense, 16x16x32 MFMAs (conv_bf6x_kernel)
+  TILE_BF6X_128x128 = 29, TILE_BF6X_128x64 = 30,  // dense, 16x16x32 MFMAs (conv_bf6x_kernel)
+  TILE_BF6X_256x128 = 31
 };
 
 // POSFEAT_BF6=1: every conv the row-tile DMA kernel serves (1x1, strided, the
@@ -2250,8 +2264,10 @@ bool bf6x_on() {
   }();
   return bf6_on() && !off && tl_halo_fp32 == 0;
 }
+// 1x1, no padding, any stride (a strided 1x1 conv is a GEMM over the
+// subsampled pixel rows: conv_bf6x_kernel maps each row to its input pixel)
 bool dense_gemm(const ConvArgs& a) {
-  return a.KH == 1 && a.KW == 1 && a.stride == 1 && a.pad == 0 && a.wb && !a.xb;
+  return a.KH == 1 && a.KW == 1 && a.pad == 0 && a.wb && !a.xb;
 }
 
 struct Plan {
@@ -2323,18 +2339,19 @@ Plan plan_for_tile(const ConvArgs& a, int tile) {
   // bf16x6 mode: halo-eligible convs keep fp32 halo tiles only, the rest
   // bf16x6 row tiles only
   if (bf6_on() && glds_ok) {
-    const bool bf6_tile = tile >= TILE_BF6_128x128 && tile <= TILE_BF6X_128x64;
+    const bool bf6_tile = tile >= TILE_BF6_128x128 && tile <= TILE_BF6X_256x128;
     if (halo_ok ? bf6_tile || tile < TILE_H8x128 : !bf6_tile) return p;
     // dense pre-split GEMMs: the 16x16x32 tiles only (and only they)
-    const bool x_tile = tile == TILE_BF6X_128x128 || tile == TILE_BF6X_128x64;
+    const bool x_tile = tile >= TILE_BF6X_128x128 && tile <= TILE_BF6X_256x128;
     if (x_tile != (bf6x_on() && dense_gemm(a))) return p;
   }
   switch (tile) {
     case TILE_BF6X_128x128:
     case TILE_BF6X_128x64:
+    case TILE_BF6X_256x128:
       if (!glds_ok || !bf6x_on() || !dense_gemm(a)) return p;
       p.kern = KERN_GLDS;
-      p.bm = 128;
+      p.bm = tile == TILE_BF6X_256x128 ? 256 : 128;
       p.bn = tile == TILE_BF6X_128x64 ? 64 : 128;
       p.ppi = 0;
       p.tiles_m = (a.M + p.bm - 1) / p.bm;
@@ -2540,6 +2557,10 @@ int conv_run(ConvArgs& a, const Plan& p, hipStream_t st) {
     case TILE_BF6X_128x64:
       hipLaunchKernelGGL((conv_bf6x_kernel<64>), dim3(a.nwg * a.ksplit, a.nbatch), dim3(256), 0,
                          st, a);
+      break;
+    case TILE_BF6X_256x128:
+      hipLaunchKernelGGL((conv_bf6x_kernel<128, 4>), dim3(a.nwg * a.ksplit, a.nbatch), dim3(256),
+                         0, st, a);
       break;
     case TILE_BF6B_128x128:
     case TILE_BF6B_128x64: {
@@ -2783,7 +2804,7 @@ static const int kAllTiles[] = {TILE_H8x128,      TILE_H8x64,       TILE_128x128
                                 TILE_BF6_128x128, TILE_BF6_128x256, TILE_BF6_64x128,
                                 TILE_BF6_128x64,  TILE_BF6B_128x128, TILE_BF6B_128x64,
                                 TILE_BF6R_128x128, TILE_BF6R_128x64,  TILE_BF6B_256x128,
-                                TILE_BF6X_128x128, TILE_BF6X_128x64};
+                                TILE_BF6X_128x128, TILE_BF6X_128x64, TILE_BF6X_256x128};
 
 int pf_conv_candidates(const posfeat_conv_desc* d, int* tiles, int max, bool wplanes) {
   ConvArgs a;
@@ -3074,7 +3095,13 @@ int pf_gemm_batched(const float* A, int lda, long long sa, const float* B, long 
     return e && e[0] == '1';
   }();
   const bool x = Bb && bf6x_on();
-  const int want = x ? (N % 128 == 0 ? TILE_BF6X_128x128 : TILE_BF6X_128x64)
+  // POSFEAT_BF6X_RB4=1 (A/B): the 256-row 16x16x32 tiles for the batched GEMMs
+  static const bool rb4 = [] {
+    const char* e = getenv("POSFEAT_BF6X_RB4");
+    return e && e[0] == '1';
+  }();
+  const int want = x ? (N % 128 == 0 ? (rb4 ? TILE_BF6X_256x128 : TILE_BF6X_128x128)
+                                     : TILE_BF6X_128x64)
                    : (Bb && b256 && N % 128 == 0) ? TILE_BF6B_256x128
                    : (N % 128 == 0 && t128 >= 1024) ? TILE_128x128
                    : (Bb && n64 && N % 128 != 0 && N % 64 == 0) ? TILE_BF6B_128x64

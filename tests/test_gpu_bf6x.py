@@ -8,8 +8,8 @@ so the bound is the bf16x6 one of test_gpu_precision.py: against an fp64
 reference, no more than 1.25x the fp32-input MFMA's own error (mode 0) plus
 1e-7 of sum|x||w|, and <= 2e-6 of sum|x||w|.  Covered: M not a multiple of
 the 128-row tile, Cout 64 / 128 / 192 / 1024 (both column tiles, ragged
-column tiles), bias + residual + ReLU / ELU epilogues, split-K, and K from
-one chunk to 32 chunks."""
+column tiles), bias + residual + ReLU / ELU epilogues, split-K, K from one
+chunk to 32 chunks, and stride-2 1x1 convs (the downsample layers)."""
 import os
 import subprocess
 import sys
@@ -22,14 +22,16 @@ pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
-CASES = [  # n, h, w, cin, cout, act, residual, split
-    (2, 40, 48, 512, 256, "none", False, False),
-    (2, 7, 9, 64, 64, "relu", True, False),        # M = 126 < one tile
-    (1, 30, 40, 1024, 256, "relu", True, True),    # layer3 conv1 shape, split-K
-    (1, 30, 40, 256, 1024, "relu", True, False),   # layer3 conv3 + residual
-    (2, 24, 40, 192, 1152, "none", False, False),  # the tap GEMM's K and N
-    (1, 33, 41, 32, 192, "elu", False, False),     # K = one chunk, ragged M, 3 x 64 columns
-    (1, 16, 20, 256, 96, "elu", True, False),      # Cout % 64 != 0: ragged column tile
+CASES = [  # n, h, w, cin, cout, act, residual, split, stride
+    (2, 40, 48, 512, 256, "none", False, False, 1),
+    (2, 7, 9, 64, 64, "relu", True, False, 1),        # M = 126 < one tile
+    (1, 30, 40, 1024, 256, "relu", True, True, 1),    # layer3 conv1 shape, split-K
+    (1, 30, 40, 256, 1024, "relu", True, False, 1),   # layer3 conv3 + residual
+    (2, 24, 40, 192, 1152, "none", False, False, 1),  # the tap GEMM's K and N
+    (1, 33, 41, 32, 192, "elu", False, False, 1),     # K = one chunk, ragged M, 3 x 64 columns
+    (1, 16, 20, 256, 96, "elu", True, False, 1),      # Cout % 64 != 0: ragged column tile
+    (2, 60, 80, 512, 1024, "none", False, False, 2),  # layer3.0.downsample (stride 2)
+    (1, 31, 41, 256, 128, "relu", True, False, 2),    # stride 2 on odd sizes + residual
 ]
 
 
@@ -44,18 +46,21 @@ def precision():
 @pytest.mark.parametrize("case", CASES)
 def test_bf6x_dense_conv_vs_fp64(gpu, precision, case):
     from posfeat_amd import ops
-    n, h, w, cin, cout, act, residual, split = case
+    n, h, w, cin, cout, act, residual, split, stride = case
     g = torch.Generator().manual_seed(7 * cin + cout)
     x = torch.randn(n, cin, h, w, generator=g)
     wt = torch.randn(cout, cin, 1, 1, generator=g) / np.sqrt(cin)
     b = torch.randn(cout, generator=g) * 0.1
-    r = torch.randn(n, h, w, cout, generator=g) if residual else None
-    pre = torch.nn.functional.conv2d(x.double(), wt.double(), b.double()).permute(0, 2, 3, 1)
+    oh, ow = (h - 1) // stride + 1, (w - 1) // stride + 1
+    r = torch.randn(n, oh, ow, cout, generator=g) if residual else None
+    pre = torch.nn.functional.conv2d(x.double(), wt.double(), b.double(),
+                                     stride=stride).permute(0, 2, 3, 1)
     if residual:
         pre = pre + r.double()
     ref = {"none": pre, "relu": pre.clamp_min(0),
            "elu": torch.nn.functional.elu(pre)}[act]
-    mag = torch.nn.functional.conv2d(x.double().abs(), wt.double().abs()).permute(0, 2, 3, 1)
+    mag = torch.nn.functional.conv2d(x.double().abs(), wt.double().abs(),
+                                     stride=stride).permute(0, 2, 3, 1)
     if residual:
         mag = mag + r.double().abs()
     xg = x.permute(0, 2, 3, 1).contiguous().to(gpu)
@@ -63,10 +68,10 @@ def test_bf6x_dense_conv_vs_fp64(gpu, precision, case):
     planes = ops.split_weight_planes(wp)
     rg = r.to(gpu) if residual else None
     precision(1)
-    y6 = ops.conv2d_nhwc_planes(xg, wp, planes, bb, cout, 1, 1, act=act, res=rg,
+    y6 = ops.conv2d_nhwc_planes(xg, wp, planes, bb, cout, 1, 1, stride=stride, act=act, res=rg,
                                 allow_split=split).cpu().double()
     precision(0)
-    y32 = ops.conv2d_nhwc(xg, wp, bb, cout, 1, 1, act=act, res=rg).cpu().double()
+    y32 = ops.conv2d_nhwc(xg, wp, bb, cout, 1, 1, stride=stride, act=act, res=rg).cpu().double()
     torch.cuda.synchronize()
     e32 = float((y32 - ref).abs().max())
     e6 = float((y6 - ref).abs().max())
@@ -110,3 +115,18 @@ def test_bf6x_engine_vs_bf6d(tmp_path):
         assert np.abs(a - b).max() <= 1e-5 * s, (k, np.abs(a - b).max(), s)
         differ |= not np.array_equal(a, b)
     assert differ, "the 16x16x32 tiles did not run"
+
+
+def test_bf6x_rb4_bit_identical(tmp_path):
+    """The 256-row 16x16x32 tiles (RB = 4: TILE_BF6X_256x128 = 31, forced on
+    every dense conv and on the batched Winograd GEMMs) run the same MFMA
+    sequence per output element as the 128-row ones: bit-identical engine
+    outputs (they are autotune candidates of each other)."""
+    res = {}
+    for tag, env in (("r2", {}), ("r4", {"POSFEAT_BF6X_RB4": "1", "POSFEAT_CONV_TILE": "31"})):
+        out = str(tmp_path / ("%s.npz" % tag))
+        subprocess.run([sys.executable, "-c", CODE % {"root": ROOT, "out": out}],
+                       env=dict(os.environ, **env), check=True, timeout=240)
+        res[tag] = np.load(out)
+    for k in ("lp", "lm", "gm"):
+        np.testing.assert_array_equal(res["r4"][k], res["r2"][k], err_msg=k)

@@ -372,14 +372,27 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
         u32x4_t ah[RB], am[RB], al[RB];
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb) split3(va[u][rb][0], va[u][rb][1], ah[rb], am[rb], al[rb]);
-#pragma unroll
-        for (int nb = 0; nb < NB; ++nb) {
+        u32x4_t bf[2][3];
+        auto readb = [&](int nb, u32x4_t (&o)[3]) {
           const int row = nb * 16 + r16;
           const int slot = kq ^ ((row >> 2) & 3);
           const unsigned short* bp = Bb + row * BK + slot * 8;
-          const u32x4_t bh = *reinterpret_cast<const u32x4_t*>(bp);
-          const u32x4_t bm = *reinterpret_cast<const u32x4_t*>(bp + BN * BK);
-          const u32x4_t bl = *reinterpret_cast<const u32x4_t*>(bp + 2 * BN * BK);
+          o[0] = *reinterpret_cast<const u32x4_t*>(bp);
+          o[1] = *reinterpret_cast<const u32x4_t*>(bp + BN * BK);
+          o[2] = *reinterpret_cast<const u32x4_t*>(bp + 2 * BN * BK);
+        };
+        if (FL & 1) readb(0, bf[0]);
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) {
+          u32x4_t cur[3];
+          if (FL & 1) {
+            if (nb + 1 < NB) readb(nb + 1, bf[(nb + 1) & 1]);
+#pragma unroll
+            for (int p = 0; p < 3; ++p) cur[p] = bf[nb & 1][p];
+          } else {
+            readb(nb, cur);
+          }
+          const u32x4_t bh = cur[0], bm = cur[1], bl = cur[2];
 #pragma unroll
           for (int rb = 0; rb < RB; ++rb) {
             f32x4 c = acc[rb][nb];
@@ -391,8 +404,12 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
             c = mfma16(am[rb], bm, c);
             acc[rb][nb] = c;
           }
-          mem();
-          if (nb >= NB - (B_G + NA - NB)) mem();
+          if (FL & 4) {
+            if (nb < NB / 2) { mem(); mem(); if (nb == NB / 2 - 1) while (op < B_G + NA) mem(); }
+          } else {
+            mem();
+            if (nb >= NB - (B_G + NA - NB)) mem();
+          }
         }
         while (op < B_G + NA) mem();
       });
@@ -464,15 +481,13 @@ int main(int argc, char** argv) {
     printf("%-28s %8.3f ms  %7.1f TF/s fp32-eq  %.3f of 416.7\n", name, ms, fl / ms / 1e9,
            fl / ms / 1e9 / 416.7);
   };
-  rep("base MI1 D2", run(k32<1, 2, 0>, a, 128, nb, reps));
-  rep("interleaved lazysplit", run(k32<1, 2, 96>, a, 128, nb, reps));
-  rep("MI2 interleaved lazy D1", run(k32<2, 1, 96>, a, 256, nb, reps));
-  rep("16x16x32 D2", run(k16<2, 0>, a, 128, nb, reps));
   rep("16x16x32 D1", run(k16<1, 0>, a, 128, nb, reps));
+  rep("16x16x32 D1 bpref", run(k16<1, 1>, a, 128, nb, reps));
+  rep("16x16x32 D1 front", run(k16<1, 4>, a, 128, nb, reps));
+  rep("16x16x32 D1 bpref front", run(k16<1, 5>, a, 128, nb, reps));
   rep("16x16x32 RB4 D1", run(k16<1, 0, 4>, a, 256, nb, reps));
-  rep("16x16x32 RB4 D2", run(k16<2, 0, 4>, a, 256, nb, reps));
-  rep("16x16x32 8w D1", run(k16<1, 0, 2, 8>, a, 256, nb, reps, 512));
-  rep("16x16x32 8w D2", run(k16<2, 0, 2, 8>, a, 256, nb, reps, 512));
+  rep("16x16x32 RB4 D1 bpref", run(k16<1, 1, 4>, a, 256, nb, reps));
+  rep("16x16x32 RB4 D1 front", run(k16<1, 4, 4>, a, 256, nb, reps));
   rep("16x16x32 D1 again", run(k16<1, 0>, a, 128, nb, reps));
   return 0;
 }
