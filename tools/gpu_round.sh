@@ -12,7 +12,8 @@ chk=tools/gpu_check.sh
 export PYTHONUNBUFFERED=1
 $chk 900 $o/gpu_tests.log python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
 $chk 200 $o/smoke.log python -c "import __graft_entry__ as g; g.smoke()"
-$chk 400 $o/bench.json python bench.py
+$chk 400 $o/bench.log python bench.py
+grep "^{" $o/bench.log > $o/bench.json || true
 [ "$2" = quick ] && exit 0
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 $chk 400 $o/prof.log rocprofv3 --kernel-trace --stats -d $o/prof -o b --output-format csv -- python3 bench.py --steps 20 --no-cpu-baseline

@@ -481,13 +481,9 @@ int main(int argc, char** argv) {
     printf("%-28s %8.3f ms  %7.1f TF/s fp32-eq  %.3f of 416.7\n", name, ms, fl / ms / 1e9,
            fl / ms / 1e9 / 416.7);
   };
+  rep("base MI1 D2", run(k32<1, 2, 0>, a, 128, nb, reps));
+  rep("noA noB", run(k32<1, 2, 3>, a, 128, nb, reps));
   rep("16x16x32 D1", run(k16<1, 0>, a, 128, nb, reps));
-  rep("16x16x32 D1 bpref", run(k16<1, 1>, a, 128, nb, reps));
   rep("16x16x32 D1 front", run(k16<1, 4>, a, 128, nb, reps));
-  rep("16x16x32 D1 bpref front", run(k16<1, 5>, a, 128, nb, reps));
-  rep("16x16x32 RB4 D1", run(k16<1, 0, 4>, a, 256, nb, reps));
-  rep("16x16x32 RB4 D1 bpref", run(k16<1, 1, 4>, a, 256, nb, reps));
-  rep("16x16x32 RB4 D1 front", run(k16<1, 4, 4>, a, 256, nb, reps));
-  rep("16x16x32 D1 again", run(k16<1, 0>, a, 128, nb, reps));
   return 0;
 }
