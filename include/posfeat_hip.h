@@ -94,11 +94,14 @@ int posfeat_conv2d_nhwc_ws(const posfeat_conv_desc *d, const float *x, const flo
  * bf16 planes (h, m, l of the packed [cout][Kpad] array, plane stride wplane
  * elements; h = RNE_bf16(w), m = RNE_bf16(w - h), l = RNE_bf16(w - h - m)),
  * as the engine passes them: the pre-split tiles run (dense 1x1 convs: the
- * 16x16x32 conv_bf6x_kernel; others: conv_bf6d_kernel).  Replaces the same
- * reference convs as posfeat_conv2d_nhwc (networks/DescNet.py:167-190). */
+ * 16x16x32 conv_bf6x_kernel; others: conv_bf6d_kernel).  tile: -1 for the
+ * default plan, else a tile id the engine's autotuner may pick (ignored where
+ * illegal) -- every legal tile of a conv gives bit-identical results.
+ * Replaces the same reference convs as posfeat_conv2d_nhwc
+ * (networks/DescNet.py:167-190). */
 int posfeat_conv2d_nhwc_planes(const posfeat_conv_desc *d, const float *x, const float *w,
                                const unsigned short *wb, long long wplane, const float *bias,
-                               const float *res, float *y, void *ws, size_t ws_bytes,
+                               const float *res, float *y, void *ws, size_t ws_bytes, int tile,
                                void *stream);
 /* Conv (no residual, no activation) whose epilogue also reduces per-tile
  * channel sums for InstanceNorm2d (networks/DeteNet.py:12-22): writes y and

@@ -2767,9 +2767,11 @@ extern "C" int posfeat_conv2d_nhwc_ws(const posfeat_conv_desc* d, const float* x
 extern "C" int posfeat_conv2d_nhwc_planes(const posfeat_conv_desc* d, const float* x,
                                           const float* w, const unsigned short* wb,
                                           long long wplane, const float* bias, const float* res,
-                                          float* y, void* ws, size_t ws_bytes, void* stream) {
+                                          float* y, void* ws, size_t ws_bytes, int tile,
+                                          void* stream) {
   if (!wb || wplane <= 0) return POSFEAT_E_INVALID;
-  return pf_conv_run_tile(d, x, w, bias, res, y, ws, ws_bytes, -1, pf_stream(stream), wb, wplane);
+  return pf_conv_run_tile(d, x, w, bias, res, y, ws, ws_bytes, tile, pf_stream(stream), wb,
+                          wplane);
 }
 
 // Stats tiling: contiguous-row tiles may straddle two images (slot 1 holds the

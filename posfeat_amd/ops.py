@@ -85,7 +85,7 @@ def split_weight_planes(w_packed):
 
 
 def conv2d_nhwc_planes(x, w_packed, planes, bias, cout, kh, kw, stride=1, pad=None, act="none",
-                       res=None, out=None, cin=None, allow_split=False):
+                       res=None, out=None, cin=None, allow_split=False, tile=-1):
     """conv2d_nhwc with the weights also given as bf16 planes
     (split_weight_planes), as the engine runs its convs: the pre-split tiles
     (dense 1x1: the 16x16x32 conv_bf6x_kernel)."""
@@ -104,7 +104,7 @@ def conv2d_nhwc_planes(x, w_packed, planes, bias, cout, kh, kw, stride=1, pad=No
     ws = torch.empty(max(need, 16), dtype=torch.uint8, device=x.device)
     check(lib().posfeat_conv2d_nhwc_planes(ctypes.byref(d), ptr(x), ptr(w_packed), ptr(planes),
                                            planes[0].numel(), ptr(bias), ptr(res), ptr(out),
-                                           ptr(ws), need, stream_ptr()))
+                                           ptr(ws), need, tile, stream_ptr()))
     return out
 
 

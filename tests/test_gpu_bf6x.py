@@ -32,7 +32,10 @@ CASES = [  # n, h, w, cin, cout, act, residual, split, stride
     (1, 16, 20, 256, 96, "elu", True, False, 1),      # Cout % 64 != 0: ragged column tile
     (2, 60, 80, 512, 1024, "none", False, False, 2),  # layer3.0.downsample (stride 2)
     (1, 31, 41, 256, 128, "relu", True, False, 2),    # stride 2 on odd sizes + residual
+    (2, 6, 13, 1152, 192, "none", False, False, 1),   # the tap adjoint's K and N, M = 156
+    (1, 12, 13, 576, 192, "none", False, False, 1),   # head.conv1 Winograd GEMM shape
 ]
+TILES = (29, 30, 31)  # TILE_BF6X_128x128, _128x64, _256x128: each legal one, bit-identical
 
 
 @pytest.fixture
@@ -70,6 +73,10 @@ def test_bf6x_dense_conv_vs_fp64(gpu, precision, case):
     precision(1)
     y6 = ops.conv2d_nhwc_planes(xg, wp, planes, bb, cout, 1, 1, stride=stride, act=act, res=rg,
                                 allow_split=split).cpu().double()
+    for t in TILES:   # every tile the autotuner may pick: the same bits
+        yt = ops.conv2d_nhwc_planes(xg, wp, planes, bb, cout, 1, 1, stride=stride, act=act,
+                                    res=rg, allow_split=split, tile=t).cpu().double()
+        assert torch.equal(yt, y6), ("tile", t, float((yt - y6).abs().max()))
     precision(0)
     y32 = ops.conv2d_nhwc(xg, wp, bb, cout, 1, 1, stride=stride, act=act, res=rg).cpu().double()
     torch.cuda.synchronize()
