@@ -2212,6 +2212,7 @@ bool bf6_on() { return pf_conv_precision() >= 1; }
 // train-mode backbone, whose fp64-pinned gradient fixtures were validated on
 // them, bbtrain.hip)
 thread_local int tl_halo_fp32 = 0;
+thread_local int tl_dense32 = 0;  // PfDense32Scope
 bool halo_bf6_on() {
   static const bool off = [] {
     const char* e = getenv("POSFEAT_BF6_HALO");
@@ -2262,7 +2263,7 @@ bool bf6x_on() {
     const char* e = getenv("POSFEAT_BF6X");
     return e && e[0] == '0';
   }();
-  return bf6_on() && !off && tl_halo_fp32 == 0;
+  return bf6_on() && !off && tl_halo_fp32 == 0 && tl_dense32 == 0;
 }
 // 1x1, no padding, any stride (a strided 1x1 conv is a GEMM over the
 // subsampled pixel rows: conv_bf6x_kernel maps each row to its input pixel)
@@ -2664,6 +2665,8 @@ void launch_up4_weights(const float* w_packed, float* wph, hipStream_t st) {
 
 PfHaloFp32Scope::PfHaloFp32Scope() { ++tl_halo_fp32; }
 PfHaloFp32Scope::~PfHaloFp32Scope() { --tl_halo_fp32; }
+PfDense32Scope::PfDense32Scope(bool on) : on_(on) { tl_dense32 += on ? 1 : 0; }
+PfDense32Scope::~PfDense32Scope() { tl_dense32 -= on_ ? 1 : 0; }
 
 extern "C" int posfeat_conv_packed_k(int cin, int kh, int kw) {
   const int cinp = (cin + 3) / 4 * 4;

@@ -894,6 +894,9 @@ int image_branch(Ctx& c, const float* img4) {
 
 int forward(Ctx& c, const float* img, posfeat_extract_out* out, int mode, const float* xhead) {
   posfeat_model* m = c.m;
+  // the keypoint-head training instance keeps the 32x32x16 dense tiles
+  // (the head gradient's fixture case is ill-conditioned)
+  const PfDense32Scope dense32(m->train);
   const int B = m->B, H = m->H, W = m->W;
   const int h2 = H / 2, w2 = W / 2, h4 = H / 4, w4 = W / 4, h8 = H / 8, w8 = W / 8, h16 = H / 16,
             w16 = W / 16;
@@ -1337,6 +1340,7 @@ extern "C" int posfeat_model_head_backward(posfeat_model* m, const float* dlocal
   if (ws_bytes < m->ws_bytes) return POSFEAT_E_WORKSPACE;
   if (reinterpret_cast<uintptr_t>(ws) & 255) return POSFEAT_E_INVALID;
   Ctx c{m, static_cast<char*>(ws), pf_stream(stream)};
+  const PfDense32Scope dense32(true);
   return head_backward(c, dlocal_point, grad);
 }
 

@@ -157,6 +157,17 @@ struct PfHaloFp32Scope {
   PfHaloFp32Scope(const PfHaloFp32Scope&) = delete;
   PfHaloFp32Scope& operator=(const PfHaloFp32Scope&) = delete;
 };
+// While alive (and `on`), the calling thread's dense pre-split GEMMs run the
+// 32x32x16 bf6d tiles instead of the 16x16x32 conv_bf6x_kernel: the training
+// steps' forward / backward keep the arithmetic their fp64-pinned fixtures
+// validated (PfHaloFp32Scope implies it).
+struct PfDense32Scope {
+  explicit PfDense32Scope(bool on);
+  ~PfDense32Scope();
+  PfDense32Scope(const PfDense32Scope&) = delete;
+  PfDense32Scope& operator=(const PfDense32Scope&) = delete;
+  bool on_;
+};
 // bf16x6 GEMMs on pre-split operands (gemm6.hip).  POSFEAT_BF6=2 turns them on
 // for the Winograd transform-domain GEMMs and head.conv2's low-res tap GEMM.
 bool pf_bf6p_on();
