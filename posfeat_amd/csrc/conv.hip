@@ -2809,7 +2809,10 @@ static const int kAllTiles[] = {TILE_H8x128,      TILE_H8x64,       TILE_128x128
                                 TILE_BF6_128x128, TILE_BF6_128x256, TILE_BF6_64x128,
                                 TILE_BF6_128x64,  TILE_BF6B_128x128, TILE_BF6B_128x64,
                                 TILE_BF6R_128x128, TILE_BF6R_128x64,  TILE_BF6B_256x128,
-                                TILE_BF6X_128x128, TILE_BF6X_128x64, TILE_BF6X_256x128};
+                                TILE_BF6X_128x128, TILE_BF6X_128x64};
+// (TILE_BF6X_256x128 is legal where forced -- POSFEAT_CONV_TILE, the planes
+// ABI's tile argument -- but not an autotune candidate: never faster, and the
+// timing noise let it take the tap GEMM at +5 %, r7i)
 
 int pf_conv_candidates(const posfeat_conv_desc* d, int* tiles, int max, bool wplanes) {
   ConvArgs a;
