@@ -83,15 +83,19 @@ __global__ __launch_bounds__(128) void gfuse_weights_kernel(
 // is read coalesced across couts and reused for the RP pixels.  y == nullptr:
 // into the ring buffer ring[b][r][128] instead (r = the ring index below, the
 // order pf_ring_index in fmap.h restates), for up4tap_gcombine_kernel.
-constexpr int GF_RP = 8;
-__global__ __launch_bounds__(GF_COUT) void gfuse_ring_kernel(
+constexpr int GF_RP = 16;  // ring pixels per block (w2t, 295 KB, is read once per block)
+__global__ __launch_bounds__(2 * GF_COUT) void gfuse_ring_kernel(
     const float* __restrict__ c, int ccs, const float* __restrict__ img4,
     const float* __restrict__ w1, int k1pad, const float* __restrict__ b1, int H, int W,
     const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ w2t,
     const float* __restrict__ b2, float* __restrict__ y, int ycs, float* __restrict__ ring) {
-  const int b = blockIdx.y, co = threadIdx.x;
+  const int b = blockIdx.y, co = threadIdx.x % GF_COUT;
   const int nring = 2 * W + 2 * (H - 2);
-  __shared__ float g[GF_RP][9][GF_CG];
+  __shared__ __attribute__((aligned(16))) float g[GF_RP][9][GF_CG];
+  // convimg's input taps at every (ring pixel, conv2 tap) position, loaded
+  // once per block (the 64 channel threads share them): xs[j][t][s * 3 + ch]
+  __shared__ float xs[GF_RP][9][27];
+  __shared__ float w1s[GF_CG][27];
   __shared__ int pys[GF_RP], pxs[GF_RP];
   if (threadIdx.x < GF_RP) {
     int r = blockIdx.x * GF_RP + threadIdx.x, py = -1, px = -1;
@@ -113,7 +117,26 @@ __global__ __launch_bounds__(GF_COUT) void gfuse_ring_kernel(
     pys[threadIdx.x] = py;
     pxs[threadIdx.x] = px;
   }
+  if (!c) {
+    for (int i = threadIdx.x; i < GF_CG * 27; i += blockDim.x) {
+      const int k = i / 27, e = i - k * 27;
+      w1s[k][e] = w1[(size_t)k * k1pad + (e / 3) * 4 + e % 3];
+    }
+  }
   __syncthreads();
+  if (!c) {  // zero-padded image taps around each tap position q (0 outside the image)
+    for (int i = threadIdx.x; i < GF_RP * 9 * 27; i += blockDim.x) {
+      const int j = i / 243, rem = i - j * 243, t = rem / 27, e = rem - t * 27;
+      const int s9 = e / 3, ch = e - s9 * 3;
+      const int qy = pys[j] + t / 3 - 1, qx = pxs[j] + t % 3 - 1;
+      const int iy = qy + s9 / 3 - 1, ix = qx + s9 % 3 - 1;
+      float v = 0.f;
+      if (pys[j] >= 0 && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
+        v = img4[(((size_t)b * H + iy) * W + ix) * 4 + ch];
+      xs[j][t][e] = v;
+    }
+    __syncthreads();
+  }
   const float* mb = mean + (size_t)b * GF_CG;
   const float* rb = rstd + (size_t)b * GF_CG;
   for (int i = threadIdx.x; i < GF_RP * 9 * GF_CG; i += blockDim.x) {
@@ -125,14 +148,12 @@ __global__ __launch_bounds__(GF_COUT) void gfuse_ring_kernel(
       float cv;
       if (c) {
         cv = c[(((size_t)b * H + qy) * W + qx) * ccs + k];
-      } else {  // convimg at q from the image (zero padded), the conv's own tap order
+      } else {  // convimg at q, the conv's own tap order (zero taps add +0: exact)
         cv = b1[k];
-        for (int s = 0; s < 9; ++s) {
-          const int iy = qy + s / 3 - 1, ix = qx + s % 3 - 1;
-          if ((unsigned)iy >= (unsigned)H || (unsigned)ix >= (unsigned)W) continue;
-          const float* px = img4 + (((size_t)b * H + iy) * W + ix) * 4;
-          const float* wk = w1 + (size_t)k * k1pad + s * 4;
-          cv += wk[0] * px[0] + wk[1] * px[1] + wk[2] * px[2];
+        for (int s9 = 0; s9 < 9; ++s9) {
+          const float* xv = &xs[j][t][s9 * 3];
+          const float* wk = &w1s[k][s9 * 3];
+          cv += wk[0] * xv[0] + wk[1] * xv[1] + wk[2] * xv[2];
         }
       }
       v = (cv - mb[k]) * rb[k];
@@ -140,25 +161,38 @@ __global__ __launch_bounds__(GF_COUT) void gfuse_ring_kernel(
     g[j][t][k] = v;
   }
   __syncthreads();
-  float acc[GF_RP];
+  // two halves of the block take GF_RP / 2 ring pixels each (same cout)
+  constexpr int HP = GF_RP / 2;
+  const int j0 = (threadIdx.x / GF_COUT) * HP;
+  float acc[HP];
 #pragma unroll
-  for (int j = 0; j < GF_RP; ++j) acc[j] = b2[co];
-  for (int tk = 0; tk < 9 * GF_CG; ++tk) {
-    const float wv = w2t[(size_t)tk * GF_COUT + co];
+  for (int j = 0; j < HP; ++j) acc[j] = b2[co];
+  // four k per step: one broadcast ds_read_b128 of g per pixel, the same
+  // sequential accumulation order as one k at a time
+  for (int tk = 0; tk < 9 * GF_CG; tk += 4) {
+    float wv[4];
 #pragma unroll
-    for (int j = 0; j < GF_RP; ++j) acc[j] += wv * (&g[j][0][0])[tk];
+    for (int u = 0; u < 4; ++u) wv[u] = w2t[(size_t)(tk + u) * GF_COUT + co];
+#pragma unroll
+    for (int j = 0; j < HP; ++j) {
+      const f32x4 gv = *reinterpret_cast<const f32x4*>(&g[j0 + j][0][0] + tk);
+      acc[j] += wv[0] * gv.x;
+      acc[j] += wv[1] * gv.y;
+      acc[j] += wv[2] * gv.z;
+      acc[j] += wv[3] * gv.w;
+    }
   }
   if (!y) {
 #pragma unroll
-    for (int j = 0; j < GF_RP; ++j) {
-      const int r = blockIdx.x * GF_RP + j;
+    for (int j = 0; j < HP; ++j) {
+      const int r = blockIdx.x * GF_RP + j0 + j;
       if (r < nring) ring[((size_t)b * nring + r) * GF_COUT + co] = acc[j];
     }
     return;
   }
 #pragma unroll
-  for (int j = 0; j < GF_RP; ++j)
-    if (pys[j] >= 0) y[(((size_t)b * H + pys[j]) * W + pxs[j]) * ycs + co] = acc[j];
+  for (int j = 0; j < HP; ++j)
+    if (pys[j0 + j] >= 0) y[(((size_t)b * H + pys[j0 + j]) * W + pxs[j0 + j]) * ycs + co] = acc[j];
 }
 
 
@@ -706,7 +740,7 @@ int pf_gfuse_conv(const float* img4, const float* c, int ccs, int n, int H, int 
   (void)w2_packed;
   const int k1pad = posfeat_conv_packed_k(3, 3, 3);
   const int nring = 2 * W + 2 * (H - 2);
-  hipLaunchKernelGGL(gfuse_ring_kernel, dim3((nring + GF_RP - 1) / GF_RP, n), dim3(GF_COUT), 0, st,
+  hipLaunchKernelGGL(gfuse_ring_kernel, dim3((nring + GF_RP - 1) / GF_RP, n), dim3(2 * GF_COUT), 0, st,
                      c, ccs, img4, w1_packed, k1pad, b1, H, W, mean, rstd,
                      bc + (size_t)n * GF_COUT, b2, y, ycs, nullptr);
   PF_CHECK_LAUNCH();
@@ -730,7 +764,7 @@ int pf_gfuse_prep(const float* img4, const float* c, int ccs, int n, int H, int 
   hipLaunchKernelGGL(gfuse_wsplit_kernel, dim3((tot + 255) / 256), dim3(256), 0, st, wc, n,
                      wplanes);
   const int nring = 2 * W + 2 * (H - 2);
-  hipLaunchKernelGGL(gfuse_ring_kernel, dim3((nring + GF_RP - 1) / GF_RP, n), dim3(GF_COUT), 0, st,
+  hipLaunchKernelGGL(gfuse_ring_kernel, dim3((nring + GF_RP - 1) / GF_RP, n), dim3(2 * GF_COUT), 0, st,
                      c, ccs, img4, w1_packed, posfeat_conv_packed_k(3, 3, 3), b1, H, W, mean, rstd,
                      bc + (size_t)n * GF_COUT, b2, nullptr, 0, ring);
   PF_CHECK_LAUNCH();
