@@ -781,7 +781,10 @@ namespace {
 // split the tile reduction so the 36 x (Cout/128) x (Cin/128) GEMM tiles reach >= 2048
 // workgroups (1024..8192 measured within 1% of each other)
 int wino_wgrad_nsplit(long long T, int Cin, int Cout) {
-  const long long tiles = 36LL * (Cout / 128) * (Cin / 128);
+  // (Cin, Cout % 128 == 0 for every caller; guarded so no shape divides by 0 --
+  // tools/asan_host.py found posfeat_wino_wgrad_workspace(.., cin = 32, ..)
+  // raising SIGFPE here)
+  const long long tiles = std::max(1LL, 36LL * (Cout / 128) * (Cin / 128));
   long long s = (2048 + tiles - 1) / tiles;
   const long long chunks = (T + 63) / 64;
   s = std::min(s, std::max(1LL, chunks / 8));  // >= 8 row chunks per split
@@ -831,7 +834,10 @@ int pf_wino_wgrad(const float* dy, int ldy, const float* x, int xcs, int n, int 
 }
 
 extern "C" size_t posfeat_wino_wgrad_workspace(int n, int h, int w, int cin, int cout) {
-  if (n <= 0 || h <= 0 || w <= 0 || (h & 3) || (w & 3)) return 0;
+  // the shapes posfeat_conv3x3_wino_wgrad accepts (pf_wino_wgrad), else 0
+  if (n <= 0 || h <= 0 || w <= 0 || (h & 3) || (w & 3) || cin <= 0 || cout <= 0 || cin % 128 ||
+      cout % 128)
+    return 0;
   return pf_wino_wgrad_ws_bytes(n, h, w, cin, cout);
 }
 
