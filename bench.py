@@ -56,9 +56,9 @@ GEMM_LABEL_KERNELS = {
               "on the 120x160 grid as one [B*19200 x 192] x [192 x 1152] GEMM)",
     "": "the autotuned conv tile of %s (conv.hip MFMA implicit GEMM)",
 }
-# conv labels whose kernels keep fp32-input MFMA in every precision mode (the
-# Cin = 4 stem on the register-staged tiles)
-FP32_MFMA_LABELS = ("conv:firstconv",)
+# conv labels whose kernels keep fp32-input MFMA in every precision mode (none
+# since the 7x7 stem runs bf16x6 on the bf6x tile's tap gather, round 3)
+FP32_MFMA_LABELS = ()
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md, dense FP32 matrix (spec)
 PEAK_BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md, dense BF16 matrix (no sparsity)
 

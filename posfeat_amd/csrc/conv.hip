@@ -1392,7 +1392,7 @@ void conv_bf6s_kernel(ConvArgs a) {
 // the 16x16x32 instruction sums 32 products per step where 32x32x16 sums 16,
 // so results are NOT bit-identical to the 32x32 tiles (fp32-exact products,
 // different fp32 accumulation grouping); the GEMMs that use it use only it.
-template <int BN, int RB = 2>
+template <int BN, int RB = 2, bool G4 = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
 void conv_bf6x_kernel(ConvArgs a) {
   constexpr int NW = 4, BM = NW * RB * 16, NB = BN / 16;
@@ -1425,17 +1425,46 @@ void conv_bf6x_kernel(ConvArgs a) {
   const int m0 = tm * BM, n0 = tn * BN;
   const int r16 = lane & 15, kq = lane >> 4;
   const float* xrow[RB];
+  int ih0[RB], iw0[RB];  // G4: the row's top-left input tap
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb) {
     const int m = min(m0 + wave * RB * 16 + rb * 16 + r16, a.M - 1);
     long long pix = m;  // stride 1: output row m is input pixel m
-    if (a.stride != 1) {
+    if (a.stride != 1 || G4) {
       const int n = m / a.hw, rem = m - n * a.hw;
       const int oh = rem / a.OW, ow = rem - oh * a.OW;
       pix = ((long long)n * a.H + oh * a.stride) * a.W + ow * a.stride;
+      if (G4) {
+        ih0[rb] = oh * a.stride - a.pad;
+        iw0[rb] = ow * a.stride - a.pad;
+        pix = (long long)n * a.H * a.W;  // the image's base
+      }
     }
-    xrow[rb] = a.x + pix * a.xcs + kq * 8;
+    xrow[rb] = a.x + pix * a.xcs + (G4 ? 0 : kq * 8);
   }
+  // G4 (4-channel input, K order (kh, kw, c4)): load jj of a lane is tap
+  // t = 8 chunk + 2 kq + jj, tracked as (kh, kw) and advanced by 8 taps per
+  // chunk (KW in [5, 8]: one conditional wrap); outside the image or past the
+  // last tap the lane reads the zeroed 16-B word
+  int tkh[2] = {0, 0}, tkw[2] = {0, 0};
+  auto a_ptr = [&](int rb, int jj, int chunk) -> const float* {
+    if (!G4) return xrow[rb] + (long long)chunk * BK + jj * 4;
+    const int ih = ih0[rb] + tkh[jj], iw = iw0[rb] + tkw[jj];
+    const bool ok = tkh[jj] < a.KH && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+    return ok ? xrow[rb] + ((long long)ih * a.W + iw) * 4 : a.zero;
+  };
+  auto advance_taps = [&]() {
+    if (!G4) return;
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      tkw[jj] += 8 - a.KW;
+      tkh[jj] += 1;
+      if (tkw[jj] >= a.KW) {
+        tkw[jj] -= a.KW;
+        tkh[jj] += 1;
+      }
+    }
+  };
   const unsigned short* bsrc[B_G];
 #pragma unroll
   for (int i = 0; i < B_G; ++i) {
@@ -1456,6 +1485,14 @@ void conv_bf6x_kernel(ConvArgs a) {
     for (int nb = 0; nb < NB; ++nb) acc[rb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
   f32x4 va[RB][2];
   int la_c = ch0;  // chunk of the next A loads (clamped at the last: same count every step)
+  if (G4) {
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int t = ch0 * 8 + kq * 2 + jj;
+      tkh[jj] = t / a.KW;
+      tkw[jj] = t - tkh[jj] * a.KW;
+    }
+  }
   if (nch > 0) {
 #pragma unroll
     for (int i = 0; i < B_G; ++i)
@@ -1465,9 +1502,11 @@ void conv_bf6x_kernel(ConvArgs a) {
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        va[rb][j] = *reinterpret_cast<const f32x4*>(xrow[rb] + (long long)ch0 * BK + j * 4);
-    if (la_c + 1 < ch1) ++la_c;
+      for (int j = 0; j < 2; ++j) va[rb][j] = *reinterpret_cast<const f32x4*>(a_ptr(rb, j, ch0));
+    if (la_c + 1 < ch1) {
+      ++la_c;
+      advance_taps();
+    }
   }
   for (int ii = 0; ii < nch; ++ii) {
     __builtin_amdgcn_s_waitcnt(0);  // (vmcnt 0; lgkm too) B(ii) and A(ii) landed
@@ -1490,8 +1529,7 @@ void conv_bf6x_kernel(ConvArgs a) {
                   0, 0);
             } else if (op < NOPS) {
               const int j = op - B_G, rb = j >> 1, jj = j & 1;
-              va[rb][jj] =
-                  *reinterpret_cast<const f32x4*>(xrow[rb] + (long long)la_c * BK + jj * 4);
+              va[rb][jj] = *reinterpret_cast<const f32x4*>(a_ptr(rb, jj, la_c));
             }
             __builtin_amdgcn_sched_barrier(PF_SCHED_PIN_VMEM_MFMA);
             ++op;
@@ -1519,7 +1557,10 @@ void conv_bf6x_kernel(ConvArgs a) {
             while (op < (nb + 1) * NOPS / NB) mem();
           }
         });
-    if (la_c + 1 < ch1) ++la_c;
+    if (la_c + 1 < ch1) {
+      ++la_c;
+      advance_taps();
+    }
   }
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
@@ -2270,6 +2311,12 @@ bool bf6x_on() {
 bool dense_gemm(const ConvArgs& a) {
   return a.KH == 1 && a.KW == 1 && a.pad == 0 && a.wb && !a.xb;
 }
+// 4-channel input (NHWC4: the 7x7 stem), K order (kh, kw, c4): the bf6x tile
+// gathers each lane's two taps per chunk (conv_bf6x_kernel G4)
+bool g4_gemm(const ConvArgs& a) {
+  return a.Cin == 4 && a.xcs == 4 && a.KW >= 5 && a.KW <= 8 && a.wb && !a.xb &&
+         a.Kpad == (a.KH * a.KW * 4 + BK - 1) / BK * BK;
+}
 
 struct Plan {
   int kern, tile, bm, bn, ppi;  // ppi: patches per image (halo), 0 = contiguous rows
@@ -2350,7 +2397,8 @@ Plan plan_for_tile(const ConvArgs& a, int tile) {
     case TILE_BF6X_128x128:
     case TILE_BF6X_128x64:
     case TILE_BF6X_256x128:
-      if (!glds_ok || !bf6x_on() || !dense_gemm(a)) return p;
+      if (!bf6x_on() || !((glds_ok && dense_gemm(a)) || g4_gemm(a))) return p;
+      if (g4_gemm(a) && tile != TILE_BF6X_128x64) return p;
       p.kern = KERN_GLDS;
       p.bm = tile == TILE_BF6X_256x128 ? 256 : 128;
       p.bn = tile == TILE_BF6X_128x64 ? 64 : 128;
@@ -2409,6 +2457,9 @@ Plan plan_for_tile(const ConvArgs& a, int tile) {
     case TILE_64x64: p.bm = 64; p.bn = 64; break;
     default: return p;
   }
+  // the 4-channel-input convs the G4 bf6x tile serves: it is their only
+  // candidate (its sums are not bit-identical to the staged tiles')
+  if (bf6x_on() && g4_gemm(a)) return p;
   p.kern = !cin32 ? KERN_STAGED
                   : (conv_env().kmax >= KERN_GLDS && a.KH * a.KW <= 32 ? KERN_GLDS : KERN_STAGED);
   if (tile == TILE_256x128 && p.kern != KERN_GLDS) {
@@ -2449,6 +2500,10 @@ Plan conv_plan(const ConvArgs& a, bool allow_split, int forced = -1) {
       tile = TILE_64x64;
     d = plan_for_tile(a, tile);
     d.ksplit = tile == TILE_128x128 ? ks : 1;
+    if (bf6x_on() && g4_gemm(a)) {  // the stem: the G4 bf6x tile only
+      d = plan_for_tile(a, TILE_BF6X_128x64);
+      d.ksplit = 1;
+    }
     if (bf6_on() && cin32 && a.KH * a.KW <= 32 && env.kmax >= KERN_GLDS) {
       const bool x = bf6x_on() && dense_gemm(a);
       Plan b = plan_for_tile(a, x ? (a.Cout > 64 ? TILE_BF6X_128x128 : TILE_BF6X_128x64)
@@ -2556,8 +2611,12 @@ int conv_run(ConvArgs& a, const Plan& p, hipStream_t st) {
                          st, a);
       break;
     case TILE_BF6X_128x64:
-      hipLaunchKernelGGL((conv_bf6x_kernel<64>), dim3(a.nwg * a.ksplit, a.nbatch), dim3(256), 0,
-                         st, a);
+      if (a.Cin == 4)  // g4_gemm: the 4-channel tap gather
+        hipLaunchKernelGGL((conv_bf6x_kernel<64, 2, true>), dim3(a.nwg * a.ksplit, a.nbatch),
+                           dim3(256), 0, st, a);
+      else
+        hipLaunchKernelGGL((conv_bf6x_kernel<64>), dim3(a.nwg * a.ksplit, a.nbatch), dim3(256), 0,
+                           st, a);
       break;
     case TILE_BF6X_256x128:
       hipLaunchKernelGGL((conv_bf6x_kernel<128, 4>), dim3(a.nwg * a.ksplit, a.nbatch), dim3(256),

@@ -137,3 +137,38 @@ def test_bf6x_rb4_bit_identical(tmp_path):
         res[tag] = np.load(out)
     for k in ("lp", "lm", "gm"):
         np.testing.assert_array_equal(res["r4"][k], res["r2"][k], err_msg=k)
+
+
+@pytest.mark.parametrize("shape", [(2, 64, 96), (1, 37, 53), (3, 480, 640)])
+def test_bf6x_stem_gather_vs_fp64(gpu, precision, shape):
+    """The 7x7 stride-2 stem (4-channel NHWC4 input, K order (kh, kw, c4)) on
+    the bf6x tile with per-lane tap gathers (conv_bf6x_kernel G4): against fp64
+    within the bf16x6 bound, on even, odd and the metric's image sizes (zero
+    padding at every border, the zero fourth channel)."""
+    from posfeat_amd import ops
+    n, h, w = shape
+    g = torch.Generator().manual_seed(h * w)
+    x = torch.randn(n, 3, h, w, generator=g)
+    wt = torch.randn(64, 3, 7, 7, generator=g) / np.sqrt(147)
+    b = torch.randn(64, generator=g) * 0.1
+    pre = torch.nn.functional.conv2d(x.double(), wt.double(), b.double(), stride=2, padding=3)
+    ref = pre.clamp_min(0).permute(0, 2, 3, 1)
+    mag = torch.nn.functional.conv2d(x.double().abs(), wt.double().abs(), None, stride=2,
+                                     padding=3).permute(0, 2, 3, 1)
+    x4 = torch.zeros(n, h, w, 4)
+    x4[..., :3] = x.permute(0, 2, 3, 1)
+    xg = x4.contiguous().to(gpu)
+    wp, bb = ops.pack_conv_weight(wt.to(gpu), b.to(gpu))
+    planes = ops.split_weight_planes(wp)
+    precision(1)
+    y6 = ops.conv2d_nhwc_planes(xg, wp, planes, bb, 64, 7, 7, stride=2, pad=3, act="relu",
+                                cin=4).cpu().double()
+    precision(0)
+    y32 = ops.conv2d_nhwc(xg, wp, bb, 64, 7, 7, stride=2, pad=3, act="relu", cin=4).cpu().double()
+    torch.cuda.synchronize()
+    e32 = float((y32 - ref).abs().max())
+    e6 = float((y6 - ref).abs().max())
+    scale = float(mag.max())
+    print("stem", shape, "fp32 err %.3e  bf16x6 G4 err %.3e  scale %.3e" % (e32, e6, scale))
+    assert e6 <= 1.25 * e32 + 1e-7 * scale, (e6, e32)
+    assert e6 <= 2e-6 * scale
