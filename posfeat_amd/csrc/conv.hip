@@ -1392,9 +1392,13 @@ void conv_bf6s_kernel(ConvArgs a) {
 // the 16x16x32 instruction sums 32 products per step where 32x32x16 sums 16,
 // so results are NOT bit-identical to the 32x32 tiles (fp32-exact products,
 // different fp32 accumulation grouping); the GEMMs that use it use only it.
-template <int BN, int RB = 2, bool G4 = false>
+// AM: the A (pixel-row) operand -- 0 dense rows (1x1 convs, GEMMs), 1 G4:
+// 4-channel input taps (the stem), 2 GT: 32-channel slab x tap chunks (3x3 /
+// strided convs with Cin % 32 == 0, the packed K order (cin/32, kh, kw, cin%32))
+template <int BN, int RB = 2, int AM = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
 void conv_bf6x_kernel(ConvArgs a) {
+  constexpr bool G4 = AM == 1, GT = AM == 2;
   constexpr int NW = 4, BM = NW * RB * 16, NB = BN / 16;
   constexpr int B_G = 3 * BN / 16 / NW;  // B DMA instructions per wave per chunk
   constexpr int NA = 2 * RB;             // A loads per lane per chunk
@@ -1430,11 +1434,11 @@ void conv_bf6x_kernel(ConvArgs a) {
   for (int rb = 0; rb < RB; ++rb) {
     const int m = min(m0 + wave * RB * 16 + rb * 16 + r16, a.M - 1);
     long long pix = m;  // stride 1: output row m is input pixel m
-    if (a.stride != 1 || G4) {
+    if (a.stride != 1 || G4 || GT) {
       const int n = m / a.hw, rem = m - n * a.hw;
       const int oh = rem / a.OW, ow = rem - oh * a.OW;
       pix = ((long long)n * a.H + oh * a.stride) * a.W + ow * a.stride;
-      if (G4) {
+      if (G4 || GT) {
         ih0[rb] = oh * a.stride - a.pad;
         iw0[rb] = ow * a.stride - a.pad;
         pix = (long long)n * a.H * a.W;  // the image's base
@@ -1446,14 +1450,32 @@ void conv_bf6x_kernel(ConvArgs a) {
   // t = 8 chunk + 2 kq + jj, tracked as (kh, kw) and advanced by 8 taps per
   // chunk (KW in [5, 8]: one conditional wrap); outside the image or past the
   // last tap the lane reads the zeroed 16-B word
+  // GT: chunk = (slab, tap), tracked as (slab, kh, kw) and advanced by one
+  // tap per chunk; a tap outside the image reads the zeroed word
   int tkh[2] = {0, 0}, tkw[2] = {0, 0};
+  int g_slab = 0, g_kh = 0, g_kw = 0;
   auto a_ptr = [&](int rb, int jj, int chunk) -> const float* {
+    if (GT) {
+      const int ih = ih0[rb] + g_kh, iw = iw0[rb] + g_kw;
+      const bool ok = (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+      return ok ? xrow[rb] + ((long long)ih * a.W + iw) * a.xcs + g_slab * BK + jj * 4 : a.zero;
+    }
     if (!G4) return xrow[rb] + (long long)chunk * BK + jj * 4;
     const int ih = ih0[rb] + tkh[jj], iw = iw0[rb] + tkw[jj];
     const bool ok = tkh[jj] < a.KH && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
     return ok ? xrow[rb] + ((long long)ih * a.W + iw) * 4 : a.zero;
   };
   auto advance_taps = [&]() {
+    if (GT) {
+      if (++g_kw == a.KW) {
+        g_kw = 0;
+        if (++g_kh == a.KH) {
+          g_kh = 0;
+          ++g_slab;
+        }
+      }
+      return;
+    }
     if (!G4) return;
 #pragma unroll
     for (int jj = 0; jj < 2; ++jj) {
@@ -1492,6 +1514,12 @@ void conv_bf6x_kernel(ConvArgs a) {
       tkh[jj] = t / a.KW;
       tkw[jj] = t - tkh[jj] * a.KW;
     }
+  }
+  if (GT) {
+    const int ntap = a.KH * a.KW, tap = ch0 % ntap;
+    g_slab = ch0 / ntap;
+    g_kh = tap / a.KW;
+    g_kw = tap - g_kh * a.KW;
   }
   if (nch > 0) {
 #pragma unroll
@@ -2311,6 +2339,12 @@ bool bf6x_on() {
 bool dense_gemm(const ConvArgs& a) {
   return a.KH == 1 && a.KW == 1 && a.pad == 0 && a.wb && !a.xb;
 }
+// Cin % 32 == 0 convs with taps or padding (3x3 stride 1 / 2): the bf6x tile
+// gathers each lane's rows per (slab, tap) chunk (conv_bf6x_kernel GT)
+bool gt_gemm(const ConvArgs& a) {
+  return a.Cin % BK == 0 && !(a.KH == 1 && a.KW == 1 && a.pad == 0) && a.KH * a.KW <= 32 &&
+         a.wb && !a.xb;
+}
 // 4-channel input (NHWC4: the 7x7 stem), K order (kh, kw, c4): the bf6x tile
 // gathers each lane's two taps per chunk (conv_bf6x_kernel G4)
 bool g4_gemm(const ConvArgs& a) {
@@ -2387,17 +2421,22 @@ Plan plan_for_tile(const ConvArgs& a, int tile) {
   // bf16x6 mode: halo-eligible convs keep fp32 halo tiles only, the rest
   // bf16x6 row tiles only
   if (bf6_on() && glds_ok) {
-    const bool bf6_tile = tile >= TILE_BF6_128x128 && tile <= TILE_BF6X_256x128;
-    if (halo_ok ? bf6_tile || tile < TILE_H8x128 : !bf6_tile) return p;
-    // dense pre-split GEMMs: the 16x16x32 tiles only (and only they)
+    // pre-split convs on the bf6x tiles (dense GEMMs, slab x tap gathers):
+    // the 16x16x32 tiles only, and only they
     const bool x_tile = tile >= TILE_BF6X_128x128 && tile <= TILE_BF6X_256x128;
-    if (x_tile != (bf6x_on() && dense_gemm(a))) return p;
+    if (bf6x_on() && (dense_gemm(a) || gt_gemm(a))) {
+      if (!x_tile) return p;
+    } else {
+      if (x_tile) return p;
+      const bool bf6_tile = tile >= TILE_BF6_128x128 && tile <= TILE_BF6B_256x128;
+      if (halo_ok ? bf6_tile || tile < TILE_H8x128 : !bf6_tile) return p;
+    }
   }
   switch (tile) {
     case TILE_BF6X_128x128:
     case TILE_BF6X_128x64:
     case TILE_BF6X_256x128:
-      if (!bf6x_on() || !((glds_ok && dense_gemm(a)) || g4_gemm(a))) return p;
+      if (!bf6x_on() || !((glds_ok && (dense_gemm(a) || gt_gemm(a))) || g4_gemm(a))) return p;
       if (g4_gemm(a) && tile != TILE_BF6X_128x64) return p;
       p.kern = KERN_GLDS;
       p.bm = tile == TILE_BF6X_256x128 ? 256 : 128;
@@ -2515,6 +2554,15 @@ Plan conv_plan(const ConvArgs& a, bool allow_split, int forced = -1) {
       }
     }
   }
+  // Cin % 32 convs with taps on the pre-split planes: the GT bf6x tile
+  if (bf6x_on() && gt_gemm(a) && env.kmax >= KERN_GLDS) {
+    Plan b = plan_for_tile(a, a.Cout > 64 ? TILE_BF6X_128x128 : TILE_BF6X_128x64);
+    if (b.kern >= 0) {
+      const long long t128 = (long long)((a.M + 127) / 128) * ((a.Cout + 127) / 128);
+      b.ksplit = allow_split ? choose_ksplit(t128, nch, 768.0) : 1;
+      d = b;
+    }
+  }
   if (forced >= 0) {
     Plan f = plan_for_tile(a, forced);
     if (f.kern >= 0) {
@@ -2607,20 +2655,31 @@ int conv_run(ConvArgs& a, const Plan& p, hipStream_t st) {
                            dim3(a.nwg * a.ksplit, a.nbatch), dim3(256), 0, st, a);
       break;
     case TILE_BF6X_128x128:
-      hipLaunchKernelGGL((conv_bf6x_kernel<128>), dim3(a.nwg * a.ksplit, a.nbatch), dim3(256), 0,
-                         st, a);
+      if (dense_gemm(a))
+        hipLaunchKernelGGL((conv_bf6x_kernel<128>), dim3(a.nwg * a.ksplit, a.nbatch), dim3(256),
+                           0, st, a);
+      else  // gt_gemm: the slab x tap gather
+        hipLaunchKernelGGL((conv_bf6x_kernel<128, 2, 2>), dim3(a.nwg * a.ksplit, a.nbatch),
+                           dim3(256), 0, st, a);
       break;
     case TILE_BF6X_128x64:
       if (a.Cin == 4)  // g4_gemm: the 4-channel tap gather
-        hipLaunchKernelGGL((conv_bf6x_kernel<64, 2, true>), dim3(a.nwg * a.ksplit, a.nbatch),
+        hipLaunchKernelGGL((conv_bf6x_kernel<64, 2, 1>), dim3(a.nwg * a.ksplit, a.nbatch),
                            dim3(256), 0, st, a);
-      else
+      else if (dense_gemm(a))
         hipLaunchKernelGGL((conv_bf6x_kernel<64>), dim3(a.nwg * a.ksplit, a.nbatch), dim3(256), 0,
                            st, a);
+      else
+        hipLaunchKernelGGL((conv_bf6x_kernel<64, 2, 2>), dim3(a.nwg * a.ksplit, a.nbatch),
+                           dim3(256), 0, st, a);
       break;
     case TILE_BF6X_256x128:
-      hipLaunchKernelGGL((conv_bf6x_kernel<128, 4>), dim3(a.nwg * a.ksplit, a.nbatch), dim3(256),
-                         0, st, a);
+      if (dense_gemm(a))
+        hipLaunchKernelGGL((conv_bf6x_kernel<128, 4>), dim3(a.nwg * a.ksplit, a.nbatch),
+                           dim3(256), 0, st, a);
+      else
+        hipLaunchKernelGGL((conv_bf6x_kernel<128, 4, 2>), dim3(a.nwg * a.ksplit, a.nbatch),
+                           dim3(256), 0, st, a);
       break;
     case TILE_BF6B_128x128:
     case TILE_BF6B_128x64: {

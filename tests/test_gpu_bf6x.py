@@ -172,3 +172,56 @@ def test_bf6x_stem_gather_vs_fp64(gpu, precision, shape):
     print("stem", shape, "fp32 err %.3e  bf16x6 G4 err %.3e  scale %.3e" % (e32, e6, scale))
     assert e6 <= 1.25 * e32 + 1e-7 * scale, (e6, e32)
     assert e6 <= 2e-6 * scale
+
+
+GT_CASES = [  # n, h, w, cin, cout, k, stride, act, residual
+    (2, 30, 40, 64, 64, 3, 1, "relu", False),     # layer1 conv2 shape (scaled)
+    (1, 33, 41, 64, 96, 3, 1, "elu", True),       # ragged M and N, residual
+    (2, 30, 40, 128, 128, 3, 2, "relu", False),   # layer2.0 conv2 (stride 2)
+    (1, 17, 23, 256, 256, 3, 2, "none", False),   # odd sizes, stride 2
+    (1, 12, 20, 512, 128, 3, 1, "none", False),   # K = 144 chunks
+]
+
+
+@pytest.mark.parametrize("case", GT_CASES)
+def test_bf6x_slab_tap_gather_vs_fp64(gpu, precision, case):
+    """3x3 convs with Cin % 32 == 0 on the bf6x tile's (slab, tap) gather
+    (conv_bf6x_kernel GT): against fp64 within the bf16x6 bound, zero padding
+    at every border, strides 1 and 2; every legal BF6X tile bit-identical."""
+    from posfeat_amd import ops
+    n, h, w, cin, cout, k, stride, act, residual = case
+    g = torch.Generator().manual_seed(cin * 3 + cout + stride)
+    x = torch.randn(n, cin, h, w, generator=g)
+    wt = torch.randn(cout, cin, k, k, generator=g) / np.sqrt(cin * k * k)
+    b = torch.randn(cout, generator=g) * 0.1
+    pre = torch.nn.functional.conv2d(x.double(), wt.double(), b.double(), stride=stride,
+                                     padding=1).permute(0, 2, 3, 1)
+    oh, ow = pre.shape[1], pre.shape[2]
+    r = torch.randn(n, oh, ow, cout, generator=g) if residual else None
+    if residual:
+        pre = pre + r.double()
+    ref = {"none": pre, "relu": pre.clamp_min(0), "elu": torch.nn.functional.elu(pre)}[act]
+    mag = torch.nn.functional.conv2d(x.double().abs(), wt.double().abs(), None, stride=stride,
+                                     padding=1).permute(0, 2, 3, 1)
+    if residual:
+        mag = mag + r.double().abs()
+    xg = x.permute(0, 2, 3, 1).contiguous().to(gpu)
+    wp, bb = ops.pack_conv_weight(wt.to(gpu), b.to(gpu))
+    planes = ops.split_weight_planes(wp)
+    rg = r.to(gpu) if residual else None
+    precision(1)
+    y6 = ops.conv2d_nhwc_planes(xg, wp, planes, bb, cout, k, k, stride=stride, act=act,
+                                res=rg).cpu().double()
+    for t in TILES:
+        yt = ops.conv2d_nhwc_planes(xg, wp, planes, bb, cout, k, k, stride=stride, act=act,
+                                    res=rg, tile=t).cpu().double()
+        assert torch.equal(yt, y6), ("tile", t, float((yt - y6).abs().max()))
+    precision(0)
+    y32 = ops.conv2d_nhwc(xg, wp, bb, cout, k, k, stride=stride, act=act, res=rg).cpu().double()
+    torch.cuda.synchronize()
+    e32 = float((y32 - ref).abs().max())
+    e6 = float((y6 - ref).abs().max())
+    scale = float(mag.max())
+    print("gt", case, "fp32 err %.3e  bf16x6 GT err %.3e  scale %.3e" % (e32, e6, scale))
+    assert e6 <= 1.25 * e32 + 1e-7 * scale, (e6, e32)
+    assert e6 <= 2e-6 * scale
