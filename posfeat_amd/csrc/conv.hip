@@ -1392,6 +1392,13 @@ void conv_bf6s_kernel(ConvArgs a) {
 // the 16x16x32 instruction sums 32 products per step where 32x32x16 sums 16,
 // so results are NOT bit-identical to the 32x32 tiles (fp32-exact products,
 // different fp32 accumulation grouping); the GEMMs that use it use only it.
+// 16-B slot swizzle of the B stage rows for the 16x16x32 reads: lane l reads
+// row (l & 15) of a 16-row block at logical slot l >> 4; with physical slot =
+// logical ^ g((row >> 2) & 3), g = (0, 2, 3, 1), the 16 lanes of each
+// ds_read_b128 lane group (MI355X_MICROARCH.md LDS table) hit 16 distinct
+// 4-bank groups (the bf6d swizzle g = identity left them 2-way conflicted)
+__device__ __forceinline__ int bx_swz(int row) { return (0x78 >> (2 * ((row >> 2) & 3))) & 3; }
+
 // AM: the A (pixel-row) operand -- 0 dense rows (1x1 convs, GEMMs), 1 G4:
 // 4-channel input taps (the stem), 2 GT: 32-channel slab x tap chunks (3x3 /
 // strided convs with Cin % 32 == 0, the packed K order (cin/32, kh, kw, cin%32))
@@ -1492,7 +1499,7 @@ void conv_bf6x_kernel(ConvArgs a) {
   for (int i = 0; i < B_G; ++i) {
     const int pr = (wave * B_G + i) * 16 + (lane >> 2);
     const int plane = pr / BN, row = pr - plane * BN;
-    const int ks = (lane & 3) ^ ((row >> 2) & 3);
+    const int ks = (lane & 3) ^ bx_swz(row);
     bsrc[i] = wb + plane * a.wplane + (long long)min(n0 + row, a.Cout - 1) * a.Kpad + ks * 8;
   }
   const int nch_all = a.Kpad / BK;
@@ -1565,7 +1572,7 @@ void conv_bf6x_kernel(ConvArgs a) {
 #pragma unroll
           for (int nb = 0; nb < NB; ++nb) {
             const int row = nb * 16 + r16;
-            const int slot = kq ^ ((row >> 2) & 3);
+            const int slot = kq ^ bx_swz(row);
             const unsigned short* bp = Bb + row * BK + slot * 8;
             const u32x4_t bh = *reinterpret_cast<const u32x4_t*>(bp);
             const u32x4_t bm = *reinterpret_cast<const u32x4_t*>(bp + BN * BK);
