@@ -2296,15 +2296,6 @@ bool halo_bf6_on() {
   }();
   return bf6_on() && !off && tl_halo_fp32 == 0;
 }
-// LDS stages of the bf16x6 row tiles (POSFEAT_BF6_NST: 2, 3 or 4)
-int bf6_nst() {
-  static const int n = [] {
-    const char* e = getenv("POSFEAT_BF6_NST");
-    const int v = e ? atoi(e) : 2;
-    return v == 3 || v == 4 ? v : 2;
-  }();
-  return n;
-}
 // Dense pre-split tiles (TILE_BF6B_*) and the register-A candidates
 // (TILE_BF6R_*: any conv, masked taps included) run conv_bf6d_kernel with A
 // prefetched POSFEAT_BF6D = 2..4 chunks ahead in registers (default 2; 0: the
@@ -2387,18 +2378,7 @@ const ConvEnv& conv_env() {
 // Split-K factor: only for deep K (>= 64 chunks) where the tile count leaves
 // the last round of resident workgroups badly underfilled.
 int choose_ksplit(long long tiles, int nch, double slots) {
-  // POSFEAT_CONV_SPLIT_SMALL=1 (A/B, off): underfilled grids (fewer tiles
-  // than CUs, e.g. layer3's M = 9600 x 256 1x1 convs) split a shorter K too;
-  // measured r3v: layer3 1x1 0.057 -> 0.050 ms, the step no faster (797 vs 800)
-  static const bool small = [] {
-    const char* e = getenv("POSFEAT_CONV_SPLIT_SMALL");
-    return e && e[0] == '1';
-  }();
-  if (small && tiles < 256 && nch >= 16) {
-    int ks = 1;
-    while (ks < 4 && tiles * (ks + 1) <= 512 && nch / (ks + 1) >= 8) ++ks;
-    return ks;
-  }
+  // (splitting underfilled grids' shorter K too was measured no faster, r3v)
   if (nch < 64) return 1;
   int best = 1;
   double best_eff = 0.0;
@@ -2580,10 +2560,6 @@ Plan conv_plan(const ConvArgs& a, bool allow_split, int forced = -1) {
   return d;
 }
 
-bool glds3_on() {
-  const char* e = getenv("POSFEAT_GLDS3");
-  return e && e[0] == '1';
-}
 
 // The Cin = 4 register-staged convs (the stem) in bf16x6 with the rest of the
 // conv family (POSFEAT_BF6_STEM=0: fp32 MFMA); the train-mode backbone keeps
@@ -2600,9 +2576,7 @@ bool stem_bf6_on() {
 template <int BM, int BN, int WM, int WN>
 void launch_rows(ConvArgs& a, int kern, hipStream_t st) {
   dim3 grid(a.nwg * a.ksplit, a.nbatch), block(WM * WN * 64);
-  if (kern == KERN_GLDS && BM >= 128 && BN >= 128 && glds3_on())
-    hipLaunchKernelGGL((conv_glds_kernel<BM, BN, WM, WN, 3>), grid, block, 0, st, a);
-  else if (kern == KERN_GLDS)
+  if (kern == KERN_GLDS)
     hipLaunchKernelGGL((conv_glds_kernel<BM, BN, WM, WN>), grid, block, 0, st, a);
   else if (a.Cin % BK == 0)
     hipLaunchKernelGGL((conv_mfma_kernel<BM, BN, WM, WN, true>), grid, block, 0, st, a);
@@ -2635,15 +2609,8 @@ int conv_run(ConvArgs& a, const Plan& p, hipStream_t st) {
       hipLaunchKernelGGL((conv_halo_kernel<16, 128, 4, 2, 3, 3>), grid, dim3(512), 0, st, a);
       break;
     case TILE_BF6_128x128:
-      if (bf6_nst() == 4)
-        hipLaunchKernelGGL((conv_glds_kernel<128, 128, 2, 2, 4, true>),
-                           dim3(a.nwg * a.ksplit, a.nbatch), dim3(256), 0, st, a);
-      else if (bf6_nst() == 3)
-        hipLaunchKernelGGL((conv_glds_kernel<128, 128, 2, 2, 3, true>),
-                           dim3(a.nwg * a.ksplit, a.nbatch), dim3(256), 0, st, a);
-      else
-        hipLaunchKernelGGL((conv_glds_kernel<128, 128, 2, 2, 2, true>),
-                           dim3(a.nwg * a.ksplit, a.nbatch), dim3(256), 0, st, a);
+      hipLaunchKernelGGL((conv_glds_kernel<128, 128, 2, 2, 2, true>),
+                         dim3(a.nwg * a.ksplit, a.nbatch), dim3(256), 0, st, a);
       break;
     case TILE_BF6_128x256:
       hipLaunchKernelGGL((conv_glds_kernel<128, 256, 2, 2, 2, true>), dim3(a.nwg * a.ksplit, a.nbatch),
@@ -2654,12 +2621,8 @@ int conv_run(ConvArgs& a, const Plan& p, hipStream_t st) {
                          dim3(256), 0, st, a);
       break;
     case TILE_BF6_128x64:
-      if (bf6_nst() == 4)
-        hipLaunchKernelGGL((conv_glds_kernel<128, 64, 2, 2, 4, true>),
-                           dim3(a.nwg * a.ksplit, a.nbatch), dim3(256), 0, st, a);
-      else
-        hipLaunchKernelGGL((conv_glds_kernel<128, 64, 2, 2, 2, true>),
-                           dim3(a.nwg * a.ksplit, a.nbatch), dim3(256), 0, st, a);
+      hipLaunchKernelGGL((conv_glds_kernel<128, 64, 2, 2, 2, true>),
+                         dim3(a.nwg * a.ksplit, a.nbatch), dim3(256), 0, st, a);
       break;
     case TILE_BF6X_128x128:
       if (dense_gemm(a))
@@ -3217,11 +3180,6 @@ int pf_gemm_batched(const float* A, int lda, long long sa, const float* B, long 
   const long long t128 = (long long)((M + 127) / 128) * ((N + 127) / 128) * nb;
   // N = 192 (head.conv1's Winograd GEMMs) on pre-split planes: three 64-wide
   // column tiles instead of two 128-wide ones, the second of them half empty
-  // (POSFEAT_GEMM_N64=0: the 128-wide tiles, A/B)
-  static const bool n64 = [] {
-    const char* e = getenv("POSFEAT_GEMM_N64");
-    return !(e && e[0] == '0');
-  }();
   // POSFEAT_GEMM_B256=1 (A/B): the 8-wave 256x128 pre-split tiles
   static const bool b256 = [] {
     const char* e = getenv("POSFEAT_GEMM_B256");
@@ -3237,7 +3195,7 @@ int pf_gemm_batched(const float* A, int lda, long long sa, const float* B, long 
                                      : TILE_BF6X_128x64)
                    : (Bb && b256 && N % 128 == 0) ? TILE_BF6B_256x128
                    : (N % 128 == 0 && t128 >= 1024) ? TILE_128x128
-                   : (Bb && n64 && N % 128 != 0 && N % 64 == 0) ? TILE_BF6B_128x64
+                   : (Bb && N % 128 != 0 && N % 64 == 0) ? TILE_BF6B_128x64
                                                                  : -1;
   const Plan p = conv_plan(a, false, want);
   if (p.kern != KERN_GLDS) return POSFEAT_E_UNSUPPORTED;

@@ -829,15 +829,8 @@ int image_branch(Ctx& c, const float* img4) {
       // every later extract fail on a null event)
       hipStream_t st = nullptr;
       hipEvent_t ef = nullptr, ej = nullptr;
-      // POSFEAT_SIDE_PRIO=1 (A/B): the side stream at the device's lowest
-      // priority, so the main stream's workgroups dispatch first
-      static const bool low = [] {
-        const char* e = getenv("POSFEAT_SIDE_PRIO");
-        return e && e[0] == '1';
-      }();
-      int plo = 0, phi = 0;
-      if (low) (void)hipDeviceGetStreamPriorityRange(&plo, &phi);
-      if (hipStreamCreateWithPriority(&st, hipStreamNonBlocking, plo) != hipSuccess ||
+      // (the side stream at the lowest priority was measured within noise, r5w)
+      if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess ||
           hipEventCreateWithFlags(&ef, hipEventDisableTiming) != hipSuccess ||
           hipEventCreateWithFlags(&ej, hipEventDisableTiming) != hipSuccess) {
         if (ef) (void)hipEventDestroy(ef);

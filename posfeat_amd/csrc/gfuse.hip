@@ -780,14 +780,9 @@ int pf_gfuse_imgstats(const float* img4, int n, int H, int W, const float* w1_pa
                       const float* b1, float* mean, float* rstd, void* ws, size_t ws_bytes,
                       hipStream_t st, double* gram) {
   if (!ws || ws_bytes < pf_gfuse_imgstats_ws_bytes(n, H)) return POSFEAT_E_WORKSPACE;
-  // blocks per image (POSFEAT_IMGMOM_BLOCKS; default one per band -- r3x: 8 or
-  // 16 band-looping blocks per image were no faster); partials = blocks
-  static const int per_img_env = [] {
-    const char* e = getenv("POSFEAT_IMGMOM_BLOCKS");
-    return e ? atoi(e) : 0;
-  }();
-  const int nb_all = (H + IM_ROWS - 1) / IM_ROWS;
-  const int nband = per_img_env > 0 ? std::max(1, std::min(nb_all, per_img_env)) : nb_all;
+  // one block per band of rows (r3x: 8 or 16 band-looping blocks per image
+  // were no faster); partials = blocks
+  const int nband = (H + IM_ROWS - 1) / IM_ROWS;
   const size_t lds = std::max((size_t)(IM_ROWS + 2) * (W + 2) * 3 * sizeof(float),
                               (size_t)4 * IM_G * IM_G * sizeof(double));
   if (lds > 160 * 1024 || W % 2) return POSFEAT_E_UNSUPPORTED;
