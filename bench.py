@@ -684,6 +684,7 @@ def corr_main(args, world, rank, dev):
     kms = e0.elapsed_time(e1) / reps
     kfl = 2.0 * b * n * n * 128
     ach = kfl / (kms * 1e-3) / 1e12
+    arith = conv_arithmetic()   # the flash passes follow the conv precision mode
     if rank == 0:
         rec = {
             "metric": "pairs/sec correlation losses + map gradients (640x480: Line2Window + "
@@ -702,8 +703,9 @@ def corr_main(args, world, rank, dev):
             "roofline": {"kernel": "disk_flash_kernel<LSE> (DiskLoss softmax normaliser: MFMA "
                                    "similarity + online logsumexp, S never stored)",
                          "bound": "mfma", "achieved": round(ach, 3),
-                         "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(ach / PEAK_FP32_MFMA_TFLOPS, 4), "traffic": None,
+                         "peak": arith["method_peak"], "unit": "TFLOP/s",
+                         "frac": round(ach / arith["method_peak"], 4), "traffic": None,
+                         "arithmetic": arith["arithmetic"],
                          "avg_launch_ms": round(kms, 4), "flop_per_launch": kfl},
         }
         print(json.dumps(rec), flush=True)

@@ -35,6 +35,7 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "fmap.h"
 
 int pf_sample_desc(const float* fmap, int b, int c, int h, int w, int cs, const float* coord,
                    int npts, const int32_t* n_valid, int normalize, float* out, hipStream_t st);
@@ -405,7 +406,13 @@ struct FlashArgs {
   double* r_part;           // SUM (want_r): [b][split][n] sum reward p (logp terms)
 };
 
-template <bool SUM>
+// BF6: the similarity products as bf16x6 on v_mfma_f32_32x32x16_bf16 (six
+// bf16 products per fp32 product, fp32-exact per product: conv.hip split3):
+// B's column (this lane's 128 k) is split once into three bf16 planes held in
+// registers, A's fragments are split as they are read from LDS; 16x the
+// matrix rate of the fp32-input MFMA, a third of its instructions' cycles per
+// product.  The default (conv precision >= 1); fp32 MFMA otherwise.
+template <bool SUM, bool BF6 = false>
 __global__ __launch_bounds__(256) void disk_flash_kernel(FlashArgs a, int want_r) {
   __shared__ __attribute__((aligned(16))) float As[2 * FSTEP * FD];  // 2 x 32 KB
   __shared__ float meta[2][FSTEP][8];  // SUM: lse, line(3), cpx(2), logp per A row
@@ -421,11 +428,22 @@ __global__ __launch_bounds__(256) void disk_flash_kernel(FlashArgs a, int want_r
   const int cl = cbase + wave * 32 + (lane & 31);
   const bool cok = cl < ncolB;
   const int cpt = SUM ? a.B.idx[pb + min(cl, ncolB - 1)] : min(cl, ncolB - 1);  // point id
-  f32x4 breg[FD / 8];
+  f32x4 breg[BF6 ? 1 : FD / 8];
+  g6_u32x4 bpl[BF6 ? FD / 16 : 1][3];  // BF6: per k16 group the h, m, l operands
   {
     const float* brow = a.B.f + (pb + cpt) * FD;
+    if (BF6) {
 #pragma unroll
-    for (int g = 0; g < FD / 8; ++g) breg[g] = *reinterpret_cast<const f32x4*>(brow + 8 * g + 4 * h);
+      for (int g = 0; g < FD / 16; ++g) {
+        const f32x4 q0 = *reinterpret_cast<const f32x4*>(brow + 16 * g + 8 * h);
+        const f32x4 q1 = *reinterpret_cast<const f32x4*>(brow + 16 * g + 8 * h + 4);
+        g6_split(q0, q1, bpl[g][0], bpl[g][1], bpl[g][2]);
+      }
+    } else {
+#pragma unroll
+      for (int g = 0; g < FD / 8; ++g)
+        breg[g] = *reinterpret_cast<const f32x4*>(brow + 8 * g + 4 * h);
+    }
   }
   float bl = 0.f, bl0 = 0.f, bl1 = 0.f, bl2 = 0.f, bx = 0.f, by = 0.f, blp = 0.f;
   if (SUM) {
@@ -479,7 +497,35 @@ __global__ __launch_bounds__(256) void disk_flash_kernel(FlashArgs a, int want_r
     f32x16 accs[2];
 #pragma unroll
     for (int r = 0; r < 16; ++r) accs[0][r] = accs[1][r] = 0.f;
-    {
+    if (BF6) {
+      // k16 group g: lane (row la, half h) supplies k = 16 g + 8 h .. + 7, the
+      // 16-B slots 4 g + 2 h and 4 g + 2 h + 1 of its LDS row (swizzled by la & 15)
+      const int la = lane & 31;
+      const float* arow0 = Ab + la * FD;
+      const float* arow1 = Ab + (32 + la) * FD;
+#pragma unroll
+      for (int g = 0; g < FD / 16; ++g) {
+        const int o0 = ((4 * g + 2 * h) ^ (la & 15)) * 4, o1 = ((4 * g + 2 * h + 1) ^ (la & 15)) * 4;
+        g6_u32x4 ah0, am0, al0, ah1, am1, al1;
+        g6_split(*reinterpret_cast<const f32x4*>(arow0 + o0),
+                 *reinterpret_cast<const f32x4*>(arow0 + o1), ah0, am0, al0);
+        g6_split(*reinterpret_cast<const f32x4*>(arow1 + o0),
+                 *reinterpret_cast<const f32x4*>(arow1 + o1), ah1, am1, al1);
+        const g6_u32x4 &bh = bpl[g][0], &bm = bpl[g][1], &bl = bpl[g][2];
+        accs[0] = g6_mfma(ah0, bh, accs[0]);
+        accs[1] = g6_mfma(ah1, bh, accs[1]);
+        accs[0] = g6_mfma(ah0, bm, accs[0]);
+        accs[1] = g6_mfma(ah1, bm, accs[1]);
+        accs[0] = g6_mfma(am0, bh, accs[0]);
+        accs[1] = g6_mfma(am1, bh, accs[1]);
+        accs[0] = g6_mfma(ah0, bl, accs[0]);
+        accs[1] = g6_mfma(ah1, bl, accs[1]);
+        accs[0] = g6_mfma(al0, bh, accs[0]);
+        accs[1] = g6_mfma(al1, bh, accs[1]);
+        accs[0] = g6_mfma(am0, bm, accs[0]);
+        accs[1] = g6_mfma(am1, bm, accs[1]);
+      }
+    } else {
       const int la = lane & 31;  // rows la and 32 + la share the swizzle (la & 15)
       const float* arow0 = Ab + la * FD;
       const float* arow1 = Ab + (32 + la) * FD;
@@ -645,6 +691,16 @@ int flash_nsplit(int n, int nb) {
 }
 
 // read per call (a few getenv per loss) so tests can A/B both paths in-process
+// the flash passes' product arithmetic follows the conv precision mode
+// (posfeat_set_conv_precision: >= 1 bf16x6, the default; 0 fp32 MFMA)
+template <bool SUM>
+void launch_flash(dim3 grid, hipStream_t st, const FlashArgs& fa, int want_r) {
+  if (pf_conv_precision() >= 1)
+    hipLaunchKernelGGL((disk_flash_kernel<SUM, true>), grid, dim3(256), 0, st, fa, want_r);
+  else
+    hipLaunchKernelGGL((disk_flash_kernel<SUM, false>), grid, dim3(256), 0, st, fa, want_r);
+}
+
 bool use_flash() {
   const char* e = getenv("POSFEAT_DISK_FLASH");
   return !(e && e[0] == '0');
@@ -771,12 +827,12 @@ static int disk_loss_impl(const float* kp1, const float* kp2, const float* xf1, 
     // column LSE (over image-1 points) and row LSE (over image-2 points), all points
     fa.A = FlashSide{f1};
     fa.B = FlashSide{f2};
-    hipLaunchKernelGGL(disk_flash_kernel<false>, fgrid, dim3(256), 0, st, fa, 0);
+    launch_flash<false>(fgrid, st, fa, 0);
     hipLaunchKernelGGL(flash_lse_final_kernel, dim3((b * n + 255) / 256), dim3(256), 0, st, lsep,
                        b, ns, n, lc);
     fa.A = FlashSide{f2};
     fa.B = FlashSide{f1};
-    hipLaunchKernelGGL(disk_flash_kernel<false>, fgrid, dim3(256), 0, st, fa, 0);
+    launch_flash<false>(fgrid, st, fa, 0);
     hipLaunchKernelGGL(flash_lse_final_kernel, dim3((b * n + 255) / 256), dim3(256), 0, st, lsep,
                        b, ns, n, lr);
     hipLaunchKernelGGL(flash_compact_kernel, dim3(b), dim3(1024), 0, st, ac1, n, id1, cnt);
@@ -793,7 +849,7 @@ static int disk_loss_impl(const float* kp1, const float* kp2, const float* xf1, 
     }
     fa.A = s1;
     fa.B = s2;
-    hipLaunchKernelGGL(disk_flash_kernel<true>, fgrid, dim3(256), 0, st, fa, 1);
+    launch_flash<true>(fgrid, st, fa, 1);
     hipLaunchKernelGGL(flash_sum_final_kernel, dim3((b * n + 255) / 256), dim3(256), 0, st, gp, rp,
                        b, ns, n, id2, cnt + b, kp_penalty, g2, rcol);
     PF_CHECK_LAUNCH();
@@ -804,7 +860,7 @@ static int disk_loss_impl(const float* kp1, const float* kp2, const float* xf1, 
     // columns = image-1 points: sum_n reward p
     fa.A = s2;
     fa.B = s1;
-    hipLaunchKernelGGL(disk_flash_kernel<true>, fgrid, dim3(256), 0, st, fa, 0);
+    launch_flash<true>(fgrid, st, fa, 0);
     hipLaunchKernelGGL(flash_sum_final_kernel, dim3((b * n + 255) / 256), dim3(256), 0, st, gp,
                        (const double*)nullptr, b, ns, n, id1, cnt, kp_penalty, g1,
                        (double*)nullptr);
@@ -889,8 +945,7 @@ extern "C" int posfeat_disk_flash_lse(const float* fa, const float* fb, int b, i
   fa_.rows_per_split = ((n + ns - 1) / ns + FSTEP - 1) / FSTEP * FSTEP;
   fa_.T = T;
   fa_.lse_part = static_cast<float2*>(ws);
-  hipLaunchKernelGGL(disk_flash_kernel<false>, dim3((n + FCOLS - 1) / FCOLS, ns, b), dim3(256), 0,
-                     st, fa_, 0);
+  launch_flash<false>(dim3((n + FCOLS - 1) / FCOLS, ns, b), st, fa_, 0);
   hipLaunchKernelGGL(flash_lse_final_kernel, dim3((b * n + 255) / 256), dim3(256), 0, st,
                      fa_.lse_part, b, ns, n, lse);
   PF_CHECK_LAUNCH();
