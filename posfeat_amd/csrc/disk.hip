@@ -33,6 +33,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.h"
 #include "fmap.h"
@@ -395,6 +396,8 @@ struct FlashSide {          // per-point data of one side (1: image 1, 2: image 
   const float* line;        // SUM: [b][n][3] normalised epipolar line of each point
   const float* cpx;         // SUM: [b][n][2] pixel coordinates
   const float* logp;        // SUM: [b][n] point log-probability
+  const unsigned short* pl = nullptr;  // BF6: [b][3][n][128] bf16 planes of f (flash_split_kernel)
+  const float* meta = nullptr;         // BF6 SUM: [b][n][8] lse, line(3), cpx(2), logp, 0
 };
 
 struct FlashArgs {
@@ -406,13 +409,7 @@ struct FlashArgs {
   double* r_part;           // SUM (want_r): [b][split][n] sum reward p (logp terms)
 };
 
-// BF6: the similarity products as bf16x6 on v_mfma_f32_32x32x16_bf16 (six
-// bf16 products per fp32 product, fp32-exact per product: conv.hip split3):
-// B's column (this lane's 128 k) is split once into three bf16 planes held in
-// registers, A's fragments are split as they are read from LDS; 16x the
-// matrix rate of the fp32-input MFMA, a third of its instructions' cycles per
-// product.  The default (conv precision >= 1); fp32 MFMA otherwise.
-template <bool SUM, bool BF6 = false>
+template <bool SUM>
 __global__ __launch_bounds__(256) void disk_flash_kernel(FlashArgs a, int want_r) {
   __shared__ __attribute__((aligned(16))) float As[2 * FSTEP * FD];  // 2 x 32 KB
   __shared__ float meta[2][FSTEP][8];  // SUM: lse, line(3), cpx(2), logp per A row
@@ -428,22 +425,11 @@ __global__ __launch_bounds__(256) void disk_flash_kernel(FlashArgs a, int want_r
   const int cl = cbase + wave * 32 + (lane & 31);
   const bool cok = cl < ncolB;
   const int cpt = SUM ? a.B.idx[pb + min(cl, ncolB - 1)] : min(cl, ncolB - 1);  // point id
-  f32x4 breg[BF6 ? 1 : FD / 8];
-  g6_u32x4 bpl[BF6 ? FD / 16 : 1][3];  // BF6: per k16 group the h, m, l operands
+  f32x4 breg[FD / 8];
   {
     const float* brow = a.B.f + (pb + cpt) * FD;
-    if (BF6) {
 #pragma unroll
-      for (int g = 0; g < FD / 16; ++g) {
-        const f32x4 q0 = *reinterpret_cast<const f32x4*>(brow + 16 * g + 8 * h);
-        const f32x4 q1 = *reinterpret_cast<const f32x4*>(brow + 16 * g + 8 * h + 4);
-        g6_split(q0, q1, bpl[g][0], bpl[g][1], bpl[g][2]);
-      }
-    } else {
-#pragma unroll
-      for (int g = 0; g < FD / 8; ++g)
-        breg[g] = *reinterpret_cast<const f32x4*>(brow + 8 * g + 4 * h);
-    }
+    for (int g = 0; g < FD / 8; ++g) breg[g] = *reinterpret_cast<const f32x4*>(brow + 8 * g + 4 * h);
   }
   float bl = 0.f, bl0 = 0.f, bl1 = 0.f, bl2 = 0.f, bx = 0.f, by = 0.f, blp = 0.f;
   if (SUM) {
@@ -497,35 +483,7 @@ __global__ __launch_bounds__(256) void disk_flash_kernel(FlashArgs a, int want_r
     f32x16 accs[2];
 #pragma unroll
     for (int r = 0; r < 16; ++r) accs[0][r] = accs[1][r] = 0.f;
-    if (BF6) {
-      // k16 group g: lane (row la, half h) supplies k = 16 g + 8 h .. + 7, the
-      // 16-B slots 4 g + 2 h and 4 g + 2 h + 1 of its LDS row (swizzled by la & 15)
-      const int la = lane & 31;
-      const float* arow0 = Ab + la * FD;
-      const float* arow1 = Ab + (32 + la) * FD;
-#pragma unroll
-      for (int g = 0; g < FD / 16; ++g) {
-        const int o0 = ((4 * g + 2 * h) ^ (la & 15)) * 4, o1 = ((4 * g + 2 * h + 1) ^ (la & 15)) * 4;
-        g6_u32x4 ah0, am0, al0, ah1, am1, al1;
-        g6_split(*reinterpret_cast<const f32x4*>(arow0 + o0),
-                 *reinterpret_cast<const f32x4*>(arow0 + o1), ah0, am0, al0);
-        g6_split(*reinterpret_cast<const f32x4*>(arow1 + o0),
-                 *reinterpret_cast<const f32x4*>(arow1 + o1), ah1, am1, al1);
-        const g6_u32x4 &bh = bpl[g][0], &bm = bpl[g][1], &bl = bpl[g][2];
-        accs[0] = g6_mfma(ah0, bh, accs[0]);
-        accs[1] = g6_mfma(ah1, bh, accs[1]);
-        accs[0] = g6_mfma(ah0, bm, accs[0]);
-        accs[1] = g6_mfma(ah1, bm, accs[1]);
-        accs[0] = g6_mfma(am0, bh, accs[0]);
-        accs[1] = g6_mfma(am1, bh, accs[1]);
-        accs[0] = g6_mfma(ah0, bl, accs[0]);
-        accs[1] = g6_mfma(ah1, bl, accs[1]);
-        accs[0] = g6_mfma(al0, bh, accs[0]);
-        accs[1] = g6_mfma(al1, bh, accs[1]);
-        accs[0] = g6_mfma(am0, bm, accs[0]);
-        accs[1] = g6_mfma(am1, bm, accs[1]);
-      }
-    } else {
+    {
       const int la = lane & 31;  // rows la and 32 + la share the swizzle (la & 15)
       const float* arow0 = Ab + la * FD;
       const float* arow1 = Ab + (32 + la) * FD;
@@ -597,6 +555,255 @@ __global__ __launch_bounds__(256) void disk_flash_kernel(FlashArgs a, int want_r
       if (want_r) a.r_part[o] = rs + orr;
     }
   }
+}
+
+// the refilled ring slot and the multiplied one as __restrict__ parameters of
+// one body, so the waitcnt pass does not order the stage's LDS reads behind
+// the younger DMA (conv.hip pf_dma_overlap_step)
+template <class F>
+__device__ __forceinline__ void flash6_step(unsigned short* __restrict__ d,
+                                            const unsigned short* __restrict__ s, F&& body) {
+  body(d, s);
+}
+
+// vmcnt(N) with expcnt / lgkmcnt left alone (gfx9 s_waitcnt encoding)
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+// The flash passes with the similarity products in bf16x6 on
+// v_mfma_f32_32x32x16_bf16 (six bf16 products per fp32 product, fp32-exact
+// per product: common.h split3).  Both sides arrive as three bf16 planes,
+// split once per loss (flash_split_kernel); the SUM passes' sides arrive
+// compacted to their accepted points in order, planes and per-point metadata
+// (flash_gather_kernel), so every A row of a step is a contiguous DMA and
+// nothing in the loop waits on an index load.  B's column (this lane's 128 k)
+// sits in registers; A's rows stream in 32-row stages (3 planes x 8 KB, plus
+// 1 KB of metadata for SUM) through a three-stage LDS ring: stages i+1 and
+// i+2 are in flight while i is multiplied, each step waits only for its own
+// DMA (counted vmcnt) and one raw s_barrier.  75 KB of LDS: two workgroups
+// per CU.  One accumulation chain per step (the 32x32x16 MFMA issues back to
+// back on one accumulator).  Row / column semantics as disk_flash_kernel.
+constexpr int F6STEP = 32;  // A rows per stage
+constexpr int F6NST = 3;    // LDS ring stages
+
+template <bool SUM>
+__global__ __launch_bounds__(256) void disk_flash6_kernel(FlashArgs a, int want_r) {
+  // a stage: 3 planes x 32 rows x 256 B, then (SUM) 32 rows x 32 B of metadata --
+  // one array, so the DMAs into a stage and the reads of another go through the
+  // same pair of __restrict__ pointers (flash6_step)
+  constexpr int PLANES = 3 * F6STEP * FD;                  // bf16 per stage's planes (24 KB)
+  constexpr int PSTAGE = PLANES + (SUM ? F6STEP * 16 : 0);  // + metadata (1 KB as bf16 units)
+  constexpr int VPS = SUM ? 7 : 6;                          // DMA wave-instructions per stage per wave
+  __shared__ __attribute__((aligned(16))) unsigned short Ps[F6NST * PSTAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, la = lane & 31;
+  const int b = blockIdx.z, split = blockIdx.y;
+  const int ncolB = SUM ? a.B.cnt[b] : a.n;
+  const int nrowA = SUM ? a.A.cnt[b] : a.n;
+  const int cbase = blockIdx.x * FCOLS;
+  const int r0 = split * a.rows_per_split;
+  const int r1 = min(nrowA, r0 + a.rows_per_split);
+  const long long pb = (long long)b * a.n;
+  if (cbase >= ncolB) return;  // block-uniform
+  const int cl = cbase + wave * 32 + la;
+  const bool cok = cl < ncolB;
+  const int cpt = min(cl, ncolB - 1);  // SUM: compacted column
+  g6_u32x4 bpl[FD / 16][3];            // per k16 group the h, m, l operands of column cpt
+  f32x4 bm0 = {0.f, 0.f, 0.f, 0.f}, bm1 = {0.f, 0.f, 0.f, 0.f};  // SUM: column metadata
+  const int nsteps = r1 > r0 ? (r1 - r0 + F6STEP - 1) / F6STEP : 0;
+  const int rlast = max(r1 - 1, 0);  // rows clamp here (the prologue always issues two stages)
+  // stage s into ring slot d: 24 wave DMAs of 4 plane rows (6 per wave); LDS
+  // row lr holds its 16-B chunk c at slot c ^ (lr & 15).  SUM: each wave also
+  // moves 8 rows of metadata (16 lanes x 16 B).
+  auto issue = [&](int s, unsigned short* d) {
+#pragma unroll
+    for (int t = 0; t < 6; ++t) {
+      const int q = wave * 6 + t, pln = q >> 3, lr = (q & 7) * 4 + (lane >> 4);
+      const int row = min(r0 + s * F6STEP + lr, rlast);
+      const int slot = (lane & 15) ^ (lr & 15);
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(a.A.pl + (3 * pb + (long long)pln * a.n +
+                                                                    row) * FD + slot * 8),
+          (__attribute__((address_space(3))) void*)(d + (pln * F6STEP + (q & 7) * 4) * FD), 16, 0,
+          0);
+    }
+    if (SUM) {  // 64 lanes x 4 B (no divergent branch around the DMA)
+      const int row = min(r0 + s * F6STEP + wave * 8 + (lane >> 3), rlast);
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(a.A.meta + (pb + row) * 8 + (lane & 7)),
+          (__attribute__((address_space(3))) void*)(d + PLANES + wave * 8 * 16), 4, 0, 0);
+    }
+  };
+  const float c2 = a.T * 1.4426950408889634f;  // T log2(e)
+  float run_m = -INFINITY, run_s = 0.f;  // LSE: running max (base 2) / sum of exp
+  float gs = 0.f;                        // SUM: sum reward p
+  double rs = 0.0;                       // SUM: sum reward p (logp terms)
+  auto compute = [&](int s, const unsigned short* __restrict__ L) {
+    const float* M = reinterpret_cast<const float*>(L + PLANES);  // SUM: [32][8] metadata
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    // k16 group g: lane (row la, half h) supplies k = 16 g + 8 h .. + 7 =
+    // chunk 2 g + h of its row in each plane
+#pragma unroll
+    for (int g = 0; g < FD / 16; ++g) {
+      const int off = la * FD + (((2 * g + h) ^ (la & 15)) * 8);
+      const g6_u32x4 ah = *reinterpret_cast<const g6_u32x4*>(L + off);
+      const g6_u32x4 am = *reinterpret_cast<const g6_u32x4*>(L + F6STEP * FD + off);
+      const g6_u32x4 al = *reinterpret_cast<const g6_u32x4*>(L + 2 * F6STEP * FD + off);
+      acc = g6_mfma(ah, bpl[g][0], acc);
+      acc = g6_mfma(ah, bpl[g][1], acc);
+      acc = g6_mfma(am, bpl[g][0], acc);
+      acc = g6_mfma(ah, bpl[g][2], acc);
+      acc = g6_mfma(al, bpl[g][0], acc);
+      acc = g6_mfma(am, bpl[g][1], acc);
+    }
+    // acc[r] = S(A row r0 + s*32 + (r&3) + 8(r>>2) + 4h, B column cl); only a
+    // split's last step can hold rows past r1 (the per-row checks are compiled
+    // into that variant alone)
+    const int rb = r0 + s * F6STEP + 4 * h;
+    auto epilogue = [&](auto full_t) {
+      constexpr bool FULL = decltype(full_t)::value;
+      auto valid = [&](int r) { return FULL || rb + (r & 3) + 8 * (r >> 2) < r1; };
+      if (!SUM) {
+        // base-2 online logsumexp of x = T (s - 1): x log2(e) = c2 s - c2; the
+        // max over the raw similarities (c2 > 0), one fma + v_exp_f32 per element
+        float sm = -INFINITY;
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (valid(r)) sm = fmaxf(sm, acc[r]);
+        if (sm > -INFINITY) {
+          const float nm = fmaxf(run_m, c2 * sm - c2), off = -c2 - nm;
+          float add = 0.f;
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (valid(r)) add += __builtin_amdgcn_exp2f(fmaf(c2, acc[r], off));
+          run_s = run_s * __builtin_amdgcn_exp2f(run_m - nm) + add;
+          run_m = nm;
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          if (!valid(r)) continue;
+          const int lr = 4 * h + (r & 3) + 8 * (r >> 2);  // row within the stage
+          const f32x4 m0 = *reinterpret_cast<const f32x4*>(M + lr * 8);
+          const f32x4 m1 = *reinterpret_cast<const f32x4*>(M + lr * 8 + 4);
+          const float aff = fmaf(a.T, acc[r], -a.T);
+          const float lp = (aff - m0[0]) + (aff - bm0[0]);  // log p = lpa + lpb
+          const float p = __builtin_amdgcn_exp2f(lp * 1.4426950408889634f);
+          const float dA = fabsf(m0[1] * bm1[0] + m0[2] * bm1[1] + m0[3]);    // A's line at B's point
+          const float dB = fabsf(bm0[1] * m1[0] + bm0[2] * m1[1] + bm0[3]);  // B's line at A's point
+          const float rp = ((dA < a.thr && dB < a.thr) ? a.good : a.bad) * p;
+          gs += rp;
+          if (want_r) rs += (double)(rp * (lp + (m1[2] + bm1[2])));
+        }
+      }
+    };
+    if (r0 + (s + 1) * F6STEP <= r1)
+      epilogue(std::true_type{});
+    else
+      epilogue(std::false_type{});
+  };
+  // straight-line prologue: stage 0, B's column, stage 1.  The explicit wait
+  // for B's loads keeps the waitcnt pass from putting a vmcnt(0) in front of
+  // every step's first MFMA (it could not prove them retired by the counted
+  // wait); a stage past the last is harmless (clamped rows, retired by the
+  // final wait below)
+  issue(0, Ps);
+  {
+    const unsigned short* bp = a.B.pl + (3 * pb + cpt) * FD;
+#pragma unroll
+    for (int g = 0; g < FD / 16; ++g)
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        bpl[g][q] = *reinterpret_cast<const g6_u32x4*>(bp + (long long)q * a.n * FD + 16 * g + 8 * h);
+  }
+  if (SUM) {
+    bm0 = *reinterpret_cast<const f32x4*>(a.B.meta + (pb + cpt) * 8);
+    bm1 = *reinterpret_cast<const f32x4*>(a.B.meta + (pb + cpt) * 8 + 4);
+  }
+  wait_vmcnt<0>();
+  issue(1, Ps + PSTAGE);
+  int slot = 0;
+  for (int i = 0; i < nsteps; ++i) {
+    if (i + 1 < nsteps)
+      wait_vmcnt<VPS>();  // stage i landed; stage i+1 may stay in flight
+    else
+      wait_vmcnt<0>();
+    // every wave: stage i landed, and stage i-1 (the slot refilled below) consumed
+    __builtin_amdgcn_s_barrier();
+    const int refill = slot == 0 ? F6NST - 1 : slot - 1;
+    flash6_step(Ps + refill * PSTAGE, Ps + slot * PSTAGE,
+                [&](unsigned short* d, const unsigned short* L) {
+                  if (i + F6NST - 1 < nsteps) issue(i + F6NST - 1, d);
+                  compute(i, L);
+                });
+    slot = slot == F6NST - 1 ? 0 : slot + 1;
+  }
+  wait_vmcnt<0>();  // no DMA may still write this workgroup's LDS after it ends
+  // merge the two lane halves (interleaved row sets) in a fixed order; the
+  // partial's max back in natural units
+  const long long o = ((long long)b * gridDim.y + split) * a.n + cl;
+  if (!SUM) {
+    const float om = __shfl_xor(run_m, 32, 64), os = __shfl_xor(run_s, 32, 64);
+    if (h == 0 && cok) {
+      const float M = fmaxf(run_m, om);
+      const float t = (M == -INFINITY) ? 0.f
+                                       : run_s * __builtin_amdgcn_exp2f(run_m - M) +
+                                             os * __builtin_amdgcn_exp2f(om - M);
+      a.lse_part[o] = make_float2(M * 0.6931471805599453f, t);
+    }
+  } else {
+    const float og = __shfl_xor(gs, 32, 64);
+    const double orr = __shfl_xor(rs, 32, 64);
+    if (h == 0 && cok) {
+      a.g_part[o] = gs + og;
+      if (want_r) a.r_part[o] = rs + orr;
+    }
+  }
+}
+
+// SUM passes' side data in accepted order (flash_compact_kernel's ids): row i
+// < cnt[b] of cpl / cmeta = planes / metadata of point idx[b][i]
+__global__ void flash_gather_kernel(const unsigned short* __restrict__ pl, FlashSide s, int nb,
+                                    int n, unsigned short* __restrict__ cpl,
+                                    float* __restrict__ cmeta) {
+  const long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x;  // (b, i, chunk)
+  if (t >= (long long)nb * n * (FD / 8)) return;
+  const long long r = t / (FD / 8);
+  const int c = (int)(t - r * (FD / 8));
+  const int bb = (int)(r / n), i = (int)(r - (long long)bb * n);
+  if (i >= s.cnt[bb]) return;
+  const long long pb = (long long)bb * n, src = s.idx[pb + i];
+#pragma unroll
+  for (int q = 0; q < 3; ++q)
+    *reinterpret_cast<g6_u32x4*>(cpl + (3 * pb + (long long)q * n + i) * FD + c * 8) =
+        *reinterpret_cast<const g6_u32x4*>(pl + (3 * pb + (long long)q * n + src) * FD + c * 8);
+  if (c == 0) {
+    const long long p = pb + src;
+    float* m = cmeta + (pb + i) * 8;
+    *reinterpret_cast<f32x4*>(m) = f32x4{s.lse[p], s.line[p * 3], s.line[p * 3 + 1], s.line[p * 3 + 2]};
+    *reinterpret_cast<f32x4*>(m + 4) = f32x4{s.cpx[p * 2], s.cpx[p * 2 + 1], s.logp[p], 0.f};
+  }
+}
+
+// the three bf16 planes of L2-normalised descriptors for the BF6 flash passes:
+// pl[b][q][n][128] = plane q (h, m, l of common.h g6_split) of f[b][n][128];
+// one thread per 8 values
+__global__ void flash_split_kernel(const float* __restrict__ f, long long rows, int n,
+                                   unsigned short* __restrict__ pl) {
+  const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (i >= rows * (FD / 8)) return;
+  const long long r = i / (FD / 8), bb = r / n, pr = r - bb * n;
+  const int c = (int)(i - r * (FD / 8));
+  g6_u32x4 hp, mp, lp;
+  g6_split(*reinterpret_cast<const f32x4*>(f + r * FD + c * 8),
+           *reinterpret_cast<const f32x4*>(f + r * FD + c * 8 + 4), hp, mp, lp);
+  unsigned short* o = pl + (3 * bb * n + pr) * FD + c * 8;
+  *reinterpret_cast<g6_u32x4*>(o) = hp;
+  *reinterpret_cast<g6_u32x4*>(o + (long long)n * FD) = mp;
+  *reinterpret_cast<g6_u32x4*>(o + 2LL * n * FD) = lp;
 }
 
 // lse[b][p] = merge of the split (max, sum) partials in split order
@@ -693,12 +900,21 @@ int flash_nsplit(int n, int nb) {
 // read per call (a few getenv per loss) so tests can A/B both paths in-process
 // the flash passes' product arithmetic follows the conv precision mode
 // (posfeat_set_conv_precision: >= 1 bf16x6, the default; 0 fp32 MFMA)
+bool flash_bf6() { return pf_conv_precision() >= 1; }
+
+// planes of f [b][n][128] into pl (flash_bf6() only; pl has b * n * 768 bytes)
+void flash_split(const float* f, int b, int n, unsigned short* pl, hipStream_t st) {
+  const long long t = (long long)b * n * (FD / 8);
+  hipLaunchKernelGGL(flash_split_kernel, dim3((unsigned)((t + 255) / 256)), dim3(256), 0, st, f,
+                     (long long)b * n, n, pl);
+}
+
 template <bool SUM>
 void launch_flash(dim3 grid, hipStream_t st, const FlashArgs& fa, int want_r) {
-  if (pf_conv_precision() >= 1)
-    hipLaunchKernelGGL((disk_flash_kernel<SUM, true>), grid, dim3(256), 0, st, fa, want_r);
+  if (flash_bf6())
+    hipLaunchKernelGGL(disk_flash6_kernel<SUM>, grid, dim3(256), 0, st, fa, want_r);
   else
-    hipLaunchKernelGGL((disk_flash_kernel<SUM, false>), grid, dim3(256), 0, st, fa, want_r);
+    hipLaunchKernelGGL(disk_flash_kernel<SUM>, grid, dim3(256), 0, st, fa, want_r);
 }
 
 bool use_flash() {
@@ -728,7 +944,9 @@ static size_t disk_flash_bytes(size_t b, size_t n) {  // flash path scratch afte
          pf_align(b * ns * n * 8, 256) +            // reinforce partials (fp64)
          2 * pf_align(b * n * 4, 256) +             // compacted ids
          pf_align(2 * b * 4, 256) +                 // counts
-         pf_align(b * n * 8, 256);                  // reinforce per column (fp64)
+         pf_align(b * n * 8, 256) +                 // reinforce per column (fp64)
+         4 * pf_align(b * n * FD * 6, 256) +        // bf16x6 planes of f1 / f2, compacted
+         2 * pf_align(b * n * 32, 256);             // compacted per-point metadata
 }
 
 static size_t disk_dense_bytes(size_t b, size_t n) {  // S-materialising path
@@ -811,6 +1029,17 @@ static int disk_loss_impl(const float* kp1, const float* kp2, const float* xf1, 
     int32_t* id2 = static_cast<int32_t*>(take((size_t)b * n * 4));
     int32_t* cnt = static_cast<int32_t*>(take((size_t)2 * b * 4));
     double* rcol = static_cast<double*>(take((size_t)b * n * 8));
+    unsigned short* pl1 = static_cast<unsigned short*>(take((size_t)b * n * FD * 6));
+    unsigned short* pl2 = static_cast<unsigned short*>(take((size_t)b * n * FD * 6));
+    unsigned short* cpl1 = static_cast<unsigned short*>(take((size_t)b * n * FD * 6));
+    unsigned short* cpl2 = static_cast<unsigned short*>(take((size_t)b * n * FD * 6));
+    float* cm1 = static_cast<float*>(take((size_t)b * n * 32));
+    float* cm2 = static_cast<float*>(take((size_t)b * n * 32));
+    const bool bf6 = flash_bf6();
+    if (bf6) {
+      flash_split(f1, b, n, pl1, st);
+      flash_split(f2, b, n, pl2, st);
+    }
     const int rps = ((n + ns - 1) / ns + FSTEP - 1) / FSTEP * FSTEP;
     const dim3 fgrid((n + FCOLS - 1) / FCOLS, ns, b);
     FlashArgs fa{};
@@ -823,20 +1052,28 @@ static int disk_loss_impl(const float* kp1, const float* kp2, const float* xf1, 
     fa.lse_part = lsep;
     fa.g_part = gp;
     fa.r_part = rp;
-    const FlashSide s1{f1, id1, cnt, lr, ln1, cpx1, lp1}, s2{f2, id2, cnt + b, lc, ln2, cpx2, lp2};
+    const FlashSide s1{f1, id1, cnt, lr, ln1, cpx1, lp1, cpl1, cm1},
+        s2{f2, id2, cnt + b, lc, ln2, cpx2, lp2, cpl2, cm2};
+    const FlashSide a1{f1, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, pl1},
+        a2{f2, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, pl2};
     // column LSE (over image-1 points) and row LSE (over image-2 points), all points
-    fa.A = FlashSide{f1};
-    fa.B = FlashSide{f2};
+    fa.A = a1;
+    fa.B = a2;
     launch_flash<false>(fgrid, st, fa, 0);
     hipLaunchKernelGGL(flash_lse_final_kernel, dim3((b * n + 255) / 256), dim3(256), 0, st, lsep,
                        b, ns, n, lc);
-    fa.A = FlashSide{f2};
-    fa.B = FlashSide{f1};
+    fa.A = a2;
+    fa.B = a1;
     launch_flash<false>(fgrid, st, fa, 0);
     hipLaunchKernelGGL(flash_lse_final_kernel, dim3((b * n + 255) / 256), dim3(256), 0, st, lsep,
                        b, ns, n, lr);
     hipLaunchKernelGGL(flash_compact_kernel, dim3(b), dim3(1024), 0, st, ac1, n, id1, cnt);
     hipLaunchKernelGGL(flash_compact_kernel, dim3(b), dim3(1024), 0, st, ac2, n, id2, cnt + b);
+    if (bf6) {  // the accepted points of each side, in order, for the SUM passes
+      const unsigned gb = (unsigned)(((long long)b * n * (FD / 8) + 255) / 256);
+      hipLaunchKernelGGL(flash_gather_kernel, dim3(gb), dim3(256), 0, st, pl1, s1, b, n, cpl1, cm1);
+      hipLaunchKernelGGL(flash_gather_kernel, dim3(gb), dim3(256), 0, st, pl2, s2, b, n, cpl2, cm2);
+    }
     PF_CHECK_LAUNCH();
     // accepted pairs, columns = image-2 points: sum_m reward p and the reinforce
     float* g1 = grad ? static_cast<float*>(take((size_t)b * n * 4)) : nullptr;
@@ -929,7 +1166,8 @@ static int disk_loss_impl(const float* kp1, const float* kp2, const float* xf1, 
 // rows of fa, for each of the n rows of fb; fa, fb [b][n][128] L2-normalised.
 extern "C" size_t posfeat_disk_flash_lse_workspace(int b, int n) {
   if (b <= 0 || n <= 0) return 0;
-  return pf_align((size_t)b * flash_nsplit(n, b) * n * 8, 256);
+  return pf_align((size_t)b * flash_nsplit(n, b) * n * 8, 256) +
+         2 * pf_align((size_t)b * n * FD * 6, 256);  // bf16x6 planes of fa / fb
 }
 
 extern "C" int posfeat_disk_flash_lse(const float* fa, const float* fb, int b, int n, float T,
@@ -939,8 +1177,15 @@ extern "C" int posfeat_disk_flash_lse(const float* fa, const float* fb, int b, i
   hipStream_t st = pf_stream(stream);
   const int ns = flash_nsplit(n, b);
   FlashArgs fa_{};
-  fa_.A = FlashSide{fa};
-  fa_.B = FlashSide{fb};
+  char* pw = static_cast<char*>(ws) + pf_align((size_t)b * ns * n * 8, 256);
+  unsigned short* pla = reinterpret_cast<unsigned short*>(pw);
+  unsigned short* plb = reinterpret_cast<unsigned short*>(pw + pf_align((size_t)b * n * FD * 6, 256));
+  if (flash_bf6()) {
+    flash_split(fa, b, n, pla, st);
+    flash_split(fb, b, n, plb, st);
+  }
+  fa_.A = FlashSide{fa, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, pla};
+  fa_.B = FlashSide{fb, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, plb};
   fa_.n = n;
   fa_.rows_per_split = ((n + ns - 1) / ns + FSTEP - 1) / FSTEP * FSTEP;
   fa_.T = T;
