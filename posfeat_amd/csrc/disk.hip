@@ -562,8 +562,9 @@ __global__ __launch_bounds__(256) void disk_flash_kernel(FlashArgs a, int want_r
 // the younger DMA (conv.hip pf_dma_overlap_step)
 template <class F>
 __device__ __forceinline__ void flash6_step(unsigned short* __restrict__ d,
-                                            const unsigned short* __restrict__ s, F&& body) {
-  body(d, s);
+                                            const unsigned short* __restrict__ s,
+                                            const unsigned short* __restrict__ sp, F&& body) {
+  body(d, s, sp);
 }
 
 // vmcnt(N) with expcnt / lgkmcnt left alone (gfx9 s_waitcnt encoding)
@@ -580,22 +581,25 @@ __device__ __forceinline__ void wait_vmcnt() {
 // (flash_gather_kernel), so every A row of a step is a contiguous DMA and
 // nothing in the loop waits on an index load.  B's column (this lane's 128 k)
 // sits in registers; A's rows stream in 32-row stages (3 planes x 8 KB, plus
-// 1 KB of metadata for SUM) through a three-stage LDS ring: stages i+1 and
-// i+2 are in flight while i is multiplied, each step waits only for its own
-// DMA (counted vmcnt) and one raw s_barrier.  75 KB of LDS: two workgroups
-// per CU.  One accumulation chain per step (the 32x32x16 MFMA issues back to
-// back on one accumulator).  Row / column semantics as disk_flash_kernel.
+// 1 KB of metadata for SUM) through a three-slot LDS ring: stages i+1 and
+// i+2 are in flight while stage i is multiplied.  LSE is software-pipelined:
+// step i multiplies stage i into one accumulator while the VALU epilogue of
+// stage i-1 (online logsumexp) is threaded through its dependent MFMA chain
+// (mma_lse), so the matrix pipe and the VALU overlap inside each wave.  Only a split's
+// last stage can hold rows past its end: its epilogue, after the loop, is the
+// one with per-row checks.  75 KB of LDS: two workgroups per CU.  Row /
+// column semantics as disk_flash_kernel; WR: the SUM pass also sums the
+// reinforce terms (fp64).
 constexpr int F6STEP = 32;  // A rows per stage
-constexpr int F6NST = 3;    // LDS ring stages
+constexpr int F6NST = 3;    // LDS slots
 
-template <bool SUM>
-__global__ __launch_bounds__(256) void disk_flash6_kernel(FlashArgs a, int want_r) {
+template <bool SUM, bool WR>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void disk_flash6_kernel(FlashArgs a) {
   // a stage: 3 planes x 32 rows x 256 B, then (SUM) 32 rows x 32 B of metadata --
-  // one array, so the DMAs into a stage and the reads of another go through the
+  // one array, so the DMAs into a slot and the reads of others go through the
   // same pair of __restrict__ pointers (flash6_step)
   constexpr int PLANES = 3 * F6STEP * FD;                  // bf16 per stage's planes (24 KB)
   constexpr int PSTAGE = PLANES + (SUM ? F6STEP * 16 : 0);  // + metadata (1 KB as bf16 units)
-  constexpr int VPS = SUM ? 7 : 6;                          // DMA wave-instructions per stage per wave
   __shared__ __attribute__((aligned(16))) unsigned short Ps[F6NST * PSTAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5, la = lane & 31;
   const int b = blockIdx.z, split = blockIdx.y;
@@ -612,11 +616,11 @@ __global__ __launch_bounds__(256) void disk_flash6_kernel(FlashArgs a, int want_
   g6_u32x4 bpl[FD / 16][3];            // per k16 group the h, m, l operands of column cpt
   f32x4 bm0 = {0.f, 0.f, 0.f, 0.f}, bm1 = {0.f, 0.f, 0.f, 0.f};  // SUM: column metadata
   const int nsteps = r1 > r0 ? (r1 - r0 + F6STEP - 1) / F6STEP : 0;
-  const int rlast = max(r1 - 1, 0);  // rows clamp here (the prologue always issues two stages)
-  // stage s into ring slot d: 24 wave DMAs of 4 plane rows (6 per wave); LDS
-  // row lr holds its 16-B chunk c at slot c ^ (lr & 15).  SUM: each wave also
-  // moves 8 rows of metadata (16 lanes x 16 B).
-  auto issue = [&](int s, unsigned short* d) {
+  const int rlast = max(r1 - 1, 0);  // rows clamp here
+  // stage s into slot d: 24 wave DMAs of 4 plane rows (6 per wave); LDS row lr
+  // holds its 16-B chunk c at slot c ^ (lr & 15).  SUM: each wave also moves 8
+  // rows of metadata (64 lanes x 4 B).
+  auto issue = [&](int s, unsigned short* d) __attribute__((always_inline)) {
 #pragma unroll
     for (int t = 0; t < 6; ++t) {
       const int q = wave * 6 + t, pln = q >> 3, lr = (q & 7) * 4 + (lane >> 4);
@@ -628,7 +632,7 @@ __global__ __launch_bounds__(256) void disk_flash6_kernel(FlashArgs a, int want_
           (__attribute__((address_space(3))) void*)(d + (pln * F6STEP + (q & 7) * 4) * FD), 16, 0,
           0);
     }
-    if (SUM) {  // 64 lanes x 4 B (no divergent branch around the DMA)
+    if (SUM) {  // no divergent branch around the DMA
       const int row = min(r0 + s * F6STEP + wave * 8 + (lane >> 3), rlast);
       __builtin_amdgcn_global_load_lds(
           (const __attribute__((address_space(1))) void*)(a.A.meta + (pb + row) * 8 + (lane & 7)),
@@ -638,14 +642,12 @@ __global__ __launch_bounds__(256) void disk_flash6_kernel(FlashArgs a, int want_
   const float c2 = a.T * 1.4426950408889634f;  // T log2(e)
   float run_m = -INFINITY, run_s = 0.f;  // LSE: running max (base 2) / sum of exp
   float gs = 0.f;                        // SUM: sum reward p
-  double rs = 0.0;                       // SUM: sum reward p (logp terms)
-  auto compute = [&](int s, const unsigned short* __restrict__ L) {
-    const float* M = reinterpret_cast<const float*>(L + PLANES);  // SUM: [32][8] metadata
-    f32x16 acc;
+  double rs = 0.0;                       // SUM (WR): sum reward p (logp terms)
+  // stage s's 32x32 similarity tile from slot L: k16 group g, lane (row la,
+  // half h) supplies k = 16 g + 8 h .. + 7 = chunk 2 g + h of its row per plane
+  auto mma = [&](const unsigned short* L, f32x16& acc) __attribute__((always_inline)) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    // k16 group g: lane (row la, half h) supplies k = 16 g + 8 h .. + 7 =
-    // chunk 2 g + h of its row in each plane
 #pragma unroll
     for (int g = 0; g < FD / 16; ++g) {
       const int off = la * FD + (((2 * g + h) ^ (la & 15)) * 8);
@@ -659,58 +661,108 @@ __global__ __launch_bounds__(256) void disk_flash6_kernel(FlashArgs a, int want_
       acc = g6_mfma(al, bpl[g][0], acc);
       acc = g6_mfma(am, bpl[g][1], acc);
     }
-    // acc[r] = S(A row r0 + s*32 + (r&3) + 8(r>>2) + 4h, B column cl); only a
-    // split's last step can hold rows past r1 (the per-row checks are compiled
-    // into that variant alone)
-    const int rb = r0 + s * F6STEP + 4 * h;
-    auto epilogue = [&](auto full_t) {
-      constexpr bool FULL = decltype(full_t)::value;
-      auto valid = [&](int r) { return FULL || rb + (r & 3) + 8 * (r >> 2) < r1; };
-      if (!SUM) {
-        // base-2 online logsumexp of x = T (s - 1): x log2(e) = c2 s - c2; the
-        // max over the raw similarities (c2 > 0), one fma + v_exp_f32 per element
-        float sm = -INFINITY;
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (valid(r)) sm = fmaxf(sm, acc[r]);
-        if (sm > -INFINITY) {
-          const float nm = fmaxf(run_m, c2 * sm - c2), off = -c2 - nm;
-          float add = 0.f;
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            if (valid(r)) add += __builtin_amdgcn_exp2f(fmaf(c2, acc[r], off));
-          run_s = run_s * __builtin_amdgcn_exp2f(run_m - nm) + add;
-          run_m = nm;
-        }
-      } else {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          if (!valid(r)) continue;
-          const int lr = 4 * h + (r & 3) + 8 * (r >> 2);  // row within the stage
-          const f32x4 m0 = *reinterpret_cast<const f32x4*>(M + lr * 8);
-          const f32x4 m1 = *reinterpret_cast<const f32x4*>(M + lr * 8 + 4);
-          const float aff = fmaf(a.T, acc[r], -a.T);
-          const float lp = (aff - m0[0]) + (aff - bm0[0]);  // log p = lpa + lpb
-          const float p = __builtin_amdgcn_exp2f(lp * 1.4426950408889634f);
-          const float dA = fabsf(m0[1] * bm1[0] + m0[2] * bm1[1] + m0[3]);    // A's line at B's point
-          const float dB = fabsf(bm0[1] * m1[0] + bm0[2] * m1[1] + bm0[3]);  // B's line at A's point
-          const float rp = ((dA < a.thr && dB < a.thr) ? a.good : a.bad) * p;
-          gs += rp;
-          if (want_r) rs += (double)(rp * (lp + (m1[2] + bm1[2])));
-        }
+  };
+  // LSE: the same tile with the previous stage's online-logsumexp epilogue
+  // (prev, FULL) threaded through the dependent MFMA chain by hand: fill(j)
+  // after the j-th MFMA, each slice at most an fma, a v_exp_f32 and an add
+  // (within the ~24 cycles an MFMA gap hides), a sched_barrier after each so
+  // the scheduler cannot cluster them again; the next k16 group's operands are
+  // read one group ahead
+  auto mma_lse = [&](const unsigned short* L, f32x16& acc, const f32x16& prev)
+      __attribute__((always_inline)) {
+    float sm = -INFINITY, nm = 0.f, nmc = 0.f, off = 0.f, scale = 0.f;
+    float ad[4] = {0.f, 0.f, 0.f, 0.f};
+    auto fill = [&](int j) __attribute__((always_inline)) {
+      if (j < 8) {
+        sm = fmaxf(sm, fmaxf(prev[2 * j], prev[2 * j + 1]));
+      } else if (j == 8) {
+        nm = fmaxf(run_m, c2 * sm - c2);
+        nmc = nm == -INFINITY ? 0.f : nm;
+        off = -c2 - nmc;
+      } else if (j == 9) {
+        scale = __builtin_amdgcn_exp2f(run_m - nmc);
+      } else if (j < 26) {
+        const int r = j - 10;
+        ad[r & 3] += __builtin_amdgcn_exp2f(fmaf(c2, prev[r], off));
+      } else if (j == 26) {
+        run_s = run_s * scale + ((ad[0] + ad[1]) + (ad[2] + ad[3]));
+        run_m = nm;
       }
     };
-    if (r0 + (s + 1) * F6STEP <= r1)
-      epilogue(std::true_type{});
-    else
-      epilogue(std::false_type{});
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    g6_u32x4 op[2][3];
+    auto ld = [&](int g, g6_u32x4* d) __attribute__((always_inline)) {
+      const int o = la * FD + (((2 * g + h) ^ (la & 15)) * 8);
+      d[0] = *reinterpret_cast<const g6_u32x4*>(L + o);
+      d[1] = *reinterpret_cast<const g6_u32x4*>(L + F6STEP * FD + o);
+      d[2] = *reinterpret_cast<const g6_u32x4*>(L + 2 * F6STEP * FD + o);
+    };
+    ld(0, op[0]);
+#pragma unroll
+    for (int g = 0; g < FD / 16; ++g) {
+      if (g + 1 < FD / 16) ld(g + 1, op[(g + 1) & 1]);
+      const g6_u32x4* A = op[g & 1];
+      const int pa[6] = {0, 0, 1, 0, 2, 1}, pb[6] = {0, 1, 0, 2, 0, 1};  // hh hm mh hl lh mm
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        acc = g6_mfma(A[pa[k]], bpl[g][pb[k]], acc);
+        fill(6 * g + k);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
   };
-  // straight-line prologue: stage 0, B's column, stage 1.  The explicit wait
-  // for B's loads keeps the waitcnt pass from putting a vmcnt(0) in front of
-  // every step's first MFMA (it could not prove them retired by the counted
-  // wait); a stage past the last is harmless (clamped rows, retired by the
-  // final wait below)
-  issue(0, Ps);
+  // acc[r] = S(A row r0 + s*32 + (r&3) + 8(r>>2) + 4h, B column cl); M: the
+  // stage's metadata (SUM).  FULL: every row of the stage exists.
+  auto epilogue = [&](auto full_t, int s, const f32x16& acc, const float* M)
+      __attribute__((always_inline)) {
+    constexpr bool FULL = decltype(full_t)::value;
+    const int rb = r0 + s * F6STEP + 4 * h;
+    auto valid = [&](int r) { return FULL || rb + (r & 3) + 8 * (r >> 2) < r1; };
+    if (!SUM) {
+      // base-2 online logsumexp of x = T (s - 1): x log2(e) = c2 s - c2; the
+      // max over the raw similarities (c2 > 0); one fma + v_exp_f32 per
+      // element, four partial sums.  Branch-free: a stage with no valid row
+      // (sm = -inf) adds exp2(-inf) = 0 and rescales by exp2(-inf - 0) = 0.
+      float sm = -INFINITY;
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (valid(r)) sm = fmaxf(sm, acc[r]);
+      const float nm = fmaxf(run_m, c2 * sm - c2);
+      const float nmc = nm == -INFINITY ? 0.f : nm;
+      const float off = -c2 - nmc;
+      float ad[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (valid(r)) ad[r & 3] += __builtin_amdgcn_exp2f(fmaf(c2, acc[r], off));
+      run_s = run_s * __builtin_amdgcn_exp2f(run_m - nmc) + ((ad[0] + ad[1]) + (ad[2] + ad[3]));
+      run_m = nm;
+    } else {
+      float gp[2] = {0.f, 0.f};
+      double rp2[2] = {0.0, 0.0};
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        if (!valid(r)) continue;
+        const int lr = 4 * h + (r & 3) + 8 * (r >> 2);  // row within the stage
+        const f32x4 m0 = *reinterpret_cast<const f32x4*>(M + lr * 8);
+        const f32x4 m1 = *reinterpret_cast<const f32x4*>(M + lr * 8 + 4);
+        const float aff = fmaf(a.T, acc[r], -a.T);
+        const float lp = (aff - m0[0]) + (aff - bm0[0]);  // log p = lpa + lpb
+        const float p = __builtin_amdgcn_exp2f(lp * 1.4426950408889634f);
+        const float dA = fabsf(m0[1] * bm1[0] + m0[2] * bm1[1] + m0[3]);    // A's line at B's point
+        const float dB = fabsf(bm0[1] * m1[0] + bm0[2] * m1[1] + bm0[3]);  // B's line at A's point
+        const float rp = ((dA < a.thr && dB < a.thr) ? a.good : a.bad) * p;
+        gp[r & 1] += rp;
+        if (WR) rp2[r & 1] += (double)(rp * (lp + (m1[2] + bm1[2])));
+      }
+      gs += gp[0] + gp[1];
+      if (WR) rs += rp2[0] + rp2[1];
+    }
+  };
+  // prologue: stage 0, then B's column (waited for explicitly: the waitcnt
+  // pass could not prove the counted waits retire it and put a vmcnt(0) in
+  // front of every step's first MFMA)
+  if (nsteps > 0) issue(0, Ps);
   {
     const unsigned short* bp = a.B.pl + (3 * pb + cpt) * FD;
 #pragma unroll
@@ -723,25 +775,61 @@ __global__ __launch_bounds__(256) void disk_flash6_kernel(FlashArgs a, int want_
     bm0 = *reinterpret_cast<const f32x4*>(a.B.meta + (pb + cpt) * 8);
     bm1 = *reinterpret_cast<const f32x4*>(a.B.meta + (pb + cpt) * 8 + 4);
   }
-  wait_vmcnt<0>();
-  issue(1, Ps + PSTAGE);
-  int slot = 0;
-  for (int i = 0; i < nsteps; ++i) {
+  // LSE: stage i's MFMAs and stage i-1's epilogue in one block (no branch
+  // between them), free to interleave.  SUM: each stage's epilogue right after
+  // its MFMAs (pipelined, its sixteen rows of metadata pushed the registers
+  // past two waves per SIMD).
+  // (two accumulators, named statically: the loop below is unrolled by two)
+  f32x16 acc0, acc1;
+  auto work = [&](int i, const unsigned short* L, f32x16& cur, const f32x16& prev)
+      __attribute__((always_inline)) {
+    if constexpr (SUM) {
+      mma(L, cur);
+      const float* M = reinterpret_cast<const float*>(L + PLANES);
+      if (!WR && i + 1 < nsteps)  // WR: the checked form (its fp64 sums need the registers)
+        epilogue(std::true_type{}, i, cur, M);
+      else
+        epilogue(std::false_type{}, i, cur, M);
+    } else {
+      mma_lse(L, cur, prev);  // + stage i-1's epilogue (i >= 1 here)
+    }
+  };
+  wait_vmcnt<0>();  // B's column and stage 0
+  if (nsteps > 1) issue(1, Ps + PSTAGE);
+  __builtin_amdgcn_s_barrier();
+  // step i: stages i+1 (issued a step earlier) and i+2 (issued now, into the
+  // slot of stage i-1, whose reads all finished before this step's barrier)
+  // stay in flight while stage i is multiplied
+  if (nsteps > 0)  // step 0 (LSE: no epilogue yet)
+    flash6_step(Ps + 2 * PSTAGE, Ps, Ps + PSTAGE,
+                [&](unsigned short* d, const unsigned short* L, const unsigned short*) {
+                  if (nsteps > 2) issue(2, d);
+                  if constexpr (SUM)
+                    work(0, L, acc0, acc1);
+                  else
+                    mma(L, acc0);
+                });
+  int slot = 1;  // stage i's slot; i-1's (= i+2's) is slot - 1 (mod 3)
+  auto step = [&](int i, f32x16& cur, const f32x16& prev) __attribute__((always_inline)) {
     if (i + 1 < nsteps)
-      wait_vmcnt<VPS>();  // stage i landed; stage i+1 may stay in flight
+      wait_vmcnt<SUM ? 7 : 6>();  // stage i landed, stage i+1 may stay in flight
     else
       wait_vmcnt<0>();
-    // every wave: stage i landed, and stage i-1 (the slot refilled below) consumed
-    __builtin_amdgcn_s_barrier();
-    const int refill = slot == 0 ? F6NST - 1 : slot - 1;
-    flash6_step(Ps + refill * PSTAGE, Ps + slot * PSTAGE,
-                [&](unsigned short* d, const unsigned short* L) {
-                  if (i + F6NST - 1 < nsteps) issue(i + F6NST - 1, d);
-                  compute(i, L);
+    __builtin_amdgcn_s_barrier();  // every wave's part of stage i; stage i-1's slot free
+    const int nxt = slot == F6NST - 1 ? 0 : slot + 1, prv = slot == 0 ? F6NST - 1 : slot - 1;
+    flash6_step(Ps + prv * PSTAGE, Ps + slot * PSTAGE, Ps + nxt * PSTAGE,
+                [&](unsigned short* d, const unsigned short* L, const unsigned short*) {
+                  if (i + 2 < nsteps) issue(i + 2, d);
+                  work(i, L, cur, prev);
                 });
-    slot = slot == F6NST - 1 ? 0 : slot + 1;
+    slot = nxt;
+  };
+  for (int i = 1; i < nsteps; i += 2) {  // odd steps into acc1, even into acc0
+    step(i, acc1, acc0);
+    if (i + 1 < nsteps) step(i + 1, acc0, acc1);
   }
-  wait_vmcnt<0>();  // no DMA may still write this workgroup's LDS after it ends
+  if (!SUM && nsteps > 0)
+    epilogue(std::false_type{}, nsteps - 1, (nsteps - 1) & 1 ? acc1 : acc0, nullptr);
   // merge the two lane halves (interleaved row sets) in a fixed order; the
   // partial's max back in natural units
   const long long o = ((long long)b * gridDim.y + split) * a.n + cl;
@@ -759,7 +847,7 @@ __global__ __launch_bounds__(256) void disk_flash6_kernel(FlashArgs a, int want_
     const double orr = __shfl_xor(rs, 32, 64);
     if (h == 0 && cok) {
       a.g_part[o] = gs + og;
-      if (want_r) a.r_part[o] = rs + orr;
+      if (WR) a.r_part[o] = rs + orr;
     }
   }
 }
@@ -911,10 +999,12 @@ void flash_split(const float* f, int b, int n, unsigned short* pl, hipStream_t s
 
 template <bool SUM>
 void launch_flash(dim3 grid, hipStream_t st, const FlashArgs& fa, int want_r) {
-  if (flash_bf6())
-    hipLaunchKernelGGL(disk_flash6_kernel<SUM>, grid, dim3(256), 0, st, fa, want_r);
-  else
+  if (!flash_bf6())
     hipLaunchKernelGGL(disk_flash_kernel<SUM>, grid, dim3(256), 0, st, fa, want_r);
+  else if (SUM && want_r)
+    hipLaunchKernelGGL((disk_flash6_kernel<true, true>), grid, dim3(256), 0, st, fa);
+  else
+    hipLaunchKernelGGL((disk_flash6_kernel<SUM, false>), grid, dim3(256), 0, st, fa);
 }
 
 bool use_flash() {

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Wave-state and instruction-mix counter passes over a short bench.py run
 # (one rocprofv3 --pmc run per group), summarised per kernel by
-# tools/pmc_summary.py.  usage: tools/pmc_kernels.sh <outdir>
+# tools/pmc_summary.py.  usage: [BENCH_ARGS="--workload corr ..."] tools/pmc_kernels.sh <outdir>
 out=${1:-gpurun_out/pmck}
 mkdir -p "$out"
 cd /tmp && export TMPDIR=/tmp
@@ -9,7 +9,8 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 run() {
   tag=$1; shift
   timeout -s KILL 200 rocprofv3 --pmc "$@" -d "$out/$tag" -o pmc --output-format csv \
-    -- python3 bench.py --steps 2 --warmup 1 --timing-steps 1 --no-cpu-baseline > "$out/$tag.log" 2>&1
+    -- python3 bench.py ${BENCH_ARGS:---steps 2 --warmup 1 --timing-steps 1 --no-cpu-baseline} \
+    > "$out/$tag.log" 2>&1
   rc=$?
   echo "[pmc] $tag rc=$rc" >> "$out/$tag.log"
   [ $rc -lt 124 ] || exit 100
