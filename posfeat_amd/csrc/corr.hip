@@ -226,33 +226,32 @@ __device__ __forceinline__ float2 bilinear128(const float* __restrict__ fm, int 
   const int x0 = (int)fx, y0 = (int)fy, x1 = x0 + 1, y1 = y0 + 1;
   const float wx1 = ix - fx, wx0 = 1.f - wx1;  // (x1 - ix), (ix - x0)
   const float wy1 = iy - fy, wy0 = 1.f - wy1;
-  float2 r = {0.f, 0.f};
+  // branch-free: every corner is loaded (index clamped into the map) and a
+  // corner outside it weighs 0, so a loop over samples can keep several
+  // samples' loads in flight; the sums keep their order (x + 0 p = x)
   const bool bx0 = (unsigned)x0 < (unsigned)w, bx1 = (unsigned)x1 < (unsigned)w;
   const bool by0 = (unsigned)y0 < (unsigned)h, by1 = (unsigned)y1 < (unsigned)h;
-  if (by0 && bx0) {
-    const float* p = fm + ((long long)y0 * w + x0) * 128;
-    const float wt = ((float)x1 - ix) * ((float)y1 - iy);
-    r.x += p[lane] * wt;
-    r.y += p[lane + 64] * wt;
-  }
-  if (by0 && bx1) {
-    const float* p = fm + ((long long)y0 * w + x1) * 128;
-    const float wt = (ix - (float)x0) * ((float)y1 - iy);
-    r.x += p[lane] * wt;
-    r.y += p[lane + 64] * wt;
-  }
-  if (by1 && bx0) {
-    const float* p = fm + ((long long)y1 * w + x0) * 128;
-    const float wt = ((float)x1 - ix) * (iy - (float)y0);
-    r.x += p[lane] * wt;
-    r.y += p[lane + 64] * wt;
-  }
-  if (by1 && bx1) {
-    const float* p = fm + ((long long)y1 * w + x1) * 128;
-    const float wt = (ix - (float)x0) * (iy - (float)y0);
-    r.x += p[lane] * wt;
-    r.y += p[lane + 64] * wt;
-  }
+  const int cx0 = min(max(x0, 0), w - 1), cx1 = min(max(x1, 0), w - 1);
+  const int cy0 = min(max(y0, 0), h - 1), cy1 = min(max(y1, 0), h - 1);
+  const float* p00 = fm + ((long long)cy0 * w + cx0) * 128 + lane;
+  const float* p01 = fm + ((long long)cy0 * w + cx1) * 128 + lane;
+  const float* p10 = fm + ((long long)cy1 * w + cx0) * 128 + lane;
+  const float* p11 = fm + ((long long)cy1 * w + cx1) * 128 + lane;
+  const float a00 = p00[0], b00 = p00[64], a01 = p01[0], b01 = p01[64];
+  const float a10 = p10[0], b10 = p10[64], a11 = p11[0], b11 = p11[64];
+  const float w00 = (by0 && bx0) ? ((float)x1 - ix) * ((float)y1 - iy) : 0.f;
+  const float w01 = (by0 && bx1) ? (ix - (float)x0) * ((float)y1 - iy) : 0.f;
+  const float w10 = (by1 && bx0) ? ((float)x1 - ix) * (iy - (float)y0) : 0.f;
+  const float w11 = (by1 && bx1) ? (ix - (float)x0) * (iy - (float)y0) : 0.f;
+  float2 r = {0.f, 0.f};
+  r.x += a00 * w00;
+  r.y += b00 * w00;
+  r.x += a01 * w01;
+  r.y += b01 * w01;
+  r.x += a10 * w10;
+  r.y += b10 * w10;
+  r.x += a11 * w11;
+  r.y += b11 * w11;
   (void)wx0;
   (void)wx1;
   (void)wy0;
@@ -305,20 +304,30 @@ __device__ __forceinline__ WinPatch window_patch_logits(const float* __restrict_
   const int np = P.PW * P.PH;
   const f32x4 qa = *reinterpret_cast<const f32x4*>(qp + cl * 8);
   const f32x4 qb = *reinterpret_cast<const f32x4*>(qp + cl * 8 + 4);
-  for (int base = 0; base < np; base += 4) {
-    const int pp = base + grp;
-    const int py = P.py0 + pp / P.PW, px = P.px0 + pp % P.PW;
-    float v = 0.f;
-    if (pp < np && (unsigned)py < (unsigned)h2 && (unsigned)px < (unsigned)w2) {
-      const float* src = fmb + ((long long)py * w2 + px) * 128 + cl * 8;
+  // 16 pixels per pass, branch-free (a pixel outside the map or past the
+  // patch reads a clamped address and yields 0), so their loads overlap
+  for (int base = 0; base < np; base += 16) {
+    float v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int pp = base + 4 * k + grp;
+      const int py = P.py0 + pp / P.PW, px = P.px0 + pp % P.PW;
+      const bool in = pp < np && (unsigned)py < (unsigned)h2 && (unsigned)px < (unsigned)w2;
+      const float* src = fmb + ((long long)min(max(py, 0), h2 - 1) * w2 + min(max(px, 0), w2 - 1)) *
+                                   128 + cl * 8;
       const f32x4 a = *reinterpret_cast<const f32x4*>(src);
       const f32x4 c = *reinterpret_cast<const f32x4*>(src + 4);
-      v = qa.x * a.x + qa.y * a.y + qa.z * a.z + qa.w * a.w + qb.x * c.x + qb.y * c.y +
-          qb.z * c.z + qb.w * c.w;
+      const float d = qa.x * a.x + qa.y * a.y + qa.z * a.z + qa.w * a.w + qb.x * c.x + qb.y * c.y +
+                      qb.z * c.z + qb.w * c.w;
+      v[k] = in ? d : 0.f;
     }
 #pragma unroll
-    for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    if (cl == 0 && pp < np) pc[pp] = v;
+    for (int k = 0; k < 4; ++k) {
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o, 64);
+      const int pp = base + 4 * k + grp;
+      if (cl == 0 && pp < np) pc[pp] = v[k];
+    }
   }
   wave_lds_sync();
   const int nw = win_h * win_w;
@@ -392,13 +401,29 @@ __global__ void line_window_kernel(const float* __restrict__ cpx,   // [b][n][2]
   const float e2x = (px[second] - c0) / c0, e2y = (py[second] - c1) / c1;
   const float dx = e2x - e1x, dy = e2y - e1y;
   // ---- line samples: logits (lane s holds logit s and s+64)
+  // four samples per pass (by hand: the wave sums are convergent, so the
+  // compiler will not unroll a loop of unknown trip count around them): their
+  // corner loads are in flight together
   float lg[2] = {-INFINITY, -INFINITY};
-  for (int s = 0; s < line_step; ++s) {
-    const float t = linspace_f(0.f, 1.f, line_step, s);
-    const float gx = __fadd_rn(__fmul_rn(dx, t), e1x), gy = __fadd_rn(__fmul_rn(dy, t), e1y);
-    const float2 v = bilinear128<true>(fmb, h2, w2, gx, gy, lane);
-    const float d = pf_wave_sum(q0 * v.x + q1 * v.y);
-    if ((s & 63) == lane) lg[s >> 6] = d;
+  for (int s0 = 0; s0 < line_step; s0 += 4) {
+    float d[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int s = min(s0 + k, line_step - 1);
+      const float t = linspace_f(0.f, 1.f, line_step, s);
+      const float gx = __fadd_rn(__fmul_rn(dx, t), e1x), gy = __fadd_rn(__fmul_rn(dy, t), e1y);
+      const float2 v = bilinear128<true>(fmb, h2, w2, gx, gy, lane);
+      d[k] = q0 * v.x + q1 * v.y;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float t = pf_wave_sum(d[k]);
+      const int s = s0 + k;
+      if (s < line_step) {
+        if (s == lane) lg[0] = t;
+        if (s == lane + 64) lg[1] = t;
+      }
+    }
   }
   float mx = fmaxf(lg[0], lg[1]);
 #pragma unroll
@@ -875,17 +900,18 @@ __global__ __launch_bounds__(256) void window_bwd_patch_kernel(
   // pass 2: dq = sum_p c_p fm[p]
   f32x4 da = {0.f, 0.f, 0.f, 0.f}, db = {0.f, 0.f, 0.f, 0.f};
   for (int base = 0; base < np; base += 4) {
+    // branch-free (clamped address, skipped pixels add nothing: the sums keep
+    // their order and values), so consecutive pixels' loads overlap
     const int pp = base + grp;
     const int py = py0 + pp / PW, px = px0 + pp % PW;
-    if (pp < np && (unsigned)py < (unsigned)h2 && (unsigned)px < (unsigned)w2) {
-      const float c = pc[pp];
-      if (c != 0.f) {
-        const long long off = ((long long)py * w2 + px) * 128;
-        const float* src = fmb + off + cl * 8;
-        da += c * *reinterpret_cast<const f32x4*>(src);
-        db += c * *reinterpret_cast<const f32x4*>(src + 4);
-      }
-    }
+    const bool in = pp < np && (unsigned)py < (unsigned)h2 && (unsigned)px < (unsigned)w2;
+    const float c = in ? pc[min(pp, np - 1)] : 0.f;
+    const float* src = fmb + ((long long)min(max(py, 0), h2 - 1) * w2 + min(max(px, 0), w2 - 1)) *
+                                 128 + cl * 8;
+    const f32x4 va = *reinterpret_cast<const f32x4*>(src);
+    const f32x4 vb = *reinterpret_cast<const f32x4*>(src + 4);
+    da += c * va;  // c = 0: adds +-0 (the map is finite)
+    db += c * vb;
   }
 #pragma unroll
   for (int o = 16; o < 64; o <<= 1) {
