@@ -923,23 +923,48 @@ __global__ __launch_bounds__(256) void tail2_partial_kernel(
   }
 }
 
-// per (image, channel): E[dx2^], E[dx2^ x2^]; summed over images: dW3[c]
-__global__ void tail2_finalize_kernel(const double* __restrict__ part, int nchunk, int nb, int hw,
-                                      float* __restrict__ e1, float* __restrict__ e2,
-                                      float* __restrict__ dw3) {
+// per (image, channel): E[dx2^], E[dx2^ x2^]; one block per image, thread
+// (channel c, lane j of 8) sums the chunks k = j mod 8, the 8 partials are
+// added in j order (fixed order, deterministic).  The image's dW3 share goes
+// to part[b][0][c][2] (this block has read the whole image's part by then);
+// tail2_dw3_kernel sums the images in order.  (One block of 128 threads
+// walking nb x nchunk chunks was latency-bound: 0.88 ms at 16 x 150.)
+__global__ __launch_bounds__(1024) void tail2_finalize_kernel(double* __restrict__ part,
+                                                              int nchunk, int hw,
+                                                              float* __restrict__ e1,
+                                                              float* __restrict__ e2) {
+  const int b = blockIdx.x, c = threadIdx.x & 127, j = threadIdx.x >> 7;
+  double* p = part + (long long)b * nchunk * 128 * 3;
+  double s1 = 0, s2 = 0, s3 = 0;
+  for (int k = j; k < nchunk; k += 8) {
+    s1 += p[(k * 128 + c) * 3];
+    s2 += p[(k * 128 + c) * 3 + 1];
+    s3 += p[(k * 128 + c) * 3 + 2];
+  }
+  __shared__ double red[8][128][3];
+  red[j][c][0] = s1;
+  red[j][c][1] = s2;
+  red[j][c][2] = s3;
+  __syncthreads();
+  if (j == 0) {
+    double t1 = 0, t2 = 0, t3 = 0;
+    for (int q = 0; q < 8; ++q) {
+      t1 += red[q][c][0];
+      t2 += red[q][c][1];
+      t3 += red[q][c][2];
+    }
+    e1[b * 128 + c] = (float)(t1 / hw);
+    e2[b * 128 + c] = (float)(t2 / hw);
+    p[c * 3 + 2] = t3;
+  }
+}
+
+// dW3[c] = sum over images (in order) of the per-image shares
+__global__ void tail2_dw3_kernel(const double* __restrict__ part, int nchunk, int nb,
+                                 float* __restrict__ dw3) {
   const int c = threadIdx.x;  // 128 threads
   double w = 0;
-  for (int b = 0; b < nb; ++b) {
-    double s1 = 0, s2 = 0;
-    const double* p = part + (long long)b * nchunk * 128 * 3;
-    for (int k = 0; k < nchunk; ++k) {
-      s1 += p[(k * 128 + c) * 3];
-      s2 += p[(k * 128 + c) * 3 + 1];
-      w += p[(k * 128 + c) * 3 + 2];
-    }
-    e1[b * 128 + c] = (float)(s1 / hw);
-    e2[b * 128 + c] = (float)(s2 / hw);
-  }
+  for (int b = 0; b < nb; ++b) w += part[(long long)b * nchunk * 128 * 3 + c * 3 + 2];
   dw3[c] = (float)w;
 }
 
@@ -1374,8 +1399,8 @@ int pf_tail_backward(const float* dlp, const float* y3, const float* m3, const f
                      t1);
   hipLaunchKernelGGL(tail2_partial_kernel, dim3(nchunk, nb), dim3(256), 0, st, dlp, y3, c2, c2cs,
                      hw, m3, r3, t1, nchunk, m2, r2, slope, w3, dy3, part, spart);
-  hipLaunchKernelGGL(tail2_finalize_kernel, dim3(1), dim3(128), 0, st, part, nchunk, nb, hw, e1, e2,
-                     dw3);
+  hipLaunchKernelGGL(tail2_finalize_kernel, dim3(nb), dim3(1024), 0, st, part, nchunk, hw, e1, e2);
+  hipLaunchKernelGGL(tail2_dw3_kernel, dim3(1), dim3(128), 0, st, part, nchunk, nb, dw3);
   const long long total = (long long)nb * hw * 32;
   hipLaunchKernelGGL(tail3_kernel, dim3(grid_for(total, 256)), dim3(256), 0, st, dy3, c2, c2cs, nb,
                      hw, m2, r2, slope, w3, e1, e2, dc2, dcs);
