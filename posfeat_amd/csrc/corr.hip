@@ -528,12 +528,15 @@ __global__ __launch_bounds__(1024) void epipolar_loss_kernel(
     float short_edge, float gthr, float wthr, float wg, float ww, float* __restrict__ out) {
   const int tid = threadIdx.x;
   const int total = nb * n;
-  __shared__ double red[16][8];
-  // four (cost, std, mask, F, coords) sets: g1, w1, g2, w2
-  double lsum[4], msum[4];
+  // one pass per set: with inv_i = 1 / std_i and m_i the mask, the weights
+  // w_i = m_i inv_i / mean(inv) give sum w = S / mean(inv) and sum w cost =
+  // C / mean(inv), S = sum m_i inv_i, C = sum m_i inv_i cost_i -- the same
+  // sums as set_weight's two passes, factored (fp64 throughout)
+  __shared__ double red[16][16];
+  double acc[4][4];
+#pragma unroll
   for (int k = 0; k < 4; ++k) {
-    // pass 1: mean of inverse std, masked count
-    double a1 = 0.0, a2 = 0.0;
+    double a1 = 0.0, a2 = 0.0, sm = 0.0, cm = 0.0;
     for (int i = tid; i < total; i += blockDim.x) {
       const int b = i / n;
       const float* F = (k < 2 ? F1 : F2) + b * 9;
@@ -542,58 +545,42 @@ __global__ __launch_bounds__(1024) void epipolar_loss_kernel(
       const float sd = (k == 0 ? sg1 : k == 1 ? sw1 : k == 2 ? sg2 : sw2)[i];
       const float cost = epi_cost(F, p[0], p[1], q[0], q[1]);
       const bool m = cost < short_edge * ((k & 1) ? wthr : gthr) && (k < 2 ? v1 : v2)[i];
-      a1 += 1.0 / fmaxf(sd, 1e-10f);
-      a2 += m ? 1.0 : 0.0;
+      const double inv = 1.0 / fmaxf(sd, 1e-10f);
+      a1 += inv;
+      if (m) {
+        a2 += 1.0;
+        sm += inv;
+        cm += inv * cost;
+      }
     }
-    // block reduce (fixed order)
-    double r1 = a1, r2 = a2;
-    for (int o = 32; o > 0; o >>= 1) {
-      r1 += __shfl_xor(r1, o, 64);
-      r2 += __shfl_xor(r2, o, 64);
+    acc[k][0] = a1;
+    acc[k][1] = a2;
+    acc[k][2] = sm;
+    acc[k][3] = cm;
+  }
+  // block reduce (fixed order)
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      double r = acc[k][j];
+      for (int o = 32; o > 0; o >>= 1) r += __shfl_xor(r, o, 64);
+      if ((tid & 63) == 0) red[tid >> 6][k * 4 + j] = r;
     }
-    if ((tid & 63) == 0) {
-      red[tid >> 6][0] = r1;
-      red[tid >> 6][1] = r2;
-    }
-    __syncthreads();
-    double inv_mean = 0.0, cnt = 0.0;
+  __syncthreads();
+  double lsum[4], msum[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    double a1 = 0.0, cnt = 0.0, sm = 0.0, cm = 0.0;
     for (int wv = 0; wv < (int)(blockDim.x >> 6); ++wv) {
-      inv_mean += red[wv][0];
-      cnt += red[wv][1];
+      a1 += red[wv][k * 4];
+      cnt += red[wv][k * 4 + 1];
+      sm += red[wv][k * 4 + 2];
+      cm += red[wv][k * 4 + 3];
     }
-    inv_mean /= total;
-    __syncthreads();
-    // set_weight: w = (inv/mean) * mask; w /= (mean(w) + 1e-8); loss = mean(w * cost)
-    double b1 = 0.0, b2 = 0.0;
-    for (int i = tid; i < total; i += blockDim.x) {
-      const int b = i / n;
-      const float* F = (k < 2 ? F1 : F2) + b * 9;
-      const float* p = (k < 2 ? c1 : c2) + 2 * i;
-      const float* q = (k == 0 ? g1 : k == 1 ? w1 : k == 2 ? g2 : w2) + 2 * i;
-      const float sd = (k == 0 ? sg1 : k == 1 ? sw1 : k == 2 ? sg2 : sw2)[i];
-      const float cost = epi_cost(F, p[0], p[1], q[0], q[1]);
-      const bool m = cost < short_edge * ((k & 1) ? wthr : gthr) && (k < 2 ? v1 : v2)[i];
-      const double wt = m ? (1.0 / fmaxf(sd, 1e-10f)) / inv_mean : 0.0;
-      b1 += wt;
-      b2 += wt * cost;
-    }
-    for (int o = 32; o > 0; o >>= 1) {
-      b1 += __shfl_xor(b1, o, 64);
-      b2 += __shfl_xor(b2, o, 64);
-    }
-    if ((tid & 63) == 0) {
-      red[tid >> 6][0] = b1;
-      red[tid >> 6][1] = b2;
-    }
-    __syncthreads();
-    double sw = 0.0, swc = 0.0;
-    for (int wv = 0; wv < (int)(blockDim.x >> 6); ++wv) {
-      sw += red[wv][0];
-      swc += red[wv][1];
-    }
-    __syncthreads();
-    const double wmean = sw / total + 1e-8;
-    lsum[k] = swc / wmean / total;
+    const double inv_mean = a1 / total;
+    const double wmean = sm / inv_mean / total + 1e-8;
+    lsum[k] = cm / inv_mean / wmean / total;
     msum[k] = cnt / total;
   }
   if (tid == 0) {
@@ -634,27 +621,31 @@ __global__ __launch_bounds__(1024) void epi_loss_bwd_kernel(
   const int tid = threadIdx.x;
   const int total = nb * n;
   __shared__ double red[16][2];
-  double a1 = 0.0;
-  for (int i = tid; i < total; i += blockDim.x) a1 += 1.0 / fmaxf(wsd[i], 1e-10f);
-  for (int o = 32; o > 0; o >>= 1) a1 += __shfl_xor(a1, o, 64);
-  if ((tid & 63) == 0) red[tid >> 6][0] = a1;
-  __syncthreads();
-  double inv_mean = 0.0;
-  for (int wv = 0; wv < (int)(blockDim.x >> 6); ++wv) inv_mean += red[wv][0];
-  inv_mean /= total;
-  __syncthreads();
-  double b1 = 0.0;
+  // sum inv and sum m inv in one pass (the forward's factored set_weight sums)
+  double a1 = 0.0, b1 = 0.0;
   for (int i = tid; i < total; i += blockDim.x) {
+    const double inv = 1.0 / fmaxf(wsd[i], 1e-10f);
     const float* F = Fm + (i / n) * 9;
     const float cost = epi_cost(F, cq[2 * i], cq[2 * i + 1], wpx[2 * i], wpx[2 * i + 1]);
-    const bool m = cost < short_edge * wthr && v[i];
-    b1 += m ? (1.0 / fmaxf(wsd[i], 1e-10f)) / inv_mean : 0.0;
+    a1 += inv;
+    if (cost < short_edge * wthr && v[i]) b1 += inv;
   }
-  for (int o = 32; o > 0; o >>= 1) b1 += __shfl_xor(b1, o, 64);
-  if ((tid & 63) == 0) red[tid >> 6][0] = b1;
+  for (int o = 32; o > 0; o >>= 1) {
+    a1 += __shfl_xor(a1, o, 64);
+    b1 += __shfl_xor(b1, o, 64);
+  }
+  if ((tid & 63) == 0) {
+    red[tid >> 6][0] = a1;
+    red[tid >> 6][1] = b1;
+  }
   __syncthreads();
-  double sw = 0.0;
-  for (int wv = 0; wv < (int)(blockDim.x >> 6); ++wv) sw += red[wv][0];
+  double sa = 0.0, sb = 0.0;
+  for (int wv = 0; wv < (int)(blockDim.x >> 6); ++wv) {
+    sa += red[wv][0];
+    sb += red[wv][1];
+  }
+  const double inv_mean = sa / total;
+  const double sw = sb / inv_mean;
   const double wmean = sw / total + 1e-8;
   for (int i = tid; i < total; i += blockDim.x) {
     const float* F = Fm + (i / n) * 9;
