@@ -305,7 +305,10 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
   const float* xrow[RB];
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb)
-    xrow[rb] = A + (long long)min(m0 + wave * RB * 16 + rb * 16 + r16, a.M - 1) * a.K + kq * 8;
+    // FL & 8: A loads 64 contiguous bytes per row per instruction (k = 16 jj + 4 kq
+    // .. + 3: timing only -- the k pairing with B is not the MFMA's)
+    xrow[rb] = A + (long long)min(m0 + wave * RB * 16 + rb * 16 + r16, a.M - 1) * a.K +
+               ((FL & 8) ? kq * 4 : kq * 8);
   const unsigned short* bsrc[B_G];
 #pragma unroll
   for (int i = 0; i < B_G; ++i) {
@@ -327,7 +330,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
     for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
-        v[rb][j] = *reinterpret_cast<const f32x4*>(xrow[rb] + (long long)la_c * BK + j * 4);
+        v[rb][j] = *reinterpret_cast<const f32x4*>(xrow[rb] + (long long)la_c * BK +
+                                                   j * ((FL & 8) ? 16 : 4));
     if (la_c + 1 < nch) ++la_c;
   };
 #pragma unroll
@@ -363,7 +367,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
                 (__attribute__((address_space(3))) void*)(Bn + (wave * B_G + op) * 16 * BK), 16, 0, 0);
           } else if (op < B_G + NA) {
             const int j = op - B_G, rb = j >> 1, jj = j & 1;
-            va[u][rb][jj] = *reinterpret_cast<const f32x4*>(xrow[rb] + (long long)la_c * BK + jj * 4);
+            va[u][rb][jj] = *reinterpret_cast<const f32x4*>(xrow[rb] + (long long)la_c * BK +
+                                                            jj * ((FL & 8) ? 16 : 4));
             if (j == NA - 1 && la_c + 1 < nch) ++la_c;
           }
           __builtin_amdgcn_sched_barrier(PIN);
@@ -481,9 +486,9 @@ int main(int argc, char** argv) {
     printf("%-28s %8.3f ms  %7.1f TF/s fp32-eq  %.3f of 416.7\n", name, ms, fl / ms / 1e9,
            fl / ms / 1e9 / 416.7);
   };
-  rep("base MI1 D2", run(k32<1, 2, 0>, a, 128, nb, reps));
-  rep("noA noB", run(k32<1, 2, 3>, a, 128, nb, reps));
   rep("16x16x32 D1", run(k16<1, 0>, a, 128, nb, reps));
-  rep("16x16x32 D1 front", run(k16<1, 4>, a, 128, nb, reps));
+  rep("16x16x32 D1 contiguous-A", run(k16<1, 8>, a, 128, nb, reps));
+  rep("16x16x32 D1 again", run(k16<1, 0>, a, 128, nb, reps));
+  rep("16x16x32 D1 contiguous-A again", run(k16<1, 8>, a, 128, nb, reps));
   return 0;
 }
