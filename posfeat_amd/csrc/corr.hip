@@ -891,19 +891,27 @@ __global__ __launch_bounds__(256) void window_bwd_patch_kernel(
   if (lane == 0) prec[wid] = make_int4(px0, py0, PW, P.PH);
   // pass 2: dq = sum_p c_p fm[p]
   f32x4 da = {0.f, 0.f, 0.f, 0.f}, db = {0.f, 0.f, 0.f, 0.f};
-  for (int base = 0; base < np; base += 4) {
-    // branch-free (clamped address, skipped pixels add nothing: the sums keep
-    // their order and values), so consecutive pixels' loads overlap
-    const int pp = base + grp;
-    const int py = py0 + pp / PW, px = px0 + pp % PW;
-    const bool in = pp < np && (unsigned)py < (unsigned)h2 && (unsigned)px < (unsigned)w2;
-    const float c = in ? pc[min(pp, np - 1)] : 0.f;
-    const float* src = fmb + ((long long)min(max(py, 0), h2 - 1) * w2 + min(max(px, 0), w2 - 1)) *
-                                 128 + cl * 8;
-    const f32x4 va = *reinterpret_cast<const f32x4*>(src);
-    const f32x4 vb = *reinterpret_cast<const f32x4*>(src + 4);
-    da += c * va;  // c = 0: adds +-0 (the map is finite)
-    db += c * vb;
+  for (int base = 0; base < np; base += 16) {
+    // 16 pixels per pass, branch-free (clamped address, skipped pixels add
+    // nothing: the sums keep their order and values), so their loads overlap
+    f32x4 va[4], vb[4];
+    float c[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int pp = base + 4 * k + grp;
+      const int py = py0 + pp / PW, px = px0 + pp % PW;
+      const bool in = pp < np && (unsigned)py < (unsigned)h2 && (unsigned)px < (unsigned)w2;
+      c[k] = in ? pc[min(pp, np - 1)] : 0.f;
+      const float* src = fmb + ((long long)min(max(py, 0), h2 - 1) * w2 + min(max(px, 0), w2 - 1)) *
+                                   128 + cl * 8;
+      va[k] = *reinterpret_cast<const f32x4*>(src);
+      vb[k] = *reinterpret_cast<const f32x4*>(src + 4);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      da += c[k] * va[k];  // c = 0: adds +-0 (the map is finite)
+      db += c[k] * vb[k];
+    }
   }
 #pragma unroll
   for (int o = 16; o < 64; o <<= 1) {
