@@ -352,16 +352,21 @@ __global__ __launch_bounds__(1024) void disk_final_kernel(const double* __restri
   __shared__ double r1[1024], r2[1024], r3[1024];
   double s = 0.0, lp = 0.0, nk = 0.0;
   for (int i = threadIdx.x; i < nparts; i += blockDim.x) s += part[i];
-  for (int i = threadIdx.x; i < nb * n1; i += blockDim.x)
-    if (acc1[i]) {
-      lp += logp1[i];
-      nk += 1.0;
-    }
-  for (int i = threadIdx.x; i < nb * n2; i += blockDim.x)
-    if (acc2[i]) {
-      lp += logp2[i];
-      nk += 1.0;
-    }
+  // branch-free (logp loaded whatever the flag, a rejected point adds 0.0):
+  // one workgroup walks every point, so the loads of consecutive iterations
+  // must not wait on each other's flags
+  for (int i = threadIdx.x; i < nb * n1; i += blockDim.x) {
+    const bool a = acc1[i] != 0;
+    const double v = logp1[i];
+    lp += a ? v : 0.0;
+    nk += a ? 1.0 : 0.0;
+  }
+  for (int i = threadIdx.x; i < nb * n2; i += blockDim.x) {
+    const bool a = acc2[i] != 0;
+    const double v = logp2[i];
+    lp += a ? v : 0.0;
+    nk += a ? 1.0 : 0.0;
+  }
   r1[threadIdx.x] = s;
   r2[threadIdx.x] = lp;
   r3[threadIdx.x] = nk;
