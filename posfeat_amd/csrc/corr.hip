@@ -544,14 +544,15 @@ __global__ __launch_bounds__(1024) void epipolar_loss_kernel(
       const float* q = (k == 0 ? g1 : k == 1 ? w1 : k == 2 ? g2 : w2) + 2 * i;
       const float sd = (k == 0 ? sg1 : k == 1 ? sw1 : k == 2 ? sg2 : sw2)[i];
       const float cost = epi_cost(F, p[0], p[1], q[0], q[1]);
-      const bool m = cost < short_edge * ((k & 1) ? wthr : gthr) && (k < 2 ? v1 : v2)[i];
+      // branch-free (the flag loaded whatever the cost; a masked point adds
+      // 0.0): one workgroup walks every point, so iterations must overlap
+      const bool vf = (k < 2 ? v1 : v2)[i] != 0;
+      const bool m = (cost < short_edge * ((k & 1) ? wthr : gthr)) & vf;
       const double inv = 1.0 / fmaxf(sd, 1e-10f);
       a1 += inv;
-      if (m) {
-        a2 += 1.0;
-        sm += inv;
-        cm += inv * cost;
-      }
+      a2 += m ? 1.0 : 0.0;
+      sm += m ? inv : 0.0;
+      cm += m ? inv * cost : 0.0;
     }
     acc[k][0] = a1;
     acc[k][1] = a2;
@@ -628,7 +629,8 @@ __global__ __launch_bounds__(1024) void epi_loss_bwd_kernel(
     const float* F = Fm + (i / n) * 9;
     const float cost = epi_cost(F, cq[2 * i], cq[2 * i + 1], wpx[2 * i], wpx[2 * i + 1]);
     a1 += inv;
-    if (cost < short_edge * wthr && v[i]) b1 += inv;
+    const bool vf = v[i] != 0;
+    b1 += ((cost < short_edge * wthr) & vf) ? inv : 0.0;  // branch-free (as the forward)
   }
   for (int o = 32; o > 0; o >>= 1) {
     a1 += __shfl_xor(a1, o, 64);
@@ -655,7 +657,8 @@ __global__ __launch_bounds__(1024) void epi_loss_bwd_kernel(
     const float c = F[6] * x1 + F[7] * y1 + F[8];
     const float nrm = fmaxf(sqrtf(a * a + b * b), 1e-8f);
     const float sv = x2 * (a / nrm) + y2 * (b / nrm) + (c / nrm);
-    const bool m = fabsf(sv) < short_edge * wthr && v[i];
+    const bool vf = v[i] != 0;
+    const bool m = (fabsf(sv) < short_edge * wthr) & vf;
     float gx = 0.f, gy = 0.f;
     if (m) {
       const double wt = (1.0 / fmaxf(wsd[i], 1e-10f)) / inv_mean / wmean;
