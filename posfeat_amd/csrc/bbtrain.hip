@@ -360,7 +360,7 @@ void plan(posfeat_bbtrain* m) {
   alloc(m->dsn, fl(MAXG));
   alloc(m->part, 2 * 1100 * 1024 * sizeof(double));
   alloc(m->coef, fl(3 * 1024));
-  alloc(m->bnsum, 4 * 1024 * sizeof(double));
+  alloc(m->bnsum, 2 * BN_SUM_SLOT * sizeof(double));
   alloc(m->ga, fl(MAXG));
   alloc(m->gb, fl(MAXG));
   alloc(m->gc, fl(MAXG));
@@ -482,14 +482,14 @@ int layer_fwd(Ctx& c, int li, const float* x, int xcs, int h, int w, float* out,
       hipLaunchKernelGGL(bn_stats_final_kernel, dim3((L.cout + 3) / 4), dim3(256), 0, c.st,
                          c.sd(m->part), g.nchunk, L.cout, P, mom, mean, rstd,
                          stats ? stats + L.rm_off : nullptr, stats ? stats + L.rv_off : nullptr);
-    } else {  // SyncBatchNorm: sums over the group, every rank's count P
+    } else {  // SyncBatchNorm: sums and pixel counts over the group
       double* sums = c.sd(m->bnsum);
       hipLaunchKernelGGL(bn_sums_kernel, dim3((L.cout + 3) / 4), dim3(256), 0, c.st,
-                         c.sd(m->part), g.nchunk, L.cout, sums, nullptr);
+                         c.sd(m->part), g.nchunk, L.cout, (double)P, sums, nullptr);
       PF_CHECK_LAUNCH();
-      PF_TRY(pf_group_allreduce(m->group, sums, 2 * L.cout, c.st));
+      PF_TRY(pf_group_allreduce(m->group, sums, 2 * L.cout + 1, c.st));
       hipLaunchKernelGGL(bn_stats_from_sums_kernel, dim3((L.cout + 255) / 256), dim3(256), 0,
-                         c.st, sums, L.cout, (double)P * world, mom, mean, rstd,
+                         c.st, sums, L.cout, mom, mean, rstd,
                          stats ? stats + L.rm_off : nullptr, stats ? stats + L.rv_off : nullptr);
     }
     if (out)
@@ -544,15 +544,15 @@ int layer_bwd(Ctx& c, int li, const float* x, int xcs, int h, int w, const float
       hipLaunchKernelGGL(bn_bwd_final_kernel, dim3((C + 3) / 4), dim3(256), 0, c.st,
                          c.sd(m->part), g.nchunk, C, P, c.prm + L.g_off, rstd, grad + L.g_off,
                          grad + L.be_off, acc, coef);
-    } else {  // SyncBatchNorm backward: E[g], E[g x^] over the group
+    } else {  // SyncBatchNorm backward: E[g], E[g x^] over the group's count
       double* loc = c.sd(m->bnsum);
-      double* grp = loc + 2 * 1024;
+      double* grp = loc + BN_SUM_SLOT;
       hipLaunchKernelGGL(bn_sums_kernel, dim3((C + 3) / 4), dim3(256), 0, c.st, c.sd(m->part),
-                         g.nchunk, C, loc, grp);
+                         g.nchunk, C, (double)P, loc, grp);
       PF_CHECK_LAUNCH();
-      PF_TRY(pf_group_allreduce(m->group, grp, 2 * C, c.st));
+      PF_TRY(pf_group_allreduce(m->group, grp, 2 * C + 1, c.st));
       hipLaunchKernelGGL(bn_bwd_from_sums_kernel, dim3((C + 255) / 256), dim3(256), 0, c.st, loc,
-                         grp, C, (double)P * world, c.prm + L.g_off, rstd, grad + L.g_off,
+                         grp, C, c.prm + L.g_off, rstd, grad + L.g_off,
                          grad + L.be_off, acc, coef);
     }
     hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(P * c4n, 256)), dim3(256), 0, c.st, y, P,

@@ -8,6 +8,9 @@ namespace bbt {
 
 enum { ACT_NONE = 0, ACT_RELU = 1, ACT_ELU = 2 };
 constexpr float BN_EPS = 1e-5f;
+// doubles per SyncBatchNorm exchange slot: [sum | sum of squares | count] of up
+// to 1024 channels (2 C + 1), padded
+constexpr int BN_SUM_SLOT = 2 * 1024 + 8;
 
 __device__ __forceinline__ float act_grad(int act, float a) {
   return act == ACT_RELU ? (a > 0.f ? 1.f : 0.f) : act == ACT_ELU ? (a > 0.f ? 1.f : a + 1.f) : 1.f;
@@ -150,13 +153,22 @@ __global__ __launch_bounds__(256) void bn_stats_final_kernel(
 // SyncBatchNorm split of the two final kernels: chunk partials -> per-channel
 // sums [2][C] (fp64), then (after the cross-rank sum) the statistics from the
 // group totals over Ptot = the group's pixel count.
+// SyncBatchNorm: this rank's [sum | sum of squares | pixel count] (2 C + 1
+// doubles) for the group all-reduce; the count travels with the sums so the
+// group normalises by the total count even when ranks hold different batches
+// (torch.nn.SyncBatchNorm gathers the per-rank counts the same way)
 __global__ __launch_bounds__(256) void bn_sums_kernel(const double* __restrict__ part, int nchunk,
-                                                      int C, double* __restrict__ sums,
+                                                      int C, double count,
+                                                      double* __restrict__ sums,
                                                       double* __restrict__ sums_copy) {
   __shared__ double red[2][64][4];
   double s, ss;
   bn_chunk_sum(part, nchunk, C, red, s, ss);
   const int c = blockIdx.x * 4 + (threadIdx.x & 3);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    sums[2 * C] = count;
+    if (sums_copy) sums_copy[2 * C] = count;
+  }
   if ((threadIdx.x >> 2) != 0 || c >= C) return;
   sums[c] = s;
   sums[C + c] = ss;
@@ -166,12 +178,12 @@ __global__ __launch_bounds__(256) void bn_sums_kernel(const double* __restrict__
   }
 }
 
-__global__ void bn_stats_from_sums_kernel(const double* __restrict__ sums, int C, double Ptot,
-                                          float mom, float* __restrict__ mean,
-                                          float* __restrict__ rstd, float* __restrict__ rm,
-                                          float* __restrict__ rv) {
+__global__ void bn_stats_from_sums_kernel(const double* __restrict__ sums, int C, float mom,
+                                          float* __restrict__ mean, float* __restrict__ rstd,
+                                          float* __restrict__ rm, float* __restrict__ rv) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
+  const double Ptot = sums[2 * C];  // the group's pixel count
   const double mu = sums[c] / Ptot;
   double var = sums[C + c] / Ptot - mu * mu;
   var = var > 0.0 ? var : 0.0;
@@ -186,13 +198,14 @@ __global__ void bn_stats_from_sums_kernel(const double* __restrict__ sums, int C
 
 // dgamma / dbeta from this rank's sums, the apply coefficients from the group's
 __global__ void bn_bwd_from_sums_kernel(const double* __restrict__ local,
-                                        const double* __restrict__ group, int C, double Ptot,
+                                        const double* __restrict__ group, int C,
                                         const float* __restrict__ gam,
                                         const float* __restrict__ rstd, float* __restrict__ dgam,
                                         float* __restrict__ dbet, int acc,
                                         float* __restrict__ coef) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
+  const double Ptot = group[2 * C];  // the group's pixel count
   const double sg = local[c], sgx = local[C + c];
   dgam[c] = acc ? dgam[c] + (float)sgx : (float)sgx;
   dbet[c] = acc ? dbet[c] + (float)sg : (float)sg;

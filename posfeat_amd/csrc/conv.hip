@@ -2751,6 +2751,8 @@ void launch_up4_weights(const float* w_packed, float* wph, hipStream_t st) {
 
 }  // namespace
 
+bool pf_bf6x_on() { return bf6x_on(); }
+bool pf_halo_bf6_on() { return halo_bf6_on(); }
 PfHaloFp32Scope::PfHaloFp32Scope() { ++tl_halo_fp32; }
 PfHaloFp32Scope::~PfHaloFp32Scope() { --tl_halo_fp32; }
 PfDense32Scope::PfDense32Scope(bool on) : on_(on) { tl_dense32 += on ? 1 : 0; }

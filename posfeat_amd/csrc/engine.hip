@@ -284,9 +284,12 @@ TileCache& tile_cache() {
 }
 std::string desc_class(const posfeat_conv_desc& d, bool res, bool wplanes) {
   char b[160];
-  snprintf(b, sizeof b, "%d/%d/%d/%dx%d/s%d/p%d/%d/%d/a%d/r%d/P%d%s", d.cin, d.x_cstride, d.cout,
-           d.kh, d.kw, d.stride, d.pad, d.y_cstride, d.res_cstride, d.act, res ? 1 : 0,
-           pf_conv_precision(), wplanes ? "B" : "");
+  // the calling thread's tile scope too (PfDense32Scope / PfHaloFp32Scope
+  // change the legal candidates: a training instance's choice must not be
+  // reused by an extraction engine)
+  snprintf(b, sizeof b, "%d/%d/%d/%dx%d/s%d/p%d/%d/%d/a%d/r%d/P%d%s/x%d%d", d.cin, d.x_cstride,
+           d.cout, d.kh, d.kw, d.stride, d.pad, d.y_cstride, d.res_cstride, d.act, res ? 1 : 0,
+           pf_conv_precision(), wplanes ? "B" : "", pf_bf6x_on() ? 1 : 0, pf_halo_bf6_on() ? 1 : 0);
   return b;
 }
 double desc_m(const posfeat_conv_desc& d) {

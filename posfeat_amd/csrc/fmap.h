@@ -150,6 +150,10 @@ int pf_imgbr_grad(const float* A, int n, int HW, const float* w2p, const float* 
 
 // conv product arithmetic: 0 fp32 MFMA, 1 bf16x6, 2 bf16x6 + pre-split GEMMs
 int pf_conv_precision();
+// the calling thread's tile arithmetic (conv.hip): the 16x16x32 dense tiles and the
+// bf16x6 halo tiles are on unless a training scope turned them off
+bool pf_bf6x_on();
+bool pf_halo_bf6_on();
 // while alive, this thread's 3x3 stride-1 (halo) convs use fp32 MFMA tiles
 struct PfHaloFp32Scope {
   PfHaloFp32Scope();

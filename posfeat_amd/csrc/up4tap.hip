@@ -217,39 +217,436 @@ __global__ __launch_bounds__(256) void up4tap_combine_kernel(const float* __rest
 // (write, read, write; 3 x 5 GB at B = 32, 480 x 640).  Here the same block
 // (image, 16 output rows, 32 output columns, 32 channels) first computes its G
 // part -- the per-image folded 5x5 conv of the image (gfuse.hip), K = 80
-// bf16x6 over pre-split weight planes -- while its P tile streams into LDS,
-// then adds the tap-summed interpolation and writes y once, with the IN
-// statistics.  The MFMA roles are swapped against the k80 kernel (A = pixels,
-// B = couts), with the 32 M rows of a tile mapped to 16 rows x 2 columns:
-// acc[r] of lane (cout n, half h) is then output row r of column 2p + h, i.e.
-// a lane holds one channel of one output column over all 16 rows -- exactly
-// the combine's per-thread sliding-window layout (one channel instead of a
-// quad), so the accumulators become the combine's running sums with no LDS
-// transpose.  Border-ring pixels take their G value from the ring buffer
-// (pf_gfuse_prep: conv2 sees G's zero padding there, not the fold).
-constexpr int GC_PR = 20, GC_PC = 36;  // image patch rows / pixels (16 x 32 + the 5x5 halo)
-constexpr int GC_PP = 38;              // LDS pixel slots per patch row (conflict-free b128 A reads)
-constexpr int GC_PDMA = 12;            // patch DMA instructions (64 slots each, >= 20 x 38)
-constexpr int GC_K = 80;               // k = dy * 16 + dx * 3 + c, k % 16 == 15: zero weight
-constexpr int GC_DMA = CB_SEGP / 8 / 4;  // P-tile DMA instructions per wave
-static_assert(CB_SEGP % 32 == 0, "P-tile DMA instructions split evenly over the 4 waves");
-static_assert(GC_PDMA % 4 == 0 && GC_PDMA * 64 >= GC_PR * GC_PP, "patch DMA covers the patch");
-__device__ float gc_zero4[4];  // the DMA source of patch pixels outside the image
+// bf16x6 over pre-split weight planes -- while its P tile streams in, then
+// adds the tap-summed interpolation and writes y once, with the IN
+// statistics.
+//
+// Round 4 layout (the round-3 form was VALU-bound: 4486 VALU per 120 MFMA per
+// wave, PMC):
+// * The image patch (20 x 36 pixels) is split into its three bf16 planes ONCE
+//   per block -- each thread splits a pixel pair from registers -- and stored
+//   3-channel packed (GC_S dwords per patch row and plane), so an MFMA operand
+//   (8 consecutive k = dx * 3 + c of one patch row) is 8 consecutive bf16.
+//   The round-3 kernel split every operand in registers (each patch pixel
+//   once per column tile and tap row).
+// * The 32 MFMA rows of tile t are 16 output rows x the columns (c, c + 4),
+//   c = 8 wave + t: an operand's start element 3c + 8h (+ 12) has the parity of
+//   t in every lane, so even tiles read whole dwords and odd tiles one extra
+//   dword and a v_alignbit each -- no lane-dependent selects -- and an output
+//   column's phase X % 4 is t, a compile-time constant of the interpolation.
+// * The P tile is staged through registers into an LDS layout that pairs tile
+//   rows: [row pair][column][tap][channel][2 rows], so the x interpolation of
+//   two rows is one ds_read_b64 and one v_pk_fma_f32 per tap.  Rows 0-3 load
+//   before the G phase and land during it; rows 4-5 share LDS with the patch
+//   planes and are written after it (68 KB: two blocks per CU).
+// * The y interpolation runs on output-row pairs in packed fp32 with
+//   compile-time coefficient pairs; y leaves through buffer stores (uniform row
+//   offset, no per-store address arithmetic).
+// * Blocks away from the image border (every clamp, the conv's zero padding,
+//   the border ring and ragged columns need no test there) take a branch-free
+//   instantiation.
+// The MFMA roles: A = pixels, B = couts; acc[t][r] of lane (cout n, half h) is
+// output row r of column 8 wave + t + 4h -- one channel of one column over all
+// 16 rows, the combine's sliding-window layout.  Border-ring pixels take their
+// G value from the ring buffer (pf_gfuse_prep: conv2 sees G's zero padding
+// there, not the fold).
+constexpr int GC_PR = 20, GC_PC = 36;       // image patch rows / pixels (16 x 32 + the 5x5 halo)
+constexpr int GC_S = 60;                    // dwords per patch row and plane (54 used; banks)
+constexpr int GC_PLANE = GC_PR * GC_S;      // dwords per plane
+constexpr int GC_PAIRS = GC_PR * GC_PC / 2;  // pixel pairs of the patch (one split each)
+constexpr int GC_K = 80;                    // k = dy * 16 + dx * 3 + c, k % 16 == 15: zero weight
+constexpr int GC_CELL = 9 * CB_CG * 2;      // floats per (row pair, column): 9 taps x 32 ch x 2 rows
+constexpr int GC_RP = CB_CX * GC_CELL;      // floats per row pair
+constexpr int GC_NA = 2 * CB_CX * 9 * (CB_CG / 4);  // P items (2 rows x 4 ch) of rows 0-3
+constexpr int GC_NB = CB_CX * 9 * (CB_CG / 4);      // ... of rows 4-5
+constexpr int GC_UA = (GC_NA + 255) / 256, GC_UB = (GC_NB + 255) / 256;  // per thread
+static_assert(3 * GC_PLANE <= GC_NB * 8, "the patch planes fit over P-tile rows 4-5");
+static_assert(16 * 32 * CB_CG + 4 * CB_CG * 4 <= (GC_NA + GC_NB) * 8, "y tile + statistics fit");
+static_assert(GC_PAIRS <= 512, "two pixel pairs per thread");
 
+// this wave's LDS operations have completed (vector memory untouched)
+__device__ __forceinline__ void gc_wait_lgkm0() {
+  __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (0 << 8) | (3 << 14));
+}
 // wait until at most N vector-memory operations of this wave are outstanding
 template <int N>
 __device__ __forceinline__ void gc_wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
 }
+// workgroup barrier without the fence __syncthreads() adds (a fence drains
+// vmcnt: the loads in flight and the y stores)
+__device__ __forceinline__ void gc_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
 
+// y-interpolation coefficient of R row i + j (j in -1..1) for output row
+// 4 i + r and tap row ky: up4_w of d = r + ky - 1
+__host__ __device__ constexpr float gc_cy(int r, int ky, int j) {
+  const int d = r + ky - 1;
+  const int lo = d <= 1 ? -1 : 0;
+  const float wa = d == -1 ? 0.625f : d == 0 ? 0.375f : d == 1 ? 0.125f
+                 : d == 2 ? 0.875f : d == 3 ? 0.625f : 0.375f;
+  return j == lo ? wa : j == lo + 1 ? 1.f - wa : 0.f;
+}
+
+__device__ unsigned long long gc_ts[80000 * 8];
+#define GC_TS(i) do { if ((ABL & 8) && tid == 0) { const long long bi = blockIdx.x; if (bi < 80000) gc_ts[bi * 8 + (i)] = (i) == 0 ? __builtin_amdgcn_s_memrealtime() : __builtin_amdgcn_s_memtime(); if ((i) == 0) gc_ts[bi * 8 + 7] = ((unsigned long long)__builtin_amdgcn_s_getreg(0xF804) << 16) | __builtin_amdgcn_s_getreg(0x7814); } } while (0)
+typedef float gc_f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ gc_f2 gc_fma2(gc_f2 a, gc_f2 b, gc_f2 c) {
+  return __builtin_elementwise_fma(a, b, c);
+}
+__device__ __forceinline__ f32x4 gc_bload(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+
+template <bool IN, int ABL>
+__device__ __forceinline__ void gc_block(const float* __restrict__ P, int h, int w,
+                                         const float* __restrict__ img4,
+                                         const unsigned short* __restrict__ wp,
+                                         const float* __restrict__ bc,
+                                         const float* __restrict__ ring, float* __restrict__ y,
+                                         int ycs, double* __restrict__ part, float* spA,
+                                         float* spB, int b, int qb, int xb, int cg, int nqb,
+                                         int nxb) {
+  const int H = 4 * h, W = 4 * w;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hl = lane >> 5, ln = lane & 31;
+  const int q0 = qb * TQ, qx0 = xb * CB_QX, Y0 = 4 * q0, X0 = 4 * qx0;
+  const int co = cg * CB_CG + ln;
+  GC_TS(0);
+  GC_TS(1);
+  // ---- loads: the B operands (this channel group's weight planes), the patch
+  // pixel pairs and P-tile rows 0-3 into registers ------------------------------
+  const __amdgpu_buffer_rsrc_t irs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(img4 + (long long)b * H * W * 4), (short)0, 0x7fffffff, 0x00020000);
+  f32x4 px[2][2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int j = min(tid + 256 * u, GC_PAIRS - 1);
+    const int py = j / (GC_PC / 2), pc = 2 * (j - py * (GC_PC / 2));
+    const int yy = Y0 - 2 + py, xx = X0 - 2 + pc;
+    if (IN) {
+      const int o = (yy * W + xx) * 16;
+      px[u][0] = gc_bload(irs, o);
+      px[u][1] = gc_bload(irs, o + 16);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const bool ok = (unsigned)yy < (unsigned)H && (unsigned)(xx + e) < (unsigned)W;
+        const f32x4 v =
+            gc_bload(irs, (min(max(yy, 0), H - 1) * W + min(max(xx + e, 0), W - 1)) * 16);
+        px[u][e] = ok ? v : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  const float bias = bc[(long long)b * TAP_CO + co];
+  g6_u32x4 wv[5][3];
+  {
+    const unsigned short* wb = wp + (long long)b * 3 * TAP_CO * GC_K + (long long)co * GC_K + 8 * hl;
+#pragma unroll
+    for (int dy = 0; dy < 5; ++dy)
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        wv[dy][pl] = *reinterpret_cast<const g6_u32x4*>(wb + (long long)pl * TAP_CO * GC_K + dy * 16);
+  }
+  // P item n of row pair rp: tile rows (2 rp, 2 rp + 1), column cx, tap k,
+  // channel quad; m = n within the row pair = (cx * 9 + k) * 8 + quad
+  const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(P + (long long)b * h * w * TAP_N + cg * CB_CG), (short)0, 0x7fffffff,
+      0x00020000);
+  auto pitem = [&](int m, int rp, int& oa, int& ob) {  // byte offsets of the two rows
+    if (IN) {
+      oa = (((q0 - 1 + 2 * rp) * w + qx0 - 1) * TAP_N + (m >> 3) * TAP_CO + (m & 7) * 4) * 4;
+      ob = oa + w * TAP_N * 4;
+    } else {
+      const int kk = m >> 3, k = kk % 9, cx = kk / 9;
+      const int ix = min(max(qx0 - 1 + cx, 0), w - 1);
+      const int ia = min(max(q0 - 1 + 2 * rp, 0), h - 1), ib = min(max(q0 + 2 * rp, 0), h - 1);
+      const int c = ix * TAP_N + k * TAP_CO + (m & 7) * 4;
+      oa = (ia * w * TAP_N + c) * 4;
+      ob = (ib * w * TAP_N + c) * 4;
+    }
+  };
+  f32x4 pA[GC_UA][2];
+#pragma unroll
+  for (int u = 0; u < GC_UA; ++u) {
+    const int n = min(tid + 256 * u, GC_NA - 1);  // the last item repeats: the same data
+    const int rp = n >= GC_NA / 2;
+    int oa, ob;
+    pitem(n - rp * (GC_NA / 2), rp, oa, ob);
+    pA[u][0] = gc_bload(prs, oa);
+    pA[u][1] = gc_bload(prs, ob);
+  }
+  // ---- the patch's bf16 planes over P-tile rows 4-5 --------------------------
+  unsigned* pl = reinterpret_cast<unsigned*>(spB);
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int j = tid + 256 * u;
+    if (u == 1 && j >= GC_PAIRS) break;
+    const int py = j / (GC_PC / 2);
+    const int d = py * GC_S + 3 * (j - py * (GC_PC / 2));
+    unsigned hh[3], mm[3], ll[3];
+    pf_split3_pair(px[u][0].x, px[u][0].y, hh[0], mm[0], ll[0]);
+    pf_split3_pair(px[u][0].z, px[u][1].x, hh[1], mm[1], ll[1]);
+    pf_split3_pair(px[u][1].y, px[u][1].z, hh[2], mm[2], ll[2]);
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {
+      pl[d + e] = hh[e];
+      pl[GC_PLANE + d + e] = mm[e];
+      pl[2 * GC_PLANE + d + e] = ll[e];
+    }
+  }
+  // dword 54 of a row is read (times a zero weight: k = 15) by the last tile
+  if (tid < 3 * GC_PR) pl[tid * GC_S + 3 * GC_PC / 2] = 0u;
+  // P-tile rows 4-5 into registers (their LDS is the planes' until after G)
+  f32x4 pB[GC_UB][2];
+#pragma unroll
+  for (int u = 0; u < GC_UB; ++u) {
+    const int n = min(tid + 256 * u, GC_NB - 1);
+    int oa, ob;
+    pitem(n, 2, oa, ob);
+    pB[u][0] = gc_bload(prs, oa);
+    pB[u][1] = gc_bload(prs, ob);
+  }
+  gc_wait_lgkm0();
+  gc_barrier();
+  GC_TS(2);
+  // ---- G part: tile t = output columns (c, c + 4), c = 8 wave + t; A row m =
+  // pixel (row (m & 3) + 4 (m >> 3), column c + 4 ((m >> 2) & 1)), k half hl:
+  // the 8 bf16 from element 3 (column) + 8 hl of patch row (row + dy), i.e.
+  // dword d0 = 12 wave + 6 colsel + 4 hl + (3 t) / 2 (+ a 16-bit shift for odd t)
+  const int arow = (ln & 3) + 4 * (ln >> 3), colsel = (ln >> 2) & 1;
+  const int pbase = arow * GC_S + 6 * colsel + 4 * hl + 12 * wave;  // even
+  f32x16 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+#pragma unroll
+  for (int dy = 0; dy < 5; ++dy) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      g6_u32x4 f[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        const int d = pbase + p * GC_PLANE + dy * GC_S;  // even
+        const uint2* q2 = reinterpret_cast<const uint2*>(pl) + (d >> 1);
+        if (t == 0) {  // dwords d .. d+3
+          const uint2 a = q2[0], c = q2[1];
+          f[p] = g6_u32x4{a.x, a.y, c.x, c.y};
+        } else if (t == 1) {  // elements from d+1 (odd): dwords d+1 .. d+5, shifted
+          const unsigned s0 = pl[d + 1];
+          const uint2 a = q2[1], c = q2[2];
+          f[p] = g6_u32x4{__builtin_amdgcn_alignbit(a.x, s0, 16), __builtin_amdgcn_alignbit(a.y, a.x, 16),
+                          __builtin_amdgcn_alignbit(c.x, a.y, 16), __builtin_amdgcn_alignbit(c.y, c.x, 16)};
+        } else if (t == 2) {  // dwords d+3 .. d+6
+          const uint2 a = q2[2];
+          f[p] = g6_u32x4{pl[d + 3], a.x, a.y, pl[d + 6]};
+        } else {  // elements from d+4 (odd): dwords d+4 .. d+8, shifted
+          const uint2 a = q2[2], c = q2[3];
+          const unsigned s4 = pl[d + 8];
+          f[p] = g6_u32x4{__builtin_amdgcn_alignbit(a.y, a.x, 16), __builtin_amdgcn_alignbit(c.x, a.y, 16),
+                          __builtin_amdgcn_alignbit(c.y, c.x, 16), __builtin_amdgcn_alignbit(s4, c.y, 16)};
+        }
+      }
+      // the k80 kernel's six products in its order, operands swapped
+      f32x16 c = acc[t];
+      if (ABL & 1) { acc[t][0] += __builtin_bit_cast(float, f[0][0] ^ f[1][1] ^ f[2][2] ^ wv[dy][0][0]); continue; }
+      c = g6_mfma(f[0], wv[dy][0], c);
+      c = g6_mfma(f[1], wv[dy][0], c);
+      c = g6_mfma(f[0], wv[dy][1], c);
+      c = g6_mfma(f[2], wv[dy][0], c);
+      c = g6_mfma(f[0], wv[dy][2], c);
+      c = g6_mfma(f[1], wv[dy][1], c);
+      acc[t] = c;
+    }
+  }
+  // ---- P tile -> LDS: [row pair][column][tap][channel][2 rows] ----------------
+  GC_TS(3);
+  auto pstore = [&](float* base, int n, const f32x4& a, const f32x4& c) {
+    f32x4* d = reinterpret_cast<f32x4*>(base + 8 * n);
+    d[0] = f32x4{a.x, c.x, a.y, c.y};
+    d[1] = f32x4{a.z, c.z, a.w, c.w};
+  };
+#pragma unroll
+  for (int u = 0; u < GC_UA; ++u) pstore(spA, min(tid + 256 * u, GC_NA - 1), pA[u][0], pA[u][1]);
+  gc_wait_lgkm0();  // every plane read of this wave has completed ...
+  gc_barrier();     // ... in every wave: rows 4-5 may overwrite the planes
+#pragma unroll
+  for (int u = 0; u < GC_UB; ++u) pstore(spB, min(tid + 256 * u, GC_NB - 1), pB[u][0], pB[u][1]);
+  // ---- bias; border-ring pixels take the ring value -------------------------
+  if (IN) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] += bias;
+  } else {
+    const int nring = 2 * W + 2 * (H - 2);
+    const float* rb = ring + (long long)b * nring * TAP_CO + co;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int X = X0 + 8 * wave + t + 4 * hl;
+      const bool edge_x = X == 0 || X == W - 1;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int Y = Y0 + r;
+        acc[t][r] = (edge_x || Y == 0 || Y == H - 1) && X < W
+                        ? rb[(long long)pf_ring_index(Y, X, H, W) * TAP_CO]
+                        : acc[t][r] + bias;
+      }
+    }
+  }
+  gc_wait_lgkm0();
+  gc_barrier();
+  GC_TS(4);
+  // ---- the upsampled part ----------------------------------------------------
+  const float ztop = q0 == 0 ? 0.f : 1.f, zbot = q0 + TQ == h ? 0.f : 1.f;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    if (ABL & 2) { acc[t][0] += spA[tid * 2 + t]; continue; }
+    const int X = X0 + 8 * wave + t + 4 * hl;  // X % 4 == t
+    // x interpolation: R[rp][ky] = sum_kx wa P[rows][ca][k] + wb P[rows][cb][k]
+    // for the tile-row pair rp (k = 3 ky + kx)
+    int oa[3], ob[3];
+    float wa[3], wb[3];
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      int lo;
+      up4_w(t + kx - 1, lo, wa[kx], wb[kx]);
+      int ca, cb;
+      if (IN) {
+        ca = 1 + 2 * wave + hl + lo;  // tile column of X >> 2, plus lo
+        cb = ca + 1;
+      } else {
+        const int u = X + kx - 1;
+        if (u < 0 || u >= W) wa[kx] = wb[kx] = 0.f;
+        const int qx = X >> 2;
+        ca = min(max(min(qx + lo, w - 1), 0) - (qx0 - 1), CB_CX - 1);
+        cb = min(max(min(qx + lo + 1, w - 1), 0) - (qx0 - 1), CB_CX - 1);
+      }
+      oa[kx] = ca * GC_CELL + kx * 2 * CB_CG + 2 * ln;
+      ob[kx] = cb * GC_CELL + kx * 2 * CB_CG + 2 * ln;
+    }
+    gc_f2 R[3][3];
+#pragma unroll
+    for (int rp = 0; rp < 3; ++rp) {
+      const float* base = rp < 2 ? spA + rp * GC_RP : spB;
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky) {
+        gc_f2 s = {0.f, 0.f};
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          const gc_f2 pa = *reinterpret_cast<const gc_f2*>(base + oa[kx] + ky * 6 * CB_CG);
+          const gc_f2 pb = *reinterpret_cast<const gc_f2*>(base + ob[kx] + ky * 6 * CB_CG);
+          s = gc_fma2(gc_f2{wa[kx], wa[kx]}, pa, s);
+          s = gc_fma2(gc_f2{wb[kx], wb[kx]}, pb, s);
+        }
+        R[rp][ky] = s;
+      }
+    }
+    // y interpolation of output rows (4 i + 2 rp2, + 1) from R rows i + j, j in -1..1
+#pragma unroll
+    for (int i = 0; i < TQ; ++i) {
+#pragma unroll
+      for (int rq = 0; rq < 2; ++rq) {
+        gc_f2 o = {acc[t][4 * i + 2 * rq], acc[t][4 * i + 2 * rq + 1]};
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+#pragma unroll
+          for (int j = -1; j <= 1; ++j) {
+            float cA = gc_cy(2 * rq, ky, j), cB = gc_cy(2 * rq + 1, ky, j);
+            if (cA == 0.f && cB == 0.f) continue;
+            if (!IN && i == 0 && rq == 0 && ky == 0) cA *= ztop;  // conv2's zero padding
+            if (!IN && i == TQ - 1 && rq == 1 && ky == 2) cB *= zbot;
+            const int ry = i + 1 + j;  // tile row
+            const float rv = R[ry >> 1][ky][ry & 1];
+            if (ABL & 16) {  // packed, op_sel broadcast: run-to-run differences
+              o = gc_fma2(gc_f2{cA, cB}, gc_f2{rv, rv}, o);
+            } else if (ABL & 32) {
+              gc_f2 r2 = {rv, rv};
+              asm volatile("" : "+v"(r2));
+              o = gc_fma2(gc_f2{cA, cB}, r2, o);
+            } else {
+              if (cA != 0.f) o.x = __builtin_fmaf(cA, rv, o.x);
+              if (cB != 0.f) o.y = __builtin_fmaf(cB, rv, o.y);
+            }
+          }
+        }
+        acc[t][4 * i + 2 * rq] = o.x;
+        acc[t][4 * i + 2 * rq + 1] = o.y;
+      }
+    }
+  }
+  GC_TS(5);
+  // ---- the instance-norm statistics (this lane's channel, its 4 columns) -----
+  double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int X = X0 + 8 * wave + t + 4 * hl;
+    if (!IN && X >= W) continue;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const double dv = acc[t][r];
+      s1 += dv;
+      s2 = fma(dv, dv, s2);
+    }
+  }
+  s1 += __shfl_xor(s1, 32, 64);  // lanes l and l ^ 32 hold the same channel
+  s2 += __shfl_xor(s2, 32, 64);
+  // ---- y through LDS: [row][column][channel], then 16-B stores of 4 channels
+  // (a lane's 16 rows x 1 channel would be 64 dword stores: store-issue bound)
+  gc_barrier();  // every wave is done reading the P tile
+  {
+    float* so = spA + (8 * wave + 4 * hl) * CB_CG + ln;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) so[(r * 32 + t) * CB_CG] = acc[t][r];
+  }
+  double* red = reinterpret_cast<double*>(spA + 16 * 32 * CB_CG);  // [wave][32 channels][2]
+  if (part && hl == 0) {
+    red[(wave * CB_CG + ln) * 2] = s1;
+    red[(wave * CB_CG + ln) * 2 + 1] = s2;
+  }
+  gc_wait_lgkm0();
+  gc_barrier();
+  {
+    const int col = tid >> 3, quad = tid & 7, X = X0 + col;
+    const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
+        y + ((long long)b * H + Y0) * W * ycs, (short)0, 0x7fffffff, 0x00020000);
+    const int yrow = W * ycs * 4, xo = (X * ycs + cg * CB_CG + quad * 4) * 4;
+    const f32x4* si = reinterpret_cast<const f32x4*>(spA) + tid;
+    if (IN || X < W) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        if (ABL & 4) { if (si[r * 256].x == 1.2345f) y[tid] = 0.f; continue; }
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(g6_u32x4, si[r * 256]), yrs, xo,
+                                               r * yrow, 0);
+      }
+    }
+  }
+  GC_TS(6);
+  // ---- statistics: the block's 32 columns of each channel, fixed order ------
+  if (part && tid < 2 * CB_CG) {
+    const int c = tid >> 1, which = tid & 1;
+    double a = 0.0;
+    for (int x = 0; x < 4; ++x) a += red[(x * CB_CG + c) * 2 + which];
+    const long long chunk = (long long)qb * nxb + xb;
+    const long long nchunk = (long long)nxb * nqb;
+    part[(((long long)b * nchunk + chunk) * TAP_CO + cg * CB_CG + c) * 2 + which] = a;
+  }
+}
+
+template <int ABL>
 __global__ __launch_bounds__(256, 2) void up4tap_gcombine_kernel(
     const float* __restrict__ P, int h, int w, const float* __restrict__ img4,
     const unsigned short* __restrict__ wp, const float* __restrict__ bc,
     const float* __restrict__ ring, float* __restrict__ y, int ycs, double* __restrict__ part) {
-  __shared__ __attribute__((aligned(16))) float sp[CB_SEGP * CB_CG];
-  __shared__ __attribute__((aligned(16))) float spat[GC_PDMA * 64 * 4];  // [row][38 slots][4]
-  const int H = 4 * h, W = 4 * w;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hl = lane >> 5, ln = lane & 31;
+  // P-tile rows 0-3 (spA), the patch planes then rows 4-5 (spB); at the end the
+  // y tile (64 KB) and the statistics
+  __shared__ __attribute__((aligned(16))) float smem[(GC_NA + GC_NB) * 8];
+  float* spA = smem;
+  float* spB = smem + GC_NA * 8;
   const int nxb = (w + CB_QX - 1) / CB_QX, nqb = h / TQ, ncg = TAP_CO / CB_CG;
   // XCD-aware order: blocks are dealt round-robin over the 8 XCDs, so block i
   // takes tile (i % 8) * (n / 8) + i / 8 -- neighbouring tiles, which share P
@@ -261,192 +658,15 @@ __global__ __launch_bounds__(256, 2) void up4tap_gcombine_kernel(
   const int xb = id % nxb;
   id /= nxb;
   const int qb = id % nqb, b = id / nqb;
-  const int q0 = qb * TQ, qx0 = xb * CB_QX, Y0 = 4 * q0, X0 = 4 * qx0;
-  // ---- loads, in this order: the B operands (this channel group's weight
-  // planes) into registers, then the image patch and the P tile by DMA.  The
-  // MFMA phase waits for all but the P tile's 17 instructions --------------
-  const int co = cg * CB_CG + ln;
-  const float bias = bc[(long long)b * TAP_CO + co];
-  g6_u32x4 wv[5][3];
-  {
-    const unsigned short* wb = wp + (long long)b * 3 * TAP_CO * GC_K + (long long)co * GC_K + 8 * hl;
-#pragma unroll
-    for (int dy = 0; dy < 5; ++dy)
-#pragma unroll
-      for (int pl = 0; pl < 3; ++pl)
-        wv[dy][pl] = *reinterpret_cast<const g6_u32x4*>(wb + (long long)pl * TAP_CO * GC_K + dy * 16);
-  }
-  __builtin_amdgcn_sched_barrier(0);
-  const float* ib = img4 + (long long)b * H * W * 4;
-#pragma unroll
-  for (int jj = 0; jj < GC_PDMA / 4; ++jj) {  // slot s -> patch pixel (s / 38, s % 38)
-    const int j = wave + 4 * jj, s = j * 64 + lane;
-    const int py = s / GC_PP, px = s - py * GC_PP;
-    const int yy = Y0 - 2 + py, xx = X0 - 2 + px;
-    const bool ok = py < GC_PR && px < GC_PC && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
-    const float* src = ok ? ib + ((long long)yy * W + xx) * 4 : gc_zero4;
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                     (__attribute__((address_space(3))) void*)(spat + j * 64 * 4),
-                                     16, 0, 0);
-  }
-  const float* Pb = P + (long long)b * h * w * TAP_N + cg * CB_CG;
-#pragma unroll
-  for (int jj = 0; jj < GC_DMA; ++jj) {  // as up4tap_combine_kernel's phase 1
-    const int j = wave + 4 * jj;
-    int seg = j * 8 + (lane >> 3);
-    seg = min(seg, CB_SEG - 1);
-    const int k = seg % 9, cell = seg / 9;
-    const int cx = cell % CB_CX, ry = cell / CB_CX;
-    const int iy = min(max(q0 - 1 + ry, 0), h - 1), ix = min(max(qx0 - 1 + cx, 0), w - 1);
-    const float* src = Pb + ((long long)iy * w + ix) * TAP_N + k * TAP_CO + (lane & 7) * 4;
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                     (__attribute__((address_space(3))) void*)(sp + j * 8 * CB_CG),
-                                     16, 0, 0);
-  }
-  __builtin_amdgcn_sched_barrier(0);
-  gc_wait_vmcnt<GC_DMA>();        // weights + this wave's patch DMA have landed
-  asm volatile("" ::: "memory");  // no LDS access moves across the barrier
-  __builtin_amdgcn_s_barrier();   // ... and every wave's (no fence: it would drain the P tile)
-  asm volatile("" ::: "memory");
-  // ---- G part: wave = 4 column pairs p = 4 wave + t; A row m = pixel (row
-  // (m & 3) + 4 (m >> 3), column 2p + ((m >> 2) & 1)), k half hl: the 8 taps
-  // k = 8 hl .. 8 hl + 7 of row dy are channels of the three pixels from
-  // column 2p + (m's column) + 2 hl on -- (c0 c1 c2 | c0 c1 c2 | c0 c1) for
-  // hl = 0, (c2 | c0 c1 c2 | c0 c1 c2 | 0) for hl = 1 (k = 15: zero weight)
-  const int arow = (ln & 3) + 4 * (ln >> 3), acol = (ln >> 2) & 1;
-  f32x16 acc[4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
-#pragma unroll
-  for (int dy = 0; dy < 5; ++dy) {
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const f32x4* pr = reinterpret_cast<const f32x4*>(spat) + (arow + dy) * GC_PP +
-                        2 * (4 * wave + t) + acol + 2 * hl;
-      const f32x4 a = pr[0], bq = pr[1], cq = pr[2];
-      f32x4 p0, p1;
-      p0[0] = hl ? a.z : a.x;
-      p0[1] = hl ? bq.x : a.y;
-      p0[2] = hl ? bq.y : a.z;
-      p0[3] = hl ? bq.z : bq.x;
-      p1[0] = hl ? cq.x : bq.y;
-      p1[1] = hl ? cq.y : bq.z;
-      p1[2] = hl ? cq.z : cq.x;
-      p1[3] = hl ? 0.f : cq.y;
-      g6_u32x4 ph, pm, plo;
-      g6_split(p0, p1, ph, pm, plo);
-      // the k80 kernel's six products in its order, operands swapped
-      f32x16 c = acc[t];
-      c = g6_mfma(ph, wv[dy][0], c);
-      c = g6_mfma(pm, wv[dy][0], c);
-      c = g6_mfma(ph, wv[dy][1], c);
-      c = g6_mfma(plo, wv[dy][0], c);
-      c = g6_mfma(ph, wv[dy][2], c);
-      c = g6_mfma(pm, wv[dy][1], c);
-      acc[t] = c;
-    }
-  }
-  const int nring = 2 * W + 2 * (H - 2);
-  const float* rb = ring + (long long)b * nring * TAP_CO + co;
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int X = X0 + 2 * (4 * wave + t) + hl;
-    const bool edge_x = X == 0 || X == W - 1;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int Y = Y0 + r;
-      acc[t][r] = (edge_x || Y == 0 || Y == H - 1) && X < W
-                      ? rb[(long long)pf_ring_index(Y, X, H, W) * TAP_CO]
-                      : acc[t][r] + bias;
-    }
-  }
-  __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA has landed
-  __syncthreads();                 // ... and every other wave's
-  // ---- the upsampled part: per column, the sliding window of
-  // up4tap_combine_kernel on one channel ---------------------------------------
-  double s1 = 0.0, s2 = 0.0;
-  const long long yrow = (long long)W * ycs;
-  float* yb = y + (long long)b * H * W * ycs + co;
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int X = X0 + 2 * (4 * wave + t) + hl, qx = X >> 2, rx = X & 3;
-    const bool xok = X < W;
-    int cola[3], colb[3];
-    float wxa[3], wxb[3];
-#pragma unroll
-    for (int kx = 0; kx < 3; ++kx) {
-      int lo;
-      up4_w(rx + kx - 1, lo, wxa[kx], wxb[kx]);
-      const int u = X + kx - 1;
-      if (u < 0 || u >= W) wxa[kx] = wxb[kx] = 0.f;
-      cola[kx] = min(max(min(qx + lo, w - 1), 0) - (qx0 - 1), CB_CX - 1);
-      colb[kx] = min(max(min(qx + lo + 1, w - 1), 0) - (qx0 - 1), CB_CX - 1);
-    }
-    auto rowR = [&](int ry, float (&R)[3]) {
-#pragma unroll
-      for (int ky = 0; ky < 3; ++ky) {
-        float s = 0.f;
-#pragma unroll
-        for (int kx = 0; kx < 3; ++kx) {
-          const int k = ky * 3 + kx;
-          const float pa = sp[((ry * CB_CX + cola[kx]) * 9 + k) * CB_CG + ln];
-          const float pb = sp[((ry * CB_CX + colb[kx]) * 9 + k) * CB_CG + ln];
-          s += wxa[kx] * pa + wxb[kx] * pb;
-        }
-        R[ky] = s;
-      }
-    };
-    float Rm[3], R0[3], Rp[3];
-    rowR(0, Rm);
-    rowR(1, R0);
-#pragma unroll
-    for (int i = 0; i < TQ; ++i) {
-      rowR(i + 2, Rp);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int Y = Y0 + 4 * i + r;
-        float o = acc[t][4 * i + r];
-#pragma unroll
-        for (int ky = 0; ky < 3; ++ky) {
-          const int v = Y + ky - 1;
-          int lo;
-          float wa, wb;
-          up4_w(r + ky - 1, lo, wa, wb);
-          if (v < 0 || v >= H) wa = wb = 0.f;
-          if (lo < 0)
-            o += wa * Rm[ky] + wb * R0[ky];
-          else
-            o += wa * R0[ky] + wb * Rp[ky];
-        }
-        if (!xok) continue;
-        yb[Y * yrow + (long long)X * ycs] = o;
-        s1 += (double)o;
-        s2 += (double)o * (double)o;
-      }
-#pragma unroll
-      for (int ky = 0; ky < 3; ++ky) {
-        Rm[ky] = R0[ky];
-        R0[ky] = Rp[ky];
-      }
-    }
-  }
-  if (!part) return;
-  // ---- statistics: the block's 32 columns of each channel, fixed order ------
-  __syncthreads();  // LDS reuse
-  double* red = reinterpret_cast<double*>(sp);  // [wave][half][32 channels][2]
-  red[((wave * 2 + hl) * CB_CG + ln) * 2] = s1;
-  red[((wave * 2 + hl) * CB_CG + ln) * 2 + 1] = s2;
-  __syncthreads();
-  if (tid < 2 * CB_CG) {
-    const int c = tid >> 1, which = tid & 1;
-    double a = 0.0;
-    for (int x = 0; x < 8; ++x) a += red[(x * CB_CG + c) * 2 + which];
-    const long long chunk = (long long)qb * nxb + xb;
-    const long long nchunk = (long long)nxb * nqb;
-    part[(((long long)b * nchunk + chunk) * TAP_CO + cg * CB_CG + c) * 2 + which] = a;
-  }
+  const bool interior = qb > 0 && qb < nqb - 1 && xb > 0 && xb * CB_QX + CB_QX < w;
+#ifdef GC_ONLY
+  if (GC_ONLY)
+#else
+  if (interior)
+#endif
+    gc_block<true, ABL>(P, h, w, img4, wp, bc, ring, y, ycs, part, spA, spB, b, qb, xb, cg, nqb, nxb);
+  else
+    gc_block<false, ABL>(P, h, w, img4, wp, bc, ring, y, ycs, part, spA, spB, b, qb, xb, cg, nqb, nxb);
 }
 
 // ---- adjoint (keypoint-head training, config 5) ------------------------------
@@ -591,7 +811,11 @@ int pf_up4tap_gcombine(int n, int H, int W, const float* P, const float* img4,
   if (H % 16 || W % 16 || ycs % 4 || ycs < TAP_CO || n <= 0) return POSFEAT_E_INVALID;
   if (!P || !img4 || !wp || !bc || !ring || !y || (mean && !part)) return POSFEAT_E_INVALID;
   const int nchunk = (h / TQ) * ((w + CB_QX - 1) / CB_QX);
-  hipLaunchKernelGGL(up4tap_gcombine_kernel, dim3(n * nchunk * (TAP_CO / CB_CG)), dim3(256), 0, st,
+  static const int abl = getenv("POSFEAT_GC_ABL") ? atoi(getenv("POSFEAT_GC_ABL")) : 0;
+  auto kern = abl == 1 ? up4tap_gcombine_kernel<1> : abl == 2 ? up4tap_gcombine_kernel<2>
+            : abl == 4 ? up4tap_gcombine_kernel<4> : abl == 6 ? up4tap_gcombine_kernel<6>
+            : abl == 7 ? up4tap_gcombine_kernel<7> : abl == 8 ? up4tap_gcombine_kernel<8> : abl == 16 ? up4tap_gcombine_kernel<16> : abl == 32 ? up4tap_gcombine_kernel<32> : up4tap_gcombine_kernel<0>;
+  hipLaunchKernelGGL(kern, dim3(n * nchunk * (TAP_CO / CB_CG)), dim3(256), 0, st,
                      P, h, w, img4, wp, bc, ring, y, ycs, mean ? part : nullptr);
   PF_CHECK_LAUNCH();
   if (mean) PF_TRY(pf_in_finalize(part, n, nchunk, H * W, TAP_CO, mean, rstd, st));
@@ -616,4 +840,14 @@ int pf_up4tap_weights_t(const float* w2_packed, float* wt, hipStream_t st) {
                      w2_packed, wt);
   PF_CHECK_LAUNCH();
   return POSFEAT_OK;
+}
+
+extern "C" int posfeat_debug_gc_ts(unsigned long long* host, long long n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(gc_ts), n * 8) == hipSuccess ? 0 : -1;
+}
+extern "C" int posfeat_debug_gcombine(int n, int H, int W, const float* P, const float* img4,
+                                      const unsigned short* wp, const float* bc, const float* ring,
+                                      float* y, double* part, float* mean, float* rstd, void* st) {
+  return pf_up4tap_gcombine(n, H, W, P, img4, wp, bc, ring, y, 128, part, mean, rstd,
+                            (hipStream_t)st);
 }

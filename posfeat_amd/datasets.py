@@ -121,7 +121,8 @@ class ETH_LFB(_FileDataset):
 
 class SyntheticImages(Dataset):
     """Seeded synthetic images for plumbing and benchmarks:
-    ``num_images`` uint8 RandomState(1000+i) images of ``height x width``."""
+    ``num_images`` uint8 RandomState(1000+i) images of ``height x width``, or
+    of ``sizes[i % len(sizes)]`` (a list of [h, w]) for mixed-size streams."""
 
     def __init__(self, configs):
         super().__init__()
@@ -129,11 +130,13 @@ class SyntheticImages(Dataset):
         self.n = int(configs.get("num_images", 8))
         self.h = int(configs.get("height", 480))
         self.w = int(configs.get("width", 640))
+        self.sizes = [tuple(int(v) for v in s) for s in configs.get("sizes", None) or []]
         self.uint8_only = False
 
     def __getitem__(self, item):
         rs = np.random.RandomState(1000 + item)
-        raw = rs.randint(0, 256, (self.h, self.w, 3)).astype(np.uint8)
+        h, w = self.sizes[item % len(self.sizes)] if self.sizes else (self.h, self.w)
+        raw = rs.randint(0, 256, (h, w, 3)).astype(np.uint8)
         if self.uint8_only:
             return {"im1_ori": torch.from_numpy(crop16(raw)), "name1": "synthetic/%05d.ppm" % item,
                     "index": item}

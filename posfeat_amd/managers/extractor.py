@@ -15,7 +15,7 @@ MI355X-specific behaviour:
 * no CPU path: without a gfx950 GPU the constructor raises;
 * the default loop is a pipeline (``_extract_pipelined``): consecutive images
   of the same size are run as one engine batch (up to
-  ``POSFEAT_EXTRACT_GROUP``, default 8; instance norm and eval BatchNorm are
+  ``POSFEAT_EXTRACT_GROUP``, default 32; instance norm and eval BatchNorm are
   per image, so each image's maps are those of a batch-1 run up to fp32
   summation order), only the uint8 image crosses PCIe (pinned, normalised on
   the device by posfeat_normalize_rgb8, bit-identical to the host transform),
@@ -291,14 +291,14 @@ class Extractor:
         on the device), ``POSFEAT_EXTRACT_LOAD_BATCH`` items per worker
         transaction (default 8) collated as a list (sizes may differ), and
         ``POSFEAT_EXTRACT_WORKERS`` decode workers (default: the config's
-        ``workers``, at least 4).  Order is the sampler's, as the reference
-        loop's."""
+        ``workers``; an explicit 0 loads in this process).  Order is the
+        sampler's, as the reference loop's.  The dataset's ``uint8_only`` flag
+        is set for this loader only (``_extract_pipelined`` restores it)."""
         ds = self.extract_loader.dataset
         if hasattr(ds, "uint8_only"):
             ds.uint8_only = True
         cfg = self.config["data_config_extract"]
-        workers = int(os.environ.get("POSFEAT_EXTRACT_WORKERS",
-                                     max(4, int(cfg.get("workers", 0) or 0))))
+        workers = int(os.environ.get("POSFEAT_EXTRACT_WORKERS", cfg.get("workers", 4) or 0))
         lb = max(1, int(os.environ.get("POSFEAT_EXTRACT_LOAD_BATCH", "8")))
         sampler = (datasets.ShardSampler(len(ds), self.rank, self.world)
                    if self.multi_gpu else None)
@@ -312,8 +312,22 @@ class Extractor:
         size, a bucket runs as one engine batch when it holds
         ``POSFEAT_EXTRACT_GROUP`` images, default 32 -- the bench batch -- and
         the remaining buckets at the end): output files are per image, so the
-        processing order is free; name_list.txt keeps the loader order."""
+        processing order is free; name_list.txt keeps the loader order.
+        Datasets with many image sizes (HPatches crops every image to /16,
+        Aachen/ETH keep full resolution) would otherwise hold most of the
+        stream in partial buckets: once ``POSFEAT_EXTRACT_HOLD`` images
+        (default 4 groups) wait, the fullest bucket launches early."""
         group = max(1, int(os.environ.get("POSFEAT_EXTRACT_GROUP", "32")))
+        hold = max(group, int(os.environ.get("POSFEAT_EXTRACT_HOLD", str(4 * group))))
+        ds = self.extract_loader.dataset
+        u8_before = getattr(ds, "uint8_only", None)
+        try:
+            return self._extract_pipelined_run(group, hold)
+        finally:
+            if u8_before is not None:
+                ds.uint8_only = u8_before
+
+    def _extract_pipelined_run(self, group, hold):
         writer = ThreadPoolExecutor(1 if self.save_h5 else 4)
         futures, pending = [], deque()
         buckets = {}
@@ -340,6 +354,7 @@ class Extractor:
             while len(pending) > 1:   # keep one group in flight behind the host
                 self._finish_group(*pending.popleft(), writer, futures)
 
+        held = max_held = 0
         for batch in self._pipelined_loader():
             for it in batch:
                 u8 = it["im1_ori"]
@@ -349,9 +364,16 @@ class Extractor:
                 b.append(item)
                 names.append((int(it["index"]), it["name1"]))
                 n += 1
+                held += 1
+                max_held = max(max_held, held)
                 if len(b) >= group:
                     launch(b)
                     buckets[key] = []
+                    held -= len(b)
+                elif held >= hold:   # bounded host memory: the fullest bucket goes now
+                    key = max(buckets, key=lambda k: len(buckets[k]))
+                    held -= len(buckets[key])
+                    launch(buckets.pop(key))
         for key in list(buckets):
             if buckets[key]:
                 launch(buckets.pop(key))
@@ -364,9 +386,10 @@ class Extractor:
         dt = time.perf_counter() - t0
         self.stats = {"images": n, "seconds": dt, "images_per_s": n / dt if dt > 0 else 0.0,
                       "stage_ms_per_image": None, "pipeline": True, "group": group,
-                      "group_marks": marks}
-        self.logger.info("extracted %d images in %.2fs (%.1f images/s, pipelined)" % (
-            n, dt, self.stats["images_per_s"]))
+                      "group_marks": marks, "max_held": max_held, "hold": hold}
+        self.logger.info("extracted %d images in %.2fs (%.1f images/s, pipelined, %d groups, "
+                         "at most %d images held)" % (n, dt, self.stats["images_per_s"],
+                                                      len(marks), max_held))
         return n
 
     def _write_name_list(self, names):

@@ -55,11 +55,13 @@ class SyncBNGroup:
     summed in-stream by ncclAllReduce inside the backbone's forward/backward.
     ``lib`` is injectable for the host-side test of the bootstrap.
 
-    ``shape`` = this rank's (batch, h, w): the in-stream exchange sums 2 C
-    doubles per BatchNorm and normalises by P * world (P = this rank's pixel
-    count), which is torch.nn.SyncBatchNorm's arithmetic only when every rank
-    holds the same pixel count (torch all-gathers per-rank counts).  The shapes
-    are therefore all-gathered once here and unequal ones are refused.
+    Per BatchNorm the in-stream exchange sums 2 C + 1 doubles -- this rank's
+    Σy and Σy² (backward: Σg, Σg·x̂) and its pixel count -- so every rank
+    normalises by the group's total count, as torch.nn.SyncBatchNorm does with
+    its all-gathered per-rank counts.  Ranks may hold different batches (the
+    reference Trainer's loader has no drop_last and my_collate drops None
+    samples, managers/trainer.py:132-134).  ``shape`` is accepted for the
+    callers that pass it and no longer checked.
 
     Ordering with torch's own communicator: the SyncBN communicator's
     all-reduces are enqueued on the trainer's stream inside the backbone
@@ -75,12 +77,7 @@ class SyncBNGroup:
         self._lib = lib or _lib.lib()
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
-        if shape is not None:
-            shapes = [None] * self.world
-            dist.all_gather_object(shapes, tuple(int(v) for v in shape), group=group)
-            if len(set(shapes)) != 1:
-                raise ValueError("SyncBatchNorm needs the same (batch, h, w) on every rank: "
-                                 "got %s" % shapes)
+        self.shape = None if shape is None else tuple(int(v) for v in shape)
         id_host = torch.zeros(128, dtype=torch.uint8)
         if self.rank == 0:
             buf = (ctypes.c_ubyte * 128)()

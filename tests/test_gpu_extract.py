@@ -216,3 +216,29 @@ def test_extract_pipelined_vs_serial(gpu, tmp_path, model, group):
                lambda n: cfg["detector_config"], model, group=3)
     check_tree(os.path.join(roots["0"], "desc"), cfg["postfix"], ims,
                lambda n: cfg["detector_config"], model, group=1)
+
+
+def test_extract_many_shapes_bounded_hold(gpu, tmp_path):
+    """Many image sizes (HPatches crops each image to /16, Aachen/ETH keep full
+    resolution): the shape buckets never fill, and without a bound the pipelined
+    loop held the whole stream until the end.  With
+    POSFEAT_EXTRACT_HOLD the fullest bucket launches early: at most HOLD images
+    wait, every image is written once, in loader order in name_list.txt, with
+    its own size's keypoint count."""
+    cfg = yaml.safe_load(open(os.path.join(ROOT, "configs", "extract_synthetic.yaml")))
+    sizes = [[64, 96], [80, 96], [64, 112], [96, 96], [80, 112], [64, 128]]
+    cfg["data_config_extract"].update(num_images=18, sizes=sizes, workers=2)
+    cfg["detector_config"]["num_pts"] = 200
+    cfg["output_root"] = "syn_shapes"
+    root = run_extract(cfg, tmp_path, env=dict(POSFEAT_EXTRACT_GROUP="4",
+                                               POSFEAT_EXTRACT_HOLD="5"))
+    names = open(os.path.join(root, "image", "name_list.txt")).read().splitlines()
+    assert names == ["%d synthetic/%05d.ppm" % (i, i) for i in range(18)]
+    files = sorted(os.listdir(os.path.join(root, "desc", "synthetic")))
+    assert len(files) == 18
+    for f in files:
+        z = np.load(os.path.join(root, "desc", "synthetic", f))
+        assert z["keypoints"].shape == (200, 2) and z["descriptors"].shape == (200, 128)
+    log = open(os.path.join(root, "logging_file.txt")).read()
+    held = [int(l.split("at most ")[1].split()[0]) for l in log.splitlines() if "at most" in l]
+    assert held and held[-1] <= 5, held

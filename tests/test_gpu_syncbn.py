@@ -100,3 +100,61 @@ def test_syncbn_two_ranks_equal_full_batch(gpu):
     for g in groups:
         lib().posfeat_group_destroy(g)
     lib().posfeat_local_group_destroy(L)
+
+
+def test_syncbn_unequal_batches_equal_full_batch(gpu):
+    """Ranks with DIFFERENT batches (2 + 1 images: the reference Trainer's
+    loader has no drop_last and my_collate drops None samples,
+    managers/trainer.py:132-134): the pixel count is all-reduced with the sums
+    (bbtrain.hip bn_sums_kernel), so both ranks normalise with the 3-image
+    batch statistics, as torch.nn.SyncBatchNorm does.  Maps 1e-4 of scale,
+    running statistics rtol 1e-5, and the summed rank gradients against the
+    full-batch gradient (two fp32 summation orders of the BatchNorm-heavy
+    backward: relative L2 2e-3 overall, 3e-2 of each tensor's max)."""
+    from test_bb_train import _inputs
+    from posfeat_amd import weights
+    from posfeat_amd._lib import check, lib
+    from posfeat_amd.training import BackboneTrainer
+    d, im1, im2, R1, R2 = _inputs()
+    _, _, H, W = im1.shape
+    ims = [torch.cat([im1, im2[:1]]).to(gpu), torch.cat([im2, im1[:1]]).to(gpu)]
+    dms = [torch.cat([R1, R2[:1]]).permute(0, 2, 3, 1).contiguous().to(gpu),
+           torch.cat([R2, R1[:1]]).permute(0, 2, 3, 1).contiguous().to(gpu)]
+    bb, _ = weights.seeded_state_dicts(0)
+    full = BackboneTrainer(bb, 3, H, W, device=gpu)
+    lm_full = _step(full, ims, dms)
+    torch.cuda.synchronize()
+
+    L = ctypes.c_void_p()
+    check(lib().posfeat_local_group_create(2, 4096, ctypes.byref(L)))
+    groups = []
+    for r in range(2):
+        g = ctypes.c_void_p()
+        check(lib().posfeat_group_create_local(L, r, ctypes.byref(g)))
+        groups.append(g)
+    split = [(0, 2), (2, 3)]
+    ranks = [BackboneTrainer(bb, b1 - b0, H, W, device=gpu) for b0, b1 in split]
+    for t, g in zip(ranks, groups):
+        t.set_group(g)
+    lms = _run_ranks(ranks, [[x[b0:b1] for x in ims] for b0, b1 in split],
+                     [[x[b0:b1] for x in dms] for b0, b1 in split])
+    for r, (b0, b1) in enumerate(split):
+        for s in range(2):
+            scale = max(1.0, float(lm_full[s].abs().max()))
+            e = float((lms[r][s] - lm_full[s][b0:b1]).abs().max())
+            assert e <= 1e-4 * scale, "rank %d image %d map err %g" % (r, s, e)
+        np.testing.assert_allclose(ranks[r].stats.cpu().numpy(), full.stats.cpu().numpy(),
+                                   rtol=1e-5, atol=1e-6)
+    gsum = weights.unpack_bbtrain((ranks[0].grad + ranks[1].grad).cpu().numpy(), full.table)
+    gref = weights.unpack_bbtrain(full.grad.cpu().numpy(), full.table)
+    num = den = 0.0
+    for k, v in gref.items():
+        e = float(np.abs(gsum[k] - v).max())
+        assert e <= 3e-2 * max(float(np.abs(v).max()), 1e-12), "%s: err %g of max %g" % (
+            k, e, float(np.abs(v).max()))
+        num += float(((gsum[k] - v) ** 2).sum())
+        den += float((v ** 2).sum())
+    assert num ** 0.5 <= 2e-3 * den ** 0.5
+    for g in groups:
+        lib().posfeat_group_destroy(g)
+    lib().posfeat_local_group_destroy(L)
