@@ -61,6 +61,7 @@ GEMM_LABEL_KERNELS = {
 FP32_MFMA_LABELS = ()
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md, dense FP32 matrix (spec)
 PEAK_BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md, dense BF16 matrix (no sparsity)
+PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md, HBM3E (~8 TB/s)
 
 
 def conv_arithmetic():
@@ -366,7 +367,7 @@ def main():
     # ---- roofline of the dominant kernel, HIP events on the engine's stream
     # around each launch, averaged over a few extra steps
     engine.set_timing(args.batch, H, W, True)
-    per_label = {}
+    per_label, other_ms = {}, {}
     c2_ms, conv_ms, conv_fl, all_ms, side_ms = [], [], [], [], []
     for _ in range(args.timing_steps):
         step(engine, ops, ws, imgs)
@@ -374,6 +375,8 @@ def main():
         for lab, ms, fl in ev:
             if lab.startswith("conv:") and fl > 0:
                 per_label.setdefault(lab, []).append((ms, fl))
+            elif not lab.startswith(("conv:", "side:")):
+                other_ms.setdefault(lab, []).append(ms)
         main = [e for e in ev if not e[0].startswith("side:")]
         c2_ms.append(sum(ms for lab, ms, _ in main if lab.startswith(("conv:head.conv2",
                                                                         "head.conv2"))))
@@ -408,6 +411,28 @@ def main():
                 traffic = t.get("bytes_per_launch")
         except Exception:
             traffic = None
+
+    # the longest non-GEMM launch (head.conv2's tap combine with the
+    # folded image conv, up4tap_gcombine_kernel) against the HBM roofline:
+    # algorithmic bytes = the tap maps P read once (B h w 1152 fp32) + y written
+    # once (B H W 128 fp32) + the NHWC4 image read once
+    hb = max(other_ms, key=lambda k: np.mean(other_ms[k]))
+    hb_ms = float(np.mean(other_ms[hb]))
+    hb_rec = {"label": hb, "avg_launch_ms": round(hb_ms, 4), "bound": "hbm", "unit": "GB/s",
+              "peak": PEAK_HBM_GBS}
+    if hb == "head.conv2.gcombine":
+        hbytes = args.batch * ((H // 4) * (W // 4) * 1152 * 4 + H * W * 128 * 4 + H * W * 16)
+        gfl = 2.0 * args.batch * H * W * 128 * 80   # the folded 5x5 image conv, K = 80
+        hb_rec.update(kernel="up4tap_gcombine_kernel (head.conv2: tap-summed x4 bilinear "
+                             "combine of the low-res tap maps + folded 5x5 image conv on "
+                             "bf16x6 MFMA + IN statistics)",
+                      algorithmic_bytes=hbytes,
+                      achieved=round(hbytes / (hb_ms * 1e-3) / 1e9, 1),
+                      frac=round(hbytes / (hb_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
+                      mfma_part={"flop_per_launch": gfl,
+                                 "achieved_tflops": round(gfl / (hb_ms * 1e-3) / 1e12, 2),
+                                 "frac_of_bf16x6_ceiling":
+                                     round(gfl / (hb_ms * 1e-3) / 1e12 / arith["method_peak"], 4)})
 
     if rank == 0:
         rec = {
@@ -446,6 +471,7 @@ def main():
                                  "mix it runs (bf16x6: dense BF16 MFMA 2500 TF / 6 products); "
                                  "frac_of_fp32_mfma_peak is the same rate against the 157.3 TF "
                                  "fp32-input MFMA peak"},
+            "roofline_hbm": hb_rec,
             "head_conv2": {"ms_per_step": round(c2, 3),
                            "note": "main-stream part (low-res tap GEMM + combine); the G part "
                                    "(IN(convimg) channels) runs on the side stream",

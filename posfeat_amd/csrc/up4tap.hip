@@ -291,8 +291,6 @@ __host__ __device__ constexpr float gc_cy(int r, int ky, int j) {
   return j == lo ? wa : j == lo + 1 ? 1.f - wa : 0.f;
 }
 
-__device__ unsigned long long gc_ts[80000 * 8];
-#define GC_TS(i) do { if ((ABL & 8) && tid == 0) { const long long bi = blockIdx.x; if (bi < 80000) gc_ts[bi * 8 + (i)] = (i) == 0 ? __builtin_amdgcn_s_memrealtime() : __builtin_amdgcn_s_memtime(); if ((i) == 0) gc_ts[bi * 8 + 7] = ((unsigned long long)__builtin_amdgcn_s_getreg(0xF804) << 16) | __builtin_amdgcn_s_getreg(0x7814); } } while (0)
 typedef float gc_f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ gc_f2 gc_fma2(gc_f2 a, gc_f2 b, gc_f2 c) {
   return __builtin_elementwise_fma(a, b, c);
@@ -301,26 +299,25 @@ __device__ __forceinline__ f32x4 gc_bload(__amdgpu_buffer_rsrc_t r, int off) {
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
 }
 
-template <bool IN, int ABL>
-__device__ __forceinline__ void gc_block(const float* __restrict__ P, int h, int w,
-                                         const float* __restrict__ img4,
-                                         const unsigned short* __restrict__ wp,
-                                         const float* __restrict__ bc,
-                                         const float* __restrict__ ring, float* __restrict__ y,
-                                         int ycs, double* __restrict__ part, float* spA,
-                                         float* spB, int b, int qb, int xb, int cg, int nqb,
-                                         int nxb) {
-  const int H = 4 * h, W = 4 * w;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, hl = lane >> 5, ln = lane & 31;
-  const int q0 = qb * TQ, qx0 = xb * CB_QX, Y0 = 4 * q0, X0 = 4 * qx0;
-  const int co = cg * CB_CG + ln;
-  GC_TS(0);
-  GC_TS(1);
-  // ---- loads: the B operands (this channel group's weight planes), the patch
-  // pixel pairs and P-tile rows 0-3 into registers ------------------------------
+// the per-launch arguments of the gcombine kernel
+struct GcArgs {
+  const float* P;
+  const float* img4;
+  const unsigned short* wp;
+  const float* bc;
+  const float* ring;
+  float* y;
+  double* part;
+  int h, w, ycs, nqb, nxb;
+};
+
+// patch pixel pairs of tile (q0, qx0) of image b into registers
+template <bool IN>
+__device__ __forceinline__ void gc_issue_patch(const GcArgs& A, int b, int q0, int qx0, int tid,
+                                               f32x4 (&px)[2][2]) {
+  const int H = 4 * A.h, W = 4 * A.w, Y0 = 4 * q0, X0 = 4 * qx0;
   const __amdgpu_buffer_rsrc_t irs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(img4 + (long long)b * H * W * 4), (short)0, 0x7fffffff, 0x00020000);
-  f32x4 px[2][2];
+      const_cast<float*>(A.img4 + (long long)b * H * W * 4), (short)0, 0x7fffffff, 0x00020000);
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int j = min(tid + 256 * u, GC_PAIRS - 1);
@@ -340,23 +337,26 @@ __device__ __forceinline__ void gc_block(const float* __restrict__ P, int h, int
       }
     }
   }
-  __builtin_amdgcn_sched_barrier(0);
-  const float bias = bc[(long long)b * TAP_CO + co];
-  g6_u32x4 wv[5][3];
-  {
-    const unsigned short* wb = wp + (long long)b * 3 * TAP_CO * GC_K + (long long)co * GC_K + 8 * hl;
-#pragma unroll
-    for (int dy = 0; dy < 5; ++dy)
-#pragma unroll
-      for (int pl = 0; pl < 3; ++pl)
-        wv[dy][pl] = *reinterpret_cast<const g6_u32x4*>(wb + (long long)pl * TAP_CO * GC_K + dy * 16);
-  }
-  // P item n of row pair rp: tile rows (2 rp, 2 rp + 1), column cx, tap k,
-  // channel quad; m = n within the row pair = (cx * 9 + k) * 8 + quad
+}
+
+// P items of tile (q0, qx0), image b, channel group cg into registers: item n
+// of row pair rp = tile rows (2 rp, 2 rp + 1), column cx, tap k, channel quad,
+// m = n within the row pair = (cx * 9 + k) * 8 + quad; rows 0-3 (RP = 0: the
+// two pairs, GC_UA items per thread) or rows 4-5 (RP = 2, GC_UB)
+template <bool IN, int RP, int U>
+__device__ __forceinline__ void gc_issue_p(const GcArgs& A, int b, int q0, int qx0, int cg,
+                                           int tid, f32x4 (&pr)[U][2]) {
+  const int h = A.h, w = A.w;
   const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(P + (long long)b * h * w * TAP_N + cg * CB_CG), (short)0, 0x7fffffff,
+      const_cast<float*>(A.P + (long long)b * h * w * TAP_N + cg * CB_CG), (short)0, 0x7fffffff,
       0x00020000);
-  auto pitem = [&](int m, int rp, int& oa, int& ob) {  // byte offsets of the two rows
+  constexpr int NI = RP == 0 ? GC_NA : GC_NB;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int n = min(tid + 256 * u, NI - 1);  // the last item repeats: the same data
+    const int rp = RP == 0 ? (n >= GC_NA / 2 ? 1 : 0) : 2;
+    const int m = n - (RP == 0 ? rp * (GC_NA / 2) : 0);
+    int oa, ob;
     if (IN) {
       oa = (((q0 - 1 + 2 * rp) * w + qx0 - 1) * TAP_N + (m >> 3) * TAP_CO + (m & 7) * 4) * 4;
       ob = oa + w * TAP_N * 4;
@@ -368,286 +368,298 @@ __device__ __forceinline__ void gc_block(const float* __restrict__ P, int h, int
       oa = (ia * w * TAP_N + c) * 4;
       ob = (ib * w * TAP_N + c) * 4;
     }
-  };
-  f32x4 pA[GC_UA][2];
-#pragma unroll
-  for (int u = 0; u < GC_UA; ++u) {
-    const int n = min(tid + 256 * u, GC_NA - 1);  // the last item repeats: the same data
-    const int rp = n >= GC_NA / 2;
-    int oa, ob;
-    pitem(n - rp * (GC_NA / 2), rp, oa, ob);
-    pA[u][0] = gc_bload(prs, oa);
-    pA[u][1] = gc_bload(prs, ob);
-  }
-  // ---- the patch's bf16 planes over P-tile rows 4-5 --------------------------
-  unsigned* pl = reinterpret_cast<unsigned*>(spB);
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int j = tid + 256 * u;
-    if (u == 1 && j >= GC_PAIRS) break;
-    const int py = j / (GC_PC / 2);
-    const int d = py * GC_S + 3 * (j - py * (GC_PC / 2));
-    unsigned hh[3], mm[3], ll[3];
-    pf_split3_pair(px[u][0].x, px[u][0].y, hh[0], mm[0], ll[0]);
-    pf_split3_pair(px[u][0].z, px[u][1].x, hh[1], mm[1], ll[1]);
-    pf_split3_pair(px[u][1].y, px[u][1].z, hh[2], mm[2], ll[2]);
-#pragma unroll
-    for (int e = 0; e < 3; ++e) {
-      pl[d + e] = hh[e];
-      pl[GC_PLANE + d + e] = mm[e];
-      pl[2 * GC_PLANE + d + e] = ll[e];
-    }
-  }
-  // dword 54 of a row is read (times a zero weight: k = 15) by the last tile
-  if (tid < 3 * GC_PR) pl[tid * GC_S + 3 * GC_PC / 2] = 0u;
-  // P-tile rows 4-5 into registers (their LDS is the planes' until after G)
-  f32x4 pB[GC_UB][2];
-#pragma unroll
-  for (int u = 0; u < GC_UB; ++u) {
-    const int n = min(tid + 256 * u, GC_NB - 1);
-    int oa, ob;
-    pitem(n, 2, oa, ob);
-    pB[u][0] = gc_bload(prs, oa);
-    pB[u][1] = gc_bload(prs, ob);
-  }
-  gc_wait_lgkm0();
-  gc_barrier();
-  GC_TS(2);
-  // ---- G part: tile t = output columns (c, c + 4), c = 8 wave + t; A row m =
-  // pixel (row (m & 3) + 4 (m >> 3), column c + 4 ((m >> 2) & 1)), k half hl:
-  // the 8 bf16 from element 3 (column) + 8 hl of patch row (row + dy), i.e.
-  // dword d0 = 12 wave + 6 colsel + 4 hl + (3 t) / 2 (+ a 16-bit shift for odd t)
-  const int arow = (ln & 3) + 4 * (ln >> 3), colsel = (ln >> 2) & 1;
-  const int pbase = arow * GC_S + 6 * colsel + 4 * hl + 12 * wave;  // even
-  f32x16 acc[4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
-#pragma unroll
-  for (int dy = 0; dy < 5; ++dy) {
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      g6_u32x4 f[3];
-#pragma unroll
-      for (int p = 0; p < 3; ++p) {
-        const int d = pbase + p * GC_PLANE + dy * GC_S;  // even
-        const uint2* q2 = reinterpret_cast<const uint2*>(pl) + (d >> 1);
-        if (t == 0) {  // dwords d .. d+3
-          const uint2 a = q2[0], c = q2[1];
-          f[p] = g6_u32x4{a.x, a.y, c.x, c.y};
-        } else if (t == 1) {  // elements from d+1 (odd): dwords d+1 .. d+5, shifted
-          const unsigned s0 = pl[d + 1];
-          const uint2 a = q2[1], c = q2[2];
-          f[p] = g6_u32x4{__builtin_amdgcn_alignbit(a.x, s0, 16), __builtin_amdgcn_alignbit(a.y, a.x, 16),
-                          __builtin_amdgcn_alignbit(c.x, a.y, 16), __builtin_amdgcn_alignbit(c.y, c.x, 16)};
-        } else if (t == 2) {  // dwords d+3 .. d+6
-          const uint2 a = q2[2];
-          f[p] = g6_u32x4{pl[d + 3], a.x, a.y, pl[d + 6]};
-        } else {  // elements from d+4 (odd): dwords d+4 .. d+8, shifted
-          const uint2 a = q2[2], c = q2[3];
-          const unsigned s4 = pl[d + 8];
-          f[p] = g6_u32x4{__builtin_amdgcn_alignbit(a.y, a.x, 16), __builtin_amdgcn_alignbit(c.x, a.y, 16),
-                          __builtin_amdgcn_alignbit(c.y, c.x, 16), __builtin_amdgcn_alignbit(s4, c.y, 16)};
-        }
-      }
-      // the k80 kernel's six products in its order, operands swapped
-      f32x16 c = acc[t];
-      if (ABL & 1) { acc[t][0] += __builtin_bit_cast(float, f[0][0] ^ f[1][1] ^ f[2][2] ^ wv[dy][0][0]); continue; }
-      c = g6_mfma(f[0], wv[dy][0], c);
-      c = g6_mfma(f[1], wv[dy][0], c);
-      c = g6_mfma(f[0], wv[dy][1], c);
-      c = g6_mfma(f[2], wv[dy][0], c);
-      c = g6_mfma(f[0], wv[dy][2], c);
-      c = g6_mfma(f[1], wv[dy][1], c);
-      acc[t] = c;
-    }
-  }
-  // ---- P tile -> LDS: [row pair][column][tap][channel][2 rows] ----------------
-  GC_TS(3);
-  auto pstore = [&](float* base, int n, const f32x4& a, const f32x4& c) {
-    f32x4* d = reinterpret_cast<f32x4*>(base + 8 * n);
-    d[0] = f32x4{a.x, c.x, a.y, c.y};
-    d[1] = f32x4{a.z, c.z, a.w, c.w};
-  };
-#pragma unroll
-  for (int u = 0; u < GC_UA; ++u) pstore(spA, min(tid + 256 * u, GC_NA - 1), pA[u][0], pA[u][1]);
-  gc_wait_lgkm0();  // every plane read of this wave has completed ...
-  gc_barrier();     // ... in every wave: rows 4-5 may overwrite the planes
-#pragma unroll
-  for (int u = 0; u < GC_UB; ++u) pstore(spB, min(tid + 256 * u, GC_NB - 1), pB[u][0], pB[u][1]);
-  // ---- bias; border-ring pixels take the ring value -------------------------
-  if (IN) {
-#pragma unroll
-    for (int t = 0; t < 4; ++t) acc[t] += bias;
-  } else {
-    const int nring = 2 * W + 2 * (H - 2);
-    const float* rb = ring + (long long)b * nring * TAP_CO + co;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int X = X0 + 8 * wave + t + 4 * hl;
-      const bool edge_x = X == 0 || X == W - 1;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int Y = Y0 + r;
-        acc[t][r] = (edge_x || Y == 0 || Y == H - 1) && X < W
-                        ? rb[(long long)pf_ring_index(Y, X, H, W) * TAP_CO]
-                        : acc[t][r] + bias;
-      }
-    }
-  }
-  gc_wait_lgkm0();
-  gc_barrier();
-  GC_TS(4);
-  // ---- the upsampled part ----------------------------------------------------
-  const float ztop = q0 == 0 ? 0.f : 1.f, zbot = q0 + TQ == h ? 0.f : 1.f;
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    if (ABL & 2) { acc[t][0] += spA[tid * 2 + t]; continue; }
-    const int X = X0 + 8 * wave + t + 4 * hl;  // X % 4 == t
-    // x interpolation: R[rp][ky] = sum_kx wa P[rows][ca][k] + wb P[rows][cb][k]
-    // for the tile-row pair rp (k = 3 ky + kx)
-    int oa[3], ob[3];
-    float wa[3], wb[3];
-#pragma unroll
-    for (int kx = 0; kx < 3; ++kx) {
-      int lo;
-      up4_w(t + kx - 1, lo, wa[kx], wb[kx]);
-      int ca, cb;
-      if (IN) {
-        ca = 1 + 2 * wave + hl + lo;  // tile column of X >> 2, plus lo
-        cb = ca + 1;
-      } else {
-        const int u = X + kx - 1;
-        if (u < 0 || u >= W) wa[kx] = wb[kx] = 0.f;
-        const int qx = X >> 2;
-        ca = min(max(min(qx + lo, w - 1), 0) - (qx0 - 1), CB_CX - 1);
-        cb = min(max(min(qx + lo + 1, w - 1), 0) - (qx0 - 1), CB_CX - 1);
-      }
-      oa[kx] = ca * GC_CELL + kx * 2 * CB_CG + 2 * ln;
-      ob[kx] = cb * GC_CELL + kx * 2 * CB_CG + 2 * ln;
-    }
-    gc_f2 R[3][3];
-#pragma unroll
-    for (int rp = 0; rp < 3; ++rp) {
-      const float* base = rp < 2 ? spA + rp * GC_RP : spB;
-#pragma unroll
-      for (int ky = 0; ky < 3; ++ky) {
-        gc_f2 s = {0.f, 0.f};
-#pragma unroll
-        for (int kx = 0; kx < 3; ++kx) {
-          const gc_f2 pa = *reinterpret_cast<const gc_f2*>(base + oa[kx] + ky * 6 * CB_CG);
-          const gc_f2 pb = *reinterpret_cast<const gc_f2*>(base + ob[kx] + ky * 6 * CB_CG);
-          s = gc_fma2(gc_f2{wa[kx], wa[kx]}, pa, s);
-          s = gc_fma2(gc_f2{wb[kx], wb[kx]}, pb, s);
-        }
-        R[rp][ky] = s;
-      }
-    }
-    // y interpolation of output rows (4 i + 2 rp2, + 1) from R rows i + j, j in -1..1
-#pragma unroll
-    for (int i = 0; i < TQ; ++i) {
-#pragma unroll
-      for (int rq = 0; rq < 2; ++rq) {
-        gc_f2 o = {acc[t][4 * i + 2 * rq], acc[t][4 * i + 2 * rq + 1]};
-#pragma unroll
-        for (int ky = 0; ky < 3; ++ky) {
-#pragma unroll
-          for (int j = -1; j <= 1; ++j) {
-            float cA = gc_cy(2 * rq, ky, j), cB = gc_cy(2 * rq + 1, ky, j);
-            if (cA == 0.f && cB == 0.f) continue;
-            if (!IN && i == 0 && rq == 0 && ky == 0) cA *= ztop;  // conv2's zero padding
-            if (!IN && i == TQ - 1 && rq == 1 && ky == 2) cB *= zbot;
-            const int ry = i + 1 + j;  // tile row
-            const float rv = R[ry >> 1][ky][ry & 1];
-            if (ABL & 16) {  // packed, op_sel broadcast: run-to-run differences
-              o = gc_fma2(gc_f2{cA, cB}, gc_f2{rv, rv}, o);
-            } else if (ABL & 32) {
-              gc_f2 r2 = {rv, rv};
-              asm volatile("" : "+v"(r2));
-              o = gc_fma2(gc_f2{cA, cB}, r2, o);
-            } else {
-              if (cA != 0.f) o.x = __builtin_fmaf(cA, rv, o.x);
-              if (cB != 0.f) o.y = __builtin_fmaf(cB, rv, o.y);
-            }
-          }
-        }
-        acc[t][4 * i + 2 * rq] = o.x;
-        acc[t][4 * i + 2 * rq + 1] = o.y;
-      }
-    }
-  }
-  GC_TS(5);
-  // ---- the instance-norm statistics (this lane's channel, its 4 columns) -----
-  double s1 = 0.0, s2 = 0.0;
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int X = X0 + 8 * wave + t + 4 * hl;
-    if (!IN && X >= W) continue;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const double dv = acc[t][r];
-      s1 += dv;
-      s2 = fma(dv, dv, s2);
-    }
-  }
-  s1 += __shfl_xor(s1, 32, 64);  // lanes l and l ^ 32 hold the same channel
-  s2 += __shfl_xor(s2, 32, 64);
-  // ---- y through LDS: [row][column][channel], then 16-B stores of 4 channels
-  // (a lane's 16 rows x 1 channel would be 64 dword stores: store-issue bound)
-  gc_barrier();  // every wave is done reading the P tile
-  {
-    float* so = spA + (8 * wave + 4 * hl) * CB_CG + ln;
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) so[(r * 32 + t) * CB_CG] = acc[t][r];
-  }
-  double* red = reinterpret_cast<double*>(spA + 16 * 32 * CB_CG);  // [wave][32 channels][2]
-  if (part && hl == 0) {
-    red[(wave * CB_CG + ln) * 2] = s1;
-    red[(wave * CB_CG + ln) * 2 + 1] = s2;
-  }
-  gc_wait_lgkm0();
-  gc_barrier();
-  {
-    const int col = tid >> 3, quad = tid & 7, X = X0 + col;
-    const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
-        y + ((long long)b * H + Y0) * W * ycs, (short)0, 0x7fffffff, 0x00020000);
-    const int yrow = W * ycs * 4, xo = (X * ycs + cg * CB_CG + quad * 4) * 4;
-    const f32x4* si = reinterpret_cast<const f32x4*>(spA) + tid;
-    if (IN || X < W) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        if (ABL & 4) { if (si[r * 256].x == 1.2345f) y[tid] = 0.f; continue; }
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(g6_u32x4, si[r * 256]), yrs, xo,
-                                               r * yrow, 0);
-      }
-    }
-  }
-  GC_TS(6);
-  // ---- statistics: the block's 32 columns of each channel, fixed order ------
-  if (part && tid < 2 * CB_CG) {
-    const int c = tid >> 1, which = tid & 1;
-    double a = 0.0;
-    for (int x = 0; x < 4; ++x) a += red[(x * CB_CG + c) * 2 + which];
-    const long long chunk = (long long)qb * nxb + xb;
-    const long long nchunk = (long long)nxb * nqb;
-    part[(((long long)b * nchunk + chunk) * TAP_CO + cg * CB_CG + c) * 2 + which] = a;
+    pr[u][0] = gc_bload(prs, oa);
+    pr[u][1] = gc_bload(prs, ob);
   }
 }
 
-template <int ABL>
-__global__ __launch_bounds__(256, 2) void up4tap_gcombine_kernel(
-    const float* __restrict__ P, int h, int w, const float* __restrict__ img4,
-    const unsigned short* __restrict__ wp, const float* __restrict__ bc,
-    const float* __restrict__ ring, float* __restrict__ y, int ycs, double* __restrict__ part) {
-  // P-tile rows 0-3 (spA), the patch planes then rows 4-5 (spB); at the end the
-  // y tile (64 KB) and the statistics
+// One block = one tile (image b, 16 output rows, 32 output columns, channel
+// group cg).  Measured and not kept (r10r): two tiles per block with the next
+// tile's patch loaded during this one's combine -- 2457 vs 2272 us (the
+// prefetch registers push the combine past 256 registers unless the block is
+// restructured around them, and the half-size grid tails worse).
+template <bool IN>
+__device__ __forceinline__ void gc_block(const GcArgs& A, float* spA, float* spB, int b, int qb,
+                                         int xb, int cg) {
+  const int h = A.h, w = A.w, H = 4 * h, W = 4 * w, nxb = A.nxb;
+  const int q0 = qb * TQ, Y0 = 4 * q0;
+  unsigned* pl = reinterpret_cast<unsigned*>(spB);
+  f32x4 px[2][2], pA[GC_UA][2], pB[GC_UB][2];
+  {
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6, hl = lane >> 5, ln = lane & 31;
+    const int qx0 = xb * CB_QX, X0 = 4 * qx0;
+    const int co = cg * CB_CG + ln;
+    const float bias = A.bc[(long long)b * TAP_CO + co];
+    const unsigned short* wbase =
+        A.wp + (long long)b * 3 * TAP_CO * GC_K + (long long)co * GC_K + 8 * hl;
+    gc_issue_patch<IN>(A, b, q0, qx0, tid, px);
+    // ---- P rows 0-3 (needed after the G phase, which hides their latency) -----
+    gc_issue_p<IN, 0>(A, b, q0, qx0, cg, tid, pA);
+    // ---- B operands: this channel group's weight planes ----------------------
+    g6_u32x4 wv[5][3];
+#pragma unroll
+    for (int dy = 0; dy < 5; ++dy)
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        wv[dy][p] = *reinterpret_cast<const g6_u32x4*>(wbase + (long long)p * TAP_CO * GC_K + dy * 16);
+    // ---- the patch's bf16 planes over P-tile rows 4-5 ------------------------
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int j = tid + 256 * u;
+      if (u == 1 && j >= GC_PAIRS) break;
+      const int py = j / (GC_PC / 2);
+      const int d = py * GC_S + 3 * (j - py * (GC_PC / 2));
+      unsigned hh[3], mm[3], ll[3];
+      pf_split3_pair(px[u][0].x, px[u][0].y, hh[0], mm[0], ll[0]);
+      pf_split3_pair(px[u][0].z, px[u][1].x, hh[1], mm[1], ll[1]);
+      pf_split3_pair(px[u][1].y, px[u][1].z, hh[2], mm[2], ll[2]);
+#pragma unroll
+      for (int e = 0; e < 3; ++e) {
+        pl[d + e] = hh[e];
+        pl[GC_PLANE + d + e] = mm[e];
+        pl[2 * GC_PLANE + d + e] = ll[e];
+      }
+    }
+    // dword 54 of a row is read (times a zero weight: k = 15) by the last tile
+    if (tid < 3 * GC_PR) pl[tid * GC_S + 3 * GC_PC / 2] = 0u;
+    // P-tile rows 4-5 into registers (their LDS is the planes' until after G)
+    gc_issue_p<IN, 2>(A, b, q0, qx0, cg, tid, pB);
+    gc_wait_lgkm0();
+    gc_barrier();
+    // ---- G part: tile t = output columns (c, c + 4), c = 8 wave + t; A row m =
+    // pixel (row (m & 3) + 4 (m >> 3), column c + 4 ((m >> 2) & 1)), k half hl:
+    // the 8 bf16 from element 3 (column) + 8 hl of patch row (row + dy), i.e.
+    // dword d0 = 12 wave + 6 colsel + 4 hl + (3 t) / 2 (+ a 16-bit shift for odd t)
+    const int arow = (ln & 3) + 4 * (ln >> 3), colsel = (ln >> 2) & 1;
+    const int pbase = arow * GC_S + 6 * colsel + 4 * hl + 12 * wave;  // even
+    f32x16 acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+#pragma unroll
+    for (int dy = 0; dy < 5; ++dy) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        g6_u32x4 f[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          const int d = pbase + p * GC_PLANE + dy * GC_S;  // even
+          const uint2* q2 = reinterpret_cast<const uint2*>(pl) + (d >> 1);
+          if (t == 0) {  // dwords d .. d+3
+            const uint2 a = q2[0], c = q2[1];
+            f[p] = g6_u32x4{a.x, a.y, c.x, c.y};
+          } else if (t == 1) {  // elements from d+1 (odd): dwords d+1 .. d+5, shifted
+            const unsigned s0 = pl[d + 1];
+            const uint2 a = q2[1], c = q2[2];
+            f[p] = g6_u32x4{__builtin_amdgcn_alignbit(a.x, s0, 16),
+                            __builtin_amdgcn_alignbit(a.y, a.x, 16),
+                            __builtin_amdgcn_alignbit(c.x, a.y, 16),
+                            __builtin_amdgcn_alignbit(c.y, c.x, 16)};
+          } else if (t == 2) {  // dwords d+3 .. d+6
+            const uint2 a = q2[2];
+            f[p] = g6_u32x4{pl[d + 3], a.x, a.y, pl[d + 6]};
+          } else {  // elements from d+4 (odd): dwords d+4 .. d+8, shifted
+            const uint2 a = q2[2], c = q2[3];
+            const unsigned s4 = pl[d + 8];
+            f[p] = g6_u32x4{__builtin_amdgcn_alignbit(a.y, a.x, 16),
+                            __builtin_amdgcn_alignbit(c.x, a.y, 16),
+                            __builtin_amdgcn_alignbit(c.y, c.x, 16),
+                            __builtin_amdgcn_alignbit(s4, c.y, 16)};
+          }
+        }
+        // the k80 kernel's six products in its order, operands swapped
+        f32x16 c = acc[t];
+        c = g6_mfma(f[0], wv[dy][0], c);
+        c = g6_mfma(f[1], wv[dy][0], c);
+        c = g6_mfma(f[0], wv[dy][1], c);
+        c = g6_mfma(f[2], wv[dy][0], c);
+        c = g6_mfma(f[0], wv[dy][2], c);
+        c = g6_mfma(f[1], wv[dy][1], c);
+        acc[t] = c;
+      }
+    }
+    // ---- P tile -> LDS: [row pair][column][tap][channel][2 rows] --------------
+    auto pstore = [&](float* base, int n, const f32x4& a, const f32x4& c) {
+      f32x4* d = reinterpret_cast<f32x4*>(base + 8 * n);
+      d[0] = f32x4{a.x, c.x, a.y, c.y};
+      d[1] = f32x4{a.z, c.z, a.w, c.w};
+    };
+#pragma unroll
+    for (int u = 0; u < GC_UA; ++u) pstore(spA, min(tid + 256 * u, GC_NA - 1), pA[u][0], pA[u][1]);
+    gc_wait_lgkm0();  // every plane read of this wave has completed ...
+    gc_barrier();     // ... in every wave: rows 4-5 may overwrite the planes
+#pragma unroll
+    for (int u = 0; u < GC_UB; ++u) pstore(spB, min(tid + 256 * u, GC_NB - 1), pB[u][0], pB[u][1]);
+    // ---- bias; border-ring pixels take the ring value -----------------------
+    if (IN) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] += bias;
+    } else {
+      const int nring = 2 * W + 2 * (H - 2);
+      const float* rb = A.ring + (long long)b * nring * TAP_CO + co;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int X = X0 + 8 * wave + t + 4 * hl;
+        const bool edge_x = X == 0 || X == W - 1;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int Y = Y0 + r;
+          acc[t][r] = (edge_x || Y == 0 || Y == H - 1) && X < W
+                          ? rb[(long long)pf_ring_index(Y, X, H, W) * TAP_CO]
+                          : acc[t][r] + bias;
+        }
+      }
+    }
+    gc_wait_lgkm0();
+    gc_barrier();
+    // ---- the upsampled part --------------------------------------------------
+    const float ztop = q0 == 0 ? 0.f : 1.f, zbot = q0 + TQ == h ? 0.f : 1.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int X = X0 + 8 * wave + t + 4 * hl;  // X % 4 == t
+      // x interpolation: R[rp][ky] = sum_kx wa P[rows][ca][k] + wb P[rows][cb][k]
+      // for the tile-row pair rp (k = 3 ky + kx), two rows per v_pk_fma_f32
+      int oa[3], ob[3];
+      float wa[3], wb[3];
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        int lo;
+        up4_w(t + kx - 1, lo, wa[kx], wb[kx]);
+        int ca, cb;
+        if (IN) {
+          ca = 1 + 2 * wave + hl + lo;  // tile column of X >> 2, plus lo
+          cb = ca + 1;
+        } else {
+          const int u = X + kx - 1;
+          if (u < 0 || u >= W) wa[kx] = wb[kx] = 0.f;
+          const int qx = X >> 2;
+          ca = min(max(min(qx + lo, w - 1), 0) - (qx0 - 1), CB_CX - 1);
+          cb = min(max(min(qx + lo + 1, w - 1), 0) - (qx0 - 1), CB_CX - 1);
+        }
+        oa[kx] = ca * GC_CELL + kx * 2 * CB_CG + 2 * ln;
+        ob[kx] = cb * GC_CELL + kx * 2 * CB_CG + 2 * ln;
+      }
+      gc_f2 R[3][3];
+#pragma unroll
+      for (int rp = 0; rp < 3; ++rp) {
+        const float* base = rp < 2 ? spA + rp * GC_RP : spB;
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+          gc_f2 s = {0.f, 0.f};
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx) {
+            const gc_f2 pa = *reinterpret_cast<const gc_f2*>(base + oa[kx] + ky * 6 * CB_CG);
+            const gc_f2 pb = *reinterpret_cast<const gc_f2*>(base + ob[kx] + ky * 6 * CB_CG);
+            s = gc_fma2(gc_f2{wa[kx], wa[kx]}, pa, s);
+            s = gc_fma2(gc_f2{wb[kx], wb[kx]}, pb, s);
+          }
+          R[rp][ky] = s;
+        }
+      }
+      // y interpolation of output rows 4 i + r from R rows i + j, j in -1..1.
+      // Scalar FMAs: the packed form (pairs of output rows, the R value
+      // broadcast by op_sel) gave run-to-run different values in lanes 48-63
+      // 
+#pragma unroll
+      for (int i = 0; i < TQ; ++i) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float o = acc[t][4 * i + r];
+#pragma unroll
+          for (int ky = 0; ky < 3; ++ky) {
+#pragma unroll
+            for (int j = -1; j <= 1; ++j) {
+              float c = gc_cy(r, ky, j);
+              if (c == 0.f) continue;
+              if (!IN && i == 0 && r == 0 && ky == 0) c *= ztop;  // conv2's zero padding
+              if (!IN && i == TQ - 1 && r == 3 && ky == 2) c *= zbot;
+              const int ry = i + 1 + j;  // tile row
+              o = __builtin_fmaf(c, R[ry >> 1][ky][ry & 1], o);
+            }
+          }
+          acc[t][4 * i + r] = o;
+        }
+      }
+    }
+    // ---- the instance-norm statistics (this lane's channel, its 4 columns) ---
+    // per column: pairwise fp32 sums of the 16 rows (depth 4; a sequential fp64
+    // chain of 64 dependent adds per lane was the tile's longest dependency),
+    // then fp64 across the columns and the block
+    double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int X = X0 + 8 * wave + t + 4 * hl;
+      if (!IN && X >= W) continue;
+      float a[16], q[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        a[r] = acc[t][r];
+        q[r] = acc[t][r] * acc[t][r];
+      }
+#pragma unroll
+      for (int st = 8; st >= 1; st >>= 1)
+#pragma unroll
+        for (int r = 0; r < st; ++r) {
+          a[r] += a[r + st];
+          q[r] += q[r + st];
+        }
+      s1 += (double)a[0];
+      s2 += (double)q[0];
+    }
+    s1 += __shfl_xor(s1, 32, 64);  // lanes l and l ^ 32 hold the same channel
+    s2 += __shfl_xor(s2, 32, 64);
+    // ---- y through LDS: [row][column][channel], then 16-B stores of 4
+    // channels (a lane's 16 rows x 1 channel would be 64 dword stores: the
+    // store tail was issue-bound) ------------------------------------------------
+    gc_barrier();  // every wave is done reading the P tile
+    {
+      float* so = spA + (8 * wave + 4 * hl) * CB_CG + ln;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) so[(r * 32 + t) * CB_CG] = acc[t][r];
+    }
+    double* red = reinterpret_cast<double*>(spA + 16 * 32 * CB_CG);  // [wave][32 channels][2]
+    if (A.part && hl == 0) {
+      red[(wave * CB_CG + ln) * 2] = s1;
+      red[(wave * CB_CG + ln) * 2 + 1] = s2;
+    }
+    gc_wait_lgkm0();
+    gc_barrier();
+    {
+      const int col = tid >> 3, quad = tid & 7, X = X0 + col;
+      const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
+          A.y + ((long long)b * H + Y0) * W * A.ycs, (short)0, 0x7fffffff, 0x00020000);
+      const int yrow = W * A.ycs * 4, xo = (X * A.ycs + cg * CB_CG + quad * 4) * 4;
+      const f32x4* si = reinterpret_cast<const f32x4*>(spA) + tid;
+      if (IN || X < W) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(g6_u32x4, si[r * 256]), yrs,
+                                                 xo, r * yrow, 0);
+      }
+    }
+    // ---- statistics: the block's 32 columns of each channel, fixed order ----
+    if (A.part && tid < 2 * CB_CG) {
+      const int c = tid >> 1, which = tid & 1;
+      double a = 0.0;
+      for (int x = 0; x < 4; ++x) a += red[(x * CB_CG + c) * 2 + which];
+      const long long chunk = (long long)qb * nxb + xb;
+      const long long nchunk = (long long)nxb * A.nqb;
+      A.part[(((long long)b * nchunk + chunk) * TAP_CO + cg * CB_CG + c) * 2 + which] = a;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256, 2) void up4tap_gcombine_kernel(GcArgs A) {
+  // P-tile rows 0-3 (spA), the patch planes then rows 4-5 (spB); at the end of
+  // each tile the y tile (64 KB) and the statistics
   __shared__ __attribute__((aligned(16))) float smem[(GC_NA + GC_NB) * 8];
   float* spA = smem;
   float* spB = smem + GC_NA * 8;
-  const int nxb = (w + CB_QX - 1) / CB_QX, nqb = h / TQ, ncg = TAP_CO / CB_CG;
+  const int ncg = TAP_CO / CB_CG;
   // XCD-aware order: blocks are dealt round-robin over the 8 XCDs, so block i
   // takes tile (i % 8) * (n / 8) + i / 8 -- neighbouring tiles, which share P
   // halo columns, run on one XCD's L2
@@ -655,18 +667,15 @@ __global__ __launch_bounds__(256, 2) void up4tap_gcombine_kernel(
   if ((gridDim.x & 7) == 0) id = (id & 7) * (gridDim.x >> 3) + (id >> 3);
   const int cg = id % ncg;
   id /= ncg;
-  const int xb = id % nxb;
-  id /= nxb;
-  const int qb = id % nqb, b = id / nqb;
-  const bool interior = qb > 0 && qb < nqb - 1 && xb > 0 && xb * CB_QX + CB_QX < w;
-#ifdef GC_ONLY
-  if (GC_ONLY)
-#else
+  const int xb = id % A.nxb;
+  id /= A.nxb;
+  const int qb = id % A.nqb, b = id / A.nqb;
+  // away from the image border: the branch-free form
+  const bool interior = qb > 0 && qb < A.nqb - 1 && xb > 0 && xb * CB_QX + CB_QX < A.w;
   if (interior)
-#endif
-    gc_block<true, ABL>(P, h, w, img4, wp, bc, ring, y, ycs, part, spA, spB, b, qb, xb, cg, nqb, nxb);
+    gc_block<true>(A, spA, spB, b, qb, xb, cg);
   else
-    gc_block<false, ABL>(P, h, w, img4, wp, bc, ring, y, ycs, part, spA, spB, b, qb, xb, cg, nqb, nxb);
+    gc_block<false>(A, spA, spB, b, qb, xb, cg);
 }
 
 // ---- adjoint (keypoint-head training, config 5) ------------------------------
@@ -811,12 +820,21 @@ int pf_up4tap_gcombine(int n, int H, int W, const float* P, const float* img4,
   if (H % 16 || W % 16 || ycs % 4 || ycs < TAP_CO || n <= 0) return POSFEAT_E_INVALID;
   if (!P || !img4 || !wp || !bc || !ring || !y || (mean && !part)) return POSFEAT_E_INVALID;
   const int nchunk = (h / TQ) * ((w + CB_QX - 1) / CB_QX);
-  static const int abl = getenv("POSFEAT_GC_ABL") ? atoi(getenv("POSFEAT_GC_ABL")) : 0;
-  auto kern = abl == 1 ? up4tap_gcombine_kernel<1> : abl == 2 ? up4tap_gcombine_kernel<2>
-            : abl == 4 ? up4tap_gcombine_kernel<4> : abl == 6 ? up4tap_gcombine_kernel<6>
-            : abl == 7 ? up4tap_gcombine_kernel<7> : abl == 8 ? up4tap_gcombine_kernel<8> : abl == 16 ? up4tap_gcombine_kernel<16> : abl == 32 ? up4tap_gcombine_kernel<32> : up4tap_gcombine_kernel<0>;
-  hipLaunchKernelGGL(kern, dim3(n * nchunk * (TAP_CO / CB_CG)), dim3(256), 0, st,
-                     P, h, w, img4, wp, bc, ring, y, ycs, mean ? part : nullptr);
+  GcArgs A;
+  A.P = P;
+  A.img4 = img4;
+  A.wp = wp;
+  A.bc = bc;
+  A.ring = ring;
+  A.y = y;
+  A.part = mean ? part : nullptr;
+  A.h = h;
+  A.w = w;
+  A.ycs = ycs;
+  A.nqb = h / TQ;
+  A.nxb = (w + CB_QX - 1) / CB_QX;
+  const int nblk = n * A.nqb * A.nxb * (TAP_CO / CB_CG);
+  hipLaunchKernelGGL(up4tap_gcombine_kernel, dim3(nblk), dim3(256), 0, st, A);
   PF_CHECK_LAUNCH();
   if (mean) PF_TRY(pf_in_finalize(part, n, nchunk, H * W, TAP_CO, mean, rstd, st));
   return POSFEAT_OK;
@@ -842,9 +860,6 @@ int pf_up4tap_weights_t(const float* w2_packed, float* wt, hipStream_t st) {
   return POSFEAT_OK;
 }
 
-extern "C" int posfeat_debug_gc_ts(unsigned long long* host, long long n) {
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(gc_ts), n * 8) == hipSuccess ? 0 : -1;
-}
 extern "C" int posfeat_debug_gcombine(int n, int H, int W, const float* P, const float* img4,
                                       const unsigned short* wp, const float* bc, const float* ring,
                                       float* y, double* part, float* mean, float* rstd, void* st) {

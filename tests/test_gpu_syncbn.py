@@ -110,7 +110,8 @@ def test_syncbn_unequal_batches_equal_full_batch(gpu):
     batch statistics, as torch.nn.SyncBatchNorm does.  Maps 1e-4 of scale,
     running statistics rtol 1e-5, and the summed rank gradients against the
     full-batch gradient (two fp32 summation orders of the BatchNorm-heavy
-    backward: relative L2 2e-3 overall, 3e-2 of each tensor's max)."""
+    backward: relative L2 2e-3 overall, 3e-2 of each tensor's max plus 1e-4 of
+    the largest entry)."""
     from test_bb_train import _inputs
     from posfeat_amd import weights
     from posfeat_amd._lib import check, lib
@@ -148,9 +149,13 @@ def test_syncbn_unequal_batches_equal_full_batch(gpu):
     gsum = weights.unpack_bbtrain((ranks[0].grad + ranks[1].grad).cpu().numpy(), full.table)
     gref = weights.unpack_bbtrain(full.grad.cpu().numpy(), full.table)
     num = den = 0.0
+    # conv biases ahead of a BatchNorm have an exactly-zero gradient in real
+    # arithmetic (fp32 noise of ~1e-5 here): a floor of 1e-4 of the largest
+    # gradient entry keeps those tensors from deciding the test
+    floor = 1e-4 * max(float(np.abs(v).max()) for v in gref.values())
     for k, v in gref.items():
         e = float(np.abs(gsum[k] - v).max())
-        assert e <= 3e-2 * max(float(np.abs(v).max()), 1e-12), "%s: err %g of max %g" % (
+        assert e <= 3e-2 * float(np.abs(v).max()) + floor, "%s: err %g of max %g" % (
             k, e, float(np.abs(v).max()))
         num += float(((gsum[k] - v) ** 2).sum())
         den += float((v ** 2).sum())
