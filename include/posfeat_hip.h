@@ -155,6 +155,16 @@ int posfeat_detect(const float *kp_map, int b, int h, int w, int nms_radius, int
                    float *score, int32_t *n_sel, int32_t *counts, void *ws, size_t ws_bytes,
                    void *stream);
 
+/* posfeat_detect with every image of the batch selected as if it were
+ * detected alone: n_sel[b] (device int32), n_sel[i] = clamp(min(num_pts,
+ * counts[i]), 128) -- the reference's extraction loop, which runs
+ * generate_kpts_single on one image at a time (extractor.py:336-342 with
+ * batch_size 1), for a group of same-size images in one call. */
+int posfeat_detect_each(const float *kp_map, int b, int h, int w, int nms_radius, int use_nms,
+                        int thr_mode, float thr, int num_pts, int cap, int32_t *idx,
+                        float *coord, float *score, int32_t *n_sel, int32_t *counts, void *ws,
+                        size_t ws_bytes, void *stream);
+
 /* NMS mask alone (losses/preprocess_utils.py:449-464 nms): mask[b][h][w] = 1
  * iff the pixel is its reflect-padded (2r+1)^2 window's first-occurrence max. */
 int posfeat_nms_mask(const float *score, int b, int h, int w, int radius, uint8_t *mask,
@@ -172,6 +182,12 @@ int posfeat_nms_mask(const float *score, int b, int h, int w, int radius, uint8_
 int posfeat_sample_desc(const float *fmap, int b, int c, int h, int w, int cstride,
                         const float *coord, int npts, const int32_t *n_valid, int normalize,
                         float *out, void *stream);
+
+/* posfeat_sample_desc with one valid-row count per image: n_valid[b] (device
+ * int32, required), e.g. posfeat_detect_each's n_sel. */
+int posfeat_sample_desc_each(const float *fmap, int b, int c, int h, int w, int cstride,
+                             const float *coord, int npts, const int32_t *n_valid, int normalize,
+                             float *out, void *stream);
 
 /* NCHW <-> NHWC helpers used at the API boundary (torch tensors are NCHW). */
 int posfeat_nchw_to_nhwc(const float *x, int n, int c, int h, int w, int cstride_out,

@@ -69,6 +69,11 @@ SIGNATURES = {
     "posfeat_detect": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_int,
                                c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                c_size_t, c_void_p]),
+    "posfeat_detect_each": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_float,
+                                    c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                    c_void_p, c_size_t, c_void_p]),
+    "posfeat_sample_desc_each": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
+                                         c_int, c_void_p, c_int, c_void_p, c_void_p]),
     "posfeat_nms_mask": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     "posfeat_sample_desc": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int,
                                     c_void_p, c_int, c_void_p, c_void_p]),

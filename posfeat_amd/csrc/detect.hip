@@ -176,7 +176,7 @@ __global__ __launch_bounds__(1024) void det_select_kernel(
     const uint32_t* __restrict__ keys, const uint32_t* __restrict__ cand_key,
     const int32_t* __restrict__ cand_idx, int nb, int P, const int32_t* __restrict__ counts,
     int num_pts, int cap, int32_t* __restrict__ sel, uint32_t* __restrict__ selkey,
-    int32_t* __restrict__ n_sel) {
+    int32_t* __restrict__ n_sel, int each) {
   const int b = blockIdx.x;
   const uint32_t ZKEY = 0x80000000u;
   const uint32_t* kb = keys + (long long)b * P;
@@ -194,8 +194,9 @@ __global__ __launch_bounds__(1024) void det_select_kernel(
   const int count = counts[b];
   const int nzero = P - count;  // masked-out cells, key ZKEY
   if (tid == 0) {
-    int minc = counts[0];
-    for (int k = 1; k < nb; ++k) minc = min(minc, counts[k]);
+    int minc = counts[each ? b : 0];
+    if (!each)
+      for (int k = 1; k < nb; ++k) minc = min(minc, counts[k]);
     int n = num_pts > 0 ? min(num_pts, minc) : minc;
     if (n < 128) n = 128;
     n = min(n, P);
@@ -205,7 +206,8 @@ __global__ __launch_bounds__(1024) void det_select_kernel(
     s_prefix = 0u;
     s_taken = 0;
     s_eqn = 0;
-    if (b == 0) *n_sel = n;
+    if (each) n_sel[b] = n;
+    else if (b == 0) *n_sel = n;
   }
   __syncthreads();
   const int n = s_n;
@@ -317,10 +319,11 @@ __global__ __launch_bounds__(1024) void det_select_kernel(
 
 __global__ void det_rank_kernel(const float* __restrict__ kp, int h, int w, int cap,
                                 const int32_t* __restrict__ sel, const uint32_t* __restrict__ selkey,
-                                const int32_t* __restrict__ n_sel, int32_t* __restrict__ idx_out,
-                                float* __restrict__ coord, float* __restrict__ score) {
+                                const int32_t* __restrict__ n_sel, int each,
+                                int32_t* __restrict__ idx_out, float* __restrict__ coord,
+                                float* __restrict__ score) {
   const int b = blockIdx.y;
-  const int n = *n_sel;
+  const int n = n_sel[each ? b : 0];
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if ((int)(blockIdx.x * blockDim.x) >= n) return;  // block-uniform
   const bool active = t < n;
@@ -386,10 +389,13 @@ extern "C" int posfeat_detect_workspace(int b, int h, int w, int cap, size_t* by
   return POSFEAT_OK;
 }
 
-extern "C" int posfeat_detect(const float* kp_map, int b, int h, int w, int nms_radius,
-                              int use_nms, int thr_mode, float thr, int num_pts, int cap,
-                              int32_t* idx, float* coord, float* score, int32_t* n_sel,
-                              int32_t* counts, void* ws, size_t ws_bytes, void* stream) {
+namespace {
+
+// each = 0: one n for the batch (posfeat_detect); 1: n per image (posfeat_detect_each)
+int detect_impl(const float* kp_map, int b, int h, int w, int nms_radius, int use_nms,
+                int thr_mode, float thr, int num_pts, int cap, int32_t* idx, float* coord,
+                float* score, int32_t* n_sel, int32_t* counts, void* ws, size_t ws_bytes,
+                void* stream, int each) {
   if (!kp_map || !idx || !coord || !score || !n_sel || !counts || !ws) return POSFEAT_E_INVALID;
   if (b <= 0 || h < 3 || w < 3 || nms_radius < 0 || thr_mode < 0 || thr_mode > 3)
     return POSFEAT_E_INVALID;
@@ -436,13 +442,31 @@ extern "C" int posfeat_detect(const float* kp_map, int b, int h, int w, int nms_
     PF_CHECK_LAUNCH();
   }
   hipLaunchKernelGGL(det_select_kernel, dim3(b), dim3(1024), 0, st, keys, cand_key, cand_idx, b,
-                     P, counts, num_pts, cap, sel, selkey, n_sel);
+                     P, counts, num_pts, cap, sel, selkey, n_sel, each);
   PF_CHECK_LAUNCH();
   const int maxn = cap < P ? cap : P;
   hipLaunchKernelGGL(det_rank_kernel, dim3((maxn + 255) / 256, b), dim3(256), 0, st, kp_map, h, w,
-                     cap, sel, selkey, n_sel, idx, coord, score);
+                     cap, sel, selkey, n_sel, each, idx, coord, score);
   PF_CHECK_LAUNCH();
   return POSFEAT_OK;
+}
+
+}  // namespace
+
+extern "C" int posfeat_detect(const float* kp_map, int b, int h, int w, int nms_radius,
+                              int use_nms, int thr_mode, float thr, int num_pts, int cap,
+                              int32_t* idx, float* coord, float* score, int32_t* n_sel,
+                              int32_t* counts, void* ws, size_t ws_bytes, void* stream) {
+  return detect_impl(kp_map, b, h, w, nms_radius, use_nms, thr_mode, thr, num_pts, cap, idx, coord,
+                     score, n_sel, counts, ws, ws_bytes, stream, 0);
+}
+
+extern "C" int posfeat_detect_each(const float* kp_map, int b, int h, int w, int nms_radius,
+                                   int use_nms, int thr_mode, float thr, int num_pts, int cap,
+                                   int32_t* idx, float* coord, float* score, int32_t* n_sel,
+                                   int32_t* counts, void* ws, size_t ws_bytes, void* stream) {
+  return detect_impl(kp_map, b, h, w, nms_radius, use_nms, thr_mode, thr, num_pts, cap, idx, coord,
+                     score, n_sel, counts, ws, ws_bytes, stream, 1);
 }
 
 extern "C" int posfeat_nms_mask(const float* score, int b, int h, int w, int radius,

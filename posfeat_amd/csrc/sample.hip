@@ -13,8 +13,8 @@ namespace {
 template <int CPL>  // channels per lane (C <= 64*CPL)
 __global__ void sample_desc_kernel(const float* __restrict__ fmap, int nb, int C, int h, int w,
                                    int cs, const float* __restrict__ coord, int npts,
-                                   const int32_t* __restrict__ n_valid, int normalize,
-                                   float* __restrict__ out) {
+                                   const int32_t* __restrict__ n_valid, int each,
+                                   int normalize, float* __restrict__ out) {
   const int lane = threadIdx.x & 63;
   const long long wid = blockIdx.x * (long long)(blockDim.x >> 6) + (threadIdx.x >> 6);
   const long long total = (long long)nb * npts;
@@ -22,7 +22,7 @@ __global__ void sample_desc_kernel(const float* __restrict__ fmap, int nb, int C
   const int b = (int)(wid / npts);
   const int k = (int)(wid - (long long)b * npts);
   float* o = out + wid * C;
-  const int nv = n_valid ? *n_valid : npts;
+  const int nv = n_valid ? n_valid[each ? b : 0] : npts;
   if (k >= nv) {
     for (int c = lane; c < C; c += 64) o[c] = 0.f;
     return;
@@ -69,28 +69,38 @@ __global__ void sample_desc_kernel(const float* __restrict__ fmap, int nb, int C
 
 }  // namespace
 
-int pf_sample_desc(const float* fmap, int b, int c, int h, int w, int cs, const float* coord,
-                   int npts, const int32_t* n_valid, int normalize, float* out, hipStream_t st) {
+namespace {
+
+int sample_impl(const float* fmap, int b, int c, int h, int w, int cs, const float* coord,
+                int npts, const int32_t* n_valid, int each, int normalize, float* out,
+                hipStream_t st) {
   const long long waves = (long long)b * npts;
   if (waves == 0) return POSFEAT_OK;
   const int wpb = 4;
   const dim3 grid((unsigned)((waves + wpb - 1) / wpb)), block(64 * wpb);
   if (c <= 64)
     hipLaunchKernelGGL(sample_desc_kernel<1>, grid, block, 0, st, fmap, b, c, h, w, cs, coord,
-                       npts, n_valid, normalize, out);
+                       npts, n_valid, each, normalize, out);
   else if (c <= 128)
     hipLaunchKernelGGL(sample_desc_kernel<2>, grid, block, 0, st, fmap, b, c, h, w, cs, coord,
-                       npts, n_valid, normalize, out);
+                       npts, n_valid, each, normalize, out);
   else if (c <= 256)
     hipLaunchKernelGGL(sample_desc_kernel<4>, grid, block, 0, st, fmap, b, c, h, w, cs, coord,
-                       npts, n_valid, normalize, out);
+                       npts, n_valid, each, normalize, out);
   else if (c <= 1024)
     hipLaunchKernelGGL(sample_desc_kernel<16>, grid, block, 0, st, fmap, b, c, h, w, cs, coord,
-                       npts, n_valid, normalize, out);
+                       npts, n_valid, each, normalize, out);
   else
     return POSFEAT_E_UNSUPPORTED;
   PF_CHECK_LAUNCH();
   return POSFEAT_OK;
+}
+
+}  // namespace
+
+int pf_sample_desc(const float* fmap, int b, int c, int h, int w, int cs, const float* coord,
+                   int npts, const int32_t* n_valid, int normalize, float* out, hipStream_t st) {
+  return sample_impl(fmap, b, c, h, w, cs, coord, npts, n_valid, 0, normalize, out, st);
 }
 
 extern "C" int posfeat_sample_desc(const float* fmap, int b, int c, int h, int w, int cstride,
@@ -100,4 +110,15 @@ extern "C" int posfeat_sample_desc(const float* fmap, int b, int c, int h, int w
     return POSFEAT_E_INVALID;
   return pf_sample_desc(fmap, b, c, h, w, cstride, coord, npts, n_valid, normalize, out,
                         pf_stream(stream));
+}
+
+extern "C" int posfeat_sample_desc_each(const float* fmap, int b, int c, int h, int w,
+                                        int cstride, const float* coord, int npts,
+                                        const int32_t* n_valid, int normalize, float* out,
+                                        void* stream) {
+  if (!fmap || !coord || !n_valid || !out || b <= 0 || c <= 0 || h <= 0 || w <= 0 || npts < 0 ||
+      cstride < c)
+    return POSFEAT_E_INVALID;
+  return sample_impl(fmap, b, c, h, w, cstride, coord, npts, n_valid, 1, normalize, out,
+                     pf_stream(stream));
 }

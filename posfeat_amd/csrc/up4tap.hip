@@ -859,10 +859,3 @@ int pf_up4tap_weights_t(const float* w2_packed, float* wt, hipStream_t st) {
   PF_CHECK_LAUNCH();
   return POSFEAT_OK;
 }
-
-extern "C" int posfeat_debug_gcombine(int n, int H, int W, const float* P, const float* img4,
-                                      const unsigned short* wp, const float* bc, const float* ring,
-                                      float* y, double* part, float* mean, float* rstd, void* st) {
-  return pf_up4tap_gcombine(n, H, W, P, img4, wp, bc, ring, y, 128, part, mean, rstd,
-                            (hipStream_t)st);
-}

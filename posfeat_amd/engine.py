@@ -18,6 +18,7 @@ so a new shape times only the convs it has not met.
 """
 import ctypes
 import os
+import time
 from collections import OrderedDict
 
 import numpy as np
@@ -48,6 +49,7 @@ class ExtractionEngine:
         self._own_ws = {}            # train=True: (b, h, w) -> own workspace
         self._shared_ws = None       # train=False: one grow-only workspace
         self.max_shapes = max(1, int(os.environ.get("POSFEAT_ENGINE_MAX_SHAPES", "8")))
+        self.stats = {"instances_created": 0, "create_s": 0.0, "workspace_grows": 0}
 
     # ------------------------------------------------------------------
     def _instance(self, b, h, w):
@@ -60,8 +62,11 @@ class ExtractionEngine:
                 self._own_ws.pop(old, None)
             handle = ctypes.c_void_p()
             create = lib().posfeat_model_create_train if self.train else lib().posfeat_model_create
+            t0 = time.perf_counter()
             check(create(b, h, w, ptr(self.wdev), ctypes.byref(handle)))
             inst = (handle, int(lib().posfeat_model_workspace(handle)))
+            self.stats["instances_created"] += 1
+            self.stats["create_s"] += time.perf_counter() - t0
             self._inst[key] = inst
         else:
             self._inst.move_to_end(key)
@@ -74,6 +79,7 @@ class ExtractionEngine:
         else:
             ws = self._shared_ws
             if ws is None or ws.numel() < nbytes + 256:
+                self.stats["workspace_grows"] += 1
                 self._shared_ws = None
                 ws = self._shared_ws = torch.empty(nbytes + 256, dtype=torch.uint8,
                                                    device=self.device)

@@ -73,6 +73,23 @@ def generate_kpts_single_async(kp_map, nms_radius, num_pts=False, scale=4, stabl
     return coord, score, n_sel
 
 
+def generate_kpts_each_async(kp_map, nms_radius, num_pts=False, scale=4, stable=True,
+                             temperature=1, stride=1, use_nms=True, thr=False, thr_mod="mean"):
+    """generate_kpts_single_async for a batch of same-size images, each
+    selected as if it were detected alone (the reference extractor calls
+    generate_kpts_single per image, batch_size 1): n is a device tensor [b]."""
+    if not stable:
+        raise NotImplementedError("stable=False (gumbel sampling) is not implemented")
+    if use_nms == "softnms":
+        raise NotImplementedError("use_nms='softnms' is not implemented")
+    if stride != 1:
+        raise NotImplementedError("stride != 1 is not implemented")
+    _, coord, score, _, n_sel = ops.detect(kp_map.float().contiguous(), nms_radius, num_pts,
+                                           use_nms=bool(use_nms), thr=thr, thr_mod=thr_mod,
+                                           sync=False, each=True)
+    return coord, score, n_sel
+
+
 def _detect(kp_map, nms_radius, num_pts, stable, stride, use_nms, thr, thr_mod, sync):
     if not stable:
         raise NotImplementedError("stable=False (gumbel sampling) is not implemented")

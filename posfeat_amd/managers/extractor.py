@@ -34,7 +34,11 @@ name, plus ``feat.h5`` groups for hloc) through h5py; h5py is not part of this
 image, so the option fails at construction when it is missing.
 Out of scope (diagnostics): save_imgs visualisation.
 """
+import copy
+import ctypes
+import functools
 import logging
+import mmap
 import os
 import time
 from collections import deque
@@ -48,6 +52,39 @@ import yaml
 from .. import datasets, networks, ops
 from ..losses import preprocess_utils as putils
 from ..losses.preprocess_utils import denormalize_coords, normalize_coords, sample_feat_by_coord
+
+
+def _staging_buffer(n):
+    """A pinned uint8 host buffer of ``n`` bytes marked MADV_DONTFORK.
+
+    The loader's decode workers are forked from this process; a pinned page
+    that is shared copy-on-write with a child is copied on the parent's next
+    write, and the device's view of the buffer is then rebuilt on the next
+    host-to-device copy: the first group of every extraction run took 0.2-3.2 s
+    to upload 29 MB (r11i: 477 ms cold, 3242 ms in a second pass) against
+    0.6 ms with the same buffers and no workers (r11j).  No worker ever reads
+    the staging buffers, so they are left out of the children altogether.
+    The caching host allocator hands out whole hipHostMalloc blocks (page
+    aligned); the advice covers the pages inside the tensor."""
+    buf = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+    page = mmap.PAGESIZE
+    a = buf.data_ptr()
+    lo = (a + page - 1) // page * page
+    hi = (a + n) // page * page
+    if hi > lo and _libc().madvise(ctypes.c_void_p(lo), ctypes.c_size_t(hi - lo),
+                                   _MADV_DONTFORK) != 0:
+        raise OSError(ctypes.get_errno(), "madvise(MADV_DONTFORK) on the staging buffer")
+    return buf
+
+
+_MADV_DONTFORK = 10   # <sys/mman.h>, Linux
+
+
+@functools.lru_cache(None)
+def _libc():
+    libc = ctypes.CDLL(None, use_errno=True)
+    libc.madvise.argtypes = (ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int)
+    return libc
 
 
 class Extractor:
@@ -81,18 +118,7 @@ class Extractor:
             raise FileNotFoundError(cfg_path)
 
         self.set_device()
-        self.set_folder_and_logger()
-
-        tmp_model = getattr(networks, self.config["model"])
-        self.model = tmp_model(self.config["model_config"], self.device)
-        if self.multi_gpu:
-            self.model.set_parallel(self.local_rank)
-        self.model.load_checkpoint(self.config["load_path"])
-        self.model.set_eval()
-
         self.detector = getattr(putils, self.config["detector"])
-        self.logger.info("use {} to detect keypoints".format(self.config["detector"]))
-
         dataset = getattr(datasets, self.config["data"])
         extract_dataset = dataset(configs=self.config["data_config_extract"])
         sampler = (datasets.ShardSampler(len(extract_dataset), self.rank, self.world)
@@ -101,6 +127,30 @@ class Extractor:
             extract_dataset, batch_size=self.config["data_config_extract"]["batch_size"],
             shuffle=False, num_workers=self.config["data_config_extract"].get("workers", 0),
             collate_fn=self.my_collate, sampler=sampler, pin_memory=True)
+        # The pipelined loop's decode workers are forked HERE, before the model
+        # and the engine workspace exist: a fork stalls this process's next
+        # device work for a time that grows with what the process has mapped
+        # on the device (r11i-r11l: the first upload after a fork took 236 ms
+        # in a fresh process, 3.2 s with a 25 GB engine workspace resident,
+        # 0.6 ms with no fork or with the workers forked at this point)
+        self._early_iter = iter(self._pipelined_loader()) if self._pipelined() else None
+        self._warm_h2d()   # async: overlaps the model construction below
+        self.set_folder_and_logger()
+
+        tmp_model = getattr(networks, self.config["model"])
+        self.model = tmp_model(self.config["model_config"], self.device)
+        if self.multi_gpu:
+            self.model.set_parallel(self.local_rank)
+        self.model.load_checkpoint(self.config["load_path"])
+        self.model.set_eval()
+        self.model.engine()   # weight packing (~120 ms) belongs to construction
+
+        self.logger.info("use {} to detect keypoints".format(self.config["detector"]))
+        if os.environ.get("POSFEAT_EXTRACT_TRACE", "0") == "1":
+            t = time.perf_counter()
+            torch.cuda.synchronize(self.device)
+            print("[extract] construction's device work drained in %.1f ms" % (
+                1e3 * (time.perf_counter() - t)), flush=True)
 
     def my_collate(self, batch):
         batch = list(filter(lambda b: b is not None, batch))
@@ -209,11 +259,14 @@ class Extractor:
             kpt = kpt * inputs["scale"].cpu().numpy()
         return {"kpt": kpt, "desc": feat_f, "kp_score": kp_score}
 
+    def _pipelined(self):
+        return not (os.environ.get("POSFEAT_EXTRACT_PIPELINE", "1") == "0"
+                    or os.environ.get("POSFEAT_EXTRACT_TIMING", "0") == "1"
+                    or self.detector is not putils.generate_kpts_single)
+
     @torch.no_grad()
     def extract(self):
-        if (os.environ.get("POSFEAT_EXTRACT_PIPELINE", "1") == "0"
-                or os.environ.get("POSFEAT_EXTRACT_TIMING", "0") == "1"
-                or self.detector is not putils.generate_kpts_single):
+        if not self._pipelined():
             return self._extract_serial()
         return self._extract_pipelined()
 
@@ -227,47 +280,89 @@ class Extractor:
         """Engine + detector + sampler for a list of same-size images, all
         enqueued on the current stream; returns (event, per-image host copies)."""
         dev = self.device
-        # per-image async copies from the loader's pinned buffers (a host-side
-        # stack would be pageable, and a pageable H2D copy waits for the stream)
+        trace = os.environ.get("POSFEAT_EXTRACT_TRACE", "0") == "1"
+        t0 = time.perf_counter()
+        # the group's uint8 images go through this extractor's own pinned
+        # staging buffer (two, alternating, excluded from fork: see
+        # _staging_buffer): one host copy per image, one async H2D
         if all(it[1] is not None for it in items):
-            # items[i][1]: the cropped uint8 image [h, w, 3] from pinned memory
-            u8 = torch.empty((len(items),) + tuple(items[0][1].shape), dtype=torch.uint8,
-                             device=dev)
+            shape = (len(items),) + tuple(items[0][1].shape)
+            n = int(np.prod(shape))
+            k = self._stage_next
+            self._stage_next ^= 1
+            buf, done = self._stage[k]
+            if done is not None:
+                done.synchronize()   # the H2D that last read this buffer has finished
+            if buf is None or buf.numel() < n:
+                buf = _staging_buffer(max(n, 2 * (buf.numel() if buf is not None else 0)))
+            st = buf[:n].view(shape)
             for i, it in enumerate(items):
-                u8[i].copy_(it[1], non_blocking=True)
+                st[i].copy_(it[1])
+            u8 = torch.empty(shape, dtype=torch.uint8, device=dev)
+            if trace:
+                torch.cuda.synchronize(dev)
+                ta = time.perf_counter()
+            u8.copy_(st, non_blocking=True)
+            ev_copy = torch.cuda.Event()
+            ev_copy.record()
+            self._stage[k] = (buf, ev_copy)
+            if trace:
+                torch.cuda.synchronize(dev)
+                tb = time.perf_counter()
+                print("[extract]   stage %.1f ms, H2D %.1f ms" % (
+                    1e3 * (ta - t0), 1e3 * (tb - ta)), flush=True)
             im = ops.normalize_rgb8(u8)
         else:
             im = torch.empty((len(items),) + tuple(items[0][0].shape), device=dev)
             for i, it in enumerate(items):
                 im[i].copy_(it[0], non_blocking=True)
         g, _, h, w = im.shape
+        if trace:
+            torch.cuda.synchronize(dev)
         t1 = time.perf_counter()
         eng = self.model.engine()
+        if trace:
+            torch.cuda.synchronize(dev)
         t2 = time.perf_counter()
         out = eng.run(im, outputs=())
+        if trace:
+            torch.cuda.synchronize(dev)
         t3 = time.perf_counter()
         nhwc = out["_local_map_nhwc"]
         host = []
-        for i, (_, _, name, scale) in enumerate(items):
-            coord_n, score, n_sel = putils.generate_kpts_single_async(
-                out["local_point"][i:i + 1], **self._det_cfg(name))
-            desc = ops.sample_desc_nhwc(nhwc[i:i + 1], coord_n, c=128,
-                                        normalize=self.config["loss_distance"] == "cos",
-                                        n_valid=n_sel)
-            host.append((name, scale, n_sel.to("cpu", non_blocking=True),
-                         coord_n.to("cpu", non_blocking=True), desc.to("cpu", non_blocking=True),
-                         score.to("cpu", non_blocking=True), w, h))
+        norm = self.config["loss_distance"] == "cos"
+        # one detect + one sample launch per run of images sharing a detector
+        # config (Aachen query / db), each image selected as if alone
+        i = 0
+        while i < g:
+            cfg = self._det_cfg(items[i][2])
+            j = i + 1
+            while j < g and self._det_cfg(items[j][2]) is cfg:
+                j += 1
+            coord_n, score, n_sel = putils.generate_kpts_each_async(
+                out["local_point"][i:j], **cfg)
+            desc = ops.sample_desc_nhwc(nhwc[i:j], coord_n, c=128, normalize=norm,
+                                        n_valid=n_sel, each=True)
+            hs = (n_sel.to("cpu", non_blocking=True), coord_n.to("cpu", non_blocking=True),
+                  desc.to("cpu", non_blocking=True), score.to("cpu", non_blocking=True))
+            for k in range(i, j):
+                host.append((items[k][2], items[k][3], hs, k - i, w, h))
+            i = j
         ev = torch.cuda.Event()
         ev.record()
-        if os.environ.get("POSFEAT_EXTRACT_TRACE", "0") == "1":
-            print("[extract]   engine() %.1f ms, run %.1f ms, detect/sample/D2H %.1f ms" % (
-                1e3 * (t2 - t1), 1e3 * (t3 - t2), 1e3 * (time.perf_counter() - t3)), flush=True)
+        if trace:
+            torch.cuda.synchronize(dev)
+            print("[extract]   upload+normalise %.1f ms, engine() %.1f ms, run %.1f ms, "
+                  "detect/sample/D2H %.1f ms (synchronised)" % (
+                      1e3 * (t1 - t0), 1e3 * (t2 - t1), 1e3 * (t3 - t2),
+                      1e3 * (time.perf_counter() - t3)), flush=True)
         return ev, host
 
     def _finish_group(self, ev, host, writer, futures):
         ev.synchronize()
-        for name, scale, n_sel, kpt, desc, score, w, h in host:
-            n = int(n_sel[0])   # the selected count (incl. the 128 raise)
+        for name, scale, (n_sel, kpt, desc, score), r, w, h in host:
+            kpt, desc, score = kpt[r:r + 1], desc[r:r + 1], score[r:r + 1]
+            n = int(n_sel[r])   # the selected count (incl. the 128 raise)
             # denormalize_coords on the host: the same two fp32 roundings
             # (x * c, then + c) as the device path; a host->device copy of c
             # here would wait for the whole queue
@@ -292,9 +387,9 @@ class Extractor:
         transaction (default 8) collated as a list (sizes may differ), and
         ``POSFEAT_EXTRACT_WORKERS`` decode workers (default: the config's
         ``workers``; an explicit 0 loads in this process).  Order is the
-        sampler's, as the reference loop's.  The dataset's ``uint8_only`` flag
-        is set for this loader only (``_extract_pipelined`` restores it)."""
-        ds = self.extract_loader.dataset
+        sampler's, as the reference loop's.  The loader reads a shallow copy of
+        the dataset with ``uint8_only`` set; the serial loader's is untouched."""
+        ds = copy.copy(self.extract_loader.dataset)
         if hasattr(ds, "uint8_only"):
             ds.uint8_only = True
         cfg = self.config["data_config_extract"]
@@ -305,7 +400,7 @@ class Extractor:
         kw = dict(prefetch_factor=4, persistent_workers=False) if workers > 0 else {}
         return torch.utils.data.DataLoader(
             ds, batch_size=lb, shuffle=False, num_workers=workers, sampler=sampler,
-            collate_fn=lambda b: [x for x in b if x is not None], pin_memory=True, **kw)
+            collate_fn=lambda b: [x for x in b if x is not None], pin_memory=False, **kw)
 
     def _extract_pipelined(self):
         """Images are grouped BY SHAPE across the whole stream (one bucket per
@@ -319,13 +414,19 @@ class Extractor:
         (default 4 groups) wait, the fullest bucket launches early."""
         group = max(1, int(os.environ.get("POSFEAT_EXTRACT_GROUP", "32")))
         hold = max(group, int(os.environ.get("POSFEAT_EXTRACT_HOLD", str(4 * group))))
-        ds = self.extract_loader.dataset
-        u8_before = getattr(ds, "uint8_only", None)
-        try:
-            return self._extract_pipelined_run(group, hold)
-        finally:
-            if u8_before is not None:
-                ds.uint8_only = u8_before
+        return self._extract_pipelined_run(group, hold)
+
+    def _warm_h2d(self):
+        """The pinned staging buffers of ``_launch_group`` (two, alternating),
+        allocated and copied to the device once here, while the model is built."""
+        n = 32 * 480 * 640 * 3   # one bench-size group; buffers grow on demand
+        self._stage, self._stage_next = [], 0
+        for _ in range(2):
+            buf = _staging_buffer(n)
+            torch.empty(n, dtype=torch.uint8, device=self.device).copy_(buf, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            self._stage.append((buf, ev))
 
     def _extract_pipelined_run(self, group, hold):
         writer = ThreadPoolExecutor(1 if self.save_h5 else 4)
@@ -355,7 +456,12 @@ class Extractor:
                 self._finish_group(*pending.popleft(), writer, futures)
 
         held = max_held = 0
-        for batch in self._pipelined_loader():
+        src = self._early_iter if self._early_iter is not None else self._pipelined_loader()
+        self._early_iter = None
+        for nbatch, batch in enumerate(src):
+            if trace and nbatch < 8:
+                print("[extract] loader batch %d (%d items) at %.3f s" % (
+                    nbatch, len(batch), time.perf_counter() - t0), flush=True)
             for it in batch:
                 u8 = it["im1_ori"]
                 item = (u8, u8, it["name1"], None)

@@ -205,13 +205,17 @@ _DEFAULT_WS = DetectWorkspace()
 
 
 def detect(kp_map, nms_radius, num_pts=False, use_nms=True, thr=False, thr_mod="mean",
-           ws=None, sync=True):
+           ws=None, sync=True, each=False):
     """GPU generate_kpts_single core.  kp_map: [b,1,h,w] fp32 on the GPU.
 
     Returns (idx [b,n] int32, coord_n [b,n,2], kp_score [b,n,1], counts [b], n).
     With ``sync=False`` the buffers are full-capacity and ``n`` is a device
-    scalar tensor (no host synchronisation).
+    scalar tensor (no host synchronisation).  ``each=True`` (needs
+    ``sync=False``): every image is selected as if detected alone and ``n`` is
+    a device tensor [b] (posfeat_detect_each).
     """
+    if each and sync:
+        raise ValueError("each=True returns per-image counts on the device: use sync=False")
     _f32(kp_map, "kp_map")
     b, c, h, w = kp_map.shape
     if c != 1:
@@ -231,6 +235,14 @@ def detect(kp_map, nms_radius, num_pts=False, use_nms=True, thr=False, thr_mod="
     idx = torch.empty(b, cap, dtype=torch.int32, device=dev)
     coord = torch.empty(b, cap, 2, dtype=torch.float32, device=dev)
     score = torch.empty(b, cap, 1, dtype=torch.float32, device=dev)
+    if each:
+        meta = torch.empty(2 * b, dtype=torch.int32, device=dev)  # [n_sel..., counts...]
+        wsb = (ws or _DEFAULT_WS).get(b, h, w, cap, dev)
+        check(lib().posfeat_detect_each(
+            ptr(kp_map), b, h, w, int(nms_radius), 1 if use_nms else 0, mode, tval,
+            int(num_pts) if num_pts else 0, cap, ptr(idx), ptr(coord), ptr(score), ptr(meta),
+            ctypes.c_void_p(meta.data_ptr() + 4 * b), ptr(wsb), wsb.numel(), stream_ptr()))
+        return idx, coord, score, meta[b:], meta[:b]
     meta = torch.empty(b + 1, dtype=torch.int32, device=dev)  # [n_sel, counts...]
     wsb = (ws or _DEFAULT_WS).get(b, h, w, cap, dev)
     check(lib().posfeat_detect(ptr(kp_map), b, h, w, int(nms_radius), 1 if use_nms else 0, mode,
@@ -255,14 +267,23 @@ def nms_mask(score, radius):
     return m.bool()
 
 
-def sample_desc_nhwc(fmap_nhwc, coord_n, c=None, normalize=True, n_valid=None):
-    """Bilinear (align_corners=False, zeros) sampling of an NHWC map at coord_n [b,n,2]."""
+def sample_desc_nhwc(fmap_nhwc, coord_n, c=None, normalize=True, n_valid=None, each=False):
+    """Bilinear (align_corners=False, zeros) sampling of an NHWC map at coord_n [b,n,2].
+    ``n_valid``: device int32, one count for the batch, or ``each=True`` one per
+    image ([b], posfeat_sample_desc_each); rows past the count are zeros."""
     _f32(fmap_nhwc, "fmap")
     coord_n = _f32(coord_n.contiguous(), "coord_n")
     b, h, w, cs = fmap_nhwc.shape
     c = cs if c is None else c
     npts = coord_n.shape[1]
     out = torch.empty(b, npts, c, device=fmap_nhwc.device, dtype=torch.float32)
+    if each:
+        if n_valid is None or n_valid.numel() != b or n_valid.dtype != torch.int32:
+            raise ValueError("each=True needs n_valid: int32 [b] on the device")
+        check(lib().posfeat_sample_desc_each(ptr(fmap_nhwc), b, c, h, w, cs, ptr(coord_n), npts,
+                                             ptr(n_valid), 1 if normalize else 0, ptr(out),
+                                             stream_ptr()))
+        return out
     check(lib().posfeat_sample_desc(ptr(fmap_nhwc), b, c, h, w, cs, ptr(coord_n), npts,
                                     ptr(n_valid), 1 if normalize else 0, ptr(out), stream_ptr()))
     return out

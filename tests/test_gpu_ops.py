@@ -275,6 +275,42 @@ def test_detector_batch_min_count(gpu):
     np.testing.assert_allclose(coord.cpu().numpy(), c_ref, atol=1e-5)
 
 
+def test_detector_each_equals_per_image(gpu):
+    """posfeat_detect_each on a batch == the oracle run on every image alone
+    (the reference extraction loop, batch 1): per-image n, idx, score, coord;
+    and posfeat_sample_desc_each == the batch-1 sampler row for row, zeros
+    past each image's n."""
+    from posfeat_amd import ops
+    from oracle import detect_ref
+    # survivor counts differ per image (thresholds bite differently), one
+    # image below the 128 raise
+    km = np.stack([np.random.RandomState(s).rand(1, 120, 160).astype(np.float32)
+                   for s in (5, 6, 7, 8)])
+    km[1] *= 0.5
+    km[3, 0, :, 40:] = 0.0
+    for r, n, thr in ((1, 4000, 0.9), (2, 600, False), (3, 5000, 0.97)):
+        idx, coord, score, counts, nsel = ops.detect(torch.from_numpy(km).to(gpu), r, n, thr=thr,
+                                                     thr_mod="abs", sync=False, each=True)
+        nsel = nsel.cpu().numpy()
+        assert len(set(nsel.tolist())) > 1 or r == 2
+        fmap = torch.randn(4, 30, 40, 128, device=gpu)
+        desc = ops.sample_desc_nhwc(fmap, coord, c=128, n_valid=torch.from_numpy(nsel).to(gpu),
+                                    each=True).cpu()
+        for i in range(4):
+            c_ref, s_ref, i_ref = detect_ref.generate_kpts_single(km[i:i + 1], r, n, thr=thr,
+                                                                  thr_mod="abs", return_idx=True)
+            k = int(nsel[i])
+            assert k == i_ref.shape[1]
+            np.testing.assert_array_equal(idx[i, :k].cpu().numpy(), i_ref[0])
+            np.testing.assert_array_equal(score[i, :k].cpu().numpy(), s_ref[0])
+            np.testing.assert_allclose(coord[i, :k].cpu().numpy(), c_ref[0], atol=1e-5)
+            one = ops.sample_desc_nhwc(fmap[i:i + 1].contiguous(), coord[i:i + 1, :k]).cpu()
+            # rows of zero-score fill in an all-zero region have NaN coords (0/0
+            # soft-argmax, as the reference): NaN == NaN here
+            np.testing.assert_array_equal(desc[i, :k].numpy(), one[0].numpy())
+            assert torch.all(desc[i, k:] == 0)
+
+
 def test_detector_many_ties_at_cut(gpu):
     """> 1024 exactly-equal scores straddling the top-k cut (fallback path) and
     the masked-zero fill path (n raised to 128)."""

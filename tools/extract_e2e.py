@@ -20,7 +20,11 @@ the same process times the kernel path (engine + detector + sampler on
 device-resident batches of the pipeline's group size, no I/O, as bench.py's
 step) so the line carries ``steady / kernel_path``.
 
-usage: python tools/extract_e2e.py [--seqs 96] [--sizes 480x640|mixed] [--timing] [--passes 1]
+``kernel_path_replay_images_per_s`` replays the run's own group composition
+(shapes and counts) on the kernel path, the denominator for mixed sizes.
+
+usage: python tools/extract_e2e.py [--seqs 96] [--sizes 480x640|mixed|hpatches] [--timing]
+                                   [--passes 1] [--no-write]
 """
 import argparse
 import json
@@ -37,6 +41,19 @@ sys.path.insert(0, ROOT)
 
 # (h, w) of HPatches-like images (the dataset crops to multiples of 16)
 SIZES = [(480, 640), (600, 800), (752, 1000)]
+
+
+def hpatches_sizes(nseq, seed=7):
+    """A distinct size per sequence, as the real HPatches release has (each
+    sequence its own camera / crop; datasets/hpatches.py:35-38 crops every
+    image to multiples of 16): h in [480, 880], w in [640, 1200], seeded."""
+    rs = np.random.RandomState(seed)
+    out = []
+    while len(out) < nseq:
+        s = (16 * rs.randint(30, 56), 16 * rs.randint(40, 76))
+        if s not in out:
+            out.append(s)
+    return out
 
 
 def make_dataset(root, nseq, sizes):
@@ -92,16 +109,53 @@ def kernel_path_rate(eng, ex, hw, group, steps=5):
     return steps * group / (time.perf_counter() - t)
 
 
+def kernel_path_replay(eng, ex, groups):
+    """The kernel path over this run's own group composition: every group
+    (shape, image count) the pipelined loop launched, in order, engine +
+    detect_each + sample_each on device-resident seeded images, timed after
+    one untimed replay (every shape planned).  Inputs are built before the
+    timed region."""
+    import torch
+    from posfeat_amd import ops
+    from posfeat_amd.weights import seeded_image
+    cfg = ex.config["detector_config"]
+    ins = [torch.from_numpy(np.stack([seeded_image(i, h, w) for i in range(k)])).cuda()
+           for (h, w, _), k in groups]
+
+    def replay():
+        for imgs in ins:
+            out = eng.run(imgs, outputs=())
+            _, coord, _, _, n_dev = ops.detect(out["local_point"], cfg["nms_radius"],
+                                               cfg["num_pts"], thr=cfg["thr"],
+                                               thr_mod=cfg["thr_mod"], sync=False, each=True)
+            ops.sample_desc_nhwc(out["_local_map_nhwc"], coord, c=128, n_valid=n_dev, each=True)
+    replay()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    replay()
+    torch.cuda.synchronize()
+    return sum(k for _, k in groups) / (time.perf_counter() - t)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seqs", type=int, default=96)
-    ap.add_argument("--sizes", default="480x640", help="HxW or 'mixed'")
+    ap.add_argument("--sizes", default="480x640",
+                    help="HxW, 'mixed' (three sizes cycled) or 'hpatches' (a distinct size per "
+                         "sequence)")
     ap.add_argument("--timing", action="store_true", help="per-stage (synchronising) timing")
     ap.add_argument("--passes", type=int, default=1, help="2: a second (warm) pass")
+    ap.add_argument("--no-write", action="store_true",
+                    help="output_desc: False (no npz files): the run without its file output")
     args = ap.parse_args()
     if args.timing:
         os.environ["POSFEAT_EXTRACT_TIMING"] = "1"
-    sizes = SIZES if args.sizes == "mixed" else [tuple(int(v) for v in args.sizes.split("x"))]
+    if args.sizes == "mixed":
+        sizes = SIZES
+    elif args.sizes == "hpatches":
+        sizes = hpatches_sizes(args.seqs)
+    else:
+        sizes = [tuple(int(v) for v in args.sizes.split("x"))]
     tmp = tempfile.mkdtemp(prefix="posfeat_e2e_")
     t = time.perf_counter()
     make_dataset(tmp, args.seqs, sizes)
@@ -110,6 +164,8 @@ def main():
     make_checkpoint(tmp)
     cfg = yaml.safe_load(open(os.path.join(ROOT, "configs", "extract_hpatches.yaml")))
     cfg["data_config_extract"]["data_path"] = os.path.join(tmp, "data", "hpatches-sequences-release")
+    if args.no_write:
+        cfg["output_desc"] = False
     os.chdir(tmp)
     from posfeat_amd.managers.extractor import Extractor
     res = {}
@@ -134,18 +190,30 @@ def main():
         st["setup_s"] = setup
         eng = ex.model._engine
         st["kernel_path_images_per_s"] = kernel_path_rate(eng, ex, sizes[0], st.get("group", 32))
+        if marks:
+            counts = [k for _, k in marks[1:]] + [st["images"]]
+            groups = [(shp, c - k) for shp, (_, k), c in zip(ex.group_shapes, marks, counts)]
+            st["kernel_path_replay_images_per_s"] = kernel_path_replay(eng, ex, groups)
+            st["whole_over_replay"] = st["images_per_s"] / st["kernel_path_replay_images_per_s"]
         if "steady_images_per_s" in st:
             st["steady_over_kernel_path"] = st["steady_images_per_s"] / st["kernel_path_images_per_s"]
+            if marks:
+                st["steady_over_replay"] = (st["steady_images_per_s"]
+                                            / st["kernel_path_replay_images_per_s"])
         st["engine_shapes"] = len(eng.cached_shapes)
+        st["engine_stats"] = dict(eng.stats)
+        if marks:
+            st["groups"] = [[round(t_, 3), k_, list(shp)] for (t_, k_), shp in
+                            zip(marks, ex.group_shapes)]
         st["engine_workspace_mb"] = eng.workspace_bytes / 2 ** 20
         res[p] = st
         ex.model._engine = None
         files = []
         for dp, _, fs in os.walk(os.path.join(tmp, "ckpts", cfg["output_root"], "desc")):
             files += [os.path.join(dp, f) for f in fs]
-        z = np.load(files[0])
         st["npz_files"] = len(files)
-        st["kpts_first"] = int(z["keypoints"].shape[0])
+        if files:
+            st["kpts_first"] = int(np.load(files[0])["keypoints"].shape[0])
         del ex, eng
         import gc
         import torch

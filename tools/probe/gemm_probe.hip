@@ -432,6 +432,139 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
       }
 }
 
+
+// k16r: three-stage B ring, B DMA two chunks ahead, A in registers D chunks
+// ahead (D buffers), one counted wait (vmcnt = the ops of the previous chunk)
+// + barrier per chunk; 72 KB LDS: two blocks per CU.
+template <int D, int FL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k16r(Args a) {
+  constexpr int RB = 2, NW = 4, BN = 128, NB = BN / 16, BM = NW * RB * 16;
+  constexpr int B_G = 3 * BN / 16 / NW;
+  constexpr int BSTAGE = 3 * BN * BK;  // u16
+  constexpr int NA = 2 * RB;
+  constexpr int NOPS = B_G + NA;
+  __shared__ __attribute__((aligned(16))) unsigned short Bs[3 * BSTAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  int bid = blockIdx.x;
+  {
+    const int nwg = a.nwg, q = nwg >> 3, r = nwg & 7, xcd = bid & 7, slot = bid >> 3;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+  }
+  const long long z = blockIdx.y;
+  const float* A = a.A + z * a.M * a.K;
+  const unsigned short* Bp = a.Bp + z * 3LL * a.N * a.K;
+  float* C = a.C + z * a.M * a.N;
+  const int tm = bid / a.tiles_n, tn = bid - tm * a.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int r16 = lane & 15, kq = lane >> 4;
+  const float* xrow[RB];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb)
+    xrow[rb] = A + (long long)min(m0 + wave * RB * 16 + rb * 16 + r16, a.M - 1) * a.K +
+               ((FL & 8) ? kq * 4 : kq * 8);
+  const unsigned short* bsrc[B_G];
+#pragma unroll
+  for (int i = 0; i < B_G; ++i) {
+    const int pr = (wave * B_G + i) * 16 + (lane >> 2);
+    const int plane = pr / BN, row = pr - plane * BN;
+    const int ks = (lane & 3) ^ ((row >> 2) & 3);
+    bsrc[i] = Bp + (long long)plane * a.N * a.K + (long long)(n0 + row) * a.K + ks * 8;
+  }
+  const int nch = a.K / BK;
+  f32x4 acc[RB][NB];
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) acc[rb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 va[D][RB][2];
+  auto aload = [&](int c, int rb, int jj) -> f32x4 {
+    return *reinterpret_cast<const f32x4*>(xrow[rb] + (long long)min(c, nch - 1) * BK +
+                                           jj * ((FL & 8) ? 16 : 4));
+  };
+  auto bdma = [&](int c, int i, unsigned short* st) {
+    __builtin_amdgcn_global_load_lds(
+        (const __attribute__((address_space(1))) void*)(bsrc[i] + (long long)min(c, nch - 1) * BK),
+        (__attribute__((address_space(3))) void*)(st + (wave * B_G + i) * 16 * BK), 16, 0, 0);
+  };
+  // prologue: B chunks 0, 1 and A chunks 0 .. D-1, in the per-chunk op order
+#pragma unroll
+  for (int c = 0; c < (D > 2 ? D : 2); ++c) {
+    __builtin_amdgcn_sched_barrier(NO_VMEM);
+    if (c < 2)
+#pragma unroll
+      for (int i = 0; i < B_G; ++i) bdma(c, i, Bs + c * BSTAGE);
+    if (c < D)
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) va[c][rb][j] = aload(c, rb, j);
+  }
+  __builtin_amdgcn_sched_barrier(NO_VMEM);
+  for (int i = 0; i < nch; i += 3 * D) {
+#pragma unroll
+    for (int u = 0; u < 3 * D; ++u) {
+      const int ii = i + u;
+      if (ii >= nch) break;
+      __builtin_amdgcn_sched_barrier(NO_VMEM);
+      // chunk ii's B (issued two chunks back) and A (D back) landed: everything
+      // but the previous chunk's ops; LDS reads of this wave done too
+      __builtin_amdgcn_s_waitcnt((NOPS & 15) | (7 << 4) | (0 << 8) | ((NOPS >> 4) << 14));
+      __builtin_amdgcn_s_barrier();
+      const int sr = u % 3, sw = (u + 2) % 3;
+      overlap2(Bs + sw * BSTAGE, Bs + sr * BSTAGE,
+               [&](unsigned short* __restrict__ Bn, const unsigned short* __restrict__ Bb) {
+        u32x4_t ah[RB], am[RB], al[RB];
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) split3(va[u % D][rb][0], va[u % D][rb][1], ah[rb], am[rb], al[rb]);
+        int op = 0;
+        auto mem = [&]() {
+          __builtin_amdgcn_sched_barrier(PIN);
+          if (op < B_G) {
+            bdma(ii + 2, op, Bn);
+          } else if (op < NOPS) {
+            const int j = op - B_G, rb = j >> 1, jj = j & 1;
+            va[u % D][rb][jj] = aload(ii + D, rb, jj);
+          }
+          __builtin_amdgcn_sched_barrier(PIN);
+          ++op;
+        };
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) {
+          const int row = nb * 16 + r16;
+          const int slot = kq ^ ((row >> 2) & 3);
+          const unsigned short* bp = Bb + row * BK + slot * 8;
+          const u32x4_t bh = *reinterpret_cast<const u32x4_t*>(bp);
+          const u32x4_t bm = *reinterpret_cast<const u32x4_t*>(bp + BN * BK);
+          const u32x4_t bl = *reinterpret_cast<const u32x4_t*>(bp + 2 * BN * BK);
+#pragma unroll
+          for (int rb = 0; rb < RB; ++rb) {
+            f32x4 c = acc[rb][nb];
+            c = mfma16(ah[rb], bh, c);
+            c = mfma16(ah[rb], bm, c);
+            c = mfma16(am[rb], bh, c);
+            c = mfma16(ah[rb], bl, c);
+            c = mfma16(al[rb], bh, c);
+            c = mfma16(am[rb], bm, c);
+            acc[rb][nb] = c;
+          }
+          while (op < (nb + 1) * NOPS / NB) mem();
+        }
+        while (op < NOPS) mem();
+      });
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wave * RB * 16 + rb * 16 + kq * 4 + r;
+        if (row < a.M) C[(long long)row * a.N + n0 + nb * 16 + r16] = acc[rb][nb][r];
+      }
+}
+
 template <class K>
 float run(K kern, Args a, int bm, int nb, int reps, int threads = 256) {
   a.tiles_n = a.N / 128;
@@ -487,8 +620,11 @@ int main(int argc, char** argv) {
            fl / ms / 1e9 / 416.7);
   };
   rep("16x16x32 D1", run(k16<1, 0>, a, 128, nb, reps));
+  rep("ring3 D2", run(k16r<2, 0>, a, 128, nb, reps));
+  rep("ring3 D2 contiguous-A", run(k16r<2, 8>, a, 128, nb, reps));
+  rep("ring3 D3", run(k16r<3, 0>, a, 128, nb, reps));
   rep("16x16x32 D1 contiguous-A", run(k16<1, 8>, a, 128, nb, reps));
   rep("16x16x32 D1 again", run(k16<1, 0>, a, 128, nb, reps));
-  rep("16x16x32 D1 contiguous-A again", run(k16<1, 8>, a, 128, nb, reps));
+  rep("ring3 D2 again", run(k16r<2, 0>, a, 128, nb, reps));
   return 0;
 }
