@@ -13,15 +13,20 @@ MI355X-specific behaviour:
   over RCCL (PoSFeat.set_parallel) and ranks extract disjoint image shards;
 * descriptors are sampled from the engine's NHWC local_map (coalesced);
 * no CPU path: without a gfx950 GPU the constructor raises;
-* the default loop is a pipeline (``_extract_pipelined``): consecutive images
-  of the same size are run as one engine batch (up to
-  ``POSFEAT_EXTRACT_GROUP``, default 32; instance norm and eval BatchNorm are
-  per image, so each image's maps are those of a batch-1 run up to fp32
-  summation order), only the uint8 image crosses PCIe (pinned, normalised on
-  the device by posfeat_normalize_rgb8, bit-identical to the host transform),
-  detection / sampling run without host synchronisation, results come back by
-  async D2H copies, and the files are written by a writer thread while the
-  GPU works on the next group.  Same files, same names, same log lines;
+* the default loop is a pipeline (``_extract_pipelined``): images are
+  bucketed by size and a bucket runs as one engine batch when it holds
+  ``POSFEAT_EXTRACT_GROUP`` images (default 32; at most
+  ``POSFEAT_EXTRACT_HOLD`` images wait, default 4 groups; instance norm and
+  eval BatchNorm are per image, so each image's maps are those of a batch-1
+  run up to fp32 summation order); only the uint8 image crosses PCIe (one
+  fork-excluded pinned staging buffer per group, normalised on the device by
+  posfeat_normalize_rgb8, bit-identical to the host transform); one detector
+  and one sampler launch per group select every image as if alone
+  (posfeat_detect_each), without host synchronisation; results come back by
+  async D2H copies, and the files are written by writer threads while the
+  GPU works on the next group.  The decode workers are forked at
+  construction, before the model exists (a later fork stalls the device work
+  that follows it).  Same files, same names, same log lines;
   ``POSFEAT_EXTRACT_PIPELINE=0`` runs the reference's serial loop;
 * ``POSFEAT_EXTRACT_TIMING=1`` (serial loop) synchronises the device at the stage
   boundaries and reports per-stage time (load = decode + normalise in the
