@@ -77,8 +77,13 @@ int posfeat_conv_packed_k(int cin, int kh, int kw); /* returns Kpad */
  * ~2e-8 relative, below an fp32 fmaf's own rounding -- fp32-accurate results
  * (tests/test_gpu_precision.py), not a reduced-precision mode.  2: as 1, with
  * the Winograd / tap GEMM operands split by their producers (A/B only).
- * 3x3 stride-1 convs always run the fp32 halo kernel.  Instances created
- * afterwards plan with the new mode.  mode = -1: query only. */
+ * 3x3 stride-1 convs with Cin % 32 == 0 and weight planes (the extraction
+ * engine's) run the bf16x6 gathered-tap tile in modes >= 1; the fp32 halo
+ * kernel is kept for convs without planes and inside the training
+ * instances' scopes.  Modes >= 1 also switch DiskLoss's flash passes
+ * (posfeat_disk_loss, posfeat_disk_flash_lse) to bf16x6 similarity products.
+ * Instances created afterwards plan with the new mode.  mode = -1: query
+ * only. */
 int posfeat_set_conv_precision(int mode);
 int posfeat_conv2d_nhwc(const posfeat_conv_desc *d, const float *x, const float *w,
                         const float *bias, const float *res, float *y, void *stream);
@@ -92,7 +97,8 @@ int posfeat_conv2d_nhwc_ws(const posfeat_conv_desc *d, const float *x, const flo
                            size_t ws_bytes, void *stream);
 /* Same as posfeat_conv2d_nhwc_ws with the weights ALSO given as their three
  * bf16 planes (h, m, l of the packed [cout][Kpad] array, plane stride wplane
- * elements; h = RNE_bf16(w), m = RNE_bf16(w - h), l = RNE_bf16(w - h - m)),
+ * elements, >= cout * posfeat_conv_packed_k(cin, kh, kw) or POSFEAT_E_INVALID;
+ * h = RNE_bf16(w), m = RNE_bf16(w - h), l = RNE_bf16(w - h - m)),
  * as the engine passes them: the pre-split tiles run (dense 1x1 convs: the
  * 16x16x32 conv_bf6x_kernel; others: conv_bf6d_kernel).  tile: -1 for the
  * default plan, else a tile id the engine's autotuner may pick (ignored where

@@ -2862,7 +2862,10 @@ extern "C" int posfeat_conv2d_nhwc_planes(const posfeat_conv_desc* d, const floa
                                           long long wplane, const float* bias, const float* res,
                                           float* y, void* ws, size_t ws_bytes, int tile,
                                           void* stream) {
-  if (!wb || wplane <= 0) return POSFEAT_E_INVALID;
+  if (!d || !wb || wplane <= 0) return POSFEAT_E_INVALID;
+  // the three planes must not overlap: each holds cout x packed-K bf16 values
+  if (wplane < (long long)d->cout * posfeat_conv_packed_k(d->cin, d->kh, d->kw))
+    return POSFEAT_E_INVALID;
   return pf_conv_run_tile(d, x, w, bias, res, y, ws, ws_bytes, tile, pf_stream(stream), wb,
                           wplane);
 }

@@ -261,15 +261,37 @@ def test_gpu_desc_train_step_vs_oracle(gpu):
     keys = [k for k in params if "stat_" + k in d.files and not k.endswith("conv.bias")]
     grads = torch.autograd.grad([x1, x2], [params[k] for k in keys],
                                 grad_outputs=[g1.double(), g2.double()])
+    # the same backward in fp32 (the reference's own arithmetic): its distance
+    # from fp64 is this step's per-tensor rounding noise
+    sd32 = {k: (v.clone().float() if v.is_floating_point() else v.clone()) for k, v in bb.items()}
+    p32 = {k: sd32[k].requires_grad_(True) for k in keys}
+    y1 = resunet_forward(sd32, im1.float(), train=True)["local_map"]
+    y2 = resunet_forward(sd32, im2.float(), train=True)["local_map"]
+    grads32 = torch.autograd.grad([y1, y2], [p32[k] for k in keys], grad_outputs=[g1, g2])
     got = tr.grad_dict()
     num = den = 0.0
-    for k, gr in zip(keys, grads):
+    bad, errs = [], []
+    for k, gr, g32 in zip(keys, grads, grads32):
         ref = gr.numpy()
         gk = np.asarray(got[k], np.float64).reshape(ref.shape)
-        err = np.abs(gk - ref).max()
-        assert err <= 3e-2 * max(np.abs(ref).max(), 1e-12), (k, err, np.abs(ref).max())
+        scale = max(np.abs(ref).max(), 1e-12)
+        e = np.abs(gk - ref).max() / scale
+        # per tensor: 3x the reference arithmetic's own fp32 error on this step
+        # (as _check_grads64 does with the fixture's noise_*), not a flat
+        # fraction of the max.  Floor 2e-2 (_check_grads64: 1e-2): here the
+        # upstream gradient differs too -- the GPU takes the loss gradient on
+        # its own fp32 maps, the oracle on the fp64 network's (r11q: worst
+        # 1.27e-2 on layer3.2.bn2.bias, whose fp32 noise is 3e-3)
+        noise = np.abs(g32.detach().double().numpy() - ref).max() / scale
+        tol = max(3.0 * noise, 2e-2)
+        errs.append((float(e), float(tol), k))
+        if e > tol:
+            bad.append((k, round(float(e), 6), round(tol, 6)))
         num += float(((gk - ref) ** 2).sum())
         den += float((ref ** 2).sum())
+    print("largest relative errors (err, tol):",
+          [(k, "%.2e" % e, "%.2e" % t) for e, t, k in sorted(errs)[-6:]])
+    assert not bad, "tensors over tolerance (key, err, tol): %s" % bad
     assert np.sqrt(num / den) <= 5e-3, np.sqrt(num / den)
     tr.adam_step()
     torch.cuda.synchronize()

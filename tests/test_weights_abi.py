@@ -99,6 +99,16 @@ def test_abi_host_only_calls():
                       y_cstride=8, res_cstride=0, act=0)
     assert L.posfeat_conv2d_nhwc(ctypes.byref(d), ctypes.c_void_p(16), ctypes.c_void_p(16), None,
                                  None, ctypes.c_void_p(16), None) == -1
+    # weight planes that would overlap (plane stride < cout x packed K) are
+    # rejected before any device work
+    d = _lib.ConvDesc(n=1, h=8, w=8, cin=64, x_cstride=64, cout=64, kh=1, kw=1, stride=1, pad=0,
+                      y_cstride=64, res_cstride=0, act=0)
+    kpad = L.posfeat_conv_packed_k(64, 1, 1)
+    p = ctypes.c_void_p(256)
+    assert L.posfeat_conv2d_nhwc_planes(ctypes.byref(d), p, p, p, 64 * kpad - 1, None, None, p,
+                                        None, 0, -1, None) == -1
+    assert L.posfeat_conv2d_nhwc_planes(ctypes.byref(d), p, p, p, 0, None, None, p, None, 0, -1,
+                                        None) == -1
 
 
 def test_engine_layer_table_matches_state_dicts():
