@@ -97,6 +97,15 @@ __device__ __forceinline__ f32x16 g6_mfma(const g6_u32x4& a, const g6_u32x4& b, 
 // channels from `base` (= map + image offset + channel offset); sh, sw =
 // (h-1)/(2h-1), (w-1)/(2w-1).  Shared by the upsample kernel and the Winograd
 // input transform that reads the low-res map directly: the same arithmetic.
+// XCD-aware bijective block remap: the hardware deals consecutive
+// workgroups round-robin over the 8 XCDs (XCD = bid & 7); XCD x gets the
+// contiguous logical range [x q + min(x, r), ...) of the nwg blocks, so
+// blocks that read the same data (e.g. one image's points) share one XCD's L2
+__device__ __forceinline__ long long pf_xcd_block(long long bid, long long nwg) {
+  const long long q = nwg >> 3, r = nwg & 7, xcd = bid & 7, slot = bid >> 3;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+}
+
 __device__ __forceinline__ f32x4 pf_up2ac_at(const float* base, int h, int w, int cs, float sh,
                                              float sw, int oy, int ox) {
 #pragma clang fp contract(off)  // one fixed mul/add sequence wherever it is inlined

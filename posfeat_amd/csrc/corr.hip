@@ -259,6 +259,47 @@ __device__ __forceinline__ float2 bilinear128(const float* __restrict__ fm, int 
   return r;
 }
 
+// bilinear128's sample (same corner weights and per-channel sums), for this
+// lane's 8 channels cl*8 .. cl*8+7 (16 lanes per sample, 16-B loads), dotted
+// with the query's same 8 channels: the 16-lane group then sums the partials
+template <bool BORDER>
+__device__ __forceinline__ float bilinear_dot8(const float* __restrict__ fm, int h, int w, float gx,
+                                               float gy, int cl, const f32x4& qa, const f32x4& qb) {
+  float ix = ((gx + 1.f) * w - 1.f) / 2.f;
+  float iy = ((gy + 1.f) * h - 1.f) / 2.f;
+  if (BORDER) {
+    ix = fminf(fmaxf(ix, 0.f), (float)(w - 1));
+    iy = fminf(fmaxf(iy, 0.f), (float)(h - 1));
+  }
+  const float fx = floorf(ix), fy = floorf(iy);
+  const int x0 = (int)fx, y0 = (int)fy, x1 = x0 + 1, y1 = y0 + 1;
+  const bool bx0 = (unsigned)x0 < (unsigned)w, bx1 = (unsigned)x1 < (unsigned)w;
+  const bool by0 = (unsigned)y0 < (unsigned)h, by1 = (unsigned)y1 < (unsigned)h;
+  const int cx0 = min(max(x0, 0), w - 1), cx1 = min(max(x1, 0), w - 1);
+  const int cy0 = min(max(y0, 0), h - 1), cy1 = min(max(y1, 0), h - 1);
+  const float* p00 = fm + ((long long)cy0 * w + cx0) * 128 + cl * 8;
+  const float* p01 = fm + ((long long)cy0 * w + cx1) * 128 + cl * 8;
+  const float* p10 = fm + ((long long)cy1 * w + cx0) * 128 + cl * 8;
+  const float* p11 = fm + ((long long)cy1 * w + cx1) * 128 + cl * 8;
+  const f32x4 a00 = *reinterpret_cast<const f32x4*>(p00), b00 = *reinterpret_cast<const f32x4*>(p00 + 4);
+  const f32x4 a01 = *reinterpret_cast<const f32x4*>(p01), b01 = *reinterpret_cast<const f32x4*>(p01 + 4);
+  const f32x4 a10 = *reinterpret_cast<const f32x4*>(p10), b10 = *reinterpret_cast<const f32x4*>(p10 + 4);
+  const f32x4 a11 = *reinterpret_cast<const f32x4*>(p11), b11 = *reinterpret_cast<const f32x4*>(p11 + 4);
+  const float w00 = (by0 && bx0) ? ((float)x1 - ix) * ((float)y1 - iy) : 0.f;
+  const float w01 = (by0 && bx1) ? (ix - (float)x0) * ((float)y1 - iy) : 0.f;
+  const float w10 = (by1 && bx0) ? ((float)x1 - ix) * (iy - (float)y0) : 0.f;
+  const float w11 = (by1 && bx1) ? (ix - (float)x0) * (iy - (float)y0) : 0.f;
+  f32x4 ra = a00 * w00, rb = b00 * w00;
+  ra += a01 * w01;
+  rb += b01 * w01;
+  ra += a10 * w10;
+  rb += b10 * w10;
+  ra += a11 * w11;
+  rb += b11 * w11;
+  return qa.x * ra.x + qa.y * ra.y + qa.z * ra.z + qa.w * ra.w + qb.x * rb.x + qb.y * rb.y +
+         qb.z * rb.z + qb.w * rb.w;
+}
+
 constexpr int MAX_LINE = 128;   // line_step <= 128 (2 logits per lane)
 constexpr int MAX_WIN = 512;    // window taps <= 512 (8 logits per lane)
 
@@ -281,6 +322,8 @@ __device__ __forceinline__ float lin_w(float f, int p) {
 // Window logits over the patch (shared by the forward and the backward):
 // fills ax (fx per ix, fy per iy), pc (q . fm per patch pixel, 0 outside the
 // map) and the tap logits wl[r] of taps lane + 64 r (-inf past nw).
+constexpr int WP_K = 8;  // patch pixels per 16-lane group per pass (round 3: 4)
+
 struct WinPatch {
   int px0, py0, PW, PH;
 };
@@ -304,12 +347,12 @@ __device__ __forceinline__ WinPatch window_patch_logits(const float* __restrict_
   const int np = P.PW * P.PH;
   const f32x4 qa = *reinterpret_cast<const f32x4*>(qp + cl * 8);
   const f32x4 qb = *reinterpret_cast<const f32x4*>(qp + cl * 8 + 4);
-  // 16 pixels per pass, branch-free (a pixel outside the map or past the
-  // patch reads a clamped address and yields 0), so their loads overlap
-  for (int base = 0; base < np; base += 16) {
-    float v[4];
+  // WP_K * 4 pixels per pass, branch-free (a pixel outside the map or past
+  // the patch reads a clamped address and yields 0), so their loads overlap
+  for (int base = 0; base < np; base += 4 * WP_K) {
+    float v[WP_K];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < WP_K; ++k) {
       const int pp = base + 4 * k + grp;
       const int py = P.py0 + pp / P.PW, px = P.px0 + pp % P.PW;
       const bool in = pp < np && (unsigned)py < (unsigned)h2 && (unsigned)px < (unsigned)w2;
@@ -322,7 +365,7 @@ __device__ __forceinline__ WinPatch window_patch_logits(const float* __restrict_
       v[k] = in ? d : 0.f;
     }
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < WP_K; ++k) {
 #pragma unroll
       for (int o = 8; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o, 64);
       const int pp = base + 4 * k + grp;
@@ -360,8 +403,12 @@ __global__ void line_window_kernel(const float* __restrict__ cpx,   // [b][n][2]
                                    float* __restrict__ w_std, int use_patch) {
   __shared__ float s_pc[4][WB_PATCH];
   __shared__ float s_ax[4][WB_AXES];
+  __shared__ float s_lg[4][MAX_LINE];
   const int lane = threadIdx.x & 63;
-  const long long wid = blockIdx.x * (long long)(blockDim.x >> 6) + (threadIdx.x >> 6);
+  // one image's points on one XCD: a line sweeps its whole map (4 corners x
+  // 512 B per sample, ~200 KB per point), so the L2 working set is one map,
+  // not all b (the kernel streams ~2 GB of corner reads per launch)
+  const long long wid = pf_xcd_block(blockIdx.x, gridDim.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (wid >= (long long)nb * n) return;
   const int b = (int)(wid / n);
   const float* F = Fm + b * 9;
@@ -400,32 +447,38 @@ __global__ void line_window_kernel(const float* __restrict__ cpx,   // [b][n][2]
   const float e1x = (px[first] - c0) / c0, e1y = (py[first] - c1) / c1;
   const float e2x = (px[second] - c0) / c0, e2y = (py[second] - c1) / c1;
   const float dx = e2x - e1x, dy = e2y - e1y;
-  // ---- line samples: logits (lane s holds logit s and s+64)
-  // LS samples per pass (by hand: the wave sums are convergent, so the
-  // compiler will not unroll a loop of unknown trip count around them): their
-  // corner loads are in flight together
-  constexpr int LS = 4;  // (8 measured slower: 281 vs 253 us, register pressure)
-  float lg[2] = {-INFINITY, -INFINITY};
-  for (int s0 = 0; s0 < line_step; s0 += LS) {
-    float d[LS];
+  // ---- line samples: logits (lane s holds logit s and s+64).  16 lanes per
+  // sample (8 channels each, 16-B corner loads), 4 samples per wave and LU per
+  // group in one pass, so 4 * LU samples' corner loads are in flight together;
+  // the logits go through LDS to their lanes.  (Round 3: 64 lanes per sample,
+  // 4-B loads, 4 samples per pass.)
+  constexpr int LU = 2;
+  const int grp = lane >> 4, cl = lane & 15;
+  const f32x4 qa = *reinterpret_cast<const f32x4*>(f1 + wid * 128 + cl * 8);
+  const f32x4 qb = *reinterpret_cast<const f32x4*>(f1 + wid * 128 + cl * 8 + 4);
+  float* slg = s_lg[threadIdx.x >> 6];
+  for (int s0 = 0; s0 < line_step; s0 += 4 * LU) {
+    float d[LU];
 #pragma unroll
-    for (int k = 0; k < LS; ++k) {
-      const int s = min(s0 + k, line_step - 1);
+    for (int u = 0; u < LU; ++u) {
+      const int s = min(s0 + grp + 4 * u, line_step - 1);
       const float t = linspace_f(0.f, 1.f, line_step, s);
       const float gx = __fadd_rn(__fmul_rn(dx, t), e1x), gy = __fadd_rn(__fmul_rn(dy, t), e1y);
-      const float2 v = bilinear128<true>(fmb, h2, w2, gx, gy, lane);
-      d[k] = q0 * v.x + q1 * v.y;
+      d[u] = bilinear_dot8<true>(fmb, h2, w2, gx, gy, cl, qa, qb);
     }
 #pragma unroll
-    for (int k = 0; k < LS; ++k) {
-      const float t = pf_wave_sum(d[k]);
-      const int s = s0 + k;
-      if (s < line_step) {
-        if (s == lane) lg[0] = t;
-        if (s == lane + 64) lg[1] = t;
-      }
+    for (int u = 0; u < LU; ++u) {
+      float v = d[u];
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      const int s = s0 + grp + 4 * u;
+      if (cl == 0 && s < line_step) slg[s] = v;
     }
   }
+  wave_lds_sync();
+  float lg[2];
+  lg[0] = lane < line_step ? slg[lane] : -INFINITY;
+  lg[1] = lane + 64 < line_step ? slg[lane + 64] : -INFINITY;
   float mx = fmaxf(lg[0], lg[1]);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
@@ -810,7 +863,7 @@ __global__ __launch_bounds__(256) void window_bwd_patch_kernel(
   __shared__ float s_ax[4][WB_AXES];   // fx per ix, then fy per iy
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int grp = lane >> 4, cl = lane & 15;
-  const long long wid = blockIdx.x * 4LL + wv;
+  const long long wid = pf_xcd_block(blockIdx.x, gridDim.x) * 4LL + wv;  // see line_window_kernel
   if (wid >= (long long)nb * n) return;
   const float gx0 = gE[wid * 2], gy0 = gE[wid * 2 + 1];
   if (gx0 == 0.f && gy0 == 0.f) {  // masked point: no gradient
