@@ -765,7 +765,12 @@ def corr_main(args, world, rank, dev, emit=True):
                          "peak": arith["method_peak"], "unit": "TFLOP/s",
                          "frac": round(ach / arith["method_peak"], 4), "traffic": None,
                          "arithmetic": arith["arithmetic"],
-                         "avg_launch_ms": round(kms, 4), "flop_per_launch": kfl},
+                         "avg_launch_ms": round(kms, 4), "flop_per_launch": kfl,
+                         "timed": "one posfeat_disk_flash_lse call: two flash_split launches "
+                                  "(~9 us each, the bf16 planes of both sides) + the LSE "
+                                  "kernel + flash_lse_final (~5 us); rocprof's per-kernel "
+                                  "time for disk_flash6_kernel<false,false> excludes the "
+                                  "three small launches (DESIGN 4.1q)"},
         }
         if emit:
             print(json.dumps(rec), flush=True)
