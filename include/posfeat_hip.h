@@ -85,6 +85,10 @@ int posfeat_conv_packed_k(int cin, int kh, int kw); /* returns Kpad */
  * Instances created afterwards plan with the new mode.  mode = -1: query
  * only. */
 int posfeat_set_conv_precision(int mode);
+/* 1 when this library is the A/B build (`make ab`, libposfeat_hip_ab.so),
+ * which reads the POSFEAT_* environment switches that select the non-default
+ * paths kept for A/B tests; 0 for the shipped library, which ignores them. */
+int posfeat_ab_build(void);
 int posfeat_conv2d_nhwc(const posfeat_conv_desc *d, const float *x, const float *w,
                         const float *bias, const float *res, float *y, void *stream);
 /* Same, allowed to split K over workgroups (deterministic: fp32 partial slabs

@@ -398,7 +398,7 @@ void plan(posfeat_bbtrain* m) {
   }
   alloc(m->wt, fl(wt));
   {
-    const char* e = getenv("POSFEAT_BF6B");
+    const char* e = pf_ab_getenv("POSFEAT_BF6B");
     m->wsplit = pf_conv_precision() == 1 && !(e && e[0] == '0') && T.params % 4 == 0;
   }
   if (m->wsplit) {
@@ -409,11 +409,11 @@ void plan(posfeat_bbtrain* m) {
   alloc(m->wgws, wg);
   alloc(m->splitk, std::max<size_t>(sk, 256));
   {
-    const char* e = getenv("POSFEAT_WINO");
+    const char* e = pf_ab_getenv("POSFEAT_WINO");
     m->wino = !(e && e[0] == '0');
   }
   {
-    const char* e = getenv("POSFEAT_S2PHASE");
+    const char* e = pf_ab_getenv("POSFEAT_S2PHASE");
     m->s2phase = !(e && e[0] == '0');
   }
   m->bf6p = pf_bf6p_on();  // fixed for the handle: the U buffer size depends on it
@@ -436,7 +436,7 @@ void plan(posfeat_bbtrain* m) {
 // executed transform-domain MACs x2 of a Winograd layer: F(4x4) 36 per 4x4
 // tile, F(2x2) 16 per 2x2 tile (what the MFMA units run, for the rooflines)
 double wino_flops(int n, int h, int w, int cin, int cout, bool wgrad = false) {
-  const char* e = getenv("POSFEAT_WINO");
+  const char* e = pf_ab_getenv("POSFEAT_WINO");
   const bool f4 = h % 4 == 0 && w % 4 == 0 && (wgrad || !(e && e[0] == '1'));
   const double T = f4 ? (double)n * (h / 4) * (w / 4) : (double)n * (h / 2) * (w / 2);
   return 2.0 * T * (f4 ? 36 : 16) * cin * cout;

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/posfeat_hip.h"
 
@@ -97,6 +98,25 @@ __device__ __forceinline__ f32x16 g6_mfma(const g6_u32x4& a, const g6_u32x4& b, 
 // channels from `base` (= map + image offset + channel offset); sh, sw =
 // (h-1)/(2h-1), (w-1)/(2w-1).  Shared by the upsample kernel and the Winograd
 // input transform that reads the low-res map directly: the same arithmetic.
+// A/B switches.  The paths that lost their A/B (bf6d / bf6b dense tiles for
+// extraction, precision mode 2, the unfused head, the Winograd / phase forms
+// of head.conv2, the dense DiskLoss, ...) are selected by POSFEAT_* variables
+// that only the A/B build reads (`make ab` -> libposfeat_hip_ab.so, built with
+// -DPOSFEAT_AB=1); the shipped library ignores them and always runs the
+// default paths.  Operational variables (POSFEAT_AUTOTUNE, _AUTOTUNE_LOG,
+// _CONV_TILE: a legal tile forced for the tile tests) use getenv directly.
+#ifndef POSFEAT_AB
+#define POSFEAT_AB 0
+#endif
+inline const char* pf_ab_getenv(const char* name) {
+#if POSFEAT_AB
+  return getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
+
 // XCD-aware bijective block remap: the hardware deals consecutive
 // workgroups round-robin over the 8 XCDs (XCD = bid & 7); XCD x gets the
 // contiguous logical range [x q + min(x, r), ...) of the nwg blocks, so

@@ -30,7 +30,7 @@
 static int g_conv_precision = -1;
 int pf_conv_precision() {
   if (g_conv_precision < 0) {
-    const char* e = getenv("POSFEAT_BF6");
+    const char* e = pf_ab_getenv("POSFEAT_BF6");
     g_conv_precision = e ? (e[0] == '0' ? 0 : e[0] == '2' ? 2 : 1) : 1;
   }
   return g_conv_precision;
@@ -2291,7 +2291,7 @@ thread_local int tl_halo_fp32 = 0;
 thread_local int tl_dense32 = 0;  // PfDense32Scope
 bool halo_bf6_on() {
   static const bool off = [] {
-    const char* e = getenv("POSFEAT_BF6_HALO");
+    const char* e = pf_ab_getenv("POSFEAT_BF6_HALO");
     return e && e[0] == '0';
   }();
   return bf6_on() && !off && tl_halo_fp32 == 0;
@@ -2308,7 +2308,7 @@ bool halo_bf6_on() {
 // bit-identical (test_gpu_bf6r.py)
 int bf6d_depth() {
   static const int d = [] {
-    const char* e = getenv("POSFEAT_BF6D");
+    const char* e = pf_ab_getenv("POSFEAT_BF6D");
     const int v = e ? atoi(e) : 2;
     return v >= 2 && v <= 4 ? v : 0;
   }();
@@ -2327,7 +2327,7 @@ int bf6d_depth() {
 // and the extraction model stay within the fp32 bounds (test_gpu_bf6x.py).
 bool bf6x_on() {
   static const bool off = [] {
-    const char* e = getenv("POSFEAT_BF6X");
+    const char* e = pf_ab_getenv("POSFEAT_BF6X");
     return e && e[0] == '0';
   }();
   return bf6_on() && !off && tl_halo_fp32 == 0 && tl_dense32 == 0;
@@ -2362,8 +2362,8 @@ struct Plan {
 struct ConvEnv {
   int kmax = KERN_HALO, tile = -1, maxsplit = 4;
   ConvEnv() {
-    if (const char* e = getenv("POSFEAT_CONV_MAXSPLIT")) maxsplit = atoi(e);
-    if (const char* e = getenv("POSFEAT_CONV_KERNEL")) {
+    if (const char* e = pf_ab_getenv("POSFEAT_CONV_MAXSPLIT")) maxsplit = atoi(e);
+    if (const char* e = pf_ab_getenv("POSFEAT_CONV_KERNEL")) {
       if (e[0] == 's') kmax = KERN_STAGED;
       else if (e[0] == 'g') kmax = KERN_GLDS;
     }
@@ -2567,7 +2567,7 @@ Plan conv_plan(const ConvArgs& a, bool allow_split, int forced = -1) {
 // conv share the arithmetic, so the autotuner's choice never changes results.
 bool stem_bf6_on() {
   static const bool off = [] {
-    const char* e = getenv("POSFEAT_BF6_STEM");
+    const char* e = pf_ab_getenv("POSFEAT_BF6_STEM");
     return e && e[0] == '0';
   }();
   return bf6_on() && !off && tl_halo_fp32 == 0;
@@ -3187,13 +3187,13 @@ int pf_gemm_batched(const float* A, int lda, long long sa, const float* B, long 
   // column tiles instead of two 128-wide ones, the second of them half empty
   // POSFEAT_GEMM_B256=1 (A/B): the 8-wave 256x128 pre-split tiles
   static const bool b256 = [] {
-    const char* e = getenv("POSFEAT_GEMM_B256");
+    const char* e = pf_ab_getenv("POSFEAT_GEMM_B256");
     return e && e[0] == '1';
   }();
   const bool x = Bb && bf6x_on();
   // POSFEAT_BF6X_RB4=1 (A/B): the 256-row 16x16x32 tiles for the batched GEMMs
   static const bool rb4 = [] {
-    const char* e = getenv("POSFEAT_BF6X_RB4");
+    const char* e = pf_ab_getenv("POSFEAT_BF6X_RB4");
     return e && e[0] == '1';
   }();
   const int want = x ? (N % 128 == 0 ? (rb4 ? TILE_BF6X_256x128 : TILE_BF6X_128x128)

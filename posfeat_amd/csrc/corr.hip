@@ -1068,7 +1068,7 @@ __global__ __launch_bounds__(256) void window_gather_kernel(
 // the patch kernel's LDS bounds (patch <= (win + 4)^2, see above)
 // POSFEAT_WINPATCH=0: the per-tap kernels (A/B runs)
 bool window_patch_on() {
-  const char* e = getenv("POSFEAT_WINPATCH");
+  const char* e = pf_ab_getenv("POSFEAT_WINPATCH");
   return !(e && e[0] == '0');
 }
 

@@ -1013,7 +1013,7 @@ void launch_flash(dim3 grid, hipStream_t st, const FlashArgs& fa, int want_r) {
 }
 
 bool use_flash() {
-  const char* e = getenv("POSFEAT_DISK_FLASH");
+  const char* e = pf_ab_getenv("POSFEAT_DISK_FLASH");
   return !(e && e[0] == '0');
 }
 

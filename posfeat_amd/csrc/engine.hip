@@ -298,7 +298,7 @@ double desc_m(const posfeat_conv_desc& d) {
 }
 bool tile_lookup(const posfeat_conv_desc& d, bool res, bool wplanes, int* tile) {
   static const bool similar = [] {
-    const char* e = getenv("POSFEAT_TUNE_SIMILAR");
+    const char* e = pf_ab_getenv("POSFEAT_TUNE_SIMILAR");
     return !(e && e[0] == '0');
   }();
   const std::string cls = desc_class(d, res, wplanes);
@@ -427,7 +427,7 @@ const int kWinoDiv[16] = {8, 8, 4, 4, 4, 4, 4, 4, 8, 8, 8, 16, 16, 16, 16, 16};
 // (its K = 64 GEMMs are too short for the transform round trip to pay)
 unsigned wino_enc_mask() {
   static const unsigned mask = [] {
-    const char* e = getenv("POSFEAT_WINO_ENC");
+    const char* e = pf_ab_getenv("POSFEAT_WINO_ENC");
     if (!e) return 6u;
     if (e[0] == '1' && e[1] == 0) return 7u;
     unsigned m = 0;
@@ -459,7 +459,7 @@ long long wino_u_offset(const std::string& name, bool planes) {
 // xup: the full-res buffer for the unfused forms
 bool up2fuse_on() {
   static const bool on = [] {
-    const char* e = getenv("POSFEAT_UP2FUSE");
+    const char* e = pf_ab_getenv("POSFEAT_UP2FUSE");
     return !(e && e[0] == '0');
   }();
   return on;
@@ -470,7 +470,7 @@ int conv3x3(Ctx& c, const std::string& name, const float* x, int n, int h, int w
   posfeat_model* m = c.m;
   const long long uo = wino_u_offset(name, m->bf6p || m->wsplit);
   const bool f4ok = m->wino && uo >= 0 && h % 4 == 0 && w % 4 == 0 &&
-                    !(getenv("POSFEAT_WINO") && getenv("POSFEAT_WINO")[0] == '1');
+                    !(pf_ab_getenv("POSFEAT_WINO") && pf_ab_getenv("POSFEAT_WINO")[0] == '1');
   if (up2 && !(f4ok && up2fuse_on())) {  // materialise the upsample, then the plain conv
     PF_TRY(timed(c, "upsample2x", 0, [&] {
       return pf_upsample2x_ac(x, n, h / 2, w / 2, xcs, xcs, xup, xcs, c.st);
@@ -488,7 +488,7 @@ int conv3x3(Ctx& c, const std::string& name, const float* x, int n, int h, int w
                                            m->bf6p || m->wsplit);
                }));
   // executed transform-domain MACs: F(4x4) 36 per 4x4 tile, F(2x2) 16 per 2x2 tile
-  const bool f4 = h % 4 == 0 && w % 4 == 0 && !(getenv("POSFEAT_WINO") && getenv("POSFEAT_WINO")[0] == '1');
+  const bool f4 = h % 4 == 0 && w % 4 == 0 && !(pf_ab_getenv("POSFEAT_WINO") && pf_ab_getenv("POSFEAT_WINO")[0] == '1');
   const double T = f4 ? (double)n * (h / 4) * (w / 4) : (double)n * (h / 2) * (w / 2);
   // three launches, timed apart: the input transform, the batched GEMMs
   // (the MFMA work), the output transform (+ bias, activation)
@@ -616,28 +616,28 @@ void plan(posfeat_model* m) {
   alloc(m->d2, B * h4 * w4 * 256);
   alloc(m->c1raw, B * h4 * w4 * 192);
   {
-    const char* e = getenv("POSFEAT_HEAD_UP4");  // 0: materialise the x4 upsample (A/B only)
+    const char* e = pf_ab_getenv("POSFEAT_HEAD_UP4");  // 0: materialise the x4 upsample (A/B only)
     m->up4 = !(e && e[0] == '0');
     const char* t = getenv("POSFEAT_AUTOTUNE");  // 0: heuristic tiles only
     m->autotune = !(t && t[0] == '0');
-    const char* wv = getenv("POSFEAT_WINO");  // 0: direct conv for the decoder 3x3 layers
+    const char* wv = pf_ab_getenv("POSFEAT_WINO");  // 0: direct conv for the decoder 3x3 layers
     m->wino = !(wv && wv[0] == '0');
-    const char* gv = getenv("POSFEAT_GFUSE");  // 0: conv2's G part as the 64-ch 3x3 conv
+    const char* gv = pf_ab_getenv("POSFEAT_GFUSE");  // 0: conv2's G part as the 64-ch 3x3 conv
     m->gfuse = !(gv && gv[0] == '0');
-    const char* uv = getenv("POSFEAT_UP4WINO");  // 0: conv_up4_kernel (bilinear phases)
+    const char* uv = pf_ab_getenv("POSFEAT_UP4WINO");  // 0: conv_up4_kernel (bilinear phases)
     m->up4wino = !(uv && uv[0] == '0') && H % 16 == 0 && W % 16 == 0;
-    const char* tv = getenv("POSFEAT_UP4TAP");  // 0: the low-res Winograd / phase forms
+    const char* tv = pf_ab_getenv("POSFEAT_UP4TAP");  // 0: the low-res Winograd / phase forms
     m->up4tap = !(tv && tv[0] == '0') && H % 16 == 0 && W % 16 == 0;
-    const char* iv = getenv("POSFEAT_IMGSTATS");  // 0: convimg conv + fused statistics
+    const char* iv = pf_ab_getenv("POSFEAT_IMGSTATS");  // 0: convimg conv + fused statistics
     m->imgstats = !(iv && iv[0] == '0');
-    const char* tt = getenv("POSFEAT_TRAINTAP");  // 0: training on the materialised conv2 input
+    const char* tt = pf_ab_getenv("POSFEAT_TRAINTAP");  // 0: training on the materialised conv2 input
     m->traintap = m->train && !(tt && tt[0] == '0') && m->up4 && m->gfuse && m->up4tap;
   }
   if (m->up4 && m->gfuse) {
     alloc(m->gf_w, B * 128 * 128);
     alloc(m->gf_b, B * 128 + 9 * 64 * 128);  // + the transposed W2 G slice (gfuse.hip)
     alloc(m->gf_wp, pf_gfuse_wplanes_bytes((int)B) / 4 + 4);  // pre-split K = 80 weights
-    const char* e = getenv("POSFEAT_HEADFUSE");
+    const char* e = pf_ab_getenv("POSFEAT_HEADFUSE");
     m->hfuse = !(e && e[0] == '0') && m->up4tap && pf_conv_precision() >= 1;
     if (m->hfuse) alloc(m->gring, pf_gfuse_ring_floats((int)B, (int)H, (int)W));
   }
@@ -646,7 +646,7 @@ void plan(posfeat_model* m) {
   if (m->imgstats) alloc(m->imws, pf_gfuse_imgstats_ws_bytes((int)B, (int)H) / 4 + 4);
   m->bf6p = pf_bf6p_on();  // fixed for the instance: buffer sizes depend on it
   {
-    const char* e = getenv("POSFEAT_BF6B");
+    const char* e = pf_ab_getenv("POSFEAT_BF6B");
     m->wsplit = pf_conv_precision() == 1 && !(e && e[0] == '0') && specs().total % 4 == 0;
   }
   if (m->wsplit) alloc(m->wpl, (size_t)specs().total * 3 / 2 + 4);
@@ -664,9 +664,9 @@ void plan(posfeat_model* m) {
   }
   if (m->train && !m->traintap) m->up4 = false;  // the backward reads the materialised conv2 input
   {
-    const char* e = getenv("POSFEAT_SIDE");
+    const char* e = pf_ab_getenv("POSFEAT_SIDE");
     m->side = !(e && e[0] == '0') && m->up4 && m->gfuse && (!m->train || m->traintap);
-    const char* a = getenv("POSFEAT_SIDE_AT");
+    const char* a = pf_ab_getenv("POSFEAT_SIDE_AT");
     m->side_at = a ? std::min(3, std::max(0, atoi(a))) : 2;
   }
   if (m->up4) {
@@ -1494,3 +1494,7 @@ extern "C" int posfeat_device_ok(void) {
   if (hipGetDeviceProperties(&p, dev) != hipSuccess) return 0;
   return strncmp(p.gcnArchName, "gfx950", 6) == 0 ? 1 : 0;
 }
+
+// 1 in the A/B build (make ab: the POSFEAT_* path switches are read), 0 in
+// the shipped library (common.h pf_ab_getenv)
+extern "C" int posfeat_ab_build(void) { return POSFEAT_AB ? 1 : 0; }

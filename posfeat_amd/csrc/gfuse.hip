@@ -669,7 +669,7 @@ __global__ __launch_bounds__(512) void gfuse_conv5_k80_kernel(const float* __res
 
 bool gfuse_k80_on() {
   static const bool on = [] {
-    const char* e = getenv("POSFEAT_GFUSE_K80");
+    const char* e = pf_ab_getenv("POSFEAT_GFUSE_K80");
     return !(e && e[0] == '0');
   }();
   return on;
@@ -719,7 +719,7 @@ int pf_gfuse_conv(const float* img4, const float* c, int ccs, int n, int H, int 
     // CUs to the main stream; tiles are independent, so the count never
     // changes results
     static const int tot_blocks = [] {
-      const char* e = getenv("POSFEAT_GFUSE_BLOCKS");
+      const char* e = pf_ab_getenv("POSFEAT_GFUSE_BLOCKS");
       // r3w sweep (B = 8): 512 820, 96 830, 64 841, 48 841, 32 837 img/s;
       // r6w (B = 32, bf6d main stream, two pairs): 32 977.1, 64 971.4, 128
       // 970.2 -- but at 32 the longer side stream lands on iconv3's GEMM

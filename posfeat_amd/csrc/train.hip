@@ -441,7 +441,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_bf6_kernel(WgradArgs a) {
 
 bool wgrad_bf6_on() {
   static const bool off = [] {
-    const char* e = getenv("POSFEAT_WGRAD_BF6");
+    const char* e = pf_ab_getenv("POSFEAT_WGRAD_BF6");
     return e && e[0] == '0';
   }();
   return pf_conv_precision() >= 1 && !off;
@@ -1088,7 +1088,7 @@ WgPlan wgrad_plan(int n, int H, int W, int Cin, int Cout, int KH, int KW, int st
 // the 9 taps (keypoint head: image-branch A 3.2 -> 5.1 ms, conv1 2.2 -> 3.0)
 bool wgrad_bf6_all() {
   static const bool on = [] {
-    const char* e = getenv("POSFEAT_WGRAD_BF6_ALL");
+    const char* e = pf_ab_getenv("POSFEAT_WGRAD_BF6_ALL");
     return e && e[0] == '1';
   }();
   return on;

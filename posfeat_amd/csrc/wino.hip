@@ -644,7 +644,7 @@ namespace {
 // unless POSFEAT_WINO=1 (F(2x2) only)
 bool use_f4(int h, int w) {
   static const bool f2only = [] {
-    const char* e = getenv("POSFEAT_WINO");
+    const char* e = pf_ab_getenv("POSFEAT_WINO");
     return e && e[0] == '1';
   }();
   return !f2only && h % 4 == 0 && w % 4 == 0;

@@ -23,3 +23,31 @@ def gpu():
 
 
 GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+# The A/B build (posfeat_amd/csrc: make ab): the shipped library ignores the
+# POSFEAT_* switches that select the non-default paths; tests that compare the
+# default path with one of them run against this library -- in a child
+# process (ab_env) or, for in-process tests, when the session itself loaded it
+# (POSFEAT_HIP_LIB=posfeat_amd/libposfeat_hip_ab.so; the `ab` fixture).
+AB_LIB = os.path.join(ROOT, "posfeat_amd", "libposfeat_hip_ab.so")
+
+
+def ab_loaded():
+    from posfeat_amd import _lib
+    return _lib.lib().posfeat_ab_build() == 1
+
+
+def ab_env():
+    """Environment entries that make a child process load the A/B build."""
+    if not os.path.exists(AB_LIB):
+        pytest.skip("A/B build missing (make -C posfeat_amd/csrc ab)")
+    return {"POSFEAT_HIP_LIB": AB_LIB}
+
+
+@pytest.fixture
+def ab(gpu):
+    """In-process A/B tests: the session must have loaded the A/B build."""
+    if not ab_loaded():
+        pytest.skip("A/B path switch: run with POSFEAT_HIP_LIB=posfeat_amd/libposfeat_hip_ab.so "
+                    "(the shipped library ignores the switch)")
+    return gpu

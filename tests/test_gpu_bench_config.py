@@ -20,10 +20,14 @@
   test_gpu_correlation.py.)
 """
 import os
+import subprocess
+import sys
 
 import numpy as np
 import pytest
 import torch
+
+from conftest import ROOT
 
 pytestmark = pytest.mark.gpu
 
@@ -41,6 +45,45 @@ def _new_engine(dev):
     from posfeat_amd.weights import seeded_state_dicts
     bb, hd = seeded_state_dicts(0)
     return ExtractionEngine(bb, hd, device=dev)
+
+
+# A/B comparisons run in a child process on the A/B build (the shipped
+# library ignores the path switches): the default path and the switched one,
+# each on a fresh engine instance (the switches are read when an instance is
+# planned), same inputs
+AB_CHILD = r"""
+import os, sys, numpy as np, torch
+sys.path.insert(0, %(root)r)
+from posfeat_amd.engine import ExtractionEngine
+from posfeat_amd.weights import seeded_state_dicts, seeded_image
+from posfeat_amd import _lib
+assert _lib.lib().posfeat_ab_build() == 1
+bb, hd = seeded_state_dicts(0)
+imgs = torch.from_numpy(np.stack([seeded_image(s, %(h)d, %(w)d) for s in %(seeds)r])).cuda()
+out = {}
+for tag, env in (("ref", {}), ("alt", %(env)r)):
+    os.environ.update(env)
+    eng = ExtractionEngine(bb, hd, device="cuda:0")
+    eng.run(imgs)
+    r = eng.run(imgs)
+    for k in ("local_point", "local_map", "global_feat"):
+        out[tag + "_" + k] = r[k].cpu().numpy()
+    eng.close()
+np.savez(%(out)r, **out)
+"""
+
+
+def _ab_pair(tmp_path, env, H, W, seeds):
+    """(default, switched) outputs from one child process on the A/B build."""
+    from conftest import ab_env
+    out = str(tmp_path / "ab_pair.npz")
+    code = AB_CHILD % dict(root=ROOT, h=H, w=W, seeds=tuple(seeds), env=env, out=out)
+    subprocess.run([sys.executable, "-c", code], env=dict(os.environ, **ab_env()), check=True,
+                   timeout=240)
+    d = np.load(out)
+    keys = ("local_point", "local_map", "global_feat")
+    return ({k: torch.from_numpy(d["ref_" + k]) for k in keys},
+            {k: torch.from_numpy(d["alt_" + k]) for k in keys})
 
 
 def _oracle(img_cpu):
@@ -147,31 +190,21 @@ def test_aachen_shapes_vs_oracle(gpu, hw):
 @pytest.mark.parametrize("switch,exact", [("POSFEAT_SIDE", True), ("POSFEAT_UP4WINO", False),
                                           ("POSFEAT_UP4TAP", False), ("POSFEAT_IMGSTATS", False),
                                           ("POSFEAT_DISK_FLASH", True)])
-def test_env_switch_paths_match_default(gpu, switch, exact, monkeypatch):
-    from posfeat_amd.weights import seeded_image
-    imgs = torch.from_numpy(np.stack([seeded_image(s, 96, 128) for s in (4, 5)])).to(gpu)
-    base = _new_engine(gpu)
-    base.run(imgs)
-    ref = base.run(imgs)
-    ref = {k: v.clone() for k, v in ref.items() if not k.startswith("_")}
-    monkeypatch.setenv(switch, "0")
+def test_env_switch_paths_match_default(gpu, switch, exact, tmp_path):
+    env = {switch: "0"}
     if switch == "POSFEAT_UP4WINO":
-        monkeypatch.setenv("POSFEAT_UP4TAP", "0")   # the phase kernel sits behind both
-    alt = _new_engine(gpu)        # the switch is read when the instance is planned
-    alt.run(imgs)
-    got = alt.run(imgs)
+        env["POSFEAT_UP4TAP"] = "0"   # the phase kernel sits behind both
+    ref, got = _ab_pair(tmp_path, env, 96, 128, (4, 5))
     for k in ("local_point", "local_map", "global_feat"):
         if exact:
             assert torch.equal(got[k], ref[k]), "%s=0 changed %s" % (switch, k)
         else:
             e, s = _maxerr(got[k], ref[k])
             assert e <= TOL * s, "%s=0: %s err %g" % (switch, k, e)
-    base.close()
-    alt.close()
 
 
 @pytest.mark.parametrize("B,hw", [(2, (96, 128)), (2, (112, 144)), (1, (112, 144))])
-def test_fused_head_matches_unfused(gpu, B, hw, monkeypatch):
+def test_fused_head_matches_unfused(gpu, B, hw, tmp_path):
     """POSFEAT_HEADFUSE: head.conv2's G part inside the tap combine
     (up4tap_gcombine_kernel, the default) against the G pass + combine
     (gfuse_conv5_k80_kernel + up4tap_combine_kernel): the same products, so
@@ -179,24 +212,24 @@ def test_fused_head_matches_unfused(gpu, B, hw, monkeypatch):
     block (W = 144: 16 of the block's 32 columns), the border ring and both
     block orders (the XCD remap applies when the grid is a multiple of 8:
     B = 2 here; B = 1 at 112 x 144 is 140 blocks)."""
-    from posfeat_amd.weights import seeded_image
     H, W = hw
-    imgs = torch.from_numpy(np.stack([seeded_image(s, H, W) for s in range(3, 3 + B)])).to(gpu)
+    seeds = tuple(range(3, 3 + B))
+    ab_ref, got = _ab_pair(tmp_path, {"POSFEAT_HEADFUSE": "0"}, H, W, seeds)
+    e, s = _maxerr(got["local_point"], ab_ref["local_point"])
+    assert e <= TOL * s, "HEADFUSE=0: local_point err %g" % e
+    assert torch.equal(got["local_map"], ab_ref["local_map"])   # the backbone is untouched
+    # the shipped library's fused head (this process) against the A/B build's
+    # default path and the oracle
+    from posfeat_amd.weights import seeded_image
+    imgs = torch.from_numpy(np.stack([seeded_image(s, H, W) for s in seeds])).to(gpu)
     base = _new_engine(gpu)
     base.run(imgs)
     ref = {k: v.clone() for k, v in base.run(imgs).items() if not k.startswith("_")}
-    monkeypatch.setenv("POSFEAT_HEADFUSE", "0")
-    alt = _new_engine(gpu)
-    alt.run(imgs)
-    got = alt.run(imgs)
-    e, s = _maxerr(got["local_point"], ref["local_point"])
-    assert e <= TOL * s, "HEADFUSE=0: local_point err %g" % e
-    assert torch.equal(got["local_map"], ref["local_map"])   # the backbone is untouched
+    base.close()
+    assert torch.equal(ref["local_point"].cpu(), ab_ref["local_point"])
     o = _oracle(imgs[:1].cpu())
     e, s = _maxerr(ref["local_point"][:1], o["local_point"])
     assert e <= TOL * s, "fused head vs oracle err %g" % e
-    base.close()
-    alt.close()
 
 
 def test_engine_shape_cache_lru_and_shared_workspace(gpu, monkeypatch):

@@ -12,6 +12,8 @@ import subprocess
 import sys
 
 import numpy as np
+
+from conftest import ab_env
 import pytest
 
 pytestmark = pytest.mark.gpu
@@ -35,7 +37,7 @@ np.savez(%(out)r, lp=r["local_point"].cpu().numpy(), lm=r["local_map"].cpu().num
 
 def _run(tmp_path, env_extra, tag):
     out = str(tmp_path / ("%s.npz" % tag))
-    env = dict(os.environ, **env_extra)
+    env = dict(os.environ, **ab_env(), **env_extra)   # the switches need the A/B build
     subprocess.run([sys.executable, "-c", CODE % {"root": ROOT, "out": out}], env=env,
                    check=True, timeout=240)
     return np.load(out)

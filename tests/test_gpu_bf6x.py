@@ -15,6 +15,8 @@ import subprocess
 import sys
 
 import numpy as np
+
+from conftest import ab_env
 import pytest
 import torch
 
@@ -110,7 +112,7 @@ def test_bf6x_engine_vs_bf6d(tmp_path):
     accumulation grouping -- within 1e-5 of each map's scale, and not
     bit-identical (the 16x16x32 path really ran)."""
     res = {}
-    for tag, env in (("x", {}), ("d", {"POSFEAT_BF6X": "0"})):
+    for tag, env in (("x", ab_env()), ("d", dict(ab_env(), POSFEAT_BF6X="0"))):
         out = str(tmp_path / ("%s.npz" % tag))
         subprocess.run([sys.executable, "-c", CODE % {"root": ROOT, "out": out}],
                        env=dict(os.environ, **env), check=True, timeout=240)
@@ -130,7 +132,8 @@ def test_bf6x_rb4_bit_identical(tmp_path):
     sequence per output element as the 128-row ones: bit-identical engine
     outputs (they are autotune candidates of each other)."""
     res = {}
-    for tag, env in (("r2", {}), ("r4", {"POSFEAT_BF6X_RB4": "1", "POSFEAT_CONV_TILE": "31"})):
+    for tag, env in (("r2", ab_env()),
+                     ("r4", dict(ab_env(), POSFEAT_BF6X_RB4="1", POSFEAT_CONV_TILE="31"))):
         out = str(tmp_path / ("%s.npz" % tag))
         subprocess.run([sys.executable, "-c", CODE % {"root": ROOT, "out": out}],
                        env=dict(os.environ, **env), check=True, timeout=240)

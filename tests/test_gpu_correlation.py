@@ -204,7 +204,8 @@ def test_disk_loss_sampling_path(gpu):
 
 
 @pytest.mark.parametrize("tag", ["s", "f"])
-def test_disk_flash_matches_dense_path(gpu, tag, monkeypatch):
+def test_disk_flash_matches_dense_path(ab, tag, monkeypatch):
+    gpu = ab
     """The flash DiskLoss (S recomputed by MFMA in four passes, never stored)
     against the S-materialising path (POSFEAT_DISK_FLASH=0) on the same draws:
     loss, components and the score-map gradients (KeypointTrainStep.loss_and_grad)."""

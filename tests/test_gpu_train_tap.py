@@ -19,6 +19,8 @@ then sit ~1e-2 from the CPU oracle, whose backbone maps differ more.  The
 end-to-end step is pinned at the fixture sizes by tests/test_train_kp.py.)
 """
 import numpy as np
+
+from conftest import ab_loaded
 import pytest
 import torch
 
@@ -143,9 +145,13 @@ def _compare(got, ref, what, rel, floor=None):
 def test_traintap_backward(gpu, monkeypatch, shape):
     b, H, W = shape
     imgs, dlp = _imgs(b, H, W, 700 + H), _dlp(b, H, W, 7 + W)
-    lp_old, g_old, x = _gpu_grads(gpu, monkeypatch, "0", imgs, dlp)
-    lp_tap, g_tap, _ = _gpu_grads(gpu, monkeypatch, "1", imgs, dlp)
-    np.testing.assert_allclose(lp_tap, lp_old, rtol=1e-4, atol=1e-5)
+    # the materialised-input path (POSFEAT_TRAINTAP=0) exists in the A/B build
+    # only; the shipped library's path is checked against fp64 either way
+    ab = ab_loaded()
+    lp_tap, g_tap, x = _gpu_grads(gpu, monkeypatch, "1", imgs, dlp)
+    if ab:
+        lp_old, g_old, _ = _gpu_grads(gpu, monkeypatch, "0", imgs, dlp)
+        np.testing.assert_allclose(lp_tap, lp_old, rtol=1e-4, atol=1e-5)
     g_or = _oracle_grads(imgs, dlp, x)
     # Bound against fp64: 2e-3 of each tensor's scale (the golden test's), or
     # 3x the fp64-measured rounding spread of this input (_rounding_spread:
@@ -155,9 +161,10 @@ def test_traintap_backward(gpu, monkeypatch, shape):
     # tap-vs-old at 1e-3 is the tight check of the factorisation.
     floor = _rounding_spread(imgs, dlp, x, seed=H * W)
     print("fp64 rounding spread: " + " ".join("%s %.3e" % (k, floor[k]) for k in KEYS))
-    bad = _compare(g_tap, g_old, "tap-vs-old", 1e-3)
-    bad += _compare(g_tap, g_or, "tap-vs-ref64", 2e-3, floor)
-    bad += ["old:" + k for k in _compare(g_old, g_or, "old-vs-ref64", 2e-3, floor)]
+    bad = _compare(g_tap, g_or, "tap-vs-ref64", 2e-3, floor)
+    if ab:
+        bad += _compare(g_tap, g_old, "tap-vs-old", 1e-3)
+        bad += ["old:" + k for k in _compare(g_old, g_or, "old-vs-ref64", 2e-3, floor)]
     assert not bad, bad
 
 
