@@ -372,6 +372,13 @@ int posfeat_model_conv_spec(int i, const char **name, int *cout, int *cin, int *
                             long long *w_off, long long *b_off);
 long long posfeat_model_weight_floats(void);
 int posfeat_model_create(int batch, int h, int w, const float *weights, posfeat_model **out);
+/* An extraction instance (posfeat_model_create) builds its derived weights --
+ * the blob's bf16 planes and the decoder's Winograd-domain weights -- once,
+ * in device memory of its own (allocated at create), by the first forward
+ * that needs them.  A caller that rewrites the weight blob in place calls
+ * this before the next forward (training instances rebuild them every
+ * forward and ignore it). */
+int posfeat_model_weights_changed(posfeat_model *m);
 size_t posfeat_model_workspace(const posfeat_model *m);
 int posfeat_model_extract(posfeat_model *m, const float *img_nchw, posfeat_extract_out *out,
                           void *ws, size_t ws_bytes, void *stream);

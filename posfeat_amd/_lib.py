@@ -70,6 +70,7 @@ SIGNATURES = {
                                c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                c_size_t, c_void_p]),
     "posfeat_ab_build": (c_int, []),
+    "posfeat_model_weights_changed": (c_int, [c_void_p]),
     "posfeat_detect_each": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_float,
                                     c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                     c_void_p, c_size_t, c_void_p]),

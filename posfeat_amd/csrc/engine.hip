@@ -20,6 +20,7 @@
 #include <cmath>
 #include <map>
 #include <mutex>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -92,6 +93,7 @@ const SpecTable& specs() {
 
 struct Buf {
   size_t off = 0, floats = 0;
+  bool persist = false;  // in the instance's own memory (posfeat_model::pbase), not the workspace
 };
 
 }  // namespace
@@ -166,6 +168,18 @@ struct posfeat_model {
   // forward of this shape (results do not depend on the tile)
   std::map<std::string, int> tuned;
   bool autotune = true;
+  // derived weights (the blob's bf16 planes, the decoder's Winograd U) of an
+  // extraction instance live in its own device memory and are built once:
+  // by the first forward that needs them, again after
+  // posfeat_model_weights_changed (training instances rebuild them every
+  // forward: their weights move every step)
+  bool wcache = false;
+  char* pbase = nullptr;
+  size_t p_bytes = 0;
+  bool wpl_done = false;
+  std::set<std::string> wino_done;
+  hipEvent_t ev_wprep = nullptr;  // recorded after the last derived-weight build
+  bool wprep_pending = false;     // built this forward: record ev_wprep at its end
   // timing
   bool timing = false;
   struct Ev {
@@ -185,8 +199,9 @@ struct Ctx {
   hipStream_t st;
   bool dry = false;  // planning pass: record scratch needs, launch nothing
   bool side = false;  // running on the model's side stream (own scratch)
-  float* f(const Buf& b) const { return reinterpret_cast<float*>(ws + b.off); }
-  double* d(const Buf& b) const { return reinterpret_cast<double*>(ws + b.off); }
+  char* base(const Buf& b) const { return (b.persist ? m->pbase : ws) + b.off; }
+  float* f(const Buf& b) const { return reinterpret_cast<float*>(base(b)); }
+  double* d(const Buf& b) const { return reinterpret_cast<double*>(base(b)); }
   const float* W(const std::string& n) const { return m->wts + specs().find(n)->w_off; }
   // the bf16 planes of blob weights w (posfeat_model::wsplit), else nothing
   void wplanes_of(const float* w, const unsigned short** wb, long long* wplane) const;
@@ -198,7 +213,7 @@ void Ctx::wplanes_of(const float* w, const unsigned short** wb, long long* wplan
   *wplane = 0;
   const long long total = specs().total;
   if (!m->wsplit || w < m->wts || w >= m->wts + total) return;
-  *wb = reinterpret_cast<const unsigned short*>(ws + m->wpl.off) + (w - m->wts);
+  *wb = reinterpret_cast<const unsigned short*>(base(m->wpl)) + (w - m->wts);
   *wplane = total;
 }
 
@@ -482,11 +497,17 @@ int conv3x3(Ctx& c, const std::string& name, const float* x, int n, int h, int w
   const Spec* s = specs().find(name);
   if (c.dry) return POSFEAT_OK;
   float* U = c.f(m->wino_u) + uo;
-  PF_TRY(timed(c, "wino:weights", 0,
-               [&] {
-                 return pf_wino_weights_hw(c.W(name), s->cout, s->cin, h, w, U, c.st,
-                                           m->bf6p || m->wsplit);
-               }));
+  if (!(m->wcache && m->wino_done.count(name))) {
+    PF_TRY(timed(c, "wino:weights", 0,
+                 [&] {
+                   return pf_wino_weights_hw(c.W(name), s->cout, s->cin, h, w, U, c.st,
+                                             m->bf6p || m->wsplit);
+                 }));
+    if (!c.dry && m->wcache) {
+      m->wino_done.insert(name);
+      m->wprep_pending = true;
+    }
+  }
   // executed transform-domain MACs: F(4x4) 36 per 4x4 tile, F(2x2) 16 per 2x2 tile
   const bool f4 = h % 4 == 0 && w % 4 == 0 && !(pf_ab_getenv("POSFEAT_WINO") && pf_ab_getenv("POSFEAT_WINO")[0] == '1');
   const double T = f4 ? (double)n * (h / 4) * (w / 4) : (double)n * (h / 2) * (w / 2);
@@ -589,11 +610,20 @@ posfeat_conv_desc dl_desc(const posfeat_model* m) {
 }
 
 void plan(posfeat_model* m) {
-  size_t cur = 0;
+  size_t cur = 0, pcur = 0;
   auto alloc = [&](Buf& b, size_t floats, size_t elem = 4) {
     b.off = cur;
     b.floats = floats;
+    b.persist = false;
     cur += pf_align(floats * elem, 256);
+  };
+  // derived weights: the instance's own memory when they are cached
+  auto palloc = [&](Buf& b, size_t floats) {
+    if (!m->wcache) return alloc(b, floats);
+    b.off = pcur;
+    b.floats = floats;
+    b.persist = true;
+    pcur += pf_align(floats * 4, 256);
   };
   const size_t B = m->B, H = m->H, W = m->W;
   const size_t h2 = H / 2, w2 = W / 2, h4 = H / 4, w4 = W / 4, h8 = H / 8, w8 = W / 8,
@@ -649,7 +679,7 @@ void plan(posfeat_model* m) {
     const char* e = pf_ab_getenv("POSFEAT_BF6B");
     m->wsplit = pf_conv_precision() == 1 && !(e && e[0] == '0') && specs().total % 4 == 0;
   }
-  if (m->wsplit) alloc(m->wpl, (size_t)specs().total * 3 / 2 + 4);
+  if (m->wsplit) palloc(m->wpl, (size_t)specs().total * 3 / 2 + 4);
   if (m->wino) {
     size_t uf = 0, wb = 0;
     const int nl = wino_enc_on() ? 16 : 5;
@@ -659,7 +689,7 @@ void plan(posfeat_model* m) {
       wb = std::max(wb, pf_wino_ws_bytes((int)B, (int)H / kWinoDiv[i], (int)W / kWinoDiv[i],
                                          s->cin, s->cout));
     }
-    alloc(m->wino_u, uf);
+    palloc(m->wino_u, uf);
     alloc(m->wino_ws, wb / 4 + 4);
   }
   if (m->train && !m->traintap) m->up4 = false;  // the backward reads the materialised conv2 input
@@ -741,6 +771,7 @@ void plan(posfeat_model* m) {
   alloc(m->splitk, m->splitk_need / 4 + 4);
   if (m->side) alloc(m->splitk2, std::max(m->splitk_need, part) / 4 + 4);
   m->ws_bytes = cur;
+  m->p_bytes = pcur;
 }
 
 // torchvision Bottleneck at (n, h, w): in -> out (out may be a concat slice)
@@ -899,11 +930,13 @@ int forward(Ctx& c, const float* img, posfeat_extract_out* out, int mode, const 
   float* img4 = c.f(m->img4);
   float* headcat = c.f(m->headcat);
   // ---- ResUNet (DescNet.py:64-84) -----------------------------------------
-  if (m->wsplit)  // the weight blob's bf16 planes for the pre-split bf16x6 tiles
+  if (m->wsplit && !(m->wcache && m->wpl_done)) {  // the blob's bf16 planes (pre-split tiles)
     PF_TRY(timed(c, "weights.split", 0, [&] {
       return pf_split3_rows(m->wts, specs().total / 4, 4, 4,
                             reinterpret_cast<unsigned short*>(c.f(m->wpl)), c.st);
     }));
+    if (!c.dry && m->wcache) m->wpl_done = m->wprep_pending = true;
+  }
   PF_TRY(timed(c, "layout:img", 0, [&] { return pf_nchw_to_nhwc(img, B, 3, H, W, 4, img4, c.st); }));
   // the first forward of a shape autotunes every main-stream conv by timing
   // it: run it serially so the side stream's kernels do not contend with
@@ -1369,8 +1402,40 @@ extern "C" int posfeat_model_create(int batch, int h, int w, const float* weight
   m->H = h;
   m->W = w;
   m->wts = weights;
+  m->wcache = true;
   plan(m);
+  if (m->p_bytes && (hipMalloc(reinterpret_cast<void**>(&m->pbase), m->p_bytes) != hipSuccess ||
+                     hipEventCreateWithFlags(&m->ev_wprep, hipEventDisableTiming) != hipSuccess)) {
+    posfeat_model_destroy(m);
+    return POSFEAT_E_HIP;
+  }
   *out = m;
+  return POSFEAT_OK;
+}
+
+// a forward that built derived weights records where they are complete; a
+// later forward (maybe on another stream) orders itself after that point
+static int wprep_begin(posfeat_model* m, hipStream_t st) {
+  if (m->wcache && m->ev_wprep && (m->wpl_done || !m->wino_done.empty()))
+    if (hipStreamWaitEvent(st, m->ev_wprep, 0) != hipSuccess) return POSFEAT_E_HIP;
+  return POSFEAT_OK;
+}
+static int wprep_end(posfeat_model* m, hipStream_t st, int r) {
+  if (m->wprep_pending) {
+    m->wprep_pending = false;
+    if (r == POSFEAT_OK && hipEventRecord(m->ev_wprep, st) != hipSuccess) return POSFEAT_E_HIP;
+    if (r != POSFEAT_OK) {  // a failed forward: build them again next time
+      m->wpl_done = false;
+      m->wino_done.clear();
+    }
+  }
+  return r;
+}
+
+extern "C" int posfeat_model_weights_changed(posfeat_model* m) {
+  if (!m) return POSFEAT_E_INVALID;
+  m->wpl_done = false;
+  m->wino_done.clear();
   return POSFEAT_OK;
 }
 
@@ -1384,7 +1449,8 @@ extern "C" int posfeat_model_extract(posfeat_model* m, const float* img_nchw,
   if (reinterpret_cast<uintptr_t>(ws) & 255) return POSFEAT_E_INVALID;
   Ctx c{m, static_cast<char*>(ws), pf_stream(stream)};
   m->ev_used = 0;
-  const int r = forward(c, img_nchw, out);
+  PF_TRY(wprep_begin(m, c.st));
+  const int r = wprep_end(m, c.st, forward(c, img_nchw, out));
   if (r == POSFEAT_OK) m->tuned_modes |= 1u << MODE_FULL;
   return r;
 }
@@ -1398,7 +1464,8 @@ extern "C" int posfeat_model_backbone(posfeat_model* m, const float* img_nchw,
   if (reinterpret_cast<uintptr_t>(ws) & 255) return POSFEAT_E_INVALID;
   Ctx c{m, static_cast<char*>(ws), pf_stream(stream)};
   m->ev_used = 0;
-  const int r = forward(c, img_nchw, out, MODE_BACKBONE);
+  PF_TRY(wprep_begin(m, c.st));
+  const int r = wprep_end(m, c.st, forward(c, img_nchw, out, MODE_BACKBONE));
   if (r == POSFEAT_OK) m->tuned_modes |= 1u << MODE_BACKBONE;
   return r;
 }
@@ -1414,7 +1481,8 @@ extern "C" int posfeat_model_keypointdet(posfeat_model* m, const float* x_nchw,
   m->ev_used = 0;
   posfeat_extract_out o{};
   o.local_point = local_point;
-  const int r = forward(c, img_nchw, &o, MODE_HEAD, x_nchw);
+  PF_TRY(wprep_begin(m, c.st));
+  const int r = wprep_end(m, c.st, forward(c, img_nchw, &o, MODE_HEAD, x_nchw));
   if (r == POSFEAT_OK) m->tuned_modes |= 1u << MODE_HEAD;
   return r;
 }
@@ -1469,6 +1537,8 @@ extern "C" void posfeat_model_destroy(posfeat_model* m) {
   if (m->ev_fork) (void)hipEventDestroy(m->ev_fork);
   if (m->ev_join) (void)hipEventDestroy(m->ev_join);
   if (m->side_st) (void)hipStreamDestroy(m->side_st);
+  if (m->ev_wprep) (void)hipEventDestroy(m->ev_wprep);
+  if (m->pbase) (void)hipFree(m->pbase);
   delete m;
 }
 

@@ -85,6 +85,13 @@ class ExtractionEngine:
                                                    device=self.device)
         return handle, ws, (-ws.data_ptr()) % 256
 
+    def weights_changed(self):
+        """Call after rewriting ``wdev`` in place: every extraction instance
+        rebuilds its derived weights (bf16 planes, Winograd-domain weights) at
+        its next forward (posfeat_model_weights_changed)."""
+        for handle, _ in self._inst.values():
+            check(lib().posfeat_model_weights_changed(handle))
+
     @property
     def cached_shapes(self):
         return list(self._inst.keys())

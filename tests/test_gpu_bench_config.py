@@ -232,6 +232,49 @@ def test_fused_head_matches_unfused(gpu, B, hw, tmp_path):
     assert e <= TOL * s, "fused head vs oracle err %g" % e
 
 
+def test_engine_weight_cache_and_weights_changed(gpu):
+    """Extraction instances build their derived weights (the blob's bf16
+    planes, the decoder's Winograd-domain weights) once, in their own memory:
+    repeated runs -- interleaved with another shape's instance on the shared
+    workspace -- equal a fresh engine's; after an in-place weight change,
+    weights_changed() makes the next run equal a fresh engine built on the
+    changed blob."""
+    from posfeat_amd.weights import seeded_image
+    imgs = torch.from_numpy(np.stack([seeded_image(s, 96, 128) for s in (7, 8)])).to(gpu)
+    other = torch.from_numpy(np.stack([seeded_image(9, 64, 96)])).to(gpu)
+    eng = _new_engine(gpu)
+    first = {k: v.clone() for k, v in eng.run(imgs).items() if not k.startswith("_")}
+    eng.run(other)          # another instance writes the shared workspace
+    again = eng.run(imgs)
+    for k in ("local_point", "local_map", "global_feat"):
+        assert torch.equal(again[k], first[k]), k
+    # rewrite a decoder conv's weights in place (a Winograd layer) and the head
+    spec = {n: (w_off, cout * kpad) for n, cout, cin, kh, kw, kpad, w_off, b_off in
+            _specs_with_kpad()}
+    for name in ("upconv2.conv", "iconv2", "head.conv1"):
+        off, n = spec[name]
+        eng.wdev[off:off + n] *= 1.25
+    eng.weights_changed()
+    got = eng.run(imgs)
+    fresh = _new_engine(gpu)
+    fresh.wdev.copy_(eng.wdev)
+    ref = fresh.run(imgs)
+    for k in ("local_point", "local_map", "global_feat"):
+        assert torch.equal(got[k], ref[k]), k
+    for k in ("local_point", "local_map"):   # global_feat does not see these layers
+        assert not torch.equal(got[k], first[k]), k
+    eng.close()
+    fresh.close()
+
+
+def _specs_with_kpad():
+    from posfeat_amd import _lib, weights
+    out = []
+    for name, cout, cin, kh, kw, w_off, b_off in _lib.model_specs():
+        out.append((name, cout, cin, kh, kw, weights.packed_k(cin, kh, kw)[2], w_off, b_off))
+    return out
+
+
 def test_engine_shape_cache_lru_and_shared_workspace(gpu, monkeypatch):
     """Many image sizes (HPatches / Aachen): at most POSFEAT_ENGINE_MAX_SHAPES
     instances are kept (least recently used evicted), inference instances
