@@ -374,7 +374,7 @@ long long posfeat_model_weight_floats(void);
 int posfeat_model_create(int batch, int h, int w, const float *weights, posfeat_model **out);
 /* An extraction instance (posfeat_model_create) builds its derived weights --
  * the blob's bf16 planes and the decoder's Winograd-domain weights -- once,
- * in device memory of its own (allocated at create), by the first forward
+ * in device memory of its own (allocated by its first forward), by the first forward
  * that needs them.  A caller that rewrites the weight blob in place calls
  * this before the next forward (training instances rebuild them every
  * forward and ignore it). */

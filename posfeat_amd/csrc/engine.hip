@@ -169,7 +169,8 @@ struct posfeat_model {
   std::map<std::string, int> tuned;
   bool autotune = true;
   // derived weights (the blob's bf16 planes, the decoder's Winograd U) of an
-  // extraction instance live in its own device memory and are built once:
+  // extraction instance live in its own device memory (allocated by its first
+  // forward) and are built once:
   // by the first forward that needs them, again after
   // posfeat_model_weights_changed (training instances rebuild them every
   // forward: their weights move every step)
@@ -1403,12 +1404,7 @@ extern "C" int posfeat_model_create(int batch, int h, int w, const float* weight
   m->W = w;
   m->wts = weights;
   m->wcache = true;
-  plan(m);
-  if (m->p_bytes && (hipMalloc(reinterpret_cast<void**>(&m->pbase), m->p_bytes) != hipSuccess ||
-                     hipEventCreateWithFlags(&m->ev_wprep, hipEventDisableTiming) != hipSuccess)) {
-    posfeat_model_destroy(m);
-    return POSFEAT_E_HIP;
-  }
+  plan(m);  // host only: the derived-weight memory is allocated by the first forward
   *out = m;
   return POSFEAT_OK;
 }
@@ -1416,6 +1412,14 @@ extern "C" int posfeat_model_create(int batch, int h, int w, const float* weight
 // a forward that built derived weights records where they are complete; a
 // later forward (maybe on another stream) orders itself after that point
 static int wprep_begin(posfeat_model* m, hipStream_t st) {
+  if (m->wcache && m->p_bytes && !m->pbase) {
+    if (hipMalloc(reinterpret_cast<void**>(&m->pbase), m->p_bytes) != hipSuccess) {
+      m->pbase = nullptr;
+      return POSFEAT_E_HIP;
+    }
+    if (hipEventCreateWithFlags(&m->ev_wprep, hipEventDisableTiming) != hipSuccess)
+      return POSFEAT_E_HIP;
+  }
   if (m->wcache && m->ev_wprep && (m->wpl_done || !m->wino_done.empty()))
     if (hipStreamWaitEvent(st, m->ev_wprep, 0) != hipSuccess) return POSFEAT_E_HIP;
   return POSFEAT_OK;
