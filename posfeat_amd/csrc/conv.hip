@@ -105,11 +105,17 @@ __device__ __forceinline__ void conv_epilogue_t(const ConvArgs& a, float* smem, 
   constexpr int TP = BN + 4;
   float* T = smem;  // the K loop ended with a barrier: staging LDS is free
   constexpr int C4 = BN / 4;
-  constexpr int RPP = THREADS / C4;  // rows per pass
+  // rows per pass: THREADS / C4, rounded down to a power of two that divides
+  // the slice (BN = 192: 48 quads, 4 rows per pass, threads 192.. idle)
+  constexpr int RPP0 = THREADS / C4;
+  constexpr int RPP = RPP0 >= 16 ? 16 : RPP0 >= 8 ? 8 : RPP0 >= 4 ? 4 : RPP0 >= 2 ? 2 : 1;
+  static_assert(RPP0 == RPP || THREADS % C4 != 0, "every thread active when the quads divide");
+  static_assert(SR % RPP == 0, "rows per pass divide the slice");
   constexpr int NP = SR / RPP;       // passes per slice
   const int q = tid % C4, r0 = tid / C4;
+  const bool active = r0 < RPP;      // every thread when THREADS % C4 == 0
   const int col = n0 + 4 * q;
-  const bool colok = col < a.Cout;
+  const bool colok = active && col < a.Cout;
   const f32x4 bv = (a.ksplit <= 1 && a.bias && colok)
                        ? *reinterpret_cast<const f32x4*>(a.bias + col)
                        : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -173,13 +179,15 @@ __device__ __forceinline__ void conv_epilogue_t(const ConvArgs& a, float* smem, 
   if (a.stats) {  // reduce the RPP row groups of each column in a fixed order
     __syncthreads();
     float* R = smem;  // [RPP][2 slots][BN][2]
+    if (active) {
 #pragma unroll
-    for (int sl = 0; sl < 2; ++sl)
+      for (int sl = 0; sl < 2; ++sl)
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        R[((r0 * 2 + sl) * BN + 4 * q + k) * 2 + 0] = s1[sl][k];
-        R[((r0 * 2 + sl) * BN + 4 * q + k) * 2 + 1] = s2[sl][k];
-      }
+        for (int k = 0; k < 4; ++k) {
+          R[((r0 * 2 + sl) * BN + 4 * q + k) * 2 + 0] = s1[sl][k];
+          R[((r0 * 2 + sl) * BN + 4 * q + k) * 2 + 1] = s2[sl][k];
+        }
+    }
     __syncthreads();
     for (int e = tid; e < 2 * BN; e += THREADS) {
       const int sl = e / BN, c = e - sl * BN;
@@ -2274,7 +2282,8 @@ enum ConvTile {
   TILE_BF6R_128x128 = 26, TILE_BF6R_128x64 = 27,  // + A straight to registers
   TILE_BF6B_256x128 = 28,  // pre-split weights, 8 waves stacked along M (one 135-KB block per CU)
   TILE_BF6X_128x128 = 29, TILE_BF6X_128x64 = 30,  // dense, 16x16x32 MFMAs (conv_bf6x_kernel)
-  TILE_BF6X_256x128 = 31
+  TILE_BF6X_256x128 = 31,
+  TILE_BF6X_128x192 = 32  // N % 192 == 0 (head.conv1's Winograd GEMMs, the tap GEMM): A read once per 192 columns
 };
 
 // POSFEAT_BF6=1: every conv the row-tile DMA kernel serves (1x1, strided, the
@@ -2410,7 +2419,7 @@ Plan plan_for_tile(const ConvArgs& a, int tile) {
   if (bf6_on() && glds_ok) {
     // pre-split convs on the bf6x tiles (dense GEMMs, slab x tap gathers):
     // the 16x16x32 tiles only, and only they
-    const bool x_tile = tile >= TILE_BF6X_128x128 && tile <= TILE_BF6X_256x128;
+    const bool x_tile = tile >= TILE_BF6X_128x128 && tile <= TILE_BF6X_128x192;
     if (bf6x_on() && (dense_gemm(a) || gt_gemm(a))) {
       if (!x_tile) return p;
     } else {
@@ -2423,11 +2432,13 @@ Plan plan_for_tile(const ConvArgs& a, int tile) {
     case TILE_BF6X_128x128:
     case TILE_BF6X_128x64:
     case TILE_BF6X_256x128:
+    case TILE_BF6X_128x192:
       if (!bf6x_on() || !((glds_ok && (dense_gemm(a) || gt_gemm(a))) || g4_gemm(a))) return p;
       if (g4_gemm(a) && tile != TILE_BF6X_128x64) return p;
+      if (tile == TILE_BF6X_128x192 && (!dense_gemm(a) || a.Cout % 192)) return p;
       p.kern = KERN_GLDS;
       p.bm = tile == TILE_BF6X_256x128 ? 256 : 128;
-      p.bn = tile == TILE_BF6X_128x64 ? 64 : 128;
+      p.bn = tile == TILE_BF6X_128x64 ? 64 : tile == TILE_BF6X_128x192 ? 192 : 128;
       p.ppi = 0;
       p.tiles_m = (a.M + p.bm - 1) / p.bm;
       return p;
@@ -2642,6 +2653,10 @@ int conv_run(ConvArgs& a, const Plan& p, hipStream_t st) {
       else
         hipLaunchKernelGGL((conv_bf6x_kernel<64, 2, 2>), dim3(a.nwg * a.ksplit, a.nbatch),
                            dim3(256), 0, st, a);
+      break;
+    case TILE_BF6X_128x192:  // dense GEMMs only (plan_for_tile)
+      hipLaunchKernelGGL((conv_bf6x_kernel<192>), dim3(a.nwg * a.ksplit, a.nbatch), dim3(256), 0,
+                         st, a);
       break;
     case TILE_BF6X_256x128:
       if (dense_gemm(a))
@@ -2902,7 +2917,7 @@ static const int kAllTiles[] = {TILE_H8x128,      TILE_H8x64,       TILE_128x128
                                 TILE_BF6_128x128, TILE_BF6_128x256, TILE_BF6_64x128,
                                 TILE_BF6_128x64,  TILE_BF6B_128x128, TILE_BF6B_128x64,
                                 TILE_BF6R_128x128, TILE_BF6R_128x64,  TILE_BF6B_256x128,
-                                TILE_BF6X_128x128, TILE_BF6X_128x64};
+                                TILE_BF6X_128x128, TILE_BF6X_128x64, TILE_BF6X_128x192};
 // (TILE_BF6X_256x128 is legal where forced -- POSFEAT_CONV_TILE, the planes
 // ABI's tile argument -- but not an autotune candidate: never faster, and the
 // timing noise let it take the tap GEMM at +5 %, r7i)
@@ -3196,8 +3211,11 @@ int pf_gemm_batched(const float* A, int lda, long long sa, const float* B, long 
     const char* e = pf_ab_getenv("POSFEAT_BF6X_RB4");
     return e && e[0] == '1';
   }();
+  // N = 192 (head.conv1): one 192-wide column tile reads A once (three
+  // 64-wide tiles read it three times)
   const int want = x ? (N % 128 == 0 ? (rb4 ? TILE_BF6X_256x128 : TILE_BF6X_128x128)
-                                     : TILE_BF6X_128x64)
+                        : N % 192 == 0 ? TILE_BF6X_128x192
+                                       : TILE_BF6X_128x64)
                    : (Bb && b256 && N % 128 == 0) ? TILE_BF6B_256x128
                    : (N % 128 == 0 && t128 >= 1024) ? TILE_128x128
                    : (Bb && N % 128 != 0 && N % 64 == 0) ? TILE_BF6B_128x64
