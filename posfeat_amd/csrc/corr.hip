@@ -328,12 +328,10 @@ struct WinPatch {
   int px0, py0, PW, PH;
 };
 
-__device__ __forceinline__ WinPatch window_patch_logits(const float* __restrict__ fmb, int h2,
-                                                        int w2, const float* __restrict__ qp,
-                                                        float jx, float jy, int win_h, int win_w,
-                                                        float window_size, float* pc, float* ax,
-                                                        float (&wl)[MAX_WIN / 64]) {
-  const int lane = threadIdx.x & 63, grp = lane >> 4, cl = lane & 15;
+// the window's tap axes (fx per ix, fy per iy) into ax and its pixel patch
+__device__ __forceinline__ WinPatch window_patch_geom(int h2, int w2, float jx, float jy, int win_h,
+                                                      int win_w, float window_size, float* ax) {
+  const int lane = threadIdx.x & 63;
   for (int i = lane; i < win_w; i += 64)
     ax[i] = ((jx + linspace_f(-window_size, window_size, win_w, i) + 1.f) * w2 - 1.f) / 2.f;
   for (int i = lane; i < win_h; i += 64)
@@ -344,6 +342,16 @@ __device__ __forceinline__ WinPatch window_patch_logits(const float* __restrict_
   P.py0 = (int)floorf(ax[win_w]);
   P.PW = (int)floorf(ax[win_w - 1]) + 2 - P.px0;
   P.PH = (int)floorf(ax[win_w + win_h - 1]) + 2 - P.py0;
+  return P;
+}
+
+__device__ __forceinline__ WinPatch window_patch_logits(const float* __restrict__ fmb, int h2,
+                                                        int w2, const float* __restrict__ qp,
+                                                        float jx, float jy, int win_h, int win_w,
+                                                        float window_size, float* pc, float* ax,
+                                                        float (&wl)[MAX_WIN / 64]) {
+  const int lane = threadIdx.x & 63, grp = lane >> 4, cl = lane & 15;
+  const WinPatch P = window_patch_geom(h2, w2, jx, jy, win_h, win_w, window_size, ax);
   const int np = P.PW * P.PH;
   const f32x4 qa = *reinterpret_cast<const f32x4*>(qp + cl * 8);
   const f32x4 qb = *reinterpret_cast<const f32x4*>(qp + cl * 8 + 4);
@@ -400,7 +408,8 @@ __global__ void line_window_kernel(const float* __restrict__ cpx,   // [b][n][2]
                                    int win_h, int win_w, float window_size,
                                    float* __restrict__ l_exp_n, float* __restrict__ l_org_n,
                                    uint8_t* __restrict__ valid, float* __restrict__ w_px,
-                                   float* __restrict__ w_std, int use_patch) {
+                                   float* __restrict__ w_std, int use_patch,
+                                   float* __restrict__ wlog) {
   __shared__ float s_pc[4][WB_PATCH];
   __shared__ float s_ax[4][WB_AXES];
   __shared__ float s_lg[4][MAX_LINE];
@@ -519,6 +528,10 @@ __global__ void line_window_kernel(const float* __restrict__ cpx,   // [b][n][2]
         if (s == lane + 64 * r) wl[r] = d;
     }
   }
+  if (wlog)  // kept for the backward (window_bwd_patch_kernel): it skips the patch pass
+#pragma unroll
+    for (int r = 0; r < MAX_WIN / 64; ++r)
+      if (lane + 64 * r < nw) wlog[wid * MAX_WIN + lane + 64 * r] = wl[r];
   float wm = -INFINITY;
 #pragma unroll
   for (int r = 0; r < MAX_WIN / 64; ++r) wm = fmaxf(wm, wl[r]);
@@ -856,7 +869,7 @@ __global__ __launch_bounds__(256) void window_bwd_patch_kernel(
     const float* __restrict__ f1, const float* __restrict__ fm2, const float* __restrict__ center,
     const float* __restrict__ gE, int nb, int n, int h2, int w2, int win_h, int win_w,
     float window_size, float* __restrict__ dq, int rec_stride, float* __restrict__ crec,
-    int4* __restrict__ prec) {
+    int4* __restrict__ prec, const float* __restrict__ wlog) {
   __shared__ float s_pc[4][WB_PATCH];  // q . fm per patch pixel, then c
   __shared__ float s_t[4][WB_PATCH];   // separable adjoint, first stage [iy][px]
   __shared__ float s_ds[4][WB_TAPS];   // dsim per tap
@@ -881,10 +894,17 @@ __global__ __launch_bounds__(256) void window_bwd_patch_kernel(
   const float jx = center[wid * 2], jy = center[wid * 2 + 1];
   const float* qp = f1 + wid * 128;
   float wl[MAX_WIN / 64];
-  const WinPatch P =
-      window_patch_logits(fmb, h2, w2, qp, jx, jy, win_h, win_w, window_size, pc, ax, wl);
-  const int px0 = P.px0, py0 = P.py0, PW = P.PW, np = P.PW * P.PH;
   const int nw = win_h * win_w;
+  WinPatch P;
+  if (wlog) {  // the forward's logits (line_window_kernel): no pass over the patch
+    P = window_patch_geom(h2, w2, jx, jy, win_h, win_w, window_size, ax);
+#pragma unroll
+    for (int r = 0; r < MAX_WIN / 64; ++r)
+      wl[r] = lane + 64 * r < nw ? wlog[wid * MAX_WIN + lane + 64 * r] : -INFINITY;
+  } else {
+    P = window_patch_logits(fmb, h2, w2, qp, jx, jy, win_h, win_w, window_size, pc, ax, wl);
+  }
+  const int px0 = P.px0, py0 = P.py0, PW = P.PW, np = P.PW * P.PH;
   float wm = -INFINITY;
 #pragma unroll
   for (int r = 0; r < MAX_WIN / 64; ++r) wm = fmaxf(wm, wl[r]);
@@ -1182,7 +1202,7 @@ __global__ void l2norm_bwd_kernel(const float* __restrict__ x, int cs,
 // Forward workspace layout (shared with posfeat_line2window_backward, which
 // reads the grid points, descriptors and T*normalize maps the forward left).
 struct L2WLayout {
-  size_t c1n, c1p, c2n, c2p, f1, f2, S, fm1, fm2, colp, total;
+  size_t c1n, c1p, c2n, c2p, f1, f2, S, fm1, fm2, colp, wl1, wl2, total;
 };
 
 static L2WLayout l2w_layout(int b, int H1, int W1, int H2, int W2, int grid) {
@@ -1204,6 +1224,9 @@ static L2WLayout l2w_layout(int b, int H1, int W1, int H2, int W2, int grid) {
   L.fm1 = take((size_t)b * (H1 / 4) * (W1 / 4) * 512);
   L.fm2 = take((size_t)b * (H2 / 4) * (W2 / 4) * 512);
   L.colp = take((size_t)b * COL_CH * n2 * sizeof(ColAcc));
+  // the window logits of both directions (MAX_WIN per point), read by the backward
+  L.wl1 = take((size_t)b * n1 * MAX_WIN * 4);
+  L.wl2 = take((size_t)b * n2 * MAX_WIN * 4);
   L.total = cur;
   return L;
 }
@@ -1299,11 +1322,13 @@ extern "C" int posfeat_line2window(const float* xf1, int cs1, const float* xf2, 
   hipLaunchKernelGGL(line_window_kernel, dim3((b * n1 + 3) / 4), dim3(256), 0, st, c1p, F1, f1,
                      fm2, rand1, b, n1, h2, w2, H2, W2, line_step, win_h2, win_w2, window_size,
                      out->l1_exp_n, out->l1_org_n, out->valid1, out->w1, out->w1_std,
-                     (int)(window_patch_on() && window_patch_fits(win_h2, win_w2)));
+                     (int)(window_patch_on() && window_patch_fits(win_h2, win_w2)),
+                     reinterpret_cast<float*>(wb + lay.wl1));
   hipLaunchKernelGGL(line_window_kernel, dim3((b * n2 + 3) / 4), dim3(256), 0, st, c2p, F2, f2,
                      fm1, rand2, b, n2, h1, w1, H1, W1, line_step, win_h1, win_w1, window_size,
                      out->l2_exp_n, out->l2_org_n, out->valid2, out->w2, out->w2_std,
-                     (int)(window_patch_on() && window_patch_fits(win_h1, win_w1)));
+                     (int)(window_patch_on() && window_patch_fits(win_h1, win_w1)),
+                     reinterpret_cast<float*>(wb + lay.wl2));
   PF_CHECK_LAUNCH();
   return POSFEAT_OK;
 }
@@ -1419,7 +1444,7 @@ extern "C" int posfeat_line2window_backward(
   if (gather1) {
     hipLaunchKernelGGL(window_bwd_patch_kernel, dim3((b * n1 + 3) / 4), dim3(256), 0, st, f1, fm2,
                        fwd->l1_exp_n, gE1, b, n1, h2, w2, win_h2, win_w2, window_size, dq1,
-                       (int)rs1, crec1, prec1);
+                       (int)rs1, crec1, prec1, reinterpret_cast<const float*>(fb + lay.wl1));
     hipLaunchKernelGGL(window_gather_kernel,
                        dim3(((w2 + WG_T - 1) / WG_T) * ((h2 + WG_T - 1) / WG_T), b), dim3(256), 0,
                        st, f1, crec1, prec1, (int)rs1, n1, h2, w2, dfm2);
@@ -1430,7 +1455,7 @@ extern "C" int posfeat_line2window_backward(
   if (gather2) {
     hipLaunchKernelGGL(window_bwd_patch_kernel, dim3((b * n2 + 3) / 4), dim3(256), 0, st, f2, fm1,
                        fwd->l2_exp_n, gE2, b, n2, h1, w1, win_h1, win_w1, window_size, dq2,
-                       (int)rs2, crec2, prec2);
+                       (int)rs2, crec2, prec2, reinterpret_cast<const float*>(fb + lay.wl2));
     hipLaunchKernelGGL(window_gather_kernel,
                        dim3(((w1 + WG_T - 1) / WG_T) * ((h1 + WG_T - 1) / WG_T), b), dim3(256), 0,
                        st, f2, crec2, prec2, (int)rs2, n2, h1, w1, dfm1);
