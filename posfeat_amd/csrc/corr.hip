@@ -1428,7 +1428,12 @@ extern "C" int posfeat_line2window_backward(
                        (size_t)(win_w2 + 4) * (win_h2 + 4) <= rs1 && n1 <= WG_MAXN;
   const bool gather2 = window_patch_on() && window_patch_fits(win_h1, win_w1) &&
                        (size_t)(win_w1 + 4) * (win_h1 + 4) <= rs2 && n2 <= WG_MAXN;
-  if (hipMemsetAsync(accs, 0, reinterpret_cast<char*>(crec1) - accs, st) != hipSuccess)
+  // zero the fixed-point accumulators; a gathered window gradient (window_gather_kernel
+  // writes every pixel of its map) needs no zeroed afm
+  (void)accs;
+  if (hipMemsetAsync(ax1, 0, p1 * 8, st) != hipSuccess || hipMemsetAsync(ax2, 0, p2 * 8, st) != hipSuccess ||
+      (!gather2 && hipMemsetAsync(afm1, 0, p1 * 8, st) != hipSuccess) ||
+      (!gather1 && hipMemsetAsync(afm2, 0, p2 * 8, st) != hipSuccess))
     return POSFEAT_E_HIP;
   // d loss / d window expectations (w1 lives in image 2, w2 in image 1)
   hipLaunchKernelGGL(epi_loss_bwd_kernel, dim3(1), dim3(1024), 0, st, b, n1, F1, fwd->coord1,
