@@ -1100,17 +1100,20 @@ bool window_patch_fits(int win_h, int win_w) {
 // Query-descriptor backward: f = normalize(s), s = grid_sample(xf, c) (zeros,
 // align_corners=False): ds = (dq - f (f.dq)) / max(|s|, 1e-12) scattered over
 // the 4 corners of c into acc (raw-map gradient, fixed point).  One wave/point.
+// Query-descriptor backward, per point: g = d(sample)/d(loss) from dq through
+// the L2 normalisation (f = s / |s|), written over dq ([b][n][128]); the
+// bilinear spread of g into the map's 4 corner pixels is gathered per pixel by
+// l2norm_bwd_kernel (no zeroed fixed-point accumulator, no atomics).
 __global__ void query_bwd_kernel(const float* __restrict__ xf, int cs, const float* __restrict__ cn,
-                                 const float* __restrict__ f, const float* __restrict__ dq, int nb,
-                                 int n, int h, int w, unsigned long long* __restrict__ acc) {
+                                 const float* __restrict__ f, float* __restrict__ dq, int nb, int n,
+                                 int h, int w) {
   const int lane = threadIdx.x & 63;
   const long long wid = blockIdx.x * (long long)(blockDim.x >> 6) + (threadIdx.x >> 6);
   if (wid >= (long long)nb * n) return;
   const int b = (int)(wid / n);
   const float d0 = dq[wid * 128 + lane], d1 = dq[wid * 128 + lane + 64];
-  if (pf_wave_sum(fabsf(d0) + fabsf(d1)) == 0.f) return;
+  if (pf_wave_sum(fabsf(d0) + fabsf(d1)) == 0.f) return;  // g = 0 = dq already
   const float* xb = xf + (long long)b * h * w * cs;
-  unsigned long long* accb = acc + (long long)b * h * w * 128;
   const float gx = cn[wid * 2], gy = cn[wid * 2 + 1];
   const float fx = ((gx + 1.f) * w - 1.f) / 2.f, fy = ((gy + 1.f) * h - 1.f) / 2.f;
   const float flx = floorf(fx), fly = floorf(fy);
@@ -1144,42 +1147,52 @@ __global__ void query_bwd_kernel(const float* __restrict__ xf, int cs, const flo
   const float f0 = f[wid * 128 + lane], f1v = f[wid * 128 + lane + 64];
   const float fd = pf_wave_sum(f0 * d0 + f1v * d1);
   const float inv = 1.f / fmaxf(nrm, 1e-12f);
-  const float g0 = nrm > 1e-12f ? (d0 - f0 * fd) * inv : d0 * inv;
-  const float g1 = nrm > 1e-12f ? (d1 - f1v * fd) * inv : d1 * inv;
-  if (by0 && bx0) {
-    unsigned long long* p = accb + ((long long)y0 * w + x0) * 128;
-    fx_add(p + lane, w00 * g0);
-    fx_add(p + lane + 64, w00 * g1);
-  }
-  if (by0 && bx1) {
-    unsigned long long* p = accb + ((long long)y0 * w + x1) * 128;
-    fx_add(p + lane, w01 * g0);
-    fx_add(p + lane + 64, w01 * g1);
-  }
-  if (by1 && bx0) {
-    unsigned long long* p = accb + ((long long)y1 * w + x0) * 128;
-    fx_add(p + lane, w10 * g0);
-    fx_add(p + lane + 64, w10 * g1);
-  }
-  if (by1 && bx1) {
-    unsigned long long* p = accb + ((long long)y1 * w + x1) * 128;
-    fx_add(p + lane, w11 * g0);
-    fx_add(p + lane + 64, w11 * g1);
-  }
+  dq[wid * 128 + lane] = nrm > 1e-12f ? (d0 - f0 * fd) * inv : d0 * inv;
+  dq[wid * 128 + lane + 64] = nrm > 1e-12f ? (d1 - f1v * fd) * inv : d1 * inv;
 }
 
 // dxf = normalize_bwd(T * acc_fm) + acc_x, one wave per pixel:
 // y = x / max(|x|, 1e-12); dx = (dy - y (y.dy)) / |x| (|x| > eps), dy / eps otherwise
 // afm: the window-backward map gradient, fixed point (per-tap scatter path) or
 // fp32 (dfm, from window_gather_kernel) when dfm != null
+// dx[p] = the window term through the T * normalize(xf) map + the query term:
+// sum over the grid points whose bilinear sample has p as a corner of
+// corner weight x g (query_bwd_kernel), over the cells that can hold such a
+// sample (a sample sits in its cell) in a fixed order
 __global__ void l2norm_bwd_kernel(const float* __restrict__ x, int cs,
                                   const unsigned long long* __restrict__ afm,
-                                  const float* __restrict__ dfm,
-                                  const unsigned long long* __restrict__ ax, long long npix,
-                                  float T, float* __restrict__ dx, int dcs) {
+                                  const float* __restrict__ dfm, const float* __restrict__ cn,
+                                  const float* __restrict__ gq, int h, int w, int grid,
+                                  int ncx, int ncy, long long npix, float T,
+                                  float* __restrict__ dx, int dcs) {
   const int lane = threadIdx.x & 63;
   const long long pix = blockIdx.x * (long long)(blockDim.x >> 6) + (threadIdx.x >> 6);
   if (pix >= npix) return;
+  const int b = (int)(pix / ((long long)h * w));
+  const int rem = (int)(pix - (long long)b * h * w), py = rem / w, px = rem - py * w;
+  float q0 = 0.f, q1 = 0.f;
+  {
+    // cells (grid image pixels wide) holding image pixels 4 (p - 2) .. 4 (p + 3):
+    // every sample whose bilinear corners can include map pixel p
+    const int cx0 = max(4 * (px - 2), 0) / grid, cx1 = min((4 * (px + 3) - 1) / grid, ncx - 1);
+    const int cy0 = max(4 * (py - 2), 0) / grid, cy1 = min((4 * (py + 3) - 1) / grid, ncy - 1);
+    const int n = ncx * ncy;
+    for (int cy = cy0; cy <= cy1; ++cy)
+      for (int cxx = cx0; cxx <= cx1; ++cxx) {
+        const long long i = (long long)b * n + cy * ncx + cxx;
+        const float fx = ((cn[i * 2] + 1.f) * w - 1.f) / 2.f;
+        const float fy = ((cn[i * 2 + 1] + 1.f) * h - 1.f) / 2.f;
+        const float flx = floorf(fx), fly = floorf(fy);
+        const int x0 = (int)flx, y0 = (int)fly;
+        if (px != x0 && px != x0 + 1) continue;  // (uniform across the wave)
+        if (py != y0 && py != y0 + 1) continue;
+        const float wx = px == x0 ? (float)(x0 + 1) - fx : fx - (float)x0;
+        const float wy = py == y0 ? (float)(y0 + 1) - fy : fy - (float)y0;
+        const float wt = wx * wy;
+        q0 += wt * gq[i * 128 + lane];
+        q1 += wt * gq[i * 128 + lane + 64];
+      }
+  }
   const float x0 = x[pix * cs + lane], x1 = x[pix * cs + lane + 64];
   const float nrm = sqrtf(pf_wave_sum(x0 * x0 + x1 * x1));
   const float inv = 1.f / fmaxf(nrm, 1e-12f);
@@ -1191,8 +1204,8 @@ __global__ void l2norm_bwd_kernel(const float* __restrict__ x, int cs,
   const float yg = pf_wave_sum(y0 * g0 + y1 * g1);
   float r0 = nrm > 1e-12f ? (g0 - y0 * yg) * inv : g0 * inv;
   float r1 = nrm > 1e-12f ? (g1 - y1 * yg) * inv : g1 * inv;
-  r0 += (float)((double)(long long)ax[pix * 128 + lane] / FX_SCALE);
-  r1 += (float)((double)(long long)ax[pix * 128 + lane + 64] / FX_SCALE);
+  r0 += q0;
+  r1 += q1;
   dx[pix * dcs + lane] = r0;
   dx[pix * dcs + lane + 64] = r1;
 }
@@ -1364,7 +1377,7 @@ extern "C" size_t posfeat_line2window_backward_workspace(int b, int H1, int W1, 
   const size_t p1 = (size_t)b * (H1 / 4) * (W1 / 4) * 128, p2 = (size_t)b * (H2 / 4) * (W2 / 4) * 128;
   const size_t r1 = wb_rec_stride(H2 / 4, W2 / 4), r2 = wb_rec_stride(H1 / 4, W1 / 4);
   return pf_align(b * n1 * 8, 256) + pf_align(b * n2 * 8, 256) + pf_align(b * n1 * 512, 256) +
-         pf_align(b * n2 * 512, 256) + 2 * pf_align(p1 * 8, 256) + 2 * pf_align(p2 * 8, 256) +
+         pf_align(b * n2 * 512, 256) + pf_align(p1 * 8, 256) + pf_align(p2 * 8, 256) +
          pf_align(b * n1 * r1 * 4, 256) + pf_align(b * n2 * r2 * 4, 256) +
          pf_align(b * n1 * 16, 256) + pf_align(b * n2 * 16, 256);
 }
@@ -1414,9 +1427,7 @@ extern "C" int posfeat_line2window_backward(
   const size_t p1 = (size_t)b * h1 * w1 * 128, p2 = (size_t)b * h2 * w2 * 128;
   char* accs = p;
   unsigned long long* afm1 = reinterpret_cast<unsigned long long*>(take(p1 * 8));
-  unsigned long long* ax1 = reinterpret_cast<unsigned long long*>(take(p1 * 8));
   unsigned long long* afm2 = reinterpret_cast<unsigned long long*>(take(p2 * 8));
-  unsigned long long* ax2 = reinterpret_cast<unsigned long long*>(take(p2 * 8));
   const size_t rs1 = wb_rec_stride(h2, w2), rs2 = wb_rec_stride(h1, w1);
   float* crec1 = reinterpret_cast<float*>(take((size_t)b * n1 * rs1 * 4));
   float* crec2 = reinterpret_cast<float*>(take((size_t)b * n2 * rs2 * 4));
@@ -1431,8 +1442,7 @@ extern "C" int posfeat_line2window_backward(
   // zero the fixed-point accumulators; a gathered window gradient (window_gather_kernel
   // writes every pixel of its map) needs no zeroed afm
   (void)accs;
-  if (hipMemsetAsync(ax1, 0, p1 * 8, st) != hipSuccess || hipMemsetAsync(ax2, 0, p2 * 8, st) != hipSuccess ||
-      (!gather2 && hipMemsetAsync(afm1, 0, p1 * 8, st) != hipSuccess) ||
+  if ((!gather2 && hipMemsetAsync(afm1, 0, p1 * 8, st) != hipSuccess) ||
       (!gather1 && hipMemsetAsync(afm2, 0, p2 * 8, st) != hipSuccess))
     return POSFEAT_E_HIP;
   // d loss / d window expectations (w1 lives in image 2, w2 in image 1)
@@ -1468,17 +1478,20 @@ extern "C" int posfeat_line2window_backward(
     hipLaunchKernelGGL(window_bwd_kernel, dim3((b * n2 + 3) / 4), dim3(256), 0, st, f2, fm1,
                        fwd->l2_exp_n, gE2, b, n2, h1, w1, win_h1, win_w1, window_size, dq2, afm1);
   }
-  // query descriptors: normalize + grid_sample backward into the raw maps
+  // query descriptors: the normalisation's backward per point (over dq), the
+  // grid_sample backward gathered per pixel below
   hipLaunchKernelGGL(query_bwd_kernel, dim3((b * n1 + 3) / 4), dim3(256), 0, st, xf1, cs1, c1n, f1,
-                     dq1, b, n1, h1, w1, ax1);
+                     dq1, b, n1, h1, w1);
   hipLaunchKernelGGL(query_bwd_kernel, dim3((b * n2 + 3) / 4), dim3(256), 0, st, xf2, cs2, c2n, f2,
-                     dq2, b, n2, h2, w2, ax2);
+                     dq2, b, n2, h2, w2);
   PF_CHECK_LAUNCH();
   const long long np1 = (long long)b * h1 * w1, np2 = (long long)b * h2 * w2;
   hipLaunchKernelGGL(l2norm_bwd_kernel, dim3((unsigned)((np1 + 3) / 4)), dim3(256), 0, st, xf1, cs1,
-                     afm1, dfm1, ax1, np1, temperature, dxf1, dcs1);
+                     afm1, dfm1, c1n, dq1, h1, w1, grid, W1 / grid, H1 / grid, np1, temperature,
+                     dxf1, dcs1);
   hipLaunchKernelGGL(l2norm_bwd_kernel, dim3((unsigned)((np2 + 3) / 4)), dim3(256), 0, st, xf2, cs2,
-                     afm2, dfm2, ax2, np2, temperature, dxf2, dcs2);
+                     afm2, dfm2, c2n, dq2, h2, w2, grid, W2 / grid, H2 / grid, np2, temperature,
+                     dxf2, dcs2);
   PF_CHECK_LAUNCH();
   return POSFEAT_OK;
 }

@@ -316,7 +316,11 @@ __global__ void norm_prelu_upsample_kernel(const float* __restrict__ x, int n, i
 }
 
 // y[b][p] = bias + sum_c w[c] * PReLU((x[b][p][c]-mean)*rstd), C == 128.
-// One wave handles two pixels per step (32 lanes x float4 each).
+// One wave handles two pixels per step (32 lanes x float4 each), over a
+// contiguous range of pixel pairs (its image's mean / rstd reloaded only when
+// the range crosses an image), HT_U steps per pass with all their loads issued
+// before the first reduction.  Same per-pixel arithmetic and order.
+constexpr int HT_U = 4;
 __global__ void head_tail_conv3_kernel(const float* __restrict__ x, int n, int hw, int cs,
                                        const float* __restrict__ mean,
                                        const float* __restrict__ rstd,
@@ -331,19 +335,38 @@ __global__ void head_tail_conv3_kernel(const float* __restrict__ x, int n, int h
   const f32x4 wv = *reinterpret_cast<const f32x4*>(w3 + l32 * 4);
   const float bias = *b3;
   const long long total = (long long)n * hw;
-  for (long long p2 = wid * 2; p2 < total; p2 += waves * 2) {
-    const long long p = p2 + half;
-    float s = 0.f;
-    if (p < total) {
+  const long long pairs = (total + 1) / 2;
+  const long long per = (pairs + waves - 1) / waves;
+  const long long q0 = wid * per, q1 = min(pairs, q0 + per);
+  int bc = -1;
+  f32x4 m = {0.f, 0.f, 0.f, 0.f}, r = {0.f, 0.f, 0.f, 0.f};
+  for (long long q = q0; q < q1; q += HT_U) {
+    f32x4 xv[HT_U];
+#pragma unroll
+    for (int u = 0; u < HT_U; ++u) {
+      const long long p = min(2 * min(q + u, q1 - 1) + half, total - 1);  // clamped: in bounds
+      xv[u] = *reinterpret_cast<const f32x4*>(x + p * cs + l32 * 4);
+    }
+    float s[HT_U];
+#pragma unroll
+    for (int u = 0; u < HT_U; ++u) {
+      const long long p = min(2 * min(q + u, q1 - 1) + half, total - 1);
       const int b = (int)(p / hw);
-      const f32x4 m = *reinterpret_cast<const f32x4*>(mean + b * 128 + l32 * 4);
-      const f32x4 r = *reinterpret_cast<const f32x4*>(rstd + b * 128 + l32 * 4);
-      const f32x4 v = norm_prelu4(*reinterpret_cast<const f32x4*>(x + p * cs + l32 * 4), m, r, a);
-      s = v.x * wv.x + v.y * wv.y + v.z * wv.z + v.w * wv.w;
+      if (b != bc) {  // wave-uniform except where a pair straddles two images
+        m = *reinterpret_cast<const f32x4*>(mean + b * 128 + l32 * 4);
+        r = *reinterpret_cast<const f32x4*>(rstd + b * 128 + l32 * 4);
+        bc = b;
+      }
+      const f32x4 v = norm_prelu4(xv[u], m, r, a);
+      s[u] = v.x * wv.x + v.y * wv.y + v.z * wv.z + v.w * wv.w;
     }
 #pragma unroll
-    for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-    if (l32 == 0 && p < total) y[p] = s + bias;
+    for (int u = 0; u < HT_U; ++u) {
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1) s[u] += __shfl_xor(s[u], o, 64);
+      const long long p = 2 * (q + u) + half;
+      if (l32 == 0 && q + u < q1 && p < total) y[p] = s[u] + bias;
+    }
   }
 }
 
