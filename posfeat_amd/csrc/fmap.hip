@@ -32,6 +32,25 @@ __global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, int n, int c, i
   }
 }
 
+// c <= 4 into a 4-float pixel (the image into the stem's NHWC4 layout): one
+// thread per pixel, one coalesced load per channel plane, one 16-B store
+__global__ void nchw_to_nhwc4_kernel(const float* __restrict__ x, int n, int c, int hw,
+                                     float* __restrict__ y) {
+  const long long total = (long long)n * hw;
+  for (long long p = blockIdx.x * (long long)blockDim.x + threadIdx.x; p < total;
+       p += (long long)gridDim.x * blockDim.x) {
+    const int b = (int)(p / hw);
+    const int pix = (int)(p - (long long)b * hw);
+    const float* xb = x + (long long)b * c * hw + pix;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (c > 0) v.x = xb[0];
+    if (c > 1) v.y = xb[hw];
+    if (c > 2) v.z = xb[2 * (long long)hw];
+    if (c > 3) v.w = xb[3 * (long long)hw];
+    *reinterpret_cast<f32x4*>(y + p * 4) = v;
+  }
+}
+
 // datasets' to_input on the device: uint8 HWC RGB -> ImageNet-normalised
 // float NCHW, ((u / 255) - mean[c]) / std[c] with IEEE round-to-nearest fp32
 // division and subtraction -- the same three roundings as numpy's
@@ -417,6 +436,12 @@ inline int grid_for(long long total, int block) {
 
 // ------------------------------------------------------------------ launchers
 int pf_nchw_to_nhwc(const float* x, int n, int c, int h, int w, int cso, float* y, hipStream_t st) {
+  if (cso == 4 && c <= 4 && (reinterpret_cast<uintptr_t>(y) & 15) == 0) {
+    hipLaunchKernelGGL(nchw_to_nhwc4_kernel, dim3(grid_for((long long)n * h * w, 256)), dim3(256),
+                       0, st, x, n, c, h * w, y);
+    PF_CHECK_LAUNCH();
+    return POSFEAT_OK;
+  }
   const long long total = (long long)n * h * w * cso;
   hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3(grid_for(total, 256)), dim3(256), 0, st, x, n, c,
                      h * w, cso, y);
