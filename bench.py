@@ -501,7 +501,11 @@ def main():
                          ("train_desc", train_desc_main)):
             a2 = argparse.Namespace(**vars(args))
             a2.batch, a2.steps, a2.warmup = 8, args.secondary_steps, 3
-            r2 = fn(a2, world, rank, dev, emit=False)
+            try:   # the headline line is printed whatever happens here
+                r2 = fn(a2, world, rank, dev, emit=False)
+            except Exception as e:  # noqa: BLE001
+                sec[name] = {"error": "%s: %s" % (type(e).__name__, e)}
+                continue
             if rank == 0:
                 sec[name] = {k: r2[k] for k in ("metric", "value", "unit", "ms_per_step", "steps",
                                                 "warmup")}
