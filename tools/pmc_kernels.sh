@@ -9,7 +9,7 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 run() {
   tag=$1; shift
   timeout -s KILL 200 rocprofv3 --pmc "$@" -d "$out/$tag" -o pmc --output-format csv \
-    -- python3 bench.py ${BENCH_ARGS:---steps 2 --warmup 1 --timing-steps 1 --no-cpu-baseline} \
+    -- python3 bench.py ${BENCH_ARGS:---steps 2 --warmup 1 --timing-steps 1 --no-cpu-baseline --no-secondary} \
     > "$out/$tag.log" 2>&1
   rc=$?
   echo "[pmc] $tag rc=$rc" >> "$out/$tag.log"
