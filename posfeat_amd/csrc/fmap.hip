@@ -406,13 +406,29 @@ __global__ void global_feat_kernel(const float* __restrict__ g, int hw, int cs,
   const int b = blockIdx.x;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
   float a0 = 0.f, a1 = 0.f;
-  for (int p = wv; p < hw; p += nw) {
-    const float* v = g + ((long long)b * hw + p) * cs;
-    const float x0 = v[lane], x1 = v[lane + 64];
-    const float ss = pf_wave_sum(x0 * x0 + x1 * x1);
-    const float inv = 1.f / fmaxf(sqrtf(ss), 1e-12f);
-    a0 += x0 * inv;
-    a1 += x1 * inv;
+  // four of this wave's pixels per pass, loads issued together (the wave
+  // sums serialised one pixel's load latency after another); the sums add in
+  // the same pixel order
+  constexpr int GU = 4;
+  for (int p = wv; p < hw; p += GU * nw) {
+    float x0[GU], x1[GU], inv[GU];
+#pragma unroll
+    for (int u = 0; u < GU; ++u) {
+      const float* v = g + ((long long)b * hw + min(p + u * nw, hw - 1)) * cs;
+      x0[u] = v[lane];
+      x1[u] = v[lane + 64];
+    }
+#pragma unroll
+    for (int u = 0; u < GU; ++u) {
+      const float ss = pf_wave_sum(x0[u] * x0[u] + x1[u] * x1[u]);
+      inv[u] = 1.f / fmaxf(sqrtf(ss), 1e-12f);
+    }
+#pragma unroll
+    for (int u = 0; u < GU; ++u)
+      if (p + u * nw < hw) {
+        a0 += x0[u] * inv[u];
+        a1 += x1[u] * inv[u];
+      }
   }
   __shared__ float red[16][128];
   red[wv][lane] = a0;
