@@ -66,10 +66,24 @@ __global__ void det_thr_kernel(const float* __restrict__ kp, int h, int w, int m
   }
 }
 
+// r = 1 (the configs' nms_radius): the eight neighbours loaded together and
+// compared branch-free (the early-exit loop below waited out one load latency
+// per neighbour); the same decision
+__device__ __forceinline__ bool nms_keep1(const float* __restrict__ m, int w, int Hi, int Wi,
+                                          int off, int i, int j, float S) {
+  const int y0 = reflect_idx(i - 1, Hi) + off, y1 = i + off, y2 = reflect_idx(i + 1, Hi) + off;
+  const int x0 = reflect_idx(j - 1, Wi) + off, x1 = j + off, x2 = reflect_idx(j + 1, Wi) + off;
+  const float v0 = m[y0 * w + x0], v1 = m[y0 * w + x1], v2 = m[y0 * w + x2], v3 = m[y1 * w + x0];
+  const float v5 = m[y1 * w + x2], v6 = m[y2 * w + x0], v7 = m[y2 * w + x1], v8 = m[y2 * w + x2];
+  // earlier window positions (0-3) must be < S, later ones (5-8) <= S
+  return (v0 < S) & (v1 < S) & (v2 < S) & (v3 < S) & (v5 <= S) & (v6 <= S) & (v7 <= S) & (v8 <= S);
+}
+
 // NMS decision for pixel (i, j) of an Hi x Wi map stored with row pitch `w`
 // at offset (off, off): reflect padding, first-occurrence tie rule.
 __device__ __forceinline__ bool nms_keep(const float* __restrict__ m, int w, int Hi, int Wi, int off,
                                          int i, int j, int r, float S) {
+  if (r == 1) return nms_keep1(m, w, Hi, Wi, off, i, j, S);
   const int ws = 2 * r + 1, center = r * ws + r;
   int pos = 0;
   for (int dy = -r; dy <= r; ++dy) {
