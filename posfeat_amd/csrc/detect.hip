@@ -232,9 +232,17 @@ __global__ __launch_bounds__(1024) void det_select_kernel(
     const uint32_t prefix = s_prefix;
     if (tid == 0 && nzero > 0 && (ZKEY & pmask) == prefix)
       atomicAdd(&hist[(ZKEY >> shift) & 0xFF], nzero);
-    for (int k = tid; k < count; k += blockDim.x) {
-      const uint32_t key = ck[k];
-      if ((key & pmask) == prefix) atomicAdd(&hist[(key >> shift) & 0xFF], 1);
+    // four candidates per thread per pass, loads first (a histogram: the
+    // counts do not depend on the order)
+    const int bd = blockDim.x;
+    for (int k = tid; k < count; k += 4 * bd) {
+      uint32_t kk[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) kk[u] = k + u * bd < count ? ck[k + u * bd] : ~pmask;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (k + u * bd < count && (kk[u] & pmask) == prefix)
+          atomicAdd(&hist[(kk[u] >> shift) & 0xFF], 1);
     }
     __syncthreads();
     if (tid == 0) {
