@@ -67,6 +67,54 @@ __global__ void sample_desc_kernel(const float* __restrict__ fmap, int nb, int C
   }
 }
 
+// C == 128: a half-wave per keypoint, 4 channels (16-B loads) per lane --
+// two keypoints per wave and half the load instructions of the one-wave form;
+// each channel's bilinear sum in the same order (the norm's sum of squares is
+// grouped differently: per-lane quads, then a 32-lane tree)
+__global__ void sample_desc128_kernel(const float* __restrict__ fmap, int nb, int h, int w, int cs,
+                                      const float* __restrict__ coord, int npts,
+                                      const int32_t* __restrict__ n_valid, int each,
+                                      int normalize, float* __restrict__ out) {
+  const int lane = threadIdx.x & 63, half = lane >> 5, l32 = lane & 31;
+  const long long kid =
+      (blockIdx.x * (long long)(blockDim.x >> 6) + (threadIdx.x >> 6)) * 2 + half;
+  const long long total = (long long)nb * npts;
+  if (kid >= total) return;  // (total is even per wave unless npts * nb is odd: the pair's
+                             // other half still runs its own shuffles below)
+  const int b = (int)(kid / npts);
+  const int k = (int)(kid - (long long)b * npts);
+  float* o = out + kid * 128 + 4 * l32;
+  const int nv = n_valid ? n_valid[each ? b : 0] : npts;
+  const bool valid = k < nv;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (valid) {
+    const float gx = coord[kid * 2 + 0], gy = coord[kid * 2 + 1];
+    const float ix = ((gx + 1.f) * w - 1.f) / 2.f;
+    const float iy = ((gy + 1.f) * h - 1.f) / 2.f;
+    const float fx = floorf(ix), fy = floorf(iy);
+    const int x0 = (int)fx, y0 = (int)fy, x1 = x0 + 1, y1 = y0 + 1;
+    const float wnw = (x1 - ix) * (y1 - iy);
+    const float wne = (ix - x0) * (y1 - iy);
+    const float wsw = (x1 - ix) * (iy - y0);
+    const float wse = (ix - x0) * (iy - y0);
+    const bool bx0 = (unsigned)x0 < (unsigned)w, bx1 = (unsigned)x1 < (unsigned)w;
+    const bool by0 = (unsigned)y0 < (unsigned)h, by1 = (unsigned)y1 < (unsigned)h;
+    const float* base = fmap + (long long)b * h * w * cs + 4 * l32;
+    if (by0 && bx0) acc += *reinterpret_cast<const f32x4*>(base + ((long long)y0 * w + x0) * cs) * wnw;
+    if (by0 && bx1) acc += *reinterpret_cast<const f32x4*>(base + ((long long)y0 * w + x1) * cs) * wne;
+    if (by1 && bx0) acc += *reinterpret_cast<const f32x4*>(base + ((long long)y1 * w + x0) * cs) * wsw;
+    if (by1 && bx1) acc += *reinterpret_cast<const f32x4*>(base + ((long long)y1 * w + x1) * cs) * wse;
+  }
+  float inv = 1.f;
+  if (normalize) {
+    float ss = acc.x * acc.x + acc.y * acc.y + acc.z * acc.z + acc.w * acc.w;
+#pragma unroll
+    for (int off = 16; off > 0; off >>= 1) ss += __shfl_xor(ss, off, 64);
+    inv = 1.f / fmaxf(sqrtf(ss), 1e-12f);
+  }
+  *reinterpret_cast<f32x4*>(o) = valid ? (normalize ? acc * inv : acc) : f32x4{0.f, 0.f, 0.f, 0.f};
+}
+
 }  // namespace
 
 namespace {
@@ -77,6 +125,15 @@ int sample_impl(const float* fmap, int b, int c, int h, int w, int cs, const flo
   const long long waves = (long long)b * npts;
   if (waves == 0) return POSFEAT_OK;
   const int wpb = 4;
+  if (c == 128 && cs % 4 == 0 && (reinterpret_cast<uintptr_t>(fmap) & 15) == 0 &&
+      (reinterpret_cast<uintptr_t>(out) & 15) == 0) {
+    const long long w2 = (waves + 1) / 2;  // two keypoints per wave
+    hipLaunchKernelGGL(sample_desc128_kernel, dim3((unsigned)((w2 + wpb - 1) / wpb)),
+                       dim3(64 * wpb), 0, st, fmap, b, h, w, cs, coord, npts, n_valid, each,
+                       normalize, out);
+    PF_CHECK_LAUNCH();
+    return POSFEAT_OK;
+  }
   const dim3 grid((unsigned)((waves + wpb - 1) / wpb)), block(64 * wpb);
   if (c <= 64)
     hipLaunchKernelGGL(sample_desc_kernel<1>, grid, block, 0, st, fmap, b, c, h, w, cs, coord,
