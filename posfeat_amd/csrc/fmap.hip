@@ -89,6 +89,34 @@ __global__ void nhwc_to_nchw_kernel(const float* __restrict__ x, int c, int hw, 
   }
 }
 
+// the same for whole 64 x 64 tiles with 16-B global accesses (c % 64 == 0,
+// hw % 64 == 0, csi % 4 == 0, 16-B aligned): a thread loads 4 channels of a
+// pixel and stores 4 pixels of a channel; the LDS tile is padded by one float
+// per row (the column reads stay conflict-free)
+__global__ void nhwc_to_nchw64_kernel(const float* __restrict__ x, int c, int hw, int csi,
+                                      float* __restrict__ y) {
+  __shared__ float t[64][65];
+  const int b = blockIdx.z;
+  const int p0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {  // 64 pixels x 16 channel quads
+    const int e = it * 256 + tid, r = e >> 4, q = e & 15;
+    const f32x4 v = *reinterpret_cast<const f32x4*>(x + ((long long)b * hw + p0 + r) * csi + c0 + 4 * q);
+    t[r][4 * q + 0] = v.x;
+    t[r][4 * q + 1] = v.y;
+    t[r][4 * q + 2] = v.z;
+    t[r][4 * q + 3] = v.w;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {  // 64 channels x 16 pixel quads
+    const int e = it * 256 + tid, ch = e >> 4, q = e & 15;
+    const f32x4 o = {t[4 * q + 0][ch], t[4 * q + 1][ch], t[4 * q + 2][ch], t[4 * q + 3][ch]};
+    *reinterpret_cast<f32x4*>(y + ((long long)b * c + c0 + ch) * hw + p0 + 4 * q) = o;
+  }
+}
+
 // ---------------------------------------------------------------- maxpool 3x3 s2 p1
 __global__ void maxpool3s2_kernel(const float* __restrict__ x, int n, int h, int w, int c4,
                                   int csi, int oh, int ow, int cso, float* __restrict__ y) {
@@ -486,7 +514,11 @@ int pf_nchw_to_nhwc(const float* x, int n, int c, int h, int w, int cso, float* 
 
 int pf_nhwc_to_nchw(const float* x, int n, int c, int h, int w, int csi, float* y, hipStream_t st) {
   dim3 grid((h * w + 63) / 64, (c + 63) / 64, n);
-  hipLaunchKernelGGL(nhwc_to_nchw_kernel, grid, dim3(256), 0, st, x, c, h * w, csi, y);
+  if (c % 64 == 0 && (h * w) % 64 == 0 && csi % 4 == 0 &&
+      ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15) == 0)
+    hipLaunchKernelGGL(nhwc_to_nchw64_kernel, grid, dim3(256), 0, st, x, c, h * w, csi, y);
+  else
+    hipLaunchKernelGGL(nhwc_to_nchw_kernel, grid, dim3(256), 0, st, x, c, h * w, csi, y);
   PF_CHECK_LAUNCH();
   return POSFEAT_OK;
 }
