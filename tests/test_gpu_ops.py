@@ -221,6 +221,16 @@ def test_layout_roundtrip(gpu):
     assert torch.all(y[..., 40:] == 0)
     z = ops.nhwc_to_nchw(y, c=40)
     assert torch.equal(z, x)
+    # whole 64 x 64 tiles (the 16-B transpose: 128 channels, 32 x 48 pixels,
+    # channel stride 132) and 3 -> 4 channels (the image's NHWC4 layout)
+    x = torch.randn(2, 128, 32, 48, device=gpu)
+    y = ops.nchw_to_nhwc(x, cstride=132)
+    assert torch.equal(y[..., :128], x.permute(0, 2, 3, 1))
+    assert torch.equal(ops.nhwc_to_nchw(y, c=128), x)
+    x = torch.randn(3, 3, 16, 24, device=gpu)
+    y = ops.nchw_to_nhwc(x, cstride=4)
+    assert torch.equal(y[..., :3], x.permute(0, 2, 3, 1))
+    assert torch.all(y[..., 3] == 0)
 
 
 # ------------------------------------------------------------------ detector
