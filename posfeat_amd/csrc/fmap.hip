@@ -129,20 +129,25 @@ __global__ void maxpool3s2_kernel(const float* __restrict__ x, int n, int h, int
     p /= ow;
     const int oy = (int)(p % oh);
     const int b = (int)(p / oh);
+    // branch-free: the nine taps' loads go out together (a tap in the padding
+    // loads a clamped address and counts as -inf, as if skipped)
+    f32x4 v[9];
+    bool ok[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int iy = 2 * oy + t / 3 - 1, ix = 2 * ox + t % 3 - 1;
+      ok[t] = (unsigned)iy < (unsigned)h && (unsigned)ix < (unsigned)w;
+      const int cy = min(max(iy, 0), h - 1), cx = min(max(ix, 0), w - 1);
+      v[t] = *reinterpret_cast<const f32x4*>(x + (((long long)b * h + cy) * w + cx) * csi + q * 4);
+    }
     f32x4 m = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-    for (int dy = -1; dy <= 1; ++dy) {
-      const int iy = 2 * oy + dy;
-      if ((unsigned)iy >= (unsigned)h) continue;
-      for (int dx = -1; dx <= 1; ++dx) {
-        const int ix = 2 * ox + dx;
-        if ((unsigned)ix >= (unsigned)w) continue;
-        const f32x4 v =
-            *reinterpret_cast<const f32x4*>(x + (((long long)b * h + iy) * w + ix) * csi + q * 4);
-        m.x = fmaxf(m.x, v.x);
-        m.y = fmaxf(m.y, v.y);
-        m.z = fmaxf(m.z, v.z);
-        m.w = fmaxf(m.w, v.w);
-      }
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      if (!ok[t]) continue;
+      m.x = fmaxf(m.x, v[t].x);
+      m.y = fmaxf(m.y, v[t].y);
+      m.z = fmaxf(m.z, v[t].z);
+      m.w = fmaxf(m.w, v[t].w);
     }
     *reinterpret_cast<f32x4*>(y + (((long long)b * oh + oy) * ow + ox) * cso + q * 4) = m;
   }
