@@ -560,8 +560,10 @@ __device__ __forceinline__ void gc_block(const GcArgs& A, float* spA, float* spB
       }
       // y interpolation of output rows 4 i + r from R rows i + j, j in -1..1.
       // Scalar FMAs: the packed form (pairs of output rows, the R value
-      // broadcast by op_sel) gave run-to-run different values in lanes 48-63
-      // 
+      // broadcast by op_sel) compiled to v_pk_fma_f32 whose low result reads
+      // the high dword of its own destination pair, and gave run-to-run
+      // different row-14 values in lanes 48-63 (isa_check
+      // fails a build holding that form)
 #pragma unroll
       for (int i = 0; i < TQ; ++i) {
 #pragma unroll
@@ -613,7 +615,12 @@ __device__ __forceinline__ void gc_block(const GcArgs& A, float* spA, float* spB
     // ---- y through LDS: [row][column][channel], then 16-B stores of 4
     // channels (a lane's 16 rows x 1 channel would be 64 dword stores: the
     // store tail was issue-bound) ------------------------------------------------
-    gc_barrier();  // every wave is done reading the P tile
+    // every wave is done reading the P tile: the y tile overwrites it.  (The
+    // ISA had no LDS access in flight here already -- the R values were all
+    // consumed above -- the wait states it in the source; tools/isa_check.py
+    // reports any s_barrier crossed with LDS accesses outstanding.)
+    gc_wait_lgkm0();
+    gc_barrier();
     {
       float* so = spA + (8 * wave + 4 * hl) * CB_CG + ln;
 #pragma unroll

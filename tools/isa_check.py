@@ -15,8 +15,29 @@ waits rely on but the source cannot pin by itself:
   VGPR write the compiler's hazard recognizer does not see: it padded
   nothing and the MFMAs read stale operands (nondeterministic results,
   DESIGN.md 4.1n).
+* every kernel: no v_pk_fma_f32 whose LOW result reads the HIGH dword of a
+  source pair that is also its destination (`v_pk_fma_f32 v[120:121], v[236:237],
+  v[120:121], v[174:175] op_sel:[0,1,0]`).  Round 4's packed y interpolation in
+  up4tap_gcombine_kernel (commit b97528c, POSFEAT_GC_ABL=16) compiled to nine
+  of these and gave run-to-run different low results in lanes 48-63 (the last
+  16-lane pass of the wave) -- 23 of 29 repeats on an MI355X, 29 of 29 with an
+  extra s_waitcnt lgkmcnt(0) before its barriers, 0 of 19 for the scalar form
+  (profiles/round5/gcombine_pk_probe_r13a.txt).  The compiler
+  pads nothing for it, so no shipped kernel may contain it.  The same in-place
+  low<-high read on v_pk_add_f32 / v_pk_mov_b32 (ocml's log1pf, 64-bit pair
+  copies) is reported, with run-to-run bit-identity tests over the kernels
+  that hold it (tests/test_gpu_repeat.py).
+* reported: s_barriers crossed with an LDS load or store of the wave still
+  outstanding (straight-line scan; the state resets at an unconditional
+  branch).  Round 4's advice suspected this in up4tap_gcombine_kernel; its
+  ISA has none, in the failing build and the shipped one, and an explicit
+  lgkmcnt(0) there did not change the failure (above).  The remaining
+  instances are the bf6d / bf6s K loops, whose last B-fragment reads of stage
+  s cross the barrier after which B(c + 2) is DMA'd into stage s: the
+  reads were issued before the barrier and the LDS serves a wave's requests
+  in order, while the DMA's write arrives a global-memory latency later.
 
-usage: python tools/isa_check.py [--dump KERNEL_SUBSTRING]
+usage: python tools/isa_check.py [--dump KERNEL_SUBSTRING] [--lib PATH]
 Exit status 1 on a violated property.  tests/test_weights_abi.py runs it.
 """
 import argparse
@@ -200,11 +221,66 @@ def check_pk_inplace_swap(name, body):
     return errs
 
 
+def _pk_parse(ins):
+    op, rest = ins.split(None, 1)
+    mods = {}
+    for key in ("op_sel_hi", "op_sel"):
+        m = re.search(key + r":\[([01,]+)\]", rest)
+        if m:
+            mods[key] = [int(x) for x in m.group(1).split(",")]
+            rest = rest.replace(m.group(0), "")
+    rest = re.sub(r"\b(neg_lo|neg_hi):\[[01,]+\]", "", rest)
+    return op, [o.strip() for o in rest.split(",")], mods
+
+
+def pk_inplace_lo_from_hi(body, ops=("v_pk_fma_f32",)):
+    """Packed ops whose low result reads the high dword of a source pair that
+    is also the destination pair (op_sel[k] = 1 on an in-place source k)."""
+    out = []
+    for ln in body:
+        ins = ln.split("//")[0].strip()
+        if not ins.startswith(ops):
+            continue
+        op, args, mods = _pk_parse(ins)
+        dst = _regs(args[0])
+        sel = mods.get("op_sel", [0, 0, 0])
+        for k, src in enumerate(args[1:4]):
+            r = _regs(src)
+            if k < len(sel) and sel[k] == 1 and len(r) == 2 and max(r) in dst:
+                out.append(ins)
+    return out
+
+
+def check_lds_barrier(name, body):
+    """s_barrier with an LDS load/store of this wave still outstanding."""
+    errs, pending = [], []
+    for ln in body:
+        ins = ln.split("//")[0].strip()
+        if not ins:
+            continue
+        op = ins.split()[0]
+        if op == "s_waitcnt":
+            m = re.search(r"lgkmcnt\((\d+)\)", ins)
+            if m:
+                n = int(m.group(1))
+                pending = pending[len(pending) - n:] if 0 < n < len(pending) else ([] if n == 0 else pending)
+        elif op.startswith("ds_") or op.startswith(("s_load", "s_buffer_load")):
+            pending.append(op)
+        elif op == "s_branch":
+            pending = []
+        elif op == "s_barrier":
+            lds = [o for o in pending if o.startswith("ds_") and "permute" not in o and "swizzle" not in o]
+            if lds:
+                errs.append("%s: s_barrier with %d LDS access(es) outstanding (%s)" % (name, len(lds), lds[-1]))
+    return errs
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--dump", default=None)
+    ap.add_argument("--lib", default=LIB, help="library or object to check (default: the shipped one)")
     args = ap.parse_args()
-    funcs = functions(disassemble(code_objects()))
+    funcs = functions(disassemble(code_objects(args.lib)))
     if args.dump:
         for k, v in funcs.items():
             if args.dump in k:
@@ -228,7 +304,7 @@ def main():
             print("%-90s steps checked %d%s%s" % (k[:90], n, "  FAIL" if e else "",
                                                   "  (warning: vmcnt(0) drain)" if drains and not e
                                                   else ""))
-    if not found:
+    if not found and args.lib == LIB:
         errs.append("no conv_bf6d_kernel instance in %s" % LIB)
     nh = 0
     for k, v in funcs.items():
@@ -246,6 +322,24 @@ def main():
         npk[k] = len(check_pk_inplace_swap(k, v))
     print("in-place cross-half packed-fp32 ops (reported): %d in %d kernels" % (
         sum(npk.values()), sum(1 for v in npk.values() if v)))
+    nfma, nother = 0, collections.Counter()
+    for k, v in funcs.items():
+        bad = pk_inplace_lo_from_hi(v)
+        nfma += len(bad)
+        errs += ["%s: v_pk_fma_f32 low result reads the high dword of its own destination: %s"
+                 % (k, b[:90]) for b in bad]
+        for b in pk_inplace_lo_from_hi(v, ("v_pk_add_f32", "v_pk_mul_f32", "v_pk_mov_b32")):
+            nother[k] += 1
+    print("in-place low<-high v_pk_fma_f32: %d" % nfma)
+    print("in-place low<-high v_pk_add/mul/mov (reported; tests/test_gpu_repeat.py): %d in %s" % (
+        sum(nother.values()), sorted(set(re.sub(r"^_ZN12_GLOBAL__N_1\d+", "", k).split("E")[0]
+                                         for k in nother))))
+    nb = collections.Counter()
+    for k, v in funcs.items():
+        nb[k] = len(check_lds_barrier(k, v))
+    print("s_barrier with LDS accesses outstanding (reported): %d in %s" % (
+        sum(nb.values()), sorted(set(re.sub(r"^_ZN12_GLOBAL__N_1\d+", "", k).split("I")[0]
+                                     for k in nb if nb[k]))))
     for e in errs:
         print("ISA CHECK FAILED:", e)
     return 1 if errs else 0
