@@ -405,9 +405,10 @@ def main():
     conv_total = float(np.mean(conv_ms))
     conv_ach = float(np.mean(conv_fl)) / (conv_total * 1e-3) / 1e12
     # HBM bytes of that launch from the committed rocprofv3 --pmc passes
-    # (tools/traffic_json.py), when they were measured for the same label
+    # (tools/traffic_json.py), when they were measured for the same label;
+    # records/ travels to the GPU box (profiles/ does not)
     traffic = None
-    tfile = os.path.join(ROOT, "profiles", "dominant_traffic.json")
+    tfile = os.path.join(ROOT, "records", "dominant_traffic.json")
     if os.path.exists(tfile):
         try:
             t = json.load(open(tfile))
@@ -482,14 +483,18 @@ def main():
                            "reference_equivalent_tflops":
                                round(HEAD_CONV2_FLOP_PER_IMAGE * args.batch / (c2 * 1e-3) / 1e12, 3)},
             "conv_total": {"executed_tflops": round(conv_ach, 3),
-                           "frac": round(conv_ach / PEAK_FP32_MFMA_TFLOPS, 4),
+                           "frac": round(conv_ach / arith["method_peak"], 4),
+                           "peak": arith["method_peak"],
+                           "frac_of_fp32_mfma_peak": round(conv_ach / PEAK_FP32_MFMA_TFLOPS, 4),
                            "reference_equivalent_tflops":
                                round(CONV_FLOP_PER_IMAGE * args.batch / (conv_total * 1e-3) / 1e12, 3),
                            "ms_per_step": round(conv_total, 3),
                            "main_stream_kernels_ms_per_step": round(float(np.mean(all_ms)), 3),
                            "side_stream_kernels_ms_per_step": round(float(np.mean(side_ms)), 3),
                            "note": "main-stream launches only; the side stream (KeypointDet's "
-                                   "image branch) overlaps them"},
+                                   "image branch) overlaps them; frac = executed fp32-equivalent "
+                                   "rate / the ceiling of the arithmetic the convs run (bf16x6: "
+                                   "2500 / 6 TF)"},
         }
     if world == 1 and not args.no_secondary:
         # the two training configs' steps and their correlation losses, timed by

@@ -372,12 +372,23 @@ int posfeat_model_conv_spec(int i, const char **name, int *cout, int *cin, int *
                             long long *w_off, long long *b_off);
 long long posfeat_model_weight_floats(void);
 int posfeat_model_create(int batch, int h, int w, const float *weights, posfeat_model **out);
+/* The same, sharing the derived-weight store of `share` (an extraction
+ * instance made from the same `weights` pointer; NULL: a store of its own):
+ * the blob's bf16 planes and the Winograd-domain weights (F(4x4) and F(2x2)
+ * slots) are built once for every instance of an engine, whatever image
+ * sizes they serve, and destroying one instance frees no device memory while
+ * another still uses the store (Extractor over many image sizes,
+ * managers/extractor.py:357-382 with datasets/hpatches.py:35-38's crops).
+ * Instances sharing a store may run on different streams: a forward orders
+ * itself after the forward that last built derived weights. */
+int posfeat_model_create_shared(int batch, int h, int w, const float *weights,
+                                posfeat_model *share, posfeat_model **out);
 /* An extraction instance (posfeat_model_create) builds its derived weights --
- * the blob's bf16 planes and the decoder's Winograd-domain weights -- once,
- * in device memory of its own (allocated by its first forward), by the first forward
+ * the blob's bf16 planes and the Winograd-domain weights -- once, in device
+ * memory of its store (allocated by its first forward), by the first forward
  * that needs them.  A caller that rewrites the weight blob in place calls
- * this before the next forward (training instances rebuild them every
- * forward and ignore it). */
+ * this before the next forward: every instance sharing the store rebuilds
+ * (training instances rebuild them every forward and ignore it). */
 int posfeat_model_weights_changed(posfeat_model *m);
 size_t posfeat_model_workspace(const posfeat_model *m);
 int posfeat_model_extract(posfeat_model *m, const float *img_nchw, posfeat_extract_out *out,

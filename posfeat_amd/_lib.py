@@ -154,6 +154,8 @@ SIGNATURES = {
                                         ctypes.POINTER(c_ll)]),
     "posfeat_model_weight_floats": (c_ll, []),
     "posfeat_model_create": (c_int, [c_int, c_int, c_int, c_void_p, ctypes.POINTER(c_void_p)]),
+    "posfeat_model_create_shared": (c_int, [c_int, c_int, c_int, c_void_p, c_void_p,
+                                            ctypes.POINTER(c_void_p)]),
     "posfeat_model_workspace": (c_size_t, [c_void_p]),
     "posfeat_model_extract": (c_int, [c_void_p, c_void_p, ctypes.POINTER(ExtractOut), c_void_p,
                                       c_size_t, c_void_p]),

@@ -93,10 +93,29 @@ const SpecTable& specs() {
 
 struct Buf {
   size_t off = 0, floats = 0;
-  bool persist = false;  // in the instance's own memory (posfeat_model::pbase), not the workspace
+  bool persist = false;  // in the derived-weight store (posfeat_wstore), not the workspace
 };
 
 }  // namespace
+
+// Derived weights of one weight blob (its bf16 planes; the Winograd-domain
+// weights of every Winograd layer, F(4x4) and F(2x2) forms in separate
+// slots), built once and shared by every extraction instance created with
+// posfeat_model_create_shared from one another: an engine meeting many image
+// sizes builds them once instead of once per instance, and an instance
+// leaving the engine's LRU frees no device memory (hipFree synchronises the
+// device).  The layout depends on the weight blob layout only, not the shape.
+// Reference-counted by its instances; freed with the last.
+struct posfeat_wstore {
+  char* base = nullptr;  // allocated by the first forward that needs it
+  size_t bytes = 0;
+  const float* wts = nullptr;
+  bool wsplit = false, bf6p = false;  // the layout's mode: sharers must agree
+  bool wpl_done = false;
+  std::set<std::string> wino_done;  // "<layer>/4" (F(4x4)) or "<layer>/2"
+  hipEvent_t ev = nullptr;          // recorded after the last build
+  int refs = 0;
+};
 
 struct posfeat_model {
   int B, H, W;
@@ -168,19 +187,17 @@ struct posfeat_model {
   // forward of this shape (results do not depend on the tile)
   std::map<std::string, int> tuned;
   bool autotune = true;
-  // derived weights (the blob's bf16 planes, the decoder's Winograd U) of an
-  // extraction instance live in its own device memory (allocated by its first
-  // forward) and are built once:
-  // by the first forward that needs them, again after
+  // derived weights (the blob's bf16 planes, the Winograd U) of an
+  // extraction instance live in a store (posfeat_wstore) it may share with
+  // the other instances of its engine, allocated by the first forward and
+  // built once: by the first forward that needs them, again after
   // posfeat_model_weights_changed (training instances rebuild them every
-  // forward: their weights move every step)
+  // forward in their workspace: their weights move every step)
   bool wcache = false;
-  char* pbase = nullptr;
+  posfeat_wstore* store = nullptr;
   size_t p_bytes = 0;
-  bool wpl_done = false;
-  std::set<std::string> wino_done;
-  hipEvent_t ev_wprep = nullptr;  // recorded after the last derived-weight build
-  bool wprep_pending = false;     // built this forward: record ev_wprep at its end
+  size_t wino_u_f2 = 0;        // floats: the F(2x2) slots after the F(4x4) ones
+  bool wprep_pending = false;  // built this forward: record the store's event at its end
   // timing
   bool timing = false;
   struct Ev {
@@ -200,7 +217,7 @@ struct Ctx {
   hipStream_t st;
   bool dry = false;  // planning pass: record scratch needs, launch nothing
   bool side = false;  // running on the model's side stream (own scratch)
-  char* base(const Buf& b) const { return (b.persist ? m->pbase : ws) + b.off; }
+  char* base(const Buf& b) const { return (b.persist ? m->store->base : ws) + b.off; }
   float* f(const Buf& b) const { return reinterpret_cast<float*>(base(b)); }
   double* d(const Buf& b) const { return reinterpret_cast<double*>(base(b)); }
   const float* W(const std::string& n) const { return m->wts + specs().find(n)->w_off; }
@@ -497,20 +514,22 @@ int conv3x3(Ctx& c, const std::string& name, const float* x, int n, int h, int w
     return conv(c, name, x, n, h, w, xcs, y, ycs, 1, act);
   const Spec* s = specs().find(name);
   if (c.dry) return POSFEAT_OK;
-  float* U = c.f(m->wino_u) + uo;
-  if (!(m->wcache && m->wino_done.count(name))) {
+  // executed transform-domain MACs: F(4x4) 36 per 4x4 tile, F(2x2) 16 per 2x2 tile
+  const bool f4 = h % 4 == 0 && w % 4 == 0 && !(pf_ab_getenv("POSFEAT_WINO") && pf_ab_getenv("POSFEAT_WINO")[0] == '1');
+  // the cached U of this layer in its F(4x4) or F(2x2) slot
+  float* U = c.f(m->wino_u) + uo + (f4 ? 0 : m->wino_u_f2);
+  const std::string ukey = name + (f4 ? "/4" : "/2");
+  if (!(m->wcache && m->store && m->store->wino_done.count(ukey))) {
     PF_TRY(timed(c, "wino:weights", 0,
                  [&] {
                    return pf_wino_weights_hw(c.W(name), s->cout, s->cin, h, w, U, c.st,
                                              m->bf6p || m->wsplit);
                  }));
     if (!c.dry && m->wcache) {
-      m->wino_done.insert(name);
+      m->store->wino_done.insert(ukey);
       m->wprep_pending = true;
     }
   }
-  // executed transform-domain MACs: F(4x4) 36 per 4x4 tile, F(2x2) 16 per 2x2 tile
-  const bool f4 = h % 4 == 0 && w % 4 == 0 && !(pf_ab_getenv("POSFEAT_WINO") && pf_ab_getenv("POSFEAT_WINO")[0] == '1');
   const double T = f4 ? (double)n * (h / 4) * (w / 4) : (double)n * (h / 2) * (w / 2);
   // three launches, timed apart: the input transform, the batched GEMMs
   // (the MFMA work), the output transform (+ bias, activation)
@@ -690,7 +709,9 @@ void plan(posfeat_model* m) {
       wb = std::max(wb, pf_wino_ws_bytes((int)B, (int)H / kWinoDiv[i], (int)W / kWinoDiv[i],
                                          s->cin, s->cout));
     }
-    palloc(m->wino_u, uf);
+    // cached: F(4x4) slots, then F(2x2) slots (a shared store serves every shape)
+    palloc(m->wino_u, m->wcache ? 2 * uf : uf);
+    m->wino_u_f2 = m->wcache ? uf : 0;
     alloc(m->wino_ws, wb / 4 + 4);
   }
   if (m->train && !m->traintap) m->up4 = false;  // the backward reads the materialised conv2 input
@@ -931,12 +952,13 @@ int forward(Ctx& c, const float* img, posfeat_extract_out* out, int mode, const 
   float* img4 = c.f(m->img4);
   float* headcat = c.f(m->headcat);
   // ---- ResUNet (DescNet.py:64-84) -----------------------------------------
-  if (m->wsplit && !(m->wcache && m->wpl_done)) {  // the blob's bf16 planes (pre-split tiles)
+  // (the planning pass runs before the instance has its store)
+  if (m->wsplit && !(m->wcache && m->store && m->store->wpl_done)) {  // the blob's bf16 planes
     PF_TRY(timed(c, "weights.split", 0, [&] {
       return pf_split3_rows(m->wts, specs().total / 4, 4, 4,
                             reinterpret_cast<unsigned short*>(c.f(m->wpl)), c.st);
     }));
-    if (!c.dry && m->wcache) m->wpl_done = m->wprep_pending = true;
+    if (!c.dry && m->wcache) m->store->wpl_done = m->wprep_pending = true;
   }
   PF_TRY(timed(c, "layout:img", 0, [&] { return pf_nchw_to_nhwc(img, B, 3, H, W, 4, img4, c.st); }));
   // the first forward of a shape autotunes every main-stream conv by timing
@@ -1393,10 +1415,18 @@ extern "C" int posfeat_model_conv_spec(int i, const char** name, int* cout, int*
 
 extern "C" long long posfeat_model_weight_floats(void) { return specs().total; }
 
-extern "C" int posfeat_model_create(int batch, int h, int w, const float* weights,
-                                    posfeat_model** out) {
+static void wstore_release(posfeat_wstore* s) {
+  if (!s || --s->refs > 0) return;
+  if (s->ev) (void)hipEventDestroy(s->ev);
+  if (s->base) (void)hipFree(s->base);
+  delete s;
+}
+
+extern "C" int posfeat_model_create_shared(int batch, int h, int w, const float* weights,
+                                           posfeat_model* share, posfeat_model** out) {
   if (!out || !weights || batch <= 0 || h < 16 || w < 16 || h % 16 || w % 16)
     return POSFEAT_E_INVALID;
+  if (share && (!share->wcache || share->wts != weights)) return POSFEAT_E_INVALID;
   posfeat_model* m = new (std::nothrow) posfeat_model();
   if (!m) return POSFEAT_E_INVALID;
   m->B = batch;
@@ -1405,32 +1435,56 @@ extern "C" int posfeat_model_create(int batch, int h, int w, const float* weight
   m->wts = weights;
   m->wcache = true;
   plan(m);  // host only: the derived-weight memory is allocated by the first forward
+  posfeat_wstore* st = share ? share->store : nullptr;
+  if (st && (st->bytes != m->p_bytes || st->wsplit != m->wsplit || st->bf6p != m->bf6p))
+    st = nullptr;  // another layout (precision mode changed between the two): own store
+  if (!st) {
+    st = new (std::nothrow) posfeat_wstore();
+    if (!st) {
+      delete m;
+      return POSFEAT_E_INVALID;
+    }
+    st->bytes = m->p_bytes;
+    st->wts = weights;
+    st->wsplit = m->wsplit;
+    st->bf6p = m->bf6p;
+  }
+  ++st->refs;
+  m->store = st;
   *out = m;
   return POSFEAT_OK;
 }
 
+extern "C" int posfeat_model_create(int batch, int h, int w, const float* weights,
+                                    posfeat_model** out) {
+  return posfeat_model_create_shared(batch, h, w, weights, nullptr, out);
+}
+
 // a forward that built derived weights records where they are complete; a
-// later forward (maybe on another stream) orders itself after that point
+// later forward of any instance sharing the store (maybe on another stream)
+// orders itself after that point
 static int wprep_begin(posfeat_model* m, hipStream_t st) {
-  if (m->wcache && m->p_bytes && !m->pbase) {
-    if (hipMalloc(reinterpret_cast<void**>(&m->pbase), m->p_bytes) != hipSuccess) {
-      m->pbase = nullptr;
+  if (!m->wcache) return POSFEAT_OK;
+  posfeat_wstore* s = m->store;
+  if (s->bytes && !s->base) {
+    if (hipMalloc(reinterpret_cast<void**>(&s->base), s->bytes) != hipSuccess) {
+      s->base = nullptr;
       return POSFEAT_E_HIP;
     }
-    if (hipEventCreateWithFlags(&m->ev_wprep, hipEventDisableTiming) != hipSuccess)
+    if (!s->ev && hipEventCreateWithFlags(&s->ev, hipEventDisableTiming) != hipSuccess)
       return POSFEAT_E_HIP;
   }
-  if (m->wcache && m->ev_wprep && (m->wpl_done || !m->wino_done.empty()))
-    if (hipStreamWaitEvent(st, m->ev_wprep, 0) != hipSuccess) return POSFEAT_E_HIP;
+  if (s->ev && (s->wpl_done || !s->wino_done.empty()))
+    if (hipStreamWaitEvent(st, s->ev, 0) != hipSuccess) return POSFEAT_E_HIP;
   return POSFEAT_OK;
 }
 static int wprep_end(posfeat_model* m, hipStream_t st, int r) {
   if (m->wprep_pending) {
     m->wprep_pending = false;
-    if (r == POSFEAT_OK && hipEventRecord(m->ev_wprep, st) != hipSuccess) return POSFEAT_E_HIP;
+    if (r == POSFEAT_OK && hipEventRecord(m->store->ev, st) != hipSuccess) return POSFEAT_E_HIP;
     if (r != POSFEAT_OK) {  // a failed forward: build them again next time
-      m->wpl_done = false;
-      m->wino_done.clear();
+      m->store->wpl_done = false;
+      m->store->wino_done.clear();
     }
   }
   return r;
@@ -1438,8 +1492,10 @@ static int wprep_end(posfeat_model* m, hipStream_t st, int r) {
 
 extern "C" int posfeat_model_weights_changed(posfeat_model* m) {
   if (!m) return POSFEAT_E_INVALID;
-  m->wpl_done = false;
-  m->wino_done.clear();
+  if (m->store) {  // every instance sharing the store rebuilds
+    m->store->wpl_done = false;
+    m->store->wino_done.clear();
+  }
   return POSFEAT_OK;
 }
 
@@ -1541,8 +1597,7 @@ extern "C" void posfeat_model_destroy(posfeat_model* m) {
   if (m->ev_fork) (void)hipEventDestroy(m->ev_fork);
   if (m->ev_join) (void)hipEventDestroy(m->ev_join);
   if (m->side_st) (void)hipStreamDestroy(m->side_st);
-  if (m->ev_wprep) (void)hipEventDestroy(m->ev_wprep);
-  if (m->pbase) (void)hipFree(m->pbase);
+  wstore_release(m->store);
   delete m;
 }
 

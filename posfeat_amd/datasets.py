@@ -62,6 +62,15 @@ class _FileDataset(Dataset):
     def name_of(self, path):
         raise NotImplementedError
 
+    def item_size(self, item):
+        """(h, w) of item ``item`` after the crop to multiples of 16, from the
+        file header alone (PIL decodes lazily): lets the Extractor size its
+        engine workspace for the whole stream before the first image is decoded."""
+        from PIL import Image
+        with Image.open(self.imfs[item]) as im:
+            w, h = im.size
+        return h - h % 16, w - w % 16
+
     def __getitem__(self, item):
         imf = self.imfs[item]
         if self.uint8_only:
@@ -143,6 +152,10 @@ class SyntheticImages(Dataset):
         x, im = to_input(raw)
         return {"im1": x, "im1_ori": im, "coord1": torch.zeros(0, 2),
                 "name1": "synthetic/%05d.ppm" % item, "pad1": (0, 0, 0, 0)}
+
+    def item_size(self, item):
+        h, w = self.sizes[item % len(self.sizes)] if self.sizes else (self.h, self.w)
+        return h - h % 16, w - w % 16
 
     def __len__(self):
         return self.n

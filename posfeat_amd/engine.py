@@ -50,23 +50,39 @@ class ExtractionEngine:
         self._shared_ws = None       # train=False: one grow-only workspace
         self.max_shapes = max(1, int(os.environ.get("POSFEAT_ENGINE_MAX_SHAPES", "8")))
         self.stats = {"instances_created": 0, "create_s": 0.0, "workspace_grows": 0}
+        # torch's version counter of the blob: an in-place torch write to wdev
+        # (or a view of it, e.g. head_weights()) rebuilds the derived weights
+        # before the next forward
+        self._wver = self.wdev._version
 
     # ------------------------------------------------------------------
     def _instance(self, b, h, w):
         key = (b, h, w)
+        if self._wver != self.wdev._version:   # wdev written in place by a torch op
+            self._wver = self.wdev._version
+            self.weights_changed()
         inst = self._inst.get(key)
         if inst is None:
+            handle = ctypes.c_void_p()
+            t0 = time.perf_counter()
+            if self.train:
+                check(lib().posfeat_model_create_train(b, h, w, ptr(self.wdev),
+                                                       ctypes.byref(handle)))
+            else:
+                # extraction instances share one derived-weight store (bf16
+                # planes, Winograd U): built once per engine, not per shape
+                share = next(iter(self._inst.values()))[0] if self._inst else None
+                check(lib().posfeat_model_create_shared(b, h, w, ptr(self.wdev), share,
+                                                        ctypes.byref(handle)))
+            inst = (handle, int(lib().posfeat_model_workspace(handle)))
+            self.stats["instances_created"] += 1
+            self.stats["create_s"] += time.perf_counter() - t0
+            # the least recently used instances leave after the new one holds
+            # the shared store
             while len(self._inst) >= self.max_shapes:
                 old, (oh, _) = self._inst.popitem(last=False)
                 lib().posfeat_model_destroy(oh)
                 self._own_ws.pop(old, None)
-            handle = ctypes.c_void_p()
-            create = lib().posfeat_model_create_train if self.train else lib().posfeat_model_create
-            t0 = time.perf_counter()
-            check(create(b, h, w, ptr(self.wdev), ctypes.byref(handle)))
-            inst = (handle, int(lib().posfeat_model_workspace(handle)))
-            self.stats["instances_created"] += 1
-            self.stats["create_s"] += time.perf_counter() - t0
             self._inst[key] = inst
         else:
             self._inst.move_to_end(key)
@@ -84,6 +100,28 @@ class ExtractionEngine:
                 ws = self._shared_ws = torch.empty(nbytes + 256, dtype=torch.uint8,
                                                    device=self.device)
         return handle, ws, (-ws.data_ptr()) % 256
+
+    def reserve(self, shapes):
+        """Grow the shared workspace once to the largest need over ``shapes``
+        ((b, h, w) tuples) instead of once per larger shape met: a workspace
+        grow is a device allocation (tens of GB at Aachen / HPatches sizes)
+        taken while the pipeline waits.  Planning a shape is host work only
+        (posfeat_model_create allocates nothing)."""
+        if self.train:
+            return
+        need = self._shared_ws.numel() if self._shared_ws is not None else 0
+        for b, h, w in set(shapes):
+            if (b, h, w) in self._inst:
+                need = max(need, self._inst[(b, h, w)][1] + 256)
+                continue
+            handle = ctypes.c_void_p()
+            check(lib().posfeat_model_create(b, h, w, ptr(self.wdev), ctypes.byref(handle)))
+            need = max(need, int(lib().posfeat_model_workspace(handle)) + 256)
+            lib().posfeat_model_destroy(handle)
+        if self._shared_ws is None or self._shared_ws.numel() < need:
+            self.stats["workspace_grows"] += 1
+            self._shared_ws = None
+            self._shared_ws = torch.empty(need, dtype=torch.uint8, device=self.device)
 
     def weights_changed(self):
         """Call after rewriting ``wdev`` in place: every extraction instance
@@ -242,6 +280,7 @@ class ExtractionEngine:
         """torch.optim.SGD (no momentum) on the head region: w -= lr * grad."""
         check(lib().posfeat_sgd(ptr(self.head_weights()), ptr(grad), self.head_floats,
                                 float(lr), stream_ptr()))
+        self.weights_changed()   # written by a kernel: torch's version counter does not see it
 
     def close(self):
         for handle, _ in self._inst.values():

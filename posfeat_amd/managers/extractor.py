@@ -149,6 +149,14 @@ class Extractor:
         self.model.load_checkpoint(self.config["load_path"])
         self.model.set_eval()
         self.model.engine()   # weight packing (~120 ms) belongs to construction
+        if self._pipelined():
+            # one workspace allocation for the whole stream (its batch shapes
+            # from the file headers), while the workers decode the first
+            # images -- not one allocation per larger size met on the way
+            group = max(1, int(os.environ.get("POSFEAT_EXTRACT_GROUP", "32")))
+            shapes = self._stream_shapes(group)
+            if shapes:
+                self.model.engine().reserve(shapes)
 
         self.logger.info("use {} to detect keypoints".format(self.config["detector"]))
         if os.environ.get("POSFEAT_EXTRACT_TRACE", "0") == "1":
@@ -421,6 +429,11 @@ class Extractor:
         hold = max(group, int(os.environ.get("POSFEAT_EXTRACT_HOLD", str(4 * group))))
         return self._extract_pipelined_run(group, hold)
 
+    @property
+    def _inflight(self):
+        """groups enqueued on the device ahead of the one the host finishes"""
+        return max(1, int(os.environ.get("POSFEAT_EXTRACT_INFLIGHT", "1")))
+
     def _warm_h2d(self):
         """The pinned staging buffers of ``_launch_group`` (two, alternating),
         allocated and copied to the device once here, while the model is built."""
@@ -433,7 +446,27 @@ class Extractor:
             ev.record()
             self._stage.append((buf, ev))
 
+    def _stream_shapes(self, group):
+        """(b, h, w) of the engine batches this stream can launch: per image
+        size of the shard, batches of up to ``group`` images (from the file
+        headers; None when the dataset cannot tell sizes without decoding)."""
+        ds = self.extract_loader.dataset
+        if not hasattr(ds, "item_size"):
+            return None
+        idx = (datasets.ShardSampler(len(ds), self.rank, self.world).idx if self.multi_gpu
+               else range(len(ds)))
+        try:
+            with ThreadPoolExecutor(8) as ex:
+                sizes = list(ex.map(ds.item_size, idx))
+        except Exception:   # unreadable header: the loader reports the file
+            return None
+        count = {}
+        for hw in sizes:
+            count[hw] = count.get(hw, 0) + 1
+        return [(min(group, c), h, w) for (h, w), c in count.items()]
+
     def _extract_pipelined_run(self, group, hold):
+        inflight = self._inflight
         writer = ThreadPoolExecutor(1 if self.save_h5 else 4)
         futures, pending = [], deque()
         buckets = {}
@@ -447,23 +480,44 @@ class Extractor:
         marks = []   # (launch time, images launched so far): steady-state rate
         launched = [0]
 
+        # host-side accounting (no extra synchronisation): time in the loader,
+        # enqueueing groups, waiting for the device, post-processing results
+        acct = {"loader_s": 0.0, "launch_s": 0.0, "device_wait_s": 0.0, "finish_s": 0.0}
+
+        def finish(p):
+            tw = time.perf_counter()
+            p[0].synchronize()
+            tf = time.perf_counter()
+            acct["device_wait_s"] += tf - tw
+            self._finish_group(*p, writer, futures)
+            acct["finish_s"] += time.perf_counter() - tf
+
         def launch(items):
             ta = time.perf_counter()
             marks.append((ta - t0, launched[0]))
             self.group_shapes.append(tuple(items[0][0].shape))
             pending.append(self._launch_group(items))
             launched[0] += len(items)
+            acct["launch_s"] += time.perf_counter() - ta
             if trace:
                 print("[extract] group %d x %s launched in %.1f ms at %.3f s" % (
                     len(items), tuple(items[0][0].shape), 1e3 * (time.perf_counter() - ta),
                     ta - t0), flush=True)
-            while len(pending) > 1:   # keep one group in flight behind the host
-                self._finish_group(*pending.popleft(), writer, futures)
+            while len(pending) > inflight:   # groups in flight behind the host
+                finish(pending.popleft())
 
         held = max_held = 0
         src = self._early_iter if self._early_iter is not None else self._pipelined_loader()
         self._early_iter = None
-        for nbatch, batch in enumerate(src):
+        src = iter(src)
+        nbatch = -1
+        while True:
+            tl = time.perf_counter()
+            batch = next(src, None)
+            acct["loader_s"] += time.perf_counter() - tl
+            if batch is None:
+                break
+            nbatch += 1
             if trace and nbatch < 8:
                 print("[extract] loader batch %d (%d items) at %.3f s" % (
                     nbatch, len(batch), time.perf_counter() - t0), flush=True)
@@ -489,15 +543,18 @@ class Extractor:
             if buckets[key]:
                 launch(buckets.pop(key))
         while pending:
-            self._finish_group(*pending.popleft(), writer, futures)
+            finish(pending.popleft())
+        tw = time.perf_counter()
         for f in futures:
             f.result()
         writer.shutdown()
+        acct["writer_tail_s"] = time.perf_counter() - tw
         self._write_name_list(names)
         dt = time.perf_counter() - t0
         self.stats = {"images": n, "seconds": dt, "images_per_s": n / dt if dt > 0 else 0.0,
                       "stage_ms_per_image": None, "pipeline": True, "group": group,
-                      "group_marks": marks, "max_held": max_held, "hold": hold}
+                      "group_marks": marks, "max_held": max_held, "hold": hold,
+                      "inflight": inflight, "host": {k: round(v, 4) for k, v in acct.items()}}
         self.logger.info("extracted %d images in %.2fs (%.1f images/s, pipelined, %d groups, "
                          "at most %d images held)" % (n, dt, self.stats["images_per_s"],
                                                       len(marks), max_held))

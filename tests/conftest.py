@@ -44,6 +44,21 @@ def ab_env():
     return {"POSFEAT_HIP_LIB": AB_LIB}
 
 
+def run_ab_child(code, out, timeout=300):
+    """Run ``code`` (a Python program that writes the npz ``out``) in a child
+    process on the A/B build, with the repository and tests/ importable;
+    returns the npz contents.  The default GPU suite thus runs every A/B
+    comparison, whatever library the session itself loaded."""
+    import subprocess
+    import numpy as np
+    env = dict(os.environ, **ab_env())
+    env["PYTHONPATH"] = os.pathsep.join([ROOT, os.path.join(ROOT, "tests"),
+                                         env.get("PYTHONPATH", "")])
+    subprocess.run([sys.executable, "-c", code], env=env, check=True, timeout=timeout)
+    d = np.load(out)
+    return {k: d[k] for k in d.files}
+
+
 @pytest.fixture
 def ab(gpu):
     """In-process A/B tests: the session must have loaded the A/B build."""

@@ -203,32 +203,49 @@ def test_disk_loss_sampling_path(gpu):
     assert 0 < c1["n_kps"].item() <= 2 * n
 
 
+# flash (POSFEAT_DISK_FLASH=1, the default) and dense (=0) DiskLoss on the A/B
+# build, in a child process (the shipped library ignores the switch)
+DISK_AB = r"""
+import os, numpy as np, torch
+from posfeat_amd import _lib, ops
+assert _lib.lib().posfeat_ab_build() == 1
+from posfeat_amd.losses import DiskLoss
+from posfeat_amd.training import KeypointTrainStep
+import test_gpu_correlation as T
+tag = %(tag)r
+d, b, H, W, inputs, outputs, _ = T._setup(tag, torch.device("cuda", 0))
+draws = [torch.from_numpy(d["%%s_%%s" %% (tag, k)]) for k in ("prop1", "prop2", "acc1", "acc2")]
+res = {}
+for flag in ("1", "0"):
+    os.environ["POSFEAT_DISK_FLASH"] = flag
+    loss, comp = DiskLoss(T.DISK_CFG)(inputs, outputs, None, draws=draws)
+    kp = torch.cat([outputs["preds1"]["local_point"], outputs["preds2"]["local_point"]], 0)
+    lm = ops.nchw_to_nhwc(torch.cat([outputs["preds1"]["local_map"],
+                                     outputs["preds2"]["local_map"]], 0).contiguous())
+    step = KeypointTrainStep.__new__(KeypointTrainStep)
+    step.cfg, step._ws = dict(T.DISK_CFG), {}
+    out, dkp = step.loss_and_grad(kp, lm, inputs["F1"], inputs["F2"], epoch=0, draws=draws)
+    res["loss" + flag] = np.float64(loss.item())
+    for k, v in comp.items():
+        res["c_%%s_%%s" %% (k, flag)] = np.float64(v.item())
+    res["out" + flag] = out.cpu().numpy()
+    res["dkp" + flag] = dkp.cpu().numpy()
+np.savez(%(out)r, **res)
+"""
+
+
 @pytest.mark.parametrize("tag", ["s", "f"])
-def test_disk_flash_matches_dense_path(ab, tag, monkeypatch):
-    gpu = ab
+def test_disk_flash_matches_dense_path(gpu, tag, tmp_path):
     """The flash DiskLoss (S recomputed by MFMA in four passes, never stored)
     against the S-materialising path (POSFEAT_DISK_FLASH=0) on the same draws:
-    loss, components and the score-map gradients (KeypointTrainStep.loss_and_grad)."""
-    from posfeat_amd.losses import DiskLoss
-    from posfeat_amd.training import KeypointTrainStep
-    from posfeat_amd import ops
-    d, b, H, W, inputs, outputs, _ = _setup(tag, gpu)
-    draws = [torch.from_numpy(d["%s_%s" % (tag, k)]) for k in ("prop1", "prop2", "acc1", "acc2")]
-    res = {}
-    for flag in ("1", "0"):
-        monkeypatch.setenv("POSFEAT_DISK_FLASH", flag)
-        loss, comp = DiskLoss(DISK_CFG)(inputs, outputs, None, draws=draws)
-        kp = torch.cat([outputs["preds1"]["local_point"], outputs["preds2"]["local_point"]], 0)
-        lm = ops.nchw_to_nhwc(torch.cat([outputs["preds1"]["local_map"],
-                                         outputs["preds2"]["local_map"]], 0).contiguous())
-        step = KeypointTrainStep.__new__(KeypointTrainStep)
-        step.cfg, step._ws = dict(DISK_CFG), {}
-        out, dkp = step.loss_and_grad(kp, lm, inputs["F1"], inputs["F2"], epoch=0, draws=draws)
-        res[flag] = (loss.item(), {k: v.item() for k, v in comp.items()}, out.cpu(), dkp.cpu())
-    (l1, c1, o1, g1), (l0, c0, o0, g0) = res["1"], res["0"]
-    np.testing.assert_allclose(l1, l0, rtol=1e-5)
-    for k in c0:
-        np.testing.assert_allclose(c1[k], c0[k], rtol=1e-5, err_msg=k)
-    np.testing.assert_allclose(o1.numpy(), o0.numpy(), rtol=1e-5)
-    scale = float(g0.abs().max())
-    assert float((g1 - g0).abs().max()) <= 1e-5 * scale
+    loss, components and the score-map gradients (KeypointTrainStep.loss_and_grad).
+    Runs on the A/B build in a child process."""
+    from conftest import run_ab_child
+    out = str(tmp_path / "disk_ab.npz")
+    r = run_ab_child(DISK_AB % dict(tag=tag, out=out), out)
+    np.testing.assert_allclose(r["loss1"], r["loss0"], rtol=1e-5)
+    for k in [k for k in r if k.startswith("c_") and k.endswith("_0")]:
+        np.testing.assert_allclose(r[k[:-1] + "1"], r[k], rtol=1e-5, err_msg=k)
+    np.testing.assert_allclose(r["out1"], r["out0"], rtol=1e-5)
+    scale = float(np.abs(r["dkp0"]).max())
+    assert float(np.abs(r["dkp1"] - r["dkp0"]).max()) <= 1e-5 * scale

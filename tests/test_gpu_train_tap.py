@@ -20,7 +20,6 @@ end-to-end step is pinned at the fixture sizes by tests/test_train_kp.py.)
 """
 import numpy as np
 
-from conftest import ab_loaded
 import pytest
 import torch
 
@@ -141,17 +140,34 @@ def _compare(got, ref, what, rel, floor=None):
     return bad
 
 
+# the materialised-input path (POSFEAT_TRAINTAP=0) on the A/B build, in a
+# child process (the shipped library ignores the switch)
+AB_OLD = r"""
+import os, numpy as np, torch
+from posfeat_amd import _lib
+assert _lib.lib().posfeat_ab_build() == 1
+import test_gpu_train_tap as T
+class _Env:
+    def setenv(self, k, v):
+        os.environ[k] = v
+b, H, W = %(shape)r
+imgs, dlp = T._imgs(b, H, W, 700 + H), T._dlp(b, H, W, 7 + W)
+lp, g, _ = T._gpu_grads(torch.device("cuda", 0), _Env(), "0", imgs, dlp)
+np.savez(%(out)r, lp=lp, **{k: np.asarray(v) for k, v in g.items()})
+"""
+
+
 @pytest.mark.parametrize("shape", [(4, 128, 160), (2, 96, 208)])
-def test_traintap_backward(gpu, monkeypatch, shape):
+def test_traintap_backward(gpu, monkeypatch, shape, tmp_path):
+    from conftest import run_ab_child
     b, H, W = shape
     imgs, dlp = _imgs(b, H, W, 700 + H), _dlp(b, H, W, 7 + W)
-    # the materialised-input path (POSFEAT_TRAINTAP=0) exists in the A/B build
-    # only; the shipped library's path is checked against fp64 either way
-    ab = ab_loaded()
     lp_tap, g_tap, x = _gpu_grads(gpu, monkeypatch, "1", imgs, dlp)
-    if ab:
-        lp_old, g_old, _ = _gpu_grads(gpu, monkeypatch, "0", imgs, dlp)
-        np.testing.assert_allclose(lp_tap, lp_old, rtol=1e-4, atol=1e-5)
+    out = str(tmp_path / "traintap_old.npz")
+    d = run_ab_child(AB_OLD % dict(shape=shape, out=out), out)
+    lp_old, g_old = d.pop("lp"), d
+    np.testing.assert_allclose(lp_tap, lp_old, rtol=1e-4, atol=1e-5)
+    ab = True
     g_or = _oracle_grads(imgs, dlp, x)
     # Bound against fp64: 2e-3 of each tensor's scale (the golden test's), or
     # 3x the fp64-measured rounding spread of this input (_rounding_spread:
