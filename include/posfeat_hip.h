@@ -264,6 +264,13 @@ int posfeat_epipolar_loss(int b, int n, const float *F1, const float *F2, const 
  * (coord*, l*_exp_n, w*, w*_std, valid* are read).  dxf1/dxf2: NHWC
  * [b][H/4][W/4] (pixel stride dcs, 128 channels), overwritten.  Scatters
  * accumulate in 64-bit fixed point, so the result is deterministic.
+ * Invariant the query-descriptor gradient relies on: fwd->coord1 / coord2
+ * are the forward's own grid points, point i inside its own grid cell i =
+ * cy (W / grid) + cx (n = (H / grid)(W / grid) points, one per cell, as
+ * posfeat_line2window draws them): each map pixel gathers its gradient from
+ * the cells whose sample can have it as a bilinear corner, so a point moved
+ * outside its cell between the two calls would lose its gradient (the
+ * descriptor-training step never edits them).
  * weight_grid != 0 returns POSFEAT_E_UNSUPPORTED. */
 size_t posfeat_line2window_backward_workspace(int b, int H1, int W1, int H2, int W2, int grid);
 int posfeat_line2window_backward(const float *xf1, int cs1, const float *xf2, int cs2, int b,

@@ -194,7 +194,34 @@ def lib():
             fn.restype = res
             fn.argtypes = args
         _lib = L
+        _warn_ab_switches(L)
     return _lib
+
+
+# path switches only the A/B build reads (common.h pf_ab_getenv); the shipped
+# library ignores them -- say so instead of silently running the default path
+# (POSFEAT_BF6=0 used to select fp32-MFMA convs)
+AB_ONLY_SWITCHES = (
+    "POSFEAT_BF6", "POSFEAT_BF6B", "POSFEAT_BF6D", "POSFEAT_BF6X", "POSFEAT_BF6X_RB4",
+    "POSFEAT_BF6_HALO", "POSFEAT_BF6_STEM", "POSFEAT_CONV_KERNEL", "POSFEAT_CONV_MAXSPLIT",
+    "POSFEAT_DISK_FLASH", "POSFEAT_GEMM_B256", "POSFEAT_GFUSE", "POSFEAT_GFUSE_BLOCKS",
+    "POSFEAT_GFUSE_K80", "POSFEAT_HEADFUSE", "POSFEAT_HEAD_UP4", "POSFEAT_IMGSTATS",
+    "POSFEAT_S2PHASE", "POSFEAT_SIDE", "POSFEAT_SIDE_AT", "POSFEAT_TRAINTAP",
+    "POSFEAT_TUNE_SIMILAR", "POSFEAT_UP2FUSE", "POSFEAT_UP4TAP", "POSFEAT_UP4WINO",
+    "POSFEAT_WGRAD_BF6", "POSFEAT_WGRAD_BF6_ALL", "POSFEAT_WINO", "POSFEAT_WINO_ENC",
+    "POSFEAT_WINPATCH")
+
+
+def _warn_ab_switches(L):
+    if L.posfeat_ab_build() == 1:
+        return
+    on = [k for k in AB_ONLY_SWITCHES if k in os.environ]
+    if on:
+        import warnings
+        warnings.warn("%s set but %s is the shipped build, which ignores these A/B path "
+                      "switches (build `make -C posfeat_amd/csrc ab` and set POSFEAT_HIP_LIB; "
+                      "the conv precision is posfeat_set_conv_precision)"
+                      % (", ".join(on), os.path.basename(LIB_PATH)), RuntimeWarning, stacklevel=3)
 
 
 def check(code):

@@ -72,10 +72,7 @@ def _staging_buffer(n):
     The caching host allocator hands out whole hipHostMalloc blocks (page
     aligned); the advice covers the pages inside the tensor."""
     buf = torch.empty(n, dtype=torch.uint8, pin_memory=True)
-    page = mmap.PAGESIZE
-    a = buf.data_ptr()
-    lo = (a + page - 1) // page * page
-    hi = (a + n) // page * page
+    lo, hi = _page_range(buf)
     if hi > lo and _libc().madvise(ctypes.c_void_p(lo), ctypes.c_size_t(hi - lo),
                                    _MADV_DONTFORK) != 0:
         raise OSError(ctypes.get_errno(), "madvise(MADV_DONTFORK) on the staging buffer")
@@ -83,6 +80,21 @@ def _staging_buffer(n):
 
 
 _MADV_DONTFORK = 10   # <sys/mman.h>, Linux
+_MADV_DOFORK = 11
+
+
+def _page_range(buf):
+    page = mmap.PAGESIZE
+    a, n = buf.data_ptr(), buf.numel()
+    return (a + page - 1) // page * page, (a + n) // page * page
+
+
+def _release_staging_buffer(buf):
+    """Undo _staging_buffer's MADV_DONTFORK before the buffer returns to torch's
+    caching host allocator, whose next user may rely on fork inheriting it."""
+    lo, hi = _page_range(buf)
+    if hi > lo:
+        _libc().madvise(ctypes.c_void_p(lo), ctypes.c_size_t(hi - lo), _MADV_DOFORK)
 
 
 @functools.lru_cache(None)
@@ -139,7 +151,8 @@ class Extractor:
         # in a fresh process, 3.2 s with a 25 GB engine workspace resident,
         # 0.6 ms with no fork or with the workers forked at this point)
         self._early_iter = iter(self._pipelined_loader()) if self._pipelined() else None
-        self._warm_h2d()   # async: overlaps the model construction below
+        if self._early_iter is not None:
+            self._warm_h2d()   # async: overlaps the model construction below
         self.set_folder_and_logger()
 
         tmp_model = getattr(networks, self.config["model"])
@@ -307,6 +320,8 @@ class Extractor:
             if done is not None:
                 done.synchronize()   # the H2D that last read this buffer has finished
             if buf is None or buf.numel() < n:
+                if buf is not None:   # back to the shared pinned cache fork-inheritable
+                    _release_staging_buffer(buf)
                 buf = _staging_buffer(max(n, 2 * (buf.numel() if buf is not None else 0)))
             st = buf[:n].view(shape)
             for i, it in enumerate(items):
