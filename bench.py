@@ -647,7 +647,18 @@ def train_desc_main(args, world, rank, dev, emit=True):
     cls = {k: tr.timing(k) for k in ("fwd:conv", "fwd:bn", "fwd:misc", "bwd:bn", "bwd:wgrad",
                                       "bwd:dgrad", "bwd:misc")}
     all_ms = tr.timing("")[0]
+    # the conv classes per layer (labels "<class>:<layer>"), largest first
+    by_layer = {}
+    for lab, ms, fl in tr.timing_events():
+        if lab.count(":") >= 2:
+            e = by_layer.setdefault(lab, [0.0, 0.0, 0])
+            e[0] += ms
+            e[1] += fl
+            e[2] += 1
     tr.set_timing(False)
+    top_layers = [{"label": k, "ms": round(v[0], 3), "launches": v[2],
+                   "tflops": round(v[1] / max(v[0], 1e-9) / 1e9, 1)}
+                  for k, v in sorted(by_layer.items(), key=lambda kv: -kv[1][0])[:16]]
     dom = max(("fwd:conv", "bwd:wgrad", "bwd:dgrad"), key=lambda k: cls[k][0])
     d_ms, d_fl, d_n = cls[dom]
     ach = d_fl / (d_ms * 1e-3) / 1e12
@@ -679,6 +690,7 @@ def train_desc_main(args, world, rank, dev, emit=True):
                          "avg_launch_ms": round(d_ms / max(d_n, 1), 4),
                          "flop_per_launch": d_fl / max(d_n, 1)},
             "breakdown_ms": {k: round(v[0], 3) for k, v in cls.items()},
+            "top_conv_layers": top_layers,
             "conv_total": {"ms_per_step": round(conv_ms, 3),
                            "tflops": round(conv_fl / (conv_ms * 1e-3) / 1e12, 3),
                            "backbone_kernels_ms": round(all_ms, 3)},

@@ -501,6 +501,11 @@ int posfeat_bbtrain_backward(posfeat_bbtrain *m, const float *params, const void
 int posfeat_bbtrain_set_timing(posfeat_bbtrain *m, int enable);
 int posfeat_bbtrain_timing(posfeat_bbtrain *m, const char *prefix, double *ms, double *flops,
                            int *launches);
+/* The i-th timed launch of the last timed step (labels "fwd:conv:<layer>",
+ * "bwd:wgrad:<layer>", "bwd:dgrad:<layer>", "fwd:bn", ...): label, ms, flops;
+ * POSFEAT_E_INVALID past the last.  Host-synchronises. */
+int posfeat_bbtrain_timing_event(posfeat_bbtrain *m, int i, const char **label, double *ms,
+                                 double *flops);
 void posfeat_bbtrain_destroy(posfeat_bbtrain *m);
 int posfeat_adam(float *p, const float *g, float *m, float *v, long long n, float lr, float beta1,
                  float beta2, float eps, float weight_decay, long long step, float grad_scale,

@@ -131,6 +131,9 @@ SIGNATURES = {
     "posfeat_bbtrain_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
                                          c_int, c_void_p, c_void_p]),
     "posfeat_bbtrain_set_timing": (c_int, [c_void_p, c_int]),
+    "posfeat_bbtrain_timing_event": (c_int, [c_void_p, c_int, ctypes.POINTER(ctypes.c_char_p),
+                                             ctypes.POINTER(ctypes.c_double),
+                                             ctypes.POINTER(ctypes.c_double)]),
     "posfeat_bbtrain_timing": (c_int, [c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
                                        ctypes.POINTER(ctypes.c_double), P_int]),
     "posfeat_bbtrain_destroy": (None, [c_void_p]),

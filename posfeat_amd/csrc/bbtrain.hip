@@ -233,7 +233,7 @@ struct Ctx {
 };
 
 template <class F>
-int timed(Ctx& c, const char* label, double flops, F&& fn) {
+int timed(Ctx& c, const std::string& label, double flops, F&& fn) {
   posfeat_bbtrain* m = c.m;
   if (!m->timing) return fn();
   if (m->ev_used == m->evs.size()) {
@@ -455,7 +455,7 @@ int layer_fwd(Ctx& c, int li, const float* x, int xcs, int h, int w, float* out,
   posfeat_conv_desc d = make_desc(m->B, h, w, L.cin, xcs, L.cout, L.k, L.stride, L.cout, 0);
   if (use_wino(m, li, h, w)) {
     float* U = c.s(m->wu);
-    PF_TRY(timed(c, "fwd:conv", wino_flops(m->B, h, w, L.cin, L.cout), [&] {
+    PF_TRY(timed(c, std::string("fwd:conv:") + L.name, wino_flops(m->B, h, w, L.cin, L.cout), [&] {
       PF_TRY(pf_wino_weights_hw(c.prm + L.w_off, L.cout, L.cin, h, w, U, c.st,
                                 m->bf6p || m->wsplit));
       return pf_wino_conv(x, xcs, m->B, h, w, L.cin, U, c.prm + L.b_off, L.cout, ACT_NONE, y,
@@ -463,7 +463,7 @@ int layer_fwd(Ctx& c, int li, const float* x, int xcs, int h, int w, float* out,
                           m->bf6p ? 2 : m->wsplit ? 1 : 0);
     }));
   } else {
-    PF_TRY(timed(c, "fwd:conv", 2.0 * P * L.cout * L.cin * L.k * L.k, [&] {
+    PF_TRY(timed(c, std::string("fwd:conv:") + L.name, 2.0 * P * L.cout * L.cin * L.k * L.k, [&] {
       return pf_conv_run_tile(&d, x, c.prm + L.w_off, L.bias ? c.prm + L.b_off : nullptr, nullptr,
                               y, c.s(m->splitk), m->splitk.bytes, -1, c.st,
                               m->wsplit ? c.su(m->wpl) + L.w_off : nullptr, tab().params);
@@ -564,13 +564,13 @@ int layer_bwd(Ctx& c, int li, const float* x, int xcs, int h, int w, const float
   const double flops = 2.0 * P * C * L.cin * L.k * L.k;
   const int cinp = (L.cin + 3) / 4 * 4;
   if (use_wino(m, li, h, w) && h % 4 == 0 && w % 4 == 0 && L.cin % 128 == 0 && C % 128 == 0) {
-    PF_TRY(timed(c, "bwd:wgrad", wino_flops(B, h, w, L.cin, C, true), [&] {
+    PF_TRY(timed(c, std::string("bwd:wgrad:") + L.name, wino_flops(B, h, w, L.cin, C, true), [&] {
       return pf_wino_wgrad(dy, C, x, xcs, B, h, w, L.cin, C, grad + L.w_off,
                            L.bias ? grad + L.b_off : nullptr, acc, c.s(m->wino_ws),
                            m->wino_ws.bytes, c.st);
     }));
   } else {
-    PF_TRY(timed(c, "bwd:wgrad", flops, [&] {
+    PF_TRY(timed(c, std::string("bwd:wgrad:") + L.name, flops, [&] {
       return pf_conv_wgrad(dy, C, x, xcs, B, h, w, cinp, C, L.k, L.k, L.stride, grad + L.w_off,
                            L.bias ? grad + L.b_off : nullptr, acc, c.s(m->wgws), m->wgws.bytes,
                            c.st);
@@ -604,7 +604,7 @@ int layer_bwd(Ctx& c, int li, const float* x, int xcs, int h, int w, const float
       PF_TRY(timed(c, "bwd:misc", 0, [&] {
         return pf_split3_rows(wt, wrows, (int)wcols, (int)wcols, c.su(m->wtp), c.st);
       }));
-    PF_TRY(timed(c, "bwd:dgrad", pf, [&] {
+    PF_TRY(timed(c, std::string("bwd:dgrad:") + L.name, pf, [&] {
       return pf_conv_run_tile(&d, dy, wt, nullptr, nullptr, dz, c.s(m->splitk), m->splitk.bytes,
                               -1, c.st, m->wsplit ? c.su(m->wtp) : nullptr, wrows * wcols);
     }));
@@ -631,7 +631,7 @@ int layer_bwd(Ctx& c, int li, const float* x, int xcs, int h, int w, const float
   }));
   if (!add && use_wino(m, li, h, w)) {
     float* U = c.s(m->wu);
-    return timed(c, "bwd:dgrad", wino_flops(B, h, w, C, L.cin), [&] {
+    return timed(c, std::string("bwd:dgrad:") + L.name, wino_flops(B, h, w, C, L.cin), [&] {
       PF_TRY(pf_wino_weights_hw(wt, L.cin, C, h, w, U, c.st, m->bf6p || m->wsplit));
       return pf_wino_conv(src, C, B, h, w, C, U, nullptr, L.cin, ACT_NONE, dx, dxcs,
                           c.s(m->wino_ws), m->wino_ws.bytes, c.st, 7,
@@ -644,7 +644,7 @@ int layer_bwd(Ctx& c, int li, const float* x, int xcs, int h, int w, const float
     PF_TRY(timed(c, "bwd:misc", 0, [&] {
       return pf_split3_rows(wt, L.cin, (int)wcols, (int)wcols, c.su(m->wtp), c.st);
     }));
-  return timed(c, "bwd:dgrad", flops, [&] {
+  return timed(c, std::string("bwd:dgrad:") + L.name, flops, [&] {
     return pf_conv_run_tile(&d, src, wt, nullptr, add, dx, c.s(m->splitk), m->splitk.bytes, -1,
                             c.st, m->wsplit ? c.su(m->wtp) : nullptr, (long long)L.cin * wcols);
   });
@@ -925,6 +925,21 @@ extern "C" int posfeat_bbtrain_timing(posfeat_bbtrain* m, const char* prefix, do
   if (ms) *ms = t;
   if (flops) *flops = f;
   if (launches) *launches = k;
+  return POSFEAT_OK;
+}
+
+// the i-th timed launch of the last timed step: label ("fwd:conv:<layer>",
+// "bwd:wgrad:<layer>", ...), ms, flops; POSFEAT_E_INVALID past the last
+extern "C" int posfeat_bbtrain_timing_event(posfeat_bbtrain* m, int i, const char** label,
+                                            double* ms, double* flops) {
+  if (!m || i < 0 || (size_t)i >= m->ev_used) return POSFEAT_E_INVALID;
+  auto& e = m->evs[i];
+  if (hipEventSynchronize(e.b) != hipSuccess) return POSFEAT_E_HIP;
+  float dt = 0.f;
+  if (hipEventElapsedTime(&dt, e.a, e.b) != hipSuccess) return POSFEAT_E_HIP;
+  if (label) *label = e.label.c_str();
+  if (ms) *ms = dt;
+  if (flops) *flops = e.flops;
   return POSFEAT_OK;
 }
 

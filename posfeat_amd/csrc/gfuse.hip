@@ -79,11 +79,15 @@ __global__ __launch_bounds__(128) void gfuse_weights_kernel(
 
 // Border ring: y[p] = b2 + sum_t sum_k W2[:, 192+k, t] G[p+t-1][k], G = rstd (c - mean)
 // inside the image, 0 outside (conv2's zero padding).  One workgroup = RP ring
-// pixels x 128 couts; the G taps go through LDS, W2 (transposed, w2t[t][k][co])
-// is read coalesced across couts and reused for the RP pixels.  y == nullptr:
+// pixels x 128 couts; W2 (transposed, w2t[t][k][co], 295 KB) is read coalesced
+// across couts once per block and reused for the RP pixels, so RP sets the
+// weight traffic: 64 pixels per block (16 before: 4480 blocks re-read 1.3 GB of
+// w2t from L2 per 32-image step, 1.06 ms).  The G taps go through LDS one
+// conv2 tap t at a time (g[RP][64], 16 KB): the sums run in the same order as
+// before -- t outer, k inner -- so the values are bit-identical.  y == nullptr:
 // into the ring buffer ring[b][r][128] instead (r = the ring index below, the
 // order pf_ring_index in fmap.h restates), for up4tap_gcombine_kernel.
-constexpr int GF_RP = 16;  // ring pixels per block (w2t, 295 KB, is read once per block)
+constexpr int GF_RP = 64;  // ring pixels per block
 __global__ __launch_bounds__(2 * GF_COUT) void gfuse_ring_kernel(
     const float* __restrict__ c, int ccs, const float* __restrict__ img4,
     const float* __restrict__ w1, int k1pad, const float* __restrict__ b1, int H, int W,
@@ -91,10 +95,11 @@ __global__ __launch_bounds__(2 * GF_COUT) void gfuse_ring_kernel(
     const float* __restrict__ b2, float* __restrict__ y, int ycs, float* __restrict__ ring) {
   const int b = blockIdx.y, co = threadIdx.x % GF_COUT;
   const int nring = 2 * W + 2 * (H - 2);
-  __shared__ __attribute__((aligned(16))) float g[GF_RP][9][GF_CG];
-  // convimg's input taps at every (ring pixel, conv2 tap) position, loaded
-  // once per block (the 64 channel threads share them): xs[j][t][s * 3 + ch]
-  __shared__ float xs[GF_RP][9][27];
+  __shared__ __attribute__((aligned(16))) float g[GF_RP][GF_CG];
+  // convimg's input taps at every ring pixel's position q = p + t - 1 of the
+  // current conv2 tap, loaded once per block (the 64 channel threads share
+  // them): xs[j][s * 3 + ch]
+  __shared__ float xs[GF_RP][27];
   __shared__ float w1s[GF_CG][27];
   __shared__ int pys[GF_RP], pxs[GF_RP];
   if (threadIdx.x < GF_RP) {
@@ -123,63 +128,66 @@ __global__ __launch_bounds__(2 * GF_COUT) void gfuse_ring_kernel(
       w1s[k][e] = w1[(size_t)k * k1pad + (e / 3) * 4 + e % 3];
     }
   }
-  __syncthreads();
-  if (!c) {  // zero-padded image taps around each tap position q (0 outside the image)
-    for (int i = threadIdx.x; i < GF_RP * 9 * 27; i += blockDim.x) {
-      const int j = i / 243, rem = i - j * 243, t = rem / 27, e = rem - t * 27;
-      const int s9 = e / 3, ch = e - s9 * 3;
-      const int qy = pys[j] + t / 3 - 1, qx = pxs[j] + t % 3 - 1;
-      const int iy = qy + s9 / 3 - 1, ix = qx + s9 % 3 - 1;
-      float v = 0.f;
-      if (pys[j] >= 0 && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
-        v = img4[(((size_t)b * H + iy) * W + ix) * 4 + ch];
-      xs[j][t][e] = v;
-    }
-    __syncthreads();
-  }
   const float* mb = mean + (size_t)b * GF_CG;
   const float* rb = rstd + (size_t)b * GF_CG;
-  for (int i = threadIdx.x; i < GF_RP * 9 * GF_CG; i += blockDim.x) {
-    const int j = i / (9 * GF_CG), rem = i - j * 9 * GF_CG, t = rem / GF_CG, k = rem - t * GF_CG;
-    const int py = pys[j], px = pxs[j];
-    const int qy = py + t / 3 - 1, qx = px + t % 3 - 1;
-    float v = 0.f;
-    if (py >= 0 && (unsigned)qy < (unsigned)H && (unsigned)qx < (unsigned)W) {
-      float cv;
-      if (c) {
-        cv = c[(((size_t)b * H + qy) * W + qx) * ccs + k];
-      } else {  // convimg at q, the conv's own tap order (zero taps add +0: exact)
-        cv = b1[k];
-        for (int s9 = 0; s9 < 9; ++s9) {
-          const float* xv = &xs[j][t][s9 * 3];
-          const float* wk = &w1s[k][s9 * 3];
-          cv += wk[0] * xv[0] + wk[1] * xv[1] + wk[2] * xv[2];
-        }
-      }
-      v = (cv - mb[k]) * rb[k];
-    }
-    g[j][t][k] = v;
-  }
-  __syncthreads();
   // two halves of the block take GF_RP / 2 ring pixels each (same cout)
   constexpr int HP = GF_RP / 2;
   const int j0 = (threadIdx.x / GF_COUT) * HP;
   float acc[HP];
+  const float bias = b2[co];
 #pragma unroll
-  for (int j = 0; j < HP; ++j) acc[j] = b2[co];
-  // four k per step: one broadcast ds_read_b128 of g per pixel, the same
-  // sequential accumulation order as one k at a time
-  for (int tk = 0; tk < 9 * GF_CG; tk += 4) {
-    float wv[4];
+  for (int j = 0; j < HP; ++j) acc[j] = bias;
+  for (int t = 0; t < 9; ++t) {
+    __syncthreads();  // pys / w1s written; the previous tap's g and xs read
+    if (!c) {  // zero-padded image taps around q (0 outside the image)
+      for (int i = threadIdx.x; i < GF_RP * 27; i += blockDim.x) {
+        const int jj = i / 27, e = i - jj * 27;
+        const int s9 = e / 3, ch = e - s9 * 3;
+        const int qy = pys[jj] + t / 3 - 1, qx = pxs[jj] + t % 3 - 1;
+        const int iy = qy + s9 / 3 - 1, ix = qx + s9 % 3 - 1;
+        float v = 0.f;
+        if (pys[jj] >= 0 && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
+          v = img4[(((size_t)b * H + iy) * W + ix) * 4 + ch];
+        xs[jj][e] = v;
+      }
+      __syncthreads();
+    }
+    for (int i = threadIdx.x; i < GF_RP * GF_CG; i += blockDim.x) {
+      const int jj = i / GF_CG, k = i - jj * GF_CG;
+      const int py = pys[jj], px = pxs[jj];
+      const int qy = py + t / 3 - 1, qx = px + t % 3 - 1;
+      float v = 0.f;
+      if (py >= 0 && (unsigned)qy < (unsigned)H && (unsigned)qx < (unsigned)W) {
+        float cv;
+        if (c) {
+          cv = c[(((size_t)b * H + qy) * W + qx) * ccs + k];
+        } else {  // convimg at q, the conv's own tap order (zero taps add +0: exact)
+          cv = b1[k];
+          for (int s9 = 0; s9 < 9; ++s9) {
+            const float* xv = &xs[jj][s9 * 3];
+            const float* wk = &w1s[k][s9 * 3];
+            cv += wk[0] * xv[0] + wk[1] * xv[1] + wk[2] * xv[2];
+          }
+        }
+        v = (cv - mb[k]) * rb[k];
+      }
+      g[jj][k] = v;
+    }
+    __syncthreads();
+    // four k per step: one broadcast ds_read_b128 of g per pixel, the same
+    // sequential accumulation order as one k at a time
+    for (int k = 0; k < GF_CG; k += 4) {
+      float wv[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) wv[u] = w2t[(size_t)(tk + u) * GF_COUT + co];
+      for (int u = 0; u < 4; ++u) wv[u] = w2t[(size_t)(t * GF_CG + k + u) * GF_COUT + co];
 #pragma unroll
-    for (int j = 0; j < HP; ++j) {
-      const f32x4 gv = *reinterpret_cast<const f32x4*>(&g[j0 + j][0][0] + tk);
-      acc[j] += wv[0] * gv.x;
-      acc[j] += wv[1] * gv.y;
-      acc[j] += wv[2] * gv.z;
-      acc[j] += wv[3] * gv.w;
+      for (int j = 0; j < HP; ++j) {
+        const f32x4 gv = *reinterpret_cast<const f32x4*>(&g[j0 + j][k]);
+        acc[j] += wv[0] * gv.x;
+        acc[j] += wv[1] * gv.y;
+        acc[j] += wv[2] * gv.z;
+        acc[j] += wv[3] * gv.w;
+      }
     }
   }
   if (!y) {

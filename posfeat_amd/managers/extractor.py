@@ -326,6 +326,7 @@ class Extractor:
             st = buf[:n].view(shape)
             for i, it in enumerate(items):
                 st[i].copy_(it[1])
+            self._acct_add("stage_s", t0)
             u8 = torch.empty(shape, dtype=torch.uint8, device=dev)
             if trace:
                 torch.cuda.synchronize(dev)
@@ -353,6 +354,7 @@ class Extractor:
             torch.cuda.synchronize(dev)
         t2 = time.perf_counter()
         out = eng.run(im, outputs=())
+        self._acct_add("engine_s", t2)
         if trace:
             torch.cuda.synchronize(dev)
         t3 = time.perf_counter()
@@ -378,6 +380,7 @@ class Extractor:
             i = j
         ev = torch.cuda.Event()
         ev.record()
+        self._acct_add("detect_s", t3)
         if trace:
             torch.cuda.synchronize(dev)
             print("[extract]   upload+normalise %.1f ms, engine() %.1f ms, run %.1f ms, "
@@ -385,6 +388,11 @@ class Extractor:
                       1e3 * (t1 - t0), 1e3 * (t2 - t1), 1e3 * (t3 - t2),
                       1e3 * (time.perf_counter() - t3)), flush=True)
         return ev, host
+
+    def _acct_add(self, key, since):
+        acct = getattr(self, "_acct", None)
+        if acct is not None:
+            acct[key] = acct.get(key, 0.0) + time.perf_counter() - since
 
     def _finish_group(self, ev, host, writer, futures):
         ev.synchronize()
@@ -422,6 +430,8 @@ class Extractor:
             ds.uint8_only = True
         cfg = self.config["data_config_extract"]
         workers = int(os.environ.get("POSFEAT_EXTRACT_WORKERS", cfg.get("workers", 4) or 0))
+        nwriter = int(os.environ.get("POSFEAT_EXTRACT_WRITERS", "4"))
+        self._nwriters = max(1, nwriter)
         lb = max(1, int(os.environ.get("POSFEAT_EXTRACT_LOAD_BATCH", "8")))
         sampler = (datasets.ShardSampler(len(ds), self.rank, self.world)
                    if self.multi_gpu else None)
@@ -482,7 +492,7 @@ class Extractor:
 
     def _extract_pipelined_run(self, group, hold):
         inflight = self._inflight
-        writer = ThreadPoolExecutor(1 if self.save_h5 else 4)
+        writer = ThreadPoolExecutor(1 if self.save_h5 else getattr(self, "_nwriters", 4))
         futures, pending = [], deque()
         buckets = {}
         self.group_shapes = []
@@ -498,6 +508,7 @@ class Extractor:
         # host-side accounting (no extra synchronisation): time in the loader,
         # enqueueing groups, waiting for the device, post-processing results
         acct = {"loader_s": 0.0, "launch_s": 0.0, "device_wait_s": 0.0, "finish_s": 0.0}
+        self._acct = acct   # launch_s split into stage_s / engine_s / detect_s (+ upload)
 
         def finish(p):
             tw = time.perf_counter()

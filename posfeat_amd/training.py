@@ -360,6 +360,18 @@ class BackboneTrainer:
                                            ctypes.byref(fl), ctypes.byref(n)))
         return ms.value, fl.value, n.value
 
+    def timing_events(self):
+        """[(label, ms, flops)] of every timed launch of the last timed step
+        (host-synchronises)."""
+        import ctypes
+        out, i = [], 0
+        lab, ms, fl = ctypes.c_char_p(), ctypes.c_double(), ctypes.c_double()
+        while lib().posfeat_bbtrain_timing_event(self._h, i, ctypes.byref(lab), ctypes.byref(ms),
+                                                 ctypes.byref(fl)) == 0:
+            out.append((lab.value.decode(), ms.value, fl.value))
+            i += 1
+        return out
+
     def state_dict(self):
         """backbone.pth contents (reference key order, PoSFeat_model.py:74-81)."""
         from . import weights
