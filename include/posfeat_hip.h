@@ -398,6 +398,15 @@ int posfeat_model_create_shared(int batch, int h, int w, const float *weights,
  * (training instances rebuild them every forward and ignore it). */
 int posfeat_model_weights_changed(posfeat_model *m);
 size_t posfeat_model_workspace(const posfeat_model *m);
+/* The process-wide conv tile choices (the engine's autotuner: tiles never
+ * change results, only speed) as text, one "<descriptor class>|<n>/<h>/<w>
+ * <tile>" line each: export writes them into buf (cap bytes; *len = bytes
+ * needed incl. the NUL; buf NULL: size query), import adds lines not yet
+ * known and returns how many.  A tuning database kept between processes
+ * (records/tile_db.txt): a new image size within 25 % of a stored GEMM M
+ * reuses its tile instead of timing every candidate. */
+int posfeat_tile_cache_export(char *buf, size_t cap, size_t *len);
+int posfeat_tile_cache_import(const char *text);
 int posfeat_model_extract(posfeat_model *m, const float *img_nchw, posfeat_extract_out *out,
                           void *ws, size_t ws_bytes, void *stream);
 /* ResUNet.forward alone (networks/DescNet.py:64-84): fills out->local_map,

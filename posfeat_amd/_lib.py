@@ -157,6 +157,8 @@ SIGNATURES = {
                                         ctypes.POINTER(c_ll)]),
     "posfeat_model_weight_floats": (c_ll, []),
     "posfeat_model_create": (c_int, [c_int, c_int, c_int, c_void_p, ctypes.POINTER(c_void_p)]),
+    "posfeat_tile_cache_export": (c_int, [ctypes.c_char_p, c_size_t, ctypes.POINTER(c_size_t)]),
+    "posfeat_tile_cache_import": (c_int, [ctypes.c_char_p]),
     "posfeat_model_create_shared": (c_int, [c_int, c_int, c_int, c_void_p, c_void_p,
                                             ctypes.POINTER(c_void_p)]),
     "posfeat_model_workspace": (c_size_t, [c_void_p]),

@@ -375,6 +375,46 @@ void tile_store(const posfeat_conv_desc& d, bool res, bool wplanes, int tile) {
   if (t.exact.emplace(cls + nhw, tile).second) t.by_class[cls].push_back({desc_m(d), tile});
 }
 
+// The process-wide tile choices as text, one "<class>|<n>/<h>/<w> <tile>"
+// line per entry (posfeat_tile_cache_export), and back
+// (posfeat_tile_cache_import): a tuning database the caller keeps between
+// processes, so a stream of image sizes is not timed conv by conv again
+// (managers/extractor.py: records/tile_db.txt).  The similar-shape reuse then
+// covers every shape within 25 % of a stored M.
+std::string tile_cache_text() {
+  TileCache& t = tile_cache();
+  std::lock_guard<std::mutex> g(t.mu);
+  std::string out;
+  for (auto& e : t.exact) out += e.first + " " + std::to_string(e.second) + "\n";
+  return out;
+}
+int tile_cache_load(const char* text) {
+  int n = 0;
+  const char* p = text;
+  while (p && *p) {
+    const char* eol = strchr(p, '\n');
+    const std::string line(p, eol ? eol - p : strlen(p));
+    p = eol ? eol + 1 : nullptr;
+    const size_t sp = line.rfind(' '), bar = line.rfind('|');
+    if (sp == std::string::npos || bar == std::string::npos || bar > sp) continue;
+    int nn, hh, ww;
+    if (sscanf(line.c_str() + bar + 1, "%d/%d/%d", &nn, &hh, &ww) != 3) continue;
+    const std::string key = line.substr(0, sp), cls = line.substr(0, bar);
+    const int tile = atoi(line.c_str() + sp + 1);
+    // M of the entry from its class's kernel and stride: (h + 2p - k) / s + 1 per side
+    int kh = 1, kw = 1, st = 1, pad = 0;
+    if (sscanf(cls.c_str(), "%*d/%*d/%*d/%dx%d/s%d/p%d", &kh, &kw, &st, &pad) != 4) continue;
+    const double m = (double)nn * ((hh + 2 * pad - kh) / st + 1) * ((ww + 2 * pad - kw) / st + 1);
+    TileCache& t = tile_cache();
+    std::lock_guard<std::mutex> g(t.mu);
+    if (t.exact.emplace(key, tile).second) {
+      t.by_class[cls].push_back({m, tile});
+      ++n;
+    }
+  }
+  return n;
+}
+
 // run (autotuned on the first forward of the instance, keyed by `key`) one
 // conv described by d with packed weights w
 // wb / wplane: the weights' bf16 planes (default: w's planes in the
@@ -1500,6 +1540,20 @@ extern "C" int posfeat_model_weights_changed(posfeat_model* m) {
 }
 
 extern "C" size_t posfeat_model_workspace(const posfeat_model* m) { return m ? m->ws_bytes : 0; }
+
+extern "C" int posfeat_tile_cache_export(char* buf, size_t cap, size_t* len) {
+  const std::string t = tile_cache_text();
+  if (len) *len = t.size() + 1;
+  if (!buf) return POSFEAT_OK;
+  if (cap < t.size() + 1) return POSFEAT_E_WORKSPACE;
+  memcpy(buf, t.c_str(), t.size() + 1);
+  return POSFEAT_OK;
+}
+
+extern "C" int posfeat_tile_cache_import(const char* text) {
+  if (!text) return POSFEAT_E_INVALID;
+  return tile_cache_load(text);
+}
 
 extern "C" int posfeat_model_extract(posfeat_model* m, const float* img_nchw,
                                      posfeat_extract_out* out, void* ws, size_t ws_bytes,

@@ -48,6 +48,32 @@ def _read(path):
     return np.asarray(Image.open(path).convert("RGB"))
 
 
+def _ppm_header(f):
+    """(width, height, data offset) of a binary RGB PPM (P6, maxval 255) from
+    open file ``f``, else None (the caller decodes with PIL)."""
+    head = f.read(512)
+    if head[:2] != b"P6":
+        return None
+    vals, i, n = [], 2, len(head)
+    while len(vals) < 3:
+        while i < n and head[i:i + 1].isspace():
+            i += 1
+        if i < n and head[i:i + 1] == b"#":   # comment to the end of the line
+            while i < n and head[i:i + 1] not in (b"\n", b"\r"):
+                i += 1
+            continue
+        j = i
+        while j < n and head[j:j + 1].isdigit():
+            j += 1
+        if j == i:
+            return None
+        vals.append(int(head[i:j]))
+        i = j
+    if i >= n or not head[i:i + 1].isspace() or vals[2] != 255:
+        return None
+    return vals[0], vals[1], i + 1
+
+
 class _FileDataset(Dataset):
     """``uint8_only`` (set by the pipelined Extractor): items carry only the
     cropped uint8 image, its name and index -- the float normalisation runs on
@@ -65,11 +91,39 @@ class _FileDataset(Dataset):
     def item_size(self, item):
         """(h, w) of item ``item`` after the crop to multiples of 16, from the
         file header alone (PIL decodes lazily): lets the Extractor size its
-        engine workspace for the whole stream before the first image is decoded."""
+        engine workspace and plan its batches before any image is decoded."""
         from PIL import Image
         with Image.open(self.imfs[item]) as im:
             w, h = im.size
         return h - h % 16, w - w % 16
+
+    def item_name(self, item):
+        return self.name_of(self.imfs[item])
+
+    def read_into(self, item, out):
+        """Decode item ``item`` cropped to multiples of 16 into ``out`` (uint8
+        [h16][w16][3], C-contiguous: a slice of the Extractor's pinned staging
+        buffer), exactly the bytes crop16(_read(path)) gives.  Binary RGB PPM
+        with maxval 255 (HPatches) is raw RGB after its header: the rows are
+        read straight into ``out`` (no decode, no intermediate copy when the
+        width needs no crop); everything else goes through PIL."""
+        path = self.imfs[item]
+        h16, w16 = out.shape[0], out.shape[1]
+        with open(path, "rb") as f:
+            hdr = _ppm_header(f)
+            if hdr is not None:
+                w, h, off = hdr
+                if h - h % 16 == h16 and w - w % 16 == w16:
+                    f.seek(off)
+                    if w == w16:
+                        n = f.readinto(memoryview(out).cast("B"))
+                    else:
+                        tmp = np.empty((h16, w, 3), np.uint8)
+                        n = f.readinto(memoryview(tmp).cast("B"))
+                        out[...] = tmp[:, :w16]
+                    if n == h16 * w * 3:
+                        return
+        out[...] = crop16(_read(path))
 
     def __getitem__(self, item):
         imf = self.imfs[item]
@@ -156,6 +210,14 @@ class SyntheticImages(Dataset):
     def item_size(self, item):
         h, w = self.sizes[item % len(self.sizes)] if self.sizes else (self.h, self.w)
         return h - h % 16, w - w % 16
+
+    def item_name(self, item):
+        return "synthetic/%05d.ppm" % item
+
+    def read_into(self, item, out):
+        rs = np.random.RandomState(1000 + item)
+        h, w = self.sizes[item % len(self.sizes)] if self.sizes else (self.h, self.w)
+        out[...] = crop16(rs.randint(0, 256, (h, w, 3)).astype(np.uint8))
 
     def __len__(self):
         return self.n

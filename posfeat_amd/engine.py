@@ -28,12 +28,48 @@ from . import _lib, weights
 from ._lib import check, lib, ptr, stream_ptr
 
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TILE_DB = os.path.join(ROOT, "records", "tile_db.txt")
+_tile_db_loaded = False
+
+
+def tile_db_export(path):
+    """Write the process-wide conv tile choices (posfeat_tile_cache_export)."""
+    need = ctypes.c_size_t()
+    check(lib().posfeat_tile_cache_export(None, 0, ctypes.byref(need)))
+    buf = ctypes.create_string_buffer(need.value)
+    check(lib().posfeat_tile_cache_export(buf, need.value, ctypes.byref(need)))
+    with open(path, "w") as f:
+        f.write(buf.value.decode())
+    return buf.value.decode().count("\n")
+
+
+def tile_db_import(path):
+    """Add a tile database's entries to the process-wide choices; returns how many."""
+    with open(path) as f:
+        return int(lib().posfeat_tile_cache_import(f.read().encode()))
+
+
+def _load_tile_db():
+    """Once per process: the tuning database shipped in records/ (made by
+    tools/tile_db.py on an MI355X; POSFEAT_TILE_DB = another file, or 0 for
+    none).  Tiles never change results, only which candidate runs."""
+    global _tile_db_loaded
+    if _tile_db_loaded:
+        return
+    _tile_db_loaded = True
+    path = os.environ.get("POSFEAT_TILE_DB", TILE_DB)
+    if path != "0" and os.path.exists(path):
+        tile_db_import(path)
+
+
 class ExtractionEngine:
     """``train=True`` builds instances that keep the head's intermediates for
     ``head_backward`` (keypoint-head training, configs/train_kp.yaml)."""
 
     def __init__(self, backbone_sd=None, head_sd=None, device="cuda", blob=None, train=False):
         _lib.require_device()
+        _load_tile_db()
         self.train = bool(train)
         self.device = torch.device(device)
         self.specs = _lib.model_specs()

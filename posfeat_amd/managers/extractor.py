@@ -104,6 +104,62 @@ def _libc():
     return libc
 
 
+class _StagedReader:
+    """Reads each planned batch's images straight into a pinned staging buffer
+    with a thread pool (the file reads release the GIL), ``ahead`` batches
+    ahead of the one the device takes next.  ahead + 1 buffers in a ring: a
+    buffer is refilled once the H2D copy that read it has finished."""
+
+    def __init__(self, ds, groups, threads, ahead):
+        self.ds, self.groups, self.ahead = ds, groups, ahead
+        self.pool = ThreadPoolExecutor(threads)
+        self.ring = [[None, None] for _ in range(ahead + 1)]   # [buffer, H2D event]
+        self.work = {}
+        self.next = 0
+
+    def _submit(self, gi):
+        (h, w), idxs = self.groups[gi]
+        shape = (len(idxs), h, w, 3)
+        n = len(idxs) * h * w * 3
+        slot = self.ring[gi % len(self.ring)]
+        if slot[1] is not None:
+            slot[1].synchronize()   # the H2D of the batch that used this buffer is done
+            slot[1] = None
+        if slot[0] is None or slot[0].numel() < n:
+            if slot[0] is not None:
+                _release_staging_buffer(slot[0])
+            slot[0] = _staging_buffer(max(n, 2 * (slot[0].numel() if slot[0] is not None else 0)))
+        st = slot[0][:n].view(shape)
+        arr = st.numpy()
+        self.work[gi] = (st, [self.pool.submit(self.ds.read_into, i, arr[k])
+                              for k, i in enumerate(idxs)])
+
+    def get(self, gi):
+        """batch gi's filled staging view (keeps the next batches reading)"""
+        while self.next < min(len(self.groups), gi + self.ahead + 1):
+            self._submit(self.next)
+            self.next += 1
+        st, futs = self.work.pop(gi)
+        for f in futs:
+            f.result()
+        return st
+
+    def done_h2d(self, gi, ev):
+        self.ring[gi % len(self.ring)][1] = ev
+
+    def close(self):
+        for _, futs in self.work.values():
+            for f in futs:
+                f.cancel()
+        self.pool.shutdown(wait=True)
+        for slot in self.ring:
+            if slot[1] is not None:
+                slot[1].synchronize()
+            if slot[0] is not None:
+                _release_staging_buffer(slot[0])
+        self.ring = []
+
+
 class Extractor:
     def __init__(self, args):
         self.args = args
@@ -150,7 +206,9 @@ class Extractor:
         # on the device (r11i-r11l: the first upload after a fork took 236 ms
         # in a fresh process, 3.2 s with a 25 GB engine workspace resident,
         # 0.6 ms with no fork or with the workers forked at this point)
-        self._early_iter = iter(self._pipelined_loader()) if self._pipelined() else None
+        self._staged = self._pipelined() and self._staged_ok()
+        self._early_iter = (iter(self._pipelined_loader())
+                            if self._pipelined() and not self._staged else None)
         if self._early_iter is not None:
             self._warm_h2d()   # async: overlaps the model construction below
         self.set_folder_and_logger()
@@ -170,6 +228,10 @@ class Extractor:
             shapes = self._stream_shapes(group)
             if shapes:
                 self.model.engine().reserve(shapes)
+            elif self._staged:   # sizes unknown: the loader path after all
+                self._staged = False
+                self._early_iter = iter(self._pipelined_loader())
+                self._warm_h2d()
 
         self.logger.info("use {} to detect keypoints".format(self.config["detector"]))
         if os.environ.get("POSFEAT_EXTRACT_TRACE", "0") == "1":
@@ -304,9 +366,9 @@ class Extractor:
 
     def _launch_group(self, items):
         """Engine + detector + sampler for a list of same-size images, all
-        enqueued on the current stream; returns (event, per-image host copies)."""
+        enqueued on the current stream; returns (event, per-image host copies).
+        items: (float image, uint8 image, name, scale)."""
         dev = self.device
-        trace = os.environ.get("POSFEAT_EXTRACT_TRACE", "0") == "1"
         t0 = time.perf_counter()
         # the group's uint8 images go through this extractor's own pinned
         # staging buffer (two, alternating, excluded from fork: see
@@ -327,31 +389,32 @@ class Extractor:
             for i, it in enumerate(items):
                 st[i].copy_(it[1])
             self._acct_add("stage_s", t0)
-            u8 = torch.empty(shape, dtype=torch.uint8, device=dev)
-            if trace:
-                torch.cuda.synchronize(dev)
-                ta = time.perf_counter()
-            u8.copy_(st, non_blocking=True)
-            ev_copy = torch.cuda.Event()
-            ev_copy.record()
+            im, ev_copy = self._upload(st)
             self._stage[k] = (buf, ev_copy)
-            if trace:
-                torch.cuda.synchronize(dev)
-                tb = time.perf_counter()
-                print("[extract]   stage %.1f ms, H2D %.1f ms" % (
-                    1e3 * (ta - t0), 1e3 * (tb - ta)), flush=True)
-            im = ops.normalize_rgb8(u8)
         else:
             im = torch.empty((len(items),) + tuple(items[0][0].shape), device=dev)
             for i, it in enumerate(items):
                 im[i].copy_(it[0], non_blocking=True)
+        return self._launch_device(im, [it[2] for it in items], [it[3] for it in items], t0)
+
+    def _upload(self, st):
+        """async H2D of a filled pinned staging view [g][h][w][3] uint8 and the
+        on-device ImageNet normalisation (bit-identical to the host transform);
+        returns (normalised [g][3][h][w] float, event after the copy)"""
+        u8 = torch.empty(tuple(st.shape), dtype=torch.uint8, device=self.device)
+        u8.copy_(st, non_blocking=True)
+        ev_copy = torch.cuda.Event()
+        ev_copy.record()
+        return ops.normalize_rgb8(u8), ev_copy
+
+    def _launch_device(self, im, names, scales, t0):
+        dev = self.device
+        trace = os.environ.get("POSFEAT_EXTRACT_TRACE", "0") == "1"
         g, _, h, w = im.shape
         if trace:
             torch.cuda.synchronize(dev)
         t1 = time.perf_counter()
         eng = self.model.engine()
-        if trace:
-            torch.cuda.synchronize(dev)
         t2 = time.perf_counter()
         out = eng.run(im, outputs=())
         self._acct_add("engine_s", t2)
@@ -365,9 +428,9 @@ class Extractor:
         # config (Aachen query / db), each image selected as if alone
         i = 0
         while i < g:
-            cfg = self._det_cfg(items[i][2])
+            cfg = self._det_cfg(names[i])
             j = i + 1
-            while j < g and self._det_cfg(items[j][2]) is cfg:
+            while j < g and self._det_cfg(names[j]) is cfg:
                 j += 1
             coord_n, score, n_sel = putils.generate_kpts_each_async(
                 out["local_point"][i:j], **cfg)
@@ -376,16 +439,16 @@ class Extractor:
             hs = (n_sel.to("cpu", non_blocking=True), coord_n.to("cpu", non_blocking=True),
                   desc.to("cpu", non_blocking=True), score.to("cpu", non_blocking=True))
             for k in range(i, j):
-                host.append((items[k][2], items[k][3], hs, k - i, w, h))
+                host.append((names[k], scales[k], hs, k - i, w, h))
             i = j
         ev = torch.cuda.Event()
         ev.record()
         self._acct_add("detect_s", t3)
         if trace:
             torch.cuda.synchronize(dev)
-            print("[extract]   upload+normalise %.1f ms, engine() %.1f ms, run %.1f ms, "
+            print("[extract]   upload+normalise %.1f ms, run %.1f ms, "
                   "detect/sample/D2H %.1f ms (synchronised)" % (
-                      1e3 * (t1 - t0), 1e3 * (t2 - t1), 1e3 * (t3 - t2),
+                      1e3 * (t1 - t0), 1e3 * (t3 - t2),
                       1e3 * (time.perf_counter() - t3)), flush=True)
         return ev, host
 
@@ -440,6 +503,34 @@ class Extractor:
             ds, batch_size=lb, shuffle=False, num_workers=workers, sampler=sampler,
             collate_fn=lambda b: [x for x in b if x is not None], pin_memory=False, **kw)
 
+    @staticmethod
+    def _plan_groups(order, sizes, group, hold):
+        """The pipelined loop's batches, planned from the header sizes: images
+        bucketed by size in stream order, a bucket launched when it holds
+        ``group`` images, the fullest one early once ``hold`` images wait, the
+        rest at the end -- the decisions the loader-driven loop takes as the
+        images arrive.  Returns [((h, w), [item indices])] and the most images
+        held at once."""
+        groups, buckets, held, max_held = [], {}, 0, 0
+        for i in order:
+            key = sizes[i]
+            b = buckets.setdefault(key, [])
+            b.append(i)
+            held += 1
+            max_held = max(max_held, held)
+            if len(b) >= group:
+                groups.append((key, b))
+                buckets[key] = []
+                held -= len(b)
+            elif held >= hold:
+                key = max(buckets, key=lambda k: len(buckets[k]))
+                held -= len(buckets[key])
+                groups.append((key, buckets.pop(key)))
+        for key in list(buckets):
+            if buckets[key]:
+                groups.append((key, buckets.pop(key)))
+        return groups, max_held
+
     def _extract_pipelined(self):
         """Images are grouped BY SHAPE across the whole stream (one bucket per
         size, a bucket runs as one engine batch when it holds
@@ -452,7 +543,81 @@ class Extractor:
         (default 4 groups) wait, the fullest bucket launches early."""
         group = max(1, int(os.environ.get("POSFEAT_EXTRACT_GROUP", "32")))
         hold = max(group, int(os.environ.get("POSFEAT_EXTRACT_HOLD", str(4 * group))))
+        if self._staged:
+            return self._extract_staged_run(group, hold)
         return self._extract_pipelined_run(group, hold)
+
+    def _extract_staged_run(self, group, hold):
+        """The pipelined loop fed by the staged reader: the batches are planned
+        from the file headers (_plan_groups: the same grouping as the
+        loader-driven loop), and a thread pool decodes each planned batch's
+        images straight into a pinned staging buffer (datasets' read_into: a
+        binary PPM's rows are read into place), ``POSFEAT_EXTRACT_AHEAD``
+        batches (default 2) ahead of the device.  No decode processes, no
+        inter-process copy of the images, no host copy into the staging
+        buffer: the host work per batch is the reads, one H2D and the launches."""
+        inflight = self._inflight
+        ds = self.extract_loader.dataset
+        groups, max_held = self._plan_groups(self._order, self._sizes, group, hold)
+        threads = max(1, int(os.environ.get("POSFEAT_EXTRACT_READERS", "8")))
+        ahead = max(1, int(os.environ.get("POSFEAT_EXTRACT_AHEAD", "2")))
+        reader = _StagedReader(ds, groups, threads, ahead)
+        writer = ThreadPoolExecutor(1 if self.save_h5 else getattr(self, "_nwriters", 4))
+        futures, pending = [], deque()
+        self.group_shapes = []
+        marks, launched = [], 0
+        acct = {"loader_s": 0.0, "launch_s": 0.0, "device_wait_s": 0.0, "finish_s": 0.0}
+        self._acct = acct
+        t0 = time.perf_counter()
+        trace = os.environ.get("POSFEAT_EXTRACT_TRACE", "0") == "1"
+
+        def finish(p):
+            tw = time.perf_counter()
+            p[0].synchronize()
+            tf = time.perf_counter()
+            acct["device_wait_s"] += tf - tw
+            self._finish_group(*p, writer, futures)
+            acct["finish_s"] += time.perf_counter() - tf
+
+        try:
+            for gi, ((h, w), idxs) in enumerate(groups):
+                tl = time.perf_counter()
+                st = reader.get(gi)
+                ta = time.perf_counter()
+                acct["loader_s"] += ta - tl
+                marks.append((ta - t0, launched))
+                self.group_shapes.append((h, w, 3))
+                im, ev_copy = self._upload(st)
+                reader.done_h2d(gi, ev_copy)
+                pending.append(self._launch_device(im, [ds.item_name(i) for i in idxs],
+                                                   [None] * len(idxs), ta))
+                launched += len(idxs)
+                acct["launch_s"] += time.perf_counter() - ta
+                if trace:
+                    print("[extract] group %d x %s launched in %.1f ms at %.3f s" % (
+                        len(idxs), (h, w, 3), 1e3 * (time.perf_counter() - ta), ta - t0),
+                        flush=True)
+                while len(pending) > inflight:
+                    finish(pending.popleft())
+            while pending:
+                finish(pending.popleft())
+        finally:
+            reader.close()
+        tw = time.perf_counter()
+        for f in futures:
+            f.result()
+        writer.shutdown()
+        acct["writer_tail_s"] = time.perf_counter() - tw
+        n = len(self._order)
+        self._write_name_list([(i, ds.item_name(i)) for i in self._order])
+        dt = time.perf_counter() - t0
+        self.stats = {"images": n, "seconds": dt, "images_per_s": n / dt if dt > 0 else 0.0,
+                      "stage_ms_per_image": None, "pipeline": True, "reader": "staged",
+                      "group": group, "group_marks": marks, "max_held": max_held, "hold": hold,
+                      "inflight": inflight, "host": {k: round(v, 4) for k, v in acct.items()}}
+        self.logger.info("extracted %d images in %.2fs (%.1f images/s, pipelined, staged reader, "
+                         "%d groups)" % (n, dt, self.stats["images_per_s"], len(marks)))
+        return n
 
     @property
     def _inflight(self):
@@ -471,20 +636,30 @@ class Extractor:
             ev.record()
             self._stage.append((buf, ev))
 
+    def _staged_ok(self):
+        """the staged reader (_extract_staged_run) serves datasets that decode
+        an item into a given buffer and tell its size from the header"""
+        ds = self.extract_loader.dataset
+        return (os.environ.get("POSFEAT_EXTRACT_READER", "staged") != "loader"
+                and hasattr(ds, "read_into") and hasattr(ds, "item_size")
+                and hasattr(ds, "item_name"))
+
     def _stream_shapes(self, group):
         """(b, h, w) of the engine batches this stream can launch: per image
         size of the shard, batches of up to ``group`` images (from the file
-        headers; None when the dataset cannot tell sizes without decoding)."""
+        headers; None when the dataset cannot tell sizes without decoding).
+        Keeps the shard's order and sizes for the staged reader."""
         ds = self.extract_loader.dataset
         if not hasattr(ds, "item_size"):
             return None
-        idx = (datasets.ShardSampler(len(ds), self.rank, self.world).idx if self.multi_gpu
-               else range(len(ds)))
+        idx = list(datasets.ShardSampler(len(ds), self.rank, self.world).idx if self.multi_gpu
+                   else range(len(ds)))
         try:
             with ThreadPoolExecutor(8) as ex:
                 sizes = list(ex.map(ds.item_size, idx))
         except Exception:   # unreadable header: the loader reports the file
             return None
+        self._order, self._sizes = idx, dict(zip(idx, sizes))
         count = {}
         for hw in sizes:
             count[hw] = count.get(hw, 0) + 1

@@ -260,3 +260,69 @@ def test_gloo_syncbn_group_bootstrap_world2():
         assert created == (2, rank, want)
         assert handle == 1000 + rank
         assert not refused
+
+
+def test_extract_plan_groups_matches_loader_bucketing():
+    """The staged reader's batches (Extractor._plan_groups, from the header
+    sizes) are the batches the loader-driven loop forms as images arrive:
+    same bucketing, group and hold rules, same order."""
+    import random
+    from posfeat_amd.managers.extractor import Extractor
+    rnd = random.Random(3)
+    for group, hold, nsizes in ((32, 128, 3), (4, 5, 6), (6, 24, 40), (1, 1, 2)):
+        order = list(range(300))
+        pool = [(480, 640), (592, 800), (752, 992)] + [(16 * (30 + j), 16 * (40 + j))
+                                                       for j in range(nsizes)]
+        sizes = {i: pool[rnd.randrange(nsizes)] for i in order}
+        groups, max_held = Extractor._plan_groups(order, sizes, group, hold)
+        # the loader-driven loop (_extract_pipelined_run), restated
+        ref, buckets, held = [], {}, 0
+        for i in order:
+            key = sizes[i]
+            b = buckets.setdefault(key, [])
+            b.append(i)
+            held += 1
+            if len(b) >= group:
+                ref.append((key, b))
+                buckets[key] = []
+                held -= len(b)
+            elif held >= hold:
+                k = max(buckets, key=lambda k: len(buckets[k]))
+                held -= len(buckets[k])
+                ref.append((k, buckets.pop(k)))
+        ref += [(k, v) for k, v in buckets.items() if v]
+        assert groups == ref
+        assert sorted(i for _, g in groups for i in g) == order
+        assert max_held <= hold
+
+
+def test_dataset_read_into_matches_decode(tmp_path):
+    """read_into (the staged reader's decode: binary PPM rows read in place,
+    else PIL) gives exactly crop16(_read(path)), for widths that need and
+    need not a crop, a header comment, and a non-PPM file."""
+    import numpy as np
+    from PIL import Image
+    from posfeat_amd import datasets
+    d = tmp_path / "seq"
+    d.mkdir()
+    rs = np.random.RandomState(0)
+    for k, (h, w) in enumerate([(480, 640), (500, 650), (97, 33)]):
+        Image.fromarray(rs.randint(0, 256, (h, w, 3)).astype(np.uint8)).save(str(d / ("%d.ppm" % k)))
+    a = rs.randint(0, 256, (64, 80, 3)).astype(np.uint8)
+    (d / "8.ppm").write_bytes(b"P6\n# comment\n80 64\n255\n" + a.tobytes())
+    Image.fromarray(rs.randint(0, 256, (50, 70)).astype(np.uint8)).save(str(d / "9.ppm"))  # P5
+    ds = datasets.HPatch_SIFT({"data_path": str(tmp_path)})
+    assert len(ds) == 5
+    for i in range(len(ds)):
+        h, w = ds.item_size(i)
+        out = np.empty((h, w, 3), np.uint8)
+        ds.read_into(i, out)
+        np.testing.assert_array_equal(out, datasets.crop16(datasets._read(ds.imfs[i])))
+    syn = datasets.SyntheticImages({"num_images": 3, "sizes": [[40, 50], [32, 48]]})
+    for i in range(3):
+        h, w = syn.item_size(i)
+        out = np.empty((h, w, 3), np.uint8)
+        syn.read_into(i, out)
+        syn.uint8_only = True
+        np.testing.assert_array_equal(out, syn[i]["im1_ori"].numpy())
+        assert syn.item_name(i) == syn[i]["name1"]
