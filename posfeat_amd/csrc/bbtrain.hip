@@ -871,6 +871,16 @@ extern "C" size_t posfeat_bbtrain_scratch_bytes(const posfeat_bbtrain* m) {
   return m ? m->scr_bytes : 0;
 }
 
+// POSFEAT_TRAIN_HALO_BF6=1 (A/B build): the 3x3 stride-1 convs on their
+// bf16x6 halo tiles instead of fp32 MFMA (speed / fixture-error probe)
+static bool train_halo_fp32() {
+  static const bool fp32 = [] {
+    const char* e = pf_ab_getenv("POSFEAT_TRAIN_HALO_BF6");
+    return !(e && e[0] == '1');
+  }();
+  return fp32;
+}
+
 extern "C" int posfeat_bbtrain_forward(posfeat_bbtrain* m, const float* params, float* stats,
                                        float momentum, const float* img_nchw, void* act,
                                        void* scratch, float** local_map_nhwc, void* stream) {
@@ -879,7 +889,8 @@ extern "C" int posfeat_bbtrain_forward(posfeat_bbtrain* m, const float* params, 
       (reinterpret_cast<uintptr_t>(params) & 15) || (reinterpret_cast<uintptr_t>(stats) & 15))
     return POSFEAT_E_INVALID;
   Ctx c{m, static_cast<char*>(act), static_cast<char*>(scratch), pf_stream(stream), params};
-  const PfHaloFp32Scope halo32;  // fp32 halo tiles: the fixture-validated numerics
+  // fp32 halo tiles: the fixture-validated numerics
+  const PfHaloFp32Scope halo32(train_halo_fp32());
   PF_TRY(forward(c, img_nchw, stats, momentum));
   if (local_map_nhwc) *local_map_nhwc = c.f(m->fa);
   return POSFEAT_OK;
@@ -895,7 +906,7 @@ extern "C" int posfeat_bbtrain_backward(posfeat_bbtrain* m, const float* params,
     return POSFEAT_E_INVALID;
   Ctx c{m, static_cast<char*>(const_cast<void*>(act)), static_cast<char*>(scratch),
         pf_stream(stream), params};
-  const PfHaloFp32Scope halo32;
+  const PfHaloFp32Scope halo32(train_halo_fp32());
   return backward(c, dlocal_map_nhwc, dcs, grad, accumulate ? 1 : 0);
 }
 

@@ -31,6 +31,20 @@ __device__ __forceinline__ float act_fwd(int act, float z) {
   return act == ACT_RELU ? fmaxf(z, 0.f) : act == ACT_ELU ? pf_elu(z) : z;
 }
 
+// (batch, row, column) of pixel p of an [n][h][w] map, 32-bit when p fits
+__device__ __forceinline__ int pix_split(long long p, int w, int h, int& x, int& y) {
+  if ((unsigned long long)p <= 0xffffffffULL) {
+    const unsigned pu = (unsigned)p, r = pu / (unsigned)w, b = r / (unsigned)h;
+    x = (int)(pu - r * (unsigned)w);
+    y = (int)(r - b * (unsigned)h);
+    return (int)b;
+  }
+  x = (int)(p % w);
+  const long long r = p / w;
+  y = (int)(r % h);
+  return (int)(r / h);
+}
+
 template <int MODE>
 __global__ __launch_bounds__(256) void bn_partial_kernel(
     const float* __restrict__ y, long long P, int C, int chunk, const float* __restrict__ a, int acs,
@@ -53,7 +67,50 @@ __global__ __launch_bounds__(256) void bn_partial_kernel(
       bt = *reinterpret_cast<const f32x4*>(bet + q * 4);
     }
   }
-  for (long long p = p0 + r; p < p1; p += R) {
+  // U rows per trip with every load issued before the first add (one 16-byte
+  // load per lane in flight left the pass at ~2.5 TB/s); the adds keep the
+  // row order p, p + R, ... so the sums are the same bits as one row per trip
+  constexpr int U = MODE == 0 ? 4 : 2;
+  const float* ap = (MODE == 1 && act != ACT_NONE) ? a : nullptr;
+  long long p = p0 + r;
+  for (; p + (U - 1) * R < p1; p += U * R) {
+    f32x4 v[U], gd[U], av[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long pu = p + u * R;
+      v[u] = *reinterpret_cast<const f32x4*>(y + pu * C + q * 4);
+      if (MODE == 1) {
+        gd[u] = *reinterpret_cast<const f32x4*>(da + pu * dacs + q * 4);
+        if (ap) av[u] = *reinterpret_cast<const f32x4*>(ap + pu * acs + q * 4);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (MODE == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          s0[j] += (double)v[u][j];
+          s1[j] += (double)v[u][j] * (double)v[u][j];
+        }
+      } else {
+        if (act == ACT_NONE) {
+          av[u] = f32x4{0, 0, 0, 0};
+        } else if (!ap) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            av[u][j] = act_fwd(act, bn_z(gm[j], v[u][j], mu[j], rs[j], bt[j]));
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float g = gd[u][j] * act_grad(act, av[u][j]);
+          const float xh = (v[u][j] - mu[j]) * rs[j];
+          s0[j] += (double)g;
+          s1[j] += (double)g * (double)xh;
+        }
+      }
+    }
+  }
+  for (; p < p1; p += R) {
     const f32x4 v = *reinterpret_cast<const f32x4*>(y + p * C + q * 4);
     if (MODE == 0) {
 #pragma unroll
@@ -108,11 +165,27 @@ __device__ __forceinline__ void bn_chunk_sum(const double* __restrict__ part, in
   const int cl = threadIdx.x & 3, kl = threadIdx.x >> 2;
   const int c = blockIdx.x * 4 + cl;
   double a = 0.0, b = 0.0;
-  if (c < C)
-    for (int k = kl; k < nchunk; k += 64) {
+  if (c < C) {
+    // four chunks' loads in flight per trip, added in chunk order
+    int k = kl;
+    for (; k + 3 * 64 < nchunk; k += 4 * 64) {
+      double va[4], vb[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        va[u] = part[(long long)(k + u * 64) * 2 * C + c];
+        vb[u] = part[(long long)(k + u * 64) * 2 * C + C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a += va[u];
+        b += vb[u];
+      }
+    }
+    for (; k < nchunk; k += 64) {
       a += part[(long long)k * 2 * C + c];
       b += part[(long long)k * 2 * C + C + c];
     }
+  }
   red[0][kl][cl] = a;
   red[1][kl][cl] = b;
   __syncthreads();
@@ -223,8 +296,8 @@ __global__ void bn_apply_kernel(const float* __restrict__ y, long long P, int c4
   const long long total = P * c4n;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
-    const int q = (int)(i % c4n);
-    const long long p = i / c4n;
+    long long p;
+    const int q = pf_quad_split(i, c4n, p);
     const f32x4 v = *reinterpret_cast<const f32x4*>(y + i * 4);
     const f32x4 mu = *reinterpret_cast<const f32x4*>(mean + q * 4);
     const f32x4 rs = *reinterpret_cast<const f32x4*>(rstd + q * 4);
@@ -269,8 +342,8 @@ __global__ void bn_bwd_apply_kernel(const float* __restrict__ y, long long P, in
   const long long total = P * c4n;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
-    const int q = (int)(i % c4n);
-    const long long p = i / c4n;
+    long long p;
+    const int q = pf_quad_split(i, c4n, p);
     const f32x4 v = *reinterpret_cast<const f32x4*>(y + i * 4);
     const f32x4 gd = *reinterpret_cast<const f32x4*>(da + p * dacs + q * 4);
     const f32x4 mu = *reinterpret_cast<const f32x4*>(mean + q * 4);
@@ -339,12 +412,10 @@ __global__ void s2_scatter_kernel(const float* __restrict__ src, int mode, int n
   const long long total = (long long)n * h * w * c4n;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
-    const int q = (int)(i % c4n);
-    const long long p = i / c4n;
-    const int ix = (int)(p % w);
-    const long long r = p / w;
-    const int iy = (int)(r % h);
-    const int b = (int)(r / h);
+    long long p;
+    const int q = pf_quad_split(i, c4n, p);
+    int ix, iy;
+    const int b = pix_split(p, w, h, ix, iy);
     f32x4 v = {0, 0, 0, 0};
     if (mode == 1) {
       const int t = (iy + 1) >> 1, s = (ix + 1) >> 1;
@@ -368,12 +439,10 @@ __global__ void zero_insert_kernel(const float* __restrict__ src, int n, int h, 
   const long long total = (long long)n * h * w * c4n;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
-    const int q = (int)(i % c4n);
-    long long p = i / c4n;
-    const int x = (int)(p % w);
-    p /= w;
-    const int yy = (int)(p % h);
-    const int b = (int)(p / h);
+    long long p;
+    const int q = pf_quad_split(i, c4n, p);
+    int x, yy;
+    const int b = pix_split(p, w, h, x, yy);
     f32x4 v = {0, 0, 0, 0};
     if (!(x & 1) && !(yy & 1))
       v = *reinterpret_cast<const f32x4*>(
@@ -392,12 +461,10 @@ __global__ void maxpool_adjoint_kernel(const float* __restrict__ x, int xcs, int
   const long long total = (long long)n * h * w * c4n;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
-    const int q = (int)(i % c4n);
-    long long p = i / c4n;
-    const int ix = (int)(p % w);
-    p /= w;
-    const int iy = (int)(p % h);
-    const int b = (int)(p / h);
+    long long p;
+    const int q = pf_quad_split(i, c4n, p);
+    int ix, iy;
+    const int b = pix_split(p, w, h, ix, iy);
     const float* xb = x + (long long)b * h * w * xcs + q * 4;
     f32x4 acc = {0, 0, 0, 0};
     const int oy0 = iy / 2, oy1 = min(oh - 1, (iy + 1) / 2);
@@ -447,8 +514,8 @@ __global__ void up2_adj_x_kernel(const float* __restrict__ g, int gcs, int nb, i
   const long long total = (long long)nb * OH * w * c4n;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
-    const int q = (int)(i % c4n);
-    const long long p = i / c4n;
+    long long p;
+    const int q = pf_quad_split(i, c4n, p);
     const int qx = (int)(p % w);
     const long long row = p / w;
     const float* gr = g + row * OW * gcs + q * 4;
@@ -470,12 +537,10 @@ __global__ void up2_adj_y_kernel(const float* __restrict__ t, int nb, int OH, in
   const long long total = (long long)nb * h * w * c4n;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
-    const int q = (int)(i % c4n);
-    long long p = i / c4n;
-    const int qx = (int)(p % w);
-    p /= w;
-    const int qy = (int)(p % h);
-    const int b = (int)(p / h);
+    long long p;
+    const int q = pf_quad_split(i, c4n, p);
+    int qx, qy;
+    const int b = pix_split(p, w, h, qx, qy);
     f32x4 acc = {0, 0, 0, 0};
     const int o0 = max(0, 2 * qy - 2), o1 = min(OH - 1, 2 * qy + 4);
     for (int oy = o0; oy <= o1; ++oy) {

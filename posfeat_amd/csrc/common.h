@@ -121,6 +121,57 @@ inline const char* pf_ab_getenv(const char* name) {
 // workgroups round-robin over the 8 XCDs (XCD = bid & 7); XCD x gets the
 // contiguous logical range [x q + min(x, r), ...) of the nwg blocks, so
 // blocks that read the same data (e.g. one image's points) share one XCD's L2
+// sum_{k < n} p[k stride] in k order (the same bits as the plain loop), with
+// 8 loads in flight per trip: a loop that adds each load before issuing the
+// next waits one memory latency per term (the split-K reductions were
+// latency-bound that way)
+__device__ __forceinline__ float pf_ordered_sum(const float* __restrict__ p, long long stride,
+                                                int n) {
+  float s = 0.f;
+  int k = 0;
+  for (; k + 8 <= n; k += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = p[(long long)(k + u) * stride];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u];
+  }
+  for (; k < n; ++k) s += p[(long long)k * stride];
+  return s;
+}
+
+// (pixel, channel quad) of flat quad index i: 32-bit division whenever i fits
+// (every map here does); a 64-bit divide is a ~50-instruction sequence per
+// element, enough to leave an elementwise pass VALU-bound
+__device__ __forceinline__ int pf_quad_split(long long i, int c4n, long long& p) {
+  if ((unsigned long long)i <= 0xffffffffULL) {
+    const unsigned iu = (unsigned)i, pu = iu / (unsigned)c4n;
+    p = pu;
+    return (int)(iu - pu * (unsigned)c4n);
+  }
+  p = i / c4n;
+  return (int)(i - p * c4n);
+}
+
+// (b, ty, tx, q) of flat index i over [n][th][tw][c4n]: 32-bit divisions
+// whenever i fits (a 64-bit divide is a ~50-instruction sequence per thread)
+__device__ __forceinline__ int pf_tile_split(long long i, int c4n, int tw, int th, int& q, int& tx,
+                                             int& ty) {
+  if ((unsigned long long)i <= 0xffffffffULL) {
+    const unsigned iu = (unsigned)i, t = iu / (unsigned)c4n, r = t / (unsigned)tw,
+                   b = r / (unsigned)th;
+    q = (int)(iu - t * (unsigned)c4n);
+    tx = (int)(t - r * (unsigned)tw);
+    ty = (int)(r - b * (unsigned)th);
+    return (int)b;
+  }
+  const long long t = i / c4n, r = t / tw;
+  q = (int)(i - t * c4n);
+  tx = (int)(t - r * tw);
+  ty = (int)(r % th);
+  return (int)(r / th);
+}
+
 __device__ __forceinline__ long long pf_xcd_block(long long bid, long long nwg) {
   const long long q = nwg >> 3, r = nwg & 7, xcd = bid & 7, slot = bid >> 3;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;

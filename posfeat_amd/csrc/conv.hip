@@ -2249,8 +2249,8 @@ __global__ void conv_splitk_reduce(const float* __restrict__ part, int ks, int M
   const size_t slab = (size_t)M * C;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
-    const int q = (int)(i % c4n);
-    const long long m = i / c4n;
+    long long m;
+    const int q = pf_quad_split(i, c4n, m);
     f32x4 v = *reinterpret_cast<const f32x4*>(part + m * C + q * 4);
     for (int s = 1; s < ks; ++s) v += *reinterpret_cast<const f32x4*>(part + s * slab + m * C + q * 4);
     if (bias) v += *reinterpret_cast<const f32x4*>(bias + q * 4);
@@ -2298,6 +2298,7 @@ bool bf6_on() { return pf_conv_precision() >= 1; }
 // them, bbtrain.hip)
 thread_local int tl_halo_fp32 = 0;
 thread_local int tl_dense32 = 0;  // PfDense32Scope
+thread_local int tl_stem32 = 0;   // PfHaloFp32Scope(false)
 bool halo_bf6_on() {
   static const bool off = [] {
     const char* e = pf_ab_getenv("POSFEAT_BF6_HALO");
@@ -2581,7 +2582,7 @@ bool stem_bf6_on() {
     const char* e = pf_ab_getenv("POSFEAT_BF6_STEM");
     return e && e[0] == '0';
   }();
-  return bf6_on() && !off && tl_halo_fp32 == 0;
+  return bf6_on() && !off && tl_halo_fp32 == 0 && tl_stem32 == 0;
 }
 
 template <int BM, int BN, int WM, int WN>
@@ -2768,8 +2769,22 @@ void launch_up4_weights(const float* w_packed, float* wph, hipStream_t st) {
 
 bool pf_bf6x_on() { return bf6x_on(); }
 bool pf_halo_bf6_on() { return halo_bf6_on(); }
-PfHaloFp32Scope::PfHaloFp32Scope() { ++tl_halo_fp32; }
-PfHaloFp32Scope::~PfHaloFp32Scope() { --tl_halo_fp32; }
+PfHaloFp32Scope::PfHaloFp32Scope(bool halo_fp32) : halo_(halo_fp32) {
+  if (halo_) {
+    ++tl_halo_fp32;
+  } else {
+    ++tl_dense32;
+    ++tl_stem32;
+  }
+}
+PfHaloFp32Scope::~PfHaloFp32Scope() {
+  if (halo_) {
+    --tl_halo_fp32;
+  } else {
+    --tl_dense32;
+    --tl_stem32;
+  }
+}
 PfDense32Scope::PfDense32Scope(bool on) : on_(on) { tl_dense32 += on ? 1 : 0; }
 PfDense32Scope::~PfDense32Scope() { tl_dense32 -= on_ ? 1 : 0; }
 

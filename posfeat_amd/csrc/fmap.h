@@ -155,11 +155,15 @@ int pf_conv_precision();
 bool pf_bf6x_on();
 bool pf_halo_bf6_on();
 // while alive, this thread's 3x3 stride-1 (halo) convs use fp32 MFMA tiles
+// (and the dense GEMMs the 32x32x16 bf6d tiles, the stem fp32 MFMA).
+// halo_fp32 = false keeps the latter two but leaves the halo convs on their
+// bf16x6 tiles (POSFEAT_TRAIN_HALO_BF6=1, A/B build: bbtrain.hip)
 struct PfHaloFp32Scope {
-  PfHaloFp32Scope();
+  explicit PfHaloFp32Scope(bool halo_fp32 = true);
   ~PfHaloFp32Scope();
   PfHaloFp32Scope(const PfHaloFp32Scope&) = delete;
   PfHaloFp32Scope& operator=(const PfHaloFp32Scope&) = delete;
+  bool halo_;
 };
 // While alive (and `on`), the calling thread's dense pre-split GEMMs run the
 // 32x32x16 bf6d tiles instead of the 16x16x32 conv_bf6x_kernel: the training

@@ -298,8 +298,8 @@ __global__ void in_apply_kernel(float* __restrict__ x, int n, int hw, int c4n, i
   const float a = prelu ? *slope : 0.f;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
-    const int q = (int)(i % c4n);
-    const long long p = i / c4n;
+    long long p;
+    const int q = pf_quad_split(i, c4n, p);
     const int b = (int)(p / hw);
     float* ptr = x + p * cs + q * 4;
     f32x4 v = *reinterpret_cast<f32x4*>(ptr);
@@ -338,8 +338,8 @@ __global__ void norm_prelu_upsample_kernel(const float* __restrict__ x, int n, i
   const long long total = (long long)n * OH * OW * c4n;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
-    const int q = (int)(i % c4n);
-    long long p = i / c4n;
+    long long p;
+    const int q = pf_quad_split(i, c4n, p);
     const int ox = (int)(p % OW);
     p /= OW;
     const int oy = (int)(p % OH);

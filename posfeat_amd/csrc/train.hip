@@ -289,8 +289,14 @@ __global__ __launch_bounds__(256) void conv_wgrad_bf6_kernel(WgradArgs a) {
   }
   const int c_begin = (int)((long long)a.nchunks * split / a.nsplit);
   const int c_end = (int)((long long)a.nchunks * (split + 1) / a.nsplit);
-  // staging role: quad q (4 couts of dy / 4 k of the im2col), pixel group pg (4 px)
-  const int q = tid & 31, pg = tid >> 5;
+  // staging role: quad q (4 couts of dy / 4 k of the im2col), pixel group pg (4 px).
+  // A wave's 64 lanes are 8 quads x the 8 pixel groups, so each 8-byte plane
+  // store of a half-wave covers 4 whole 64-byte rows (row pitch 20 dwords =
+  // 4 mod 8: consecutive rows alternate bank halves): two cycles, the
+  // minimum.  (32 quads x 2 groups per wave put every lane of a store on the
+  // same two banks: PMC 18.7 conflict cycles per LDS instruction, a third of
+  // the wave cycles waiting on LDS issue.)  Same elements per thread.
+  const int q = tid >> 3, pg = tid & 7;
   const bool aok = co0 + 4 * q < a.Cout;
   const int k = n0 + 4 * q;  // 4 consecutive k share one tap (Cin % 32 == 0)
   const int ntap = a.KH * a.KW;
@@ -586,13 +592,11 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ part, const float*
   const long long n = (long long)Cout * Kpad;
   const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
   if (i < n) {
-    float s = 0.f;
-    for (int k = 0; k < nsplit; ++k) s += part[(long long)k * n + i];
+    const float s = pf_ordered_sum(part + i, n, nsplit);
     dw[i] = acc ? dw[i] + s : s;
   }
   if (db && i < Cout) {
-    float s = 0.f;
-    for (int k = 0; k < nsplit; ++k) s += partb[(long long)k * Cout + i];
+    const float s = pf_ordered_sum(partb + i, Cout, nsplit);
     db[i] = acc ? db[i] + s : s;
   }
 }
@@ -633,8 +637,8 @@ __global__ void up4_adj_x_kernel(const float* __restrict__ g, int gcs, int nb, i
   const long long total = (long long)nb * OH * w * c4n;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
-    const int q = (int)(i % c4n);
-    long long p = i / c4n;
+    long long p;
+    const int q = pf_quad_split(i, c4n, p);
     const int qx = (int)(p % w);
     const long long row = p / w;  // b*OH + oy
     const float* gr = g + row * OW * gcs + q * 4;
@@ -656,8 +660,8 @@ __global__ void up4_adj_y_kernel(const float* __restrict__ t, int nb, int OH, in
   const int C = c4n * 4;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
-    const int q = (int)(i % c4n);
-    long long p = i / c4n;
+    long long p;
+    const int q = pf_quad_split(i, c4n, p);
     const int qx = (int)(p % w);
     p /= w;
     const int qy = (int)(p % h);
@@ -778,8 +782,8 @@ __global__ void in_bwd_apply_kernel(const float* __restrict__ x, int xcs, const 
   const float a = PRELU ? *slope : 0.f;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
-    const int q = (int)(i % c4n);
-    const long long pix = i / c4n;
+    long long pix;
+    const int q = pf_quad_split(i, c4n, pix);
     const int b = (int)(pix / hw);
     // identity mode: x is already normalised (mean is NULL); rstd still scales dx
     const f32x4 m = PRELU ? *reinterpret_cast<const f32x4*>(mean + b * C + q * 4)
@@ -1216,10 +1220,7 @@ __global__ void wgrad_reduce_images_kernel(const float* __restrict__ part, int k
   const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
   if (i >= per * n) return;
   const long long z = i / per, e = i - z * per;
-  const float* p = part + z * k * per + e;
-  float s = 0.f;
-  for (int j = 0; j < k; ++j) s += p[j * per];
-  dw[i] = s;
+  dw[i] = pf_ordered_sum(part + z * k * per + e, per, k);
 }
 }  // namespace
 

@@ -82,12 +82,9 @@ __global__ void wino_input_kernel(const float* __restrict__ x, int xcs, int n, i
   const int C = c4n * 4;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
-    const int q = (int)(i % c4n);
-    const long long tile = i / c4n;
-    const int tx = (int)(tile % tw);
-    const long long r0 = tile / tw;
-    const int ty = (int)(r0 % th);
-    const int b = (int)(r0 / th);
+    int q, tx, ty;
+    const int b = pf_tile_split(i, c4n, tw, th, q, tx, ty);
+    const long long tile = ((long long)b * th + ty) * tw + tx;
     f32x4 d[4][4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -131,12 +128,9 @@ __global__ void wino_output_kernel(const float* __restrict__ M, int n, int h, in
   const int C = c4n * 4;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
-    const int q = (int)(i % c4n);
-    const long long tile = i / c4n;
-    const int tx = (int)(tile % tw);
-    const long long r0 = tile / tw;
-    const int ty = (int)(r0 % th);
-    const int b = (int)(r0 / th);
+    int q, tx, ty;
+    const int b = pf_tile_split(i, c4n, tw, th, q, tx, ty);
+    const long long tile = ((long long)b * th + ty) * tw + tx;
     const float* mi = M + tile * C + q * 4;
     const long long xs = T * C;
     f32x4 m[4][4];
@@ -244,12 +238,9 @@ __global__ __launch_bounds__(256) void wino4_input_kernel(const float* __restric
   const int C = c4n * 4;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
-    const int q = (int)(i % c4n);
-    const long long tile = i / c4n;
-    const int tx = (int)(tile % tw);
-    const long long r0 = tile / tw;
-    const int ty = (int)(r0 % th);
-    const int b = (int)(r0 / th);
+    int q, tx, ty;
+    const int b = pf_tile_split(i, c4n, tw, th, q, tx, ty);
+    const long long tile = ((long long)b * th + ty) * tw + tx;
     f32x4 t[6][6];  // B^T d, built row by row of d
 #pragma unroll
     for (int a = 0; a < 6; ++a)
@@ -311,12 +302,9 @@ __global__ __launch_bounds__(256) void wino4_output_kernel(const float* __restri
   const int C = c4n * 4;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
-    const int q = (int)(i % c4n);
-    const long long tile = i / c4n;
-    const int tx = (int)(tile % tw);
-    const long long r0 = tile / tw;
-    const int ty = (int)(r0 % th);
-    const int b = (int)(r0 / th);
+    int q, tx, ty;
+    const int b = pf_tile_split(i, c4n, tw, th, q, tx, ty);
+    const long long tile = ((long long)b * th + ty) * tw + tx;
     const float* mi = M + tile * C + q * 4;
     const long long xs = T * C;
     f32x4 s[4][6];  // A^T M
@@ -370,12 +358,9 @@ __global__ __launch_bounds__(256) void wino4_dy_kernel(const float* __restrict__
   const int C = c4n * 4;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
-    const int q = (int)(i % c4n);
-    const long long tile = i / c4n;
-    const int tx = (int)(tile % tw);
-    const long long r0 = tile / tw;
-    const int ty = (int)(r0 % th);
-    const int b = (int)(r0 / th);
+    int q, tx, ty;
+    const int b = pf_tile_split(i, c4n, tw, th, q, tx, ty);
+    const long long tile = ((long long)b * th + ty) * tw + tx;
     f32x4 t[6][4];  // A dY
 #pragma unroll
     for (int r = 0; r < 6; ++r)
@@ -419,16 +404,22 @@ __global__ void wino4_wgrad_out_kernel(const float* __restrict__ part, int nspli
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
        i += (long long)gridDim.x * blockDim.x) {
     const int co = (int)(i / Cin), ci = (int)(i - (long long)co * Cin);
+    // split-outer: the 36 loads of one split are in flight together, each
+    // u[a][b] still sums its splits in order s = 0, 1, ...
     float u[6][6];
 #pragma unroll
     for (int a = 0; a < 6; ++a)
 #pragma unroll
-      for (int b = 0; b < 6; ++b) {
-        const float* pz = part + (long long)(a * 6 + b) * nsplit * n + i;
-        float v = 0.f;
-        for (int s = 0; s < nsplit; ++s) v += pz[s * n];
-        u[a][b] = v;
-      }
+      for (int b = 0; b < 6; ++b) u[a][b] = 0.f;
+    for (int s = 0; s < nsplit; ++s) {
+      float v[36];
+#pragma unroll
+      for (int x = 0; x < 36; ++x) v[x] = part[((long long)x * nsplit + s) * n + i];
+#pragma unroll
+      for (int a = 0; a < 6; ++a)
+#pragma unroll
+        for (int b = 0; b < 6; ++b) u[a][b] += v[a * 6 + b];
+    }
     float sv[3][6];
 #pragma unroll
     for (int kh = 0; kh < 3; ++kh)
@@ -453,8 +444,7 @@ __global__ void wino4_wgrad_out_kernel(const float* __restrict__ part, int nspli
         *o = acc ? *o + v : v;
       }
     if (db && ci == 0) {
-      float v = 0.f;
-      for (int s = 0; s < nsplit; ++s) v += partb[s * Cout + co];
+      const float v = pf_ordered_sum(partb + co, Cout, nsplit);
       db[co] = acc ? db[co] + v : v;
     }
   }
@@ -516,12 +506,9 @@ __global__ __launch_bounds__(256) void up4_wino_output_kernel(const float* __res
   const long long T = (long long)n * th * tw;
   {
     const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-    const int q = (int)(i % c4n);
-    const long long tile = i / c4n;
-    const int tx = (int)(tile % tw);
-    const long long r0 = tile / tw;
-    const int ty = (int)(r0 % th);
-    const int b = (int)(r0 / th);
+    int q, tx, ty;
+    const int b = pf_tile_split(i, c4n, tw, th, q, tx, ty);
+    const long long tile = ((long long)b * th + ty) * tw + tx;
     const int phase = (q * 4) / UW_COUT, co = q * 4 - phase * UW_COUT;
     const int ry = phase >> 2, rx = phase & 3;
     const float* mi = M + tile * UW_NO + q * 4;

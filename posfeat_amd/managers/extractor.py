@@ -615,8 +615,11 @@ class Extractor:
                       "stage_ms_per_image": None, "pipeline": True, "reader": "staged",
                       "group": group, "group_marks": marks, "max_held": max_held, "hold": hold,
                       "inflight": inflight, "host": {k: round(v, 4) for k, v in acct.items()}}
+        # max_held: the planned buckets' bound (the same grouping as the loader
+        # loop); the reader itself holds at most ``ahead`` + 1 batches
         self.logger.info("extracted %d images in %.2fs (%.1f images/s, pipelined, staged reader, "
-                         "%d groups)" % (n, dt, self.stats["images_per_s"], len(marks)))
+                         "%d groups, at most %d images held)" % (n, dt, self.stats["images_per_s"],
+                                                                 len(marks), max_held))
         return n
 
     @property
