@@ -49,7 +49,7 @@ HEAD_CONV2_FLOP_PER_IMAGE = 2.0 * 480 * 640 * 128 * 256 * 9   # reference layer
 # the 1x1 / strided / halo convs, the stem).  The engine's timing events carry
 # the FLOPs each launch executes.
 GEMM_LABEL_KERNELS = {
-    ".wino": "conv_bf6x_kernel<128> x36 batched (Winograd F(4x4) transform-domain GEMMs of "
+    ".wino": "conv_bf6x_kernel<128> x64 batched (Winograd F(6x6) transform-domain GEMMs of "
              "%s; bf16x6 on pre-split U planes, v_mfma_f32_16x16x32_bf16, memory instructions "
              "interleaved among the MFMAs)",
     "up4tap": "conv_bf6x_kernel<128> (head.conv2's 192 x4-upsampled channels: nine 1x1 convs "

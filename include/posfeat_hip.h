@@ -336,6 +336,19 @@ int posfeat_conv3x3_wino(const float *x, int x_cstride, int n, int h, int w, int
                          const float *U, const float *bias, int cout, int act, float *y,
                          int y_cstride, void *ws, size_t ws_bytes, void *stream);
 
+/* The same conv by Winograd F(6x6,3x3) (the extraction engine's decoder and
+ * head.conv1, networks/DescNet.py:41-45 and DeteNet.py:102-121): 64
+ * transformed weight matrices U ([64][cout][cin] floats, posfeat_wino6_weights),
+ * 6x6 output tiles (the last tile row / column cut at h, w), 1.27x fewer
+ * transform-domain MACs than F(4x4).  Any h, w; cin % 32 == 0, cout % 4 == 0,
+ * even pitches.  Same result as posfeat_conv2d_nhwc within fp32 rounding
+ * grown by the transforms (B^T, A^T exact; G in ninths). */
+size_t posfeat_wino6_workspace(int n, int h, int w, int cin, int cout);
+int posfeat_wino6_weights(const float *w_packed, int cout, int cin, float *U, void *stream);
+int posfeat_conv3x3_wino6(const float *x, int x_cstride, int n, int h, int w, int cin,
+                          const float *U, const float *bias, int cout, int act, float *y,
+                          int y_cstride, void *ws, size_t ws_bytes, void *stream);
+
 /* Weight gradient of the same decoder convs by F(4x4,3x3) (the autograd
  * conv2d weight/bias backward behind managers/trainer.py:331 for
  * networks/DescNet.py:41-45): dM = A dY A^T per 4x4 output tile, the 36

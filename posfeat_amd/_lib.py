@@ -115,6 +115,11 @@ SIGNATURES = {
     "posfeat_conv3x3_wino": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
                                      c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_size_t,
                                      c_void_p]),
+    "posfeat_wino6_workspace": (c_size_t, [c_int] * 5),
+    "posfeat_wino6_weights": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "posfeat_conv3x3_wino6": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
+                                      c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_size_t,
+                                      c_void_p]),
     "posfeat_wino_wgrad_workspace": (c_size_t, [c_int] * 5),
     "posfeat_conv3x3_wino_wgrad": (c_int, [c_void_p, c_int, c_void_p, c_int] + [c_int] * 5 +
                                    [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
@@ -212,10 +217,10 @@ AB_ONLY_SWITCHES = (
     "POSFEAT_DISK_FLASH", "POSFEAT_GEMM_B256", "POSFEAT_GFUSE", "POSFEAT_GFUSE_BLOCKS",
     "POSFEAT_GFUSE_K80", "POSFEAT_HEADFUSE", "POSFEAT_HEAD_UP4", "POSFEAT_IMGSTATS",
     "POSFEAT_S2PHASE", "POSFEAT_SIDE", "POSFEAT_SIDE_AT", "POSFEAT_TRAINTAP",
-    "POSFEAT_TRAIN_HALO_BF6",
+    "POSFEAT_TRAIN_HALO_BF6", "POSFEAT_TRAIN_WINO6",
     "POSFEAT_TUNE_SIMILAR", "POSFEAT_UP2FUSE", "POSFEAT_UP4TAP", "POSFEAT_UP4WINO",
-    "POSFEAT_WGRAD_BF6", "POSFEAT_WGRAD_BF6_ALL", "POSFEAT_WINO", "POSFEAT_WINO_ENC",
-    "POSFEAT_WINPATCH")
+    "POSFEAT_WGRAD_BF6", "POSFEAT_WGRAD_BF6_ALL", "POSFEAT_WINO", "POSFEAT_WINO6",
+    "POSFEAT_WINO6_ENC", "POSFEAT_WINO_ENC", "POSFEAT_WINPATCH")
 
 
 def _warn_ab_switches(L):

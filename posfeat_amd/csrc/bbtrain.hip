@@ -163,6 +163,7 @@ struct posfeat_bbtrain {
   // Winograd F(2x2,3x3) for the decoder's 3x3 convs, forward and input
   // gradient (wino.hip; POSFEAT_WINO=0: direct conv)
   bool wino = true;
+  bool wino6 = true;  // F(6x6) forward + input gradient (POSFEAT_TRAIN_WINO6=0, A/B: F(4x4))
   bool bf6p = false;     // conv precision mode 2 at create (pre-split Winograd operands)
   bool s2phase = true;  // stride-2 input gradients by output phases (POSFEAT_S2PHASE=0: zero insertion)
   Buf wu, wino_ws;
@@ -417,11 +418,20 @@ void plan(posfeat_bbtrain* m) {
     m->s2phase = !(e && e[0] == '0');
   }
   m->bf6p = pf_bf6p_on();  // fixed for the handle: the U buffer size depends on it
+  {
+    const char* e = pf_ab_getenv("POSFEAT_TRAIN_WINO6");
+    m->wino6 = !(e && e[0] == '0') && !m->bf6p;
+  }
   if (m->wino) {
     size_t uf = 0, wb = 0;
     for (int li : {T.up3, T.ic3, T.up2, T.ic2}) {
       const TLayer& L = T.v[li];
       uf = std::max(uf, (size_t)(m->bf6p || m->wsplit ? 54 : 36) * L.cin * L.cout);
+      if (m->wino6) {
+        uf = std::max(uf, pf_wino6_weights_floats(L.cin, L.cout, m->wsplit));
+        wb = std::max(wb, pf_wino6_ws_bytes((int)B, lih[li], liw[li], L.cin, L.cout));
+        wb = std::max(wb, pf_wino6_ws_bytes((int)B, lih[li], liw[li], L.cout, L.cin));
+      }
       wb = std::max(wb, pf_wino_ws_bytes((int)B, lih[li], liw[li], L.cin, L.cout));
       wb = std::max(wb, pf_wino_ws_bytes((int)B, lih[li], liw[li], L.cout, L.cin));
       if (lih[li] % 4 == 0 && liw[li] % 4 == 0)
@@ -453,7 +463,15 @@ int layer_fwd(Ctx& c, int li, const float* x, int xcs, int h, int w, float* out,
   const long long P = (long long)m->B * oh * ow;
   float* y = c.f(m->y[li]);
   posfeat_conv_desc d = make_desc(m->B, h, w, L.cin, xcs, L.cout, L.k, L.stride, L.cout, 0);
-  if (use_wino(m, li, h, w)) {
+  if (use_wino(m, li, h, w) && m->wino6) {
+    float* U = c.s(m->wu);
+    const double T6 = (double)m->B * ((h + 5) / 6) * ((w + 5) / 6);
+    PF_TRY(timed(c, std::string("fwd:conv:") + L.name, 2.0 * T6 * 64 * L.cin * L.cout, [&] {
+      PF_TRY(pf_wino6_weights(c.prm + L.w_off, L.cout, L.cin, U, c.st, m->wsplit));
+      return pf_wino6_conv(x, xcs, m->B, h, w, L.cin, U, c.prm + L.b_off, L.cout, ACT_NONE, y,
+                           L.cout, c.s(m->wino_ws), m->wino_ws.bytes, c.st, 7, m->wsplit ? 1 : 0);
+    }));
+  } else if (use_wino(m, li, h, w)) {
     float* U = c.s(m->wu);
     PF_TRY(timed(c, std::string("fwd:conv:") + L.name, wino_flops(m->B, h, w, L.cin, L.cout), [&] {
       PF_TRY(pf_wino_weights_hw(c.prm + L.w_off, L.cout, L.cin, h, w, U, c.st,
@@ -629,6 +647,15 @@ int layer_bwd(Ctx& c, int li, const float* x, int xcs, int h, int w, const float
     }
     return (int)POSFEAT_OK;
   }));
+  if (!add && use_wino(m, li, h, w) && m->wino6) {
+    float* U = c.s(m->wu);
+    const double T6 = (double)B * ((h + 5) / 6) * ((w + 5) / 6);
+    return timed(c, std::string("bwd:dgrad:") + L.name, 2.0 * T6 * 64 * C * L.cin, [&] {
+      PF_TRY(pf_wino6_weights(wt, L.cin, C, U, c.st, m->wsplit));
+      return pf_wino6_conv(src, C, B, h, w, C, U, nullptr, L.cin, ACT_NONE, dx, dxcs,
+                           c.s(m->wino_ws), m->wino_ws.bytes, c.st, 7, m->wsplit ? 1 : 0);
+    });
+  }
   if (!add && use_wino(m, li, h, w)) {
     float* U = c.s(m->wu);
     return timed(c, std::string("bwd:dgrad:") + L.name, wino_flops(B, h, w, C, L.cin), [&] {

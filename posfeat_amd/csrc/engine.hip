@@ -197,6 +197,8 @@ struct posfeat_model {
   posfeat_wstore* store = nullptr;
   size_t p_bytes = 0;
   size_t wino_u_f2 = 0;        // floats: the F(2x2) slots after the F(4x4) ones
+  size_t wino_u_f6 = 0;        // floats: the F(6x6) slots after those
+  bool wino6 = true;           // F(6x6) for the decoder + head.conv1 (POSFEAT_WINO6=0: F(4x4))
   bool wprep_pending = false;  // built this forward: record the store's event at its end
   // timing
   bool timing = false;
@@ -526,6 +528,35 @@ long long wino_u_offset(const std::string& name, bool planes) {
   return -1;
 }
 
+// F(6x6) (1.27x fewer transform-domain MACs and 0.79x the V / M bytes of
+// F(4x4); 2.25x fewer than F(2x2), which layer3's 30x40 maps took) for the
+// decoder + head.conv1 and the encoder stages in POSFEAT_WINO6_ENC (A/B
+// build; default "23": layer2 / layer3 conv2)
+unsigned wino6_enc_mask() {
+  static const unsigned mask = [] {
+    const char* e = pf_ab_getenv("POSFEAT_WINO6_ENC");
+    if (!e) return 6u;
+    unsigned m = 0;
+    for (const char* q = e; *q; ++q)
+      if (*q >= '1' && *q <= '3') m |= 1u << (*q - '1');
+    return m;
+  }();
+  return mask;
+}
+constexpr int kWino6Layers = 16;  // slots for every kWinoLayers entry
+long long wino6_u_offset(const std::string& name, bool planes) {
+  long long off = 0;
+  for (int i = 0; i < kWino6Layers; ++i) {
+    if (name == kWinoLayers[i]) {
+      if (i >= 5 && !((wino6_enc_mask() >> (name[5] - '1')) & 1u)) return -1;
+      return off;
+    }
+    const Spec* s = specs().find(kWinoLayers[i]);
+    off += (long long)pf_wino6_weights_floats(s->cin, s->cout, planes);
+  }
+  return -1;
+}
+
 // up2: x is the (h/2, w/2) map and the conv input its x2 align_corners
 // upsample (DescNet.py:182-190 upconv), interpolated inside the F(4x4)
 // input transform (POSFEAT_UP2FUSE=0: materialised by the upsample kernel);
@@ -541,6 +572,32 @@ bool up2fuse_on() {
 int conv3x3(Ctx& c, const std::string& name, const float* x, int n, int h, int w, int xcs, float* y,
             int ycs, int act, int up2 = 0, float* xup = nullptr) {
   posfeat_model* m = c.m;
+  const long long uo6 = wino6_u_offset(name, m->wsplit);
+  if (m->wino && m->wino6 && !m->bf6p && uo6 >= 0 && (!up2 || up2fuse_on())) {
+    const Spec* s = specs().find(name);
+    if (c.dry) return POSFEAT_OK;
+    float* U = c.f(m->wino_u) + m->wino_u_f6 + uo6;
+    const std::string ukey = name + "/6";
+    if (!(m->wcache && m->store && m->store->wino_done.count(ukey))) {
+      PF_TRY(timed(c, "wino:weights", 0, [&] {
+        return pf_wino6_weights(c.W(name), s->cout, s->cin, U, c.st, m->wsplit);
+      }));
+      if (m->wcache) {
+        m->store->wino_done.insert(ukey);
+        m->wprep_pending = true;
+      }
+    }
+    const double T = (double)n * ((h + 5) / 6) * ((w + 5) / 6);
+    auto stage = [&](int st_bits) {
+      return pf_wino6_conv(x, xcs, n, h, w, s->cin, U, c.Bi(name), s->cout, act, y, ycs,
+                           c.f(m->wino_ws), m->wino_ws.floats * sizeof(float), c.st, st_bits,
+                           m->wsplit ? 1 : 0, up2);
+    };
+    PF_TRY(timed(c, "wino:in:" + name, 0, [&] { return stage(1); }));
+    PF_TRY(timed(c, "conv:" + name + ".wino", 2.0 * T * 64 * s->cin * s->cout,
+                 [&] { return stage(2); }));
+    return timed(c, "wino:out:" + name, 0, [&] { return stage(4); });
+  }
   const long long uo = wino_u_offset(name, m->bf6p || m->wsplit);
   const bool f4ok = m->wino && uo >= 0 && h % 4 == 0 && w % 4 == 0 &&
                     !(pf_ab_getenv("POSFEAT_WINO") && pf_ab_getenv("POSFEAT_WINO")[0] == '1');
@@ -712,6 +769,8 @@ void plan(posfeat_model* m) {
     m->autotune = !(t && t[0] == '0');
     const char* wv = pf_ab_getenv("POSFEAT_WINO");  // 0: direct conv for the decoder 3x3 layers
     m->wino = !(wv && wv[0] == '0');
+    const char* w6 = pf_ab_getenv("POSFEAT_WINO6");  // 0: F(4x4) for the decoder / head.conv1
+    m->wino6 = !(w6 && w6[0] == '0') && !(wv && wv[0] == '1');
     const char* gv = pf_ab_getenv("POSFEAT_GFUSE");  // 0: conv2's G part as the 64-ch 3x3 conv
     m->gfuse = !(gv && gv[0] == '0');
     const char* uv = pf_ab_getenv("POSFEAT_UP4WINO");  // 0: conv_up4_kernel (bilinear phases)
@@ -749,9 +808,19 @@ void plan(posfeat_model* m) {
       wb = std::max(wb, pf_wino_ws_bytes((int)B, (int)H / kWinoDiv[i], (int)W / kWinoDiv[i],
                                          s->cin, s->cout));
     }
-    // cached: F(4x4) slots, then F(2x2) slots (a shared store serves every shape)
-    palloc(m->wino_u, m->wcache ? 2 * uf : uf);
+    size_t uf6 = 0;
+    if (m->wino6 && !m->bf6p)
+      for (int i = 0; i < nl; ++i) {
+        const Spec* s = specs().find(kWinoLayers[i]);
+        uf6 += pf_wino6_weights_floats(s->cin, s->cout, m->wsplit);
+        wb = std::max(wb, pf_wino6_ws_bytes((int)B, (int)H / kWinoDiv[i], (int)W / kWinoDiv[i],
+                                            s->cin, s->cout));
+      }
+    // cached: F(4x4) slots, then F(2x2) slots (a shared store serves every
+    // shape), then the F(6x6) slots
+    palloc(m->wino_u, (m->wcache ? 2 * uf : uf) + uf6);
     m->wino_u_f2 = m->wcache ? uf : 0;
+    m->wino_u_f6 = m->wcache ? 2 * uf : uf;
     alloc(m->wino_ws, wb / 4 + 4);
   }
   if (m->train && !m->traintap) m->up4 = false;  // the backward reads the materialised conv2 input

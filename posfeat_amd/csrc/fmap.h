@@ -70,6 +70,15 @@ size_t pf_wino_weights_floats_bf6p(int Cin, int Cout);
 int pf_wino_conv(const float* x, int xcs, int n, int h, int w, int Cin, const float* U,
                  const float* bias, int Cout, int act, float* y, int ycs, void* ws, size_t ws_bytes,
                  hipStream_t st, int stages = 7, int planes = 0, int up2 = 0);
+// Winograd F(6x6,3x3) (wino.hip): U = [64][Cout][Cin] (planes: three bf16
+// planes, Cout % 64 == 0, 96 floats per pair); tiles ceil(h/6) x ceil(w/6);
+// pf_wino6_conv planes 0 / 1 as pf_wino_conv's, stages and up2 likewise
+size_t pf_wino6_ws_bytes(int n, int h, int w, int Cin, int Cout);
+size_t pf_wino6_weights_floats(int Cin, int Cout, bool planes);
+int pf_wino6_weights(const float* wpk, int Cout, int Cin, float* U, hipStream_t st, bool planes);
+int pf_wino6_conv(const float* x, int xcs, int n, int h, int w, int Cin, const float* U,
+                  const float* bias, int Cout, int act, float* y, int ycs, void* ws,
+                  size_t ws_bytes, hipStream_t st, int stages = 7, int planes = 0, int up2 = 0);
 // head.conv2's G part as one per-image 5x5 conv of the image (gfuse.hip)
 size_t pf_gfuse_weights_floats(int n);
 int pf_gfuse_weights(const float* w2_packed, const float* b2, const float* w1_packed,

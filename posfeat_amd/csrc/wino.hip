@@ -625,6 +625,344 @@ int pf_up4_wino(int n, int H, int W, const float* L, int lcs, const float* U, fl
   return POSFEAT_OK;
 }
 
+// U as bf16 planes for the pre-split bf16x6 GEMM tiles: Cout a multiple of
+// 64 (128-wide tiles, or 64-wide ones for 192 = head.conv1; the tiles clamp
+// their rows past Cout, the epilogue never stores them)
+static bool wino_planes_ok(int Cout) { return Cout % 64 == 0; }
+
+// ---------------------------------------------------------------- F(6x6, 3x3)
+// 64 multiplies per 36 outputs: 1.27x fewer MACs than F(4x4) (2.25 -> 1.78 per
+// output and channel pair) and 0.79x its transform-domain bytes.  Points 0,
+// +-1, +-2, +-1/2 (Lavin & Gray's construction): B^T and A^T are exact in
+// fp32 (quarters and powers of two), G carries ninths; tests/test_gpu_ops.py
+// bounds the result against the direct conv.  Tiles are ceil(h/6) x ceil(w/6):
+// the last row / column of tiles reads zeros past the map (the conv's own
+// padding for the outputs kept) and drops the outputs past it.  One channel
+// PAIR per thread: the 8x8 transform of four channels would hold 256 VGPRs.
+namespace {
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+constexpr float W6_BT[8][8] = {{1, 0, -5.25f, 0, 5.25f, 0, -1, 0},
+                               {0, 1, 1, -4.25f, -4.25f, 1, 1, 0},
+                               {0, -1, 1, 4.25f, -4.25f, -1, 1, 0},
+                               {0, 0.5f, 0.25f, -2.5f, -1.25f, 2, 1, 0},
+                               {0, -0.5f, 0.25f, 2.5f, -1.25f, -2, 1, 0},
+                               {0, 2, 4, -2.5f, -5, 0.5f, 1, 0},
+                               {0, -2, 4, 2.5f, -5, -0.5f, 1, 0},
+                               {0, -1, 0, 5.25f, 0, -5.25f, 0, 1}};
+constexpr float W6_G[8][3] = {{1, 0, 0},
+                              {-2.f / 9, -2.f / 9, -2.f / 9},
+                              {-2.f / 9, 2.f / 9, -2.f / 9},
+                              {1.f / 90, 1.f / 45, 2.f / 45},
+                              {1.f / 90, -1.f / 45, 2.f / 45},
+                              {32.f / 45, 16.f / 45, 8.f / 45},
+                              {32.f / 45, -16.f / 45, 8.f / 45},
+                              {0, 0, 1}};
+constexpr float W6_AT[6][8] = {{1, 1, 1, 1, 1, 1, 1, 0},
+                               {0, 1, -1, 2, -2, 0.5f, -0.5f, 0},
+                               {0, 1, 1, 4, 4, 0.25f, 0.25f, 0},
+                               {0, 1, -1, 8, -8, 0.125f, -0.125f, 0},
+                               {0, 1, 1, 16, 16, 0.0625f, 0.0625f, 0},
+                               {0, 1, -1, 32, -32, 0.03125f, -0.03125f, 1}};
+
+// U[xi][co][ci] (64 matrices), Ub != nullptr: three bf16 planes (stride 64 Cout Cin)
+__global__ void wino6_weights_kernel(const float* __restrict__ wpk, int Cout, int Cin, int kpad,
+                                     float* __restrict__ U, unsigned short* __restrict__ Ub) {
+  const long long n = (long long)Cout * Cin;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int co = (int)(i / Cin), ci = (int)(i - (long long)co * Cin);
+    const float* w = wpk + (long long)co * kpad + (ci >> 5) * 9 * 32 + (ci & 31);
+    float g[3][3];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) g[t / 3][t % 3] = w[t * 32];
+    float r[8][3];
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        r[a][c] = W6_G[a][0] * g[0][c] + W6_G[a][1] * g[1][c] + W6_G[a][2] * g[2][c];
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        const float u = r[a][0] * W6_G[b][0] + r[a][1] * W6_G[b][1] + r[a][2] * W6_G[b][2];
+        const long long o = ((long long)(a * 8 + b) * Cout + co) * Cin + ci;
+        if (Ub) {
+          unsigned hh, mm, ll;
+          pf_split3_pair(u, 0.f, hh, mm, ll);
+          Ub[o] = (unsigned short)hh;
+          Ub[o + 64 * n] = (unsigned short)mm;
+          Ub[o + 128 * n] = (unsigned short)ll;
+        } else {
+          U[o] = u;
+        }
+      }
+  }
+}
+
+template <int VW> struct W6Vec;
+template <> struct W6Vec<1> { typedef float t; };
+template <> struct W6Vec<2> { typedef f32x2 t; };
+// acc + k x as one explicit fma: the transform's arithmetic is then the same
+// per channel whether a thread holds one channel or a pair (the fused-upsample
+// kernel and the plain one must agree bit for bit, test_gpu_bf6r.py)
+__device__ __forceinline__ float w6_fma(float k, float x, float acc) {
+  return __builtin_fmaf(k, x, acc);
+}
+__device__ __forceinline__ f32x2 w6_fma(float k, f32x2 x, f32x2 acc) {
+  return __builtin_elementwise_fma(f32x2{k, k}, x, acc);
+}
+
+// x-interpolated half-res row sy at the 8 patch columns (pf_up2ac_at's inner
+// terms hx v(sy, x0) + lx v(sy, x1), same operations): 0 past the map
+template <typename T>
+__device__ __forceinline__ void up2_row8(const float* base, int w2, int cs, float sw, int w, int sy,
+                                         int xc0, T (&X)[8]) {
+#pragma clang fp contract(off)
+  const float* row = base + (long long)sy * w2 * cs;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    // branch-free: a column past the map interpolates column w - 1, then 0
+    const int xx = xc0 + c;
+    const bool in = (unsigned)xx < (unsigned)w;
+    const float rx = sw * (in ? xx : w - 1);
+    const int x0 = (int)rx;
+    const int x1 = x0 + (x0 < w2 - 1 ? 1 : 0);
+    const float lx = rx - x0, hx = 1.f - lx;
+    const T v0 = *reinterpret_cast<const T*>(row + x0 * cs);
+    const T v1 = *reinterpret_cast<const T*>(row + x1 * cs);
+    const T v = hx * v0 + lx * v1;
+    X[c] = in ? v : T(0.f);
+  }
+}
+
+// pf_up2ac_at's outer term hy X(y0) + ly X(y1), same operations
+template <typename T>
+__device__ __forceinline__ T up2_lerp_y(float hy, T a, float ly, T b) {
+#pragma clang fp contract(off)
+  return hy * a + ly * b;
+}
+
+// V[xi][tile][c] = (B^T d B)[xi], d the 8x8 patch at rows 6ty-1.., cols 6tx-1..
+// (zero outside the map), VW channels per thread (the 8x8 accumulator is 64 VW
+// VGPRs).  UP2: x is the h/2 x w/2 map whose x2 align_corners upsample is the
+// conv input (upconv, DescNet.py:182-190), interpolated here with
+// pf_up2ac_at's arithmetic (x then y, no contraction: the upsample kernel's
+// bits) -- each half-res row's x interpolation is formed once and kept in a
+// two-row window that slides down the patch (the patch's 8 rows read 5-6
+// half-res rows), instead of four gathered loads per tap.  A wave is 64
+// channel groups of one tile (Cin / VW >= 64 on every caller), so the window's
+// branches are wave-uniform.
+template <bool UP2, int VW>
+__global__ __launch_bounds__(256) void wino6_input_kernel(const float* __restrict__ x, int xcs,
+                                                          int n, int h, int w, int cvn,
+                                                          float* __restrict__ V) {
+  typedef typename W6Vec<VW>::t T;
+  const int th = (h + 5) / 6, tw = (w + 5) / 6;
+  const int h2 = h / 2, w2 = w / 2;
+  const float sh = h > 1 ? (float)(h2 - 1) / (float)(h - 1) : 0.f;
+  const float sw = w > 1 ? (float)(w2 - 1) / (float)(w - 1) : 0.f;
+  const long long Tn = (long long)n * th * tw;
+  const long long total = Tn * cvn;
+  const int C = cvn * VW;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    int q, tx, ty;
+    const int b = pf_tile_split(i, cvn, tw, th, q, tx, ty);
+    const long long tile = ((long long)b * th + ty) * tw + tx;
+    T t[8][8];  // B^T d, built row by row of d
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+      for (int c = 0; c < 8; ++c) t[a][c] = T(0.f);
+    const float* base = UP2 ? x + (long long)b * h2 * w2 * xcs + q * VW : nullptr;
+    T XA[8], XB[8];  // UP2: x-interpolated half-res rows ka, kb
+    int ka = -1, kb = -1;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int yy = 6 * ty - 1 + r;
+      T d[8];
+      if (UP2) {
+#pragma unroll
+        for (int c = 0; c < 8; ++c) d[c] = T(0.f);
+        if ((unsigned)yy < (unsigned)h) {
+          const float ry = sh * yy;
+          const int y0 = (int)ry;
+          const int y1 = y0 + (y0 < h2 - 1 ? 1 : 0);
+          const float ly = ry - y0, hy = 1.f - ly;
+          if (y0 != ka) {
+            if (y0 == kb) {
+#pragma unroll
+              for (int c = 0; c < 8; ++c) XA[c] = XB[c];
+            } else {
+              up2_row8(base, w2, xcs, sw, w, y0, 6 * tx - 1, XA);
+            }
+            ka = y0;
+          }
+          if (y1 != kb) {
+            if (y1 == ka) {
+#pragma unroll
+              for (int c = 0; c < 8; ++c) XB[c] = XA[c];
+            } else {
+              up2_row8(base, w2, xcs, sw, w, y1, 6 * tx - 1, XB);
+            }
+            kb = y1;
+          }
+#pragma unroll
+          for (int c = 0; c < 8; ++c) d[c] = up2_lerp_y(hy, XA[c], ly, XB[c]);
+          // (columns past the map: XA = XB = 0 there, so d = 0 as required)
+        }
+      } else {
+        // branch-free taps (clamped address, 0 outside the map)
+        const bool rin = (unsigned)yy < (unsigned)h;
+        const float* xr = x + ((long long)b * h + min(max(yy, 0), h - 1)) * w * xcs + q * VW;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          const int xx = 6 * tx - 1 + c;
+          const bool in = rin && (unsigned)xx < (unsigned)w;
+          const T v = *reinterpret_cast<const T*>(xr + min(max(xx, 0), w - 1) * xcs);
+          d[c] = in ? v : T(0.f);
+        }
+      }
+#pragma unroll
+      for (int a = 0; a < 8; ++a)
+        if (W6_BT[a][r] != 0.f)
+#pragma unroll
+          for (int c = 0; c < 8; ++c) t[a][c] = w6_fma(W6_BT[a][r], d[c], t[a][c]);
+    }
+    // one running store pointer: 64 precomputed plane offsets (64-bit,
+    // uniform) took 128 SGPRs and spilled
+    const long long xs = Tn * C;
+    float* vp = V + tile * C + q * VW;
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+      for (int bb = 0; bb < 8; ++bb) {
+        T v = T(0.f);
+#pragma unroll
+        for (int c = 0; c < 8; ++c)
+          if (W6_BT[bb][c] != 0.f) v = w6_fma(W6_BT[bb][c], t[a][c], v);
+        *reinterpret_cast<T*>(vp) = v;
+        vp += xs;
+        asm volatile("" : "+v"(vp));
+      }
+  }
+}
+
+// y = act(A^T M A + bias) for the 6x6 outputs of each tile inside the map
+__global__ __launch_bounds__(256) void wino6_output_kernel(const float* __restrict__ M, int n,
+                                                           int h, int w, int c2n,
+                                                           const float* __restrict__ bias, int act,
+                                                           float* __restrict__ y, int ycs) {
+  const int th = (h + 5) / 6, tw = (w + 5) / 6;
+  const long long T = (long long)n * th * tw;
+  const long long total = T * c2n;
+  const int C = c2n * 2;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    int q, tx, ty;
+    const int b = pf_tile_split(i, c2n, tw, th, q, tx, ty);
+    const long long tile = ((long long)b * th + ty) * tw + tx;
+    const float* mi = M + tile * C + q * 2;
+    const long long xs = T * C;
+    f32x2 s[6][8];  // A^T M
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+#pragma unroll
+      for (int c = 0; c < 8; ++c) s[a][c] = f32x2{0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      f32x2 m[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) m[c] = *reinterpret_cast<const f32x2*>(mi + (r * 8 + c) * xs);
+#pragma unroll
+      for (int a = 0; a < 6; ++a)
+        if (W6_AT[a][r] != 0.f)
+#pragma unroll
+          for (int c = 0; c < 8; ++c) s[a][c] += W6_AT[a][r] * m[c];
+    }
+    f32x2 bv = {0.f, 0.f};
+    if (bias) bv = *reinterpret_cast<const f32x2*>(bias + q * 2);
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+      const int oy = 6 * ty + a;
+#pragma unroll
+      for (int bb = 0; bb < 6; ++bb) {
+        const int ox = 6 * tx + bb;
+        f32x2 o = bv;
+#pragma unroll
+        for (int c = 0; c < 8; ++c)
+          if (W6_AT[bb][c] != 0.f) o += W6_AT[bb][c] * s[a][c];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const float v = o[j];
+          o[j] = act == POSFEAT_ACT_RELU ? fmaxf(v, 0.f) : act == POSFEAT_ACT_ELU ? pf_elu(v) : v;
+        }
+        if (oy < h && ox < w)
+          *reinterpret_cast<f32x2*>(y + (((long long)b * h + oy) * w + ox) * ycs + q * 2) = o;
+      }
+    }
+  }
+}
+}  // namespace
+
+size_t pf_wino6_ws_bytes(int n, int h, int w, int Cin, int Cout) {
+  const size_t T = (size_t)n * ((h + 5) / 6) * ((w + 5) / 6);
+  return pf_align(64 * T * Cin * 4, 256) + pf_align(64 * T * Cout * 4, 256);
+}
+
+size_t pf_wino6_weights_floats(int Cin, int Cout, bool planes) {
+  return (size_t)(planes ? 96 : 64) * Cin * Cout;
+}
+
+int pf_wino6_weights(const float* wpk, int Cout, int Cin, float* U, hipStream_t st, bool planes) {
+  if (Cin % 32 || Cout % 4) return POSFEAT_E_INVALID;
+  const int kpad = posfeat_conv_packed_k(Cin, 3, 3);
+  planes = planes && wino_planes_ok(Cout);  // the condition pf_wino6_conv checks
+  hipLaunchKernelGGL(wino6_weights_kernel, dim3(grid_for((long long)Cout * Cin, 256)), dim3(256), 0,
+                     st, wpk, Cout, Cin, kpad, U,
+                     planes ? reinterpret_cast<unsigned short*>(U) : nullptr);
+  PF_CHECK_LAUNCH();
+  return POSFEAT_OK;
+}
+
+// planes 1: U holds the bf16 planes of pf_wino6_weights(.., planes = true)
+// (Cout % 64 == 0), the GEMM splits V on the fly; 0: fp32 U.  up2: x is the
+// (h/2, w/2) map, h and w even.
+int pf_wino6_conv(const float* x, int xcs, int n, int h, int w, int Cin, const float* U,
+                  const float* bias, int Cout, int act, float* y, int ycs, void* ws,
+                  size_t ws_bytes, hipStream_t st, int stages, int planes, int up2) {
+  if (Cin % 32 || Cout % 4 || xcs % 2 || ycs % 2 || n <= 0 || h <= 0 || w <= 0 || planes > 1)
+    return POSFEAT_E_INVALID;
+  if (up2 && ((h & 1) || (w & 1))) return POSFEAT_E_INVALID;
+  if (ws_bytes < pf_wino6_ws_bytes(n, h, w, Cin, Cout)) return POSFEAT_E_WORKSPACE;
+  const long long T = (long long)n * ((h + 5) / 6) * ((w + 5) / 6);
+  float* V = static_cast<float*>(ws);
+  float* M = reinterpret_cast<float*>(static_cast<char*>(ws) + pf_align(64 * T * Cin * 4, 256));
+  if (stages & 1) {
+    // fused upsample: one channel per thread (occupancy); plain: channel pairs
+    if (up2)
+      hipLaunchKernelGGL((wino6_input_kernel<true, 1>), dim3(grid_for(T * Cin, 256)), dim3(256), 0,
+                         st, x, xcs, n, h, w, Cin, V);
+    else
+      hipLaunchKernelGGL((wino6_input_kernel<false, 2>), dim3(grid_for(T * (Cin / 2), 256)),
+                         dim3(256), 0, st, x, xcs, n, h, w, Cin / 2, V);
+    PF_CHECK_LAUNCH();
+  }
+  const unsigned short* Ub =
+      planes == 1 && wino_planes_ok(Cout) ? reinterpret_cast<const unsigned short*>(U) : nullptr;
+  if (stages & 2)
+    PF_TRY(pf_gemm_batched(V, Cin, T * Cin, U, (long long)Cout * Cin, M, Cout, T * Cout, 64, (int)T,
+                           Cout, Cin, st, Ub, 64LL * Cout * Cin));
+  if (stages & 4) {
+    hipLaunchKernelGGL(wino6_output_kernel, dim3(grid_for(T * (Cout / 2), 256)), dim3(256), 0, st,
+                       M, n, h, w, Cout / 2, bias, act, y, ycs);
+    PF_CHECK_LAUNCH();
+  }
+  return POSFEAT_OK;
+}
+
 namespace {
 
 // F(4x4) when both dims are multiples of 4 (all decoder layers at 480x640)
@@ -651,10 +989,6 @@ size_t pf_wino_weights_floats(int Cin, int Cout) { return (size_t)36 * Cin * Cou
 // U for the variant pf_wino_conv will pick at (h, w); h = w = 0: F(2x2)
 size_t pf_wino_weights_floats_bf6p(int Cin, int Cout) { return (size_t)54 * Cin * Cout; }
 
-// U as bf16 planes for the pre-split bf16x6 GEMM tiles: Cout a multiple of
-// 64 (128-wide tiles, or 64-wide ones for 192 = head.conv1; the tiles clamp
-// their rows past Cout, the epilogue never stores them)
-static bool wino_planes_ok(int Cout) { return Cout % 64 == 0; }
 
 int pf_wino_weights_hw(const float* wpk, int Cout, int Cin, int h, int w, float* U,
                        hipStream_t st, bool bf6p) {
@@ -854,4 +1188,23 @@ extern "C" int posfeat_conv3x3_wino(const float* x, int x_cstride, int n, int h,
   if (!x || !U || !y || !ws) return POSFEAT_E_INVALID;
   return pf_wino_conv(x, x_cstride, n, h, w, cin, U, bias, cout, act, y, y_cstride, ws, ws_bytes,
                       pf_stream(stream));
+}
+
+extern "C" size_t posfeat_wino6_workspace(int n, int h, int w, int cin, int cout) {
+  if (n <= 0 || h <= 0 || w <= 0) return 0;
+  return pf_wino6_ws_bytes(n, h, w, cin, cout);
+}
+
+extern "C" int posfeat_wino6_weights(const float* w_packed, int cout, int cin, float* U,
+                                     void* stream) {
+  if (!w_packed || !U) return POSFEAT_E_INVALID;
+  return pf_wino6_weights(w_packed, cout, cin, U, pf_stream(stream), false);
+}
+
+extern "C" int posfeat_conv3x3_wino6(const float* x, int x_cstride, int n, int h, int w, int cin,
+                                     const float* U, const float* bias, int cout, int act, float* y,
+                                     int y_cstride, void* ws, size_t ws_bytes, void* stream) {
+  if (!x || !U || !y || !ws) return POSFEAT_E_INVALID;
+  return pf_wino6_conv(x, x_cstride, n, h, w, cin, U, bias, cout, act, y, y_cstride, ws, ws_bytes,
+                       pf_stream(stream), 7, 0, 0);
 }

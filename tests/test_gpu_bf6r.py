@@ -69,10 +69,15 @@ def test_bf6d_bit_identical_to_bf6b(tmp_path):
                      ("r26", {"POSFEAT_CONV_TILE": "26"}),
                      ("b256", {"POSFEAT_CONV_TILE": "28", "POSFEAT_GEMM_B256": "1"}),
                      ("b256d4", {"POSFEAT_CONV_TILE": "28", "POSFEAT_GEMM_B256": "1",
-                                 "POSFEAT_BF6D": "4"}),
-                     # conv precision mode 2: the Winograd / tap GEMM A operands
-                     # pre-split by their producers (conv_bf6s_kernel)
-                     ("mode2", {"POSFEAT_BF6": "2"})):
+                                 "POSFEAT_BF6D": "4"})):
         got = _run(tmp_path, dict(x0, **env), tag)
         for k in ("lp", "lm", "gm"):
             np.testing.assert_array_equal(got[k], ref[k], err_msg="%s %s" % (tag, k))
+    # conv precision mode 2: the Winograd / tap GEMM A operands pre-split by
+    # their producers (conv_bf6s_kernel).  Its V planes exist for F(4x4) only,
+    # so mode 2 runs the decoder on F(4x4): compared with the bf6b reference
+    # on F(4x4) (POSFEAT_WINO6=0)
+    ref4 = _run(tmp_path, dict(x0, POSFEAT_BF6D="0", POSFEAT_WINO6="0"), "b4")
+    got = _run(tmp_path, dict(x0, POSFEAT_BF6="2"), "mode2")
+    for k in ("lp", "lm", "gm"):
+        np.testing.assert_array_equal(got[k], ref4[k], err_msg="mode2 %s" % k)

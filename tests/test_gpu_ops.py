@@ -122,6 +122,54 @@ def test_conv3x3_wino_vs_torch(gpu, case):
         assert torch.all(out[..., cout:] == 7.0).item(), "wrote outside its channel slice"
 
 
+WINO6_CASES = [
+    # n, h, w, cin, cout, act, in_extra, out_extra
+    (2, 18, 24, 64, 64, "none", 0, 0),       # whole 6x6 tiles
+    (2, 20, 26, 64, 128, "elu", 0, 0),       # last tile row / column cut
+    (1, 13, 7, 96, 64, "relu", 32, 0),       # odd sizes, strided input
+    (1, 30, 40, 1024, 512, "elu", 0, 512),   # upconv3 shape into a concat slice
+    (2, 60, 80, 512, 256, "elu", 0, 256),    # upconv2 / iconv2 shape (80 = 13 tiles + 2)
+    (1, 24, 32, 192, 192, "none", 0, 0),     # head.conv1
+]
+
+
+@pytest.mark.parametrize("case", WINO6_CASES)
+def test_conv3x3_wino6_vs_torch(gpu, case):
+    """Winograd F(6x6,3x3) (wino.hip, the extraction engine's decoder and
+    head.conv1) against the fp64 conv, with the F(4x4) test's bound: B^T and
+    A^T are exact in fp32 (quarters, powers of two to 32), G carries ninths and
+    1/90; measured errors sit well inside it."""
+    from posfeat_amd import ops
+    from posfeat_amd._lib import check, lib, ptr, stream_ptr
+    n, h, w, cin, cout, act, in_extra, out_extra = case
+    g = torch.Generator().manual_seed(sum(case[:5]) + 6)
+    x = torch.randn(n, cin, h, w, generator=g)
+    wt = torch.randn(cout, cin, 3, 3, generator=g) * (2.0 / (cin * 9)) ** 0.5
+    b = torch.randn(cout, generator=g) * 0.1
+    ref, bound = _conv_ref64(x, wt, b, 1, 1, None, act)
+    xcs = cin + in_extra
+    xd = torch.zeros(n, h, w, xcs)
+    xd[..., :cin] = x.permute(0, 2, 3, 1)
+    xd = xd.to(gpu)
+    wp, bp = ops.pack_conv_weight(wt.to(gpu), b.to(gpu))
+    U = torch.empty(64 * cout * cin, device=gpu)
+    check(lib().posfeat_wino6_weights(ptr(wp), cout, cin, ptr(U), stream_ptr()))
+    need = lib().posfeat_wino6_workspace(n, h, w, cin, cout)
+    ws = torch.empty(need, dtype=torch.uint8, device=gpu)
+    out = torch.full((n, h, w, cout + out_extra), 7.0, device=gpu)
+    actc = {"none": 0, "relu": 1, "elu": 2}[act]
+    check(lib().posfeat_conv3x3_wino6(ptr(xd), xcs, n, h, w, cin, ptr(U), ptr(bp), cout, actc,
+                                      ptr(out), cout + out_extra, ptr(ws), need, stream_ptr()))
+    torch.cuda.synchronize()
+    got = out[..., :cout].permute(0, 3, 1, 2).double().cpu()
+    err = (got - ref).abs()
+    tol = 3e-5 * bound + 1e-6
+    assert torch.all(err <= tol), "max err %g (ratio %g)" % (err.max(), (err / tol).max())
+    print("wino6 %s: max err / bound %.2e" % (case, (err / bound.clamp_min(1e-30)).max()))
+    if out_extra:
+        assert torch.all(out[..., cout:] == 7.0).item(), "wrote outside its channel slice"
+
+
 @pytest.mark.parametrize("act,has_res", [("elu", False), ("relu", True)])
 def test_conv_splitk_vs_torch(gpu, act, has_res):
     """Deep-K shape that takes the split-K path (partials + ordered reduce)."""
