@@ -482,7 +482,11 @@ int posfeat_model_head_backward(posfeat_model *m, const float *dlocal_point, flo
  * forward: img [b][3][h][w] NCHW; *local_map_nhwc = the NHWC local map
  *   [b][h/4][w/4][128] inside `act`.  stats may be NULL (no running update).
  * backward: dlocal_map NHWC (pixel stride dcs); grad = (accumulate ? grad : 0)
- *   + dL/d params.  h and w must be multiples of 16.
+ *   + dL/d params.  h and w must be multiples of 16.  An accumulate = 0 call
+ *   derives every layer's input-gradient weights (transposed / phase weights,
+ *   their bf16 planes, the Winograd U) into `scratch`; an accumulate = 1 call
+ *   reuses them, so it must follow an accumulate = 0 call with the SAME params
+ *   and scratch (the second image batch of one step, as the trainer does).
  * posfeat_adam: torch.optim.Adam (no amsgrad) on n floats; g is scaled by
  *   grad_scale first (1/world after a summing all-reduce = DDP's mean). */
 typedef struct posfeat_bbtrain posfeat_bbtrain;

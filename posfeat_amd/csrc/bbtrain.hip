@@ -150,12 +150,12 @@ struct posfeat_bbtrain {
   int B, H, W;
   // activation workspace (one per image batch)
   size_t act_bytes = 0;
-  Buf img4, a0, mp, cat2, cat3, l3out, up3, i3a, up2, i2a, fa;
+  Buf img4, a0, mp, mpidx, cat2, cat3, l3out, up3, i3a, up2, i2a, fa;
   std::vector<Buf> y, st;         // per layer: raw conv output, mean|rstd
   std::vector<Buf> a1, a2, bout;  // per bottleneck
   // scratch (shared by the batches: forward transients + backward)
   size_t scr_bytes = 0;
-  Buf dsn, part, coef, ga, gb, gc, gd, gres, dy, dz, dcat2, dcat3, dup, upt, wt, wgws, splitk;
+  Buf dsn, part, coef, ga, gb, gc, gd, gres, dy, dz, dcat2, dcat3, dup, upt, wgws, splitk;
   // SyncBatchNorm (posfeat_bbtrain_set_group): statistics summed over the
   // group's ranks; bnsum holds [local | group] sums of one layer
   posfeat_group* group = nullptr;
@@ -174,7 +174,12 @@ struct posfeat_bbtrain {
   // (weights read ready-made) instead of splitting both operands per wave --
   // the same products in the same order: bit-identical results
   bool wsplit = false;
-  Buf wpl, wtp;
+  Buf wpl;
+  // the input-gradient weights of every layer (transposed / phase weights,
+  // their bf16 planes, the Winograd U): derived by an accumulate = 0
+  // backward, reused by the accumulate = 1 call of the same step
+  Buf bw;
+  std::vector<size_t> bw_wt, bw_wtp, bw_u;  // float offsets into bw
   // optional per-launch timing (labels "fwd:conv", "bwd:wgrad", ...)
   bool timing = false;
   struct Ev {
@@ -326,6 +331,7 @@ void plan(posfeat_bbtrain* m) {
   alloc(m->img4, fl(B * H * W * 4));
   alloc(m->a0, fl(B * h2 * w2 * 64));
   alloc(m->mp, fl(B * h4 * w4 * 64));
+  alloc(m->mpidx, fl(B * h4 * w4 * 16));  // arg-max taps, one byte per channel
   alloc(m->cat2, fl(B * h4 * w4 * 512));
   alloc(m->cat3, fl(B * h8 * w8 * 1024));
   alloc(m->l3out, fl(B * h16 * w16 * 1024));
@@ -373,7 +379,7 @@ void plan(posfeat_bbtrain* m) {
   alloc(m->dcat3, fl(B * h8 * w8 * 1024));
   alloc(m->dup, fl(std::max(B * h4 * w4 * 512, B * h8 * w8 * 1024)));
   alloc(m->upt, fl(std::max(B * h4 * w8 * 512, B * h8 * w16 * 1024)));
-  size_t wt = 0, wg = 0, sk = 0, dzf = 0;
+  size_t wg = 0, sk = 0, dzf = 0;
   for (size_t li = 0; li < T.v.size(); ++li) {
     const TLayer& L = T.v[li];
     const int cinp = (L.cin + 3) / 4 * 4;
@@ -383,9 +389,7 @@ void plan(posfeat_bbtrain* m) {
                                     L.cout, 0);
     sk = std::max(sk, posfeat_conv2d_workspace(&d));
     if ((int)li != T.first) {
-      wt = std::max(wt, (size_t)L.cin * posfeat_conv_packed_k(L.cout, L.k, L.k));
       if (L.stride == 2 && L.k == 3) {
-        wt = std::max(wt, (size_t)4 * L.cin * posfeat_conv_packed_k(L.cout, 2, 2));
         posfeat_conv_desc e2 = make_desc((int)B, lih[li] / 2, liw[li] / 2, L.cout, L.cout,
                                          4 * L.cin, 2, 1, 4 * L.cin, 0);
         e2.pad = 1;
@@ -397,15 +401,11 @@ void plan(posfeat_bbtrain* m) {
       sk = std::max(sk, posfeat_conv2d_workspace(&e));
     }
   }
-  alloc(m->wt, fl(wt));
   {
     const char* e = pf_ab_getenv("POSFEAT_BF6B");
     m->wsplit = pf_conv_precision() == 1 && !(e && e[0] == '0') && T.params % 4 == 0;
   }
-  if (m->wsplit) {
-    alloc(m->wpl, (size_t)T.params * 6);
-    alloc(m->wtp, wt * 6 + 256);
-  }
+  if (m->wsplit) alloc(m->wpl, (size_t)T.params * 6);
   alloc(m->dz, fl(std::max(dzf, 2 * MAXG)));
   alloc(m->wgws, wg);
   alloc(m->splitk, std::max<size_t>(sk, 256));
@@ -439,6 +439,32 @@ void plan(posfeat_bbtrain* m) {
     }
     alloc(m->wu, fl(uf));
     alloc(m->wino_ws, wb);
+  }
+  {  // per-layer input-gradient weights (layer_bwd), 64-float aligned slots
+    size_t tot = 0;
+    auto slot = [&](size_t floats) {
+      const size_t o = tot;
+      tot += (floats + 63) / 64 * 64;
+      return o;
+    };
+    m->bw_wt.assign(T.v.size(), 0);
+    m->bw_wtp.assign(T.v.size(), 0);
+    m->bw_u.assign(T.v.size(), 0);
+    for (size_t li = 0; li < T.v.size(); ++li) {
+      if ((int)li == T.first) continue;
+      const TLayer& L = T.v[li];
+      const bool s2k3 = L.stride == 2 && m->s2phase && L.k == 3;
+      const size_t rows = s2k3 ? 4 * (size_t)L.cin : L.cin;
+      const size_t cols = s2k3 ? posfeat_conv_packed_k(L.cout, 2, 2)
+                               : posfeat_conv_packed_k(L.cout, L.k, L.k);
+      m->bw_wt[li] = slot(rows * cols);
+      if (m->wsplit) m->bw_wtp[li] = slot(rows * cols * 3 / 2 + 64);
+      if (m->wino && (li == (size_t)T.up3 || li == (size_t)T.ic3 || li == (size_t)T.up2 ||
+                      li == (size_t)T.ic2))
+        m->bw_u[li] = slot(std::max(pf_wino6_weights_floats(L.cout, L.cin, m->wsplit),
+                                    (size_t)54 * L.cin * L.cout));
+    }
+    alloc(m->bw, fl(tot));
   }
   m->scr_bytes = cur;
 }
@@ -595,7 +621,13 @@ int layer_bwd(Ctx& c, int li, const float* x, int xcs, int h, int w, const float
     }));
   }
   if (!dx) return POSFEAT_OK;
-  float* wt = c.s(m->wt);
+  // the input-gradient weights: derived here on an accumulate = 0 call, the
+  // accumulate = 1 call of the same step (same parameters, same scratch) reuses
+  // them (posfeat_bbtrain_backward)
+  const bool derive = !acc;
+  float* wt = c.s(m->bw) + m->bw_wt[li];
+  unsigned short* wtp = reinterpret_cast<unsigned short*>(c.s(m->bw) + m->bw_wtp[li]);
+  float* Ud = c.s(m->bw) + m->bw_u[li];
   if (L.stride == 2 && m->s2phase) {
     // output-phase input gradient (bbtrain_kernels.h): 1x1 -> compact GEMM,
     // 3x3 -> one 2x2 pad-1 conv with 4 Cin phase channels; then one scatter
@@ -604,7 +636,7 @@ int layer_bwd(Ctx& c, int li, const float* x, int xcs, int h, int w, const float
     const int oh2 = h / 2, ow2 = w / 2;
     float* dz = c.s(m->dz);
     const bool k3 = L.k == 3;
-    PF_TRY(timed(c, "bwd:misc", 0, [&] {
+    if (derive) PF_TRY(timed(c, "bwd:misc", 0, [&] {
       if (!k3) return pf_dgrad_weights(c.prm + L.w_off, C, L.cin, 1, 1, wt, c.st);
       hipLaunchKernelGGL(s2_phase_weights_kernel,
                          dim3(grid_for(16LL * L.cin * C, 256)), dim3(256), 0, c.st,
@@ -618,13 +650,13 @@ int layer_bwd(Ctx& c, int li, const float* x, int xcs, int h, int w, const float
     const double pf = k3 ? 2.0 * B * (oh2 + 1) * (ow2 + 1) * 4 * C * 4 * L.cin
                          : 2.0 * B * oh2 * ow2 * C * L.cin;
     const long long wrows = k3 ? 4LL * L.cin : L.cin, wcols = posfeat_conv_packed_k(C, d.kh, d.kw);
-    if (m->wsplit)
+    if (m->wsplit && derive)
       PF_TRY(timed(c, "bwd:misc", 0, [&] {
-        return pf_split3_rows(wt, wrows, (int)wcols, (int)wcols, c.su(m->wtp), c.st);
+        return pf_split3_rows(wt, wrows, (int)wcols, (int)wcols, wtp, c.st);
       }));
     PF_TRY(timed(c, std::string("bwd:dgrad:") + L.name, pf, [&] {
       return pf_conv_run_tile(&d, dy, wt, nullptr, nullptr, dz, c.s(m->splitk), m->splitk.bytes,
-                              -1, c.st, m->wsplit ? c.su(m->wtp) : nullptr, wrows * wcols);
+                              -1, c.st, m->wsplit ? wtp : nullptr, wrows * wcols);
     }));
     return timed(c, "bwd:misc", 0, [&] {
       hipLaunchKernelGGL(s2_scatter_kernel, dim3(grid_for((long long)B * h * w * (L.cin / 4), 256)),
@@ -636,7 +668,7 @@ int layer_bwd(Ctx& c, int li, const float* x, int xcs, int h, int w, const float
   }
   const float* src = dy;
   PF_TRY(timed(c, "bwd:misc", 0, [&] {
-    PF_TRY(pf_dgrad_weights(c.prm + L.w_off, C, L.cin, L.k, L.k, wt, c.st));
+    if (derive) PF_TRY(pf_dgrad_weights(c.prm + L.w_off, C, L.cin, L.k, L.k, wt, c.st));
     if (L.stride == 2) {
       if ((h & 1) || (w & 1)) return (int)POSFEAT_E_UNSUPPORTED;
       float* dz = c.s(m->dz);
@@ -648,18 +680,18 @@ int layer_bwd(Ctx& c, int li, const float* x, int xcs, int h, int w, const float
     return (int)POSFEAT_OK;
   }));
   if (!add && use_wino(m, li, h, w) && m->wino6) {
-    float* U = c.s(m->wu);
+    float* U = Ud;
     const double T6 = (double)B * ((h + 5) / 6) * ((w + 5) / 6);
     return timed(c, std::string("bwd:dgrad:") + L.name, 2.0 * T6 * 64 * C * L.cin, [&] {
-      PF_TRY(pf_wino6_weights(wt, L.cin, C, U, c.st, m->wsplit));
+      if (derive) PF_TRY(pf_wino6_weights(wt, L.cin, C, U, c.st, m->wsplit));
       return pf_wino6_conv(src, C, B, h, w, C, U, nullptr, L.cin, ACT_NONE, dx, dxcs,
                            c.s(m->wino_ws), m->wino_ws.bytes, c.st, 7, m->wsplit ? 1 : 0);
     });
   }
   if (!add && use_wino(m, li, h, w)) {
-    float* U = c.s(m->wu);
+    float* U = Ud;
     return timed(c, std::string("bwd:dgrad:") + L.name, wino_flops(B, h, w, C, L.cin), [&] {
-      PF_TRY(pf_wino_weights_hw(wt, L.cin, C, h, w, U, c.st, m->bf6p || m->wsplit));
+      if (derive) PF_TRY(pf_wino_weights_hw(wt, L.cin, C, h, w, U, c.st, m->bf6p || m->wsplit));
       return pf_wino_conv(src, C, B, h, w, C, U, nullptr, L.cin, ACT_NONE, dx, dxcs,
                           c.s(m->wino_ws), m->wino_ws.bytes, c.st, 7,
                           m->bf6p ? 2 : m->wsplit ? 1 : 0);
@@ -667,13 +699,13 @@ int layer_bwd(Ctx& c, int li, const float* x, int xcs, int h, int w, const float
   }
   posfeat_conv_desc d = make_desc(B, h, w, C, C, L.cin, L.k, 1, dxcs, add ? addcs : 0);
   const long long wcols = posfeat_conv_packed_k(C, L.k, L.k);
-  if (m->wsplit)
+  if (m->wsplit && derive)
     PF_TRY(timed(c, "bwd:misc", 0, [&] {
-      return pf_split3_rows(wt, L.cin, (int)wcols, (int)wcols, c.su(m->wtp), c.st);
+      return pf_split3_rows(wt, L.cin, (int)wcols, (int)wcols, wtp, c.st);
     }));
   return timed(c, std::string("bwd:dgrad:") + L.name, flops, [&] {
     return pf_conv_run_tile(&d, src, wt, nullptr, add, dx, c.s(m->splitk), m->splitk.bytes, -1,
-                            c.st, m->wsplit ? c.su(m->wtp) : nullptr, (long long)L.cin * wcols);
+                            c.st, m->wsplit ? wtp : nullptr, (long long)L.cin * wcols);
   });
 }
 
@@ -732,7 +764,11 @@ int forward(Ctx& c, const float* img, float* stats, float mom) {
                [&] { return pf_nchw_to_nhwc(img, B, 3, H, W, 4, c.f(m->img4), c.st); }));
   PF_TRY(layer_fwd(c, T.first, c.f(m->img4), 4, H, W, c.f(m->a0), 64, stats, mom));
   PF_TRY(timed(c, "fwd:misc", 0, [&] {
-    return pf_maxpool3s2(c.f(m->a0), B, h2, w2, 64, 64, c.f(m->mp), 64, c.st);
+    hipLaunchKernelGGL(maxpool3s2_idx_kernel, dim3(grid_for((long long)B * h4 * w4 * 16, 256)),
+                       dim3(256), 0, c.st, c.f(m->a0), 64, B, h2, w2, 16, h4, w4, c.f(m->mp), 64,
+                       reinterpret_cast<unsigned*>(c.f(m->mpidx)));
+    PF_CHECK_LAUNCH();
+    return (int)POSFEAT_OK;
   }));
   const auto& bl = blocks();
   const auto io = block_io(c);
@@ -841,8 +877,10 @@ int backward(Ctx& c, const float* dfa, int dfcs, float* grad, int acc) {
   // stem: cur = d(maxpool output)
   float* da0 = cur == ga ? gb : ga;
   PF_TRY(timed(c, "bwd:misc", 0, [&] {
-    hipLaunchKernelGGL(maxpool_adjoint_kernel, dim3(grid_for((long long)B * h2 * w2 * 16, 256)),
-                       dim3(256), 0, c.st, c.f(m->a0), 64, B, h2, w2, 16, cur, ccs, h4, w4, da0, 64);
+    hipLaunchKernelGGL(maxpool_adjoint_idx_kernel,
+                       dim3(grid_for((long long)B * h2 * w2 * 16, 256)), dim3(256), 0, c.st,
+                       reinterpret_cast<const unsigned*>(c.f(m->mpidx)), B, h2, w2, 16, cur, ccs,
+                       h4, w4, da0, 64);
     PF_CHECK_LAUNCH();
     return POSFEAT_OK;
   }));

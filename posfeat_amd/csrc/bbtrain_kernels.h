@@ -451,13 +451,55 @@ __global__ void zero_insert_kernel(const float* __restrict__ src, int n, int h, 
   }
 }
 
-// max_pool2d(3, 2, 1) adjoint as a gather: input pixel (iy, ix) collects the
-// gradient of every window whose arg-max it is; the arg-max is recomputed with
-// ATen's rule (scan order, replace on '>' or NaN, start at the window's first
-// valid pixel).
-__global__ void maxpool_adjoint_kernel(const float* __restrict__ x, int xcs, int n, int h, int w,
-                                       int c4n, const float* __restrict__ g, int gcs, int oh, int ow,
-                                       float* __restrict__ dx, int dxcs) {
+// max_pool2d(3, 2, 1) forward that also records each output's arg-max tap
+// t = 3 (iy - 2 oy + 1) + (ix - 2 ox + 1) per channel (one byte, idx
+// [n][oh][ow][C]), chosen by the adjoint's rule (scan order, replace on '>'
+// or NaN, start at the window's first valid pixel); y = the value there
+// (= fmaxf over the window for finite input, as maxpool3s2_kernel)
+__global__ void maxpool3s2_idx_kernel(const float* __restrict__ x, int xcs, int n, int h, int w,
+                                      int c4n, int oh, int ow, float* __restrict__ y, int ycs,
+                                      unsigned* __restrict__ idx) {
+  const long long total = (long long)n * oh * ow * c4n;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    long long p;
+    const int q = pf_quad_split(i, c4n, p);
+    int ox, oy;
+    const int b = pix_split(p, ow, oh, ox, oy);
+    f32x4 v[9];
+    bool ok[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int iy = 2 * oy + t / 3 - 1, ix = 2 * ox + t % 3 - 1;
+      ok[t] = (unsigned)iy < (unsigned)h && (unsigned)ix < (unsigned)w;
+      const int cy = min(max(iy, 0), h - 1), cx = min(max(ix, 0), w - 1);
+      v[t] = *reinterpret_cast<const f32x4*>(x + (((long long)b * h + cy) * w + cx) * xcs + q * 4);
+    }
+    f32x4 mv = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    int mt[4] = {-1, -1, -1, -1};
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      if (!ok[t]) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (mt[j] < 0 || v[t][j] > mv[j] || isnan(v[t][j])) {
+          mv[j] = v[t][j];
+          mt[j] = t;
+        }
+    }
+    *reinterpret_cast<f32x4*>(y + p * ycs + q * 4) = mv;
+    idx[i] = (unsigned)mt[0] | ((unsigned)mt[1] << 8) | ((unsigned)mt[2] << 16) |
+             ((unsigned)mt[3] << 24);
+  }
+}
+
+// max_pool2d(3, 2, 1) adjoint as a gather from the recorded arg-max taps:
+// input pixel (iy, ix) sums the gradient of every window whose tap points at
+// it, windows in row-major order (the sums of the round-4 form, which re-read
+// and re-ranked the nine inputs of each window: 4 + 16 bytes per window now)
+__global__ void maxpool_adjoint_idx_kernel(const unsigned* __restrict__ idx, int n, int h, int w,
+                                           int c4n, const float* __restrict__ g, int gcs, int oh,
+                                           int ow, float* __restrict__ dx, int dxcs) {
   const long long total = (long long)n * h * w * c4n;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
@@ -465,35 +507,22 @@ __global__ void maxpool_adjoint_kernel(const float* __restrict__ x, int xcs, int
     const int q = pf_quad_split(i, c4n, p);
     int ix, iy;
     const int b = pix_split(p, w, h, ix, iy);
-    const float* xb = x + (long long)b * h * w * xcs + q * 4;
     f32x4 acc = {0, 0, 0, 0};
     const int oy0 = iy / 2, oy1 = min(oh - 1, (iy + 1) / 2);
     const int ox0 = ix / 2, ox1 = min(ow - 1, (ix + 1) / 2);
     for (int oy = oy0; oy <= oy1; ++oy) {
       for (int ox = ox0; ox <= ox1; ++ox) {
-        const int ys = max(2 * oy - 1, 0), ye = min(2 * oy + 1, h - 1);
-        const int xs = max(2 * ox - 1, 0), xe = min(2 * ox + 1, w - 1);
-        f32x4 mv = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-        int my[4] = {ys, ys, ys, ys}, mx[4] = {xs, xs, xs, xs};
-        for (int yy = ys; yy <= ye; ++yy)
-          for (int xx = xs; xx <= xe; ++xx) {
-            const f32x4 v = *reinterpret_cast<const f32x4*>(xb + ((long long)yy * w + xx) * xcs);
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              if (v[j] > mv[j] || isnan(v[j])) {
-                mv[j] = v[j];
-                my[j] = yy;
-                mx[j] = xx;
-              }
-          }
-        const f32x4 gv =
-            *reinterpret_cast<const f32x4*>(g + (((long long)b * oh + oy) * ow + ox) * gcs + q * 4);
+        const long long o = ((long long)b * oh + oy) * ow + ox;
+        const unsigned tw = idx[o * c4n + q];
+        const f32x4 gv = *reinterpret_cast<const f32x4*>(g + o * gcs + q * 4);
+        const int ty = iy - 2 * oy + 1, tx = ix - 2 * ox + 1;
+        const unsigned me = (unsigned)(3 * ty + tx);
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          if (my[j] == iy && mx[j] == ix) acc[j] += gv[j];
+          if (((tw >> (8 * j)) & 255u) == me) acc[j] += gv[j];
       }
     }
-    *reinterpret_cast<f32x4*>(dx + (((long long)b * h + iy) * w + ix) * dxcs + q * 4) = acc;
+    *reinterpret_cast<f32x4*>(dx + p * dxcs + q * 4) = acc;
   }
 }
 
