@@ -164,6 +164,7 @@ struct posfeat_bbtrain {
   // gradient (wino.hip; POSFEAT_WINO=0: direct conv)
   bool wino = true;
   bool wino6 = true;  // F(6x6) forward + input gradient (POSFEAT_TRAIN_WINO6=0, A/B: F(4x4))
+  bool wino6_wg = true;  // F(6x6) weight gradient (POSFEAT_TRAIN_WINO6_WGRAD=0, A/B: F(4x4))
   bool bf6p = false;     // conv precision mode 2 at create (pre-split Winograd operands)
   bool s2phase = true;  // stride-2 input gradients by output phases (POSFEAT_S2PHASE=0: zero insertion)
   Buf wu, wino_ws;
@@ -421,6 +422,8 @@ void plan(posfeat_bbtrain* m) {
   {
     const char* e = pf_ab_getenv("POSFEAT_TRAIN_WINO6");
     m->wino6 = !(e && e[0] == '0') && !m->bf6p;
+    const char* g = pf_ab_getenv("POSFEAT_TRAIN_WINO6_WGRAD");
+    m->wino6_wg = !(g && g[0] == '0');
   }
   if (m->wino) {
     size_t uf = 0, wb = 0;
@@ -436,6 +439,8 @@ void plan(posfeat_bbtrain* m) {
       wb = std::max(wb, pf_wino_ws_bytes((int)B, lih[li], liw[li], L.cout, L.cin));
       if (lih[li] % 4 == 0 && liw[li] % 4 == 0)
         wb = std::max(wb, pf_wino_wgrad_ws_bytes((int)B, lih[li], liw[li], L.cin, L.cout));
+      if (m->wino6_wg && L.cin % 128 == 0 && L.cout % 128 == 0)
+        wb = std::max(wb, pf_wino6_wgrad_ws_bytes((int)B, lih[li], liw[li], L.cin, L.cout));
     }
     alloc(m->wu, fl(uf));
     alloc(m->wino_ws, wb);
@@ -607,7 +612,15 @@ int layer_bwd(Ctx& c, int li, const float* x, int xcs, int h, int w, const float
   }));
   const double flops = 2.0 * P * C * L.cin * L.k * L.k;
   const int cinp = (L.cin + 3) / 4 * 4;
-  if (use_wino(m, li, h, w) && h % 4 == 0 && w % 4 == 0 && L.cin % 128 == 0 && C % 128 == 0) {
+  if (use_wino(m, li, h, w) && m->wino6_wg && L.cin % 128 == 0 && C % 128 == 0) {
+    const double T6 = (double)B * ((h + 5) / 6) * ((w + 5) / 6);
+    PF_TRY(timed(c, std::string("bwd:wgrad:") + L.name, 2.0 * T6 * 64 * L.cin * C, [&] {
+      return pf_wino6_wgrad(dy, C, x, xcs, B, h, w, L.cin, C, grad + L.w_off,
+                            L.bias ? grad + L.b_off : nullptr, acc, c.s(m->wino_ws),
+                            m->wino_ws.bytes, c.st);
+    }));
+  } else if (use_wino(m, li, h, w) && h % 4 == 0 && w % 4 == 0 && L.cin % 128 == 0 &&
+             C % 128 == 0) {
     PF_TRY(timed(c, std::string("bwd:wgrad:") + L.name, wino_flops(B, h, w, L.cin, C, true), [&] {
       return pf_wino_wgrad(dy, C, x, xcs, B, h, w, L.cin, C, grad + L.w_off,
                            L.bias ? grad + L.b_off : nullptr, acc, c.s(m->wino_ws),

@@ -645,6 +645,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void d
     }
   };
   const float c2 = a.T * 1.4426950408889634f;  // T log2(e)
+  float t2 = 0.f, k2 = 0.f;  // SUM: 2 T log2(e), (-2 T - lse_B) log2(e) (set with B's metadata)
+  // the two rewards held in VGPRs once (as kernel arguments they were moved
+  // from SGPRs into VGPRs for every element's select)
+  float vgood = a.good, vbad = a.bad;
+  asm volatile("" : "+v"(vgood), "+v"(vbad));
   float run_m = -INFINITY, run_s = 0.f;  // LSE: running max (base 2) / sum of exp
   float gs = 0.f;                        // SUM: sum reward p
   double rs = 0.0;                       // SUM (WR): sum reward p (logp terms)
@@ -743,6 +748,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void d
       run_s = run_s * __builtin_amdgcn_exp2f(run_m - nmc) + ((ad[0] + ad[1]) + (ad[2] + ad[3]));
       run_m = nm;
     } else {
+      // log2 p = 2 T log2(e) s + (-2 T - lse_A - lse_B) log2(e): one sub (the
+      // column's part is a lane constant, the row's is metadata [7]), one fma,
+      // one v_exp_f32 -- the round-4 form took 2 subs, an add, an fma and a mul;
+      // the two line tests as one max of their magnitudes (the SUM passes
+      // were VALU-bound, 8.8-13 k VALU per 1.1 k MFMA per wave)
       float gp[2] = {0.f, 0.f};
       double rp2[2] = {0.0, 0.0};
 #pragma unroll
@@ -751,14 +761,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void d
         const int lr = 4 * h + (r & 3) + 8 * (r >> 2);  // row within the stage
         const f32x4 m0 = *reinterpret_cast<const f32x4*>(M + lr * 8);
         const f32x4 m1 = *reinterpret_cast<const f32x4*>(M + lr * 8 + 4);
-        const float aff = fmaf(a.T, acc[r], -a.T);
-        const float lp = (aff - m0[0]) + (aff - bm0[0]);  // log p = lpa + lpb
-        const float p = __builtin_amdgcn_exp2f(lp * 1.4426950408889634f);
-        const float dA = fabsf(m0[1] * bm1[0] + m0[2] * bm1[1] + m0[3]);    // A's line at B's point
-        const float dB = fabsf(bm0[1] * m1[0] + bm0[2] * m1[1] + bm0[3]);  // B's line at A's point
-        const float rp = ((dA < a.thr && dB < a.thr) ? a.good : a.bad) * p;
+        const float lp2 = fmaf(t2, acc[r], k2 - m1[3]);  // log2 p
+        const float p = __builtin_amdgcn_exp2f(lp2);
+        const float dA = fmaf(m0[1], bm1[0], fmaf(m0[2], bm1[1], m0[3]));    // A's line at B's pt
+        const float dB = fmaf(bm0[1], m1[0], fmaf(bm0[2], m1[1], bm0[3]));  // B's line at A's pt
+        const float rp = (fmaxf(fabsf(dA), fabsf(dB)) < a.thr ? vgood : vbad) * p;
         gp[r & 1] += rp;
-        if (WR) rp2[r & 1] += (double)(rp * (lp + (m1[2] + bm1[2])));
+        if (WR) rp2[r & 1] += (double)(rp * (lp2 * 0.6931471805599453f + (m1[2] + bm1[2])));
       }
       gs += gp[0] + gp[1];
       if (WR) rs += rp2[0] + rp2[1];
@@ -779,6 +788,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void d
   if (SUM) {
     bm0 = *reinterpret_cast<const f32x4*>(a.B.meta + (pb + cpt) * 8);
     bm1 = *reinterpret_cast<const f32x4*>(a.B.meta + (pb + cpt) * 8 + 4);
+    t2 = 2.f * c2;
+    k2 = -t2 - bm1[3];
   }
   // LSE: stage i's MFMAs and stage i-1's epilogue in one block (no branch
   // between them), free to interleave.  SUM: each stage's epilogue right after
@@ -877,7 +888,9 @@ __global__ void flash_gather_kernel(const unsigned short* __restrict__ pl, Flash
     const long long p = pb + src;
     float* m = cmeta + (pb + i) * 8;
     *reinterpret_cast<f32x4*>(m) = f32x4{s.lse[p], s.line[p * 3], s.line[p * 3 + 1], s.line[p * 3 + 2]};
-    *reinterpret_cast<f32x4*>(m + 4) = f32x4{s.cpx[p * 2], s.cpx[p * 2 + 1], s.logp[p], 0.f};
+    // [7]: lse in base 2, the SUM epilogue's per-row term (disk_flash6_kernel)
+    *reinterpret_cast<f32x4*>(m + 4) =
+        f32x4{s.cpx[p * 2], s.cpx[p * 2 + 1], s.logp[p], s.lse[p] * 1.4426950408889634f};
   }
 }
 

@@ -907,6 +907,114 @@ __global__ __launch_bounds__(256) void wino6_output_kernel(const float* __restri
 }
 }  // namespace
 
+// ---- F(6x6) weight gradient (the train-mode decoder): dM = A dY A^T per 6x6
+// output tile (8x8, dY = 0 past the map), dU_xi = sum_tiles dM_xi (x) V_xi
+// (64 batched GEMMs), dg = G^T dU G.  xi = (1, 1) sums dY (column 1 of A is
+// all ones): the bias gradient.
+namespace {
+__global__ __launch_bounds__(256) void wino6_dy_kernel(const float* __restrict__ dy, int ldy, int n,
+                                                       int h, int w, int c2n,
+                                                       float* __restrict__ dM) {
+  const int th = (h + 5) / 6, tw = (w + 5) / 6;
+  const long long T = (long long)n * th * tw;
+  const long long total = T * c2n;
+  const int C = c2n * 2;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    int q, tx, ty;
+    const int b = pf_tile_split(i, c2n, tw, th, q, tx, ty);
+    const long long tile = ((long long)b * th + ty) * tw + tx;
+    f32x2 t[8][6];  // A dY
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+#pragma unroll
+      for (int j = 0; j < 6; ++j) t[r][j] = f32x2{0.f, 0.f};
+#pragma unroll
+    for (int ii = 0; ii < 6; ++ii) {
+      const int yy = 6 * ty + ii;
+      const bool rin = yy < h;
+      const float* dr = dy + ((long long)b * h + min(yy, h - 1)) * w * ldy + q * 2;
+      f32x2 g[6];
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        const int xx = 6 * tx + j;
+        const f32x2 v = *reinterpret_cast<const f32x2*>(dr + min(xx, w - 1) * ldy);
+        g[j] = rin && xx < w ? v : f32x2{0.f, 0.f};
+      }
+#pragma unroll
+      for (int r = 0; r < 8; ++r)
+        if (W6_AT[ii][r] != 0.f)
+#pragma unroll
+          for (int j = 0; j < 6; ++j) t[r][j] = w6_fma(W6_AT[ii][r], g[j], t[r][j]);
+    }
+    const long long xs = T * C;
+    float* mo = dM + tile * C + q * 2;
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        f32x2 v = {0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < 6; ++j)
+          if (W6_AT[j][c] != 0.f) v = w6_fma(W6_AT[j][c], t[r][j], v);
+        *reinterpret_cast<f32x2*>(mo) = v;
+        mo += xs;
+        asm volatile("" : "+v"(mo));
+      }
+  }
+}
+
+// dU = the nsplit GEMM partials summed in order; dW[co][(ci/32, tap, ci%32)]
+// (+)= (G^T dU G)[tap]; db (+)= the bias partials summed in order
+__global__ void wino6_wgrad_out_kernel(const float* __restrict__ part, int nsplit, int Cout,
+                                       int Cin, int kpad, float* __restrict__ dw,
+                                       const float* __restrict__ partb, float* __restrict__ db,
+                                       int acc) {
+  const long long n = (long long)Cout * Cin;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int co = (int)(i / Cin), ci = (int)(i - (long long)co * Cin);
+    float u[64];
+#pragma unroll
+    for (int x = 0; x < 64; ++x) u[x] = 0.f;
+    for (int s = 0; s < nsplit; ++s) {  // the 64 loads of a split in flight together
+      float v[64];
+#pragma unroll
+      for (int x = 0; x < 64; ++x) v[x] = part[((long long)x * nsplit + s) * n + i];
+#pragma unroll
+      for (int x = 0; x < 64; ++x) u[x] += v[x];
+    }
+    float sv[3][8];
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        float v = 0.f;
+#pragma unroll
+        for (int a = 0; a < 8; ++a)
+          if (W6_G[a][kh] != 0.f) v += W6_G[a][kh] * u[a * 8 + b];
+        sv[kh][b] = v;
+      }
+    float* out = dw + (long long)co * kpad + (ci >> 5) * 9 * 32 + (ci & 31);
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        float v = 0.f;
+#pragma unroll
+        for (int b = 0; b < 8; ++b)
+          if (W6_G[b][kw] != 0.f) v += sv[kh][b] * W6_G[b][kw];
+        float* o = out + (kh * 3 + kw) * 32;
+        *o = acc ? *o + v : v;
+      }
+    if (db && ci == 0) {
+      const float v = pf_ordered_sum(partb + co, Cout, nsplit);
+      db[co] = acc ? db[co] + v : v;
+    }
+  }
+}
+}  // namespace
+
 size_t pf_wino6_ws_bytes(int n, int h, int w, int Cin, int Cout) {
   const size_t T = (size_t)n * ((h + 5) / 6) * ((w + 5) / 6);
   return pf_align(64 * T * Cin * 4, 256) + pf_align(64 * T * Cout * 4, 256);
@@ -1101,11 +1209,11 @@ int pf_wino_conv(const float* x, int xcs, int n, int h, int w, int Cin, const fl
 namespace {
 // split the tile reduction so the 36 x (Cout/128) x (Cin/128) GEMM tiles reach >= 2048
 // workgroups (1024..8192 measured within 1% of each other)
-int wino_wgrad_nsplit(long long T, int Cin, int Cout) {
+int wino_wgrad_nsplit(long long T, int Cin, int Cout, int nb = 36) {
   // (Cin, Cout % 128 == 0 for every caller; guarded so no shape divides by 0 --
   // tools/asan_host.py found posfeat_wino_wgrad_workspace(.., cin = 32, ..)
   // raising SIGFPE here)
-  const long long tiles = std::max(1LL, 36LL * (Cout / 128) * (Cin / 128));
+  const long long tiles = std::max(1LL, (long long)nb * (Cout / 128) * (Cin / 128));
   long long s = (2048 + tiles - 1) / tiles;
   const long long chunks = (T + 63) / 64;
   s = std::min(s, std::max(1LL, chunks / 8));  // >= 8 row chunks per split
@@ -1149,6 +1257,46 @@ int pf_wino_wgrad(const float* dy, int ldy, const float* x, int xcs, int n, int 
                                part, db ? partb : nullptr, 7, st));
   const int kpad = posfeat_conv_packed_k(Cin, 3, 3);
   hipLaunchKernelGGL(wino4_wgrad_out_kernel, dim3(grid_for((long long)Cout * Cin, 256)), dim3(256),
+                     0, st, part, ns, Cout, Cin, kpad, dw, partb, db, acc);
+  PF_CHECK_LAUNCH();
+  return POSFEAT_OK;
+}
+
+// V [64][T][Cin] | dM [64][T][Cout] | GEMM partials [64][nsplit][Cout][Cin] | bias partials
+size_t pf_wino6_wgrad_ws_bytes(int n, int h, int w, int Cin, int Cout) {
+  const long long T = (long long)n * ((h + 5) / 6) * ((w + 5) / 6);
+  const int ns = wino_wgrad_nsplit(T, Cin, Cout, 64);
+  return pf_align(64 * T * Cin * 4, 256) + pf_align(64 * T * Cout * 4, 256) +
+         pf_align((size_t)64 * ns * Cout * Cin * 4, 256) + pf_align((size_t)ns * Cout * 4, 256);
+}
+
+// Weight gradient of a 3x3 stride-1 pad-1 conv by F(6x6) (any h, w; Cin,
+// Cout % 128 == 0), arguments as pf_wino_wgrad's
+int pf_wino6_wgrad(const float* dy, int ldy, const float* x, int xcs, int n, int h, int w, int Cin,
+                   int Cout, float* dw, float* db, int acc, void* ws, size_t ws_bytes,
+                   hipStream_t st) {
+  if (Cin % 128 || Cout % 128 || ldy % 2 || xcs % 2 || n <= 0 || h <= 0 || w <= 0)
+    return POSFEAT_E_INVALID;
+  if (ws_bytes < pf_wino6_wgrad_ws_bytes(n, h, w, Cin, Cout)) return POSFEAT_E_WORKSPACE;
+  const long long T = (long long)n * ((h + 5) / 6) * ((w + 5) / 6);
+  const int ns = wino_wgrad_nsplit(T, Cin, Cout, 64);
+  char* p = static_cast<char*>(ws);
+  float* V = reinterpret_cast<float*>(p);
+  p += pf_align(64 * T * Cin * 4, 256);
+  float* dM = reinterpret_cast<float*>(p);
+  p += pf_align(64 * T * Cout * 4, 256);
+  float* part = reinterpret_cast<float*>(p);
+  p += pf_align((size_t)64 * ns * Cout * Cin * 4, 256);
+  float* partb = reinterpret_cast<float*>(p);
+  hipLaunchKernelGGL((wino6_input_kernel<false, 2>), dim3(grid_for(T * (Cin / 2), 256)), dim3(256),
+                     0, st, x, xcs, n, h, w, Cin / 2, V);
+  hipLaunchKernelGGL(wino6_dy_kernel, dim3(grid_for(T * (Cout / 2), 256)), dim3(256), 0, st, dy,
+                     ldy, n, h, w, Cout / 2, dM);
+  PF_CHECK_LAUNCH();
+  PF_TRY(pf_wgrad_gemm_batched(dM, Cout, T * Cout, V, Cin, T * Cin, (int)T, Cin, Cout, 64, ns,
+                               part, db ? partb : nullptr, 9, st));
+  const int kpad = posfeat_conv_packed_k(Cin, 3, 3);
+  hipLaunchKernelGGL(wino6_wgrad_out_kernel, dim3(grid_for((long long)Cout * Cin, 256)), dim3(256),
                      0, st, part, ns, Cout, Cin, kpad, dw, partb, db, acc);
   PF_CHECK_LAUNCH();
   return POSFEAT_OK;
