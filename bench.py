@@ -411,9 +411,11 @@ def main():
     tfile = os.path.join(ROOT, "records", "dominant_traffic.json")
     if os.path.exists(tfile):
         try:
-            t = json.load(open(tfile))
-            if dom in t.get("labels", []) and t.get("batch") == args.batch:
-                traffic = t.get("bytes_per_launch")
+            recs = json.load(open(tfile))
+            for t in recs.get("records", [recs]):  # one record or {"records": [...]}
+                if dom in t.get("labels", []) and t.get("batch") == args.batch:
+                    traffic = t.get("bytes_per_launch")
+                    break
         except Exception:
             traffic = None
 

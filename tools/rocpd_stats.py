@@ -1,10 +1,11 @@
-"""Per-kernel summary of a rocprofv3 kernel-trace database (the rocpd SQLite
-output rocprofv3 7.x writes by default): kernel name + grid, calls, average
+"""Per-kernel summary of a rocprofv3 kernel trace (the rocpd SQLite output
+rocprofv3 7.x writes by default, or its --output-format csv kernel_trace.csv):
+kernel name + grid, calls, average
 and total duration, share of the total.  Optional --per NAME divides the
 totals by the call count of that kernel (e.g. a once-per-step kernel) to give
 microseconds per step.
 
-usage: python tools/rocpd_stats.py <results.db> [--top N] [--per KERNEL] [--grep S]
+usage: python tools/rocpd_stats.py <results.db | kernel_trace.csv> [--top N] [--per KERNEL] [--grep S]
 """
 import argparse
 import re
@@ -29,8 +30,16 @@ def main(argv=None):
     ap.add_argument("--grep", default=None)
     ap.add_argument("--by-name", action="store_true", help="merge grids of one kernel")
     a = ap.parse_args(argv)
-    c = sqlite3.connect(a.db)
-    rows = c.execute("select name, grid_x, grid_y, grid_z, workgroup_x, duration from kernels").fetchall()
+    if a.db.endswith(".csv"):  # rocprofv3 --output-format csv kernel trace
+        import csv
+        rows = [(r["Kernel_Name"], int(r["Grid_Size_X"]), int(r["Grid_Size_Y"]),
+                 int(r["Grid_Size_Z"]), int(r["Workgroup_Size_X"]),
+                 int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+                for r in csv.DictReader(open(a.db))]
+    else:
+        c = sqlite3.connect(a.db)
+        rows = c.execute("select name, grid_x, grid_y, grid_z, workgroup_x, duration "
+                         "from kernels").fetchall()
     agg = defaultdict(lambda: [0, 0.0])
     calls_by_name = defaultdict(int)
     for name, gx, gy, gz, wx, dur in rows:
