@@ -152,6 +152,7 @@ struct posfeat_bbtrain {
   size_t act_bytes = 0;
   Buf img4, a0, mp, mpidx, cat2, cat3, l3out, up3, i3a, up2, i2a, fa;
   std::vector<Buf> y, st;         // per layer: raw conv output, mean|rstd
+  std::vector<Buf> vk;            // per F(6x6) decoder layer: the forward's V
   std::vector<Buf> a1, a2, bout;  // per bottleneck
   // scratch (shared by the batches: forward transients + backward)
   size_t scr_bytes = 0;
@@ -285,6 +286,12 @@ bool use_wino(const posfeat_bbtrain* m, int li, int h, int w) {
          !(w & 1);
 }
 
+// a decoder layer whose F(6x6) forward keeps V for its F(6x6) weight gradient
+bool vkeep_layer(const posfeat_bbtrain* m, int li) {
+  const TLayer& L = tab().v[li];
+  return m->wino && m->wino6 && m->wino6_wg && L.cin % 128 == 0 && L.cout % 128 == 0;
+}
+
 // input spatial size of every layer (forward order of DescNet.py:64-84)
 void layer_inputs(int H, int W, std::vector<int>& ih, std::vector<int>& iw) {
   const TTable& T = tab();
@@ -328,6 +335,17 @@ void plan(posfeat_bbtrain* m) {
   auto fl = [](size_t n) { return n * sizeof(float); };
   std::vector<int> lih, liw;
   layer_inputs(m->H, m->W, lih, liw);
+  {  // path switches (A/B build), fixed for the handle: buffer sizes depend on them
+    const char* e = pf_ab_getenv("POSFEAT_WINO");
+    m->wino = !(e && e[0] == '0');
+    const char* s2 = pf_ab_getenv("POSFEAT_S2PHASE");
+    m->s2phase = !(s2 && s2[0] == '0');
+    m->bf6p = pf_bf6p_on();
+    const char* w6 = pf_ab_getenv("POSFEAT_TRAIN_WINO6");
+    m->wino6 = !(w6 && w6[0] == '0') && !m->bf6p;
+    const char* g = pf_ab_getenv("POSFEAT_TRAIN_WINO6_WGRAD");
+    m->wino6_wg = !(g && g[0] == '0');
+  }
   // ---- activations
   alloc(m->img4, fl(B * H * W * 4));
   alloc(m->a0, fl(B * h2 * w2 * 64));
@@ -361,6 +379,12 @@ void plan(posfeat_bbtrain* m) {
     alloc(m->y[li], fl(B * oh * ow * L.cout));
     alloc(m->st[li], fl(2 * (size_t)L.cout));
   }
+  // the F(6x6) decoder layers' transformed inputs V, kept from the forward for
+  // their weight gradient (pf_wino6_conv vkeep -> pf_wino6_wgrad vpre)
+  m->vk.assign(T.v.size(), Buf());
+  for (int li : {T.up3, T.ic3, T.up2, T.ic2})
+    if (vkeep_layer(m, li))
+      alloc(m->vk[li], fl(pf_wino6_v_floats((int)B, lih[li], liw[li], T.v[li].cin)));
   m->act_bytes = cur;
   // ---- scratch
   cur = 0;
@@ -410,21 +434,6 @@ void plan(posfeat_bbtrain* m) {
   alloc(m->dz, fl(std::max(dzf, 2 * MAXG)));
   alloc(m->wgws, wg);
   alloc(m->splitk, std::max<size_t>(sk, 256));
-  {
-    const char* e = pf_ab_getenv("POSFEAT_WINO");
-    m->wino = !(e && e[0] == '0');
-  }
-  {
-    const char* e = pf_ab_getenv("POSFEAT_S2PHASE");
-    m->s2phase = !(e && e[0] == '0');
-  }
-  m->bf6p = pf_bf6p_on();  // fixed for the handle: the U buffer size depends on it
-  {
-    const char* e = pf_ab_getenv("POSFEAT_TRAIN_WINO6");
-    m->wino6 = !(e && e[0] == '0') && !m->bf6p;
-    const char* g = pf_ab_getenv("POSFEAT_TRAIN_WINO6_WGRAD");
-    m->wino6_wg = !(g && g[0] == '0');
-  }
   if (m->wino) {
     size_t uf = 0, wb = 0;
     for (int li : {T.up3, T.ic3, T.up2, T.ic2}) {
@@ -500,7 +509,8 @@ int layer_fwd(Ctx& c, int li, const float* x, int xcs, int h, int w, float* out,
     PF_TRY(timed(c, std::string("fwd:conv:") + L.name, 2.0 * T6 * 64 * L.cin * L.cout, [&] {
       PF_TRY(pf_wino6_weights(c.prm + L.w_off, L.cout, L.cin, U, c.st, m->wsplit));
       return pf_wino6_conv(x, xcs, m->B, h, w, L.cin, U, c.prm + L.b_off, L.cout, ACT_NONE, y,
-                           L.cout, c.s(m->wino_ws), m->wino_ws.bytes, c.st, 7, m->wsplit ? 1 : 0);
+                           L.cout, c.s(m->wino_ws), m->wino_ws.bytes, c.st, 7, m->wsplit ? 1 : 0,
+                           0, vkeep_layer(m, li) ? c.f(m->vk[li]) : nullptr);
     }));
   } else if (use_wino(m, li, h, w)) {
     float* U = c.s(m->wu);
@@ -617,7 +627,8 @@ int layer_bwd(Ctx& c, int li, const float* x, int xcs, int h, int w, const float
     PF_TRY(timed(c, std::string("bwd:wgrad:") + L.name, 2.0 * T6 * 64 * L.cin * C, [&] {
       return pf_wino6_wgrad(dy, C, x, xcs, B, h, w, L.cin, C, grad + L.w_off,
                             L.bias ? grad + L.b_off : nullptr, acc, c.s(m->wino_ws),
-                            m->wino_ws.bytes, c.st);
+                            m->wino_ws.bytes, c.st,
+                            vkeep_layer(m, li) ? c.f(m->vk[li]) : nullptr);
     }));
   } else if (use_wino(m, li, h, w) && h % 4 == 0 && w % 4 == 0 && L.cin % 128 == 0 &&
              C % 128 == 0) {

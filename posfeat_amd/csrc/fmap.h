@@ -76,14 +76,21 @@ int pf_wino_conv(const float* x, int xcs, int n, int h, int w, int Cin, const fl
 size_t pf_wino6_ws_bytes(int n, int h, int w, int Cin, int Cout);
 size_t pf_wino6_weights_floats(int Cin, int Cout, bool planes);
 int pf_wino6_weights(const float* wpk, int Cout, int Cin, float* U, hipStream_t st, bool planes);
+// vkeep: V ([64][T][Cin] fp32, pf_wino6_v_floats) goes there instead of ws,
+// for the weight gradient of the same x (pf_wino6_wgrad's vpre)
 int pf_wino6_conv(const float* x, int xcs, int n, int h, int w, int Cin, const float* U,
                   const float* bias, int Cout, int act, float* y, int ycs, void* ws,
-                  size_t ws_bytes, hipStream_t st, int stages = 7, int planes = 0, int up2 = 0);
-// F(6x6) weight gradient (any h, w; Cin, Cout % 128 == 0), as pf_wino_wgrad
+                  size_t ws_bytes, hipStream_t st, int stages = 7, int planes = 0, int up2 = 0,
+                  float* vkeep = nullptr);
+inline size_t pf_wino6_v_floats(int n, int h, int w, int Cin) {
+  return (size_t)64 * n * ((h + 5) / 6) * ((w + 5) / 6) * Cin;
+}
+// F(6x6) weight gradient (any h, w; Cin, Cout % 128 == 0), as pf_wino_wgrad;
+// vpre: x's V from the forward (skips the input transform)
 size_t pf_wino6_wgrad_ws_bytes(int n, int h, int w, int Cin, int Cout);
 int pf_wino6_wgrad(const float* dy, int ldy, const float* x, int xcs, int n, int h, int w, int Cin,
                    int Cout, float* dw, float* db, int acc, void* ws, size_t ws_bytes,
-                   hipStream_t st);
+                   hipStream_t st, const float* vpre = nullptr);
 // head.conv2's G part as one per-image 5x5 conv of the image (gfuse.hip)
 size_t pf_gfuse_weights_floats(int n);
 int pf_gfuse_weights(const float* w2_packed, const float* b2, const float* w1_packed,

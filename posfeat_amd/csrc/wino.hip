@@ -1040,13 +1040,14 @@ int pf_wino6_weights(const float* wpk, int Cout, int Cin, float* U, hipStream_t 
 // (h/2, w/2) map, h and w even.
 int pf_wino6_conv(const float* x, int xcs, int n, int h, int w, int Cin, const float* U,
                   const float* bias, int Cout, int act, float* y, int ycs, void* ws,
-                  size_t ws_bytes, hipStream_t st, int stages, int planes, int up2) {
+                  size_t ws_bytes, hipStream_t st, int stages, int planes, int up2,
+                  float* vkeep) {
   if (Cin % 32 || Cout % 4 || xcs % 2 || ycs % 2 || n <= 0 || h <= 0 || w <= 0 || planes > 1)
     return POSFEAT_E_INVALID;
   if (up2 && ((h & 1) || (w & 1))) return POSFEAT_E_INVALID;
   if (ws_bytes < pf_wino6_ws_bytes(n, h, w, Cin, Cout)) return POSFEAT_E_WORKSPACE;
   const long long T = (long long)n * ((h + 5) / 6) * ((w + 5) / 6);
-  float* V = static_cast<float*>(ws);
+  float* V = vkeep ? vkeep : static_cast<float*>(ws);
   float* M = reinterpret_cast<float*>(static_cast<char*>(ws) + pf_align(64 * T * Cin * 4, 256));
   if (stages & 1) {
     // fused upsample: one channel per thread (occupancy); plain: channel pairs
@@ -1274,7 +1275,7 @@ size_t pf_wino6_wgrad_ws_bytes(int n, int h, int w, int Cin, int Cout) {
 // Cout % 128 == 0), arguments as pf_wino_wgrad's
 int pf_wino6_wgrad(const float* dy, int ldy, const float* x, int xcs, int n, int h, int w, int Cin,
                    int Cout, float* dw, float* db, int acc, void* ws, size_t ws_bytes,
-                   hipStream_t st) {
+                   hipStream_t st, const float* vpre) {
   if (Cin % 128 || Cout % 128 || ldy % 2 || xcs % 2 || n <= 0 || h <= 0 || w <= 0)
     return POSFEAT_E_INVALID;
   if (ws_bytes < pf_wino6_wgrad_ws_bytes(n, h, w, Cin, Cout)) return POSFEAT_E_WORKSPACE;
@@ -1288,8 +1289,11 @@ int pf_wino6_wgrad(const float* dy, int ldy, const float* x, int xcs, int n, int
   float* part = reinterpret_cast<float*>(p);
   p += pf_align((size_t)64 * ns * Cout * Cin * 4, 256);
   float* partb = reinterpret_cast<float*>(p);
-  hipLaunchKernelGGL((wino6_input_kernel<false, 2>), dim3(grid_for(T * (Cin / 2), 256)), dim3(256),
-                     0, st, x, xcs, n, h, w, Cin / 2, V);
+  if (vpre)  // the forward's V of the same x (pf_wino6_conv's vkeep)
+    V = const_cast<float*>(vpre);
+  else
+    hipLaunchKernelGGL((wino6_input_kernel<false, 2>), dim3(grid_for(T * (Cin / 2), 256)),
+                       dim3(256), 0, st, x, xcs, n, h, w, Cin / 2, V);
   hipLaunchKernelGGL(wino6_dy_kernel, dim3(grid_for(T * (Cout / 2), 256)), dim3(256), 0, st, dy,
                      ldy, n, h, w, Cout / 2, dM);
   PF_CHECK_LAUNCH();
