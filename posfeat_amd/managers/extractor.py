@@ -400,11 +400,20 @@ class Extractor:
     def _upload(self, st):
         """async H2D of a filled pinned staging view [g][h][w][3] uint8 and the
         on-device ImageNet normalisation (bit-identical to the host transform);
-        returns (normalised [g][3][h][w] float, event after the copy)"""
-        u8 = torch.empty(tuple(st.shape), dtype=torch.uint8, device=self.device)
-        u8.copy_(st, non_blocking=True)
-        ev_copy = torch.cuda.Event()
-        ev_copy.record()
+        returns (normalised [g][3][h][w] float, event after the copy).  The
+        copy runs on its own stream: queued behind the compute stream's earlier
+        groups, it held the staging buffer (and so the reader) until the device
+        reached it; the compute stream waits on the copy's event instead."""
+        cur = torch.cuda.current_stream(self.device)
+        if getattr(self, "_h2d_stream", None) is None:
+            self._h2d_stream = torch.cuda.Stream(self.device)
+        with torch.cuda.stream(self._h2d_stream):   # u8 from the copy stream's pool
+            u8 = torch.empty(tuple(st.shape), dtype=torch.uint8, device=self.device)
+            u8.copy_(st, non_blocking=True)
+            ev_copy = torch.cuda.Event()
+            ev_copy.record(self._h2d_stream)
+        cur.wait_event(ev_copy)
+        u8.record_stream(cur)   # not reused by a later copy before the compute stream read it
         return ops.normalize_rgb8(u8), ev_copy
 
     def _launch_device(self, im, names, scales, t0):

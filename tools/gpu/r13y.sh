@@ -1,0 +1,17 @@
+# round 5: H2D of the staged batches on a copy stream: extract tests, e2e streams
+set -o pipefail
+mkdir -p gpurun_out/r13y
+export PYTHONUNBUFFERED=1
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_gpu_extract.py > gpurun_out/r13y/tests.txt 2>&1 || { tail -30 gpurun_out/r13y/tests.txt; exit 1; }
+tail -2 gpurun_out/r13y/tests.txt
+run() {  # tag sizes env...
+  local tag=$1 sz=$2; shift 2
+  env "$@" timeout -k 10 300 python -u tools/extract_e2e.py --sizes $sz --seqs 96 > gpurun_out/r13y/e2e_$tag.txt 2>&1 || { tail -20 gpurun_out/r13y/e2e_$tag.txt; return 1; }
+  tail -1 gpurun_out/r13y/e2e_$tag.txt | python -c "import json,sys; d=json.loads(sys.stdin.read()); c=d['cold']; print('$tag', round(c['images_per_s'],1), round(c.get('steady_images_per_s',0),1), 'replay', round(c['kernel_path_replay_images_per_s'],1), c['host'])"
+}
+run hp hpatches || exit 1
+run hp_inf2 hpatches POSFEAT_EXTRACT_INFLIGHT=2 || exit 1
+run mixed mixed || exit 1
+run mixed_inf2 mixed POSFEAT_EXTRACT_INFLIGHT=2 || exit 1
+run 480 480x640 || exit 1
+run 480_inf2 480x640 POSFEAT_EXTRACT_INFLIGHT=2 || exit 1
