@@ -114,6 +114,11 @@ struct posfeat_wstore {
   bool wpl_done = false;
   std::set<std::string> wino_done;  // "<layer>/4" (F(4x4)) or "<layer>/2"
   hipEvent_t ev = nullptr;          // recorded after the last build
+  // the side stream + fork / join events of image_branch, shared by the
+  // instances: one per new shape cost a stream creation, and LRU eviction a
+  // hipStreamDestroy (which waits for the stream) in the middle of a stream
+  hipStream_t side_st = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   int refs = 0;
 };
 
@@ -989,7 +994,11 @@ int image_branch(Ctx& c, const float* img4) {
   Ctx s = c;
   s.side = true;
   if (!c.dry) {
-    if (!m->side_st) {
+    // the engine's shared store holds them when there is one (posfeat_wstore)
+    hipStream_t& side_st = m->store ? m->store->side_st : m->side_st;
+    hipEvent_t& ev_fork = m->store ? m->store->ev_fork : m->ev_fork;
+    hipEvent_t& ev_join = m->store ? m->store->ev_join : m->ev_join;
+    if (!side_st) {
       // commit the stream and both events together (a partial set would make
       // every later extract fail on a null event)
       hipStream_t st = nullptr;
@@ -1002,10 +1011,13 @@ int image_branch(Ctx& c, const float* img4) {
         if (st) (void)hipStreamDestroy(st);
         return POSFEAT_E_HIP;
       }
-      m->side_st = st;
-      m->ev_fork = ef;
-      m->ev_join = ej;
+      side_st = st;
+      ev_fork = ef;
+      ev_join = ej;
     }
+    m->side_st = side_st;  // this run's handles (owned by the store when shared)
+    m->ev_fork = ev_fork;
+    m->ev_join = ev_join;
     if (hipEventRecord(m->ev_fork, c.st) != hipSuccess ||
         hipStreamWaitEvent(m->side_st, m->ev_fork, 0) != hipSuccess)
       return POSFEAT_E_HIP;
@@ -1526,6 +1538,9 @@ extern "C" long long posfeat_model_weight_floats(void) { return specs().total; }
 
 static void wstore_release(posfeat_wstore* s) {
   if (!s || --s->refs > 0) return;
+  if (s->ev_fork) (void)hipEventDestroy(s->ev_fork);
+  if (s->ev_join) (void)hipEventDestroy(s->ev_join);
+  if (s->side_st) (void)hipStreamDestroy(s->side_st);
   if (s->ev) (void)hipEventDestroy(s->ev);
   if (s->base) (void)hipFree(s->base);
   delete s;
@@ -1717,9 +1732,11 @@ extern "C" void posfeat_model_destroy(posfeat_model* m) {
     (void)hipEventDestroy(e.a);
     (void)hipEventDestroy(e.b);
   }
-  if (m->ev_fork) (void)hipEventDestroy(m->ev_fork);
-  if (m->ev_join) (void)hipEventDestroy(m->ev_join);
-  if (m->side_st) (void)hipStreamDestroy(m->side_st);
+  if (!m->store) {  // else the store's (released with its last instance)
+    if (m->ev_fork) (void)hipEventDestroy(m->ev_fork);
+    if (m->ev_join) (void)hipEventDestroy(m->ev_join);
+    if (m->side_st) (void)hipStreamDestroy(m->side_st);
+  }
   wstore_release(m->store);
   delete m;
 }
