@@ -1170,37 +1170,70 @@ __global__ void l2norm_bwd_kernel(const float* __restrict__ x, int cs,
   if (pix >= npix) return;
   const int b = (int)(pix / ((long long)h * w));
   const int rem = (int)(pix - (long long)b * h * w), py = rem / w, px = rem - py * w;
+  // the pixel's own loads first, all independent of the cell search below
+  const float x0 = x[pix * cs + lane], x1 = x[pix * cs + lane + 64];
+  const float gl0 = dfm ? dfm[pix * 128 + lane]
+                        : (float)((double)(long long)afm[pix * 128 + lane] / FX_SCALE);
+  const float gl1 = dfm ? dfm[pix * 128 + lane + 64]
+                        : (float)((double)(long long)afm[pix * 128 + lane + 64] / FX_SCALE);
   float q0 = 0.f, q1 = 0.f;
   {
     // cells (grid image pixels wide) holding image pixels 4 (p - 2) .. 4 (p + 3):
-    // every sample whose bilinear corners can include map pixel p
+    // every sample whose bilinear corners can include map pixel p -- at most
+    // 3 x 3 for grid >= 10 (the caller's grid 16); their sample coordinates
+    // are loaded together (clamped cell, masked), then visited in the same
+    // row-major order (the same sums as one dependent load per cell)
     const int cx0 = max(4 * (px - 2), 0) / grid, cx1 = min((4 * (px + 3) - 1) / grid, ncx - 1);
     const int cy0 = max(4 * (py - 2), 0) / grid, cy1 = min((4 * (py + 3) - 1) / grid, ncy - 1);
     const int n = ncx * ncy;
-    for (int cy = cy0; cy <= cy1; ++cy)
-      for (int cxx = cx0; cxx <= cx1; ++cxx) {
+    if (cx1 - cx0 < 3 && cy1 - cy0 < 3) {
+      float cxv[9], cyv[9];
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        const int cy = min(cy0 + k / 3, cy1), cxx = min(cx0 + k % 3, cx1);
         const long long i = (long long)b * n + cy * ncx + cxx;
-        const float fx = ((cn[i * 2] + 1.f) * w - 1.f) / 2.f;
-        const float fy = ((cn[i * 2 + 1] + 1.f) * h - 1.f) / 2.f;
+        cxv[k] = cn[i * 2];
+        cyv[k] = cn[i * 2 + 1];
+      }
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        const int cy = cy0 + k / 3, cxx = cx0 + k % 3;
+        if (cy > cy1 || cxx > cx1) continue;
+        const long long i = (long long)b * n + cy * ncx + cxx;
+        const float fx = ((cxv[k] + 1.f) * w - 1.f) / 2.f;
+        const float fy = ((cyv[k] + 1.f) * h - 1.f) / 2.f;
         const float flx = floorf(fx), fly = floorf(fy);
-        const int x0 = (int)flx, y0 = (int)fly;
-        if (px != x0 && px != x0 + 1) continue;  // (uniform across the wave)
-        if (py != y0 && py != y0 + 1) continue;
-        const float wx = px == x0 ? (float)(x0 + 1) - fx : fx - (float)x0;
-        const float wy = py == y0 ? (float)(y0 + 1) - fy : fy - (float)y0;
+        const int ix0 = (int)flx, iy0 = (int)fly;
+        if (px != ix0 && px != ix0 + 1) continue;  // (uniform across the wave)
+        if (py != iy0 && py != iy0 + 1) continue;
+        const float wx = px == ix0 ? (float)(ix0 + 1) - fx : fx - (float)ix0;
+        const float wy = py == iy0 ? (float)(iy0 + 1) - fy : fy - (float)iy0;
         const float wt = wx * wy;
         q0 += wt * gq[i * 128 + lane];
         q1 += wt * gq[i * 128 + lane + 64];
       }
+    } else {
+      for (int cy = cy0; cy <= cy1; ++cy)
+        for (int cxx = cx0; cxx <= cx1; ++cxx) {
+          const long long i = (long long)b * n + cy * ncx + cxx;
+          const float fx = ((cn[i * 2] + 1.f) * w - 1.f) / 2.f;
+          const float fy = ((cn[i * 2 + 1] + 1.f) * h - 1.f) / 2.f;
+          const float flx = floorf(fx), fly = floorf(fy);
+          const int ix0 = (int)flx, iy0 = (int)fly;
+          if (px != ix0 && px != ix0 + 1) continue;
+          if (py != iy0 && py != iy0 + 1) continue;
+          const float wx = px == ix0 ? (float)(ix0 + 1) - fx : fx - (float)ix0;
+          const float wy = py == iy0 ? (float)(iy0 + 1) - fy : fy - (float)iy0;
+          const float wt = wx * wy;
+          q0 += wt * gq[i * 128 + lane];
+          q1 += wt * gq[i * 128 + lane + 64];
+        }
+    }
   }
-  const float x0 = x[pix * cs + lane], x1 = x[pix * cs + lane + 64];
   const float nrm = sqrtf(pf_wave_sum(x0 * x0 + x1 * x1));
   const float inv = 1.f / fmaxf(nrm, 1e-12f);
   const float y0 = x0 * inv, y1 = x1 * inv;
-  const float g0 = T * (dfm ? dfm[pix * 128 + lane]
-                            : (float)((double)(long long)afm[pix * 128 + lane] / FX_SCALE));
-  const float g1 = T * (dfm ? dfm[pix * 128 + lane + 64]
-                            : (float)((double)(long long)afm[pix * 128 + lane + 64] / FX_SCALE));
+  const float g0 = T * gl0, g1 = T * gl1;
   const float yg = pf_wave_sum(y0 * g0 + y1 * g1);
   float r0 = nrm > 1e-12f ? (g0 - y0 * yg) * inv : g0 * inv;
   float r1 = nrm > 1e-12f ? (g1 - y1 * yg) * inv : g1 * inv;
