@@ -110,10 +110,13 @@ class _StagedReader:
     ahead of the one the device takes next.  ahead + 1 buffers in a ring: a
     buffer is refilled once the H2D copy that read it has finished."""
 
-    def __init__(self, ds, groups, threads, ahead):
+    def __init__(self, ds, groups, threads, ahead, bufs=None):
         self.ds, self.groups, self.ahead = ds, groups, ahead
         self.pool = ThreadPoolExecutor(threads)
-        self.ring = [[None, None] for _ in range(ahead + 1)]   # [buffer, H2D event]
+        # [buffer, H2D event]; ``bufs``: staging buffers allocated beforehand
+        # (Extractor._prewarm_host: sized for the plan's largest batch)
+        bufs = list(bufs or [])[:ahead + 1]
+        self.ring = [[bufs[k] if k < len(bufs) else None, None] for k in range(ahead + 1)]
         self.work = {}
         self.next = 0
 
@@ -224,10 +227,12 @@ class Extractor:
             # one workspace allocation for the whole stream (its batch shapes
             # from the file headers), while the workers decode the first
             # images -- not one allocation per larger size met on the way
-            group = max(1, int(os.environ.get("POSFEAT_EXTRACT_GROUP", "32")))
+            group, _ = self._group_hold()
             shapes = self._stream_shapes(group)
             if shapes:
                 self.model.engine().reserve(shapes)
+                if self._staged:
+                    self._prewarm_host(group)
             elif self._staged:   # sizes unknown: the loader path after all
                 self._staged = False
                 self._early_iter = iter(self._pipelined_loader())
@@ -431,10 +436,10 @@ class Extractor:
             torch.cuda.synchronize(dev)
         t3 = time.perf_counter()
         nhwc = out["_local_map_nhwc"]
-        host = []
         norm = self.config["loss_distance"] == "cos"
         # one detect + one sample launch per run of images sharing a detector
         # config (Aachen query / db), each image selected as if alone
+        runs = []
         i = 0
         while i < g:
             cfg = self._det_cfg(names[i])
@@ -445,13 +450,28 @@ class Extractor:
                 out["local_point"][i:j], **cfg)
             desc = ops.sample_desc_nhwc(nhwc[i:j], coord_n, c=128, normalize=norm,
                                         n_valid=n_sel, each=True)
-            hs = (n_sel.to("cpu", non_blocking=True), coord_n.to("cpu", non_blocking=True),
-                  desc.to("cpu", non_blocking=True), score.to("cpu", non_blocking=True))
-            for k in range(i, j):
-                host.append((names[k], scales[k], hs, k - i, w, h))
+            runs.append((i, j, (n_sel, coord_n, desc, score)))
             i = j
-        ev = torch.cuda.Event()
-        ev.record()
+        # the results' D2H on a copy stream: the copy (a blit kernel for a
+        # device-to-pinned-host copy, 0.46 ms for a 6-image group's 25 MB of
+        # descriptors, r14d) overlaps the next group's kernels instead of
+        # running between them on the compute stream
+        cur = torch.cuda.current_stream(dev)
+        if getattr(self, "_d2h_stream", None) is None:
+            self._d2h_stream = torch.cuda.Stream(dev)
+        ev_done = torch.cuda.Event()
+        ev_done.record(cur)
+        self._d2h_stream.wait_event(ev_done)
+        host = []
+        with torch.cuda.stream(self._d2h_stream):
+            for i, j, ts in runs:
+                for t in ts:   # not reused by the compute stream before the copy read it
+                    t.record_stream(self._d2h_stream)
+                hs = tuple(t.to("cpu", non_blocking=True) for t in ts)
+                for k in range(i, j):
+                    host.append((names[k], scales[k], hs, k - i, w, h))
+            ev = torch.cuda.Event()
+            ev.record(self._d2h_stream)
         self._acct_add("detect_s", t3)
         if trace:
             torch.cuda.synchronize(dev)
@@ -550,11 +570,47 @@ class Extractor:
         Aachen/ETH keep full resolution) would otherwise hold most of the
         stream in partial buckets: once ``POSFEAT_EXTRACT_HOLD`` images
         (default 4 groups) wait, the fullest bucket launches early."""
-        group = max(1, int(os.environ.get("POSFEAT_EXTRACT_GROUP", "32")))
-        hold = max(group, int(os.environ.get("POSFEAT_EXTRACT_HOLD", str(4 * group))))
+        group, hold = self._group_hold()
         if self._staged:
             return self._extract_staged_run(group, hold)
         return self._extract_pipelined_run(group, hold)
+
+    def _group_hold(self):
+        group = max(1, int(os.environ.get("POSFEAT_EXTRACT_GROUP", "32")))
+        hold = max(group, int(os.environ.get("POSFEAT_EXTRACT_HOLD", str(4 * group))))
+        return group, hold
+
+    def _prewarm_host(self, group):
+        """Pinned host memory for the staged run, allocated at construction
+        (with the engine's workspace reserve) instead of on the way: the
+        reader's ring at the plan's largest batch, and the caching host
+        allocator's blocks for each batch's result copies (two per batch
+        shape, freed here and reused by the run's D2H).  A pinned allocation
+        is a ~8 ms hipHostMalloc of tens of MB that the launching thread waits
+        for: in the HPatches-size stream nine of them sat in the first groups,
+        the device idle meanwhile (r14d)."""
+        _, hold = self._group_hold()
+        groups, _ = self._plan_groups(self._order, self._sizes, group, hold)
+        if not groups:
+            return
+        ahead = max(1, int(os.environ.get("POSFEAT_EXTRACT_AHEAD", "2")))
+        nmax = max(len(idxs) * h * w * 3 for (h, w), idxs in groups)
+        self._ring_bufs = [_staging_buffer(nmax) for _ in range(ahead + 1)]
+        cfg = self.config["detector_config"]
+        npts = cfg.get("num_pts", False)
+        shapes = set()
+        for (h, w), idxs in groups:
+            P = (h - 2) * (w - 2)
+            cap = min(max(int(npts), 128), P) if npts else P
+            shapes.add((len(idxs), cap))
+        warm = []
+        for g, cap in sorted(shapes)[-4:]:   # the largest few (bounded pinned memory)
+            for _ in range(2):
+                warm += [torch.empty(g, dtype=torch.int32, pin_memory=True),
+                         torch.empty(g, cap, 2, pin_memory=True),
+                         torch.empty(g, cap, 128, pin_memory=True),
+                         torch.empty(g, cap, 1, pin_memory=True)]
+        del warm   # back to the caching host allocator, same size classes as the D2H
 
     def _extract_staged_run(self, group, hold):
         """The pipelined loop fed by the staged reader: the batches are planned
@@ -570,7 +626,8 @@ class Extractor:
         groups, max_held = self._plan_groups(self._order, self._sizes, group, hold)
         threads = max(1, int(os.environ.get("POSFEAT_EXTRACT_READERS", "8")))
         ahead = max(1, int(os.environ.get("POSFEAT_EXTRACT_AHEAD", "2")))
-        reader = _StagedReader(ds, groups, threads, ahead)
+        reader = _StagedReader(ds, groups, threads, ahead, getattr(self, "_ring_bufs", None))
+        self._ring_bufs = None   # released by the reader's close
         writer = ThreadPoolExecutor(1 if self.save_h5 else getattr(self, "_nwriters", 4))
         futures, pending = [], deque()
         self.group_shapes = []
