@@ -166,6 +166,9 @@ struct posfeat_bbtrain {
   bool wino = true;
   bool wino6 = true;  // F(6x6) forward + input gradient (POSFEAT_TRAIN_WINO6=0, A/B: F(4x4))
   bool wino6_wg = true;  // F(6x6) weight gradient (POSFEAT_TRAIN_WINO6_WGRAD=0, A/B: F(4x4))
+  // BatchNorm forward statistics from the conv epilogue (fp64 per-tile sums of
+  // y; POSFEAT_TRAIN_BN_EPI=0, A/B: the separate bn_partial_kernel<0> pass)
+  bool bn_epi = true;
   bool bf6p = false;     // conv precision mode 2 at create (pre-split Winograd operands)
   bool s2phase = true;  // stride-2 input gradients by output phases (POSFEAT_S2PHASE=0: zero insertion)
   Buf wu, wino_ws;
@@ -345,6 +348,8 @@ void plan(posfeat_bbtrain* m) {
     m->wino6 = !(w6 && w6[0] == '0') && !m->bf6p;
     const char* g = pf_ab_getenv("POSFEAT_TRAIN_WINO6_WGRAD");
     m->wino6_wg = !(g && g[0] == '0');
+    const char* be = pf_ab_getenv("POSFEAT_TRAIN_BN_EPI");
+    m->bn_epi = !(be && be[0] == '0');
   }
   // ---- activations
   alloc(m->img4, fl(B * H * W * 4));
@@ -521,30 +526,41 @@ int layer_fwd(Ctx& c, int li, const float* x, int xcs, int h, int w, float* out,
                           L.cout, c.s(m->wino_ws), m->wino_ws.bytes, c.st, 7,
                           m->bf6p ? 2 : m->wsplit ? 1 : 0);
     }));
-  } else {
+  }
+  // BN statistics: the conv epilogue's per-tile fp64 sums when the direct
+  // conv produced them (nparts > 0), else the statistics pass over y
+  int nparts = 0;
+  if (!use_wino(m, li, h, w)) {
     PF_TRY(timed(c, std::string("fwd:conv:") + L.name, 2.0 * P * L.cout * L.cin * L.k * L.k, [&] {
-      return pf_conv_run_tile(&d, x, c.prm + L.w_off, L.bias ? c.prm + L.b_off : nullptr, nullptr,
-                              y, c.s(m->splitk), m->splitk.bytes, -1, c.st,
-                              m->wsplit ? c.su(m->wpl) + L.w_off : nullptr, tab().params);
+      const unsigned short* wb = m->wsplit ? c.su(m->wpl) + L.w_off : nullptr;
+      const float* bias = L.bias ? c.prm + L.b_off : nullptr;
+      if (m->bn_epi)
+        return pf_conv_run_tile_bn(&d, x, c.prm + L.w_off, bias, y, c.s(m->splitk),
+                                   m->splitk.bytes, -1, c.st, wb, tab().params, c.sd(m->part),
+                                   m->part.bytes, &nparts);
+      return pf_conv_run_tile(&d, x, c.prm + L.w_off, bias, nullptr, y, c.s(m->splitk),
+                              m->splitk.bytes, -1, c.st, wb, tab().params);
     }));
   }
   float* mean = c.f(m->st[li]);
   float* rstd = mean + L.cout;
   const BnGrid g = bn_grid(P, L.cout);
+  const int nchunk = nparts > 0 ? nparts : g.nchunk;
   const int c4n = L.cout / 4;
   const int world = pf_group_world(m->group);
   return timed(c, "fwd:bn", 0, [&] {
-    hipLaunchKernelGGL(bn_partial_kernel<0>, dim3(g.nchunk, g.gy), dim3(256), 0, c.st, y, P,
-                       L.cout, g.chunk, nullptr, 0, nullptr, 0, 0, nullptr, nullptr, nullptr,
-                       nullptr, c.sd(m->part));
+    if (nparts == 0)
+      hipLaunchKernelGGL(bn_partial_kernel<0>, dim3(g.nchunk, g.gy), dim3(256), 0, c.st, y, P,
+                         L.cout, g.chunk, nullptr, 0, nullptr, 0, 0, nullptr, nullptr, nullptr,
+                         nullptr, c.sd(m->part));
     if (world == 1) {
       hipLaunchKernelGGL(bn_stats_final_kernel, dim3((L.cout + 3) / 4), dim3(256), 0, c.st,
-                         c.sd(m->part), g.nchunk, L.cout, P, mom, mean, rstd,
+                         c.sd(m->part), nchunk, L.cout, P, mom, mean, rstd,
                          stats ? stats + L.rm_off : nullptr, stats ? stats + L.rv_off : nullptr);
     } else {  // SyncBatchNorm: sums and pixel counts over the group
       double* sums = c.sd(m->bnsum);
       hipLaunchKernelGGL(bn_sums_kernel, dim3((L.cout + 3) / 4), dim3(256), 0, c.st,
-                         c.sd(m->part), g.nchunk, L.cout, (double)P, sums, nullptr);
+                         c.sd(m->part), nchunk, L.cout, (double)P, sums, nullptr);
       PF_CHECK_LAUNCH();
       PF_TRY(pf_group_allreduce(m->group, sums, 2 * L.cout + 1, c.st));
       hipLaunchKernelGGL(bn_stats_from_sums_kernel, dim3((L.cout + 255) / 256), dim3(256), 0,

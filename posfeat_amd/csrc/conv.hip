@@ -63,6 +63,8 @@ struct ConvArgs {
   int ksplit;        // > 1: grid = nwg * ksplit, raw partials to `part`
   float* part;       // [ksplit][M][Cout] fp32 partial sums
   float* stats;      // optional [tiles_m][2 slots][Cout][2] per-tile (sum, sumsq)
+  double* bnpart;    // optional [tiles_m][2][Cout] per-tile fp64 (sum, sum of squares) of y
+                     // over every image: train-mode BatchNorm statistics (pf_conv_run_tile_bn)
   int hw;            // OH*OW (image boundary inside a tile for `stats`)
   // conv_up4_kernel only: the low-res grid
   int lh, lw;
@@ -120,6 +122,7 @@ __device__ __forceinline__ void conv_epilogue_t(const ConvArgs& a, float* smem, 
                        ? *reinterpret_cast<const f32x4*>(a.bias + col)
                        : f32x4{0.f, 0.f, 0.f, 0.f};
   f32x4 s1[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}}, s2[2] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+  double b1[4] = {0, 0, 0, 0}, b2[4] = {0, 0, 0, 0};  // a.bnpart: this thread's rows, in order
 #pragma unroll
   for (int s = 0; s < SL; ++s) {
     if (s > 0) __syncthreads();  // the previous slice's rows are read
@@ -163,6 +166,13 @@ __device__ __forceinline__ void conv_epilogue_t(const ConvArgs& a, float* smem, 
         v.w = pf_elu(v.w);
       }
       *reinterpret_cast<f32x4*>(a.y + (size_t)m * a.ycs + col) = v;
+      if (a.bnpart) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          b1[k] += (double)v[k];
+          b2[k] += (double)v[k] * (double)v[k];
+        }
+      }
       if (a.stats) {
         const int sl = (m / a.hw) != img0;
         if (sl) {
@@ -176,6 +186,25 @@ __device__ __forceinline__ void conv_epilogue_t(const ConvArgs& a, float* smem, 
     }
   }
   if (a.ksplit > 1) return;
+  if (a.bnpart) {  // the RPP row groups of each column summed in a fixed order (fp64)
+    __syncthreads();
+    double* R = reinterpret_cast<double*>(smem);  // [RPP][2][BN]: the IN path's 64 B / thread
+    if (active) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        R[(r0 * 2 + 0) * BN + 4 * q + k] = b1[k];
+        R[(r0 * 2 + 1) * BN + 4 * q + k] = b2[k];
+      }
+    }
+    __syncthreads();
+    for (int e = tid; e < 2 * BN; e += THREADS) {
+      const int which = e / BN, c = e - which * BN;
+      if (n0 + c >= a.Cout) continue;
+      double t = 0.0;
+      for (int rr = 0; rr < RPP; ++rr) t += R[(rr * 2 + which) * BN + c];
+      a.bnpart[((size_t)tm * 2 + which) * a.Cout + n0 + c] = t;
+    }
+  }
   if (a.stats) {  // reduce the RPP row groups of each column in a fixed order
     __syncthreads();
     float* R = smem;  // [RPP][2 slots][BN][2]
@@ -2849,6 +2878,7 @@ static int conv_prepare(const posfeat_conv_desc* d, const float* x, const float*
   a.ksplit = 1;
   a.part = nullptr;
   a.stats = nullptr;
+  a.bnpart = nullptr;
   a.hw = a.OH * a.OW;
   a.nbatch = 1;
   a.bx = a.bw = a.by = 0;
@@ -2960,6 +2990,38 @@ int pf_conv_run_tile(const posfeat_conv_desc* d, const float* x, const float* w,
   const Plan p = conv_plan(a, split, tile);
   if (p.ksplit > 1) a.part = static_cast<float*>(ws);
   return conv_run(a, p, st);
+}
+
+// pf_conv_run_tile with the train-mode BatchNorm partial sums of y from the
+// epilogue (bbtrain.hip layer_fwd): part[tile][2][Cout] fp64 (sum, sum of
+// squares over the tile's pixels of every image; the layout of
+// bn_partial_kernel<0>'s chunks, which bn_stats_final_kernel / bn_sums_kernel
+// reduce), *nparts = the tile count.  A split-K plan (raw partials: the reduce
+// writes y) or a part buffer too small for the plan's tiles runs the plain
+// conv with *nparts = 0: the caller then takes the statistics pass.
+int pf_conv_run_tile_bn(const posfeat_conv_desc* d, const float* x, const float* w,
+                        const float* bias, float* y, void* ws, size_t ws_bytes, int tile,
+                        hipStream_t st, const unsigned short* wb, long long wplane, double* part,
+                        size_t part_bytes, int* nparts) {
+  ConvArgs a;
+  PF_TRY(conv_prepare(d, x, w, bias, nullptr, y, a));
+  if (!nparts) return POSFEAT_E_INVALID;
+  *nparts = 0;
+  a.wb = wb;
+  a.wplane = wplane;
+  const size_t need = posfeat_conv2d_workspace(d);
+  const bool split = need > 0 && ws && ws_bytes >= need;
+  const Plan p = conv_plan(a, split, tile);
+  if (p.ksplit > 1) {
+    a.part = static_cast<float*>(ws);
+  } else if (part && p.tiles_m * 2 * (size_t)a.Cout * sizeof(double) <= part_bytes &&
+             p.tiles_m <= 0x7fffffff) {
+    a.bnpart = part;
+    *nparts = (int)p.tiles_m;
+  }
+  const int rc = conv_run(a, p, st);
+  if (rc != POSFEAT_OK) *nparts = 0;
+  return rc;
 }
 
 static size_t stats_ws_for(const ConvArgs& a, const Plan& p, int n) {

@@ -41,6 +41,12 @@ int pf_conv_run_tile(const posfeat_conv_desc* d, const float* x, const float* w,
                      const float* bias, const float* res, float* y, void* ws, size_t ws_bytes,
                      int tile, hipStream_t st, const unsigned short* wb = nullptr,
                      long long wplane = 0);
+// the same with the train-mode BatchNorm partial sums from the epilogue
+// (conv.hip; *nparts = 0: not produced, run the statistics pass)
+int pf_conv_run_tile_bn(const posfeat_conv_desc* d, const float* x, const float* w,
+                        const float* bias, float* y, void* ws, size_t ws_bytes, int tile,
+                        hipStream_t st, const unsigned short* wb, long long wplane, double* part,
+                        size_t part_bytes, int* nparts);
 size_t pf_conv_stats_ws_max(const posfeat_conv_desc* d);
 int pf_conv_stats_run_tile(const posfeat_conv_desc* d, const float* x, const float* w,
                            const float* bias, float* y, void* ws, size_t ws_bytes, float* mean,
