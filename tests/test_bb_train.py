@@ -300,3 +300,31 @@ def test_gpu_desc_train_step_vs_oracle(gpu):
     for name, cin, cout, k, s, hb, offs in layers:
         w = moved[offs[0]:offs[0] + cout]
         assert bool(w.any()) == (name != "conv_coarse"), name
+
+
+_BN_EPI_CHILD = r"""
+import numpy as np, torch
+import test_bb_train as t
+_, tr, lm1, lm2 = t._gpu_grads(torch.device("cuda", 0))
+np.savez(%(out)r, grad=tr.grad.cpu().numpy(), stats=tr.stats.cpu().numpy(), lm1=lm1, lm2=lm2)
+"""
+
+
+@pytest.mark.gpu
+def test_gpu_bn_epilogue_stats_match_pass(gpu, tmp_path):
+    """The forward BatchNorm statistics from the direct convs' epilogue (the
+    default) against the separate statistics pass (POSFEAT_TRAIN_BN_EPI=0, A/B
+    build, child process), the same forward + two backward calls: both sum y
+    and y^2 in fp64 (per tile vs per pixel chunk), so the maps, running
+    statistics and gradients agree to the rounding of those sums."""
+    from conftest import run_ab_child
+    out = str(tmp_path / "pass.npz")
+    ref = run_ab_child("import os; os.environ['POSFEAT_TRAIN_BN_EPI'] = '0'\n" +
+                       _BN_EPI_CHILD % {"out": out}, out)
+    _, tr, lm1, lm2 = _gpu_grads(gpu)
+    for got, want, name in ((lm1, ref["lm1"], "lm1"), (lm2, ref["lm2"], "lm2")):
+        np.testing.assert_allclose(got, want, atol=1e-5 * np.abs(want).max(), err_msg=name)
+    st = tr.stats.cpu().numpy()
+    np.testing.assert_allclose(st, ref["stats"], rtol=1e-5, atol=1e-6 * np.abs(ref["stats"]).max())
+    g = tr.grad.cpu().numpy()
+    assert np.abs(g - ref["grad"]).max() <= 1e-4 * np.abs(ref["grad"]).max()
