@@ -169,6 +169,9 @@ struct posfeat_bbtrain {
   // BatchNorm forward statistics from the conv epilogue (fp64 per-tile sums of
   // y; POSFEAT_TRAIN_BN_EPI=0, A/B: the separate bn_partial_kernel<0> pass)
   bool bn_epi = true;
+  // the direct convs on the engine's autotuned tiles (process-wide cache, timed
+  // on first sight; POSFEAT_TRAIN_TUNE=0, A/B: the default plan)
+  bool tune = true;
   bool bf6p = false;     // conv precision mode 2 at create (pre-split Winograd operands)
   bool s2phase = true;  // stride-2 input gradients by output phases (POSFEAT_S2PHASE=0: zero insertion)
   Buf wu, wino_ws;
@@ -350,6 +353,8 @@ void plan(posfeat_bbtrain* m) {
     m->wino6_wg = !(g && g[0] == '0');
     const char* be = pf_ab_getenv("POSFEAT_TRAIN_BN_EPI");
     m->bn_epi = !(be && be[0] == '0');
+    const char* tu = pf_ab_getenv("POSFEAT_TRAIN_TUNE");
+    m->tune = !(tu && tu[0] == '0');
   }
   // ---- activations
   alloc(m->img4, fl(B * H * W * 4));
@@ -534,12 +539,15 @@ int layer_fwd(Ctx& c, int li, const float* x, int xcs, int h, int w, float* out,
     PF_TRY(timed(c, std::string("fwd:conv:") + L.name, 2.0 * P * L.cout * L.cin * L.k * L.k, [&] {
       const unsigned short* wb = m->wsplit ? c.su(m->wpl) + L.w_off : nullptr;
       const float* bias = L.bias ? c.prm + L.b_off : nullptr;
-      if (m->bn_epi)
-        return pf_conv_run_tile_bn(&d, x, c.prm + L.w_off, bias, y, c.s(m->splitk),
-                                   m->splitk.bytes, -1, c.st, wb, tab().params, c.sd(m->part),
-                                   m->part.bytes, &nparts);
-      return pf_conv_run_tile(&d, x, c.prm + L.w_off, bias, nullptr, y, c.s(m->splitk),
-                              m->splitk.bytes, -1, c.st, wb, tab().params);
+      auto run = [&](int tile) {
+        if (m->bn_epi)
+          return pf_conv_run_tile_bn(&d, x, c.prm + L.w_off, bias, y, c.s(m->splitk),
+                                     m->splitk.bytes, tile, c.st, wb, tab().params,
+                                     c.sd(m->part), m->part.bytes, &nparts);
+        return pf_conv_run_tile(&d, x, c.prm + L.w_off, bias, nullptr, y, c.s(m->splitk),
+                                m->splitk.bytes, tile, c.st, wb, tab().params);
+      };
+      return m->tune ? pf_conv_tuned_run(&d, false, wb != nullptr, c.st, run) : run(-1);
     }));
   }
   float* mean = c.f(m->st[li]);
@@ -695,8 +703,12 @@ int layer_bwd(Ctx& c, int li, const float* x, int xcs, int h, int w, const float
         return pf_split3_rows(wt, wrows, (int)wcols, (int)wcols, wtp, c.st);
       }));
     PF_TRY(timed(c, std::string("bwd:dgrad:") + L.name, pf, [&] {
-      return pf_conv_run_tile(&d, dy, wt, nullptr, nullptr, dz, c.s(m->splitk), m->splitk.bytes,
-                              -1, c.st, m->wsplit ? wtp : nullptr, wrows * wcols);
+      auto run = [&](int tile) {
+        return pf_conv_run_tile(&d, dy, wt, nullptr, nullptr, dz, c.s(m->splitk),
+                                m->splitk.bytes, tile, c.st, m->wsplit ? wtp : nullptr,
+                                wrows * wcols);
+      };
+      return m->tune ? pf_conv_tuned_run(&d, false, m->wsplit, c.st, run) : run(-1);
     }));
     return timed(c, "bwd:misc", 0, [&] {
       hipLaunchKernelGGL(s2_scatter_kernel, dim3(grid_for((long long)B * h * w * (L.cin / 4), 256)),
@@ -744,8 +756,11 @@ int layer_bwd(Ctx& c, int li, const float* x, int xcs, int h, int w, const float
       return pf_split3_rows(wt, L.cin, (int)wcols, (int)wcols, wtp, c.st);
     }));
   return timed(c, std::string("bwd:dgrad:") + L.name, flops, [&] {
-    return pf_conv_run_tile(&d, src, wt, nullptr, add, dx, c.s(m->splitk), m->splitk.bytes, -1,
-                            c.st, m->wsplit ? wtp : nullptr, (long long)L.cin * wcols);
+    auto run = [&](int tile) {
+      return pf_conv_run_tile(&d, src, wt, nullptr, add, dx, c.s(m->splitk), m->splitk.bytes,
+                              tile, c.st, m->wsplit ? wtp : nullptr, (long long)L.cin * wcols);
+    };
+    return m->tune ? pf_conv_tuned_run(&d, add != nullptr, m->wsplit, c.st, run) : run(-1);
   });
 }
 

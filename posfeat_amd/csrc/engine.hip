@@ -15,6 +15,7 @@
 //                                 low-res map head.conv2 reads per bilinear phase)
 //   g64     [b][h][w][64]      = IN(convimg)
 #include <algorithm>
+#include <functional>
 #include <cstdio>
 #include <cstring>
 #include <cmath>
@@ -1486,6 +1487,23 @@ int head_backward(Ctx& c, const float* dlp, float* grad) {
 }
 
 }  // namespace
+
+// The engine's tile choice (process-wide cache, timed on first sight) for a
+// conv the caller runs itself: the training step's direct convs (bbtrain.hip).
+// `run(tile)` launches the conv with that tile (-1: default plan); results do
+// not depend on the tile.  The calling thread's tile scope is part of the key.
+// A choice taken from a similar conv is stored for this exact descriptor too,
+// so the process repeats it: a later lookup could otherwise meet a closer
+// entry stored meanwhile, and the training step's direct convs are not all
+// bit-identical across tiles (its pre-split tiles differ from the fp32 ones).
+int pf_conv_tuned_run(const posfeat_conv_desc* d, bool res, bool wplanes, hipStream_t st,
+                      const std::function<int(int)>& run) {
+  int tile = -1;
+  if (!tile_lookup(*d, res, wplanes, &tile))
+    tile = tune("train", *d, st, run, wplanes);
+  tile_store(*d, res, wplanes, tile);
+  return run(tile);
+}
 
 extern "C" long long posfeat_model_head_offset(void) { return head_offset(); }
 extern "C" long long posfeat_model_head_floats(void) { return specs().total - head_offset(); }

@@ -1,5 +1,6 @@
 // fmap.h -- internal (non-ABI) launchers shared by the engine.
 #pragma once
+#include <functional>
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 
@@ -47,6 +48,9 @@ int pf_conv_run_tile_bn(const posfeat_conv_desc* d, const float* x, const float*
                         const float* bias, float* y, void* ws, size_t ws_bytes, int tile,
                         hipStream_t st, const unsigned short* wb, long long wplane, double* part,
                         size_t part_bytes, int* nparts);
+// engine.hip: run(tile) with the process-wide autotuned tile of this conv
+int pf_conv_tuned_run(const posfeat_conv_desc* d, bool res, bool wplanes, hipStream_t st,
+                      const std::function<int(int)>& run);
 size_t pf_conv_stats_ws_max(const posfeat_conv_desc* d);
 int pf_conv_stats_run_tile(const posfeat_conv_desc* d, const float* x, const float* w,
                            const float* bias, float* y, void* ws, size_t ws_bytes, float* mean,
