@@ -98,7 +98,10 @@ struct ConvArgs {
 // BN + 4, rows s * BM / SL ..) left to `stage(T, s)` -- the accumulator layout
 // of the MFMA shape the kernel ran (conv_epilogue below: 32x32 blocks;
 // conv_bf6x_kernel: 16x16 blocks).
-template <int BM, int BN, int THREADS, int SL, class RowMap, class ResMap, class Stage>
+// BNS: the BatchNorm partial-sum mode is compiled in (off for the bf6x tiles,
+// which the train-mode step never runs: pf_conv_run_tile_bn falls back there)
+template <int BM, int BN, int THREADS, int SL, bool BNS = true, class RowMap, class ResMap,
+          class Stage>
 __device__ __forceinline__ void conv_epilogue_t(const ConvArgs& a, float* smem, int tm, int n0,
                                                 int split, RowMap rowm, int img0, ResMap resp,
                                                 Stage&& stage) {
@@ -166,7 +169,7 @@ __device__ __forceinline__ void conv_epilogue_t(const ConvArgs& a, float* smem, 
         v.w = pf_elu(v.w);
       }
       *reinterpret_cast<f32x4*>(a.y + (size_t)m * a.ycs + col) = v;
-      if (a.bnpart) {
+      if (BNS && a.bnpart) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           b1[k] += (double)v[k];
@@ -186,7 +189,7 @@ __device__ __forceinline__ void conv_epilogue_t(const ConvArgs& a, float* smem, 
     }
   }
   if (a.ksplit > 1) return;
-  if (a.bnpart) {  // the RPP row groups of each column summed in a fixed order (fp64)
+  if (BNS && a.bnpart) {  // the RPP row groups of each column summed in a fixed order (fp64)
     __syncthreads();
     double* R = reinterpret_cast<double*>(smem);  // [RPP][2][BN]: the IN path's 64 B / thread
     if (active) {
@@ -1636,7 +1639,7 @@ void conv_bf6x_kernel(ConvArgs a) {
   }
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
-  conv_epilogue_t<BM, BN, 256, SL>(
+  conv_epilogue_t<BM, BN, 256, SL, false>(
       a, smem, tm, n0, split, [&](int row) { return m0 + row < a.M ? m0 + row : -1; }, m0 / a.hw,
       [&](int, int m) { return a.res ? a.res + (size_t)m * a.rcs : (const float*)nullptr; },
       [&](float* T, int sl) {
@@ -3015,7 +3018,8 @@ int pf_conv_run_tile_bn(const posfeat_conv_desc* d, const float* x, const float*
   if (p.ksplit > 1) {
     a.part = static_cast<float*>(ws);
   } else if (part && p.tiles_m * 2 * (size_t)a.Cout * sizeof(double) <= part_bytes &&
-             p.tiles_m <= 0x7fffffff) {
+             p.tiles_m <= 0x7fffffff &&
+             !(p.tile >= TILE_BF6X_128x128 && p.tile <= TILE_BF6X_128x192)) {
     a.bnpart = part;
     *nparts = (int)p.tiles_m;
   }
