@@ -754,7 +754,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void d
       // the two line tests as one max of their magnitudes (the SUM passes
       // were VALU-bound, 8.8-13 k VALU per 1.1 k MFMA per wave)
       float gp[2] = {0.f, 0.f};
-      double rp2[2] = {0.0, 0.0};
+      // WR: the stage's 16 reinforce terms summed in fp32 (two interleaved
+      // partials), then added to the fp64 total once per stage (a cvt and an
+      // fp64 add per element made the WR pass the slowest, r14a: 302 vs 252 us)
+      float rp2[2] = {0.f, 0.f};
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         if (!valid(r)) continue;
@@ -767,10 +770,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void d
         const float dB = fmaf(bm0[1], m1[0], fmaf(bm0[2], m1[1], bm0[3]));  // B's line at A's pt
         const float rp = (fmaxf(fabsf(dA), fabsf(dB)) < a.thr ? vgood : vbad) * p;
         gp[r & 1] += rp;
-        if (WR) rp2[r & 1] += (double)(rp * (lp2 * 0.6931471805599453f + (m1[2] + bm1[2])));
+        if (WR) rp2[r & 1] = fmaf(rp, lp2 * 0.6931471805599453f + (m1[2] + bm1[2]), rp2[r & 1]);
       }
       gs += gp[0] + gp[1];
-      if (WR) rs += rp2[0] + rp2[1];
+      if (WR) rs += (double)rp2[0] + (double)rp2[1];
     }
   };
   // prologue: stage 0, then B's column (waited for explicitly: the waitcnt
