@@ -684,11 +684,14 @@ int layer_bwd(Ctx& c, int li, const float* x, int xcs, int h, int w, const float
     const int oh2 = h / 2, ow2 = w / 2;
     float* dz = c.s(m->dz);
     const bool k3 = L.k == 3;
+    // the derived weights and (pre-split tiles) their bf16 planes in one pass
     if (derive) PF_TRY(timed(c, "bwd:misc", 0, [&] {
-      if (!k3) return pf_dgrad_weights(c.prm + L.w_off, C, L.cin, 1, 1, wt, c.st);
+      if (!k3)
+        return pf_dgrad_weights(c.prm + L.w_off, C, L.cin, 1, 1, wt, c.st,
+                                m->wsplit ? wtp : nullptr);
       hipLaunchKernelGGL(s2_phase_weights_kernel,
                          dim3(grid_for(16LL * L.cin * C, 256)), dim3(256), 0, c.st,
-                         c.prm + L.w_off, C, L.cin, wt);
+                         c.prm + L.w_off, C, L.cin, wt, m->wsplit ? wtp : nullptr);
       PF_CHECK_LAUNCH();
       return (int)POSFEAT_OK;
     }));
@@ -698,10 +701,6 @@ int layer_bwd(Ctx& c, int li, const float* x, int xcs, int h, int w, const float
     const double pf = k3 ? 2.0 * B * (oh2 + 1) * (ow2 + 1) * 4 * C * 4 * L.cin
                          : 2.0 * B * oh2 * ow2 * C * L.cin;
     const long long wrows = k3 ? 4LL * L.cin : L.cin, wcols = posfeat_conv_packed_k(C, d.kh, d.kw);
-    if (m->wsplit && derive)
-      PF_TRY(timed(c, "bwd:misc", 0, [&] {
-        return pf_split3_rows(wt, wrows, (int)wcols, (int)wcols, wtp, c.st);
-      }));
     PF_TRY(timed(c, std::string("bwd:dgrad:") + L.name, pf, [&] {
       auto run = [&](int tile) {
         return pf_conv_run_tile(&d, dy, wt, nullptr, nullptr, dz, c.s(m->splitk),
@@ -720,7 +719,11 @@ int layer_bwd(Ctx& c, int li, const float* x, int xcs, int h, int w, const float
   }
   const float* src = dy;
   PF_TRY(timed(c, "bwd:misc", 0, [&] {
-    if (derive) PF_TRY(pf_dgrad_weights(c.prm + L.w_off, C, L.cin, L.k, L.k, wt, c.st));
+    // the direct input gradient's bf16 planes with the derived weights (one pass)
+    const bool direct = add || !use_wino(m, li, h, w);
+    if (derive)
+      PF_TRY(pf_dgrad_weights(c.prm + L.w_off, C, L.cin, L.k, L.k, wt, c.st,
+                              m->wsplit && direct ? wtp : nullptr));
     if (L.stride == 2) {
       if ((h & 1) || (w & 1)) return (int)POSFEAT_E_UNSUPPORTED;
       float* dz = c.s(m->dz);
@@ -751,10 +754,6 @@ int layer_bwd(Ctx& c, int li, const float* x, int xcs, int h, int w, const float
   }
   posfeat_conv_desc d = make_desc(B, h, w, C, C, L.cin, L.k, 1, dxcs, add ? addcs : 0);
   const long long wcols = posfeat_conv_packed_k(C, L.k, L.k);
-  if (m->wsplit && derive)
-    PF_TRY(timed(c, "bwd:misc", 0, [&] {
-      return pf_split3_rows(wt, L.cin, (int)wcols, (int)wcols, wtp, c.st);
-    }));
   return timed(c, std::string("bwd:dgrad:") + L.name, flops, [&] {
     auto run = [&](int tile) {
       return pf_conv_run_tile(&d, src, wt, nullptr, add, dx, c.s(m->splitk), m->splitk.bytes,

@@ -385,8 +385,9 @@ __global__ void bn_bwd_apply_kernel(const float* __restrict__ y, long long P, in
 // w [C][((ci/32)*9 + tap)*32 + ci%32]; Cin, C % 32 == 0.
 __device__ __forceinline__ int s2_kmap(int pe, int r) { return pe ? (r ? 1 : -1) : (r ? 0 : 2); }
 
+// planes (optional): wp also as three bf16 planes (pf_split3_rows' layout)
 __global__ void s2_phase_weights_kernel(const float* __restrict__ w, int C, int Cin,
-                                        float* __restrict__ wp) {
+                                        float* __restrict__ wp, unsigned short* __restrict__ planes) {
   const int kp4 = C * 4, kp9 = C * 9;
   const long long total = 4LL * Cin * kp4;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
@@ -395,9 +396,17 @@ __global__ void s2_phase_weights_kernel(const float* __restrict__ w, int C, int 
     const int ph = o / Cin, ci = o - ph * Cin;
     const int tap = (k >> 5) & 3, c = (k >> 7) * 32 + (k & 31);
     const int ky = s2_kmap(ph >> 1, tap >> 1), kx = s2_kmap(ph & 1, tap & 1);
-    wp[i] = (ky >= 0 && kx >= 0)
-                ? w[(long long)c * kp9 + ((ci >> 5) * 9 + ky * 3 + kx) * 32 + (ci & 31)]
-                : 0.f;
+    const float v = (ky >= 0 && kx >= 0)
+                        ? w[(long long)c * kp9 + ((ci >> 5) * 9 + ky * 3 + kx) * 32 + (ci & 31)]
+                        : 0.f;
+    wp[i] = v;
+    if (planes) {
+      unsigned hh, mm, ll;
+      pf_split3_pair(v, 0.f, hh, mm, ll);
+      planes[i] = (unsigned short)hh;
+      planes[i + total] = (unsigned short)mm;
+      planes[i + 2 * total] = (unsigned short)ll;
+    }
   }
 }
 

@@ -14,7 +14,10 @@ int pf_conv_wgrad(const float* dy, int ldy, const float* x, int xcs, int n, int 
                   int Cout, int KH, int KW, int stride, float* dw, float* db, int acc, void* ws,
                   size_t ws_bytes, hipStream_t st);
 // packed weights of the input-gradient conv (flipped taps, cin <-> cout)
-int pf_dgrad_weights(const float* w, int Cout, int Cin, int KH, int KW, float* wt, hipStream_t st);
+// planes (optional): wt also as three bf16 planes (pf_split3_rows' layout:
+// pitch = wt's row length, plane stride = its element count)
+int pf_dgrad_weights(const float* w, int Cout, int Cin, int KH, int KW, float* wt, hipStream_t st,
+                     unsigned short* planes = nullptr);
 // adjoint of the bilinear (align_corners=False) resize h x w -> OH x OW over C
 // channels: g [nb][OH][OW] (pitch gcs) -> d [nb][h][w] (pitch dcs); t: nb*OH*w*C floats
 int pf_up4_adjoint(const float* g, int gcs, int nb, int OH, int OW, int h, int w, int C, float* t,

@@ -604,9 +604,11 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ part, const float*
 // W'[ci][k'] with k' = ((co/32)*ntap + tap')*32 + co%32, tap' = ntap-1-tap:
 // the spatially flipped, channel-transposed kernel (stride 1, same padding)
 __global__ void dgrad_weights_kernel(const float* __restrict__ w, int Cout, int Cin, int ntap,
-                                     int kpad_f, float* __restrict__ wt, int kpad_t) {
+                                     int kpad_f, float* __restrict__ wt, int kpad_t,
+                                     unsigned short* __restrict__ planes) {
   const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-  if (i >= (long long)Cin * kpad_t) return;
+  const long long n = (long long)Cin * kpad_t;
+  if (i >= n) return;
   const int ci = (int)(i / kpad_t), kp = (int)(i - (long long)ci * kpad_t);
   const int c = kp >> 5, slab = c / ntap, tapp = c - slab * ntap, co = slab * 32 + (kp & 31);
   float v = 0.f;
@@ -615,6 +617,13 @@ __global__ void dgrad_weights_kernel(const float* __restrict__ w, int Cout, int 
     v = w[(long long)co * kpad_f + ((ci >> 5) * ntap + tap) * 32 + (ci & 31)];
   }
   wt[i] = v;
+  if (planes) {  // split3 per element: the same bits as pf_split3_rows
+    unsigned hh, mm, ll;
+    pf_split3_pair(v, 0.f, hh, mm, ll);
+    planes[i] = (unsigned short)hh;
+    planes[i + n] = (unsigned short)mm;
+    planes[i + 2 * n] = (unsigned short)ll;
+  }
 }
 
 // ---------------------------------------------------------------- x4 upsample adjoint
@@ -1329,12 +1338,12 @@ int pf_wgrad_gemm_batched(const float* dy, int ldy, long long sdy, const float* 
 }
 
 int pf_dgrad_weights(const float* w, int Cout, int Cin, int KH, int KW, float* wt,
-                     hipStream_t st) {
+                     hipStream_t st, unsigned short* planes) {
   if (Cout % 32 || Cin % 32) return POSFEAT_E_INVALID;
   const int kf = posfeat_conv_packed_k(Cin, KH, KW), kt = posfeat_conv_packed_k(Cout, KH, KW);
   const long long n = (long long)Cin * kt;
   hipLaunchKernelGGL(dgrad_weights_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, w,
-                     Cout, Cin, KH * KW, kf, wt, kt);
+                     Cout, Cin, KH * KW, kf, wt, kt, planes);
   PF_CHECK_LAUNCH();
   return POSFEAT_OK;
 }
