@@ -2,7 +2,8 @@
 head.conv2's tap GEMM (B x 120 x 160 x 192 -> 1152) and a 512 -> 256 1x1
 of the decoder F(6x6) GEMMs' size, one tile (conv2d_nhwc_planes), HIP
 events over REPS launches.  A/B switches (POSFEAT_BF6X_MEMF ...) need the A/B
-library (POSFEAT_HIP_LIB=posfeat_amd/libposfeat_hip_ab.so).
+library (POSFEAT_HIP_LIB=posfeat_amd/libposfeat_hip_ab.so).  PROBE_SHAPES=enc:
+the encoder's short-K 1x1 convs instead.
 usage: python tools/tapgemm_probe.py [tile] [reps]"""
 import os
 import sys
@@ -15,6 +16,10 @@ from posfeat_amd import ops  # noqa: E402
 TILE = int(sys.argv[1]) if len(sys.argv) > 1 else 29
 REPS = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 SHAPES = [("tap", 32, 120, 160, 192, 1152), ("f6", 64, 120, 144, 512, 256)]
+if os.environ.get("PROBE_SHAPES") == "enc":   # the encoder's short-K 1x1 convs at B = 32
+    SHAPES = [("l3conv3", 32, 30, 40, 256, 1024), ("l2conv3", 32, 60, 80, 128, 512),
+              ("l3conv1", 32, 30, 40, 1024, 256), ("l2conv1", 32, 60, 80, 512, 128),
+              ("l1conv1", 32, 120, 160, 256, 64)]
 g = torch.Generator(device="cuda").manual_seed(0)
 for name, n, h, w, cin, cout in SHAPES:
     x = torch.randn(n, h, w, cin, device="cuda", generator=g)
@@ -33,6 +38,6 @@ for name, n, h, w, cin, cout in SHAPES:
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / REPS
     tf = 2.0 * n * h * w * cin * cout / ms / 1e9
-    print("%s tile %d memf %s: %.3f ms  %.1f TF/s  frac %.3f  repeat %s" % (
-        name, TILE, os.environ.get("POSFEAT_BF6X_MEMF", "1"), ms, tf, tf / 416.7,
+    print("%s tile %d: %.3f ms  %.1f TF/s  frac %.3f  repeat %s" % (
+        name, TILE, ms, tf, tf / 416.7,
         bool(torch.equal(ref, y))), flush=True)
