@@ -309,6 +309,7 @@ struct GcArgs {
   float* y;
   double* part;
   int h, w, ycs, nqb, nxb;
+  int colmajor;  // block order: tile rows fastest (1) or tile columns fastest (0)
 };
 
 // patch pixel pairs of tile (q0, qx0) of image b into registers
@@ -660,6 +661,19 @@ __device__ __forceinline__ void gc_block(const GcArgs& A, float* spA, float* spB
   }
 }
 
+// the gcombine block order: tile rows fastest, so a tile's vertical
+// neighbours (which share its P halo rows) run 4 blocks later on the same
+// XCD while those rows are still in its L2 (gcombine 2.39 -> 2.35 ms, r15b;
+// strips of 2 / 4 tile columns measured no better, r15c).  A/B:
+// POSFEAT_GC_ORDER=0 -- tile columns fastest
+int gc_colmajor() {
+  static const int v = [] {
+    const char* e = pf_ab_getenv("POSFEAT_GC_ORDER");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return v;
+}
+
 __global__ __launch_bounds__(256, 2) void up4tap_gcombine_kernel(GcArgs A) {
   // P-tile rows 0-3 (spA), the patch planes then rows 4-5 (spB); at the end of
   // each tile the y tile (64 KB) and the statistics
@@ -674,9 +688,18 @@ __global__ __launch_bounds__(256, 2) void up4tap_gcombine_kernel(GcArgs A) {
   if ((gridDim.x & 7) == 0) id = (id & 7) * (gridDim.x >> 3) + (id >> 3);
   const int cg = id % ncg;
   id /= ncg;
-  const int xb = id % A.nxb;
-  id /= A.nxb;
-  const int qb = id % A.nqb, b = id / A.nqb;
+  int xb, qb, b;
+  if (A.colmajor) {  // tile rows fastest: a tile's vertical neighbours run 4 blocks apart
+    qb = id % A.nqb;
+    id /= A.nqb;
+    xb = id % A.nxb;
+    b = id / A.nxb;
+  } else {
+    xb = id % A.nxb;
+    id /= A.nxb;
+    qb = id % A.nqb;
+    b = id / A.nqb;
+  }
   // away from the image border: the branch-free form
   const bool interior = qb > 0 && qb < A.nqb - 1 && xb > 0 && xb * CB_QX + CB_QX < A.w;
   if (interior)
@@ -840,6 +863,7 @@ int pf_up4tap_gcombine(int n, int H, int W, const float* P, const float* img4,
   A.ycs = ycs;
   A.nqb = h / TQ;
   A.nxb = (w + CB_QX - 1) / CB_QX;
+  A.colmajor = gc_colmajor();
   const int nblk = n * A.nqb * A.nxb * (TAP_CO / CB_CG);
   hipLaunchKernelGGL(up4tap_gcombine_kernel, dim3(nblk), dim3(256), 0, st, A);
   PF_CHECK_LAUNCH();
