@@ -1059,6 +1059,22 @@ inline int grid_for(long long total, int block) {
   return (int)g;
 }
 
+// A/B knobs (POSFEAT_WG_TARGET / POSFEAT_WG_MINCH; unset: 1024 workgroups,
+// >= 8 chunks per split)
+int wg_knob(const char* name, int dflt) {
+  const char* e = pf_ab_getenv(name);
+  const int v = e ? atoi(e) : 0;
+  return v > 0 ? v : dflt;
+}
+int wg_target() {
+  static const int v = wg_knob("POSFEAT_WG_TARGET", 1024);
+  return v;
+}
+int wg_minch() {
+  static const int v = wg_knob("POSFEAT_WG_MINCH", 8);
+  return v;
+}
+
 struct WgPlan {
   bool halo;
   int BM, BN, tiles_m, tiles_n, nsplit, nchunks, Kpad, K, ntiles;
@@ -1088,8 +1104,8 @@ WgPlan wgrad_plan(int n, int H, int W, int Cin, int Cout, int KH, int KW, int st
   p.ntiles = p.tiles_m * p.tiles_n;
   // >= 1024 workgroups (2 rounds of the 2-per-CU residency), >= 8 chunks each,
   // partial slabs capped at 128 per tile
-  const int s = (1024 + p.ntiles - 1) / p.ntiles;
-  const int maxs = std::max(1, p.nchunks / 8);
+  const int s = (wg_target() + p.ntiles - 1) / p.ntiles;
+  const int maxs = std::max(1, p.nchunks / wg_minch());
   p.nsplit = std::max(1, std::min(std::min(s, maxs), 128));
   return p;
 }
@@ -1117,8 +1133,8 @@ WgPlan wgrad_plan_bf6(int n, int H, int W, int Cin, int Cout, int KH, int KW) {
   const long long M = (long long)n * H * W;
   p.nchunks = (int)((M + WG_RB - 1) / WG_RB);
   p.ntiles = p.tiles_m * p.tiles_n;
-  const int s = (1024 + p.ntiles - 1) / p.ntiles;
-  const int maxs = std::max(1, p.nchunks / 8);
+  const int s = (wg_target() + p.ntiles - 1) / p.ntiles;
+  const int maxs = std::max(1, p.nchunks / wg_minch());
   p.nsplit = std::max(1, std::min(std::min(s, maxs), 128));
   return p;
 }

@@ -1215,7 +1215,12 @@ int wino_wgrad_nsplit(long long T, int Cin, int Cout, int nb = 36) {
   // tools/asan_host.py found posfeat_wino_wgrad_workspace(.., cin = 32, ..)
   // raising SIGFPE here)
   const long long tiles = std::max(1LL, (long long)nb * (Cout / 128) * (Cin / 128));
-  long long s = (2048 + tiles - 1) / tiles;
+  static const int target = [] {  // A/B knob POSFEAT_WINO_WG_TARGET (unset: 2048)
+    const char* e = pf_ab_getenv("POSFEAT_WINO_WG_TARGET");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? v : 2048;
+  }();
+  long long s = (target + tiles - 1) / tiles;
   const long long chunks = (T + 63) / 64;
   s = std::min(s, std::max(1LL, chunks / 8));  // >= 8 row chunks per split
   return (int)std::max(1LL, std::min(s, 16LL));
