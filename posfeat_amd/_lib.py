@@ -215,7 +215,7 @@ AB_ONLY_SWITCHES = (
     "POSFEAT_BF6", "POSFEAT_BF6B", "POSFEAT_BF6D", "POSFEAT_BF6X", "POSFEAT_BF6X_RB4",
     "POSFEAT_BF6_HALO", "POSFEAT_BF6_STEM", "POSFEAT_CONV_KERNEL", "POSFEAT_CONV_MAXSPLIT",
     "POSFEAT_DISK_FLASH", "POSFEAT_GEMM_B256", "POSFEAT_GFUSE", "POSFEAT_GFUSE_BLOCKS",
-    "POSFEAT_GC_ORDER", "POSFEAT_WG_TARGET", "POSFEAT_WG_MINCH", "POSFEAT_WINO_WG_TARGET", "POSFEAT_GFUSE_K80", "POSFEAT_HEADFUSE", "POSFEAT_HEAD_UP4", "POSFEAT_IMGSTATS",
+    "POSFEAT_GC_ORDER", "POSFEAT_TRAIN_WINO_BF6X", "POSFEAT_WG_TARGET", "POSFEAT_WG_MINCH", "POSFEAT_WINO_WG_TARGET", "POSFEAT_GFUSE_K80", "POSFEAT_HEADFUSE", "POSFEAT_HEAD_UP4", "POSFEAT_IMGSTATS",
     "POSFEAT_S2PHASE", "POSFEAT_SIDE", "POSFEAT_SIDE_AT", "POSFEAT_TRAINTAP",
     "POSFEAT_TRAIN_BN_EPI", "POSFEAT_TRAIN_HALO_BF6", "POSFEAT_TRAIN_TUNE", "POSFEAT_TRAIN_WINO6", "POSFEAT_TRAIN_WINO6_WGRAD",
     "POSFEAT_TUNE_SIMILAR", "POSFEAT_UP2FUSE", "POSFEAT_UP4TAP", "POSFEAT_UP4WINO",

@@ -3286,6 +3286,27 @@ int pf_gemm_batched(const float* A, int lda, long long sa, const float* B, long 
     const char* e = pf_ab_getenv("POSFEAT_GEMM_B256");
     return e && e[0] == '1';
   }();
+  // POSFEAT_TRAIN_WINO_BF6X=1 (A/B, off): the train-mode backbone's batched
+  // (Winograd decoder) GEMMs on the 16x16x32 tiles too, its halo scope lifted
+  // for them.  The fp64 fixture step's per-tensor errors unchanged to the
+  // digits shown; same-box train_desc +0.5..2 % over four pairs, but the
+  // four decoder GEMM launches 1704 us (32x32x16, r15e) vs 1718 us (16x16x32,
+  // r15j) per set and the per-label breakdown flat: not the
+  // default.
+  static const bool twx = [] {
+    const char* e = pf_ab_getenv("POSFEAT_TRAIN_WINO_BF6X");
+    return e && e[0] == '1';
+  }();
+  struct HaloLift {  // the calling thread's halo scope lifted for this call
+    int saved;
+    bool on;
+    explicit HaloLift(bool o) : saved(tl_halo_fp32), on(o) {
+      if (on) tl_halo_fp32 = 0;
+    }
+    ~HaloLift() {
+      if (on) tl_halo_fp32 = saved;
+    }
+  } const lift(twx && Bb);
   const bool x = Bb && bf6x_on();
   // POSFEAT_BF6X_RB4=1 (A/B): the 256-row 16x16x32 tiles for the batched GEMMs
   static const bool rb4 = [] {
