@@ -80,6 +80,17 @@ def conv_arithmetic():
             PEAK_FP32_MFMA_TFLOPS}
 
 
+def launch_ceiling(mask):
+    """(peak TFLOP/s, arithmetic) for a timing label's PF_ARITH mask
+    (posfeat_*_timing_event_arith: 1 fp32 MFMA, 2 bf16x6, 3 both).  A label
+    mixing both is priced against the higher (bf16x6) ceiling, the stricter
+    fraction."""
+    if mask & 2:
+        return round(PEAK_BF16_MFMA_TFLOPS / 6, 1), ("bf16x6" if mask == 2 else
+                                                     "bf16x6 + fp32 MFMA (priced at bf16x6)")
+    return PEAK_FP32_MFMA_TFLOPS, "fp32 MFMA (v_mfma_f32_32x32x2_f32)"
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -519,7 +530,7 @@ def main():
                 sec[name]["batch_pairs"] = a2.batch
                 sec[name]["roofline"] = {k: r2["roofline"].get(k) for k in
                                          ("kernel", "achieved", "peak", "unit", "frac",
-                                          "avg_launch_ms")}
+                                          "arithmetic", "avg_launch_ms")}
     if rank == 0:
         if world == 1 and not args.no_secondary:
             rec["secondary_workloads"] = sec
@@ -561,16 +572,18 @@ def train_main(args, world, rank, dev, emit=True):
     # per-kernel timing of one extra step (HIP events on the engine's stream)
     engine.set_timing(2 * b, H, W, True)
     step.step(im1, im2, F1, F2, epoch=1)
-    evs = engine.timing_events(2 * b, H, W)
+    evs = engine.timing_events(2 * b, H, W, arith=True)
     engine.set_timing(2 * b, H, W, False)
-    bwd_ms = sum(ms for lab, ms, _ in evs if lab.startswith("bwd"))
-    fwd_ms = sum(ms for lab, ms, _ in evs if lab.startswith("conv:"))
-    all_ms = sum(ms for _, ms, _ in evs)
-    # dominant MFMA launch of the step (forward or backward)
+    bwd_ms = sum(e[1] for e in evs if e[0].startswith("bwd"))
+    fwd_ms = sum(e[1] for e in evs if e[0].startswith("conv:"))
+    all_ms = sum(e[1] for e in evs)
+    # dominant MFMA launch of the step (forward or backward), priced against
+    # the ceiling of the arithmetic it runs
     dom = max((e for e in evs if e[2] > 0 and not e[0].startswith("side:")), key=lambda e: e[1])
     ach = dom[2] / (dom[1] * 1e-3) / 1e12
+    peak, arith_name = launch_ceiling(dom[3])
     by_label = {}
-    for lab, ms, _ in evs:
+    for lab, ms, _, _ in evs:
         by_label[lab] = by_label.get(lab, 0.0) + ms
     top = sorted(by_label.items(), key=lambda kv: -kv[1])[:12]
     if rank == 0:
@@ -590,8 +603,9 @@ def train_main(args, world, rank, dev, emit=True):
                        "parallelism": "dp%d (RCCL all-reduce of head grads)" % world},
             "roofline": {"kernel": dom[0], "label": dom[0],
                          "bound": "mfma", "achieved": round(ach, 3),
-                         "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(ach / PEAK_FP32_MFMA_TFLOPS, 4), "traffic": None,
+                         "peak": peak, "unit": "TFLOP/s",
+                         "frac": round(ach / peak, 4), "traffic": None,
+                         "arithmetic": arith_name,
                          "avg_launch_ms": round(dom[1], 4), "flop_per_launch": dom[2]},
             "breakdown_ms": {"forward_convs": round(fwd_ms, 3), "backward_all": round(bwd_ms, 3),
                              "engine_all": round(all_ms, 3),
@@ -602,11 +616,11 @@ def train_main(args, world, rank, dev, emit=True):
             print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return rec if rank == 0 else None
 
 
 # ----------------------------------------------------------------------------
 # configs[2]: descriptor training step (configs/train_desc.yaml)
-    return rec if rank == 0 else None
 
 
 def train_desc_main(args, world, rank, dev, emit=True):
@@ -651,13 +665,21 @@ def train_desc_main(args, world, rank, dev, emit=True):
     all_ms = tr.timing("")[0]
     # the conv classes per layer (labels "<class>:<layer>"), largest first
     by_layer = {}
-    for lab, ms, fl in tr.timing_events():
+    evs = tr.timing_events(arith=True)
+    for lab, ms, fl, _ in evs:
         if lab.count(":") >= 2:
             e = by_layer.setdefault(lab, [0.0, 0.0, 0])
             e[0] += ms
             e[1] += fl
             e[2] += 1
     tr.set_timing(False)
+    # the roofline names ONE launch: the step's longest MFMA conv launch,
+    # priced against the ceiling of the arithmetic it runs (bf16x6 416.7,
+    # fp32 MFMA 157.3)
+    dom1 = max((e for e in evs if e[2] > 0 and e[0].split(":")[0] in ("fwd", "bwd")
+                and e[0].split(":")[1] in ("conv", "wgrad", "dgrad")), key=lambda e: e[1])
+    peak1, arith1 = launch_ceiling(dom1[3])
+    ach1 = dom1[2] / (dom1[1] * 1e-3) / 1e12
     top_layers = [{"label": k, "ms": round(v[0], 3), "launches": v[2],
                    "tflops": round(v[1] / max(v[0], 1e-9) / 1e9, 1)}
                   for k, v in sorted(by_layer.items(), key=lambda kv: -kv[1][0])[:16]]
@@ -684,13 +706,16 @@ def train_desc_main(args, world, rank, dev, emit=True):
                        "global_batch_pairs": b * world, "image": [H, W],
                        "parallelism": "dp%d (RCCL all-reduce of backbone grads%s)" % (
                            world, ", SyncBatchNorm" if world > 1 else "")},
-            "roofline": {"kernel": "%s class (%d launches: %s MFMA convs of the train-mode "
-                                   "ResUNet, flop-weighted)" % (dom, d_n, dom),
-                         "bound": "mfma", "achieved": round(ach, 3),
-                         "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(ach / PEAK_FP32_MFMA_TFLOPS, 4), "traffic": None,
-                         "avg_launch_ms": round(d_ms / max(d_n, 1), 4),
-                         "flop_per_launch": d_fl / max(d_n, 1)},
+            "roofline": {"kernel": dom1[0], "label": dom1[0],
+                         "bound": "mfma", "achieved": round(ach1, 3),
+                         "peak": peak1, "unit": "TFLOP/s",
+                         "frac": round(ach1 / peak1, 4), "traffic": None,
+                         "arithmetic": arith1,
+                         "avg_launch_ms": round(dom1[1], 4), "flop_per_launch": dom1[2],
+                         "note": "the step's longest MFMA conv launch (one label = one "
+                                 "conv call of one layer)"},
+            "dominant_class": {"class": dom, "launches": d_n, "ms": round(d_ms, 3),
+                               "tflops": round(ach, 3)},
             "breakdown_ms": {k: round(v[0], 3) for k, v in cls.items()},
             "top_conv_layers": top_layers,
             "conv_total": {"ms_per_step": round(conv_ms, 3),
@@ -702,11 +727,11 @@ def train_desc_main(args, world, rank, dev, emit=True):
             print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return rec if rank == 0 else None
 
 
 # ----------------------------------------------------------------------------
 # correlation losses of the two training configs, forward + map gradients
-    return rec if rank == 0 else None
 
 
 def corr_main(args, world, rank, dev, emit=True):

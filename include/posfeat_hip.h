@@ -444,6 +444,11 @@ int posfeat_model_timing(posfeat_model *m, const char *prefix, double *ms, doubl
  * engine counts for it.  POSFEAT_E_INVALID past the last launch. */
 int posfeat_model_timing_event(posfeat_model *m, int i, const char **label, double *ms,
                                double *flops);
+/* the arithmetic of the i-th timed label's MFMA launches: a mask of 1 (fp32
+ * MFMA) and 2 (bf16x6, fp32-exact products on the bf16 matrix cores); 0 for a
+ * label without MFMA work.  Diagnostics for bench.py's rooflines (no
+ * reference counterpart). */
+int posfeat_model_timing_event_arith(posfeat_model *m, int i);
 void posfeat_model_destroy(posfeat_model *m);
 
 /* Keypoint-head training (config 5, configs/train_kp.yaml: optimal_modules
@@ -532,6 +537,8 @@ int posfeat_bbtrain_timing(posfeat_bbtrain *m, const char *prefix, double *ms, d
  * POSFEAT_E_INVALID past the last.  Host-synchronises. */
 int posfeat_bbtrain_timing_event(posfeat_bbtrain *m, int i, const char **label, double *ms,
                                  double *flops);
+/* as posfeat_model_timing_event_arith, for the training step's labels */
+int posfeat_bbtrain_timing_event_arith(posfeat_bbtrain *m, int i);
 void posfeat_bbtrain_destroy(posfeat_bbtrain *m);
 int posfeat_adam(float *p, const float *g, float *m, float *v, long long n, float lr, float beta1,
                  float beta2, float eps, float weight_decay, long long step, float grad_scale,

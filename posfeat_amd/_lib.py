@@ -139,6 +139,7 @@ SIGNATURES = {
     "posfeat_bbtrain_timing_event": (c_int, [c_void_p, c_int, ctypes.POINTER(ctypes.c_char_p),
                                              ctypes.POINTER(ctypes.c_double),
                                              ctypes.POINTER(ctypes.c_double)]),
+    "posfeat_bbtrain_timing_event_arith": (c_int, [c_void_p, c_int]),
     "posfeat_bbtrain_timing": (c_int, [c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
                                        ctypes.POINTER(ctypes.c_double), P_int]),
     "posfeat_bbtrain_destroy": (None, [c_void_p]),
@@ -176,6 +177,7 @@ SIGNATURES = {
     "posfeat_model_set_timing": (c_int, [c_void_p, c_int]),
     "posfeat_model_timing": (c_int, [c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
                                      ctypes.POINTER(ctypes.c_double), P_int]),
+    "posfeat_model_timing_event_arith": (c_int, [c_void_p, c_int]),
     "posfeat_model_timing_event": (c_int, [c_void_p, c_int, ctypes.POINTER(ctypes.c_char_p),
                                            ctypes.POINTER(ctypes.c_double),
                                            ctypes.POINTER(ctypes.c_double)]),

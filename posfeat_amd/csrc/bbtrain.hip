@@ -169,8 +169,9 @@ struct posfeat_bbtrain {
   // BatchNorm forward statistics from the conv epilogue (fp64 per-tile sums of
   // y; POSFEAT_TRAIN_BN_EPI=0, A/B: the separate bn_partial_kernel<0> pass)
   bool bn_epi = true;
-  // the direct convs on the engine's autotuned tiles (process-wide cache, timed
-  // on first sight; POSFEAT_TRAIN_TUNE=0, A/B: the default plan)
+  // the direct convs on the tile database's tiles (engine.hip
+  // pf_conv_tuned_run: exact entries only, never timed live unless
+  // POSFEAT_TRAIN_TUNE_LIVE=1; POSFEAT_TRAIN_TUNE=0, A/B: the default plan)
   bool tune = true;
   bool bf6p = false;     // conv precision mode 2 at create (pre-split Winograd operands)
   bool s2phase = true;  // stride-2 input gradients by output phases (POSFEAT_S2PHASE=0: zero insertion)
@@ -185,14 +186,21 @@ struct posfeat_bbtrain {
   Buf wpl;
   // the input-gradient weights of every layer (transposed / phase weights,
   // their bf16 planes, the Winograd U): derived by an accumulate = 0
-  // backward, reused by the accumulate = 1 call of the same step
+  // backward, reused by the accumulate = 1 call of the same step.  bw_valid
+  // records that they were derived from `bw_params` into `bw_scratch` with no
+  // forward since (a forward starts a new step: the parameters may have moved);
+  // an accumulate = 1 call without that rebuilds them
   Buf bw;
+  bool bw_valid = false, derive_now = true;
+  const float* bw_params = nullptr;
+  const void* bw_scratch = nullptr;
   std::vector<size_t> bw_wt, bw_wtp, bw_u;  // float offsets into bw
   // optional per-launch timing (labels "fwd:conv", "bwd:wgrad", ...)
   bool timing = false;
   struct Ev {
     std::string label;
     double flops;
+    int arith = 0;  // PF_ARITH_* mask of the label's MFMA launches
     hipEvent_t a, b;
   };
   std::vector<Ev> evs;
@@ -260,7 +268,11 @@ int timed(Ctx& c, const std::string& label, double flops, F&& fn) {
   e.label = label;
   e.flops = flops;
   if (hipEventRecord(e.a, c.st) != hipSuccess) return POSFEAT_E_HIP;
+  const int outer = pf_arith_mask();  // (labels may nest)
+  pf_arith_mask() = 0;
   const int r = fn();
+  e.arith = pf_arith_mask();
+  pf_arith_mask() = outer | e.arith;
   if (hipEventRecord(e.b, c.st) != hipSuccess) return POSFEAT_E_HIP;
   return r;
 }
@@ -672,7 +684,7 @@ int layer_bwd(Ctx& c, int li, const float* x, int xcs, int h, int w, const float
   // the input-gradient weights: derived here on an accumulate = 0 call, the
   // accumulate = 1 call of the same step (same parameters, same scratch) reuses
   // them (posfeat_bbtrain_backward)
-  const bool derive = !acc;
+  const bool derive = m->derive_now;
   float* wt = c.s(m->bw) + m->bw_wt[li];
   unsigned short* wtp = reinterpret_cast<unsigned short*>(c.s(m->bw) + m->bw_wtp[li]);
   float* Ud = c.s(m->bw) + m->bw_u[li];
@@ -1010,6 +1022,7 @@ extern "C" int posfeat_bbtrain_forward(posfeat_bbtrain* m, const float* params, 
   Ctx c{m, static_cast<char*>(act), static_cast<char*>(scratch), pf_stream(stream), params};
   // fp32 halo tiles: the fixture-validated numerics
   const PfHaloFp32Scope halo32(train_halo_fp32());
+  m->bw_valid = false;  // a new step: the next backward derives its weights again
   PF_TRY(forward(c, img_nchw, stats, momentum));
   if (local_map_nhwc) *local_map_nhwc = c.f(m->fa);
   return POSFEAT_OK;
@@ -1026,7 +1039,17 @@ extern "C" int posfeat_bbtrain_backward(posfeat_bbtrain* m, const float* params,
   Ctx c{m, static_cast<char*>(const_cast<void*>(act)), static_cast<char*>(scratch),
         pf_stream(stream), params};
   const PfHaloFp32Scope halo32(train_halo_fp32());
-  return backward(c, dlocal_map_nhwc, dcs, grad, accumulate ? 1 : 0);
+  // reuse the input-gradient weights only when an accumulate = 0 call of this
+  // step derived them from the same parameters into the same scratch
+  m->derive_now = !accumulate || !m->bw_valid || m->bw_params != params || m->bw_scratch != scratch;
+  m->bw_valid = false;
+  const int rc = backward(c, dlocal_map_nhwc, dcs, grad, accumulate ? 1 : 0);
+  if (rc == POSFEAT_OK) {
+    m->bw_valid = true;
+    m->bw_params = params;
+    m->bw_scratch = scratch;
+  }
+  return rc;
 }
 
 extern "C" int posfeat_bbtrain_set_timing(posfeat_bbtrain* m, int enable) {
@@ -1101,4 +1124,11 @@ extern "C" int posfeat_adam(float* p, const float* g, float* m, float* v, long l
                      v, n, neg_step, beta1, beta2, eps, bc2s, grad_scale, weight_decay);
   PF_CHECK_LAUNCH();
   return POSFEAT_OK;
+}
+
+// the PF_ARITH_* mask of the i-th timed label's MFMA launches (1: fp32 MFMA,
+// 2: bf16x6, 3: both, 0: none), for bench.py's rooflines
+extern "C" int posfeat_bbtrain_timing_event_arith(posfeat_bbtrain* m, int i) {
+  if (!m || i < 0 || (size_t)i >= m->ev_used) return POSFEAT_E_INVALID;
+  return m->evs[i].arith;
 }

@@ -23,6 +23,15 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
     if (_r != POSFEAT_OK) return _r;  \
   } while (0)
 
+// The arithmetic of the MFMA launches a timing label covers (bench.py prices
+// each roofline against the ceiling of the arithmetic its kernel runs): the
+// conv / weight-gradient launchers OR their mode into the calling thread's
+// mask; the timed() helpers clear it before a label's launches and read it
+// after (posfeat_*_timing_event_arith).
+enum { PF_ARITH_FP32 = 1, PF_ARITH_BF6 = 2 };
+int &pf_arith_mask();
+static inline void pf_note_arith(int a) { pf_arith_mask() |= a; }
+
 static inline hipStream_t pf_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
 
 static inline size_t pf_align(size_t x, size_t a) { return (x + a - 1) / a * a; }

@@ -2777,6 +2777,13 @@ int conv_run(ConvArgs& a, const Plan& p, hipStream_t st) {
     default: launch_rows<64, 64, 2, 2>(a, p.kern, st); break;
   }
   PF_CHECK_LAUNCH();
+  // bf16x6: every BF6* tile, the bf16x6 halo twins and the bf16x6 stem;
+  // fp32 MFMA: the fp32 halo / row tiles
+  const bool bf6 = p.tile >= TILE_BF6_128x128 ||
+                   ((p.tile == TILE_H8x128 || p.tile == TILE_H8x64) && halo_bf6_on()) ||
+                   (p.tile < TILE_H8x128 && p.kern == KERN_STAGED && a.Cin % BK != 0 &&
+                    stem_bf6_on());
+  pf_note_arith(bf6 ? PF_ARITH_BF6 : PF_ARITH_FP32);
   if (a.ksplit > 1) {
     const long long total = (long long)a.M * (a.Cout / 4);
     long long g = (total + 255) / 256;
@@ -2789,6 +2796,7 @@ int conv_run(ConvArgs& a, const Plan& p, hipStream_t st) {
 }
 
 void launch_up4(const ConvArgs& a, hipStream_t st) {
+  pf_note_arith(PF_ARITH_FP32);
   hipLaunchKernelGGL(conv_up4_kernel<8>, dim3(a.nwg), dim3(256), 0, st, a);
 }
 
@@ -3332,3 +3340,8 @@ int pf_gemm_batched(const float* A, int lda, long long sa, const float* B, long 
   return conv_run(a, p, st);
 }
 
+
+int& pf_arith_mask() {
+  static thread_local int m = 0;
+  return m;
+}

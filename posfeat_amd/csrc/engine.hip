@@ -211,6 +211,7 @@ struct posfeat_model {
   struct Ev {
     std::string label;
     double flops;
+    int arith = 0;  // PF_ARITH_* mask of the label's MFMA launches
     hipEvent_t a, b;
   };
   std::vector<Ev> evs;
@@ -261,7 +262,11 @@ int timed(Ctx& c, const std::string& label, double flops, F&& fn) {
   e.label = c.side ? "side:" + label : label;
   e.flops = flops;
   if (hipEventRecord(e.a, c.st) != hipSuccess) return POSFEAT_E_HIP;
+  const int outer = pf_arith_mask();  // (labels may nest)
+  pf_arith_mask() = 0;
   const int r = fn();
+  e.arith = pf_arith_mask();
+  pf_arith_mask() = outer | e.arith;
   if (hipEventRecord(e.b, c.st) != hipSuccess) return POSFEAT_E_HIP;
   return r;
 }
@@ -313,7 +318,8 @@ int tune(const std::string& name, const posfeat_conv_desc& d, hipStream_t st, Ru
 // met before with the same class (everything but n, h, w) and a GEMM M
 // (= n * oh * ow) within 25 % reuses that tile without timing (HPatches and
 // Aachen images come in many sizes; POSFEAT_TUNE_SIMILAR=0 turns this off).
-// Results never depend on the tile.
+// An extraction conv's candidates share one arithmetic, so its results never
+// depend on the tile; the training step's direct convs do (pf_conv_tuned_run).
 struct TileCache {
   std::mutex mu;
   std::map<std::string, int> exact;
@@ -337,7 +343,8 @@ double desc_m(const posfeat_conv_desc& d) {
   const int oh = (d.h + 2 * d.pad - d.kh) / d.stride + 1, ow = (d.w + 2 * d.pad - d.kw) / d.stride + 1;
   return (double)d.n * oh * ow;
 }
-bool tile_lookup(const posfeat_conv_desc& d, bool res, bool wplanes, int* tile) {
+bool tile_lookup(const posfeat_conv_desc& d, bool res, bool wplanes, int* tile,
+                 bool exact_only = false) {
   static const bool similar = [] {
     const char* e = pf_ab_getenv("POSFEAT_TUNE_SIMILAR");
     return !(e && e[0] == '0');
@@ -349,10 +356,17 @@ bool tile_lookup(const posfeat_conv_desc& d, bool res, bool wplanes, int* tile) 
   std::lock_guard<std::mutex> g(t.mu);
   auto it = t.exact.find(cls + nhw);
   if (it != t.exact.end()) {
+    // an imported entry (records/tile_db.txt, tuned on another machine or
+    // build) must still be a legal candidate here
+    if (it->second >= 0) {
+      int cand[16];
+      const int nc = pf_conv_candidates(&d, cand, 16, wplanes);
+      if (std::find(cand, cand + nc, it->second) == cand + nc) return false;
+    }
     *tile = it->second;
     return true;
   }
-  if (!similar) return false;
+  if (!similar || exact_only) return false;
   auto ct = t.by_class.find(cls);
   if (ct == t.by_class.end()) return false;
   const double m = desc_m(d);
@@ -1488,20 +1502,35 @@ int head_backward(Ctx& c, const float* dlp, float* grad) {
 
 }  // namespace
 
-// The engine's tile choice (process-wide cache, timed on first sight) for a
-// conv the caller runs itself: the training step's direct convs (bbtrain.hip).
-// `run(tile)` launches the conv with that tile (-1: default plan); results do
-// not depend on the tile.  The calling thread's tile scope is part of the key.
-// A choice taken from a similar conv is stored for this exact descriptor too,
-// so the process repeats it: a later lookup could otherwise meet a closer
-// entry stored meanwhile, and the training step's direct convs are not all
-// bit-identical across tiles (its pre-split tiles differ from the fp32 ones).
+// The tile of a conv the training step runs itself (bbtrain.hip: forward
+// convs, stride-1 input gradients, stride-2 phase convs).  Its direct convs
+// are not all bit-identical across tiles (the pre-split tiles' sums differ
+// from the fp32 ones, and the BatchNorm epilogue's fp64 partials follow the
+// tile), so a choice timed live would make the step's numerics depend on a
+// timing race -- between two runs, and between DDP ranks.  The
+// training step therefore takes a tile only from an EXACT entry of the tile
+// database every rank loads (records/tile_db.txt; its training entries are
+// made by `tools/tile_db.py --train`, which sets POSFEAT_TRAIN_TUNE_LIVE=1 to
+// time the candidates live), and runs the default plan for a conv it does not
+// hold.  `run(tile)` launches the conv with that tile (-1: default plan).
+static bool train_tune_live() {
+  static const bool v = [] {
+    const char* e = getenv("POSFEAT_TRAIN_TUNE_LIVE");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
 int pf_conv_tuned_run(const posfeat_conv_desc* d, bool res, bool wplanes, hipStream_t st,
                       const std::function<int(int)>& run) {
   int tile = -1;
-  if (!tile_lookup(*d, res, wplanes, &tile))
-    tile = tune("train", *d, st, run, wplanes);
-  tile_store(*d, res, wplanes, tile);
+  if (!tile_lookup(*d, res, wplanes, &tile, /*exact_only=*/true)) {
+    tile = -1;
+    if (train_tune_live()) {
+      tile = tune("train", *d, st, run, wplanes);
+      tile_store(*d, res, wplanes, tile);
+    }
+  }
   return run(tile);
 }
 
@@ -1785,3 +1814,10 @@ extern "C" int posfeat_device_ok(void) {
 // 1 in the A/B build (make ab: the POSFEAT_* path switches are read), 0 in
 // the shipped library (common.h pf_ab_getenv)
 extern "C" int posfeat_ab_build(void) { return POSFEAT_AB ? 1 : 0; }
+
+// the PF_ARITH_* mask of the i-th timed label's MFMA launches (1: fp32 MFMA,
+// 2: bf16x6, 3: both, 0: none), for bench.py's rooflines
+extern "C" int posfeat_model_timing_event_arith(posfeat_model* m, int i) {
+  if (!m || i < 0 || (size_t)i >= m->ev_used) return POSFEAT_E_INVALID;
+  return m->evs[i].arith;
+}

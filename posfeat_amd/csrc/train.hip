@@ -1217,6 +1217,9 @@ int pf_conv_wgrad(const float* dy, int ldy, const float* x, int xcs, int n, int 
   else
     hipLaunchKernelGGL((conv_wgrad_kernel<64, 64>), grid, dim3(256), 0, st, a);
   PF_CHECK_LAUNCH();
+  pf_note_arith(b6all || (!p.halo && p.BM == 128 && p.BN == 128 && Cin % 32 == 0 && wgrad_bf6_on())
+                    ? PF_ARITH_BF6
+                    : PF_ARITH_FP32);
   const long long ne = (long long)Cout * p.Kpad;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, st,
                      a.part, a.partb, p.nsplit, Cout, p.Kpad, dw, db, acc);
@@ -1298,6 +1301,7 @@ int pf_conv_wgrad_per_image(const float* dy, int ldy, const float* x, int xcs, i
   else
     hipLaunchKernelGGL(conv_wgrad_halo_kernel<2>, grid, dim3(128), 0, st, a);
   PF_CHECK_LAUNCH();
+  pf_note_arith(b6 ? PF_ARITH_BF6 : PF_ARITH_FP32);
   const long long per = (long long)Cout * p.Kpad;
   hipLaunchKernelGGL(wgrad_reduce_images_kernel, dim3((unsigned)((per * n + 255) / 256)), dim3(256),
                      0, st, a.part, k, per, n, dw);
@@ -1350,6 +1354,7 @@ int pf_wgrad_gemm_batched(const float* dy, int ldy, long long sdy, const float* 
     hipLaunchKernelGGL((conv_wgrad_kernel<128, 128>), dim3(a.ntiles * nsplit, nb), dim3(256), 0,
                        st, a);
   PF_CHECK_LAUNCH();
+  pf_note_arith(wgrad_bf6_on() ? PF_ARITH_BF6 : PF_ARITH_FP32);
   return POSFEAT_OK;
 }
 

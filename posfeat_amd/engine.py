@@ -53,7 +53,9 @@ def tile_db_import(path):
 def _load_tile_db():
     """Once per process: the tuning database shipped in records/ (made by
     tools/tile_db.py on an MI355X; POSFEAT_TILE_DB = another file, or 0 for
-    none).  Tiles never change results, only which candidate runs."""
+    none).  An extraction conv's tiles never change its results, only which
+    candidate runs; the training step (BackboneTrainer) uses only the exact
+    entries for its convs, so every rank and run picks the same tiles."""
     global _tile_db_loaded
     if _tile_db_loaded:
         return
@@ -189,14 +191,19 @@ class ExtractionEngine:
                                          ctypes.byref(fl), ctypes.byref(n)))
         return ms.value, fl.value, n.value
 
-    def timing_events(self, b, h, w):
-        """[(label, ms, flops)] of every timed launch of the last run (host-synchronises)."""
+    def timing_events(self, b, h, w, arith=False):
+        """[(label, ms, flops)] of every timed launch of the last run
+        (host-synchronises); ``arith=True`` appends the arithmetic mask of the
+        label's MFMA launches (1 fp32 MFMA, 2 bf16x6, 3 both, 0 none)."""
         handle, _, _ = self._instance(b, h, w)
         out, i = [], 0
         lab, ms, fl = ctypes.c_char_p(), ctypes.c_double(), ctypes.c_double()
         while lib().posfeat_model_timing_event(handle, i, ctypes.byref(lab), ctypes.byref(ms),
                                                ctypes.byref(fl)) == 0:
-            out.append((lab.value.decode(), ms.value, fl.value))
+            ev = (lab.value.decode(), ms.value, fl.value)
+            if arith:
+                ev += (int(lib().posfeat_model_timing_event_arith(handle, i)),)
+            out.append(ev)
             i += 1
         return out
 

@@ -25,7 +25,7 @@ import torch.distributed as dist
 
 from . import _lib
 from ._lib import c_int, check, lib, ptr, stream_ptr
-from .engine import ExtractionEngine
+from .engine import ExtractionEngine, _load_tile_db
 from .parallel import allreduce_head_grad
 
 DISK_DEFAULTS = {"grid_size": 8, "loss_distance": "cos", "temperature_base": 60,
@@ -247,6 +247,9 @@ class BackboneTrainer:
         import ctypes
         from . import weights
         _lib.require_device()
+        # the training convs' tiles: exact tile-database entries only (the same
+        # file on every rank -> the same tiles, engine.hip pf_conv_tuned_run)
+        _load_tile_db()
         L = lib()
         self.table = _lib.bbtrain_table()
         params, stats = weights.pack_bbtrain(backbone_sd, self.table)
@@ -360,15 +363,19 @@ class BackboneTrainer:
                                            ctypes.byref(fl), ctypes.byref(n)))
         return ms.value, fl.value, n.value
 
-    def timing_events(self):
+    def timing_events(self, arith=False):
         """[(label, ms, flops)] of every timed launch of the last timed step
-        (host-synchronises)."""
+        (host-synchronises); ``arith=True`` appends the arithmetic mask of the
+        label's MFMA launches (1 fp32 MFMA, 2 bf16x6, 3 both, 0 none)."""
         import ctypes
         out, i = [], 0
         lab, ms, fl = ctypes.c_char_p(), ctypes.c_double(), ctypes.c_double()
         while lib().posfeat_bbtrain_timing_event(self._h, i, ctypes.byref(lab), ctypes.byref(ms),
                                                  ctypes.byref(fl)) == 0:
-            out.append((lab.value.decode(), ms.value, fl.value))
+            ev = (lab.value.decode(), ms.value, fl.value)
+            if arith:
+                ev += (int(lib().posfeat_bbtrain_timing_event_arith(self._h, i)),)
+            out.append(ev)
             i += 1
         return out
 
