@@ -310,6 +310,7 @@ struct GcArgs {
   double* part;
   int h, w, ycs, nqb, nxb;
   int colmajor;  // block order: tile rows fastest (1) or tile columns fastest (0)
+  int ystore;    // 0 (A/B ablation POSFEAT_GC_NOSTORE=1): statistics only, y not written
 };
 
 // patch pixel pairs of tile (q0, qx0) of image b into registers
@@ -622,7 +623,7 @@ __device__ __forceinline__ void gc_block(const GcArgs& A, float* spA, float* spB
     // reports any s_barrier crossed with LDS accesses outstanding.)
     gc_wait_lgkm0();
     gc_barrier();
-    {
+    if (A.ystore) {
       float* so = spA + (8 * wave + 4 * hl) * CB_CG + ln;
 #pragma unroll
       for (int t = 0; t < 4; ++t)
@@ -636,7 +637,7 @@ __device__ __forceinline__ void gc_block(const GcArgs& A, float* spA, float* spB
     }
     gc_wait_lgkm0();
     gc_barrier();
-    {
+    if (A.ystore) {
       const int col = tid >> 3, quad = tid & 7, X = X0 + col;
       const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
           A.y + ((long long)b * H + Y0) * W * A.ycs, (short)0, 0x7fffffff, 0x00020000);
@@ -864,6 +865,13 @@ int pf_up4tap_gcombine(int n, int H, int W, const float* P, const float* img4,
   A.nqb = h / TQ;
   A.nxb = (w + CB_QX - 1) / CB_QX;
   A.colmajor = gc_colmajor();
+  {
+    static const bool nostore = [] {
+      const char* e = pf_ab_getenv("POSFEAT_GC_NOSTORE");
+      return e && e[0] == '1';
+    }();
+    A.ystore = nostore ? 0 : 1;
+  }
   const int nblk = n * A.nqb * A.nxb * (TAP_CO / CB_CG);
   hipLaunchKernelGGL(up4tap_gcombine_kernel, dim3(nblk), dim3(256), 0, st, A);
   PF_CHECK_LAUNCH();
