@@ -505,11 +505,18 @@ typedef struct posfeat_bbtrain posfeat_bbtrain;
  * RCCL: rank 0 calls posfeat_group_unique_id (128 bytes), the host broadcasts
  *   them (torch.distributed), every rank calls posfeat_group_create_rccl.
  * local: `world` ranks that are threads of one process on one device (the
- *   one-GPU test of the cross-rank semantics). */
+ *   one-GPU test of the cross-rank semantics).
+ * host: a process group without RCCL (torch.distributed over gloo, e.g. ranks
+ *   that share one device): each exchange copies the n doubles to the host
+ *   (the stream is synchronised), calls allreduce(buf, n, user) -- which must
+ *   sum buf in place over the ranks and return 0 -- and copies them back. */
 typedef struct posfeat_group posfeat_group;
 typedef struct posfeat_local_group posfeat_local_group;
+typedef int (*posfeat_host_allreduce_fn)(double *buf, int n, void *user);
 int posfeat_group_unique_id(void *out128);
 int posfeat_group_create_rccl(int world, int rank, const void *id128, posfeat_group **out);
+int posfeat_group_create_host(int world, int rank, posfeat_host_allreduce_fn allreduce,
+                              void *user, posfeat_group **out);
 int posfeat_local_group_create(int world, int max_doubles, posfeat_local_group **out);
 int posfeat_group_create_local(posfeat_local_group *L, int rank, posfeat_group **out);
 void posfeat_group_destroy(posfeat_group *g);

@@ -148,6 +148,8 @@ SIGNATURES = {
     "posfeat_group_create_rccl": (c_int, [c_int, c_int, c_void_p, ctypes.POINTER(c_void_p)]),
     "posfeat_local_group_create": (c_int, [c_int, c_int, ctypes.POINTER(c_void_p)]),
     "posfeat_group_create_local": (c_int, [c_void_p, c_int, ctypes.POINTER(c_void_p)]),
+    "posfeat_group_create_host": (c_int, [c_int, c_int, c_void_p, c_void_p,
+                                          ctypes.POINTER(c_void_p)]),
     "posfeat_group_destroy": (None, [c_void_p]),
     "posfeat_local_group_destroy": (None, [c_void_p]),
     "posfeat_adam": (c_int, [c_void_p] * 4 + [c_ll] + [c_float] * 5 + [c_ll, c_float, c_void_p]),

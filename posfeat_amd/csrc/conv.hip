@@ -548,6 +548,16 @@ __device__ __forceinline__ void wait_vmcnt() {
   static_assert(N >= 0 && N < 64, "vmcnt");
   __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
 }
+// ... and every LDS access of this wave completed: the K loops' barriers
+// then never overtake one of the wave's own fragment reads, whatever the
+// relative latency of the LDS and of the DMA that refills the stage after
+// the barrier (tools/isa_check.py fails an s_barrier crossed with LDS
+// accesses outstanding)
+template <int N>
+__device__ __forceinline__ void wait_vmcnt_lgkm0() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (0 << 8) | ((N >> 4) << 14));
+}
 
 // ---- fp32-exact products on the bf16 matrix cores ("bf16x6") -------------
 // gfx950 runs v_mfma_f32_32x32x16_bf16 at 16x the rate of the fp32-input MFMA
@@ -1198,7 +1208,7 @@ void conv_bf6d_kernel(ConvArgs a) {
       // B(ii) landed (and with it every older load, A(ii) included): it was
       // issued right before the 4 A loads of the previous step / the prologue
       __builtin_amdgcn_sched_barrier(PF_SCHED_NO_VMEM);
-      wait_vmcnt<4>();
+      wait_vmcnt_lgkm0<4>();
       __builtin_amdgcn_s_barrier();
       const int s = ii & 1;
       // split this chunk's A (frees va[u] for chunk ii + D)
@@ -1349,7 +1359,7 @@ void conv_bf6s_kernel(ConvArgs a) {
     for (int u = 0; u < D; ++u) {
       const int ii = i + u;
       __builtin_amdgcn_sched_barrier(PF_SCHED_NO_VMEM);
-      wait_vmcnt<6>();  // B(ii) and everything older (A(ii) included) landed
+      wait_vmcnt_lgkm0<6>();  // B(ii) and everything older (A(ii) included) landed
       __builtin_amdgcn_s_barrier();
       const int s = ii & 1;
       const u32x4_t ah0 = va[u][0], am0 = va[u][1], al0 = va[u][2];

@@ -399,7 +399,7 @@ __device__ __forceinline__ WinPatch window_patch_logits(const float* __restrict_
 }
 
 // One wave per query point: epipolar line search + window expectation.
-__global__ void line_window_kernel(const float* __restrict__ cpx,   // [b][n][2] query pixels
+__global__ PF_NO_PK_FP32 void line_window_kernel(const float* __restrict__ cpx,   // [b][n][2] query pixels
                                    const float* __restrict__ Fm,    // [b][3][3]
                                    const float* __restrict__ f1,    // [b][n][128] L2-normed
                                    const float* __restrict__ fm2,   // [b][h2][w2][128] T*norm
@@ -585,7 +585,7 @@ __device__ __forceinline__ float epi_cost(const float* F, float x1, float y1, fl
 
 // EpipolarLoss_full.forward: one workgroup.  out[0] = loss, out[1..6] =
 // loss_g1, loss_w1, loss_g2, loss_w2, percent_g, percent_w.
-__global__ __launch_bounds__(1024) void epipolar_loss_kernel(
+__global__ __launch_bounds__(1024) PF_NO_PK_FP32 void epipolar_loss_kernel(
     int nb, int n, const float* __restrict__ F1, const float* __restrict__ F2,
     const float* __restrict__ c1, const float* __restrict__ c2, const float* __restrict__ g1,
     const float* __restrict__ g2, const float* __restrict__ w1, const float* __restrict__ w2,
@@ -681,7 +681,7 @@ __device__ __forceinline__ void fx_add(unsigned long long* p, float v) {
 // with F1, coords1, image-2 size; k = 3: w2): one workgroup, the forward's
 // fixed-order reductions recomputed.  d loss/d cost_i = ww * wt_i / total,
 // d cost/d x2 = sign(x2^T l) l[:2] (l normalised), x2 = E * c + c.
-__global__ __launch_bounds__(1024) void epi_loss_bwd_kernel(
+__global__ __launch_bounds__(1024) PF_NO_PK_FP32 void epi_loss_bwd_kernel(
     int nb, int n, const float* __restrict__ Fm, const float* __restrict__ cq,
     const float* __restrict__ wpx, const float* __restrict__ wsd, const uint8_t* __restrict__ v,
     float short_edge, float wthr, float ww, float c0, float c1, float* __restrict__ gE) {
@@ -742,7 +742,7 @@ __global__ __launch_bounds__(1024) void epi_loss_bwd_kernel(
 //   dp_s = gE . g_s,  dsim_s = p_s (dp_s - sum p dp),
 //   dq   = sum_s dsim_s v_s            (query descriptor, written to dq)
 //   d fm[corner] += bilinear_w * dsim_s * q   (fixed-point scatter)
-__global__ void window_bwd_kernel(const float* __restrict__ f1, const float* __restrict__ fm2,
+__global__ PF_NO_PK_FP32 void window_bwd_kernel(const float* __restrict__ f1, const float* __restrict__ fm2,
                                   const float* __restrict__ center, const float* __restrict__ gE,
                                   int nb, int n, int h2, int w2, int win_h, int win_w,
                                   float window_size, float* __restrict__ dq,
@@ -1104,7 +1104,7 @@ bool window_patch_fits(int win_h, int win_w) {
 // the L2 normalisation (f = s / |s|), written over dq ([b][n][128]); the
 // bilinear spread of g into the map's 4 corner pixels is gathered per pixel by
 // l2norm_bwd_kernel (no zeroed fixed-point accumulator, no atomics).
-__global__ void query_bwd_kernel(const float* __restrict__ xf, int cs, const float* __restrict__ cn,
+__global__ PF_NO_PK_FP32 void query_bwd_kernel(const float* __restrict__ xf, int cs, const float* __restrict__ cn,
                                  const float* __restrict__ f, float* __restrict__ dq, int nb, int n,
                                  int h, int w) {
   const int lane = threadIdx.x & 63;
@@ -1159,7 +1159,7 @@ __global__ void query_bwd_kernel(const float* __restrict__ xf, int cs, const flo
 // sum over the grid points whose bilinear sample has p as a corner of
 // corner weight x g (query_bwd_kernel), over the cells that can hold such a
 // sample (a sample sits in its cell) in a fixed order
-__global__ void l2norm_bwd_kernel(const float* __restrict__ x, int cs,
+__global__ PF_NO_PK_FP32 void l2norm_bwd_kernel(const float* __restrict__ x, int cs,
                                   const unsigned long long* __restrict__ afm,
                                   const float* __restrict__ dfm, const float* __restrict__ cn,
                                   const float* __restrict__ gq, int h, int w, int grid,

@@ -49,7 +49,7 @@ __device__ __forceinline__ float bern_logp(float x, bool y) {
   return y ? -(fmaxf(-x, 0.f) + t) : -(fmaxf(x, 0.f) + t);
 }
 
-__global__ void disk_point_kernel(const float* __restrict__ kp, int nb, int H, int W,
+__global__ PF_NO_PK_FP32 void disk_point_kernel(const float* __restrict__ kp, int nb, int H, int W,
                                   const int32_t* __restrict__ prop_in,
                                   const uint8_t* __restrict__ acc_in,
                                   const float* __restrict__ uni,  // [b][n][65] if sampling

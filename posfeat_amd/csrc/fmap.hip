@@ -422,7 +422,7 @@ __global__ void head_tail_conv3_kernel(const float* __restrict__ x, int n, int h
   }
 }
 
-__global__ void softplus_norm_kernel(const float* __restrict__ x, int n, int hw,
+__global__ PF_NO_PK_FP32 void softplus_norm_kernel(const float* __restrict__ x, int n, int hw,
                                      const float* __restrict__ mean,
                                      const float* __restrict__ rstd, float* __restrict__ y) {
   const long long total = (long long)n * hw;
@@ -434,7 +434,7 @@ __global__ void softplus_norm_kernel(const float* __restrict__ x, int n, int hw,
 }
 
 // the same, four pixels (16 B) per thread (hw % 4 == 0: one image per quad)
-__global__ void softplus_norm4_kernel(const float* __restrict__ x, int n, int hw,
+__global__ PF_NO_PK_FP32 void softplus_norm4_kernel(const float* __restrict__ x, int n, int hw,
                                       const float* __restrict__ mean,
                                       const float* __restrict__ rstd, float* __restrict__ y) {
   const long long total4 = (long long)n * hw / 4;

@@ -88,7 +88,7 @@ __global__ __launch_bounds__(128) void gfuse_weights_kernel(
 // into the ring buffer ring[b][r][128] instead (r = the ring index below, the
 // order pf_ring_index in fmap.h restates), for up4tap_gcombine_kernel.
 constexpr int GF_RP = 64;  // ring pixels per block
-__global__ __launch_bounds__(2 * GF_COUT) void gfuse_ring_kernel(
+__global__ __launch_bounds__(2 * GF_COUT) PF_NO_PK_FP32 void gfuse_ring_kernel(
     const float* __restrict__ c, int ccs, const float* __restrict__ img4,
     const float* __restrict__ w1, int k1pad, const float* __restrict__ b1, int H, int W,
     const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ w2t,

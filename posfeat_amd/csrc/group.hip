@@ -7,11 +7,15 @@
 //   the ranks' batches (forward: sum y, sum y^2; backward: sum g, sum g x^).
 //
 // One exchange = an in-place sum over ranks of `n` doubles on the caller's
-// stream.  Two implementations behind one handle:
+// stream.  Three implementations behind one handle:
 //   * RCCL: ncclAllReduce(fp64, sum) on a communicator created from a unique
 //     id the host broadcasts (torch.distributed on the host side).  librccl is
 //     resolved at run time (dlopen; the copy torch already loaded first), so
 //     this library has no link-time RCCL dependency.
+//   * host: a process group without RCCL (gloo; e.g. ranks sharing one
+//     device, where RCCL refuses a second rank on the same GPU): the vector
+//     goes to pinned host memory, a caller callback sums it over the ranks
+//     (torch.distributed.all_reduce in parallel.SyncBNGroup), and back.
 //   * local: N "ranks" that are threads of one process on one device (tests:
 //     two half-batch ranks against one full-batch run on a one-GPU box).  Rank
 //     r copies its vector into slot r of a shared device buffer; after a host
@@ -100,6 +104,10 @@ struct posfeat_group {
   int world = 1, rank = 0;
   Comm comm = nullptr;                     // RCCL
   posfeat_local_group* local = nullptr;    // local emulation
+  posfeat_host_allreduce_fn host = nullptr;  // host transport (gloo process groups)
+  void* user = nullptr;
+  double* hbuf = nullptr;  // pinned staging of the host transport
+  int hcap = 0;
 };
 
 int pf_group_world(const posfeat_group* g) { return g ? g->world : 1; }
@@ -109,6 +117,27 @@ int pf_group_allreduce(posfeat_group* g, double* buf, int n, hipStream_t st) {
   if (g->comm) {
     const int r = rccl().allreduce(buf, buf, (size_t)n, 8 /*fp64*/, 0 /*sum*/, g->comm, st);
     return r == 0 ? POSFEAT_OK : POSFEAT_E_HIP;
+  }
+  if (g->host) {
+    if (n > g->hcap) {
+      if (g->hbuf) (void)hipHostFree(g->hbuf);
+      g->hbuf = nullptr;
+      g->hcap = 0;
+      if (hipHostMalloc(reinterpret_cast<void**>(&g->hbuf), (size_t)n * sizeof(double), 0) !=
+          hipSuccess)
+        return POSFEAT_E_HIP;
+      g->hcap = n;
+    }
+    if (hipMemcpyAsync(g->hbuf, buf, (size_t)n * sizeof(double), hipMemcpyDeviceToHost, st) !=
+            hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+      return POSFEAT_E_HIP;
+    if (g->host(g->hbuf, n, g->user) != 0) return POSFEAT_E_INVALID;
+    if (hipMemcpyAsync(buf, g->hbuf, (size_t)n * sizeof(double), hipMemcpyHostToDevice, st) !=
+            hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+      return POSFEAT_E_HIP;
+    return POSFEAT_OK;
   }
   posfeat_local_group* L = g->local;
   if (n > L->stride) return POSFEAT_E_INVALID;
@@ -173,9 +202,22 @@ extern "C" int posfeat_group_create_local(posfeat_local_group* L, int rank, posf
   return POSFEAT_OK;
 }
 
+extern "C" int posfeat_group_create_host(int world, int rank, posfeat_host_allreduce_fn allreduce,
+                                         void* user, posfeat_group** out) {
+  if (!out || !allreduce || world < 1 || rank < 0 || rank >= world) return POSFEAT_E_INVALID;
+  posfeat_group* g = new posfeat_group();
+  g->world = world;
+  g->rank = rank;
+  g->host = allreduce;
+  g->user = user;
+  *out = g;
+  return POSFEAT_OK;
+}
+
 extern "C" void posfeat_group_destroy(posfeat_group* g) {
   if (!g) return;
   if (g->comm && rccl().ok) (void)rccl().destroy(g->comm);
+  if (g->hbuf) (void)hipHostFree(g->hbuf);
   delete g;
 }
 

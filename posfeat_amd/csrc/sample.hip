@@ -71,7 +71,7 @@ __global__ void sample_desc_kernel(const float* __restrict__ fmap, int nb, int C
 // two keypoints per wave and half the load instructions of the one-wave form;
 // each channel's bilinear sum in the same order (the norm's sum of squares is
 // grouped differently: per-lane quads, then a 32-lane tree)
-__global__ void sample_desc128_kernel(const float* __restrict__ fmap, int nb, int h, int w, int cs,
+__global__ PF_NO_PK_FP32 void sample_desc128_kernel(const float* __restrict__ fmap, int nb, int h, int w, int cs,
                                       const float* __restrict__ coord, int npts,
                                       const int32_t* __restrict__ n_valid, int each,
                                       int normalize, float* __restrict__ out) {

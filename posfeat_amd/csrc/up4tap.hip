@@ -77,7 +77,7 @@ constexpr int CB_QX = 8, CB_CG = 32, CB_RY = TQ + 2, CB_CX = CB_QX + 2;
 constexpr int CB_SEG = CB_RY * CB_CX * 9;  // 128-B (32-channel) segments per block
 constexpr int CB_SEGP = (CB_SEG + 7) / 8 * 8;  // padded to whole DMA wave-instructions
 
-__global__ __launch_bounds__(256) void up4tap_combine_kernel(const float* __restrict__ P, int h,
+__global__ __launch_bounds__(256) PF_NO_PK_FP32 void up4tap_combine_kernel(const float* __restrict__ P, int h,
                                                              int w, float* __restrict__ y, int ycs,
                                                              double* __restrict__ part) {
   __shared__ __attribute__((aligned(16))) float sp[CB_SEGP * CB_CG];
@@ -735,7 +735,7 @@ __device__ __forceinline__ float up4_cw(int u, int i, int n) {
 // support [4 iy - 2, 4 iy + 5] (which pairs those are is fixed at compile time;
 // the weight itself clamps at the borders).
 template <int TQ>
-__global__ __launch_bounds__(256) void up4tap_adjoint_kernel(const float* __restrict__ dy, int dycs,
+__global__ __launch_bounds__(256) PF_NO_PK_FP32 void up4tap_adjoint_kernel(const float* __restrict__ dy, int dycs,
                                                              int h, int w, float* __restrict__ D) {
   const int H = 4 * h, W = 4 * w;
   const int tid = threadIdx.x, cq = tid & 31, xl = tid >> 5;

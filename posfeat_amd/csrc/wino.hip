@@ -224,7 +224,7 @@ __global__ void wino4_weights_kernel(const float* __restrict__ wpk, int Cout, in
 // input (upconv, DescNet.py:182-190): its values are interpolated here
 // (pf_up2ac_at, the upsample kernel's own arithmetic) instead of read from a
 // materialised upsample
-__global__ __launch_bounds__(256) void wino4_input_kernel(const float* __restrict__ x, int xcs,
+__global__ __launch_bounds__(256) PF_NO_PK_FP32 void wino4_input_kernel(const float* __restrict__ x, int xcs,
                                                           int n, int h, int w, int c4n,
                                                           float* __restrict__ V, int clamp = 0,
                                                           unsigned short* __restrict__ Vb = nullptr,

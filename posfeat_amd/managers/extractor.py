@@ -260,7 +260,9 @@ class Extractor:
             torch.cuda.set_device(self.local_rank)
             self.device = torch.device("cuda", self.local_rank)
             if not dist.is_initialized():
-                dist.init_process_group(backend="nccl")
+                # RCCL; POSFEAT_DIST_BACKEND=gloo: ranks sharing one device (tests)
+                from ..parallel import dist_backend
+                dist.init_process_group(backend=dist_backend())
             self.multi_gpu = True
             self.output_flag = self.rank == 0
         else:

@@ -13,8 +13,20 @@ import torch
 import torch.distributed as dist
 
 
+def dist_backend():
+    """The process-group backend a rank initialises: RCCL ("nccl") on the GPU
+    box.  POSFEAT_DIST_BACKEND=gloo (tests) selects gloo, so several ranks can
+    share one device -- RCCL refuses two ranks on the same GPU; the SyncBN
+    statistics then take SyncBNGroup's host transport."""
+    import os
+    return os.environ.get("POSFEAT_DIST_BACKEND", "nccl")
+
+
 def broadcast_weights(state_dicts, device, src=0):
     """In-place broadcast of every tensor in ``state_dicts`` from ``src``."""
+    # gloo broadcasts host tensors (the RCCL path keeps the buffer on the device)
+    if dist.get_backend() != "nccl":
+        device = "cpu"
     floats, ints = [], []
     for sd in state_dicts:
         for k, v in sd.items():
@@ -72,18 +84,33 @@ class SyncBNGroup:
     differently across ranks (the condition under which two RCCL
     communicators can deadlock)."""
 
-    def __init__(self, group=None, lib=None, shape=None):
+    _HostFn = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.c_int,
+                               ctypes.c_void_p)
+
+    def __init__(self, group=None, lib=None, shape=None, transport=None):
         from . import _lib
         self._lib = lib or _lib.lib()
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
+        self.group = group
         self.shape = None if shape is None else tuple(int(v) for v in shape)
+        backend = dist.get_backend(group)
+        # RCCL in-stream for an RCCL process group; over any other backend
+        # (gloo: e.g. ranks that share one device) the host transport
+        self.transport = transport or ("rccl" if backend == "nccl" else "host")
+        if self.transport == "host":
+            self._cb = self._HostFn(self._host_allreduce)   # kept alive with the group
+            h = ctypes.c_void_p()
+            _lib.check(self._lib.posfeat_group_create_host(
+                self.world, self.rank, ctypes.cast(self._cb, ctypes.c_void_p), None,
+                ctypes.byref(h)))
+            self.handle = h
+            return
         id_host = torch.zeros(128, dtype=torch.uint8)
         if self.rank == 0:
             buf = (ctypes.c_ubyte * 128)()
             _lib.check(self._lib.posfeat_group_unique_id(ctypes.addressof(buf)))
             id_host.copy_(torch.frombuffer(bytearray(buf), dtype=torch.uint8))
-        backend = dist.get_backend(group)
         dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else "cpu"
         t = id_host.to(dev)
         dist.broadcast(t, src=dist.get_global_rank(group, 0) if group is not None else 0,
@@ -94,6 +121,16 @@ class SyncBNGroup:
         _lib.check(self._lib.posfeat_group_create_rccl(self.world, self.rank,
                                                         ctypes.addressof(raw), ctypes.byref(h)))
         self.handle = h
+
+    def _host_allreduce(self, buf, n, user):
+        """host transport: sum n doubles in place over the group's ranks"""
+        try:
+            import numpy as np
+            t = torch.from_numpy(np.ctypeslib.as_array(buf, shape=(n,)))
+            dist.all_reduce(t, group=self.group)
+            return 0
+        except Exception:  # noqa: BLE001 - reported to the C side as a failed exchange
+            return -1
 
     def close(self):
         if getattr(self, "handle", None) is not None and self.handle.value:

@@ -9,6 +9,8 @@ import numpy as np
 import pytest
 import torch
 
+import tol
+
 from conftest import GOLDEN, ROOT
 
 pytestmark = pytest.mark.gpu
@@ -42,9 +44,7 @@ def test_posfeat_extract_matches_golden(gpu, model):
                                "local_thr", "global_point"}
     assert out["local_thr"].abs().sum() == 0 and out["global_point"].shape == (1, 1, 6, 8)
     for k in ("local_map", "global_map", "local_point", "global_feat"):
-        ref = d["a_" + k]
-        err = np.abs(out[k].cpu().numpy() - ref).max()
-        assert err <= 1e-4 * max(1.0, np.abs(ref).max()), k
+        tol.check(k, out[k], d["a_" + k], "PoSFeat.extract vs golden")
 
 
 def test_checkpoint_roundtrip(gpu, model, tmp_path):
@@ -80,8 +80,7 @@ def test_resunet_forward(gpu, model):
     out = model.backbone(img.to(gpu))
     ref = model_ref.resunet_forward({k: v.cpu() for k, v in model.backbone.state_dict().items()}, img)
     for k in ("global_map", "local_map", "local_map_small"):
-        err = (out[k].cpu() - ref[k]).abs().max().item()
-        assert err <= 1e-4 * max(1.0, ref[k].abs().max().item()), k
+        tol.check(k, out[k], ref[k], "ResUNet.forward vs oracle")
 
 
 def test_keypointdet_forward_standalone(gpu, model):
@@ -97,8 +96,7 @@ def test_keypointdet_forward_standalone(gpu, model):
         lp = model.localheader([x, img])
         ref = d[tag + "_local_point"]
         assert lp.shape == ref.shape
-        err = np.abs(lp.cpu().numpy() - ref).max()
-        assert err <= 1e-4 * max(1.0, np.abs(ref).max()), (tag, err)
+        tol.check("local_point", lp, ref, "KeypointDet.forward %s vs golden" % tag)
     # and it equals the fused PoSFeat.extract path on the same inputs
     img = torch.from_numpy(seeded_image(3, 96, 128))[None].to(gpu)
     full = model.extract(img)

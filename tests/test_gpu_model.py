@@ -7,13 +7,14 @@ import numpy as np
 import pytest
 import torch
 
+import tol
 from conftest import GOLDEN
 
 pytestmark = pytest.mark.gpu
 
-# fp32 tolerance of SURVEY §8c / north_star: 1e-4 (scaled by magnitude for
-# the unnormalised backbone maps, whose values reach O(10))
-RTOL, ATOL = 1e-4, 1e-4
+# SURVEY §8c / north_star: scores and global_feat within 1e-4 absolute; the
+# unnormalised backbone maps (values up to O(30)) within 1e-5 of their scale
+# (tests/tol.py, measured errors in DESIGN.md §3)
 
 
 @pytest.fixture(scope="module")
@@ -26,11 +27,9 @@ def engine():
     return ExtractionEngine(bb, hd, device="cuda")
 
 
-def _close(got, ref, name, rtol=RTOL, atol=ATOL):
-    got = got.detach().cpu().numpy() if torch.is_tensor(got) else got
-    scale = max(1.0, float(np.abs(ref).max()))
-    err = np.abs(got - ref).max()
-    assert err <= atol * scale + rtol * 0, "%s: max abs err %g (scale %g)" % (name, err, scale)
+def _close(got, ref, name):
+    """tests/tol.py's bound of the output ``name`` names (its first word)"""
+    tol.check(name.split()[0], got, ref, name)
 
 
 @pytest.mark.parametrize("tag,hw,seed", [("a", (96, 128), 0), ("b", (64, 96), 1)])

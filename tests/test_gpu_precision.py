@@ -14,6 +14,8 @@ import numpy as np
 import pytest
 import torch
 
+import tol
+
 pytestmark = pytest.mark.gpu
 
 
@@ -68,7 +70,7 @@ def test_bf6_winograd_gemm_and_model(gpu, precision):
     mode 1 vs mode 0 within the fp32 noise of the model (1e-5 of the map
     scale), and mode 1's error vs the torch-CPU oracle of the same order as
     mode 0's (both are fp32 rounding noise of different summation orders)
-    and within the 1e-4 parity bar."""
+    and within the parity bounds of tests/tol.py."""
     from oracle import model_ref
     from posfeat_amd.engine import ExtractionEngine
     from posfeat_amd.weights import seeded_image, seeded_state_dicts
@@ -88,4 +90,5 @@ def test_bf6_winograd_gemm_and_model(gpu, precision):
         e0 = float((res[0][k] - ref[k].double()).abs().max())
         e1 = float((res[1][k] - ref[k].double()).abs().max())
         assert d01 <= 1e-5 * s, (k, d01)
-        assert e1 <= 2 * e0 + 1e-6 * s and e1 <= 1e-4 * s, (k, e1, e0)
+        assert e1 <= 2 * e0 + 1e-6 * s, (k, e1, e0)
+        tol.check(k, res[1][k], ref[k], "bf16x6 model vs oracle")

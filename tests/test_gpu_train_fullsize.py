@@ -5,9 +5,9 @@ bit-identical results for a repeated step from the same state and draws
 (deterministic reductions, no atomics in the reductions that feed the
 gradient), the gradient is not trivially zero, and the fused keypoint step
 equals the autograd plug point (model.forward + DiskLoss + backward) on the
-same draws; and the descriptor step's gradients against a plain PyTorch fp32
-reference of the same step (r12p: worst tensor 3.6e-2 of its max, relative
-L2 2.3e-3 over all).
+same draws; and the descriptor step's gradients against the same step in
+fp64, per tensor within 3x the fp32 reference's own error (r12p against fp32:
+worst tensor 3.6e-2 of its max, relative L2 2.3e-3 over all).
 """
 import numpy as np
 import pytest
@@ -109,10 +109,13 @@ def test_desc_train_step_bs8_vs_torch_fp32(gpu):
     train-mode ResUNet (oracle/model_ref.py, torch ops) and desc loss
     (oracle/desc_train_ref.py) under torch autograd, sharing the HIP step's
     window centres and loss weights (arg-max near-ties, as the fixture test
-    does).  The loss within 2e-3; every backbone gradient tensor within 5e-2
-    of its max (the fixture case measures this network's own fp32 gradient
-    noise at up to ~3e-2 of the max, tests/test_bb_train.py), all of them
-    together within 5e-3 relative L2."""
+    does).  The loss within 2e-3 of the fp32 reference; every backbone
+    gradient tensor within max(3 x the fp32 reference's own error, 1e-2) of
+    the same backward run in fp64 (the bound of test_bb_train's fp64 fixture,
+    this 13-block train-mode network's fp32 gradients carrying up to ~3e-2
+    relative rounding noise of their own; a tensor's noise is one sample of
+    that error, so it counts as at least the median over the tensors), all of
+    them together within 5e-3 relative L2 of fp64."""
     from oracle.desc_train_ref import desc_loss_grad, loss_weights
     from oracle.model_ref import resunet_forward
     from posfeat_amd.training import (BackboneTrainer, DescriptorLossGrad, DESC_EPI_DEFAULTS,
@@ -155,21 +158,46 @@ def test_desc_train_step_bs8_vs_torch_fp32(gpu):
     np.testing.assert_allclose(float(out[0]), float(loss), rtol=2e-3)
     grads = torch.autograd.grad([x1, x2], [params[k] for k in keys],
                                 grad_outputs=[g1.to(gpu), g2.to(gpu)], allow_unused=True)
+    g32 = {k: (None if gr is None else gr.detach().double().cpu().numpy())
+           for k, gr in zip(keys, grads)}
+    del grads, x1, x2, params
+    torch.cuda.empty_cache()
+    # the same network backward in fp64 (torch's native double convs on the
+    # GPU), fed the same map gradients: the reference's own fp32 noise per
+    # tensor is |g32 - g64|, and the HIP step must sit within 3x that noise
+    # (floor 1e-2) of fp64 -- test_bb_train's fixture bound at this size
+    sd64 = {k: v.clone().to(gpu).double() for k, v in bb.items()}
+    p64 = {k: sd64[k].requires_grad_(True) for k in keys}
+    y1 = resunet_forward(sd64, im1.double(), train=True)["local_map"]
+    y2 = resunet_forward(sd64, im2.double(), train=True)["local_map"]
+    grads64 = torch.autograd.grad([y1, y2], [p64[k] for k in keys],
+                                  grad_outputs=[g1.to(gpu).double(), g2.to(gpu).double()],
+                                  allow_unused=True)
     num = den = 0.0
-    bad, errs = [], []
-    for k, gr in zip(keys, grads):
+    rows = []
+    for k, gr in zip(keys, grads64):
         if gr is None:   # not on local_map's path (conv_coarse): no gradient either way
-            assert not np.any(np.asarray(got[k])), k
+            assert g32[k] is None and not np.any(np.asarray(got[k])), k
             continue
-        ref = gr.detach().double().cpu().numpy()
+        ref = gr.detach().cpu().numpy()
         gk = np.asarray(got[k], np.float64).reshape(ref.shape)
-        e = np.abs(gk - ref).max() / max(np.abs(ref).max(), 1e-12)
-        errs.append((float(e), k))
-        if e > 5e-2:
-            bad.append((k, round(float(e), 5)))
+        mx = max(np.abs(ref).max(), 1e-30)
+        rows.append((float(np.abs(gk - ref).max() / mx), float(np.abs(g32[k] - ref).max() / mx), k))
         num += float(((gk - ref) ** 2).sum())
         den += float((ref ** 2).sum())
-    print("largest relative errors vs torch fp32:", [(k, "%.2e" % e) for e, k in sorted(errs)[-6:]],
+    # a tensor's noise is ONE sample of the fp32 rounding error and can come out
+    # small by chance: it is taken as at least the median over the tensors
+    med = float(np.median([n for _, n, _ in rows]))
+    bad, errs = [], []
+    for e, noise, k in rows:
+        tol_k = max(3.0 * max(noise, med), 1e-2)
+        errs.append((e, noise, k))
+        if e > tol_k:
+            bad.append((k, round(e, 5), round(tol_k, 5)))
+    print("largest relative errors vs fp64 (err, torch fp32 noise):",
+          [(k, "%.2e" % e, "%.2e" % n) for e, n, k in sorted(errs)[-8:]],
+          "median noise %.2e, largest err / max(noise, median): %.2f" % (
+              med, max(e / max(n, med) for e, n, _ in rows)),
           "rel L2 %.2e" % np.sqrt(num / den))
-    assert not bad, bad
+    assert not bad, "tensors over max(3 x fp32 noise, 1e-2) (key, err, tol): %s" % bad
     assert np.sqrt(num / den) <= 5e-3, np.sqrt(num / den)

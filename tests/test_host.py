@@ -220,6 +220,11 @@ class _FakeGroupLib:
         out._obj.value = 1000 + rank
         return 0
 
+    def posfeat_group_create_host(self, world, rank, fn, user, out):
+        self.host = (world, rank, fn)
+        out._obj.value = 2000 + rank
+        return 0
+
     def posfeat_group_destroy(self, h):
         pass
 
@@ -229,10 +234,10 @@ def _syncbn_worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from posfeat_amd.parallel import SyncBNGroup
     fake = _FakeGroupLib()
-    g = SyncBNGroup(lib=fake, shape=(4, 96, 128))
+    g = SyncBNGroup(lib=fake, shape=(4, 96, 128), transport="rccl")
     refused = False
     try:   # unequal per-rank batches are a real case (the counts are all-reduced)
-        SyncBNGroup(lib=_FakeGroupLib(), shape=(4 + rank, 96, 128)).close()
+        SyncBNGroup(lib=_FakeGroupLib(), shape=(4 + rank, 96, 128), transport="rccl").close()
     except ValueError:
         refused = True
     q.put((rank, fake.created, g.handle.value, refused))
@@ -260,6 +265,41 @@ def test_gloo_syncbn_group_bootstrap_world2():
         assert created == (2, rank, want)
         assert handle == 1000 + rank
         assert not refused
+
+
+def _syncbn_host_worker(rank, world, port, q):
+    import ctypes
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from posfeat_amd.parallel import SyncBNGroup
+    fake = _FakeGroupLib()
+    g = SyncBNGroup(lib=fake)            # a gloo group: the host transport
+    w, r, fn = fake.host
+    # the C side's call: n doubles in a host buffer, summed in place over ranks
+    buf = (ctypes.c_double * 5)(*[rank + 0.5 * i for i in range(5)])
+    rc = ctypes.cast(fn, SyncBNGroup._HostFn)(buf, 5, None)
+    q.put((rank, g.transport, w, r, g.handle.value, rc, list(buf)))
+    g.close()
+    dist.destroy_process_group()
+
+
+def test_gloo_syncbn_host_transport_world2():
+    """SyncBatchNorm over a gloo process group (parallel.SyncBNGroup host
+    transport, group.hip posfeat_group_create_host): the callback the C side
+    calls with a host copy of each statistics vector sums it over the ranks
+    in place (dist.all_reduce).  The GPU side runs in test_gpu_multirank.py."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29600 + os.getpid() % 1000
+    procs = [ctx.Process(target=_syncbn_host_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=300) for _ in procs), key=lambda r: r[0])
+    for p in procs:
+        p.join(60)
+    for rank, transport, w, r, handle, rc, buf in res:
+        assert (transport, w, r, handle, rc) == ("host", 2, rank, 2000 + rank, 0)
+        assert buf == [1.0 + i for i in range(5)]   # (0 + .5 i) + (1 + .5 i)
 
 
 def test_extract_plan_groups_matches_loader_bucketing():
