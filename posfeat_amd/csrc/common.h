@@ -47,9 +47,46 @@ static inline hipStream_t pf_stream(void *s) { return reinterpret_cast<hipStream
 
 static inline size_t pf_align(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// __syncthreads / __shfl / __shfl_xor (width 64) as always-inline code: the
+// HIP runtime's versions are plain inline functions, which a kernel built
+// without packed-fp32 ops (PF_NO_PK_FP32) does not inline -- they became
+// device-function calls there (tools/isa_check.py fails any s_swappc).  Same
+// instructions as the runtime's: fence + s_barrier + fence; ds_bpermute.
+__device__ __forceinline__ void pf_syncthreads() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+__device__ __forceinline__ int pf_lane() {
+  return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+template <class T>
+__device__ __forceinline__ T pf_bperm(T v, int addr) {
+  static_assert(sizeof(T) == 4 || sizeof(T) == 8, "4- or 8-byte lanes");
+  if constexpr (sizeof(T) == 4) {
+    return __builtin_bit_cast(T, __builtin_amdgcn_ds_bpermute(addr, __builtin_bit_cast(int, v)));
+  } else {
+    typedef int i2 __attribute__((ext_vector_type(2)));
+    i2 w = __builtin_bit_cast(i2, v);
+    w.x = __builtin_amdgcn_ds_bpermute(addr, w.x);
+    w.y = __builtin_amdgcn_ds_bpermute(addr, w.y);
+    return __builtin_bit_cast(T, w);
+  }
+}
+template <class T>
+__device__ __forceinline__ T pf_shfl_xor(T v, int mask, int width = 64) {
+  (void)width;  // whole waves only (every caller passes 64)
+  return pf_bperm(v, (pf_lane() ^ mask) << 2);
+}
+template <class T>
+__device__ __forceinline__ T pf_shfl(T v, int src, int width = 64) {
+  (void)width;
+  return pf_bperm(v, (src & 63) << 2);
+}
+
 __device__ __forceinline__ float pf_wave_sum(float v) {
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  for (int o = 32; o > 0; o >>= 1) v += pf_shfl_xor(v, o, 64);
   return v;
 }
 

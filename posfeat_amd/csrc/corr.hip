@@ -31,7 +31,7 @@ namespace {
 
 __device__ __forceinline__ double wave_sum_d(double v) {
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  for (int o = 32; o > 0; o >>= 1) v += pf_shfl_xor(v, o, 64);
   return v;
 }
 
@@ -89,7 +89,7 @@ __global__ void corr_row_kernel(const float* __restrict__ S, int nb, int n1, int
   float mx = -INFINITY;
   for (int k = lane; k < n2; k += 64) mx = fmaxf(mx, T * row[k]);
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, pf_shfl_xor(mx, o, 64));
   // fp64 accumulation of the softmax moments: var = E[n^2] - E[n]^2 cancels
   // catastrophically in fp32 when the softmax is peaked (small std); the
   // weights e and the coordinates stay the fp32 values the reference uses
@@ -163,7 +163,7 @@ __global__ __launch_bounds__(256) void corr_col_partial_kernel(
   }
   __shared__ ColAcc sh[4][64];
   sh[rg][cl] = a;
-  __syncthreads();
+  pf_syncthreads();
   if (rg == 0 && col < n2) {
     float M = sh[0][cl].mx;
     for (int r = 1; r < 4; ++r) M = fmaxf(M, sh[r][cl].mx);
@@ -375,7 +375,7 @@ __device__ __forceinline__ WinPatch window_patch_logits(const float* __restrict_
 #pragma unroll
     for (int k = 0; k < WP_K; ++k) {
 #pragma unroll
-      for (int o = 8; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o, 64);
+      for (int o = 8; o > 0; o >>= 1) v[k] += pf_shfl_xor(v[k], o, 64);
       const int pp = base + 4 * k + grp;
       if (cl == 0 && pp < np) pc[pp] = v[k];
     }
@@ -479,7 +479,7 @@ __global__ PF_NO_PK_FP32 void line_window_kernel(const float* __restrict__ cpx, 
     for (int u = 0; u < LU; ++u) {
       float v = d[u];
 #pragma unroll
-      for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      for (int o = 8; o > 0; o >>= 1) v += pf_shfl_xor(v, o, 64);
       const int s = s0 + grp + 4 * u;
       if (cl == 0 && s < line_step) slg[s] = v;
     }
@@ -490,7 +490,7 @@ __global__ PF_NO_PK_FP32 void line_window_kernel(const float* __restrict__ cpx, 
   lg[1] = lane + 64 < line_step ? slg[lane + 64] : -INFINITY;
   float mx = fmaxf(lg[0], lg[1]);
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, pf_shfl_xor(mx, o, 64));
   // use_nn: sum of the grid points whose prob equals the max
   float ox = 0.f, oy = 0.f;
 #pragma unroll
@@ -536,7 +536,7 @@ __global__ PF_NO_PK_FP32 void line_window_kernel(const float* __restrict__ cpx, 
 #pragma unroll
   for (int r = 0; r < MAX_WIN / 64; ++r) wm = fmaxf(wm, wl[r]);
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) wm = fmaxf(wm, __shfl_xor(wm, o, 64));
+  for (int o = 32; o > 0; o >>= 1) wm = fmaxf(wm, pf_shfl_xor(wm, o, 64));
   // softmax moments over the window in fp64 (get_expected_correspondence_
   // within_window, preprocess_utils.py:745-750): the fp32 E[g^2] - E[g]^2 of
   // the reference loses most of its digits when the window softmax is peaked;
@@ -631,10 +631,10 @@ __global__ __launch_bounds__(1024) PF_NO_PK_FP32 void epipolar_loss_kernel(
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       double r = acc[k][j];
-      for (int o = 32; o > 0; o >>= 1) r += __shfl_xor(r, o, 64);
+      for (int o = 32; o > 0; o >>= 1) r += pf_shfl_xor(r, o, 64);
       if ((tid & 63) == 0) red[tid >> 6][k * 4 + j] = r;
     }
-  __syncthreads();
+  pf_syncthreads();
   double lsum[4], msum[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -699,14 +699,14 @@ __global__ __launch_bounds__(1024) PF_NO_PK_FP32 void epi_loss_bwd_kernel(
     b1 += ((cost < short_edge * wthr) & vf) ? inv : 0.0;  // branch-free (as the forward)
   }
   for (int o = 32; o > 0; o >>= 1) {
-    a1 += __shfl_xor(a1, o, 64);
-    b1 += __shfl_xor(b1, o, 64);
+    a1 += pf_shfl_xor(a1, o, 64);
+    b1 += pf_shfl_xor(b1, o, 64);
   }
   if ((tid & 63) == 0) {
     red[tid >> 6][0] = a1;
     red[tid >> 6][1] = b1;
   }
-  __syncthreads();
+  pf_syncthreads();
   double sa = 0.0, sb = 0.0;
   for (int wv = 0; wv < (int)(blockDim.x >> 6); ++wv) {
     sa += red[wv][0];
@@ -779,7 +779,7 @@ __global__ PF_NO_PK_FP32 void window_bwd_kernel(const float* __restrict__ f1, co
 #pragma unroll
   for (int r = 0; r < MAX_WIN / 64; ++r) wm = fmaxf(wm, wl[r]);
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) wm = fmaxf(wm, __shfl_xor(wm, o, 64));
+  for (int o = 32; o > 0; o >>= 1) wm = fmaxf(wm, pf_shfl_xor(wm, o, 64));
   float se = 0.f;
   float pr[MAX_WIN / 64], dp[MAX_WIN / 64];
 #pragma unroll
@@ -812,7 +812,7 @@ __global__ PF_NO_PK_FP32 void window_bwd_kernel(const float* __restrict__ f1, co
     float dsv = 0.f;
 #pragma unroll
     for (int r = 0; r < MAX_WIN / 64; ++r)
-      if ((s >> 6) == r) dsv = __shfl(ds[r], s & 63, 64);
+      if ((s >> 6) == r) dsv = pf_shfl(ds[r], s & 63, 64);
     const int iy = s / win_w, ix = s - iy * win_w;
     const float gx = jx + linspace_f(-window_size, window_size, win_w, ix);
     const float gy = jy + linspace_f(-window_size, window_size, win_h, iy);
@@ -909,7 +909,7 @@ __global__ __launch_bounds__(256) void window_bwd_patch_kernel(
 #pragma unroll
   for (int r = 0; r < MAX_WIN / 64; ++r) wm = fmaxf(wm, wl[r]);
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) wm = fmaxf(wm, __shfl_xor(wm, o, 64));
+  for (int o = 32; o > 0; o >>= 1) wm = fmaxf(wm, pf_shfl_xor(wm, o, 64));
   float pr[MAX_WIN / 64], dp[MAX_WIN / 64];
   float se = 0.f;
 #pragma unroll
@@ -991,14 +991,14 @@ __global__ __launch_bounds__(256) void window_bwd_patch_kernel(
   }
 #pragma unroll
   for (int o = 16; o < 64; o <<= 1) {
-    da.x += __shfl_xor(da.x, o, 64);
-    da.y += __shfl_xor(da.y, o, 64);
-    da.z += __shfl_xor(da.z, o, 64);
-    da.w += __shfl_xor(da.w, o, 64);
-    db.x += __shfl_xor(db.x, o, 64);
-    db.y += __shfl_xor(db.y, o, 64);
-    db.z += __shfl_xor(db.z, o, 64);
-    db.w += __shfl_xor(db.w, o, 64);
+    da.x += pf_shfl_xor(da.x, o, 64);
+    da.y += pf_shfl_xor(da.y, o, 64);
+    da.z += pf_shfl_xor(da.z, o, 64);
+    da.w += pf_shfl_xor(da.w, o, 64);
+    db.x += pf_shfl_xor(db.x, o, 64);
+    db.y += pf_shfl_xor(db.y, o, 64);
+    db.z += pf_shfl_xor(db.z, o, 64);
+    db.w += pf_shfl_xor(db.w, o, 64);
   }
   if (grp == 0) {
     *reinterpret_cast<f32x4*>(dq + wid * 128 + cl * 8) = da;
@@ -1034,16 +1034,16 @@ __global__ __launch_bounds__(256) void window_gather_kernel(
       f = r.z > 0 && r.x < tx0 + WG_T && r.x + r.z > tx0 && r.y < ty0 + WG_T && r.y + r.w > ty0;
     }
     s_cnt[t] = f;
-    __syncthreads();
+    pf_syncthreads();
     for (int d = 1; d < 256; d <<= 1) {
       const int v = t >= d ? s_cnt[t - d] : 0;
-      __syncthreads();
+      pf_syncthreads();
       s_cnt[t] += v;
-      __syncthreads();
+      pf_syncthreads();
     }
     if (f) s_list[total + s_cnt[t] - 1] = i;
     total += s_cnt[255];
-    __syncthreads();
+    pf_syncthreads();
   }
   const int row = t >> 5, cq = t & 31;
   f32x4 acc[WG_T];
@@ -1067,13 +1067,13 @@ __global__ __launch_bounds__(256) void window_gather_kernel(
                        ? cb[(long long)i * rec_stride + py * r.z + px]
                        : 0.f;
     }
-    __syncthreads();
+    pf_syncthreads();
     for (int k = 0; k < m; ++k) {
       const f32x4 qv = *reinterpret_cast<const f32x4*>(&s_q[k][cq * 4]);
 #pragma unroll
       for (int j = 0; j < WG_T; ++j) acc[j] += s_c[k][row * WG_T + j] * qv;
     }
-    __syncthreads();
+    pf_syncthreads();
   }
   const int py = ty0 + row;
   if (py >= h2) return;

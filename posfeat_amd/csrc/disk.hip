@@ -66,7 +66,7 @@ __global__ PF_NO_PK_FP32 void disk_point_kernel(const float* __restrict__ kp, in
   const float v = kp[((long long)b * H + cy * G + lane / G) * W + cx * G + lane % G];
   float mx = v;
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, pf_shfl_xor(mx, o, 64));
   const float lse = mx + logf(pf_wave_sum(expf(v - mx)));
   int p;
   bool a;
@@ -76,21 +76,21 @@ __global__ PF_NO_PK_FP32 void disk_point_kernel(const float* __restrict__ kp, in
     int arg = lane;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
-      const float ok = __shfl_xor(key, o, 64);
-      const int oa = __shfl_xor(arg, o, 64);
+      const float ok = pf_shfl_xor(key, o, 64);
+      const int oa = pf_shfl_xor(arg, o, 64);
       if (ok > key || (ok == key && oa < arg)) {
         key = ok;
         arg = oa;
       }
     }
     p = arg;
-    const float lp = __shfl(v, p, 64);
+    const float lp = pf_shfl(v, p, 64);
     a = uni[wid * 65 + 64] < 1.f / (1.f + expf(-lp));
   } else {
     p = prop_in[wid];
     a = acc_in[wid] != 0;
   }
-  const float lv = __shfl(v, p, 64);
+  const float lv = pf_shfl(v, p, 64);
   if (lane == 0) {
     prop_out[wid] = p;
     acc_out[wid] = a ? 1 : 0;
@@ -114,7 +114,7 @@ __global__ void row_lse_kernel(const float* __restrict__ S, long long rows, int 
   float mx = -INFINITY;
   for (int k = lane; k < n2; k += 64) mx = fmaxf(mx, T * r[k] - T);
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, pf_shfl_xor(mx, o, 64));
   float s = 0.f;
   for (int k = lane; k < n2; k += 64) s += expf((T * r[k] - T) - mx);
   s = pf_wave_sum(s);
@@ -148,7 +148,7 @@ __global__ __launch_bounds__(256) void col_lse_partial_kernel(const float* __res
   __shared__ float smx[4][64], ssm[4][64];
   smx[rg][threadIdx.x & 63] = mx;
   ssm[rg][threadIdx.x & 63] = sm;
-  __syncthreads();
+  pf_syncthreads();
   if (rg == 0 && col < n2) {
     float M = smx[0][threadIdx.x];
     for (int r = 1; r < 4; ++r) M = fmaxf(M, smx[r][threadIdx.x]);
@@ -230,10 +230,10 @@ __global__ __launch_bounds__(RB) void reinforce_kernel(
   // fixed-order block reduction
   __shared__ double red[RB];
   red[threadIdx.x] = acc;
-  __syncthreads();
+  pf_syncthreads();
   for (int o = RB / 2; o > 0; o >>= 1) {
     if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-    __syncthreads();
+    pf_syncthreads();
   }
   if (threadIdx.x == 0) part[(long long)b * gridDim.x + blockIdx.x] = red[0];
 }
@@ -297,7 +297,7 @@ __global__ __launch_bounds__(256) void grad_col_partial_kernel(PairCtx c,
       if (acc1[(long long)b * c.n1 + m]) s += pair_rp(c, b, m, col);
   __shared__ float ss[4][64];
   ss[rg][threadIdx.x & 63] = s;
-  __syncthreads();
+  pf_syncthreads();
   if (rg == 0 && col < c.n2)
     part[((long long)b * COL_CH + ch) * c.n2 + col] =
         ((ss[0][threadIdx.x] + ss[1][threadIdx.x]) + ss[2][threadIdx.x]) + ss[3][threadIdx.x];
@@ -331,11 +331,11 @@ __global__ void disk_point_grad_kernel(const float* __restrict__ kp, int nb, int
   const float v = kp[pix];
   float mx = v;
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, pf_shfl_xor(mx, o, 64));
   const float e = expf(v - mx);
   const float sm = e / pf_wave_sum(e);
   const int p = prop[wid];
-  const float lv = __shfl(v, p, 64);
+  const float lv = pf_shfl(v, p, 64);
   const float sg = 1.f / (1.f + expf(-lv));
   const float dacc = acc[wid] ? 1.f - sg : -sg;
   const float gg = g[wid];
@@ -370,14 +370,14 @@ __global__ __launch_bounds__(1024) void disk_final_kernel(const double* __restri
   r1[threadIdx.x] = s;
   r2[threadIdx.x] = lp;
   r3[threadIdx.x] = nk;
-  __syncthreads();
+  pf_syncthreads();
   for (int o = 512; o > 0; o >>= 1) {
     if ((int)threadIdx.x < o) {
       r1[threadIdx.x] += r1[threadIdx.x + o];
       r2[threadIdx.x] += r2[threadIdx.x + o];
       r3[threadIdx.x] += r3[threadIdx.x + o];
     }
-    __syncthreads();
+    pf_syncthreads();
   }
   if (threadIdx.x == 0) {
     const double reinforce = r1[0], pen = (double)kp_penalty * r2[0];
@@ -478,7 +478,7 @@ __global__ __launch_bounds__(256) void disk_flash_kernel(FlashArgs a, int want_r
   double rs = 0.0;                       // SUM: sum reward p (logp terms)
   if (nsteps > 0) issue(0, 0);
   __builtin_amdgcn_s_waitcnt(0);
-  __syncthreads();
+  pf_syncthreads();
   for (int s = 0; s < nsteps; ++s) {
     const int cur = s & 1;
     if (s + 1 < nsteps) issue(s + 1, cur ^ 1);
@@ -541,20 +541,20 @@ __global__ __launch_bounds__(256) void disk_flash_kernel(FlashArgs a, int want_r
       }
     }
     __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
+    pf_syncthreads();
   }
   // merge the two lane halves (interleaved row sets) in a fixed order
   const long long o = ((long long)b * gridDim.y + split) * a.n + cl;
   if (!SUM) {
-    const float om = __shfl_xor(run_m, 32, 64), os = __shfl_xor(run_s, 32, 64);
+    const float om = pf_shfl_xor(run_m, 32, 64), os = pf_shfl_xor(run_s, 32, 64);
     if (h == 0 && cok) {
       const float M = fmaxf(run_m, om);
       const float t = (M == -INFINITY) ? 0.f : run_s * expf(run_m - M) + os * expf(om - M);
       a.lse_part[o] = make_float2(M, t);
     }
   } else {
-    const float og = __shfl_xor(gs, 32, 64);
-    const double orr = __shfl_xor(rs, 32, 64);
+    const float og = pf_shfl_xor(gs, 32, 64);
+    const double orr = pf_shfl_xor(rs, 32, 64);
     if (h == 0 && cok) {
       a.g_part[o] = gs + og;
       if (want_r) a.r_part[o] = rs + orr;
@@ -853,7 +853,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void d
   // partial's max back in natural units
   const long long o = ((long long)b * gridDim.y + split) * a.n + cl;
   if (!SUM) {
-    const float om = __shfl_xor(run_m, 32, 64), os = __shfl_xor(run_s, 32, 64);
+    const float om = pf_shfl_xor(run_m, 32, 64), os = pf_shfl_xor(run_s, 32, 64);
     if (h == 0 && cok) {
       const float M = fmaxf(run_m, om);
       const float t = (M == -INFINITY) ? 0.f
@@ -862,8 +862,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void d
       a.lse_part[o] = make_float2(M * 0.6931471805599453f, t);
     }
   } else {
-    const float og = __shfl_xor(gs, 32, 64);
-    const double orr = __shfl_xor(rs, 32, 64);
+    const float og = pf_shfl_xor(gs, 32, 64);
+    const double orr = pf_shfl_xor(rs, 32, 64);
     if (h == 0 && cok) {
       a.g_part[o] = gs + og;
       if (WR) a.r_part[o] = rs + orr;
@@ -942,12 +942,12 @@ __global__ __launch_bounds__(1024) void flash_compact_kernel(const uint8_t* __re
   int c = 0;
   for (int i = i0; i < i1; ++i) c += ab[i] ? 1 : 0;
   off[t] = c;
-  __syncthreads();
+  pf_syncthreads();
   for (int d = 1; d < 1024; d <<= 1) {
     const int v = t >= d ? off[t - d] : 0;
-    __syncthreads();
+    pf_syncthreads();
     off[t] += v;
-    __syncthreads();
+    pf_syncthreads();
   }
   int o = off[t] - c;
   for (int i = i0; i < i1; ++i)

@@ -82,7 +82,7 @@ __global__ void nhwc_to_nchw_kernel(const float* __restrict__ x, int c, int hw, 
     const int p = p0 + r, ch = c0 + tx;
     t[r][tx] = (p < hw && ch < c) ? x[((long long)b * hw + p) * csi + ch] : 0.f;
   }
-  __syncthreads();
+  pf_syncthreads();
   for (int r = ty; r < 64; r += 4) {
     const int ch = c0 + r, p = p0 + tx;
     if (ch < c && p < hw) y[((long long)b * c + ch) * hw + p] = t[tx][r];
@@ -108,7 +108,7 @@ __global__ void nhwc_to_nchw64_kernel(const float* __restrict__ x, int c, int hw
     t[r][4 * q + 2] = v.z;
     t[r][4 * q + 3] = v.w;
   }
-  __syncthreads();
+  pf_syncthreads();
 #pragma unroll
   for (int it = 0; it < 4; ++it) {  // 64 channels x 16 pixel quads
     const int e = it * 256 + tid, ch = e >> 4, q = e & 15;
@@ -207,7 +207,7 @@ __global__ void in_partial_kernel(const float* __restrict__ x, int hw, int C, in
   red[tid * 8 + 5] = s2.y;
   red[tid * 8 + 6] = s2.z;
   red[tid * 8 + 7] = s2.w;
-  __syncthreads();
+  pf_syncthreads();
   if (tid < c4n) {
     double a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int r = 0; r < rows; ++r)
@@ -239,13 +239,13 @@ __global__ __launch_bounds__(256) void in_finalize_kernel(
     }
   red[0][kl][cl] = s1;
   red[1][kl][cl] = s2;
-  __syncthreads();
+  pf_syncthreads();
   for (int o = 32; o > 0; o >>= 1) {
     if (kl < o) {
       red[0][kl][cl] += red[0][kl + o][cl];
       red[1][kl][cl] += red[1][kl + o][cl];
     }
-    __syncthreads();
+    pf_syncthreads();
   }
   if (kl != 0 || c >= C) return;
   s1 = red[0][0][cl];
@@ -275,13 +275,13 @@ __global__ void in1_partial_kernel(const float* __restrict__ x, int hw, int chun
   __shared__ double r1[256], r2[256];
   r1[threadIdx.x] = s1;
   r2[threadIdx.x] = s2;
-  __syncthreads();
+  pf_syncthreads();
   for (int o = 128; o > 0; o >>= 1) {
     if ((int)threadIdx.x < o) {
       r1[threadIdx.x] += r1[threadIdx.x + o];
       r2[threadIdx.x] += r2[threadIdx.x + o];
     }
-    __syncthreads();
+    pf_syncthreads();
   }
   if (threadIdx.x == 0) {
     part[((long long)b * nchunk + chunk) * 2] = r1[0];
@@ -415,7 +415,7 @@ __global__ void head_tail_conv3_kernel(const float* __restrict__ x, int n, int h
 #pragma unroll
     for (int u = 0; u < HT_U; ++u) {
 #pragma unroll
-      for (int o = 16; o > 0; o >>= 1) s[u] += __shfl_xor(s[u], o, 64);
+      for (int o = 16; o > 0; o >>= 1) s[u] += pf_shfl_xor(s[u], o, 64);
       const long long p = 2 * (q + u) + half;
       if (l32 == 0 && q + u < q1 && p < total) y[p] = s[u] + bias;
     }
@@ -485,7 +485,7 @@ __global__ void global_feat_kernel(const float* __restrict__ g, int hw, int cs,
   __shared__ float red[16][128];
   red[wv][lane] = a0;
   red[wv][lane + 64] = a1;
-  __syncthreads();
+  pf_syncthreads();
   if (threadIdx.x < 128) {
     float s = 0.f;
     for (int k = 0; k < nw; ++k) s += red[k][threadIdx.x];

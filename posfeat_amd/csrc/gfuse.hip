@@ -138,7 +138,7 @@ __global__ __launch_bounds__(2 * GF_COUT) PF_NO_PK_FP32 void gfuse_ring_kernel(
 #pragma unroll
   for (int j = 0; j < HP; ++j) acc[j] = bias;
   for (int t = 0; t < 9; ++t) {
-    __syncthreads();  // pys / w1s written; the previous tap's g and xs read
+    pf_syncthreads();  // pys / w1s written; the previous tap's g and xs read
     if (!c) {  // zero-padded image taps around q (0 outside the image)
       for (int i = threadIdx.x; i < GF_RP * 27; i += blockDim.x) {
         const int jj = i / 27, e = i - jj * 27;
@@ -150,7 +150,7 @@ __global__ __launch_bounds__(2 * GF_COUT) PF_NO_PK_FP32 void gfuse_ring_kernel(
           v = img4[(((size_t)b * H + iy) * W + ix) * 4 + ch];
         xs[jj][e] = v;
       }
-      __syncthreads();
+      pf_syncthreads();
     }
     for (int i = threadIdx.x; i < GF_RP * GF_CG; i += blockDim.x) {
       const int jj = i / GF_CG, k = i - jj * GF_CG;
@@ -173,7 +173,7 @@ __global__ __launch_bounds__(2 * GF_COUT) PF_NO_PK_FP32 void gfuse_ring_kernel(
       }
       g[jj][k] = v;
     }
-    __syncthreads();
+    pf_syncthreads();
     // four k per step: one broadcast ds_read_b128 of g per pixel, the same
     // sequential accumulation order as one k at a time
     for (int k = 0; k < GF_CG; k += 4) {
@@ -237,7 +237,7 @@ __global__ __launch_bounds__(256) void gfuse_imgmom_kernel(const float* __restri
   for (int r = 0; r < 16; ++r) tot[r] = 0.0;
   for (int band = blockIdx.x; band < nband; band += gridDim.x) {
   const int r0 = band * IM_ROWS;
-  __syncthreads();  // the previous band's tile is consumed
+  pf_syncthreads();  // the previous band's tile is consumed
   for (int i = threadIdx.x; i < (IM_ROWS + 2) * TW; i += blockDim.x) {
     const int ty = i / TW, tx = i - ty * TW;
     const int y = r0 - 1 + ty, x = tx - 1;
@@ -248,7 +248,7 @@ __global__ __launch_bounds__(256) void gfuse_imgmom_kernel(const float* __restri
     tile[i * 3 + 1] = v.y;
     tile[i * 3 + 2] = v.z;
   }
-  __syncthreads();
+  pf_syncthreads();
   // this lane's moment index i = lane % 32: tap (ky, kx), channel c, or 27: 1
   const int i = lane & 31;
   const int ti = i / 3, ci = i - ti * 3;
@@ -281,14 +281,14 @@ __global__ __launch_bounds__(256) void gfuse_imgmom_kernel(const float* __restri
 #pragma unroll
   for (int r = 0; r < 16; ++r) tot[r] += (double)acc0[r] + (double)acc1[r];
   }
-  __syncthreads();  // the tile is dead: reuse LDS for the wave sum
+  pf_syncthreads();  // the tile is dead: reuse LDS for the wave sum
   double* red = reinterpret_cast<double*>(tile);  // [4 waves][32][32]
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int gi = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5), gj = lane & 31;
     red[(wave * IM_G + gi) * IM_G + gj] = tot[r];
   }
-  __syncthreads();
+  pf_syncthreads();
   for (int e = threadIdx.x; e < IM_G * IM_G; e += blockDim.x)
     part[((long long)b * gridDim.x + blockIdx.x) * IM_G * IM_G + e] =
         (red[e] + red[IM_G * IM_G + e]) + (red[2 * IM_G * IM_G + e] + red[3 * IM_G * IM_G + e]);
@@ -321,7 +321,7 @@ __global__ __launch_bounds__(1024) void gfuse_imgstats_kernel(const double* __re
     G[e] = ((s0 + s1) + (s2 + s3)) / HW;  // E[x_i x_j], row 27: E[x_j]
     if (gram) gram[(long long)b * IM_G * IM_G + e] = G[e];  // kept for the training backward
   }
-  __syncthreads();
+  pf_syncthreads();
   const int k = threadIdx.x;
   if (k >= GF_CG) return;
   double w[IM_TAPS];
@@ -378,7 +378,7 @@ __global__ __launch_bounds__(256) void gfuse_conv5_kernel(const float* __restric
       v = *reinterpret_cast<const f32x4*>(ib + ((long long)yy * W + xx) * 4);
     *reinterpret_cast<f32x4*>(sp + i * 4) = v;
   }
-  __syncthreads();
+  pf_syncthreads();
   f32x16 acc[2][4];
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
@@ -463,7 +463,7 @@ __global__ __launch_bounds__(256) void gfuse_conv5_bf6_kernel(const float* __res
       v = *reinterpret_cast<const f32x4*>(ib + ((long long)yy * W + xx) * 4);
     *reinterpret_cast<f32x4*>(sp + i * 4) = v;
   }
-  __syncthreads();
+  pf_syncthreads();
   f32x16 acc[2][4];
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
@@ -608,9 +608,9 @@ __global__ __launch_bounds__(512) void gfuse_conv5_k80_kernel(const float* __res
   int t = blockIdx.x;
   if (t < ntiles) load_patch(t, pv);
   for (; t < ntiles; t += gridDim.x) {
-    __syncthreads();  // the previous tile's patch is consumed
+    pf_syncthreads();  // the previous tile's patch is consumed
     store_patch(pv);
-    __syncthreads();
+    pf_syncthreads();
     if (t + (int)gridDim.x < ntiles) load_patch(t + gridDim.x, pv);  // in flight during the MFMAs
     f32x16 acc[4][2];
 #pragma unroll

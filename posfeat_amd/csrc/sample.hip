@@ -109,7 +109,7 @@ __global__ PF_NO_PK_FP32 void sample_desc128_kernel(const float* __restrict__ fm
   if (normalize) {
     float ss = acc.x * acc.x + acc.y * acc.y + acc.z * acc.z + acc.w * acc.w;
 #pragma unroll
-    for (int off = 16; off > 0; off >>= 1) ss += __shfl_xor(ss, off, 64);
+    for (int off = 16; off > 0; off >>= 1) ss += pf_shfl_xor(ss, off, 64);
     inv = 1.f / fmaxf(sqrtf(ss), 1e-12f);
   }
   *reinterpret_cast<f32x4*>(o) = valid ? (normalize ? acc * inv : acc) : f32x4{0.f, 0.f, 0.f, 0.f};

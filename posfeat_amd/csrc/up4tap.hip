@@ -137,9 +137,9 @@ __global__ __launch_bounds__(256) PF_NO_PK_FP32 void up4tap_combine_kernel(const
     colb[kx] = min(max(min(qx + lo + 1, w - 1), 0) - (qx0 - 1), CB_CX - 1);
   }
   __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA has landed (y too)
-  __syncthreads();                 // ... and every other wave's
+  pf_syncthreads();                 // ... and every other wave's
   // ---- phase 2 --------------------------------------------------------------
-  auto rowR = [&](int ry, f32x4 (&R)[3]) {  // ry: tile row (iy = q0 - 1 + ry)
+  auto rowR = [&](int ry, f32x4 (&R)[3]) __attribute__((always_inline)) {  // ry: tile row (iy = q0 - 1 + ry)
 #pragma unroll
     for (int ky = 0; ky < 3; ++ky) {
       f32x4 s = {0.f, 0.f, 0.f, 0.f};
@@ -193,14 +193,14 @@ __global__ __launch_bounds__(256) PF_NO_PK_FP32 void up4tap_combine_kernel(const
   }
   if (!part) return;
   // ---- statistics: reduce the 32 columns of each channel (fixed order) -------
-  __syncthreads();  // LDS reuse
+  pf_syncthreads();  // LDS reuse
   double* red = reinterpret_cast<double*>(sp);  // [32 columns][32 channels][2]
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     red[(xl * CB_CG + c4 * 4 + j) * 2] = s1[j];
     red[(xl * CB_CG + c4 * 4 + j) * 2 + 1] = s2[j];
   }
-  __syncthreads();
+  pf_syncthreads();
   if (tid < 2 * CB_CG) {
     const int c = tid >> 1, which = tid & 1;
     double a = 0.0;

@@ -555,7 +555,7 @@ __global__ __launch_bounds__(256) void up4_wino_output_kernel(const float* __res
         red[pl][cq][j] = s1[j];
         red[pl][cq][4 + j] = s2[j];
       }
-      __syncthreads();
+      pf_syncthreads();
       if (pl == 0) {
         double a[8];
 #pragma unroll

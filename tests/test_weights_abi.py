@@ -6,6 +6,7 @@ import os
 import re
 
 import numpy as np
+import pytest
 import torch
 import torch.nn.functional as F
 
@@ -134,14 +135,24 @@ def test_engine_layer_table_matches_state_dicts():
     assert np.isfinite(blob).all()
 
 
-def test_isa_bf6d_vmem_order():
-    """conv_bf6d_kernel's counted waits (vmcnt(4) / vmcnt(4 D)) hold only if
-    each step's B-plane DMA is issued before its four A register loads and no
-    vmcnt(0) drain sits between them: checked on the built library's gfx950
-    ISA (tools/isa_check.py; the order is pinned in the source by
-    sched barriers, this catches a compiler that reorders anyway)."""
+@pytest.mark.parametrize("lib", ["libposfeat_hip.so", "libposfeat_hip_ab.so"])
+def test_isa_hazard_guard(lib):
+    """tools/isa_check.py on the built gfx950 ISA of the shipped library and
+    of the A/B build: conv_bf6d_kernel's counted waits (each step's B-plane DMA
+    issued before its four A register loads, no vmcnt(0) drain between them);
+    no MFMA reading a v_cvt_pk_bf16_f32 result without wait states; no
+    in-place cross-half packed-fp32 op; no s_barrier crossed with the wave's
+    own LDS accesses outstanding; no device-function call in a kernel.  Every
+    one of these fails (none is only reported)."""
     import subprocess
     import sys
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "isa_check.py")],
+    path = os.path.join(ROOT, "posfeat_amd", lib)
+    if not os.path.exists(path):
+        pytest.skip("%s not built" % lib)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "isa_check.py"), "--lib", path],
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+    for line in ("in-place cross-half packed-fp32 ops: 0 in 0 kernels",
+                 "s_barrier with LDS accesses outstanding: 0 in []",
+                 "device-function calls (s_swappc): 0"):
+        assert line in r.stdout, r.stdout[-2000:]

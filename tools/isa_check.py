@@ -24,18 +24,19 @@ waits rely on but the source cannot pin by itself:
   extra s_waitcnt lgkmcnt(0) before its barriers, 0 of 19 for the scalar form
   (profiles/round5/gcombine_pk_probe_r13a.txt).  The compiler
   pads nothing for it, so no shipped kernel may contain it.  The same in-place
-  low<-high read on v_pk_add_f32 / v_pk_mov_b32 (ocml's log1pf, 64-bit pair
-  copies) is reported, with run-to-run bit-identity tests over the kernels
-  that hold it (tests/test_gpu_repeat.py).
-* reported: s_barriers crossed with an LDS load or store of the wave still
-  outstanding (straight-line scan; the state resets at an unconditional
-  branch).  Round 4's advice suspected this in up4tap_gcombine_kernel; its
-  ISA has none, in the failing build and the shipped one, and an explicit
-  lgkmcnt(0) there did not change the failure (above).  The remaining
-  instances are the bf6d / bf6s K loops, whose last B-fragment reads of stage
-  s cross the barrier after which B(c + 2) is DMA'd into stage s: the
-  reads were issued before the barrier and the LDS serves a wave's requests
-  in order, while the DMA's write arrives a global-memory latency later.
+  low<-high read on v_pk_add_f32 / v_pk_mul_f32 / v_pk_mov_b32 (ocml's
+  log1pf, 64-bit pair copies), and every other in-place cross-half read
+  (op_sel_hi selecting the low dword for the high result), fail too (round
+  6): the kernels that held them are built without packed-fp32 ops
+  (PF_NO_PK_FP32 in common.h).
+* every kernel: no s_barrier crossed with an LDS load or store of the wave
+  still outstanding (straight-line scan; the state resets at an
+  unconditional branch).  The bf6d / bf6s K loops held ten, whose safety
+  rested on timing (the DMA refilling the stage after the barrier lands a
+  global-memory latency after the wave's last fragment reads); they wait
+  lgkmcnt(0) with their counted vmcnt now.
+* every kernel: no device-function call (s_swappc): a kernel built without
+  packed-fp32 ops does not inline a callee built with them.
 
 usage: python tools/isa_check.py [--dump KERNEL_SUBSTRING] [--lib PATH]
 Exit status 1 on a violated property.  tests/test_weights_abi.py runs it.
@@ -312,15 +313,18 @@ def main():
         nh += len(e)
         errs += e
     print("cvt_pk_bf16 -> MFMA operand hazards: %d" % nh)
-    # reported, not failed: tools/probe/pk_hazard.hip could not reproduce a
-    # wrong result from the pattern in isolation (30 variants, with and without
-    # co-executing MFMAs), so it is a suspect of DESIGN.md 4.1q, not a proven
-    # hazard; the kernel where it coincided with run-to-run differences
-    # (up4tap_gcombine_kernel's y interpolation) runs scalar FMAs instead
+    # every in-place cross-half packed op FAILS: the low<-high
+    # v_pk_fma_f32 form gave run-to-run different results,
+    # and the other forms (v_pk_add/mul/mov, and op_sel_hi reading the low
+    # dword for the high result) are the same in-place cross-half read; the
+    # kernels the compiler emitted them in are built without packed-fp32 ops
+    # (PF_NO_PK_FP32, common.h)
     npk = collections.Counter()
     for k, v in funcs.items():
-        npk[k] = len(check_pk_inplace_swap(k, v))
-    print("in-place cross-half packed-fp32 ops (reported): %d in %d kernels" % (
+        e = check_pk_inplace_swap(k, v)
+        npk[k] = len(e)
+        errs += e
+    print("in-place cross-half packed-fp32 ops: %d in %d kernels" % (
         sum(npk.values()), sum(1 for v in npk.values() if v)))
     nfma, nother = 0, collections.Counter()
     for k, v in funcs.items():
@@ -330,16 +334,33 @@ def main():
                  % (k, b[:90]) for b in bad]
         for b in pk_inplace_lo_from_hi(v, ("v_pk_add_f32", "v_pk_mul_f32", "v_pk_mov_b32")):
             nother[k] += 1
+            errs.append("%s: packed op low result reads the high dword of its own destination: %s"
+                        % (k, b[:90]))
     print("in-place low<-high v_pk_fma_f32: %d" % nfma)
-    print("in-place low<-high v_pk_add/mul/mov (reported; tests/test_gpu_repeat.py): %d in %s" % (
+    print("in-place low<-high v_pk_add/mul/mov: %d in %s" % (
         sum(nother.values()), sorted(set(re.sub(r"^_ZN12_GLOBAL__N_1\d+", "", k).split("E")[0]
                                          for k in nother))))
+    # an s_barrier crossed with the wave's own LDS accesses outstanding FAILS:
+    # the ordering must not rest on the LDS answering before another wave's
+    # DMA lands (the bf6d / bf6s K loops wait lgkmcnt(0) with their vmcnt)
     nb = collections.Counter()
     for k, v in funcs.items():
-        nb[k] = len(check_lds_barrier(k, v))
-    print("s_barrier with LDS accesses outstanding (reported): %d in %s" % (
+        e = check_lds_barrier(k, v)
+        nb[k] = len(e)
+        errs += e
+    print("s_barrier with LDS accesses outstanding: %d in %s" % (
         sum(nb.values()), sorted(set(re.sub(r"^_ZN12_GLOBAL__N_1\d+", "", k).split("I")[0]
                                      for k in nb if nb[k]))))
+    # no kernel calls a device function: a kernel built without packed-fp32
+    # ops cannot inline a callee built with them, and the call would carry
+    # the callee's own packed code (and a call's cost) into the kernel
+    ncall = 0
+    for k, v in funcs.items():
+        calls = [ln for ln in v if ln.split("//")[0].strip().startswith("s_swappc")]
+        if calls:
+            ncall += len(calls)
+            errs.append("%s: %d device-function call(s) (s_swappc)" % (k, len(calls)))
+    print("device-function calls (s_swappc): %d" % ncall)
     for e in errs:
         print("ISA CHECK FAILED:", e)
     return 1 if errs else 0
