@@ -687,6 +687,17 @@ bool gfuse_k80_on() {
 
 size_t pf_gfuse_wplanes_bytes(int n) { return (size_t)n * 3 * GF_COUT * G8_K * 2; }
 
+// A/B timing ablation of the image branch (POSFEAT_SIDE_ABL, A/B build only;
+// wrong results): bit 1 skips the border-ring kernel, 2 the image-moment
+// kernel, 4 the composite-weight kernel
+static int side_abl() {
+  static const int v = [] {
+    const char* e = pf_ab_getenv("POSFEAT_SIDE_ABL");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 // wc (n*128*128) | bc (n*128) | w2t (9*64*128)
 size_t pf_gfuse_weights_floats(int n) {
   return (size_t)n * GF_COUT * (GF_KPAD + 1) + (size_t)9 * GF_CG * GF_COUT;
@@ -699,8 +710,9 @@ int pf_gfuse_weights(const float* w2_packed, const float* b2, const float* w1_pa
                      float* bc, hipStream_t st) {
   const int k2pad = posfeat_conv_packed_k(GF_CL + GF_CG, 3, 3);
   const int k1pad = posfeat_conv_packed_k(3, 3, 3);
-  hipLaunchKernelGGL(gfuse_weights_kernel, dim3(GF_COUT, n), dim3(128), 0, st, w2_packed, k2pad,
-                     b2, w1_packed, k1pad, b1, mean, rstd, wc, bc);
+  if (!(side_abl() & 4))
+    hipLaunchKernelGGL(gfuse_weights_kernel, dim3(GF_COUT, n), dim3(128), 0, st, w2_packed, k2pad,
+                       b2, w1_packed, k1pad, b1, mean, rstd, wc, bc);
   hipLaunchKernelGGL(gfuse_w2t_kernel, dim3(9 * GF_CG), dim3(GF_COUT), 0, st, w2_packed, k2pad,
                      bc + (size_t)n * GF_COUT);
   PF_CHECK_LAUNCH();
@@ -772,9 +784,10 @@ int pf_gfuse_prep(const float* img4, const float* c, int ccs, int n, int H, int 
   hipLaunchKernelGGL(gfuse_wsplit_kernel, dim3((tot + 255) / 256), dim3(256), 0, st, wc, n,
                      wplanes);
   const int nring = 2 * W + 2 * (H - 2);
-  hipLaunchKernelGGL(gfuse_ring_kernel, dim3((nring + GF_RP - 1) / GF_RP, n), dim3(2 * GF_COUT), 0, st,
-                     c, ccs, img4, w1_packed, posfeat_conv_packed_k(3, 3, 3), b1, H, W, mean, rstd,
-                     bc + (size_t)n * GF_COUT, b2, nullptr, 0, ring);
+  if (!(side_abl() & 1))
+    hipLaunchKernelGGL(gfuse_ring_kernel, dim3((nring + GF_RP - 1) / GF_RP, n), dim3(2 * GF_COUT), 0,
+                       st, c, ccs, img4, w1_packed, posfeat_conv_packed_k(3, 3, 3), b1, H, W, mean,
+                       rstd, bc + (size_t)n * GF_COUT, b2, nullptr, 0, ring);
   PF_CHECK_LAUNCH();
   return POSFEAT_OK;
 }
@@ -795,7 +808,8 @@ int pf_gfuse_imgstats(const float* img4, int n, int H, int W, const float* w1_pa
                               (size_t)4 * IM_G * IM_G * sizeof(double));
   if (lds > 160 * 1024 || W % 2) return POSFEAT_E_UNSUPPORTED;
   double* part = static_cast<double*>(ws);
-  hipLaunchKernelGGL(gfuse_imgmom_kernel, dim3(nband, n), dim3(256), lds, st, img4, H, W, part);
+  if (!(side_abl() & 2))
+    hipLaunchKernelGGL(gfuse_imgmom_kernel, dim3(nband, n), dim3(256), lds, st, img4, H, W, part);
   PF_CHECK_LAUNCH();
   hipLaunchKernelGGL(gfuse_imgstats_kernel, dim3(n), dim3(IM_G * IM_G), 0, st, part, nband, H * W,
                      w1_packed, posfeat_conv_packed_k(3, 3, 3), b1, 1e-5f, mean, rstd, gram);

@@ -23,7 +23,18 @@ step) so the line carries ``steady / kernel_path``.
 ``kernel_path_replay_images_per_s`` replays the run's own group composition
 (shapes and counts) on the kernel path, the denominator for mixed sizes.
 
-usage: python tools/extract_e2e.py [--seqs 96] [--sizes 480x640|mixed|hpatches] [--timing]
+``--sizes aachen``: an Aachen Day-Night layout (db/*.jpg, query/day/*/*.jpg,
+query/night/nexus5x/*.jpg) at the dataset's own image sizes (db 1063x1600 and
+1600x1063, queries 1200x1600; cropped to multiples of 16 by the loader as
+datasets/aachen.py does), run with the reference's configs/extract_aachen.yaml
+(20480 points, nms r 3, thr 0.5, detector_config_query for the queries);
+``--seqs`` then counts groups of 14 images (10 db, 3 day, 1 night).
+
+Every run reports ``images_per_s`` (from the Extractor's first image to its
+last file) and ``images_per_s_incl_setup`` (construction included: weights,
+engine planning, workers).
+
+usage: python tools/extract_e2e.py [--seqs 96] [--sizes 480x640|mixed|hpatches|aachen] [--timing]
                                    [--passes 1] [--no-write]
 """
 import argparse
@@ -54,6 +65,34 @@ def hpatches_sizes(nseq, seed=7):
         if s not in out:
             out.append(s)
     return out
+
+
+# Aachen Day-Night image sizes (h, w) before the loader's crop to multiples of 16
+AACHEN_DB = [(1063, 1600), (1600, 1063)]
+AACHEN_QUERY = (1200, 1600)
+
+
+def make_aachen(root, ngroups):
+    """<root>/data/aachen/images_upright/{db, query/day/milestone, query/night/nexus5x}
+    with 10 db, 3 day and 1 night JPEG per group, seeded smooth noise (quality
+    95, as the test trees); returns the cropped sizes."""
+    from PIL import Image
+    base = os.path.join(root, "data", "aachen", "images_upright")
+    rs = np.random.RandomState(17)
+    sizes = set()
+    for g in range(ngroups):
+        for sub, n, hw_of in (("db", 10, lambda i: AACHEN_DB[i % 2]),
+                              (os.path.join("query", "day", "milestone"), 3, lambda i: AACHEN_QUERY),
+                              (os.path.join("query", "night", "nexus5x"), 1, lambda i: AACHEN_QUERY)):
+            d = os.path.join(base, sub)
+            os.makedirs(d, exist_ok=True)
+            for i in range(n):
+                h, w = hw_of(g * n + i)
+                small = rs.randint(0, 256, (h // 8, w // 8, 3)).astype(np.uint8)
+                im = Image.fromarray(small).resize((w, h), Image.BILINEAR)
+                im.save(os.path.join(d, "%04d_%d.jpg" % (g, i)), quality=95)
+                sizes.add((h - h % 16, w - w % 16))
+    return base, sorted(sizes)
 
 
 def make_dataset(root, nseq, sizes):
@@ -158,19 +197,28 @@ def main():
         sizes = [tuple(int(v) for v in args.sizes.split("x"))]
     tmp = tempfile.mkdtemp(prefix="posfeat_e2e_")
     t = time.perf_counter()
-    make_dataset(tmp, args.seqs, sizes)
-    print("[e2e] dataset of %d images built in %.1f s" % (6 * args.seqs, time.perf_counter() - t),
+    aachen = args.sizes == "aachen"
+    if aachen:
+        data_path, sizes = make_aachen(tmp, args.seqs)
+        nimg = 14 * args.seqs
+        cfg = yaml.safe_load(open(os.path.join(ROOT, "configs", "extract_aachen.yaml")))
+        cfg["data_config_extract"]["data_path"] = data_path
+    else:
+        make_dataset(tmp, args.seqs, sizes)
+        nimg = 6 * args.seqs
+        cfg = yaml.safe_load(open(os.path.join(ROOT, "configs", "extract_hpatches.yaml")))
+        cfg["data_config_extract"]["data_path"] = os.path.join(tmp, "data",
+                                                               "hpatches-sequences-release")
+    print("[e2e] dataset of %d images built in %.1f s" % (nimg, time.perf_counter() - t),
           flush=True)
     make_checkpoint(tmp)
-    cfg = yaml.safe_load(open(os.path.join(ROOT, "configs", "extract_hpatches.yaml")))
-    cfg["data_config_extract"]["data_path"] = os.path.join(tmp, "data", "hpatches-sequences-release")
     if args.no_write:
         cfg["output_desc"] = False
     os.chdir(tmp)
     from posfeat_amd.managers.extractor import Extractor
     res = {}
     for p in ("cold", "warm")[:args.passes]:
-        cfg["output_root"] = "hpatches/e2e_" + p
+        cfg["output_root"] = ("aachen/e2e_" if aachen else "hpatches/e2e_") + p
         cp = os.path.join(tmp, "cfg_%s.yaml" % p)
         yaml.safe_dump(cfg, open(cp, "w"))
         t = time.perf_counter()
@@ -188,6 +236,7 @@ def main():
             if first is not None:
                 st["steady_images_per_s"] = (st["images"] - first[1]) / (st["seconds"] - first[0])
         st["setup_s"] = setup
+        st["images_per_s_incl_setup"] = st["images"] / (st["seconds"] + setup)
         eng = ex.model._engine
         st["kernel_path_images_per_s"] = kernel_path_rate(eng, ex, sizes[0], st.get("group", 32))
         if marks:
@@ -195,6 +244,8 @@ def main():
             groups = [(shp, c - k) for shp, (_, k), c in zip(ex.group_shapes, marks, counts)]
             st["kernel_path_replay_images_per_s"] = kernel_path_replay(eng, ex, groups)
             st["whole_over_replay"] = st["images_per_s"] / st["kernel_path_replay_images_per_s"]
+            st["whole_incl_setup_over_replay"] = (st["images_per_s_incl_setup"]
+                                                  / st["kernel_path_replay_images_per_s"])
         if "steady_images_per_s" in st:
             st["steady_over_kernel_path"] = st["steady_images_per_s"] / st["kernel_path_images_per_s"]
             if marks:
@@ -220,10 +271,16 @@ def main():
         gc.collect()
         torch.cuda.empty_cache()
     import torch
-    print(json.dumps({"workload": "extract.py e2e (configs/extract_hpatches.yaml: loader batch 1 "
-                                  "in the reference; the pipelined loop groups by shape)",
-                      "data": "synthetic HPatches layout, %d seqs x 6 ppm, sizes %s" % (
-                          args.seqs, sorted({sizes[s % len(sizes)] for s in range(args.seqs)})),
+    if aachen:
+        data = "synthetic Aachen Day-Night layout, %d groups x (10 db + 3 day + 1 night) jpg, " \
+               "cropped sizes %s" % (args.seqs, sizes)
+    else:
+        data = "synthetic HPatches layout, %d seqs x 6 ppm, sizes %s" % (
+            args.seqs, sorted({sizes[s % len(sizes)] for s in range(args.seqs)}))
+    print(json.dumps({"workload": "extract.py e2e (configs/extract_%s.yaml: loader batch 1 "
+                                  "in the reference; the pipelined loop groups by shape)"
+                                  % ("aachen" if aachen else "hpatches"),
+                      "data": data,
                       "device": torch.cuda.get_device_name(0), **res}))
 
 
