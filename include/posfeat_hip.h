@@ -348,6 +348,27 @@ int posfeat_wino6_weights(const float *w_packed, int cout, int cin, float *U, vo
 int posfeat_conv3x3_wino6(const float *x, int x_cstride, int n, int h, int w, int cin,
                           const float *U, const float *bias, int cout, int act, float *y,
                           int y_cstride, void *ws, size_t ws_bytes, void *stream);
+/* The engine's variants of the same conv: planes = 1 -- U as three bf16
+ * planes (96 x cout x cin halves, posfeat_wino6_weights_planes; cout % 64 ==
+ * 0), the GEMM splitting V on the fly (bf16x6); up2 = 1 -- x is the (h/2, w/2)
+ * map and the conv reads its x2 bilinear upsample (align_corners = True,
+ * DescNet.py:182-190 upconv), formed inside the input transform (h, w even).
+ * posfeat_wino6_weights_floats: the U size in floats for those arguments. */
+size_t posfeat_wino6_weights_floats(int cin, int cout, int planes);
+int posfeat_wino6_weights_planes(const float *w_packed, int cout, int cin, int planes, float *U,
+                                 void *stream);
+int posfeat_conv3x3_wino6_ex(const float *x, int x_cstride, int n, int h, int w, int cin,
+                             const float *U, int planes, int up2, const float *bias, int cout,
+                             int act, float *y, int y_cstride, void *ws, size_t ws_bytes,
+                             void *stream);
+/* Weight gradient of the same conv by F(6x6) (the training step's decoder,
+ * behind managers/trainer.py:331): dM = A dY A^T, 64 transform-domain GEMMs,
+ * dw = G^T dU G in the packed K order; db (may be NULL) = sum of dy.  Any h,
+ * w; cin, cout % 128 == 0.  Deterministic. */
+size_t posfeat_wino6_wgrad_workspace(int n, int h, int w, int cin, int cout);
+int posfeat_conv3x3_wino6_wgrad(const float *dy, int dy_cstride, const float *x, int x_cstride,
+                                int n, int h, int w, int cin, int cout, float *dw, float *db,
+                                void *ws, size_t ws_bytes, void *stream);
 
 /* Weight gradient of the same decoder convs by F(4x4,3x3) (the autograd
  * conv2d weight/bias backward behind managers/trainer.py:331 for
@@ -400,7 +421,11 @@ int posfeat_model_create(int batch, int h, int w, const float *weights, posfeat_
  * another still uses the store (Extractor over many image sizes,
  * managers/extractor.py:357-382 with datasets/hpatches.py:35-38's crops).
  * Instances sharing a store may run on different streams: a forward orders
- * itself after the forward that last built derived weights. */
+ * itself after the forward that last built derived weights.  They also share
+ * one side stream and its fork / join events (KeypointDet's image branch):
+ * instances sharing a store must be driven from ONE host thread (their
+ * forwards then serialise on that side stream, as the Extractor's loop
+ * does); give concurrent host threads separate stores (share = NULL). */
 int posfeat_model_create_shared(int batch, int h, int w, const float *weights,
                                 posfeat_model *share, posfeat_model **out);
 /* An extraction instance (posfeat_model_create) builds its derived weights --

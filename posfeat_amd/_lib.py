@@ -117,6 +117,15 @@ SIGNATURES = {
                                      c_void_p]),
     "posfeat_wino6_workspace": (c_size_t, [c_int] * 5),
     "posfeat_wino6_weights": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "posfeat_wino6_weights_floats": (c_size_t, [c_int, c_int, c_int]),
+    "posfeat_wino6_weights_planes": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "posfeat_conv3x3_wino6_ex": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
+                                         c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int,
+                                         c_void_p, c_size_t, c_void_p]),
+    "posfeat_wino6_wgrad_workspace": (c_size_t, [c_int] * 5),
+    "posfeat_conv3x3_wino6_wgrad": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int,
+                                            c_int, c_int, c_void_p, c_void_p, c_void_p, c_size_t,
+                                            c_void_p]),
     "posfeat_conv3x3_wino6": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
                                       c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_size_t,
                                       c_void_p]),

@@ -34,21 +34,38 @@ __global__ __launch_bounds__(128) void gfuse_w2t_kernel(const float* __restrict_
       w2[(size_t)co * k2pad + ((ci >> 5) * 9 + t) * 32 + (ci & 31)];
 }
 
-// Wc[b][co][(u*5+v)*4 + ci] (ci < 3; zero-padded to 128), bc[b][co]
+// Wc[b][co][(u*5+v)*4 + ci] (ci < 3; zero-padded to 128), bc[b][co].  One
+// block per (co, image): the block's W2 row slice (9 taps x 64 G channels,
+// times rstd -- the product the sums below take first) and convimg's weights
+// are staged in LDS once, so each of the 100 composite taps reads its operands
+// from LDS instead of three dependent global loads per term (310 -> ~20 us
+// per 32-image step, r16d; the side stream's kernels slow the main stream
+// almost one for one).  Same terms in the same order: t outer,
+// k inner, (w2 rstd) w1 -- bit-identical to the round-5 kernel.
+constexpr int GW_W1S = 37;  // floats per k row of W1 in LDS (36 used: 9 taps x 4 channels)
 __global__ __launch_bounds__(128) void gfuse_weights_kernel(
     const float* __restrict__ w2, int k2pad, const float* __restrict__ b2,
     const float* __restrict__ w1, int k1pad, const float* __restrict__ b1,
     const float* __restrict__ mean, const float* __restrict__ rstd, float* __restrict__ wc,
     float* __restrict__ bc) {
   const int co = blockIdx.x, b = blockIdx.y, e = threadIdx.x;
+  __shared__ float a_s[9][GF_CG];          // W2[co][192 + k][t] * rstd[k]
+  __shared__ float w1_s[GF_CG][GW_W1S];    // W1[k][s * 4 + ci]
+  __shared__ float d_s[GF_CG];             // b1[k] - mean[k]
   const float* mb = mean + (size_t)b * GF_CG;
   const float* rb = rstd + (size_t)b * GF_CG;
   const float* w2r = w2 + (size_t)co * k2pad;
-  // W2 packed K index of channel 192 + k, tap t: ((ci/32)*9 + t)*32 + ci%32
-  auto w2at = [&](int k, int t) {
-    const int ci = GF_CL + k;
-    return w2r[((ci >> 5) * 9 + t) * 32 + (ci & 31)];
-  };
+  for (int i = e; i < 9 * GF_CG; i += blockDim.x) {
+    const int t = i / GF_CG, k = i - t * GF_CG;
+    const int ci = GF_CL + k;  // W2 packed K index of channel 192 + k, tap t
+    a_s[t][k] = w2r[((ci >> 5) * 9 + t) * 32 + (ci & 31)] * rb[k];
+  }
+  for (int i = e; i < GF_CG * 36; i += blockDim.x) {
+    const int k = i / 36, j = i - k * 36;
+    w1_s[k][j] = w1[(size_t)k * k1pad + j];
+  }
+  if (e < GF_CG) d_s[e] = b1[e] - mb[e];
+  __syncthreads();
   float v = 0.f;
   if (e < 100) {
     const int ci = e & 3, uv = e >> 2, u = uv / 5, vv = uv - u * 5;
@@ -59,10 +76,9 @@ __global__ __launch_bounds__(128) void gfuse_weights_kernel(
         for (int tx = 0; tx < 3; ++tx) {
           const int sx = vv - tx;
           if (sx < 0 || sx > 2) continue;
-          const int t = ty * 3 + tx, s = sy * 3 + sx;
+          const int t = ty * 3 + tx, s4 = (sy * 3 + sx) * 4 + ci;
           float acc = 0.f;
-          for (int k = 0; k < GF_CG; ++k)
-            acc += w2at(k, t) * rb[k] * w1[(size_t)k * k1pad + s * 4 + ci];
+          for (int k = 0; k < GF_CG; ++k) acc += a_s[t][k] * w1_s[k][s4];
           v += acc;
         }
       }
@@ -72,7 +88,7 @@ __global__ __launch_bounds__(128) void gfuse_weights_kernel(
   if (e == 0) {
     float acc = b2[co];
     for (int t = 0; t < 9; ++t)
-      for (int k = 0; k < GF_CG; ++k) acc += w2at(k, t) * rb[k] * (b1[k] - mb[k]);
+      for (int k = 0; k < GF_CG; ++k) acc += a_s[t][k] * d_s[k];
     bc[(size_t)b * GF_COUT + co] = acc;
   }
 }
@@ -767,8 +783,168 @@ int pf_gfuse_conv(const float* img4, const float* c, int ccs, int n, int H, int 
   return POSFEAT_OK;
 }
 
+// ---- the border ring for the fused head, in two passes ----------------------
+// gfuse_ring_kernel recomputes convimg's normalised output G at each ring
+// pixel's nine conv2 taps (64 channels x 27 MACs per tap, each value three
+// times over, since neighbouring ring pixels share taps) and contracts the
+// 576 (tap, channel) terms per output on the VALU: 0.66-0.70 ms per 32-image
+// step on the side stream, where it slows the main stream's kernels almost
+// one for one (r16d: the step 1.4 % faster without it).  Here:
+// (1) gfuse_band_kernel: G once at every position a ring pixel's taps reach
+//     inside the image -- the border itself (ring 0, pf_ring_index order)
+//     and the ring one pixel in (ring 1, the border of the inner
+//     (H-2) x (W-2) image) -- band[b][pos][64];
+// (2) gfuse_ring_mfma_kernel: y_ring[r][co] = b2[co] + sum_t sum_k
+//     W2[co][192+k][t] G(q_t(r))[k] as a gathered [64 ring pixels x 576] x
+//     [576 x 128] product on the fp32 matrix cores (v_mfma_f32_32x32x2_f32:
+//     fp32 products, fp32 accumulation -- the VALU form's arithmetic class, in
+//     another order), taps outside the image contributing 0 (conv2's zero
+//     padding of G).
+__host__ __device__ inline int gf_nring(int H, int W) { return 2 * W + 2 * (H - 2); }
+__host__ __device__ inline int gf_nband(int H, int W) {
+  return gf_nring(H, W) + gf_nring(H - 2, W - 2);
+}
+// (Y, X) of ring index r of an H x W image (the inverse of pf_ring_index)
+__device__ __forceinline__ void gf_ring_pos(int r, int H, int W, int& Y, int& X) {
+  if (r < W) {
+    Y = 0;
+    X = r;
+  } else if (r < 2 * W) {
+    Y = H - 1;
+    X = r - W;
+  } else if (r < 2 * W + H - 2) {
+    Y = 1 + (r - 2 * W);
+    X = 0;
+  } else {
+    Y = 1 + (r - 2 * W - (H - 2));
+    X = W - 1;
+  }
+}
+// band index of position (Y, X): ring 0, then ring 1; -1 outside the image or
+// deeper inside (no ring pixel's tap lands there)
+__device__ __forceinline__ int gf_band_index(int Y, int X, int H, int W) {
+  if ((unsigned)Y >= (unsigned)H || (unsigned)X >= (unsigned)W) return -1;
+  if (Y == 0 || Y == H - 1 || X == 0 || X == W - 1) return pf_ring_index(Y, X, H, W);
+  if (Y == 1 || Y == H - 2 || X == 1 || X == W - 2)
+    return gf_nring(H, W) + pf_ring_index(Y - 1, X - 1, H - 2, W - 2);
+  return -1;
+}
+
+// band[b][pos][k] = (c(q)[k] - mean[k]) rstd[k], c = convimg's raw output
+// (read from c when given, else recomputed from the zero-padded image in the
+// ring kernel's tap order); one thread per (position, channel)
+__global__ __launch_bounds__(256) void gfuse_band_kernel(
+    const float* __restrict__ c, int ccs, const float* __restrict__ img4,
+    const float* __restrict__ w1, int k1pad, const float* __restrict__ b1, int H, int W,
+    const float* __restrict__ mean, const float* __restrict__ rstd, float* __restrict__ band) {
+  const int b = blockIdx.y;
+  const int nb = gf_nband(H, W), n0 = gf_nring(H, W);
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nb * GF_CG) return;
+  const int pos = i / GF_CG, k = i - pos * GF_CG;
+  int Y, X;
+  if (pos < n0) {
+    gf_ring_pos(pos, H, W, Y, X);
+  } else {
+    gf_ring_pos(pos - n0, H - 2, W - 2, Y, X);
+    ++Y;
+    ++X;
+  }
+  float cv;
+  if (c) {
+    cv = c[(((size_t)b * H + Y) * W + X) * ccs + k];
+  } else {
+    cv = b1[k];
+    const float* wk = w1 + (size_t)k * k1pad;
+    for (int s9 = 0; s9 < 9; ++s9) {
+      const int iy = Y + s9 / 3 - 1, ix = X + s9 % 3 - 1;
+      float x0 = 0.f, x1 = 0.f, x2 = 0.f;
+      if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W) {
+        const float* xp = img4 + (((size_t)b * H + iy) * W + ix) * 4;
+        x0 = xp[0];
+        x1 = xp[1];
+        x2 = xp[2];
+      }
+      cv += wk[s9 * 4] * x0 + wk[s9 * 4 + 1] * x1 + wk[s9 * 4 + 2] * x2;
+    }
+  }
+  band[((size_t)b * nb + pos) * GF_CG + k] = (cv - mean[(size_t)b * GF_CG + k]) *
+                                            rstd[(size_t)b * GF_CG + k];
+}
+
+// Block = 64 ring pixels of one image x all 128 outputs, 4 waves: wave w owns
+// pixels 32 (w & 1) .. + 32 and outputs 64 (w >> 1) .. + 64 (two 32 x 32
+// fp32-MFMA tiles).  Per conv2 tap t: the 64 pixels' G rows (gathered from
+// the band, 0 outside the image) and W2's 64 x 128 slice of that tap go to
+// LDS, then 32 K-steps of two MFMAs.
+constexpr int GR_P = 64;       // ring pixels per block
+constexpr int GR_GS = GF_CG + 1;   // LDS row pitch of the gathered G (banks)
+constexpr int GR_WS = GF_COUT + 4;  // LDS row pitch of the W2 slice
+__global__ __launch_bounds__(256) void gfuse_ring_mfma_kernel(
+    const float* __restrict__ band, int H, int W, const float* __restrict__ w2t,
+    const float* __restrict__ b2, float* __restrict__ ring) {
+  __shared__ float gs[GR_P][GR_GS];
+  __shared__ float ws[GF_CG][GR_WS];
+  __shared__ int ppy[GR_P], ppx[GR_P];
+  const int b = blockIdx.y, tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6, ph = wave & 1, chh = wave >> 1;
+  const int nr = gf_nring(H, W), nb = gf_nband(H, W);
+  const int r0 = blockIdx.x * GR_P;
+  if (tid < GR_P) {
+    int Y = -4, X = -4;  // past the last ring pixel: every tap outside
+    if (r0 + tid < nr) gf_ring_pos(r0 + tid, H, W, Y, X);
+    ppy[tid] = Y;
+    ppx[tid] = X;
+  }
+  const float* bb = band + (size_t)b * nb * GF_CG;
+  f32x16 acc[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+  for (int t = 0; t < 9; ++t) {
+    pf_syncthreads();  // pixel positions written; the previous tap's operands read
+    const int dy = t / 3 - 1, dx = t % 3 - 1;
+#pragma unroll 4
+    for (int i = tid; i < GR_P * GF_CG; i += 256) {
+      const int j = i / GF_CG, k = i - j * GF_CG;
+      const int idx = gf_band_index(ppy[j] + dy, ppx[j] + dx, H, W);
+      gs[j][k] = idx >= 0 ? bb[(size_t)idx * GF_CG + k] : 0.f;
+    }
+#pragma unroll 4
+    for (int i = tid; i < GF_CG * GF_COUT; i += 256) {
+      const int k = i / GF_COUT, co = i - k * GF_COUT;
+      ws[k][co] = w2t[((size_t)t * GF_CG + k) * GF_COUT + co];
+    }
+    pf_syncthreads();
+    const int arow = 32 * ph + (lane & 31), kh = lane >> 5;
+#pragma unroll 8
+    for (int kk = 0; kk < GF_CG / 2; ++kk) {
+      const int k = 2 * kk + kh;
+      const float a = gs[arow][k];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const float bv = ws[k][64 * chh + 32 * i + (lane & 31)];
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bv, acc[i], 0, 0, 0);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int co = 64 * chh + 32 * i + (lane & 31);
+    const float bias = b2[co];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      const int rr = r0 + 32 * ph + m;
+      if (rr < nr) ring[((size_t)b * nr + rr) * GF_COUT + co] = acc[i][r] + bias;
+    }
+  }
+}
+
+// the ring buffer of the fused head, then the band scratch of its two passes
 size_t pf_gfuse_ring_floats(int n, int H, int W) {
-  return (size_t)n * (2 * W + 2 * (H - 2)) * GF_COUT;
+  return (size_t)n * gf_nring(H, W) * GF_COUT + (size_t)n * gf_nband(H, W) * GF_CG;
 }
 
 // Everything of the G part but the interior conv itself, which
@@ -779,15 +955,19 @@ int pf_gfuse_prep(const float* img4, const float* c, int ccs, int n, int H, int 
                   const float* b2, const float* w1_packed, const float* b1,
                   unsigned short* wplanes, float* ring, hipStream_t st) {
   if (!c && !(w1_packed && b1)) return POSFEAT_E_INVALID;
-  if (n <= 0 || H < 2 || W < 2 || !wplanes || !ring) return POSFEAT_E_INVALID;
+  if (n <= 0 || H < 4 || W < 4 || !wplanes || !ring) return POSFEAT_E_INVALID;
   const int tot = n * GF_COUT * G8_K;
   hipLaunchKernelGGL(gfuse_wsplit_kernel, dim3((tot + 255) / 256), dim3(256), 0, st, wc, n,
                      wplanes);
-  const int nring = 2 * W + 2 * (H - 2);
-  if (!(side_abl() & 1))
-    hipLaunchKernelGGL(gfuse_ring_kernel, dim3((nring + GF_RP - 1) / GF_RP, n), dim3(2 * GF_COUT), 0,
-                       st, c, ccs, img4, w1_packed, posfeat_conv_packed_k(3, 3, 3), b1, H, W, mean,
-                       rstd, bc + (size_t)n * GF_COUT, b2, nullptr, 0, ring);
+  const int nring = gf_nring(H, W), nband = gf_nband(H, W);
+  float* band = ring + (size_t)n * nring * GF_COUT;
+  if (!(side_abl() & 1)) {
+    hipLaunchKernelGGL(gfuse_band_kernel, dim3((nband * GF_CG + 255) / 256, n), dim3(256), 0, st,
+                       c, ccs, img4, w1_packed, posfeat_conv_packed_k(3, 3, 3), b1, H, W, mean,
+                       rstd, band);
+    hipLaunchKernelGGL(gfuse_ring_mfma_kernel, dim3((nring + GR_P - 1) / GR_P, n), dim3(256), 0,
+                       st, band, H, W, bc + (size_t)n * GF_COUT, b2, ring);
+  }
   PF_CHECK_LAUNCH();
   return POSFEAT_OK;
 }

@@ -1365,3 +1365,42 @@ extern "C" int posfeat_conv3x3_wino6(const float* x, int x_cstride, int n, int h
   return pf_wino6_conv(x, x_cstride, n, h, w, cin, U, bias, cout, act, y, y_cstride, ws, ws_bytes,
                        pf_stream(stream), 7, 0, 0);
 }
+
+// ---- test surfaces of the engine's F(6x6) paths -----------------------------
+// (the extraction engine's bf16 three-plane U, the decoder's fused x2
+// upsample, and the training step's F(6x6) weight gradient)
+extern "C" size_t posfeat_wino6_weights_floats(int cin, int cout, int planes) {
+  if (cin <= 0 || cout <= 0) return 0;
+  return pf_wino6_weights_floats(cin, cout, planes != 0 && wino_planes_ok(cout));
+}
+
+extern "C" int posfeat_wino6_weights_planes(const float* w_packed, int cout, int cin, int planes,
+                                            float* U, void* stream) {
+  if (!w_packed || !U || planes < 0 || planes > 1) return POSFEAT_E_INVALID;
+  return pf_wino6_weights(w_packed, cout, cin, U, pf_stream(stream), planes != 0);
+}
+
+extern "C" int posfeat_conv3x3_wino6_ex(const float* x, int x_cstride, int n, int h, int w,
+                                        int cin, const float* U, int planes, int up2,
+                                        const float* bias, int cout, int act, float* y,
+                                        int y_cstride, void* ws, size_t ws_bytes, void* stream) {
+  if (!x || !U || !y || !ws || planes < 0 || planes > 1 || up2 < 0 || up2 > 1)
+    return POSFEAT_E_INVALID;
+  if (planes && !wino_planes_ok(cout)) return POSFEAT_E_INVALID;
+  return pf_wino6_conv(x, x_cstride, n, h, w, cin, U, bias, cout, act, y, y_cstride, ws, ws_bytes,
+                       pf_stream(stream), 7, planes, up2);
+}
+
+extern "C" size_t posfeat_wino6_wgrad_workspace(int n, int h, int w, int cin, int cout) {
+  if (n <= 0 || h <= 0 || w <= 0 || cin % 128 || cout % 128 || cin <= 0 || cout <= 0) return 0;
+  return pf_wino6_wgrad_ws_bytes(n, h, w, cin, cout);
+}
+
+extern "C" int posfeat_conv3x3_wino6_wgrad(const float* dy, int dy_cstride, const float* x,
+                                           int x_cstride, int n, int h, int w, int cin, int cout,
+                                           float* dw, float* db, void* ws, size_t ws_bytes,
+                                           void* stream) {
+  if (!dy || !x || !dw || !ws || n <= 0) return POSFEAT_E_INVALID;
+  return pf_wino6_wgrad(dy, dy_cstride, x, x_cstride, n, h, w, cin, cout, dw, db, 0, ws, ws_bytes,
+                        pf_stream(stream), nullptr);
+}

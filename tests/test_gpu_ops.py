@@ -170,6 +170,108 @@ def test_conv3x3_wino6_vs_torch(gpu, case):
         assert torch.all(out[..., cout:] == 7.0).item(), "wrote outside its channel slice"
 
 
+WINO6_EX_CASES = [
+    # n, h, w, cin, cout, act, planes, up2
+    (2, 18, 24, 64, 64, "none", 1, 0),       # three-plane U, whole tiles
+    (1, 30, 40, 1024, 512, "elu", 1, 0),     # iconv3 shape, planes (the engine's default)
+    (2, 60, 80, 512, 256, "elu", 1, 1),      # upconv2 shape: x2 upsample in the transform
+    (1, 30, 40, 1024, 512, "elu", 1, 1),     # upconv3 shape
+    (2, 20, 26, 64, 128, "relu", 0, 1),      # fp32 U + upsample, cut tiles
+]
+
+
+@pytest.mark.parametrize("case", WINO6_EX_CASES)
+def test_conv3x3_wino6_planes_up2_vs_torch(gpu, case):
+    """The extraction engine's F(6x6) variants: U as three bf16
+    planes (planes = 1, the GEMM splitting V on the fly: bf16x6) and the
+    decoder's x2 bilinear upsample (align_corners = True,
+    DescNet.py:182-190) formed inside the input transform (up2 = 1), against
+    the fp64 conv of the fp64-upsampled input, with test_conv3x3_wino6's
+    bound."""
+    from posfeat_amd import ops
+    from posfeat_amd._lib import check, lib, ptr, stream_ptr
+    n, h, w, cin, cout, act, planes, up2 = case
+    g = torch.Generator().manual_seed(sum(case[:5]) + 60)
+    hi, wi = (h // 2, w // 2) if up2 else (h, w)
+    x = torch.randn(n, cin, hi, wi, generator=g)
+    wt = torch.randn(cout, cin, 3, 3, generator=g) * (2.0 / (cin * 9)) ** 0.5
+    b = torch.randn(cout, generator=g) * 0.1
+    xu = F.interpolate(x.double(), scale_factor=2, mode="bilinear",
+                       align_corners=True) if up2 else x.double()
+    assert xu.shape[-2:] == (h, w)
+    ref, bound = _conv_ref64(xu, wt, b, 1, 1, None, act)
+    xd = x.permute(0, 2, 3, 1).contiguous().to(gpu)
+    wp, bp = ops.pack_conv_weight(wt.to(gpu), b.to(gpu))
+    U = torch.empty(lib().posfeat_wino6_weights_floats(cin, cout, planes), device=gpu)
+    check(lib().posfeat_wino6_weights_planes(ptr(wp), cout, cin, planes, ptr(U), stream_ptr()))
+    need = lib().posfeat_wino6_workspace(n, h, w, cin, cout)
+    ws = torch.empty(need, dtype=torch.uint8, device=gpu)
+    out = torch.full((n, h, w, cout), 7.0, device=gpu)
+    actc = {"none": 0, "relu": 1, "elu": 2}[act]
+    check(lib().posfeat_conv3x3_wino6_ex(ptr(xd), cin, n, h, w, cin, ptr(U), planes, up2, ptr(bp),
+                                         cout, actc, ptr(out), cout, ptr(ws), need, stream_ptr()))
+    torch.cuda.synchronize()
+    got = out.permute(0, 3, 1, 2).double().cpu()
+    err = (got - ref).abs()
+    tol = 3e-5 * bound + 1e-6
+    print("wino6 ex %s: max err / bound %.2e" % (case, (err / bound.clamp_min(1e-30)).max()))
+    assert torch.all(err <= tol), "max err %g (ratio %g)" % (err.max(), (err / tol).max())
+    # the plain fp32-U / materialised-upsample form of the same conv agrees
+    if planes or up2:
+        xm = xu.float().permute(0, 2, 3, 1).contiguous().to(gpu)
+        U0 = torch.empty(64 * cout * cin, device=gpu)
+        check(lib().posfeat_wino6_weights(ptr(wp), cout, cin, ptr(U0), stream_ptr()))
+        out0 = torch.empty_like(out)
+        check(lib().posfeat_conv3x3_wino6(ptr(xm), cin, n, h, w, cin, ptr(U0), ptr(bp), cout, actc,
+                                          ptr(out0), cout, ptr(ws), need, stream_ptr()))
+        torch.cuda.synchronize()
+        d = (out0 - out).abs().max().item()
+        assert d <= 2e-5 * float(bound.max()), d
+
+
+@pytest.mark.parametrize("n,h,w,cin,cout", [(2, 18, 24, 128, 128), (1, 20, 26, 256, 128),
+                                             (2, 60, 80, 512, 256)])
+def test_conv3x3_wino6_wgrad_vs_torch_and_f4(gpu, n, h, w, cin, cout):
+    """posfeat_conv3x3_wino6_wgrad (the training step's F(6x6) weight
+    gradient: dY transform, 64 split transform-domain GEMMs, G^T dU G) against
+    torch's fp64 conv2d weight/bias gradient, with the F(4x4) test's bound
+    (tests/test_train_kp.py), and against the F(4x4) weight gradient where
+    h, w % 4 == 0."""
+    from posfeat_amd import weights
+    from posfeat_amd._lib import check, lib, ptr, stream_ptr
+    rs = np.random.RandomState(n * h + w + cin)
+    x = rs.randn(n, cin, h, w).astype(np.float32)
+    dy = rs.randn(n, cout, h, w).astype(np.float32)
+    xt = torch.from_numpy(x).double()
+    wt = torch.zeros(cout, cin, 3, 3, dtype=torch.float64, requires_grad=True)
+    F.conv2d(xt, wt, padding=1).backward(torch.from_numpy(dy).double())
+    ref_w = wt.grad.numpy()
+    ref_b = dy.astype(np.float64).sum((0, 2, 3))
+    xd = torch.from_numpy(np.ascontiguousarray(x.transpose(0, 2, 3, 1))).to(gpu)
+    dyd = torch.from_numpy(np.ascontiguousarray(dy.transpose(0, 2, 3, 1))).to(gpu)
+    kpad = lib().posfeat_conv_packed_k(cin, 3, 3)
+
+    def run(fn, wsfn):
+        dw = torch.full((cout * kpad,), float("nan"), device=gpu)
+        db = torch.empty(cout, device=gpu)
+        need = wsfn(n, h, w, cin, cout)
+        assert need > 0
+        ws = torch.empty(need, dtype=torch.uint8, device=gpu)
+        check(fn(ptr(dyd), cout, ptr(xd), cin, n, h, w, cin, cout, ptr(dw), ptr(db), ptr(ws), need,
+                 stream_ptr()))
+        torch.cuda.synchronize()
+        return weights.unpack_conv(dw.cpu().numpy(), cout, cin, 3, 3), db.cpu().numpy()
+    got, gb = run(lib().posfeat_conv3x3_wino6_wgrad, lib().posfeat_wino6_wgrad_workspace)
+    err = np.abs(got - ref_w).max() / np.sqrt(n * h * w)
+    print("wino6 wgrad %s: err %.2e" % ((n, h, w, cin, cout), err))
+    assert err <= 2e-4, err
+    assert np.abs(gb - ref_b).max() <= 1e-4 * np.sqrt(n * h * w)
+    if h % 4 == 0 and w % 4 == 0:
+        g4, _ = run(lib().posfeat_conv3x3_wino_wgrad, lib().posfeat_wino_wgrad_workspace)
+        e4 = np.abs(g4 - ref_w).max() / np.sqrt(n * h * w)
+        assert np.abs(got - g4).max() / np.sqrt(n * h * w) <= 2e-4 + e4
+
+
 @pytest.mark.parametrize("act,has_res", [("elu", False), ("relu", True)])
 def test_conv_splitk_vs_torch(gpu, act, has_res):
     """Deep-K shape that takes the split-K path (partials + ordered reduce)."""

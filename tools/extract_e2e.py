@@ -193,6 +193,8 @@ def main():
         sizes = SIZES
     elif args.sizes == "hpatches":
         sizes = hpatches_sizes(args.seqs)
+    elif args.sizes == "aachen":
+        sizes = None   # make_aachen's
     else:
         sizes = [tuple(int(v) for v in args.sizes.split("x"))]
     tmp = tempfile.mkdtemp(prefix="posfeat_e2e_")
