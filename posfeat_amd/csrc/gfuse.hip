@@ -832,52 +832,66 @@ __device__ __forceinline__ int gf_band_index(int Y, int X, int H, int W) {
 
 // band[b][pos][k] = (c(q)[k] - mean[k]) rstd[k], c = convimg's raw output
 // (read from c when given, else recomputed from the zero-padded image in the
-// ring kernel's tap order); one thread per (position, channel)
+// ring kernel's tap order).  Block = GB_POS positions x 64 channels (thread
+// = channel, one position per wave step); convimg's 64 x 36 weights in LDS
+// (a lane per channel would otherwise read 64 different rows per load)
+constexpr int GB_POS = 16;  // positions per block
 __global__ __launch_bounds__(256) void gfuse_band_kernel(
     const float* __restrict__ c, int ccs, const float* __restrict__ img4,
     const float* __restrict__ w1, int k1pad, const float* __restrict__ b1, int H, int W,
     const float* __restrict__ mean, const float* __restrict__ rstd, float* __restrict__ band) {
-  const int b = blockIdx.y;
+  __shared__ float w1s[GF_CG][37];
+  const int b = blockIdx.y, tid = threadIdx.x;
   const int nb = gf_nband(H, W), n0 = gf_nring(H, W);
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nb * GF_CG) return;
-  const int pos = i / GF_CG, k = i - pos * GF_CG;
-  int Y, X;
-  if (pos < n0) {
-    gf_ring_pos(pos, H, W, Y, X);
-  } else {
-    gf_ring_pos(pos - n0, H - 2, W - 2, Y, X);
-    ++Y;
-    ++X;
-  }
-  float cv;
-  if (c) {
-    cv = c[(((size_t)b * H + Y) * W + X) * ccs + k];
-  } else {
-    cv = b1[k];
-    const float* wk = w1 + (size_t)k * k1pad;
-    for (int s9 = 0; s9 < 9; ++s9) {
-      const int iy = Y + s9 / 3 - 1, ix = X + s9 % 3 - 1;
-      float x0 = 0.f, x1 = 0.f, x2 = 0.f;
-      if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W) {
-        const float* xp = img4 + (((size_t)b * H + iy) * W + ix) * 4;
-        x0 = xp[0];
-        x1 = xp[1];
-        x2 = xp[2];
-      }
-      cv += wk[s9 * 4] * x0 + wk[s9 * 4 + 1] * x1 + wk[s9 * 4 + 2] * x2;
+  if (!c)
+    for (int i = tid; i < GF_CG * 36; i += 256) {
+      const int k = i / 36, j = i - k * 36;
+      w1s[k][j] = w1[(size_t)k * k1pad + j];
     }
+  pf_syncthreads();
+  const int k = tid & 63;
+  const float mk = mean[(size_t)b * GF_CG + k], rk = rstd[(size_t)b * GF_CG + k];
+  const float bk = c ? 0.f : b1[k];
+  for (int j = tid >> 6; j < GB_POS; j += 4) {
+    const int pos = blockIdx.x * GB_POS + j;
+    if (pos >= nb) break;
+    int Y, X;
+    if (pos < n0) {
+      gf_ring_pos(pos, H, W, Y, X);
+    } else {
+      gf_ring_pos(pos - n0, H - 2, W - 2, Y, X);
+      ++Y;
+      ++X;
+    }
+    float cv;
+    if (c) {
+      cv = c[(((size_t)b * H + Y) * W + X) * ccs + k];
+    } else {
+      cv = bk;
+      for (int s9 = 0; s9 < 9; ++s9) {
+        const int iy = Y + s9 / 3 - 1, ix = X + s9 % 3 - 1;
+        float x0 = 0.f, x1 = 0.f, x2 = 0.f;
+        if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W) {
+          const float* xp = img4 + (((size_t)b * H + iy) * W + ix) * 4;
+          x0 = xp[0];
+          x1 = xp[1];
+          x2 = xp[2];
+        }
+        cv += w1s[k][s9 * 4] * x0 + w1s[k][s9 * 4 + 1] * x1 + w1s[k][s9 * 4 + 2] * x2;
+      }
+    }
+    band[((size_t)b * nb + pos) * GF_CG + k] = (cv - mk) * rk;
   }
-  band[((size_t)b * nb + pos) * GF_CG + k] = (cv - mean[(size_t)b * GF_CG + k]) *
-                                            rstd[(size_t)b * GF_CG + k];
 }
 
 // Block = 64 ring pixels of one image x all 128 outputs, 4 waves: wave w owns
 // pixels 32 (w & 1) .. + 32 and outputs 64 (w >> 1) .. + 64 (two 32 x 32
-// fp32-MFMA tiles).  Per conv2 tap t: the 64 pixels' G rows (gathered from
-// the band, 0 outside the image) and W2's 64 x 128 slice of that tap go to
-// LDS, then 32 K-steps of two MFMAs.
-constexpr int GR_P = 64;       // ring pixels per block
+// fp32-MFMA tiles).  The pixels' band indices of all nine conv2 taps are
+// tabulated once; a tap no pixel of the block reaches inside the image (the
+// outward row or column of a straight ring segment: 3 of 9) is skipped; the
+// next tap's gathered G rows and W2 slice are loaded into registers while the
+// current tap's 64 MFMAs run, then stored to LDS.
+constexpr int GR_P = 64;           // ring pixels per block
 constexpr int GR_GS = GF_CG + 1;   // LDS row pitch of the gathered G (banks)
 constexpr int GR_WS = GF_COUT + 4;  // LDS row pitch of the W2 slice
 __global__ __launch_bounds__(256) void gfuse_ring_mfma_kernel(
@@ -885,38 +899,64 @@ __global__ __launch_bounds__(256) void gfuse_ring_mfma_kernel(
     const float* __restrict__ b2, float* __restrict__ ring) {
   __shared__ float gs[GR_P][GR_GS];
   __shared__ float ws[GF_CG][GR_WS];
-  __shared__ int ppy[GR_P], ppx[GR_P];
+  __shared__ int bidx[9][GR_P];
+  __shared__ int tap_live[9];
   const int b = blockIdx.y, tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6, ph = wave & 1, chh = wave >> 1;
   const int nr = gf_nring(H, W), nb = gf_nband(H, W);
   const int r0 = blockIdx.x * GR_P;
-  if (tid < GR_P) {
-    int Y = -4, X = -4;  // past the last ring pixel: every tap outside
-    if (r0 + tid < nr) gf_ring_pos(r0 + tid, H, W, Y, X);
-    ppy[tid] = Y;
-    ppx[tid] = X;
+  if (tid < 9) tap_live[tid] = 0;
+  pf_syncthreads();
+  for (int i = tid; i < 9 * GR_P; i += 256) {
+    const int t = i / GR_P, j = i - t * GR_P;
+    int idx = -1;
+    if (r0 + j < nr) {
+      int Y, X;
+      gf_ring_pos(r0 + j, H, W, Y, X);
+      idx = gf_band_index(Y + t / 3 - 1, X + t % 3 - 1, H, W);
+    }
+    bidx[t][j] = idx;
+    if (idx >= 0) tap_live[t] = 1;  // benign race: every writer stores 1
   }
+  pf_syncthreads();
   const float* bb = band + (size_t)b * nb * GF_CG;
+  // per thread: 16 gathered G values (pixel j = i / 64, channel k = i % 64,
+  // i = tid + 256 u) and 32 W2 values (k = i / 128, co = i % 128)
+  float gv[16], wv[32];
+  auto load = [&](int t) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int i = tid + 256 * u, j = i >> 6, k = i & 63;
+      const int idx = bidx[t][j];
+      gv[u] = idx >= 0 ? bb[(size_t)idx * GF_CG + k] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 32; ++u) wv[u] = w2t[(size_t)t * GF_CG * GF_COUT + tid + 256 * u];
+  };
   f32x16 acc[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
-  for (int t = 0; t < 9; ++t) {
-    pf_syncthreads();  // pixel positions written; the previous tap's operands read
-    const int dy = t / 3 - 1, dx = t % 3 - 1;
-#pragma unroll 4
-    for (int i = tid; i < GR_P * GF_CG; i += 256) {
-      const int j = i / GF_CG, k = i - j * GF_CG;
-      const int idx = gf_band_index(ppy[j] + dy, ppx[j] + dx, H, W);
-      gs[j][k] = idx >= 0 ? bb[(size_t)idx * GF_CG + k] : 0.f;
+  int t = 0;
+  while (t < 9 && !tap_live[t]) ++t;
+  if (t < 9) load(t);
+  while (t < 9) {
+    pf_syncthreads();  // the previous tap's operands are read
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int i = tid + 256 * u;
+      gs[i >> 6][i & 63] = gv[u];
     }
-#pragma unroll 4
-    for (int i = tid; i < GF_CG * GF_COUT; i += 256) {
-      const int k = i / GF_COUT, co = i - k * GF_COUT;
-      ws[k][co] = w2t[((size_t)t * GF_CG + k) * GF_COUT + co];
+#pragma unroll
+    for (int u = 0; u < 32; ++u) {
+      const int i = tid + 256 * u;
+      ws[i >> 7][i & 127] = wv[u];
     }
     pf_syncthreads();
+    int tn = t + 1;
+    while (tn < 9 && !tap_live[tn]) ++tn;
+    if (tn < 9) load(tn);  // in flight during this tap's MFMAs
     const int arow = 32 * ph + (lane & 31), kh = lane >> 5;
 #pragma unroll 8
     for (int kk = 0; kk < GF_CG / 2; ++kk) {
@@ -928,6 +968,7 @@ __global__ __launch_bounds__(256) void gfuse_ring_mfma_kernel(
         acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bv, acc[i], 0, 0, 0);
       }
     }
+    t = tn;
   }
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -962,7 +1003,7 @@ int pf_gfuse_prep(const float* img4, const float* c, int ccs, int n, int H, int 
   const int nring = gf_nring(H, W), nband = gf_nband(H, W);
   float* band = ring + (size_t)n * nring * GF_COUT;
   if (!(side_abl() & 1)) {
-    hipLaunchKernelGGL(gfuse_band_kernel, dim3((nband * GF_CG + 255) / 256, n), dim3(256), 0, st,
+    hipLaunchKernelGGL(gfuse_band_kernel, dim3((nband + GB_POS - 1) / GB_POS, n), dim3(256), 0, st,
                        c, ccs, img4, w1_packed, posfeat_conv_packed_k(3, 3, 3), b1, H, W, mean,
                        rstd, band);
     hipLaunchKernelGGL(gfuse_ring_mfma_kernel, dim3((nring + GR_P - 1) / GR_P, n), dim3(256), 0,
