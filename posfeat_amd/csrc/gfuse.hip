@@ -225,13 +225,9 @@ __global__ __launch_bounds__(2 * GF_COUT) PF_NO_PK_FP32 void gfuse_ring_kernel(
 // taps around p, so per image mean_k = b1_k + w_k . E[x] and var_k =
 // w_k^T (E[x x^T] - E[x] E[x]^T) w_k.  With x extended by a constant 1 (row
 // 27) the moments are one Gram matrix G = X^T X of the [HW x 32] im2col
-// matrix X: G[27][j] = sum x_j, G[i][j] = sum x_i x_j.  X^T X runs on the
-// matrix cores with the SAME registers as A and B operand: round 3, one
-// fp32 v_mfma_f32_32x32x2_f32 per pixel pair (lane l: x_{l%32} of pixel
-// 2s + l/32); round 6, bf16x6 over 16 pixels per step (four
-// v_mfma_f32_32x32x16_bf16: fp32-exact products, 2.7x the fp32 MFMA's
-// rate; the image branch runs beside the main stream and slows it about one
-// for one).  gfuse_imgmom_kernel:
+// matrix X: G[27][j] = sum x_j, G[i][j] = sum x_i x_j.  X^T X on fp32 MFMA is
+// one v_mfma_f32_32x32x2_f32 per pixel PAIR whose A and B operands are the
+// SAME register (lane l: x_{l%32} of pixel 2s + l/32).  gfuse_imgmom_kernel:
 // one block per band of 4 rows (staged in LDS), each wave a quarter of the
 // band's pixel pairs; the four 32x32 accumulators are summed into an fp64
 // band partial.  gfuse_imgstats_kernel sums the band partials in order (fp64)
@@ -252,9 +248,9 @@ __global__ __launch_bounds__(256) void gfuse_imgmom_kernel(const float* __restri
   // a block walks bands blockIdx.x, + gridDim.x, ...: each band's fp32 MFMA sum
   // is added into per-lane fp64 totals (the per-band rounding of one band /
   // block; few blocks leave the CUs to the main stream's kernels)
-  double tot[16], totx[16];
+  double tot[16];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) tot[r] = totx[r] = 0.0;
+  for (int r = 0; r < 16; ++r) tot[r] = 0.0;
   for (int band = blockIdx.x; band < nband; band += gridDim.x) {
   const int r0 = band * IM_ROWS;
   pf_syncthreads();  // the previous band's tile is consumed
@@ -275,78 +271,43 @@ __global__ __launch_bounds__(256) void gfuse_imgmom_kernel(const float* __restri
   const int off = i < IM_TAPS ? ((ti / 3) * TW + ti % 3) * 3 + ci : 0;
   const float cst = i == IM_TAPS ? 1.f : 0.f;
   const bool tap = i < IM_TAPS;
-  // wave w owns output row r0 + w.  16 pixels per step on the bf16 matrix
-  // cores: lane l holds tap l % 32 of pixels 8 (l / 32) .. + 8 as three bf16
-  // planes (h + m + l = x exactly), and A = B = those operands give
-  // sum_p x_i x_j over the 16 pixels.  The six bf16x6 products hh, mm,
-  // hm, mh, hl, lh in four MFMAs: the Gram is symmetric, so mh + lh is the
-  // transpose of X = hm + hl, added when the block's partial is written
-  // (S = hh + mm + X + X^T).  A ragged row end (W % 16) takes the fp32 MFMA
-  // pixel pairs of round 3.
-  static_assert(IM_G * IM_G % 256 == 0, "Gram entries per thread");
-  f32x16 sym, xx, acc0;
+  // wave w owns output row r0 + w; two interleaved accumulator chains so
+  // consecutive MFMAs do not wait on each other
+  f32x16 acc0, acc1;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) sym[r] = xx[r] = acc0[r] = 0.f;
+  for (int r = 0; r < 16; ++r) acc0[r] = acc1[r] = 0.f;
   if (r0 + wave < H) {
-    const float* trow = tile + wave * TW * 3 + off + (lane >> 5) * 8 * 3;
+    const float* trow = tile + wave * TW * 3 + off + (lane >> 5) * 3;
     int s = 0;
-    for (; s + 16 <= W; s += 16) {
-      f32x4 p0, p1;
+    for (; s + 8 <= W / 2; s += 8) {
+      float v[8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        p0[u] = tap ? trow[(s + u) * 3] : cst;
-        p1[u] = tap ? trow[(s + 4 + u) * 3] : cst;
+      for (int u = 0; u < 8; ++u) v[u] = tap ? trow[(2 * (s + u)) * 3] : cst;
+#pragma unroll
+      for (int u = 0; u < 8; u += 2) {
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(v[u], v[u], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(v[u + 1], v[u + 1], acc1, 0, 0, 0);
       }
-      g6_u32x4 h, m, l;
-      g6_split(p0, p1, h, m, l);
-      sym = g6_mfma(h, h, sym);
-      xx = g6_mfma(h, m, xx);
-      sym = g6_mfma(m, m, sym);
-      xx = g6_mfma(h, l, xx);
     }
-    const float* prow = tile + wave * TW * 3 + off + (lane >> 5) * 3;
-    for (; s < W; s += 2) {  // pixel pairs (W even)
-      const float v = tap ? prow[s * 3] : cst;
+    for (; s < W / 2; ++s) {
+      const float v = tap ? trow[(2 * s) * 3] : cst;
       acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(v, v, acc0, 0, 0, 0);
     }
   }
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    tot[r] += (double)sym[r] + (double)acc0[r];
-    totx[r] += (double)xx[r];
+  for (int r = 0; r < 16; ++r) tot[r] += (double)acc0[r] + (double)acc1[r];
   }
-  }
-  pf_syncthreads();  // the tile is dead: reuse LDS for the wave sums
-  double* red = reinterpret_cast<double*>(tile);  // [4 waves][32][32]: S, then X
-  constexpr int EPT = IM_G * IM_G / 256;            // entries per thread
-  double v[EPT];
+  pf_syncthreads();  // the tile is dead: reuse LDS for the wave sum
+  double* red = reinterpret_cast<double*>(tile);  // [4 waves][32][32]
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int gi = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5), gj = lane & 31;
     red[(wave * IM_G + gi) * IM_G + gj] = tot[r];
   }
   pf_syncthreads();
-#pragma unroll
-  for (int u = 0; u < EPT; ++u) {
-    const int e = threadIdx.x + 256 * u;
-    v[u] = (red[e] + red[IM_G * IM_G + e]) + (red[2 * IM_G * IM_G + e] + red[3 * IM_G * IM_G + e]);
-  }
-  pf_syncthreads();
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int gi = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5), gj = lane & 31;
-    red[(wave * IM_G + gi) * IM_G + gj] = totx[r];
-  }
-  pf_syncthreads();
-#pragma unroll
-  for (int u = 0; u < EPT; ++u) {
-    const int e = threadIdx.x + 256 * u;
-    const int gi = e / IM_G, gj = e - gi * IM_G, et = gj * IM_G + gi;
-    const double x = (red[e] + red[IM_G * IM_G + e]) + (red[2 * IM_G * IM_G + e] + red[3 * IM_G * IM_G + e]);
-    const double xt = (red[et] + red[IM_G * IM_G + et]) +
-                      (red[2 * IM_G * IM_G + et] + red[3 * IM_G * IM_G + et]);
-    part[((long long)b * gridDim.x + blockIdx.x) * IM_G * IM_G + e] = v[u] + (x + xt);
-  }
+  for (int e = threadIdx.x; e < IM_G * IM_G; e += blockDim.x)
+    part[((long long)b * gridDim.x + blockIdx.x) * IM_G * IM_G + e] =
+        (red[e] + red[IM_G * IM_G + e]) + (red[2 * IM_G * IM_G + e] + red[3 * IM_G * IM_G + e]);
 }
 
 // one block per image, one thread per Gram entry: sum the band partials
