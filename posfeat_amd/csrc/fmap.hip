@@ -372,7 +372,7 @@ __global__ void norm_prelu_upsample_kernel(const float* __restrict__ x, int n, i
 // contiguous range of pixel pairs (its image's mean / rstd reloaded only when
 // the range crosses an image), HT_U steps per pass with all their loads issued
 // before the first reduction.  Same per-pixel arithmetic and order.
-constexpr int HT_U = 4;
+template <int HT_U, bool NT>
 __global__ void head_tail_conv3_kernel(const float* __restrict__ x, int n, int hw, int cs,
                                        const float* __restrict__ mean,
                                        const float* __restrict__ rstd,
@@ -397,7 +397,8 @@ __global__ void head_tail_conv3_kernel(const float* __restrict__ x, int n, int h
 #pragma unroll
     for (int u = 0; u < HT_U; ++u) {
       const long long p = min(2 * min(q + u, q1 - 1) + half, total - 1);  // clamped: in bounds
-      xv[u] = *reinterpret_cast<const f32x4*>(x + p * cs + l32 * 4);
+      const f32x4* src = reinterpret_cast<const f32x4*>(x + p * cs + l32 * 4);
+      xv[u] = NT ? __builtin_nontemporal_load(src) : *src;
     }
     float s[HT_U];
 #pragma unroll
@@ -614,11 +615,31 @@ int pf_head_tail(const float* x, int n, int hw, int cs, const float* mean, const
                  const float* slope, const float* w3, const float* b3, float* yraw, float* out,
                  float* mean1, float* rstd1, double* part, hipStream_t st) {
   const long long total = (long long)n * hw;
+  // A/B (POSFEAT_TAIL=<u><n>, A/B build): u pixel pairs per wave step in
+  // flight (default 4), n = 1: nontemporal loads (y is read once)
+  static const int ab = [] {
+    const char* e = pf_ab_getenv("POSFEAT_TAIL");
+    return e ? atoi(e) : 40;
+  }();
+  static const int tmax = [] {
+    const char* e = pf_ab_getenv("POSFEAT_TAIL_BLOCKS");
+    return e ? atoi(e) : 8192;
+  }();
   int blocks = (int)((total / 2 + 3) / 4);
-  if (blocks > 8192) blocks = 8192;
+  if (blocks > tmax) blocks = tmax;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(head_tail_conv3_kernel, dim3(blocks), dim3(256), 0, st, x, n, hw, cs, mean,
-                     rstd, slope, w3, b3, yraw);
+  if (ab == 80)
+    hipLaunchKernelGGL((head_tail_conv3_kernel<8, false>), dim3(blocks), dim3(256), 0, st, x, n, hw,
+                       cs, mean, rstd, slope, w3, b3, yraw);
+  else if (ab == 81)
+    hipLaunchKernelGGL((head_tail_conv3_kernel<8, true>), dim3(blocks), dim3(256), 0, st, x, n, hw,
+                       cs, mean, rstd, slope, w3, b3, yraw);
+  else if (ab == 41)
+    hipLaunchKernelGGL((head_tail_conv3_kernel<4, true>), dim3(blocks), dim3(256), 0, st, x, n, hw,
+                       cs, mean, rstd, slope, w3, b3, yraw);
+  else
+    hipLaunchKernelGGL((head_tail_conv3_kernel<4, false>), dim3(blocks), dim3(256), 0, st, x, n, hw,
+                       cs, mean, rstd, slope, w3, b3, yraw);
   PF_CHECK_LAUNCH();
   PF_TRY(pf_in_stats(yraw, n, hw, 1, 1, mean1, rstd1, part, st));
   if (hw % 4 == 0 && ((reinterpret_cast<uintptr_t>(yraw) | reinterpret_cast<uintptr_t>(out)) & 15) == 0)
