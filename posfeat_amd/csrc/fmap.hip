@@ -616,10 +616,12 @@ int pf_head_tail(const float* x, int n, int hw, int cs, const float* mean, const
                  float* mean1, float* rstd1, double* part, hipStream_t st) {
   const long long total = (long long)n * hw;
   // A/B (POSFEAT_TAIL=<u><n>, A/B build): u pixel pairs per wave step in
-  // flight (default 4), n = 1: nontemporal loads (y is read once)
+  // flight, n = 1: nontemporal loads (y is read once).  Default 41 (r16i,
+  // same box, B = 32: 40 1.091, 41 1.031, 80 1.493, 81 1.338 ms for the
+  // tail; 8192 / 16384 / 32768 blocks at 40: 1.091 / 1.073 / 1.053)
   static const int ab = [] {
     const char* e = pf_ab_getenv("POSFEAT_TAIL");
-    return e ? atoi(e) : 40;
+    return e ? atoi(e) : 41;
   }();
   static const int tmax = [] {
     const char* e = pf_ab_getenv("POSFEAT_TAIL_BLOCKS");

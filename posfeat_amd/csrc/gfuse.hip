@@ -1029,10 +1029,17 @@ int pf_gfuse_imgstats(const float* img4, int n, int H, int W, const float* w1_pa
                               (size_t)4 * IM_G * IM_G * sizeof(double));
   if (lds > 160 * 1024 || W % 2) return POSFEAT_E_UNSUPPORTED;
   double* part = static_cast<double*>(ws);
+  // blocks per image (A/B POSFEAT_IMGMOM_BPI; default one per band): a
+  // block walks bands blockIdx.x, + gridDim.x, ...
+  static const int bpi = [] {
+    const char* e = pf_ab_getenv("POSFEAT_IMGMOM_BPI");
+    return e ? atoi(e) : 0;
+  }();
+  const int nblk = bpi > 0 && bpi < nband ? bpi : nband;
   if (!(side_abl() & 2))
-    hipLaunchKernelGGL(gfuse_imgmom_kernel, dim3(nband, n), dim3(256), lds, st, img4, H, W, part);
+    hipLaunchKernelGGL(gfuse_imgmom_kernel, dim3(nblk, n), dim3(256), lds, st, img4, H, W, part);
   PF_CHECK_LAUNCH();
-  hipLaunchKernelGGL(gfuse_imgstats_kernel, dim3(n), dim3(IM_G * IM_G), 0, st, part, nband, H * W,
+  hipLaunchKernelGGL(gfuse_imgstats_kernel, dim3(n), dim3(IM_G * IM_G), 0, st, part, nblk, H * W,
                      w1_packed, posfeat_conv_packed_k(3, 3, 3), b1, 1e-5f, mean, rstd, gram);
   PF_CHECK_LAUNCH();
   return POSFEAT_OK;
