@@ -2325,7 +2325,8 @@ enum ConvTile {
   TILE_BF6B_256x128 = 28,  // pre-split weights, 8 waves stacked along M (one 135-KB block per CU)
   TILE_BF6X_128x128 = 29, TILE_BF6X_128x64 = 30,  // dense, 16x16x32 MFMAs (conv_bf6x_kernel)
   TILE_BF6X_256x128 = 31,
-  TILE_BF6X_128x192 = 32  // N % 192 == 0 (head.conv1's Winograd GEMMs, the tap GEMM): A read once per 192 columns
+  TILE_BF6X_128x192 = 32,  // N % 192 == 0 (head.conv1's Winograd GEMMs, the tap GEMM): A read once per 192 columns
+  TILE_BF6X_128x256 = 33   // N % 256 == 0 batched GEMMs (A/B POSFEAT_BF6X_N256: A read once per 256 columns)
 };
 
 // POSFEAT_BF6=1: every conv the row-tile DMA kernel serves (1x1, strided, the
@@ -2462,7 +2463,7 @@ Plan plan_for_tile(const ConvArgs& a, int tile) {
   if (bf6_on() && glds_ok) {
     // pre-split convs on the bf6x tiles (dense GEMMs, slab x tap gathers):
     // the 16x16x32 tiles only, and only they
-    const bool x_tile = tile >= TILE_BF6X_128x128 && tile <= TILE_BF6X_128x192;
+    const bool x_tile = tile >= TILE_BF6X_128x128 && tile <= TILE_BF6X_128x256;
     if (bf6x_on() && (dense_gemm(a) || gt_gemm(a))) {
       if (!x_tile) return p;
     } else {
@@ -2476,12 +2477,17 @@ Plan plan_for_tile(const ConvArgs& a, int tile) {
     case TILE_BF6X_128x64:
     case TILE_BF6X_256x128:
     case TILE_BF6X_128x192:
+    case TILE_BF6X_128x256:
       if (!bf6x_on() || !((glds_ok && (dense_gemm(a) || gt_gemm(a))) || g4_gemm(a))) return p;
       if (g4_gemm(a) && tile != TILE_BF6X_128x64) return p;
       if (tile == TILE_BF6X_128x192 && (!dense_gemm(a) || a.Cout % 192)) return p;
+      if (tile == TILE_BF6X_128x256 && (!dense_gemm(a) || a.Cout % 256)) return p;
       p.kern = KERN_GLDS;
       p.bm = tile == TILE_BF6X_256x128 ? 256 : 128;
-      p.bn = tile == TILE_BF6X_128x64 ? 64 : tile == TILE_BF6X_128x192 ? 192 : 128;
+      p.bn = tile == TILE_BF6X_128x64    ? 64
+             : tile == TILE_BF6X_128x192 ? 192
+             : tile == TILE_BF6X_128x256 ? 256
+                                         : 128;
       p.ppi = 0;
       p.tiles_m = (a.M + p.bm - 1) / p.bm;
       return p;
@@ -2699,6 +2705,10 @@ int conv_run(ConvArgs& a, const Plan& p, hipStream_t st) {
       break;
     case TILE_BF6X_128x192:  // dense GEMMs only (plan_for_tile)
       hipLaunchKernelGGL((conv_bf6x_kernel<192>), dim3(a.nwg * a.ksplit, a.nbatch), dim3(256), 0,
+                         st, a);
+      break;
+    case TILE_BF6X_128x256:  // dense GEMMs only (plan_for_tile)
+      hipLaunchKernelGGL((conv_bf6x_kernel<256>), dim3(a.nwg * a.ksplit, a.nbatch), dim3(256), 0,
                          st, a);
       break;
     case TILE_BF6X_256x128:
@@ -3037,7 +3047,7 @@ int pf_conv_run_tile_bn(const posfeat_conv_desc* d, const float* x, const float*
     a.part = static_cast<float*>(ws);
   } else if (part && p.tiles_m * 2 * (size_t)a.Cout * sizeof(double) <= part_bytes &&
              p.tiles_m <= 0x7fffffff &&
-             !(p.tile >= TILE_BF6X_128x128 && p.tile <= TILE_BF6X_128x192)) {
+             !(p.tile >= TILE_BF6X_128x128 && p.tile <= TILE_BF6X_128x256)) {
     a.bnpart = part;
     *nparts = (int)p.tiles_m;
   }
@@ -3333,7 +3343,14 @@ int pf_gemm_batched(const float* A, int lda, long long sa, const float* B, long 
   }();
   // N = 192 (head.conv1): one 192-wide column tile reads A once (three
   // 64-wide tiles read it three times)
-  const int want = x ? (N % 128 == 0 ? (rb4 ? TILE_BF6X_256x128 : TILE_BF6X_128x128)
+  // POSFEAT_BF6X_N256=1 (A/B): one 256-wide column tile for N % 256 == 0
+  // (the decoder's Winograd GEMMs: A read once per 256 columns, not twice)
+  static const bool n256 = [] {
+    const char* e = pf_ab_getenv("POSFEAT_BF6X_N256");
+    return e && e[0] == '1';
+  }();
+  const int want = x ? (n256 && N % 256 == 0 ? TILE_BF6X_128x256
+                        : N % 128 == 0 ? (rb4 ? TILE_BF6X_256x128 : TILE_BF6X_128x128)
                         : N % 192 == 0 ? TILE_BF6X_128x192
                                        : TILE_BF6X_128x64)
                    : (Bb && b256 && N % 128 == 0) ? TILE_BF6B_256x128
