@@ -848,7 +848,7 @@ void plan(posfeat_model* m) {
     const char* e = pf_ab_getenv("POSFEAT_SIDE");
     m->side = !(e && e[0] == '0') && m->up4 && m->gfuse && (!m->train || m->traintap);
     const char* a = pf_ab_getenv("POSFEAT_SIDE_AT");
-    m->side_at = a ? std::min(3, std::max(0, atoi(a))) : 2;
+    m->side_at = a ? std::min(4, std::max(0, atoi(a))) : 2;
   }
   if (m->up4) {
     if (!m->imgstats) alloc(m->g64, B * H * W * 64);
@@ -1104,7 +1104,8 @@ int forward(Ctx& c, const float* img, posfeat_extract_out* out, int mode, const 
                     (c.dry || ((m->tuned_modes >> mode) & 1u) || !m->autotune);
   // where the image branch forks (POSFEAT_SIDE_AT): 0 after the image layout,
   // 1 before layer2, 2 before layer3 (default: the 60x80 layers underfill the
-  // chip; overlapping layer1 slowed its convs 2-4x), 3 before the decoder
+  // chip; overlapping layer1 slowed its convs 2-4x), 3 before the decoder,
+  // 4 before the head (beside head.conv1 and the tap GEMM)
   const int side_at = mode == MODE_HEAD ? 0 : m->side_at;
   if (side && side_at == 0) PF_TRY(image_branch(c, img4));
   if (mode == MODE_HEAD) {
@@ -1138,6 +1139,7 @@ int forward(Ctx& c, const float* img, posfeat_extract_out* out, int mode, const 
   PF_TRY(conv3x3(c, "iconv2", cat2, B, h4, w4, 512, c.f(m->d2), 256, POSFEAT_ACT_ELU));
   PF_TRY(conv(c, "conv_fine", c.f(m->d2), B, h4, w4, 256, headcat, 192, 1, POSFEAT_ACT_ELU));
   }
+  if (side && side_at == 4 && mode != MODE_HEAD) PF_TRY(image_branch(c, img4));
   if (mode != MODE_BACKBONE) PF_TRY(head_forward(c, img4, out->local_point, side));
   // ---- outputs -------------------------------------------------------------
   if (mode != MODE_HEAD) {
