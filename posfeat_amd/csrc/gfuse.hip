@@ -55,32 +55,14 @@ __global__ __launch_bounds__(128) void gfuse_weights_kernel(
   const float* mb = mean + (size_t)b * GF_CG;
   const float* rb = rstd + (size_t)b * GF_CG;
   const float* w2r = w2 + (size_t)co * k2pad;
-  // staged with every load of a thread issued before its LDS stores (128
-  // threads: 5 W2 terms and 18 W1 entries each)
-  {
-    float av[5], wv[18];
-#pragma unroll
-    for (int u = 0; u < 5; ++u) {
-      const int i = min(e + 128 * u, 9 * GF_CG - 1);
-      const int t = i / GF_CG, k = i - t * GF_CG;
-      const int ci = GF_CL + k;  // W2 packed K index of channel 192 + k, tap t
-      av[u] = w2r[((ci >> 5) * 9 + t) * 32 + (ci & 31)] * rb[k];
-    }
-#pragma unroll
-    for (int u = 0; u < 18; ++u) {
-      const int i = e + 128 * u, k = i / 36, j = i - k * 36;
-      wv[u] = w1[(size_t)k * k1pad + j];
-    }
-#pragma unroll
-    for (int u = 0; u < 5; ++u) {
-      const int i = e + 128 * u;
-      if (i < 9 * GF_CG) a_s[i / GF_CG][i % GF_CG] = av[u];
-    }
-#pragma unroll
-    for (int u = 0; u < 18; ++u) {
-      const int i = e + 128 * u;
-      w1_s[i / 36][i % 36] = wv[u];
-    }
+  for (int i = e; i < 9 * GF_CG; i += blockDim.x) {
+    const int t = i / GF_CG, k = i - t * GF_CG;
+    const int ci = GF_CL + k;  // W2 packed K index of channel 192 + k, tap t
+    a_s[t][k] = w2r[((ci >> 5) * 9 + t) * 32 + (ci & 31)] * rb[k];
+  }
+  for (int i = e; i < GF_CG * 36; i += blockDim.x) {
+    const int k = i / 36, j = i - k * 36;
+    w1_s[k][j] = w1[(size_t)k * k1pad + j];
   }
   if (e < GF_CG) d_s[e] = b1[e] - mb[e];
   __syncthreads();
@@ -272,32 +254,15 @@ __global__ __launch_bounds__(256) void gfuse_imgmom_kernel(const float* __restri
   for (int band = blockIdx.x; band < nband; band += gridDim.x) {
   const int r0 = band * IM_ROWS;
   pf_syncthreads();  // the previous band's tile is consumed
-  // the band's pixels in batches of IM_LB per thread, every load of a batch
-  // issued before the first LDS write (one load -> wait -> write per pixel
-  // had serialised ~15 global-memory latencies per thread per band)
-  constexpr int IM_LB = 16;
-  const int npix = (IM_ROWS + 2) * TW;
-  for (int i0 = 0; i0 < npix; i0 += IM_LB * 256) {
-    f32x4 v[IM_LB];
-#pragma unroll
-    for (int u = 0; u < IM_LB; ++u) {
-      const int i = i0 + threadIdx.x + 256 * u;
-      const int ty = i / TW, tx = i - ty * TW;
-      const int y = r0 - 1 + ty, x = tx - 1;
-      const bool ok = i < npix && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
-      const f32x4 t = *reinterpret_cast<const f32x4*>(
-          ib + ((long long)min(max(y, 0), H - 1) * W + min(max(x, 0), W - 1)) * 4);
-      v[u] = ok ? t : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-#pragma unroll
-    for (int u = 0; u < IM_LB; ++u) {
-      const int i = i0 + threadIdx.x + 256 * u;
-      if (i < npix) {
-        tile[i * 3] = v[u].x;
-        tile[i * 3 + 1] = v[u].y;
-        tile[i * 3 + 2] = v[u].z;
-      }
-    }
+  for (int i = threadIdx.x; i < (IM_ROWS + 2) * TW; i += blockDim.x) {
+    const int ty = i / TW, tx = i - ty * TW;
+    const int y = r0 - 1 + ty, x = tx - 1;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W)
+      v = *reinterpret_cast<const f32x4*>(ib + ((long long)y * W + x) * 4);
+    tile[i * 3] = v.x;
+    tile[i * 3 + 1] = v.y;
+    tile[i * 3 + 2] = v.z;
   }
   pf_syncthreads();
   // this lane's moment index i = lane % 32: tap (ky, kx), channel c, or 27: 1
