@@ -851,56 +851,62 @@ __global__ __launch_bounds__(256) void wino6_input_kernel(const float* __restric
 }
 
 // y = act(A^T M A + bias) for the 6x6 outputs of each tile inside the map
+template <int VW>
 __global__ __launch_bounds__(256) void wino6_output_kernel(const float* __restrict__ M, int n,
-                                                           int h, int w, int c2n,
+                                                           int h, int w, int cvn,
                                                            const float* __restrict__ bias, int act,
                                                            float* __restrict__ y, int ycs) {
+  typedef typename W6Vec<VW>::t TV;
   const int th = (h + 5) / 6, tw = (w + 5) / 6;
   const long long T = (long long)n * th * tw;
-  const long long total = T * c2n;
-  const int C = c2n * 2;
+  const long long total = T * cvn;
+  const int C = cvn * VW;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
     int q, tx, ty;
-    const int b = pf_tile_split(i, c2n, tw, th, q, tx, ty);
+    const int b = pf_tile_split(i, cvn, tw, th, q, tx, ty);
     const long long tile = ((long long)b * th + ty) * tw + tx;
-    const float* mi = M + tile * C + q * 2;
+    const float* mi = M + tile * C + q * VW;
     const long long xs = T * C;
-    f32x2 s[6][8];  // A^T M
+    TV s[6][8];  // A^T M
 #pragma unroll
     for (int a = 0; a < 6; ++a)
 #pragma unroll
-      for (int c = 0; c < 8; ++c) s[a][c] = f32x2{0.f, 0.f};
+      for (int c = 0; c < 8; ++c) s[a][c] = TV(0.f);
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
-      f32x2 m[8];
+      TV m[8];
 #pragma unroll
-      for (int c = 0; c < 8; ++c) m[c] = *reinterpret_cast<const f32x2*>(mi + (r * 8 + c) * xs);
+      for (int c = 0; c < 8; ++c) m[c] = *reinterpret_cast<const TV*>(mi + (r * 8 + c) * xs);
 #pragma unroll
       for (int a = 0; a < 6; ++a)
         if (W6_AT[a][r] != 0.f)
 #pragma unroll
           for (int c = 0; c < 8; ++c) s[a][c] += W6_AT[a][r] * m[c];
     }
-    f32x2 bv = {0.f, 0.f};
-    if (bias) bv = *reinterpret_cast<const f32x2*>(bias + q * 2);
+    TV bv = TV(0.f);
+    if (bias) bv = *reinterpret_cast<const TV*>(bias + q * VW);
 #pragma unroll
     for (int a = 0; a < 6; ++a) {
       const int oy = 6 * ty + a;
 #pragma unroll
       for (int bb = 0; bb < 6; ++bb) {
         const int ox = 6 * tx + bb;
-        f32x2 o = bv;
+        TV o = bv;
 #pragma unroll
         for (int c = 0; c < 8; ++c)
           if (W6_AT[bb][c] != 0.f) o += W6_AT[bb][c] * s[a][c];
+        if constexpr (VW == 1) {
+          o = act == POSFEAT_ACT_RELU ? fmaxf(o, 0.f) : act == POSFEAT_ACT_ELU ? pf_elu(o) : o;
+        } else {
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const float v = o[j];
-          o[j] = act == POSFEAT_ACT_RELU ? fmaxf(v, 0.f) : act == POSFEAT_ACT_ELU ? pf_elu(v) : v;
+          for (int j = 0; j < VW; ++j) {
+            const float v = o[j];
+            o[j] = act == POSFEAT_ACT_RELU ? fmaxf(v, 0.f) : act == POSFEAT_ACT_ELU ? pf_elu(v) : v;
+          }
         }
         if (oy < h && ox < w)
-          *reinterpret_cast<f32x2*>(y + (((long long)b * h + oy) * w + ox) * ycs + q * 2) = o;
+          *reinterpret_cast<TV*>(y + (((long long)b * h + oy) * w + ox) * ycs + q * VW) = o;
       }
     }
   }
@@ -1035,6 +1041,23 @@ int pf_wino6_weights(const float* wpk, int Cout, int Cin, float* U, hipStream_t 
   return POSFEAT_OK;
 }
 
+// POSFEAT_W6IN_VW1=1 (A/B): the plain F(6x6) input transform one channel per
+// thread (232 -> fewer VGPRs: two waves per SIMD -> more) instead of pairs
+static bool w6out_vw1() {
+  static const bool v = [] {
+    const char* e = pf_ab_getenv("POSFEAT_W6OUT_VW1");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+static bool w6in_vw1() {
+  static const bool v = [] {
+    const char* e = pf_ab_getenv("POSFEAT_W6IN_VW1");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
 // planes 1: U holds the bf16 planes of pf_wino6_weights(.., planes = true)
 // (Cout % 64 == 0), the GEMM splits V on the fly; 0: fp32 U.  up2: x is the
 // (h/2, w/2) map, h and w even.
@@ -1054,6 +1077,9 @@ int pf_wino6_conv(const float* x, int xcs, int n, int h, int w, int Cin, const f
     if (up2)
       hipLaunchKernelGGL((wino6_input_kernel<true, 1>), dim3(grid_for(T * Cin, 256)), dim3(256), 0,
                          st, x, xcs, n, h, w, Cin, V);
+    else if (w6in_vw1())  // A/B: one channel per thread (fewer VGPRs, more waves)
+      hipLaunchKernelGGL((wino6_input_kernel<false, 1>), dim3(grid_for(T * Cin, 256)), dim3(256),
+                         0, st, x, xcs, n, h, w, Cin, V);
     else
       hipLaunchKernelGGL((wino6_input_kernel<false, 2>), dim3(grid_for(T * (Cin / 2), 256)),
                          dim3(256), 0, st, x, xcs, n, h, w, Cin / 2, V);
@@ -1065,8 +1091,12 @@ int pf_wino6_conv(const float* x, int xcs, int n, int h, int w, int Cin, const f
     PF_TRY(pf_gemm_batched(V, Cin, T * Cin, U, (long long)Cout * Cin, M, Cout, T * Cout, 64, (int)T,
                            Cout, Cin, st, Ub, 64LL * Cout * Cin));
   if (stages & 4) {
-    hipLaunchKernelGGL(wino6_output_kernel, dim3(grid_for(T * (Cout / 2), 256)), dim3(256), 0, st,
-                       M, n, h, w, Cout / 2, bias, act, y, ycs);
+    if (w6out_vw1())  // A/B: one channel per thread
+      hipLaunchKernelGGL((wino6_output_kernel<1>), dim3(grid_for(T * Cout, 256)), dim3(256), 0, st,
+                         M, n, h, w, Cout, bias, act, y, ycs);
+    else
+      hipLaunchKernelGGL((wino6_output_kernel<2>), dim3(grid_for(T * (Cout / 2), 256)), dim3(256),
+                         0, st, M, n, h, w, Cout / 2, bias, act, y, ycs);
     PF_CHECK_LAUNCH();
   }
   return POSFEAT_OK;
