@@ -1041,19 +1041,24 @@ int pf_wino6_weights(const float* wpk, int Cout, int Cin, float* U, hipStream_t 
   return POSFEAT_OK;
 }
 
-// POSFEAT_W6IN_VW1=1 (A/B): the plain F(6x6) input transform one channel per
-// thread (232 -> fewer VGPRs: two waves per SIMD -> more) instead of pairs
+// The F(6x6) transforms one channel per thread (default, r16m) or channel
+// pairs (POSFEAT_W6IN_VW1=0 / POSFEAT_W6OUT_VW1=0, A/B): the pair forms held
+// 232 / 176 VGPRs (two waves per SIMD), the single-channel ones 111 / 104
+// (four).  Same box, B = 32: output transforms 0.353 -> 0.322 ms
+// (upconv2 / iconv2), 0.194 -> 0.163 (iconv3); the plain input transform
+// 0.663 -> 0.654, 0.355 -> 0.345; bench 1299.0 -> 1308.1 img/s.  The same
+// fma per channel: bit-identical.
 static bool w6out_vw1() {
   static const bool v = [] {
     const char* e = pf_ab_getenv("POSFEAT_W6OUT_VW1");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
   }();
   return v;
 }
 static bool w6in_vw1() {
   static const bool v = [] {
     const char* e = pf_ab_getenv("POSFEAT_W6IN_VW1");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
   }();
   return v;
 }
