@@ -883,11 +883,20 @@ int pf_up4tap_gcombine(int n, int H, int W, const float* P, const float* img4,
 // (n x H x W x 128, pitch dycs): dL/dP.  H, W % 16 == 0.
 int pf_up4tap_adjoint(int n, int H, int W, const float* dy, int dycs, float* D, hipStream_t st) {
   const int h = H / 4, w = W / 4;
-  constexpr int TQA = 4;
   if (H % 16 || W % 16 || dycs % 4 || n <= 0) return POSFEAT_E_INVALID;
-  const long long nb = (long long)n * ((h + TQA - 1) / TQA) * ((w + 7) / 8);
-  hipLaunchKernelGGL(up4tap_adjoint_kernel<TQA>, dim3((unsigned)nb), dim3(256), 0, st, dy, dycs, h,
-                     w, D);
+  // low-res rows per block (A/B POSFEAT_ADJ_TQ=2: 2 -- fewer accumulators,
+  // more waves per SIMD, more dy rows re-read; default 4)
+  static const int tq = [] {
+    const char* e = pf_ab_getenv("POSFEAT_ADJ_TQ");
+    return e && e[0] == '2' ? 2 : 4;
+  }();
+  const long long nb = (long long)n * ((h + tq - 1) / tq) * ((w + 7) / 8);
+  if (tq == 2)
+    hipLaunchKernelGGL(up4tap_adjoint_kernel<2>, dim3((unsigned)nb), dim3(256), 0, st, dy, dycs, h,
+                       w, D);
+  else
+    hipLaunchKernelGGL(up4tap_adjoint_kernel<4>, dim3((unsigned)nb), dim3(256), 0, st, dy, dycs, h,
+                       w, D);
   PF_CHECK_LAUNCH();
   return POSFEAT_OK;
 }
