@@ -6,15 +6,18 @@
 //   K1 det_mask    : reflect-padded NMS with the first-occurrence tie rule,
 //                    threshold, order-preserving uint32 key of the masked
 //                    score; survivors compacted (wave ballot + one atomic per
-//                    block) into a per-image candidate list, whose length is
-//                    the survivor count
+//                    block, four pixels per thread) into a per-image
+//                    candidate list, whose length is the survivor count
 //   K2 det_select  : one workgroup per image -- n = clamp(min count), 4-pass
 //                    8-bit radix select of the n-th largest key over the
 //                    candidates only (masked-out cells are counted, not
-//                    read); keys == T resolved by smallest index
+//                    read; 16 loads in flight per thread, the digit from a
+//                    parallel suffix scan); keys == T resolved by smallest
+//                    index
 //   K3 det_rank    : rank each selected cell by (key desc, index asc) with an
-//                    LDS-tiled counting sort (n^2 compares, exact; the
-//                    selected list may be in any order), compute the 3x3
+//                    LDS-tiled counting sort (n^2 compares, exact, eight
+//                    entries per step; the selected list may be in any
+//                    order), compute the 3x3
 //                    soft-argmax refine and 3x3 max score and scatter to the
 //                    output row = rank
 // Everything is integer/compare work, so the result is bit-exact and
@@ -107,42 +110,69 @@ __global__ void nms_mask_kernel(const float* __restrict__ score, int h, int w, i
   }
 }
 
-__global__ void det_mask_kernel(const float* __restrict__ kp, int h, int w, int r, int use_nms,
-                                int use_thr, const float* __restrict__ thr_t,
-                                uint32_t* __restrict__ keys, uint32_t* __restrict__ cand_key,
-                                int32_t* __restrict__ cand_idx, int32_t* __restrict__ counts) {
+// PX pixels per thread (p = base + k * 1024 + tid): the PX decisions' loads
+// are independent and go out together, one LDS atomic per wave and one
+// global atomic per block cover all PX * 1024 pixels.  With one pixel per
+// thread (PX = 1, A/B: POSFEAT_DET_PX=1) each 1024-pixel block paid a chain
+// of load -> compare -> LDS atomic -> barrier -> global atomic -> barrier
+// latencies for its 1024 pixels (112 us for 32 x 478 x 638 cells, r16n).
+template <int PX>
+__global__ __launch_bounds__(1024) void det_mask_kernel(const float* __restrict__ kp, int h, int w,
+                                                        int r, int use_nms, int use_thr,
+                                                        const float* __restrict__ thr_t,
+                                                        uint32_t* __restrict__ keys,
+                                                        uint32_t* __restrict__ cand_key,
+                                                        int32_t* __restrict__ cand_idx,
+                                                        int32_t* __restrict__ counts) {
   const int b = blockIdx.y;  // one image per grid row: block-uniform counter
   const int Hi = h - 2, Wi = w - 2, P = Hi * Wi;
   const float* m = kp + (long long)b * h * w;
   const float t = use_thr ? thr_t[b] : 0.f;
-  __shared__ uint32_t s_key[1024];
-  __shared__ int32_t s_idx[1024];
+  __shared__ uint32_t s_key[PX * 1024];
+  __shared__ int32_t s_idx[PX * 1024];
   __shared__ int s_cnt, s_base;
   const int lane = threadIdx.x & 63;
-  const int stride = gridDim.x * blockDim.x;
-  for (int base = blockIdx.x * blockDim.x; base < P; base += stride) {
+  constexpr int CH = PX * 1024;
+  const int stride = gridDim.x * CH;
+  for (int base = blockIdx.x * CH; base < P; base += stride) {
     if (threadIdx.x == 0) s_cnt = 0;
     __syncthreads();
-    const int p = base + threadIdx.x;
-    bool keep = false;
-    uint32_t key = 0x80000000u;
-    if (p < P) {
-      const int i = p / Wi, j = p - (p / Wi) * Wi;
-      const float S = m[(i + 1) * w + j + 1];
-      keep = use_thr ? (S > t) : true;
-      if (keep && use_nms) keep = nms_keep(m, w, Hi, Wi, 1, i, j, r, S);
-      key = pf_fkey(keep ? S : 0.0f);
-      keys[(long long)b * P + p] = key;
+    bool keep[PX];
+    uint32_t key[PX];
+#pragma unroll
+    for (int k = 0; k < PX; ++k) {
+      const int p = base + k * 1024 + threadIdx.x;
+      keep[k] = false;
+      key[k] = 0x80000000u;
+      if (p < P) {
+        const int i = p / Wi, j = p - (p / Wi) * Wi;
+        const float S = m[(i + 1) * w + j + 1];
+        bool kk = use_thr ? (S > t) : true;
+        if (kk && use_nms) kk = nms_keep(m, w, Hi, Wi, 1, i, j, r, S);
+        keep[k] = kk;
+        key[k] = pf_fkey(kk ? S : 0.0f);
+        keys[(long long)b * P + p] = key[k];
+      }
     }
-    // wave-aggregated LDS compaction of the survivors
-    const unsigned long long bal = __ballot(keep);
+    // wave-aggregated LDS compaction of the survivors: one atomic per wave
+    unsigned long long bal[PX];
+    int tot = 0;
+#pragma unroll
+    for (int k = 0; k < PX; ++k) {
+      bal[k] = __ballot(keep[k]);
+      tot += __popcll(bal[k]);
+    }
     int wbase = 0;
-    if (lane == 0 && bal) wbase = atomicAdd(&s_cnt, __popcll(bal));
+    if (lane == 0 && tot) wbase = atomicAdd(&s_cnt, tot);
     wbase = __shfl(wbase, 0, 64);
-    if (keep) {
-      const int o = wbase + __popcll(bal & ((1ull << lane) - 1ull));
-      s_key[o] = key;
-      s_idx[o] = p;
+#pragma unroll
+    for (int k = 0; k < PX; ++k) {
+      if (keep[k]) {
+        const int o = wbase + __popcll(bal[k] & ((1ull << lane) - 1ull));
+        s_key[o] = key[k];
+        s_idx[o] = base + k * 1024 + threadIdx.x;
+      }
+      wbase += __popcll(bal[k]);
     }
     __syncthreads();
     const int cnt = s_cnt;
@@ -201,7 +231,7 @@ __global__ __launch_bounds__(1024) void det_select_kernel(
   __shared__ int hist[256];
   __shared__ int wsum[16];
   __shared__ uint32_t s_prefix;
-  __shared__ int s_krem, s_n, s_taken;
+  __shared__ int s_krem, s_n, s_taken, s_dig, s_above;
   __shared__ int s_eqidx[1024];
   __shared__ int s_eqn;
   const int tid = threadIdx.x;
@@ -232,27 +262,51 @@ __global__ __launch_bounds__(1024) void det_select_kernel(
     const uint32_t prefix = s_prefix;
     if (tid == 0 && nzero > 0 && (ZKEY & pmask) == prefix)
       atomicAdd(&hist[(ZKEY >> shift) & 0xFF], nzero);
-    // four candidates per thread per pass, loads first (a histogram: the
-    // counts do not depend on the order)
+    // DU candidates per thread per round trip, loads first (a histogram: the
+    // counts do not depend on the order; round 5 loaded four, and each pass
+    // was a chain of count / 4096 dependent global-load latencies)
+    constexpr int DU = 16;
     const int bd = blockDim.x;
-    for (int k = tid; k < count; k += 4 * bd) {
-      uint32_t kk[4];
+    for (int k = tid; k < count; k += DU * bd) {
+      uint32_t kk[DU];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) kk[u] = k + u * bd < count ? ck[k + u * bd] : ~pmask;
+      for (int u = 0; u < DU; ++u) kk[u] = k + u * bd < count ? ck[k + u * bd] : ~pmask;
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int u = 0; u < DU; ++u)
         if (k + u * bd < count && (kk[u] & pmask) == prefix)
           atomicAdd(&hist[(kk[u] >> shift) & 0xFF], 1);
     }
     __syncthreads();
-    if (tid == 0) {
-      int krem = s_krem, above = 0, d = 255;
-      for (; d > 0; --d) {
-        if (above + hist[d] >= krem) break;
-        above += hist[d];
+    // the digit: the largest d with S(d) = sum_{d' >= d} hist[d'] >= krem (d = 0
+    // if none), found by threads 0-255 from a suffix scan (the round-5 form
+    // walked the 256 bins serially in one thread: 256 dependent LDS reads per
+    // pass)
+    int hd = 0, sfx = 0;
+    if (tid < 256) {  // waves 0-3: the within-wave suffix sums
+      const int lane = tid & 63;
+      hd = hist[tid];
+      sfx = hd;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_down(sfx, o, 64);
+        if (lane + o < 64) sfx += v;
       }
-      s_krem = krem - above;
-      s_prefix = prefix | ((uint32_t)d << shift);
+      if (lane == 0) wsum[tid >> 6] = sfx;  // the wave's total
+    }
+    __syncthreads();
+    if (tid < 256) {
+      for (int k = (tid >> 6) + 1; k < 4; ++k) sfx += wsum[k];
+      const int krem = s_krem;
+      const int above = sfx - hd;  // S(d + 1)
+      if ((sfx >= krem || tid == 0) && above < krem) {
+        s_dig = tid;
+        s_above = above;
+      }
+    }
+    __syncthreads();
+    if (tid == 0) {
+      s_krem -= s_above;
+      s_prefix = prefix | ((uint32_t)s_dig << shift);
     }
     pmask |= 0xFFu << shift;
     __syncthreads();
@@ -260,16 +314,24 @@ __global__ __launch_bounds__(1024) void det_select_kernel(
   const uint32_t T = s_prefix;
   const int need_eq = s_krem;  // how many keys == T are taken (>= 1)
   if (T > ZKEY) {
-    // (a) every candidate key > T; collect the == T ones
-    for (int k = tid; k < count; k += blockDim.x) {
-      const uint32_t key = ck[k];
-      if (key > T) {
-        const int pos = atomicAdd(&s_taken, 1);
-        so[pos] = ci[k];
-        sko[pos] = key;
-      } else if (key == T) {
-        const int e = atomicAdd(&s_eqn, 1);
-        if (e < 1024) s_eqidx[e] = ci[k];
+    // (a) every candidate key > T; collect the == T ones (keys loaded DU at
+    // a time: the index is read only for the ~n taken ones)
+    constexpr int DU = 8;
+    for (int k0 = tid; k0 < count; k0 += DU * (int)blockDim.x) {
+      uint32_t kk[DU];
+#pragma unroll
+      for (int u = 0; u < DU; ++u) kk[u] = k0 + u * (int)blockDim.x < count ? ck[k0 + u * blockDim.x] : 0u;
+#pragma unroll
+      for (int u = 0; u < DU; ++u) {
+        const int k = k0 + u * blockDim.x;
+        if (kk[u] > T) {  // (0 < T for the padding lanes)
+          const int pos = atomicAdd(&s_taken, 1);
+          so[pos] = ci[k];
+          sko[pos] = kk[u];
+        } else if (kk[u] == T) {
+          const int e = atomicAdd(&s_eqn, 1);
+          if (e < 1024) s_eqidx[e] = ci[k];
+        }
       }
     }
     __syncthreads();
@@ -292,13 +354,18 @@ __global__ __launch_bounds__(1024) void det_select_kernel(
   }
   else if (T == ZKEY) {
     // all positive candidates, then the need_eq lowest-index cells with key ZKEY
-    for (int k = tid; k < count; k += blockDim.x) {
-      const uint32_t key = ck[k];
-      if (key > ZKEY) {
-        const int pos = atomicAdd(&s_taken, 1);
-        so[pos] = ci[k];
-        sko[pos] = key;
-      }
+    constexpr int DU = 8;
+    for (int k0 = tid; k0 < count; k0 += DU * (int)blockDim.x) {
+      uint32_t kk[DU];
+#pragma unroll
+      for (int u = 0; u < DU; ++u) kk[u] = k0 + u * (int)blockDim.x < count ? ck[k0 + u * blockDim.x] : 0u;
+#pragma unroll
+      for (int u = 0; u < DU; ++u)
+        if (kk[u] > ZKEY) {
+          const int pos = atomicAdd(&s_taken, 1);
+          so[pos] = ci[k0 + u * blockDim.x];
+          sko[pos] = kk[u];
+        }
     }
     __syncthreads();
     int taken = s_taken, eq_seen = 0;
@@ -353,21 +420,39 @@ __global__ void det_rank_kernel(const float* __restrict__ kp, int h, int w, int 
   const int32_t* ib = sel + (long long)b * cap;
   const uint32_t myk = active ? kb[t] : 0u;
   const int myi = active ? ib[t] : 0;
-  __shared__ uint32_t tile[1024];
-  __shared__ int32_t tidx[1024];
+  // (key, index) pairs, two per 16-B LDS read; the compare loop reads eight
+  // entries per step with four partial counts (round 5: one dependent LDS
+  // read per entry, 59 us at n = 2048, B = 32)
+  __shared__ uint4 tile[512];
   int rank = 0;
   for (int base = 0; base < n; base += 1024) {
-    for (int k = threadIdx.x; k < 1024; k += blockDim.x) {
-      tile[k] = (base + k < n) ? kb[base + k] : 0u;
-      tidx[k] = (base + k < n) ? ib[base + k] : 0;
+    for (int k = threadIdx.x; k < 512; k += blockDim.x) {
+      const int e0 = base + 2 * k, e1 = e0 + 1;
+      tile[k] = make_uint4(e0 < n ? kb[e0] : 0u, e0 < n ? (uint32_t)ib[e0] : 0u,
+                           e1 < n ? kb[e1] : 0u, e1 < n ? (uint32_t)ib[e1] : 0u);
     }
     __syncthreads();
     const int lim = min(1024, n - base);
     if (active) {
-      for (int k = 0; k < lim; ++k) {
-        const uint32_t o = tile[k];
-        rank += (o > myk) || (o == myk && tidx[k] < myi);
+      int r4[4] = {0, 0, 0, 0};
+      const int full = lim & ~7;
+      for (int k = 0; k < full; k += 8) {
+        uint4 o[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) o[u] = tile[(k >> 1) + u];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          r4[u] += (o[u].x > myk) || (o[u].x == myk && (int)o[u].y < myi);
+          r4[u] += (o[u].z > myk) || (o[u].z == myk && (int)o[u].w < myi);
+        }
       }
+      for (int k = full; k < lim; ++k) {
+        const uint4 o = tile[k >> 1];
+        const uint32_t ok = (k & 1) ? o.z : o.x;
+        const int oi = (int)((k & 1) ? o.w : o.y);
+        r4[0] += (ok > myk) || (ok == myk && oi < myi);
+      }
+      rank += (r4[0] + r4[1]) + (r4[2] + r4[3]);
     }
     __syncthreads();
   }
@@ -457,10 +542,22 @@ int detect_impl(const float* kp_map, int b, int h, int w, int nms_radius, int us
     PF_CHECK_LAUNCH();
   }
   {
-    int g = (P + 1023) / 1024;
+    static const int px = [] {  // A/B: POSFEAT_DET_PX=1 / 8
+      const char* e = pf_ab_getenv("POSFEAT_DET_PX");
+      const int v = e ? atoi(e) : 4;
+      return v == 1 || v == 8 ? v : 4;
+    }();
+    int g = (P + px * 1024 - 1) / (px * 1024);
     if (g > 1024) g = 1024;
-    hipLaunchKernelGGL(det_mask_kernel, dim3(g, b), dim3(1024), 0, st, kp_map, h, w, nms_radius,
-                       use_nms, use_thr, thr_t, keys, cand_key, cand_idx, counts);
+    if (px == 1)
+      hipLaunchKernelGGL(det_mask_kernel<1>, dim3(g, b), dim3(1024), 0, st, kp_map, h, w,
+                         nms_radius, use_nms, use_thr, thr_t, keys, cand_key, cand_idx, counts);
+    else if (px == 8)
+      hipLaunchKernelGGL(det_mask_kernel<8>, dim3(g, b), dim3(1024), 0, st, kp_map, h, w,
+                         nms_radius, use_nms, use_thr, thr_t, keys, cand_key, cand_idx, counts);
+    else
+      hipLaunchKernelGGL(det_mask_kernel<4>, dim3(g, b), dim3(1024), 0, st, kp_map, h, w,
+                         nms_radius, use_nms, use_thr, thr_t, keys, cand_key, cand_idx, counts);
     PF_CHECK_LAUNCH();
   }
   hipLaunchKernelGGL(det_select_kernel, dim3(b), dim3(1024), 0, st, keys, cand_key, cand_idx, b,

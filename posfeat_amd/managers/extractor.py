@@ -166,6 +166,15 @@ class _StagedReader:
 class Extractor:
     def __init__(self, args):
         self.args = args
+        # construction phases in seconds (tools/extract_e2e.py reports them)
+        self.setup_marks = {}
+        t_mark = [time.perf_counter()]
+
+        def mark(name):
+            now = time.perf_counter()
+            self.setup_marks[name] = now - t_mark[0]
+            t_mark[0] = now
+
         with open(self.args.config, "r") as f:
             self.config = yaml.load(f, Loader=yaml.SafeLoader)
         self.save_root = os.path.join(".", "ckpts", self.config["output_root"])
@@ -193,7 +202,9 @@ class Extractor:
         elif self.config["model_config"].get("backbone") in (None, "None"):
             raise FileNotFoundError(cfg_path)
 
+        mark("config")
         self.set_device()
+        mark("device")
         self.detector = getattr(putils, self.config["detector"])
         dataset = getattr(datasets, self.config["data"])
         extract_dataset = dataset(configs=self.config["data_config_extract"])
@@ -215,6 +226,7 @@ class Extractor:
         if self._early_iter is not None:
             self._warm_h2d()   # async: overlaps the model construction below
         self.set_folder_and_logger()
+        mark("loader")
 
         tmp_model = getattr(networks, self.config["model"])
         self.model = tmp_model(self.config["model_config"], self.device)
@@ -222,7 +234,9 @@ class Extractor:
             self.model.set_parallel(self.local_rank)
         self.model.load_checkpoint(self.config["load_path"])
         self.model.set_eval()
+        mark("model")
         self.model.engine()   # weight packing (~120 ms) belongs to construction
+        mark("engine")
         if self._pipelined():
             # one workspace allocation for the whole stream (its batch shapes
             # from the file headers), while the workers decode the first
@@ -231,8 +245,10 @@ class Extractor:
             shapes = self._stream_shapes(group)
             if shapes:
                 self.model.engine().reserve(shapes)
+                mark("reserve")
                 if self._staged:
                     self._prewarm_host(group)
+                    mark("prewarm_host")
             elif self._staged:   # sizes unknown: the loader path after all
                 self._staged = False
                 self._early_iter = iter(self._pipelined_loader())

@@ -238,6 +238,7 @@ def main():
             if first is not None:
                 st["steady_images_per_s"] = (st["images"] - first[1]) / (st["seconds"] - first[0])
         st["setup_s"] = setup
+        st["setup_phases_s"] = {k: round(v, 4) for k, v in getattr(ex, "setup_marks", {}).items()}
         st["images_per_s_incl_setup"] = st["images"] / (st["seconds"] + setup)
         eng = ex.model._engine
         st["kernel_path_images_per_s"] = kernel_path_rate(eng, ex, sizes[0], st.get("group", 32))
