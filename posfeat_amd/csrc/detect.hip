@@ -420,38 +420,32 @@ __global__ void det_rank_kernel(const float* __restrict__ kp, int h, int w, int 
   const int32_t* ib = sel + (long long)b * cap;
   const uint32_t myk = active ? kb[t] : 0u;
   const int myi = active ? ib[t] : 0;
-  // (key, index) pairs, two per 16-B LDS read; the compare loop reads eight
+  // (key desc, index asc) as one 64-bit composite, (key << 32) | ~index:
+  // "o ranks before me" is one unsigned 64-bit compare (the && / || form
+  // compiled to a branch per entry); two composites per 16-B LDS read, eight
   // entries per step with four partial counts (round 5: one dependent LDS
   // read per entry, 59 us at n = 2048, B = 32)
-  __shared__ uint4 tile[512];
+  typedef unsigned long long u64;
+  const u64 myc = ((u64)myk << 32) | (u64)(0xFFFFFFFFu - (uint32_t)myi);
+  __shared__ __attribute__((aligned(16))) u64 tile[1024];
   int rank = 0;
   for (int base = 0; base < n; base += 1024) {
-    for (int k = threadIdx.x; k < 512; k += blockDim.x) {
-      const int e0 = base + 2 * k, e1 = e0 + 1;
-      tile[k] = make_uint4(e0 < n ? kb[e0] : 0u, e0 < n ? (uint32_t)ib[e0] : 0u,
-                           e1 < n ? kb[e1] : 0u, e1 < n ? (uint32_t)ib[e1] : 0u);
-    }
+    for (int k = threadIdx.x; k < 1024; k += blockDim.x)
+      tile[k] = base + k < n ? ((u64)kb[base + k] << 32) | (u64)(0xFFFFFFFFu - (uint32_t)ib[base + k])
+                             : 0ull;
     __syncthreads();
     const int lim = min(1024, n - base);
     if (active) {
       int r4[4] = {0, 0, 0, 0};
       const int full = lim & ~7;
       for (int k = 0; k < full; k += 8) {
-        uint4 o[4];
+        ulonglong2 o[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) o[u] = tile[(k >> 1) + u];
+        for (int u = 0; u < 4; ++u) o[u] = *reinterpret_cast<const ulonglong2*>(tile + k + 2 * u);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          r4[u] += (o[u].x > myk) || (o[u].x == myk && (int)o[u].y < myi);
-          r4[u] += (o[u].z > myk) || (o[u].z == myk && (int)o[u].w < myi);
-        }
+        for (int u = 0; u < 4; ++u) r4[u] += (int)(o[u].x > myc) + (int)(o[u].y > myc);
       }
-      for (int k = full; k < lim; ++k) {
-        const uint4 o = tile[k >> 1];
-        const uint32_t ok = (k & 1) ? o.z : o.x;
-        const int oi = (int)((k & 1) ? o.w : o.y);
-        r4[0] += (ok > myk) || (ok == myk && oi < myi);
-      }
+      for (int k = full; k < lim; ++k) r4[0] += (int)(tile[k] > myc);
       rank += (r4[0] + r4[1]) + (r4[2] + r4[3]);
     }
     __syncthreads();

@@ -232,9 +232,10 @@ class Extractor:
         self.model = tmp_model(self.config["model_config"], self.device)
         if self.multi_gpu:
             self.model.set_parallel(self.local_rank)
+        mark("model_build")
         self.model.load_checkpoint(self.config["load_path"])
         self.model.set_eval()
-        mark("model")
+        mark("checkpoint")
         self.model.engine()   # weight packing (~120 ms) belongs to construction
         mark("engine")
         if self._pipelined():
