@@ -54,7 +54,7 @@ import torch
 import torch.distributed as dist
 import yaml
 
-from .. import datasets, networks, ops
+from .. import datasets, networks, ops, weights
 from ..losses import preprocess_utils as putils
 from ..losses.preprocess_utils import denormalize_coords, normalize_coords, sample_feat_by_coord
 
@@ -229,7 +229,10 @@ class Extractor:
         mark("loader")
 
         tmp_model = getattr(networks, self.config["model"])
-        self.model = tmp_model(self.config["model_config"], self.device)
+        # the seeded initial weights are drawn only if the checkpoint below
+        # does not replace them (weights.deferred_seed)
+        with weights.deferred_seed():
+            self.model = tmp_model(self.config["model_config"], self.device)
         if self.multi_gpu:
             self.model.set_parallel(self.local_rank)
         mark("model_build")

@@ -26,8 +26,7 @@ class ResUNet(nn.Module):
         # parameters start from the seeded recipe and are replaced by
         # load_checkpoint / load_state_dict exactly as in the reference flow.
         build_param_tree(self, weights.backbone_param_shapes())
-        bb, _ = weights.seeded_state_dicts(0)
-        self.load_state_dict(bb)
+        weights.seed_module(self, "backbone")
         self.out_channels = [fine_out_ch, coarse_out_ch]
         self._runner = None
 

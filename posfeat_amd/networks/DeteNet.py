@@ -20,8 +20,7 @@ class KeypointDet(nn.Module):
                 "posfeat_amd implements KeypointDet(in_channels=192, out_channels=1, "
                 "prior='identity', act='Softplus') -- configs/train_desc.yaml:24-28")
         build_param_tree(self, weights.head_param_shapes(in_channels, out_channels))
-        _, hd = weights.seeded_state_dicts(0)
-        self.load_state_dict(hd)
+        weights.seed_module(self, "localheader")
 
     def forward(self, fine_maps):
         """fine_maps = [x, img]: x = cat[local_map, local_map_small] [b,192,h/4,w/4],

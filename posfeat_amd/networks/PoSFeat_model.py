@@ -89,6 +89,8 @@ class PoSFeat:
 
     def engine(self):
         from ..engine import ExtractionEngine
+        weights.materialize_seed(self.backbone)   # built inside weights.deferred_seed()
+        weights.materialize_seed(self.localheader)
         key = self._param_key()
         if self._engine is None or key != self._engine_key:
             self._engine = ExtractionEngine(self.backbone.state_dict(),
@@ -119,9 +121,11 @@ class PoSFeat:
         for name, sd in (("backbone", bb), ("localheader", hd)):
             if sd is None:
                 print("{} does not exist, skipping load".format(name))
+                weights.materialize_seed(getattr(self, name))
                 continue
             print("load {} from checkpoint".format(name))
             getattr(self, name).load_state_dict(sd)
+            getattr(self, name)._seed_pending = None   # every tensor replaced (strict load)
         self._engine = None
 
     def save_checkpoint(self, save_path):

@@ -103,24 +103,71 @@ def _draw(rs, key, shape):
     return rs.uniform(-0.1, 0.1, shape).astype(np.float32)
 
 
-def seeded_state_dicts(seed=0, as_torch=True):
+def seeded_state_dicts(seed=0, as_torch=True, parts=("backbone", "localheader")):
     """Deterministic random weights for (backbone, localheader).
 
     Tensor i of the backbone comes from ``RandomState(seed*100003 + i)``,
     tensor i of the head from ``RandomState(seed*100003 + 50000 + i)``.
+    ``parts``: which of the two to draw (the other is returned as None; the
+    values of a drawn part do not depend on it).
     """
     base = seed * 100003
-    bb = OrderedDict()
-    for i, (k, s) in enumerate(backbone_param_shapes()):
-        bb[k] = _draw(np.random.RandomState(base + i), k, s)
-    hd = OrderedDict()
-    for i, (k, s) in enumerate(head_param_shapes()):
-        hd[k] = _draw(np.random.RandomState(base + 50000 + i), k, s)
+    bb = hd = None
+    if "backbone" in parts:
+        bb = OrderedDict()
+        for i, (k, s) in enumerate(backbone_param_shapes()):
+            bb[k] = _draw(np.random.RandomState(base + i), k, s)
+    if "localheader" in parts:
+        hd = OrderedDict()
+        for i, (k, s) in enumerate(head_param_shapes()):
+            hd[k] = _draw(np.random.RandomState(base + 50000 + i), k, s)
     if as_torch:
         import torch
-        bb = OrderedDict((k, torch.from_numpy(np.ascontiguousarray(v))) for k, v in bb.items())
-        hd = OrderedDict((k, torch.from_numpy(np.ascontiguousarray(v))) for k, v in hd.items())
+        conv = lambda d: None if d is None else OrderedDict(
+            (k, torch.from_numpy(np.ascontiguousarray(v))) for k, v in d.items())
+        bb, hd = conv(bb), conv(hd)
     return bb, hd
+
+
+# Deferred seeding: modules built inside ``deferred_seed()`` skip the seeded
+# draw (20.5 M normal draws for the backbone, ~0.25 s on the GPU box's host)
+# and mark themselves pending; ``materialize_seed`` draws it later unless a
+# checkpoint replaced every tensor first (PoSFeat.load_checkpoint,
+# Extractor: the reference flow always loads one right after construction).
+_DEFER = [0]
+
+
+class deferred_seed:
+    def __enter__(self):
+        _DEFER[0] += 1
+        return self
+
+    def __exit__(self, *exc):
+        _DEFER[0] -= 1
+        return False
+
+
+def seed_deferred():
+    return _DEFER[0] > 0
+
+
+def seed_module(module, part):
+    """Load the seeded recipe's ``part`` into ``module`` now, or mark it
+    pending inside ``deferred_seed()``."""
+    if seed_deferred():
+        module._seed_pending = part
+        return
+    bb, hd = seeded_state_dicts(0, parts=(part,))
+    module.load_state_dict(bb if part == "backbone" else hd)
+    module._seed_pending = None
+
+
+def materialize_seed(module):
+    part = getattr(module, "_seed_pending", None)
+    if part:
+        bb, hd = seeded_state_dicts(0, parts=(part,))
+        module.load_state_dict(bb if part == "backbone" else hd)
+        module._seed_pending = None
 
 
 def seeded_image(i, h=480, w=640):
