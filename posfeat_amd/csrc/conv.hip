@@ -79,6 +79,11 @@ struct ConvArgs {
   // plane stride xplane, batch stride bxb (elements)
   const unsigned short* xb;
   long long xplane, bxb;
+  // two-source 1x1 GEMM (conv_bf6x_kernel AM = 3, pf_conv_dual): K chunks
+  // [0, k1ch) read x at the output pixel (stride 1), chunks [k1ch, Kpad / BK)
+  // read x2 at input pixel (n, oh * s2, ow * s2) of its H2 x W2 map
+  const float* x2;
+  int x2cs, k1ch, H2, W2, s2;
 };
 
 // Epilogue shared by both kernels: acc -> LDS T[BM][BN+4] (conflict-free: a
@@ -1451,11 +1456,13 @@ __device__ __forceinline__ int bx_swz(int row) { return (0x78 >> (2 * ((row >> 2
 
 // AM: the A (pixel-row) operand -- 0 dense rows (1x1 convs, GEMMs), 1 G4:
 // 4-channel input taps (the stem), 2 GT: 32-channel slab x tap chunks (3x3 /
-// strided convs with Cin % 32 == 0, the packed K order (cin/32, kh, kw, cin%32))
+// strided convs with Cin % 32 == 0, the packed K order (cin/32, kh, kw, cin%32)),
+// 3 DU: dense rows from two maps (a bottleneck's conv3 + its downsample as one
+// GEMM, ConvArgs x2)
 template <int BN, int RB = 2, int AM = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
 void conv_bf6x_kernel(ConvArgs a) {
-  constexpr bool G4 = AM == 1, GT = AM == 2;
+  constexpr bool G4 = AM == 1, GT = AM == 2, DU = AM == 3;
   constexpr int NW = 4, BM = NW * RB * 16, NB = BN / 16;
   constexpr int B_G = 3 * BN / 16 / NW;  // B DMA instructions per wave per chunk
   constexpr int NA = 2 * RB;             // A loads per lane per chunk
@@ -1486,10 +1493,16 @@ void conv_bf6x_kernel(ConvArgs a) {
   const int m0 = tm * BM, n0 = tn * BN;
   const int r16 = lane & 15, kq = lane >> 4;
   const float* xrow[RB];
+  const float* xrow2[DU ? RB : 1];  // DU: the row in x2
   int ih0[RB], iw0[RB];  // G4: the row's top-left input tap
 #pragma unroll
   for (int rb = 0; rb < RB; ++rb) {
     const int m = min(m0 + wave * RB * 16 + rb * 16 + r16, a.M - 1);
+    if (DU) {
+      const int n = m / a.hw, rem = m - n * a.hw;
+      const int oh = rem / a.OW, ow = rem - oh * a.OW;
+      xrow2[rb] = a.x2 + (((long long)n * a.H2 + oh * a.s2) * a.W2 + ow * a.s2) * a.x2cs + kq * 8;
+    }
     long long pix = m;  // stride 1: output row m is input pixel m
     if (a.stride != 1 || G4 || GT) {
       const int n = m / a.hw, rem = m - n * a.hw;
@@ -1517,6 +1530,9 @@ void conv_bf6x_kernel(ConvArgs a) {
       const bool ok = (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
       return ok ? xrow[rb] + ((long long)ih * a.W + iw) * a.xcs + g_slab * BK + jj * 4 : a.zero;
     }
+    if (DU)  // uniform: every lane is at the same chunk
+      return chunk < a.k1ch ? xrow[rb] + (long long)chunk * BK + jj * 4
+                            : xrow2[rb] + (long long)(chunk - a.k1ch) * BK + jj * 4;
     if (!G4) return xrow[rb] + (long long)chunk * BK + jj * 4;
     const int ih = ih0[rb] + tkh[jj], iw = iw0[rb] + tkw[jj];
     const bool ok = tkh[jj] < a.KH && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
@@ -2685,7 +2701,10 @@ int conv_run(ConvArgs& a, const Plan& p, hipStream_t st) {
                          dim3(a.nwg * a.ksplit, a.nbatch), dim3(256), 0, st, a);
       break;
     case TILE_BF6X_128x128:
-      if (dense_gemm(a))
+      if (a.x2)  // pf_conv_dual
+        hipLaunchKernelGGL((conv_bf6x_kernel<128, 2, 3>), dim3(a.nwg * a.ksplit, a.nbatch),
+                           dim3(256), 0, st, a);
+      else if (dense_gemm(a))
         hipLaunchKernelGGL((conv_bf6x_kernel<128>), dim3(a.nwg * a.ksplit, a.nbatch), dim3(256),
                            0, st, a);
       else  // gt_gemm: the slab x tap gather
@@ -2917,6 +2936,8 @@ static int conv_prepare(const posfeat_conv_desc* d, const float* x, const float*
   a.xb = nullptr;
   a.xplane = a.bxb = 0;
   a.wplane = a.bwb = 0;
+  a.x2 = nullptr;
+  a.x2cs = a.k1ch = a.H2 = a.W2 = a.s2 = 0;
   a.zero = conv_zero_ptr();  // checked at launch (planning calls need no device)
   return POSFEAT_OK;
 }
@@ -3021,6 +3042,81 @@ int pf_conv_run_tile(const posfeat_conv_desc* d, const float* x, const float* w,
   const Plan p = conv_plan(a, split, tile);
   if (p.ksplit > 1) a.part = static_cast<float*>(ws);
   return conv_run(a, p, st);
+}
+
+// y = act(x1 . W1^T + x2(strided) . W2^T + bias): a torchvision bottleneck's
+// conv3 and its downsample branch (networks/DescNet.py:29-35, the encoder's
+// first block of each stage) as ONE GEMM over K = k1 + k2 -- the downsample
+// output never crosses HBM (it was written, then re-read as conv3's residual).
+// x1: [n][oh][ow] rows of k1 channels (pitch x1cs); x2: [n][h2][w2] rows of k2
+// channels (pitch x2cs) read at (oh * s2, ow * s2); wb: three bf16 planes of
+// the [cout][k1 + k2] weights (plane stride wplane); bias: the summed biases.
+// k1, k2 % 32 == 0, cout % 128 == 0.
+int pf_conv_dual(int n, int oh, int ow, const float* x1, int x1cs, int k1, const float* x2,
+                 int x2cs, int h2, int w2, int s2, int k2, int cout,
+                 const unsigned short* wb, long long wplane, const float* bias, int act, float* y,
+                 int ycs, hipStream_t st) {
+  if (k1 <= 0 || k2 <= 0 || k1 % BK || k2 % BK || cout % 128 || !x2 || !wb || s2 < 1 ||
+      (oh - 1) * s2 >= h2 || (ow - 1) * s2 >= w2 || x2cs % 4 || (reinterpret_cast<uintptr_t>(x2) & 15))
+    return POSFEAT_E_INVALID;
+  posfeat_conv_desc d{};
+  d.n = n;
+  d.h = oh;
+  d.w = ow;
+  d.cin = k1 + k2;
+  d.x_cstride = x1cs;
+  d.cout = cout;
+  d.kh = d.kw = 1;
+  d.stride = 1;
+  d.pad = 0;
+  d.y_cstride = ycs;
+  d.res_cstride = 0;
+  d.act = act;
+  ConvArgs a;
+  PF_TRY(conv_prepare(&d, x1, bias, bias, nullptr, y, a));
+  a.wb = wb;
+  a.wplane = wplane;
+  a.x2 = x2;
+  a.x2cs = x2cs;
+  a.k1ch = k1 / BK;
+  a.H2 = h2;
+  a.W2 = w2;
+  a.s2 = s2;
+  Plan p = plan_for_tile(a, TILE_BF6X_128x128);
+  if (p.kern < 0) return POSFEAT_E_INVALID;
+  return conv_run(a, p, st);
+}
+
+namespace {
+__global__ void dual_weights_kernel(const unsigned short* __restrict__ w1, int k1,
+                                    const unsigned short* __restrict__ w2, int k2, long long sp,
+                                    int cout, const float* __restrict__ b1,
+                                    const float* __restrict__ b2, unsigned short* __restrict__ dst,
+                                    float* __restrict__ bdst) {
+  const int kc = k1 + k2;
+  const long long per = (long long)cout * kc, total = 3 * per;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int pl = (int)(i / per);
+    const long long r = i - pl * per;
+    const int co = (int)(r / kc), k = (int)(r - (long long)co * kc);
+    dst[i] = k < k1 ? w1[pl * sp + (long long)co * k1 + k] : w2[pl * sp + (long long)co * k2 + k - k1];
+  }
+  if (blockIdx.x == 0)
+    for (int c = threadIdx.x; c < cout; c += blockDim.x) bdst[c] = b1[c] + b2[c];
+}
+}  // namespace
+
+int pf_dual_weights(const unsigned short* w1, int k1, const unsigned short* w2, int k2,
+                    long long sp, int cout, const float* b1, const float* b2,
+                    unsigned short* dst, float* bdst, hipStream_t st) {
+  if (!w1 || !w2 || !dst || !b1 || !b2 || !bdst || k1 <= 0 || k2 <= 0 || cout <= 0)
+    return POSFEAT_E_INVALID;
+  const long long total = 3LL * cout * (k1 + k2);
+  hipLaunchKernelGGL(dual_weights_kernel, dim3((unsigned)std::min<long long>((total + 255) / 256, 4096)),
+                     dim3(256), 0, st, w1, k1, w2, k2, sp, cout, b1, b2, dst, bdst);
+  PF_CHECK_LAUNCH();
+  return POSFEAT_OK;
 }
 
 // pf_conv_run_tile with the train-mode BatchNorm partial sums of y from the

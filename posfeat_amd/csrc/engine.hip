@@ -164,6 +164,11 @@ struct posfeat_model {
   // the start of every forward, Winograd U and the tap weights as planes
   bool wsplit = false;
   Buf wpl;
+  // each stage's first bottleneck: conv3 + downsample as one two-source GEMM
+  // (pf_conv_dual) on [cout][k1 + k2] planes + summed biases built with wpl
+  // (A/B: POSFEAT_DSFUSE=0 -- the downsample conv, then conv3 with it as residual)
+  bool dsfuse = false;
+  Buf dsw;
   bool tapb = false;  // bf16x6 tap GEMM on pre-split planes (POSFEAT_BF6=2)
   Buf tapwb, tapLb;
   Buf gf_w, gf_b, gf_wp;
@@ -746,6 +751,32 @@ posfeat_conv_desc dl_desc(const posfeat_model* m) {
   return d;
 }
 
+// the fused conv3 + downsample weights of stage l (dsw): planes at u16 offset
+// off, then the summed biases at float offset boff
+struct DualLayout {
+  int cout, k1, k2;
+  size_t off, boff;
+};
+DualLayout dual_layout(int l) {
+  const int planes[3] = {64, 128, 256}, inpl[3] = {64, 256, 512};
+  size_t off = 0;
+  DualLayout d{};
+  for (int i = 0; i <= l; ++i) {
+    d.cout = planes[i] * 4;
+    d.k1 = planes[i];
+    d.k2 = inpl[i];
+    d.off = off;
+    off += pf_align((size_t)3 * d.cout * (d.k1 + d.k2) * 2, 256) / 2;
+    d.boff = off / 2;
+    off += pf_align((size_t)d.cout * 4, 256) / 2;
+  }
+  return d;
+}
+size_t dual_floats() {
+  const DualLayout d = dual_layout(2);
+  return d.boff + pf_align((size_t)d.cout * 4, 256) / 4;
+}
+
 void plan(posfeat_model* m) {
   size_t cur = 0, pcur = 0;
   auto alloc = [&](Buf& b, size_t floats, size_t elem = 4) {
@@ -819,6 +850,11 @@ void plan(posfeat_model* m) {
     m->wsplit = pf_conv_precision() == 1 && !(e && e[0] == '0') && specs().total % 4 == 0;
   }
   if (m->wsplit) palloc(m->wpl, (size_t)specs().total * 3 / 2 + 4);
+  {
+    const char* e = pf_ab_getenv("POSFEAT_DSFUSE");
+    m->dsfuse = m->wsplit && !m->train && pf_bf6x_on() && !(e && e[0] == '0');
+  }
+  if (m->dsfuse) palloc(m->dsw, dual_floats());
   if (m->wino) {
     size_t uf = 0, wb = 0;
     const int nl = wino_enc_on() ? 16 : 5;
@@ -939,6 +975,18 @@ int bottleneck(Ctx& c, const std::string& p, const float* in, int n, int h, int 
     PF_TRY(conv(c, p + ".conv2", t1, n, h, w, planes, t2, planes, stride, POSFEAT_ACT_RELU));
   const float* res = in;
   int rcs = ics;
+  if (has_ds && m->dsfuse && pf_bf6x_on()) {  // (a tile scope may have turned bf6x off)
+    const int l = planes == 64 ? 0 : planes == 128 ? 1 : 2;
+    const DualLayout d = dual_layout(l);
+    if (c.dry) return POSFEAT_OK;
+    const double flops = 2.0 * n * oh * ow * (double)d.cout * (d.k1 + d.k2);
+    return timed(c, "conv:" + p + ".conv3ds", flops, [&] {
+      return pf_conv_dual(n, oh, ow, t2, planes, d.k1, in, ics, h, w, stride, d.k2, d.cout,
+                          reinterpret_cast<const unsigned short*>(c.f(m->dsw)) + d.off,
+                          (long long)d.cout * (d.k1 + d.k2), c.f(m->dsw) + d.boff,
+                          POSFEAT_ACT_RELU, out, ocs, c.st);
+    });
+  }
   if (has_ds) {
     float* ds = c.f(m->ds);
     PF_TRY(conv(c, p + ".downsample", in, n, h, w, ics, ds, planes * 4, stride, POSFEAT_ACT_NONE));
@@ -1091,8 +1139,20 @@ int forward(Ctx& c, const float* img, posfeat_extract_out* out, int mode, const 
   // (the planning pass runs before the instance has its store)
   if (m->wsplit && !(m->wcache && m->store && m->store->wpl_done)) {  // the blob's bf16 planes
     PF_TRY(timed(c, "weights.split", 0, [&] {
-      return pf_split3_rows(m->wts, specs().total / 4, 4, 4,
-                            reinterpret_cast<unsigned short*>(c.f(m->wpl)), c.st);
+      PF_TRY(pf_split3_rows(m->wts, specs().total / 4, 4, 4,
+                            reinterpret_cast<unsigned short*>(c.f(m->wpl)), c.st));
+      if (!m->dsfuse) return POSFEAT_OK;
+      const unsigned short* wpl = reinterpret_cast<const unsigned short*>(c.f(m->wpl));
+      unsigned short* dsw = reinterpret_cast<unsigned short*>(c.f(m->dsw));
+      for (int l = 0; l < 3; ++l) {
+        const DualLayout d = dual_layout(l);
+        const std::string p = "layer" + std::to_string(l + 1) + ".0";
+        PF_TRY(pf_dual_weights(wpl + specs().find(p + ".conv3")->w_off, d.k1,
+                               wpl + specs().find(p + ".downsample")->w_off, d.k2, specs().total,
+                               d.cout, c.Bi(p + ".conv3"), c.Bi(p + ".downsample"), dsw + d.off,
+                               c.f(m->dsw) + d.boff, c.st));
+      }
+      return POSFEAT_OK;
     }));
     if (!c.dry && m->wcache) m->store->wpl_done = m->wprep_pending = true;
   }

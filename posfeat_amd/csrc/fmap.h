@@ -42,6 +42,16 @@ int pf_conv_run_tile(const posfeat_conv_desc* d, const float* x, const float* w,
                      const float* bias, const float* res, float* y, void* ws, size_t ws_bytes,
                      int tile, hipStream_t st, const unsigned short* wb = nullptr,
                      long long wplane = 0);
+// a bottleneck's conv3 + downsample as one two-source GEMM (conv.hip), and its
+// weights: the [cout][k1 + k2] bf16 planes (plane stride cout * (k1 + k2)) from
+// the two layers' planes (source plane stride sp) and the summed biases
+int pf_conv_dual(int n, int oh, int ow, const float* x1, int x1cs, int k1, const float* x2,
+                 int x2cs, int h2, int w2, int s2, int k2, int cout,
+                 const unsigned short* wb, long long wplane, const float* bias, int act, float* y,
+                 int ycs, hipStream_t st);
+int pf_dual_weights(const unsigned short* w1, int k1, const unsigned short* w2, int k2,
+                    long long sp, int cout, const float* b1, const float* b2,
+                    unsigned short* dst, float* bdst, hipStream_t st);
 // the same with the train-mode BatchNorm partial sums from the epilogue
 // (conv.hip; *nparts = 0: not produced, run the statistics pass)
 int pf_conv_run_tile_bn(const posfeat_conv_desc* d, const float* x, const float* w,
