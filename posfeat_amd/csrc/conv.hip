@@ -3064,7 +3064,7 @@ int pf_conv_dual(int n, int oh, int ow, const float* x1, int x1cs, int k1, const
   d.h = oh;
   d.w = ow;
   d.cin = k1 + k2;
-  d.x_cstride = x1cs;
+  d.x_cstride = std::max(x1cs, k1 + k2);  // (conv_prepare's one-source check; x1's pitch below)
   d.cout = cout;
   d.kh = d.kw = 1;
   d.stride = 1;
@@ -3073,7 +3073,9 @@ int pf_conv_dual(int n, int oh, int ow, const float* x1, int x1cs, int k1, const
   d.res_cstride = 0;
   d.act = act;
   ConvArgs a;
+  if (x1cs < k1 || x1cs % 4) return POSFEAT_E_INVALID;
   PF_TRY(conv_prepare(&d, x1, bias, bias, nullptr, y, a));
+  a.xcs = x1cs;
   a.wb = wb;
   a.wplane = wplane;
   a.x2 = x2;
