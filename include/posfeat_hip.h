@@ -113,6 +113,20 @@ int posfeat_conv2d_nhwc_planes(const posfeat_conv_desc *d, const float *x, const
                                const unsigned short *wb, long long wplane, const float *bias,
                                const float *res, float *y, void *ws, size_t ws_bytes, int tile,
                                void *stream);
+/* A torchvision Bottleneck's conv3 + downsample branch as ONE GEMM (the
+ * reference's ResUNet encoder, networks/DescNet.py:29-35, through torchvision's
+ * Bottleneck: relu(bn3(conv3(t)) + bn_ds(conv_ds(x))) with both BatchNorms
+ * folded; replaces conv3 and the downsample conv of layer1.0 / layer2.0 /
+ * layer3.0): y[n][oh][ow] = act(x1[n][oh][ow] . W1^T + x2[n][oh*s2][ow*s2] .
+ * W2^T + bias), K = k1 + k2, bf16x6 products on the 16x16x32 tiles.  x1: rows
+ * of k1 channels (pitch x1cs), x2: an h2 x w2 map of k2 channels (pitch x2cs),
+ * wb: the three bf16 planes of the [cout][k1 + k2] weights (plane stride
+ * cout * (k1 + k2)), bias: the two biases summed.  k1, k2 % 32 == 0,
+ * cout % 128 == 0, 16-B aligned pointers, else POSFEAT_E_INVALID. */
+int posfeat_conv1x1_dual(int n, int oh, int ow, const float *x1, int x1cs, int k1,
+                         const float *x2, int x2cs, int h2, int w2, int s2, int k2, int cout,
+                         const unsigned short *wb, const float *bias, int act, float *y, int ycs,
+                         void *stream);
 /* Conv (no residual, no activation) whose epilogue also reduces per-tile
  * channel sums for InstanceNorm2d (networks/DeteNet.py:12-22): writes y and
  * mean/rstd [n][cout] of y over each image (biased var, rstd=1/sqrt(var+eps)).

@@ -55,6 +55,9 @@ SIGNATURES = {
     "posfeat_conv2d_nhwc_planes": (c_int, [ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_void_p,
                                            ctypes.c_longlong, c_void_p, c_void_p, c_void_p,
                                            c_void_p, c_size_t, c_int, c_void_p]),
+    "posfeat_conv1x1_dual": (c_int, [c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_int,
+                                     c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
+                                     c_void_p, c_int, c_void_p]),
     "posfeat_conv2d_stats_workspace": (c_size_t, [ctypes.POINTER(ConvDesc)]),
     "posfeat_conv2d_nhwc_stats": (c_int, [ctypes.POINTER(ConvDesc), c_void_p, c_void_p, c_void_p,
                                           c_void_p, c_void_p, c_size_t, c_void_p, c_void_p,

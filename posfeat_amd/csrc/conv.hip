@@ -3089,6 +3089,15 @@ int pf_conv_dual(int n, int oh, int ow, const float* x1, int x1cs, int k1, const
   return conv_run(a, p, st);
 }
 
+extern "C" int posfeat_conv1x1_dual(int n, int oh, int ow, const float* x1, int x1cs, int k1,
+                                    const float* x2, int x2cs, int h2, int w2, int s2, int k2,
+                                    int cout, const unsigned short* wb, const float* bias,
+                                    int act, float* y, int ycs, void* stream) {
+  if (!bias) return POSFEAT_E_INVALID;
+  return pf_conv_dual(n, oh, ow, x1, x1cs, k1, x2, x2cs, h2, w2, s2, k2, cout, wb,
+                      (long long)cout * (k1 + k2), bias, act, y, ycs, pf_stream(stream));
+}
+
 namespace {
 __global__ void dual_weights_kernel(const unsigned short* __restrict__ w1, int k1,
                                     const unsigned short* __restrict__ w2, int k2, long long sp,

@@ -108,6 +108,26 @@ def conv2d_nhwc_planes(x, w_packed, planes, bias, cout, kh, kw, stride=1, pad=No
     return out
 
 
+def conv1x1_dual(x1, x2, w1, w2, bias1, bias2, stride2=1, act="relu", out=None):
+    """y = act(x1 . w1^T + x2[:, ::s, ::s] . w2^T + bias1 + bias2) as one GEMM
+    (posfeat_conv1x1_dual: a bottleneck's conv3 + downsample, the engine's
+    layer1.0 / layer2.0 / layer3.0).  x1 [n, oh, ow, k1], x2 [n, h2, w2, k2]
+    NHWC fp32; w1 [cout, k1], w2 [cout, k2]."""
+    _f32(x1, "x1")
+    _f32(x2, "x2")
+    n, oh, ow, k1 = x1.shape
+    _, h2, w2, k2 = x2.shape
+    cout = w1.shape[0]
+    planes = split_weight_planes(torch.cat([_f32(w1, "w1"), _f32(w2, "w2")], dim=1))
+    bias = (_f32(bias1, "bias1") + _f32(bias2, "bias2")).contiguous()
+    if out is None:
+        out = torch.empty(n, oh, ow, cout, device=x1.device, dtype=torch.float32)
+    check(lib().posfeat_conv1x1_dual(n, oh, ow, ptr(x1), k1, k1, ptr(x2), k2, h2, w2, stride2, k2,
+                                     cout, ptr(planes), ptr(bias), ACT[act], ptr(out),
+                                     out.shape[-1], stream_ptr()))
+    return out
+
+
 def conv2d_nhwc_instnorm_stats(x, w_packed, bias, cout, kh, kw, eps=1e-5, out=None, cin=None):
     """Conv (stride 1, 'same' pad, no act) + per-image channel mean/rstd of its
     output from the fused epilogue.  Returns (y, mean [n,cout], rstd [n,cout])."""

@@ -76,6 +76,43 @@ def test_conv_vs_torch(gpu, case):
         assert torch.all(out[..., cout:] == 7.0).item(), "wrote outside its channel slice"
 
 
+DUAL_CASES = [
+    # n, oh, ow, k1 (conv3 input), k2 (downsample input), cout, stride of the downsample
+    (2, 24, 40, 64, 64, 256, 1),      # layer1.0 (ragged last tile: 1920 rows)
+    (1, 15, 20, 128, 256, 512, 2),    # layer2.0
+    (2, 8, 10, 256, 512, 1024, 2),    # layer3.0
+]
+
+
+@pytest.mark.parametrize("case", DUAL_CASES)
+def test_conv1x1_dual_vs_torch(gpu, case):
+    """A bottleneck's conv3 + downsample as one two-source GEMM
+    (posfeat_conv1x1_dual) vs relu(conv3(t) + conv_ds(x) + biases) in fp64,
+    the bound of test_conv_vs_torch over both K ranges."""
+    from posfeat_amd import ops
+    n, oh, ow, k1, k2, cout, s = case
+    h2, w2 = (oh - 1) * s + 1 + (s - 1), (ow - 1) * s + 1 + (s - 1)
+    g = torch.Generator().manual_seed(hash(case) % 1000)
+    t = torch.randn(n, k1, oh, ow, generator=g)
+    x = torch.randn(n, k2, h2, w2, generator=g)
+    w1 = torch.randn(cout, k1, 1, 1, generator=g) * (2.0 / k1) ** 0.5
+    w2 = torch.randn(cout, k2, 1, 1, generator=g) * (2.0 / k2) ** 0.5
+    b1 = torch.randn(cout, generator=g) * 0.1
+    b2 = torch.randn(cout, generator=g) * 0.1
+    r1, bd1 = _conv_ref64(t, w1, b1, 1, 0)
+    r2, bd2 = _conv_ref64(x, w2, b2, s, 0)
+    ref = torch.relu(r1 + r2)
+    bound = bd1 + bd2
+    out = ops.conv1x1_dual(t.permute(0, 2, 3, 1).contiguous().to(gpu),
+                           x.permute(0, 2, 3, 1).contiguous().to(gpu), w1[:, :, 0, 0].to(gpu),
+                           w2[:, :, 0, 0].to(gpu), b1.to(gpu), b2.to(gpu), stride2=s, act="relu")
+    torch.cuda.synchronize()
+    got = out.permute(0, 3, 1, 2).double().cpu()
+    err = (got - ref).abs()
+    tol = 2e-6 * bound + 1e-6
+    assert torch.all(err <= tol), "max err %g (bound %g)" % (err.max(), (err / tol).max())
+
+
 WINO_CASES = [
     # n, h, w, cin, cout, act, in_extra, out_extra
     (2, 16, 24, 64, 64, "none", 0, 0),       # F(4x4)
