@@ -116,13 +116,13 @@ def conv1x1_dual(x1, x2, w1, w2, bias1, bias2, stride2=1, act="relu", out=None):
     _f32(x1, "x1")
     _f32(x2, "x2")
     n, oh, ow, k1 = x1.shape
-    _, h2, w2, k2 = x2.shape
+    _, xh, xw, k2 = x2.shape
     cout = w1.shape[0]
     planes = split_weight_planes(torch.cat([_f32(w1, "w1"), _f32(w2, "w2")], dim=1))
     bias = (_f32(bias1, "bias1") + _f32(bias2, "bias2")).contiguous()
     if out is None:
         out = torch.empty(n, oh, ow, cout, device=x1.device, dtype=torch.float32)
-    check(lib().posfeat_conv1x1_dual(n, oh, ow, ptr(x1), k1, k1, ptr(x2), k2, h2, w2, stride2, k2,
+    check(lib().posfeat_conv1x1_dual(n, oh, ow, ptr(x1), k1, k1, ptr(x2), k2, xh, xw, stride2, k2,
                                      cout, ptr(planes), ptr(bias), ACT[act], ptr(out),
                                      out.shape[-1], stream_ptr()))
     return out

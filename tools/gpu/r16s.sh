@@ -9,7 +9,7 @@ mkdir -p "$o"
 chk=tools/gpu_check.sh
 export PYTHONUNBUFFERED=1
 AB=$PWD/posfeat_amd/libposfeat_hip_ab.so
-$chk 600 $o/tests.log python -u -m pytest tests/test_gpu_ops.py -k "dual or conv_vs" tests/test_gpu_model.py tests/test_gpu_api.py tests/test_gpu_bench_config.py tests/test_gpu_extract.py tests/test_gpu_precision.py -m gpu -q -rf --timeout 300 --timeout-method thread
+$chk 600 $o/tests.log python -u -m pytest tests/test_gpu_ops.py::test_conv1x1_dual_vs_torch tests/test_gpu_model.py tests/test_gpu_api.py tests/test_gpu_bench_config.py tests/test_gpu_extract.py tests/test_gpu_precision.py -m gpu -q -rf --timeout 300 --timeout-method thread
 tail -3 $o/tests.log
 $chk 200 $o/lt_new.log python -u tools/layer_timing.py 32
 POSFEAT_HIP_LIB=$AB POSFEAT_DSFUSE=0 $chk 200 $o/lt_old.log python -u tools/layer_timing.py 32
