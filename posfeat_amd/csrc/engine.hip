@@ -169,6 +169,9 @@ struct posfeat_model {
   // (A/B: POSFEAT_DSFUSE=0 -- the downsample conv, then conv3 with it as residual)
   bool dsfuse = false;
   Buf dsw;
+  // head.conv2's tap GEMM + combine in chunks of hchunk images reusing one P
+  // slab (A/B: POSFEAT_HEAD_CHUNK=G; 0 = the whole batch per launch)
+  int hchunk = 0;
   bool tapb = false;  // bf16x6 tap GEMM on pre-split planes (POSFEAT_BF6=2)
   Buf tapwb, tapLb;
   Buf gf_w, gf_b, gf_wp;
@@ -855,6 +858,10 @@ void plan(posfeat_model* m) {
     m->dsfuse = m->wsplit && !m->train && pf_bf6x_on() && !(e && e[0] == '0');
   }
   if (m->dsfuse) palloc(m->dsw, dual_floats());
+  {
+    const char* e = pf_ab_getenv("POSFEAT_HEAD_CHUNK");
+    m->hchunk = e ? std::max(0, atoi(e)) : 0;
+  }
   if (m->wino) {
     size_t uf = 0, wb = 0;
     const int nl = wino_enc_on() ? 16 : 5;
@@ -1339,6 +1346,29 @@ int head_forward(Ctx& c, float* img4, float* local_point, bool side) {
                               reinterpret_cast<const unsigned short*>(c.f(m->tapwb)), 192,
                               1152LL * 192, 0, c.f(m->tapP), 1152, 0, 1, (int)M, 1152, 192, c.st);
         }));
+      } else if (m->hchunk > 0 && m->hchunk < B && hfuse_now(m)) {
+        // chunks of G images through one P slab (its lines may still be in
+        // the memory-side cache when the combine reads them)
+        const int G = m->hchunk;
+        const size_t wpi = pf_gfuse_wplanes_bytes(1) / 2, rpi = pf_gfuse_ring_image_floats(H, W);
+        for (int b0 = 0; b0 < B; b0 += G) {
+          const int g = std::min(G, B - b0);
+          d.n = g;
+          PF_TRY(conv_desc_run(c, "head.conv2.up4tap", d, L + (size_t)b0 * h4 * w4 * 192,
+                               c.f(m->tapw), nullptr, nullptr, c.f(m->tapP),
+                               2.0 * g * h4 * w4 * 1152.0 * 192,
+                               m->wsplit ? reinterpret_cast<const unsigned short*>(c.f(m->tapwb))
+                                         : nullptr,
+                               1152LL * 192));
+          PF_TRY(timed(c, "head.conv2.gcombine", 0, [&] {
+            return pf_up4tap_gcombine(
+                g, H, W, c.f(m->tapP), img4 + (size_t)b0 * H * W * 4,
+                reinterpret_cast<const unsigned short*>(c.f(m->gf_wp)) + b0 * wpi,
+                c.f(m->gf_b) + (size_t)b0 * 128, c.f(m->gring) + b0 * rpi,
+                c2 + (size_t)b0 * H * W * 128, 128, c.d(m->tappart), mean + (size_t)b0 * 128,
+                rstd + (size_t)b0 * 128, c.st);
+          }));
+        }
       } else {
         PF_TRY(conv_desc_run(c, "head.conv2.up4tap", d, L, c.f(m->tapw), nullptr, nullptr,
                              c.f(m->tapP), 2.0 * B * h4 * w4 * 1152.0 * 192,
@@ -1346,7 +1376,9 @@ int head_forward(Ctx& c, float* img4, float* local_point, bool side) {
                                        : nullptr,
                              1152LL * 192));
       }
-      if (hfuse_now(m))
+      if (m->hchunk > 0 && m->hchunk < B && hfuse_now(m) && !m->tapb) {
+        // (done above, chunk by chunk)
+      } else if (hfuse_now(m))
         PF_TRY(timed(c, "head.conv2.gcombine", 0, [&] {
           return pf_up4tap_gcombine(B, H, W, c.f(m->tapP), img4,
                                     reinterpret_cast<const unsigned short*>(c.f(m->gf_wp)),

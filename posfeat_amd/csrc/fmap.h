@@ -128,6 +128,8 @@ size_t pf_gfuse_wplanes_bytes(int n);
 // the fused head (pf_up4tap_gcombine): weight planes + the border ring's G
 // values ring[b][r][128], r in pf_ring_index order
 size_t pf_gfuse_ring_floats(int n, int H, int W);
+// one image's border-ring floats (the ring part of pf_gfuse_ring_floats is image-major)
+size_t pf_gfuse_ring_image_floats(int H, int W);
 int pf_gfuse_prep(const float* img4, const float* c, int ccs, int n, int H, int W,
                   const float* wc, const float* bc, const float* mean, const float* rstd,
                   const float* b2, const float* w1_packed, const float* b1,

@@ -984,6 +984,8 @@ __global__ __launch_bounds__(256) void gfuse_ring_mfma_kernel(
 }
 
 // the ring buffer of the fused head, then the band scratch of its two passes
+size_t pf_gfuse_ring_image_floats(int H, int W) { return (size_t)gf_nring(H, W) * GF_COUT; }
+
 size_t pf_gfuse_ring_floats(int n, int H, int W) {
   return (size_t)n * gf_nring(H, W) * GF_COUT + (size_t)n * gf_nband(H, W) * GF_CG;
 }
