@@ -119,7 +119,10 @@ __device__ __forceinline__ void conv_epilogue_t(const ConvArgs& a, float* smem, 
   // the slice (BN = 192: 48 quads, 4 rows per pass, threads 192.. idle)
   constexpr int RPP0 = THREADS / C4;
   constexpr int RPP = RPP0 >= 16 ? 16 : RPP0 >= 8 ? 8 : RPP0 >= 4 ? 4 : RPP0 >= 2 ? 2 : 1;
-  static_assert(RPP0 == RPP || THREADS % C4 != 0, "every thread active when the quads divide");
+  // (every thread active when the quads divide a power-of-two block; six
+  // waves with BN = 128: 12 rows per pass rounded to 8, a third idle)
+  static_assert(RPP0 == RPP || THREADS % C4 != 0 || (THREADS & (THREADS - 1)) != 0,
+                "every thread active when the quads divide");
   static_assert(SR % RPP == 0, "rows per pass divide the slice");
   constexpr int NP = SR / RPP;       // passes per slice
   const int q = tid % C4, r0 = tid / C4;
@@ -1459,18 +1462,25 @@ __device__ __forceinline__ int bx_swz(int row) { return (0x78 >> (2 * ((row >> 2
 // strided convs with Cin % 32 == 0, the packed K order (cin/32, kh, kw, cin%32)),
 // 3 DU: dense rows from two maps (a bottleneck's conv3 + its downsample as one
 // GEMM, ConvArgs x2)
-template <int BN, int RB = 2, int AM = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
+// NW: waves stacked along M (4; 6 for TILE_BF6X_192x128)
+template <int BN, int RB = 2, int AM = 0, int NW = 4>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2)))
 void conv_bf6x_kernel(ConvArgs a) {
   constexpr bool G4 = AM == 1, GT = AM == 2, DU = AM == 3;
-  constexpr int NW = 4, BM = NW * RB * 16, NB = BN / 16;
+  constexpr int BM = NW * RB * 16, NB = BN / 16;
   constexpr int B_G = 3 * BN / 16 / NW;  // B DMA instructions per wave per chunk
   constexpr int NA = 2 * RB;             // A loads per lane per chunk
   constexpr int NOPS = B_G + NA;
   static_assert((3 * BN / 16) % NW == 0 && NOPS <= 2 * NB && (RB == 2 || RB == 4), "tile");
   constexpr int BSTAGE = 3 * BN * BK / 2;  // floats (u16 pairs)
   constexpr int RING = 2 * BSTAGE;
-  constexpr int SL = BM * (BN + 4) <= RING ? 1 : BM / 2 * (BN + 4) <= RING ? 2 : 4;
+  // epilogue row slices: whole waves per slice, the slice within the B ring
+  constexpr int WR = RB * 16;  // rows per wave
+  constexpr int SL = BM * (BN + 4) <= RING                                  ? 1
+                     : (BM / 2) % WR == 0 && BM / 2 * (BN + 4) <= RING     ? 2
+                     : BM % 3 == 0 && (BM / 3) % WR == 0 && BM / 3 * (BN + 4) <= RING ? 3
+                                                                            : 4;
+  static_assert(BM % SL == 0 && (BM / SL) % WR == 0 && BM / SL * (BN + 4) <= RING, "slices");
   constexpr int EPI = BM / SL * (BN + 4);
   __shared__ __attribute__((aligned(16))) float smem[RING > EPI ? RING : EPI];
   unsigned short* const Bs = reinterpret_cast<unsigned short*>(smem);
@@ -1665,7 +1675,7 @@ void conv_bf6x_kernel(ConvArgs a) {
   }
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
-  conv_epilogue_t<BM, BN, 256, SL, false>(
+  conv_epilogue_t<BM, BN, NW * 64, SL, false>(
       a, smem, tm, n0, split, [&](int row) { return m0 + row < a.M ? m0 + row : -1; }, m0 / a.hw,
       [&](int, int m) { return a.res ? a.res + (size_t)m * a.rcs : (const float*)nullptr; },
       [&](float* T, int sl) {
@@ -2342,7 +2352,8 @@ enum ConvTile {
   TILE_BF6X_128x128 = 29, TILE_BF6X_128x64 = 30,  // dense, 16x16x32 MFMAs (conv_bf6x_kernel)
   TILE_BF6X_256x128 = 31,
   TILE_BF6X_128x192 = 32,  // N % 192 == 0 (head.conv1's Winograd GEMMs, the tap GEMM): A read once per 192 columns
-  TILE_BF6X_128x256 = 33   // N % 256 == 0 batched GEMMs (A/B POSFEAT_BF6X_N256: A read once per 256 columns)
+  TILE_BF6X_128x256 = 33,  // N % 256 == 0 batched GEMMs (A/B POSFEAT_BF6X_N256: A read once per 256 columns)
+  TILE_BF6X_192x128 = 34   // dense: six waves stacked along M, the B tile's L2 -> CU bytes per output 2/3
 };
 
 // POSFEAT_BF6=1: every conv the row-tile DMA kernel serves (1x1, strided, the
@@ -2479,7 +2490,7 @@ Plan plan_for_tile(const ConvArgs& a, int tile) {
   if (bf6_on() && glds_ok) {
     // pre-split convs on the bf6x tiles (dense GEMMs, slab x tap gathers):
     // the 16x16x32 tiles only, and only they
-    const bool x_tile = tile >= TILE_BF6X_128x128 && tile <= TILE_BF6X_128x256;
+    const bool x_tile = tile >= TILE_BF6X_128x128 && tile <= TILE_BF6X_192x128;
     if (bf6x_on() && (dense_gemm(a) || gt_gemm(a))) {
       if (!x_tile) return p;
     } else {
@@ -2494,12 +2505,14 @@ Plan plan_for_tile(const ConvArgs& a, int tile) {
     case TILE_BF6X_256x128:
     case TILE_BF6X_128x192:
     case TILE_BF6X_128x256:
+    case TILE_BF6X_192x128:
       if (!bf6x_on() || !((glds_ok && (dense_gemm(a) || gt_gemm(a))) || g4_gemm(a))) return p;
       if (g4_gemm(a) && tile != TILE_BF6X_128x64) return p;
       if (tile == TILE_BF6X_128x192 && (!dense_gemm(a) || a.Cout % 192)) return p;
       if (tile == TILE_BF6X_128x256 && (!dense_gemm(a) || a.Cout % 256)) return p;
+      if (tile == TILE_BF6X_192x128 && !dense_gemm(a) && !a.x2) return p;
       p.kern = KERN_GLDS;
-      p.bm = tile == TILE_BF6X_256x128 ? 256 : 128;
+      p.bm = tile == TILE_BF6X_256x128 ? 256 : tile == TILE_BF6X_192x128 ? 192 : 128;
       p.bn = tile == TILE_BF6X_128x64    ? 64
              : tile == TILE_BF6X_128x192 ? 192
              : tile == TILE_BF6X_128x256 ? 256
@@ -2662,8 +2675,23 @@ void launch_rows(ConvArgs& a, int kern, hipStream_t st) {
     hipLaunchKernelGGL((conv_mfma_kernel<BM, BN, WM, WN, false>), grid, block, 0, st, a);
 }
 
-int conv_run(ConvArgs& a, const Plan& p, hipStream_t st) {
+// A/B (POSFEAT_BF6X_BM192=1): the dense / two-source 128 x 128 bf6x plans
+// run as 192 x 128 tiles
+static bool bf6x_bm192() {
+  static const bool on = [] {
+    const char* e = pf_ab_getenv("POSFEAT_BF6X_BM192");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
+int conv_run(ConvArgs& a, const Plan& p0, hipStream_t st) {
   if (!a.zero) return POSFEAT_E_HIP;
+  Plan p = p0;
+  if (bf6x_bm192() && p.tile == TILE_BF6X_128x128 && p.ksplit == 1 && (dense_gemm(a) || a.x2)) {
+    const Plan q = plan_for_tile(a, TILE_BF6X_192x128);
+    if (q.kern >= 0) p = q;
+  }
   a.tiles_n = (a.Cout + p.bn - 1) / p.bn;
   a.nwg = (int)(p.tiles_m * a.tiles_n);
   a.ksplit = p.ksplit;
@@ -2725,6 +2753,14 @@ int conv_run(ConvArgs& a, const Plan& p, hipStream_t st) {
     case TILE_BF6X_128x192:  // dense GEMMs only (plan_for_tile)
       hipLaunchKernelGGL((conv_bf6x_kernel<192>), dim3(a.nwg * a.ksplit, a.nbatch), dim3(256), 0,
                          st, a);
+      break;
+    case TILE_BF6X_192x128:  // dense / two-source GEMMs only (plan_for_tile)
+      if (a.x2)
+        hipLaunchKernelGGL((conv_bf6x_kernel<128, 2, 3, 6>), dim3(a.nwg * a.ksplit, a.nbatch),
+                           dim3(384), 0, st, a);
+      else
+        hipLaunchKernelGGL((conv_bf6x_kernel<128, 2, 0, 6>), dim3(a.nwg * a.ksplit, a.nbatch),
+                           dim3(384), 0, st, a);
       break;
     case TILE_BF6X_128x256:  // dense GEMMs only (plan_for_tile)
       hipLaunchKernelGGL((conv_bf6x_kernel<256>), dim3(a.nwg * a.ksplit, a.nbatch), dim3(256), 0,
@@ -3154,7 +3190,7 @@ int pf_conv_run_tile_bn(const posfeat_conv_desc* d, const float* x, const float*
     a.part = static_cast<float*>(ws);
   } else if (part && p.tiles_m * 2 * (size_t)a.Cout * sizeof(double) <= part_bytes &&
              p.tiles_m <= 0x7fffffff &&
-             !(p.tile >= TILE_BF6X_128x128 && p.tile <= TILE_BF6X_128x256)) {
+             !(p.tile >= TILE_BF6X_128x128 && p.tile <= TILE_BF6X_192x128)) {
     a.bnpart = part;
     *nparts = (int)p.tiles_m;
   }
