@@ -1471,7 +1471,7 @@ void conv_bf6x_kernel(ConvArgs a) {
   constexpr int B_G = 3 * BN / 16 / NW;  // B DMA instructions per wave per chunk
   constexpr int NA = 2 * RB;             // A loads per lane per chunk
   constexpr int NOPS = B_G + NA;
-  static_assert((3 * BN / 16) % NW == 0 && NOPS <= 2 * NB && (RB == 2 || RB == 4), "tile");
+  static_assert((3 * BN / 16) % NW == 0 && NOPS <= 3 * NB && (RB == 2 || RB == 4), "tile");
   constexpr int BSTAGE = 3 * BN * BK / 2;  // floats (u16 pairs)
   constexpr int RING = 2 * BSTAGE;
   // epilogue row slices: whole waves per slice, the slice within the B ring
@@ -2353,7 +2353,8 @@ enum ConvTile {
   TILE_BF6X_256x128 = 31,
   TILE_BF6X_128x192 = 32,  // N % 192 == 0 (head.conv1's Winograd GEMMs, the tap GEMM): A read once per 192 columns
   TILE_BF6X_128x256 = 33,  // N % 256 == 0 batched GEMMs (A/B POSFEAT_BF6X_N256: A read once per 256 columns)
-  TILE_BF6X_192x128 = 34   // dense: six waves stacked along M, the B tile's L2 -> CU bytes per output 2/3
+  TILE_BF6X_192x128 = 34,  // dense: six waves stacked along M, the B tile's L2 -> CU bytes per output 2/3
+  TILE_BF6X_256x64 = 35    // dense / G4 (the stem), 64 columns: RB = 4, half the B bytes per output
 };
 
 // POSFEAT_BF6=1: every conv the row-tile DMA kernel serves (1x1, strided, the
@@ -2490,7 +2491,7 @@ Plan plan_for_tile(const ConvArgs& a, int tile) {
   if (bf6_on() && glds_ok) {
     // pre-split convs on the bf6x tiles (dense GEMMs, slab x tap gathers):
     // the 16x16x32 tiles only, and only they
-    const bool x_tile = tile >= TILE_BF6X_128x128 && tile <= TILE_BF6X_192x128;
+    const bool x_tile = tile >= TILE_BF6X_128x128 && tile <= TILE_BF6X_256x64;
     if (bf6x_on() && (dense_gemm(a) || gt_gemm(a))) {
       if (!x_tile) return p;
     } else {
@@ -2506,14 +2507,18 @@ Plan plan_for_tile(const ConvArgs& a, int tile) {
     case TILE_BF6X_128x192:
     case TILE_BF6X_128x256:
     case TILE_BF6X_192x128:
+    case TILE_BF6X_256x64:
       if (!bf6x_on() || !((glds_ok && (dense_gemm(a) || gt_gemm(a))) || g4_gemm(a))) return p;
-      if (g4_gemm(a) && tile != TILE_BF6X_128x64) return p;
+      if (g4_gemm(a) && tile != TILE_BF6X_128x64 && tile != TILE_BF6X_256x64) return p;
       if (tile == TILE_BF6X_128x192 && (!dense_gemm(a) || a.Cout % 192)) return p;
       if (tile == TILE_BF6X_128x256 && (!dense_gemm(a) || a.Cout % 256)) return p;
       if (tile == TILE_BF6X_192x128 && !dense_gemm(a) && !a.x2) return p;
+      if (tile == TILE_BF6X_256x64 && !dense_gemm(a) && !g4_gemm(a)) return p;
       p.kern = KERN_GLDS;
-      p.bm = tile == TILE_BF6X_256x128 ? 256 : tile == TILE_BF6X_192x128 ? 192 : 128;
-      p.bn = tile == TILE_BF6X_128x64    ? 64
+      p.bm = tile == TILE_BF6X_256x128 || tile == TILE_BF6X_256x64 ? 256
+             : tile == TILE_BF6X_192x128                          ? 192
+                                                                  : 128;
+      p.bn = tile == TILE_BF6X_128x64 || tile == TILE_BF6X_256x64 ? 64
              : tile == TILE_BF6X_128x192 ? 192
              : tile == TILE_BF6X_128x256 ? 256
                                          : 128;
@@ -2692,6 +2697,15 @@ int conv_run(ConvArgs& a, const Plan& p0, hipStream_t st) {
     const Plan q = plan_for_tile(a, TILE_BF6X_192x128);
     if (q.kern >= 0) p = q;
   }
+  static const bool rb4n64 = [] {  // A/B: the 128 x 64 dense / stem plans on 256 x 64 tiles
+    const char* e = pf_ab_getenv("POSFEAT_BF6X_RB4N64");
+    return e && e[0] == '1';
+  }();
+  if (rb4n64 && p.tile == TILE_BF6X_128x64 && p.ksplit == 1 && (dense_gemm(a) || g4_gemm(a)) &&
+      !a.x2) {
+    const Plan q = plan_for_tile(a, TILE_BF6X_256x64);
+    if (q.kern >= 0) p = q;
+  }
   a.tiles_n = (a.Cout + p.bn - 1) / p.bn;
   a.nwg = (int)(p.tiles_m * a.tiles_n);
   a.ksplit = p.ksplit;
@@ -2753,6 +2767,14 @@ int conv_run(ConvArgs& a, const Plan& p0, hipStream_t st) {
     case TILE_BF6X_128x192:  // dense GEMMs only (plan_for_tile)
       hipLaunchKernelGGL((conv_bf6x_kernel<192>), dim3(a.nwg * a.ksplit, a.nbatch), dim3(256), 0,
                          st, a);
+      break;
+    case TILE_BF6X_256x64:
+      if (a.Cin == 4)
+        hipLaunchKernelGGL((conv_bf6x_kernel<64, 4, 1>), dim3(a.nwg * a.ksplit, a.nbatch),
+                           dim3(256), 0, st, a);
+      else
+        hipLaunchKernelGGL((conv_bf6x_kernel<64, 4>), dim3(a.nwg * a.ksplit, a.nbatch), dim3(256),
+                           0, st, a);
       break;
     case TILE_BF6X_192x128:  // dense / two-source GEMMs only (plan_for_tile)
       if (a.x2)
@@ -3190,7 +3212,7 @@ int pf_conv_run_tile_bn(const posfeat_conv_desc* d, const float* x, const float*
     a.part = static_cast<float*>(ws);
   } else if (part && p.tiles_m * 2 * (size_t)a.Cout * sizeof(double) <= part_bytes &&
              p.tiles_m <= 0x7fffffff &&
-             !(p.tile >= TILE_BF6X_128x128 && p.tile <= TILE_BF6X_192x128)) {
+             !(p.tile >= TILE_BF6X_128x128 && p.tile <= TILE_BF6X_256x64)) {
     a.bnpart = part;
     *nparts = (int)p.tiles_m;
   }
