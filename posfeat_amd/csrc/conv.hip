@@ -84,6 +84,13 @@ struct ConvArgs {
   // read x2 at input pixel (n, oh * s2, ow * s2) of its H2 x W2 map
   const float* x2;
   int x2cs, k1ch, H2, W2, s2;
+  // normalised A (conv_bf6x_kernel AM = 4, pf_conv_run_tile_np): each A value
+  // of image n, channel c enters as PReLU((x - amean[n][c]) * arstd[n][c])
+  // with slope *aslope -- instance norm + PReLU applied on load (in_apply's
+  // arithmetic), the normalised map never written
+  const float* amean;
+  const float* arstd;
+  const float* aslope;
 };
 
 // Epilogue shared by both kernels: acc -> LDS T[BM][BN+4] (conflict-free: a
@@ -1466,8 +1473,9 @@ __device__ __forceinline__ int bx_swz(int row) { return (0x78 >> (2 * ((row >> 2
 template <int BN, int RB = 2, int AM = 0, int NW = 4>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2)))
 void conv_bf6x_kernel(ConvArgs a) {
-  constexpr bool G4 = AM == 1, GT = AM == 2, DU = AM == 3;
+  constexpr bool G4 = AM == 1, GT = AM == 2, DU = AM == 3, NP = AM == 4;
   constexpr int BM = NW * RB * 16, NB = BN / 16;
+  constexpr int NPK = 256;  // NP: K <= NPK (the tap GEMM: 192)
   constexpr int B_G = 3 * BN / 16 / NW;  // B DMA instructions per wave per chunk
   constexpr int NA = 2 * RB;             // A loads per lane per chunk
   constexpr int NOPS = B_G + NA;
@@ -1483,6 +1491,8 @@ void conv_bf6x_kernel(ConvArgs a) {
   static_assert(BM % SL == 0 && (BM / SL) % WR == 0 && BM / SL * (BN + 4) <= RING, "slices");
   constexpr int EPI = BM / SL * (BN + 4);
   __shared__ __attribute__((aligned(16))) float smem[RING > EPI ? RING : EPI];
+  // NP: mean / rstd of the (at most two) images of the tile's rows, [2][2][NPK]
+  __shared__ __attribute__((aligned(16))) float anp[NP ? 4 * NPK : 4];
   unsigned short* const Bs = reinterpret_cast<unsigned short*>(smem);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1502,6 +1512,22 @@ void conv_bf6x_kernel(ConvArgs a) {
   const int tm = bid / a.tiles_n, tn = bid - tm * a.tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
   const int r16 = lane & 15, kq = lane >> 4;
+  int npo[NP ? RB : 1];  // NP: this lane's rows' parameter offsets in anp
+  float slope = 0.f;
+  if (NP) {
+    const int img0 = m0 / a.hw, img1 = min(m0 + BM - 1, a.M - 1) / a.hw;
+    for (int e = tid; e < 4 * NPK; e += NW * 64) {
+      const int im = e / (2 * NPK), which = (e / NPK) & 1, c = e % NPK;
+      const float* src = which ? a.arstd : a.amean;
+      anp[e] = c < a.Kpad ? src[(long long)(im ? img1 : img0) * a.Kpad + c] : 0.f;
+    }
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+      const int m = min(m0 + wave * RB * 16 + rb * 16 + r16, a.M - 1);
+      npo[rb] = (m / a.hw == img0 ? 0 : 2 * NPK) + kq * 8;
+    }
+    slope = *a.aslope;
+  }
   const float* xrow[RB];
   const float* xrow2[DU ? RB : 1];  // DU: the row in x2
   int ih0[RB], iw0[RB];  // G4: the row's top-left input tap
@@ -1624,6 +1650,23 @@ void conv_bf6x_kernel(ConvArgs a) {
     __builtin_amdgcn_s_barrier();   // every wave's B(ii) part landed; stage s^1 free
     const int s = ii & 1;
     u32x4_t ah[RB], am[RB], al[RB];
+    if (NP) {  // in_apply's arithmetic: (x - mean) * rstd, then PReLU
+      const int cb0 = (ch0 + ii) * BK;
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          const float* pp = anp + npo[rb] + cb0 + jj * 4;
+          const f32x4 mu = *reinterpret_cast<const f32x4*>(pp);
+          const f32x4 rs = *reinterpret_cast<const f32x4*>(pp + NPK);
+          f32x4 v = (va[rb][jj] - mu) * rs;
+          v.x = v.x > 0.f ? v.x : slope * v.x;
+          v.y = v.y > 0.f ? v.y : slope * v.y;
+          v.z = v.z > 0.f ? v.z : slope * v.z;
+          v.w = v.w > 0.f ? v.w : slope * v.w;
+          va[rb][jj] = v;
+        }
+    }
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) split3(va[rb][0], va[rb][1], ah[rb], am[rb], al[rb]);
     const int cb = min(ch0 + ii + 1, ch1 - 1);  // next B chunk (the last one re-read at the end)
@@ -2746,6 +2789,9 @@ int conv_run(ConvArgs& a, const Plan& p0, hipStream_t st) {
       if (a.x2)  // pf_conv_dual
         hipLaunchKernelGGL((conv_bf6x_kernel<128, 2, 3>), dim3(a.nwg * a.ksplit, a.nbatch),
                            dim3(256), 0, st, a);
+      else if (a.amean)  // pf_conv_run_tile_np
+        hipLaunchKernelGGL((conv_bf6x_kernel<128, 2, 4>), dim3(a.nwg * a.ksplit, a.nbatch),
+                           dim3(256), 0, st, a);
       else if (dense_gemm(a))
         hipLaunchKernelGGL((conv_bf6x_kernel<128>), dim3(a.nwg * a.ksplit, a.nbatch), dim3(256),
                            0, st, a);
@@ -2996,6 +3042,7 @@ static int conv_prepare(const posfeat_conv_desc* d, const float* x, const float*
   a.wplane = a.bwb = 0;
   a.x2 = nullptr;
   a.x2cs = a.k1ch = a.H2 = a.W2 = a.s2 = 0;
+  a.amean = a.arstd = a.aslope = nullptr;
   a.zero = conv_zero_ptr();  // checked at launch (planning calls need no device)
   return POSFEAT_OK;
 }
@@ -3144,6 +3191,30 @@ int pf_conv_dual(int n, int oh, int ow, const float* x1, int x1cs, int k1, const
   a.s2 = s2;
   Plan p = plan_for_tile(a, TILE_BF6X_128x128);
   if (p.kern < 0) return POSFEAT_E_INVALID;
+  return conv_run(a, p, st);
+}
+
+// pf_conv_run_tile for a dense 1x1 GEMM whose A is normalised on load
+// (ConvArgs amean / arstd / aslope: x's per-image channel mean / rstd, the
+// PReLU slope): head.conv2's tap GEMM straight from conv1's raw output, the
+// normalised L never written.  Only the 128 x 128 bf6x tile carries it
+// (POSFEAT_E_UNSUPPORTED otherwise: the caller normalises and runs the plain
+// GEMM).  Bit-identical to in_apply + the plain GEMM.
+int pf_conv_run_tile_np(const posfeat_conv_desc* d, const float* x, const float* w,
+                        float* y, int tile, hipStream_t st, const unsigned short* wb,
+                        long long wplane, const float* mean, const float* rstd,
+                        const float* slope) {
+  ConvArgs a;
+  PF_TRY(conv_prepare(d, x, w, nullptr, nullptr, y, a));
+  if (!wb || !mean || !rstd || !slope || a.Kpad > 256 || d->cin != a.Kpad) return POSFEAT_E_INVALID;
+  a.wb = wb;
+  a.wplane = wplane;
+  const Plan p = conv_plan(a, false, tile);
+  if (p.tile != TILE_BF6X_128x128 || p.ksplit != 1 || !dense_gemm(a) || bf6x_bm192())
+    return POSFEAT_E_UNSUPPORTED;
+  a.amean = mean;
+  a.arstd = rstd;
+  a.aslope = slope;
   return conv_run(a, p, st);
 }
 

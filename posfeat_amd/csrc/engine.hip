@@ -172,6 +172,9 @@ struct posfeat_model {
   // head.conv2's tap GEMM + combine in chunks of hchunk images reusing one P
   // slab (A/B: POSFEAT_HEAD_CHUNK=G; 0 = the whole batch per launch)
   int hchunk = 0;
+  // head.conv1's IN + PReLU applied inside the tap GEMM's A loads (conv1's raw
+  // output read directly; A/B: POSFEAT_NPFUSE=0 -- in_apply, then the GEMM)
+  bool npfuse = false;
   bool tapb = false;  // bf16x6 tap GEMM on pre-split planes (POSFEAT_BF6=2)
   Buf tapwb, tapLb;
   Buf gf_w, gf_b, gf_wp;
@@ -861,6 +864,8 @@ void plan(posfeat_model* m) {
   {
     const char* e = pf_ab_getenv("POSFEAT_HEAD_CHUNK");
     m->hchunk = e ? std::max(0, atoi(e)) : 0;
+    const char* f = pf_ab_getenv("POSFEAT_NPFUSE");
+    m->npfuse = m->wsplit && !m->train && !(f && f[0] == '0');
   }
   if (m->wino) {
     size_t uf = 0, wb = 0;
@@ -1271,9 +1276,15 @@ int head_forward(Ctx& c, float* img4, float* local_point, bool side) {
                    ? POSFEAT_OK
                    : POSFEAT_E_HIP;
       }));
-    PF_TRY(timed(c, "norm_prelu", 0, [&] {
-      return pf_in_apply(L, B, h4 * w4, 192, 192, mean1, rstd1, slope, c.st);
-    }));
+    // npf: the tap GEMM normalises conv1's output on load (below)
+    const bool npf = m->npfuse && !m->traintap && !m->tapb && m->up4tap && hfuse_now(m) &&
+                     !(m->hchunk > 0 && m->hchunk < B) && pf_bf6x_on();
+    auto norm_prelu = [&] {
+      return timed(c, "norm_prelu", 0, [&] {
+        return pf_in_apply(L, B, h4 * w4, 192, 192, mean1, rstd1, slope, c.st);
+      });
+    };
+    if (!npf) PF_TRY(norm_prelu());
     float* g64 = m->imgstats ? nullptr : c.f(m->g64);
     if (!side && m->imgstats)
       PF_TRY(timed(c, "head.convimg.stats", 0, [&] {
@@ -1370,11 +1381,30 @@ int head_forward(Ctx& c, float* img4, float* local_point, bool side) {
           }));
         }
       } else {
-        PF_TRY(conv_desc_run(c, "head.conv2.up4tap", d, L, c.f(m->tapw), nullptr, nullptr,
-                             c.f(m->tapP), 2.0 * B * h4 * w4 * 1152.0 * 192,
-                             m->wsplit ? reinterpret_cast<const unsigned short*>(c.f(m->tapwb))
-                                       : nullptr,
-                             1152LL * 192));
+        int rc = POSFEAT_E_UNSUPPORTED;
+        if (npf && !c.dry) {
+          // the tuned tile if there is one (else the DB's / the default plan)
+          int tile = -1;
+          auto it = m->tuned.find("head.conv2.up4tap");
+          if (it != m->tuned.end())
+            tile = it->second;
+          else if (!tile_lookup(d, false, true, &tile))
+            tile = -1;
+          rc = timed(c, "conv:head.conv2.up4tap", 2.0 * B * h4 * w4 * 1152.0 * 192, [&] {
+            return pf_conv_run_tile_np(&d, c1, c.f(m->tapw), c.f(m->tapP), tile, c.st,
+                                       reinterpret_cast<const unsigned short*>(c.f(m->tapwb)),
+                                       1152LL * 192, mean1, rstd1, slope);
+          });
+          if (rc != POSFEAT_OK && rc != POSFEAT_E_UNSUPPORTED) return rc;
+        }
+        if (rc != POSFEAT_OK) {  // (the planning pass, or a tile without the fused load)
+          if (npf) PF_TRY(norm_prelu());
+          PF_TRY(conv_desc_run(c, "head.conv2.up4tap", d, L, c.f(m->tapw), nullptr, nullptr,
+                               c.f(m->tapP), 2.0 * B * h4 * w4 * 1152.0 * 192,
+                               m->wsplit ? reinterpret_cast<const unsigned short*>(c.f(m->tapwb))
+                                         : nullptr,
+                               1152LL * 192));
+        }
       }
       if (m->hchunk > 0 && m->hchunk < B && hfuse_now(m) && !m->tapb) {
         // (done above, chunk by chunk)

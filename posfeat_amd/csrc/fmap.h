@@ -49,6 +49,12 @@ int pf_conv_dual(int n, int oh, int ow, const float* x1, int x1cs, int k1, const
                  int x2cs, int h2, int w2, int s2, int k2, int cout,
                  const unsigned short* wb, long long wplane, const float* bias, int act, float* y,
                  int ycs, hipStream_t st);
+// a dense 1x1 GEMM with A normalised on load: PReLU((x - mean) * rstd) per
+// image / channel (the 128 x 128 bf6x tile only, else POSFEAT_E_UNSUPPORTED)
+int pf_conv_run_tile_np(const posfeat_conv_desc* d, const float* x, const float* w,
+                        float* y, int tile, hipStream_t st, const unsigned short* wb,
+                        long long wplane, const float* mean, const float* rstd,
+                        const float* slope);
 int pf_dual_weights(const unsigned short* w1, int k1, const unsigned short* w2, int k2,
                     long long sp, int cout, const float* b1, const float* b2,
                     unsigned short* dst, float* bdst, hipStream_t st);

@@ -1,0 +1,66 @@
+"""Round-6 engine fusions against their unfused forms (the A/B build, in a
+child process):
+
+* POSFEAT_NPFUSE -- head.conv1's instance norm + PReLU applied inside the tap
+  GEMM's A loads (conv_bf6x_kernel AM = 4) instead of in_apply writing the
+  normalised map: the same arithmetic on the same values, so every output is
+  bit-identical;
+* POSFEAT_DSFUSE -- each stage's first bottleneck conv3 + downsample as one
+  two-source GEMM (posfeat_conv1x1_dual) instead of two convs: a different
+  fp32 summation order, so the maps agree within tests/tol.py's bounds.
+"""
+import numpy as np
+import pytest
+import torch
+
+import tol
+
+pytestmark = pytest.mark.gpu
+
+KEYS = ("local_map", "global_map", "local_map_small", "local_point", "global_feat")
+
+CHILD = """
+import os
+os.environ[%(var)r] = '0'
+import numpy as np, torch
+from posfeat_amd.engine import ExtractionEngine
+from posfeat_amd.weights import seeded_state_dicts, seeded_image
+bb, hd = seeded_state_dicts(0)
+eng = ExtractionEngine(bb, hd, device="cuda:0")
+img = torch.stack([torch.from_numpy(seeded_image(s, *%(hw)r)) for s in (4, 5)]).to("cuda:0")
+out = eng.run(img)
+torch.cuda.synchronize()
+np.savez(%(out)r, **{k: out[k].cpu().numpy() for k in %(keys)r})
+"""
+
+
+def _run_default(hw):
+    from posfeat_amd.engine import ExtractionEngine
+    from posfeat_amd.weights import seeded_image, seeded_state_dicts
+    bb, hd = seeded_state_dicts(0)
+    eng = ExtractionEngine(bb, hd, device="cuda:0")
+    img = torch.stack([torch.from_numpy(seeded_image(s, *hw)) for s in (4, 5)]).to("cuda:0")
+    out = eng.run(img)
+    torch.cuda.synchronize()
+    return {k: out[k].cpu().numpy() for k in KEYS}
+
+
+@pytest.mark.parametrize("hw", [(128, 160), (96, 224)])
+def test_tap_gemm_normalise_on_load_bit_identical(gpu, hw, tmp_path):
+    from conftest import run_ab_child
+    got = _run_default(hw)
+    out = str(tmp_path / "npfuse_off.npz")
+    ref = run_ab_child(CHILD % dict(var="POSFEAT_NPFUSE", hw=hw, out=out, keys=KEYS), out)
+    for k in KEYS:
+        assert np.array_equal(got[k], ref[k]), "%s differs (max %g)" % (
+            k, np.abs(got[k] - ref[k]).max())
+
+
+@pytest.mark.parametrize("hw", [(128, 160), (96, 224)])
+def test_conv3_downsample_gemm_vs_two_convs(gpu, hw, tmp_path):
+    from conftest import run_ab_child
+    got = _run_default(hw)
+    out = str(tmp_path / "dsfuse_off.npz")
+    ref = run_ab_child(CHILD % dict(var="POSFEAT_DSFUSE", hw=hw, out=out, keys=KEYS), out)
+    for k in KEYS:
+        tol.check(k, torch.from_numpy(got[k]), ref[k], "dsfuse " + k)
