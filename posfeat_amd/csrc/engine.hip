@@ -173,8 +173,12 @@ struct posfeat_model {
   // slab (A/B: POSFEAT_HEAD_CHUNK=G; 0 = the whole batch per launch)
   int hchunk = 0;
   // head.conv1's IN + PReLU applied inside the tap GEMM's A loads (conv1's raw
-  // output read directly; A/B: POSFEAT_NPFUSE=0 -- in_apply, then the GEMM)
+  // output read directly; A/B only, POSFEAT_NPFUSE=1: the tap GEMM slower by
+  // more than in_apply costs)
   bool npfuse = false;
+  // head.conv1's IN statistics from its F(6x6) output transform (A/B:
+  // POSFEAT_W6STATS=0 -- a statistics pass over conv1's output)
+  bool w6stats = true;
   bool tapb = false;  // bf16x6 tap GEMM on pre-split planes (POSFEAT_BF6=2)
   Buf tapwb, tapLb;
   Buf gf_w, gf_b, gf_wp;
@@ -600,13 +604,19 @@ bool up2fuse_on() {
   return on;
 }
 
+// stats (act none, F(6x6) only): the output transform also writes the
+// instance-norm partials of y (pf_wino6_conv); *stats_done says whether it did
 int conv3x3(Ctx& c, const std::string& name, const float* x, int n, int h, int w, int xcs, float* y,
-            int ycs, int act, int up2 = 0, float* xup = nullptr) {
+            int ycs, int act, int up2 = 0, float* xup = nullptr, double* stats = nullptr,
+            bool* stats_done = nullptr) {
   posfeat_model* m = c.m;
+  if (stats_done) *stats_done = false;
   const long long uo6 = wino6_u_offset(name, m->wsplit);
   if (m->wino && m->wino6 && !m->bf6p && uo6 >= 0 && (!up2 || up2fuse_on())) {
     const Spec* s = specs().find(name);
     if (c.dry) return POSFEAT_OK;
+    if (stats && (act != POSFEAT_ACT_NONE || s->cout % 64)) stats = nullptr;
+    if (stats_done) *stats_done = stats != nullptr;
     float* U = c.f(m->wino_u) + m->wino_u_f6 + uo6;
     const std::string ukey = name + "/6";
     if (!(m->wcache && m->store && m->store->wino_done.count(ukey))) {
@@ -622,7 +632,7 @@ int conv3x3(Ctx& c, const std::string& name, const float* x, int n, int h, int w
     auto stage = [&](int st_bits) {
       return pf_wino6_conv(x, xcs, n, h, w, s->cin, U, c.Bi(name), s->cout, act, y, ycs,
                            c.f(m->wino_ws), m->wino_ws.floats * sizeof(float), c.st, st_bits,
-                           m->wsplit ? 1 : 0, up2);
+                           m->wsplit ? 1 : 0, up2, nullptr, (st_bits & 4) ? stats : nullptr);
     };
     PF_TRY(timed(c, "wino:in:" + name, 0, [&] { return stage(1); }));
     PF_TRY(timed(c, "conv:" + name + ".wino", 2.0 * T * 64 * s->cin * s->cout,
@@ -865,7 +875,9 @@ void plan(posfeat_model* m) {
     const char* e = pf_ab_getenv("POSFEAT_HEAD_CHUNK");
     m->hchunk = e ? std::max(0, atoi(e)) : 0;
     const char* f = pf_ab_getenv("POSFEAT_NPFUSE");
-    m->npfuse = m->wsplit && !m->train && !(f && f[0] == '0');
+    m->npfuse = m->wsplit && !m->train && f && f[0] == '1';
+    const char* g = pf_ab_getenv("POSFEAT_W6STATS");
+    m->w6stats = !(g && g[0] == '0');
   }
   if (m->wino) {
     size_t uf = 0, wb = 0;
@@ -1257,11 +1269,23 @@ int head_forward(Ctx& c, float* img4, float* local_point, bool side) {
   float* c1 = c.f(m->c1raw);
   float* c2 = c.f(m->c2raw);
   if (m->wino && h4 % 2 == 0 && w4 % 2 == 0) {
-    // Winograd conv (bias, no act) + a separate statistics pass
-    PF_TRY(conv3x3(c, "head.conv1", headcat, B, h4, w4, 192, c1, 192, POSFEAT_ACT_NONE));
-    PF_TRY(timed(c, "instnorm", 0, [&] {
-      return pf_in_stats(c1, B, h4 * w4, 192, 192, mean1, rstd1, c.d(m->st_part), c.st);
-    }));
+    // Winograd conv (bias, no act); its output transform also sums the IN
+    // statistics when it can (F(6x6): pf_wino6_conv stats, A/B
+    // POSFEAT_W6STATS=0), else a separate statistics pass
+    const size_t need = (size_t)B * pf_wino6_stats_groups(h4, w4) * 192 * 2;
+    double* sp = m->w6stats && need <= m->st_part.floats / 2 ? c.d(m->st_part) : nullptr;
+    bool done = false;
+    PF_TRY(conv3x3(c, "head.conv1", headcat, B, h4, w4, 192, c1, 192, POSFEAT_ACT_NONE, 0,
+                   nullptr, sp, &done));
+    if (done)
+      PF_TRY(timed(c, "instnorm", 0, [&] {
+        return pf_in_finalize(sp, B, pf_wino6_stats_groups(h4, w4), h4 * w4, 192, mean1, rstd1,
+                              c.st);
+      }));
+    else
+      PF_TRY(timed(c, "instnorm", 0, [&] {
+        return pf_in_stats(c1, B, h4 * w4, 192, 192, mean1, rstd1, c.d(m->st_part), c.st);
+      }));
   } else {
     PF_TRY(conv_in(c, "head.conv1", headcat, B, h4, w4, 192, c1, 192, mean1, rstd1));
   }

@@ -104,10 +104,15 @@ size_t pf_wino6_weights_floats(int Cin, int Cout, bool planes);
 int pf_wino6_weights(const float* wpk, int Cout, int Cin, float* U, hipStream_t st, bool planes);
 // vkeep: V ([64][T][Cin] fp32, pf_wino6_v_floats) goes there instead of ws,
 // for the weight gradient of the same x (pf_wino6_wgrad's vpre)
+// stats (act none, Cout % 64 == 0): the output transform also writes the
+// instance-norm partial sums of y, stats[b][g][Cout][2] fp64 (sum, sum of
+// squares) over tile group g = 4 consecutive tiles of image b
+// (pf_wino6_stats_groups per image: pf_in_finalize's unshifted chunks)
 int pf_wino6_conv(const float* x, int xcs, int n, int h, int w, int Cin, const float* U,
                   const float* bias, int Cout, int act, float* y, int ycs, void* ws,
                   size_t ws_bytes, hipStream_t st, int stages = 7, int planes = 0, int up2 = 0,
-                  float* vkeep = nullptr);
+                  float* vkeep = nullptr, double* stats = nullptr);
+inline int pf_wino6_stats_groups(int h, int w) { return (((h + 5) / 6) * ((w + 5) / 6) + 3) / 4; }
 inline size_t pf_wino6_v_floats(int n, int h, int w, int Cin) {
   return (size_t)64 * n * ((h + 5) / 6) * ((w + 5) / 6) * Cin;
 }

@@ -911,6 +911,72 @@ __global__ __launch_bounds__(256) void wino6_output_kernel(const float* __restri
     }
   }
 }
+// wino6_output_kernel<1> (act none) whose block is 4 consecutive tiles of one
+// image x 64 channels, with the instance-norm partial sums of its outputs:
+// per thread fp64 sums over the tile's 36 outputs inside the map, the block's
+// four tiles summed in tile order (deterministic), written per (image, tile
+// group, channel) -- head.conv1's statistics without a pass over its output
+__global__ __launch_bounds__(256) void wino6_output_stats_kernel(
+    const float* __restrict__ M, int n, int h, int w, int C, const float* __restrict__ bias,
+    float* __restrict__ y, int ycs, double* __restrict__ part) {
+  const int th = (h + 5) / 6, tw = (w + 5) / 6, tpi = th * tw;
+  const int ng = (tpi + 3) / 4, ncq = C / 64;
+  const int cq = blockIdx.x % ncq, bg = blockIdx.x / ncq;
+  const int b = bg / ng, g = bg - b * ng;
+  const int ql = threadIdx.x & 63, tl = threadIdx.x >> 6;
+  const int q = cq * 64 + ql, ti = g * 4 + tl;  // tile within the image
+  const long long T = (long long)n * tpi;
+  double s1 = 0.0, s2 = 0.0;
+  if (ti < tpi) {
+    const int ty = ti / tw, tx = ti - ty * tw;
+    const long long tile = (long long)b * tpi + ti;
+    const float* mi = M + tile * C + q;
+    const long long xs = T * C;
+    float sa[6][8];  // A^T M
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+#pragma unroll
+      for (int c = 0; c < 8; ++c) sa[a][c] = 0.f;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      float m[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) m[c] = mi[(r * 8 + c) * xs];
+#pragma unroll
+      for (int a = 0; a < 6; ++a)
+        if (W6_AT[a][r] != 0.f)
+#pragma unroll
+          for (int c = 0; c < 8; ++c) sa[a][c] += W6_AT[a][r] * m[c];
+    }
+    const float bv = bias ? bias[q] : 0.f;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+      const int oy = 6 * ty + a;
+#pragma unroll
+      for (int bb = 0; bb < 6; ++bb) {
+        const int ox = 6 * tx + bb;
+        float o = bv;
+#pragma unroll
+        for (int c = 0; c < 8; ++c)
+          if (W6_AT[bb][c] != 0.f) o += W6_AT[bb][c] * sa[a][c];
+        if (oy < h && ox < w) {
+          y[(((long long)b * h + oy) * w + ox) * ycs + q] = o;
+          s1 += (double)o;
+          s2 += (double)o * (double)o;
+        }
+      }
+    }
+  }
+  __shared__ double red[4][64][2];
+  red[tl][ql][0] = s1;
+  red[tl][ql][1] = s2;
+  pf_syncthreads();
+  if (tl == 0) {
+    double* o = part + (((long long)b * ng + g) * C + q) * 2;
+    o[0] = ((red[0][ql][0] + red[1][ql][0]) + red[2][ql][0]) + red[3][ql][0];
+    o[1] = ((red[0][ql][1] + red[1][ql][1]) + red[2][ql][1]) + red[3][ql][1];
+  }
+}
 }  // namespace
 
 // ---- F(6x6) weight gradient (the train-mode decoder): dM = A dY A^T per 6x6
@@ -1069,7 +1135,8 @@ static bool w6in_vw1() {
 int pf_wino6_conv(const float* x, int xcs, int n, int h, int w, int Cin, const float* U,
                   const float* bias, int Cout, int act, float* y, int ycs, void* ws,
                   size_t ws_bytes, hipStream_t st, int stages, int planes, int up2,
-                  float* vkeep) {
+                  float* vkeep, double* stats) {
+  if (stats && (act != POSFEAT_ACT_NONE || Cout % 64)) return POSFEAT_E_INVALID;
   if (Cin % 32 || Cout % 4 || xcs % 2 || ycs % 2 || n <= 0 || h <= 0 || w <= 0 || planes > 1)
     return POSFEAT_E_INVALID;
   if (up2 && ((h & 1) || (w & 1))) return POSFEAT_E_INVALID;
@@ -1095,7 +1162,12 @@ int pf_wino6_conv(const float* x, int xcs, int n, int h, int w, int Cin, const f
   if (stages & 2)
     PF_TRY(pf_gemm_batched(V, Cin, T * Cin, U, (long long)Cout * Cin, M, Cout, T * Cout, 64, (int)T,
                            Cout, Cin, st, Ub, 64LL * Cout * Cin));
-  if (stages & 4) {
+  if ((stages & 4) && stats) {
+    const int ng = pf_wino6_stats_groups(h, w);
+    hipLaunchKernelGGL(wino6_output_stats_kernel, dim3((unsigned)(n * ng * (Cout / 64))),
+                       dim3(256), 0, st, M, n, h, w, Cout, bias, y, ycs, stats);
+    PF_CHECK_LAUNCH();
+  } else if (stages & 4) {
     if (w6out_vw1())  // A/B: one channel per thread
       hipLaunchKernelGGL((wino6_output_kernel<1>), dim3(grid_for(T * Cout, 256)), dim3(256), 0, st,
                          M, n, h, w, Cout, bias, act, y, ycs);

@@ -1,10 +1,12 @@
 """Round-6 engine fusions against their unfused forms (the A/B build, in a
 child process):
 
-* POSFEAT_NPFUSE -- head.conv1's instance norm + PReLU applied inside the tap
-  GEMM's A loads (conv_bf6x_kernel AM = 4) instead of in_apply writing the
-  normalised map: the same arithmetic on the same values, so every output is
-  bit-identical;
+* POSFEAT_NPFUSE=1 (A/B, off by default) -- head.conv1's instance norm +
+  PReLU applied inside the tap GEMM's A loads (conv_bf6x_kernel AM = 4)
+  instead of in_apply writing the normalised map: the same arithmetic on the
+  same values, so every output is bit-identical;
+* POSFEAT_W6STATS -- head.conv1's instance-norm statistics from its F(6x6)
+  output transform instead of a pass over its output;
 * POSFEAT_DSFUSE -- each stage's first bottleneck conv3 + downsample as one
   two-source GEMM (posfeat_conv1x1_dual) instead of two convs: a different
   fp32 summation order, so the maps agree within tests/tol.py's bounds.
@@ -21,7 +23,7 @@ KEYS = ("local_map", "global_map", "local_map_small", "local_point", "global_fea
 
 CHILD = """
 import os
-os.environ[%(var)r] = '0'
+os.environ[%(var)r] = %(val)r
 import numpy as np, torch
 from posfeat_amd.engine import ExtractionEngine
 from posfeat_amd.weights import seeded_state_dicts, seeded_image
@@ -49,8 +51,8 @@ def _run_default(hw):
 def test_tap_gemm_normalise_on_load_bit_identical(gpu, hw, tmp_path):
     from conftest import run_ab_child
     got = _run_default(hw)
-    out = str(tmp_path / "npfuse_off.npz")
-    ref = run_ab_child(CHILD % dict(var="POSFEAT_NPFUSE", hw=hw, out=out, keys=KEYS), out)
+    out = str(tmp_path / "npfuse_on.npz")
+    ref = run_ab_child(CHILD % dict(var="POSFEAT_NPFUSE", val="1", hw=hw, out=out, keys=KEYS), out)
     for k in KEYS:
         assert np.array_equal(got[k], ref[k]), "%s differs (max %g)" % (
             k, np.abs(got[k] - ref[k]).max())
@@ -61,6 +63,22 @@ def test_conv3_downsample_gemm_vs_two_convs(gpu, hw, tmp_path):
     from conftest import run_ab_child
     got = _run_default(hw)
     out = str(tmp_path / "dsfuse_off.npz")
-    ref = run_ab_child(CHILD % dict(var="POSFEAT_DSFUSE", hw=hw, out=out, keys=KEYS), out)
+    ref = run_ab_child(CHILD % dict(var="POSFEAT_DSFUSE", val="0", hw=hw, out=out, keys=KEYS), out)
     for k in KEYS:
         tol.check(k, torch.from_numpy(got[k]), ref[k], "dsfuse " + k)
+
+
+@pytest.mark.parametrize("hw", [(128, 160), (96, 224)])
+def test_conv1_stats_from_output_transform(gpu, hw, tmp_path):
+    """POSFEAT_W6STATS: head.conv1's instance-norm statistics summed by its
+    F(6x6) output transform (fp64 per tile group) vs the statistics pass over
+    its output; the backbone maps are untouched (bit-identical), the score map
+    within its bound."""
+    from conftest import run_ab_child
+    got = _run_default(hw)
+    out = str(tmp_path / "w6stats_off.npz")
+    ref = run_ab_child(CHILD % dict(var="POSFEAT_W6STATS", val="0", hw=hw, out=out, keys=KEYS), out)
+    for k in ("local_map", "global_map", "local_map_small", "global_feat"):
+        assert np.array_equal(got[k], ref[k]), k
+    tol.check("local_point", torch.from_numpy(got["local_point"]), ref["local_point"],
+              "w6stats local_point")
