@@ -91,6 +91,8 @@ struct ConvArgs {
   const float* amean;
   const float* arstd;
   const float* aslope;
+  // also write y NCHW here ([n][Cout][OH*OW]; PfNchwSink): conv_epilogue_t
+  float* ynchw;
 };
 
 // Epilogue shared by both kernels: acc -> LDS T[BM][BN+4] (conflict-free: a
@@ -199,6 +201,41 @@ __device__ __forceinline__ void conv_epilogue_t(const ConvArgs& a, float* smem, 
         } else {
           s1[0] += v;
           s2[0] += v * v;
+        }
+      }
+    }
+    if (a.ynchw) {
+      // the slice again, column-major: 4 consecutive rows (pixels) of one
+      // column per float4 store into [n][Cout][hw]; the same bias + act
+      // arithmetic as the NHWC store above (no residual on this path)
+      constexpr int R4 = SR / 4;           // 4-row groups in the slice
+      for (int e = tid; e < R4 * BN; e += THREADS) {
+        const int cc = e % BN, g4 = e / BN;
+        const int colx = n0 + cc;
+        if (colx >= a.Cout) continue;
+        const float bcol = (a.ksplit <= 1 && a.bias) ? a.bias[colx] : 0.f;
+        float o4[4];
+        int mm[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int row = g4 * 4 + k;
+          mm[k] = rowm(s * SR + row);
+          float v = T[row * TP + cc] + bcol;
+          if (a.act == POSFEAT_ACT_RELU) v = fmaxf(v, 0.f);
+          else if (a.act == POSFEAT_ACT_ELU) v = pf_elu(v);
+          o4[k] = v;
+        }
+        const int nimg = mm[0] >= 0 ? mm[0] / a.hw : -1, p0 = mm[0] - nimg * a.hw;
+        if (nimg >= 0 && mm[3] == mm[0] + 3 && (p0 & 3) == 0 && p0 + 3 < a.hw) {
+          *reinterpret_cast<f32x4*>(a.ynchw + ((size_t)nimg * a.Cout + colx) * a.hw + p0) =
+              f32x4{o4[0], o4[1], o4[2], o4[3]};
+        } else {
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (mm[k] >= 0) {
+              const int ni = mm[k] / a.hw;
+              a.ynchw[((size_t)ni * a.Cout + colx) * a.hw + (mm[k] - ni * a.hw)] = o4[k];
+            }
         }
       }
     }
@@ -2733,9 +2770,19 @@ static bool bf6x_bm192() {
   return on;
 }
 
+thread_local float* tl_nchw_sink = nullptr;
+thread_local bool tl_nchw_done = false;
+
 int conv_run(ConvArgs& a, const Plan& p0, hipStream_t st) {
   if (!a.zero) return POSFEAT_E_HIP;
   Plan p = p0;
+  // (the bf6x tiles' epilogue, conv_epilogue_t, carries the NCHW pass;
+  // split-K plans write y in the reduce kernel instead)
+  const bool xt = p.tile >= TILE_BF6X_128x128 && p.tile <= TILE_BF6X_256x64;
+  a.ynchw = (tl_nchw_sink && xt && p.ksplit <= 1 && a.nbatch <= 1 && !a.res && a.hw % 4 == 0)
+                ? tl_nchw_sink
+                : nullptr;
+  tl_nchw_done = a.ynchw != nullptr;
   if (bf6x_bm192() && p.tile == TILE_BF6X_128x128 && p.ksplit == 1 && (dense_gemm(a) || a.x2)) {
     const Plan q = plan_for_tile(a, TILE_BF6X_192x128);
     if (q.kern >= 0) p = q;
@@ -2968,6 +3015,12 @@ PfHaloFp32Scope::~PfHaloFp32Scope() {
     --tl_stem32;
   }
 }
+PfNchwSink::PfNchwSink(float* dst) {
+  tl_nchw_sink = dst;
+  tl_nchw_done = false;
+}
+PfNchwSink::~PfNchwSink() { tl_nchw_sink = nullptr; }
+bool PfNchwSink::done() const { return tl_nchw_done; }
 PfDense32Scope::PfDense32Scope(bool on) : on_(on) { tl_dense32 += on ? 1 : 0; }
 PfDense32Scope::~PfDense32Scope() { tl_dense32 -= on_ ? 1 : 0; }
 
@@ -3043,6 +3096,7 @@ static int conv_prepare(const posfeat_conv_desc* d, const float* x, const float*
   a.x2 = nullptr;
   a.x2cs = a.k1ch = a.H2 = a.W2 = a.s2 = 0;
   a.amean = a.arstd = a.aslope = nullptr;
+  a.ynchw = nullptr;
   a.zero = conv_zero_ptr();  // checked at launch (planning calls need no device)
   return POSFEAT_OK;
 }

@@ -179,6 +179,9 @@ struct posfeat_model {
   // head.conv1's IN statistics from its F(6x6) output transform (A/B:
   // POSFEAT_W6STATS=0 -- a statistics pass over conv1's output)
   bool w6stats = true;
+  // conv_fine's epilogue writes local_map NCHW too (A/B: POSFEAT_NCHWSINK=0 --
+  // the layout pass)
+  bool nchwsink = true;
   bool tapb = false;  // bf16x6 tap GEMM on pre-split planes (POSFEAT_BF6=2)
   Buf tapwb, tapLb;
   Buf gf_w, gf_b, gf_wp;
@@ -878,6 +881,8 @@ void plan(posfeat_model* m) {
     m->npfuse = m->wsplit && !m->train && f && f[0] == '1';
     const char* g = pf_ab_getenv("POSFEAT_W6STATS");
     m->w6stats = !(g && g[0] == '0');
+    const char* k = pf_ab_getenv("POSFEAT_NCHWSINK");
+    m->nchwsink = !(k && k[0] == '0');
   }
   if (m->wino) {
     size_t uf = 0, wb = 0;
@@ -1159,6 +1164,7 @@ int forward(Ctx& c, const float* img, posfeat_extract_out* out, int mode, const 
             w16 = W / 16;
   float* img4 = c.f(m->img4);
   float* headcat = c.f(m->headcat);
+  bool lm_nchw = false;  // conv_fine wrote local_map NCHW (PfNchwSink)
   // ---- ResUNet (DescNet.py:64-84) -----------------------------------------
   // (the planning pass runs before the instance has its store)
   if (m->wsplit && !(m->wcache && m->store && m->store->wpl_done)) {  // the blob's bf16 planes
@@ -1221,7 +1227,13 @@ int forward(Ctx& c, const float* img, posfeat_extract_out* out, int mode, const 
   PF_TRY(conv3x3(c, "upconv2.conv", c.f(m->d3), B, h4, w4, 512, cat2, 512, POSFEAT_ACT_ELU, 1,
                  c.f(m->up2)));
   PF_TRY(conv3x3(c, "iconv2", cat2, B, h4, w4, 512, c.f(m->d2), 256, POSFEAT_ACT_ELU));
-  PF_TRY(conv(c, "conv_fine", c.f(m->d2), B, h4, w4, 256, headcat, 192, 1, POSFEAT_ACT_ELU));
+  // conv_fine also writes local_map NCHW from its epilogue when the caller
+  // wants it (PfNchwSink; else the layout pass below)
+  {
+    const PfNchwSink sink(out && out->local_map && !c.dry && m->nchwsink ? out->local_map : nullptr);
+    PF_TRY(conv(c, "conv_fine", c.f(m->d2), B, h4, w4, 256, headcat, 192, 1, POSFEAT_ACT_ELU));
+    lm_nchw = sink.done();
+  }
   }
   if (side && side_at == 4 && mode != MODE_HEAD) PF_TRY(image_branch(c, img4));
   if (mode != MODE_BACKBONE) PF_TRY(head_forward(c, img4, out->local_point, side));
@@ -1231,7 +1243,7 @@ int forward(Ctx& c, const float* img, posfeat_extract_out* out, int mode, const 
       PF_TRY(timed(c, "global_feat", 0, [&] {
         return pf_global_feat(c.f(m->gmap), B, h16 * w16, 128, out->global_feat, c.st);
       }));
-    if (out->local_map)
+    if (out->local_map && !lm_nchw)
       PF_TRY(timed(c, "layout:out", 0, [&] {
         return pf_nhwc_to_nchw(headcat, B, 128, h4, w4, 192, out->local_map, c.st);
       }));

@@ -223,6 +223,17 @@ struct PfHaloFp32Scope {
 // 32x32x16 bf6d tiles instead of the 16x16x32 conv_bf6x_kernel: the training
 // steps' forward / backward keep the arithmetic their fp64-pinned fixtures
 // validated (PfHaloFp32Scope implies it).
+// The convs run in this scope also write their output NCHW ([n][cout][oh*ow],
+// fp32) to `dst` from the epilogue (conv_epilogue_t; not for split-K plans):
+// conv_fine's local_map without the layout pass.  done() says whether the last
+// conv in the scope did.
+struct PfNchwSink {
+  explicit PfNchwSink(float* dst);
+  ~PfNchwSink();
+  bool done() const;
+  PfNchwSink(const PfNchwSink&) = delete;
+  PfNchwSink& operator=(const PfNchwSink&) = delete;
+};
 struct PfDense32Scope {
   explicit PfDense32Scope(bool on);
   ~PfDense32Scope();
