@@ -208,9 +208,10 @@ __device__ __forceinline__ void conv_epilogue_t(const ConvArgs& a, float* smem, 
       // the slice again, column-major: 4 consecutive rows (pixels) of one
       // column per float4 store into [n][Cout][hw]; the same bias + act
       // arithmetic as the NHWC store above (no residual on this path)
+      // (lanes walk the pixels of one column: a wave stores 256-B runs)
       constexpr int R4 = SR / 4;           // 4-row groups in the slice
       for (int e = tid; e < R4 * BN; e += THREADS) {
-        const int cc = e % BN, g4 = e / BN;
+        const int g4 = e % R4, cc = e / R4;
         const int colx = n0 + cc;
         if (colx >= a.Cout) continue;
         const float bcol = (a.ksplit <= 1 && a.bias) ? a.bias[colx] : 0.f;
