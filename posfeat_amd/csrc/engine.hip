@@ -179,9 +179,9 @@ struct posfeat_model {
   // head.conv1's IN statistics from its F(6x6) output transform (A/B:
   // POSFEAT_W6STATS=0 -- a statistics pass over conv1's output)
   bool w6stats = true;
-  // conv_fine's epilogue writes local_map NCHW too (A/B: POSFEAT_NCHWSINK=0 --
-  // the layout pass)
-  bool nchwsink = true;
+  // conv_fine's epilogue writes local_map NCHW too (A/B only,
+  // POSFEAT_NCHWSINK=1: measured even with the layout pass)
+  bool nchwsink = false;
   bool tapb = false;  // bf16x6 tap GEMM on pre-split planes (POSFEAT_BF6=2)
   Buf tapwb, tapLb;
   Buf gf_w, gf_b, gf_wp;
@@ -882,7 +882,7 @@ void plan(posfeat_model* m) {
     const char* g = pf_ab_getenv("POSFEAT_W6STATS");
     m->w6stats = !(g && g[0] == '0');
     const char* k = pf_ab_getenv("POSFEAT_NCHWSINK");
-    m->nchwsink = !(k && k[0] == '0');
+    m->nchwsink = k && k[0] == '1';
   }
   if (m->wino) {
     size_t uf = 0, wb = 0;

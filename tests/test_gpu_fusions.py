@@ -7,8 +7,8 @@ child process):
   same values, so every output is bit-identical;
 * POSFEAT_W6STATS -- head.conv1's instance-norm statistics from its F(6x6)
   output transform instead of a pass over its output;
-* POSFEAT_NCHWSINK -- conv_fine's epilogue writes local_map NCHW too (no layout
-  pass): bit-identical;
+* POSFEAT_NCHWSINK=1 (A/B, off by default) -- conv_fine's epilogue writes
+  local_map NCHW too (no layout pass): bit-identical;
 * POSFEAT_DSFUSE -- each stage's first bottleneck conv3 + downsample as one
   two-source GEMM (posfeat_conv1x1_dual) instead of two convs: a different
   fp32 summation order, so the maps agree within tests/tol.py's bounds.
@@ -88,13 +88,13 @@ def test_conv1_stats_from_output_transform(gpu, hw, tmp_path):
 
 @pytest.mark.parametrize("hw", [(128, 160), (96, 224)])
 def test_local_map_nchw_from_conv_fine_epilogue(gpu, hw, tmp_path):
-    """POSFEAT_NCHWSINK: conv_fine's epilogue writes local_map NCHW as well
+    """POSFEAT_NCHWSINK=1: conv_fine's epilogue writes local_map NCHW as well
     (the same bias + ELU on the same tile values) instead of the layout pass
     over its NHWC output: every output bit-identical."""
     from conftest import run_ab_child
     got = _run_default(hw)
-    out = str(tmp_path / "nchwsink_off.npz")
-    ref = run_ab_child(CHILD % dict(var="POSFEAT_NCHWSINK", val="0", hw=hw, out=out, keys=KEYS), out)
+    out = str(tmp_path / "nchwsink_on.npz")
+    ref = run_ab_child(CHILD % dict(var="POSFEAT_NCHWSINK", val="1", hw=hw, out=out, keys=KEYS), out)
     for k in KEYS:
         assert np.array_equal(got[k], ref[k]), "%s differs (max %g)" % (
             k, np.abs(got[k] - ref[k]).max())
