@@ -1775,6 +1775,131 @@ void conv_bf6x_kernel(ConvArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Weight-stationary tap GEMM (head.conv2's [M x 192] x [192 x 1152], K = 192):
+// in conv_bf6x_kernel every 128-row M tile re-reads its 128 x 192 weight
+// planes (147 KB, 6 B per weight) from L2 -- 1.5 K / BM of the output bytes,
+// the largest operand stream of a short-K GEMM.  Here a persistent block
+// keeps its 128 output columns' planes resident in LDS (loaded once, in the
+// bf6x stage layout and swizzle) and walks M tiles of 256 rows (8 waves x 32
+// rows, A straight to registers one chunk ahead, split3, the same six bf16
+// MFMA terms per 16x16x32 step and the same k order as conv_bf6x_kernel: the
+// same sums); the accumulators are stored straight from the registers.
+// Block b: column tile b % (N / 128), M tiles b / (N / 128) + i * per_n.
+constexpr int WS_BN = 128, WS_K = 192, WS_NCH = WS_K / BK, WS_NW = 8, WS_BM = WS_NW * 32;
+struct WsArgs {
+  const float* x;
+  const unsigned short* wb;
+  float* y;
+  long long wplane;
+  int lda, ldc, M, N, per_n;
+};
+
+__global__ __launch_bounds__(512) void tap_gemm_ws_kernel(WsArgs a) {
+  __shared__ __attribute__((aligned(16))) unsigned short Bres[WS_NCH * 3 * WS_BN * BK];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ntn = a.N / WS_BN;
+  const int tn = blockIdx.x % ntn, j = blockIdx.x / ntn;
+  const int n0 = tn * WS_BN;
+  const int ntm = (a.M + WS_BM - 1) / WS_BM;
+  if (j >= ntm) return;  // block-uniform, before the only barrier
+  // the block's weight planes, resident: [chunk][plane][row][BK], 16-B slot s
+  // of row r at s ^ bx_swz(r) (conv_bf6x_kernel's stage layout)
+  for (int e = tid; e < WS_NCH * 3 * WS_BN * 4; e += WS_NW * 64) {
+    const int sl = e & 3, row = (e >> 2) % WS_BN, cp = (e >> 2) / WS_BN;
+    const int c = cp / 3, pl = cp - c * 3;
+    const u32x4_t v = *reinterpret_cast<const u32x4_t*>(
+        a.wb + pl * a.wplane + (long long)(n0 + row) * WS_K + c * BK + sl * 8);
+    *reinterpret_cast<u32x4_t*>(Bres + (cp * WS_BN + row) * BK + (sl ^ bx_swz(row)) * 8) = v;
+  }
+  pf_syncthreads();
+  const int r16 = lane & 15, kq = lane >> 4;
+  auto rowp = [&](int mt, int rb) {
+    const int m = min(mt * WS_BM + wave * 32 + rb * 16 + r16, a.M - 1);
+    return a.x + (long long)m * a.lda + kq * 8;
+  };
+  int mt = j;
+  const float* xr[2] = {rowp(mt, 0), rowp(mt, 1)};
+  f32x4 va[2][2][2];  // [buffer][rb][jj]
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) va[0][rb][jj] = *reinterpret_cast<const f32x4*>(xr[rb] + jj * 4);
+  for (;;) {
+    f32x4 acc[2][8];
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int nb = 0; nb < 8; ++nb) acc[rb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int nmt = mt + a.per_n;
+    const bool more = nmt < ntm;
+    // one chunk: split buffer `cur`, load the next chunk into the other, 96 MFMAs
+    auto step = [&](int c, auto cur_t) __attribute__((always_inline)) {
+      constexpr int cur = decltype(cur_t)::value;
+      u32x4_t ah[2], am[2], al[2];
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) split3(va[cur][rb][0], va[cur][rb][1], ah[rb], am[rb], al[rb]);
+      // the next chunk's A (the next M tile's first chunk after the last)
+      if (c + 1 < WS_NCH) {
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj)
+            va[cur ^ 1][rb][jj] =
+                *reinterpret_cast<const f32x4*>(xr[rb] + (c + 1) * BK + jj * 4);
+      } else if (more) {
+        xr[0] = rowp(nmt, 0);
+        xr[1] = rowp(nmt, 1);
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj)
+            va[cur ^ 1][rb][jj] = *reinterpret_cast<const f32x4*>(xr[rb] + jj * 4);
+      }
+      const unsigned short* Bc = Bres + c * 3 * WS_BN * BK;
+#pragma unroll
+      for (int nb = 0; nb < 8; ++nb) {
+        const int row = nb * 16 + r16;
+        const unsigned short* bp = Bc + row * BK + (kq ^ bx_swz(row)) * 8;
+        const u32x4_t bh = *reinterpret_cast<const u32x4_t*>(bp);
+        const u32x4_t bm = *reinterpret_cast<const u32x4_t*>(bp + WS_BN * BK);
+        const u32x4_t bl = *reinterpret_cast<const u32x4_t*>(bp + 2 * WS_BN * BK);
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+          f32x4 cc = acc[rb][nb];
+          cc = mfma16_bf16(ah[rb], bh, cc);
+          cc = mfma16_bf16(ah[rb], bm, cc);
+          cc = mfma16_bf16(am[rb], bh, cc);
+          cc = mfma16_bf16(ah[rb], bl, cc);
+          cc = mfma16_bf16(al[rb], bh, cc);
+          cc = mfma16_bf16(am[rb], bm, cc);
+          acc[rb][nb] = cc;
+        }
+      }
+    };
+#pragma unroll 1
+    for (int c = 0; c < WS_NCH; c += 2) {
+      step(c, std::integral_constant<int, 0>{});
+      step(c + 1, std::integral_constant<int, 1>{});
+    }
+    // (WS_NCH even: the next tile's first chunk sits in buffer 0)
+    static_assert(WS_NCH % 2 == 0, "chunk parity");
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+      const int mb = mt * WS_BM + wave * 32 + rb * 16 + kq * 4;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (mb + i >= a.M) continue;
+        float* yr = a.y + (long long)(mb + i) * a.ldc + n0 + r16;
+#pragma unroll
+        for (int nb = 0; nb < 8; ++nb) yr[nb * 16] = acc[rb][nb][i];
+      }
+    }
+    if (!more) break;
+    mt = nmt;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Spatial-halo variant for stride-1 convs with Cin % 32 == 0 (every 3x3
 // decoder/head layer).  The M tile is a PH x 16 patch of output pixels of one
 // image; for each 32-channel slab its (PH+KH-1) x (16+KW-1) input halo is
@@ -3247,6 +3372,27 @@ int pf_conv_dual(int n, int oh, int ow, const float* x1, int x1cs, int k1, const
   Plan p = plan_for_tile(a, TILE_BF6X_128x128);
   if (p.kern < 0) return POSFEAT_E_INVALID;
   return conv_run(a, p, st);
+}
+
+// head.conv2's tap GEMM on the weight-stationary persistent kernel
+// (tap_gemm_ws_kernel): y [M][ldc] = x [M][lda] . W^T, W as three bf16 planes
+// [3][N][192] (plane stride wplane).  K = 192, N % 128 == 0.
+int pf_tap_gemm_ws(const float* x, int lda, int M, const unsigned short* wb, long long wplane,
+                   int N, float* y, int ldc, hipStream_t st) {
+  if (!x || !wb || !y || M <= 0 || N % WS_BN || lda < WS_K || ldc < N || lda % 4 || ldc % 4)
+    return POSFEAT_E_INVALID;
+  int dev = 0, ncu = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return POSFEAT_E_HIP;
+  const int ntn = N / WS_BN, ntm = (M + WS_BM - 1) / WS_BM;
+  const int per_n = std::max(1, std::min(ntm, ncu / ntn));  // one block per CU
+  WsArgs a{x, wb, y, wplane, lda, ldc, M, N, per_n};
+  hipLaunchKernelGGL(tap_gemm_ws_kernel, dim3((unsigned)(per_n * ntn)), dim3(WS_NW * 64), 0, st,
+                     a);
+  PF_CHECK_LAUNCH();
+  pf_note_arith(PF_ARITH_BF6);
+  return POSFEAT_OK;
 }
 
 // pf_conv_run_tile for a dense 1x1 GEMM whose A is normalised on load

@@ -182,6 +182,9 @@ struct posfeat_model {
   // conv_fine's epilogue writes local_map NCHW too (A/B only,
   // POSFEAT_NCHWSINK=1: measured even with the layout pass)
   bool nchwsink = false;
+  // head.conv2's tap GEMM on the weight-stationary persistent kernel
+  // (pf_tap_gemm_ws; A/B: POSFEAT_TAPWS)
+  bool tapws = false;
   bool tapb = false;  // bf16x6 tap GEMM on pre-split planes (POSFEAT_BF6=2)
   Buf tapwb, tapLb;
   Buf gf_w, gf_b, gf_wp;
@@ -883,6 +886,8 @@ void plan(posfeat_model* m) {
     m->w6stats = !(g && g[0] == '0');
     const char* k = pf_ab_getenv("POSFEAT_NCHWSINK");
     m->nchwsink = k && k[0] == '1';
+    const char* tw = pf_ab_getenv("POSFEAT_TAPWS");
+    m->tapws = m->wsplit && !m->train && tw && tw[0] == '1';
   }
   if (m->wino) {
     size_t uf = 0, wb = 0;
@@ -1418,7 +1423,15 @@ int head_forward(Ctx& c, float* img4, float* local_point, bool side) {
         }
       } else {
         int rc = POSFEAT_E_UNSUPPORTED;
-        if (npf && !c.dry) {
+        if (m->tapws && !npf && !c.dry) {
+          const int M = B * h4 * w4;
+          rc = timed(c, "conv:head.conv2.up4tap", 2.0 * M * 1152.0 * 192, [&] {
+            return pf_tap_gemm_ws(L, 192, M, reinterpret_cast<const unsigned short*>(c.f(m->tapwb)),
+                                  1152LL * 192, 1152, c.f(m->tapP), 1152, c.st);
+          });
+          if (rc != POSFEAT_OK && rc != POSFEAT_E_INVALID) return rc;
+        }
+        if (rc != POSFEAT_OK && npf && !c.dry) {
           // the tuned tile if there is one (else the DB's / the default plan)
           int tile = -1;
           auto it = m->tuned.find("head.conv2.up4tap");

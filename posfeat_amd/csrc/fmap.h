@@ -49,6 +49,9 @@ int pf_conv_dual(int n, int oh, int ow, const float* x1, int x1cs, int k1, const
                  int x2cs, int h2, int w2, int s2, int k2, int cout,
                  const unsigned short* wb, long long wplane, const float* bias, int act, float* y,
                  int ycs, hipStream_t st);
+// head.conv2's tap GEMM on the weight-stationary persistent kernel (conv.hip)
+int pf_tap_gemm_ws(const float* x, int lda, int M, const unsigned short* wb, long long wplane,
+                   int N, float* y, int ldc, hipStream_t st);
 // a dense 1x1 GEMM with A normalised on load: PReLU((x - mean) * rstd) per
 // image / channel (the 128 x 128 bf6x tile only, else POSFEAT_E_UNSUPPORTED)
 int pf_conv_run_tile_np(const posfeat_conv_desc* d, const float* x, const float* w,

@@ -98,3 +98,20 @@ def test_local_map_nchw_from_conv_fine_epilogue(gpu, hw, tmp_path):
     for k in KEYS:
         assert np.array_equal(got[k], ref[k]), "%s differs (max %g)" % (
             k, np.abs(got[k] - ref[k]).max())
+
+
+@pytest.mark.parametrize("hw", [(128, 160), (96, 224)])
+def test_tap_gemm_weight_stationary(gpu, hw, tmp_path):
+    """POSFEAT_TAPWS=1: head.conv2's tap GEMM on the persistent weight-
+    stationary kernel (tap_gemm_ws_kernel: the bf6x tile's six bf16 terms in
+    the same k order) vs the engine's tuned tile: the backbone maps
+    bit-identical, the score map within its bound (bit-identical where the
+    tuned tile is the 128 x 128 bf6x tile without split-K)."""
+    from conftest import run_ab_child
+    got = _run_default(hw)
+    out = str(tmp_path / "tapws_on.npz")
+    ref = run_ab_child(CHILD % dict(var="POSFEAT_TAPWS", val="1", hw=hw, out=out, keys=KEYS), out)
+    for k in ("local_map", "global_map", "local_map_small", "global_feat"):
+        assert np.array_equal(got[k], ref[k]), k
+    tol.check("local_point", torch.from_numpy(got["local_point"]), ref["local_point"],
+              "tapws local_point")
