@@ -1792,6 +1792,7 @@ struct WsArgs {
   float* y;
   long long wplane;
   int lda, ldc, M, N, per_n;
+  int abl;  // timing ablation (A/B build, POSFEAT_TAPWS_ABL; wrong results): 1 no stores, 2 no A loads
 };
 
 __global__ __launch_bounds__(512) void tap_gemm_ws_kernel(WsArgs a) {
@@ -1839,7 +1840,12 @@ __global__ __launch_bounds__(512) void tap_gemm_ws_kernel(WsArgs a) {
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb) split3(va[cur][rb][0], va[cur][rb][1], ah[rb], am[rb], al[rb]);
       // the next chunk's A (the next M tile's first chunk after the last)
-      if (c + 1 < WS_NCH) {
+      if (a.abl & 2) {
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) va[cur ^ 1][rb][jj] = va[cur][rb][jj];
+      } else if (c + 1 < WS_NCH) {
 #pragma unroll
         for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
@@ -1885,6 +1891,7 @@ __global__ __launch_bounds__(512) void tap_gemm_ws_kernel(WsArgs a) {
     static_assert(WS_NCH % 2 == 0, "chunk parity");
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb) {
+      if (a.abl & 1) break;
       const int mb = mt * WS_BM + wave * 32 + rb * 16 + kq * 4;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -3387,7 +3394,11 @@ int pf_tap_gemm_ws(const float* x, int lda, int M, const unsigned short* wb, lon
     return POSFEAT_E_HIP;
   const int ntn = N / WS_BN, ntm = (M + WS_BM - 1) / WS_BM;
   const int per_n = std::max(1, std::min(ntm, ncu / ntn));  // one block per CU
-  WsArgs a{x, wb, y, wplane, lda, ldc, M, N, per_n};
+  static const int abl = [] {
+    const char* e = pf_ab_getenv("POSFEAT_TAPWS_ABL");
+    return e ? atoi(e) : 0;
+  }();
+  WsArgs a{x, wb, y, wplane, lda, ldc, M, N, per_n, abl};
   hipLaunchKernelGGL(tap_gemm_ws_kernel, dim3((unsigned)(per_n * ntn)), dim3(WS_NW * 64), 0, st,
                      a);
   PF_CHECK_LAUNCH();
