@@ -1785,7 +1785,7 @@ void conv_bf6x_kernel(ConvArgs a) {
 // MFMA terms per 16x16x32 step and the same k order as conv_bf6x_kernel: the
 // same sums); the accumulators are stored straight from the registers.
 // Block b: column tile b % (N / 128), M tiles b / (N / 128) + i * per_n.
-constexpr int WS_BN = 128, WS_K = 192, WS_NCH = WS_K / BK, WS_NW = 8, WS_BM = WS_NW * 32;
+constexpr int WS_BN = 128, WS_K = 192, WS_NCH = WS_K / BK;
 struct WsArgs {
   const float* x;
   const unsigned short* wb;
@@ -1795,7 +1795,12 @@ struct WsArgs {
   int abl;  // timing ablation (A/B build, POSFEAT_TAPWS_ABL; wrong results): 1 no stores, 2 no A loads
 };
 
-__global__ __launch_bounds__(512) void tap_gemm_ws_kernel(WsArgs a) {
+// PD: A prefetch distance in chunks (PD + 1 register buffers); NW waves (2 or
+// 3 per SIMD: the block holds the CU's LDS), 32 rows each
+template <int PD, int NW>
+__global__ __launch_bounds__(NW * 64) void tap_gemm_ws_kernel(WsArgs a) {
+  constexpr int NBUF = PD + 1, WS_NW = NW, WS_BM = NW * 32;
+  static_assert(WS_NCH % NBUF == 0 && PD >= 1 && PD < WS_NCH, "a tile starts at buffer 0");
   __shared__ __attribute__((aligned(16))) unsigned short Bres[WS_NCH * 3 * WS_BN * BK];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int ntn = a.N / WS_BN;
@@ -1820,11 +1825,14 @@ __global__ __launch_bounds__(512) void tap_gemm_ws_kernel(WsArgs a) {
   };
   int mt = j;
   const float* xr[2] = {rowp(mt, 0), rowp(mt, 1)};
-  f32x4 va[2][2][2];  // [buffer][rb][jj]
+  f32x4 va[NBUF][2][2];  // [buffer][rb][jj]: chunk g of the block's walk in buffer g % NBUF
 #pragma unroll
-  for (int rb = 0; rb < 2; ++rb)
+  for (int c = 0; c < PD; ++c)
 #pragma unroll
-    for (int jj = 0; jj < 2; ++jj) va[0][rb][jj] = *reinterpret_cast<const f32x4*>(xr[rb] + jj * 4);
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj)
+        va[c][rb][jj] = *reinterpret_cast<const f32x4*>(xr[rb] + c * BK + jj * 4);
   for (;;) {
     f32x4 acc[2][8];
 #pragma unroll
@@ -1833,33 +1841,29 @@ __global__ __launch_bounds__(512) void tap_gemm_ws_kernel(WsArgs a) {
       for (int nb = 0; nb < 8; ++nb) acc[rb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int nmt = mt + a.per_n;
     const bool more = nmt < ntm;
-    // one chunk: split buffer `cur`, load the next chunk into the other, 96 MFMAs
+    const float* xn[2] = {rowp(more ? nmt : mt, 0), rowp(more ? nmt : mt, 1)};
+    // one chunk: split buffer `cur`, load chunk c + PD (this tile's, else the
+    // next tile's) into buffer (cur + PD) % NBUF, 96 MFMAs
     auto step = [&](int c, auto cur_t) __attribute__((always_inline)) {
-      constexpr int cur = decltype(cur_t)::value;
+      constexpr int cur = decltype(cur_t)::value, nxt = (cur + PD) % NBUF;
       u32x4_t ah[2], am[2], al[2];
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb) split3(va[cur][rb][0], va[cur][rb][1], ah[rb], am[rb], al[rb]);
-      // the next chunk's A (the next M tile's first chunk after the last)
+      const int cl = c + PD;
       if (a.abl & 2) {
 #pragma unroll
         for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
-          for (int jj = 0; jj < 2; ++jj) va[cur ^ 1][rb][jj] = va[cur][rb][jj];
-      } else if (c + 1 < WS_NCH) {
+          for (int jj = 0; jj < 2; ++jj) va[nxt][rb][jj] = va[cur][rb][jj];
+      } else if (cl < WS_NCH || more) {
+        const int cc = cl < WS_NCH ? cl : cl - WS_NCH;
 #pragma unroll
-        for (int rb = 0; rb < 2; ++rb)
-#pragma unroll
-          for (int jj = 0; jj < 2; ++jj)
-            va[cur ^ 1][rb][jj] =
-                *reinterpret_cast<const f32x4*>(xr[rb] + (c + 1) * BK + jj * 4);
-      } else if (more) {
-        xr[0] = rowp(nmt, 0);
-        xr[1] = rowp(nmt, 1);
-#pragma unroll
-        for (int rb = 0; rb < 2; ++rb)
+        for (int rb = 0; rb < 2; ++rb) {
+          const float* src = (cl < WS_NCH ? xr[rb] : xn[rb]) + cc * BK;
 #pragma unroll
           for (int jj = 0; jj < 2; ++jj)
-            va[cur ^ 1][rb][jj] = *reinterpret_cast<const f32x4*>(xr[rb] + jj * 4);
+            va[nxt][rb][jj] = *reinterpret_cast<const f32x4*>(src + jj * 4);
+        }
       }
       const unsigned short* Bc = Bres + c * 3 * WS_BN * BK;
 #pragma unroll
@@ -1883,12 +1887,12 @@ __global__ __launch_bounds__(512) void tap_gemm_ws_kernel(WsArgs a) {
       }
     };
 #pragma unroll 1
-    for (int c = 0; c < WS_NCH; c += 2) {
+    for (int c = 0; c < WS_NCH; c += NBUF) {
       step(c, std::integral_constant<int, 0>{});
-      step(c + 1, std::integral_constant<int, 1>{});
+      step(c + 1, std::integral_constant<int, 1 % NBUF>{});
+      if constexpr (NBUF > 2) step(c + 2, std::integral_constant<int, 2 % NBUF>{});
     }
-    // (WS_NCH even: the next tile's first chunk sits in buffer 0)
-    static_assert(WS_NCH % 2 == 0, "chunk parity");
+    static_assert(NBUF <= 3, "step group");
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb) {
       if (a.abl & 1) break;
@@ -1903,6 +1907,8 @@ __global__ __launch_bounds__(512) void tap_gemm_ws_kernel(WsArgs a) {
     }
     if (!more) break;
     mt = nmt;
+    xr[0] = xn[0];
+    xr[1] = xn[1];
   }
 }
 
@@ -3392,15 +3398,29 @@ int pf_tap_gemm_ws(const float* x, int lda, int M, const unsigned short* wb, lon
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return POSFEAT_E_HIP;
-  const int ntn = N / WS_BN, ntm = (M + WS_BM - 1) / WS_BM;
+  static const int pd = [] {  // A/B: POSFEAT_TAPWS_PD=2 (three A buffers)
+    const char* e = pf_ab_getenv("POSFEAT_TAPWS_PD");
+    return e && e[0] == '2' ? 2 : 1;
+  }();
+  static const int nw = [] {  // A/B: POSFEAT_TAPWS_NW=12 (three waves per SIMD)
+    const char* e = pf_ab_getenv("POSFEAT_TAPWS_NW");
+    return e && atoi(e) == 12 ? 12 : 8;
+  }();
+  const int bm = nw * 32;
+  const int ntn = N / WS_BN, ntm = (M + bm - 1) / bm;
   const int per_n = std::max(1, std::min(ntm, ncu / ntn));  // one block per CU
   static const int abl = [] {
     const char* e = pf_ab_getenv("POSFEAT_TAPWS_ABL");
     return e ? atoi(e) : 0;
   }();
   WsArgs a{x, wb, y, wplane, lda, ldc, M, N, per_n, abl};
-  hipLaunchKernelGGL(tap_gemm_ws_kernel, dim3((unsigned)(per_n * ntn)), dim3(WS_NW * 64), 0, st,
-                     a);
+  const dim3 grid((unsigned)(per_n * ntn));
+  if (nw == 12)
+    hipLaunchKernelGGL((tap_gemm_ws_kernel<1, 12>), grid, dim3(12 * 64), 0, st, a);
+  else if (pd == 2)
+    hipLaunchKernelGGL((tap_gemm_ws_kernel<2, 8>), grid, dim3(8 * 64), 0, st, a);
+  else
+    hipLaunchKernelGGL((tap_gemm_ws_kernel<1, 8>), grid, dim3(8 * 64), 0, st, a);
   PF_CHECK_LAUNCH();
   pf_note_arith(PF_ARITH_BF6);
   return POSFEAT_OK;
