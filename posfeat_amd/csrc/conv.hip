@@ -3402,9 +3402,9 @@ int pf_tap_gemm_ws(const float* x, int lda, int M, const unsigned short* wb, lon
     const char* e = pf_ab_getenv("POSFEAT_TAPWS_PD");
     return e && e[0] == '2' ? 2 : 1;
   }();
-  static const int nw = [] {  // A/B: POSFEAT_TAPWS_NW=12 (three waves per SIMD)
+  static const int nw = [] {  // twelve waves: three per SIMD (A/B: POSFEAT_TAPWS_NW=8)
     const char* e = pf_ab_getenv("POSFEAT_TAPWS_NW");
-    return e && atoi(e) == 12 ? 12 : 8;
+    return e && atoi(e) == 8 ? 8 : 12;
   }();
   const int bm = nw * 32;
   const int ntn = N / WS_BN, ntm = (M + bm - 1) / bm;
@@ -3415,7 +3415,7 @@ int pf_tap_gemm_ws(const float* x, int lda, int M, const unsigned short* wb, lon
   }();
   WsArgs a{x, wb, y, wplane, lda, ldc, M, N, per_n, abl};
   const dim3 grid((unsigned)(per_n * ntn));
-  if (nw == 12)
+  if (nw == 12 && pd == 1)
     hipLaunchKernelGGL((tap_gemm_ws_kernel<1, 12>), grid, dim3(12 * 64), 0, st, a);
   else if (pd == 2)
     hipLaunchKernelGGL((tap_gemm_ws_kernel<2, 8>), grid, dim3(8 * 64), 0, st, a);

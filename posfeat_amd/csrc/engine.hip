@@ -183,7 +183,7 @@ struct posfeat_model {
   // POSFEAT_NCHWSINK=1: measured even with the layout pass)
   bool nchwsink = false;
   // head.conv2's tap GEMM on the weight-stationary persistent kernel
-  // (pf_tap_gemm_ws; A/B: POSFEAT_TAPWS)
+  // (pf_tap_gemm_ws; A/B: POSFEAT_TAPWS=0 -- the tuned bf6x tile)
   bool tapws = false;
   bool tapb = false;  // bf16x6 tap GEMM on pre-split planes (POSFEAT_BF6=2)
   Buf tapwb, tapLb;
@@ -887,7 +887,7 @@ void plan(posfeat_model* m) {
     const char* k = pf_ab_getenv("POSFEAT_NCHWSINK");
     m->nchwsink = k && k[0] == '1';
     const char* tw = pf_ab_getenv("POSFEAT_TAPWS");
-    m->tapws = m->wsplit && !m->train && tw && tw[0] == '1';
+    m->tapws = m->wsplit && !m->train && !(tw && tw[0] == '0');
   }
   if (m->wino) {
     size_t uf = 0, wb = 0;

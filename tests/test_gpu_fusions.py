@@ -102,15 +102,16 @@ def test_local_map_nchw_from_conv_fine_epilogue(gpu, hw, tmp_path):
 
 @pytest.mark.parametrize("hw", [(128, 160), (96, 224)])
 def test_tap_gemm_weight_stationary(gpu, hw, tmp_path):
-    """POSFEAT_TAPWS=1: head.conv2's tap GEMM on the persistent weight-
-    stationary kernel (tap_gemm_ws_kernel: the bf6x tile's six bf16 terms in
-    the same k order) vs the engine's tuned tile: the backbone maps
-    bit-identical, the score map within its bound (bit-identical where the
-    tuned tile is the 128 x 128 bf6x tile without split-K)."""
+    """POSFEAT_TAPWS (default on): head.conv2's tap GEMM on the persistent
+    weight-stationary kernel (tap_gemm_ws_kernel: the bf6x tile's six bf16
+    terms in the same k order) vs the engine's tuned bf6x tile (A/B
+    POSFEAT_TAPWS=0): the backbone maps bit-identical, the score map within
+    its bound (bit-identical where the tuned tile is the 128 x 128 bf6x tile
+    without split-K)."""
     from conftest import run_ab_child
     got = _run_default(hw)
-    out = str(tmp_path / "tapws_on.npz")
-    ref = run_ab_child(CHILD % dict(var="POSFEAT_TAPWS", val="1", hw=hw, out=out, keys=KEYS), out)
+    out = str(tmp_path / "tapws_off.npz")
+    ref = run_ab_child(CHILD % dict(var="POSFEAT_TAPWS", val="0", hw=hw, out=out, keys=KEYS), out)
     for k in ("local_map", "global_map", "local_map_small", "global_feat"):
         assert np.array_equal(got[k], ref[k]), k
     tol.check("local_point", torch.from_numpy(got["local_point"]), ref["local_point"],
