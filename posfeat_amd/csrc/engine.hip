@@ -1423,7 +1423,7 @@ int head_forward(Ctx& c, float* img4, float* local_point, bool side) {
         }
       } else {
         int rc = POSFEAT_E_UNSUPPORTED;
-        if (m->tapws && !npf && !c.dry) {
+        if (m->tapws && !npf && !c.dry && pf_bf6x_on()) {  // (16x16x32 terms: the bf6x family)
           const int M = B * h4 * w4;
           rc = timed(c, "conv:head.conv2.up4tap", 2.0 * M * 1152.0 * 192, [&] {
             return pf_tap_gemm_ws(L, 192, M, reinterpret_cast<const unsigned short*>(c.f(m->tapwb)),
