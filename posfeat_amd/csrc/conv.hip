@@ -1792,7 +1792,8 @@ struct WsArgs {
   float* y;
   long long wplane;
   int lda, ldc, M, N, per_n;
-  int abl;  // timing ablation (A/B build, POSFEAT_TAPWS_ABL; wrong results): 1 no stores, 2 no A loads
+  int abl;  // A/B build, POSFEAT_TAPWS_ABL: 1 no stores, 2 no A loads (timing ablations, wrong
+            // results), 4 the plain block -> tile order
 };
 
 // PD: A prefetch distance in chunks (PD + 1 register buffers); NW waves (2 or
@@ -1804,7 +1805,14 @@ __global__ __launch_bounds__(NW * 64) void tap_gemm_ws_kernel(WsArgs a) {
   __shared__ __attribute__((aligned(16))) unsigned short Bres[WS_NCH * 3 * WS_BN * BK];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int ntn = a.N / WS_BN;
-  const int tn = blockIdx.x % ntn, j = blockIdx.x / ntn;
+  // (j, tn) pairs p = j * ntn + tn in contiguous runs per XCD (block b runs on
+  // XCD b % 8): the ntn blocks that walk the same M tiles share an L2 for A
+  int p = blockIdx.x;
+  if (!(a.abl & 4)) {  // (A/B: POSFEAT_TAPWS_ABL=4 -- p = block index)
+    const int nb = gridDim.x, q = nb >> 3, r = nb & 7, xcd = p & 7, slot = p >> 3;
+    p = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+  }
+  const int tn = p % ntn, j = p / ntn;
   const int n0 = tn * WS_BN;
   const int ntm = (a.M + WS_BM - 1) / WS_BM;
   if (j >= ntm) return;  // block-uniform, before the only barrier
