@@ -1785,7 +1785,6 @@ void conv_bf6x_kernel(ConvArgs a) {
 // MFMA terms per 16x16x32 step and the same k order as conv_bf6x_kernel: the
 // same sums); the accumulators are stored straight from the registers.
 // Block b: column tile b % (N / 128), M tiles b / (N / 128) + i * per_n.
-constexpr int WS_BN = 128, WS_K = 192, WS_NCH = WS_K / BK;
 struct WsArgs {
   const float* x;
   const unsigned short* wb;
@@ -1794,14 +1793,21 @@ struct WsArgs {
   int lda, ldc, M, N, per_n;
   int abl;  // A/B build, POSFEAT_TAPWS_ABL: 1 no stores, 2 no A loads (timing ablations, wrong
             // results), 4 the plain block -> tile order
+  // epilogue (the 1x1 convs): y = act(acc + bias (+ res)), conv_bf6x_kernel's order
+  const float* bias;
+  const float* res;
+  int rcs, act;
 };
 
 // PD: A prefetch distance in chunks (PD + 1 register buffers); NW waves (2 or
-// 3 per SIMD: the block holds the CU's LDS), 32 rows each
-template <int PD, int NW>
-__global__ __launch_bounds__(NW * 64) void tap_gemm_ws_kernel(WsArgs a) {
-  constexpr int NBUF = PD + 1, WS_NW = NW, WS_BM = NW * 32;
+// 3 per SIMD: the block holds the CU's LDS), 32 rows each; KC k chunks of 32
+// (K = 32 KC, the weights' row pitch); NB column blocks of 16 (BN = 16 NB)
+template <int PD, int NW, int KC, int NB, bool RES = false>
+__global__ __launch_bounds__(NW * 64) void gemm_ws_kernel(WsArgs a) {
+  constexpr int NBUF = PD + 1, WS_NW = NW, WS_BM = NW * 32, WS_NCH = KC, WS_K = KC * BK;
+  constexpr int WS_BN = 16 * NB;
   static_assert(WS_NCH % NBUF == 0 && PD >= 1 && PD < WS_NCH, "a tile starts at buffer 0");
+  static_assert(WS_NCH * 3 * WS_BN * BK * 2 <= 160 * 1024, "resident weight planes");
   __shared__ __attribute__((aligned(16))) unsigned short Bres[WS_NCH * 3 * WS_BN * BK];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int ntn = a.N / WS_BN;
@@ -1842,16 +1848,20 @@ __global__ __launch_bounds__(NW * 64) void tap_gemm_ws_kernel(WsArgs a) {
       for (int jj = 0; jj < 2; ++jj)
         va[c][rb][jj] = *reinterpret_cast<const f32x4*>(xr[rb] + c * BK + jj * 4);
   for (;;) {
-    f32x4 acc[2][8];
+    f32x4 acc[2][NB];
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
-      for (int nb = 0; nb < 8; ++nb) acc[rb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int nb = 0; nb < NB; ++nb) acc[rb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int nmt = mt + a.per_n;
     const bool more = nmt < ntm;
+    // opaque per tile: with one chunk group (K = 64) the B fragment reads are
+    // loop-invariant, and hoisting all of them out of the tile loop spills
+    int boff = 0;
+    if constexpr (KC == 2) asm volatile("" : "+s"(boff));
     const float* xn[2] = {rowp(more ? nmt : mt, 0), rowp(more ? nmt : mt, 1)};
     // one chunk: split buffer `cur`, load chunk c + PD (this tile's, else the
-    // next tile's) into buffer (cur + PD) % NBUF, 96 MFMAs
+    // next tile's) into buffer (cur + PD) % NBUF, 6 RB NB MFMAs
     auto step = [&](int c, auto cur_t) __attribute__((always_inline)) {
       constexpr int cur = decltype(cur_t)::value, nxt = (cur + PD) % NBUF;
       u32x4_t ah[2], am[2], al[2];
@@ -1873,9 +1883,9 @@ __global__ __launch_bounds__(NW * 64) void tap_gemm_ws_kernel(WsArgs a) {
             va[nxt][rb][jj] = *reinterpret_cast<const f32x4*>(src + jj * 4);
         }
       }
-      const unsigned short* Bc = Bres + c * 3 * WS_BN * BK;
+      const unsigned short* Bc = Bres + boff + c * 3 * WS_BN * BK;
 #pragma unroll
-      for (int nb = 0; nb < 8; ++nb) {
+      for (int nb = 0; nb < NB; ++nb) {
         const int row = nb * 16 + r16;
         const unsigned short* bp = Bc + row * BK + (kq ^ bx_swz(row)) * 8;
         const u32x4_t bh = *reinterpret_cast<const u32x4_t*>(bp);
@@ -1897,10 +1907,14 @@ __global__ __launch_bounds__(NW * 64) void tap_gemm_ws_kernel(WsArgs a) {
 #pragma unroll 1
     for (int c = 0; c < WS_NCH; c += NBUF) {
       step(c, std::integral_constant<int, 0>{});
+      if constexpr (KC == 2) __builtin_amdgcn_sched_barrier(0);
       step(c + 1, std::integral_constant<int, 1 % NBUF>{});
       if constexpr (NBUF > 2) step(c + 2, std::integral_constant<int, 2 % NBUF>{});
     }
     static_assert(NBUF <= 3, "step group");
+    float bcol[NB];  // this lane's columns' biases (loaded here: no registers held over the k loop)
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) bcol[nb] = a.bias ? a.bias[n0 + nb * 16 + r16] : 0.f;
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb) {
       if (a.abl & 1) break;
@@ -1909,8 +1923,22 @@ __global__ __launch_bounds__(NW * 64) void tap_gemm_ws_kernel(WsArgs a) {
       for (int i = 0; i < 4; ++i) {
         if (mb + i >= a.M) continue;
         float* yr = a.y + (long long)(mb + i) * a.ldc + n0 + r16;
+        // the row's residual loaded together, ahead of its stores (which the
+        // compiler may not move loads past): one round trip per row, not NB
+        float rv[NB];
+        if constexpr (RES) {
+          const float* rr = a.res + (long long)(mb + i) * a.rcs + n0 + r16;
 #pragma unroll
-        for (int nb = 0; nb < 8; ++nb) yr[nb * 16] = acc[rb][nb][i];
+          for (int nb = 0; nb < NB; ++nb) rv[nb] = __builtin_nontemporal_load(rr + nb * 16);
+        }
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) {
+          float v = acc[rb][nb][i] + bcol[nb];
+          if constexpr (RES) v += rv[nb];
+          if (a.act == POSFEAT_ACT_RELU) v = fmaxf(v, 0.f);
+          else if (a.act == POSFEAT_ACT_ELU) v = pf_elu(v);
+          yr[nb * 16] = v;
+        }
       }
     }
     if (!more) break;
@@ -3395,43 +3423,81 @@ int pf_conv_dual(int n, int oh, int ow, const float* x1, int x1cs, int k1, const
   return conv_run(a, p, st);
 }
 
-// head.conv2's tap GEMM on the weight-stationary persistent kernel
-// (tap_gemm_ws_kernel): y [M][ldc] = x [M][lda] . W^T, W as three bf16 planes
-// [3][N][192] (plane stride wplane).  K = 192, N % 128 == 0.
-int pf_tap_gemm_ws(const float* x, int lda, int M, const unsigned short* wb, long long wplane,
-                   int N, float* y, int ldc, hipStream_t st) {
-  if (!x || !wb || !y || M <= 0 || N % WS_BN || lda < WS_K || ldc < N || lda % 4 || ldc % 4)
+// GEMMs on the weight-stationary persistent kernel (gemm_ws_kernel):
+// y [M][ldc] = act(x [M][lda] . W^T + bias (+ res)), W as three bf16 planes
+// [3][N][K] (plane stride wplane, row pitch K).  Instantiated shapes: head.conv2's
+// tap GEMM (K = 192, N % 128 == 0) and the short-K 1x1 convs (pf_ws_gemm_ok);
+// POSFEAT_E_UNSUPPORTED for another K / N.
+static bool ws_shape(int K, int N, int* kc, int* nb) {
+  *kc = K / BK;
+  if (K % BK) return false;
+  // the resident planes must fit the CU's LDS: 3 x BN x K bf16
+  if (K == 192 && N % 128 == 0) { *nb = 8; return true; }
+  if ((K == 64 || K == 128) && N % 128 == 0) { *nb = 8; return true; }
+  if (K == 256 && N % 64 == 0) { *nb = 4; return true; }
+  return false;
+}
+bool pf_ws_gemm_ok(int K, int N) {
+  int kc, nb;
+  return ws_shape(K, N, &kc, &nb);
+}
+int pf_gemm_ws(const float* x, int lda, int M, int K, const unsigned short* wb, long long wplane,
+               int N, const float* bias, const float* res, int rcs, int act, float* y, int ldc,
+               hipStream_t st) {
+  int kc = 0, nbk = 0;
+  if (!ws_shape(K, N, &kc, &nbk)) return POSFEAT_E_UNSUPPORTED;
+  const int bn = 16 * nbk;
+  if (!x || !wb || !y || M <= 0 || lda < K || ldc < N || lda % 4 || (res && rcs < N))
     return POSFEAT_E_INVALID;
   int dev = 0, ncu = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return POSFEAT_E_HIP;
-  static const int pd = [] {  // A/B: POSFEAT_TAPWS_PD=2 (three A buffers)
+  static const int pd = [] {  // A/B: POSFEAT_TAPWS_PD=2 (three A buffers; the tap GEMM)
     const char* e = pf_ab_getenv("POSFEAT_TAPWS_PD");
     return e && e[0] == '2' ? 2 : 1;
   }();
-  static const int nw = [] {  // twelve waves: three per SIMD (A/B: POSFEAT_TAPWS_NW=8)
+  static const int nw0 = [] {  // twelve waves: three per SIMD (A/B: POSFEAT_TAPWS_NW=8)
     const char* e = pf_ab_getenv("POSFEAT_TAPWS_NW");
     return e && atoi(e) == 8 ? 8 : 12;
   }();
+  const bool tap = kc == 6 && nbk == 8;
+  const int nw = tap ? nw0 : 12;
   const int bm = nw * 32;
-  const int ntn = N / WS_BN, ntm = (M + bm - 1) / bm;
-  const int per_n = std::max(1, std::min(ntm, ncu / ntn));  // one block per CU
+  const int ntn = N / bn, ntm = (M + bm - 1) / bm;
+  const int per_n = std::max(1, std::min(ntm, ncu / std::max(1, std::min(ntn, ncu))));
   static const int abl = [] {
     const char* e = pf_ab_getenv("POSFEAT_TAPWS_ABL");
     return e ? atoi(e) : 0;
   }();
-  WsArgs a{x, wb, y, wplane, lda, ldc, M, N, per_n, abl};
+  WsArgs a{x, wb, y, wplane, lda, ldc, M, N, per_n, abl, bias, res, rcs, act};
   const dim3 grid((unsigned)(per_n * ntn));
-  if (nw == 12 && pd == 1)
-    hipLaunchKernelGGL((tap_gemm_ws_kernel<1, 12>), grid, dim3(12 * 64), 0, st, a);
-  else if (pd == 2)
-    hipLaunchKernelGGL((tap_gemm_ws_kernel<2, 8>), grid, dim3(8 * 64), 0, st, a);
+  if (tap && pd == 2)
+    hipLaunchKernelGGL((gemm_ws_kernel<2, 8, 6, 8>), grid, dim3(8 * 64), 0, st, a);
+  else if (tap && nw == 8)
+    hipLaunchKernelGGL((gemm_ws_kernel<1, 8, 6, 8>), grid, dim3(8 * 64), 0, st, a);
+  else if (tap)
+    hipLaunchKernelGGL((gemm_ws_kernel<1, 12, 6, 8>), grid, dim3(12 * 64), 0, st, a);
+  else if (kc == 2 && res)
+    hipLaunchKernelGGL((gemm_ws_kernel<1, 12, 2, 8, true>), grid, dim3(12 * 64), 0, st, a);
+  else if (kc == 2)
+    hipLaunchKernelGGL((gemm_ws_kernel<1, 12, 2, 8>), grid, dim3(12 * 64), 0, st, a);
+  else if (kc == 4 && res)
+    hipLaunchKernelGGL((gemm_ws_kernel<1, 12, 4, 8, true>), grid, dim3(12 * 64), 0, st, a);
+  else if (kc == 4)
+    hipLaunchKernelGGL((gemm_ws_kernel<1, 12, 4, 8>), grid, dim3(12 * 64), 0, st, a);
+  else if (res)
+    hipLaunchKernelGGL((gemm_ws_kernel<1, 12, 8, 4, true>), grid, dim3(12 * 64), 0, st, a);
   else
-    hipLaunchKernelGGL((tap_gemm_ws_kernel<1, 8>), grid, dim3(8 * 64), 0, st, a);
+    hipLaunchKernelGGL((gemm_ws_kernel<1, 12, 8, 4>), grid, dim3(12 * 64), 0, st, a);
   PF_CHECK_LAUNCH();
   pf_note_arith(PF_ARITH_BF6);
   return POSFEAT_OK;
+}
+int pf_tap_gemm_ws(const float* x, int lda, int M, const unsigned short* wb, long long wplane,
+                   int N, float* y, int ldc, hipStream_t st) {
+  return pf_gemm_ws(x, lda, M, 192, wb, wplane, N, nullptr, nullptr, 0, POSFEAT_ACT_NONE, y, ldc,
+                    st);
 }
 
 // pf_conv_run_tile for a dense 1x1 GEMM whose A is normalised on load

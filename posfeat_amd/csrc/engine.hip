@@ -185,6 +185,12 @@ struct posfeat_model {
   // head.conv2's tap GEMM on the weight-stationary persistent kernel
   // (pf_tap_gemm_ws; A/B: POSFEAT_TAPWS=0 -- the tuned bf6x tile)
   bool tapws = false;
+  // the short-K dense 1x1 convs on the same kernel (pf_gemm_ws): by default
+  // (3) only where it measured faster than the tuned tiles, layer1's K = 256,
+  // N = 64 conv1 (0.20 -> 0.18 ms at B = 32; conv3 with its residual and the
+  // N = 128 / 1024 convs slower). A/B: POSFEAT_WS1X1=1 every
+  // instantiated shape, 2 those without a residual, 0 none
+  int ws1x1 = 0;
   bool tapb = false;  // bf16x6 tap GEMM on pre-split planes (POSFEAT_BF6=2)
   Buf tapwb, tapLb;
   Buf gf_w, gf_b, gf_wp;
@@ -512,6 +518,21 @@ int conv(Ctx& c, const std::string& name, const float* x, int n, int h, int w, i
   d.act = act;
   const int oh = (h + 2 * d.pad - d.kh) / stride + 1, ow = (w + 2 * d.pad - d.kw) / stride + 1;
   const double flops = 2.0 * n * oh * ow * (double)s->cout * s->cin * s->kh * s->kw;
+  // a short-K 1x1 conv: the weight-stationary GEMM (its three planes resident
+  // in LDS, A streamed once per column tile; the bf6x tile's six terms in the
+  // same order). Not under conv_fine's NCHW sink (the tile epilogue's)
+  const int wsm = c.m->ws1x1;
+  if (wsm && !(wsm >= 2 && res) && !(wsm == 3 && s->cout != 64) && !c.dry && s->kh == 1 && s->kw == 1 && stride == 1 && s->cin % 32 == 0 &&
+      pf_bf6x_on() && pf_ws_gemm_ok(s->cin, s->cout) && !(c.m->nchwsink && name == "conv_fine")) {
+    const unsigned short* wb = nullptr;
+    long long wplane = 0;
+    c.wplanes_of(c.W(name), &wb, &wplane);
+    if (wb)
+      return timed(c, "conv:" + name, flops, [&] {
+        return pf_gemm_ws(x, xcs, n * h * w, s->cin, wb, wplane, s->cout, c.Bi(name), res, rcs,
+                          act, y, ycs, c.st);
+      });
+  }
   return conv_desc_run(c, name, d, x, c.W(name), c.Bi(name), res, y, flops);
 }
 
@@ -888,6 +909,10 @@ void plan(posfeat_model* m) {
     m->nchwsink = k && k[0] == '1';
     const char* tw = pf_ab_getenv("POSFEAT_TAPWS");
     m->tapws = m->wsplit && !m->train && !(tw && tw[0] == '0');
+    const char* w1 = pf_ab_getenv("POSFEAT_WS1X1");
+    m->ws1x1 = !m->wsplit || m->train || (w1 && w1[0] == '0') ? 0
+               : w1 && (w1[0] == '1' || w1[0] == '2')   ? w1[0] - '0'
+                                                        : 3;
   }
   if (m->wino) {
     size_t uf = 0, wb = 0;

@@ -52,6 +52,12 @@ int pf_conv_dual(int n, int oh, int ow, const float* x1, int x1cs, int k1, const
 // head.conv2's tap GEMM on the weight-stationary persistent kernel (conv.hip)
 int pf_tap_gemm_ws(const float* x, int lda, int M, const unsigned short* wb, long long wplane,
                    int N, float* y, int ldc, hipStream_t st);
+// the same kernel for a short-K dense 1x1 conv (y = act(x W^T + bias (+ res)));
+// pf_ws_gemm_ok(K, N): a shape it is instantiated for
+bool pf_ws_gemm_ok(int K, int N);
+int pf_gemm_ws(const float* x, int lda, int M, int K, const unsigned short* wb, long long wplane,
+               int N, const float* bias, const float* res, int rcs, int act, float* y, int ldc,
+               hipStream_t st);
 // a dense 1x1 GEMM with A normalised on load: PReLU((x - mean) * rstd) per
 // image / channel (the 128 x 128 bf6x tile only, else POSFEAT_E_UNSUPPORTED)
 int pf_conv_run_tile_np(const posfeat_conv_desc* d, const float* x, const float* w,

@@ -9,6 +9,8 @@ child process):
   output transform instead of a pass over its output;
 * POSFEAT_NCHWSINK=1 (A/B, off by default) -- conv_fine's epilogue writes
   local_map NCHW too (no layout pass): bit-identical;
+* POSFEAT_TAPWS / POSFEAT_WS1X1 -- head.conv2's tap GEMM and the short-K
+  1x1 convs on the weight-stationary kernel vs the tuned tiles;
 * POSFEAT_DSFUSE -- each stage's first bottleneck conv3 + downsample as one
   two-source GEMM (posfeat_conv1x1_dual) instead of two convs: a different
   fp32 summation order, so the maps agree within tests/tol.py's bounds.
@@ -116,3 +118,24 @@ def test_tap_gemm_weight_stationary(gpu, hw, tmp_path):
         assert np.array_equal(got[k], ref[k]), k
     tol.check("local_point", torch.from_numpy(got["local_point"]), ref["local_point"],
               "tapws local_point")
+
+
+@pytest.mark.parametrize("hw", [(128, 160), (96, 224)])
+def test_short_k_1x1_weight_stationary(gpu, hw, tmp_path):
+    """POSFEAT_WS1X1: dense 1x1 convs on the weight-stationary kernel with
+    bias + residual + activation from registers (A/B =1: every K = 64 / 128 /
+    256 conv -- bottleneck conv1 / conv3 with the residual add, conv_fine; the
+    default: layer1's N = 64 conv1) vs the tuned bf6x tiles (=0): the same six
+    bf16 terms per product in a tile's k order, so every map within its bound
+    (measured bit-identical, r16zh)."""
+    from conftest import run_ab_child
+    got = _run_default(hw)
+    out = str(tmp_path / "ws1x1_off.npz")
+    ref = run_ab_child(CHILD % dict(var="POSFEAT_WS1X1", val="0", hw=hw, out=out, keys=KEYS), out)
+    out1 = str(tmp_path / "ws1x1_all.npz")
+    every = run_ab_child(CHILD % dict(var="POSFEAT_WS1X1", val="1", hw=hw, out=out1, keys=KEYS), out1)
+    for k in KEYS:
+        tol.check(k, torch.from_numpy(got[k]), ref[k], "ws1x1 " + k)
+        tol.check(k, torch.from_numpy(every[k]), ref[k], "ws1x1=1 " + k)
+        print("ws1x1=1", hw, k, float(np.abs(every[k] - ref[k]).max()))
+        print("ws1x1", hw, k, float(np.abs(got[k] - ref[k]).max()))
