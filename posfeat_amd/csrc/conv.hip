@@ -1802,8 +1802,11 @@ struct WsArgs {
 // PD: A prefetch distance in chunks (PD + 1 register buffers); NW waves (2 or
 // 3 per SIMD: the block holds the CU's LDS), 32 rows each; KC k chunks of 32
 // (K = 32 KC, the weights' row pitch); NB column blocks of 16 (BN = 16 NB)
-template <int PD, int NW, int KC, int NB, bool RES = false>
+// EP: the epilogue -- 0 the accumulators stored as they are (the tap GEMM), 1
+// bias + activation, 2 bias + residual + activation
+template <int PD, int NW, int KC, int NB, int EP = 0>
 __global__ __launch_bounds__(NW * 64) void gemm_ws_kernel(WsArgs a) {
+  constexpr bool RES = EP == 2;
   constexpr int NBUF = PD + 1, WS_NW = NW, WS_BM = NW * 32, WS_NCH = KC, WS_K = KC * BK;
   constexpr int WS_BN = 16 * NB;
   static_assert(WS_NCH % NBUF == 0 && PD >= 1 && PD < WS_NCH, "a tile starts at buffer 0");
@@ -1914,7 +1917,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_ws_kernel(WsArgs a) {
     static_assert(NBUF <= 3, "step group");
     float bcol[NB];  // this lane's columns' biases (loaded here: no registers held over the k loop)
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb) bcol[nb] = a.bias ? a.bias[n0 + nb * 16 + r16] : 0.f;
+    for (int nb = 0; nb < NB; ++nb) bcol[nb] = EP && a.bias ? a.bias[n0 + nb * 16 + r16] : 0.f;
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb) {
       if (a.abl & 1) break;
@@ -1933,10 +1936,13 @@ __global__ __launch_bounds__(NW * 64) void gemm_ws_kernel(WsArgs a) {
         }
 #pragma unroll
         for (int nb = 0; nb < NB; ++nb) {
-          float v = acc[rb][nb][i] + bcol[nb];
-          if constexpr (RES) v += rv[nb];
-          if (a.act == POSFEAT_ACT_RELU) v = fmaxf(v, 0.f);
-          else if (a.act == POSFEAT_ACT_ELU) v = pf_elu(v);
+          float v = acc[rb][nb][i];
+          if constexpr (EP > 0) {
+            v += bcol[nb];
+            if constexpr (RES) v += rv[nb];
+            if (a.act == POSFEAT_ACT_RELU) v = fmaxf(v, 0.f);
+            else if (a.act == POSFEAT_ACT_ELU) v = pf_elu(v);
+          }
           yr[nb * 16] = v;
         }
       }
@@ -3461,7 +3467,8 @@ int pf_gemm_ws(const float* x, int lda, int M, int K, const unsigned short* wb, 
     const char* e = pf_ab_getenv("POSFEAT_TAPWS_NW");
     return e && atoi(e) == 8 ? 8 : 12;
   }();
-  const bool tap = kc == 6 && nbk == 8;
+  const bool tap = kc == 6 && nbk == 8;  // (the tap GEMM: no epilogue)
+  if (tap && (bias || res || act != POSFEAT_ACT_NONE)) return POSFEAT_E_UNSUPPORTED;
   const int nw = tap ? nw0 : 12;
   const int bm = nw * 32;
   const int ntn = N / bn, ntm = (M + bm - 1) / bm;
@@ -3479,17 +3486,17 @@ int pf_gemm_ws(const float* x, int lda, int M, int K, const unsigned short* wb, 
   else if (tap)
     hipLaunchKernelGGL((gemm_ws_kernel<1, 12, 6, 8>), grid, dim3(12 * 64), 0, st, a);
   else if (kc == 2 && res)
-    hipLaunchKernelGGL((gemm_ws_kernel<1, 12, 2, 8, true>), grid, dim3(12 * 64), 0, st, a);
+    hipLaunchKernelGGL((gemm_ws_kernel<1, 12, 2, 8, 2>), grid, dim3(12 * 64), 0, st, a);
   else if (kc == 2)
-    hipLaunchKernelGGL((gemm_ws_kernel<1, 12, 2, 8>), grid, dim3(12 * 64), 0, st, a);
+    hipLaunchKernelGGL((gemm_ws_kernel<1, 12, 2, 8, 1>), grid, dim3(12 * 64), 0, st, a);
   else if (kc == 4 && res)
-    hipLaunchKernelGGL((gemm_ws_kernel<1, 12, 4, 8, true>), grid, dim3(12 * 64), 0, st, a);
+    hipLaunchKernelGGL((gemm_ws_kernel<1, 12, 4, 8, 2>), grid, dim3(12 * 64), 0, st, a);
   else if (kc == 4)
-    hipLaunchKernelGGL((gemm_ws_kernel<1, 12, 4, 8>), grid, dim3(12 * 64), 0, st, a);
+    hipLaunchKernelGGL((gemm_ws_kernel<1, 12, 4, 8, 1>), grid, dim3(12 * 64), 0, st, a);
   else if (res)
-    hipLaunchKernelGGL((gemm_ws_kernel<1, 12, 8, 4, true>), grid, dim3(12 * 64), 0, st, a);
+    hipLaunchKernelGGL((gemm_ws_kernel<1, 12, 8, 4, 2>), grid, dim3(12 * 64), 0, st, a);
   else
-    hipLaunchKernelGGL((gemm_ws_kernel<1, 12, 8, 4>), grid, dim3(12 * 64), 0, st, a);
+    hipLaunchKernelGGL((gemm_ws_kernel<1, 12, 8, 4, 1>), grid, dim3(12 * 64), 0, st, a);
   PF_CHECK_LAUNCH();
   pf_note_arith(PF_ARITH_BF6);
   return POSFEAT_OK;
