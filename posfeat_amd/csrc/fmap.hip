@@ -372,7 +372,9 @@ __global__ void norm_prelu_upsample_kernel(const float* __restrict__ x, int n, i
 // contiguous range of pixel pairs (its image's mean / rstd reloaded only when
 // the range crosses an image), HT_U steps per pass with all their loads issued
 // before the first reduction.  Same per-pixel arithmetic and order.
-template <int HT_U, bool NT>
+// IL: the waves interleaved over the pixels (each step's HT_U pairs of all
+// waves one contiguous stream) instead of a contiguous range per wave
+template <int HT_U, bool NT, bool IL = false>
 __global__ void head_tail_conv3_kernel(const float* __restrict__ x, int n, int hw, int cs,
                                        const float* __restrict__ mean,
                                        const float* __restrict__ rstd,
@@ -389,10 +391,14 @@ __global__ void head_tail_conv3_kernel(const float* __restrict__ x, int n, int h
   const long long total = (long long)n * hw;
   const long long pairs = (total + 1) / 2;
   const long long per = (pairs + waves - 1) / waves;
-  const long long q0 = wid * per, q1 = min(pairs, q0 + per);
-  int bc = -1;
+  const long long q0 = IL ? wid * HT_U : wid * per, q1 = IL ? pairs : min(pairs, q0 + per);
+  const long long qstep = IL ? waves * HT_U : HT_U;
+  // this lane's image and its pixel range [lo, hi): a 64-bit division only
+  // where the lane's pixels cross into the next image (one per pixel was the
+  // loop's largest VALU cost)
+  long long lo = 0, hi = -1;
   f32x4 m = {0.f, 0.f, 0.f, 0.f}, r = {0.f, 0.f, 0.f, 0.f};
-  for (long long q = q0; q < q1; q += HT_U) {
+  for (long long q = q0; q < q1; q += qstep) {
     f32x4 xv[HT_U];
 #pragma unroll
     for (int u = 0; u < HT_U; ++u) {
@@ -404,11 +410,12 @@ __global__ void head_tail_conv3_kernel(const float* __restrict__ x, int n, int h
 #pragma unroll
     for (int u = 0; u < HT_U; ++u) {
       const long long p = min(2 * min(q + u, q1 - 1) + half, total - 1);
-      const int b = (int)(p / hw);
-      if (b != bc) {  // wave-uniform except where a pair straddles two images
+      if (p < lo || p >= hi) {  // wave-uniform except where a pair straddles two images
+        const int b = (int)(p / hw);
         m = *reinterpret_cast<const f32x4*>(mean + b * 128 + l32 * 4);
         r = *reinterpret_cast<const f32x4*>(rstd + b * 128 + l32 * 4);
-        bc = b;
+        lo = (long long)b * hw;
+        hi = lo + hw;
       }
       const f32x4 v = norm_prelu4(xv[u], m, r, a);
       s[u] = v.x * wv.x + v.y * wv.y + v.z * wv.z + v.w * wv.w;
@@ -616,12 +623,15 @@ int pf_head_tail(const float* x, int n, int hw, int cs, const float* mean, const
                  float* mean1, float* rstd1, double* part, hipStream_t st) {
   const long long total = (long long)n * hw;
   // A/B (POSFEAT_TAIL=<u><n>, A/B build): u pixel pairs per wave step in
-  // flight, n = 1: nontemporal loads (y is read once).  Default 41 (r16i,
-  // same box, B = 32: 40 1.091, 41 1.031, 80 1.493, 81 1.338 ms for the
-  // tail; 8192 / 16384 / 32768 blocks at 40: 1.091 / 1.073 / 1.053)
+  // flight, n = 1: nontemporal loads (y is read once), n = 2 / 3: the waves
+  // interleaved over the pixels, nontemporal / plain loads.  Default 43
+  // (r16zm, same box, B = 32, two runs each: 41 1.035 / 1.041, 42 1.020 /
+  // 1.020, 43 1.007 / 1.005 ms for the tail; earlier, r16i: 40 1.091, 41
+  // 1.031, 80 1.493, 81 1.338; 8192 / 16384 / 32768 blocks at 40: 1.091 /
+  // 1.073 / 1.053, 2048 at 42: 1.07)
   static const int ab = [] {
     const char* e = pf_ab_getenv("POSFEAT_TAIL");
-    return e ? atoi(e) : 41;
+    return e ? atoi(e) : 43;
   }();
   static const int tmax = [] {
     const char* e = pf_ab_getenv("POSFEAT_TAIL_BLOCKS");
@@ -630,7 +640,13 @@ int pf_head_tail(const float* x, int n, int hw, int cs, const float* mean, const
   int blocks = (int)((total / 2 + 3) / 4);
   if (blocks > tmax) blocks = tmax;
   if (blocks < 1) blocks = 1;
-  if (ab == 80)
+  if (ab == 42)  // (A/B: interleaved waves)
+    hipLaunchKernelGGL((head_tail_conv3_kernel<4, true, true>), dim3(blocks), dim3(256), 0, st, x, n,
+                       hw, cs, mean, rstd, slope, w3, b3, yraw);
+  else if (ab == 43)
+    hipLaunchKernelGGL((head_tail_conv3_kernel<4, false, true>), dim3(blocks), dim3(256), 0, st, x,
+                       n, hw, cs, mean, rstd, slope, w3, b3, yraw);
+  else if (ab == 80)
     hipLaunchKernelGGL((head_tail_conv3_kernel<8, false>), dim3(blocks), dim3(256), 0, st, x, n, hw,
                        cs, mean, rstd, slope, w3, b3, yraw);
   else if (ab == 81)
