@@ -52,7 +52,7 @@ GEMM_LABEL_KERNELS = {
     ".wino": "conv_bf6x_kernel<128> x64 batched (Winograd F(6x6) transform-domain GEMMs of "
              "%s; bf16x6 on pre-split U planes, v_mfma_f32_16x16x32_bf16, memory instructions "
              "interleaved among the MFMAs)",
-    "up4tap": "tap_gemm_ws_kernel<1,12> (head.conv2's 192 x4-upsampled channels: nine 1x1 "
+    "up4tap": "gemm_ws_kernel<1,12,6,8> (head.conv2's 192 x4-upsampled channels: nine 1x1 "
               "convs on the 120x160 grid as one [B*19200 x 192] x [192 x 1152] GEMM; persistent, "
               "each block's 128 x 192 weight planes resident in LDS)",
     "": "the autotuned conv tile of %s (conv.hip MFMA implicit GEMM)",

@@ -105,7 +105,7 @@ def test_local_map_nchw_from_conv_fine_epilogue(gpu, hw, tmp_path):
 @pytest.mark.parametrize("hw", [(128, 160), (96, 224)])
 def test_tap_gemm_weight_stationary(gpu, hw, tmp_path):
     """POSFEAT_TAPWS (default on): head.conv2's tap GEMM on the persistent
-    weight-stationary kernel (tap_gemm_ws_kernel: the bf6x tile's six bf16
+    weight-stationary kernel (gemm_ws_kernel: the bf6x tile's six bf16
     terms in the same k order) vs the engine's tuned bf6x tile (A/B
     POSFEAT_TAPWS=0): the backbone maps bit-identical, the score map within
     its bound (bit-identical where the tuned tile is the 128 x 128 bf6x tile
