@@ -737,37 +737,18 @@ __device__ __forceinline__ void up2_row8(const float* base, int w2, int cs, floa
   }
 }
 
-// the same row from the six half-res columns bx .. bx + 5 the 8 patch columns
-// touch (x0 - bx <= 4 for the in-map columns: sw < 1/2), each loaded once and
-// picked per column (the pick is wave-uniform: a wave is one tile's channels)
-// instead of two loads per column -- the same v0 / v1 values and operations
+// X = rows[k] for a wave-uniform k in [0, 6): uniform branches, no selects
 template <typename T>
-__device__ __forceinline__ void up2_row8w(const float* base, int w2, int cs, float sw, int w, int sy,
-                                          int xc0, T (&X)[8]) {
-#pragma clang fp contract(off)
-  const float* row = base + (long long)sy * w2 * cs;
-  const int bx = (int)(sw * (xc0 > 0 ? xc0 : 0));
-  T L[6];
-#pragma unroll
-  for (int j = 0; j < 6; ++j) L[j] = *reinterpret_cast<const T*>(row + min(bx + j, w2 - 1) * cs);
-#pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    const int xx = xc0 + c;
-    const bool in = (unsigned)xx < (unsigned)w;
-    const float rx = sw * (in ? xx : w - 1);
-    const int x0 = (int)rx;
-    const int x1 = x0 + (x0 < w2 - 1 ? 1 : 0);
-    const float lx = rx - x0, hx = 1.f - lx;
-    // (out-of-map columns pick any in-window value: X = 0 there)
-    const int k0 = min(max(x0 - bx, 0), 5), k1 = min(max(x1 - bx, 0), 5);
-    T v0 = L[0], v1 = L[0];
-#pragma unroll
-    for (int j = 1; j < 6; ++j) {
-      v0 = k0 == j ? L[j] : v0;
-      v1 = k1 == j ? L[j] : v1;
-    }
-    const T v = hx * v0 + lx * v1;
-    X[c] = in ? v : T(0.f);
+__device__ __forceinline__ void up2_pick(const T (&rows)[6][8], int k, T (&X)[8]) {
+  switch (__builtin_amdgcn_readfirstlane(k)) {
+#define UP2_PICK_CASE(j) \
+  case j:                \
+    for (int c = 0; c < 8; ++c) X[c] = rows[j][c]; \
+    break;
+    UP2_PICK_CASE(0) UP2_PICK_CASE(1) UP2_PICK_CASE(2) UP2_PICK_CASE(3) UP2_PICK_CASE(4)
+    default:
+      for (int c = 0; c < 8; ++c) X[c] = rows[5][c];
+#undef UP2_PICK_CASE
   }
 }
 
@@ -788,7 +769,10 @@ __device__ __forceinline__ T up2_lerp_y(float hy, T a, float ly, T b) {
 // half-res rows), instead of four gathered loads per tap.  A wave is 64
 // channel groups of one tile (Cin / VW >= 64 on every caller), so the window's
 // branches are wave-uniform.
-template <bool UP2, int VW, bool UPW = true>
+// UPM (UP2): 0 the half-res rows x-interpolated as the patch rows reach them
+// (a two-row window); 1 all six the patch can touch loaded and interpolated
+// first (every load in flight at once), the patch rows picked from them
+template <bool UP2, int VW, int UPM = 0>
 __global__ __launch_bounds__(256) void wino6_input_kernel(const float* __restrict__ x, int xcs,
                                                           int n, int h, int w, int cvn,
                                                           float* __restrict__ V) {
@@ -813,6 +797,16 @@ __global__ __launch_bounds__(256) void wino6_input_kernel(const float* __restric
     const float* base = UP2 ? x + (long long)b * h2 * w2 * xcs + q * VW : nullptr;
     T XA[8], XB[8];  // UP2: x-interpolated half-res rows ka, kb
     int ka = -1, kb = -1;
+    // UPM 1: the half-res rows ybase .. ybase + 5 (sh < 1/2: the patch's 8
+    // rows need at most rows y0 - ybase <= 4 and y1 - ybase <= 5)
+    constexpr int NXR = UP2 && UPM == 1 ? 6 : 1;
+    T XR[NXR][8];
+    int ybase = 0;
+    if constexpr (UP2 && UPM == 1) {
+      ybase = (int)(sh * max(6 * ty - 1, 0));
+#pragma unroll
+      for (int j = 0; j < 6; ++j) up2_row8(base, w2, xcs, sw, w, min(ybase + j, h2 - 1), 6 * tx - 1, XR[j]);
+    }
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
       const int yy = 6 * ty - 1 + r;
@@ -825,12 +819,14 @@ __global__ __launch_bounds__(256) void wino6_input_kernel(const float* __restric
           const int y0 = (int)ry;
           const int y1 = y0 + (y0 < h2 - 1 ? 1 : 0);
           const float ly = ry - y0, hy = 1.f - ly;
+          if constexpr (UPM == 1) {
+            up2_pick(XR, y0 - ybase, XA);
+            up2_pick(XR, y1 - ybase, XB);
+          } else {
           if (y0 != ka) {
             if (y0 == kb) {
 #pragma unroll
               for (int c = 0; c < 8; ++c) XA[c] = XB[c];
-            } else if (UPW) {
-              up2_row8w(base, w2, xcs, sw, w, y0, 6 * tx - 1, XA);
             } else {
               up2_row8(base, w2, xcs, sw, w, y0, 6 * tx - 1, XA);
             }
@@ -840,12 +836,11 @@ __global__ __launch_bounds__(256) void wino6_input_kernel(const float* __restric
             if (y1 == ka) {
 #pragma unroll
               for (int c = 0; c < 8; ++c) XB[c] = XA[c];
-            } else if (UPW) {
-              up2_row8w(base, w2, xcs, sw, w, y1, 6 * tx - 1, XB);
             } else {
               up2_row8(base, w2, xcs, sw, w, y1, 6 * tx - 1, XB);
             }
             kb = y1;
+          }
           }
 #pragma unroll
           for (int c = 0; c < 8; ++c) d[c] = up2_lerp_y(hy, XA[c], ly, XB[c]);
@@ -1159,14 +1154,15 @@ static bool w6out_vw1() {
   }();
   return v;
 }
-// the fused upsample's half-res rows from a six-column window (up2_row8w;
-// A/B only, POSFEAT_W6IN_UPW=1: bit-identical, but 781 -> 839 us for
-// upconv2's transform and 365 -> 379 for upconv3's, r16zn -- the loads it
-// saves hit in cache, the picks cost more)
-static bool w6in_upw() {
+// the fused upsample's half-res rows all loaded first (UPM = 1; A/B:
+// POSFEAT_W6IN_UPM=0 -- the two-row window).  (Measured and removed, r16zn:
+// each row from a six-column window with per-column picks instead of two
+// loads per column -- bit-identical, 781 -> 839 us for upconv2's transform:
+// the loads it saved hit in cache)
+static bool w6in_upm() {
   static const bool v = [] {
-    const char* e = pf_ab_getenv("POSFEAT_W6IN_UPW");
-    return e && e[0] == '1';
+    const char* e = pf_ab_getenv("POSFEAT_W6IN_UPM");
+    return !(e && e[0] == '0');
   }();
   return v;
 }
@@ -1195,12 +1191,12 @@ int pf_wino6_conv(const float* x, int xcs, int n, int h, int w, int Cin, const f
   float* M = reinterpret_cast<float*>(static_cast<char*>(ws) + pf_align(64 * T * Cin * 4, 256));
   if (stages & 1) {
     // fused upsample: one channel per thread (occupancy); plain: channel pairs
-    if (up2 && w6in_upw())
+    if (up2 && w6in_upm())
+      hipLaunchKernelGGL((wino6_input_kernel<true, 1, 1>), dim3(grid_for(T * Cin, 256)), dim3(256),
+                         0, st, x, xcs, n, h, w, Cin, V);
+    else if (up2)
       hipLaunchKernelGGL((wino6_input_kernel<true, 1>), dim3(grid_for(T * Cin, 256)), dim3(256), 0,
                          st, x, xcs, n, h, w, Cin, V);
-    else if (up2)
-      hipLaunchKernelGGL((wino6_input_kernel<true, 1, false>), dim3(grid_for(T * Cin, 256)),
-                         dim3(256), 0, st, x, xcs, n, h, w, Cin, V);
     else if (w6in_vw1())  // A/B: one channel per thread (fewer VGPRs, more waves)
       hipLaunchKernelGGL((wino6_input_kernel<false, 1>), dim3(grid_for(T * Cin, 256)), dim3(256),
                          0, st, x, xcs, n, h, w, Cin, V);
