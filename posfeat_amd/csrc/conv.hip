@@ -1797,6 +1797,11 @@ struct WsArgs {
   const float* bias;
   const float* res;
   int rcs, act;
+  int kpad;  // the weights' row pitch (<= 32 KC: chunks past it are zero)
+  // AM = 1 (G4, the stem): 4-channel NHWC input H x W, output OW wide, ohw
+  // pixels per image, stride / pad; taps outside the image read `zero`
+  int H, W, OW, ohw, stride, pad;
+  const float* zero;
 };
 
 // PD: A prefetch distance in chunks (PD + 1 register buffers); NW waves (2 or
@@ -1804,9 +1809,13 @@ struct WsArgs {
 // (K = 32 KC, the weights' row pitch); NB column blocks of 16 (BN = 16 NB)
 // EP: the epilogue -- 0 the accumulators stored as they are (the tap GEMM), 1
 // bias + activation, 2 bias + residual + activation
-template <int PD, int NW, int KC, int NB, int EP = 0>
+// AM: the A rows -- 0 dense (pitch lda), 1 G4: the 7x7 taps of a 4-channel
+// image (K order (kh, kw, c4), conv_bf6x_kernel's G4 gather: a lane's load jj
+// of chunk c is tap 8 c + 2 kq + jj)
+template <int PD, int NW, int KC, int NB, int EP = 0, int AM = 0>
 __global__ __launch_bounds__(NW * 64) void gemm_ws_kernel(WsArgs a) {
-  constexpr bool RES = EP == 2;
+  constexpr bool RES = EP == 2, G4 = AM == 1;
+  constexpr int G4K = 7;  // the stem's kernel size
   constexpr int NBUF = PD + 1, WS_NW = NW, WS_BM = NW * 32, WS_NCH = KC, WS_K = KC * BK;
   constexpr int WS_BN = 16 * NB;
   static_assert(WS_NCH % NBUF == 0 && PD >= 1 && PD < WS_NCH, "a tile starts at buffer 0");
@@ -1830,18 +1839,40 @@ __global__ __launch_bounds__(NW * 64) void gemm_ws_kernel(WsArgs a) {
   for (int e = tid; e < WS_NCH * 3 * WS_BN * 4; e += WS_NW * 64) {
     const int sl = e & 3, row = (e >> 2) % WS_BN, cp = (e >> 2) / WS_BN;
     const int c = cp / 3, pl = cp - c * 3;
-    const u32x4_t v = *reinterpret_cast<const u32x4_t*>(
-        a.wb + pl * a.wplane + (long long)(n0 + row) * WS_K + c * BK + sl * 8);
+    const int k = c * BK + sl * 8;
+    const u32x4_t v = k < a.kpad ? *reinterpret_cast<const u32x4_t*>(
+                                       a.wb + pl * a.wplane + (long long)(n0 + row) * a.kpad + k)
+                                 : u32x4_t{0u, 0u, 0u, 0u};
     *reinterpret_cast<u32x4_t*>(Bres + (cp * WS_BN + row) * BK + (sl ^ bx_swz(row)) * 8) = v;
   }
   pf_syncthreads();
   const int r16 = lane & 15, kq = lane >> 4;
-  auto rowp = [&](int mt, int rb) {
+  struct Row {
+    const float* p;  // dense: the row (+ this lane's k offset); G4: the image
+    int ih0, iw0;    // G4: the output pixel's top-left tap
+  };
+  auto rowp = [&](int mt, int rb) -> Row {
     const int m = min(mt * WS_BM + wave * 32 + rb * 16 + r16, a.M - 1);
-    return a.x + (long long)m * a.lda + kq * 8;
+    if constexpr (G4) {
+      const int n = m / a.ohw, rem = m - n * a.ohw, oh = rem / a.OW, ow = rem - oh * a.OW;
+      return Row{a.x + (long long)n * a.H * a.W * 4, oh * a.stride - a.pad, ow * a.stride - a.pad};
+    } else {
+      return Row{a.x + (long long)m * a.lda + kq * 8, 0, 0};
+    }
+  };
+  // load jj of chunk cc of row r
+  auto aptr = [&](const Row& r, int cc, int jj) -> const float* {
+    if constexpr (G4) {
+      const int t = 8 * cc + 2 * kq + jj, kh = t / G4K, kw = t - kh * G4K;
+      const int ih = r.ih0 + kh, iw = r.iw0 + kw;
+      const bool ok = kh < G4K && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+      return ok ? r.p + ((long long)ih * a.W + iw) * 4 : a.zero;
+    } else {
+      return r.p + cc * BK + jj * 4;
+    }
   };
   int mt = j;
-  const float* xr[2] = {rowp(mt, 0), rowp(mt, 1)};
+  Row xr[2] = {rowp(mt, 0), rowp(mt, 1)};
   f32x4 va[NBUF][2][2];  // [buffer][rb][jj]: chunk g of the block's walk in buffer g % NBUF
 #pragma unroll
   for (int c = 0; c < PD; ++c)
@@ -1849,7 +1880,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_ws_kernel(WsArgs a) {
     for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj)
-        va[c][rb][jj] = *reinterpret_cast<const f32x4*>(xr[rb] + c * BK + jj * 4);
+        va[c][rb][jj] = *reinterpret_cast<const f32x4*>(aptr(xr[rb], c, jj));
   for (;;) {
     f32x4 acc[2][NB];
 #pragma unroll
@@ -1862,7 +1893,7 @@ __global__ __launch_bounds__(NW * 64) void gemm_ws_kernel(WsArgs a) {
     // loop-invariant, and hoisting all of them out of the tile loop spills
     int boff = 0;
     if constexpr (KC == 2) asm volatile("" : "+s"(boff));
-    const float* xn[2] = {rowp(more ? nmt : mt, 0), rowp(more ? nmt : mt, 1)};
+    const Row xn[2] = {rowp(more ? nmt : mt, 0), rowp(more ? nmt : mt, 1)};
     // one chunk: split buffer `cur`, load chunk c + PD (this tile's, else the
     // next tile's) into buffer (cur + PD) % NBUF, 6 RB NB MFMAs
     auto step = [&](int c, auto cur_t) __attribute__((always_inline)) {
@@ -1880,10 +1911,10 @@ __global__ __launch_bounds__(NW * 64) void gemm_ws_kernel(WsArgs a) {
         const int cc = cl < WS_NCH ? cl : cl - WS_NCH;
 #pragma unroll
         for (int rb = 0; rb < 2; ++rb) {
-          const float* src = (cl < WS_NCH ? xr[rb] : xn[rb]) + cc * BK;
+          const Row& src = cl < WS_NCH ? xr[rb] : xn[rb];
 #pragma unroll
           for (int jj = 0; jj < 2; ++jj)
-            va[nxt][rb][jj] = *reinterpret_cast<const f32x4*>(src + jj * 4);
+            va[nxt][rb][jj] = *reinterpret_cast<const f32x4*>(aptr(src, cc, jj));
         }
       }
       const unsigned short* Bc = Bres + boff + c * 3 * WS_BN * BK;
@@ -3478,6 +3509,7 @@ int pf_gemm_ws(const float* x, int lda, int M, int K, const unsigned short* wb, 
     return e ? atoi(e) : 0;
   }();
   WsArgs a{x, wb, y, wplane, lda, ldc, M, N, per_n, abl, bias, res, rcs, act};
+  a.kpad = K;
   const dim3 grid((unsigned)(per_n * ntn));
   if (tap && pd == 2)
     hipLaunchKernelGGL((gemm_ws_kernel<2, 8, 6, 8>), grid, dim3(8 * 64), 0, st, a);
@@ -3501,6 +3533,39 @@ int pf_gemm_ws(const float* x, int lda, int M, int K, const unsigned short* wb, 
   pf_note_arith(PF_ARITH_BF6);
   return POSFEAT_OK;
 }
+// the stem (7x7 stride-s conv of a 4-channel NHWC image, weights [N][kpad]
+// with kpad = 224: the G4 K order) on the weight-stationary kernel: eight
+// chunks resident (the eighth zero), N = 64, bias + activation epilogue
+int pf_gemm_ws_stem(const float* x, int n, int H, int W, int OH, int OW, int stride, int pad,
+                    const unsigned short* wb, long long wplane, int kpad, int N, const float* bias,
+                    int act, float* y, int ldc, hipStream_t st) {
+  if (N != 64 || kpad != 224 || !x || !wb || !y || n <= 0 || OH <= 0 || OW <= 0 || ldc < N ||
+      (OH - 1) * stride - pad >= H || (OW - 1) * stride - pad >= W)
+    return POSFEAT_E_UNSUPPORTED;
+  int dev = 0, ncu = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return POSFEAT_E_HIP;
+  const float* zero = conv_zero_ptr();
+  if (!zero) return POSFEAT_E_HIP;
+  const int M = n * OH * OW, bm = 12 * 32, ntm = (M + bm - 1) / bm;
+  const int per_n = std::max(1, std::min(ntm, ncu));
+  WsArgs a{x, wb, y, wplane, 4, ldc, M, N, per_n, 0, bias, nullptr, 0, act};
+  a.kpad = kpad;
+  a.H = H;
+  a.W = W;
+  a.OW = OW;
+  a.ohw = OH * OW;
+  a.stride = stride;
+  a.pad = pad;
+  a.zero = zero;
+  hipLaunchKernelGGL((gemm_ws_kernel<1, 12, 8, 4, 1, 1>), dim3((unsigned)per_n), dim3(12 * 64), 0,
+                     st, a);
+  PF_CHECK_LAUNCH();
+  pf_note_arith(PF_ARITH_BF6);
+  return POSFEAT_OK;
+}
+
 int pf_tap_gemm_ws(const float* x, int lda, int M, const unsigned short* wb, long long wplane,
                    int N, float* y, int ldc, hipStream_t st) {
   return pf_gemm_ws(x, lda, M, 192, wb, wplane, N, nullptr, nullptr, 0, POSFEAT_ACT_NONE, y, ldc,

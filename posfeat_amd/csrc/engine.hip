@@ -191,6 +191,9 @@ struct posfeat_model {
   // N = 128 / 1024 convs slower). A/B: POSFEAT_WS1X1=1 every
   // instantiated shape, 2 those without a residual, 0 none
   int ws1x1 = 0;
+  // the stem on it too (pf_gemm_ws_stem, the G4 gather; A/B only,
+  // POSFEAT_WSSTEM=1: bit-identical, but 0.447 -> 0.557 ms at B = 32, r16zs)
+  bool wsstem = false;
   bool tapb = false;  // bf16x6 tap GEMM on pre-split planes (POSFEAT_BF6=2)
   Buf tapwb, tapLb;
   Buf gf_w, gf_b, gf_wp;
@@ -521,6 +524,18 @@ int conv(Ctx& c, const std::string& name, const float* x, int n, int h, int w, i
   // a short-K 1x1 conv: the weight-stationary GEMM (its three planes resident
   // in LDS, A streamed once per column tile; the bf6x tile's six terms in the
   // same order). Not under conv_fine's NCHW sink (the tile epilogue's)
+  if (c.m->wsstem && !c.dry && s->kh == 7 && s->kw == 7 && d.cin == 4 && xcs == 4 &&
+      s->cout == 64 && pf_bf6x_on()) {
+    const unsigned short* wb = nullptr;
+    long long wplane = 0;
+    c.wplanes_of(c.W(name), &wb, &wplane);
+    if (wb)
+      return timed(c, "conv:" + name, flops, [&] {
+        return pf_gemm_ws_stem(x, n, h, w, oh, ow, stride, d.pad, wb, wplane,
+                               (d.kh * d.kw * 4 + 31) / 32 * 32, s->cout, c.Bi(name), act, y, ycs,
+                               c.st);
+      });
+  }
   const int wsm = c.m->ws1x1;
   if (wsm && !(wsm >= 2 && res) && !(wsm == 3 && s->cout != 64) && !c.dry && s->kh == 1 && s->kw == 1 && stride == 1 && s->cin % 32 == 0 &&
       pf_bf6x_on() && pf_ws_gemm_ok(s->cin, s->cout) && !(c.m->nchwsink && name == "conv_fine")) {
@@ -909,6 +924,8 @@ void plan(posfeat_model* m) {
     m->nchwsink = k && k[0] == '1';
     const char* tw = pf_ab_getenv("POSFEAT_TAPWS");
     m->tapws = m->wsplit && !m->train && !(tw && tw[0] == '0');
+    const char* ws = pf_ab_getenv("POSFEAT_WSSTEM");
+    m->wsstem = m->wsplit && !m->train && ws && ws[0] == '1';
     const char* w1 = pf_ab_getenv("POSFEAT_WS1X1");
     m->ws1x1 = !m->wsplit || m->train || (w1 && w1[0] == '0') ? 0
                : w1 && (w1[0] == '1' || w1[0] == '2')   ? w1[0] - '0'

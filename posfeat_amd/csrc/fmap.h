@@ -55,6 +55,10 @@ int pf_tap_gemm_ws(const float* x, int lda, int M, const unsigned short* wb, lon
 // the same kernel for a short-K dense 1x1 conv (y = act(x W^T + bias (+ res)));
 // pf_ws_gemm_ok(K, N): a shape it is instantiated for
 bool pf_ws_gemm_ok(int K, int N);
+// ... and the stem (7x7, 4-channel NHWC image, N = 64, kpad = 224)
+int pf_gemm_ws_stem(const float* x, int n, int H, int W, int OH, int OW, int stride, int pad,
+                    const unsigned short* wb, long long wplane, int kpad, int N, const float* bias,
+                    int act, float* y, int ldc, hipStream_t st);
 int pf_gemm_ws(const float* x, int lda, int M, int K, const unsigned short* wb, long long wplane,
                int N, const float* bias, const float* res, int rcs, int act, float* y, int ldc,
                hipStream_t st);

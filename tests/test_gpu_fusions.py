@@ -139,3 +139,18 @@ def test_short_k_1x1_weight_stationary(gpu, hw, tmp_path):
         tol.check(k, torch.from_numpy(every[k]), ref[k], "ws1x1=1 " + k)
         print("ws1x1=1", hw, k, float(np.abs(every[k] - ref[k]).max()))
         print("ws1x1", hw, k, float(np.abs(got[k] - ref[k]).max()))
+
+
+@pytest.mark.parametrize("hw", [(128, 160), (96, 224)])
+def test_stem_weight_stationary(gpu, hw, tmp_path):
+    """POSFEAT_WSSTEM=1 (A/B, off by default: slower): the 7x7
+    stem on the weight-stationary kernel with the G4 gather (the tap order of
+    conv_bf6x_kernel's G4 tile, an eighth all-zero chunk) vs the G4 bf6x
+    tile: the same sums, so every map bit-identical."""
+    from conftest import run_ab_child
+    got = _run_default(hw)
+    out = str(tmp_path / "wsstem_on.npz")
+    ref = run_ab_child(CHILD % dict(var="POSFEAT_WSSTEM", val="1", hw=hw, out=out, keys=KEYS), out)
+    for k in KEYS:
+        assert np.array_equal(got[k], ref[k]), "%s differs (max %g)" % (
+            k, np.abs(got[k] - ref[k]).max())
