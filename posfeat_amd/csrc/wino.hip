@@ -799,10 +799,10 @@ __global__ __launch_bounds__(256) void wino6_input_kernel(const float* __restric
     int ka = -1, kb = -1;
     // UPM 1: the half-res rows ybase .. ybase + 5 (sh < 1/2: the patch's 8
     // rows need at most rows y0 - ybase <= 4 and y1 - ybase <= 5)
-    constexpr int NXR = UP2 && UPM == 1 ? 6 : 1;
+    constexpr int NXR = UP2 && UPM >= 1 ? 6 : 1;
     T XR[NXR][8];
     int ybase = 0;
-    if constexpr (UP2 && UPM == 1) {
+    if constexpr (UP2 && UPM >= 1) {
       ybase = (int)(sh * max(6 * ty - 1, 0));
 #pragma unroll
       for (int j = 0; j < 6; ++j) up2_row8(base, w2, xcs, sw, w, min(ybase + j, h2 - 1), 6 * tx - 1, XR[j]);
@@ -819,7 +819,7 @@ __global__ __launch_bounds__(256) void wino6_input_kernel(const float* __restric
           const int y0 = (int)ry;
           const int y1 = y0 + (y0 < h2 - 1 ? 1 : 0);
           const float ly = ry - y0, hy = 1.f - ly;
-          if constexpr (UPM == 1) {
+          if constexpr (UPM >= 1) {
             up2_pick(XR, y0 - ybase, XA);
             up2_pick(XR, y1 - ybase, XB);
           } else {
@@ -1158,7 +1158,8 @@ static bool w6out_vw1() {
 // POSFEAT_W6IN_UPM=0 -- the two-row window).  (Measured and removed, r16zn:
 // each row from a six-column window with per-column picks instead of two
 // loads per column -- bit-identical, 781 -> 839 us for upconv2's transform:
-// the loads it saved hit in cache)
+// the loads it saved hit in cache; and, r16zu, UPM = 1 forced to four waves
+// per SIMD: 128 VGPRs with 24 spilled, 0.59 -> 0.82 ms)
 static bool w6in_upm() {
   static const bool v = [] {
     const char* e = pf_ab_getenv("POSFEAT_W6IN_UPM");
