@@ -1775,16 +1775,18 @@ void conv_bf6x_kernel(ConvArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Weight-stationary tap GEMM (head.conv2's [M x 192] x [192 x 1152], K = 192):
-// in conv_bf6x_kernel every 128-row M tile re-reads its 128 x 192 weight
-// planes (147 KB, 6 B per weight) from L2 -- 1.5 K / BM of the output bytes,
-// the largest operand stream of a short-K GEMM.  Here a persistent block
-// keeps its 128 output columns' planes resident in LDS (loaded once, in the
-// bf6x stage layout and swizzle) and walks M tiles of 256 rows (8 waves x 32
-// rows, A straight to registers one chunk ahead, split3, the same six bf16
-// MFMA terms per 16x16x32 step and the same k order as conv_bf6x_kernel: the
-// same sums); the accumulators are stored straight from the registers.
-// Block b: column tile b % (N / 128), M tiles b / (N / 128) + i * per_n.
+// Weight-stationary GEMM (head.conv2's tap GEMM [M x 192] x [192 x 1152],
+// and the short-K 1x1 convs): in conv_bf6x_kernel every 128-row M tile
+// re-reads its 128 x K weight planes (147 KB at K = 192, 6 B per weight) from
+// L2 -- 1.5 K / BM of the output bytes, the largest operand stream of a
+// short-K GEMM.  Here a persistent block keeps its BN output columns' planes
+// resident in LDS (loaded once, in the bf6x stage layout and swizzle) and
+// walks M tiles of 32 NW rows (A straight to registers one chunk ahead,
+// split3, the same six bf16 MFMA terms per 16x16x32 step and the same k order
+// as conv_bf6x_kernel: the same sums); the accumulators are stored straight
+// from the registers, through the conv epilogue's order where there is one.
+// Block b (after the XCD remap): column tile b % (N / BN), M tiles
+// b / (N / BN) + i * per_n.
 struct WsArgs {
   const float* x;
   const unsigned short* wb;
