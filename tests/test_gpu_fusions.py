@@ -9,8 +9,9 @@ child process):
   output transform instead of a pass over its output;
 * POSFEAT_NCHWSINK=1 (A/B, off by default) -- conv_fine's epilogue writes
   local_map NCHW too (no layout pass): bit-identical;
-* POSFEAT_TAPWS / POSFEAT_WS1X1 -- head.conv2's tap GEMM and the short-K
-  1x1 convs on the weight-stationary kernel vs the tuned tiles;
+* POSFEAT_TAPWS / POSFEAT_WS1X1 / POSFEAT_WSSTEM -- head.conv2's tap GEMM,
+  the short-K 1x1 convs and the stem on the weight-stationary kernel vs the
+  tuned tiles;
 * POSFEAT_DSFUSE -- each stage's first bottleneck conv3 + downsample as one
   two-source GEMM (posfeat_conv1x1_dual) instead of two convs: a different
   fp32 summation order, so the maps agree within tests/tol.py's bounds.
