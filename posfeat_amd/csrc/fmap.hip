@@ -430,6 +430,55 @@ __global__ void head_tail_conv3_kernel(const float* __restrict__ x, int n, int h
   }
 }
 
+// head_tail_conv3_kernel<HT_U, false, true> with 32-bit pixel and element
+// indices (n hw cs < 2^31: the 64-bit index math held a third of its
+// registers) -- the same loads, arithmetic and order
+template <int HT_U>
+__global__ __launch_bounds__(256) void head_tail_il32_kernel(
+    const float* __restrict__ x, int n, int hw, int cs, const float* __restrict__ mean,
+    const float* __restrict__ rstd, const float* __restrict__ slope,
+    const float* __restrict__ w3, const float* __restrict__ b3, float* __restrict__ y) {
+  const float a = *slope;
+  const int lane = threadIdx.x & 63;
+  const int half = lane >> 5, l32 = lane & 31;
+  const int waves = gridDim.x * (blockDim.x >> 6);
+  const int wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const f32x4 wv = *reinterpret_cast<const f32x4*>(w3 + l32 * 4);
+  const float bias = *b3;
+  const int total = n * hw, pairs = (total + 1) / 2;
+  int lo = 0, hi = -1;
+  f32x4 m = {0.f, 0.f, 0.f, 0.f}, r = {0.f, 0.f, 0.f, 0.f};
+  for (int q = wid * HT_U; q < pairs; q += waves * HT_U) {
+    f32x4 xv[HT_U];
+#pragma unroll
+    for (int u = 0; u < HT_U; ++u) {
+      const int p = min(2 * min(q + u, pairs - 1) + half, total - 1);
+      xv[u] = *reinterpret_cast<const f32x4*>(x + (unsigned)(p * cs + l32 * 4));
+    }
+    float s[HT_U];
+#pragma unroll
+    for (int u = 0; u < HT_U; ++u) {
+      const int p = min(2 * min(q + u, pairs - 1) + half, total - 1);
+      if (p < lo || p >= hi) {
+        const int b = p / hw;
+        m = *reinterpret_cast<const f32x4*>(mean + b * 128 + l32 * 4);
+        r = *reinterpret_cast<const f32x4*>(rstd + b * 128 + l32 * 4);
+        lo = b * hw;
+        hi = lo + hw;
+      }
+      const f32x4 v = norm_prelu4(xv[u], m, r, a);
+      s[u] = v.x * wv.x + v.y * wv.y + v.z * wv.z + v.w * wv.w;
+    }
+#pragma unroll
+    for (int u = 0; u < HT_U; ++u) {
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1) s[u] += pf_shfl_xor(s[u], o, 64);
+      const int p = 2 * (q + u) + half;
+      if (l32 == 0 && q + u < pairs && p < total) y[p] = s[u] + bias;
+    }
+  }
+}
+
 __global__ PF_NO_PK_FP32 void softplus_norm_kernel(const float* __restrict__ x, int n, int hw,
                                      const float* __restrict__ mean,
                                      const float* __restrict__ rstd, float* __restrict__ y) {
@@ -640,7 +689,14 @@ int pf_head_tail(const float* x, int n, int hw, int cs, const float* mean, const
   int blocks = (int)((total / 2 + 3) / 4);
   if (blocks > tmax) blocks = tmax;
   if (blocks < 1) blocks = 1;
-  if (ab == 42)  // (A/B: interleaved waves)
+  const bool i32 = (long long)total * cs + 128 < (1LL << 31);
+  if (ab == 46 && i32)  // (A/B: 32-bit indices, 4 / 8 pairs per step)
+    hipLaunchKernelGGL((head_tail_il32_kernel<4>), dim3(blocks), dim3(256), 0, st, x, n, hw, cs,
+                       mean, rstd, slope, w3, b3, yraw);
+  else if (ab == 47 && i32)
+    hipLaunchKernelGGL((head_tail_il32_kernel<8>), dim3(blocks), dim3(256), 0, st, x, n, hw, cs,
+                       mean, rstd, slope, w3, b3, yraw);
+  else if (ab == 42)  // (A/B: interleaved waves)
     hipLaunchKernelGGL((head_tail_conv3_kernel<4, true, true>), dim3(blocks), dim3(256), 0, st, x, n,
                        hw, cs, mean, rstd, slope, w3, b3, yraw);
   else if (ab == 43)
