@@ -1804,6 +1804,8 @@ struct WsArgs {
   // pixels per image, stride / pad; taps outside the image read `zero`
   int H, W, OW, ohw, stride, pad;
   const float* zero;
+  // batched (grid.y GEMMs): element strides of A, C and the B planes
+  long long bx, by, bwb;
 };
 
 // PD: A prefetch distance in chunks (PD + 1 register buffers); NW waves (2 or
@@ -1825,6 +1827,11 @@ __global__ __launch_bounds__(NW * 64) void gemm_ws_kernel(WsArgs a) {
   __shared__ __attribute__((aligned(16))) unsigned short Bres[WS_NCH * 3 * WS_BN * BK];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int ntn = a.N / WS_BN;
+  if (gridDim.y > 1) {  // GEMM blockIdx.y of a batch
+    a.x += blockIdx.y * a.bx;
+    a.y += blockIdx.y * a.by;
+    a.wb += blockIdx.y * a.bwb;
+  }
   // (j, tn) pairs p = j * ntn + tn in contiguous runs per XCD (block b runs on
   // XCD b % 8): the ntn blocks that walk the same M tiles share an L2 for A
   int p = blockIdx.x;
@@ -3568,6 +3575,52 @@ int pf_gemm_ws_stem(const float* x, int n, int H, int W, int OH, int OW, int str
   return POSFEAT_OK;
 }
 
+// batched short-K GEMMs on the weight-stationary kernel, one GEMM per grid.y:
+// head.conv1's F(6x6) transform-domain GEMMs (K = N = 192: 96-column tiles,
+// 110 KB of planes per block), layer2's (K = N = 128: one 128-column
+// tile) and layer3's (K = N = 256: 64-column tiles) -- the same sums as the
+// bf6x tiles
+static int ws_batched_cfg(int K, int N, int* nbk) {
+  if (K == 192 && N % 96 == 0 && N <= 192) return *nbk = 6, 6;
+  if (K == 128 && N % 128 == 0) return *nbk = 8, 4;
+  if (K == 256 && N % 64 == 0) return *nbk = 4, 8;
+  return 0;
+}
+bool pf_gemm_ws_batched_ok(int K, int N) {
+  int nbk = 0;
+  return ws_batched_cfg(K, N, &nbk) != 0;
+}
+int pf_gemm_ws_batched(const float* A, int lda, long long sa, const unsigned short* Bb,
+                       long long bplane, long long sb, float* C, int ldc, long long sc, int nb,
+                       int M, int N, int K, hipStream_t st) {
+  if (!pf_gemm_ws_batched_ok(K, N) || !A || !Bb || !C || M <= 0 || nb < 1 || nb > 65535 ||
+      lda < K || lda % 4 || ldc < N)
+    return POSFEAT_E_UNSUPPORTED;
+  int dev = 0, ncu = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return POSFEAT_E_HIP;
+  int nbk = 0;
+  const int kc = ws_batched_cfg(K, N, &nbk);
+  const int bm = 12 * 32, ntn = N / (16 * nbk), ntm = (M + bm - 1) / bm;
+  const int per_n = std::max(1, std::min(ntm, ncu / std::max(1, ntn * nb)));
+  WsArgs a{A, Bb, C, bplane, lda, ldc, M, N, per_n, 0, nullptr, nullptr, 0, POSFEAT_ACT_NONE};
+  a.kpad = K;
+  a.bx = sa;
+  a.by = sc;
+  a.bwb = sb;
+  const dim3 grid((unsigned)(per_n * ntn), (unsigned)nb);
+  if (kc == 6)
+    hipLaunchKernelGGL((gemm_ws_kernel<1, 12, 6, 6>), grid, dim3(12 * 64), 0, st, a);
+  else if (kc == 4)
+    hipLaunchKernelGGL((gemm_ws_kernel<1, 12, 4, 8>), grid, dim3(12 * 64), 0, st, a);
+  else
+    hipLaunchKernelGGL((gemm_ws_kernel<1, 12, 8, 4>), grid, dim3(12 * 64), 0, st, a);
+  PF_CHECK_LAUNCH();
+  pf_note_arith(PF_ARITH_BF6);
+  return POSFEAT_OK;
+}
+
 int pf_tap_gemm_ws(const float* x, int lda, int M, const unsigned short* wb, long long wplane,
                    int N, float* y, int ldc, hipStream_t st) {
   return pf_gemm_ws(x, lda, M, 192, wb, wplane, N, nullptr, nullptr, 0, POSFEAT_ACT_NONE, y, ldc,
@@ -3903,6 +3956,17 @@ int pf_gemm_batched(const float* A, int lda, long long sa, const float* B, long 
                     int ldc, long long sc, int nb, int M, int N, int K, hipStream_t st,
                     const unsigned short* Bb, long long bplane) {
   if (K % BK || N % 4 || nb < 1) return POSFEAT_E_INVALID;
+  // the short-K batched GEMMs on the weight-stationary kernel: head.conv1's
+  // (K = 192), layer2's and layer3's conv2 (K = 128, 256) Winograd GEMMs
+  // (r16zz4, B = 32, two runs: 0.628 -> 0.484, 0.087 -> 0.076, 0.078 -> 0.070
+  // ms; bit-identical).  A/B POSFEAT_WSB: 0 off, 1 K = 192 only, 2 K <= 192
+  static const int wsb = [] {
+    const char* e = pf_ab_getenv("POSFEAT_WSB");
+    return e ? atoi(e) : 3;
+  }();
+  if (wsb && Bb && bf6x_on() && pf_gemm_ws_batched_ok(K, N) && lda % 4 == 0 &&
+      (K == 192 || (K == 128 && wsb >= 2) || (K == 256 && wsb >= 3)))
+    return pf_gemm_ws_batched(A, lda, sa, Bb, bplane, sb, C, ldc, sc, nb, M, N, K, st);
   posfeat_conv_desc d;
   d.n = 1;
   d.h = 1;

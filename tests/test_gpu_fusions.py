@@ -155,3 +155,22 @@ def test_stem_weight_stationary(gpu, hw, tmp_path):
     for k in KEYS:
         assert np.array_equal(got[k], ref[k]), "%s differs (max %g)" % (
             k, np.abs(got[k] - ref[k]).max())
+
+
+@pytest.mark.parametrize("hw", [(128, 160), (96, 224)])
+@pytest.mark.parametrize("mode", ["0", "1"])
+def test_head_conv1_gemm_weight_stationary(gpu, hw, mode, tmp_path):
+    """POSFEAT_WSB (default 3): the batched F(6x6) transform-domain GEMMs of
+    head.conv1 (K = N = 192, 96-column tiles) and of layer2 / layer3's conv2
+    (K = 128 / 256) on the weight-stationary kernel (grid.y = the transform
+    point) vs the bf6x tiles (=0) and vs head.conv1's alone (=1): the same six
+    bf16 terms per product in the same k order, so every map within its bound
+    (measured bit-identical, r16zz3 / r16zz4)."""
+    from conftest import run_ab_child
+    got = _run_default(hw)
+    out = str(tmp_path / ("wsb_%s.npz" % mode))
+    ref = run_ab_child(CHILD % dict(var="POSFEAT_WSB", val=mode, hw=hw, out=out, keys=KEYS), out)
+    for k in KEYS:
+        tol.check(k, torch.from_numpy(got[k]), ref[k], "wsb " + k)
+        print("wsb", mode, hw, k, float(np.abs(got[k] - ref[k]).max()),
+              bool(np.array_equal(got[k], ref[k])))
