@@ -3493,7 +3493,9 @@ int pf_gemm_ws(const float* x, int lda, int M, int K, const unsigned short* wb, 
   int kc = 0, nbk = 0;
   if (!ws_shape(K, N, &kc, &nbk)) return POSFEAT_E_UNSUPPORTED;
   const int bn = 16 * nbk;
-  if (!x || !wb || !y || M <= 0 || lda < K || ldc < N || lda % 4 || (res && rcs < N))
+  // (16-B A loads and weight-plane loads: aligned bases)
+  if (!x || !wb || !y || M <= 0 || lda < K || ldc < N || lda % 4 || (res && rcs < N) ||
+      ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(wb)) & 15) || wplane % 8)
     return POSFEAT_E_INVALID;
   int dev = 0, ncu = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
@@ -3549,7 +3551,8 @@ int pf_gemm_ws_stem(const float* x, int n, int H, int W, int OH, int OW, int str
                     const unsigned short* wb, long long wplane, int kpad, int N, const float* bias,
                     int act, float* y, int ldc, hipStream_t st) {
   if (N != 64 || kpad != 224 || !x || !wb || !y || n <= 0 || OH <= 0 || OW <= 0 || ldc < N ||
-      (OH - 1) * stride - pad >= H || (OW - 1) * stride - pad >= W)
+      (OH - 1) * stride - pad >= H || (OW - 1) * stride - pad >= W || wplane % 8 ||
+      ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(wb)) & 15))
     return POSFEAT_E_UNSUPPORTED;
   int dev = 0, ncu = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
@@ -3594,7 +3597,8 @@ int pf_gemm_ws_batched(const float* A, int lda, long long sa, const unsigned sho
                        long long bplane, long long sb, float* C, int ldc, long long sc, int nb,
                        int M, int N, int K, hipStream_t st) {
   if (!pf_gemm_ws_batched_ok(K, N) || !A || !Bb || !C || M <= 0 || nb < 1 || nb > 65535 ||
-      lda < K || lda % 4 || ldc < N)
+      lda < K || lda % 4 || ldc < N || sa % 4 || sb % 8 || bplane % 8 ||
+      ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(Bb)) & 15))
     return POSFEAT_E_UNSUPPORTED;
   int dev = 0, ncu = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
@@ -3965,8 +3969,10 @@ int pf_gemm_batched(const float* A, int lda, long long sa, const float* B, long 
     return e ? atoi(e) : 3;
   }();
   if (wsb && Bb && bf6x_on() && pf_gemm_ws_batched_ok(K, N) && lda % 4 == 0 &&
-      (K == 192 || (K == 128 && wsb >= 2) || (K == 256 && wsb >= 3)))
-    return pf_gemm_ws_batched(A, lda, sa, Bb, bplane, sb, C, ldc, sc, nb, M, N, K, st);
+      (K == 192 || (K == 128 && wsb >= 2) || (K == 256 && wsb >= 3))) {
+    const int r = pf_gemm_ws_batched(A, lda, sa, Bb, bplane, sb, C, ldc, sc, nb, M, N, K, st);
+    if (r != POSFEAT_E_UNSUPPORTED) return r;  // (else: the bf6x tiles below)
+  }
   posfeat_conv_desc d;
   d.n = 1;
   d.h = 1;

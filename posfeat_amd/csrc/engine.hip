@@ -542,7 +542,9 @@ int conv(Ctx& c, const std::string& name, const float* x, int n, int h, int w, i
     const unsigned short* wb = nullptr;
     long long wplane = 0;
     c.wplanes_of(c.W(name), &wb, &wplane);
-    if (wb)
+    // (pf_gemm_ws's operand alignment: else the tiles)
+    if (wb && wplane % 8 == 0 && xcs % 4 == 0 &&
+        ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(wb)) & 15) == 0)
       return timed(c, "conv:" + name, flops, [&] {
         return pf_gemm_ws(x, xcs, n * h * w, s->cin, wb, wplane, s->cout, c.Bi(name), res, rcs,
                           act, y, ycs, c.st);
@@ -1471,7 +1473,7 @@ int head_forward(Ctx& c, float* img4, float* local_point, bool side) {
             return pf_tap_gemm_ws(L, 192, M, reinterpret_cast<const unsigned short*>(c.f(m->tapwb)),
                                   1152LL * 192, 1152, c.f(m->tapP), 1152, c.st);
           });
-          if (rc != POSFEAT_OK && rc != POSFEAT_E_INVALID) return rc;
+          if (rc != POSFEAT_OK && rc != POSFEAT_E_INVALID && rc != POSFEAT_E_UNSUPPORTED) return rc;
         }
         if (rc != POSFEAT_OK && npf && !c.dry) {
           // the tuned tile if there is one (else the DB's / the default plan)
